@@ -1,0 +1,206 @@
+/*
+ * rt_render.h — C-ABI drop-in boundary for the per-pixel render path of
+ * tlinford/raytracer-challenge-rs (`Camera::render(&World) -> Canvas -> PPM`),
+ * implemented by hand-written HIP kernels for MI355X (gfx950).
+ *
+ * Plain C types only: pointers, sizes, doubles. No torch, no HIP types in the
+ * signatures (`stream` is an opaque hipStream_t passed as void*).
+ *
+ * Every entry point cites the reference interface it replaces
+ * (paths relative to the reference repository root).
+ *
+ * Conventions
+ *   - All matrices are 4x4, row-major, element (i,j) at [i*4+j]
+ *     (reference `Matrix::idx`, raytracer/src/matrix.rs:75-77).
+ *   - All arithmetic is IEEE-754 binary64 in the reference's operation order.
+ *   - Return value: RT_OK (0) on success, a negative RT_ERR_* code otherwise;
+ *     the message is available from rt_last_error() on the calling thread.
+ *     The library never aborts across the ABI (the reference panics instead:
+ *     raytracer/src/geometry/intersection.rs:113, matrix.rs:139, canvas.rs:45-46).
+ */
+#ifndef RT_RENDER_H
+#define RT_RENDER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------ */
+enum {
+  RT_OK = 0,
+  RT_ERR_INVALID_ARGUMENT = -1,
+  RT_ERR_UNSUPPORTED_SHAPE = -2,
+  RT_ERR_HIP = -3,
+  RT_ERR_RCCL = -4,
+  RT_ERR_DUPLICATE_SHAPES = -5, /* structurally-equal shapes: see DESIGN.md */
+  RT_ERR_NOT_INVERTIBLE = -6,   /* Matrix::inverse assert, matrix.rs:139 */
+  RT_ERR_BUFFER_TOO_SMALL = -7,
+  RT_ERR_NO_DEVICE = -8
+};
+
+/* ---- shape kinds / pattern kinds ---------------------------------------- */
+enum { RT_SHAPE_SPHERE = 0, RT_SHAPE_PLANE = 1 };
+enum {
+  RT_PATTERN_NONE = -1,
+  RT_PATTERN_TEST = 0,     /* pattern/test_pattern.rs:7-9 */
+  RT_PATTERN_STRIPE = 1,   /* pattern/stripe.rs:14-20     */
+  RT_PATTERN_GRADIENT = 2, /* pattern/gradient.rs:14-18   */
+  RT_PATTERN_RING = 3,     /* pattern/ring.rs:14-21       */
+  RT_PATTERN_CHECKERS = 4  /* pattern/checkers.rs:14-21   */
+};
+
+/*
+ * One flattened `Box<dyn Shape>` of `World::objects` (world.rs:18-21),
+ * in the reference's object order. Fields mirror `BaseShape`
+ * (geometry/mod.rs:12-20) and `Material` (material.rs:10-21).
+ * `inverse` is `BaseShape::transform_inverse` as computed by the reference's
+ * cofactor-expansion `Matrix::inverse` (matrix.rs:138-153); rt_matrix_inverse()
+ * below computes exactly that. The transpose (`transform_inverse_transpose`)
+ * is formed by the library.
+ */
+typedef struct rt_shape_desc {
+  int32_t kind;            /* RT_SHAPE_* */
+  int32_t casts_shadow;    /* BaseShape::shadow (geometry/mod.rs:19, :101-103) */
+  double transform[16];    /* BaseShape::transform */
+  double inverse[16];      /* BaseShape::transform_inverse */
+  /* Material (material.rs:10-21) */
+  double color[3];
+  double ambient, diffuse, specular, shininess;
+  double reflective, transparency, refractive_index;
+  /* Material::pattern (Option<Pattern>, pattern/mod.rs:17-22) */
+  int32_t pattern_kind;    /* RT_PATTERN_*, RT_PATTERN_NONE if None */
+  int32_t _pad;
+  double pattern_a[3], pattern_b[3];
+  double pattern_transform[16];
+  double pattern_inverse[16];
+} rt_shape_desc;
+
+/* `PointLight` (light.rs:4-24), in `World::lights` insertion order. */
+typedef struct rt_light_desc {
+  double position[3];
+  double intensity[3];
+} rt_light_desc;
+
+/* `Camera` (camera.rs:19-30) with its host-computed derived fields. */
+typedef struct rt_camera_desc {
+  uint32_t hsize, vsize;
+  double pixel_size, half_width, half_height;
+  double inverse[16]; /* Camera::transform_inverse */
+} rt_camera_desc;
+
+/* Exact work counters. One "ray" = one `World::intersect` invocation
+ * (world.rs:71 for radiance rays, world.rs:101 for shadow rays). */
+typedef struct rt_stats {
+  uint64_t rays_primary;
+  uint64_t rays_reflect;
+  uint64_t rays_refract;
+  uint64_t rays_shadow;
+  uint64_t sphere_tests;
+  uint64_t plane_tests;
+  uint64_t sphere_disc_ge0;
+  double ms_kernel; /* device time of the render kernel(s), HIP events */
+  double ms_total;  /* wall time of the call */
+} rt_stats;
+
+typedef struct rt_scene rt_scene; /* opaque: device-resident flattened World */
+
+/* ---- host math helpers (exact restatements used to build descs) --------- */
+
+/* `Matrix::inverse` (matrix.rs:138-153) by cofactor expansion, bit-exact.
+ * Returns RT_ERR_NOT_INVERTIBLE when |det| < 1e-5 (matrix.rs:134-136). */
+int rt_matrix_inverse(const double m[16], double out[16]);
+
+/* `Camera::new` (camera.rs:33-55) + `Camera::set_transform` (camera.rs:128-131). */
+int rt_camera_init(uint32_t hsize, uint32_t vsize, double field_of_view,
+                   const double transform[16], rt_camera_desc* out);
+
+/* ---- scene lifetime ------------------------------------------------------ */
+
+/* Flatten + upload a World (replaces building `World` for `Camera::render`).
+ * `device` is the HIP ordinal. Fails with RT_ERR_DUPLICATE_SHAPES when two
+ * shapes may be structurally equal (the refractive-index `containers` walk,
+ * geometry/intersection.rs:63-90, then depends on structural equality). */
+int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes,
+                    const rt_light_desc* lights, size_t n_lights, int device,
+                    rt_scene** out);
+void rt_scene_destroy(rt_scene* scene);
+
+/* ---- render entry points -------------------------------------------------- */
+
+/* `Camera::render(&mut self, &World) -> Canvas` (camera.rs:133-148) with
+ * `MAX_RECURSION_DEPTH` replaced by `max_depth` (world.rs:16; 5 = reference).
+ * `out_rgb` is a caller-owned HOST buffer of vsize*hsize*3 doubles, row-major
+ * `y*w + x` (canvas.rs:44-48). Synchronous. */
+int rt_render(const rt_scene* scene, const rt_camera_desc* camera,
+              uint32_t max_depth, double* out_rgb, rt_stats* stats);
+
+/* Device-resident shard render (used by multi-GPU and the benchmark).
+ * Renders the rows y with (y / row_block) % n_shards == shard, in increasing
+ * y order, into `d_out_rgb` (a DEVICE buffer on the scene's device holding
+ * rows_in_shard*hsize*3 doubles). `stream` is a hipStream_t (NULL = default).
+ * Asynchronous unless `stats` is non-NULL (then it synchronises to read the
+ * counters). `n_shards == 1` renders the whole frame. */
+int rt_render_shard_device(const rt_scene* scene, const rt_camera_desc* camera,
+                           uint32_t max_depth, uint32_t row_block,
+                           uint32_t shard, uint32_t n_shards,
+                           double* d_out_rgb, void* stream, rt_stats* stats);
+
+/* Number of rows shard `shard` of `n_shards` owns (for sizing buffers). */
+uint32_t rt_shard_rows(uint32_t vsize, uint32_t row_block, uint32_t shard,
+                       uint32_t n_shards);
+
+/* `World::color_at(&Ray, remaining)` (world.rs:70-81) for a batch of rays.
+ * rays: n*6 doubles (origin xyz, direction xyz); out_rgb: n*3 doubles (host). */
+int rt_color_at_batch(const rt_scene* scene, const double* rays, size_t n,
+                      uint32_t remaining, double* out_rgb, rt_stats* stats);
+
+/* `World::is_shadowed(point, light)` (world.rs:95-105) for a batch of points
+ * against light index `light`. out: n uint8 (1 = shadowed). */
+int rt_is_shadowed_batch(const rt_scene* scene, const double* points, size_t n,
+                         uint32_t light, uint8_t* out);
+
+/* `World::intersect` + `hit` + `prepare_computations` + `schlick`
+ * (world.rs:31-38, intersection.rs:53-105,118-120,147-162) for a batch of
+ * rays. Per ray, out holds 24 doubles:
+ *   [0] hit object index (-1 = miss)  [1] t   [2..4] point
+ *   [5..7] over_point  [8..10] under_point  [11..13] eyev  [14..16] normalv
+ *   [17] inside (0/1)  [18..20] reflectv  [21] n1  [22] n2  [23] schlick */
+int rt_hit_batch(const rt_scene* scene, const double* rays, size_t n,
+                 double* out24);
+
+/* ---- multi-GPU (one process, several devices; the per-process path for
+ *      torch.distributed is rt_render_shard_device) ------------------------ */
+
+/* Render on `n_devices` devices (ordinals 0..n-1) with interleaved row blocks
+ * and assemble the canvas with one RCCL gather to device 0. `scenes[i]` must
+ * have been created on device i. Output to a HOST buffer like rt_render. */
+int rt_render_multi(rt_scene* const* scenes, int n_devices,
+                    const rt_camera_desc* camera, uint32_t max_depth,
+                    uint32_t row_block, double* out_rgb, rt_stats* stats);
+
+/* ---- output (image/ppm.rs) ------------------------------------------------ */
+
+/* `canvas_to_ppm` (image/ppm.rs:24-51): plain P3 text, 70-column wrapping,
+ * `(v*255).round() as u8` quantisation. If out == NULL or cap too small,
+ * *out_len receives the required size and RT_ERR_BUFFER_TOO_SMALL (or RT_OK
+ * with out == NULL) is returned. No terminating NUL is written. */
+int rt_canvas_to_ppm(const double* rgb, uint32_t width, uint32_t height,
+                     char* out, size_t cap, size_t* out_len);
+
+/* `scale_color_component` (image/ppm.rs:73-75) over n values. */
+int rt_quantize_u8(const double* values, size_t n, uint8_t* out);
+
+/* ---- diagnostics ----------------------------------------------------------- */
+const char* rt_last_error(void);
+int rt_abi_version(void);
+int rt_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_RENDER_H */

@@ -1,0 +1,276 @@
+// rt_world.hpp — C++ host mirror of the reference's scene API, driving the
+// C-ABI (include/rt_render.h). Same names and argument meaning as
+// raytracer/src/{material,light,pattern/mod,geometry/mod,world,camera,canvas}.rs,
+// so a caller of `Camera::render(&World) -> Canvas` switches by changing the
+// namespace. Rendering, `color_at`, `is_shadowed` and the per-hit
+// `prepare_computations` all run on the GPU through the ABI; this header only
+// builds and flattens the scene (host-side, like the reference's setup code).
+#pragma once
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../../include/rt_render.h"
+#include "rt_math.hpp"
+
+namespace rt {
+
+struct RtError : std::runtime_error {
+  int code;
+  RtError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+inline void check(int rc, const char* what) {
+  if (rc != RT_OK) throw RtError(rc, std::string(what) + ": " + rt_last_error());
+}
+
+// pattern/mod.rs:17-91
+struct Pattern {
+  int kind = RT_PATTERN_TEST;
+  Color a, b;
+  Matrix transform = Matrix::identity(4, 4);
+  Matrix transform_inverse = Matrix::identity(4, 4);
+  void set_transform(const Matrix& t) {  // pattern/mod.rs:34-37
+    transform = t;
+    transform_inverse = t.inverse();
+  }
+};
+inline Pattern test_pattern() { return Pattern{}; }
+inline Pattern make_pattern(int kind, const Color& a, const Color& b) {
+  Pattern p;
+  p.kind = kind;
+  p.a = a;
+  p.b = b;
+  return p;
+}
+inline Pattern stripe_pattern(const Color& a, const Color& b) { return make_pattern(RT_PATTERN_STRIPE, a, b); }
+inline Pattern gradient_pattern(const Color& a, const Color& b) { return make_pattern(RT_PATTERN_GRADIENT, a, b); }
+inline Pattern ring_pattern(const Color& a, const Color& b) { return make_pattern(RT_PATTERN_RING, a, b); }
+inline Pattern checkers_pattern(const Color& a, const Color& b) { return make_pattern(RT_PATTERN_CHECKERS, a, b); }
+
+// material.rs:10-36
+struct Material {
+  Color color{1.0, 1.0, 1.0};
+  double ambient = 0.1, diffuse = 0.9, specular = 0.9, shininess = 200.0;
+  double reflective = 0.0, transparency = 0.0, refractive_index = 1.0;
+  bool has_pattern = false;
+  Pattern pattern;
+  void set_pattern(const Pattern& p) {
+    pattern = p;
+    has_pattern = true;
+  }
+};
+
+// light.rs:4-24
+struct PointLight {
+  Point position;
+  Color intensity;
+  PointLight() = default;
+  PointLight(const Point& p, const Color& i) : position(p), intensity(i) {}
+};
+
+// geometry/mod.rs:12-108 (BaseShape + the parts of `trait Shape` on the path)
+struct Shape {
+  int kind = RT_SHAPE_SPHERE;
+  Matrix transform = Matrix::identity(4, 4);
+  Matrix transform_inverse = Matrix::identity(4, 4);
+  Material material;
+  bool shadow = true;
+  void set_transform(const Matrix& t) {  // geometry/mod.rs:74-85
+    transform_inverse = t.inverse();
+    transform = t;
+  }
+  void no_shadow() { shadow = false; }            // :105-107
+  bool has_shadow() const { return shadow; }      // :101-103
+  Matrix transform_inverse_transpose() const { return transform_inverse.transpose(); }
+};
+// sphere.rs:16-25, :70-77
+inline Shape Sphere() { return Shape{}; }
+inline Shape glass_sphere() {
+  Shape s;
+  s.material.transparency = 1.0;
+  s.material.refractive_index = 1.5;
+  return s;
+}
+inline Shape Plane() {  // plane.rs:19-31
+  Shape s;
+  s.kind = RT_SHAPE_PLANE;
+  return s;
+}
+
+// canvas.rs:8-52 + image/ppm.rs
+class Canvas {
+ public:
+  Canvas(size_t w, size_t h) : w_(w), h_(h), px_(w * h * 3, 0.0) {}
+  size_t width() const { return w_; }
+  size_t height() const { return h_; }
+  Color get_pixel(size_t x, size_t y) const {
+    const double* p = &px_[idx(x, y)];
+    return Color(p[0], p[1], p[2]);
+  }
+  void set_pixel(size_t x, size_t y, const Color& c) {
+    double* p = &px_[idx(x, y)];
+    p[0] = c.red; p[1] = c.green; p[2] = c.blue;
+  }
+  double* data() { return px_.data(); }
+  const double* data() const { return px_.data(); }
+  std::string to_ppm() const {  // canvas_to_ppm (image/ppm.rs:24-51)
+    size_t len = 0;
+    check(rt_canvas_to_ppm(px_.data(), (uint32_t)w_, (uint32_t)h_, nullptr, 0, &len), "rt_canvas_to_ppm");
+    std::string s(len, '\0');
+    check(rt_canvas_to_ppm(px_.data(), (uint32_t)w_, (uint32_t)h_, &s[0], len, &len), "rt_canvas_to_ppm");
+    return s;
+  }
+
+ private:
+  size_t idx(size_t x, size_t y) const {  // canvas.rs:44-48 (asserts -> exceptions)
+    if (x >= w_ || y >= h_) throw std::out_of_range("Canvas: pixel out of bounds");
+    return (y * w_ + x) * 3;
+  }
+  size_t w_, h_;
+  std::vector<double> px_;
+};
+
+inline rt_shape_desc to_desc(const Shape& s) {
+  rt_shape_desc d;
+  std::memset(&d, 0, sizeof d);
+  d.kind = s.kind;
+  d.casts_shadow = s.shadow ? 1 : 0;
+  std::memcpy(d.transform, s.transform.data(), sizeof d.transform);
+  std::memcpy(d.inverse, s.transform_inverse.data(), sizeof d.inverse);
+  const Material& m = s.material;
+  d.color[0] = m.color.red; d.color[1] = m.color.green; d.color[2] = m.color.blue;
+  d.ambient = m.ambient; d.diffuse = m.diffuse; d.specular = m.specular; d.shininess = m.shininess;
+  d.reflective = m.reflective; d.transparency = m.transparency; d.refractive_index = m.refractive_index;
+  d.pattern_kind = m.has_pattern ? m.pattern.kind : RT_PATTERN_NONE;
+  const Pattern& p = m.pattern;
+  d.pattern_a[0] = p.a.red; d.pattern_a[1] = p.a.green; d.pattern_a[2] = p.a.blue;
+  d.pattern_b[0] = p.b.red; d.pattern_b[1] = p.b.green; d.pattern_b[2] = p.b.blue;
+  std::memcpy(d.pattern_transform, p.transform.data(), sizeof d.pattern_transform);
+  std::memcpy(d.pattern_inverse, p.transform_inverse.data(), sizeof d.pattern_inverse);
+  return d;
+}
+
+// world.rs:18-151. The flattened device copy is built lazily and dropped on
+// any mutation through this API.
+class World {
+ public:
+  World() = default;
+  World(const World&) = delete;
+  World& operator=(const World&) = delete;
+  ~World() { drop(); }
+  static std::unique_ptr<World> make_default() {  // world.rs:137-151
+    auto w = std::make_unique<World>();
+    w->add_light(PointLight(Point(-10, 10, -10), Color(1.0, 1.0, 1.0)));
+    Shape s1 = Sphere();
+    s1.material.color = Color(0.8, 1.0, 0.6);
+    s1.material.diffuse = 0.7;
+    s1.material.specular = 0.2;
+    Shape s2 = Sphere();
+    s2.set_transform(scaling(0.5, 0.5, 0.5));
+    w->add_object(s1);
+    w->add_object(s2);
+    return w;
+  }
+  void add_object(const Shape& s) { drop(); objects_.push_back(s); }     // :87-89
+  void add_light(const PointLight& l) { drop(); lights_.push_back(l); }  // :83-85
+  size_t n_objects() const { return objects_.size(); }
+  size_t n_lights() const { return lights_.size(); }
+  Shape& object(size_t i) { drop(); return objects_.at(i); }
+  const Shape& object_c(size_t i) const { return objects_.at(i); }
+  PointLight& light(size_t i) { drop(); return lights_.at(i); }
+  std::vector<rt_shape_desc> descs() const {
+    std::vector<rt_shape_desc> v;
+    v.reserve(objects_.size());
+    for (const Shape& s : objects_) v.push_back(to_desc(s));
+    return v;
+  }
+  std::vector<rt_light_desc> light_descs() const {
+    std::vector<rt_light_desc> v(lights_.size());
+    for (size_t i = 0; i < lights_.size(); ++i) {
+      v[i].position[0] = lights_[i].position.x; v[i].position[1] = lights_[i].position.y;
+      v[i].position[2] = lights_[i].position.z;
+      v[i].intensity[0] = lights_[i].intensity.red; v[i].intensity[1] = lights_[i].intensity.green;
+      v[i].intensity[2] = lights_[i].intensity.blue;
+    }
+    return v;
+  }
+  // Device-resident flattened world (uploaded on first use).
+  const rt_scene* scene(int device = 0) const {
+    if (!scene_ || scene_device_ != device) {
+      const_cast<World*>(this)->drop();
+      auto d = descs();
+      auto l = light_descs();
+      rt_scene* s = nullptr;
+      check(rt_scene_create(d.data(), d.size(), l.data(), l.size(), device, &s), "rt_scene_create");
+      scene_ = s;
+      scene_device_ = device;
+    }
+    return scene_;
+  }
+  // world.rs:70-81 on the GPU
+  Color color_at(const Ray& r, unsigned remaining) const {
+    double ray[6] = {r.origin.x, r.origin.y, r.origin.z, r.direction.x, r.direction.y, r.direction.z};
+    double c[3];
+    check(rt_color_at_batch(scene(), ray, 1, remaining, c, nullptr), "rt_color_at_batch");
+    return Color(c[0], c[1], c[2]);
+  }
+  // world.rs:95-105 on the GPU (light given by index into `lights`)
+  bool is_shadowed(const Point& p, size_t light) const {
+    double pt[3] = {p.x, p.y, p.z};
+    uint8_t o = 0;
+    check(rt_is_shadowed_batch(scene(), pt, 1, (uint32_t)light, &o), "rt_is_shadowed_batch");
+    return o != 0;
+  }
+
+ private:
+  void drop() {
+    if (scene_) rt_scene_destroy(scene_);
+    scene_ = nullptr;
+  }
+  std::vector<Shape> objects_;
+  std::vector<PointLight> lights_;
+  mutable rt_scene* scene_ = nullptr;
+  mutable int scene_device_ = -1;
+};
+
+// camera.rs:19-253
+class Camera {
+ public:
+  Camera(size_t hsize, size_t vsize, double field_of_view) : fov_(field_of_view) {
+    check(rt_camera_init((uint32_t)hsize, (uint32_t)vsize, field_of_view, nullptr, &desc_), "rt_camera_init");
+  }
+  void set_transform(const Matrix& t) {  // camera.rs:128-131
+    transform_ = t;
+    check(rt_camera_init(desc_.hsize, desc_.vsize, fov_, t.data(), &desc_), "rt_camera_init");
+  }
+  size_t hsize() const { return desc_.hsize; }
+  size_t vsize() const { return desc_.vsize; }
+  double pixel_size() const { return desc_.pixel_size; }
+  const Matrix& transform() const { return transform_; }
+  const rt_camera_desc& desc() const { return desc_; }
+  Ray ray_for_pixel(size_t px, size_t py) const {  // camera.rs:57-69 (host restatement)
+    const double xoffset = ((double)px + 0.5) * desc_.pixel_size;
+    const double yoffset = ((double)py + 0.5) * desc_.pixel_size;
+    const double world_x = desc_.half_width - xoffset;
+    const double world_y = desc_.half_height - yoffset;
+    const Matrix inv = Matrix::from_slice(4, 4, desc_.inverse);
+    const Point pixel = inv * Point(world_x, world_y, -1.0);
+    const Point origin = inv * Point::origin();
+    return Ray(origin, (pixel - origin).normalize());
+  }
+  // camera.rs:133-148: the drop-in. `max_depth` = MAX_RECURSION_DEPTH (5).
+  Canvas render(const World& world, unsigned max_depth = 5, rt_stats* stats = nullptr) const {
+    Canvas c(desc_.hsize, desc_.vsize);
+    check(rt_render(world.scene(), &desc_, max_depth, c.data(), stats), "rt_render");
+    return c;
+  }
+
+ private:
+  double fov_;
+  Matrix transform_ = Matrix::identity(4, 4);
+  rt_camera_desc desc_{};
+};
+
+}  // namespace rt

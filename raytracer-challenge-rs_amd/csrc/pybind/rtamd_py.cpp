@@ -1,0 +1,316 @@
+// rtamd_py.cpp — pybind11 bindings of the C++ host API (host/rt_world.hpp) so
+// Python tests and bench.py drive exactly the code a C++/FFI caller would.
+// Nothing here computes a pixel: render / color_at / is_shadowed / hits go
+// through the C-ABI into the HIP kernels.
+#include <pybind11/numpy.h>
+#include <pybind11/operators.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "../host/rt_world.hpp"
+
+namespace py = pybind11;
+using namespace rt;
+
+static py::dict stats_dict(const rt_stats& s) {
+  py::dict d;
+  d["rays_primary"] = s.rays_primary;
+  d["rays_reflect"] = s.rays_reflect;
+  d["rays_refract"] = s.rays_refract;
+  d["rays_shadow"] = s.rays_shadow;
+  d["sphere_tests"] = s.sphere_tests;
+  d["plane_tests"] = s.plane_tests;
+  d["sphere_disc_ge0"] = s.sphere_disc_ge0;
+  d["ms_kernel"] = s.ms_kernel;
+  d["ms_total"] = s.ms_total;
+  return d;
+}
+
+static py::bytes pod_bytes(const void* p, size_t n) { return py::bytes((const char*)p, n); }
+
+static py::array_t<double> check_rays(py::array_t<double, py::array::c_style | py::array::forcecast> a,
+                                      size_t width) {
+  if (a.ndim() != 2 || (size_t)a.shape(1) != width)
+    throw std::invalid_argument("expected an (n, " + std::to_string(width) + ") float64 array");
+  return a;
+}
+
+PYBIND11_MODULE(_rtamd, m) {
+  m.doc() = "MI355X-native render path of raytracer-challenge-rs (host API over the C-ABI)";
+  py::register_exception<RtError>(m, "RtError");
+  m.attr("EPSILON") = EPSILON;
+  m.attr("ABI_VERSION") = RT_ABI_VERSION;
+  m.def("equal", &equal);
+  m.def("device_count", &rt_device_count);
+  m.def("abi_version", &rt_abi_version);
+
+  py::class_<Point>(m, "Point")
+      .def(py::init<double, double, double>())
+      .def_static("origin", &Point::origin)
+      .def_readwrite("x", &Point::x).def_readwrite("y", &Point::y).def_readwrite("z", &Point::z)
+      .def("__eq__", [](const Point& a, const Point& b) { return a == b; })
+      .def("__add__", [](const Point& p, const Vector& v) { return p + v; })
+      .def("__sub__", [](const Point& a, const Point& b) { return a - b; })
+      .def("__sub__", [](const Point& p, const Vector& v) { return p - v; })
+      .def("tuple", [](const Point& p) { return py::make_tuple(p.x, p.y, p.z); })
+      .def("__repr__", [](const Point& p) { return "Point(" + std::to_string(p.x) + ", " + std::to_string(p.y) + ", " + std::to_string(p.z) + ")"; });
+  py::class_<Vector>(m, "Vector")
+      .def(py::init<double, double, double>())
+      .def_readwrite("x", &Vector::x).def_readwrite("y", &Vector::y).def_readwrite("z", &Vector::z)
+      .def("magnitude", &Vector::magnitude)
+      .def("normalize", &Vector::normalize)
+      .def("reflect", &Vector::reflect)
+      .def("__eq__", [](const Vector& a, const Vector& b) { return a == b; })
+      .def("__add__", [](const Vector& a, const Vector& b) { return a + b; })
+      .def("__sub__", [](const Vector& a, const Vector& b) { return a - b; })
+      .def("__neg__", [](const Vector& a) { return -a; })
+      .def("__mul__", [](const Vector& a, double s) { return a * s; })
+      .def("tuple", [](const Vector& p) { return py::make_tuple(p.x, p.y, p.z); })
+      .def("__repr__", [](const Vector& p) { return "Vector(" + std::to_string(p.x) + ", " + std::to_string(p.y) + ", " + std::to_string(p.z) + ")"; });
+  m.def("dot", &dot);
+  m.def("cross", &cross);
+  py::class_<Color>(m, "Color")
+      .def(py::init<double, double, double>())
+      .def_static("black", &Color::black)
+      .def_static("white", &Color::white)
+      .def_readwrite("red", &Color::red).def_readwrite("green", &Color::green).def_readwrite("blue", &Color::blue)
+      .def("__eq__", [](const Color& a, const Color& b) { return a == b; })
+      .def("tuple", [](const Color& c) { return py::make_tuple(c.red, c.green, c.blue); })
+      .def("__repr__", [](const Color& c) { return "Color(" + std::to_string(c.red) + ", " + std::to_string(c.green) + ", " + std::to_string(c.blue) + ")"; });
+  py::class_<Ray>(m, "Ray")
+      .def(py::init<const Point&, const Vector&>())
+      .def_readwrite("origin", &Ray::origin)
+      .def_readwrite("direction", &Ray::direction)
+      .def("position", &Ray::position)
+      .def("transform", [](const Ray& r, const Matrix& mm) { return transform(r, mm); });
+
+  py::class_<Matrix>(m, "Matrix")
+      .def(py::init<int, int>())
+      .def_static("identity", &Matrix::identity)
+      .def_static("from_rows", [](const std::vector<std::vector<double>>& rows) {
+        int r = (int)rows.size(), c = r ? (int)rows[0].size() : 0;
+        Matrix mm(r, c);
+        for (int i = 0; i < r; ++i) {
+          if ((int)rows[i].size() != c) throw std::invalid_argument("ragged rows");
+          for (int j = 0; j < c; ++j) mm(i, j) = rows[i][j];
+        }
+        return mm;
+      })
+      .def("rows", &Matrix::rows)
+      .def("columns", &Matrix::columns)
+      .def("__getitem__", [](const Matrix& mm, std::pair<int, int> ij) {
+        if (ij.first < 0 || ij.first >= mm.rows() || ij.second < 0 || ij.second >= mm.columns())
+          throw py::index_error();
+        return mm(ij.first, ij.second);
+      })
+      .def("__setitem__", [](Matrix& mm, std::pair<int, int> ij, double v) {
+        if (ij.first < 0 || ij.first >= mm.rows() || ij.second < 0 || ij.second >= mm.columns())
+          throw py::index_error();
+        mm(ij.first, ij.second) = v;
+      })
+      .def("transpose", &Matrix::transpose)
+      .def("determinant", &Matrix::determinant)
+      .def("submatrix", &Matrix::submatrix)
+      .def("minor", &Matrix::minor)
+      .def("cofactor", &Matrix::cofactor)
+      .def("is_invertible", &Matrix::is_invertible)
+      .def("inverse", [](const Matrix& mm) {
+        if (!mm.is_invertible()) throw RtError(RT_ERR_NOT_INVERTIBLE, "matrix is not invertible");
+        return mm.inverse();
+      })
+      .def("translate", &Matrix::translate)
+      .def("scale", &Matrix::scale)
+      .def("rotate_x", &Matrix::rotate_x)
+      .def("rotate_y", &Matrix::rotate_y)
+      .def("rotate_z", &Matrix::rotate_z)
+      .def("shear", &Matrix::shear)
+      .def("__eq__", [](const Matrix& a, const Matrix& b) { return a == b; })
+      .def("__mul__", [](const Matrix& a, const Matrix& b) { return a * b; })
+      .def("__mul__", [](const Matrix& a, const Point& p) { return a * p; })
+      .def("__mul__", [](const Matrix& a, const Vector& v) { return a * v; })
+      .def("to_list", [](const Matrix& mm) {
+        std::vector<double> v(mm.data(), mm.data() + mm.rows() * mm.columns());
+        return v;
+      });
+  m.def("translation", &translation);
+  m.def("scaling", &scaling);
+  m.def("rotation_x", &rotation_x);
+  m.def("rotation_y", &rotation_y);
+  m.def("rotation_z", &rotation_z);
+  m.def("shearing", &shearing);
+  m.def("view_transform", &view_transform);
+
+  py::class_<Pattern>(m, "Pattern")
+      .def_readonly("kind", &Pattern::kind)
+      .def_readwrite("a", &Pattern::a)
+      .def_readwrite("b", &Pattern::b)
+      .def_readonly("transform", &Pattern::transform)
+      .def_readonly("transform_inverse", &Pattern::transform_inverse)
+      .def("set_transform", &Pattern::set_transform);
+  m.def("test_pattern", &test_pattern);
+  m.def("stripe_pattern", &stripe_pattern);
+  m.def("gradient_pattern", &gradient_pattern);
+  m.def("ring_pattern", &ring_pattern);
+  m.def("checkers_pattern", &checkers_pattern);
+
+  py::class_<Material>(m, "Material")
+      .def(py::init<>())
+      .def_readwrite("color", &Material::color)
+      .def_readwrite("ambient", &Material::ambient)
+      .def_readwrite("diffuse", &Material::diffuse)
+      .def_readwrite("specular", &Material::specular)
+      .def_readwrite("shininess", &Material::shininess)
+      .def_readwrite("reflective", &Material::reflective)
+      .def_readwrite("transparency", &Material::transparency)
+      .def_readwrite("refractive_index", &Material::refractive_index)
+      .def_readonly("has_pattern", &Material::has_pattern)
+      .def_readonly("pattern", &Material::pattern)
+      .def("set_pattern", &Material::set_pattern);
+
+  py::class_<PointLight>(m, "PointLight")
+      .def(py::init<const Point&, const Color&>())
+      .def_readwrite("position", &PointLight::position)
+      .def_readwrite("intensity", &PointLight::intensity);
+
+  py::class_<Shape>(m, "Shape")
+      .def_readonly("kind", &Shape::kind)
+      .def_readwrite("material", &Shape::material)
+      .def_readonly("transform", &Shape::transform)
+      .def_readonly("transform_inverse", &Shape::transform_inverse)
+      .def("transform_inverse_transpose", &Shape::transform_inverse_transpose)
+      .def("set_transform", &Shape::set_transform)
+      .def("no_shadow", &Shape::no_shadow)
+      .def("has_shadow", &Shape::has_shadow)
+      .def("desc_bytes", [](const Shape& s) { rt_shape_desc d = to_desc(s); return pod_bytes(&d, sizeof d); });
+  m.def("Sphere", &Sphere);
+  m.def("glass_sphere", &glass_sphere);
+  m.def("Plane", &Plane);
+
+  py::class_<Canvas>(m, "Canvas")
+      .def(py::init<size_t, size_t>())
+      .def("width", &Canvas::width)
+      .def("height", &Canvas::height)
+      .def("get_pixel", &Canvas::get_pixel)
+      .def("set_pixel", &Canvas::set_pixel)
+      .def("to_ppm", [](const Canvas& c) { return py::bytes(c.to_ppm()); })
+      .def("to_numpy", [](const Canvas& c) {
+        py::array_t<double> a({(py::ssize_t)c.height(), (py::ssize_t)c.width(), (py::ssize_t)3});
+        std::memcpy(a.mutable_data(), c.data(), c.width() * c.height() * 3 * sizeof(double));
+        return a;
+      });
+  m.def("canvas_to_ppm", [](py::array_t<double, py::array::c_style | py::array::forcecast> rgb) {
+    if (rgb.ndim() != 3 || rgb.shape(2) != 3) throw std::invalid_argument("expected (h, w, 3)");
+    size_t len = 0;
+    const uint32_t h = (uint32_t)rgb.shape(0), w = (uint32_t)rgb.shape(1);
+    check(rt_canvas_to_ppm(rgb.data(), w, h, nullptr, 0, &len), "rt_canvas_to_ppm");
+    std::string s(len, '\0');
+    check(rt_canvas_to_ppm(rgb.data(), w, h, &s[0], len, &len), "rt_canvas_to_ppm");
+    return py::bytes(s);
+  });
+  m.def("quantize_u8", [](py::array_t<double, py::array::c_style | py::array::forcecast> v) {
+    py::array_t<uint8_t> o(v.size());
+    check(rt_quantize_u8(v.data(), (size_t)v.size(), o.mutable_data()), "rt_quantize_u8");
+    return o;
+  });
+  m.def("matrix_inverse_raw", [](const std::vector<double>& mm) {
+    if (mm.size() != 16) throw std::invalid_argument("need 16 values");
+    std::vector<double> out(16);
+    check(rt_matrix_inverse(mm.data(), out.data()), "rt_matrix_inverse");
+    return out;
+  });
+
+  py::class_<World>(m, "World")
+      .def(py::init<>())
+      .def_static("default", &World::make_default)
+      .def("add_object", &World::add_object)
+      .def("add_light", &World::add_light)
+      .def("n_objects", &World::n_objects)
+      .def("n_lights", &World::n_lights)
+      .def("object", &World::object, py::return_value_policy::reference_internal)
+      .def("light", &World::light, py::return_value_policy::reference_internal)
+      .def("upload", [](const World& w, int device) { w.scene(device); }, py::arg("device") = 0)
+      .def("color_at", &World::color_at, py::arg("ray"), py::arg("remaining") = 5)
+      .def("is_shadowed", &World::is_shadowed)
+      .def("descs_bytes", [](const World& w) {
+        auto d = w.descs();
+        return pod_bytes(d.data(), d.size() * sizeof(rt_shape_desc));
+      })
+      .def("lights_bytes", [](const World& w) {
+        auto l = w.light_descs();
+        return pod_bytes(l.data(), l.size() * sizeof(rt_light_desc));
+      })
+      .def("color_at_batch", [](const World& w, py::array_t<double, py::array::c_style | py::array::forcecast> rays,
+                                unsigned remaining) {
+        check_rays(rays, 6);
+        const size_t n = (size_t)rays.shape(0);
+        py::array_t<double> out({(py::ssize_t)n, (py::ssize_t)3});
+        rt_stats st{};
+        {
+          py::gil_scoped_release nogil;
+          check(rt_color_at_batch(w.scene(), rays.data(), n, remaining, out.mutable_data(), &st), "rt_color_at_batch");
+        }
+        return py::make_tuple(out, stats_dict(st));
+      }, py::arg("rays"), py::arg("remaining") = 5)
+      .def("hit_batch", [](const World& w, py::array_t<double, py::array::c_style | py::array::forcecast> rays) {
+        check_rays(rays, 6);
+        const size_t n = (size_t)rays.shape(0);
+        py::array_t<double> out({(py::ssize_t)n, (py::ssize_t)24});
+        check(rt_hit_batch(w.scene(), rays.data(), n, out.mutable_data()), "rt_hit_batch");
+        return out;
+      })
+      .def("is_shadowed_batch", [](const World& w, py::array_t<double, py::array::c_style | py::array::forcecast> pts,
+                                   unsigned light) {
+        check_rays(pts, 3);
+        const size_t n = (size_t)pts.shape(0);
+        py::array_t<uint8_t> out(n);
+        check(rt_is_shadowed_batch(w.scene(), pts.data(), n, light, out.mutable_data()), "rt_is_shadowed_batch");
+        return out;
+      });
+
+  py::class_<Camera>(m, "Camera")
+      .def(py::init<size_t, size_t, double>())
+      .def("set_transform", &Camera::set_transform)
+      .def_property_readonly("hsize", &Camera::hsize)
+      .def_property_readonly("vsize", &Camera::vsize)
+      .def_property_readonly("pixel_size", &Camera::pixel_size)
+      .def_property_readonly("transform", &Camera::transform)
+      .def("ray_for_pixel", &Camera::ray_for_pixel)
+      .def("desc_bytes", [](const Camera& c) { return pod_bytes(&c.desc(), sizeof(rt_camera_desc)); })
+      .def("render", [](const Camera& c, const World& w, unsigned max_depth) {
+        rt_stats st{};
+        Canvas* out;
+        {
+          py::gil_scoped_release nogil;
+          out = new Canvas(c.render(w, max_depth, &st));
+        }
+        return py::make_tuple(std::unique_ptr<Canvas>(out), stats_dict(st));
+      }, py::arg("world"), py::arg("max_depth") = 5)
+      .def("render_shard_device", [](const Camera& c, const World& w, unsigned max_depth, unsigned row_block,
+                                     unsigned shard, unsigned n_shards, uintptr_t d_out, uintptr_t stream,
+                                     bool want_stats) {
+        rt_stats st{};
+        int rc;
+        {
+          py::gil_scoped_release nogil;
+          rc = rt_render_shard_device(w.scene(), &c.desc(), max_depth, row_block, shard, n_shards, (double*)d_out,
+                                      (void*)stream, want_stats ? &st : nullptr);
+        }
+        check(rc, "rt_render_shard_device");
+        return stats_dict(st);
+      }, py::arg("world"), py::arg("max_depth"), py::arg("row_block"), py::arg("shard"), py::arg("n_shards"),
+         py::arg("d_out"), py::arg("stream") = 0, py::arg("want_stats") = false)
+      .def("render_multi", [](const Camera& c, std::vector<World*> worlds, unsigned max_depth, unsigned row_block) {
+        std::vector<rt_scene*> sc;
+        for (size_t i = 0; i < worlds.size(); ++i) sc.push_back(const_cast<rt_scene*>(worlds[i]->scene((int)i)));
+        Canvas* out = new Canvas(c.hsize(), c.vsize());
+        rt_stats st{};
+        int rc;
+        {
+          py::gil_scoped_release nogil;
+          rc = rt_render_multi(sc.data(), (int)sc.size(), &c.desc(), max_depth, row_block, out->data(), &st);
+        }
+        if (rc != RT_OK) { delete out; check(rc, "rt_render_multi"); }
+        return py::make_tuple(std::unique_ptr<Canvas>(out), stats_dict(st));
+      });
+  m.def("shard_rows", &rt_shard_rows);
+}

@@ -1,0 +1,599 @@
+// rt_api.cpp — the C-ABI (include/rt_render.h): scene flattening/validation,
+// device upload, render entry points, multi-GPU gather, PPM output.
+//
+// Product code: no CPU fallback anywhere. Every render entry point runs the
+// HIP kernels in rt_kernels.hip and fails loudly (RT_ERR_HIP / RT_ERR_NO_DEVICE)
+// when no device is usable.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_render.h"
+#include "host/rt_math.hpp"
+#include "rt_kernels.hpp"
+#include "rt_layout.hpp"
+
+using namespace rtamd;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define RT_HIP(call)                                                                   \
+  do {                                                                                 \
+    hipError_t _e = (call);                                                            \
+    if (_e != hipSuccess)                                                              \
+      return fail(RT_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(_e));      \
+  } while (0)
+
+}  // namespace
+
+struct rt_scene {
+  int device = 0;
+  DevScene dev{};
+  // device allocations
+  void* d_blob = nullptr;       // trace + shade + light records
+  unsigned* d_counter = nullptr;
+  DevStats* d_stats = nullptr;
+  double* d_out = nullptr;      // cached output for host-buffer entry points
+  size_t out_cap = 0;           // doubles
+  double* d_in = nullptr;       // cached input for batch entry points
+  size_t in_cap = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::mutex mu;  // one call at a time per scene (shared workspace)
+  int n_objects = 0, n_lights = 0;
+};
+
+namespace {
+
+bool is_diag_inverse(const double* inv) {
+  return inv[1] == 0.0 && inv[2] == 0.0 && inv[4] == 0.0 && inv[6] == 0.0 && inv[8] == 0.0 &&
+         inv[9] == 0.0;
+}
+
+bool m16_eq(const double* a, const double* b) {
+  for (int i = 0; i < 16; ++i)
+    if (!rt::equal(a[i], b[i])) return false;
+  return true;
+}
+bool c3_eq(const double* a, const double* b) {
+  return rt::equal(a[0], b[0]) && rt::equal(a[1], b[1]) && rt::equal(a[2], b[2]);
+}
+
+// Necessary condition for the reference's structural `Shape` equality
+// (derived PartialEq of BaseShape, geometry/mod.rs:12; Material, material.rs:10;
+// Pattern, pattern/mod.rs:17). The bounding box is left out, so this is a
+// SUPERSET of the reference relation: "no pair passes" certifies that the
+// containers walk never sees two structurally-equal objects.
+bool may_be_equal(const rt_shape_desc& a, const rt_shape_desc& b) {
+  if (a.kind != b.kind || (a.casts_shadow != 0) != (b.casts_shadow != 0)) return false;
+  if (!m16_eq(a.transform, b.transform) || !m16_eq(a.inverse, b.inverse)) return false;
+  if (!c3_eq(a.color, b.color)) return false;
+  if (!(a.ambient == b.ambient && a.diffuse == b.diffuse && a.specular == b.specular &&
+        a.shininess == b.shininess && a.reflective == b.reflective &&
+        a.transparency == b.transparency && a.refractive_index == b.refractive_index))
+    return false;
+  if (a.pattern_kind != b.pattern_kind) return false;
+  if (a.pattern_kind != RT_PATTERN_NONE) {
+    if (!m16_eq(a.pattern_transform, b.pattern_transform) ||
+        !m16_eq(a.pattern_inverse, b.pattern_inverse))
+      return false;
+    if (a.pattern_kind != RT_PATTERN_TEST && !(c3_eq(a.pattern_a, b.pattern_a) && c3_eq(a.pattern_b, b.pattern_b)))
+      return false;
+  }
+  return true;
+}
+
+int find_duplicate(const rt_shape_desc* s, size_t n, size_t* ia, size_t* ib) {
+  std::vector<size_t> idx(n);
+  for (size_t i = 0; i < n; ++i) idx[i] = i;
+  // equal shapes have |translation-x difference| < EPSILON: sweep a sorted key
+  std::sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return s[a].transform[3] < s[b].transform[3]; });
+  for (size_t p = 0; p < n; ++p)
+    for (size_t q = p + 1; q < n && s[idx[q]].transform[3] - s[idx[p]].transform[3] < rt::EPSILON; ++q)
+      if (may_be_equal(s[idx[p]], s[idx[q]])) {
+        *ia = std::min(idx[p], idx[q]);
+        *ib = std::max(idx[p], idx[q]);
+        return 1;
+      }
+  return 0;
+}
+
+int ensure_dev_buffer(double** buf, size_t* cap, size_t need) {
+  if (*cap >= need) return RT_OK;
+  if (*buf) (void)hipFree(*buf);
+  *buf = nullptr;
+  *cap = 0;
+  RT_HIP(hipMalloc(buf, std::max<size_t>(need, 1) * sizeof(double)));
+  *cap = need;
+  return RT_OK;
+}
+
+DevCamera to_dev_camera(const rt_camera_desc& c) {
+  DevCamera d{};
+  d.pixel_size = c.pixel_size;
+  d.half_width = c.half_width;
+  d.half_height = c.half_height;
+  for (int i = 0; i < 12; ++i) d.inv[i] = c.inverse[i];
+  d.hsize = c.hsize;
+  d.vsize = c.vsize;
+  return d;
+}
+
+int copy_stats(rt_scene* s, rt_stats* st, float ms_kernel, double ms_total) {
+  DevStats ds{};
+  RT_HIP(hipMemcpyAsync(&ds, s->d_stats, sizeof ds, hipMemcpyDeviceToHost, s->stream));
+  RT_HIP(hipStreamSynchronize(s->stream));
+  st->rays_primary = ds.rays_primary;
+  st->rays_reflect = ds.rays_reflect;
+  st->rays_refract = ds.rays_refract;
+  st->rays_shadow = ds.rays_shadow;
+  st->sphere_tests = ds.sphere_tests;
+  st->plane_tests = ds.plane_tests;
+  st->sphere_disc_ge0 = ds.sphere_disc_ge0;
+  st->ms_kernel = ms_kernel;
+  st->ms_total = ms_total;
+  return RT_OK;
+}
+
+// Launch one render (camera shard or ray batch) on the scene's stream.
+int run_render(rt_scene* s, const DevCamera& cam, const double* d_rays, uint32_t n_tasks,
+               uint32_t max_depth, uint32_t row_block, uint32_t shard, uint32_t n_shards,
+               double* d_out, hipStream_t stream, bool timed) {
+  if (max_depth > (uint32_t)kMaxDepth)
+    return fail(RT_ERR_INVALID_ARGUMENT, "max_depth > " + std::to_string(kMaxDepth));
+  RenderArgs a{};
+  a.out = d_out;
+  a.rays = d_rays;
+  a.counter = s->d_counter;
+  a.stats = s->d_stats;
+  a.n_tasks = n_tasks;
+  a.max_depth = max_depth;
+  a.row_block = row_block;
+  a.shard = shard;
+  a.n_shards = n_shards;
+  a.grid_cap = 0;
+  RT_HIP(hipMemsetAsync(s->d_counter, 0, 64, stream));
+  RT_HIP(hipMemsetAsync(s->d_stats, 0, sizeof(DevStats), stream));
+  if (n_tasks == 0) return RT_OK;
+  if (timed) RT_HIP(hipEventRecord(s->ev0, stream));
+  RT_HIP(launch_render(s->dev, cam, a, stream));
+  if (timed) RT_HIP(hipEventRecord(s->ev1, stream));
+  return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rt_last_error(void) { return g_err.c_str(); }
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+int rt_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int rt_matrix_inverse(const double m[16], double out[16]) {
+  if (!m || !out) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
+  rt::Matrix a = rt::Matrix::from_slice(4, 4, m);
+  if (!a.is_invertible()) return fail(RT_ERR_NOT_INVERTIBLE, "matrix is not invertible (matrix.rs:139)");
+  rt::Matrix inv = a.inverse();
+  std::memcpy(out, inv.data(), 16 * sizeof(double));
+  return RT_OK;
+}
+
+// camera.rs:33-55 (+ set_transform :128-131)
+int rt_camera_init(uint32_t hsize, uint32_t vsize, double field_of_view, const double transform[16],
+                   rt_camera_desc* out) {
+  if (!out || hsize == 0 || vsize == 0) return fail(RT_ERR_INVALID_ARGUMENT, "bad camera size");
+  const double half_view = std::tan(field_of_view / 2.0);
+  const double aspect = (double)hsize / (double)vsize;
+  double half_width, half_height;
+  if (aspect >= 1.0) {
+    half_width = half_view;
+    half_height = half_view / aspect;
+  } else {
+    half_width = half_view * aspect;
+    half_height = half_view;
+  }
+  out->hsize = hsize;
+  out->vsize = vsize;
+  out->pixel_size = half_width * 2.0 / (double)hsize;
+  out->half_width = half_width;
+  out->half_height = half_height;
+  if (transform) {
+    int rc = rt_matrix_inverse(transform, out->inverse);
+    if (rc != RT_OK) return rc;
+  } else {
+    rt::Matrix id = rt::Matrix::identity(4, 4);
+    std::memcpy(out->inverse, id.data(), sizeof out->inverse);
+  }
+  return RT_OK;
+}
+
+int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light_desc* lights,
+                    size_t n_lights, int device, rt_scene** out) {
+  if (!out || (n_shapes && !shapes) || (n_lights && !lights))
+    return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
+  *out = nullptr;
+  if (n_shapes > (size_t)(1u << 29)) return fail(RT_ERR_INVALID_ARGUMENT, "too many shapes");
+  for (size_t i = 0; i < n_shapes; ++i) {
+    if (shapes[i].kind != RT_SHAPE_SPHERE && shapes[i].kind != RT_SHAPE_PLANE)
+      return fail(RT_ERR_UNSUPPORTED_SHAPE, "shape " + std::to_string(i) + ": only Sphere and Plane are supported");
+    if (shapes[i].pattern_kind < RT_PATTERN_NONE || shapes[i].pattern_kind > RT_PATTERN_CHECKERS)
+      return fail(RT_ERR_INVALID_ARGUMENT, "shape " + std::to_string(i) + ": bad pattern kind");
+  }
+  size_t da, db;
+  if (find_duplicate(shapes, n_shapes, &da, &db))
+    return fail(RT_ERR_DUPLICATE_SHAPES, "shapes " + std::to_string(da) + " and " + std::to_string(db) +
+                                             " may be structurally equal (containers walk, intersection.rs:63-90)");
+
+  int ndev = rt_device_count();
+  if (ndev <= 0) return fail(RT_ERR_NO_DEVICE, "no HIP device available (no CPU fallback)");
+  if (device < 0 || device >= ndev) return fail(RT_ERR_INVALID_ARGUMENT, "bad device ordinal");
+
+  // ---- flatten (reference object order preserved through `meta`)
+  std::vector<SphereDiag> diag;
+  std::vector<SphereGen> gen;
+  std::vector<PlaneRec> planes;
+  std::vector<ShadeRec> shade(n_shapes);
+  for (size_t i = 0; i < n_shapes; ++i) {
+    const rt_shape_desc& d = shapes[i];
+    const int64_t meta = ((int64_t)i << 1) | (d.casts_shadow ? 1 : 0);
+    if (d.kind == RT_SHAPE_SPHERE) {
+      if (is_diag_inverse(d.inverse)) {
+        SphereDiag r{};
+        r.s[0] = d.inverse[0]; r.s[1] = d.inverse[5]; r.s[2] = d.inverse[10];
+        r.t[0] = d.inverse[3]; r.t[1] = d.inverse[7]; r.t[2] = d.inverse[11];
+        r.meta = meta;
+        diag.push_back(r);
+      } else {
+        SphereGen r{};
+        for (int e = 0; e < 12; ++e) r.m[e] = d.inverse[e];
+        r.meta = meta;
+        gen.push_back(r);
+      }
+    } else {
+      PlaneRec r{};
+      for (int e = 0; e < 4; ++e) r.m[e] = d.inverse[4 + e];
+      r.meta = meta;
+      planes.push_back(r);
+    }
+    ShadeRec& s = shade[i];
+    std::memset(&s, 0, sizeof s);
+    for (int e = 0; e < 12; ++e) s.inv[e] = d.inverse[e];
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c) s.invT[r * 3 + c] = d.inverse[c * 4 + r];  // transpose (matrix.rs:79-89)
+    for (int c = 0; c < 3; ++c) s.color[c] = d.color[c];
+    s.ambient = d.ambient; s.diffuse = d.diffuse; s.specular = d.specular; s.shininess = d.shininess;
+    s.reflective = d.reflective; s.transparency = d.transparency; s.refractive_index = d.refractive_index;
+    s.pattern_kind = d.pattern_kind;
+    for (int c = 0; c < 3; ++c) { s.pat_a[c] = d.pattern_a[c]; s.pat_b[c] = d.pattern_b[c]; }
+    for (int e = 0; e < 12; ++e) s.pat_inv[e] = d.pattern_inverse[e];
+    s.kind = d.kind;
+    s.shadow = d.casts_shadow ? 1 : 0;
+  }
+  std::vector<LightRec> lrec(n_lights);
+  for (size_t i = 0; i < n_lights; ++i)
+    for (int c = 0; c < 3; ++c) { lrec[i].pos[c] = lights[i].position[c]; lrec[i].intensity[c] = lights[i].intensity[c]; }
+
+  // ---- one blob, 64-B aligned sections
+  auto align = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t o_diag = 0;
+  const size_t o_gen = align(o_diag + diag.size() * sizeof(SphereDiag));
+  const size_t o_pl = align(o_gen + gen.size() * sizeof(SphereGen));
+  const size_t o_sh = align(o_pl + planes.size() * sizeof(PlaneRec));
+  const size_t o_li = align(o_sh + shade.size() * sizeof(ShadeRec));
+  const size_t total = align(o_li + lrec.size() * sizeof(LightRec)) + 256;
+  std::vector<unsigned char> host(total, 0);
+  if (!diag.empty()) std::memcpy(&host[o_diag], diag.data(), diag.size() * sizeof(SphereDiag));
+  if (!gen.empty()) std::memcpy(&host[o_gen], gen.data(), gen.size() * sizeof(SphereGen));
+  if (!planes.empty()) std::memcpy(&host[o_pl], planes.data(), planes.size() * sizeof(PlaneRec));
+  if (!shade.empty()) std::memcpy(&host[o_sh], shade.data(), shade.size() * sizeof(ShadeRec));
+  if (!lrec.empty()) std::memcpy(&host[o_li], lrec.data(), lrec.size() * sizeof(LightRec));
+
+  rt_scene* s = new rt_scene();
+  s->device = device;
+  auto cleanup = [&](int rc) {
+    rt_scene_destroy(s);
+    return rc;
+  };
+  int rc;
+  if ((rc = [&]() -> int {
+         RT_HIP(hipSetDevice(device));
+         RT_HIP(hipMalloc(&s->d_blob, total));
+         RT_HIP(hipMemcpy(s->d_blob, host.data(), total, hipMemcpyHostToDevice));
+         RT_HIP(hipMalloc(&s->d_counter, 256));
+         RT_HIP(hipMalloc(&s->d_stats, sizeof(DevStats)));
+         RT_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+         RT_HIP(hipEventCreate(&s->ev0));
+         RT_HIP(hipEventCreate(&s->ev1));
+         return RT_OK;
+       }()) != RT_OK)
+    return cleanup(rc);
+  unsigned char* b = (unsigned char*)s->d_blob;
+  s->dev.sph_diag = (const SphereDiag*)(b + o_diag);
+  s->dev.sph_gen = (const SphereGen*)(b + o_gen);
+  s->dev.planes = (const PlaneRec*)(b + o_pl);
+  s->dev.shade = (const ShadeRec*)(b + o_sh);
+  s->dev.lights = (const LightRec*)(b + o_li);
+  s->dev.n_diag = (int32_t)diag.size();
+  s->dev.n_gen = (int32_t)gen.size();
+  s->dev.n_planes = (int32_t)planes.size();
+  s->dev.n_objects = (int32_t)n_shapes;
+  s->dev.n_lights = (int32_t)n_lights;
+  s->n_objects = (int)n_shapes;
+  s->n_lights = (int)n_lights;
+  *out = s;
+  return RT_OK;
+}
+
+void rt_scene_destroy(rt_scene* s) {
+  if (!s) return;
+  (void)hipSetDevice(s->device);
+  if (s->stream) (void)hipStreamSynchronize(s->stream);
+  if (s->d_blob) (void)hipFree(s->d_blob);
+  if (s->d_counter) (void)hipFree(s->d_counter);
+  if (s->d_stats) (void)hipFree(s->d_stats);
+  if (s->d_out) (void)hipFree(s->d_out);
+  if (s->d_in) (void)hipFree(s->d_in);
+  if (s->ev0) (void)hipEventDestroy(s->ev0);
+  if (s->ev1) (void)hipEventDestroy(s->ev1);
+  if (s->stream) (void)hipStreamDestroy(s->stream);
+  delete s;
+}
+
+uint32_t rt_shard_rows(uint32_t vsize, uint32_t row_block, uint32_t shard, uint32_t n_shards) {
+  if (row_block == 0 || n_shards == 0 || shard >= n_shards) return 0;
+  uint32_t rows = 0;
+  for (uint32_t blk = shard; (uint64_t)blk * row_block < vsize; blk += n_shards) {
+    uint32_t y0 = blk * row_block;
+    rows += std::min(row_block, vsize - y0);
+  }
+  return rows;
+}
+
+int rt_render_shard_device(const rt_scene* scene, const rt_camera_desc* camera, uint32_t max_depth,
+                           uint32_t row_block, uint32_t shard, uint32_t n_shards, double* d_out_rgb,
+                           void* stream, rt_stats* stats) {
+  if (!scene || !camera || !d_out_rgb) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
+  if (row_block == 0 || n_shards == 0 || shard >= n_shards)
+    return fail(RT_ERR_INVALID_ARGUMENT, "bad shard specification");
+  if (camera->hsize == 0 || camera->vsize == 0) return fail(RT_ERR_INVALID_ARGUMENT, "empty camera");
+  rt_scene* s = const_cast<rt_scene*>(scene);
+  std::lock_guard<std::mutex> lk(s->mu);
+  auto t0 = std::chrono::steady_clock::now();
+  RT_HIP(hipSetDevice(s->device));
+  const uint32_t rows = rt_shard_rows(camera->vsize, row_block, shard, n_shards);
+  const uint64_t n_tasks = (uint64_t)rows * camera->hsize;
+  if (n_tasks >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "shard too large");
+  hipStream_t st = stream ? (hipStream_t)stream : s->stream;
+  int rc = run_render(s, to_dev_camera(*camera), nullptr, (uint32_t)n_tasks, max_depth, row_block, shard,
+                      n_shards, d_out_rgb, st, stats != nullptr);
+  if (rc != RT_OK) return rc;
+  if (stats) {
+    RT_HIP(hipStreamSynchronize(st));
+    float ms = 0.f;
+    if (n_tasks) RT_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+    double tot = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (st != s->stream) RT_HIP(hipStreamSynchronize(st));
+    DevStats ds{};
+    RT_HIP(hipMemcpy(&ds, s->d_stats, sizeof ds, hipMemcpyDeviceToHost));
+    stats->rays_primary = ds.rays_primary; stats->rays_reflect = ds.rays_reflect;
+    stats->rays_refract = ds.rays_refract; stats->rays_shadow = ds.rays_shadow;
+    stats->sphere_tests = ds.sphere_tests; stats->plane_tests = ds.plane_tests;
+    stats->sphere_disc_ge0 = ds.sphere_disc_ge0;
+    stats->ms_kernel = ms;
+    stats->ms_total = tot;
+  }
+  return RT_OK;
+}
+
+int rt_render(const rt_scene* scene, const rt_camera_desc* camera, uint32_t max_depth, double* out_rgb,
+              rt_stats* stats) {
+  if (!scene || !camera || !out_rgb) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
+  if (camera->hsize == 0 || camera->vsize == 0) return fail(RT_ERR_INVALID_ARGUMENT, "empty camera");
+  rt_scene* s = const_cast<rt_scene*>(scene);
+  std::lock_guard<std::mutex> lk(s->mu);
+  auto t0 = std::chrono::steady_clock::now();
+  RT_HIP(hipSetDevice(s->device));
+  const uint64_t n = (uint64_t)camera->hsize * camera->vsize;
+  if (n >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "canvas too large for one launch");
+  int rc = ensure_dev_buffer(&s->d_out, &s->out_cap, n * 3);
+  if (rc != RT_OK) return rc;
+  rc = run_render(s, to_dev_camera(*camera), nullptr, (uint32_t)n, max_depth, camera->vsize, 0, 1, s->d_out,
+                  s->stream, true);
+  if (rc != RT_OK) return rc;
+  RT_HIP(hipMemcpyAsync(out_rgb, s->d_out, n * 3 * sizeof(double), hipMemcpyDeviceToHost, s->stream));
+  RT_HIP(hipStreamSynchronize(s->stream));
+  if (stats) {
+    float ms = 0.f;
+    if (n) RT_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+    double tot = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return copy_stats(s, stats, ms, tot);
+  }
+  return RT_OK;
+}
+
+int rt_color_at_batch(const rt_scene* scene, const double* rays, size_t n, uint32_t remaining,
+                      double* out_rgb, rt_stats* stats) {
+  if (!scene || (n && (!rays || !out_rgb))) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
+  if (n >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "batch too large");
+  rt_scene* s = const_cast<rt_scene*>(scene);
+  std::lock_guard<std::mutex> lk(s->mu);
+  auto t0 = std::chrono::steady_clock::now();
+  RT_HIP(hipSetDevice(s->device));
+  int rc = ensure_dev_buffer(&s->d_in, &s->in_cap, n * 6);
+  if (rc != RT_OK) return rc;
+  rc = ensure_dev_buffer(&s->d_out, &s->out_cap, n * 3);
+  if (rc != RT_OK) return rc;
+  if (n) RT_HIP(hipMemcpyAsync(s->d_in, rays, n * 6 * sizeof(double), hipMemcpyHostToDevice, s->stream));
+  DevCamera cam{};
+  rc = run_render(s, cam, s->d_in, (uint32_t)n, remaining, 1, 0, 1, s->d_out, s->stream, true);
+  if (rc != RT_OK) return rc;
+  if (n) RT_HIP(hipMemcpyAsync(out_rgb, s->d_out, n * 3 * sizeof(double), hipMemcpyDeviceToHost, s->stream));
+  RT_HIP(hipStreamSynchronize(s->stream));
+  if (stats) {
+    float ms = 0.f;
+    if (n) RT_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+    double tot = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return copy_stats(s, stats, ms, tot);
+  }
+  return RT_OK;
+}
+
+int rt_is_shadowed_batch(const rt_scene* scene, const double* points, size_t n, uint32_t light,
+                         uint8_t* out) {
+  if (!scene || (n && (!points || !out))) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
+  rt_scene* s = const_cast<rt_scene*>(scene);
+  if ((int)light >= s->n_lights) return fail(RT_ERR_INVALID_ARGUMENT, "light index out of range");
+  if (n >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "batch too large");
+  std::lock_guard<std::mutex> lk(s->mu);
+  RT_HIP(hipSetDevice(s->device));
+  if (n == 0) return RT_OK;
+  int rc = ensure_dev_buffer(&s->d_in, &s->in_cap, n * 3);
+  if (rc != RT_OK) return rc;
+  rc = ensure_dev_buffer(&s->d_out, &s->out_cap, (n + 7) / 8);
+  if (rc != RT_OK) return rc;
+  RT_HIP(hipMemcpyAsync(s->d_in, points, n * 3 * sizeof(double), hipMemcpyHostToDevice, s->stream));
+  RT_HIP(launch_shadow(s->dev, s->d_in, (int)n, (int)light, (uint8_t*)s->d_out, s->stream));
+  RT_HIP(hipMemcpyAsync(out, s->d_out, n, hipMemcpyDeviceToHost, s->stream));
+  RT_HIP(hipStreamSynchronize(s->stream));
+  return RT_OK;
+}
+
+int rt_hit_batch(const rt_scene* scene, const double* rays, size_t n, double* out24) {
+  if (!scene || (n && (!rays || !out24))) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
+  if (n >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "batch too large");
+  rt_scene* s = const_cast<rt_scene*>(scene);
+  std::lock_guard<std::mutex> lk(s->mu);
+  RT_HIP(hipSetDevice(s->device));
+  if (n == 0) return RT_OK;
+  int rc = ensure_dev_buffer(&s->d_in, &s->in_cap, n * 6);
+  if (rc != RT_OK) return rc;
+  rc = ensure_dev_buffer(&s->d_out, &s->out_cap, n * 24);
+  if (rc != RT_OK) return rc;
+  RT_HIP(hipMemcpyAsync(s->d_in, rays, n * 6 * sizeof(double), hipMemcpyHostToDevice, s->stream));
+  RT_HIP(launch_hit(s->dev, s->d_in, (int)n, s->d_out, s->stream));
+  RT_HIP(hipMemcpyAsync(out24, s->d_out, n * 24 * sizeof(double), hipMemcpyDeviceToHost, s->stream));
+  RT_HIP(hipStreamSynchronize(s->stream));
+  return RT_OK;
+}
+
+// Single-process multi-GPU render: interleaved row blocks, one RCCL gather.
+int rt_render_multi(rt_scene* const* scenes, int n_devices, const rt_camera_desc* camera,
+                    uint32_t max_depth, uint32_t row_block, double* out_rgb, rt_stats* stats) {
+  if (!scenes || n_devices < 1 || !camera || !out_rgb || row_block == 0)
+    return fail(RT_ERR_INVALID_ARGUMENT, "bad arguments");
+  for (int i = 0; i < n_devices; ++i)
+    if (!scenes[i] || scenes[i]->device != i)
+      return fail(RT_ERR_INVALID_ARGUMENT, "scenes[i] must live on device i");
+  auto t0 = std::chrono::steady_clock::now();
+  const uint32_t W = camera->hsize, H = camera->vsize;
+  uint32_t max_rows = 0;
+  for (int i = 0; i < n_devices; ++i) max_rows = std::max(max_rows, rt_shard_rows(H, row_block, i, n_devices));
+  const size_t per = (size_t)max_rows * W * 3;  // padded per-rank element count
+  std::vector<double*> send(n_devices, nullptr);
+  double* recv = nullptr;
+  std::vector<ncclComm_t> comms(n_devices);
+  std::vector<int> devs(n_devices);
+  for (int i = 0; i < n_devices; ++i) devs[i] = i;
+  int rc = RT_OK;
+  bool comm_ok = false;
+  std::vector<rt_stats> st(n_devices);
+  auto body = [&]() -> int {
+    for (int i = 0; i < n_devices; ++i) {
+      RT_HIP(hipSetDevice(i));
+      RT_HIP(hipMalloc(&send[i], std::max<size_t>(per, 1) * sizeof(double)));
+      RT_HIP(hipMemsetAsync(send[i], 0, std::max<size_t>(per, 1) * sizeof(double), scenes[i]->stream));
+    }
+    RT_HIP(hipSetDevice(0));
+    RT_HIP(hipMalloc(&recv, std::max<size_t>(per * n_devices, 1) * sizeof(double)));
+    if (n_devices > 1) {
+      if (ncclCommInitAll(comms.data(), n_devices, devs.data()) != ncclSuccess)
+        return fail(RT_ERR_RCCL, "ncclCommInitAll failed");
+      comm_ok = true;
+    }
+    for (int i = 0; i < n_devices; ++i) {
+      RT_HIP(hipSetDevice(i));
+      std::lock_guard<std::mutex> lk(scenes[i]->mu);
+      const uint32_t rows = rt_shard_rows(H, row_block, i, n_devices);
+      int r = run_render(scenes[i], to_dev_camera(*camera), nullptr, rows * W, max_depth, row_block, i, n_devices,
+                         send[i], scenes[i]->stream, true);
+      if (r != RT_OK) return r;
+    }
+    if (n_devices > 1) {
+      if (ncclGroupStart() != ncclSuccess) return fail(RT_ERR_RCCL, "ncclGroupStart");
+      for (int i = 0; i < n_devices; ++i) {
+        if (ncclGather(send[i], i == 0 ? recv : nullptr, per, ncclDouble, 0, comms[i], scenes[i]->stream) !=
+            ncclSuccess)
+          return fail(RT_ERR_RCCL, "ncclGather");
+      }
+      if (ncclGroupEnd() != ncclSuccess) return fail(RT_ERR_RCCL, "ncclGroupEnd");
+    } else {
+      RT_HIP(hipMemcpyAsync(recv, send[0], per * sizeof(double), hipMemcpyDeviceToDevice, scenes[0]->stream));
+    }
+    for (int i = 0; i < n_devices; ++i) {
+      RT_HIP(hipSetDevice(i));
+      RT_HIP(hipStreamSynchronize(scenes[i]->stream));
+      float ms = 0.f;
+      RT_HIP(hipEventElapsedTime(&ms, scenes[i]->ev0, scenes[i]->ev1));
+      DevStats ds{};
+      RT_HIP(hipMemcpy(&ds, scenes[i]->d_stats, sizeof ds, hipMemcpyDeviceToHost));
+      st[i].rays_primary = ds.rays_primary; st[i].rays_reflect = ds.rays_reflect;
+      st[i].rays_refract = ds.rays_refract; st[i].rays_shadow = ds.rays_shadow;
+      st[i].sphere_tests = ds.sphere_tests; st[i].plane_tests = ds.plane_tests;
+      st[i].sphere_disc_ge0 = ds.sphere_disc_ge0; st[i].ms_kernel = ms;
+    }
+    // un-interleave rank-major rows into the canvas
+    std::vector<double> host(per * n_devices);
+    RT_HIP(hipSetDevice(0));
+    RT_HIP(hipMemcpy(host.data(), recv, host.size() * sizeof(double), hipMemcpyDeviceToHost));
+    for (int i = 0; i < n_devices; ++i) {
+      uint32_t lr = 0;
+      for (uint32_t blk = i; (uint64_t)blk * row_block < H; blk += n_devices)
+        for (uint32_t y = blk * row_block; y < std::min(H, (blk + 1) * row_block); ++y, ++lr)
+          std::memcpy(out_rgb + (size_t)y * W * 3, host.data() + (size_t)i * per + (size_t)lr * W * 3,
+                      (size_t)W * 3 * sizeof(double));
+    }
+    return RT_OK;
+  };
+  rc = body();
+  for (int i = 0; i < n_devices; ++i) {
+    (void)hipSetDevice(i);
+    if (send[i]) (void)hipFree(send[i]);
+    if (comm_ok) ncclCommDestroy(comms[i]);
+  }
+  (void)hipSetDevice(0);
+  if (recv) (void)hipFree(recv);
+  if (rc == RT_OK && stats) {
+    std::memset(stats, 0, sizeof *stats);
+    for (auto& x : st) {
+      stats->rays_primary += x.rays_primary; stats->rays_reflect += x.rays_reflect;
+      stats->rays_refract += x.rays_refract; stats->rays_shadow += x.rays_shadow;
+      stats->sphere_tests += x.sphere_tests; stats->plane_tests += x.plane_tests;
+      stats->sphere_disc_ge0 += x.sphere_disc_ge0;
+      stats->ms_kernel = std::max(stats->ms_kernel, x.ms_kernel);
+    }
+    stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,584 @@
+// rt_kernels.hip — MI355X (gfx950) kernels for the per-pixel render path of
+// tlinford/raytracer-challenge-rs: `Camera::render` (camera.rs:133-148) ->
+// `World::color_at` (world.rs:70-81) -> intersect / hit / prepare_computations /
+// shade_hit / lighting / is_shadowed / reflected_color / refracted_color.
+//
+// Design (DESIGN.md "Kernel"):
+//  * One lane = one pixel's whole recursion tree, evaluated depth-first with an
+//    explicit per-lane stack in scratch. The stack reproduces the reference's
+//    post-order combine exactly: surface (left fold over lights), then
+//    reflected, then refracted, combined as (surface + refl) + refr or with the
+//    Schlick weights (world.rs:40-68). No path-weight re-association.
+//  * Persistent waves: a lane whose tree is finished takes the next pixel from
+//    a global counter (one atomic per wave per refill), so every trace step
+//    runs with (almost) all 64 lanes busy, whatever the tree sizes.
+//  * Every trace step tests every shape (the reference's brute-force
+//    `World::intersect`). Shape records are wave-uniform: they are read with
+//    scalar loads (s_load) from the constant address space and feed the f64
+//    VALU as SGPR operands; no LDS and no per-lane shape loads in the hot loop.
+//  * Nearest hit without the sorted list: min over (t, key) with key =
+//    2*object + root (the stable-sort order of the reference's list).
+//    `containers` (intersection.rs:63-90) is replaced by the exact top-2
+//    formulation over the strictly-negative roots (DESIGN.md "n1/n2").
+//  * All arithmetic is binary64 in the reference's operation order; the file
+//    is compiled with -ffp-contract=off and also pins `fp contract(off)`.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "rt_kernels.hpp"
+
+#pragma clang fp contract(off)
+
+namespace rtamd {
+
+// --------------------------------------------------------------- vector math
+// vector.rs / point.rs / color.rs, left-associative like the Rust expressions.
+struct V3 {
+  double x, y, z;
+};
+__device__ __forceinline__ V3 v3(double x, double y, double z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 vadd(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V3 vsub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V3 vneg(V3 a) { return v3(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ V3 vscale(V3 a, double s) { return v3(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ V3 vmul(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
+// vector.rs:99-101
+__device__ __forceinline__ double vdot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+// vector.rs:21-28 (three divisions, not a reciprocal)
+__device__ __forceinline__ V3 vnormalize(V3 a) {
+  double m = sqrt(a.x * a.x + a.y * a.y + a.z * a.z);
+  return v3(a.x / m, a.y / m, a.z / m);
+}
+// vector.rs:30-32: self - normal * 2.0 * dot(self, normal)
+__device__ __forceinline__ V3 vreflect(V3 v, V3 n) { return vsub(v, vscale(vscale(n, 2.0), vdot(v, n))); }
+// lib.rs:20-22
+__device__ __forceinline__ bool req(double a, double b) { return fabs(a - b) < kEpsilon; }
+// matrix.rs:232-245 (point, rows 0..2 with translation) and :247-260 (vector)
+__device__ __forceinline__ V3 m34_point(const double* m, V3 p) {
+  return v3(m[0] * p.x + m[1] * p.y + m[2] * p.z + m[3],
+            m[4] * p.x + m[5] * p.y + m[6] * p.z + m[7],
+            m[8] * p.x + m[9] * p.y + m[10] * p.z + m[11]);
+}
+__device__ __forceinline__ V3 m33_vector(const double* m, V3 v) {  // m: 3x3 row-major
+  return v3(m[0] * v.x + m[1] * v.y + m[2] * v.z,
+            m[3] * v.x + m[4] * v.y + m[5] * v.z,
+            m[6] * v.x + m[7] * v.y + m[8] * v.z);
+}
+
+// Wave-uniform records through the constant address space -> s_load.
+#define RT_CONST __attribute__((address_space(4)))
+typedef const RT_CONST SphereDiag* cSphereDiag;
+typedef const RT_CONST SphereGen* cSphereGen;
+typedef const RT_CONST PlaneRec* cPlaneRec;
+typedef const RT_CONST LightRec* cLightRec;
+
+// ------------------------------------------------------------ trace (hot loop)
+struct Hit {
+  double t;   // nearest t >= 0 (over eligible objects)
+  int key;    // 2*object + root, -1 = miss
+  // containers candidates (radiance rays): top-2 by (entry t, key) among
+  // spheres with t1 < 0 <= t2 and planes with t < 0.
+  double c1t, c2t;
+  int c1k, c2k;
+};
+
+__device__ __forceinline__ bool better(double t, int k, double bt, int bk) {
+  return t < bt || (t == bt && k < bk);
+}
+__device__ __forceinline__ void push_container(Hit& h, double t, int k) {
+  if (t > h.c1t || (t == h.c1t && k > h.c1k)) {
+    h.c2t = h.c1t; h.c2k = h.c1k; h.c1t = t; h.c1k = k;
+  } else if (t > h.c2t || (t == h.c2t && k > h.c2k)) {
+    h.c2t = t; h.c2k = k;
+  }
+}
+
+// Sphere::local_intersect (sphere.rs:47-62) on the object-space ray.
+// With b = 2*dt and disc = b*b - (4a)*c = 4*(dt*dt - a*c) exactly (power-of-two
+// scaling commutes with rounding), t = (-b -/+ sqrt(disc)) / (2a) equals
+// (-dt -/+ sqrt(dt*dt - a*c)) / a bit for bit (DESIGN.md "Sphere roots").
+__device__ __forceinline__ void sphere_roots(double ox, double oy, double oz, double dx, double dy,
+                                             double dz, int64_t meta, bool shadow_mode, Hit& h,
+                                             unsigned& n_disc) {
+  const double a = dx * dx + dy * dy + dz * dz;
+  const double dt = dx * ox + dy * oy + dz * oz;
+  const double c = ox * ox + oy * oy + oz * oz - 1.0;
+  const double disc = dt * dt - a * c;
+  if (disc >= 0.0) {
+    ++n_disc;
+    const double q = sqrt(disc);
+    const double t1 = (-dt - q) / a;
+    const double t2 = (-dt + q) / a;
+    const int k1 = (int)(meta >> 1) * 2;
+    const bool eligible = !shadow_mode || (meta & 1);
+    if (eligible) {
+      if (t1 >= 0.0) {
+        if (better(t1, k1, h.t, h.key)) { h.t = t1; h.key = k1; }
+      } else if (t2 >= 0.0) {
+        if (better(t2, k1 + 1, h.t, h.key)) { h.t = t2; h.key = k1 + 1; }
+      }
+    }
+    if (t1 < 0.0 && t2 >= 0.0) push_container(h, t1, k1);
+  }
+}
+
+// World::intersect + hit (world.rs:31-38, intersection.rs:118-125): every
+// object, in three wave-uniform record streams.
+__device__ __forceinline__ void trace(const DevScene& sc, V3 o, V3 d, bool shadow_mode, Hit& h,
+                                      unsigned& n_disc) {
+  h.t = INFINITY; h.key = -1;
+  h.c1t = -INFINITY; h.c2t = -INFINITY; h.c1k = -1; h.c2k = -1;
+  h.key = 0x7fffffff;
+  // Shape::intersect (geometry/mod.rs:46-49): Ray::transform by the inverse.
+  cSphereDiag sd = (cSphereDiag)sc.sph_diag;
+  for (int j = 0; j < sc.n_diag; ++j) {
+    const double s0 = sd[j].s[0], s1 = sd[j].s[1], s2 = sd[j].s[2];
+    const double t0 = sd[j].t[0], t1 = sd[j].t[1], t2 = sd[j].t[2];
+    const int64_t meta = sd[j].meta;
+    // off-diagonal entries are exact zeros: ((m00*x + 0) + 0) + m03 == m00*x + m03
+    sphere_roots(s0 * o.x + t0, s1 * o.y + t1, s2 * o.z + t2, s0 * d.x, s1 * d.y, s2 * d.z, meta,
+                 shadow_mode, h, n_disc);
+  }
+  cSphereGen sg = (cSphereGen)sc.sph_gen;
+  for (int j = 0; j < sc.n_gen; ++j) {
+    double m[12];
+#pragma unroll
+    for (int e = 0; e < 12; ++e) m[e] = sg[j].m[e];
+    const V3 lo = m34_point(m, o);
+    const V3 ld = v3(m[0] * d.x + m[1] * d.y + m[2] * d.z, m[4] * d.x + m[5] * d.y + m[6] * d.z,
+                     m[8] * d.x + m[9] * d.y + m[10] * d.z);
+    sphere_roots(lo.x, lo.y, lo.z, ld.x, ld.y, ld.z, sg[j].meta, shadow_mode, h, n_disc);
+  }
+  // Plane::local_intersect (plane.rs:53-60): only object-space y matters.
+  cPlaneRec pl = (cPlaneRec)sc.planes;
+  for (int j = 0; j < sc.n_planes; ++j) {
+    const double m0 = pl[j].m[0], m1 = pl[j].m[1], m2 = pl[j].m[2], m3 = pl[j].m[3];
+    const int64_t meta = pl[j].meta;
+    const double oy = m0 * o.x + m1 * o.y + m2 * o.z + m3;
+    const double dy = m0 * d.x + m1 * d.y + m2 * d.z;
+    if (!(fabs(dy) < kEpsilon)) {
+      const double t = -oy / dy;
+      const int k = (int)(meta >> 1) * 2;
+      const bool eligible = !shadow_mode || (meta & 1);
+      if (eligible && t >= 0.0 && better(t, k, h.t, h.key)) { h.t = t; h.key = k; }
+      if (t < 0.0) push_container(h, t, k);
+    }
+  }
+  if (h.key == 0x7fffffff) h.key = -1;
+}
+
+// --------------------------------------------------------------- shading
+struct Comps {
+  V3 point, over, under, eyev, normal;
+  double n1, n2;
+  int obj;
+  bool inside;
+};
+
+// Intersection::prepare_computations (intersection.rs:53-105) with the exact
+// top-2 replacement of the containers walk.
+__device__ __forceinline__ Comps prepare(const DevScene& sc, V3 o, V3 d, const Hit& h) {
+  Comps c;
+  const int obj = h.key >> 1;
+  const ShadeRec& s = sc.shade[obj];
+  c.obj = obj;
+  c.point = vadd(o, vscale(d, h.t));  // ray.rs:22-24
+  c.eyev = vneg(d);
+  // Shape::normal_at (geometry/mod.rs:51-56)
+  const V3 lp = m34_point(s.inv, c.point);
+  const V3 ln = s.kind == 0 ? vsub(lp, v3(0.0, 0.0, 0.0)) : v3(0.0, 1.0, 0.0);
+  V3 n = vnormalize(m33_vector(s.invT, ln));
+  c.inside = false;
+  if (vdot(n, c.eyev) < 0.0) { c.inside = true; n = vneg(n); }
+  c.normal = n;
+  // n1 / n2 (intersection.rs:63-90, DESIGN.md "n1/n2")
+  const bool hit_is_container = (h.key & 1) != 0;  // exit root of a sphere whose t1 < 0
+  c.n1 = h.c1k >= 0 ? sc.shade[h.c1k >> 1].refractive_index : 1.0;
+  if (!hit_is_container) {
+    c.n2 = s.refractive_index;
+  } else if ((h.c1k >> 1) == obj) {
+    c.n2 = h.c2k >= 0 ? sc.shade[h.c2k >> 1].refractive_index : 1.0;
+  } else {
+    c.n2 = sc.shade[h.c1k >> 1].refractive_index;
+  }
+  c.over = vadd(c.point, vscale(n, kEpsilon));
+  c.under = vsub(c.point, vscale(n, kEpsilon));
+  return c;
+}
+
+// Computations::schlick (intersection.rs:147-162); powi(2) = q*q,
+// powi(5) = x*((x*x)*(x*x)) (LLVM powi expansion / __powidf2).
+__device__ __forceinline__ double schlick(V3 eyev, V3 normal, double n1, double n2) {
+  double cosv = vdot(eyev, normal);
+  if (n1 > n2) {
+    const double nn = n1 / n2;
+    const double sin2_t = nn * nn * (1.0 - cosv * cosv);
+    if (sin2_t > 1.0) return 1.0;
+    cosv = sqrt(1.0 - sin2_t);
+  }
+  const double q = (n1 - n2) / (n1 + n2);
+  const double r0 = q * q;
+  const double x = 1.0 - cosv;
+  const double x5 = x * ((x * x) * (x * x));
+  return r0 + (1.0 - r0) * x5;
+}
+
+// Pattern::color_at_shape (pattern/mod.rs:39-49) and the five kinds.
+__device__ __forceinline__ V3 pattern_color(const ShadeRec& s, V3 world_point) {
+  const V3 op = m34_point(s.inv, world_point);
+  const V3 pp = m34_point(s.pat_inv, op);
+  const V3 a = v3(s.pat_a[0], s.pat_a[1], s.pat_a[2]);
+  const V3 b = v3(s.pat_b[0], s.pat_b[1], s.pat_b[2]);
+  switch (s.pattern_kind) {
+    case 0:  // test_pattern.rs:7-9
+      return pp;
+    case 1:  // stripe.rs:14-20
+      return fmod(floor(pp.x), 2.0) == 0.0 ? a : b;
+    case 2: {  // gradient.rs:14-18
+      const V3 distance = vsub(b, a);
+      const double fraction = pp.x - floor(pp.x);
+      return vadd(a, vscale(distance, fraction));
+    }
+    case 3: {  // ring.rs:14-21
+      const double distance = floor(sqrt(pp.x * pp.x + pp.z * pp.z));
+      return fmod(distance, 2.0) == 0.0 ? a : b;
+    }
+    default: {  // checkers.rs:14-21: `as isize` (saturating) then % 2
+      const double distance = floor(pp.x) + floor(pp.y) + floor(pp.z);
+      bool even;
+      if (isnan(distance)) even = true;                          // NaN as isize = 0
+      else if (distance >= 9223372036854775808.0) even = false;  // isize::MAX is odd
+      else if (distance < -9223372036854775808.0) even = true;   // isize::MIN is even
+      else even = fmod(distance, 2.0) == 0.0;                   // exact integer parity
+      return even ? a : b;
+    }
+  }
+}
+
+// Material::lighting (material.rs:38-82)
+__device__ __forceinline__ V3 lighting(const ShadeRec& m, cLightRec L, V3 point, V3 eyev, V3 normal,
+                                       bool in_shadow) {
+  const V3 color = m.pattern_kind >= 0 ? pattern_color(m, point)
+                                       : v3(m.color[0], m.color[1], m.color[2]);
+  const V3 intensity = v3(L->intensity[0], L->intensity[1], L->intensity[2]);
+  const V3 effective_color = vmul(color, intensity);
+  const V3 lightv = vnormalize(vsub(v3(L->pos[0], L->pos[1], L->pos[2]), point));
+  const V3 ambient = vscale(effective_color, m.ambient);
+  if (in_shadow) return ambient;
+  const double light_dot_normal = vdot(lightv, normal);
+  V3 diffuse = v3(0.0, 0.0, 0.0), specular = v3(0.0, 0.0, 0.0);
+  if (!(light_dot_normal < 0.0)) {
+    diffuse = vscale(vscale(effective_color, m.diffuse), light_dot_normal);
+    const V3 reflectv = vreflect(vneg(lightv), normal);
+    const double reflect_dot_eye = vdot(reflectv, eyev);
+    if (!(reflect_dot_eye <= 0.0)) {
+      const double factor = pow(reflect_dot_eye, m.shininess);
+      specular = vscale(vscale(intensity, m.specular), factor);
+    }
+  }
+  return vadd(vadd(ambient, diffuse), specular);
+}
+
+// --------------------------------------------------------------- the stack
+struct Frame {
+  V3 over, under, eyev, normal;
+  V3 surf;  // running sum over lights (world.rs:41-56)
+  V3 refl;  // reflected_color(...) already multiplied by `reflective`
+  double n1, n2;
+  int obj, light, phase, pad;
+};
+enum : int { PH_AWAIT_REFL = 1, PH_AWAIT_REFR = 2 };
+enum : int { OP_NEXT_LIGHT = 0, OP_REFLECT = 1, OP_REFRACT = 2, OP_FINISH = 3, OP_RETURN = 4 };
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// camera.rs:57-69
+__device__ __forceinline__ void ray_for_pixel(const DevCamera& cam, uint32_t px, uint32_t py, V3& o,
+                                              V3& d) {
+  const double xoffset = ((double)px + 0.5) * cam.pixel_size;
+  const double yoffset = ((double)py + 0.5) * cam.pixel_size;
+  const double world_x = cam.half_width - xoffset;
+  const double world_y = cam.half_height - yoffset;
+  const V3 pixel = m34_point(cam.inv, v3(world_x, world_y, -1.0));
+  o = m34_point(cam.inv, v3(0.0, 0.0, 0.0));
+  d = vnormalize(vsub(pixel, o));
+}
+
+template <int MAXF, bool FROM_RAYS>
+__global__ __launch_bounds__(256) void render_kernel(DevScene sc, DevCamera cam, RenderArgs args) {
+  Frame stk[MAXF];
+  const int lane = threadIdx.x & 63;
+  int task = -1;  // pixel (render) or ray (batch) index, -1 = idle
+  int depth = 0;
+  V3 ro = v3(0, 0, 0), rd = v3(0, 0, 0);
+  bool shadow_mode = false;
+  double sdist = 0.0;
+  unsigned long long n_prim = 0, n_refl = 0, n_refr = 0, n_shadow = 0, n_traces = 0;
+  unsigned n_disc = 0;
+  bool no_more = false;
+  cLightRec lights = (cLightRec)sc.lights;
+
+  while (true) {
+    // ---- refill idle lanes: one atomic per wave (wave-uniform control flow)
+    if (!no_more) {
+      const unsigned long long want = __ballot(task < 0);
+      if (want) {
+        const unsigned cnt = (unsigned)__popcll(want);
+        unsigned base = 0;
+        if (lane == 0) base = atomicAdd(args.counter, cnt);
+        base = __shfl(base, 0, 64);
+        if (task < 0) {
+          const unsigned rank = (unsigned)__popcll(want & ((1ull << lane) - 1ull));
+          const unsigned my = base + rank;
+          if (my < args.n_tasks) {
+            task = (int)my;
+            depth = 0;
+            shadow_mode = false;
+            ++n_prim;
+            if constexpr (FROM_RAYS) {
+              const double* r = args.rays + (size_t)my * 6;
+              ro = v3(r[0], r[1], r[2]);
+              rd = v3(r[3], r[4], r[5]);
+            } else {
+              // shard row mapping: local row lr -> global row y
+              const uint32_t lr = my / cam.hsize, x = my - lr * cam.hsize;
+              const uint32_t blk = lr / args.row_block, off = lr - blk * args.row_block;
+              const uint32_t y = (blk * args.n_shards + args.shard) * args.row_block + off;
+              ray_for_pixel(cam, x, y, ro, rd);
+            }
+          }
+        }
+        if (base + cnt >= args.n_tasks) no_more = true;
+      }
+    }
+    if (__ballot(task >= 0) == 0ull) break;
+    if (task < 0) continue;
+
+    // ---- one trace per active lane (all lanes walk the same shape stream)
+    Hit h;
+    trace(sc, ro, rd, shadow_mode, h, n_disc);
+    ++n_traces;
+
+    // ---- advance this lane's recursion until it needs the next trace
+    int op;
+    V3 ret = v3(0.0, 0.0, 0.0);
+    V3 refr = v3(0.0, 0.0, 0.0);
+    if (shadow_mode) {
+      // World::is_shadowed (world.rs:95-105): first shadow-casting t >= 0 < distance
+      Frame& f = stk[depth];
+      const bool shadowed = h.key >= 0 && h.t < sdist;
+      const ShadeRec& m = sc.shade[f.obj];
+      const V3 c = lighting(m, lights + f.light, f.over, f.eyev, f.normal, shadowed);
+      f.surf = vadd(f.surf, c);
+      f.light += 1;
+      op = OP_NEXT_LIGHT;
+    } else if (h.key < 0) {
+      ret = v3(0.0, 0.0, 0.0);  // miss -> Color::black() (world.rs:74-75)
+      op = OP_RETURN;
+    } else {
+      const Comps c = prepare(sc, ro, rd, h);
+      Frame& f = stk[depth];
+      f.over = c.over; f.under = c.under; f.eyev = c.eyev; f.normal = c.normal;
+      f.n1 = c.n1; f.n2 = c.n2; f.obj = c.obj;
+      f.surf = v3(0.0, 0.0, 0.0);  // Sum starts from (0,0,0) (color.rs:96-103)
+      f.light = 0;
+      op = OP_NEXT_LIGHT;
+    }
+    bool need_trace = false;
+    while (!need_trace && task >= 0) {
+      Frame& f = stk[depth];
+      if (op == OP_NEXT_LIGHT) {
+        if (f.light < sc.n_lights) {
+          cLightRec L = lights + f.light;
+          const V3 v = vsub(v3(L->pos[0], L->pos[1], L->pos[2]), f.over);
+          sdist = sqrt(v.x * v.x + v.y * v.y + v.z * v.z);  // magnitude
+          rd = vnormalize(v);
+          ro = f.over;
+          shadow_mode = true;
+          ++n_shadow;
+          need_trace = true;
+        } else {
+          op = OP_REFLECT;
+        }
+      } else if (op == OP_REFLECT) {
+        // World::reflected_color (world.rs:107-114)
+        const ShadeRec& m = sc.shade[f.obj];
+        const uint32_t remaining = args.max_depth - (uint32_t)depth;
+        if (req(m.reflective, 0.0) || remaining == 0) {
+          f.refl = v3(0.0, 0.0, 0.0);
+          op = OP_REFRACT;
+        } else {
+          f.phase = PH_AWAIT_REFL;
+          const V3 d = vneg(f.eyev);  // the incoming direction, exactly
+          ro = f.over;
+          rd = vreflect(d, f.normal);  // comps.reflectv (intersection.rs:101)
+          shadow_mode = false;
+          ++depth;
+          ++n_refl;
+          need_trace = true;
+        }
+      } else if (op == OP_REFRACT) {
+        // World::refracted_color (world.rs:116-134)
+        const ShadeRec& m = sc.shade[f.obj];
+        const uint32_t remaining = args.max_depth - (uint32_t)depth;
+        refr = v3(0.0, 0.0, 0.0);
+        op = OP_FINISH;
+        if (!(req(m.transparency, 0.0) || remaining == 0)) {
+          const double n_ratio = f.n1 / f.n2;
+          const double cos_i = vdot(f.eyev, f.normal);
+          const double sin2_t = n_ratio * n_ratio * (1.0 - cos_i * cos_i);
+          if (!(sin2_t > 1.0)) {
+            const double cos_t = sqrt(1.0 - sin2_t);
+            rd = vsub(vscale(f.normal, n_ratio * cos_i - cos_t), vscale(f.eyev, n_ratio));
+            ro = f.under;
+            f.phase = PH_AWAIT_REFR;
+            shadow_mode = false;
+            ++depth;
+            ++n_refr;
+            need_trace = true;
+          }
+        }
+      } else if (op == OP_FINISH) {
+        // world.rs:61-67
+        const ShadeRec& m = sc.shade[f.obj];
+        if (m.reflective > 0.0 && m.transparency > 0.0) {
+          const double r = schlick(f.eyev, f.normal, f.n1, f.n2);
+          ret = vadd(vadd(f.surf, vscale(f.refl, r)), vscale(refr, 1.0 - r));
+        } else {
+          ret = vadd(vadd(f.surf, f.refl), refr);
+        }
+        op = OP_RETURN;
+      } else {  // OP_RETURN: hand `ret` to the parent frame
+        if (depth == 0) {
+          double* out = args.out + (size_t)task * 3;
+          out[0] = ret.x; out[1] = ret.y; out[2] = ret.z;
+          task = -1;
+        } else {
+          --depth;
+          Frame& p = stk[depth];
+          const ShadeRec& m = sc.shade[p.obj];
+          if (p.phase == PH_AWAIT_REFL) {
+            p.refl = vscale(ret, m.reflective);  // world.rs:113
+            op = OP_REFRACT;
+          } else {
+            refr = vscale(ret, m.transparency);  // world.rs:133
+            op = OP_FINISH;
+          }
+        }
+      }
+    }
+  }
+
+  // ---- counters: one atomic per wave per field
+  const unsigned long long s_prim = wave_sum(n_prim), s_refl = wave_sum(n_refl);
+  const unsigned long long s_refr = wave_sum(n_refr), s_shadow = wave_sum(n_shadow);
+  const unsigned long long s_tr = wave_sum(n_traces), s_disc = wave_sum(n_disc);
+  if (lane == 0 && args.stats) {
+    atomicAdd(&args.stats->rays_primary, s_prim);
+    atomicAdd(&args.stats->rays_reflect, s_refl);
+    atomicAdd(&args.stats->rays_refract, s_refr);
+    atomicAdd(&args.stats->rays_shadow, s_shadow);
+    atomicAdd(&args.stats->sphere_tests, s_tr * (unsigned long long)(sc.n_diag + sc.n_gen));
+    atomicAdd(&args.stats->plane_tests, s_tr * (unsigned long long)sc.n_planes);
+    atomicAdd(&args.stats->sphere_disc_ge0, s_disc);
+  }
+}
+
+// rt_hit_batch: World::intersect + hit + prepare_computations + schlick per ray.
+__global__ __launch_bounds__(256) void hit_kernel(DevScene sc, const double* rays, int n, double* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const V3 o = v3(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]);
+  const V3 d = v3(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
+  Hit h;
+  unsigned nd = 0;
+  trace(sc, o, d, false, h, nd);
+  double* r = out + (size_t)i * 24;
+  for (int k = 0; k < 24; ++k) r[k] = 0.0;
+  r[0] = -1.0;
+  if (h.key < 0) return;
+  const Comps c = prepare(sc, o, d, h);
+  r[0] = c.obj; r[1] = h.t;
+  r[2] = c.point.x; r[3] = c.point.y; r[4] = c.point.z;
+  r[5] = c.over.x; r[6] = c.over.y; r[7] = c.over.z;
+  r[8] = c.under.x; r[9] = c.under.y; r[10] = c.under.z;
+  r[11] = c.eyev.x; r[12] = c.eyev.y; r[13] = c.eyev.z;
+  r[14] = c.normal.x; r[15] = c.normal.y; r[16] = c.normal.z;
+  r[17] = c.inside ? 1.0 : 0.0;
+  const V3 rv = vreflect(d, c.normal);
+  r[18] = rv.x; r[19] = rv.y; r[20] = rv.z;
+  r[21] = c.n1; r[22] = c.n2;
+  r[23] = schlick(c.eyev, c.normal, c.n1, c.n2);
+}
+
+// rt_is_shadowed_batch: World::is_shadowed for each point against one light.
+__global__ __launch_bounds__(256) void shadow_kernel(DevScene sc, const double* pts, int n, int light,
+                                                     uint8_t* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const V3 p = v3(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]);
+  const LightRec L = sc.lights[light];
+  const V3 v = vsub(v3(L.pos[0], L.pos[1], L.pos[2]), p);
+  const double distance = sqrt(v.x * v.x + v.y * v.y + v.z * v.z);
+  const V3 d = vnormalize(v);
+  Hit h;
+  unsigned nd = 0;
+  trace(sc, p, d, true, h, nd);
+  out[i] = (h.key >= 0 && h.t < distance) ? 1 : 0;
+}
+
+// ------------------------------------------------------------ host launchers
+template <int MAXF, bool FROM_RAYS>
+static hipError_t launch_render_t(const DevScene& sc, const DevCamera& cam, const RenderArgs& args,
+                                  hipStream_t stream) {
+  auto kern = render_kernel<MAXF, FROM_RAYS>;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  int n_cu = 0;
+  e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e != hipSuccess) return e;
+  int per_cu = 0;
+  e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0);
+  if (e != hipSuccess || per_cu < 1) per_cu = 1;
+  long long want = ((long long)args.n_tasks + 255) / 256;
+  long long cap = (long long)n_cu * per_cu;
+  if (args.grid_cap > 0 && args.grid_cap < cap) cap = args.grid_cap;
+  long long grid = want < cap ? want : cap;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), 0, stream, sc, cam, args);
+  return hipGetLastError();
+}
+
+template <bool FROM_RAYS>
+static hipError_t launch_render_depth(const DevScene& sc, const DevCamera& cam, const RenderArgs& a,
+                                      hipStream_t s) {
+  if (a.max_depth <= 5) return launch_render_t<6, FROM_RAYS>(sc, cam, a, s);
+  if (a.max_depth <= 8) return launch_render_t<9, FROM_RAYS>(sc, cam, a, s);
+  if (a.max_depth <= 16) return launch_render_t<17, FROM_RAYS>(sc, cam, a, s);
+  return launch_render_t<kMaxDepth + 1, FROM_RAYS>(sc, cam, a, s);
+}
+
+hipError_t launch_render(const DevScene& sc, const DevCamera& cam, const RenderArgs& args,
+                         hipStream_t stream) {
+  if (args.rays) return launch_render_depth<true>(sc, cam, args, stream);
+  return launch_render_depth<false>(sc, cam, args, stream);
+}
+
+hipError_t launch_hit(const DevScene& sc, const double* d_rays, int n, double* d_out, hipStream_t s) {
+  hipLaunchKernelGGL(hit_kernel, dim3((n + 255) / 256), dim3(256), 0, s, sc, d_rays, n, d_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_shadow(const DevScene& sc, const double* d_pts, int n, int light, uint8_t* d_out,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(shadow_kernel, dim3((n + 255) / 256), dim3(256), 0, s, sc, d_pts, n, light, d_out);
+  return hipGetLastError();
+}
+
+}  // namespace rtamd

@@ -1,0 +1,80 @@
+// rt_layout.hpp — device-resident layout of a flattened `World` (world.rs:18-21)
+// shared by the host uploader (rt_scene.cpp) and the HIP kernels.
+//
+// HBM layout (all 64-B aligned, all read-only during a render):
+//   trace records  : the per-ray hot loop reads EVERY record of its class once
+//                    per ray, wave-uniformly (s_load -> SGPR operands):
+//       SphereDiag  8 doubles  (64 B)  inverse = diag(s) + translation t
+//       SphereGen  16 doubles (128 B)  inverse rows 0-2 (general affine)
+//       PlaneRec    8 doubles  (64 B)  inverse row 1 (only y matters)
+//     each carries `meta` = (object index << 1) | casts_shadow as a double slot.
+//   shade records  : ShadeRec per object index (AoS, 64 doubles = 512 B),
+//                    gathered per lane only at a hit.
+//   lights         : 6 doubles each (position, intensity), wave-uniform.
+#pragma once
+#include <stdint.h>
+
+namespace rtamd {
+
+constexpr double kEpsilon = 0.00001;  // raytracer/src/lib.rs:18
+
+struct alignas(64) SphereDiag {  // translation . axis scaling (e.g. all C3/C5 spheres)
+  double s[3];                   // inverse diagonal m00, m11, m22
+  double t[3];                   // inverse translation m03, m13, m23
+  int64_t meta;
+  int64_t pad;
+};
+struct alignas(64) SphereGen {  // any invertible affine transform
+  double m[12];                 // inverse rows 0..2
+  int64_t meta;
+  int64_t pad[3];
+};
+struct alignas(64) PlaneRec {
+  double m[4];  // inverse row 1: m10 m11 m12 m13
+  int64_t meta;
+  int64_t pad[3];
+};
+
+struct alignas(64) ShadeRec {
+  double inv[12];   // transform_inverse rows 0..2
+  double invT[9];   // transform_inverse_transpose upper 3x3 (= inv^T)
+  double color[3];
+  double ambient, diffuse, specular, shininess;
+  double reflective, transparency, refractive_index;
+  double pat_a[3], pat_b[3];
+  double pat_inv[12];
+  int32_t kind, pattern_kind, shadow, pad0;
+  double pad1[6];
+};
+static_assert(sizeof(ShadeRec) == 512, "ShadeRec must stay 512 B");
+
+struct LightRec {
+  double pos[3];
+  double intensity[3];
+};
+
+// Kernel-argument view of a scene (passed by value; pointers live in SGPRs).
+struct DevScene {
+  const SphereDiag* sph_diag;
+  const SphereGen* sph_gen;
+  const PlaneRec* planes;
+  const ShadeRec* shade;
+  const LightRec* lights;
+  int32_t n_diag, n_gen, n_planes, n_objects, n_lights;
+  int32_t pad;
+};
+
+struct DevCamera {
+  double pixel_size, half_width, half_height;
+  double inv[12];
+  uint32_t hsize, vsize;
+};
+
+// Counters accumulated by the kernels (order = rt_stats prefix).
+struct DevStats {
+  unsigned long long rays_primary, rays_reflect, rays_refract, rays_shadow;
+  unsigned long long sphere_tests, plane_tests, sphere_disc_ge0;
+  unsigned long long pad;
+};
+
+}  // namespace rtamd

@@ -1,0 +1,28 @@
+"""rtamd — MI355X-native drop-in for raytracer-challenge-rs's render path.
+
+`Camera.render(world)` (reference camera.rs:133-148) renders on the GPU through
+the C-ABI in include/rt_render.h (librtamd.so, HIP kernels for gfx950). The
+scene-building API mirrors the reference's Rust API (world.rs, camera.rs,
+geometry/, material.rs, pattern/, transform.rs, matrix.rs).
+
+Importing this package loads the native extension; it raises if the extension
+has not been built (run `make -C raytracer-challenge-rs_amd` or
+`python -c "import __graft_entry__ as g; g.build()"`). There is no CPU
+fallback: rendering without a GPU raises RtError (RT_ERR_NO_DEVICE).
+"""
+import os as _os
+
+_here = _os.path.dirname(_os.path.abspath(__file__))
+try:
+    from . import _rtamd  # noqa: F401
+except ImportError as e:  # pragma: no cover - exercised when the build is missing
+    raise ImportError(
+        "rtamd native extension not built (expected rtamd/_rtamd*.so and lib/librtamd.so "
+        f"under {_os.path.dirname(_here)}): {e}"
+    ) from e
+
+from ._rtamd import *  # noqa: F401,F403,E402
+from ._rtamd import RtError, EPSILON  # noqa: E402
+
+LIB_PATH = _os.path.join(_os.path.dirname(_here), "lib", "librtamd.so")
+MAX_RECURSION_DEPTH = 5  # reference world.rs:16

@@ -1,0 +1,233 @@
+"""Scene recipes for the benchmark configurations.
+
+Built only through the public host API (the same calls the reference's demo
+binaries make: Sphere()/Plane(), set_transform, material fields, add_object,
+add_light, view_transform). Random scenes use splitmix64 so that any language
+can regenerate them bit-for-bit.
+
+  C1  200x100, one sphere, one light (bin/sphere_with_light.rs:34-40)
+  C2  800x600, 3 spheres on a plane, Phong only, depth 1 (bin/first_scene.rs)
+  C3  1920x1080, floor + 1000 random spheres, depth 5   <- headline workload
+  C5  4096x4096, 4 planes + 9996 spheres, 2 lights, depth 8
+  zoo a feature scene: patterns of every kind, rotated/sheared transforms,
+      nested glass, a shadowless object, two lights (parity coverage)
+"""
+import math
+
+from . import _rtamd as rt
+
+PI = math.pi
+MASK64 = (1 << 64) - 1
+
+
+class SplitMix64:
+    """splitmix64; u() = (z >> 11) * 2**-53 in [0, 1)."""
+
+    def __init__(self, seed):
+        self.state = seed & MASK64
+
+    def next_u64(self):
+        self.state = (self.state + 0x9E3779B97F4A7C15) & MASK64
+        z = self.state
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & MASK64
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & MASK64
+        return z ^ (z >> 31)
+
+    def u(self):
+        return (self.next_u64() >> 11) * (1.0 / 9007199254740992.0)
+
+
+def _camera(w, h, fov, frm, to, up=(0, 1, 0)):
+    c = rt.Camera(w, h, fov)
+    c.set_transform(rt.view_transform(rt.Point(*frm), rt.Point(*to), rt.Vector(*up)))
+    return c
+
+
+def c1(width=200, height=100):
+    """C1: Sphere::default() coloured (1, 0.2, 1), light (-10,10,-10)."""
+    w = rt.World()
+    s = rt.Sphere()
+    s.material.color = rt.Color(1.0, 0.2, 1.0)
+    w.add_object(s)
+    w.add_light(rt.PointLight(rt.Point(-10, 10, -10), rt.Color(1.0, 1.0, 1.0)))
+    return w, _camera(width, height, PI / 3.0, (0, 0, -5), (0, 0, 0)), 5
+
+
+def c2(width=800, height=600):
+    """C2: floor + middle/right/left spheres, Phong only; color_at(ray, 1)."""
+    w = rt.World()
+    floor = rt.Plane()
+    floor.material.color = rt.Color(1.0, 0.9, 0.9)
+    floor.material.specular = 0.0
+    w.add_object(floor)
+    middle = rt.Sphere()
+    middle.set_transform(rt.translation(-0.5, 1.0, 0.5))
+    middle.material.color = rt.Color(0.1, 1.0, 0.5)
+    middle.material.diffuse = 0.7
+    middle.material.specular = 0.3
+    w.add_object(middle)
+    right = rt.Sphere()
+    right.set_transform(rt.translation(1.5, 0.5, -0.5) * rt.scaling(0.5, 0.5, 0.5))
+    right.material.color = rt.Color(0.5, 1.0, 0.1)
+    right.material.diffuse = 0.7
+    right.material.specular = 0.3
+    w.add_object(right)
+    left = rt.Sphere()
+    left.set_transform(rt.translation(-1.5, 0.33, -0.75) * rt.scaling(0.33, 0.33, 0.33))
+    left.material.color = rt.Color(1.0, 0.8, 0.1)
+    left.material.diffuse = 0.7
+    left.material.specular = 0.3
+    w.add_object(left)
+    w.add_light(rt.PointLight(rt.Point(-10, 10, -10), rt.Color(1.0, 1.0, 1.0)))
+    return w, _camera(width, height, PI / 3.0, (0, 1.5, -5), (0, 1, 0)), 1
+
+
+def _random_sphere(rng, box_lo, box_hi):
+    """One C3/C5 sphere: r, centre, then a material class draw."""
+    r = 0.15 + 0.35 * rng.u()
+    cx = box_lo[0] + (box_hi[0] - box_lo[0]) * rng.u()
+    cy = r + (box_hi[1] - box_lo[1]) * rng.u()
+    cz = box_lo[2] + (box_hi[2] - box_lo[2]) * rng.u()
+    s = rt.Sphere()
+    s.set_transform(rt.translation(cx, cy, cz) * rt.scaling(r, r, r))
+    m = s.material
+    k = rng.u()
+    if k < 0.5:  # diffuse
+        m.color = rt.Color(0.1 + 0.9 * rng.u(), 0.1 + 0.9 * rng.u(), 0.1 + 0.9 * rng.u())
+        m.ambient = 0.1
+        m.diffuse = 0.9
+        m.specular = 0.3
+        m.shininess = 50.0
+    elif k < 0.8:  # mirror
+        m.reflective = 0.5 + 0.4 * rng.u()
+        m.specular = 0.9
+        m.shininess = 200.0
+    else:  # glass
+        m.color = rt.Color(0.05, 0.05, 0.05)
+        m.ambient = 0.0
+        m.diffuse = 0.1
+        m.specular = 0.9
+        m.shininess = 300.0
+        m.reflective = 0.9
+        m.transparency = 0.9
+        m.refractive_index = 1.5
+    return s
+
+
+def c3(width=1920, height=1080, n_spheres=1000, seed=0x5EED0003):
+    """C3 (headline): floor plane + n random spheres, 1 light, depth 5."""
+    rng = SplitMix64(seed)
+    w = rt.World()
+    floor = rt.Plane()
+    floor.material.color = rt.Color(0.8, 0.8, 0.8)
+    floor.material.specular = 0.0
+    floor.material.reflective = 0.2
+    w.add_object(floor)
+    for _ in range(n_spheres):
+        w.add_object(_random_sphere(rng, (-10.0, 0.0, -2.0), (10.0, 3.0, 20.0)))
+    w.add_light(rt.PointLight(rt.Point(-10, 20, -10), rt.Color(1.0, 1.0, 1.0)))
+    return w, _camera(width, height, PI / 3.0, (0, 3, -12), (0, 1, 5)), 5
+
+
+def c5(width=4096, height=4096, n_spheres=9996, seed=0x5EED0005):
+    """C5: room of 4 planes (reflect-refract.yml:55-104 style) + spheres, 2 lights, depth 8."""
+    rng = SplitMix64(seed)
+    w = rt.World()
+    floor = rt.Plane()
+    floor.material.color = rt.Color(0.8, 0.8, 0.8)
+    floor.material.specular = 0.0
+    floor.material.reflective = 0.2
+    w.add_object(floor)
+    back = rt.Plane()
+    back.set_transform(rt.translation(0, 0, 30) * rt.rotation_x(PI / 2.0))
+    back.material.color = rt.Color(0.6, 0.7, 0.9)
+    back.material.specular = 0.0
+    w.add_object(back)
+    for x in (-25.0, 25.0):
+        wall = rt.Plane()
+        wall.set_transform(rt.translation(x, 0, 0) * rt.rotation_z(PI / 2.0))
+        wall.material.color = rt.Color(0.9, 0.8, 0.7)
+        wall.material.specular = 0.0
+        wall.material.reflective = 0.1
+        w.add_object(wall)
+    for _ in range(n_spheres):
+        w.add_object(_random_sphere(rng, (-25.0, 0.0, -10.0), (25.0, 30.0, 30.0)))
+    w.add_light(rt.PointLight(rt.Point(-10, 25, -20), rt.Color(0.8, 0.8, 0.8)))
+    w.add_light(rt.PointLight(rt.Point(15, 20, -15), rt.Color(0.4, 0.4, 0.45)))
+    return w, _camera(width, height, PI / 3.0, (0, 8, -30), (0, 6, 10)), 8
+
+
+def zoo(width=160, height=120):
+    """Feature coverage: every pattern kind, rotated/sheared shapes, nested
+    glass (n1/n2), a shadowless object, two lights, reflection + refraction."""
+    w = rt.World()
+    floor = rt.Plane()
+    floor.material.set_pattern(rt.checkers_pattern(rt.Color(0.0, 0.5, 0.5), rt.Color(0.5, 0.0, 0.5)))
+    floor.material.reflective = 0.1
+    w.add_object(floor)
+    left_wall = rt.Plane()
+    left_wall.set_transform(rt.Matrix.identity(4, 4).rotate_x(PI / 2.0).rotate_y(-PI / 4.0).translate(0, 0, 5))
+    ring = rt.ring_pattern(rt.Color(0.0, 0.0, 1.0), rt.Color(0.0, 1.0, 1.0))
+    ring.set_transform(rt.scaling(0.333, 0.333, 0.333))
+    left_wall.material.set_pattern(ring)
+    w.add_object(left_wall)
+    right_wall = rt.Plane()
+    right_wall.set_transform(rt.Matrix.identity(4, 4).rotate_x(PI / 2.0).rotate_y(PI / 4.0).translate(0, 0, 5))
+    stripe = rt.stripe_pattern(rt.Color.white(), rt.Color.black())
+    stripe.set_transform(rt.rotation_y(0.3) * rt.scaling(0.5, 1.0, 1.0))
+    right_wall.material.set_pattern(stripe)
+    w.add_object(right_wall)
+    middle = rt.Sphere()
+    middle.set_transform(rt.translation(-0.5, 1.0, 0.5))
+    middle.material.color = rt.Color(0.1, 1.0, 0.5)
+    middle.material.diffuse = 0.7
+    middle.material.specular = 0.3
+    middle.material.reflective = 0.9
+    w.add_object(middle)
+    right = rt.Sphere()
+    right.set_transform(rt.translation(1.5, 0.5, -0.5) * rt.scaling(0.5, 0.5, 0.5))
+    right.material.set_pattern(rt.checkers_pattern(rt.Color(1.0, 0.0, 0.0), rt.Color(0.0, 1.0, 0.0)))
+    w.add_object(right)
+    left = rt.glass_sphere()
+    left.material.color = rt.Color(0.1, 0.0, 0.0)
+    left.material.diffuse = 0.05
+    left.material.reflective = 0.3
+    left.material.specular = 1.0
+    left.material.shininess = 300.0
+    left.set_transform(rt.translation(-1.5, 0.33, -0.75) * rt.scaling(0.33, 0.33, 0.33))
+    w.add_object(left)
+    # nested glass: outer shell with an inner air bubble and an inner denser core
+    outer = rt.glass_sphere()
+    outer.set_transform(rt.translation(0.6, 0.6, -1.6) * rt.scaling(0.6, 0.6, 0.6))
+    outer.material.reflective = 0.5
+    outer.material.color = rt.Color(0.0, 0.0, 0.1)
+    outer.material.ambient = 0.0
+    w.add_object(outer)
+    bubble = rt.glass_sphere()
+    bubble.set_transform(rt.translation(0.55, 0.6, -1.6) * rt.scaling(0.3, 0.3, 0.3))
+    bubble.material.refractive_index = 1.0000034
+    bubble.material.reflective = 0.2
+    w.add_object(bubble)
+    core = rt.glass_sphere()
+    core.set_transform(rt.translation(0.75, 0.55, -1.6) * rt.scaling(0.2, 0.2, 0.2))
+    core.material.refractive_index = 2.4
+    w.add_object(core)
+    # sheared/rotated ellipsoid with a gradient, and a shadowless test-pattern sphere
+    ell = rt.Sphere()
+    ell.set_transform(rt.translation(-0.3, 0.35, -2.2) * rt.shearing(0.3, 0, 0.2, 0, 0, 0.1)
+                      * rt.rotation_z(0.7) * rt.scaling(0.4, 0.2, 0.3))
+    grad = rt.gradient_pattern(rt.Color(1.0, 0.2, 0.1), rt.Color(0.1, 0.2, 1.0))
+    grad.set_transform(rt.scaling(2.0, 1.0, 1.0) * rt.translation(1.0, 0, 0))
+    ell.material.set_pattern(grad)
+    w.add_object(ell)
+    ghost = rt.Sphere()
+    ghost.set_transform(rt.translation(1.2, 1.6, 0.3) * rt.scaling(0.25, 0.25, 0.25))
+    ghost.material.set_pattern(rt.test_pattern())
+    ghost.no_shadow()
+    w.add_object(ghost)
+    w.add_light(rt.PointLight(rt.Point(-10, 10, -10), rt.Color(1.0, 1.0, 1.0)))
+    w.add_light(rt.PointLight(rt.Point(-5.0, 10.0, -6.0), rt.Color(0.33, 0.33, 0.33)))
+    return w, _camera(width, height, PI / 3.0, (0.0, 1.5, -5.0), (0, 1, 0)), 5
+
+
+CONFIGS = {"c1": c1, "c2": c2, "c3": c3, "c5": c5, "zoo": zoo}

@@ -1,0 +1,65 @@
+"""The C-ABI boundary (include/rt_render.h) on CPU: the library loads,
+exports every declared entry point, and fails loudly (no CPU fallback) when no
+GPU is present. Validation that needs no device is exercised here too."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import PKG, REPO
+
+HEADER = os.path.join(REPO, "include", "rt_render.h")
+LIB = os.path.join(PKG, "lib", "librtamd.so")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rt_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_the_boundary():
+    names = declared_functions()
+    for must in ("rt_scene_create", "rt_scene_destroy", "rt_render", "rt_render_shard_device",
+                 "rt_render_multi", "rt_color_at_batch", "rt_is_shadowed_batch", "rt_hit_batch",
+                 "rt_canvas_to_ppm", "rt_quantize_u8", "rt_matrix_inverse", "rt_camera_init",
+                 "rt_last_error", "rt_abi_version", "rt_device_count", "rt_shard_rows"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(LIB)
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_abi_version_and_shard_rows():
+    lib = ctypes.CDLL(LIB)
+    assert lib.rt_abi_version() == 1
+    f = lib.rt_shard_rows
+    f.restype = ctypes.c_uint32
+    f.argtypes = [ctypes.c_uint32] * 4
+    # interleaved row blocks: every row owned exactly once
+    for H, B, S in [(1080, 8, 1), (1080, 8, 2), (1080, 8, 8), (1081, 16, 3), (5, 8, 4), (0, 4, 2)]:
+        assert sum(f(H, B, s, S) for s in range(S)) == H
+    assert f(100, 0, 0, 1) == 0 and f(100, 4, 3, 3) == 0
+
+
+def test_duplicate_shapes_rejected_before_any_device_work(rt):
+    w = rt.World()
+    w.add_object(rt.Sphere())
+    w.add_object(rt.Sphere())  # structurally equal -> containers semantics ambiguous
+    w.add_light(rt.PointLight(rt.Point(0, 0, -10), rt.Color(1, 1, 1)))
+    with pytest.raises(rt.RtError, match="structurally equal"):
+        w.upload()
+
+
+@pytest.mark.skipif(os.environ.get("RT_EXPECT_GPU") == "1", reason="GPU present")
+def test_no_cpu_fallback_without_gpu(rt):
+    if rt.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    w = rt.World.default()
+    c = rt.Camera(11, 11, 1.0)
+    with pytest.raises(rt.RtError, match="no HIP device"):
+        c.render(w)

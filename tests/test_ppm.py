@@ -1,0 +1,38 @@
+"""Output format (image/ppm.rs): the product writer vs the reference KATs and,
+byte for byte, vs the oracle's writer."""
+import numpy as np
+
+
+def test_ppm_reference_kats(rt):
+    c = rt.Canvas(5, 3)  # ppm.rs:90-109
+    c.set_pixel(0, 0, rt.Color(1.5, 0.0, 0.0))
+    c.set_pixel(2, 1, rt.Color(0.0, 0.5, 0.0))
+    c.set_pixel(4, 2, rt.Color(-0.5, 0.0, 1.0))
+    assert c.to_ppm() == (b"P3\n5 3\n255\n"
+                          b"255 0 0 0 0 0 0 0 0 0 0 0 0 0 0\n"
+                          b"0 0 0 0 0 0 0 128 0 0 0 0 0 0 0\n"
+                          b"0 0 0 0 0 0 0 0 0 0 0 0 0 0 255\n")
+    c = rt.Canvas(10, 2)  # ppm.rs:127-150
+    for j in range(2):
+        for i in range(10):
+            c.set_pixel(i, j, rt.Color(1.0, 0.8, 0.6))
+    line1 = b"255 204 153 255 204 153 255 204 153 255 204 153 255 204 153 255 204\n"
+    line2 = b"153 255 204 153 255 204 153 255 204 153 255 204 153\n"
+    assert c.to_ppm() == b"P3\n10 2\n255\n" + (line1 + line2) * 2
+
+
+def test_quantizer_rules(rt):
+    # ppm.rs:111-118 plus Rust `round()` / saturating `as u8` edge cases
+    v = np.array([0.0, 255.0, -0.5, 1.5, 0.5, 0.1, np.nan, np.inf, -np.inf, -0.0,
+                  0.5 / 255, (0.5 - 1e-12) / 255, 254.5 / 255])
+    assert rt.quantize_u8(v).tolist() == [0, 255, 0, 255, 128, 26, 0, 255, 0, 0, 1, 0, 255]
+
+
+def test_ppm_bytes_match_oracle(rt, oracle):
+    rng = np.random.default_rng(7)
+    for (h, w) in [(1, 1), (3, 5), (7, 23), (40, 31), (2, 70), (1, 0), (0, 3)]:
+        img = rng.uniform(-0.2, 1.3, size=(h, w, 3))
+        if img.size:
+            img.flat[::17] = 0.1  # exact .5 ties after scaling
+            img.flat[::29] = np.nan
+        assert rt.canvas_to_ppm(img) == oracle.canvas_to_ppm(img)
