@@ -1,0 +1,236 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mrays/s on the 1920x1080 / 1000-sphere / depth-5 scene.
+
+A "step" renders ONE full frame of the C3 workload (SURVEY.md §8d,
+rtamd.scenes.c3): `Camera::render(&World)` with MAX_RECURSION_DEPTH = 5, all
+of primary + reflection + refraction + shadow rays (each one a
+`World::intersect`, world.rs:71,101). With N GPUs (one process per GPU,
+launched by torch.distributed.run) the frame is split into interleaved 8-row
+blocks, each rank renders its rows into HBM, and the canvas is assembled on
+rank 0 with one RCCL gather (strong scaling: the frame is fixed).
+
+The scene is uploaded before timing (inputs resident in HBM). The timed
+region holds exactly K steps bracketed by barrier + synchronize; the
+reported time is the max over ranks.
+
+Printed JSON line (rank 0): metric/value/unit per BASELINE.json, plus
+  roofline      f64 VALU roofline of the render kernel, kernel time from HIP
+                events on the launch stream inside the timed region
+  cpu_baseline  the C oracle (a port of the reference algorithm) on a bounded
+                row sample on this host's cores (N=1, rank 0 only)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [REPO, os.path.join(REPO, "raytracer-challenge-rs_amd")]
+
+import torch  # noqa: E402  (load torch's HIP runtime first: see rtamd/__init__.py)
+import torch.distributed as dist  # noqa: E402
+
+import rtamd  # noqa: E402
+from rtamd import scenes  # noqa: E402
+
+METRIC = "Mrays/s (primary+secondary) on 1920×1080/1000-sphere/depth-5; 1→8 GPU scaling"
+PEAK_F64_VALU_TFLOPS = 39.3  # 256 CU x 64 f64 lanes/clk x 2.4 GHz, non-fused add/mul (MI355X_MICROARCH.md)
+
+# Executed f64 VALU operations per unit of work (DESIGN.md "Roofline"):
+#   diagonal-inverse sphere test: 9 (object-space ray) + 5 (a) + 5 (d.o) + 6 (c) + 3 (disc) = 28
+#   roots when disc >= 0: sqrt + 2 sub/neg + 2 div, priced as 1+2+2 = 5 (counted per event)
+#   plane test: 6 (o'.y) + 5 (d'.y) + 1 (|d'.y| test) = 12, root division priced 1
+OPS_SPHERE_DIAG = 28
+OPS_ROOTS = 5
+OPS_PLANE = 12
+# SURVEY.md §8(d) convention (the reference's general 4x4 path): 57 / 34 / +6
+SURVEY_OPS_SPHERE, SURVEY_OPS_PLANE, SURVEY_OPS_ROOTS = 57, 34, 6
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--width", type=int, default=1920)
+    p.add_argument("--height", type=int, default=1080)
+    p.add_argument("--spheres", type=int, default=1000)
+    p.add_argument("--depth", type=int, default=5)
+    p.add_argument("--row-block", type=int, default=8)
+    p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget for the CPU baseline sample")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--pmc-summary", default=os.path.join(REPO, "profiles", "r01_pmc_summary.json"),
+                   help="HBM traffic per launch measured by rocprofv3 --pmc for this workload")
+    return p.parse_args()
+
+
+def cpu_baseline(world, cam, depth, budget_s):
+    """Oracle (C port of the reference algorithm, threads in row blocks like
+    render_multithreaded) on evenly spaced rows, sized to ~budget_s."""
+    from oracle import pyoracle
+    ow = pyoracle.OracleWorld.from_world(world)
+    nthreads = max(1, min(16, os.cpu_count() or 1))
+    desc = cam.desc_bytes()
+
+    def run(rows):
+        t0 = time.perf_counter()
+        _, st = ow.render_rows(desc, depth, rows, nthreads)
+        dt = time.perf_counter() - t0
+        return dt, st["rays_primary"] + st["rays_reflect"] + st["rays_refract"] + st["rays_shadow"]
+
+    H = cam.vsize
+    # calibrate: one row per thread, spread over the frame
+    probe = [int((i + 0.5) * H / nthreads) for i in range(nthreads)]
+    t_probe, _ = run(probe)
+    n_rows = int(max(1, min(H, nthreads * budget_s / max(t_probe, 1e-6))))
+    stride = max(1, H // n_rows)
+    rows = list(range(stride // 2, H, stride))
+    dt, rays = run(rows)
+    return {
+        "value": rays / dt / 1e6,
+        "unit": "Mrays/s",
+        "cores": nthreads,
+        "kind": "port",
+        "sample": f"{len(rows)} of {H} rows (every {stride}th), {rays} rays in {dt:.2f}s; "
+                  f"C restatement of the reference algorithm (oracle/rt_oracle.c: full intersection list + "
+                  f"sort + containers walk, recursion depth {depth}), {nthreads} threads in row blocks",
+    }
+
+
+def main():
+    a = parse()
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus != world_size and world_size > 1:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world_size}; using WORLD_SIZE", file=sys.stderr)
+    n = world_size
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if n > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    world, cam, depth = scenes.c3(a.width, a.height, a.spheres)
+    if a.depth != depth:
+        depth = a.depth
+    world.upload(local_rank)  # flatten + upload: outside the timed region
+    W, H, B = cam.hsize, cam.vsize, a.row_block
+    my_rows = rtamd.shard_rows(H, B, rank, n)
+    max_rows = max(rtamd.shard_rows(H, B, s, n) for s in range(n))
+    shard = torch.zeros((max_rows, W, 3), dtype=torch.float64, device=dev)  # padded for the gather
+    if rank == 0:
+        gathered = [torch.empty_like(shard) for _ in range(n)]
+        canvas = torch.empty((H, W, 3), dtype=torch.float64, device=dev)
+        # rank-major gathered rows -> canvas rows (un-interleave index)
+        src = []
+        for s in range(n):
+            rows_s = [y for y in range(H) if (y // B) % n == s]
+            src += [s * max_rows + i for i in range(len(rows_s))]
+        dst = [y for s in range(n) for y in range(H) if (y // B) % n == s]
+        src_idx = torch.tensor(src, device=dev)
+        dst_idx = torch.tensor(dst, device=dev)
+    stream = torch.cuda.current_stream()
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        cam.render_shard_device(world, depth, B, rank, n, shard.data_ptr(), stream.cuda_stream, False)
+        if ev is not None:
+            ev[1].record(stream)
+        if n > 1:
+            dist.gather(shard, gathered if rank == 0 else None, dst=0)
+            if rank == 0:
+                canvas.index_copy_(0, dst_idx, torch.cat(gathered).index_select(0, src_idx))
+        # n == 1: the shard buffer already is the row-major canvas
+
+    # exact work counters of one frame (deterministic), from a counted warm-up launch
+    st = cam.render_shard_device(world, depth, B, rank, n, shard.data_ptr(), stream.cuda_stream, True)
+    counts = torch.tensor([st["rays_primary"], st["rays_reflect"], st["rays_refract"], st["rays_shadow"],
+                           st["sphere_tests"], st["plane_tests"], st["sphere_disc_ge0"]],
+                          dtype=torch.float64, device=dev)
+    if n > 1:
+        dist.all_reduce(counts)
+    rays_per_frame = float(counts[:4].sum())
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    if n > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(a.steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    if n > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / a.steps
+    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+    if n > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kernel_ms = float(t[0]), float(t[1])
+
+    if rank == 0:
+        value = rays_per_frame * a.steps / elapsed / 1e6
+        # roofline of the render kernel on rank 0 (per launch = this rank's shard)
+        sph, pln, roots = (float(x) for x in (st["sphere_tests"], st["plane_tests"], st["sphere_disc_ge0"]))
+        ops = OPS_SPHERE_DIAG * sph + OPS_PLANE * pln + OPS_ROOTS * roots
+        achieved = ops / (kernel_ms * 1e-3) / 1e12
+        survey_ops = SURVEY_OPS_SPHERE * sph + SURVEY_OPS_PLANE * pln + SURVEY_OPS_ROOTS * roots
+        traffic, traffic_src = None, None
+        if os.path.exists(a.pmc_summary):
+            try:
+                pm = json.load(open(a.pmc_summary))
+                if (pm.get("width"), pm.get("height"), pm.get("spheres"), pm.get("n_gpus")) == (W, H, a.spheres, n):
+                    traffic, traffic_src = pm.get("hbm_bytes_per_launch"), os.path.relpath(a.pmc_summary, REPO)
+            except Exception:
+                pass
+        out = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "Mrays/s",
+            "n_gpus": n,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {
+                "workload": f"c3: {W}x{H}, floor plane + {a.spheres} random spheres (splitmix64 seed 0x5EED0003), "
+                            f"1 light, reflect+refract depth {depth}",
+                "width": W, "height": H, "spheres": a.spheres, "depth": depth,
+                "rays_per_frame": int(rays_per_frame),
+                "parallelism": f"{n} GPU(s): interleaved {B}-row blocks, RCCL gather to rank 0" if n > 1
+                               else "1 GPU: persistent render kernel",
+            },
+            "roofline": {
+                "bound": "valu_f64",
+                "achieved": round(achieved, 3),
+                "peak": PEAK_F64_VALU_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": round(achieved / PEAK_F64_VALU_TFLOPS, 4),
+                "traffic": traffic,
+                "kernel_ms": round(kernel_ms, 4),
+                "ops_per_launch": ops,
+                "per_unit": f"{OPS_SPHERE_DIAG} f64 ops/sphere test + {OPS_PLANE}/plane test + "
+                            f"{OPS_ROOTS}/root pair (DESIGN.md 'Roofline')",
+                "survey_convention_tflops": round(survey_ops / (kernel_ms * 1e-3) / 1e12, 3),
+                "traffic_source": traffic_src,
+            },
+        }
+        if n == 1 and not a.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(world, cam, depth, a.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if n > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

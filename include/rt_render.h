@@ -142,7 +142,9 @@ int rt_render(const rt_scene* scene, const rt_camera_desc* camera,
 /* Device-resident shard render (used by multi-GPU and the benchmark).
  * Renders the rows y with (y / row_block) % n_shards == shard, in increasing
  * y order, into `d_out_rgb` (a DEVICE buffer on the scene's device holding
- * rows_in_shard*hsize*3 doubles). `stream` is a hipStream_t (NULL = default).
+ * rows_in_shard*hsize*3 doubles). `stream` is a hipStream_t; NULL means the
+ * default (null) stream, so the work is ordered with the caller's other work
+ * there (torch's current stream is often the null stream).
  * Asynchronous unless `stats` is non-NULL (then it synchronises to read the
  * counters). `n_shards == 1` renders the whole frame. */
 int rt_render_shard_device(const rt_scene* scene, const rt_camera_desc* camera,

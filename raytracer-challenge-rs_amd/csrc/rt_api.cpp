@@ -383,7 +383,7 @@ int rt_render_shard_device(const rt_scene* scene, const rt_camera_desc* camera, 
   const uint32_t rows = rt_shard_rows(camera->vsize, row_block, shard, n_shards);
   const uint64_t n_tasks = (uint64_t)rows * camera->hsize;
   if (n_tasks >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "shard too large");
-  hipStream_t st = stream ? (hipStream_t)stream : s->stream;
+  hipStream_t st = (hipStream_t)stream;  // NULL = the default stream (torch's current stream is often 0)
   int rc = run_render(s, to_dev_camera(*camera), nullptr, (uint32_t)n_tasks, max_depth, row_block, shard,
                       n_shards, d_out_rgb, st, stats != nullptr);
   if (rc != RT_OK) return rc;
@@ -392,7 +392,6 @@ int rt_render_shard_device(const rt_scene* scene, const rt_camera_desc* camera, 
     float ms = 0.f;
     if (n_tasks) RT_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
     double tot = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    if (st != s->stream) RT_HIP(hipStreamSynchronize(st));
     DevStats ds{};
     RT_HIP(hipMemcpy(&ds, s->d_stats, sizeof ds, hipMemcpyDeviceToHost));
     stats->rays_primary = ds.rays_primary; stats->rays_reflect = ds.rays_reflect;

@@ -13,6 +13,17 @@ fallback: rendering without a GPU raises RtError (RT_ERR_NO_DEVICE).
 import os as _os
 
 _here = _os.path.dirname(_os.path.abspath(__file__))
+
+# One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64 /
+# libhsa-runtime64 (same SONAMEs as /opt/rocm's). Loading torch first makes
+# librtamd.so bind to that already-loaded runtime, so device pointers and
+# streams can be shared with torch (bench.py, torch.distributed). Without
+# torch installed the system ROCm runtime is used.
+try:  # pragma: no cover - environment dependent
+    import torch as _torch  # noqa: F401
+except ImportError:  # pragma: no cover
+    _torch = None
+
 try:
     from . import _rtamd  # noqa: F401
 except ImportError as e:  # pragma: no cover - exercised when the build is missing
