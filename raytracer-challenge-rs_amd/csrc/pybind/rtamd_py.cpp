@@ -35,6 +35,9 @@ static py::array_t<double> check_rays(py::array_t<double, py::array::c_style | p
   return a;
 }
 
+extern "C" int rtamd_tuning_set(const char* key, int value);
+extern "C" int rtamd_diag_last(const rt_scene* s, unsigned long long out[3]);
+
 PYBIND11_MODULE(_rtamd, m) {
   m.doc() = "MI355X-native render path of raytracer-challenge-rs (host API over the C-ABI)";
   py::register_exception<RtError>(m, "RtError");
@@ -313,4 +316,10 @@ PYBIND11_MODULE(_rtamd, m) {
         return py::make_tuple(std::unique_ptr<Canvas>(out), stats_dict(st));
       });
   m.def("shard_rows", &rt_shard_rows);
+  m.def("_diag_last", [](const World& w) {
+    unsigned long long o[3];
+    check(rtamd_diag_last(w.scene(), o), "diag");
+    return py::make_tuple(o[0], o[1], o[2]);
+  });
+  m.def("_tuning_set", [](const std::string& k, int v) { check(rtamd_tuning_set(k.c_str(), v), "tuning"); });
 }

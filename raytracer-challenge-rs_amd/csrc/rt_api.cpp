@@ -11,6 +11,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -26,6 +27,12 @@ using namespace rtamd;
 namespace {
 
 thread_local std::string g_err;
+
+// Tuning knobs (development only; not part of the public ABI).
+int g_tune_waves = [] {
+  const char* e = std::getenv("RTAMD_WAVES");
+  return e ? std::atoi(e) : 0;
+}();
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -167,6 +174,7 @@ int run_render(rt_scene* s, const DevCamera& cam, const double* d_rays, uint32_t
   a.shard = shard;
   a.n_shards = n_shards;
   a.grid_cap = 0;
+  a.waves = g_tune_waves;
   RT_HIP(hipMemsetAsync(s->d_counter, 0, 64, stream));
   RT_HIP(hipMemsetAsync(s->d_stats, 0, sizeof(DevStats), stream));
   if (n_tasks == 0) return RT_OK;
@@ -181,6 +189,29 @@ int run_render(rt_scene* s, const DevCamera& cam, const double* d_rays, uint32_t
 extern "C" {
 
 const char* rt_last_error(void) { return g_err.c_str(); }
+
+// Development-only diagnostics of the last launch on a scene (not in the public ABI):
+// out[0] = wave-level trace steps, out[1] = DIAG trace cycles, out[2] = DIAG total cycles.
+int rtamd_diag_last(const rt_scene* s, unsigned long long out[3]) {
+  if (!s || !out) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
+  DevStats ds{};
+  RT_HIP(hipSetDevice(s->device));
+  RT_HIP(hipDeviceSynchronize());
+  RT_HIP(hipMemcpy(&ds, s->d_stats, sizeof ds, hipMemcpyDeviceToHost));
+  out[0] = ds.wave_steps;
+  out[1] = ds.diag_trace_cycles;
+  out[2] = ds.diag_total_cycles;
+  return RT_OK;
+}
+
+// Development-only tuning hook (not declared in include/rt_render.h).
+int rtamd_tuning_set(const char* key, int value) {
+  if (key && std::strcmp(key, "waves") == 0) {
+    g_tune_waves = value;
+    return RT_OK;
+  }
+  return fail(RT_ERR_INVALID_ARGUMENT, "unknown tuning key");
+}
 int rt_abi_version(void) { return RT_ABI_VERSION; }
 
 int rt_device_count(void) {
@@ -296,9 +327,10 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   // ---- one blob, 64-B aligned sections
   auto align = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const size_t o_diag = 0;
-  const size_t o_gen = align(o_diag + diag.size() * sizeof(SphereDiag));
-  const size_t o_pl = align(o_gen + gen.size() * sizeof(SphereGen));
-  const size_t o_sh = align(o_pl + planes.size() * sizeof(PlaneRec));
+  // one zeroed padding record after each trace section (look-ahead loads)
+  const size_t o_gen = align(o_diag + (diag.size() + 1) * sizeof(SphereDiag));
+  const size_t o_pl = align(o_gen + (gen.size() + 1) * sizeof(SphereGen));
+  const size_t o_sh = align(o_pl + (planes.size() + 1) * sizeof(PlaneRec));
   const size_t o_li = align(o_sh + shade.size() * sizeof(ShadeRec));
   const size_t total = align(o_li + lrec.size() * sizeof(LightRec)) + 256;
   std::vector<unsigned char> host(total, 0);

@@ -123,43 +123,217 @@ __device__ __forceinline__ void sphere_roots(double ox, double oy, double oz, do
   }
 }
 
+// Same test with the object index / shadow flag fetched only when the
+// discriminant is non-negative (LDS path: the meta word is not needed per test).
+__device__ __forceinline__ void sphere_roots_lazy(double ox, double oy, double oz, double dx, double dy,
+                                                  double dz, const int* meta_p, bool shadow_mode, Hit& h,
+                                                  unsigned& n_disc) {
+  const double a = dx * dx + dy * dy + dz * dz;
+  const double dt = dx * ox + dy * oy + dz * oz;
+  const double c = ox * ox + oy * oy + oz * oz - 1.0;
+  const double disc = dt * dt - a * c;
+  if (disc >= 0.0) {
+    ++n_disc;
+    const int meta = *meta_p;
+    const double q = sqrt(disc);
+    const double t1 = (-dt - q) / a;
+    const double t2 = (-dt + q) / a;
+    const int k1 = (meta >> 1) * 2;
+    const bool eligible = !shadow_mode || (meta & 1);
+    if (eligible) {
+      if (t1 >= 0.0) {
+        if (better(t1, k1, h.t, h.key)) { h.t = t1; h.key = k1; }
+      } else if (t2 >= 0.0) {
+        if (better(t2, k1 + 1, h.t, h.key)) { h.t = t2; h.key = k1 + 1; }
+      }
+    }
+    if (t1 < 0.0 && t2 >= 0.0) push_container(h, t1, k1);
+  }
+}
+
+// Two-phase form of the same test: the discriminant of several spheres can be
+// formed in one basic block (independent chains the scheduler interleaves),
+// then the rare non-negative cases are resolved one by one.
+struct Disc {
+  double a, dt, disc;
+};
+__device__ __forceinline__ Disc sphere_disc(double ox, double oy, double oz, double dx, double dy, double dz) {
+  Disc r;
+  r.a = dx * dx + dy * dy + dz * dz;
+  r.dt = dx * ox + dy * oy + dz * oz;
+  const double c = ox * ox + oy * oy + oz * oz - 1.0;
+  r.disc = r.dt * r.dt - r.a * c;
+  return r;
+}
+__device__ __forceinline__ void sphere_resolve(const Disc& s, int meta, bool shadow_mode, Hit& h) {
+  const double q = sqrt(s.disc);
+  const double t1 = (-s.dt - q) / s.a;
+  const double t2 = (-s.dt + q) / s.a;
+  const int k1 = (meta >> 1) * 2;
+  const bool eligible = !shadow_mode || (meta & 1);
+  if (eligible) {
+    if (t1 >= 0.0) {
+      if (better(t1, k1, h.t, h.key)) { h.t = t1; h.key = k1; }
+    } else if (t2 >= 0.0) {
+      if (better(t2, k1 + 1, h.t, h.key)) { h.t = t2; h.key = k1 + 1; }
+    }
+  }
+  if (t1 < 0.0 && t2 >= 0.0) push_container(h, t1, k1);
+}
+
+// LDS image of the trace records (one copy per workgroup = per CU):
+//   diag: 6 doubles (s0 s1 s2 t0 t1 t2) per sphere, gen: 12 doubles, plane: 4
+//   doubles; then int32 meta arrays. Reads are wave-uniform (broadcast).
+struct LdsView {
+  const double* diag;
+  const double* gen;
+  const double* plane;
+  const int* diag_meta;
+  const int* gen_meta;
+  const int* plane_meta;
+};
+typedef double d2 __attribute__((ext_vector_type(2)));
+
+__host__ __device__ constexpr size_t lds_align16(size_t x) { return (x + 15) & ~(size_t)15; }
+__host__ __device__ inline size_t lds_bytes(int nd, int ng, int np) {
+  return lds_align16((size_t)(nd + 4) * 48) + lds_align16((size_t)ng * 96) + lds_align16((size_t)np * 32) +
+         lds_align16((size_t)nd * 4) + lds_align16((size_t)ng * 4) + lds_align16((size_t)np * 4);
+}
+
+__device__ LdsView lds_stage(const DevScene& sc, unsigned char* base) {
+  LdsView v;
+  size_t off = 0;
+  v.diag = (const double*)(base + off); off += lds_align16((size_t)(sc.n_diag + 4) * 48);
+  v.gen = (const double*)(base + off); off += lds_align16((size_t)sc.n_gen * 96);
+  v.plane = (const double*)(base + off); off += lds_align16((size_t)sc.n_planes * 32);
+  v.diag_meta = (const int*)(base + off); off += lds_align16((size_t)sc.n_diag * 4);
+  v.gen_meta = (const int*)(base + off); off += lds_align16((size_t)sc.n_gen * 4);
+  v.plane_meta = (const int*)(base + off);
+  double* dd = (double*)v.diag;
+  double* dg = (double*)v.gen;
+  double* dp = (double*)v.plane;
+  for (int i = threadIdx.x; i < (sc.n_diag + 4) * 6; i += blockDim.x) {
+    const int r = i / 6, e = i - r * 6;
+    dd[i] = r >= sc.n_diag ? 0.0 : e < 3 ? sc.sph_diag[r].s[e] : sc.sph_diag[r].t[e - 3];
+  }
+  for (int i = threadIdx.x; i < sc.n_gen * 12; i += blockDim.x) dg[i] = sc.sph_gen[i / 12].m[i % 12];
+  for (int i = threadIdx.x; i < sc.n_planes * 4; i += blockDim.x) dp[i] = sc.planes[i / 4].m[i % 4];
+  for (int i = threadIdx.x; i < sc.n_diag; i += blockDim.x) ((int*)v.diag_meta)[i] = (int)sc.sph_diag[i].meta;
+  for (int i = threadIdx.x; i < sc.n_gen; i += blockDim.x) ((int*)v.gen_meta)[i] = (int)sc.sph_gen[i].meta;
+  for (int i = threadIdx.x; i < sc.n_planes; i += blockDim.x) ((int*)v.plane_meta)[i] = (int)sc.planes[i].meta;
+  __syncthreads();
+  return v;
+}
+
 // World::intersect + hit (world.rs:31-38, intersection.rs:118-125): every
 // object, in three wave-uniform record streams.
-__device__ __forceinline__ void trace(const DevScene& sc, V3 o, V3 d, bool shadow_mode, Hit& h,
-                                      unsigned& n_disc) {
-  h.t = INFINITY; h.key = -1;
+template <bool USE_LDS, int LOOPV = 0>
+__device__ __forceinline__ void trace(const DevScene& sc, const LdsView& lv, V3 o, V3 d, bool shadow_mode,
+                                      Hit& h, unsigned& n_disc) {
+  h.t = INFINITY;
   h.c1t = -INFINITY; h.c2t = -INFINITY; h.c1k = -1; h.c2k = -1;
   h.key = 0x7fffffff;
   // Shape::intersect (geometry/mod.rs:46-49): Ray::transform by the inverse.
-  cSphereDiag sd = (cSphereDiag)sc.sph_diag;
-  for (int j = 0; j < sc.n_diag; ++j) {
-    const double s0 = sd[j].s[0], s1 = sd[j].s[1], s2 = sd[j].s[2];
-    const double t0 = sd[j].t[0], t1 = sd[j].t[1], t2 = sd[j].t[2];
-    const int64_t meta = sd[j].meta;
-    // off-diagonal entries are exact zeros: ((m00*x + 0) + 0) + m03 == m00*x + m03
-    sphere_roots(s0 * o.x + t0, s1 * o.y + t1, s2 * o.z + t2, s0 * d.x, s1 * d.y, s2 * d.z, meta,
-                 shadow_mode, h, n_disc);
+  if constexpr (USE_LDS && LOOPV == 1) {
+    if (sc.n_diag > 0) {
+      // pairs of spheres per basic block: two independent dependency chains
+      const d2* r = (const d2*)lv.diag;
+      d2 a0 = r[0], a1 = r[1], a2 = r[2], b0 = r[3], b1 = r[4], b2 = r[5];
+      for (int j = 0; j < sc.n_diag; j += 2) {
+        const int jn = j + 2;  // padding records make jn, jn+1 readable
+        const d2 c0 = r[3 * jn], c1 = r[3 * jn + 1], c2 = r[3 * jn + 2];
+        const d2 e0 = r[3 * jn + 3], e1 = r[3 * jn + 4], e2 = r[3 * jn + 5];
+        const Disc A = sphere_disc(a0.x * o.x + a1.y, a0.y * o.y + a2.x, a1.x * o.z + a2.y, a0.x * d.x,
+                                   a0.y * d.y, a1.x * d.z);
+        const Disc B = sphere_disc(b0.x * o.x + b1.y, b0.y * o.y + b2.x, b1.x * o.z + b2.y, b0.x * d.x,
+                                   b0.y * d.y, b1.x * d.z);
+        if (A.disc >= 0.0) {
+          ++n_disc;
+          sphere_resolve(A, lv.diag_meta[j], shadow_mode, h);
+        }
+        if (B.disc >= 0.0 && j + 1 < sc.n_diag) {
+          ++n_disc;
+          sphere_resolve(B, lv.diag_meta[j + 1], shadow_mode, h);
+        }
+        a0 = c0; a1 = c1; a2 = c2; b0 = e0; b1 = e1; b2 = e2;
+      }
+    }
+  } else if constexpr (USE_LDS) {
+    if (sc.n_diag > 0) {
+      // ping-pong look-ahead from LDS (3 x ds_read_b128 per record, broadcast);
+      // the image holds zero padding records, so record j+1 always exists.
+      // record layout: (s0 s1) (s2 t0) (t1 t2); off-diagonal inverse entries are exact zeros
+      const d2* r = (const d2*)lv.diag;
+      d2 a0 = r[0], a1 = r[1], a2 = r[2];
+      int j = 0;
+      for (; j + 1 < sc.n_diag; j += 2) {
+        const d2 b0 = r[3 * j + 3], b1 = r[3 * j + 4], b2 = r[3 * j + 5];
+        sphere_roots_lazy(a0.x * o.x + a1.y, a0.y * o.y + a2.x, a1.x * o.z + a2.y, a0.x * d.x, a0.y * d.y,
+                          a1.x * d.z, lv.diag_meta + j, shadow_mode, h, n_disc);
+        a0 = r[3 * j + 6]; a1 = r[3 * j + 7]; a2 = r[3 * j + 8];
+        sphere_roots_lazy(b0.x * o.x + b1.y, b0.y * o.y + b2.x, b1.x * o.z + b2.y, b0.x * d.x, b0.y * d.y,
+                          b1.x * d.z, lv.diag_meta + j + 1, shadow_mode, h, n_disc);
+      }
+      if (j < sc.n_diag)
+        sphere_roots_lazy(a0.x * o.x + a1.y, a0.y * o.y + a2.x, a1.x * o.z + a2.y, a0.x * d.x, a0.y * d.y,
+                          a1.x * d.z, lv.diag_meta + j, shadow_mode, h, n_disc);
+    }
+  } else {
+    cSphereDiag sd = (cSphereDiag)sc.sph_diag;
+    if (sc.n_diag > 0) {
+      // software pipeline: the scalar loads of record j+1 are in flight while
+      // record j is tested (each section ends with one padding record, so the
+      // look-ahead load is always in bounds)
+      double s0 = sd[0].s[0], s1 = sd[0].s[1], s2 = sd[0].s[2];
+      double t0 = sd[0].t[0], t1 = sd[0].t[1], t2 = sd[0].t[2];
+      int64_t meta = sd[0].meta;
+      for (int j = 0; j < sc.n_diag; ++j) {
+        const double n_s0 = sd[j + 1].s[0], n_s1 = sd[j + 1].s[1], n_s2 = sd[j + 1].s[2];
+        const double n_t0 = sd[j + 1].t[0], n_t1 = sd[j + 1].t[1], n_t2 = sd[j + 1].t[2];
+        const int64_t n_meta = sd[j + 1].meta;
+        // off-diagonal entries are exact zeros: ((m00*x + 0) + 0) + m03 == m00*x + m03
+        sphere_roots(s0 * o.x + t0, s1 * o.y + t1, s2 * o.z + t2, s0 * d.x, s1 * d.y, s2 * d.z, meta,
+                     shadow_mode, h, n_disc);
+        s0 = n_s0; s1 = n_s1; s2 = n_s2; t0 = n_t0; t1 = n_t1; t2 = n_t2; meta = n_meta;
+      }
+    }
   }
-  cSphereGen sg = (cSphereGen)sc.sph_gen;
   for (int j = 0; j < sc.n_gen; ++j) {
     double m[12];
+    if constexpr (USE_LDS) {
 #pragma unroll
-    for (int e = 0; e < 12; ++e) m[e] = sg[j].m[e];
+      for (int e = 0; e < 12; ++e) m[e] = lv.gen[12 * j + e];
+    } else {
+      cSphereGen sg = (cSphereGen)sc.sph_gen;
+#pragma unroll
+      for (int e = 0; e < 12; ++e) m[e] = sg[j].m[e];
+    }
     const V3 lo = m34_point(m, o);
     const V3 ld = v3(m[0] * d.x + m[1] * d.y + m[2] * d.z, m[4] * d.x + m[5] * d.y + m[6] * d.z,
                      m[8] * d.x + m[9] * d.y + m[10] * d.z);
-    sphere_roots(lo.x, lo.y, lo.z, ld.x, ld.y, ld.z, sg[j].meta, shadow_mode, h, n_disc);
+    if constexpr (USE_LDS) {
+      sphere_roots_lazy(lo.x, lo.y, lo.z, ld.x, ld.y, ld.z, lv.gen_meta + j, shadow_mode, h, n_disc);
+    } else {
+      sphere_roots(lo.x, lo.y, lo.z, ld.x, ld.y, ld.z, ((cSphereGen)sc.sph_gen)[j].meta, shadow_mode, h, n_disc);
+    }
   }
   // Plane::local_intersect (plane.rs:53-60): only object-space y matters.
-  cPlaneRec pl = (cPlaneRec)sc.planes;
   for (int j = 0; j < sc.n_planes; ++j) {
-    const double m0 = pl[j].m[0], m1 = pl[j].m[1], m2 = pl[j].m[2], m3 = pl[j].m[3];
-    const int64_t meta = pl[j].meta;
+    double m0, m1, m2, m3;
+    int meta;
+    if constexpr (USE_LDS) {
+      m0 = lv.plane[4 * j]; m1 = lv.plane[4 * j + 1]; m2 = lv.plane[4 * j + 2]; m3 = lv.plane[4 * j + 3];
+      meta = lv.plane_meta[j];
+    } else {
+      cPlaneRec pl = (cPlaneRec)sc.planes;
+      m0 = pl[j].m[0]; m1 = pl[j].m[1]; m2 = pl[j].m[2]; m3 = pl[j].m[3];
+      meta = (int)pl[j].meta;
+    }
     const double oy = m0 * o.x + m1 * o.y + m2 * o.z + m3;
     const double dy = m0 * d.x + m1 * d.y + m2 * d.z;
     if (!(fabs(dy) < kEpsilon)) {
       const double t = -oy / dy;
-      const int k = (int)(meta >> 1) * 2;
+      const int k = (meta >> 1) * 2;
       const bool eligible = !shadow_mode || (meta & 1);
       if (eligible && t >= 0.0 && better(t, k, h.t, h.key)) { h.t = t; h.key = k; }
       if (t < 0.0) push_container(h, t, k);
@@ -309,8 +483,13 @@ __device__ __forceinline__ void ray_for_pixel(const DevCamera& cam, uint32_t px,
   d = vnormalize(vsub(pixel, o));
 }
 
-template <int MAXF, bool FROM_RAYS>
-__global__ __launch_bounds__(256) void render_kernel(DevScene sc, DevCamera cam, RenderArgs args) {
+template <int MAXF, bool FROM_RAYS, int BLOCK, int WAVES, bool USE_LDS, int LOOPV, bool DIAG = false>
+__global__ __launch_bounds__(BLOCK, WAVES) void render_kernel(DevScene sc, DevCamera cam, RenderArgs args) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  unsigned long long diag_t0 = 0, diag_trace = 0, wave_steps = 0;
+  if constexpr (DIAG) diag_t0 = __builtin_amdgcn_s_memtime();
+  LdsView lv{};
+  if constexpr (USE_LDS) lv = lds_stage(sc, lds_raw);
   Frame stk[MAXF];
   const int lane = threadIdx.x & 63;
   int task = -1;  // pixel (render) or ray (batch) index, -1 = idle
@@ -318,7 +497,7 @@ __global__ __launch_bounds__(256) void render_kernel(DevScene sc, DevCamera cam,
   V3 ro = v3(0, 0, 0), rd = v3(0, 0, 0);
   bool shadow_mode = false;
   double sdist = 0.0;
-  unsigned long long n_prim = 0, n_refl = 0, n_refr = 0, n_shadow = 0, n_traces = 0;
+  unsigned n_prim = 0, n_refl = 0, n_refr = 0, n_shadow = 0, n_traces = 0;
   unsigned n_disc = 0;
   bool no_more = false;
   cLightRec lights = (cLightRec)sc.lights;
@@ -357,12 +536,16 @@ __global__ __launch_bounds__(256) void render_kernel(DevScene sc, DevCamera cam,
       }
     }
     if (__ballot(task >= 0) == 0ull) break;
+    ++wave_steps;
+    unsigned long long diag_s0 = 0;
+    if constexpr (DIAG) diag_s0 = __builtin_amdgcn_s_memtime();
     if (task < 0) continue;
 
     // ---- one trace per active lane (all lanes walk the same shape stream)
     Hit h;
-    trace(sc, ro, rd, shadow_mode, h, n_disc);
+    trace<USE_LDS, LOOPV>(sc, lv, ro, rd, shadow_mode, h, n_disc);
     ++n_traces;
+    if constexpr (DIAG) diag_trace += __builtin_amdgcn_s_memtime() - diag_s0;
 
     // ---- advance this lane's recursion until it needs the next trace
     int op;
@@ -486,6 +669,11 @@ __global__ __launch_bounds__(256) void render_kernel(DevScene sc, DevCamera cam,
     atomicAdd(&args.stats->sphere_tests, s_tr * (unsigned long long)(sc.n_diag + sc.n_gen));
     atomicAdd(&args.stats->plane_tests, s_tr * (unsigned long long)sc.n_planes);
     atomicAdd(&args.stats->sphere_disc_ge0, s_disc);
+    atomicAdd(&args.stats->wave_steps, wave_steps);
+    if constexpr (DIAG) {
+      atomicAdd(&args.stats->diag_trace_cycles, diag_trace);
+      atomicAdd(&args.stats->diag_total_cycles, __builtin_amdgcn_s_memtime() - diag_t0);
+    }
   }
 }
 
@@ -497,7 +685,7 @@ __global__ __launch_bounds__(256) void hit_kernel(DevScene sc, const double* ray
   const V3 d = v3(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
   Hit h;
   unsigned nd = 0;
-  trace(sc, o, d, false, h, nd);
+  trace<false>(sc, LdsView{}, o, d, false, h, nd);
   double* r = out + (size_t)i * 24;
   for (int k = 0; k < 24; ++k) r[k] = 0.0;
   r[0] = -1.0;
@@ -528,31 +716,61 @@ __global__ __launch_bounds__(256) void shadow_kernel(DevScene sc, const double* 
   const V3 d = vnormalize(v);
   Hit h;
   unsigned nd = 0;
-  trace(sc, p, d, true, h, nd);
+  trace<false>(sc, LdsView{}, p, d, true, h, nd);
   out[i] = (h.key >= 0 && h.t < distance) ? 1 : 0;
 }
 
 // ------------------------------------------------------------ host launchers
-template <int MAXF, bool FROM_RAYS>
-static hipError_t launch_render_t(const DevScene& sc, const DevCamera& cam, const RenderArgs& args,
+template <int MAXF, bool FROM_RAYS, int BLOCK, int WAVES, bool USE_LDS, int LOOPV = 0, bool DIAG = false>
+static hipError_t launch_render_w(const DevScene& sc, const DevCamera& cam, const RenderArgs& args,
                                   hipStream_t stream) {
-  auto kern = render_kernel<MAXF, FROM_RAYS>;
+  auto kern = render_kernel<MAXF, FROM_RAYS, BLOCK, WAVES, USE_LDS, LOOPV, DIAG>;
+  const size_t lds = USE_LDS ? lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes) : 0;
+  hipError_t e;
+  if (USE_LDS) {
+    e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
   int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
+  e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
   int n_cu = 0;
   e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
   if (e != hipSuccess) return e;
   int per_cu = 0;
-  e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0);
+  e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, BLOCK, lds);
   if (e != hipSuccess || per_cu < 1) per_cu = 1;
-  long long want = ((long long)args.n_tasks + 255) / 256;
+  long long want = ((long long)args.n_tasks + BLOCK - 1) / BLOCK;
   long long cap = (long long)n_cu * per_cu;
   if (args.grid_cap > 0 && args.grid_cap < cap) cap = args.grid_cap;
   long long grid = want < cap ? want : cap;
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), 0, stream, sc, cam, args);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(BLOCK), lds, stream, sc, cam, args);
   return hipGetLastError();
+}
+
+// LDS staging when the whole record list fits in one CU's LDS (one 768-thread
+// workgroup per CU = 3 waves per SIMD, one copy per CU), else scalar loads.
+constexpr size_t kLdsLimit = 160 * 1024 - 1024;
+
+// Variants (RenderArgs::waves, tuning knob): 0 = default (LDS if it fits).
+template <int MAXF, bool FROM_RAYS>
+static hipError_t launch_render_t(const DevScene& sc, const DevCamera& cam, const RenderArgs& a,
+                                  hipStream_t s) {
+  const bool fits = lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes) <= kLdsLimit;
+  switch (a.waves) {
+    case 3: return launch_render_w<MAXF, FROM_RAYS, 256, 3, false>(sc, cam, a, s);
+    case 4: return launch_render_w<MAXF, FROM_RAYS, 256, 4, false>(sc, cam, a, s);
+    case 20:  // diagnostic build: s_memtime around every trace step (never the default)
+      if (fits && !FROM_RAYS) return launch_render_w<MAXF, FROM_RAYS, 768, 3, true, 0, true>(sc, cam, a, s);
+      return launch_render_w<MAXF, FROM_RAYS, 256, kDefaultWaves, false, 0, true>(sc, cam, a, s);
+    case 10:
+      if (fits && !FROM_RAYS) return launch_render_w<MAXF, FROM_RAYS, 768, 3, true, 1>(sc, cam, a, s);
+      return launch_render_w<MAXF, FROM_RAYS, 256, kDefaultWaves, false>(sc, cam, a, s);
+    default:
+      if (fits && !FROM_RAYS) return launch_render_w<MAXF, FROM_RAYS, 768, 3, true>(sc, cam, a, s);
+      return launch_render_w<MAXF, FROM_RAYS, 256, kDefaultWaves, false>(sc, cam, a, s);
+  }
 }
 
 template <bool FROM_RAYS>

@@ -8,6 +8,7 @@
 namespace rtamd {
 
 constexpr int kMaxDepth = 64;  // deepest recursion a launch supports
+constexpr int kDefaultWaves = 3;  // min waves/SIMD the render kernel is compiled for
 
 struct RenderArgs {
   double* out;              // device: n_tasks * 3 doubles
@@ -18,6 +19,7 @@ struct RenderArgs {
   uint32_t max_depth;       // MAX_RECURSION_DEPTH (world.rs:16) / `remaining`
   uint32_t row_block, shard, n_shards;
   int grid_cap;             // 0 = occupancy-limited persistent grid
+  int waves;                // occupancy variant (0 = kDefaultWaves); tuning knob
 };
 
 hipError_t launch_render(const DevScene& sc, const DevCamera& cam, const RenderArgs& args,

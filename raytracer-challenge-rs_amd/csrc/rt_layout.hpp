@@ -74,6 +74,8 @@ struct DevCamera {
 struct DevStats {
   unsigned long long rays_primary, rays_reflect, rays_refract, rays_shadow;
   unsigned long long sphere_tests, plane_tests, sphere_disc_ge0;
+  unsigned long long wave_steps;    // diagnostic: wave-level trace steps
+  unsigned long long diag_trace_cycles, diag_total_cycles;  // DIAG variant only (s_memtime)
   unsigned long long pad;
 };
 

@@ -1,0 +1,19 @@
+#!/bin/bash
+# Profile the bench workload: kernel-trace stats + PMC passes (one counter group per run,
+# never combined with sys/runtime traces). Usage: bash tools/gpu_prof.sh TAG [bench args]
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
+TAG=${1:-r01}; shift
+ARGS="--steps 3 --warmup 1 --no-cpu-baseline $*"
+OUT=gpurun_out/prof_$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+run() { name=$1; shift; timeout -k 10 300 rocprofv3 "$@" -d $OUT/$name -o $name --output-format csv -- python bench.py $ARGS > $OUT/$name.log 2>&1; rc=$?; echo "$name rc=$rc" | tee -a $OUT/steps.log; return $rc; }
+run kt --kernel-trace --stats && \
+run p1 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE && \
+run p2 --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_INSTS_VMEM && \
+run p3 --pmc SQC_DCACHE_HITS SQC_DCACHE_MISSES SQC_DCACHE_REQ SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_ANY SQ_INST_LEVEL_SMEM SQ_WAVES_EQ_64 && \
+run p4 --pmc FETCH_SIZE && \
+run p5 --pmc WRITE_SIZE && \
+run p6 --pmc TCC_HIT_sum TCC_MISS_sum && \
+python tools/pmc_summary.py $OUT/pmc_summary.json $OUT/p1 $OUT/p2 $OUT/p3 $OUT/p4 $OUT/p5 $OUT/p6 > /dev/null && echo "summary ok" | tee -a $OUT/steps.log
