@@ -14,8 +14,9 @@ region holds exactly K steps bracketed by barrier + synchronize; the
 reported time is the max over ranks.
 
 Printed JSON line (rank 0): metric/value/unit per BASELINE.json, plus
-  roofline      f64 VALU roofline of the render kernel, kernel time from HIP
-                events on the launch stream inside the timed region
+  roofline      f64 VALU roofline of the dominant trace-kernel class of the
+                wavefront pipeline; kernel time from HIP events the library
+                records on the launch stream inside the timed region
   cpu_baseline  the C oracle (a port of the reference algorithm) on a bounded
                 row sample on this host's cores (N=1, rank 0 only)
 """
@@ -37,11 +38,14 @@ from rtamd import scenes  # noqa: E402
 METRIC = "Mrays/s (primary+secondary) on 1920×1080/1000-sphere/depth-5; 1→8 GPU scaling"
 PEAK_F64_VALU_TFLOPS = 39.3  # 256 CU x 64 f64 lanes/clk x 2.4 GHz, non-fused add/mul (MI355X_MICROARCH.md)
 
-# Executed f64 VALU operations per unit of work (DESIGN.md "Roofline"):
-#   diagonal-inverse sphere test: 9 (object-space ray) + 5 (a) + 5 (d.o) + 6 (c) + 3 (disc) = 28
-#   roots when disc >= 0: sqrt + 2 sub/neg + 2 div, priced as 1+2+2 = 5 (counted per event)
-#   plane test: 6 (o'.y) + 5 (d'.y) + 1 (|d'.y| test) = 12, root division priced 1
-OPS_SPHERE_DIAG = 28
+# Algorithmic f64 operations per unit of work (DESIGN.md "Roofline"): the
+# minimum non-fused add/mul count that reproduces the reference's bits.
+#   sphere test, diagonal inverse:   9 (object-space ray) + 5 (a) + 5 (d.o) + 6 (c) + 3 (disc) = 28
+#   sphere test, primary ray:        3 (d' = s*d) + 5 (a) + 5 (d'.o') + 3 (disc) = 16  (o', c shared per frame)
+#   sphere test, general inverse:   33 (object-space ray) + 5 + 5 + 6 + 3 = 52
+#   roots when disc >= 0:            sqrt + 2 add + 2 div, priced 5
+#   plane test:                      6 (o'.y) + 5 (d'.y) + 1 (|d'.y| compare) = 12
+OPS_SPHERE_DIAG, OPS_SPHERE_PRIMARY, OPS_SPHERE_GEN = 28, 16, 52
 OPS_ROOTS = 5
 OPS_PLANE = 12
 # SURVEY.md §8(d) convention (the reference's general 4x4 path): 57 / 34 / +6
@@ -132,12 +136,8 @@ def main():
         dst_idx = torch.tensor(dst, device=dev)
     stream = torch.cuda.current_stream()
 
-    def step(ev=None):
-        if ev is not None:
-            ev[0].record(stream)
+    def step():
         cam.render_shard_device(world, depth, B, rank, n, shard.data_ptr(), stream.cuda_stream, False)
-        if ev is not None:
-            ev[1].record(stream)
         if n > 1:
             dist.gather(shard, gathered if rank == 0 else None, dst=0)
             if rank == 0:
@@ -145,6 +145,7 @@ def main():
         # n == 1: the shard buffer already is the row-major canvas
 
     # exact work counters of one frame (deterministic), from a counted warm-up launch
+    # (this first launch also sizes the wavefront queues of this camera/shard)
     st = cam.render_shard_device(world, depth, B, rank, n, shard.data_ptr(), stream.cuda_stream, True)
     counts = torch.tensor([st["rays_primary"], st["rays_reflect"], st["rays_refract"], st["rays_shadow"],
                            st["sphere_tests"], st["plane_tests"], st["sphere_disc_ge0"]],
@@ -156,39 +157,28 @@ def main():
         step()
     torch.cuda.synchronize()
 
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    # Timed region. The library records HIP events around every kernel launch
+    # on the launch stream (per kernel class) while profiling is enabled.
+    rtamd._rtamd._wf_profile(world, 1, False)
     if n > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(a.steps):
-        step(evs[k])
+    for _ in range(a.steps):
+        step()
     torch.cuda.synchronize()
     if n > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kernel_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / a.steps
-    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+    prof = rtamd._rtamd._wf_profile(world, 0, True)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if n > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kernel_ms = float(t[0]), float(t[1])
+    elapsed = float(t[0])
 
     if rank == 0:
         value = rays_per_frame * a.steps / elapsed / 1e6
-        # roofline of the render kernel on rank 0 (per launch = this rank's shard)
-        sph, pln, roots = (float(x) for x in (st["sphere_tests"], st["plane_tests"], st["sphere_disc_ge0"]))
-        ops = OPS_SPHERE_DIAG * sph + OPS_PLANE * pln + OPS_ROOTS * roots
-        achieved = ops / (kernel_ms * 1e-3) / 1e12
-        survey_ops = SURVEY_OPS_SPHERE * sph + SURVEY_OPS_PLANE * pln + SURVEY_OPS_ROOTS * roots
-        traffic, traffic_src = None, None
-        if os.path.exists(a.pmc_summary):
-            try:
-                pm = json.load(open(a.pmc_summary))
-                if (pm.get("width"), pm.get("height"), pm.get("spheres"), pm.get("n_gpus")) == (W, H, a.spheres, n):
-                    traffic, traffic_src = pm.get("hbm_bytes_per_launch"), os.path.relpath(a.pmc_summary, REPO)
-            except Exception:
-                pass
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -207,29 +197,67 @@ def main():
                             f"1 light, reflect+refract depth {depth}",
                 "width": W, "height": H, "spheres": a.spheres, "depth": depth,
                 "rays_per_frame": int(rays_per_frame),
-                "parallelism": f"{n} GPU(s): interleaved {B}-row blocks, RCCL gather to rank 0" if n > 1
-                               else "1 GPU: persistent render kernel",
+                "parallelism": f"{n} GPUs, one process each: interleaved {B}-row blocks, RCCL gather to rank 0"
+                               if n > 1 else "1 GPU: wavefront pipeline",
             },
-            "roofline": {
-                "bound": "valu_f64",
-                "achieved": round(achieved, 3),
-                "peak": PEAK_F64_VALU_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_F64_VALU_TFLOPS, 4),
-                "traffic": traffic,
-                "kernel_ms": round(kernel_ms, 4),
-                "ops_per_launch": ops,
-                "per_unit": f"{OPS_SPHERE_DIAG} f64 ops/sphere test + {OPS_PLANE}/plane test + "
-                            f"{OPS_ROOTS}/root pair (DESIGN.md 'Roofline')",
-                "survey_convention_tflops": round(survey_ops / (kernel_ms * 1e-3) / 1e12, 3),
-                "traffic_source": traffic_src,
-            },
+            "roofline": roofline(prof, W, H, a, n),
         }
         if n == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(world, cam, depth, a.cpu_seconds)
         print(json.dumps(out), flush=True)
     if n > 1:
         dist.destroy_process_group()
+
+
+def roofline(prof, W, H, a, n):
+    """f64 VALU roofline of the dominant trace-kernel class (its launches in
+    one frame on rank 0), from the library's HIP events over the timed region."""
+    nd, ng, npl = prof["n_diag"], prof["n_gen"], prof["n_planes"]
+    per_ray = {"primary": OPS_SPHERE_PRIMARY * nd + OPS_SPHERE_GEN * ng + OPS_PLANE * npl,
+               "closest": OPS_SPHERE_DIAG * nd + OPS_SPHERE_GEN * ng + OPS_PLANE * npl,
+               "shadow": OPS_SPHERE_DIAG * nd + OPS_SPHERE_GEN * ng + OPS_PLANE * npl}
+    kernels = {}
+    for c in ("primary", "closest", "shadow"):
+        ms_c = prof["ms"][c]
+        ops_c = prof["rays"][c] * per_ray[c] + OPS_ROOTS * prof["disc"][c]
+        kernels[c] = {"ms_per_frame": round(ms_c, 4), "rays": int(prof["rays"][c]),
+                      "tflops": round(ops_c / (ms_c * 1e-3) / 1e12, 3) if ms_c > 0 else None}
+    for c in ("prep", "combine"):
+        kernels[c] = {"ms_per_frame": round(prof["ms"][c], 4)}
+    dom = max(("primary", "closest", "shadow"), key=lambda c: prof["ms"][c])
+    kernel_ms = prof["ms"][dom]
+    if kernel_ms <= 0:  # megakernel variant selected (RTAMD_WAVES=1): no per-class events
+        return {"bound": "valu_f64", "kernel": None, "achieved": None, "peak": PEAK_F64_VALU_TFLOPS,
+                "unit": "TFLOP/s", "frac": None, "traffic": None}
+    ops = prof["rays"][dom] * per_ray[dom] + OPS_ROOTS * prof["disc"][dom]
+    achieved = ops / (kernel_ms * 1e-3) / 1e12
+    survey_ops = (SURVEY_OPS_SPHERE * (nd + ng) + SURVEY_OPS_PLANE * npl) * prof["rays"][dom] + \
+        SURVEY_OPS_ROOTS * prof["disc"][dom]
+    traffic, traffic_src = None, None
+    if os.path.exists(a.pmc_summary):
+        try:
+            pm = json.load(open(a.pmc_summary))
+            if (pm.get("width"), pm.get("height"), pm.get("spheres"), pm.get("n_gpus"),
+                    pm.get("kernel_class")) == (W, H, a.spheres, n, dom):
+                traffic, traffic_src = pm.get("hbm_bytes_per_frame"), os.path.relpath(a.pmc_summary, REPO)
+        except Exception:
+            pass
+    return {
+        "bound": "valu_f64",
+        "kernel": f"wf_trace_{dom}: its launches in one frame",
+        "achieved": round(achieved, 3),
+        "peak": PEAK_F64_VALU_TFLOPS,
+        "unit": "TFLOP/s",
+        "frac": round(achieved / PEAK_F64_VALU_TFLOPS, 4),
+        "traffic": traffic,
+        "kernel_ms": round(kernel_ms, 4),
+        "ops_per_frame": ops,
+        "per_unit": f"{OPS_SPHERE_DIAG} f64 ops per sphere test ({OPS_SPHERE_PRIMARY} for primary rays), "
+                    f"{OPS_PLANE} per plane test, {OPS_ROOTS} per root pair (DESIGN.md 'Roofline')",
+        "survey_convention_tflops": round(survey_ops / (kernel_ms * 1e-3) / 1e12, 3),
+        "traffic_source": traffic_src,
+        "kernels": kernels,
+    }
 
 
 if __name__ == "__main__":

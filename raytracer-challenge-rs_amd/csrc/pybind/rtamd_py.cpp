@@ -37,6 +37,7 @@ static py::array_t<double> check_rays(py::array_t<double, py::array::c_style | p
 
 extern "C" int rtamd_tuning_set(const char* key, int value);
 extern "C" int rtamd_diag_last(const rt_scene* s, unsigned long long out[3]);
+extern "C" int rtamd_wf_profile(const rt_scene* s, int enable, double out[16]);
 
 PYBIND11_MODULE(_rtamd, m) {
   m.doc() = "MI355X-native render path of raytracer-challenge-rs (host API over the C-ABI)";
@@ -321,5 +322,19 @@ PYBIND11_MODULE(_rtamd, m) {
     check(rtamd_diag_last(w.scene(), o), "diag");
     return py::make_tuple(o[0], o[1], o[2]);
   });
+  m.def("_wf_profile", [](const World& w, int enable, bool read) {
+    double o[16] = {0};
+    check(rtamd_wf_profile(w.scene(), enable, read ? o : nullptr), "wf_profile");
+    py::dict d;
+    if (read) {
+      const char* cls[5] = {"primary", "closest", "shadow", "prep", "combine"};
+      py::dict ms, rays, disc;
+      for (int i = 0; i < 5; ++i) ms[cls[i]] = o[i];
+      for (int i = 0; i < 3; ++i) { rays[cls[i]] = o[5 + i]; disc[cls[i]] = o[8 + i]; }
+      d["ms"] = ms; d["rays"] = rays; d["disc"] = disc;
+      d["n_diag"] = o[11]; d["n_gen"] = o[12]; d["n_planes"] = o[13]; d["n_lights"] = o[14];
+    }
+    return d;
+  }, py::arg("world"), py::arg("enable") = -1, py::arg("read") = true);
   m.def("_tuning_set", [](const std::string& k, int v) { check(rtamd_tuning_set(k.c_str(), v), "tuning"); });
 }

@@ -21,6 +21,7 @@
 #include "host/rt_math.hpp"
 #include "rt_kernels.hpp"
 #include "rt_layout.hpp"
+#include "rt_wavefront.hpp"
 
 using namespace rtamd;
 
@@ -62,6 +63,7 @@ struct rt_scene {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::mutex mu;  // one call at a time per scene (shared workspace)
+  Wavefront wf;   // wavefront pipeline workspace (queues grow on demand)
   int n_objects = 0, n_lights = 0;
 };
 
@@ -141,28 +143,33 @@ DevCamera to_dev_camera(const rt_camera_desc& c) {
   return d;
 }
 
-int copy_stats(rt_scene* s, rt_stats* st, float ms_kernel, double ms_total) {
-  DevStats ds{};
-  RT_HIP(hipMemcpyAsync(&ds, s->d_stats, sizeof ds, hipMemcpyDeviceToHost, s->stream));
-  RT_HIP(hipStreamSynchronize(s->stream));
-  st->rays_primary = ds.rays_primary;
-  st->rays_reflect = ds.rays_reflect;
-  st->rays_refract = ds.rays_refract;
-  st->rays_shadow = ds.rays_shadow;
-  st->sphere_tests = ds.sphere_tests;
-  st->plane_tests = ds.plane_tests;
-  st->sphere_disc_ge0 = ds.sphere_disc_ge0;
-  st->ms_kernel = ms_kernel;
-  st->ms_total = ms_total;
-  return RT_OK;
-}
-
-// Launch one render (camera shard or ray batch) on the scene's stream.
+// Launch one render (camera shard or ray batch) on `stream`. Default: the
+// wavefront pipeline; tuning knob `waves` != 0 selects the persistent
+// megakernel variants (1 = its default). `timed` records kernel events;
+// `stats_out`, when given, receives the exact counters (synchronises).
 int run_render(rt_scene* s, const DevCamera& cam, const double* d_rays, uint32_t n_tasks,
                uint32_t max_depth, uint32_t row_block, uint32_t shard, uint32_t n_shards,
-               double* d_out, hipStream_t stream, bool timed) {
+               double* d_out, hipStream_t stream, bool timed, DevStats* stats_out = nullptr,
+               float* ms_out = nullptr) {
   if (max_depth > (uint32_t)kMaxDepth)
     return fail(RT_ERR_INVALID_ARGUMENT, "max_depth > " + std::to_string(kMaxDepth));
+  if (g_tune_waves == 0) {
+    std::string sig;
+    if (!d_rays) {  // camera renders are deterministic per (camera, shard, depth)
+      sig.assign((const char*)&cam, sizeof cam);
+      const uint32_t p[5] = {n_tasks, max_depth, row_block, shard, n_shards};
+      sig.append((const char*)p, sizeof p);
+    }
+    if (n_tasks == 0) {
+      if (stats_out) *stats_out = DevStats{};
+      if (ms_out) *ms_out = 0.f;
+      return RT_OK;
+    }
+    hipError_t e = s->wf.render(s->dev, cam, d_rays == nullptr, d_rays, n_tasks, max_depth, row_block, shard,
+                                n_shards, d_out, stream, sig, stats_out, (timed || ms_out) ? ms_out : nullptr);
+    if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("wavefront render: ") + hipGetErrorString(e));
+    return RT_OK;
+  }
   RenderArgs a{};
   a.out = d_out;
   a.rays = d_rays;
@@ -174,14 +181,35 @@ int run_render(rt_scene* s, const DevCamera& cam, const double* d_rays, uint32_t
   a.shard = shard;
   a.n_shards = n_shards;
   a.grid_cap = 0;
-  a.waves = g_tune_waves;
+  a.waves = g_tune_waves == 1 ? 0 : g_tune_waves;
   RT_HIP(hipMemsetAsync(s->d_counter, 0, 64, stream));
   RT_HIP(hipMemsetAsync(s->d_stats, 0, sizeof(DevStats), stream));
-  if (n_tasks == 0) return RT_OK;
-  if (timed) RT_HIP(hipEventRecord(s->ev0, stream));
+  if (n_tasks == 0) {
+    if (stats_out) *stats_out = DevStats{};
+    if (ms_out) *ms_out = 0.f;
+    return RT_OK;
+  }
+  RT_HIP(hipEventRecord(s->ev0, stream));
   RT_HIP(launch_render(s->dev, cam, a, stream));
-  if (timed) RT_HIP(hipEventRecord(s->ev1, stream));
+  RT_HIP(hipEventRecord(s->ev1, stream));
+  if (stats_out || ms_out) {
+    RT_HIP(hipStreamSynchronize(stream));
+    if (ms_out) RT_HIP(hipEventElapsedTime(ms_out, s->ev0, s->ev1));
+    if (stats_out) RT_HIP(hipMemcpy(stats_out, s->d_stats, sizeof(DevStats), hipMemcpyDeviceToHost));
+  }
   return RT_OK;
+}
+
+void fill_stats(rt_stats* st, const DevStats& ds, float ms_kernel, double ms_total) {
+  st->rays_primary = ds.rays_primary;
+  st->rays_reflect = ds.rays_reflect;
+  st->rays_refract = ds.rays_refract;
+  st->rays_shadow = ds.rays_shadow;
+  st->sphere_tests = ds.sphere_tests;
+  st->plane_tests = ds.plane_tests;
+  st->sphere_disc_ge0 = ds.sphere_disc_ge0;
+  st->ms_kernel = ms_kernel;
+  st->ms_total = ms_total;
 }
 
 }  // namespace
@@ -204,10 +232,35 @@ int rtamd_diag_last(const rt_scene* s, unsigned long long out[3]) {
   return RT_OK;
 }
 
+// Development/benchmark hook (not in the public ABI): per-kernel-class timing
+// of the wavefront pipeline. enable: 1 = on, 0 = off, -1 = just read. out[16]:
+// ms[5] (primary, closest, shadow, prep, combine), rays[3], disc[3],
+// n_diag, n_gen, n_planes.
+int rtamd_wf_profile(const rt_scene* cs, int enable, double out[16]) {
+  if (!cs) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
+  rt_scene* s = const_cast<rt_scene*>(cs);
+  std::lock_guard<std::mutex> lk(s->mu);
+  if (enable >= 0) s->wf.set_profiling(enable != 0);
+  if (out) {
+    RT_HIP(hipSetDevice(s->device));
+    WfProfile p;
+    RT_HIP(s->wf.last_profile(&p));
+    for (int i = 0; i < 5; ++i) out[i] = p.ms[i];
+    for (int i = 0; i < 3; ++i) { out[5 + i] = p.rays[i]; out[8 + i] = p.disc[i]; }
+    out[11] = s->dev.n_diag; out[12] = s->dev.n_gen; out[13] = s->dev.n_planes;
+    out[14] = s->dev.n_lights; out[15] = 0;
+  }
+  return RT_OK;
+}
+
 // Development-only tuning hook (not declared in include/rt_render.h).
 int rtamd_tuning_set(const char* key, int value) {
   if (key && std::strcmp(key, "waves") == 0) {
     g_tune_waves = value;
+    return RT_OK;
+  }
+  if (key && std::strcmp(key, "wf_waves") == 0) {
+    rtamd::g_wf_trace_waves = value;
     return RT_OK;
   }
   return fail(RT_ERR_INVALID_ARGUMENT, "unknown tuning key");
@@ -416,23 +469,13 @@ int rt_render_shard_device(const rt_scene* scene, const rt_camera_desc* camera, 
   const uint64_t n_tasks = (uint64_t)rows * camera->hsize;
   if (n_tasks >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "shard too large");
   hipStream_t st = (hipStream_t)stream;  // NULL = the default stream (torch's current stream is often 0)
+  DevStats ds{};
+  float ms = 0.f;
   int rc = run_render(s, to_dev_camera(*camera), nullptr, (uint32_t)n_tasks, max_depth, row_block, shard,
-                      n_shards, d_out_rgb, st, stats != nullptr);
+                      n_shards, d_out_rgb, st, stats != nullptr, stats ? &ds : nullptr, stats ? &ms : nullptr);
   if (rc != RT_OK) return rc;
-  if (stats) {
-    RT_HIP(hipStreamSynchronize(st));
-    float ms = 0.f;
-    if (n_tasks) RT_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
-    double tot = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    DevStats ds{};
-    RT_HIP(hipMemcpy(&ds, s->d_stats, sizeof ds, hipMemcpyDeviceToHost));
-    stats->rays_primary = ds.rays_primary; stats->rays_reflect = ds.rays_reflect;
-    stats->rays_refract = ds.rays_refract; stats->rays_shadow = ds.rays_shadow;
-    stats->sphere_tests = ds.sphere_tests; stats->plane_tests = ds.plane_tests;
-    stats->sphere_disc_ge0 = ds.sphere_disc_ge0;
-    stats->ms_kernel = ms;
-    stats->ms_total = tot;
-  }
+  if (stats)
+    fill_stats(stats, ds, ms, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
   return RT_OK;
 }
 
@@ -448,17 +491,15 @@ int rt_render(const rt_scene* scene, const rt_camera_desc* camera, uint32_t max_
   if (n >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "canvas too large for one launch");
   int rc = ensure_dev_buffer(&s->d_out, &s->out_cap, n * 3);
   if (rc != RT_OK) return rc;
+  DevStats ds{};
+  float ms = 0.f;
   rc = run_render(s, to_dev_camera(*camera), nullptr, (uint32_t)n, max_depth, camera->vsize, 0, 1, s->d_out,
-                  s->stream, true);
+                  s->stream, true, stats ? &ds : nullptr, &ms);
   if (rc != RT_OK) return rc;
   RT_HIP(hipMemcpyAsync(out_rgb, s->d_out, n * 3 * sizeof(double), hipMemcpyDeviceToHost, s->stream));
   RT_HIP(hipStreamSynchronize(s->stream));
-  if (stats) {
-    float ms = 0.f;
-    if (n) RT_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
-    double tot = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    return copy_stats(s, stats, ms, tot);
-  }
+  if (stats)
+    fill_stats(stats, ds, ms, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
   return RT_OK;
 }
 
@@ -476,16 +517,15 @@ int rt_color_at_batch(const rt_scene* scene, const double* rays, size_t n, uint3
   if (rc != RT_OK) return rc;
   if (n) RT_HIP(hipMemcpyAsync(s->d_in, rays, n * 6 * sizeof(double), hipMemcpyHostToDevice, s->stream));
   DevCamera cam{};
-  rc = run_render(s, cam, s->d_in, (uint32_t)n, remaining, 1, 0, 1, s->d_out, s->stream, true);
+  DevStats ds{};
+  float ms = 0.f;
+  rc = run_render(s, cam, s->d_in, (uint32_t)n, remaining, 1, 0, 1, s->d_out, s->stream, true, stats ? &ds : nullptr,
+                  &ms);
   if (rc != RT_OK) return rc;
   if (n) RT_HIP(hipMemcpyAsync(out_rgb, s->d_out, n * 3 * sizeof(double), hipMemcpyDeviceToHost, s->stream));
   RT_HIP(hipStreamSynchronize(s->stream));
-  if (stats) {
-    float ms = 0.f;
-    if (n) RT_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
-    double tot = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    return copy_stats(s, stats, ms, tot);
-  }
+  if (stats)
+    fill_stats(stats, ds, ms, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
   return RT_OK;
 }
 
@@ -566,7 +606,7 @@ int rt_render_multi(rt_scene* const* scenes, int n_devices, const rt_camera_desc
       std::lock_guard<std::mutex> lk(scenes[i]->mu);
       const uint32_t rows = rt_shard_rows(H, row_block, i, n_devices);
       int r = run_render(scenes[i], to_dev_camera(*camera), nullptr, rows * W, max_depth, row_block, i, n_devices,
-                         send[i], scenes[i]->stream, true);
+                         send[i], scenes[i]->stream, false);
       if (r != RT_OK) return r;
     }
     if (n_devices > 1) {
@@ -583,14 +623,20 @@ int rt_render_multi(rt_scene* const* scenes, int n_devices, const rt_camera_desc
     for (int i = 0; i < n_devices; ++i) {
       RT_HIP(hipSetDevice(i));
       RT_HIP(hipStreamSynchronize(scenes[i]->stream));
-      float ms = 0.f;
-      RT_HIP(hipEventElapsedTime(&ms, scenes[i]->ev0, scenes[i]->ev1));
-      DevStats ds{};
-      RT_HIP(hipMemcpy(&ds, scenes[i]->d_stats, sizeof ds, hipMemcpyDeviceToHost));
-      st[i].rays_primary = ds.rays_primary; st[i].rays_reflect = ds.rays_reflect;
-      st[i].rays_refract = ds.rays_refract; st[i].rays_shadow = ds.rays_shadow;
-      st[i].sphere_tests = ds.sphere_tests; st[i].plane_tests = ds.plane_tests;
-      st[i].sphere_disc_ge0 = ds.sphere_disc_ge0; st[i].ms_kernel = ms;
+    }
+    // exact counters: one more counted render per device (same deterministic work)
+    if (stats) {
+      for (int i = 0; i < n_devices; ++i) {
+        RT_HIP(hipSetDevice(i));
+        std::lock_guard<std::mutex> lk(scenes[i]->mu);
+        const uint32_t rows = rt_shard_rows(H, row_block, i, n_devices);
+        DevStats ds{};
+        float ms = 0.f;
+        int r = run_render(scenes[i], to_dev_camera(*camera), nullptr, rows * W, max_depth, row_block, i, n_devices,
+                           send[i], scenes[i]->stream, true, &ds, &ms);
+        if (r != RT_OK) return r;
+        fill_stats(&st[i], ds, ms, 0.0);
+      }
     }
     // un-interleave rank-major rows into the canvas
     std::vector<double> host(per * n_devices);

@@ -1,0 +1,730 @@
+// rt_wavefront.hip — the wavefront render pipeline (see rt_wavefront.hpp).
+//
+// Why wavefront on MI355X: the work per ray is a brute-force loop over every
+// shape (the reference's `World::intersect`), identical for every ray of a
+// kind. Flat per-generation queues keep every lane of every wave busy (no
+// recursion-tree tail), and the trace kernels are small loops with few live
+// registers, so 8 waves per SIMD hide the ~20-cycle dependent f64 latency.
+// Primary rays share the camera origin, so their object-space origin o' and
+// c = o'.o' - 1 are computed once per sphere per frame (exactly the same
+// operations, so bit-identical) and each primary sphere test drops from 28 to
+// 16 f64 operations.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "rt_device.hpp"
+#include "rt_wavefront.hpp"
+
+#pragma clang fp contract(off)
+
+namespace rtamd {
+
+constexpr int kTraceBlock = 1024;  // trace kernels: 16 waves, one LDS image per block
+// Occupancy of the trace kernels (min waves per SIMD for the register
+// allocator): 8 = two 1024-thread blocks per CU (<= 64 VGPRs), 4 = one.
+int g_wf_trace_waves = 8;  // tuning knob (rtamd_tuning_set("wf_waves", n))
+constexpr int kWfBlock = 256;      // prep / shadow / combine
+
+#define WF_CHECK(x)                        \
+  do {                                     \
+    hipError_t _e = (x);                   \
+    if (_e != hipSuccess) return _e;       \
+  } while (0)
+
+__device__ __forceinline__ unsigned lane_id() { return __lane_id(); }
+
+// Wave-aggregated queue append: every active lane calls it (convergent);
+// lanes with want=true get consecutive slots (in lane order) of `per` entries.
+__device__ __forceinline__ unsigned wave_append(unsigned* counter, bool want, unsigned per) {
+  const unsigned long long m = __ballot(want);
+  if (m == 0) return 0;
+  const int leader = __ffsll((long long)m) - 1;
+  unsigned base = 0;
+  if ((int)lane_id() == leader) base = atomicAdd(counter, (unsigned)__popcll(m) * per);
+  base = __shfl(base, leader, 64);
+  const unsigned rank = (unsigned)__popcll(m & ((1ull << lane_id()) - 1ull));
+  return base + rank * per;
+}
+
+// Root rays of generation 0: camera pixel of the shard (camera.rs:57-69) or
+// an explicit ray; deeper generations read their queue.
+__device__ __forceinline__ void wf_ray(const WfArgs& a, const DevCamera& cam, unsigned i, V3& o, V3& d) {
+  if (a.g == 0 && a.camera_mode) {
+    const uint32_t lr = i / cam.hsize, x = i - lr * cam.hsize;
+    const uint32_t blk = lr / a.row_block, off = lr - blk * a.row_block;
+    const uint32_t y = (blk * a.n_shards + a.shard) * a.row_block + off;
+    ray_for_pixel(cam, x, y, o, d);
+  } else {
+    const WfRay& r = a.rays[i];
+    o = v3(r.o[0], r.o[1], r.o[2]);
+    d = v3(r.d[0], r.d[1], r.d[2]);
+  }
+}
+
+// ------------------------------------------------------------ primary records
+// Per diagonal sphere: s (inverse diagonal), o' = s*o + t for the camera origin
+// o, and c = o'.o' - 1 — the same operations the general test performs, so the
+// values are bit-identical to what each primary ray would compute.
+__global__ void wf_prim_prep(DevScene sc, DevCamera cam, PrimRec* prim) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= sc.n_diag + 4) return;
+  PrimRec p{};
+  if (j < sc.n_diag) {
+    const V3 o = m34_point(cam.inv, v3(0.0, 0.0, 0.0));  // camera.rs:65
+    const SphereDiag& r = sc.sph_diag[j];
+    p.s[0] = r.s[0]; p.s[1] = r.s[1]; p.s[2] = r.s[2];
+    p.op[0] = r.s[0] * o.x + r.t[0];
+    p.op[1] = r.s[1] * o.y + r.t[1];
+    p.op[2] = r.s[2] * o.z + r.t[2];
+    p.c = p.op[0] * p.op[0] + p.op[1] * p.op[1] + p.op[2] * p.op[2] - 1.0;
+  }
+  prim[j] = p;  // j >= n_diag: zero padding records
+}
+
+// LDS image for the trace kernels: [diag or prim records][gen][planes][metas]
+struct WfLds {
+  const double* diag;  // 6 doubles per record (general) or 8 (primary)
+  const double* gen;
+  const double* plane;
+  const int* diag_meta;
+  const int* gen_meta;
+  const int* plane_meta;
+};
+__host__ __device__ inline size_t wf_lds_bytes(int nd, int ng, int np, bool primary) {
+  return lds_align16((size_t)(nd + 4) * (primary ? 64 : 48)) + lds_align16((size_t)ng * 96) +
+         lds_align16((size_t)np * 32) + lds_align16((size_t)nd * 4) + lds_align16((size_t)ng * 4) +
+         lds_align16((size_t)np * 4);
+}
+template <bool PRIMARY>
+__device__ WfLds wf_lds_stage(const DevScene& sc, const PrimRec* prim, unsigned char* base) {
+  WfLds v;
+  size_t off = 0;
+  const int rec = PRIMARY ? 8 : 6;
+  v.diag = (const double*)(base + off); off += lds_align16((size_t)(sc.n_diag + 4) * rec * 8);
+  v.gen = (const double*)(base + off); off += lds_align16((size_t)sc.n_gen * 96);
+  v.plane = (const double*)(base + off); off += lds_align16((size_t)sc.n_planes * 32);
+  v.diag_meta = (const int*)(base + off); off += lds_align16((size_t)sc.n_diag * 4);
+  v.gen_meta = (const int*)(base + off); off += lds_align16((size_t)sc.n_gen * 4);
+  v.plane_meta = (const int*)(base + off);
+  double* dd = (double*)v.diag;
+  if constexpr (PRIMARY) {
+    const double* src = (const double*)prim;
+    for (int i = threadIdx.x; i < (sc.n_diag + 4) * 8; i += blockDim.x) dd[i] = src[i];
+  } else {
+    for (int i = threadIdx.x; i < (sc.n_diag + 4) * 6; i += blockDim.x) {
+      const int r = i / 6, e = i - r * 6;
+      dd[i] = r >= sc.n_diag ? 0.0 : e < 3 ? sc.sph_diag[r].s[e] : sc.sph_diag[r].t[e - 3];
+    }
+  }
+  for (int i = threadIdx.x; i < sc.n_gen * 12; i += blockDim.x) ((double*)v.gen)[i] = sc.sph_gen[i / 12].m[i % 12];
+  for (int i = threadIdx.x; i < sc.n_planes * 4; i += blockDim.x) ((double*)v.plane)[i] = sc.planes[i / 4].m[i % 4];
+  for (int i = threadIdx.x; i < sc.n_diag; i += blockDim.x) ((int*)v.diag_meta)[i] = (int)sc.sph_diag[i].meta;
+  for (int i = threadIdx.x; i < sc.n_gen; i += blockDim.x) ((int*)v.gen_meta)[i] = (int)sc.sph_gen[i].meta;
+  for (int i = threadIdx.x; i < sc.n_planes; i += blockDim.x) ((int*)v.plane_meta)[i] = (int)sc.planes[i].meta;
+  __syncthreads();
+  return v;
+}
+
+// The sphere test from (a, dt, c) — sphere.rs:47-62 as in sphere_roots_lazy.
+__device__ __forceinline__ void sphere_from_adc(double a, double dt, double c, const int* meta_p, bool shadow_mode,
+                                                Hit& h, unsigned& n_disc) {
+  const double disc = dt * dt - a * c;
+  if (disc >= 0.0) {
+    ++n_disc;
+    const int meta = *meta_p;
+    const double q = sqrt(disc);
+    const double t1 = (-dt - q) / a;
+    const double t2 = (-dt + q) / a;
+    const int k1 = (meta >> 1) * 2;
+    const bool eligible = !shadow_mode || (meta & 1);
+    if (eligible) {
+      if (t1 >= 0.0) {
+        if (better(t1, k1, h.t, h.key)) { h.t = t1; h.key = k1; }
+      } else if (t2 >= 0.0) {
+        if (better(t2, k1 + 1, h.t, h.key)) { h.t = t2; h.key = k1 + 1; }
+      }
+    }
+    if (t1 < 0.0 && t2 >= 0.0) push_container(h, t1, k1);
+  }
+}
+
+// World::intersect + hit over the LDS image (closest hit + containers top-2).
+template <bool PRIMARY>
+__device__ __forceinline__ void wf_trace_lds(const DevScene& sc, const WfLds& lv, V3 o, V3 d, Hit& h,
+                                             unsigned& n_disc) {
+  h.t = INFINITY;
+  h.c1t = -INFINITY; h.c2t = -INFINITY; h.c1k = -1; h.c2k = -1;
+  h.key = 0x7fffffff;
+  const d2* r = (const d2*)lv.diag;
+  if constexpr (PRIMARY) {
+    // record: (s0 s1) (s2 o'x) (o'y o'z) (c pad); 16 f64 ops per test
+    d2 a0 = r[0], a1 = r[1], a2 = r[2], a3 = r[3];
+    int j = 0;
+    for (; j + 1 < sc.n_diag; j += 2) {
+      const d2 b0 = r[4 * j + 4], b1 = r[4 * j + 5], b2 = r[4 * j + 6], b3 = r[4 * j + 7];
+      {
+        const double dx = a0.x * d.x, dy = a0.y * d.y, dz = a1.x * d.z;
+        const double a = dx * dx + dy * dy + dz * dz;
+        const double dt = dx * a1.y + dy * a2.x + dz * a2.y;
+        sphere_from_adc(a, dt, a3.x, lv.diag_meta + j, false, h, n_disc);
+      }
+      a0 = r[4 * j + 8]; a1 = r[4 * j + 9]; a2 = r[4 * j + 10]; a3 = r[4 * j + 11];
+      {
+        const double dx = b0.x * d.x, dy = b0.y * d.y, dz = b1.x * d.z;
+        const double a = dx * dx + dy * dy + dz * dz;
+        const double dt = dx * b1.y + dy * b2.x + dz * b2.y;
+        sphere_from_adc(a, dt, b3.x, lv.diag_meta + j + 1, false, h, n_disc);
+      }
+    }
+    if (j < sc.n_diag) {
+      const double dx = a0.x * d.x, dy = a0.y * d.y, dz = a1.x * d.z;
+      const double a = dx * dx + dy * dy + dz * dz;
+      const double dt = dx * a1.y + dy * a2.x + dz * a2.y;
+      sphere_from_adc(a, dt, a3.x, lv.diag_meta + j, false, h, n_disc);
+    }
+  } else {
+    // record: (s0 s1) (s2 t0) (t1 t2); 28 f64 ops per test
+    d2 a0 = r[0], a1 = r[1], a2 = r[2];
+    int j = 0;
+    for (; j + 1 < sc.n_diag; j += 2) {
+      const d2 b0 = r[3 * j + 3], b1 = r[3 * j + 4], b2 = r[3 * j + 5];
+      sphere_roots_lazy(a0.x * o.x + a1.y, a0.y * o.y + a2.x, a1.x * o.z + a2.y, a0.x * d.x, a0.y * d.y,
+                        a1.x * d.z, lv.diag_meta + j, false, h, n_disc);
+      a0 = r[3 * j + 6]; a1 = r[3 * j + 7]; a2 = r[3 * j + 8];
+      sphere_roots_lazy(b0.x * o.x + b1.y, b0.y * o.y + b2.x, b1.x * o.z + b2.y, b0.x * d.x, b0.y * d.y,
+                        b1.x * d.z, lv.diag_meta + j + 1, false, h, n_disc);
+    }
+    if (j < sc.n_diag)
+      sphere_roots_lazy(a0.x * o.x + a1.y, a0.y * o.y + a2.x, a1.x * o.z + a2.y, a0.x * d.x, a0.y * d.y,
+                        a1.x * d.z, lv.diag_meta + j, false, h, n_disc);
+  }
+  for (int j = 0; j < sc.n_gen; ++j) {
+    double m[12];
+#pragma unroll
+    for (int e = 0; e < 12; ++e) m[e] = lv.gen[12 * j + e];
+    const V3 lo = m34_point(m, o);
+    const V3 ld = v3(m[0] * d.x + m[1] * d.y + m[2] * d.z, m[4] * d.x + m[5] * d.y + m[6] * d.z,
+                     m[8] * d.x + m[9] * d.y + m[10] * d.z);
+    sphere_roots_lazy(lo.x, lo.y, lo.z, ld.x, ld.y, ld.z, lv.gen_meta + j, false, h, n_disc);
+  }
+  for (int j = 0; j < sc.n_planes; ++j) {  // plane.rs:53-60
+    const double m0 = lv.plane[4 * j], m1 = lv.plane[4 * j + 1], m2 = lv.plane[4 * j + 2], m3 = lv.plane[4 * j + 3];
+    const double oy = m0 * o.x + m1 * o.y + m2 * o.z + m3;
+    const double dy = m0 * d.x + m1 * d.y + m2 * d.z;
+    if (!(fabs(dy) < kEpsilon)) {
+      const double t = -oy / dy;
+      const int k = (lv.plane_meta[j] >> 1) * 2;
+      if (t >= 0.0 && better(t, k, h.t, h.key)) { h.t = t; h.key = k; }
+      if (t < 0.0) push_container(h, t, k);
+    }
+  }
+  if (h.key == 0x7fffffff) h.key = -1;
+}
+
+// ---------------------------------------------------------- trace kernels
+template <bool USE_LDS, bool PRIMARY, int TW>
+__global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest(DevScene sc, DevCamera cam, WfArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  unsigned n_disc = 0;
+  WfLds lv{};
+  if constexpr (USE_LDS) lv = wf_lds_stage<PRIMARY>(sc, a.prim, lds_raw);
+  const unsigned stride = gridDim.x * blockDim.x;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
+    V3 o, d;
+    wf_ray(a, cam, i, o, d);
+    Hit h;
+    if constexpr (USE_LDS) wf_trace_lds<PRIMARY>(sc, lv, o, d, h, n_disc);
+    else trace<false>(sc, LdsView{}, o, d, false, h, n_disc);
+    WfHit w;
+    w.t = h.t; w.key = h.key; w.c1k = h.c1k; w.c2k = h.c2k; w.pad = 0;
+    a.hits[i] = w;
+  }
+  const unsigned long long s = wave_sum(n_disc);
+  if (lane_id() == 0 && s) atomicAdd(&a.cnt->disc[a.disc_slot], s);
+}
+
+// World::is_shadowed (world.rs:95-105): shadowed iff some shadow-casting
+// object has a root t with 0 <= t < distance (the first t >= 0 among shadow
+// casters in the sorted list is the minimum one). Full traversal: the exact
+// counters (sphere_disc_ge0) need every test.
+template <bool USE_LDS, int TW>
+__global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow(DevScene sc, WfArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  unsigned n_disc = 0;
+  WfLds lv{};
+  if constexpr (USE_LDS) lv = wf_lds_stage<false>(sc, nullptr, lds_raw);
+  const unsigned stride = gridDim.x * blockDim.x;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n_shadow; i += stride) {
+    const WfShadow s = a.shadows[i];
+    const V3 o = v3(s.o[0], s.o[1], s.o[2]);
+    const V3 d = v3(s.d[0], s.d[1], s.d[2]);
+    Hit h;
+    if constexpr (USE_LDS) {
+      // shadow_mode variant of the LDS loop: eligibility = casts_shadow
+      h.t = INFINITY; h.c1t = -INFINITY; h.c2t = -INFINITY; h.c1k = -1; h.c2k = -1; h.key = 0x7fffffff;
+      const d2* r = (const d2*)lv.diag;
+      d2 a0 = r[0], a1 = r[1], a2 = r[2];
+      int j = 0;
+      for (; j + 1 < sc.n_diag; j += 2) {
+        const d2 b0 = r[3 * j + 3], b1 = r[3 * j + 4], b2 = r[3 * j + 5];
+        sphere_roots_lazy(a0.x * o.x + a1.y, a0.y * o.y + a2.x, a1.x * o.z + a2.y, a0.x * d.x, a0.y * d.y,
+                          a1.x * d.z, lv.diag_meta + j, true, h, n_disc);
+        a0 = r[3 * j + 6]; a1 = r[3 * j + 7]; a2 = r[3 * j + 8];
+        sphere_roots_lazy(b0.x * o.x + b1.y, b0.y * o.y + b2.x, b1.x * o.z + b2.y, b0.x * d.x, b0.y * d.y,
+                          b1.x * d.z, lv.diag_meta + j + 1, true, h, n_disc);
+      }
+      if (j < sc.n_diag)
+        sphere_roots_lazy(a0.x * o.x + a1.y, a0.y * o.y + a2.x, a1.x * o.z + a2.y, a0.x * d.x, a0.y * d.y,
+                          a1.x * d.z, lv.diag_meta + j, true, h, n_disc);
+      for (int q = 0; q < sc.n_gen; ++q) {
+        double m[12];
+#pragma unroll
+        for (int e = 0; e < 12; ++e) m[e] = lv.gen[12 * q + e];
+        const V3 lo = m34_point(m, o);
+        const V3 ld = v3(m[0] * d.x + m[1] * d.y + m[2] * d.z, m[4] * d.x + m[5] * d.y + m[6] * d.z,
+                         m[8] * d.x + m[9] * d.y + m[10] * d.z);
+        sphere_roots_lazy(lo.x, lo.y, lo.z, ld.x, ld.y, ld.z, lv.gen_meta + q, true, h, n_disc);
+      }
+      for (int q = 0; q < sc.n_planes; ++q) {
+        const double m0 = lv.plane[4 * q], m1 = lv.plane[4 * q + 1], m2 = lv.plane[4 * q + 2], m3 = lv.plane[4 * q + 3];
+        const double oy = m0 * o.x + m1 * o.y + m2 * o.z + m3;
+        const double dy = m0 * d.x + m1 * d.y + m2 * d.z;
+        if (!(fabs(dy) < kEpsilon)) {
+          const double t = -oy / dy;
+          const int meta = lv.plane_meta[q];
+          if ((meta & 1) && t >= 0.0 && better(t, (meta >> 1) * 2, h.t, h.key)) { h.t = t; h.key = (meta >> 1) * 2; }
+        }
+      }
+      if (h.key == 0x7fffffff) h.key = -1;
+    } else {
+      trace<false>(sc, LdsView{}, o, d, true, h, n_disc);
+    }
+    a.sflags[s.slot] = (h.key >= 0 && h.t < s.dist) ? 1 : 0;
+  }
+  const unsigned long long s = wave_sum(n_disc);
+  if (lane_id() == 0 && s) atomicAdd(&a.cnt->disc[a.disc_slot], s);
+}
+
+// ---------------------------------------------------------- prep (spawn)
+__global__ __launch_bounds__(kWfBlock) void wf_prep(DevScene sc, DevCamera cam, WfArgs a) {
+  const unsigned stride = gridDim.x * blockDim.x;
+  const unsigned L = (unsigned)sc.n_lights;
+  cLightRec lights = (cLightRec)sc.lights;
+  const unsigned remaining = a.max_depth - a.g;
+  // every lane of a wave runs the same number of iterations (appends are convergent)
+  const unsigned n_iter = (a.n + stride - 1) / stride;
+  unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+  for (unsigned it = 0; it < n_iter; ++it, i += stride) {
+    const bool valid = i < a.n;
+    bool hit = false, want_refl = false, want_refr = false;
+    Comps c{};
+    V3 d = v3(0, 0, 0), refr_dir = v3(0, 0, 0);
+    const ShadeRec* m = nullptr;
+    if (valid) {
+      V3 o;
+      wf_ray(a, cam, i, o, d);
+      const WfHit w = a.hits[i];
+      if (w.key >= 0) {
+        Hit h;
+        h.t = w.t; h.key = w.key; h.c1k = w.c1k; h.c2k = w.c2k; h.c1t = 0; h.c2t = 0;
+        c = prepare(sc, o, d, h);
+        hit = true;
+        m = &sc.shade[c.obj];
+        // reflected_color (world.rs:107-114)
+        want_refl = !(req(m->reflective, 0.0) || remaining == 0);
+        // refracted_color (world.rs:116-134)
+        if (!(req(m->transparency, 0.0) || remaining == 0)) {
+          const double n_ratio = c.n1 / c.n2;
+          const double cos_i = vdot(c.eyev, c.normal);
+          const double sin2_t = n_ratio * n_ratio * (1.0 - cos_i * cos_i);
+          if (!(sin2_t > 1.0)) {
+            const double cos_t = sqrt(1.0 - sin2_t);
+            refr_dir = vsub(vscale(c.normal, n_ratio * cos_i - cos_t), vscale(c.eyev, n_ratio));
+            want_refr = true;
+          }
+        }
+      }
+    }
+    // shadow rays: one per light, in light order (world.rs:41-56)
+    const unsigned sbase = wave_append(&a.cnt->n_shadow[a.g], hit && L > 0, L);
+    const unsigned rbase = wave_append(&a.cnt->n_rays[a.g + 1], want_refl, 1);
+    const unsigned fbase = wave_append(&a.cnt->n_rays[a.g + 1], want_refr, 1);
+    if (!valid) continue;
+    WfNode nd;
+    nd.obj = -1; nd.child_refl = -1; nd.child_refr = -1; nd.pad = 0;
+    if (hit) {
+      nd.obj = c.obj;
+      nd.over[0] = c.over.x; nd.over[1] = c.over.y; nd.over[2] = c.over.z;
+      nd.under[0] = c.under.x; nd.under[1] = c.under.y; nd.under[2] = c.under.z;
+      nd.normal[0] = c.normal.x; nd.normal[1] = c.normal.y; nd.normal[2] = c.normal.z;
+      nd.n1 = c.n1; nd.n2 = c.n2;
+      for (unsigned l = 0; l < L; ++l) {
+        cLightRec Lr = lights + l;
+        const V3 v = vsub(v3(Lr->pos[0], Lr->pos[1], Lr->pos[2]), c.over);
+        WfShadow s;
+        s.dist = sqrt(v.x * v.x + v.y * v.y + v.z * v.z);  // magnitude (vector.rs:21-23)
+        const V3 dir = vnormalize(v);
+        s.o[0] = c.over.x; s.o[1] = c.over.y; s.o[2] = c.over.z;
+        s.d[0] = dir.x; s.d[1] = dir.y; s.d[2] = dir.z;
+        s.slot = (int)(i * L + l);
+        s.pad = 0;
+        a.shadows[sbase + l] = s;
+      }
+      if (want_refl && rbase < a.cap_next) {
+        const V3 rv = vreflect(d, c.normal);  // comps.reflectv (intersection.rs:101)
+        WfRay r;
+        r.o[0] = c.over.x; r.o[1] = c.over.y; r.o[2] = c.over.z;
+        r.d[0] = rv.x; r.d[1] = rv.y; r.d[2] = rv.z;
+        r.pad = 0;
+        a.next_rays[rbase] = r;
+        nd.child_refl = (int)rbase;
+      }
+      if (want_refr && fbase < a.cap_next) {
+        WfRay r;
+        r.o[0] = c.under.x; r.o[1] = c.under.y; r.o[2] = c.under.z;
+        r.d[0] = refr_dir.x; r.d[1] = refr_dir.y; r.d[2] = refr_dir.z;
+        r.pad = 0;
+        a.next_rays[fbase] = r;
+        nd.child_refr = (int)fbase;
+      }
+    }
+    a.nodes[i] = nd;
+  }
+}
+
+// ---------------------------------------------------------- combine
+// World::shade_hit (world.rs:40-68) from the node, the shadow flags and the
+// children's colours; color_at miss -> black (world.rs:74-75).
+__global__ __launch_bounds__(kWfBlock) void wf_combine(DevScene sc, DevCamera cam, WfArgs a) {
+  const unsigned stride = gridDim.x * blockDim.x;
+  const unsigned L = (unsigned)sc.n_lights;
+  cLightRec lights = (cLightRec)sc.lights;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
+    const WfNode nd = a.nodes[i];
+    V3 color = v3(0.0, 0.0, 0.0);
+    if (nd.obj >= 0) {
+      V3 o, d;
+      wf_ray(a, cam, i, o, d);
+      const ShadeRec& m = sc.shade[nd.obj];
+      const V3 over = v3(nd.over[0], nd.over[1], nd.over[2]);
+      const V3 normal = v3(nd.normal[0], nd.normal[1], nd.normal[2]);
+      const V3 eyev = vneg(d);
+      V3 surface = v3(0.0, 0.0, 0.0);  // Sum = fold from (0,0,0) (color.rs:96-103)
+      for (unsigned l = 0; l < L; ++l) {
+        const bool shadowed = a.sflags[i * L + l] != 0;
+        surface = vadd(surface, lighting(m, lights + l, over, eyev, normal, shadowed));
+      }
+      V3 refl = v3(0.0, 0.0, 0.0), refr = v3(0.0, 0.0, 0.0);
+      if (nd.child_refl >= 0) {
+        const double* cc = a.child_colors + (size_t)nd.child_refl * 3;
+        refl = vscale(v3(cc[0], cc[1], cc[2]), m.reflective);  // world.rs:113
+      }
+      if (nd.child_refr >= 0) {
+        const double* cc = a.child_colors + (size_t)nd.child_refr * 3;
+        refr = vscale(v3(cc[0], cc[1], cc[2]), m.transparency);  // world.rs:133
+      }
+      if (m.reflective > 0.0 && m.transparency > 0.0) {
+        const double r = schlick(eyev, normal, nd.n1, nd.n2);
+        color = vadd(vadd(surface, vscale(refl, r)), vscale(refr, 1.0 - r));
+      } else {
+        color = vadd(vadd(surface, refl), refr);
+      }
+    }
+    double* out = a.colors + (size_t)i * 3;
+    out[0] = color.x; out[1] = color.y; out[2] = color.z;
+  }
+}
+
+// Reflected / refracted ray counts per generation (stats only).
+__global__ void wf_count_kinds(WfArgs a) {
+  unsigned nrefl = 0, nrefr = 0;
+  const unsigned stride = gridDim.x * blockDim.x;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
+    const WfNode nd = a.nodes[i];
+    nrefl += nd.child_refl >= 0;
+    nrefr += nd.child_refr >= 0;
+  }
+  const unsigned long long s1 = wave_sum(nrefl), s2 = wave_sum(nrefr);
+  if (lane_id() == 0) {
+    if (s1) atomicAdd(&a.cnt->n_refl[a.g], (unsigned)s1);
+    if (s2) atomicAdd(&a.cnt->n_refr[a.g], (unsigned)s2);
+  }
+}
+
+// ---------------------------------------------------------- host side
+Wavefront::~Wavefront() {
+  for (auto& g : gens_) {
+    (void)hipFree(g.rays); (void)hipFree(g.hits); (void)hipFree(g.nodes); (void)hipFree(g.colors);
+    (void)hipFree(g.shadows); (void)hipFree(g.sflags);
+  }
+  if (d_cnt_) (void)hipFree(d_cnt_);
+  if (d_prim_) (void)hipFree(d_prim_);
+  if (ev0_) (void)hipEventDestroy(ev0_);
+  if (ev1_) (void)hipEventDestroy(ev1_);
+  for (hipEvent_t e : pev_) (void)hipEventDestroy(e);
+}
+
+hipError_t Wavefront::pmark(hipStream_t s, int cls, bool begin) {
+  if (!profiling_) return hipSuccess;
+  const size_t idx = 2 * pn_ + (begin ? 0 : 1);
+  while (pev_.size() <= idx) {
+    hipEvent_t e;
+    WF_CHECK(hipEventCreate(&e));
+    pev_.push_back(e);
+  }
+  if (begin) {
+    if (pcls_.size() <= pn_) pcls_.resize(pn_ + 1);
+    pcls_[pn_] = cls;
+  }
+  WF_CHECK(hipEventRecord(pev_[idx], s));
+  if (!begin) ++pn_;
+  return hipSuccess;
+}
+
+hipError_t Wavefront::last_profile(WfProfile* out) {
+  *out = WfProfile{};
+  for (size_t i = 0; i < pn_; ++i) {
+    WF_CHECK(hipEventSynchronize(pev_[2 * i + 1]));
+    float ms = 0.f;
+    WF_CHECK(hipEventElapsedTime(&ms, pev_[2 * i], pev_[2 * i + 1]));
+    out->ms[pcls_[i]] += ms;
+  }
+  if (pframes_ > 1)
+    for (int c = 0; c < WF_NCLASS; ++c) out->ms[c] /= (double)pframes_;
+  WfCounters hc;
+  WF_CHECK(hipMemcpy(&hc, d_cnt_, sizeof hc, hipMemcpyDeviceToHost));
+  for (int c = 0; c < 3; ++c) {
+    out->rays[c] = prof_rays_[c];
+    out->disc[c] = (double)hc.disc[c];
+  }
+  return hipSuccess;
+}
+
+// Grow-only per-generation buffers. The shadow queue and the shadow flags are
+// sized rays * n_lights (at most one shadow ray per light per hit).
+hipError_t Wavefront::ensure_gen(size_t g, size_t rays, size_t n_lights) {
+  if (gens_.size() <= g) gens_.resize(g + 1);
+  WfGenBuf& b = gens_[g];
+  rays = std::max<size_t>(rays, 1);
+  if (b.cap_rays < rays) {
+    (void)hipFree(b.rays); (void)hipFree(b.hits); (void)hipFree(b.nodes); (void)hipFree(b.colors);
+    b.rays = nullptr; b.hits = nullptr; b.nodes = nullptr; b.colors = nullptr;
+    b.cap_rays = 0;
+    const size_t cap = rays + rays / 8;
+    WF_CHECK(hipMalloc(&b.rays, cap * sizeof(WfRay)));
+    WF_CHECK(hipMalloc(&b.hits, cap * sizeof(WfHit)));
+    WF_CHECK(hipMalloc(&b.nodes, cap * sizeof(WfNode)));
+    WF_CHECK(hipMalloc(&b.colors, cap * 3 * sizeof(double)));
+    b.cap_rays = cap;
+  }
+  const size_t need_sh = std::max<size_t>(b.cap_rays * n_lights, 1);
+  if (b.cap_shadows < need_sh) {
+    (void)hipFree(b.shadows); (void)hipFree(b.sflags);
+    b.shadows = nullptr; b.sflags = nullptr;
+    b.cap_shadows = 0;
+    WF_CHECK(hipMalloc(&b.shadows, need_sh * sizeof(WfShadow)));
+    WF_CHECK(hipMalloc(&b.sflags, need_sh));
+    b.cap_shadows = need_sh;
+  }
+  return hipSuccess;
+}
+
+hipError_t Wavefront::ensure_misc(size_t n_diag) {
+  if (!d_cnt_) WF_CHECK(hipMalloc(&d_cnt_, sizeof(WfCounters)));
+  if (!ev0_) WF_CHECK(hipEventCreate(&ev0_));
+  if (!ev1_) WF_CHECK(hipEventCreate(&ev1_));
+  if (prim_cap_ < n_diag + 4) {
+    if (d_prim_) (void)hipFree(d_prim_);
+    d_prim_ = nullptr;
+    WF_CHECK(hipMalloc(&d_prim_, (n_diag + 4) * sizeof(PrimRec)));
+    prim_cap_ = n_diag + 4;
+  }
+  return hipSuccess;
+}
+
+template <typename K>
+static int occupancy_grid(K kern, int block, size_t lds, unsigned n) {
+  int dev = 0, n_cu = 0, per_cu = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, block, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+  long long want = ((long long)n + block - 1) / block;
+  long long cap = (long long)n_cu * per_cu;
+  long long g = std::min(want, cap);
+  return (int)std::max(g, 1LL);
+}
+
+static constexpr size_t kWfLdsLimit = 160 * 1024 - 1024;
+
+template <int TW>
+static hipError_t launch_closest(const DevScene& sc, const DevCamera& cam, const WfArgs& a, bool primary, bool lds_ok,
+                                 unsigned n, hipStream_t stream) {
+  if (primary) {
+    const size_t lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, true);
+    auto k = wf_trace_closest<true, true, TW>;
+    WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, lds, n)), dim3(kTraceBlock), lds, stream, sc, cam, a);
+  } else if (lds_ok) {
+    const size_t lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, false);
+    auto k = wf_trace_closest<true, false, TW>;
+    WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, lds, n)), dim3(kTraceBlock), lds, stream, sc, cam, a);
+  } else {
+    auto k = wf_trace_closest<false, false, TW>;
+    hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
+  }
+  return hipGetLastError();
+}
+
+template <int TW>
+static hipError_t launch_shadow_wf(const DevScene& sc, const WfArgs& a, bool lds_ok, hipStream_t stream) {
+  if (lds_ok) {
+    const size_t lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, false);
+    auto k = wf_trace_shadow<true, TW>;
+    WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, lds, a.n_shadow)), dim3(kTraceBlock), lds, stream, sc, a);
+  } else {
+    auto k = wf_trace_shadow<false, TW>;
+    hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, 0, a.n_shadow)), dim3(kTraceBlock), 0, stream, sc, a);
+  }
+  return hipGetLastError();
+}
+
+hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool camera_mode, const double* d_in_rays,
+                             unsigned n0, unsigned max_depth, unsigned row_block, unsigned shard, unsigned n_shards,
+                             double* d_out, hipStream_t stream, const std::string& signature, DevStats* stats,
+                             float* ms_kernel) {
+  if (max_depth + 2 > (unsigned)kMaxGen) return hipErrorInvalidValue;
+  WF_CHECK(ensure_misc((size_t)sc.n_diag));
+  const unsigned L = (unsigned)sc.n_lights;
+  auto it = signature.empty() ? cache_.end() : cache_.find(signature);
+  const bool calibrated = it != cache_.end();
+  Counts counts;
+  if (calibrated) counts = it->second;
+  counts.rays.resize(max_depth + 2, 0);
+  counts.shadows.resize(max_depth + 2, 0);
+  counts.rays[0] = n0;
+
+  WF_CHECK(hipMemsetAsync(d_cnt_, 0, sizeof(WfCounters), stream));
+  WF_CHECK(ensure_gen(0, n0, L));
+  if (!camera_mode) {
+    // batch rays: n0 x 6 doubles -> WfRay queue of generation 0
+    WF_CHECK(hipMemcpy2DAsync(gens_[0].rays, sizeof(WfRay), d_in_rays, 6 * sizeof(double), 6 * sizeof(double), n0,
+                              hipMemcpyDeviceToDevice, stream));
+  }
+  const bool prim_lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, true) <= kWfLdsLimit;
+  const bool gen_lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, false) <= kWfLdsLimit;
+  const bool use_prim = camera_mode && prim_lds && sc.n_diag > 0;
+  if (use_prim) {
+    hipLaunchKernelGGL(wf_prim_prep, dim3((sc.n_diag + 4 + 255) / 256), dim3(256), 0, stream, sc, cam, d_prim_);
+    WF_CHECK(hipGetLastError());
+  }
+  WF_CHECK(hipEventRecord(ev0_, stream));
+  if (profiling_) ++pframes_;
+  prof_rays_[0] = prof_rays_[1] = prof_rays_[2] = 0;
+  unsigned last = 0;
+  for (unsigned g = 0; g <= max_depth; ++g) {
+    const unsigned n = counts.rays[g];
+    if (n == 0) break;
+    last = g;
+    // capacity of the next generation: exact when calibrated, else the bound 2n
+    const size_t cap_next = calibrated ? counts.rays[g + 1] : (g < max_depth ? 2ull * n : 0ull);
+    WF_CHECK(ensure_gen(g, n, L));
+    WF_CHECK(ensure_gen(g + 1, cap_next, L));
+    WfArgs a{};
+    WfGenBuf& B = gens_[g];
+    a.rays = B.rays; a.hits = B.hits; a.nodes = B.nodes; a.shadows = B.shadows; a.sflags = B.sflags;
+    a.colors = g == 0 ? d_out : B.colors;
+    a.next_rays = gens_[g + 1].rays;
+    a.child_colors = gens_[g + 1].colors;
+    a.cnt = d_cnt_;
+    a.prim = d_prim_;
+    a.n = n;
+    a.cap_next = (unsigned)cap_next;
+    a.g = g; a.max_depth = max_depth;
+    a.camera_mode = camera_mode ? 1u : 0u;
+    a.row_block = row_block; a.shard = shard; a.n_shards = n_shards;
+    // 1. closest hit
+    const bool prim_launch = g == 0 && use_prim;
+    const int ccls = prim_launch ? WF_PRIMARY : WF_CLOSEST;
+    a.disc_slot = (unsigned)ccls;
+    prof_rays_[ccls] += n;
+    WF_CHECK(pmark(stream, ccls, true));
+    if (g_wf_trace_waves == 4) WF_CHECK(launch_closest<4>(sc, cam, a, prim_launch, gen_lds, n, stream));
+    else WF_CHECK(launch_closest<8>(sc, cam, a, prim_launch, gen_lds, n, stream));
+    WF_CHECK(pmark(stream, ccls, false));
+    // 2. prepare_computations + spawn
+    WF_CHECK(pmark(stream, WF_PREP, true));
+    hipLaunchKernelGGL(wf_prep, dim3(occupancy_grid(wf_prep, kWfBlock, 0, n)), dim3(kWfBlock), 0, stream, sc, cam, a);
+    WF_CHECK(hipGetLastError());
+    WF_CHECK(pmark(stream, WF_PREP, false));
+    if (!calibrated) {
+      WfCounters hc;
+      WF_CHECK(hipMemcpyAsync(&hc, d_cnt_, sizeof hc, hipMemcpyDeviceToHost, stream));
+      WF_CHECK(hipStreamSynchronize(stream));
+      counts.rays[g + 1] = g < max_depth ? hc.n_rays[g + 1] : 0;
+      counts.shadows[g] = hc.n_shadow[g];
+    }
+    a.n_shadow = counts.shadows[g];
+    // 3. shadow rays
+    if (a.n_shadow) {
+      a.disc_slot = WF_SHADOW;
+      prof_rays_[WF_SHADOW] += a.n_shadow;
+      WF_CHECK(pmark(stream, WF_SHADOW, true));
+      if (g_wf_trace_waves == 4) WF_CHECK(launch_shadow_wf<4>(sc, a, gen_lds, stream));
+      else WF_CHECK(launch_shadow_wf<8>(sc, a, gen_lds, stream));
+      WF_CHECK(pmark(stream, WF_SHADOW, false));
+    }
+    if (stats) {
+      hipLaunchKernelGGL(wf_count_kinds, dim3(occupancy_grid(wf_count_kinds, 256, 0, n)), dim3(256), 0, stream, a);
+      WF_CHECK(hipGetLastError());
+    }
+  }
+  // 4. combine, deepest generation first
+  for (int g = (int)last; g >= 0; --g) {
+    WfArgs a{};
+    WfGenBuf& B = gens_[g];
+    a.rays = B.rays; a.nodes = B.nodes; a.sflags = B.sflags;
+    a.colors = g == 0 ? d_out : B.colors;
+    a.child_colors = gens_[g + 1].colors;
+    a.n = counts.rays[g];
+    a.g = (unsigned)g; a.max_depth = max_depth;
+    a.camera_mode = camera_mode ? 1u : 0u;
+    a.row_block = row_block; a.shard = shard; a.n_shards = n_shards;
+    WF_CHECK(pmark(stream, WF_COMBINE, true));
+    hipLaunchKernelGGL(wf_combine, dim3(occupancy_grid(wf_combine, kWfBlock, 0, a.n)), dim3(kWfBlock), 0, stream, sc,
+                       cam, a);
+    WF_CHECK(hipGetLastError());
+    WF_CHECK(pmark(stream, WF_COMBINE, false));
+  }
+  WF_CHECK(hipEventRecord(ev1_, stream));
+  if (!calibrated && !signature.empty()) cache_[signature] = counts;
+  if (stats || ms_kernel) {
+    WF_CHECK(hipStreamSynchronize(stream));
+    if (ms_kernel) WF_CHECK(hipEventElapsedTime(ms_kernel, ev0_, ev1_));
+  }
+  if (stats) {
+    WfCounters hc;
+    WF_CHECK(hipMemcpy(&hc, d_cnt_, sizeof hc, hipMemcpyDeviceToHost));
+    DevStats s{};
+    unsigned long long rays = 0, shadows = 0;
+    for (unsigned g = 0; g <= last; ++g) {
+      rays += counts.rays[g];
+      shadows += counts.shadows[g];
+      s.rays_reflect += hc.n_refl[g];
+      s.rays_refract += hc.n_refr[g];
+    }
+    s.rays_primary = n0;
+    s.rays_shadow = shadows;
+    s.sphere_tests = (rays + shadows) * (unsigned long long)(sc.n_diag + sc.n_gen);
+    s.plane_tests = (rays + shadows) * (unsigned long long)sc.n_planes;
+    s.sphere_disc_ge0 = hc.disc[0] + hc.disc[1] + hc.disc[2];
+    s.wave_steps = 0;
+    *stats = s;
+  }
+  return hipSuccess;
+}
+
+}  // namespace rtamd

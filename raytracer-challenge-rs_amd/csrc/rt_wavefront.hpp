@@ -1,0 +1,153 @@
+// rt_wavefront.hpp — host side of the wavefront render pipeline.
+//
+// The recursion tree of `World::color_at` (world.rs:70-81) is evaluated one
+// GENERATION (recursion depth) at a time over flat ray queues:
+//
+//   for g = 0 .. max_depth:                       (radiance rays of depth g)
+//     trace_closest(g)  World::intersect + hit          -> hits_g
+//     prep(g)           prepare_computations; spawn the shadow rays
+//                       (is_shadowed, world.rs:95-105) and the reflected /
+//                       refracted children (world.rs:107-134)   -> nodes_g,
+//                       shadow queue S_g, rays_{g+1}
+//     trace_shadow(g)   any-hit test of S_g                     -> flags_g
+//   for g = max_depth .. 0:
+//     combine(g)        lighting over lights (left fold) + children colours,
+//                       Schlick or plain sum (world.rs:40-68)   -> colors_g
+//
+// Every node's colour is computed from its children's colours with exactly
+// the reference's expression, so the result equals the recursive evaluation
+// bit for bit (no path-weight re-association). Queue order does not affect
+// any value.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <string>
+#include <vector>
+
+#include "rt_layout.hpp"
+
+namespace rtamd {
+
+struct WfRay {  // 64 B
+  double o[3];
+  double d[3];
+  int64_t pad;
+};
+struct WfHit {  // 24 B: nearest hit + containers top-2 (rt_device.hpp Hit)
+  double t;
+  int32_t key, c1k, c2k, pad;
+};
+struct WfNode {  // prepare_computations results needed by combine
+  double over[3], under[3], normal[3];
+  double n1, n2;
+  int32_t obj;         // -1 = miss
+  int32_t child_refl;  // index into rays_{g+1}, -1 = none (black)
+  int32_t child_refr;
+  int32_t pad;
+};
+struct WfShadow {  // 64 B
+  double o[3];
+  double d[3];
+  double dist;
+  int32_t slot;  // node * n_lights + light
+  int32_t pad;
+};
+struct PrimRec {  // primary rays share the origin: per diag sphere (s, o', c)
+  double s[3];
+  double op[3];
+  double c;
+  double pad;
+};
+
+constexpr int kMaxGen = 66;
+extern int g_wf_trace_waves;  // tuning knob: trace-kernel occupancy (4 or 8 waves/SIMD)
+
+struct WfCounters {
+  unsigned n_rays[kMaxGen];    // appended rays per generation (index g+1 filled by prep(g))
+  unsigned n_shadow[kMaxGen];  // shadow rays per generation
+  unsigned n_refl[kMaxGen], n_refr[kMaxGen];
+  unsigned long long disc[3];  // disc >= 0 tests: [0] primary closest, [1] closest, [2] shadow
+};
+
+struct WfGenBuf {
+  WfRay* rays = nullptr;
+  WfHit* hits = nullptr;
+  WfNode* nodes = nullptr;
+  double* colors = nullptr;
+  WfShadow* shadows = nullptr;
+  uint8_t* sflags = nullptr;
+  size_t cap_rays = 0, cap_shadows = 0;
+};
+
+// Kernel arguments for one generation.
+struct WfArgs {
+  WfRay* rays;          // rays_g (g >= 1 or batch mode)
+  WfHit* hits;
+  WfNode* nodes;
+  double* colors;       // colors_g (g >= 1) or the output (g == 0)
+  WfShadow* shadows;
+  uint8_t* sflags;
+  WfRay* next_rays;     // rays_{g+1}
+  const double* child_colors;  // colors_{g+1}
+  WfCounters* cnt;
+  const PrimRec* prim;  // per-frame primary records (camera mode, g == 0)
+  unsigned n;           // rays in this generation
+  unsigned n_shadow;    // shadow rays in this generation
+  unsigned cap_next;    // capacity of rays_{g+1}
+  unsigned g, max_depth;
+  unsigned camera_mode; // g == 0 rays come from the camera (1) or from `rays` (0)
+  unsigned row_block, shard, n_shards;
+  unsigned disc_slot;   // WfCounters::disc index of this trace launch
+};
+
+// Per-kernel-class timing of the last frame (profiling mode only).
+enum WfClass { WF_PRIMARY = 0, WF_CLOSEST = 1, WF_SHADOW = 2, WF_PREP = 3, WF_COMBINE = 4, WF_NCLASS = 5 };
+struct WfProfile {
+  double ms[WF_NCLASS];
+  double rays[3];   // rays traced by the three trace classes
+  double disc[3];   // disc >= 0 tests per trace class
+};
+
+class Wavefront {
+ public:
+  ~Wavefront();
+  // Profiling mode: HIP events around every launch, per kernel class.
+  void set_profiling(bool on) {
+    profiling_ = on;
+    if (on) { pn_ = 0; pframes_ = 0; }
+  }
+  // Per-class times averaged over the frames rendered since profiling was
+  // enabled; rays / disc counts of the last frame (synchronises).
+  hipError_t last_profile(WfProfile* out);
+  // Render n0 root rays (camera pixels of a shard, or explicit rays) into
+  // `out` (n0*3 doubles, device). Counts of a signature seen before are
+  // reused (fully asynchronous); otherwise each generation is sized by a
+  // synchronous count read-back. stats (host) may be null.
+  hipError_t render(const DevScene& sc, const DevCamera& cam, bool camera_mode, const double* d_in_rays,
+                    unsigned n0, unsigned max_depth, unsigned row_block, unsigned shard, unsigned n_shards,
+                    double* d_out, hipStream_t stream, const std::string& signature, DevStats* stats,
+                    float* ms_kernel);
+
+ private:
+  hipError_t ensure_gen(size_t g, size_t rays, size_t n_lights);
+  hipError_t ensure_misc(size_t n_diag);
+  std::vector<WfGenBuf> gens_;
+  WfCounters* d_cnt_ = nullptr;
+  PrimRec* d_prim_ = nullptr;
+  size_t prim_cap_ = 0;
+  hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
+  struct Counts {
+    std::vector<unsigned> rays, shadows;
+  };
+  std::map<std::string, Counts> cache_;
+  bool profiling_ = false;
+  std::vector<hipEvent_t> pev_;        // event pool (pairs)
+  std::vector<int> pcls_;              // class of each recorded pair
+  size_t pn_ = 0;                      // pairs recorded since profiling was enabled
+  size_t pframes_ = 0;
+  double prof_rays_[3] = {0, 0, 0};
+  hipError_t pmark(hipStream_t s, int cls, bool begin);
+};
+
+}  // namespace rtamd

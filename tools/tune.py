@@ -8,6 +8,7 @@ import rtamd
 from rtamd import scenes
 ap = argparse.ArgumentParser()
 ap.add_argument("--waves", default="3,4,5,6")
+ap.add_argument("--knob", default="waves")
 ap.add_argument("--rounds", type=int, default=4)
 ap.add_argument("--scene", default="c3")
 a = ap.parse_args()
@@ -17,14 +18,14 @@ res = {v: [] for v in a.waves.split(",")}
 ref = None
 for r in range(a.rounds):
     for v in res:
-        rtamd._rtamd._tuning_set("waves", int(v))
+        rtamd._rtamd._tuning_set(a.knob, int(v))
         canvas, st = cam.render(w, depth)
         img = canvas.to_numpy()
         if ref is None:
             ref = img
         assert img.tobytes() == ref.tobytes(), f"variant {v} changed the image"
         res[v].append(st["ms_kernel"])
-        if r == a.rounds - 1:
+        if r == a.rounds - 1 and a.knob == "waves":
             ws, tc, tot = rtamd._rtamd._diag_last(w)
             lanes = st["rays_primary"] + st["rays_reflect"] + st["rays_refract"] + st["rays_shadow"]
             msg = f"  [{v}] wave_steps={ws} lane_util={lanes/(64*ws):.3f}"
@@ -33,4 +34,4 @@ for r in range(a.rounds):
             print(msg, flush=True)
 n = st["rays_primary"] + st["rays_reflect"] + st["rays_refract"] + st["rays_shadow"]
 for v, ms in res.items():
-    print(f"waves={v}: median {statistics.median(ms):.3f} ms  min {min(ms):.3f}  -> {n/min(ms)/1e3:.1f} Mrays/s  all={['%.2f'%x for x in ms]}", flush=True)
+    print(f"{a.knob}={v}: median {statistics.median(ms):.3f} ms  min {min(ms):.3f}  -> {n/min(ms)/1e3:.1f} Mrays/s  all={['%.2f'%x for x in ms]}", flush=True)
