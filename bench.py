@@ -34,6 +34,7 @@ import torch.distributed as dist  # noqa: E402
 
 import rtamd  # noqa: E402
 from rtamd import scenes  # noqa: E402
+from rtamd.distributed import FrameAssembler  # noqa: E402
 
 METRIC = "Mrays/s (primary+secondary) on 1920×1080/1000-sphere/depth-5; 1→8 GPU scaling"
 PEAK_F64_VALU_TFLOPS = 39.3  # 256 CU x 64 f64 lanes/clk x 2.4 GHz, non-fused add/mul (MI355X_MICROARCH.md)
@@ -120,29 +121,14 @@ def main():
         depth = a.depth
     world.upload(local_rank)  # flatten + upload: outside the timed region
     W, H, B = cam.hsize, cam.vsize, a.row_block
-    my_rows = rtamd.shard_rows(H, B, rank, n)
-    max_rows = max(rtamd.shard_rows(H, B, s, n) for s in range(n))
-    shard = torch.zeros((max_rows, W, 3), dtype=torch.float64, device=dev)  # padded for the gather
-    if rank == 0:
-        gathered = [torch.empty_like(shard) for _ in range(n)]
-        canvas = torch.empty((H, W, 3), dtype=torch.float64, device=dev)
-        # rank-major gathered rows -> canvas rows (un-interleave index)
-        src = []
-        for s in range(n):
-            rows_s = [y for y in range(H) if (y // B) % n == s]
-            src += [s * max_rows + i for i in range(len(rows_s))]
-        dst = [y for s in range(n) for y in range(H) if (y // B) % n == s]
-        src_idx = torch.tensor(src, device=dev)
-        dst_idx = torch.tensor(dst, device=dev)
+    fa = FrameAssembler(H, W, B, rank, n, dev)  # interleaved row blocks + one RCCL gather
+    assert len(fa.rows) == rtamd.shard_rows(H, B, rank, n)
+    shard = fa.shard
     stream = torch.cuda.current_stream()
 
     def step():
         cam.render_shard_device(world, depth, B, rank, n, shard.data_ptr(), stream.cuda_stream, False)
-        if n > 1:
-            dist.gather(shard, gathered if rank == 0 else None, dst=0)
-            if rank == 0:
-                canvas.index_copy_(0, dst_idx, torch.cat(gathered).index_select(0, src_idx))
-        # n == 1: the shard buffer already is the row-major canvas
+        fa.assemble()  # n == 1: the shard buffer already is the row-major canvas
 
     # exact work counters of one frame (deterministic), from a counted warm-up launch
     # (this first launch also sizes the wavefront queues of this camera/shard)

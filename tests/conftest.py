@@ -11,8 +11,9 @@ import sys
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TESTS = os.path.join(REPO, "tests")
 PKG = os.path.join(REPO, "raytracer-challenge-rs_amd")
-for p in (REPO, PKG):
+for p in (REPO, PKG, TESTS):
     if p not in sys.path:
         sys.path.insert(0, p)
 

@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Generate the committed whole-frame golden fixtures (TEST INFRASTRUCTURE).
+
+The reference holds no golden images (`renders/` is
+git-ignored and the Rust crate cannot be built here), so whole-frame goldens
+come from the C oracle (oracle/rt_oracle.c), which is itself pinned by the
+reference's 49 known-answer tests (tests/test_oracle_kat.py). The fixtures
+freeze the oracle's output so that (1) a change to the oracle is caught on CPU
+and (2) the GPU path is checked against files, not only against a live oracle.
+
+Per case <name>:
+  <name>.ppm        P3 bytes of the frame (canvas.rs:43-48 / ppm.rs:24-75)
+  <name>.npz        f64 canvas (H, W, 3) `canvas` + the camera descriptor bytes
+  index.json        per case: scene, size, depth, the exact counters, sha256
+                    of the PPM and of the canvas bytes
+
+Run from the repo root:  python tests/golden/make_golden.py
+"""
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path[:0] = [REPO, os.path.join(REPO, "raytracer-challenge-rs_amd"), os.path.join(REPO, "tests")]
+
+import rtamd  # noqa: E402  (host-side scene builder; no GPU needed)
+from oracle import pyoracle  # noqa: E402
+from golden_cases import scene  # noqa: E402
+
+# (name, scene factory, kwargs): small enough for the oracle to finish in seconds
+CASES = [
+    ("kat11", "kat11", {}),
+    ("c1", "c1", {"width": 200, "height": 100}),
+    ("c2_80x60", "c2", {"width": 80, "height": 60}),
+    ("c3_96x54", "c3", {"width": 96, "height": 54}),
+    ("c3_64x36_s200", "c3", {"width": 64, "height": 36, "n_spheres": 200}),
+    ("zoo_64x48", "zoo", {"width": 64, "height": 48}),
+]
+COUNTERS = ("rays_primary", "rays_reflect", "rays_refract", "rays_shadow",
+            "sphere_tests", "plane_tests", "sphere_disc_ge0")
+
+
+def main():
+    index = {}
+    for name, kind, kw in CASES:
+        w, cam, depth = scene(rtamd, kind, kw)
+        ow = pyoracle.OracleWorld.from_world(w)
+        canvas, st = ow.render(cam.desc_bytes(), depth, nthreads=8)
+        ppm = pyoracle.canvas_to_ppm(canvas)
+        with open(os.path.join(HERE, name + ".ppm"), "wb") as f:
+            f.write(ppm)
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), canvas=canvas,
+                            camera=np.frombuffer(cam.desc_bytes(), dtype=np.uint8))
+        index[name] = {
+            "scene": kind, "args": kw, "width": cam.hsize, "height": cam.vsize, "depth": depth,
+            "counters": {k: int(st[k]) for k in COUNTERS},
+            "ppm_sha256": hashlib.sha256(ppm).hexdigest(),
+            "canvas_sha256": hashlib.sha256(np.ascontiguousarray(canvas).tobytes()).hexdigest(),
+        }
+        print(name, cam.hsize, cam.vsize, index[name]["counters"])
+    with open(os.path.join(HERE, "index.json"), "w") as f:
+        json.dump(index, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,34 +1,75 @@
-"""Summarise rocprofv3 PMC passes for the render kernel into JSON (dev tool).
+"""Summarise rocprofv3 PMC passes of the bench workload per kernel class (dev tool).
 
-Usage: pmc_summary.py OUT.json DIR [DIR ...]  (each DIR holds one
---pmc pass: *_counter_collection.csv). Per-dispatch values of the render
-kernel are averaged over dispatches. HBM bytes follow MI355X_MICROARCH.md
-§HBM: FETCH_SIZE (KiB) reads half the bytes of a wide coalesced stream on
-gfx950, so hbm_read = 2 * FETCH_SIZE * 1024 is an upper estimate; WRITE_SIZE
-(KiB) is exact for 16-B stores.
+Usage: pmc_summary.py OUT.json [--width W --height H --spheres S --n-gpus N
+       --dominant CLASS] DIR [DIR ...]
+Each DIR holds one --pmc pass (*_counter_collection.csv). Counters are summed
+over all dispatches of a kernel class and divided by the number of frames
+(= wf_prim_prep dispatches, one per rendered frame), i.e. per-FRAME values of
+that class's launches — the same unit as bench.py's roofline.
+
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE (KiB) under-reports a
+wide coalesced stream by 2x on gfx950, so hbm_read = 2 * FETCH_SIZE * 1024 is
+an upper estimate; WRITE_SIZE (KiB) is exact for 16-B stores.
 """
-import csv, glob, json, sys, collections
+import argparse, collections, csv, glob, json
 
-out, dirs = sys.argv[1], sys.argv[2:]
-per = collections.defaultdict(list)
-for d in dirs:
+CLASSES = [  # (class, predicate on the demangled kernel name)
+    ("primary", lambda n: "wf_trace_closest<" in n and ", true," in n),
+    ("closest", lambda n: "wf_trace_closest<" in n and ", false," in n),
+    ("shadow", lambda n: "wf_trace_shadow<" in n),
+    ("prep", lambda n: "wf_prep(" in n),
+    ("combine", lambda n: "wf_combine(" in n),
+    ("megakernel", lambda n: "render_kernel<" in n),
+    ("frame", lambda n: "wf_prim_prep(" in n),
+]
+
+
+def klass(name):
+    for c, f in CLASSES:
+        if f(name):
+            return c
+    return None
+
+
+ap = argparse.ArgumentParser()
+ap.add_argument("out")
+ap.add_argument("dirs", nargs="+")
+ap.add_argument("--width", type=int, default=1920)
+ap.add_argument("--height", type=int, default=1080)
+ap.add_argument("--spheres", type=int, default=1000)
+ap.add_argument("--n-gpus", type=int, default=1)
+ap.add_argument("--dominant", default="closest")
+a = ap.parse_args()
+
+tot = collections.defaultdict(lambda: collections.defaultdict(float))
+frames = {}
+for d in a.dirs:
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
-        byd = collections.defaultdict(lambda: collections.defaultdict(float))
+        seen = set()
         for r in csv.DictReader(open(f)):
-            if "render_kernel" not in r["Kernel_Name"]:
+            c = klass(r["Kernel_Name"])
+            if c is None:
                 continue
-            byd[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
-        for disp, cs in byd.items():
-            for k, v in cs.items():
-                per[k].append(v)
-avg = {k: sum(v) / len(v) for k, v in per.items()}
-res = {"counters_per_dispatch": avg, "dispatches": {k: len(v) for k, v in per.items()}}
-if "FETCH_SIZE" in avg or "WRITE_SIZE" in avg:
-    fetch = avg.get("FETCH_SIZE", 0.0) * 1024
-    write = avg.get("WRITE_SIZE", 0.0) * 1024
-    res["hbm_read_bytes_raw"] = fetch
-    res["hbm_read_bytes_corrected"] = 2 * fetch
-    res["hbm_write_bytes"] = write
-    res["hbm_bytes_per_launch"] = 2 * fetch + write
-json.dump(res, open(out, "w"), indent=1, sort_keys=True)
+            if c == "frame":
+                seen.add(r["Dispatch_Id"])
+                continue
+            tot[c][r["Counter_Name"]] += float(r["Counter_Value"])
+        frames[f] = len(seen)
+nf = max(frames.values()) if frames else 0
+res = {"width": a.width, "height": a.height, "spheres": a.spheres, "n_gpus": a.n_gpus,
+       "frames_per_pass": nf, "per_frame": {}}
+for c, cs in tot.items():
+    pf = {k: v / max(nf, 1) for k, v in cs.items()}
+    if "FETCH_SIZE" in pf or "WRITE_SIZE" in pf:
+        fetch = pf.get("FETCH_SIZE", 0.0) * 1024
+        write = pf.get("WRITE_SIZE", 0.0) * 1024
+        pf["hbm_read_bytes_raw"] = fetch
+        pf["hbm_read_bytes_corrected"] = 2 * fetch
+        pf["hbm_write_bytes"] = write
+        pf["hbm_bytes"] = 2 * fetch + write
+    res["per_frame"][c] = pf
+dom = res["per_frame"].get(a.dominant, {})
+res["kernel_class"] = a.dominant
+res["hbm_bytes_per_frame"] = dom.get("hbm_bytes")
+json.dump(res, open(a.out, "w"), indent=1, sort_keys=True)
 print(json.dumps(res, indent=1, sort_keys=True))
