@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------ */
 enum {
@@ -44,7 +44,16 @@ enum {
 };
 
 /* ---- shape kinds / pattern kinds ---------------------------------------- */
-enum { RT_SHAPE_SPHERE = 0, RT_SHAPE_PLANE = 1 };
+enum {
+  RT_SHAPE_SPHERE = 0,   /* geometry/shape/sphere.rs:16-77   */
+  RT_SHAPE_PLANE = 1,    /* geometry/shape/plane.rs:19-64    */
+  RT_SHAPE_CUBE = 2,     /* geometry/shape/cube.rs:17-106    */
+  RT_SHAPE_CYLINDER = 3, /* geometry/shape/cylinder.rs:12-130 */
+  RT_SHAPE_CONE = 4      /* geometry/shape/cone.rs:12-149    */
+};
+
+/* Anti-aliasing sample counts of `RenderOpts::aa_samples` (camera.rs:221-233). */
+enum { RT_AA_X1 = 1, RT_AA_X2 = 2, RT_AA_X4 = 4, RT_AA_X8 = 8, RT_AA_X16 = 16 };
 enum {
   RT_PATTERN_NONE = -1,
   RT_PATTERN_TEST = 0,     /* pattern/test_pattern.rs:7-9 */
@@ -78,6 +87,12 @@ typedef struct rt_shape_desc {
   double pattern_a[3], pattern_b[3];
   double pattern_transform[16];
   double pattern_inverse[16];
+  /* Cylinder / Cone `minimum`, `maximum`, `closed` (cylinder.rs:12-18,
+   * cone.rs:12-18); Cylinder::default / Cone::default = (-inf, +inf, false).
+   * Ignored for the other kinds. */
+  double minimum, maximum;
+  int32_t closed;
+  int32_t _pad2;
 } rt_shape_desc;
 
 /* `PointLight` (light.rs:4-24), in `World::lights` insertion order. */
@@ -103,6 +118,7 @@ typedef struct rt_stats {
   uint64_t sphere_tests;
   uint64_t plane_tests;
   uint64_t sphere_disc_ge0;
+  uint64_t other_tests; /* Cube / Cylinder / Cone local_intersect calls */
   double ms_kernel; /* device time of the render kernel(s), HIP events */
   double ms_total;  /* wall time of the call */
 } rt_stats;
@@ -139,6 +155,15 @@ void rt_scene_destroy(rt_scene* scene);
 int rt_render(const rt_scene* scene, const rt_camera_desc* camera,
               uint32_t max_depth, double* out_rgb, rt_stats* stats);
 
+/* `Camera::render_multithreaded` (camera.rs:150-214): every pixel is the
+ * `Color::average` (color.rs:26-33) of `color_at` over the rays of
+ * `rays_for_pixel` (camera.rs:71-126) for `aa_samples` in {1,2,4,8,16}
+ * (`RenderOpts::aa_samples`). The reference's `num_threads` only partitions
+ * CPU work and does not change the image. aa_samples == 1 equals rt_render. */
+int rt_render_aa(const rt_scene* scene, const rt_camera_desc* camera,
+                 uint32_t max_depth, uint32_t aa_samples, double* out_rgb,
+                 rt_stats* stats);
+
 /* Device-resident shard render (used by multi-GPU and the benchmark).
  * Renders the rows y with (y / row_block) % n_shards == shard, in increasing
  * y order, into `d_out_rgb` (a DEVICE buffer on the scene's device holding
@@ -146,9 +171,11 @@ int rt_render(const rt_scene* scene, const rt_camera_desc* camera,
  * default (null) stream, so the work is ordered with the caller's other work
  * there (torch's current stream is often the null stream).
  * Asynchronous unless `stats` is non-NULL (then it synchronises to read the
- * counters). `n_shards == 1` renders the whole frame. */
+ * counters). `n_shards == 1` renders the whole frame. `aa_samples` as in
+ * rt_render_aa (1 = `Camera::render`). */
 int rt_render_shard_device(const rt_scene* scene, const rt_camera_desc* camera,
-                           uint32_t max_depth, uint32_t row_block,
+                           uint32_t max_depth, uint32_t aa_samples,
+                           uint32_t row_block,
                            uint32_t shard, uint32_t n_shards,
                            double* d_out_rgb, void* stream, rt_stats* stats);
 
@@ -183,7 +210,8 @@ int rt_hit_batch(const rt_scene* scene, const double* rays, size_t n,
  * have been created on device i. Output to a HOST buffer like rt_render. */
 int rt_render_multi(rt_scene* const* scenes, int n_devices,
                     const rt_camera_desc* camera, uint32_t max_depth,
-                    uint32_t row_block, double* out_rgb, rt_stats* stats);
+                    uint32_t aa_samples, uint32_t row_block, double* out_rgb,
+                    rt_stats* stats);
 
 /* ---- output (image/ppm.rs) ------------------------------------------------ */
 

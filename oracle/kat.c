@@ -37,12 +37,172 @@ static oray R(double ox, double oy, double oz, double dx, double dy, double dz) 
   return r;
 }
 static void set_tf(oshape* s, omat t) { or_shape_set_transform(s, &t); }
-static int count_intersect(const oshape* s, oray r, double t[2]) { return or_shape_intersect(s, &r, t, NULL); }
+/* local_intersect with a normalised direction (the shape tests normalise) */
+static int local_xs(const oshape* s, ot3 o, ot3 d, int normalise, double t[OR_MAX_LOCAL_XS]) {
+  oray r = {o, normalise ? or_normalize(d) : d};
+  return or_local_intersect(s, &r, t);
+}
+static int count_intersect(const oshape* s, oray r, double t[OR_MAX_LOCAL_XS]) { return or_shape_intersect(s, &r, t, NULL); }
 
 int main(void) {
   const double S2 = sqrt(2.0) / 2.0;
   const double S3 = sqrt(3.0) / 3.0;
   const double PI = 3.14159265358979323846;
+
+  /* -------------------------------------------------------------- cube.rs */
+  CASE("ray_intersects_cube") { /* cube.rs:114-148 */
+    oshape c = or_cube_default();
+    const double tc[7][8] = {{5, 0.5, 0, -1, 0, 0, 4, 6},  {-5, 0.5, 0, 1, 0, 0, 4, 6},
+                             {0.5, 5, 0, 0, -1, 0, 4, 6},  {0.5, -5, 0, 0, 1, 0, 4, 6},
+                             {0.5, 0, 5, 0, 0, -1, 4, 6},  {0.5, 0, -5, 0, 0, 1, 4, 6},
+                             {0, 0.5, 0, 0, 0, 1, -1, 1}};
+    for (int i = 0; i < 7; ++i) {
+      double t[OR_MAX_LOCAL_XS];
+      int n = local_xs(&c, or_t3(tc[i][0], tc[i][1], tc[i][2]), or_t3(tc[i][3], tc[i][4], tc[i][5]), 0, t);
+      CHECK(n == 2); CHECK_EQ(t[0], tc[i][6]); CHECK_EQ(t[1], tc[i][7]);
+    }
+  }
+  CASE("ray_misses_cube") { /* cube.rs:150-181 */
+    oshape c = or_cube_default();
+    const double tc[6][6] = {{-2, 0, 0, 0.2673, 0.5345, 0.8018}, {0, -2, 0, 0.8018, 0.2673, 0.5345},
+                             {0, 0, -2, 0.5345, 0.8018, 0.2673}, {2, 0, 2, 0, 0, -1},
+                             {0, 2, 2, 0, -1, 0},                {2, 2, 0, -1, 0, 0}};
+    for (int i = 0; i < 6; ++i) {
+      double t[OR_MAX_LOCAL_XS];
+      CHECK(local_xs(&c, or_t3(tc[i][0], tc[i][1], tc[i][2]), or_t3(tc[i][3], tc[i][4], tc[i][5]), 0, t) == 0);
+    }
+  }
+  CASE("normal_on_cube_surface") { /* cube.rs:183-214 */
+    oshape c = or_cube_default();
+    const double tc[8][6] = {{1, 0.5, -0.8, 1, 0, 0},   {-1, -0.2, -0.9, -1, 0, 0}, {-0.4, 1, -0.1, 0, 1, 0},
+                             {0.3, -1, -0.7, 0, -1, 0}, {-0.6, 0.3, 1, 0, 0, 1},    {0.4, 0.4, -1, 0, 0, -1},
+                             {1, 1, 1, 1, 0, 0},        {-1, -1, -1, -1, 0, 0}};
+    for (int i = 0; i < 8; ++i)
+      CHECK_T3(or_local_normal_at(&c, or_t3(tc[i][0], tc[i][1], tc[i][2])), tc[i][3], tc[i][4], tc[i][5]);
+  }
+  CASE("cube_bounding_box") { /* cube.rs:216-222 */
+    oshape c = or_cube_default();
+    CHECK_T3(c.bbox.min, -1, -1, -1); CHECK_T3(c.bbox.max, 1, 1, 1);
+  }
+
+  /* ---------------------------------------------------------- cylinder.rs */
+  CASE("ray_misses_cylinder") { /* cylinder.rs:138-152 */
+    oshape c = or_cylinder_new(-INFINITY, INFINITY, 0);
+    const double tc[3][6] = {{1, 0, 0, 0, 1, 0}, {0, 0, 0, 0, 1, 0}, {0, 0, -5, 1, 1, 1}};
+    for (int i = 0; i < 3; ++i) {
+      double t[OR_MAX_LOCAL_XS];
+      CHECK(local_xs(&c, or_t3(tc[i][0], tc[i][1], tc[i][2]), or_t3(tc[i][3], tc[i][4], tc[i][5]), 0, t) == 0);
+    }
+  }
+  CASE("ray_strikes_cylinder") { /* cylinder.rs:154-196 */
+    oshape c = or_cylinder_new(-INFINITY, INFINITY, 0);
+    const double tc[3][8] = {{1, 0, -5, 0, 0, 1, 5, 5}, {0, 0, -5, 0, 0, 1, 4, 6},
+                             {0.5, 0, -5, 0.1, 1, 1, 6.80798, 7.08872}};
+    for (int i = 0; i < 3; ++i) {
+      double t[OR_MAX_LOCAL_XS];
+      int n = local_xs(&c, or_t3(tc[i][0], tc[i][1], tc[i][2]), or_t3(tc[i][3], tc[i][4], tc[i][5]), 1, t);
+      CHECK(n == 2); CHECK_EQ(t[0], tc[i][6]); CHECK_EQ(t[1], tc[i][7]);
+    }
+  }
+  CASE("normal_vector_on_cylinder") { /* cylinder.rs:198-212 */
+    oshape c = or_cylinder_new(-INFINITY, INFINITY, 0);
+    const double tc[4][6] = {{1, 0, 0, 1, 0, 0}, {0, 5, -1, 0, 0, -1}, {0, -2, 1, 0, 0, 1}, {-1, 1, 0, -1, 0, 0}};
+    for (int i = 0; i < 4; ++i)
+      CHECK_T3(or_local_normal_at(&c, or_t3(tc[i][0], tc[i][1], tc[i][2])), tc[i][3], tc[i][4], tc[i][5]);
+  }
+  CASE("default_cylinder_min_max_closed") { /* cylinder.rs:214-246 */
+    oshape c = or_cylinder_new(-INFINITY, INFINITY, 0);
+    CHECK(isinf(c.minimum) && c.minimum < 0); CHECK(isinf(c.maximum) && c.maximum > 0); CHECK(c.closed == 0);
+  }
+  CASE("intersect_constrained_cylinder") { /* cylinder.rs:220-240 */
+    oshape c = or_cylinder_new(1.0, 2.0, 0);
+    const double tc[6][7] = {{0, 1.5, 0, 0.1, 1, 0, 0}, {0, 3, -5, 0, 0, 1, 0}, {0, 0, -5, 0, 0, 1, 0},
+                             {0, 2, -5, 0, 0, 1, 0},    {0, 1, -5, 0, 0, 1, 0}, {0, 1.5, -2, 0, 0, 1, 2}};
+    for (int i = 0; i < 6; ++i) {
+      double t[OR_MAX_LOCAL_XS];
+      CHECK(local_xs(&c, or_t3(tc[i][0], tc[i][1], tc[i][2]), or_t3(tc[i][3], tc[i][4], tc[i][5]), 1, t) ==
+            (int)tc[i][6]);
+    }
+  }
+  CASE("intersect_caps_closed_cylinder") { /* cylinder.rs:248-264 */
+    oshape c = or_cylinder_new(1.0, 2.0, 1);
+    const double tc[5][6] = {{0, 3, 0, 0, -1, 0}, {0, 3, -2, 0, -1, 2}, {0, 4, -2, 0, -1, 1},
+                             {0, 0, -2, 0, 1, 2}, {0, -1, -2, 0, 1, 1}};
+    for (int i = 0; i < 5; ++i) {
+      double t[OR_MAX_LOCAL_XS];
+      CHECK(local_xs(&c, or_t3(tc[i][0], tc[i][1], tc[i][2]), or_t3(tc[i][3], tc[i][4], tc[i][5]), 1, t) == 2);
+    }
+  }
+  CASE("normal_vector_on_cylinder_end_cap") { /* cylinder.rs:266-282 */
+    oshape c = or_cylinder_new(1.0, 2.0, 1);
+    const double tc[6][6] = {{0, 1, 0, 0, -1, 0},   {0.5, 1, 0, 0, -1, 0}, {0, 1, 0.5, 0, -1, 0},
+                             {0, 2, 0, 0, 1, 0},    {0.5, 2, 0, 0, 1, 0},  {0, 2, 0.5, 0, 1, 0}};
+    for (int i = 0; i < 6; ++i)
+      CHECK_T3(or_local_normal_at(&c, or_t3(tc[i][0], tc[i][1], tc[i][2])), tc[i][3], tc[i][4], tc[i][5]);
+  }
+  CASE("bounded_cylinder_bounding_box") { /* cylinder.rs:296-302 */
+    oshape c = or_cylinder_new(-5, 3, 0);
+    CHECK_T3(c.bbox.min, -1, -5, -1); CHECK_T3(c.bbox.max, 1, 3, 1);
+  }
+
+  /* -------------------------------------------------------------- cone.rs */
+  CASE("intersect_cone_with_ray") { /* cone.rs:155-192 */
+    oshape c = or_cone_new(-INFINITY, INFINITY, 0);
+    const double tc[3][8] = {{0, 0, -5, 0, 0, 1, 5, 5}, {0, 0, -5, 1, 1, 1, 8.66025, 8.66025},
+                             {1, 1, -5, -0.5, -1, 1, 4.55006, 49.44994}};
+    for (int i = 0; i < 3; ++i) {
+      double t[OR_MAX_LOCAL_XS];
+      int n = local_xs(&c, or_t3(tc[i][0], tc[i][1], tc[i][2]), or_t3(tc[i][3], tc[i][4], tc[i][5]), 1, t);
+      CHECK(n == 2); CHECK_EQ(t[0], tc[i][6]); CHECK_EQ(t[1], tc[i][7]);
+    }
+  }
+  CASE("intersect_cone_parallel_to_half") { /* book: ray parallel to one half, t = 0.35355 */
+    /* The reference computes `-c / 2.0 * b` (cone.rs:104) and has no test for
+     * this branch; the oracle keeps the reference's expression. */
+    oshape c = or_cone_new(-INFINITY, INFINITY, 0);
+    double t[OR_MAX_LOCAL_XS];
+    int n = local_xs(&c, or_t3(0, 0, -1), or_t3(0, 1, 1), 1, t);
+    CHECK(n == 1);
+    oray r = {or_t3(0, 0, -1), or_normalize(or_t3(0, 1, 1))};
+    double b = 2.0 * r.origin.x * r.direction.x - 2.0 * r.origin.y * r.direction.y + 2.0 * r.origin.z * r.direction.z;
+    double cc = r.origin.x * r.origin.x - r.origin.y * r.origin.y + r.origin.z * r.origin.z;
+    CHECK(t[0] == -cc / 2.0 * b);
+  }
+  CASE("intersect_cone_end_caps") { /* cone.rs:194-228 */
+    oshape c = or_cone_new(-0.5, 0.5, 1);
+    const double tc[3][7] = {{0, 0, -5, 0, 1, 0, 0}, {0, 0, -0.25, 0, 1, 1, 2}, {0, 0, -0.25, 0, 1, 0, 4}};
+    for (int i = 0; i < 3; ++i) {
+      double t[OR_MAX_LOCAL_XS];
+      CHECK(local_xs(&c, or_t3(tc[i][0], tc[i][1], tc[i][2]), or_t3(tc[i][3], tc[i][4], tc[i][5]), 1, t) ==
+            (int)tc[i][6]);
+    }
+  }
+  CASE("computing_normal_vector_cone") { /* cone.rs:230-242 */
+    oshape c = or_cone_new(-INFINITY, INFINITY, 0);
+    CHECK_T3(or_local_normal_at(&c, or_t3(0, 0, 0)), 0, 0, 0);
+    CHECK_T3(or_local_normal_at(&c, or_t3(1, 1, 1)), 1, -sqrt(2.0), 1);
+    CHECK_T3(or_local_normal_at(&c, or_t3(-1, -1, 0)), -1, 1, 0);
+  }
+  CASE("bounded_cone_bounding_box") { /* cone.rs:256-262 */
+    oshape c = or_cone_new(-5, 3, 0);
+    CHECK_T3(c.bbox.min, -5, -5, -5); CHECK_T3(c.bbox.max, 5, 3, 5);
+  }
+
+  /* ------------------------------------------------- camera.rs (AA offsets) */
+  CASE("rays_for_pixel_offsets") { /* camera.rs:71-126: X1 equals ray_for_pixel; Xn offsets */
+    ocamera cam;
+    or_camera_new(&cam, 201, 101, PI / 2.0);
+    oray one = or_ray_for_pixel(&cam, 100, 50), rs[16];
+    CHECK(or_rays_for_pixel(&cam, 100, 50, 1, rs) == 1);
+    CHECK(memcmp(&one, &rs[0], sizeof one) == 0);
+    CHECK(or_rays_for_pixel(&cam, 100, 50, 16, rs) == 16);
+    CHECK(or_rays_for_pixel(&cam, 100, 50, 3, rs) == 0);
+    CHECK(or_rays_for_pixel(&cam, 0, 0, 4, rs) == 4);
+    /* sample (0.25, 0.25) of pixel (0,0): world (hw - 0.25*ps, hh - 0.25*ps, -1) */
+    double wx = cam.half_width - 0.25 * cam.pixel_size, wy = cam.half_height - 0.25 * cam.pixel_size;
+    CHECK_T3(rs[0].direction, or_normalize(or_t3(wx, wy, -1)).x, or_normalize(or_t3(wx, wy, -1)).y,
+             or_normalize(or_t3(wx, wy, -1)).z);
+  }
 
   /* ------------------------------------------------------------ matrix.rs */
   CASE("matrix_multiply_two_matrices") { /* matrix.rs:373 */
@@ -137,7 +297,7 @@ int main(void) {
   /* ----------------------------------------------------- shapes / geometry */
   CASE("sphere_intersections") { /* sphere.rs:91-159 */
     oshape s = or_sphere_default();
-    double t[2];
+    double t[OR_MAX_LOCAL_XS];
     CHECK(count_intersect(&s, R(0, 0, -5, 0, 0, 1), t) == 2); CHECK_EQ(t[0], 4.0); CHECK_EQ(t[1], 6.0);
     CHECK(count_intersect(&s, R(0, 1, -5, 0, 0, 1), t) == 2); CHECK_EQ(t[0], 5.0); CHECK_EQ(t[1], 5.0);
     CHECK(count_intersect(&s, R(0, 2, -5, 0, 0, 1), t) == 0);
@@ -170,7 +330,7 @@ int main(void) {
     oshape p = or_plane_default();
     CHECK_T3(or_normal_at(&p, or_t3(0, 0, 0)), 0, 1, 0);
     CHECK_T3(or_normal_at(&p, or_t3(10, 0, -10)), 0, 1, 0);
-    double t[2];
+    double t[OR_MAX_LOCAL_XS];
     oray r = R(0, 10, 0, 0, 0, 1);
     CHECK(or_local_intersect(&p, &r, t) == 0);
     r = R(0, 0, 0, 0, 0, 1);
@@ -543,7 +703,7 @@ int main(void) {
     rt_camera_desc cd;
     double* img = (double*)calloc(11 * 11 * 3, sizeof(double));
     oracle_camera_init(11, 11, PI / 2.0, vt.e, &cd);
-    oracle_render_rows(&w, &cd, 5, NULL, 11, 2, img, NULL);
+    oracle_render_rows(&w, &cd, 5, 1, NULL, 11, 2, img, NULL);
     const double* px = img + (5 * 11 + 5) * 3;
     CHECK_T3(or_t3(px[0], px[1], px[2]), 0.38066, 0.47583, 0.2855);
     free(img);

@@ -22,7 +22,7 @@ LIB = os.path.join(BUILD, "liboracle.so")
 class Stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in (
         "rays_primary", "rays_reflect", "rays_refract", "rays_shadow",
-        "sphere_tests", "plane_tests", "sphere_disc_ge0")] + [
+        "sphere_tests", "plane_tests", "sphere_disc_ge0", "other_tests")] + [
         ("ms_kernel", ctypes.c_double), ("ms_total", ctypes.c_double)]
 
     def as_dict(self):
@@ -52,7 +52,7 @@ def _load():
     lib.oracle_is_shadowed.argtypes = [P, D, U]
     lib.oracle_is_shadowed.restype = I
     lib.oracle_hit.argtypes = [P, D, D]
-    lib.oracle_render_rows.argtypes = [P, ctypes.c_char_p, U, ctypes.POINTER(ctypes.c_uint32), U, U, D,
+    lib.oracle_render_rows.argtypes = [P, ctypes.c_char_p, U, U, ctypes.POINTER(ctypes.c_uint32), U, U, D,
                                        ctypes.POINTER(Stats)]
     lib.oracle_render_rows.restype = I
     lib.oracle_canvas_to_ppm.argtypes = [D, U, U, ctypes.c_char_p, S]
@@ -136,21 +136,24 @@ class OracleWorld:
         lib().oracle_hit(self._w, _dptr(ray), _dptr(out))
         return out
 
-    def render_rows(self, camera_desc, max_depth, rows, nthreads=1):
-        """Render the given rows (list of y) with the reference algorithm.
-        Returns (rgb[len(rows), hsize, 3], stats)."""
+    def render_rows(self, camera_desc, max_depth, rows, nthreads=1, aa_samples=1):
+        """Render the given rows (list of y) with the reference algorithm:
+        `Camera::render` (aa_samples 1) or `render_multithreaded` with
+        AA X2..X16. Returns (rgb[len(rows), hsize, 3], stats)."""
         hsize = np.frombuffer(camera_desc[:4], dtype=np.uint32)[0]
         rows = np.ascontiguousarray(rows, dtype=np.uint32)
         out = np.zeros((len(rows), hsize, 3))
         st = Stats()
-        lib().oracle_render_rows(self._w, camera_desc, max_depth,
+        rc = lib().oracle_render_rows(self._w, camera_desc, max_depth, aa_samples,
                                  rows.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), len(rows),
                                  nthreads, _dptr(out), ctypes.byref(st))
+        if rc != 0:
+            raise ValueError(f"oracle_render_rows rc={rc}")
         return out, st.as_dict()
 
-    def render(self, camera_desc, max_depth, nthreads=1):
+    def render(self, camera_desc, max_depth, nthreads=1, aa_samples=1):
         vsize = int(np.frombuffer(camera_desc[4:8], dtype=np.uint32)[0])
-        return self.render_rows(camera_desc, max_depth, list(range(vsize)), nthreads)
+        return self.render_rows(camera_desc, max_depth, list(range(vsize)), nthreads, aa_samples)
 
 
 def matrix_inverse(m16):

@@ -345,6 +345,28 @@ oshape or_plane_default(void) { /* plane.rs:19-31 */
   s.bbox.max = or_t3(INFINITY, 0.0, INFINITY);
   return s;
 }
+oshape or_cube_default(void) { /* cube.rs:17-26 */
+  oshape s = or_shape_base(RT_SHAPE_CUBE);
+  s.bbox.min = or_t3(-1, -1, -1);
+  s.bbox.max = or_t3(1, 1, 1);
+  return s;
+}
+oshape or_cylinder_new(double minimum, double maximum, int closed) { /* cylinder.rs:27-42 */
+  oshape s = or_shape_base(RT_SHAPE_CYLINDER);
+  s.bbox.min = or_t3(-1.0, minimum, -1.0);
+  s.bbox.max = or_t3(1.0, maximum, 1.0);
+  s.minimum = minimum; s.maximum = maximum; s.closed = closed ? 1 : 0;
+  return s;
+}
+oshape or_cone_new(double minimum, double maximum, int closed) { /* cone.rs:26-47 */
+  oshape s = or_shape_base(RT_SHAPE_CONE);
+  double a = fabs(minimum), b = fabs(maximum);
+  double limit = fmax(a, b); /* f64::max */
+  s.bbox.min = or_t3(-limit, minimum, -limit);
+  s.bbox.max = or_t3(limit, maximum, limit);
+  s.minimum = minimum; s.maximum = maximum; s.closed = closed ? 1 : 0;
+  return s;
+}
 /* geometry/mod.rs:74-85 */
 int or_shape_set_transform(oshape* s, const omat* t) {
   s->bbox = or_bbox_transform(&s->bbox, &s->inverse);
@@ -357,16 +379,102 @@ int or_shape_set_transform(oshape* s, const omat* t) {
   s->bbox = or_bbox_transform(&s->bbox, &s->transform);
   return RT_OK;
 }
-/* sphere.rs:40-45 / plane.rs:46-51 -> derived PartialEq of BaseShape (mod.rs:12) */
+/* sphere.rs:40-45 / plane.rs:46-51 / cube.rs:63-68 -> derived PartialEq of
+ * BaseShape (mod.rs:12); Cylinder / Cone also compare minimum, maximum,
+ * closed (derived PartialEq, cylinder.rs:12, cone.rs:12). */
 int or_shape_equals(const oshape* a, const oshape* b) {
   if (a->kind != b->kind) return 0;
+  if ((a->kind == RT_SHAPE_CYLINDER || a->kind == RT_SHAPE_CONE) &&
+      !(a->minimum == b->minimum && a->maximum == b->maximum && a->closed == b->closed))
+    return 0;
   return om_eq(&a->transform, &b->transform) && om_eq(&a->inverse, &b->inverse) &&
          om_eq(&a->inverse_t, &b->inverse_t) && or_material_eq(&a->material, &b->material) &&
          or_bbox_eq(&a->bbox, &b->bbox) && a->shadow == b->shadow;
 }
 
-/* sphere.rs:47-62 / plane.rs:53-60. Returns the number of roots. */
-int or_local_intersect(const oshape* s, const oray* ray, double t_out[2]) {
+/* cube.rs:29-47 */
+static void or_cube_check_axis(double origin, double direction, double* tmin_out, double* tmax_out) {
+  double tmin_numerator = -1.0 - origin;
+  double tmax_numerator = 1.0 - origin;
+  double tmin, tmax;
+  if (fabs(direction) >= OR_EPSILON) {
+    tmin = tmin_numerator / direction;
+    tmax = tmax_numerator / direction;
+  } else {
+    tmin = tmin_numerator * INFINITY;
+    tmax = tmax_numerator * INFINITY;
+  }
+  if (tmin > tmax) { double t = tmin; tmin = tmax; tmax = t; }
+  *tmin_out = tmin; *tmax_out = tmax;
+}
+/* cylinder.rs:44-48 (radius 1) and cone.rs:70-74 (radius = the cap's y) */
+static int or_check_cap(const oray* ray, double t, double radius) {
+  double x = ray->origin.x + t * ray->direction.x;
+  double z = ray->origin.z + t * ray->direction.z;
+  return (x * x + z * z) <= radius * radius;
+}
+/* cylinder.rs:50-67 / cone.rs:52-68 */
+static int or_intersect_caps(const oshape* s, const oray* ray, double* t_out, int n) {
+  if (!s->closed) return n;
+  int cone = s->kind == RT_SHAPE_CONE;
+  double t = (s->minimum - ray->origin.y) / ray->direction.y;
+  if (cone ? or_check_cap(ray, t, s->minimum) : or_check_cap(ray, t, 1.0)) t_out[n++] = t;
+  t = (s->maximum - ray->origin.y) / ray->direction.y;
+  if (cone ? or_check_cap(ray, t, s->maximum) : or_check_cap(ray, t, 1.0)) t_out[n++] = t;
+  return n;
+}
+
+/* sphere.rs:47-62 / plane.rs:53-60 / cube.rs:71-93 / cylinder.rs:92-120 /
+ * cone.rs:92-133. Returns the number of roots, in the reference's push order. */
+int or_local_intersect(const oshape* s, const oray* ray, double t_out[OR_MAX_LOCAL_XS]) {
+  const ot3 o = ray->origin, d = ray->direction;
+  if (s->kind == RT_SHAPE_CUBE) {
+    double xtmin, xtmax, ytmin, ytmax, ztmin, ztmax;
+    or_cube_check_axis(o.x, d.x, &xtmin, &xtmax);
+    or_cube_check_axis(o.y, d.y, &ytmin, &ytmax);
+    or_cube_check_axis(o.z, d.z, &ztmin, &ztmax);
+    double tmin = fmax(fmax(xtmin, ytmin), ztmin); /* f64::max ignores NaN like fmax */
+    double tmax = fmin(fmin(xtmax, ytmax), ztmax);
+    if (tmin > tmax) return 0;
+    t_out[0] = tmin; t_out[1] = tmax;
+    return 2;
+  }
+  if (s->kind == RT_SHAPE_CYLINDER) {
+    double a = d.x * d.x + d.z * d.z; /* powi(2) = x*x */
+    if (fabs(a) < OR_EPSILON) return or_intersect_caps(s, ray, t_out, 0);
+    double b = 2.0 * o.x * d.x + 2.0 * o.z * d.z;
+    double c = o.x * o.x + o.z * o.z - 1.0;
+    double disc = b * b - 4.0 * a * c;
+    if (disc < 0.0) return 0; /* no caps either (cylinder.rs:103-105) */
+    double t0 = (-b - sqrt(disc)) / (2.0 * a);
+    double t1 = (-b + sqrt(disc)) / (2.0 * a);
+    int n = 0;
+    double y0 = o.y + t0 * d.y;
+    if (s->minimum < y0 && y0 < s->maximum) t_out[n++] = t0;
+    double y1 = o.y + t1 * d.y;
+    if (s->minimum < y1 && y1 < s->maximum) t_out[n++] = t1;
+    return or_intersect_caps(s, ray, t_out, n);
+  }
+  if (s->kind == RT_SHAPE_CONE) {
+    double a = d.x * d.x - d.y * d.y + d.z * d.z;
+    double b = 2.0 * o.x * d.x - 2.0 * o.y * d.y + 2.0 * o.z * d.z;
+    double c = o.x * o.x - o.y * o.y + o.z * o.z;
+    if (fabs(a) < OR_EPSILON) {
+      if (fabs(b) < OR_EPSILON) return or_intersect_caps(s, ray, t_out, 0);
+      t_out[0] = -c / 2.0 * b; /* sic: (-c / 2) * b (cone.rs:104) */
+      return or_intersect_caps(s, ray, t_out, 1);
+    }
+    double disc = b * b - 4.0 * a * c;
+    if (disc < 0.0) return 0;
+    double t0 = (-b - sqrt(disc)) / (2.0 * a);
+    double t1 = (-b + sqrt(disc)) / (2.0 * a);
+    int n = 0;
+    double y0 = o.y + t0 * d.y;
+    if (s->minimum < y0 && y0 < s->maximum) t_out[n++] = t0;
+    double y1 = o.y + t1 * d.y;
+    if (s->minimum < y1 && y1 < s->maximum) t_out[n++] = t1;
+    return or_intersect_caps(s, ray, t_out, n);
+  }
   if (s->kind == RT_SHAPE_SPHERE) {
     ot3 sphere_to_ray = or_sub(ray->origin, or_t3(0, 0, 0));
     double a = or_dot(ray->direction, ray->direction);
@@ -384,22 +492,43 @@ int or_local_intersect(const oshape* s, const oray* ray, double t_out[2]) {
   }
 }
 /* geometry/mod.rs:46-49 + ray.rs:26-28 */
-int or_shape_intersect(const oshape* s, const oray* r, double t_out[2], rt_stats* st) {
+int or_shape_intersect(const oshape* s, const oray* r, double t_out[OR_MAX_LOCAL_XS], rt_stats* st) {
   oray local;
   local.origin = om_mul_point(&s->inverse, r->origin);
   local.direction = om_mul_vector(&s->inverse, r->direction);
   int n = or_local_intersect(s, &local, t_out);
   if (st) {
     if (s->kind == RT_SHAPE_SPHERE) { st->sphere_tests++; if (n) st->sphere_disc_ge0++; }
-    else st->plane_tests++;
+    else if (s->kind == RT_SHAPE_PLANE) st->plane_tests++;
+    else st->other_tests++;
   }
   return n;
 }
 /* geometry/mod.rs:51-56 */
+ot3 or_local_normal_at(const oshape* s, ot3 p) {
+  switch (s->kind) {
+    case RT_SHAPE_SPHERE: return or_sub(p, or_t3(0, 0, 0)); /* sphere.rs:64-67 */
+    case RT_SHAPE_PLANE: return or_t3(0, 1, 0);              /* plane.rs:62-64 */
+    case RT_SHAPE_CUBE: {                                     /* cube.rs:95-106 */
+      double maxc = fmax(fmax(fabs(p.x), fabs(p.y)), fabs(p.z));
+      if (or_equal(maxc, fabs(p.x))) return or_t3(p.x, 0.0, 0.0);
+      if (or_equal(maxc, fabs(p.y))) return or_t3(0.0, p.y, 0.0);
+      return or_t3(0.0, 0.0, p.z);
+    }
+    default: { /* cylinder.rs:122-130 / cone.rs:135-149 */
+      double dist = p.x * p.x + p.z * p.z;
+      if (dist < 1.0 && p.y >= s->maximum - OR_EPSILON) return or_t3(0, 1, 0);
+      if (dist < 1.0 && p.y <= s->minimum + OR_EPSILON) return or_t3(0, -1, 0);
+      if (s->kind == RT_SHAPE_CYLINDER) return or_t3(p.x, 0.0, p.z);
+      double y = sqrt(p.x * p.x + p.z * p.z);
+      if (p.y > 0.0) y = -y;
+      return or_t3(p.x, y, p.z);
+    }
+  }
+}
 ot3 or_normal_at(const oshape* s, ot3 point) {
   ot3 local_point = om_mul_point(&s->inverse, point);
-  ot3 local_normal = s->kind == RT_SHAPE_SPHERE ? or_sub(local_point, or_t3(0, 0, 0))
-                                                : or_t3(0, 1, 0);
+  ot3 local_normal = or_local_normal_at(s, local_point);
   ot3 world_normal = om_mul_vector(&s->inverse_t, local_normal);
   return or_normalize(world_normal);
 }
@@ -432,7 +561,7 @@ oxs* or_world_intersect(const oworld* w, const oray* r, int* n_out, rt_stats* st
   int cap = 8, n = 0;
   oxs* xs = (oxs*)malloc(sizeof(oxs) * cap);
   for (int i = 0; i < w->n; ++i) {
-    double t[2];
+    double t[OR_MAX_LOCAL_XS];
     int k = or_shape_intersect(&w->objects[i], r, t, st);
     for (int j = 0; j < k; ++j) {
       if (n == cap) { cap *= 2; xs = (oxs*)realloc(xs, sizeof(oxs) * cap); }
@@ -675,6 +804,39 @@ oray or_ray_for_pixel(const ocamera* c, uint32_t px, uint32_t py) {
   r.direction = or_normalize(or_sub(pixel, origin));
   return r;
 }
+/* :92-126 get_offsets */
+static const double OR_AA_X1[] = {0.5, 0.5};
+static const double OR_AA_X2[] = {0.25, 0.5, 0.75, 0.5};
+static const double OR_AA_X4[] = {0.25, 0.25, 0.75, 0.25, 0.25, 0.75, 0.75, 0.75};
+static const double OR_AA_X8[] = {0.25, 0.25, 0.5, 0.25, 0.75, 0.25, 0.25, 0.5,
+                                  0.75, 0.5,  0.25, 0.75, 0.5, 0.75, 0.75, 0.75};
+static const double OR_AA_X16[] = {0.125, 0.125, 0.375, 0.125, 0.625, 0.125, 0.875, 0.125,
+                                   0.125, 0.375, 0.375, 0.375, 0.625, 0.375, 0.875, 0.375,
+                                   0.125, 0.625, 0.375, 0.625, 0.625, 0.625, 0.875, 0.625,
+                                   0.125, 0.875, 0.375, 0.875, 0.625, 0.875, 0.875, 0.875};
+/* :71-90. Returns the number of rays (0 for an unsupported sample count). */
+int or_rays_for_pixel(const ocamera* c, uint32_t px, uint32_t py, uint32_t aa_samples, oray* out) {
+  const double* off;
+  switch (aa_samples) {
+    case 1: off = OR_AA_X1; break;
+    case 2: off = OR_AA_X2; break;
+    case 4: off = OR_AA_X4; break;
+    case 8: off = OR_AA_X8; break;
+    case 16: off = OR_AA_X16; break;
+    default: return 0;
+  }
+  for (uint32_t i = 0; i < aa_samples; ++i) {
+    double xoffset = ((double)px + off[2 * i]) * c->pixel_size;
+    double yoffset = ((double)py + off[2 * i + 1]) * c->pixel_size;
+    double world_x = c->half_width - xoffset;
+    double world_y = c->half_height - yoffset;
+    ot3 pixel = om_mul_point(&c->inverse, or_t3(world_x, world_y, -1.0));
+    ot3 origin = om_mul_point(&c->inverse, or_t3(0, 0, 0));
+    out[i].origin = origin;
+    out[i].direction = or_normalize(or_sub(pixel, origin));
+  }
+  return (int)aa_samples;
+}
 
 /* ---------------------------------------------------------- image/ppm.rs */
 /* :73-75: (v*255.0).round() as u8 — round half away from zero, saturating */
@@ -736,6 +898,9 @@ int oracle_world_add_desc(oworld* w, const rt_shape_desc* d) {
   oshape s;
   if (d->kind == RT_SHAPE_SPHERE) s = or_sphere_default();
   else if (d->kind == RT_SHAPE_PLANE) s = or_plane_default();
+  else if (d->kind == RT_SHAPE_CUBE) s = or_cube_default();
+  else if (d->kind == RT_SHAPE_CYLINDER) s = or_cylinder_new(d->minimum, d->maximum, d->closed);
+  else if (d->kind == RT_SHAPE_CONE) s = or_cone_new(d->minimum, d->maximum, d->closed);
   else return RT_ERR_UNSUPPORTED_SHAPE;
   omaterial* m = &s.material;
   m->color = or_v3(d->color);
@@ -766,6 +931,7 @@ int oracle_world_export_desc(const oworld* w, rt_shape_desc* out, size_t cap) {
     rt_shape_desc* d = &out[i];
     memset(d, 0, sizeof *d);
     d->kind = s->kind; d->casts_shadow = s->shadow;
+    d->minimum = s->minimum; d->maximum = s->maximum; d->closed = s->closed;
     memcpy(d->transform, s->transform.e, sizeof d->transform);
     memcpy(d->inverse, s->inverse.e, sizeof d->inverse);
     const omaterial* m = &s->material;
@@ -845,7 +1011,7 @@ void oracle_hit(const oworld* w, const double ray[6], double o[24]) {
 typedef struct {
   const oworld* w;
   ocamera cam;
-  uint32_t max_depth;
+  uint32_t max_depth, aa;
   const uint32_t* rows;
   uint32_t i0, i1; /* indices into the row list */
   double* out;
@@ -857,8 +1023,17 @@ static void* or_render_worker(void* arg) {
   for (uint32_t i = j->i0; i < j->i1; ++i) {
     uint32_t y = j->rows[i];
     for (uint32_t x = 0; x < j->cam.hsize; ++x) {
-      oray r = or_ray_for_pixel(&j->cam, x, y);
-      ot3 c = or_color_at(j->w, &r, j->max_depth, &j->st);
+      ot3 c;
+      if (j->aa <= 1) { /* Camera::render (camera.rs:141-143) */
+        oray r = or_ray_for_pixel(&j->cam, x, y);
+        c = or_color_at(j->w, &r, j->max_depth, &j->st);
+      } else { /* render_multithreaded (camera.rs:176-185) + Color::average (color.rs:26-33) */
+        oray rays[16];
+        int n = or_rays_for_pixel(&j->cam, x, y, j->aa, rays);
+        c = or_t3(0, 0, 0);
+        for (int s = 0; s < n; ++s) c = or_add(c, or_color_at(j->w, &rays[s], j->max_depth, &j->st));
+        c = or_scale(c, 1.0 / (double)n);
+      }
       double* px = j->out + ((size_t)i * j->cam.hsize + x) * 3;
       px[0] = c.x; px[1] = c.y; px[2] = c.z;
     }
@@ -867,8 +1042,10 @@ static void* or_render_worker(void* arg) {
 }
 
 int oracle_render_rows(const oworld* w, const rt_camera_desc* cam, uint32_t max_depth,
-                       const uint32_t* rows, uint32_t n_rows, uint32_t nthreads, double* out_rgb,
-                       rt_stats* st) {
+                       uint32_t aa_samples, const uint32_t* rows, uint32_t n_rows, uint32_t nthreads,
+                       double* out_rgb, rt_stats* st) {
+  if (!(aa_samples == 1 || aa_samples == 2 || aa_samples == 4 || aa_samples == 8 || aa_samples == 16))
+    return RT_ERR_INVALID_ARGUMENT;
   ocamera c;
   memset(&c, 0, sizeof c);
   c.hsize = cam->hsize; c.vsize = cam->vsize;
@@ -886,7 +1063,7 @@ int oracle_render_rows(const oworld* w, const rt_camera_desc* cam, uint32_t max_
   pthread_t* th = (pthread_t*)calloc(nthreads, sizeof(pthread_t));
   uint32_t per = n_rows / nthreads; /* camera.rs:157, last block takes the rest :169-172 */
   for (uint32_t t = 0; t < nthreads; ++t) {
-    jobs[t].w = w; jobs[t].cam = c; jobs[t].max_depth = max_depth; jobs[t].rows = rows;
+    jobs[t].w = w; jobs[t].cam = c; jobs[t].max_depth = max_depth; jobs[t].aa = aa_samples; jobs[t].rows = rows;
     jobs[t].i0 = t * per; jobs[t].i1 = (t == nthreads - 1) ? n_rows : (t + 1) * per;
     jobs[t].out = out_rgb;
     if (nthreads == 1) or_render_worker(&jobs[t]);
@@ -899,7 +1076,7 @@ int oracle_render_rows(const oworld* w, const rt_camera_desc* cam, uint32_t max_
       st->rays_primary += jobs[t].st.rays_primary; st->rays_reflect += jobs[t].st.rays_reflect;
       st->rays_refract += jobs[t].st.rays_refract; st->rays_shadow += jobs[t].st.rays_shadow;
       st->sphere_tests += jobs[t].st.sphere_tests; st->plane_tests += jobs[t].st.plane_tests;
-      st->sphere_disc_ge0 += jobs[t].st.sphere_disc_ge0;
+      st->sphere_disc_ge0 += jobs[t].st.sphere_disc_ge0; st->other_tests += jobs[t].st.other_tests;
     }
   }
   free(jobs); free(th); free(own);

@@ -59,6 +59,8 @@ typedef struct {
   omaterial material;
   obbox bbox;
   int shadow;
+  double minimum, maximum; /* Cylinder / Cone (cylinder.rs:12-18, cone.rs:12-18) */
+  int closed;
 } oshape;
 
 typedef struct { ot3 position, intensity; } olight;
@@ -136,6 +138,9 @@ ot3 or_pattern_color_at_shape(const opattern* p, const oshape* s, ot3 world_poin
 oshape or_sphere_default(void);
 oshape or_sphere_glass(void);
 oshape or_plane_default(void);
+oshape or_cube_default(void);
+oshape or_cylinder_new(double minimum, double maximum, int closed);
+oshape or_cone_new(double minimum, double maximum, int closed);
 int or_shape_set_transform(oshape* s, const omat* t);
 int or_shape_equals(const oshape* a, const oshape* b);
 
@@ -146,11 +151,13 @@ int or_world_add_light(oworld* w, ot3 pos, ot3 intensity);
 void or_world_default(oworld* w);
 
 /* ---- hot path (world.rs, geometry/{mod,intersection,shape}.rs, material.rs, camera.rs) ---- */
-int or_local_intersect(const oshape* s, const oray* local, double t_out[2]);
-int or_shape_intersect(const oshape* s, const oray* r, double t_out[2], rt_stats* st);
+#define OR_MAX_LOCAL_XS 4 /* most intersections one local_intersect returns (cylinder/cone) */
+int or_local_intersect(const oshape* s, const oray* local, double t_out[OR_MAX_LOCAL_XS]);
+int or_shape_intersect(const oshape* s, const oray* r, double t_out[OR_MAX_LOCAL_XS], rt_stats* st);
 oxs* or_world_intersect(const oworld* w, const oray* r, int* n_out, rt_stats* st);
 void or_sort_intersections(oxs* xs, int n);
 int or_hit(const oxs* xs, int n); /* index into xs or -1 */
+ot3 or_local_normal_at(const oshape* s, ot3 local_point);
 ot3 or_normal_at(const oshape* s, ot3 point);
 ocomps or_prepare_computations(const oworld* w, const oxs* hit, const oray* r,
                                const oxs* xs, int n);
@@ -166,6 +173,7 @@ ot3 or_refracted_color(const oworld* w, const ocomps* c, unsigned remaining, rt_
 void or_camera_new(ocamera* c, uint32_t hsize, uint32_t vsize, double fov);
 int or_camera_set_transform(ocamera* c, const omat* t);
 oray or_ray_for_pixel(const ocamera* c, uint32_t px, uint32_t py);
+int or_rays_for_pixel(const ocamera* c, uint32_t px, uint32_t py, uint32_t aa_samples, oray* out);
 
 uint8_t or_scale_color_component(double v);
 size_t or_canvas_to_ppm(const double* rgb, uint32_t w, uint32_t h, char* out, size_t cap);
@@ -184,12 +192,14 @@ void oracle_color_at(const oworld* w, const double ray[6], uint32_t remaining,
                      double out[3], rt_stats* st);
 int oracle_is_shadowed(const oworld* w, const double p[3], uint32_t light);
 void oracle_hit(const oworld* w, const double ray[6], double out24[24]);
-/* Render rows [y0, y1) (or the explicit list `rows` of n_rows rows when
+/* Render rows [0, n_rows) (or the explicit list `rows` of n_rows rows when
  * rows != NULL) into out_rgb (n_rows*hsize*3, rows in the given order) with
- * nthreads threads in contiguous row blocks (camera.rs:150-217). */
+ * nthreads threads in contiguous row blocks (camera.rs:150-217).
+ * aa_samples == 1: `Camera::render` (camera.rs:133-148, ray_for_pixel);
+ * 2/4/8/16: `render_multithreaded` with `rays_for_pixel` + `Color::average`. */
 int oracle_render_rows(const oworld* w, const rt_camera_desc* cam, uint32_t max_depth,
-                       const uint32_t* rows, uint32_t n_rows, uint32_t nthreads,
-                       double* out_rgb, rt_stats* st);
+                       uint32_t aa_samples, const uint32_t* rows, uint32_t n_rows,
+                       uint32_t nthreads, double* out_rgb, rt_stats* st);
 size_t oracle_canvas_to_ppm(const double* rgb, uint32_t w, uint32_t h, char* out, size_t cap);
 int oracle_nan_seen(void);
 

@@ -7,6 +7,7 @@
 // builds and flattens the scene (host-side, like the reference's setup code).
 #pragma once
 #include <cstring>
+#include <limits>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -77,6 +78,10 @@ struct Shape {
   Matrix transform_inverse = Matrix::identity(4, 4);
   Material material;
   bool shadow = true;
+  // Cylinder / Cone bounds (cylinder.rs:12-18, cone.rs:12-18)
+  double minimum = -std::numeric_limits<double>::infinity();
+  double maximum = std::numeric_limits<double>::infinity();
+  bool closed = false;
   void set_transform(const Matrix& t) {  // geometry/mod.rs:74-85
     transform_inverse = t.inverse();
     transform = t;
@@ -96,6 +101,26 @@ inline Shape glass_sphere() {
 inline Shape Plane() {  // plane.rs:19-31
   Shape s;
   s.kind = RT_SHAPE_PLANE;
+  return s;
+}
+inline Shape Cube() {  // cube.rs:17-26
+  Shape s;
+  s.kind = RT_SHAPE_CUBE;
+  return s;
+}
+// cylinder.rs:20-40 (Cylinder::default = new(-inf, inf, false))
+inline Shape Cylinder(double minimum = -std::numeric_limits<double>::infinity(),
+                      double maximum = std::numeric_limits<double>::infinity(), bool closed = false) {
+  Shape s;
+  s.kind = RT_SHAPE_CYLINDER;
+  s.minimum = minimum; s.maximum = maximum; s.closed = closed;
+  return s;
+}
+// cone.rs:20-46
+inline Shape Cone(double minimum = -std::numeric_limits<double>::infinity(),
+                  double maximum = std::numeric_limits<double>::infinity(), bool closed = false) {
+  Shape s = Cylinder(minimum, maximum, closed);
+  s.kind = RT_SHAPE_CONE;
   return s;
 }
 
@@ -149,6 +174,7 @@ inline rt_shape_desc to_desc(const Shape& s) {
   d.pattern_b[0] = p.b.red; d.pattern_b[1] = p.b.green; d.pattern_b[2] = p.b.blue;
   std::memcpy(d.pattern_transform, p.transform.data(), sizeof d.pattern_transform);
   std::memcpy(d.pattern_inverse, p.transform_inverse.data(), sizeof d.pattern_inverse);
+  d.minimum = s.minimum; d.maximum = s.maximum; d.closed = s.closed ? 1 : 0;
   return d;
 }
 
@@ -235,6 +261,18 @@ class World {
   mutable int scene_device_ = -1;
 };
 
+// camera.rs:220-253
+enum class AASamples { X1 = 1, X2 = 2, X4 = 4, X8 = 8, X16 = 16 };
+struct RenderOpts {
+  size_t n_threads = 1;  // CPU partitioning in the reference; no effect on the image here
+  AASamples samples = AASamples::X1;
+  void num_threads(size_t n) {  // camera.rs:244-247
+    if (n == 0) throw std::invalid_argument("num_threads must be > 0");
+    n_threads = n;
+  }
+  void aa_samples(AASamples s) { samples = s; }  // camera.rs:249-251
+};
+
 // camera.rs:19-253
 class Camera {
  public:
@@ -266,6 +304,14 @@ class Camera {
     check(rt_render(world.scene(), &desc_, max_depth, c.data(), stats), "rt_render");
     return c;
   }
+  // camera.rs:150-214: average of `rays_for_pixel` per pixel (render_opts.aa_samples).
+  Canvas render_multithreaded(const World& world, unsigned max_depth = 5, rt_stats* stats = nullptr) const {
+    Canvas c(desc_.hsize, desc_.vsize);
+    check(rt_render_aa(world.scene(), &desc_, max_depth, (uint32_t)render_opts.samples, c.data(), stats),
+          "rt_render_aa");
+    return c;
+  }
+  RenderOpts render_opts;
 
  private:
   double fov_;

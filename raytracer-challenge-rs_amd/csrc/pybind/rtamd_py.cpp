@@ -21,6 +21,7 @@ static py::dict stats_dict(const rt_stats& s) {
   d["sphere_tests"] = s.sphere_tests;
   d["plane_tests"] = s.plane_tests;
   d["sphere_disc_ge0"] = s.sphere_disc_ge0;
+  d["other_tests"] = s.other_tests;
   d["ms_kernel"] = s.ms_kernel;
   d["ms_total"] = s.ms_total;
   return d;
@@ -36,7 +37,6 @@ static py::array_t<double> check_rays(py::array_t<double, py::array::c_style | p
 }
 
 extern "C" int rtamd_tuning_set(const char* key, int value);
-extern "C" int rtamd_diag_last(const rt_scene* s, unsigned long long out[3]);
 extern "C" int rtamd_wf_profile(const rt_scene* s, int enable, double out[16]);
 
 PYBIND11_MODULE(_rtamd, m) {
@@ -179,6 +179,9 @@ PYBIND11_MODULE(_rtamd, m) {
   py::class_<Shape>(m, "Shape")
       .def_readonly("kind", &Shape::kind)
       .def_readwrite("material", &Shape::material)
+      .def_readwrite("minimum", &Shape::minimum)
+      .def_readwrite("maximum", &Shape::maximum)
+      .def_readwrite("closed", &Shape::closed)
       .def_readonly("transform", &Shape::transform)
       .def_readonly("transform_inverse", &Shape::transform_inverse)
       .def("transform_inverse_transpose", &Shape::transform_inverse_transpose)
@@ -189,6 +192,19 @@ PYBIND11_MODULE(_rtamd, m) {
   m.def("Sphere", &Sphere);
   m.def("glass_sphere", &glass_sphere);
   m.def("Plane", &Plane);
+  m.def("Cube", &Cube);
+  m.def("Cylinder", &Cylinder, py::arg("minimum") = -std::numeric_limits<double>::infinity(),
+        py::arg("maximum") = std::numeric_limits<double>::infinity(), py::arg("closed") = false);
+  m.def("Cone", &Cone, py::arg("minimum") = -std::numeric_limits<double>::infinity(),
+        py::arg("maximum") = std::numeric_limits<double>::infinity(), py::arg("closed") = false);
+
+  py::enum_<AASamples>(m, "AASamples")
+      .value("X1", AASamples::X1).value("X2", AASamples::X2).value("X4", AASamples::X4)
+      .value("X8", AASamples::X8).value("X16", AASamples::X16);
+  py::class_<RenderOpts>(m, "RenderOpts")
+      .def("num_threads", &RenderOpts::num_threads)
+      .def("aa_samples", &RenderOpts::aa_samples)
+      .def_property_readonly("samples", [](const RenderOpts& o) { return (int)o.samples; });
 
   py::class_<Canvas>(m, "Canvas")
       .def(py::init<size_t, size_t>())
@@ -289,21 +305,32 @@ PYBIND11_MODULE(_rtamd, m) {
         }
         return py::make_tuple(std::unique_ptr<Canvas>(out), stats_dict(st));
       }, py::arg("world"), py::arg("max_depth") = 5)
+      .def_readwrite("render_opts", &Camera::render_opts, py::return_value_policy::reference_internal)
+      .def("render_multithreaded", [](const Camera& c, const World& w, unsigned max_depth) {
+        rt_stats st{};
+        Canvas* out;
+        {
+          py::gil_scoped_release nogil;
+          out = new Canvas(c.render_multithreaded(w, max_depth, &st));
+        }
+        return py::make_tuple(std::unique_ptr<Canvas>(out), stats_dict(st));
+      }, py::arg("world"), py::arg("max_depth") = 5)
       .def("render_shard_device", [](const Camera& c, const World& w, unsigned max_depth, unsigned row_block,
                                      unsigned shard, unsigned n_shards, uintptr_t d_out, uintptr_t stream,
-                                     bool want_stats) {
+                                     bool want_stats, unsigned aa_samples) {
         rt_stats st{};
         int rc;
         {
           py::gil_scoped_release nogil;
-          rc = rt_render_shard_device(w.scene(), &c.desc(), max_depth, row_block, shard, n_shards, (double*)d_out,
-                                      (void*)stream, want_stats ? &st : nullptr);
+          rc = rt_render_shard_device(w.scene(), &c.desc(), max_depth, aa_samples, row_block, shard, n_shards,
+                                      (double*)d_out, (void*)stream, want_stats ? &st : nullptr);
         }
         check(rc, "rt_render_shard_device");
         return stats_dict(st);
       }, py::arg("world"), py::arg("max_depth"), py::arg("row_block"), py::arg("shard"), py::arg("n_shards"),
-         py::arg("d_out"), py::arg("stream") = 0, py::arg("want_stats") = false)
-      .def("render_multi", [](const Camera& c, std::vector<World*> worlds, unsigned max_depth, unsigned row_block) {
+         py::arg("d_out"), py::arg("stream") = 0, py::arg("want_stats") = false, py::arg("aa_samples") = 1)
+      .def("render_multi", [](const Camera& c, std::vector<World*> worlds, unsigned max_depth, unsigned row_block,
+                              unsigned aa_samples) {
         std::vector<rt_scene*> sc;
         for (size_t i = 0; i < worlds.size(); ++i) sc.push_back(const_cast<rt_scene*>(worlds[i]->scene((int)i)));
         Canvas* out = new Canvas(c.hsize(), c.vsize());
@@ -311,17 +338,13 @@ PYBIND11_MODULE(_rtamd, m) {
         int rc;
         {
           py::gil_scoped_release nogil;
-          rc = rt_render_multi(sc.data(), (int)sc.size(), &c.desc(), max_depth, row_block, out->data(), &st);
+          rc = rt_render_multi(sc.data(), (int)sc.size(), &c.desc(), max_depth, aa_samples, row_block, out->data(),
+                               &st);
         }
         if (rc != RT_OK) { delete out; check(rc, "rt_render_multi"); }
         return py::make_tuple(std::unique_ptr<Canvas>(out), stats_dict(st));
-      });
+      }, py::arg("worlds"), py::arg("max_depth") = 5, py::arg("row_block") = 8, py::arg("aa_samples") = 1);
   m.def("shard_rows", &rt_shard_rows);
-  m.def("_diag_last", [](const World& w) {
-    unsigned long long o[3];
-    check(rtamd_diag_last(w.scene(), o), "diag");
-    return py::make_tuple(o[0], o[1], o[2]);
-  });
   m.def("_wf_profile", [](const World& w, int enable, bool read) {
     double o[16] = {0};
     check(rtamd_wf_profile(w.scene(), enable, read ? o : nullptr), "wf_profile");

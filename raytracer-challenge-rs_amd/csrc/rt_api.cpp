@@ -2,8 +2,8 @@
 // device upload, render entry points, multi-GPU gather, PPM output.
 //
 // Product code: no CPU fallback anywhere. Every render entry point runs the
-// HIP kernels in rt_kernels.hip and fails loudly (RT_ERR_HIP / RT_ERR_NO_DEVICE)
-// when no device is usable.
+// HIP kernels (rt_wavefront.hip, rt_kernels.hip) and fails loudly
+// (RT_ERR_HIP / RT_ERR_NO_DEVICE) when no device is usable.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -29,12 +29,6 @@ namespace {
 
 thread_local std::string g_err;
 
-// Tuning knobs (development only; not part of the public ABI).
-int g_tune_waves = [] {
-  const char* e = std::getenv("RTAMD_WAVES");
-  return e ? std::atoi(e) : 0;
-}();
-
 int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
@@ -54,14 +48,11 @@ struct rt_scene {
   DevScene dev{};
   // device allocations
   void* d_blob = nullptr;       // trace + shade + light records
-  unsigned* d_counter = nullptr;
-  DevStats* d_stats = nullptr;
   double* d_out = nullptr;      // cached output for host-buffer entry points
   size_t out_cap = 0;           // doubles
   double* d_in = nullptr;       // cached input for batch entry points
   size_t in_cap = 0;
   hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::mutex mu;  // one call at a time per scene (shared workspace)
   Wavefront wf;   // wavefront pipeline workspace (queues grow on demand)
   int n_objects = 0, n_lights = 0;
@@ -95,6 +86,9 @@ bool may_be_equal(const rt_shape_desc& a, const rt_shape_desc& b) {
   if (!(a.ambient == b.ambient && a.diffuse == b.diffuse && a.specular == b.specular &&
         a.shininess == b.shininess && a.reflective == b.reflective &&
         a.transparency == b.transparency && a.refractive_index == b.refractive_index))
+    return false;
+  if ((a.kind == RT_SHAPE_CYLINDER || a.kind == RT_SHAPE_CONE) &&
+      !(a.minimum == b.minimum && a.maximum == b.maximum && (a.closed != 0) == (b.closed != 0)))
     return false;
   if (a.pattern_kind != b.pattern_kind) return false;
   if (a.pattern_kind != RT_PATTERN_NONE) {
@@ -143,60 +137,32 @@ DevCamera to_dev_camera(const rt_camera_desc& c) {
   return d;
 }
 
-// Launch one render (camera shard or ray batch) on `stream`. Default: the
-// wavefront pipeline; tuning knob `waves` != 0 selects the persistent
-// megakernel variants (1 = its default). `timed` records kernel events;
-// `stats_out`, when given, receives the exact counters (synchronises).
-int run_render(rt_scene* s, const DevCamera& cam, const double* d_rays, uint32_t n_tasks,
-               uint32_t max_depth, uint32_t row_block, uint32_t shard, uint32_t n_shards,
-               double* d_out, hipStream_t stream, bool timed, DevStats* stats_out = nullptr,
-               float* ms_out = nullptr) {
+bool valid_aa(uint32_t aa) { return aa == 1 || aa == 2 || aa == 4 || aa == 8 || aa == 16; }
+
+// Launch one render (camera shard or ray batch) on `stream` through the
+// wavefront pipeline. `n_tasks` root rays = pixels x aa (camera) or rays
+// (batch). `stats_out`, when given, receives the exact counters and
+// `ms_out` the kernel time (both synchronise).
+int run_render(rt_scene* s, const DevCamera& cam, const double* d_rays, uint32_t n_tasks, uint32_t aa,
+               uint32_t max_depth, uint32_t row_block, uint32_t shard, uint32_t n_shards, double* d_out,
+               hipStream_t stream, DevStats* stats_out = nullptr, float* ms_out = nullptr) {
   if (max_depth > (uint32_t)kMaxDepth)
     return fail(RT_ERR_INVALID_ARGUMENT, "max_depth > " + std::to_string(kMaxDepth));
-  if (g_tune_waves == 0) {
-    std::string sig;
-    if (!d_rays) {  // camera renders are deterministic per (camera, shard, depth)
-      sig.assign((const char*)&cam, sizeof cam);
-      const uint32_t p[5] = {n_tasks, max_depth, row_block, shard, n_shards};
-      sig.append((const char*)p, sizeof p);
-    }
-    if (n_tasks == 0) {
-      if (stats_out) *stats_out = DevStats{};
-      if (ms_out) *ms_out = 0.f;
-      return RT_OK;
-    }
-    hipError_t e = s->wf.render(s->dev, cam, d_rays == nullptr, d_rays, n_tasks, max_depth, row_block, shard,
-                                n_shards, d_out, stream, sig, stats_out, (timed || ms_out) ? ms_out : nullptr);
-    if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("wavefront render: ") + hipGetErrorString(e));
-    return RT_OK;
-  }
-  RenderArgs a{};
-  a.out = d_out;
-  a.rays = d_rays;
-  a.counter = s->d_counter;
-  a.stats = s->d_stats;
-  a.n_tasks = n_tasks;
-  a.max_depth = max_depth;
-  a.row_block = row_block;
-  a.shard = shard;
-  a.n_shards = n_shards;
-  a.grid_cap = 0;
-  a.waves = g_tune_waves == 1 ? 0 : g_tune_waves;
-  RT_HIP(hipMemsetAsync(s->d_counter, 0, 64, stream));
-  RT_HIP(hipMemsetAsync(s->d_stats, 0, sizeof(DevStats), stream));
+  if (!valid_aa(aa)) return fail(RT_ERR_INVALID_ARGUMENT, "aa_samples must be 1, 2, 4, 8 or 16");
   if (n_tasks == 0) {
     if (stats_out) *stats_out = DevStats{};
     if (ms_out) *ms_out = 0.f;
     return RT_OK;
   }
-  RT_HIP(hipEventRecord(s->ev0, stream));
-  RT_HIP(launch_render(s->dev, cam, a, stream));
-  RT_HIP(hipEventRecord(s->ev1, stream));
-  if (stats_out || ms_out) {
-    RT_HIP(hipStreamSynchronize(stream));
-    if (ms_out) RT_HIP(hipEventElapsedTime(ms_out, s->ev0, s->ev1));
-    if (stats_out) RT_HIP(hipMemcpy(stats_out, s->d_stats, sizeof(DevStats), hipMemcpyDeviceToHost));
+  std::string sig;
+  if (!d_rays) {  // camera renders are deterministic per (camera, shard, depth, aa)
+    sig.assign((const char*)&cam, sizeof cam);
+    const uint32_t p[6] = {n_tasks, aa, max_depth, row_block, shard, n_shards};
+    sig.append((const char*)p, sizeof p);
   }
+  hipError_t e = s->wf.render(s->dev, cam, d_rays == nullptr, d_rays, n_tasks, aa, max_depth, row_block, shard,
+                              n_shards, d_out, stream, sig, stats_out, ms_out);
+  if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("wavefront render: ") + hipGetErrorString(e));
   return RT_OK;
 }
 
@@ -208,6 +174,7 @@ void fill_stats(rt_stats* st, const DevStats& ds, float ms_kernel, double ms_tot
   st->sphere_tests = ds.sphere_tests;
   st->plane_tests = ds.plane_tests;
   st->sphere_disc_ge0 = ds.sphere_disc_ge0;
+  st->other_tests = ds.other_tests;
   st->ms_kernel = ms_kernel;
   st->ms_total = ms_total;
 }
@@ -218,24 +185,10 @@ extern "C" {
 
 const char* rt_last_error(void) { return g_err.c_str(); }
 
-// Development-only diagnostics of the last launch on a scene (not in the public ABI):
-// out[0] = wave-level trace steps, out[1] = DIAG trace cycles, out[2] = DIAG total cycles.
-int rtamd_diag_last(const rt_scene* s, unsigned long long out[3]) {
-  if (!s || !out) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
-  DevStats ds{};
-  RT_HIP(hipSetDevice(s->device));
-  RT_HIP(hipDeviceSynchronize());
-  RT_HIP(hipMemcpy(&ds, s->d_stats, sizeof ds, hipMemcpyDeviceToHost));
-  out[0] = ds.wave_steps;
-  out[1] = ds.diag_trace_cycles;
-  out[2] = ds.diag_total_cycles;
-  return RT_OK;
-}
-
 // Development/benchmark hook (not in the public ABI): per-kernel-class timing
 // of the wavefront pipeline. enable: 1 = on, 0 = off, -1 = just read. out[16]:
 // ms[5] (primary, closest, shadow, prep, combine), rays[3], disc[3],
-// n_diag, n_gen, n_planes.
+// n_diag, n_gen, n_planes, n_lights, n_quads.
 int rtamd_wf_profile(const rt_scene* cs, int enable, double out[16]) {
   if (!cs) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
   rt_scene* s = const_cast<rt_scene*>(cs);
@@ -248,18 +201,15 @@ int rtamd_wf_profile(const rt_scene* cs, int enable, double out[16]) {
     for (int i = 0; i < 5; ++i) out[i] = p.ms[i];
     for (int i = 0; i < 3; ++i) { out[5 + i] = p.rays[i]; out[8 + i] = p.disc[i]; }
     out[11] = s->dev.n_diag; out[12] = s->dev.n_gen; out[13] = s->dev.n_planes;
-    out[14] = s->dev.n_lights; out[15] = 0;
+    out[14] = s->dev.n_lights; out[15] = s->dev.n_quads;
   }
   return RT_OK;
 }
 
 // Development-only tuning hook (not declared in include/rt_render.h).
 int rtamd_tuning_set(const char* key, int value) {
-  if (key && std::strcmp(key, "waves") == 0) {
-    g_tune_waves = value;
-    return RT_OK;
-  }
   if (key && std::strcmp(key, "wf_waves") == 0) {
+    if (value != 4 && value != 8) return fail(RT_ERR_INVALID_ARGUMENT, "wf_waves must be 4 or 8");
     rtamd::g_wf_trace_waves = value;
     return RT_OK;
   }
@@ -318,8 +268,9 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   *out = nullptr;
   if (n_shapes > (size_t)(1u << 29)) return fail(RT_ERR_INVALID_ARGUMENT, "too many shapes");
   for (size_t i = 0; i < n_shapes; ++i) {
-    if (shapes[i].kind != RT_SHAPE_SPHERE && shapes[i].kind != RT_SHAPE_PLANE)
-      return fail(RT_ERR_UNSUPPORTED_SHAPE, "shape " + std::to_string(i) + ": only Sphere and Plane are supported");
+    if (shapes[i].kind < RT_SHAPE_SPHERE || shapes[i].kind > RT_SHAPE_CONE)
+      return fail(RT_ERR_UNSUPPORTED_SHAPE, "shape " + std::to_string(i) +
+                                                ": supported kinds are Sphere, Plane, Cube, Cylinder, Cone");
     if (shapes[i].pattern_kind < RT_PATTERN_NONE || shapes[i].pattern_kind > RT_PATTERN_CHECKERS)
       return fail(RT_ERR_INVALID_ARGUMENT, "shape " + std::to_string(i) + ": bad pattern kind");
   }
@@ -336,6 +287,7 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   std::vector<SphereDiag> diag;
   std::vector<SphereGen> gen;
   std::vector<PlaneRec> planes;
+  std::vector<QuadRec> quads;
   std::vector<ShadeRec> shade(n_shapes);
   for (size_t i = 0; i < n_shapes; ++i) {
     const rt_shape_desc& d = shapes[i];
@@ -353,11 +305,20 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
         r.meta = meta;
         gen.push_back(r);
       }
-    } else {
+    } else if (d.kind == RT_SHAPE_PLANE) {
       PlaneRec r{};
       for (int e = 0; e < 4; ++e) r.m[e] = d.inverse[4 + e];
       r.meta = meta;
       planes.push_back(r);
+    } else {
+      QuadRec r{};
+      for (int e = 0; e < 12; ++e) r.m[e] = d.inverse[e];
+      r.minimum = d.minimum;
+      r.maximum = d.maximum;
+      r.kind = d.kind;
+      r.closed = d.closed ? 1 : 0;
+      r.meta = (int32_t)meta;
+      quads.push_back(r);
     }
     ShadeRec& s = shade[i];
     std::memset(&s, 0, sizeof s);
@@ -372,6 +333,8 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
     for (int e = 0; e < 12; ++e) s.pat_inv[e] = d.pattern_inverse[e];
     s.kind = d.kind;
     s.shadow = d.casts_shadow ? 1 : 0;
+    s.minimum = d.minimum;
+    s.maximum = d.maximum;
   }
   std::vector<LightRec> lrec(n_lights);
   for (size_t i = 0; i < n_lights; ++i)
@@ -383,13 +346,15 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   // one zeroed padding record after each trace section (look-ahead loads)
   const size_t o_gen = align(o_diag + (diag.size() + 1) * sizeof(SphereDiag));
   const size_t o_pl = align(o_gen + (gen.size() + 1) * sizeof(SphereGen));
-  const size_t o_sh = align(o_pl + (planes.size() + 1) * sizeof(PlaneRec));
+  const size_t o_qd = align(o_pl + (planes.size() + 1) * sizeof(PlaneRec));
+  const size_t o_sh = align(o_qd + (quads.size() + 1) * sizeof(QuadRec));
   const size_t o_li = align(o_sh + shade.size() * sizeof(ShadeRec));
   const size_t total = align(o_li + lrec.size() * sizeof(LightRec)) + 256;
   std::vector<unsigned char> host(total, 0);
   if (!diag.empty()) std::memcpy(&host[o_diag], diag.data(), diag.size() * sizeof(SphereDiag));
   if (!gen.empty()) std::memcpy(&host[o_gen], gen.data(), gen.size() * sizeof(SphereGen));
   if (!planes.empty()) std::memcpy(&host[o_pl], planes.data(), planes.size() * sizeof(PlaneRec));
+  if (!quads.empty()) std::memcpy(&host[o_qd], quads.data(), quads.size() * sizeof(QuadRec));
   if (!shade.empty()) std::memcpy(&host[o_sh], shade.data(), shade.size() * sizeof(ShadeRec));
   if (!lrec.empty()) std::memcpy(&host[o_li], lrec.data(), lrec.size() * sizeof(LightRec));
 
@@ -404,11 +369,7 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
          RT_HIP(hipSetDevice(device));
          RT_HIP(hipMalloc(&s->d_blob, total));
          RT_HIP(hipMemcpy(s->d_blob, host.data(), total, hipMemcpyHostToDevice));
-         RT_HIP(hipMalloc(&s->d_counter, 256));
-         RT_HIP(hipMalloc(&s->d_stats, sizeof(DevStats)));
          RT_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-         RT_HIP(hipEventCreate(&s->ev0));
-         RT_HIP(hipEventCreate(&s->ev1));
          return RT_OK;
        }()) != RT_OK)
     return cleanup(rc);
@@ -416,11 +377,13 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   s->dev.sph_diag = (const SphereDiag*)(b + o_diag);
   s->dev.sph_gen = (const SphereGen*)(b + o_gen);
   s->dev.planes = (const PlaneRec*)(b + o_pl);
+  s->dev.quads = (const QuadRec*)(b + o_qd);
   s->dev.shade = (const ShadeRec*)(b + o_sh);
   s->dev.lights = (const LightRec*)(b + o_li);
   s->dev.n_diag = (int32_t)diag.size();
   s->dev.n_gen = (int32_t)gen.size();
   s->dev.n_planes = (int32_t)planes.size();
+  s->dev.n_quads = (int32_t)quads.size();
   s->dev.n_objects = (int32_t)n_shapes;
   s->dev.n_lights = (int32_t)n_lights;
   s->n_objects = (int)n_shapes;
@@ -434,12 +397,8 @@ void rt_scene_destroy(rt_scene* s) {
   (void)hipSetDevice(s->device);
   if (s->stream) (void)hipStreamSynchronize(s->stream);
   if (s->d_blob) (void)hipFree(s->d_blob);
-  if (s->d_counter) (void)hipFree(s->d_counter);
-  if (s->d_stats) (void)hipFree(s->d_stats);
   if (s->d_out) (void)hipFree(s->d_out);
   if (s->d_in) (void)hipFree(s->d_in);
-  if (s->ev0) (void)hipEventDestroy(s->ev0);
-  if (s->ev1) (void)hipEventDestroy(s->ev1);
   if (s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
 }
@@ -455,8 +414,8 @@ uint32_t rt_shard_rows(uint32_t vsize, uint32_t row_block, uint32_t shard, uint3
 }
 
 int rt_render_shard_device(const rt_scene* scene, const rt_camera_desc* camera, uint32_t max_depth,
-                           uint32_t row_block, uint32_t shard, uint32_t n_shards, double* d_out_rgb,
-                           void* stream, rt_stats* stats) {
+                           uint32_t aa_samples, uint32_t row_block, uint32_t shard, uint32_t n_shards,
+                           double* d_out_rgb, void* stream, rt_stats* stats) {
   if (!scene || !camera || !d_out_rgb) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
   if (row_block == 0 || n_shards == 0 || shard >= n_shards)
     return fail(RT_ERR_INVALID_ARGUMENT, "bad shard specification");
@@ -466,14 +425,39 @@ int rt_render_shard_device(const rt_scene* scene, const rt_camera_desc* camera, 
   auto t0 = std::chrono::steady_clock::now();
   RT_HIP(hipSetDevice(s->device));
   const uint32_t rows = rt_shard_rows(camera->vsize, row_block, shard, n_shards);
-  const uint64_t n_tasks = (uint64_t)rows * camera->hsize;
+  const uint64_t n_tasks = (uint64_t)rows * camera->hsize * aa_samples;
   if (n_tasks >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "shard too large");
   hipStream_t st = (hipStream_t)stream;  // NULL = the default stream (torch's current stream is often 0)
   DevStats ds{};
   float ms = 0.f;
-  int rc = run_render(s, to_dev_camera(*camera), nullptr, (uint32_t)n_tasks, max_depth, row_block, shard,
-                      n_shards, d_out_rgb, st, stats != nullptr, stats ? &ds : nullptr, stats ? &ms : nullptr);
+  int rc = run_render(s, to_dev_camera(*camera), nullptr, (uint32_t)n_tasks, aa_samples, max_depth, row_block, shard,
+                      n_shards, d_out_rgb, st, stats ? &ds : nullptr, stats ? &ms : nullptr);
   if (rc != RT_OK) return rc;
+  if (stats)
+    fill_stats(stats, ds, ms, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+  return RT_OK;
+}
+
+int rt_render_aa(const rt_scene* scene, const rt_camera_desc* camera, uint32_t max_depth, uint32_t aa_samples,
+                 double* out_rgb, rt_stats* stats) {
+  if (!scene || !camera || !out_rgb) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
+  if (camera->hsize == 0 || camera->vsize == 0) return fail(RT_ERR_INVALID_ARGUMENT, "empty camera");
+  if (!valid_aa(aa_samples)) return fail(RT_ERR_INVALID_ARGUMENT, "aa_samples must be 1, 2, 4, 8 or 16");
+  rt_scene* s = const_cast<rt_scene*>(scene);
+  std::lock_guard<std::mutex> lk(s->mu);
+  auto t0 = std::chrono::steady_clock::now();
+  RT_HIP(hipSetDevice(s->device));
+  const uint64_t n_pix = (uint64_t)camera->hsize * camera->vsize;
+  if (n_pix * aa_samples >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "canvas too large for one launch");
+  int rc = ensure_dev_buffer(&s->d_out, &s->out_cap, n_pix * 3);
+  if (rc != RT_OK) return rc;
+  DevStats ds{};
+  float ms = 0.f;
+  rc = run_render(s, to_dev_camera(*camera), nullptr, (uint32_t)(n_pix * aa_samples), aa_samples, max_depth,
+                  camera->vsize, 0, 1, s->d_out, s->stream, stats ? &ds : nullptr, &ms);
+  if (rc != RT_OK) return rc;
+  RT_HIP(hipMemcpyAsync(out_rgb, s->d_out, n_pix * 3 * sizeof(double), hipMemcpyDeviceToHost, s->stream));
+  RT_HIP(hipStreamSynchronize(s->stream));
   if (stats)
     fill_stats(stats, ds, ms, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
   return RT_OK;
@@ -481,26 +465,7 @@ int rt_render_shard_device(const rt_scene* scene, const rt_camera_desc* camera, 
 
 int rt_render(const rt_scene* scene, const rt_camera_desc* camera, uint32_t max_depth, double* out_rgb,
               rt_stats* stats) {
-  if (!scene || !camera || !out_rgb) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
-  if (camera->hsize == 0 || camera->vsize == 0) return fail(RT_ERR_INVALID_ARGUMENT, "empty camera");
-  rt_scene* s = const_cast<rt_scene*>(scene);
-  std::lock_guard<std::mutex> lk(s->mu);
-  auto t0 = std::chrono::steady_clock::now();
-  RT_HIP(hipSetDevice(s->device));
-  const uint64_t n = (uint64_t)camera->hsize * camera->vsize;
-  if (n >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "canvas too large for one launch");
-  int rc = ensure_dev_buffer(&s->d_out, &s->out_cap, n * 3);
-  if (rc != RT_OK) return rc;
-  DevStats ds{};
-  float ms = 0.f;
-  rc = run_render(s, to_dev_camera(*camera), nullptr, (uint32_t)n, max_depth, camera->vsize, 0, 1, s->d_out,
-                  s->stream, true, stats ? &ds : nullptr, &ms);
-  if (rc != RT_OK) return rc;
-  RT_HIP(hipMemcpyAsync(out_rgb, s->d_out, n * 3 * sizeof(double), hipMemcpyDeviceToHost, s->stream));
-  RT_HIP(hipStreamSynchronize(s->stream));
-  if (stats)
-    fill_stats(stats, ds, ms, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
-  return RT_OK;
+  return rt_render_aa(scene, camera, max_depth, 1, out_rgb, stats);
 }
 
 int rt_color_at_batch(const rt_scene* scene, const double* rays, size_t n, uint32_t remaining,
@@ -519,7 +484,7 @@ int rt_color_at_batch(const rt_scene* scene, const double* rays, size_t n, uint3
   DevCamera cam{};
   DevStats ds{};
   float ms = 0.f;
-  rc = run_render(s, cam, s->d_in, (uint32_t)n, remaining, 1, 0, 1, s->d_out, s->stream, true, stats ? &ds : nullptr,
+  rc = run_render(s, cam, s->d_in, (uint32_t)n, 1, remaining, 1, 0, 1, s->d_out, s->stream, stats ? &ds : nullptr,
                   &ms);
   if (rc != RT_OK) return rc;
   if (n) RT_HIP(hipMemcpyAsync(out_rgb, s->d_out, n * 3 * sizeof(double), hipMemcpyDeviceToHost, s->stream));
@@ -569,9 +534,11 @@ int rt_hit_batch(const rt_scene* scene, const double* rays, size_t n, double* ou
 
 // Single-process multi-GPU render: interleaved row blocks, one RCCL gather.
 int rt_render_multi(rt_scene* const* scenes, int n_devices, const rt_camera_desc* camera,
-                    uint32_t max_depth, uint32_t row_block, double* out_rgb, rt_stats* stats) {
+                    uint32_t max_depth, uint32_t aa_samples, uint32_t row_block, double* out_rgb,
+                    rt_stats* stats) {
   if (!scenes || n_devices < 1 || !camera || !out_rgb || row_block == 0)
     return fail(RT_ERR_INVALID_ARGUMENT, "bad arguments");
+  if (!valid_aa(aa_samples)) return fail(RT_ERR_INVALID_ARGUMENT, "aa_samples must be 1, 2, 4, 8 or 16");
   for (int i = 0; i < n_devices; ++i)
     if (!scenes[i] || scenes[i]->device != i)
       return fail(RT_ERR_INVALID_ARGUMENT, "scenes[i] must live on device i");
@@ -605,8 +572,8 @@ int rt_render_multi(rt_scene* const* scenes, int n_devices, const rt_camera_desc
       RT_HIP(hipSetDevice(i));
       std::lock_guard<std::mutex> lk(scenes[i]->mu);
       const uint32_t rows = rt_shard_rows(H, row_block, i, n_devices);
-      int r = run_render(scenes[i], to_dev_camera(*camera), nullptr, rows * W, max_depth, row_block, i, n_devices,
-                         send[i], scenes[i]->stream, false);
+      int r = run_render(scenes[i], to_dev_camera(*camera), nullptr, rows * W * aa_samples, aa_samples, max_depth,
+                         row_block, i, n_devices, send[i], scenes[i]->stream);
       if (r != RT_OK) return r;
     }
     if (n_devices > 1) {
@@ -632,8 +599,8 @@ int rt_render_multi(rt_scene* const* scenes, int n_devices, const rt_camera_desc
         const uint32_t rows = rt_shard_rows(H, row_block, i, n_devices);
         DevStats ds{};
         float ms = 0.f;
-        int r = run_render(scenes[i], to_dev_camera(*camera), nullptr, rows * W, max_depth, row_block, i, n_devices,
-                           send[i], scenes[i]->stream, true, &ds, &ms);
+        int r = run_render(scenes[i], to_dev_camera(*camera), nullptr, rows * W * aa_samples, aa_samples, max_depth,
+                           row_block, i, n_devices, send[i], scenes[i]->stream, &ds, &ms);
         if (r != RT_OK) return r;
         fill_stats(&st[i], ds, ms, 0.0);
       }
@@ -665,7 +632,7 @@ int rt_render_multi(rt_scene* const* scenes, int n_devices, const rt_camera_desc
       stats->rays_primary += x.rays_primary; stats->rays_reflect += x.rays_reflect;
       stats->rays_refract += x.rays_refract; stats->rays_shadow += x.rays_shadow;
       stats->sphere_tests += x.sphere_tests; stats->plane_tests += x.plane_tests;
-      stats->sphere_disc_ge0 += x.sphere_disc_ge0;
+      stats->sphere_disc_ge0 += x.sphere_disc_ge0; stats->other_tests += x.other_tests;
       stats->ms_kernel = std::max(stats->ms_kernel, x.ms_kernel);
     }
     stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

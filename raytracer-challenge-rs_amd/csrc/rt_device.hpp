@@ -1,6 +1,6 @@
 // rt_device.hpp — device-side building blocks of the render path, shared by
-// the persistent megakernel (rt_kernels.hip) and the wavefront pipeline
-// (rt_wavefront.hip). Every function restates a reference function (cited),
+// the wavefront pipeline (rt_wavefront.hip) and the batch kernels
+// (rt_kernels.hip). Every function restates a reference function (cited),
 // in binary64 with the reference's operation order; include only from .hip
 // files compiled with -ffp-contract=off.
 #pragma once
@@ -53,18 +53,37 @@ __device__ __forceinline__ V3 m33_vector(const double* m, V3 v) {  // m: 3x3 row
 typedef const RT_CONST SphereDiag* cSphereDiag;
 typedef const RT_CONST SphereGen* cSphereGen;
 typedef const RT_CONST PlaneRec* cPlaneRec;
+typedef const RT_CONST QuadRec* cQuadRec;
 typedef const RT_CONST LightRec* cLightRec;
 
+typedef double d2 __attribute__((ext_vector_type(2)));  // ds_read_b128 operand
+__host__ __device__ constexpr size_t lds_align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
 // ------------------------------------------------------------ trace (hot loop)
+// World::intersect + intersections + hit (world.rs:31-38, intersection.rs:
+// 108-125) without building or sorting the list: the nearest t >= 0 by
+// (t, key) is the element the stable sort puts first, and the `containers`
+// walk of prepare_computations (intersection.rs:63-90) only ever needs the two
+// most recently entered containers (DESIGN.md "containers walk -> top-2").
 struct Hit {
   double t;   // nearest t >= 0 (over eligible objects)
-  int key;    // 2*object + root, -1 = miss
-  // containers candidates (radiance rays): top-2 by (entry t, key) among
-  // spheres with t1 < 0 <= t2 and planes with t < 0.
+  int key;    // (object << kKeyShift) | list position, -1 = miss
+  int hin;    // the hit object is in `containers` when the hit is reached
+  // containers candidates (radiance rays): objects with an odd number of
+  // intersections t < 0, keyed by their last such intersection; top 2.
   double c1t, c2t;
   int c1k, c2k;
 };
 
+__device__ __forceinline__ void hit_init(Hit& h) {
+  h.t = INFINITY;
+  h.key = 0x7fffffff;
+  h.hin = 0;
+  h.c1t = -INFINITY; h.c2t = -INFINITY; h.c1k = -1; h.c2k = -1;
+}
+__device__ __forceinline__ void hit_finish(Hit& h) {
+  if (h.key == 0x7fffffff) h.key = -1;
+}
 __device__ __forceinline__ bool better(double t, int k, double bt, int bk) {
   return t < bt || (t == bt && k < bk);
 }
@@ -76,198 +95,195 @@ __device__ __forceinline__ void push_container(Hit& h, double t, int k) {
   }
 }
 
-// Sphere::local_intersect (sphere.rs:47-62) on the object-space ray.
-// With b = 2*dt and disc = b*b - (4a)*c = 4*(dt*dt - a*c) exactly (power-of-two
-// scaling commutes with rounding), t = (-b -/+ sqrt(disc)) / (2a) equals
-// (-dt -/+ sqrt(dt*dt - a*c)) / a bit for bit (DESIGN.md "Sphere roots").
-__device__ __forceinline__ void sphere_roots(double ox, double oy, double oz, double dx, double dy,
-                                             double dz, int64_t meta, bool shadow_mode, Hit& h,
-                                             unsigned& n_disc) {
-  const double a = dx * dx + dy * dy + dz * dz;
-  const double dt = dx * ox + dy * oy + dz * oz;
-  const double c = ox * ox + oy * oy + oz * oz - 1.0;
+// Sphere::local_intersect (sphere.rs:47-62) from (a, dt = d.o, c) of the
+// object-space ray. With b = 2*dt and disc = b*b - (4a)*c = 4*(dt*dt - a*c)
+// exactly (power-of-two scaling commutes with rounding), t = (-b -/+
+// sqrt(disc)) / (2a) equals (-dt -/+ sqrt(dt*dt - a*c)) / a bit for bit
+// (DESIGN.md "Sphere roots"). The object index / shadow flag (`meta`) is read
+// only when disc >= 0. Root 1 can only be the hit when root 0 < 0, i.e. when
+// the sphere is a container at the hit.
+template <bool SHADOW, typename MetaFn>
+__device__ __forceinline__ void sphere_adc(double a, double dt, double c, MetaFn meta_fn, Hit& h,
+                                           unsigned& n_disc) {
   const double disc = dt * dt - a * c;
   if (disc >= 0.0) {
     ++n_disc;
+    const int meta = meta_fn();
     const double q = sqrt(disc);
     const double t1 = (-dt - q) / a;
     const double t2 = (-dt + q) / a;
-    const int k1 = (int)(meta >> 1) * 2;
-    const bool eligible = !shadow_mode || (meta & 1);
+    const int k1 = (meta >> 1) << kKeyShift;
+    const bool eligible = !SHADOW || (meta & 1);
     if (eligible) {
       if (t1 >= 0.0) {
-        if (better(t1, k1, h.t, h.key)) { h.t = t1; h.key = k1; }
+        if (better(t1, k1, h.t, h.key)) { h.t = t1; h.key = k1; h.hin = 0; }
       } else if (t2 >= 0.0) {
-        if (better(t2, k1 + 1, h.t, h.key)) { h.t = t2; h.key = k1 + 1; }
+        if (better(t2, k1 + 1, h.t, h.key)) { h.t = t2; h.key = k1 + 1; h.hin = 1; }
       }
     }
-    if (t1 < 0.0 && t2 >= 0.0) push_container(h, t1, k1);
+    if (!SHADOW && t1 < 0.0 && t2 >= 0.0) push_container(h, t1, k1);
   }
 }
-
-// Same test with the object index / shadow flag fetched only when the
-// discriminant is non-negative (LDS path: the meta word is not needed per test).
-__device__ __forceinline__ void sphere_roots_lazy(double ox, double oy, double oz, double dx, double dy,
-                                                  double dz, const int* meta_p, bool shadow_mode, Hit& h,
-                                                  unsigned& n_disc) {
+template <bool SHADOW, typename MetaFn>
+__device__ __forceinline__ void sphere_test(double ox, double oy, double oz, double dx, double dy, double dz,
+                                            MetaFn meta_fn, Hit& h, unsigned& n_disc) {
   const double a = dx * dx + dy * dy + dz * dz;
   const double dt = dx * ox + dy * oy + dz * oz;
   const double c = ox * ox + oy * oy + oz * oz - 1.0;
-  const double disc = dt * dt - a * c;
-  if (disc >= 0.0) {
-    ++n_disc;
-    const int meta = *meta_p;
-    const double q = sqrt(disc);
-    const double t1 = (-dt - q) / a;
-    const double t2 = (-dt + q) / a;
-    const int k1 = (meta >> 1) * 2;
-    const bool eligible = !shadow_mode || (meta & 1);
-    if (eligible) {
-      if (t1 >= 0.0) {
-        if (better(t1, k1, h.t, h.key)) { h.t = t1; h.key = k1; }
-      } else if (t2 >= 0.0) {
-        if (better(t2, k1 + 1, h.t, h.key)) { h.t = t2; h.key = k1 + 1; }
-      }
-    }
-    if (t1 < 0.0 && t2 >= 0.0) push_container(h, t1, k1);
+  sphere_adc<SHADOW>(a, dt, c, meta_fn, h, n_disc);
+}
+
+// Plane::local_intersect (plane.rs:53-60) from the object-space y of origin
+// and direction.
+template <bool SHADOW>
+__device__ __forceinline__ void plane_test(double oy, double dy, int meta, Hit& h) {
+  if (!(fabs(dy) < kEpsilon)) {
+    const double t = -oy / dy;
+    const int k = (meta >> 1) << kKeyShift;
+    const bool eligible = !SHADOW || (meta & 1);
+    if (eligible && t >= 0.0 && better(t, k, h.t, h.key)) { h.t = t; h.key = k; h.hin = 0; }
+    if (!SHADOW && t < 0.0) push_container(h, t, k);
   }
 }
 
-// LDS image of the trace records (one copy per workgroup = per CU):
-//   diag: 6 doubles (s0 s1 s2 t0 t1 t2) per sphere, gen: 12 doubles, plane: 4
-//   doubles; then int32 meta arrays. Reads are wave-uniform (broadcast).
-struct LdsView {
-  const double* diag;
-  const double* gen;
-  const double* plane;
-  const int* diag_meta;
-  const int* gen_meta;
-  const int* plane_meta;
-};
-typedef double d2 __attribute__((ext_vector_type(2)));
-
-__host__ __device__ constexpr size_t lds_align16(size_t x) { return (x + 15) & ~(size_t)15; }
-__host__ __device__ inline size_t lds_bytes(int nd, int ng, int np) {
-  return lds_align16((size_t)(nd + 4) * 48) + lds_align16((size_t)ng * 96) + lds_align16((size_t)np * 32) +
-         lds_align16((size_t)nd * 4) + lds_align16((size_t)ng * 4) + lds_align16((size_t)np * 4);
-}
-
-__device__ LdsView lds_stage(const DevScene& sc, unsigned char* base) {
-  LdsView v;
-  size_t off = 0;
-  v.diag = (const double*)(base + off); off += lds_align16((size_t)(sc.n_diag + 4) * 48);
-  v.gen = (const double*)(base + off); off += lds_align16((size_t)sc.n_gen * 96);
-  v.plane = (const double*)(base + off); off += lds_align16((size_t)sc.n_planes * 32);
-  v.diag_meta = (const int*)(base + off); off += lds_align16((size_t)sc.n_diag * 4);
-  v.gen_meta = (const int*)(base + off); off += lds_align16((size_t)sc.n_gen * 4);
-  v.plane_meta = (const int*)(base + off);
-  double* dd = (double*)v.diag;
-  double* dg = (double*)v.gen;
-  double* dp = (double*)v.plane;
-  for (int i = threadIdx.x; i < (sc.n_diag + 4) * 6; i += blockDim.x) {
-    const int r = i / 6, e = i - r * 6;
-    dd[i] = r >= sc.n_diag ? 0.0 : e < 3 ? sc.sph_diag[r].s[e] : sc.sph_diag[r].t[e - 3];
-  }
-  for (int i = threadIdx.x; i < sc.n_gen * 12; i += blockDim.x) dg[i] = sc.sph_gen[i / 12].m[i % 12];
-  for (int i = threadIdx.x; i < sc.n_planes * 4; i += blockDim.x) dp[i] = sc.planes[i / 4].m[i % 4];
-  for (int i = threadIdx.x; i < sc.n_diag; i += blockDim.x) ((int*)v.diag_meta)[i] = (int)sc.sph_diag[i].meta;
-  for (int i = threadIdx.x; i < sc.n_gen; i += blockDim.x) ((int*)v.gen_meta)[i] = (int)sc.sph_gen[i].meta;
-  for (int i = threadIdx.x; i < sc.n_planes; i += blockDim.x) ((int*)v.plane_meta)[i] = (int)sc.planes[i].meta;
-  __syncthreads();
-  return v;
-}
-
-// World::intersect + hit (world.rs:31-38, intersection.rs:118-125): every
-// object, in three wave-uniform record streams.
-template <bool USE_LDS>
-__device__ __forceinline__ void trace(const DevScene& sc, const LdsView& lv, V3 o, V3 d, bool shadow_mode,
-                                      Hit& h, unsigned& n_disc) {
-  h.t = INFINITY;
-  h.c1t = -INFINITY; h.c2t = -INFINITY; h.c1k = -1; h.c2k = -1;
-  h.key = 0x7fffffff;
-  // Shape::intersect (geometry/mod.rs:46-49): Ray::transform by the inverse.
-  if constexpr (USE_LDS) {
-    if (sc.n_diag > 0) {
-      // ping-pong look-ahead from LDS (3 x ds_read_b128 per record, broadcast);
-      // the image holds zero padding records, so record j+1 always exists.
-      // record layout: (s0 s1) (s2 t0) (t1 t2); off-diagonal inverse entries are exact zeros
-      const d2* r = (const d2*)lv.diag;
-      d2 a0 = r[0], a1 = r[1], a2 = r[2];
-      int j = 0;
-      for (; j + 1 < sc.n_diag; j += 2) {
-        const d2 b0 = r[3 * j + 3], b1 = r[3 * j + 4], b2 = r[3 * j + 5];
-        sphere_roots_lazy(a0.x * o.x + a1.y, a0.y * o.y + a2.x, a1.x * o.z + a2.y, a0.x * d.x, a0.y * d.y,
-                          a1.x * d.z, lv.diag_meta + j, shadow_mode, h, n_disc);
-        a0 = r[3 * j + 6]; a1 = r[3 * j + 7]; a2 = r[3 * j + 8];
-        sphere_roots_lazy(b0.x * o.x + b1.y, b0.y * o.y + b2.x, b1.x * o.z + b2.y, b0.x * d.x, b0.y * d.y,
-                          b1.x * d.z, lv.diag_meta + j + 1, shadow_mode, h, n_disc);
-      }
-      if (j < sc.n_diag)
-        sphere_roots_lazy(a0.x * o.x + a1.y, a0.y * o.y + a2.x, a1.x * o.z + a2.y, a0.x * d.x, a0.y * d.y,
-                          a1.x * d.z, lv.diag_meta + j, shadow_mode, h, n_disc);
-    }
+// Cube::check_axis (cube.rs:30-47)
+__device__ __forceinline__ void cube_check_axis(double origin, double direction, double& tmin, double& tmax) {
+  const double tmin_numerator = -1.0 - origin;
+  const double tmax_numerator = 1.0 - origin;
+  if (fabs(direction) >= kEpsilon) {
+    tmin = tmin_numerator / direction;
+    tmax = tmax_numerator / direction;
   } else {
-    cSphereDiag sd = (cSphereDiag)sc.sph_diag;
-    if (sc.n_diag > 0) {
-      // software pipeline: the scalar loads of record j+1 are in flight while
-      // record j is tested (each section ends with one padding record, so the
-      // look-ahead load is always in bounds)
-      double s0 = sd[0].s[0], s1 = sd[0].s[1], s2 = sd[0].s[2];
-      double t0 = sd[0].t[0], t1 = sd[0].t[1], t2 = sd[0].t[2];
-      int64_t meta = sd[0].meta;
-      for (int j = 0; j < sc.n_diag; ++j) {
-        const double n_s0 = sd[j + 1].s[0], n_s1 = sd[j + 1].s[1], n_s2 = sd[j + 1].s[2];
-        const double n_t0 = sd[j + 1].t[0], n_t1 = sd[j + 1].t[1], n_t2 = sd[j + 1].t[2];
-        const int64_t n_meta = sd[j + 1].meta;
-        // off-diagonal entries are exact zeros: ((m00*x + 0) + 0) + m03 == m00*x + m03
-        sphere_roots(s0 * o.x + t0, s1 * o.y + t1, s2 * o.z + t2, s0 * d.x, s1 * d.y, s2 * d.z, meta,
-                     shadow_mode, h, n_disc);
-        s0 = n_s0; s1 = n_s1; s2 = n_s2; t0 = n_t0; t1 = n_t1; t2 = n_t2; meta = n_meta;
-      }
+    tmin = tmin_numerator * INFINITY;
+    tmax = tmax_numerator * INFINITY;
+  }
+  if (tmin > tmax) { const double x = tmin; tmin = tmax; tmax = x; }
+}
+// Cylinder::check_cap (cylinder.rs:42-46, radius 1) / Cone::check_cap
+// (cone.rs:67-71, radius = the cap's y)
+__device__ __forceinline__ bool check_cap(V3 o, V3 d, double t, double radius) {
+  const double x = o.x + t * d.x;
+  const double z = o.z + t * d.z;
+  return (x * x + z * z) <= radius * radius;
+}
+// intersect_caps (cylinder.rs:48-65, cone.rs:48-65): appends to t[n..]
+__device__ __forceinline__ int intersect_caps(int kind, double mn, double mx, bool closed, V3 o, V3 d, double* t,
+                                              int n) {
+  if (!closed) return n;
+  const bool cone = kind == 4;
+  double tc = (mn - o.y) / d.y;
+  if (check_cap(o, d, tc, cone ? mn : 1.0)) t[n++] = tc;
+  tc = (mx - o.y) / d.y;
+  if (check_cap(o, d, tc, cone ? mx : 1.0)) t[n++] = tc;
+  return n;
+}
+// Cube / Cylinder / Cone local_intersect (cube.rs:71-93, cylinder.rs:88-119,
+// cone.rs:94-134): the reference's list, in push order, into t[0..n).
+__device__ __forceinline__ int quad_local_intersect(int kind, double mn, double mx, bool closed, V3 o, V3 d,
+                                                    double t[4]) {
+  if (kind == 2) {
+    double xtmin, xtmax, ytmin, ytmax, ztmin, ztmax;
+    cube_check_axis(o.x, d.x, xtmin, xtmax);
+    cube_check_axis(o.y, d.y, ytmin, ytmax);
+    cube_check_axis(o.z, d.z, ztmin, ztmax);
+    const double tmin = fmax(fmax(xtmin, ytmin), ztmin);  // f64::max: NaN-ignoring
+    const double tmax = fmin(fmin(xtmax, ytmax), ztmax);
+    if (tmin > tmax) return 0;
+    t[0] = tmin; t[1] = tmax;
+    return 2;
+  }
+  double a, b, c;
+  if (kind == 3) {
+    a = d.x * d.x + d.z * d.z;
+    if (fabs(a) < kEpsilon) return intersect_caps(kind, mn, mx, closed, o, d, t, 0);
+    b = 2.0 * o.x * d.x + 2.0 * o.z * d.z;
+    c = o.x * o.x + o.z * o.z - 1.0;
+  } else {
+    a = d.x * d.x - d.y * d.y + d.z * d.z;
+    b = 2.0 * o.x * d.x - 2.0 * o.y * d.y + 2.0 * o.z * d.z;
+    c = o.x * o.x - o.y * o.y + o.z * o.z;
+    if (fabs(a) < kEpsilon) {
+      if (fabs(b) < kEpsilon) return intersect_caps(kind, mn, mx, closed, o, d, t, 0);
+      t[0] = -c / 2.0 * b;  // sic (cone.rs:104)
+      return intersect_caps(kind, mn, mx, closed, o, d, t, 1);
     }
   }
+  const double disc = b * b - 4.0 * a * c;
+  if (disc < 0.0) return 0;  // no caps either (cylinder.rs:103-105, cone.rs:113-115)
+  const double q = sqrt(disc);
+  const double t0 = (-b - q) / (2.0 * a);
+  const double t1 = (-b + q) / (2.0 * a);
+  int n = 0;
+  const double y0 = o.y + t0 * d.y;
+  if (mn < y0 && y0 < mx) t[n++] = t0;
+  const double y1 = o.y + t1 * d.y;
+  if (mn < y1 && y1 < mx) t[n++] = t1;
+  return intersect_caps(kind, mn, mx, closed, o, d, t, n);
+}
+// Shape::intersect (geometry/mod.rs:46-49) of one QuadRec, folded into `h`:
+// the nearest t >= 0 of the object's list competes by (t, key); an object
+// with an odd number of t < 0 is a container, ordered by its last one.
+template <bool SHADOW>
+__device__ __forceinline__ void quad_test(cQuadRec q, V3 o, V3 d, Hit& h) {
+  const V3 lo = v3(q->m[0] * o.x + q->m[1] * o.y + q->m[2] * o.z + q->m[3],
+                   q->m[4] * o.x + q->m[5] * o.y + q->m[6] * o.z + q->m[7],
+                   q->m[8] * o.x + q->m[9] * o.y + q->m[10] * o.z + q->m[11]);
+  const V3 ld = v3(q->m[0] * d.x + q->m[1] * d.y + q->m[2] * d.z, q->m[4] * d.x + q->m[5] * d.y + q->m[6] * d.z,
+                   q->m[8] * d.x + q->m[9] * d.y + q->m[10] * d.z);
+  double t[4];
+  const int n = quad_local_intersect(q->kind, q->minimum, q->maximum, q->closed != 0, lo, ld, t);
+  if (n == 0) return;
+  const int meta = q->meta;
+  const int k0 = (meta >> 1) << kKeyShift;
+  int n_neg = 0, neg_i = -1, best_i = -1;
+  double neg_t = -INFINITY, best_t = INFINITY;
+  for (int i = 0; i < n; ++i) {
+    if (t[i] < 0.0) {
+      ++n_neg;
+      if (t[i] >= neg_t) { neg_t = t[i]; neg_i = i; }
+    } else if (t[i] >= 0.0 && t[i] < best_t) {
+      best_t = t[i]; best_i = i;
+    }
+  }
+  const bool eligible = !SHADOW || (meta & 1);
+  if (eligible && best_i >= 0 && better(best_t, k0 + best_i, h.t, h.key)) {
+    h.t = best_t; h.key = k0 + best_i; h.hin = n_neg & 1;
+  }
+  if (!SHADOW && (n_neg & 1)) push_container(h, neg_t, k0 + neg_i);
+}
+
+// Generic trace over the scene's records in global memory (scalar loads):
+// the batch entry points (rt_hit_batch, rt_is_shadowed_batch) and the
+// wavefront fallback when the trace image does not fit in LDS.
+template <bool SHADOW>
+__device__ __forceinline__ void trace(const DevScene& sc, V3 o, V3 d, Hit& h, unsigned& n_disc) {
+  hit_init(h);
+  cSphereDiag sd = (cSphereDiag)sc.sph_diag;
+  for (int j = 0; j < sc.n_diag; ++j) {
+    // off-diagonal inverse entries are exact zeros: ((m00*x + 0) + 0) + m03 == m00*x + m03
+    const double s0 = sd[j].s[0], s1 = sd[j].s[1], s2 = sd[j].s[2];
+    sphere_test<SHADOW>(s0 * o.x + sd[j].t[0], s1 * o.y + sd[j].t[1], s2 * o.z + sd[j].t[2], s0 * d.x, s1 * d.y,
+                        s2 * d.z, [&] { return (int)sd[j].meta; }, h, n_disc);
+  }
+  cSphereGen sg = (cSphereGen)sc.sph_gen;
   for (int j = 0; j < sc.n_gen; ++j) {
     double m[12];
-    if constexpr (USE_LDS) {
 #pragma unroll
-      for (int e = 0; e < 12; ++e) m[e] = lv.gen[12 * j + e];
-    } else {
-      cSphereGen sg = (cSphereGen)sc.sph_gen;
-#pragma unroll
-      for (int e = 0; e < 12; ++e) m[e] = sg[j].m[e];
-    }
+    for (int e = 0; e < 12; ++e) m[e] = sg[j].m[e];
     const V3 lo = m34_point(m, o);
     const V3 ld = v3(m[0] * d.x + m[1] * d.y + m[2] * d.z, m[4] * d.x + m[5] * d.y + m[6] * d.z,
                      m[8] * d.x + m[9] * d.y + m[10] * d.z);
-    if constexpr (USE_LDS) {
-      sphere_roots_lazy(lo.x, lo.y, lo.z, ld.x, ld.y, ld.z, lv.gen_meta + j, shadow_mode, h, n_disc);
-    } else {
-      sphere_roots(lo.x, lo.y, lo.z, ld.x, ld.y, ld.z, ((cSphereGen)sc.sph_gen)[j].meta, shadow_mode, h, n_disc);
-    }
+    sphere_test<SHADOW>(lo.x, lo.y, lo.z, ld.x, ld.y, ld.z, [&] { return (int)sg[j].meta; }, h, n_disc);
   }
-  // Plane::local_intersect (plane.rs:53-60): only object-space y matters.
+  cPlaneRec pl = (cPlaneRec)sc.planes;
   for (int j = 0; j < sc.n_planes; ++j) {
-    double m0, m1, m2, m3;
-    int meta;
-    if constexpr (USE_LDS) {
-      m0 = lv.plane[4 * j]; m1 = lv.plane[4 * j + 1]; m2 = lv.plane[4 * j + 2]; m3 = lv.plane[4 * j + 3];
-      meta = lv.plane_meta[j];
-    } else {
-      cPlaneRec pl = (cPlaneRec)sc.planes;
-      m0 = pl[j].m[0]; m1 = pl[j].m[1]; m2 = pl[j].m[2]; m3 = pl[j].m[3];
-      meta = (int)pl[j].meta;
-    }
-    const double oy = m0 * o.x + m1 * o.y + m2 * o.z + m3;
-    const double dy = m0 * d.x + m1 * d.y + m2 * d.z;
-    if (!(fabs(dy) < kEpsilon)) {
-      const double t = -oy / dy;
-      const int k = (meta >> 1) * 2;
-      const bool eligible = !shadow_mode || (meta & 1);
-      if (eligible && t >= 0.0 && better(t, k, h.t, h.key)) { h.t = t; h.key = k; }
-      if (t < 0.0) push_container(h, t, k);
-    }
+    const double oy = pl[j].m[0] * o.x + pl[j].m[1] * o.y + pl[j].m[2] * o.z + pl[j].m[3];
+    const double dy = pl[j].m[0] * d.x + pl[j].m[1] * d.y + pl[j].m[2] * d.z;
+    plane_test<SHADOW>(oy, dy, (int)pl[j].meta, h);
   }
-  if (h.key == 0x7fffffff) h.key = -1;
+  cQuadRec qr = (cQuadRec)sc.quads;
+  for (int j = 0; j < sc.n_quads; ++j) quad_test<SHADOW>(qr + j, o, d, h);
+  hit_finish(h);
 }
 
 // --------------------------------------------------------------- shading
@@ -278,31 +294,54 @@ struct Comps {
   bool inside;
 };
 
+// Shape::local_normal_at per kind (sphere.rs:64-67, plane.rs:62-64,
+// cube.rs:95-106, cylinder.rs:121-130, cone.rs:136-149).
+__device__ __forceinline__ V3 local_normal_at(const ShadeRec& s, V3 p) {
+  switch (s.kind) {
+    case 0: return vsub(p, v3(0.0, 0.0, 0.0));
+    case 1: return v3(0.0, 1.0, 0.0);
+    case 2: {
+      const double maxc = fmax(fmax(fabs(p.x), fabs(p.y)), fabs(p.z));
+      if (req(maxc, fabs(p.x))) return v3(p.x, 0.0, 0.0);
+      if (req(maxc, fabs(p.y))) return v3(0.0, p.y, 0.0);
+      return v3(0.0, 0.0, p.z);
+    }
+    default: {
+      const double dist = p.x * p.x + p.z * p.z;
+      if (dist < 1.0 && p.y >= s.maximum - kEpsilon) return v3(0.0, 1.0, 0.0);
+      if (dist < 1.0 && p.y <= s.minimum + kEpsilon) return v3(0.0, -1.0, 0.0);
+      if (s.kind == 3) return v3(p.x, 0.0, p.z);
+      double y = sqrt(p.x * p.x + p.z * p.z);
+      if (p.y > 0.0) y = -y;
+      return v3(p.x, y, p.z);
+    }
+  }
+}
+
 // Intersection::prepare_computations (intersection.rs:53-105) with the exact
 // top-2 replacement of the containers walk.
 __device__ __forceinline__ Comps prepare(const DevScene& sc, V3 o, V3 d, const Hit& h) {
   Comps c;
-  const int obj = h.key >> 1;
+  const int obj = h.key >> kKeyShift;
   const ShadeRec& s = sc.shade[obj];
   c.obj = obj;
   c.point = vadd(o, vscale(d, h.t));  // ray.rs:22-24
   c.eyev = vneg(d);
   // Shape::normal_at (geometry/mod.rs:51-56)
   const V3 lp = m34_point(s.inv, c.point);
-  const V3 ln = s.kind == 0 ? vsub(lp, v3(0.0, 0.0, 0.0)) : v3(0.0, 1.0, 0.0);
-  V3 n = vnormalize(m33_vector(s.invT, ln));
+  V3 n = vnormalize(m33_vector(s.invT, local_normal_at(s, lp)));
   c.inside = false;
   if (vdot(n, c.eyev) < 0.0) { c.inside = true; n = vneg(n); }
   c.normal = n;
-  // n1 / n2 (intersection.rs:63-90, DESIGN.md "n1/n2")
-  const bool hit_is_container = (h.key & 1) != 0;  // exit root of a sphere whose t1 < 0
-  c.n1 = h.c1k >= 0 ? sc.shade[h.c1k >> 1].refractive_index : 1.0;
-  if (!hit_is_container) {
+  // n1 / n2 (intersection.rs:63-90, DESIGN.md "containers walk -> top-2"):
+  // n1 = last container before the hit; n2 = last after toggling the hit object
+  c.n1 = h.c1k >= 0 ? sc.shade[h.c1k >> kKeyShift].refractive_index : 1.0;
+  if (!h.hin) {
     c.n2 = s.refractive_index;
-  } else if ((h.c1k >> 1) == obj) {
-    c.n2 = h.c2k >= 0 ? sc.shade[h.c2k >> 1].refractive_index : 1.0;
+  } else if ((h.c1k >> kKeyShift) == obj) {
+    c.n2 = h.c2k >= 0 ? sc.shade[h.c2k >> kKeyShift].refractive_index : 1.0;
   } else {
-    c.n2 = sc.shade[h.c1k >> 1].refractive_index;
+    c.n2 = sc.shade[h.c1k >> kKeyShift].refractive_index;
   }
   c.over = vadd(c.point, vscale(n, kEpsilon));
   c.under = vsub(c.point, vscale(n, kEpsilon));
@@ -388,11 +427,12 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
   return v;
 }
 
-// camera.rs:57-69
-__device__ __forceinline__ void ray_for_pixel(const DevCamera& cam, uint32_t px, uint32_t py, V3& o,
-                                              V3& d) {
-  const double xoffset = ((double)px + 0.5) * cam.pixel_size;
-  const double yoffset = ((double)py + 0.5) * cam.pixel_size;
+// camera.rs:57-69 (offsets 0.5, 0.5) and rays_for_pixel (camera.rs:71-90)
+// with the AA sample offsets of get_offsets (camera.rs:92-126).
+__device__ __forceinline__ void ray_for_pixel(const DevCamera& cam, uint32_t px, uint32_t py, V3& o, V3& d,
+                                              double offx = 0.5, double offy = 0.5) {
+  const double xoffset = ((double)px + offx) * cam.pixel_size;
+  const double yoffset = ((double)py + offy) * cam.pixel_size;
   const double world_x = cam.half_width - xoffset;
   const double world_y = cam.half_height - yoffset;
   const V3 pixel = m34_point(cam.inv, v3(world_x, world_y, -1.0));

@@ -1,5 +1,5 @@
 // rt_layout.hpp — device-resident layout of a flattened `World` (world.rs:18-21)
-// shared by the host uploader (rt_scene.cpp) and the HIP kernels.
+// shared by the host uploader (rt_api.cpp) and the HIP kernels.
 //
 // HBM layout (all 64-B aligned, all read-only during a render):
 //   trace records  : the per-ray hot loop reads EVERY record of its class once
@@ -7,7 +7,9 @@
 //       SphereDiag  8 doubles  (64 B)  inverse = diag(s) + translation t
 //       SphereGen  16 doubles (128 B)  inverse rows 0-2 (general affine)
 //       PlaneRec    8 doubles  (64 B)  inverse row 1 (only y matters)
-//     each carries `meta` = (object index << 1) | casts_shadow as a double slot.
+//       QuadRec    16 doubles (128 B)  Cube / Cylinder / Cone: inverse rows 0-2,
+//                                      minimum, maximum, kind, closed
+//     each carries `meta` = (object index << 1) | casts_shadow.
 //   shade records  : ShadeRec per object index (AoS, 64 doubles = 512 B),
 //                    gathered per lane only at a hit.
 //   lights         : 6 doubles each (position, intensity), wave-uniform.
@@ -34,6 +36,18 @@ struct alignas(64) PlaneRec {
   int64_t meta;
   int64_t pad[3];
 };
+struct alignas(64) QuadRec {  // cube.rs / cylinder.rs / cone.rs
+  double m[12];  // inverse rows 0..2
+  double minimum, maximum;
+  int32_t kind, closed;
+  int32_t meta, pad;
+};
+static_assert(sizeof(QuadRec) == 128, "QuadRec must stay 128 B");
+
+// Intersection ordering key: (object index << 2) | position in the object's
+// local_intersect list (at most 4 entries, cylinder/cone). Equal t resolve by
+// this key exactly like the reference's stable sort (intersection.rs:108-116).
+constexpr int kKeyShift = 2;
 
 struct alignas(64) ShadeRec {
   double inv[12];   // transform_inverse rows 0..2
@@ -44,7 +58,8 @@ struct alignas(64) ShadeRec {
   double pat_a[3], pat_b[3];
   double pat_inv[12];
   int32_t kind, pattern_kind, shadow, pad0;
-  double pad1[6];
+  double minimum, maximum;  // Cylinder / Cone (local_normal_at)
+  double pad1[4];
 };
 static_assert(sizeof(ShadeRec) == 512, "ShadeRec must stay 512 B");
 
@@ -60,8 +75,9 @@ struct DevScene {
   const PlaneRec* planes;
   const ShadeRec* shade;
   const LightRec* lights;
+  const QuadRec* quads;
   int32_t n_diag, n_gen, n_planes, n_objects, n_lights;
-  int32_t pad;
+  int32_t n_quads;
 };
 
 struct DevCamera {
@@ -73,10 +89,7 @@ struct DevCamera {
 // Counters accumulated by the kernels (order = rt_stats prefix).
 struct DevStats {
   unsigned long long rays_primary, rays_reflect, rays_refract, rays_shadow;
-  unsigned long long sphere_tests, plane_tests, sphere_disc_ge0;
-  unsigned long long wave_steps;    // diagnostic: wave-level trace steps
-  unsigned long long diag_trace_cycles, diag_total_cycles;  // DIAG variant only (s_memtime)
-  unsigned long long pad;
+  unsigned long long sphere_tests, plane_tests, sphere_disc_ge0, other_tests;
 };
 
 }  // namespace rtamd

@@ -48,14 +48,33 @@ __device__ __forceinline__ unsigned wave_append(unsigned* counter, bool want, un
   return base + rank * per;
 }
 
-// Root rays of generation 0: camera pixel of the shard (camera.rs:57-69) or
-// an explicit ray; deeper generations read their queue.
+// AA sample offsets of Camera::get_offsets (camera.rs:92-126), per count
+// 1, 2, 4, 8, 16 at offsets 0, 1, 3, 7, 15 of the table.
+__constant__ double kAaOffsets[31][2] = {
+    {0.5, 0.5},
+    {0.25, 0.5}, {0.75, 0.5},
+    {0.25, 0.25}, {0.75, 0.25}, {0.25, 0.75}, {0.75, 0.75},
+    {0.25, 0.25}, {0.5, 0.25}, {0.75, 0.25}, {0.25, 0.5}, {0.75, 0.5}, {0.25, 0.75}, {0.5, 0.75}, {0.75, 0.75},
+    {0.125, 0.125}, {0.375, 0.125}, {0.625, 0.125}, {0.875, 0.125},
+    {0.125, 0.375}, {0.375, 0.375}, {0.625, 0.375}, {0.875, 0.375},
+    {0.125, 0.625}, {0.375, 0.625}, {0.625, 0.625}, {0.875, 0.625},
+    {0.125, 0.875}, {0.375, 0.875}, {0.625, 0.875}, {0.875, 0.875}};
+
+// Root rays of generation 0: sample `i % aa` of pixel `i / aa` of the shard
+// (camera.rs:57-69 / 71-90), or an explicit ray; deeper generations read
+// their queue.
 __device__ __forceinline__ void wf_ray(const WfArgs& a, const DevCamera& cam, unsigned i, V3& o, V3& d) {
   if (a.g == 0 && a.camera_mode) {
-    const uint32_t lr = i / cam.hsize, x = i - lr * cam.hsize;
+    const uint32_t p = i / a.aa, smp = i - p * a.aa;
+    const uint32_t lr = p / cam.hsize, x = p - lr * cam.hsize;
     const uint32_t blk = lr / a.row_block, off = lr - blk * a.row_block;
     const uint32_t y = (blk * a.n_shards + a.shard) * a.row_block + off;
-    ray_for_pixel(cam, x, y, o, d);
+    if (a.aa == 1) {
+      ray_for_pixel(cam, x, y, o, d);
+    } else {
+      const double* ofs = kAaOffsets[a.aa - 1 + smp];
+      ray_for_pixel(cam, x, y, o, d, ofs[0], ofs[1]);
+    }
   } else {
     const WfRay& r = a.rays[i];
     o = v3(r.o[0], r.o[1], r.o[2]);
@@ -127,36 +146,14 @@ __device__ WfLds wf_lds_stage(const DevScene& sc, const PrimRec* prim, unsigned 
   return v;
 }
 
-// The sphere test from (a, dt, c) — sphere.rs:47-62 as in sphere_roots_lazy.
-__device__ __forceinline__ void sphere_from_adc(double a, double dt, double c, const int* meta_p, bool shadow_mode,
-                                                Hit& h, unsigned& n_disc) {
-  const double disc = dt * dt - a * c;
-  if (disc >= 0.0) {
-    ++n_disc;
-    const int meta = *meta_p;
-    const double q = sqrt(disc);
-    const double t1 = (-dt - q) / a;
-    const double t2 = (-dt + q) / a;
-    const int k1 = (meta >> 1) * 2;
-    const bool eligible = !shadow_mode || (meta & 1);
-    if (eligible) {
-      if (t1 >= 0.0) {
-        if (better(t1, k1, h.t, h.key)) { h.t = t1; h.key = k1; }
-      } else if (t2 >= 0.0) {
-        if (better(t2, k1 + 1, h.t, h.key)) { h.t = t2; h.key = k1 + 1; }
-      }
-    }
-    if (t1 < 0.0 && t2 >= 0.0) push_container(h, t1, k1);
-  }
-}
-
-// World::intersect + hit over the LDS image (closest hit + containers top-2).
-template <bool PRIMARY>
+// World::intersect + hit over the LDS image (closest hit + containers top-2,
+// or the shadow-caster variant). Sphere records are read as wave-uniform
+// ds_read_b128 broadcasts with a one-record look-ahead; the image holds zero
+// padding records, so record j+1 always exists.
+template <bool PRIMARY, bool SHADOW>
 __device__ __forceinline__ void wf_trace_lds(const DevScene& sc, const WfLds& lv, V3 o, V3 d, Hit& h,
                                              unsigned& n_disc) {
-  h.t = INFINITY;
-  h.c1t = -INFINITY; h.c2t = -INFINITY; h.c1k = -1; h.c2k = -1;
-  h.key = 0x7fffffff;
+  hit_init(h);
   const d2* r = (const d2*)lv.diag;
   if constexpr (PRIMARY) {
     // record: (s0 s1) (s2 o'x) (o'y o'z) (c pad); 16 f64 ops per test
@@ -166,23 +163,20 @@ __device__ __forceinline__ void wf_trace_lds(const DevScene& sc, const WfLds& lv
       const d2 b0 = r[4 * j + 4], b1 = r[4 * j + 5], b2 = r[4 * j + 6], b3 = r[4 * j + 7];
       {
         const double dx = a0.x * d.x, dy = a0.y * d.y, dz = a1.x * d.z;
-        const double a = dx * dx + dy * dy + dz * dz;
-        const double dt = dx * a1.y + dy * a2.x + dz * a2.y;
-        sphere_from_adc(a, dt, a3.x, lv.diag_meta + j, false, h, n_disc);
+        sphere_adc<SHADOW>(dx * dx + dy * dy + dz * dz, dx * a1.y + dy * a2.x + dz * a2.y, a3.x,
+                           [&] { return lv.diag_meta[j]; }, h, n_disc);
       }
       a0 = r[4 * j + 8]; a1 = r[4 * j + 9]; a2 = r[4 * j + 10]; a3 = r[4 * j + 11];
       {
         const double dx = b0.x * d.x, dy = b0.y * d.y, dz = b1.x * d.z;
-        const double a = dx * dx + dy * dy + dz * dz;
-        const double dt = dx * b1.y + dy * b2.x + dz * b2.y;
-        sphere_from_adc(a, dt, b3.x, lv.diag_meta + j + 1, false, h, n_disc);
+        sphere_adc<SHADOW>(dx * dx + dy * dy + dz * dz, dx * b1.y + dy * b2.x + dz * b2.y, b3.x,
+                           [&] { return lv.diag_meta[j + 1]; }, h, n_disc);
       }
     }
     if (j < sc.n_diag) {
       const double dx = a0.x * d.x, dy = a0.y * d.y, dz = a1.x * d.z;
-      const double a = dx * dx + dy * dy + dz * dz;
-      const double dt = dx * a1.y + dy * a2.x + dz * a2.y;
-      sphere_from_adc(a, dt, a3.x, lv.diag_meta + j, false, h, n_disc);
+      sphere_adc<SHADOW>(dx * dx + dy * dy + dz * dz, dx * a1.y + dy * a2.x + dz * a2.y, a3.x,
+                         [&] { return lv.diag_meta[j]; }, h, n_disc);
     }
   } else {
     // record: (s0 s1) (s2 t0) (t1 t2); 28 f64 ops per test
@@ -190,15 +184,15 @@ __device__ __forceinline__ void wf_trace_lds(const DevScene& sc, const WfLds& lv
     int j = 0;
     for (; j + 1 < sc.n_diag; j += 2) {
       const d2 b0 = r[3 * j + 3], b1 = r[3 * j + 4], b2 = r[3 * j + 5];
-      sphere_roots_lazy(a0.x * o.x + a1.y, a0.y * o.y + a2.x, a1.x * o.z + a2.y, a0.x * d.x, a0.y * d.y,
-                        a1.x * d.z, lv.diag_meta + j, false, h, n_disc);
+      sphere_test<SHADOW>(a0.x * o.x + a1.y, a0.y * o.y + a2.x, a1.x * o.z + a2.y, a0.x * d.x, a0.y * d.y,
+                          a1.x * d.z, [&] { return lv.diag_meta[j]; }, h, n_disc);
       a0 = r[3 * j + 6]; a1 = r[3 * j + 7]; a2 = r[3 * j + 8];
-      sphere_roots_lazy(b0.x * o.x + b1.y, b0.y * o.y + b2.x, b1.x * o.z + b2.y, b0.x * d.x, b0.y * d.y,
-                        b1.x * d.z, lv.diag_meta + j + 1, false, h, n_disc);
+      sphere_test<SHADOW>(b0.x * o.x + b1.y, b0.y * o.y + b2.x, b1.x * o.z + b2.y, b0.x * d.x, b0.y * d.y,
+                          b1.x * d.z, [&] { return lv.diag_meta[j + 1]; }, h, n_disc);
     }
     if (j < sc.n_diag)
-      sphere_roots_lazy(a0.x * o.x + a1.y, a0.y * o.y + a2.x, a1.x * o.z + a2.y, a0.x * d.x, a0.y * d.y,
-                        a1.x * d.z, lv.diag_meta + j, false, h, n_disc);
+      sphere_test<SHADOW>(a0.x * o.x + a1.y, a0.y * o.y + a2.x, a1.x * o.z + a2.y, a0.x * d.x, a0.y * d.y,
+                          a1.x * d.z, [&] { return lv.diag_meta[j]; }, h, n_disc);
   }
   for (int j = 0; j < sc.n_gen; ++j) {
     double m[12];
@@ -207,20 +201,15 @@ __device__ __forceinline__ void wf_trace_lds(const DevScene& sc, const WfLds& lv
     const V3 lo = m34_point(m, o);
     const V3 ld = v3(m[0] * d.x + m[1] * d.y + m[2] * d.z, m[4] * d.x + m[5] * d.y + m[6] * d.z,
                      m[8] * d.x + m[9] * d.y + m[10] * d.z);
-    sphere_roots_lazy(lo.x, lo.y, lo.z, ld.x, ld.y, ld.z, lv.gen_meta + j, false, h, n_disc);
+    sphere_test<SHADOW>(lo.x, lo.y, lo.z, ld.x, ld.y, ld.z, [&] { return lv.gen_meta[j]; }, h, n_disc);
   }
   for (int j = 0; j < sc.n_planes; ++j) {  // plane.rs:53-60
     const double m0 = lv.plane[4 * j], m1 = lv.plane[4 * j + 1], m2 = lv.plane[4 * j + 2], m3 = lv.plane[4 * j + 3];
-    const double oy = m0 * o.x + m1 * o.y + m2 * o.z + m3;
-    const double dy = m0 * d.x + m1 * d.y + m2 * d.z;
-    if (!(fabs(dy) < kEpsilon)) {
-      const double t = -oy / dy;
-      const int k = (lv.plane_meta[j] >> 1) * 2;
-      if (t >= 0.0 && better(t, k, h.t, h.key)) { h.t = t; h.key = k; }
-      if (t < 0.0) push_container(h, t, k);
-    }
+    plane_test<SHADOW>(m0 * o.x + m1 * o.y + m2 * o.z + m3, m0 * d.x + m1 * d.y + m2 * d.z, lv.plane_meta[j], h);
   }
-  if (h.key == 0x7fffffff) h.key = -1;
+  cQuadRec qr = (cQuadRec)sc.quads;  // cubes / cylinders / cones: scalar loads
+  for (int j = 0; j < sc.n_quads; ++j) quad_test<SHADOW>(qr + j, o, d, h);
+  hit_finish(h);
 }
 
 // ---------------------------------------------------------- trace kernels
@@ -235,10 +224,10 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest(DevScene sc,
     V3 o, d;
     wf_ray(a, cam, i, o, d);
     Hit h;
-    if constexpr (USE_LDS) wf_trace_lds<PRIMARY>(sc, lv, o, d, h, n_disc);
-    else trace<false>(sc, LdsView{}, o, d, false, h, n_disc);
+    if constexpr (USE_LDS) wf_trace_lds<PRIMARY, false>(sc, lv, o, d, h, n_disc);
+    else trace<false>(sc, o, d, h, n_disc);
     WfHit w;
-    w.t = h.t; w.key = h.key; w.c1k = h.c1k; w.c2k = h.c2k; w.pad = 0;
+    w.t = h.t; w.key = h.key; w.c1k = h.c1k; w.c2k = h.c2k; w.hin = h.hin;
     a.hits[i] = w;
   }
   const unsigned long long s = wave_sum(n_disc);
@@ -261,46 +250,8 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow(DevScene sc, 
     const V3 o = v3(s.o[0], s.o[1], s.o[2]);
     const V3 d = v3(s.d[0], s.d[1], s.d[2]);
     Hit h;
-    if constexpr (USE_LDS) {
-      // shadow_mode variant of the LDS loop: eligibility = casts_shadow
-      h.t = INFINITY; h.c1t = -INFINITY; h.c2t = -INFINITY; h.c1k = -1; h.c2k = -1; h.key = 0x7fffffff;
-      const d2* r = (const d2*)lv.diag;
-      d2 a0 = r[0], a1 = r[1], a2 = r[2];
-      int j = 0;
-      for (; j + 1 < sc.n_diag; j += 2) {
-        const d2 b0 = r[3 * j + 3], b1 = r[3 * j + 4], b2 = r[3 * j + 5];
-        sphere_roots_lazy(a0.x * o.x + a1.y, a0.y * o.y + a2.x, a1.x * o.z + a2.y, a0.x * d.x, a0.y * d.y,
-                          a1.x * d.z, lv.diag_meta + j, true, h, n_disc);
-        a0 = r[3 * j + 6]; a1 = r[3 * j + 7]; a2 = r[3 * j + 8];
-        sphere_roots_lazy(b0.x * o.x + b1.y, b0.y * o.y + b2.x, b1.x * o.z + b2.y, b0.x * d.x, b0.y * d.y,
-                          b1.x * d.z, lv.diag_meta + j + 1, true, h, n_disc);
-      }
-      if (j < sc.n_diag)
-        sphere_roots_lazy(a0.x * o.x + a1.y, a0.y * o.y + a2.x, a1.x * o.z + a2.y, a0.x * d.x, a0.y * d.y,
-                          a1.x * d.z, lv.diag_meta + j, true, h, n_disc);
-      for (int q = 0; q < sc.n_gen; ++q) {
-        double m[12];
-#pragma unroll
-        for (int e = 0; e < 12; ++e) m[e] = lv.gen[12 * q + e];
-        const V3 lo = m34_point(m, o);
-        const V3 ld = v3(m[0] * d.x + m[1] * d.y + m[2] * d.z, m[4] * d.x + m[5] * d.y + m[6] * d.z,
-                         m[8] * d.x + m[9] * d.y + m[10] * d.z);
-        sphere_roots_lazy(lo.x, lo.y, lo.z, ld.x, ld.y, ld.z, lv.gen_meta + q, true, h, n_disc);
-      }
-      for (int q = 0; q < sc.n_planes; ++q) {
-        const double m0 = lv.plane[4 * q], m1 = lv.plane[4 * q + 1], m2 = lv.plane[4 * q + 2], m3 = lv.plane[4 * q + 3];
-        const double oy = m0 * o.x + m1 * o.y + m2 * o.z + m3;
-        const double dy = m0 * d.x + m1 * d.y + m2 * d.z;
-        if (!(fabs(dy) < kEpsilon)) {
-          const double t = -oy / dy;
-          const int meta = lv.plane_meta[q];
-          if ((meta & 1) && t >= 0.0 && better(t, (meta >> 1) * 2, h.t, h.key)) { h.t = t; h.key = (meta >> 1) * 2; }
-        }
-      }
-      if (h.key == 0x7fffffff) h.key = -1;
-    } else {
-      trace<false>(sc, LdsView{}, o, d, true, h, n_disc);
-    }
+    if constexpr (USE_LDS) wf_trace_lds<false, true>(sc, lv, o, d, h, n_disc);
+    else trace<true>(sc, o, d, h, n_disc);
     a.sflags[s.slot] = (h.key >= 0 && h.t < s.dist) ? 1 : 0;
   }
   const unsigned long long s = wave_sum(n_disc);
@@ -328,7 +279,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_prep(DevScene sc, DevCamera cam, 
       const WfHit w = a.hits[i];
       if (w.key >= 0) {
         Hit h;
-        h.t = w.t; h.key = w.key; h.c1k = w.c1k; h.c2k = w.c2k; h.c1t = 0; h.c2t = 0;
+        h.t = w.t; h.key = w.key; h.hin = w.hin; h.c1k = w.c1k; h.c2k = w.c2k; h.c1t = 0; h.c2t = 0;
         c = prepare(sc, o, d, h);
         hit = true;
         m = &sc.shade[c.obj];
@@ -434,6 +385,23 @@ __global__ __launch_bounds__(kWfBlock) void wf_combine(DevScene sc, DevCamera ca
     }
     double* out = a.colors + (size_t)i * 3;
     out[0] = color.x; out[1] = color.y; out[2] = color.z;
+  }
+}
+
+// Color::average (color.rs:26-33) of the AA samples of each pixel: a left
+// fold from black, then * (1 / n).
+__global__ __launch_bounds__(kWfBlock) void wf_average(const double* colors, unsigned n_pix, unsigned aa,
+                                                       double* out) {
+  const unsigned stride = gridDim.x * blockDim.x;
+  for (unsigned p = blockIdx.x * blockDim.x + threadIdx.x; p < n_pix; p += stride) {
+    V3 sum = v3(0.0, 0.0, 0.0);
+    for (unsigned s = 0; s < aa; ++s) {
+      const double* c = colors + ((size_t)p * aa + s) * 3;
+      sum = vadd(sum, v3(c[0], c[1], c[2]));
+    }
+    const V3 avg = vscale(sum, 1.0 / (double)aa);
+    double* o = out + (size_t)p * 3;
+    o[0] = avg.x; o[1] = avg.y; o[2] = avg.z;
   }
 }
 
@@ -593,10 +561,14 @@ static hipError_t launch_shadow_wf(const DevScene& sc, const WfArgs& a, bool lds
 }
 
 hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool camera_mode, const double* d_in_rays,
-                             unsigned n0, unsigned max_depth, unsigned row_block, unsigned shard, unsigned n_shards,
-                             double* d_out, hipStream_t stream, const std::string& signature, DevStats* stats,
-                             float* ms_kernel) {
+                             unsigned n0, unsigned aa, unsigned max_depth, unsigned row_block, unsigned shard,
+                             unsigned n_shards, double* d_out, hipStream_t stream, const std::string& signature,
+                             DevStats* stats, float* ms_kernel) {
   if (max_depth + 2 > (unsigned)kMaxGen) return hipErrorInvalidValue;
+  if (aa == 0 || aa > 16 || (aa & (aa - 1)) != 0 || (!camera_mode && aa != 1) || n0 % aa != 0)
+    return hipErrorInvalidValue;
+  // with AA the root colours are averaged into d_out by wf_average
+  const bool averaged = aa > 1;
   WF_CHECK(ensure_misc((size_t)sc.n_diag));
   const unsigned L = (unsigned)sc.n_lights;
   auto it = signature.empty() ? cache_.end() : cache_.find(signature);
@@ -636,7 +608,8 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     WfArgs a{};
     WfGenBuf& B = gens_[g];
     a.rays = B.rays; a.hits = B.hits; a.nodes = B.nodes; a.shadows = B.shadows; a.sflags = B.sflags;
-    a.colors = g == 0 ? d_out : B.colors;
+    a.colors = (g == 0 && !averaged) ? d_out : B.colors;
+    a.aa = aa;
     a.next_rays = gens_[g + 1].rays;
     a.child_colors = gens_[g + 1].colors;
     a.cnt = d_cnt_;
@@ -687,7 +660,8 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     WfArgs a{};
     WfGenBuf& B = gens_[g];
     a.rays = B.rays; a.nodes = B.nodes; a.sflags = B.sflags;
-    a.colors = g == 0 ? d_out : B.colors;
+    a.colors = (g == 0 && !averaged) ? d_out : B.colors;
+    a.aa = aa;
     a.child_colors = gens_[g + 1].colors;
     a.n = counts.rays[g];
     a.g = (unsigned)g; a.max_depth = max_depth;
@@ -696,6 +670,14 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     WF_CHECK(pmark(stream, WF_COMBINE, true));
     hipLaunchKernelGGL(wf_combine, dim3(occupancy_grid(wf_combine, kWfBlock, 0, a.n)), dim3(kWfBlock), 0, stream, sc,
                        cam, a);
+    WF_CHECK(hipGetLastError());
+    WF_CHECK(pmark(stream, WF_COMBINE, false));
+  }
+  if (averaged) {
+    const unsigned n_pix = n0 / aa;
+    WF_CHECK(pmark(stream, WF_COMBINE, true));
+    hipLaunchKernelGGL(wf_average, dim3(occupancy_grid(wf_average, kWfBlock, 0, n_pix)), dim3(kWfBlock), 0, stream,
+                       gens_[0].colors, n_pix, aa, d_out);
     WF_CHECK(hipGetLastError());
     WF_CHECK(pmark(stream, WF_COMBINE, false));
   }
@@ -720,8 +702,8 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     s.rays_shadow = shadows;
     s.sphere_tests = (rays + shadows) * (unsigned long long)(sc.n_diag + sc.n_gen);
     s.plane_tests = (rays + shadows) * (unsigned long long)sc.n_planes;
+    s.other_tests = (rays + shadows) * (unsigned long long)sc.n_quads;
     s.sphere_disc_ge0 = hc.disc[0] + hc.disc[1] + hc.disc[2];
-    s.wave_steps = 0;
     *stats = s;
   }
   return hipSuccess;

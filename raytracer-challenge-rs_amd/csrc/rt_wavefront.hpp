@@ -36,7 +36,7 @@ struct WfRay {  // 64 B
 };
 struct WfHit {  // 24 B: nearest hit + containers top-2 (rt_device.hpp Hit)
   double t;
-  int32_t key, c1k, c2k, pad;
+  int32_t key, c1k, c2k, hin;
 };
 struct WfNode {  // prepare_computations results needed by combine
   double over[3], under[3], normal[3];
@@ -99,6 +99,7 @@ struct WfArgs {
   unsigned camera_mode; // g == 0 rays come from the camera (1) or from `rays` (0)
   unsigned row_block, shard, n_shards;
   unsigned disc_slot;   // WfCounters::disc index of this trace launch
+  unsigned aa;          // AA samples per pixel (generation 0 in camera mode)
 };
 
 // Per-kernel-class timing of the last frame (profiling mode only).
@@ -120,14 +121,15 @@ class Wavefront {
   // Per-class times averaged over the frames rendered since profiling was
   // enabled; rays / disc counts of the last frame (synchronises).
   hipError_t last_profile(WfProfile* out);
-  // Render n0 root rays (camera pixels of a shard, or explicit rays) into
-  // `out` (n0*3 doubles, device). Counts of a signature seen before are
-  // reused (fully asynchronous); otherwise each generation is sized by a
-  // synchronous count read-back. stats (host) may be null.
+  // Render n0 root rays (camera pixels x `aa` samples of a shard, or explicit
+  // rays) into `out` (n0/aa*3 doubles, device; AA samples are averaged like
+  // Color::average). Counts of a signature seen before are reused (fully
+  // asynchronous); otherwise each generation is sized by a synchronous count
+  // read-back. stats (host) may be null.
   hipError_t render(const DevScene& sc, const DevCamera& cam, bool camera_mode, const double* d_in_rays,
-                    unsigned n0, unsigned max_depth, unsigned row_block, unsigned shard, unsigned n_shards,
-                    double* d_out, hipStream_t stream, const std::string& signature, DevStats* stats,
-                    float* ms_kernel);
+                    unsigned n0, unsigned aa, unsigned max_depth, unsigned row_block, unsigned shard,
+                    unsigned n_shards, double* d_out, hipStream_t stream, const std::string& signature,
+                    DevStats* stats, float* ms_kernel);
 
  private:
   hipError_t ensure_gen(size_t g, size_t rays, size_t n_lights);

@@ -230,4 +230,130 @@ def zoo(width=160, height=120):
     return w, _camera(width, height, PI / 3.0, (0.0, 1.5, -5.0), (0, 1, 0)), 5
 
 
-CONFIGS = {"c1": c1, "c2": c2, "c3": c3, "c5": c5, "zoo": zoo}
+def first_scene(width=2560, height=1440):
+    """The reference demo bin/first_scene.rs:22-109 (checkered floor, ring and
+    stripe walls, three spheres, a rotated cube, a closed cylinder and a closed
+    cone, two lights), rendered there with render_multithreaded at X1."""
+    w = rt.World()
+    floor = rt.Plane()
+    floor.material.set_pattern(rt.checkers_pattern(rt.Color(0.0, 0.5, 0.5), rt.Color(0.5, 0.0, 0.5)))
+    left_wall = rt.Plane()
+    left_wall.set_transform(rt.Matrix.identity(4, 4).rotate_x(PI / 2.0).rotate_y(-PI / 4.0).translate(0, 0, 5))
+    ring = rt.ring_pattern(rt.Color(0.0, 0.0, 1.0), rt.Color(0.0, 1.0, 1.0))
+    ring.set_transform(rt.scaling(0.333, 0.333, 0.333))
+    left_wall.material.set_pattern(ring)
+    right_wall = rt.Plane()
+    right_wall.set_transform(rt.Matrix.identity(4, 4).rotate_x(PI / 2.0).rotate_y(PI / 4.0).translate(0, 0, 5))
+    right_wall.material.set_pattern(rt.stripe_pattern(rt.Color.white(), rt.Color.black()))
+    middle = rt.Sphere()
+    middle.set_transform(rt.translation(-0.5, 1.0, 0.5))
+    middle.material.color = rt.Color(0.1, 1.0, 0.5)
+    middle.material.diffuse = 0.7
+    middle.material.specular = 0.3
+    middle.material.reflective = 0.9
+    right = rt.Sphere()
+    right.set_transform(rt.translation(1.5, 0.5, -0.5) * rt.scaling(0.5, 0.5, 0.5))
+    right.material.set_pattern(rt.checkers_pattern(rt.Color(1.0, 0.0, 0.0), rt.Color(0.0, 1.0, 0.0)))
+    left = rt.glass_sphere()
+    left.material.color = rt.Color(0.1, 0.0, 0.0)
+    left.material.ambient = 0.1
+    left.material.diffuse = 0.05
+    left.material.reflective = 0.3
+    left.material.specular = 1.0
+    left.material.shininess = 300.0
+    left.set_transform(rt.translation(-1.5, 0.33, -0.75) * rt.scaling(0.33, 0.33, 0.33))
+    cube = rt.Cube()
+    cube.set_transform(rt.Matrix.identity(4, 4).rotate_y(PI / 4.0).scale(0.25, 0.25, 0.25).translate(0.0, 0.25, -1.0))
+    cylinder = rt.Cylinder(0.0, 1.0, True)
+    cylinder.set_transform(rt.translation(1.0, 0.0, -1.2) * rt.scaling(0.33, 0.33, 0.33))
+    cone = rt.Cone(-1.0, 0.0, True)
+    cone.set_transform(rt.translation(-1.0, 0.33, -1.2) * rt.scaling(0.33, 0.33, 0.33))
+    w.add_light(rt.PointLight(rt.Point(-10, 10, -10), rt.Color(1.0, 1.0, 1.0)))
+    w.add_light(rt.PointLight(rt.Point(-5.0, 10.0, -6.0), rt.Color(0.33, 0.33, 0.33)))
+    for o in (floor, left_wall, right_wall, middle, right, left, cube, cylinder, cone):
+        w.add_object(o)
+    return w, _camera(width, height, PI / 3.0, (0.0, 1.5, -5.0), (0, 1, 0)), 5
+
+
+def solids(width=160, height=120):
+    """Cube / Cylinder / Cone coverage: glass solids nested in each other and
+    in spheres (containers with up to 4 intersections per object), open,
+    closed and unbounded cylinders and cones, rotated and sheared solids,
+    mirrors, patterns, a shadowless cone."""
+    w = rt.World()
+    floor = rt.Plane()
+    floor.material.set_pattern(rt.checkers_pattern(rt.Color(0.9, 0.9, 0.9), rt.Color(0.2, 0.2, 0.3)))
+    floor.material.reflective = 0.15
+    w.add_object(floor)
+    back = rt.Plane()
+    back.set_transform(rt.translation(0, 0, 8) * rt.rotation_x(PI / 2.0))
+    back.material.set_pattern(rt.stripe_pattern(rt.Color(0.8, 0.4, 0.2), rt.Color(0.2, 0.4, 0.8)))
+    w.add_object(back)
+    # glass cube with a glass cylinder core and an air-bubble sphere
+    gcube = rt.Cube()
+    gcube.set_transform(rt.translation(-1.2, 1.0, 0.0) * rt.rotation_y(0.5) * rt.rotation_x(0.3)
+                        * rt.scaling(0.8, 0.8, 0.8))
+    gcube.material.transparency = 0.9
+    gcube.material.reflective = 0.6
+    gcube.material.refractive_index = 1.5
+    gcube.material.color = rt.Color(0.05, 0.1, 0.05)
+    gcube.material.diffuse = 0.1
+    gcube.material.specular = 1.0
+    gcube.material.shininess = 300.0
+    w.add_object(gcube)
+    core = rt.Cylinder(-0.5, 0.5, True)
+    core.set_transform(rt.translation(-1.2, 1.0, 0.0) * rt.rotation_z(0.4) * rt.scaling(0.3, 1.0, 0.3))
+    core.material.transparency = 0.8
+    core.material.refractive_index = 2.0
+    core.material.color = rt.Color(0.2, 0.0, 0.0)
+    w.add_object(core)
+    bubble = rt.glass_sphere()
+    bubble.set_transform(rt.translation(-1.0, 1.3, -0.3) * rt.scaling(0.2, 0.2, 0.2))
+    bubble.material.refractive_index = 1.0
+    w.add_object(bubble)
+    # glass double-napped closed cone, and an open cone inside a glass sphere
+    cone = rt.Cone(-1.0, 1.0, True)
+    cone.set_transform(rt.translation(1.3, 1.0, 0.3) * rt.scaling(0.5, 1.0, 0.5))
+    cone.material.transparency = 0.7
+    cone.material.reflective = 0.4
+    cone.material.refractive_index = 1.33
+    cone.material.color = rt.Color(0.0, 0.05, 0.1)
+    w.add_object(cone)
+    shell = rt.glass_sphere()
+    shell.set_transform(rt.translation(0.1, 0.6, -1.5) * rt.scaling(0.6, 0.6, 0.6))
+    shell.material.reflective = 0.5
+    w.add_object(shell)
+    inner = rt.Cone(-0.5, 0.0, False)
+    inner.set_transform(rt.translation(0.1, 0.8, -1.5) * rt.scaling(0.4, 0.8, 0.4))
+    inner.material.color = rt.Color(1.0, 0.8, 0.1)
+    w.add_object(inner)
+    # opaque solids: open cylinder tube, unbounded thin cylinder (pole), sheared cube, mirror cube
+    tube = rt.Cylinder(0.0, 0.7, False)
+    tube.set_transform(rt.translation(-0.2, 0.0, 1.2) * rt.rotation_y(0.2) * rt.scaling(0.5, 1.0, 0.5))
+    tube.material.set_pattern(rt.ring_pattern(rt.Color(1, 1, 1), rt.Color(0.1, 0.6, 0.1)))
+    w.add_object(tube)
+    pole = rt.Cylinder()
+    pole.set_transform(rt.translation(2.4, 0.0, 2.5) * rt.scaling(0.1, 1.0, 0.1))
+    pole.material.color = rt.Color(0.6, 0.6, 0.6)
+    w.add_object(pole)
+    shear = rt.Cube()
+    shear.set_transform(rt.translation(0.9, 0.3, -2.3) * rt.shearing(0.4, 0.0, 0.0, 0.2, 0.0, 0.0)
+                        * rt.scaling(0.3, 0.3, 0.3))
+    shear.material.set_pattern(rt.gradient_pattern(rt.Color(1, 0, 0), rt.Color(0, 0, 1)))
+    w.add_object(shear)
+    mirror = rt.Cube()
+    mirror.set_transform(rt.translation(-2.6, 1.0, 2.0) * rt.rotation_y(-0.6) * rt.scaling(0.05, 1.0, 1.0))
+    mirror.material.reflective = 1.0
+    mirror.material.color = rt.Color(0.05, 0.05, 0.05)
+    w.add_object(mirror)
+    ghost = rt.Cone(0.0, 0.6, True)
+    ghost.set_transform(rt.translation(-0.5, 0.0, -2.5) * rt.scaling(0.3, 0.5, 0.3))
+    ghost.material.set_pattern(rt.test_pattern())
+    ghost.no_shadow()
+    w.add_object(ghost)
+    w.add_light(rt.PointLight(rt.Point(-6, 8, -8), rt.Color(1.0, 1.0, 1.0)))
+    w.add_light(rt.PointLight(rt.Point(5.0, 6.0, -4.0), rt.Color(0.3, 0.3, 0.3)))
+    return w, _camera(width, height, PI / 3.0, (0.0, 2.0, -5.5), (0, 0.8, 0)), 6
+
+
+CONFIGS = {"c1": c1, "c2": c2, "c3": c3, "c5": c5, "zoo": zoo, "first_scene": first_scene, "solids": solids}

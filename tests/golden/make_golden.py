@@ -8,7 +8,7 @@ reference's 49 known-answer tests (tests/test_oracle_kat.py). The fixtures
 freeze the oracle's output so that (1) a change to the oracle is caught on CPU
 and (2) the GPU path is checked against files, not only against a live oracle.
 
-Per case <name>:
+Per case <name> (aa > 1: `render_multithreaded` with that many AA samples):
   <name>.ppm        P3 bytes of the frame (canvas.rs:43-48 / ppm.rs:24-75)
   <name>.npz        f64 canvas (H, W, 3) `canvas` + the camera descriptor bytes
   index.json        per case: scene, size, depth, the exact counters, sha256
@@ -39,24 +39,33 @@ CASES = [
     ("c3_96x54", "c3", {"width": 96, "height": 54}),
     ("c3_64x36_s200", "c3", {"width": 64, "height": 36, "n_spheres": 200}),
     ("zoo_64x48", "zoo", {"width": 64, "height": 48}),
+    ("first_scene_96x54", "first_scene", {"width": 96, "height": 54}),
+    ("solids_64x48", "solids", {"width": 64, "height": 48}),
+    # render_multithreaded with AA (camera.rs:150-214)
+    ("first_scene_48x27_aa4", "first_scene", {"width": 48, "height": 27}, 4),
+    ("solids_40x30_aa16", "solids", {"width": 40, "height": 30}, 16),
+    ("c3_48x27_s100_aa2", "c3", {"width": 48, "height": 27, "n_spheres": 100}, 2),
+    ("zoo_32x24_aa8", "zoo", {"width": 32, "height": 24}, 8),
 ]
 COUNTERS = ("rays_primary", "rays_reflect", "rays_refract", "rays_shadow",
-            "sphere_tests", "plane_tests", "sphere_disc_ge0")
+            "sphere_tests", "plane_tests", "sphere_disc_ge0", "other_tests")
 
 
 def main():
     index = {}
-    for name, kind, kw in CASES:
+    for case in CASES:
+        name, kind, kw = case[:3]
+        aa = case[3] if len(case) > 3 else 1
         w, cam, depth = scene(rtamd, kind, kw)
         ow = pyoracle.OracleWorld.from_world(w)
-        canvas, st = ow.render(cam.desc_bytes(), depth, nthreads=8)
+        canvas, st = ow.render(cam.desc_bytes(), depth, nthreads=8, aa_samples=aa)
         ppm = pyoracle.canvas_to_ppm(canvas)
         with open(os.path.join(HERE, name + ".ppm"), "wb") as f:
             f.write(ppm)
         np.savez_compressed(os.path.join(HERE, name + ".npz"), canvas=canvas,
                             camera=np.frombuffer(cam.desc_bytes(), dtype=np.uint8))
         index[name] = {
-            "scene": kind, "args": kw, "width": cam.hsize, "height": cam.vsize, "depth": depth,
+            "scene": kind, "args": kw, "width": cam.hsize, "height": cam.vsize, "depth": depth, "aa": aa,
             "counters": {k: int(st[k]) for k in COUNTERS},
             "ppm_sha256": hashlib.sha256(ppm).hexdigest(),
             "canvas_sha256": hashlib.sha256(np.ascontiguousarray(canvas).tobytes()).hexdigest(),

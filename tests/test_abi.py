@@ -24,7 +24,7 @@ def test_header_declares_the_boundary():
     for must in ("rt_scene_create", "rt_scene_destroy", "rt_render", "rt_render_shard_device",
                  "rt_render_multi", "rt_color_at_batch", "rt_is_shadowed_batch", "rt_hit_batch",
                  "rt_canvas_to_ppm", "rt_quantize_u8", "rt_matrix_inverse", "rt_camera_init",
-                 "rt_last_error", "rt_abi_version", "rt_device_count", "rt_shard_rows"):
+                 "rt_last_error", "rt_abi_version", "rt_device_count", "rt_shard_rows", "rt_render_aa"):
         assert must in names
 
 
@@ -36,7 +36,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_shard_rows():
     lib = ctypes.CDLL(LIB)
-    assert lib.rt_abi_version() == 1
+    assert lib.rt_abi_version() == 2
     f = lib.rt_shard_rows
     f.restype = ctypes.c_uint32
     f.argtypes = [ctypes.c_uint32] * 4
@@ -51,6 +51,36 @@ def test_duplicate_shapes_rejected_before_any_device_work(rt):
     w.add_object(rt.Sphere())
     w.add_object(rt.Sphere())  # structurally equal -> containers semantics ambiguous
     w.add_light(rt.PointLight(rt.Point(0, 0, -10), rt.Color(1, 1, 1)))
+    with pytest.raises(rt.RtError, match="structurally equal"):
+        w.upload()
+
+
+def test_descriptor_layout_matches_oracle(rt, oracle):
+    # the oracle and the product read the same rt_shape_desc / rt_camera_desc bytes
+    L = oracle.lib()
+    assert len(rt.Sphere().desc_bytes()) == L.oracle_sizeof_shape_desc() == 680
+    assert len(rt.Camera(4, 3, 1.0).desc_bytes()) == L.oracle_sizeof_camera_desc() == 160
+    assert L.oracle_sizeof_stats() == ctypes.sizeof(oracle.Stats) == 8 * 8 + 2 * 8
+
+
+def test_cylinders_differing_only_in_bounds_are_not_duplicates(rt):
+    w = rt.World()
+    w.add_object(rt.Cylinder(0.0, 1.0, True))
+    w.add_object(rt.Cylinder(0.0, 2.0, True))
+    w.add_object(rt.Cone(-1.0, 0.0, False))
+    w.add_object(rt.Cone(-1.0, 0.0, True))
+    w.add_light(rt.PointLight(rt.Point(0, 0, -10), rt.Color(1, 1, 1)))
+    try:
+        w.upload()
+    except rt.RtError as e:
+        assert "structurally equal" not in str(e)
+        assert "no HIP device" in str(e)
+
+
+def test_duplicate_cubes_rejected(rt):
+    w = rt.World()
+    w.add_object(rt.Cube())
+    w.add_object(rt.Cube())
     with pytest.raises(rt.RtError, match="structurally equal"):
         w.upload()
 

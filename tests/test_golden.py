@@ -41,7 +41,7 @@ def test_oracle_reproduces_golden(rt, oracle, name):
     w, cam, depth = golden_cases.scene(rt, e["scene"], e["args"])
     assert cam.desc_bytes() == cam_bytes, "host camera builder drifted"
     assert depth == e["depth"]
-    ref, st = oracle.OracleWorld.from_world(w).render(cam.desc_bytes(), depth, nthreads=4)
+    ref, st = oracle.OracleWorld.from_world(w).render(cam.desc_bytes(), depth, nthreads=4, aa_samples=e["aa"])
     assert np.array_equal(ref, canvas)
     assert oracle.canvas_to_ppm(ref) == ppm
     assert {k: int(st[k]) for k in e["counters"]} == e["counters"]
@@ -65,7 +65,11 @@ def test_gpu_matches_golden(rt, name):
     e = INDEX[name]
     canvas, _, ppm = _load(name)
     w, cam, depth = golden_cases.scene(rt, e["scene"], e["args"])
-    out, st = cam.render(w, depth)
+    if e["aa"] == 1:
+        out, st = cam.render(w, depth)
+    else:
+        cam.render_opts.aa_samples(getattr(rt.AASamples, f"X{e['aa']}"))
+        out, st = cam.render_multithreaded(w, depth)
     g = out.to_numpy()
     assert np.isfinite(g).all()
     assert np.abs(g - canvas).max() <= TOL

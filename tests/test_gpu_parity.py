@@ -22,12 +22,16 @@ def _oracle_world(oracle, w):
     return oracle.OracleWorld.from_world(w)
 
 
-def _compare_frame(rt, oracle, w, cam, depth, rows=None):
-    canvas, st = cam.render(w, depth)
+def _compare_frame(rt, oracle, w, cam, depth, rows=None, aa=1):
+    if aa == 1:
+        canvas, st = cam.render(w, depth)
+    else:
+        cam.render_opts.aa_samples(getattr(rt.AASamples, f"X{aa}"))
+        canvas, st = cam.render_multithreaded(w, depth)
     gpu = canvas.to_numpy()
     ow = _oracle_world(oracle, w)
     rows = list(range(cam.vsize)) if rows is None else rows
-    ref, rst = ow.render_rows(cam.desc_bytes(), depth, rows, NTHREADS)
+    ref, rst = ow.render_rows(cam.desc_bytes(), depth, rows, NTHREADS, aa_samples=aa)
     g = gpu[rows]
     diff = np.abs(g - ref)
     assert np.isfinite(g).all()
@@ -35,7 +39,7 @@ def _compare_frame(rt, oracle, w, cam, depth, rows=None):
     assert rt.canvas_to_ppm(g) == oracle.canvas_to_ppm(ref)
     if len(rows) == cam.vsize:
         for k in ("rays_primary", "rays_reflect", "rays_refract", "rays_shadow",
-                  "sphere_tests", "plane_tests", "sphere_disc_ge0"):
+                  "sphere_tests", "plane_tests", "sphere_disc_ge0", "other_tests"):
             assert st[k] == rst[k], (k, st[k], rst[k])
     return gpu, ref, st
 
@@ -108,7 +112,7 @@ def test_hit_batch_bitwise_vs_oracle(rt, oracle):
     """World::intersect + hit + prepare_computations (+ n1/n2, schlick) per ray."""
     from rtamd import scenes
     rng = np.random.default_rng(11)
-    for make in (scenes.zoo, lambda: scenes.c3(64, 36, n_spheres=200)):
+    for make in (scenes.zoo, lambda: scenes.c3(64, 36, n_spheres=200), scenes.solids, scenes.first_scene):
         w, cam, _ = make()
         ow = _oracle_world(oracle, w)
         n = 3000
@@ -264,3 +268,80 @@ def test_deep_recursion_limit(rt, oracle):
         assert np.abs(g - ref).max() <= TOL and st["rays_reflect"] == rst["rays_reflect"] == depth
     with pytest.raises(rt.RtError):
         w.color_at_batch(rays, 65)
+
+
+# ------------------------------------------------- SURVEY §8f rows 1-2
+def test_solids_full_frame(rt, oracle):
+    """Cube / Cylinder / Cone (cube.rs, cylinder.rs, cone.rs): glass solids
+    nested in each other (containers with up to 4 intersections per object)."""
+    from rtamd import scenes
+    w, cam, depth = scenes.solids(200, 150)
+    gpu, ref, st = _compare_frame(rt, oracle, w, cam, depth)
+    assert st["other_tests"] > 0 and st["rays_refract"] > 0
+
+
+def test_first_scene_demo(rt, oracle):
+    """The reference's bin/first_scene.rs (cube + cylinder + cone + 2 lights)."""
+    from rtamd import scenes
+    w, cam, depth = scenes.first_scene(256, 144)
+    _compare_frame(rt, oracle, w, cam, depth)
+
+
+@pytest.mark.parametrize("aa", [1, 2, 4, 8, 16])
+def test_render_multithreaded_aa(rt, oracle, aa):
+    """render_multithreaded: rays_for_pixel offsets + Color::average."""
+    from rtamd import scenes
+    w, cam, depth = scenes.first_scene(64, 36)
+    gpu, ref, st = _compare_frame(rt, oracle, w, cam, depth, aa=aa)
+    assert st["rays_primary"] == 64 * 36 * aa
+
+
+def test_aa_shards_reassemble_bitwise(rt):
+    import torch
+    from rtamd import scenes
+    w, cam, depth = scenes.solids(96, 70)
+    cam.render_opts.aa_samples(rt.AASamples.X4)
+    full, _ = cam.render_multithreaded(w, depth)
+    full = full.to_numpy()
+    for n_shards, block in [(2, 8), (3, 5)]:
+        out = np.zeros_like(full)
+        for s in range(n_shards):
+            rows = rt.shard_rows(cam.vsize, block, s, n_shards)
+            buf = torch.empty((rows, cam.hsize, 3), dtype=torch.float64, device="cuda")
+            cam.render_shard_device(w, depth, block, s, n_shards, buf.data_ptr(),
+                                    torch.cuda.current_stream().cuda_stream, False, aa_samples=4)
+            torch.cuda.synchronize()
+            ys = [y for y in range(cam.vsize) if (y // block) % n_shards == s]
+            out[ys] = buf.cpu().numpy()
+        assert out.tobytes() == full.tobytes()
+
+
+def test_solid_shadows_and_color_at(rt, oracle):
+    from rtamd import scenes
+    w, cam, _ = scenes.solids()
+    ow = _oracle_world(oracle, w)
+    rng = np.random.default_rng(17)
+    pts = rng.uniform([-3, -0.2, -3], [3, 2.5, 3], size=(3000, 3))
+    for light in range(w.n_lights()):
+        g = w.is_shadowed_batch(pts, light)
+        ref = np.array([ow.is_shadowed(p, light) for p in pts])
+        assert np.array_equal(g.astype(bool), ref)
+    o = np.tile([0.0, 2.0, -5.5], (500, 1))
+    d = rng.normal([0, -0.2, 1], [0.3, 0.2, 0.05], size=(500, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.hstack([o, d])
+    for depth in (0, 3, 8):
+        g, st = w.color_at_batch(rays, depth)
+        r, rst = ow.color_at_batch(rays, depth)
+        assert np.abs(g - r).max() <= TOL
+        for k in rst:
+            assert st[k] == rst[k], (depth, k)
+
+
+def test_bad_aa_rejected(rt):
+    w = rt.World.default()
+    c = rt.Camera(4, 4, 1.0)
+    import torch
+    buf = torch.empty((4, 4, 3), dtype=torch.float64, device="cuda")
+    with pytest.raises(rt.RtError, match="aa_samples"):
+        c.render_shard_device(w, 5, 8, 0, 1, buf.data_ptr(), 0, False, aa_samples=3)

@@ -2,7 +2,8 @@
 
 oracle/kat.c transcribes every #[test] on the render path (matrix.rs,
 transform.rs, sphere.rs, plane.rs, intersection.rs, material.rs, pattern/,
-world.rs, camera.rs, image/ppm.rs) at the reference tolerance (1e-5,
+world.rs, camera.rs, image/ppm.rs, and cube.rs / cylinder.rs / cone.rs) at
+the reference tolerance (1e-5,
 lib.rs:18-22). This is what pins the oracle.
 """
 import os
@@ -38,6 +39,13 @@ EXPECTED = [
     "shade_hit_transparent", "shade_hit_schlick", "camera_pixel_size", "camera_rays",
     "render_world_with_camera", "ppm_header_and_pixels", "ppm_color_component_scaling",
     "ppm_split_long_lines",
+    # cube.rs / cylinder.rs / cone.rs and camera.rs AA offsets (row 2)
+    "ray_intersects_cube", "ray_misses_cube", "normal_on_cube_surface", "cube_bounding_box",
+    "ray_misses_cylinder", "ray_strikes_cylinder", "normal_vector_on_cylinder", "default_cylinder_min_max_closed",
+    "intersect_constrained_cylinder", "intersect_caps_closed_cylinder", "normal_vector_on_cylinder_end_cap",
+    "bounded_cylinder_bounding_box", "intersect_cone_with_ray", "intersect_cone_parallel_to_half",
+    "intersect_cone_end_caps", "computing_normal_vector_cone", "bounded_cone_bounding_box",
+    "rays_for_pixel_offsets",
 ]
 
 

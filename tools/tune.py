@@ -1,5 +1,6 @@
-"""A/B occupancy/tuning variants of the render kernel in ONE process,
-interleaved rounds (cdna_hip_programming.md §5.4 rule 24). Dev tool."""
+"""A/B tuning variants of the wavefront pipeline in ONE process, interleaved
+rounds (cdna_hip_programming.md §5.4 rule 24). Dev tool.
+Knob: wf_waves (trace-kernel occupancy, 4 or 8 waves/SIMD)."""
 import os, sys, statistics, argparse
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "raytracer-challenge-rs_amd")]
@@ -7,8 +8,8 @@ import torch  # noqa
 import rtamd
 from rtamd import scenes
 ap = argparse.ArgumentParser()
-ap.add_argument("--waves", default="3,4,5,6")
-ap.add_argument("--knob", default="waves")
+ap.add_argument("--waves", default="8,4")
+ap.add_argument("--knob", default="wf_waves")
 ap.add_argument("--rounds", type=int, default=4)
 ap.add_argument("--scene", default="c3")
 a = ap.parse_args()
@@ -25,13 +26,6 @@ for r in range(a.rounds):
             ref = img
         assert img.tobytes() == ref.tobytes(), f"variant {v} changed the image"
         res[v].append(st["ms_kernel"])
-        if r == a.rounds - 1 and a.knob == "waves":
-            ws, tc, tot = rtamd._rtamd._diag_last(w)
-            lanes = st["rays_primary"] + st["rays_reflect"] + st["rays_refract"] + st["rays_shadow"]
-            msg = f"  [{v}] wave_steps={ws} lane_util={lanes/(64*ws):.3f}"
-            if tot:
-                msg += f" trace_frac={tc/tot:.3f}"
-            print(msg, flush=True)
 n = st["rays_primary"] + st["rays_reflect"] + st["rays_refract"] + st["rays_shadow"]
 for v, ms in res.items():
     print(f"{a.knob}={v}: median {statistics.median(ms):.3f} ms  min {min(ms):.3f}  -> {n/min(ms)/1e3:.1f} Mrays/s  all={['%.2f'%x for x in ms]}", flush=True)
