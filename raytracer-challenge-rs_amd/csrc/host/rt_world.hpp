@@ -287,6 +287,7 @@ class Camera {
   size_t vsize() const { return desc_.vsize; }
   double pixel_size() const { return desc_.pixel_size; }
   const Matrix& transform() const { return transform_; }
+  double field_of_view() const { return fov_; }
   const rt_camera_desc& desc() const { return desc_; }
   Ray ray_for_pixel(size_t px, size_t py) const {  // camera.rs:57-69 (host restatement)
     const double xoffset = ((double)px + 0.5) * desc_.pixel_size;

@@ -8,6 +8,7 @@
 #include <pybind11/stl.h>
 
 #include "../host/rt_world.hpp"
+#include "../host/scene_parser.hpp"
 
 namespace py = pybind11;
 using namespace rt;
@@ -169,7 +170,8 @@ PYBIND11_MODULE(_rtamd, m) {
       .def_readwrite("refractive_index", &Material::refractive_index)
       .def_readonly("has_pattern", &Material::has_pattern)
       .def_readonly("pattern", &Material::pattern)
-      .def("set_pattern", &Material::set_pattern);
+      .def("set_pattern", &Material::set_pattern)
+      .def("copy", [](const Material& mm) { return mm; });
 
   py::class_<PointLight>(m, "PointLight")
       .def(py::init<const Point&, const Color&>())
@@ -294,6 +296,7 @@ PYBIND11_MODULE(_rtamd, m) {
       .def_property_readonly("vsize", &Camera::vsize)
       .def_property_readonly("pixel_size", &Camera::pixel_size)
       .def_property_readonly("transform", &Camera::transform)
+      .def_property_readonly("field_of_view", &Camera::field_of_view)
       .def("ray_for_pixel", &Camera::ray_for_pixel)
       .def("desc_bytes", [](const Camera& c) { return pod_bytes(&c.desc(), sizeof(rt_camera_desc)); })
       .def("render", [](const Camera& c, const World& w, unsigned max_depth) {
@@ -345,6 +348,34 @@ PYBIND11_MODULE(_rtamd, m) {
         return py::make_tuple(std::unique_ptr<Canvas>(out), stats_dict(st));
       }, py::arg("worlds"), py::arg("max_depth") = 5, py::arg("row_block") = 8, py::arg("aa_samples") = 1);
   m.def("shard_rows", &rt_shard_rows);
+
+  // scene-parser/src/lib.rs: the YAML front-end (C++ restatement)
+  py::register_exception<SceneParserError>(m, "SceneParserError");
+  py::register_exception<yaml::ParseError>(m, "YamlError");
+  py::class_<SceneParser>(m, "SceneParser")
+      .def(py::init<>())
+      .def("load_file", &SceneParser::load_file)
+      .def("load_str", &SceneParser::load_str, py::arg("text"), py::arg("name") = "<string>")
+      .def_readonly("messages", &SceneParser::messages)
+      .def_property_readonly("camera", [](const SceneParser& p) -> py::object {
+        if (!p.scene().camera) return py::none();
+        return py::cast(*p.scene().camera);
+      })
+      .def_property_readonly("lights", [](const SceneParser& p) { return p.scene().lights; })
+      .def_property_readonly("shapes", [](const SceneParser& p) { return p.scene().shapes; })
+      .def_property_readonly("materials", [](const SceneParser& p) { return p.scene().materials; })
+      .def_property_readonly("transforms", [](const SceneParser& p) { return p.scene().transforms; })
+      .def("build_world", &SceneParser::build_world)
+      .def("render", [](const SceneParser& p, unsigned max_depth) {
+        rt_stats st{};
+        Canvas* out;
+        {
+          py::gil_scoped_release nogil;
+          out = new Canvas(p.render(max_depth, &st));
+        }
+        return py::make_tuple(std::unique_ptr<Canvas>(out), stats_dict(st));
+      }, py::arg("max_depth") = 5)
+      .def("render_to", &SceneParser::render_to, py::arg("path"), py::arg("max_depth") = 5);
   m.def("_wf_profile", [](const World& w, int enable, bool read) {
     double o[16] = {0};
     check(rtamd_wf_profile(w.scene(), enable, read ? o : nullptr), "wf_profile");

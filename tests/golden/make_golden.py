@@ -41,6 +41,9 @@ CASES = [
     ("zoo_64x48", "zoo", {"width": 64, "height": 48}),
     ("first_scene_96x54", "first_scene", {"width": 96, "height": 54}),
     ("solids_64x48", "solids", {"width": 64, "height": 48}),
+    # YAML scenes through rtamd.SceneParser (scene-parser/examples, camera resized)
+    ("yaml_reflect_refract_128x72", "yaml", {"file": "reflect-refract.yml", "width": 128, "height": 72}),
+    ("yaml_cover_80x80", "yaml", {"file": "cover.yml", "width": 80, "height": 80}),
     # render_multithreaded with AA (camera.rs:150-214)
     ("first_scene_48x27_aa4", "first_scene", {"width": 48, "height": 27}, 4),
     ("solids_40x30_aa16", "solids", {"width": 40, "height": 30}, 16),
