@@ -46,9 +46,11 @@ PEAK_F64_VALU_TFLOPS = 39.3  # 256 CU x 64 f64 lanes/clk x 2.4 GHz, non-fused ad
 #   sphere test, general inverse:   33 (object-space ray) + 5 + 5 + 6 + 3 = 52
 #   roots when disc >= 0:            sqrt + 2 add + 2 div, priced 5
 #   plane test:                      6 (o'.y) + 5 (d'.y) + 1 (|d'.y| compare) = 12
+#   BVH child-box slab test:         6 sub + 6 mul + 8 min/max = 20
 OPS_SPHERE_DIAG, OPS_SPHERE_PRIMARY, OPS_SPHERE_GEN = 28, 16, 52
 OPS_ROOTS = 5
 OPS_PLANE = 12
+OPS_BOX = 20
 # SURVEY.md §8(d) convention (the reference's general 4x4 path): 57 / 34 / +6
 SURVEY_OPS_SPHERE, SURVEY_OPS_PLANE, SURVEY_OPS_ROOTS = 57, 34, 6
 
@@ -65,6 +67,8 @@ def parse():
     p.add_argument("--row-block", type=int, default=8)
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget for the CPU baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--exhaustive", action="store_true",
+                   help="disable the exact-culling BVH: every ray tests every shape (the reference's loop)")
     p.add_argument("--pmc-summary", default=os.path.join(REPO, "profiles", "r01_pmc_summary.json"),
                    help="HBM traffic per launch measured by rocprofv3 --pmc for this workload")
     return p.parse_args()
@@ -120,6 +124,8 @@ def main():
     if a.depth != depth:
         depth = a.depth
     world.upload(local_rank)  # flatten + upload: outside the timed region
+    if a.exhaustive:
+        rtamd._rtamd._tuning_set("accel", 0)
     W, H, B = cam.hsize, cam.vsize, a.row_block
     fa = FrameAssembler(H, W, B, rank, n, dev)  # interleaved row blocks + one RCCL gather
     assert len(fa.rows) == rtamd.shard_rows(H, B, rank, n)
@@ -139,6 +145,10 @@ def main():
     if n > 1:
         dist.all_reduce(counts)
     rays_per_frame = float(counts[:4].sum())
+    # SURVEY §8(d) reference work F of one frame (the reference's exhaustive general-4x4
+    # loop): 57 per sphere test, 34 per plane test, +6 per disc >= 0 (exact counters)
+    ref_work = (SURVEY_OPS_SPHERE * float(counts[4]) + SURVEY_OPS_PLANE * float(counts[5])
+                + SURVEY_OPS_ROOTS * float(counts[6]))
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
@@ -186,7 +196,7 @@ def main():
                 "parallelism": f"{n} GPUs, one process each: interleaved {B}-row blocks, RCCL gather to rank 0"
                                if n > 1 else "1 GPU: wavefront pipeline",
             },
-            "roofline": roofline(prof, W, H, a, n),
+            "roofline": roofline(prof, W, H, a, n, ref_work, elapsed / a.steps * 1e3),
         }
         if n == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(world, cam, depth, a.cpu_seconds)
@@ -195,18 +205,23 @@ def main():
         dist.destroy_process_group()
 
 
-def roofline(prof, W, H, a, n):
+def roofline(prof, W, H, a, n, ref_work, frame_ms):
     """f64 VALU roofline of the dominant trace-kernel class (its launches in
     one frame on rank 0), from the library's HIP events over the timed region."""
     nd, ng, npl = prof["n_diag"], prof["n_gen"], prof["n_planes"]
-    per_ray = {"primary": OPS_SPHERE_PRIMARY * nd + OPS_SPHERE_GEN * ng + OPS_PLANE * npl,
-               "closest": OPS_SPHERE_DIAG * nd + OPS_SPHERE_GEN * ng + OPS_PLANE * npl,
-               "shadow": OPS_SPHERE_DIAG * nd + OPS_SPHERE_GEN * ng + OPS_PLANE * npl}
+    per_sphere = {"primary": OPS_SPHERE_PRIMARY, "closest": OPS_SPHERE_DIAG, "shadow": OPS_SPHERE_DIAG}
+
+    def class_ops(c):
+        # executed work: diag-sphere tests (every sphere per ray when exhaustive, the
+        # visited leaves' spheres under the BVH), child-box tests, the rest exhaustively
+        return (prof["tests"][c] * per_sphere[c] + OPS_BOX * prof["boxes"][c]
+                + prof["rays"][c] * (OPS_SPHERE_GEN * ng + OPS_PLANE * npl) + OPS_ROOTS * prof["disc"][c])
     kernels = {}
     for c in ("primary", "closest", "shadow"):
         ms_c = prof["ms"][c]
-        ops_c = prof["rays"][c] * per_ray[c] + OPS_ROOTS * prof["disc"][c]
+        ops_c = class_ops(c)
         kernels[c] = {"ms_per_frame": round(ms_c, 4), "rays": int(prof["rays"][c]),
+                      "sphere_tests": int(prof["tests"][c]), "box_tests": int(prof["boxes"][c]),
                       "tflops": round(ops_c / (ms_c * 1e-3) / 1e12, 3) if ms_c > 0 else None}
     for c in ("prep", "combine"):
         kernels[c] = {"ms_per_frame": round(prof["ms"][c], 4)}
@@ -215,10 +230,8 @@ def roofline(prof, W, H, a, n):
     if kernel_ms <= 0:  # megakernel variant selected (RTAMD_WAVES=1): no per-class events
         return {"bound": "valu_f64", "kernel": None, "achieved": None, "peak": PEAK_F64_VALU_TFLOPS,
                 "unit": "TFLOP/s", "frac": None, "traffic": None}
-    ops = prof["rays"][dom] * per_ray[dom] + OPS_ROOTS * prof["disc"][dom]
+    ops = class_ops(dom)
     achieved = ops / (kernel_ms * 1e-3) / 1e12
-    survey_ops = (SURVEY_OPS_SPHERE * (nd + ng) + SURVEY_OPS_PLANE * npl) * prof["rays"][dom] + \
-        SURVEY_OPS_ROOTS * prof["disc"][dom]
     traffic, traffic_src = None, None
     if os.path.exists(a.pmc_summary):
         try:
@@ -239,8 +252,10 @@ def roofline(prof, W, H, a, n):
         "kernel_ms": round(kernel_ms, 4),
         "ops_per_frame": ops,
         "per_unit": f"{OPS_SPHERE_DIAG} f64 ops per sphere test ({OPS_SPHERE_PRIMARY} for primary rays), "
-                    f"{OPS_PLANE} per plane test, {OPS_ROOTS} per root pair (DESIGN.md 'Roofline')",
-        "survey_convention_tflops": round(survey_ops / (kernel_ms * 1e-3) / 1e12, 3),
+                    f"{OPS_BOX} per BVH box test, {OPS_PLANE} per plane test, {OPS_ROOTS} per root pair "
+                    f"(DESIGN.md 'Roofline'); executed tests counted on the device",
+        "traversal": "bvh" if prof["bvh"] else "exhaustive",
+        "reference_work_tflops": round(ref_work / (frame_ms * 1e-3) / 1e12, 3),
         "traffic_source": traffic_src,
         "kernels": kernels,
     }

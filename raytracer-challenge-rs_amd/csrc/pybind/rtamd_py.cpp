@@ -38,7 +38,7 @@ static py::array_t<double> check_rays(py::array_t<double, py::array::c_style | p
 }
 
 extern "C" int rtamd_tuning_set(const char* key, int value);
-extern "C" int rtamd_wf_profile(const rt_scene* s, int enable, double out[16]);
+extern "C" int rtamd_wf_profile(const rt_scene* s, int enable, double out[24]);
 
 PYBIND11_MODULE(_rtamd, m) {
   m.doc() = "MI355X-native render path of raytracer-challenge-rs (host API over the C-ABI)";
@@ -262,17 +262,18 @@ PYBIND11_MODULE(_rtamd, m) {
         return pod_bytes(l.data(), l.size() * sizeof(rt_light_desc));
       })
       .def("color_at_batch", [](const World& w, py::array_t<double, py::array::c_style | py::array::forcecast> rays,
-                                unsigned remaining) {
+                                unsigned remaining, bool want_stats) {
         check_rays(rays, 6);
         const size_t n = (size_t)rays.shape(0);
         py::array_t<double> out({(py::ssize_t)n, (py::ssize_t)3});
         rt_stats st{};
         {
           py::gil_scoped_release nogil;
-          check(rt_color_at_batch(w.scene(), rays.data(), n, remaining, out.mutable_data(), &st), "rt_color_at_batch");
+          check(rt_color_at_batch(w.scene(), rays.data(), n, remaining, out.mutable_data(), want_stats ? &st : nullptr),
+                "rt_color_at_batch");
         }
         return py::make_tuple(out, stats_dict(st));
-      }, py::arg("rays"), py::arg("remaining") = 5)
+      }, py::arg("rays"), py::arg("remaining") = 5, py::arg("want_stats") = true)
       .def("hit_batch", [](const World& w, py::array_t<double, py::array::c_style | py::array::forcecast> rays) {
         check_rays(rays, 6);
         const size_t n = (size_t)rays.shape(0);
@@ -299,25 +300,26 @@ PYBIND11_MODULE(_rtamd, m) {
       .def_property_readonly("field_of_view", &Camera::field_of_view)
       .def("ray_for_pixel", &Camera::ray_for_pixel)
       .def("desc_bytes", [](const Camera& c) { return pod_bytes(&c.desc(), sizeof(rt_camera_desc)); })
-      .def("render", [](const Camera& c, const World& w, unsigned max_depth) {
+      // want_stats: exact (exhaustive) counters; False runs the fast path (BVH traversal)
+      .def("render", [](const Camera& c, const World& w, unsigned max_depth, bool want_stats) {
         rt_stats st{};
         Canvas* out;
         {
           py::gil_scoped_release nogil;
-          out = new Canvas(c.render(w, max_depth, &st));
+          out = new Canvas(c.render(w, max_depth, want_stats ? &st : nullptr));
         }
         return py::make_tuple(std::unique_ptr<Canvas>(out), stats_dict(st));
-      }, py::arg("world"), py::arg("max_depth") = 5)
+      }, py::arg("world"), py::arg("max_depth") = 5, py::arg("want_stats") = true)
       .def_readwrite("render_opts", &Camera::render_opts, py::return_value_policy::reference_internal)
-      .def("render_multithreaded", [](const Camera& c, const World& w, unsigned max_depth) {
+      .def("render_multithreaded", [](const Camera& c, const World& w, unsigned max_depth, bool want_stats) {
         rt_stats st{};
         Canvas* out;
         {
           py::gil_scoped_release nogil;
-          out = new Canvas(c.render_multithreaded(w, max_depth, &st));
+          out = new Canvas(c.render_multithreaded(w, max_depth, want_stats ? &st : nullptr));
         }
         return py::make_tuple(std::unique_ptr<Canvas>(out), stats_dict(st));
-      }, py::arg("world"), py::arg("max_depth") = 5)
+      }, py::arg("world"), py::arg("max_depth") = 5, py::arg("want_stats") = true)
       .def("render_shard_device", [](const Camera& c, const World& w, unsigned max_depth, unsigned row_block,
                                      unsigned shard, unsigned n_shards, uintptr_t d_out, uintptr_t stream,
                                      bool want_stats, unsigned aa_samples) {
@@ -377,7 +379,7 @@ PYBIND11_MODULE(_rtamd, m) {
       }, py::arg("max_depth") = 5)
       .def("render_to", &SceneParser::render_to, py::arg("path"), py::arg("max_depth") = 5);
   m.def("_wf_profile", [](const World& w, int enable, bool read) {
-    double o[16] = {0};
+    double o[24] = {0};
     check(rtamd_wf_profile(w.scene(), enable, read ? o : nullptr), "wf_profile");
     py::dict d;
     if (read) {
@@ -387,6 +389,10 @@ PYBIND11_MODULE(_rtamd, m) {
       for (int i = 0; i < 3; ++i) { rays[cls[i]] = o[5 + i]; disc[cls[i]] = o[8 + i]; }
       d["ms"] = ms; d["rays"] = rays; d["disc"] = disc;
       d["n_diag"] = o[11]; d["n_gen"] = o[12]; d["n_planes"] = o[13]; d["n_lights"] = o[14];
+      d["n_quads"] = o[15];
+      py::dict tests, boxes;
+      for (int i = 0; i < 3; ++i) { tests[cls[i]] = o[16 + i]; boxes[cls[i]] = o[19 + i]; }
+      d["tests"] = tests; d["boxes"] = boxes; d["bvh"] = (bool)o[22]; d["n_bvh_nodes"] = o[23];
     }
     return d;
   }, py::arg("world"), py::arg("enable") = -1, py::arg("read") = true);

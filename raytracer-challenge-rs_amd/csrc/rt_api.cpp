@@ -19,6 +19,7 @@
 
 #include "../../include/rt_render.h"
 #include "host/rt_math.hpp"
+#include "rt_bvh.hpp"
 #include "rt_kernels.hpp"
 #include "rt_layout.hpp"
 #include "rt_wavefront.hpp"
@@ -28,6 +29,7 @@ using namespace rtamd;
 namespace {
 
 thread_local std::string g_err;
+int g_bvh_leaf = 4;  // BVH leaf size at scene creation (tuning knob "bvh_leaf")
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -188,8 +190,9 @@ const char* rt_last_error(void) { return g_err.c_str(); }
 // Development/benchmark hook (not in the public ABI): per-kernel-class timing
 // of the wavefront pipeline. enable: 1 = on, 0 = off, -1 = just read. out[16]:
 // ms[5] (primary, closest, shadow, prep, combine), rays[3], disc[3],
-// n_diag, n_gen, n_planes, n_lights, n_quads.
-int rtamd_wf_profile(const rt_scene* cs, int enable, double out[16]) {
+// n_diag, n_gen, n_planes, n_lights, n_quads, tests[3], boxes[3], bvh,
+// n_bvh_nodes.
+int rtamd_wf_profile(const rt_scene* cs, int enable, double out[24]) {
   if (!cs) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
   rt_scene* s = const_cast<rt_scene*>(cs);
   std::lock_guard<std::mutex> lk(s->mu);
@@ -202,12 +205,27 @@ int rtamd_wf_profile(const rt_scene* cs, int enable, double out[16]) {
     for (int i = 0; i < 3; ++i) { out[5 + i] = p.rays[i]; out[8 + i] = p.disc[i]; }
     out[11] = s->dev.n_diag; out[12] = s->dev.n_gen; out[13] = s->dev.n_planes;
     out[14] = s->dev.n_lights; out[15] = s->dev.n_quads;
+    for (int i = 0; i < 3; ++i) {
+      out[16 + i] = p.bvh ? p.tests[i] : p.rays[i] * s->dev.n_diag;  // exhaustive: every ray tests every sphere
+      out[19 + i] = p.boxes[i];
+    }
+    out[22] = p.bvh;
+    out[23] = s->dev.n_bvh;
   }
   return RT_OK;
 }
 
 // Development-only tuning hook (not declared in include/rt_render.h).
 int rtamd_tuning_set(const char* key, int value) {
+  if (key && std::strcmp(key, "accel") == 0) {
+    rtamd::g_wf_accel = value != 0;
+    return RT_OK;
+  }
+  if (key && std::strcmp(key, "bvh_leaf") == 0) {
+    if (value < 1 || value > kBvhLeafMax) return fail(RT_ERR_INVALID_ARGUMENT, "bvh_leaf must be in [1, 127]");
+    g_bvh_leaf = value;
+    return RT_OK;
+  }
   if (key && std::strcmp(key, "wf_waves") == 0) {
     if (value != 4 && value != 8) return fail(RT_ERR_INVALID_ARGUMENT, "wf_waves must be 4 or 8");
     rtamd::g_wf_trace_waves = value;
@@ -336,6 +354,9 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
     s.minimum = d.minimum;
     s.maximum = d.maximum;
   }
+  // exact-culling hierarchy over the diagonal spheres (reorders `diag`; keys
+  // come from `meta`, so the order changes no result)
+  std::vector<BvhNode> bvh = build_sphere_bvh(diag, g_bvh_leaf);
   std::vector<LightRec> lrec(n_lights);
   for (size_t i = 0; i < n_lights; ++i)
     for (int c = 0; c < 3; ++c) { lrec[i].pos[c] = lights[i].position[c]; lrec[i].intensity[c] = lights[i].intensity[c]; }
@@ -347,7 +368,8 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   const size_t o_gen = align(o_diag + (diag.size() + 1) * sizeof(SphereDiag));
   const size_t o_pl = align(o_gen + (gen.size() + 1) * sizeof(SphereGen));
   const size_t o_qd = align(o_pl + (planes.size() + 1) * sizeof(PlaneRec));
-  const size_t o_sh = align(o_qd + (quads.size() + 1) * sizeof(QuadRec));
+  const size_t o_bv = align(o_qd + (quads.size() + 1) * sizeof(QuadRec));
+  const size_t o_sh = align(o_bv + (bvh.size() + 1) * sizeof(BvhNode));
   const size_t o_li = align(o_sh + shade.size() * sizeof(ShadeRec));
   const size_t total = align(o_li + lrec.size() * sizeof(LightRec)) + 256;
   std::vector<unsigned char> host(total, 0);
@@ -355,6 +377,7 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   if (!gen.empty()) std::memcpy(&host[o_gen], gen.data(), gen.size() * sizeof(SphereGen));
   if (!planes.empty()) std::memcpy(&host[o_pl], planes.data(), planes.size() * sizeof(PlaneRec));
   if (!quads.empty()) std::memcpy(&host[o_qd], quads.data(), quads.size() * sizeof(QuadRec));
+  if (!bvh.empty()) std::memcpy(&host[o_bv], bvh.data(), bvh.size() * sizeof(BvhNode));
   if (!shade.empty()) std::memcpy(&host[o_sh], shade.data(), shade.size() * sizeof(ShadeRec));
   if (!lrec.empty()) std::memcpy(&host[o_li], lrec.data(), lrec.size() * sizeof(LightRec));
 
@@ -378,6 +401,8 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   s->dev.sph_gen = (const SphereGen*)(b + o_gen);
   s->dev.planes = (const PlaneRec*)(b + o_pl);
   s->dev.quads = (const QuadRec*)(b + o_qd);
+  s->dev.bvh = bvh.empty() ? nullptr : (const BvhNode*)(b + o_bv);
+  s->dev.n_bvh = (int32_t)bvh.size();
   s->dev.shade = (const ShadeRec*)(b + o_sh);
   s->dev.lights = (const LightRec*)(b + o_li);
   s->dev.n_diag = (int32_t)diag.size();

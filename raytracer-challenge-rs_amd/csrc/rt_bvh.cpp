@@ -1,0 +1,207 @@
+// rt_bvh.cpp — host-side BVH over the SphereDiag records.
+//
+// The reference accelerates only through `Group` (bounding-box early-out,
+// group.rs:50-70) and `Group::divide` (split the children by the halves of
+// the group's box, group.rs:108-188; AABB slab test bounding_box.rs:95-136).
+// This builder plays that role for the flattened world, with two changes
+// that matter on the GPU:
+//   * binned-SAH splits over the sphere centroids (a wave traverses the tree
+//     together, so the cost of a node is the union over 64 rays), and
+//   * every box is padded outward, so the traversal never culls a sphere the
+//     exhaustive loop would have hit: culling is exact by construction
+//     (DESIGN.md "Exact culling").
+#include "rt_bvh.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+
+namespace rtamd {
+namespace {
+
+struct Box {
+  double lo[3] = {INFINITY, INFINITY, INFINITY};
+  double hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  void grow(const Box& b) {
+    for (int a = 0; a < 3; ++a) {
+      lo[a] = std::min(lo[a], b.lo[a]);
+      hi[a] = std::max(hi[a], b.hi[a]);
+    }
+  }
+  void grow(const double* p) {
+    for (int a = 0; a < 3; ++a) {
+      lo[a] = std::min(lo[a], p[a]);
+      hi[a] = std::max(hi[a], p[a]);
+    }
+  }
+  double area() const {
+    const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+    if (!(dx >= 0 && dy >= 0 && dz >= 0)) return 0.0;
+    return 2.0 * (dx * dy + dy * dz + dz * dx);
+  }
+};
+
+// World-space extent of the record's unit sphere: the stored inverse maps
+// p -> s*p + t per axis, and |s*p + t| <= 1 means p in [(-1-t)/s, (1-t)/s].
+// Padded by 1e-6 of the box's size and position (far above the rounding of
+// any root computed from the record).
+Box sphere_box(const SphereDiag& r) {
+  Box b;
+  for (int a = 0; a < 3; ++a) {
+    const double p0 = (-1.0 - r.t[a]) / r.s[a];
+    const double p1 = (1.0 - r.t[a]) / r.s[a];
+    double lo = std::min(p0, p1), hi = std::max(p0, p1);
+    const double pad = 1e-6 * ((hi - lo) + std::fabs(lo) + std::fabs(hi)) + 1e-9;
+    b.lo[a] = lo - pad;
+    b.hi[a] = hi + pad;
+  }
+  return b;
+}
+
+struct Builder {
+  std::vector<SphereDiag>& sph;
+  std::vector<Box> box;
+  std::vector<double> cen;  // 3 per sphere
+  std::vector<BvhNode> nodes;
+  int leaf_size;
+
+  static constexpr int kBins = 16;
+
+  // Returns the child code for spheres [b, e) at `depth`.
+  int32_t build(int b, int e, int depth, Box* out_box) {
+    Box bb, cb;
+    for (int i = b; i < e; ++i) {
+      bb.grow(box[i]);
+      cb.grow(&cen[3 * i]);
+    }
+    *out_box = bb;
+    const int n = e - b;
+    if (n <= leaf_size) return leaf(b, n);
+    int axis = 0;
+    double ext = -1;
+    for (int a = 0; a < 3; ++a)
+      if (cb.hi[a] - cb.lo[a] > ext) { ext = cb.hi[a] - cb.lo[a]; axis = a; }
+    int mid = -1;
+    if (ext > 0 && depth < kBvhMaxDepth - 24) {
+      // binned SAH along the widest centroid axis
+      Box bin_box[kBins];
+      int bin_n[kBins] = {0};
+      auto bin_of = [&](int i) {
+        int k = (int)((cen[3 * i + axis] - cb.lo[axis]) / ext * kBins);
+        return std::min(std::max(k, 0), kBins - 1);
+      };
+      for (int i = b; i < e; ++i) {
+        const int k = bin_of(i);
+        ++bin_n[k];
+        bin_box[k].grow(box[i]);
+      }
+      double best = INFINITY;
+      int best_k = -1;
+      for (int k = 1; k < kBins; ++k) {
+        Box l, r;
+        int nl = 0, nr = 0;
+        for (int j = 0; j < k; ++j) { if (bin_n[j]) { l.grow(bin_box[j]); nl += bin_n[j]; } }
+        for (int j = k; j < kBins; ++j) { if (bin_n[j]) { r.grow(bin_box[j]); nr += bin_n[j]; } }
+        if (!nl || !nr) continue;
+        const double c = l.area() * nl + r.area() * nr;
+        if (c < best) { best = c; best_k = k; }
+      }
+      if (best_k > 0) {
+        // leaf if splitting does not pay (traversal cost ~ one sphere test)
+        const double leaf_cost = bb.area() * n;
+        if (n <= kBvhLeafMax && best + bb.area() >= leaf_cost) return leaf(b, n);
+        mid = partition(b, e, [&](int i) { return bin_of(i) < best_k; });
+      }
+    }
+    if (mid <= b || mid >= e) {  // degenerate centroids or depth guard: median split
+      mid = b + n / 2;
+      sort_range(b, e, axis);
+    }
+    const int idx = (int)nodes.size();
+    nodes.emplace_back();
+    nodes[idx].axis = axis;
+    Box lb, rb;
+    const int32_t c0 = build(b, mid, depth + 1, &lb);
+    const int32_t c1 = build(mid, e, depth + 1, &rb);
+    BvhNode& nd = nodes[idx];
+    nd.child[0] = c0;
+    nd.child[1] = c1;
+    for (int a = 0; a < 3; ++a) {
+      nd.lo[0][a] = lb.lo[a]; nd.hi[0][a] = lb.hi[a];
+      nd.lo[1][a] = rb.lo[a]; nd.hi[1][a] = rb.hi[a];
+    }
+    return idx;
+  }
+
+  int32_t leaf(int b, int n) { return -(1 + ((b << 7) | n)); }
+
+  template <typename Pred>
+  int partition(int b, int e, Pred left) {
+    int i = b, j = e - 1;
+    while (true) {
+      while (i <= j && left(i)) ++i;
+      while (i <= j && !left(j)) --j;
+      if (i >= j) break;
+      swap_items(i, j);
+      ++i; --j;
+    }
+    return i;
+  }
+  void sort_range(int b, int e, int axis) {
+    std::vector<int> idx(e - b);
+    for (int i = 0; i < e - b; ++i) idx[i] = b + i;
+    std::sort(idx.begin(), idx.end(), [&](int x, int y) {
+      return cen[3 * x + axis] < cen[3 * y + axis] || (cen[3 * x + axis] == cen[3 * y + axis] && x < y);
+    });
+    std::vector<SphereDiag> s2;
+    std::vector<Box> b2;
+    std::vector<double> c2;
+    for (int i : idx) {
+      s2.push_back(sph[i]);
+      b2.push_back(box[i]);
+      c2.insert(c2.end(), &cen[3 * i], &cen[3 * i] + 3);
+    }
+    for (int i = b; i < e; ++i) {
+      sph[i] = s2[i - b];
+      box[i] = b2[i - b];
+      std::memcpy(&cen[3 * i], &c2[3 * (i - b)], 3 * sizeof(double));
+    }
+  }
+  void swap_items(int i, int j) {
+    std::swap(sph[i], sph[j]);
+    std::swap(box[i], box[j]);
+    for (int a = 0; a < 3; ++a) std::swap(cen[3 * i + a], cen[3 * j + a]);
+  }
+};
+
+}  // namespace
+
+std::vector<BvhNode> build_sphere_bvh(std::vector<SphereDiag>& spheres, int leaf_size) {
+  std::vector<BvhNode> out;
+  const int n = (int)spheres.size();
+  if (n == 0) return out;
+  // the leaf code stores the first index in 24 bits
+  if (n >= (1 << 24)) return out;
+  leaf_size = std::max(1, std::min(leaf_size, kBvhLeafMax));
+  Builder bd{spheres, {}, {}, {}, leaf_size};
+  bd.box.resize(n);
+  bd.cen.resize(3 * n);
+  for (int i = 0; i < n; ++i) {
+    bd.box[i] = sphere_box(spheres[i]);
+    for (int a = 0; a < 3; ++a) bd.cen[3 * i + a] = 0.5 * (bd.box[i].lo[a] + bd.box[i].hi[a]);
+  }
+  bd.nodes.reserve(2 * n / std::max(1, leaf_size) + 2);
+  Box all;
+  const int32_t root = bd.build(0, n, 0, &all);
+  if (root < 0) {  // a single leaf: wrap it in a root node (the traversal starts at node 0)
+    BvhNode r{};
+    r.child[0] = root;
+    r.child[1] = kBvhEmpty;
+    for (int a = 0; a < 3; ++a) { r.lo[0][a] = all.lo[a]; r.hi[0][a] = all.hi[a]; }
+    bd.nodes.assign(1, r);
+  }
+  return bd.nodes;
+}
+
+}  // namespace rtamd

@@ -252,19 +252,12 @@ __device__ __forceinline__ void quad_test(cQuadRec q, V3 o, V3 d, Hit& h) {
   if (!SHADOW && (n_neg & 1)) push_container(h, neg_t, k0 + neg_i);
 }
 
-// Generic trace over the scene's records in global memory (scalar loads):
-// the batch entry points (rt_hit_batch, rt_is_shadowed_batch) and the
-// wavefront fallback when the trace image does not fit in LDS.
-template <bool SHADOW>
-__device__ __forceinline__ void trace(const DevScene& sc, V3 o, V3 d, Hit& h, unsigned& n_disc) {
-  hit_init(h);
-  cSphereDiag sd = (cSphereDiag)sc.sph_diag;
-  for (int j = 0; j < sc.n_diag; ++j) {
-    // off-diagonal inverse entries are exact zeros: ((m00*x + 0) + 0) + m03 == m00*x + m03
-    const double s0 = sd[j].s[0], s1 = sd[j].s[1], s2 = sd[j].s[2];
-    sphere_test<SHADOW>(s0 * o.x + sd[j].t[0], s1 * o.y + sd[j].t[1], s2 * o.z + sd[j].t[2], s0 * d.x, s1 * d.y,
-                        s2 * d.z, [&] { return (int)sd[j].meta; }, h, n_disc);
-  }
+// The records outside the sphere BVH (general-transform spheres, planes,
+// cubes / cylinders / cones), tested exhaustively from global memory.
+// QUADS = false compiles the solids out (kernel variants for scenes without
+// them keep the sphere loops' register allocation, hence their occupancy).
+template <bool SHADOW, bool QUADS = true>
+__device__ __forceinline__ void trace_rest(const DevScene& sc, V3 o, V3 d, Hit& h, unsigned& n_disc) {
   cSphereGen sg = (cSphereGen)sc.sph_gen;
   for (int j = 0; j < sc.n_gen; ++j) {
     double m[12];
@@ -281,8 +274,30 @@ __device__ __forceinline__ void trace(const DevScene& sc, V3 o, V3 d, Hit& h, un
     const double dy = pl[j].m[0] * d.x + pl[j].m[1] * d.y + pl[j].m[2] * d.z;
     plane_test<SHADOW>(oy, dy, (int)pl[j].meta, h);
   }
-  cQuadRec qr = (cQuadRec)sc.quads;
-  for (int j = 0; j < sc.n_quads; ++j) quad_test<SHADOW>(qr + j, o, d, h);
+  if constexpr (QUADS) {
+    cQuadRec qr = (cQuadRec)sc.quads;
+    for (int j = 0; j < sc.n_quads; ++j) quad_test<SHADOW>(qr + j, o, d, h);
+  }
+}
+
+// One diagonal-inverse sphere record (global memory, scalar loads).
+template <bool SHADOW>
+__device__ __forceinline__ void diag_test(cSphereDiag r, V3 o, V3 d, Hit& h, unsigned& n_disc) {
+  // off-diagonal inverse entries are exact zeros: ((m00*x + 0) + 0) + m03 == m00*x + m03
+  const double s0 = r->s[0], s1 = r->s[1], s2 = r->s[2];
+  sphere_test<SHADOW>(s0 * o.x + r->t[0], s1 * o.y + r->t[1], s2 * o.z + r->t[2], s0 * d.x, s1 * d.y, s2 * d.z,
+                      [&] { return (int)r->meta; }, h, n_disc);
+}
+
+// Generic exhaustive trace over the scene's records in global memory (scalar
+// loads): the batch entry points (rt_hit_batch, rt_is_shadowed_batch) and
+// the wavefront fallback when the trace image does not fit in LDS.
+template <bool SHADOW>
+__device__ __forceinline__ void trace(const DevScene& sc, V3 o, V3 d, Hit& h, unsigned& n_disc) {
+  hit_init(h);
+  cSphereDiag sd = (cSphereDiag)sc.sph_diag;
+  for (int j = 0; j < sc.n_diag; ++j) diag_test<SHADOW>(sd + j, o, d, h, n_disc);
+  trace_rest<SHADOW>(sc, o, d, h, n_disc);
   hit_finish(h);
 }
 

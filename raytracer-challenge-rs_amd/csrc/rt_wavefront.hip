@@ -25,6 +25,7 @@ constexpr int kTraceBlock = 1024;  // trace kernels: 16 waves, one LDS image per
 // Occupancy of the trace kernels (min waves per SIMD for the register
 // allocator): 8 = two 1024-thread blocks per CU (<= 64 VGPRs), 4 = one.
 int g_wf_trace_waves = 8;  // tuning knob (rtamd_tuning_set("wf_waves", n))
+int g_wf_accel = 1;        // 1 = BVH traversal when counters are not requested, 0 = exhaustive always
 constexpr int kWfBlock = 256;      // prep / shadow / combine
 
 #define WF_CHECK(x)                        \
@@ -60,13 +61,33 @@ __constant__ double kAaOffsets[31][2] = {
     {0.125, 0.625}, {0.375, 0.625}, {0.625, 0.625}, {0.875, 0.625},
     {0.125, 0.875}, {0.375, 0.875}, {0.625, 0.875}, {0.875, 0.875}};
 
-// Root rays of generation 0: sample `i % aa` of pixel `i / aa` of the shard
+// Generation-0 ray order of a camera shard: the shard's local rows in bands
+// of 8, each band in tiles of 8 columns, AA samples innermost, so one wave
+// holds an 8x8 pixel tile (coherent rays for the BVH traversal). Returns the
+// pixel (x, local row) and the sample index of ray i.
+__device__ __forceinline__ void gen0_pixel(const WfArgs& a, uint32_t hsize, uint32_t i, uint32_t& x, uint32_t& lr,
+                                           uint32_t& smp) {
+  const uint32_t p = i / a.aa;
+  smp = i - p * a.aa;
+  const uint32_t band = p / (8u * hsize);
+  const uint32_t r0 = band * 8u;
+  const uint32_t R = min(8u, a.rows - r0);
+  const uint32_t j = p - band * 8u * hsize;
+  const uint32_t t = j / (8u * R);
+  const uint32_t w = min(8u, hsize - 8u * t);
+  const uint32_t within = j - t * 8u * R;
+  const uint32_t wy = within / w;
+  x = 8u * t + (within - wy * w);
+  lr = r0 + wy;
+}
+
+// Root rays of generation 0: sample `smp` of a pixel of the shard
 // (camera.rs:57-69 / 71-90), or an explicit ray; deeper generations read
 // their queue.
 __device__ __forceinline__ void wf_ray(const WfArgs& a, const DevCamera& cam, unsigned i, V3& o, V3& d) {
   if (a.g == 0 && a.camera_mode) {
-    const uint32_t p = i / a.aa, smp = i - p * a.aa;
-    const uint32_t lr = p / cam.hsize, x = p - lr * cam.hsize;
+    uint32_t x, lr, smp;
+    gen0_pixel(a, cam.hsize, i, x, lr, smp);
     const uint32_t blk = lr / a.row_block, off = lr - blk * a.row_block;
     const uint32_t y = (blk * a.n_shards + a.shard) * a.row_block + off;
     if (a.aa == 1) {
@@ -150,7 +171,7 @@ __device__ WfLds wf_lds_stage(const DevScene& sc, const PrimRec* prim, unsigned 
 // or the shadow-caster variant). Sphere records are read as wave-uniform
 // ds_read_b128 broadcasts with a one-record look-ahead; the image holds zero
 // padding records, so record j+1 always exists.
-template <bool PRIMARY, bool SHADOW>
+template <bool PRIMARY, bool SHADOW, bool QUADS>
 __device__ __forceinline__ void wf_trace_lds(const DevScene& sc, const WfLds& lv, V3 o, V3 d, Hit& h,
                                              unsigned& n_disc) {
   hit_init(h);
@@ -207,13 +228,15 @@ __device__ __forceinline__ void wf_trace_lds(const DevScene& sc, const WfLds& lv
     const double m0 = lv.plane[4 * j], m1 = lv.plane[4 * j + 1], m2 = lv.plane[4 * j + 2], m3 = lv.plane[4 * j + 3];
     plane_test<SHADOW>(m0 * o.x + m1 * o.y + m2 * o.z + m3, m0 * d.x + m1 * d.y + m2 * d.z, lv.plane_meta[j], h);
   }
-  cQuadRec qr = (cQuadRec)sc.quads;  // cubes / cylinders / cones: scalar loads
-  for (int j = 0; j < sc.n_quads; ++j) quad_test<SHADOW>(qr + j, o, d, h);
+  if constexpr (QUADS) {
+    cQuadRec qr = (cQuadRec)sc.quads;  // cubes / cylinders / cones: scalar loads
+    for (int j = 0; j < sc.n_quads; ++j) quad_test<SHADOW>(qr + j, o, d, h);
+  }
   hit_finish(h);
 }
 
 // ---------------------------------------------------------- trace kernels
-template <bool USE_LDS, bool PRIMARY, int TW>
+template <bool USE_LDS, bool PRIMARY, bool QUADS, int TW>
 __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest(DevScene sc, DevCamera cam, WfArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   unsigned n_disc = 0;
@@ -224,7 +247,7 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest(DevScene sc,
     V3 o, d;
     wf_ray(a, cam, i, o, d);
     Hit h;
-    if constexpr (USE_LDS) wf_trace_lds<PRIMARY, false>(sc, lv, o, d, h, n_disc);
+    if constexpr (USE_LDS) wf_trace_lds<PRIMARY, false, QUADS>(sc, lv, o, d, h, n_disc);
     else trace<false>(sc, o, d, h, n_disc);
     WfHit w;
     w.t = h.t; w.key = h.key; w.c1k = h.c1k; w.c2k = h.c2k; w.hin = h.hin;
@@ -238,7 +261,7 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest(DevScene sc,
 // object has a root t with 0 <= t < distance (the first t >= 0 among shadow
 // casters in the sorted list is the minimum one). Full traversal: the exact
 // counters (sphere_disc_ge0) need every test.
-template <bool USE_LDS, int TW>
+template <bool USE_LDS, bool QUADS, int TW>
 __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow(DevScene sc, WfArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   unsigned n_disc = 0;
@@ -250,12 +273,136 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow(DevScene sc, 
     const V3 o = v3(s.o[0], s.o[1], s.o[2]);
     const V3 d = v3(s.d[0], s.d[1], s.d[2]);
     Hit h;
-    if constexpr (USE_LDS) wf_trace_lds<false, true>(sc, lv, o, d, h, n_disc);
+    if constexpr (USE_LDS) wf_trace_lds<false, true, QUADS>(sc, lv, o, d, h, n_disc);
     else trace<true>(sc, o, d, h, n_disc);
     a.sflags[s.slot] = (h.key >= 0 && h.t < s.dist) ? 1 : 0;
   }
   const unsigned long long s = wave_sum(n_disc);
   if (lane_id() == 0 && s) atomicAdd(&a.cnt->disc[a.disc_slot], s);
+}
+
+// ------------------------------------------------------------ BVH traversal
+// Exact culling (DESIGN.md "Exact culling"): the wave traverses the sphere
+// BVH together (wave-uniform stack in LDS, wave-uniform 128-B node loads) and
+// skips a child only when NO lane's ray meets its padded box within
+// [0, t_hi] (t_hi = the lane's current nearest hit, or the light distance for
+// shadow rays). A sphere the exhaustive loop would hit always lies in a box
+// that passes, and the per-lane results are order-independent minima, so the
+// results are bit-identical to the exhaustive loop. Lanes whose rays miss a
+// visited leaf still test its spheres (harmless: exhaustive work).
+typedef const RT_CONST BvhNode* cBvhNode;
+typedef const RT_CONST PrimRec* cPrimRec;
+
+__device__ __forceinline__ double slab_inv(double d) {
+  // 1/d, with a huge finite value for d == 0 (no NaN from 0 * inf)
+  return d == 0.0 ? copysign(1e300, d) : 1.0 / d;
+}
+__device__ __forceinline__ bool slab_hit(const RT_CONST double* lo, const RT_CONST double* hi, V3 o, V3 inv,
+                                         double t_hi) {
+  const double x0 = (lo[0] - o.x) * inv.x, x1 = (hi[0] - o.x) * inv.x;
+  const double y0 = (lo[1] - o.y) * inv.y, y1 = (hi[1] - o.y) * inv.y;
+  const double z0 = (lo[2] - o.z) * inv.z, z1 = (hi[2] - o.z) * inv.z;
+  const double tmin = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmin(z0, z1));
+  const double tmax = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmax(z0, z1));
+  return tmin <= tmax && tmax >= 0.0 && tmin <= t_hi;
+}
+
+template <bool PRIMARY, bool SHADOW>
+__device__ __forceinline__ void bvh_trace(const DevScene& sc, cPrimRec prim, int* stk, V3 o, V3 d, double t_shadow,
+                                          Hit& h, unsigned& n_disc, unsigned& n_tests, unsigned& n_boxes) {
+  hit_init(h);
+  const V3 inv = v3(slab_inv(d.x), slab_inv(d.y), slab_inv(d.z));
+  const cBvhNode nodes = (cBvhNode)sc.bvh;
+  const cSphereDiag sd = (cSphereDiag)sc.sph_diag;
+  int sp = 1;
+  stk[0] = 0;
+  while (sp > 0) {
+    --sp;
+    const int e = __builtin_amdgcn_readfirstlane(stk[sp]);
+    if (e < 0) {  // leaf: first << 7 | count
+      const int code = -(e + 1);
+      const int first = code >> 7, cnt = code & 127;
+      for (int k = first; k < first + cnt; ++k) {
+        if constexpr (PRIMARY) {
+          const cPrimRec r = prim + k;
+          const double dx = r->s[0] * d.x, dy = r->s[1] * d.y, dz = r->s[2] * d.z;
+          sphere_adc<false>(dx * dx + dy * dy + dz * dz, dx * r->op[0] + dy * r->op[1] + dz * r->op[2], r->c,
+                            [&] { return (int)sd[k].meta; }, h, n_disc);
+        } else {
+          diag_test<SHADOW>(sd + k, o, d, h, n_disc);
+        }
+      }
+      n_tests += (unsigned)cnt;
+      if constexpr (SHADOW) {
+        if (!__any(!(h.key >= 0 && h.t < t_shadow))) break;  // every lane is shadowed
+      }
+      continue;
+    }
+    const cBvhNode nd = nodes + e;
+    const double t_hi = SHADOW ? t_shadow : h.t;
+    const int c0 = nd->child[0], c1 = nd->child[1];
+    const bool h0 = slab_hit(nd->lo[0], nd->hi[0], o, inv, t_hi);
+    const bool h1 = c1 != kBvhEmpty && slab_hit(nd->lo[1], nd->hi[1], o, inv, t_hi);
+    n_boxes += 2;
+    const bool any0 = __any(h0), any1 = __any(h1);
+    // push the far child first so the near one (by the lead lane's direction) pops first
+    const int axis = nd->axis;
+    const double dax = axis == 0 ? d.x : axis == 1 ? d.y : d.z;
+    const bool flip = __builtin_amdgcn_readfirstlane(dax < 0.0 ? 1 : 0) != 0;
+    const int near_c = flip ? c1 : c0, far_c = flip ? c0 : c1;
+    const bool near_hit = flip ? any1 : any0, far_hit = flip ? any0 : any1;
+    if (far_hit) stk[sp++] = far_c;
+    if (near_hit) stk[sp++] = near_c;
+  }
+}
+
+template <bool PRIMARY, bool QUADS, int TW>
+__global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest_bvh(DevScene sc, DevCamera cam, WfArgs a) {
+  __shared__ int stack_lds[kTraceBlock / 64][kBvhMaxDepth + 4];
+  int* stk = stack_lds[threadIdx.x / 64];
+  unsigned n_disc = 0, n_tests = 0, n_boxes = 0;
+  const unsigned stride = gridDim.x * blockDim.x;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
+    V3 o, d;
+    wf_ray(a, cam, i, o, d);
+    Hit h;
+    bvh_trace<PRIMARY, false>(sc, (cPrimRec)a.prim, stk, o, d, 0.0, h, n_disc, n_tests, n_boxes);
+    trace_rest<false, QUADS>(sc, o, d, h, n_disc);
+    hit_finish(h);
+    WfHit w;
+    w.t = h.t; w.key = h.key; w.c1k = h.c1k; w.c2k = h.c2k; w.hin = h.hin;
+    a.hits[i] = w;
+  }
+  const unsigned long long s = wave_sum(n_disc), st = wave_sum(n_tests), sb = wave_sum(n_boxes);
+  if (lane_id() == 0) {
+    if (s) atomicAdd(&a.cnt->disc[a.disc_slot], s);
+    if (st) atomicAdd(&a.cnt->tests[a.disc_slot], st);
+    if (sb) atomicAdd(&a.cnt->boxes[a.disc_slot], sb);
+  }
+}
+
+template <bool QUADS, int TW>
+__global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow_bvh(DevScene sc, WfArgs a) {
+  __shared__ int stack_lds[kTraceBlock / 64][kBvhMaxDepth + 4];
+  int* stk = stack_lds[threadIdx.x / 64];
+  unsigned n_disc = 0, n_tests = 0, n_boxes = 0;
+  const unsigned stride = gridDim.x * blockDim.x;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n_shadow; i += stride) {
+    const WfShadow s = a.shadows[i];
+    const V3 o = v3(s.o[0], s.o[1], s.o[2]);
+    const V3 d = v3(s.d[0], s.d[1], s.d[2]);
+    Hit h;
+    bvh_trace<false, true>(sc, nullptr, stk, o, d, s.dist, h, n_disc, n_tests, n_boxes);
+    if (__any(!(h.key >= 0 && h.t < s.dist))) trace_rest<true, QUADS>(sc, o, d, h, n_disc);
+    hit_finish(h);
+    a.sflags[s.slot] = (h.key >= 0 && h.t < s.dist) ? 1 : 0;
+  }
+  const unsigned long long sd = wave_sum(n_disc), st = wave_sum(n_tests), sb = wave_sum(n_boxes);
+  if (lane_id() == 0) {
+    if (sd) atomicAdd(&a.cnt->disc[a.disc_slot], sd);
+    if (st) atomicAdd(&a.cnt->tests[a.disc_slot], st);
+    if (sb) atomicAdd(&a.cnt->boxes[a.disc_slot], sb);
+  }
 }
 
 // ---------------------------------------------------------- prep (spawn)
@@ -383,16 +530,23 @@ __global__ __launch_bounds__(kWfBlock) void wf_combine(DevScene sc, DevCamera ca
         color = vadd(vadd(surface, refl), refr);
       }
     }
-    double* out = a.colors + (size_t)i * 3;
+    size_t oi = i;
+    if (a.g == 0 && a.camera_mode && a.aa == 1) {  // generation 0 is tile-ordered: write row-major
+      uint32_t x, lr, smp;
+      gen0_pixel(a, cam.hsize, i, x, lr, smp);
+      oi = (size_t)lr * cam.hsize + x;
+    }
+    double* out = a.colors + oi * 3;
     out[0] = color.x; out[1] = color.y; out[2] = color.z;
   }
 }
 
 // Color::average (color.rs:26-33) of the AA samples of each pixel: a left
-// fold from black, then * (1 / n).
-__global__ __launch_bounds__(kWfBlock) void wf_average(const double* colors, unsigned n_pix, unsigned aa,
+// fold from black, then * (1 / n); written row-major.
+__global__ __launch_bounds__(kWfBlock) void wf_average(WfArgs a, unsigned hsize, const double* colors, unsigned n_pix,
                                                        double* out) {
   const unsigned stride = gridDim.x * blockDim.x;
+  const unsigned aa = a.aa;
   for (unsigned p = blockIdx.x * blockDim.x + threadIdx.x; p < n_pix; p += stride) {
     V3 sum = v3(0.0, 0.0, 0.0);
     for (unsigned s = 0; s < aa; ++s) {
@@ -400,7 +554,9 @@ __global__ __launch_bounds__(kWfBlock) void wf_average(const double* colors, uns
       sum = vadd(sum, v3(c[0], c[1], c[2]));
     }
     const V3 avg = vscale(sum, 1.0 / (double)aa);
-    double* o = out + (size_t)p * 3;
+    uint32_t x, lr, smp;
+    gen0_pixel(a, hsize, p * aa, x, lr, smp);
+    double* o = out + ((size_t)lr * hsize + x) * 3;
     o[0] = avg.x; o[1] = avg.y; o[2] = avg.z;
   }
 }
@@ -466,7 +622,10 @@ hipError_t Wavefront::last_profile(WfProfile* out) {
   for (int c = 0; c < 3; ++c) {
     out->rays[c] = prof_rays_[c];
     out->disc[c] = (double)hc.disc[c];
+    out->tests[c] = (double)hc.tests[c];
+    out->boxes[c] = (double)hc.boxes[c];
   }
+  out->bvh = last_bvh_ ? 1 : 0;
   return hipSuccess;
 }
 
@@ -526,38 +685,60 @@ static int occupancy_grid(K kern, int block, size_t lds, unsigned n) {
 
 static constexpr size_t kWfLdsLimit = 160 * 1024 - 1024;
 
-template <int TW>
-static hipError_t launch_closest(const DevScene& sc, const DevCamera& cam, const WfArgs& a, bool primary, bool lds_ok,
-                                 unsigned n, hipStream_t stream) {
-  if (primary) {
+template <bool QUADS, int TW>
+static hipError_t launch_closest_q(const DevScene& sc, const DevCamera& cam, const WfArgs& a, bool primary,
+                                   bool lds_ok, bool bvh, unsigned n, hipStream_t stream) {
+  if (bvh) {
+    if (primary) {
+      auto k = wf_trace_closest_bvh<true, QUADS, TW>;
+      hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
+    } else {
+      auto k = wf_trace_closest_bvh<false, QUADS, TW>;
+      hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
+    }
+  } else if (primary) {
     const size_t lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, true);
-    auto k = wf_trace_closest<true, true, TW>;
+    auto k = wf_trace_closest<true, true, QUADS, TW>;
     WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, lds, n)), dim3(kTraceBlock), lds, stream, sc, cam, a);
   } else if (lds_ok) {
     const size_t lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, false);
-    auto k = wf_trace_closest<true, false, TW>;
+    auto k = wf_trace_closest<true, false, QUADS, TW>;
     WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, lds, n)), dim3(kTraceBlock), lds, stream, sc, cam, a);
   } else {
-    auto k = wf_trace_closest<false, false, TW>;
+    auto k = wf_trace_closest<false, false, QUADS, TW>;
     hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
   }
   return hipGetLastError();
 }
-
 template <int TW>
-static hipError_t launch_shadow_wf(const DevScene& sc, const WfArgs& a, bool lds_ok, hipStream_t stream) {
-  if (lds_ok) {
+static hipError_t launch_closest(const DevScene& sc, const DevCamera& cam, const WfArgs& a, bool primary, bool lds_ok,
+                                 bool bvh, unsigned n, hipStream_t stream) {
+  return sc.n_quads > 0 ? launch_closest_q<true, TW>(sc, cam, a, primary, lds_ok, bvh, n, stream)
+                        : launch_closest_q<false, TW>(sc, cam, a, primary, lds_ok, bvh, n, stream);
+}
+
+template <bool QUADS, int TW>
+static hipError_t launch_shadow_q(const DevScene& sc, const WfArgs& a, bool lds_ok, bool bvh, hipStream_t stream) {
+  if (bvh) {
+    auto k = wf_trace_shadow_bvh<QUADS, TW>;
+    hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, 0, a.n_shadow)), dim3(kTraceBlock), 0, stream, sc, a);
+  } else if (lds_ok) {
     const size_t lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, false);
-    auto k = wf_trace_shadow<true, TW>;
+    auto k = wf_trace_shadow<true, QUADS, TW>;
     WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, lds, a.n_shadow)), dim3(kTraceBlock), lds, stream, sc, a);
   } else {
-    auto k = wf_trace_shadow<false, TW>;
+    auto k = wf_trace_shadow<false, QUADS, TW>;
     hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, 0, a.n_shadow)), dim3(kTraceBlock), 0, stream, sc, a);
   }
   return hipGetLastError();
+}
+template <int TW>
+static hipError_t launch_shadow_wf(const DevScene& sc, const WfArgs& a, bool lds_ok, bool bvh, hipStream_t stream) {
+  return sc.n_quads > 0 ? launch_shadow_q<true, TW>(sc, a, lds_ok, bvh, stream)
+                        : launch_shadow_q<false, TW>(sc, a, lds_ok, bvh, stream);
 }
 
 hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool camera_mode, const double* d_in_rays,
@@ -588,7 +769,10 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
   }
   const bool prim_lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, true) <= kWfLdsLimit;
   const bool gen_lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, false) <= kWfLdsLimit;
-  const bool use_prim = camera_mode && prim_lds && sc.n_diag > 0;
+  // BVH traversal unless the exact exhaustive counters are requested
+  const bool bvh = g_wf_accel != 0 && stats == nullptr && sc.n_bvh > 0;
+  last_bvh_ = bvh;
+  const bool use_prim = camera_mode && (prim_lds || bvh) && sc.n_diag > 0;
   if (use_prim) {
     hipLaunchKernelGGL(wf_prim_prep, dim3((sc.n_diag + 4 + 255) / 256), dim3(256), 0, stream, sc, cam, d_prim_);
     WF_CHECK(hipGetLastError());
@@ -610,6 +794,7 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     a.rays = B.rays; a.hits = B.hits; a.nodes = B.nodes; a.shadows = B.shadows; a.sflags = B.sflags;
     a.colors = (g == 0 && !averaged) ? d_out : B.colors;
     a.aa = aa;
+    a.rows = n0 / aa / (cam.hsize ? cam.hsize : 1);
     a.next_rays = gens_[g + 1].rays;
     a.child_colors = gens_[g + 1].colors;
     a.cnt = d_cnt_;
@@ -625,8 +810,8 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     a.disc_slot = (unsigned)ccls;
     prof_rays_[ccls] += n;
     WF_CHECK(pmark(stream, ccls, true));
-    if (g_wf_trace_waves == 4) WF_CHECK(launch_closest<4>(sc, cam, a, prim_launch, gen_lds, n, stream));
-    else WF_CHECK(launch_closest<8>(sc, cam, a, prim_launch, gen_lds, n, stream));
+    if (g_wf_trace_waves == 4) WF_CHECK(launch_closest<4>(sc, cam, a, prim_launch, gen_lds, bvh, n, stream));
+    else WF_CHECK(launch_closest<8>(sc, cam, a, prim_launch, gen_lds, bvh, n, stream));
     WF_CHECK(pmark(stream, ccls, false));
     // 2. prepare_computations + spawn
     WF_CHECK(pmark(stream, WF_PREP, true));
@@ -646,8 +831,8 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
       a.disc_slot = WF_SHADOW;
       prof_rays_[WF_SHADOW] += a.n_shadow;
       WF_CHECK(pmark(stream, WF_SHADOW, true));
-      if (g_wf_trace_waves == 4) WF_CHECK(launch_shadow_wf<4>(sc, a, gen_lds, stream));
-      else WF_CHECK(launch_shadow_wf<8>(sc, a, gen_lds, stream));
+      if (g_wf_trace_waves == 4) WF_CHECK(launch_shadow_wf<4>(sc, a, gen_lds, bvh, stream));
+      else WF_CHECK(launch_shadow_wf<8>(sc, a, gen_lds, bvh, stream));
       WF_CHECK(pmark(stream, WF_SHADOW, false));
     }
     if (stats) {
@@ -662,6 +847,7 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     a.rays = B.rays; a.nodes = B.nodes; a.sflags = B.sflags;
     a.colors = (g == 0 && !averaged) ? d_out : B.colors;
     a.aa = aa;
+    a.rows = n0 / aa / (cam.hsize ? cam.hsize : 1);
     a.child_colors = gens_[g + 1].colors;
     a.n = counts.rays[g];
     a.g = (unsigned)g; a.max_depth = max_depth;
@@ -676,8 +862,10 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
   if (averaged) {
     const unsigned n_pix = n0 / aa;
     WF_CHECK(pmark(stream, WF_COMBINE, true));
+    WfArgs a{};
+    a.aa = aa; a.rows = n_pix / cam.hsize;
     hipLaunchKernelGGL(wf_average, dim3(occupancy_grid(wf_average, kWfBlock, 0, n_pix)), dim3(kWfBlock), 0, stream,
-                       gens_[0].colors, n_pix, aa, d_out);
+                       a, cam.hsize, gens_[0].colors, n_pix, d_out);
     WF_CHECK(hipGetLastError());
     WF_CHECK(pmark(stream, WF_COMBINE, false));
   }

@@ -62,12 +62,15 @@ struct PrimRec {  // primary rays share the origin: per diag sphere (s, o', c)
 
 constexpr int kMaxGen = 66;
 extern int g_wf_trace_waves;  // tuning knob: trace-kernel occupancy (4 or 8 waves/SIMD)
+extern int g_wf_accel;        // tuning knob: 1 = BVH traversal (when no counters are requested), 0 = exhaustive
 
 struct WfCounters {
   unsigned n_rays[kMaxGen];    // appended rays per generation (index g+1 filled by prep(g))
   unsigned n_shadow[kMaxGen];  // shadow rays per generation
   unsigned n_refl[kMaxGen], n_refr[kMaxGen];
   unsigned long long disc[3];  // disc >= 0 tests: [0] primary closest, [1] closest, [2] shadow
+  unsigned long long tests[3];  // BVH mode: sphere tests executed (lanes x spheres), per trace class
+  unsigned long long boxes[3];  // BVH mode: child-box tests executed (lanes x boxes)
 };
 
 struct WfGenBuf {
@@ -100,6 +103,7 @@ struct WfArgs {
   unsigned row_block, shard, n_shards;
   unsigned disc_slot;   // WfCounters::disc index of this trace launch
   unsigned aa;          // AA samples per pixel (generation 0 in camera mode)
+  unsigned rows;        // local rows of the camera shard (generation-0 tiling)
 };
 
 // Per-kernel-class timing of the last frame (profiling mode only).
@@ -108,6 +112,9 @@ struct WfProfile {
   double ms[WF_NCLASS];
   double rays[3];   // rays traced by the three trace classes
   double disc[3];   // disc >= 0 tests per trace class
+  double tests[3];  // sphere tests executed per trace class (exhaustive: rays x n_diag)
+  double boxes[3];  // BVH child-box tests executed per trace class (0 when exhaustive)
+  int bvh;          // the last frame traversed the BVH
 };
 
 class Wavefront {
@@ -143,6 +150,7 @@ class Wavefront {
     std::vector<unsigned> rays, shadows;
   };
   std::map<std::string, Counts> cache_;
+  bool last_bvh_ = false;
   bool profiling_ = false;
   std::vector<hipEvent_t> pev_;        // event pool (pairs)
   std::vector<int> pcls_;              // class of each recorded pair

@@ -1,0 +1,141 @@
+"""Exact culling: the BVH traversal must reproduce the
+exhaustive `World::intersect` bit for bit.
+
+The counted launches (want_stats=True) run the exhaustive loops, whose
+counters equal the oracle's; the fast path (want_stats=False, what bench.py
+and the C++ drop-in run) traverses the sphere BVH. Every comparison here is
+bitwise between the two, plus the oracle on a few frames.
+"""
+import math
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+PI = math.pi
+
+
+def _both(rt, w, cam, depth, aa=1):
+    if aa == 1:
+        fast, _ = cam.render(w, depth, want_stats=False)
+        exact, st = cam.render(w, depth, want_stats=True)
+    else:
+        cam.render_opts.aa_samples(getattr(rt.AASamples, f"X{aa}"))
+        fast, _ = cam.render_multithreaded(w, depth, want_stats=False)
+        exact, st = cam.render_multithreaded(w, depth, want_stats=True)
+    prof = rt._rtamd._wf_profile(w, -1, True)
+    return fast.to_numpy(), exact.to_numpy(), st
+
+
+def _glass_cluster(rt, n=300, seed=7, inside=True):
+    """Overlapping glass and mirror spheres (containers several deep), and a
+    camera that may sit inside one of them."""
+    rng = np.random.default_rng(seed)
+    w = rt.World()
+    floor = rt.Plane()
+    floor.material.reflective = 0.3
+    w.add_object(floor)
+    for i in range(n):
+        s = rt.glass_sphere() if i % 3 else rt.Sphere()
+        r = rng.uniform(0.2, 0.9)
+        c = rng.uniform([-3, r, -3], [3, 3, 3])
+        s.set_transform(rt.translation(*c) * rt.scaling(r, r, r))
+        s.material.refractive_index = 1.0 + rng.uniform(0, 1.5)
+        s.material.reflective = rng.uniform(0, 0.9)
+        s.material.color = rt.Color(*rng.uniform(0, 1, 3))
+        w.add_object(s)
+    w.add_light(rt.PointLight(rt.Point(-10, 10, -10), rt.Color(1, 1, 1)))
+    cam = rt.Camera(96, 64, PI / 2.5)
+    frm = (0.2, 1.1, -0.4) if inside else (0, 2, -9)
+    cam.set_transform(rt.view_transform(rt.Point(*frm), rt.Point(0, 1, 2), rt.Vector(0, 1, 0)))
+    return w, cam, 6
+
+
+SCENES = {
+    "c3_192x108": lambda rt: __import__("rtamd.scenes", fromlist=["c3"]).c3(192, 108),
+    "c3_3000": lambda rt: __import__("rtamd.scenes", fromlist=["c3"]).c3(160, 90, n_spheres=3000, seed=99),
+    "zoo": lambda rt: __import__("rtamd.scenes", fromlist=["zoo"]).zoo(120, 90),
+    "solids": lambda rt: __import__("rtamd.scenes", fromlist=["solids"]).solids(120, 90),
+    "first_scene": lambda rt: __import__("rtamd.scenes", fromlist=["first_scene"]).first_scene(160, 90),
+    "glass_inside": lambda rt: _glass_cluster(rt, inside=True),
+    "glass_outside": lambda rt: _glass_cluster(rt, n=500, seed=3, inside=False),
+}
+
+
+@pytest.mark.parametrize("name", sorted(SCENES))
+def test_bvh_frames_bitwise_equal_exhaustive(rt, name):
+    w, cam, depth = SCENES[name](rt)
+    fast, exact, _ = _both(rt, w, cam, depth)
+    assert rt._rtamd._wf_profile(w, -1, True)["n_bvh_nodes"] > 0
+    assert fast.tobytes() == exact.tobytes()
+
+
+def test_bvh_is_the_fast_path(rt):
+    from rtamd import scenes
+    w, cam, depth = scenes.c3(64, 36, n_spheres=200)
+    rt._rtamd._wf_profile(w, 1, False)
+    cam.render(w, depth, want_stats=False)
+    p = rt._rtamd._wf_profile(w, 0, True)
+    assert p["bvh"] and 0 < p["tests"]["primary"] < p["rays"]["primary"] * 200
+    cam.render(w, depth, want_stats=True)
+    assert not rt._rtamd._wf_profile(w, -1, True)["bvh"]
+
+
+def test_bvh_vs_oracle_c3(rt, oracle):
+    from rtamd import scenes
+    w, cam, depth = scenes.c3(128, 72)
+    fast, _ = cam.render(w, depth, want_stats=False)
+    ref, _ = oracle.OracleWorld.from_world(w).render(cam.desc_bytes(), depth, nthreads=16)
+    g = fast.to_numpy()
+    assert np.abs(g - ref).max() <= 1e-5
+    assert rt.canvas_to_ppm(g) == oracle.canvas_to_ppm(ref)
+
+
+@pytest.mark.parametrize("aa", [4, 16])
+def test_bvh_aa_bitwise(rt, aa):
+    w, cam, depth = _glass_cluster(rt, n=120, seed=11, inside=False)
+    fast, exact, _ = _both(rt, w, cam, depth, aa=aa)
+    assert fast.tobytes() == exact.tobytes()
+
+
+def test_bvh_color_at_batch_random_rays(rt):
+    """Rays from everywhere (inside spheres, grazing, behind) at several depths."""
+    w, _, _ = _glass_cluster(rt, n=400, seed=5)
+    rng = np.random.default_rng(1)
+    o = rng.uniform([-4, -0.5, -4], [4, 4, 4], size=(20000, 3))
+    d = rng.normal(size=(20000, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.hstack([o, d])
+    for depth in (0, 1, 4):
+        fast, _ = w.color_at_batch(rays, depth, want_stats=False)
+        exact, _ = w.color_at_batch(rays, depth, want_stats=True)
+        assert fast.tobytes() == exact.tobytes(), depth
+
+
+def test_bvh_shard_device_bitwise(rt):
+    import torch
+    from rtamd import scenes
+    w, cam, depth = scenes.c3(200, 120, n_spheres=700)
+    full, _ = cam.render(w, depth, want_stats=True)
+    full = full.to_numpy()
+    out = np.zeros_like(full)
+    for s in range(3):
+        rows = rt.shard_rows(cam.vsize, 8, s, 3)
+        buf = torch.empty((rows, cam.hsize, 3), dtype=torch.float64, device="cuda")
+        cam.render_shard_device(w, depth, 8, s, 3, buf.data_ptr(), torch.cuda.current_stream().cuda_stream, False)
+        torch.cuda.synchronize()
+        out[[y for y in range(cam.vsize) if (y // 8) % 3 == s]] = buf.cpu().numpy()
+    assert out.tobytes() == full.tobytes()
+
+
+def test_accel_knob_off_matches(rt):
+    from rtamd import scenes
+    w, cam, depth = scenes.zoo(80, 60)
+    a, _ = cam.render(w, depth, want_stats=False)
+    rt._rtamd._tuning_set("accel", 0)
+    try:
+        b, _ = cam.render(w, depth, want_stats=False)
+        assert not rt._rtamd._wf_profile(w, -1, True)["bvh"]
+    finally:
+        rt._rtamd._tuning_set("accel", 1)
+    assert a.to_numpy().tobytes() == b.to_numpy().tobytes()
