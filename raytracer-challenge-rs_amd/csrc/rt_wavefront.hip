@@ -81,6 +81,44 @@ __device__ __forceinline__ void gen0_pixel(const WfArgs& a, uint32_t hsize, uint
   lr = r0 + wy;
 }
 
+// Block-aggregated queue appends for wf_prep (one atomic per counter per
+// block instead of per wave: the counters are single hot addresses).
+// Called by every thread of the block (it synchronises). Lanes with want_s
+// get `per_s` consecutive shadow slots, lanes with want_r / want_f one ray
+// slot each in the next generation (reflected rays of the block first).
+__device__ __forceinline__ void block_append(unsigned* shadow_ctr, unsigned per_s, bool want_s, unsigned* ray_ctr,
+                                             bool want_r, bool want_f, unsigned& so, unsigned& ro, unsigned& fo) {
+  __shared__ unsigned s_cnt[kWfBlock / 64][3];
+  __shared__ unsigned s_base[3];
+  const unsigned lane = lane_id(), wave = threadIdx.x / 64;
+  const unsigned long long ms = __ballot(want_s), mr = __ballot(want_r), mf = __ballot(want_f);
+  const unsigned long long below = (1ull << lane) - 1ull;
+  if (lane == 0) {
+    s_cnt[wave][0] = (unsigned)__popcll(ms) * per_s;
+    s_cnt[wave][1] = (unsigned)__popcll(mr);
+    s_cnt[wave][2] = (unsigned)__popcll(mf);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned t[3] = {0, 0, 0};
+    for (unsigned w = 0; w < kWfBlock / 64; ++w)
+      for (int k = 0; k < 3; ++k) {
+        const unsigned c = s_cnt[w][k];
+        s_cnt[w][k] = t[k];  // exclusive prefix over the block's waves
+        t[k] += c;
+      }
+    s_base[0] = t[0] ? atomicAdd(shadow_ctr, t[0]) : 0u;
+    const unsigned rb = (t[1] + t[2]) ? atomicAdd(ray_ctr, t[1] + t[2]) : 0u;
+    s_base[1] = rb;
+    s_base[2] = rb + t[1];
+  }
+  __syncthreads();
+  so = s_base[0] + s_cnt[wave][0] + (unsigned)__popcll(ms & below) * per_s;
+  ro = s_base[1] + s_cnt[wave][1] + (unsigned)__popcll(mr & below);
+  fo = s_base[2] + s_cnt[wave][2] + (unsigned)__popcll(mf & below);
+  __syncthreads();  // s_cnt / s_base are reused by the next call
+}
+
 // Root rays of generation 0: sample `smp` of a pixel of the shard
 // (camera.rs:57-69 / 71-90), or an explicit ray; deeper generations read
 // their queue.
@@ -446,18 +484,18 @@ __global__ __launch_bounds__(kWfBlock) void wf_prep(DevScene sc, DevCamera cam, 
       }
     }
     // shadow rays: one per light, in light order (world.rs:41-56)
-    const unsigned sbase = wave_append(&a.cnt->n_shadow[a.g], hit && L > 0, L);
-    const unsigned rbase = wave_append(&a.cnt->n_rays[a.g + 1], want_refl, 1);
-    const unsigned fbase = wave_append(&a.cnt->n_rays[a.g + 1], want_refr, 1);
+    unsigned sbase, rbase, fbase;
+    block_append(&a.cnt->n_shadow[a.g], L, hit && L > 0, &a.cnt->n_rays[a.g + 1], want_refl, want_refr, sbase, rbase,
+                 fbase);
     if (!valid) continue;
     WfNode nd;
     nd.obj = -1; nd.child_refl = -1; nd.child_refr = -1; nd.pad = 0;
     if (hit) {
       nd.obj = c.obj;
       nd.over[0] = c.over.x; nd.over[1] = c.over.y; nd.over[2] = c.over.z;
-      nd.under[0] = c.under.x; nd.under[1] = c.under.y; nd.under[2] = c.under.z;
       nd.normal[0] = c.normal.x; nd.normal[1] = c.normal.y; nd.normal[2] = c.normal.z;
-      nd.n1 = c.n1; nd.n2 = c.n2;
+      // shade_hit's Schlick factor (world.rs:62-64), same inputs as the reference's call
+      nd.schlick = (m->reflective > 0.0 && m->transparency > 0.0) ? schlick(c.eyev, c.normal, c.n1, c.n2) : 0.0;
       for (unsigned l = 0; l < L; ++l) {
         cLightRec Lr = lights + l;
         const V3 v = vsub(v3(Lr->pos[0], Lr->pos[1], Lr->pos[2]), c.over);
@@ -524,7 +562,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_combine(DevScene sc, DevCamera ca
         refr = vscale(v3(cc[0], cc[1], cc[2]), m.transparency);  // world.rs:133
       }
       if (m.reflective > 0.0 && m.transparency > 0.0) {
-        const double r = schlick(eyev, normal, nd.n1, nd.n2);
+        const double r = nd.schlick;
         color = vadd(vadd(surface, vscale(refl, r)), vscale(refr, 1.0 - r));
       } else {
         color = vadd(vadd(surface, refl), refr);

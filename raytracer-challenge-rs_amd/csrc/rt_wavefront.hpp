@@ -38,9 +38,9 @@ struct WfHit {  // 24 B: nearest hit + containers top-2 (rt_device.hpp Hit)
   double t;
   int32_t key, c1k, c2k, hin;
 };
-struct WfNode {  // prepare_computations results needed by combine
-  double over[3], under[3], normal[3];
-  double n1, n2;
+struct WfNode {  // 72 B: what shade_hit needs from prepare_computations
+  double over[3], normal[3];
+  double schlick;      // Computations::schlick (only read when reflective && transparent)
   int32_t obj;         // -1 = miss
   int32_t child_refl;  // index into rays_{g+1}, -1 = none (black)
   int32_t child_refr;

@@ -4,11 +4,11 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 TAG=${1:-r01}; shift
-ARGS="--steps 3 --warmup 1 --no-cpu-baseline $*"
+ARGS="--frames 5 $*"
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-run() { name=$1; shift; timeout -k 10 300 rocprofv3 "$@" -d $OUT/$name -o $name --output-format csv -- python bench.py $ARGS > $OUT/$name.log 2>&1; rc=$?; echo "$name rc=$rc" | tee -a $OUT/steps.log; return $rc; }
+run() { name=$1; shift; timeout -k 10 300 rocprofv3 "$@" -d $OUT/$name -o $name --output-format csv -- python tools/prof_frames.py $ARGS > $OUT/$name.log 2>&1; rc=$?; echo "$name rc=$rc" | tee -a $OUT/steps.log; return $rc; }
 run kt --kernel-trace --stats && \
 run p1 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE && \
 run p2 --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_INSTS_VMEM && \

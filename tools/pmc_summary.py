@@ -13,21 +13,26 @@ an upper estimate; WRITE_SIZE (KiB) is exact for 16-B stores.
 """
 import argparse, collections, csv, glob, json
 
-CLASSES = [  # (class, predicate on the demangled kernel name)
-    ("primary", lambda n: "wf_trace_closest<" in n and ", true," in n),
-    ("closest", lambda n: "wf_trace_closest<" in n and ", false," in n),
-    ("shadow", lambda n: "wf_trace_shadow<" in n),
-    ("prep", lambda n: "wf_prep(" in n),
-    ("combine", lambda n: "wf_combine(" in n),
-    ("megakernel", lambda n: "render_kernel<" in n),
-    ("frame", lambda n: "wf_prim_prep(" in n),
-]
+def _targs(n, name):
+    i = n.index(name + "<") + len(name) + 1
+    return [t.strip() for t in n[i:n.index(">", i)].split(",")]
 
 
-def klass(name):
-    for c, f in CLASSES:
-        if f(name):
-            return c
+def klass(n):
+    """Kernel class of a demangled name: primary / closest / shadow / prep /
+    combine / frame (wf_prim_prep: one per rendered frame)."""
+    if "wf_trace_closest_bvh<" in n:
+        return "primary" if _targs(n, "wf_trace_closest_bvh")[0] == "true" else "closest"
+    if "wf_trace_closest<" in n:
+        return "primary" if _targs(n, "wf_trace_closest")[1] == "true" else "closest"
+    if "wf_trace_shadow" in n:
+        return "shadow"
+    if "wf_prep(" in n:
+        return "prep"
+    if "wf_combine(" in n or "wf_average(" in n:
+        return "combine"
+    if "wf_prim_prep(" in n:
+        return "frame"
     return None
 
 
