@@ -191,8 +191,8 @@ const char* rt_last_error(void) { return g_err.c_str(); }
 // of the wavefront pipeline. enable: 1 = on, 0 = off, -1 = just read. out[16]:
 // ms[5] (primary, closest, shadow, prep, combine), rays[3], disc[3],
 // n_diag, n_gen, n_planes, n_lights, n_quads, tests[3], boxes[3], bvh,
-// n_bvh_nodes.
-int rtamd_wf_profile(const rt_scene* cs, int enable, double out[24]) {
+// n_bvh_nodes, bvh_depth.
+int rtamd_wf_profile(const rt_scene* cs, int enable, double out[25]) {
   if (!cs) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
   rt_scene* s = const_cast<rt_scene*>(cs);
   std::lock_guard<std::mutex> lk(s->mu);
@@ -211,12 +211,25 @@ int rtamd_wf_profile(const rt_scene* cs, int enable, double out[24]) {
     }
     out[22] = p.bvh;
     out[23] = s->dev.n_bvh;
+    out[24] = s->dev.bvh_depth;
   }
   return RT_OK;
 }
 
 // Development-only tuning hook (not declared in include/rt_render.h).
 int rtamd_tuning_set(const char* key, int value) {
+  int* tw = !key ? nullptr : std::strcmp(key, "tw_primary") == 0 ? &rtamd::g_tw_primary
+                           : std::strcmp(key, "tw_closest") == 0 ? &rtamd::g_tw_closest
+                           : std::strcmp(key, "tw_shadow") == 0  ? &rtamd::g_tw_shadow : nullptr;
+  if (tw) {
+    if (value != 4 && value != 5 && value != 6 && value != 8) return fail(RT_ERR_INVALID_ARGUMENT, "waves must be 4, 5, 6 or 8");
+    *tw = value;
+    return RT_OK;
+  }
+  if (key && std::strcmp(key, "lane") == 0) {
+    rtamd::g_wf_lane = value;  // 0 = wave traversal, 1 = per-lane (LDS stack when it fits), 2 = per-lane, scratch stack
+    return RT_OK;
+  }
   if (key && std::strcmp(key, "accel") == 0) {
     rtamd::g_wf_accel = value != 0;
     return RT_OK;
@@ -356,7 +369,8 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   }
   // exact-culling hierarchy over the diagonal spheres (reorders `diag`; keys
   // come from `meta`, so the order changes no result)
-  std::vector<BvhNode> bvh = build_sphere_bvh(diag, g_bvh_leaf);
+  int bvh_depth = 0;
+  std::vector<BvhNode> bvh = build_sphere_bvh(diag, g_bvh_leaf, &bvh_depth);
   std::vector<LightRec> lrec(n_lights);
   for (size_t i = 0; i < n_lights; ++i)
     for (int c = 0; c < 3; ++c) { lrec[i].pos[c] = lights[i].position[c]; lrec[i].intensity[c] = lights[i].intensity[c]; }
@@ -403,6 +417,7 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   s->dev.quads = (const QuadRec*)(b + o_qd);
   s->dev.bvh = bvh.empty() ? nullptr : (const BvhNode*)(b + o_bv);
   s->dev.n_bvh = (int32_t)bvh.size();
+  s->dev.bvh_depth = bvh_depth;
   s->dev.shade = (const ShadeRec*)(b + o_sh);
   s->dev.lights = (const LightRec*)(b + o_li);
   s->dev.n_diag = (int32_t)diag.size();

@@ -59,6 +59,18 @@ Box sphere_box(const SphereDiag& r) {
   return b;
 }
 
+// binary32 rounded outward (the node boxes only ever grow)
+float f32_down(double x) {
+  float f = (float)x;
+  if ((double)f > x) f = std::nextafter(f, -INFINITY);
+  return f;
+}
+float f32_up(double x) {
+  float f = (float)x;
+  if ((double)f < x) f = std::nextafter(f, INFINITY);
+  return f;
+}
+
 struct Builder {
   std::vector<SphereDiag>& sph;
   std::vector<Box> box;
@@ -128,8 +140,8 @@ struct Builder {
     nd.child[0] = c0;
     nd.child[1] = c1;
     for (int a = 0; a < 3; ++a) {
-      nd.lo[0][a] = lb.lo[a]; nd.hi[0][a] = lb.hi[a];
-      nd.lo[1][a] = rb.lo[a]; nd.hi[1][a] = rb.hi[a];
+      nd.lo[0][a] = f32_down(lb.lo[a]); nd.hi[0][a] = f32_up(lb.hi[a]);
+      nd.lo[1][a] = f32_down(rb.lo[a]); nd.hi[1][a] = f32_up(rb.hi[a]);
     }
     return idx;
   }
@@ -177,7 +189,13 @@ struct Builder {
 
 }  // namespace
 
-std::vector<BvhNode> build_sphere_bvh(std::vector<SphereDiag>& spheres, int leaf_size) {
+static int tree_depth(const std::vector<BvhNode>& nodes, int32_t e) {
+  if (e < 0) return 0;
+  return 1 + std::max(tree_depth(nodes, nodes[e].child[0]), tree_depth(nodes, nodes[e].child[1]));
+}
+
+std::vector<BvhNode> build_sphere_bvh(std::vector<SphereDiag>& spheres, int leaf_size, int* depth) {
+  if (depth) *depth = 0;
   std::vector<BvhNode> out;
   const int n = (int)spheres.size();
   if (n == 0) return out;
@@ -198,9 +216,10 @@ std::vector<BvhNode> build_sphere_bvh(std::vector<SphereDiag>& spheres, int leaf
     BvhNode r{};
     r.child[0] = root;
     r.child[1] = kBvhEmpty;
-    for (int a = 0; a < 3; ++a) { r.lo[0][a] = all.lo[a]; r.hi[0][a] = all.hi[a]; }
+    for (int a = 0; a < 3; ++a) { r.lo[0][a] = f32_down(all.lo[a]); r.hi[0][a] = f32_up(all.hi[a]); }
     bd.nodes.assign(1, r);
   }
+  if (depth) *depth = tree_depth(bd.nodes, 0);  // kBvhEmpty < 0 counts as a leaf
   return bd.nodes;
 }
 

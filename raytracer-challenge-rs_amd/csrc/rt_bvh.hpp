@@ -12,6 +12,8 @@ namespace rtamd {
 // unit sphere under its stored inverse, padded outward (conservative
 // culling: DESIGN.md "Exact culling"). Returns the node array (root = 0),
 // empty when there are no spheres.
-std::vector<BvhNode> build_sphere_bvh(std::vector<SphereDiag>& spheres, int leaf_size);
+// `depth` receives the most far children a near-first traversal keeps
+// pending (the number of internal nodes on the longest root-leaf path).
+std::vector<BvhNode> build_sphere_bvh(std::vector<SphereDiag>& spheres, int leaf_size, int* depth = nullptr);
 
 }  // namespace rtamd

@@ -45,20 +45,23 @@ struct alignas(64) QuadRec {  // cube.rs / cylinder.rs / cone.rs
 static_assert(sizeof(QuadRec) == 128, "QuadRec must stay 128 B");
 
 // Bounding-volume hierarchy over the SphereDiag records (built on the host,
-// rt_bvh.cpp). Binary nodes carry both children's boxes, so one wave-uniform
-// 128-B load decides both children. A child is an internal node index
-// (>= 0), a leaf code -(1 + (first << 7 | count)) over the (reordered)
-// SphereDiag array, or kBvhEmpty.
+// rt_bvh.cpp). Binary nodes carry both children's boxes, so one 64-B load
+// (one s_load_dwordx16 for a wave, four 16-B loads for a lane) decides both
+// children. Boxes are binary32 rounded OUTWARD from the padded binary64
+// boxes (the slab test itself runs in binary64, so culling stays
+// conservative). A child is an internal node index (>= 0), a leaf code
+// -(1 + (first << 7 | count)) over the (reordered) SphereDiag array, or
+// kBvhEmpty.
 struct alignas(64) BvhNode {
-  double lo[2][3], hi[2][3];
+  float lo[2][3], hi[2][3];
   int32_t child[2];
   int32_t axis, pad;
-  int64_t pad2[2];
 };
-static_assert(sizeof(BvhNode) == 128, "BvhNode must stay 128 B");
+static_assert(sizeof(BvhNode) == 64, "BvhNode must stay 64 B");
 constexpr int32_t kBvhEmpty = (int32_t)0x80000000;
 constexpr int kBvhLeafMax = 127;
 constexpr int kBvhMaxDepth = 60;  // traversal stack entries per wave
+constexpr int kLaneLdsDepth = 32;  // per-lane traversal: LDS stack when bvh_depth fits
 
 // Intersection ordering key: (object index << 2) | position in the object's
 // local_intersect list (at most 4 entries, cylinder/cone). Equal t resolve by
@@ -95,7 +98,8 @@ struct DevScene {
   const BvhNode* bvh;  // nullptr when the scene has no BVH
   int32_t n_diag, n_gen, n_planes, n_objects, n_lights;
   int32_t n_quads;
-  int32_t n_bvh, pad;
+  int32_t n_bvh;
+  int32_t bvh_depth;  // most far children pending on a traversal stack
 };
 
 struct DevCamera {

@@ -26,6 +26,9 @@ constexpr int kTraceBlock = 1024;  // trace kernels: 16 waves, one LDS image per
 // allocator): 8 = two 1024-thread blocks per CU (<= 64 VGPRs), 4 = one.
 int g_wf_trace_waves = 8;  // tuning knob (rtamd_tuning_set("wf_waves", n))
 int g_wf_accel = 1;        // 1 = BVH traversal when counters are not requested, 0 = exhaustive always
+int g_wf_lane = 1;         // 1 = per-lane traversal for secondary / shadow rays, 0 = wave (packet) traversal
+// occupancy (waves per SIMD the register allocator targets) of the BVH trace kernels
+int g_tw_primary = 4, g_tw_closest = 4, g_tw_shadow = 4;
 constexpr int kWfBlock = 256;      // prep / shadow / combine
 
 #define WF_CHECK(x)                        \
@@ -321,7 +324,7 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow(DevScene sc, 
 
 // ------------------------------------------------------------ BVH traversal
 // Exact culling (DESIGN.md "Exact culling"): the wave traverses the sphere
-// BVH together (wave-uniform stack in LDS, wave-uniform 128-B node loads) and
+// BVH together (wave-uniform stack in LDS, wave-uniform 64-B node loads) and
 // skips a child only when NO lane's ray meets its padded box within
 // [0, t_hi] (t_hi = the lane's current nearest hit, or the light distance for
 // shadow rays). A sphere the exhaustive loop would hit always lies in a box
@@ -335,11 +338,12 @@ __device__ __forceinline__ double slab_inv(double d) {
   // 1/d, with a huge finite value for d == 0 (no NaN from 0 * inf)
   return d == 0.0 ? copysign(1e300, d) : 1.0 / d;
 }
-__device__ __forceinline__ bool slab_hit(const RT_CONST double* lo, const RT_CONST double* hi, V3 o, V3 inv,
-                                         double t_hi) {
-  const double x0 = (lo[0] - o.x) * inv.x, x1 = (hi[0] - o.x) * inv.x;
-  const double y0 = (lo[1] - o.y) * inv.y, y1 = (hi[1] - o.y) * inv.y;
-  const double z0 = (lo[2] - o.z) * inv.z, z1 = (hi[2] - o.z) * inv.z;
+template <typename P>  // P: constant-address (scalar loads) or generic (per-lane loads) float pointer
+__device__ __forceinline__ bool slab_hit(P lo, P hi, V3 o, V3 inv, double t_hi) {
+  // binary32 box corners widened exactly to binary64; the test runs in binary64
+  const double x0 = ((double)lo[0] - o.x) * inv.x, x1 = ((double)hi[0] - o.x) * inv.x;
+  const double y0 = ((double)lo[1] - o.y) * inv.y, y1 = ((double)hi[1] - o.y) * inv.y;
+  const double z0 = ((double)lo[2] - o.z) * inv.z, z1 = ((double)hi[2] - o.z) * inv.z;
   const double tmin = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmin(z0, z1));
   const double tmax = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmax(z0, z1));
   return tmin <= tmax && tmax >= 0.0 && tmin <= t_hi;
@@ -394,17 +398,74 @@ __device__ __forceinline__ void bvh_trace(const DevScene& sc, cPrimRec prim, int
   }
 }
 
-template <bool PRIMARY, bool QUADS, int TW>
+// Per-lane traversal for incoherent rays (secondary and shadow generations):
+// every lane walks the BVH on its own (near child first by its own direction,
+// a private stack), so a wave pays for the longest path instead of the union
+// of 64 paths. Same culling rule and the same exactness argument as the wave
+// traversal above.
+// LDS_STACK: the stack lives in LDS, entry k of lane t at lds[k * kTraceBlock + t]
+// (needs bvh_depth <= kLaneLdsDepth); otherwise in private (scratch) memory.
+template <bool SHADOW, bool LDS_STACK>
+__device__ __forceinline__ void lane_trace(const DevScene& sc, V3 o, V3 d, double t_shadow, Hit& h, unsigned& n_disc,
+                                           unsigned& n_tests, unsigned& n_boxes, int* lds) {
+  hit_init(h);
+  const V3 inv = v3(slab_inv(d.x), slab_inv(d.y), slab_inv(d.z));
+  const BvhNode* nodes = sc.bvh;
+  const SphereDiag* sd = sc.sph_diag;
+  int pstk[LDS_STACK ? 1 : kBvhMaxDepth + 4];
+  auto stk = [&](int k) -> int& { if constexpr (LDS_STACK) return lds[k * kTraceBlock]; else return pstk[k]; };
+  int sp = 0;
+  int e = 0;  // current entry: internal node index, leaf code, or kBvhEmpty (done)
+  while (e != kBvhEmpty) {
+    if (e >= 0) {
+      const BvhNode& nd = nodes[e];
+      const double t_hi = SHADOW ? t_shadow : h.t;
+      const int c0 = nd.child[0], c1 = nd.child[1];
+      const bool h0 = slab_hit(nd.lo[0], nd.hi[0], o, inv, t_hi);
+      const bool h1 = c1 != kBvhEmpty && slab_hit(nd.lo[1], nd.hi[1], o, inv, t_hi);
+      n_boxes += 2;
+      if (h0 && h1) {
+        const int axis = nd.axis;
+        const double dax = axis == 0 ? d.x : axis == 1 ? d.y : d.z;
+        const bool flip = dax < 0.0;
+        stk(sp++) = flip ? c0 : c1;
+        e = flip ? c1 : c0;
+      } else if (h0) {
+        e = c0;
+      } else if (h1) {
+        e = c1;
+      } else {
+        e = sp > 0 ? stk(--sp) : kBvhEmpty;
+      }
+    } else {
+      const int code = -(e + 1);
+      const int first = code >> 7, cnt = code & 127;
+      for (int k = first; k < first + cnt; ++k) {
+        const SphereDiag& r = sd[k];
+        const double s0 = r.s[0], s1 = r.s[1], s2 = r.s[2];
+        sphere_test<SHADOW>(s0 * o.x + r.t[0], s1 * o.y + r.t[1], s2 * o.z + r.t[2], s0 * d.x, s1 * d.y, s2 * d.z,
+                            [&] { return (int)r.meta; }, h, n_disc);
+      }
+      n_tests += (unsigned)cnt;
+      if (SHADOW && h.key >= 0 && h.t < t_shadow) break;  // this lane is shadowed
+      e = sp > 0 ? stk(--sp) : kBvhEmpty;
+    }
+  }
+}
+
+// LANE: 0 = wave traversal, 1 = per-lane with a scratch stack, 2 = per-lane with an LDS stack
+template <bool PRIMARY, bool QUADS, int LANE, int TW>
 __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest_bvh(DevScene sc, DevCamera cam, WfArgs a) {
-  __shared__ int stack_lds[kTraceBlock / 64][kBvhMaxDepth + 4];
-  int* stk = stack_lds[threadIdx.x / 64];
+  __shared__ int stack_lds[LANE == 2 ? kLaneLdsDepth * kTraceBlock : (kTraceBlock / 64) * (kBvhMaxDepth + 4)];
+  int* stk = LANE == 2 ? stack_lds + threadIdx.x : stack_lds + (threadIdx.x / 64) * (kBvhMaxDepth + 4);
   unsigned n_disc = 0, n_tests = 0, n_boxes = 0;
   const unsigned stride = gridDim.x * blockDim.x;
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
     V3 o, d;
     wf_ray(a, cam, i, o, d);
     Hit h;
-    bvh_trace<PRIMARY, false>(sc, (cPrimRec)a.prim, stk, o, d, 0.0, h, n_disc, n_tests, n_boxes);
+    if constexpr (LANE && !PRIMARY) lane_trace<false, LANE == 2>(sc, o, d, 0.0, h, n_disc, n_tests, n_boxes, stk);
+    else bvh_trace<PRIMARY, false>(sc, (cPrimRec)a.prim, stk, o, d, 0.0, h, n_disc, n_tests, n_boxes);
     trace_rest<false, QUADS>(sc, o, d, h, n_disc);
     hit_finish(h);
     WfHit w;
@@ -419,10 +480,10 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest_bvh(DevScene
   }
 }
 
-template <bool QUADS, int TW>
+template <bool QUADS, int LANE, int TW>
 __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow_bvh(DevScene sc, WfArgs a) {
-  __shared__ int stack_lds[kTraceBlock / 64][kBvhMaxDepth + 4];
-  int* stk = stack_lds[threadIdx.x / 64];
+  __shared__ int stack_lds[LANE == 2 ? kLaneLdsDepth * kTraceBlock : (kTraceBlock / 64) * (kBvhMaxDepth + 4)];
+  int* stk = LANE == 2 ? stack_lds + threadIdx.x : stack_lds + (threadIdx.x / 64) * (kBvhMaxDepth + 4);
   unsigned n_disc = 0, n_tests = 0, n_boxes = 0;
   const unsigned stride = gridDim.x * blockDim.x;
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n_shadow; i += stride) {
@@ -430,7 +491,8 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow_bvh(DevScene 
     const V3 o = v3(s.o[0], s.o[1], s.o[2]);
     const V3 d = v3(s.d[0], s.d[1], s.d[2]);
     Hit h;
-    bvh_trace<false, true>(sc, nullptr, stk, o, d, s.dist, h, n_disc, n_tests, n_boxes);
+    if constexpr (LANE) lane_trace<true, LANE == 2>(sc, o, d, s.dist, h, n_disc, n_tests, n_boxes, stk);
+    else bvh_trace<false, true>(sc, nullptr, stk, o, d, s.dist, h, n_disc, n_tests, n_boxes);
     if (__any(!(h.key >= 0 && h.t < s.dist))) trace_rest<true, QUADS>(sc, o, d, h, n_disc);
     hit_finish(h);
     a.sflags[s.slot] = (h.key >= 0 && h.t < s.dist) ? 1 : 0;
@@ -728,10 +790,16 @@ static hipError_t launch_closest_q(const DevScene& sc, const DevCamera& cam, con
                                    bool lds_ok, bool bvh, unsigned n, hipStream_t stream) {
   if (bvh) {
     if (primary) {
-      auto k = wf_trace_closest_bvh<true, QUADS, TW>;
+      auto k = wf_trace_closest_bvh<true, QUADS, 0, TW>;
+      hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
+    } else if (g_wf_lane == 1 && sc.bvh_depth <= kLaneLdsDepth) {
+      auto k = wf_trace_closest_bvh<false, QUADS, 2, TW>;
+      hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
+    } else if (g_wf_lane) {
+      auto k = wf_trace_closest_bvh<false, QUADS, 1, TW>;
       hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
     } else {
-      auto k = wf_trace_closest_bvh<false, QUADS, TW>;
+      auto k = wf_trace_closest_bvh<false, QUADS, 0, TW>;
       hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
     }
   } else if (primary) {
@@ -760,8 +828,16 @@ static hipError_t launch_closest(const DevScene& sc, const DevCamera& cam, const
 template <bool QUADS, int TW>
 static hipError_t launch_shadow_q(const DevScene& sc, const WfArgs& a, bool lds_ok, bool bvh, hipStream_t stream) {
   if (bvh) {
-    auto k = wf_trace_shadow_bvh<QUADS, TW>;
-    hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, 0, a.n_shadow)), dim3(kTraceBlock), 0, stream, sc, a);
+    if (g_wf_lane == 1 && sc.bvh_depth <= kLaneLdsDepth) {
+      auto k = wf_trace_shadow_bvh<QUADS, 2, TW>;
+      hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, 0, a.n_shadow)), dim3(kTraceBlock), 0, stream, sc, a);
+    } else if (g_wf_lane) {
+      auto k = wf_trace_shadow_bvh<QUADS, 1, TW>;
+      hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, 0, a.n_shadow)), dim3(kTraceBlock), 0, stream, sc, a);
+    } else {
+      auto k = wf_trace_shadow_bvh<QUADS, 0, TW>;
+      hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, 0, a.n_shadow)), dim3(kTraceBlock), 0, stream, sc, a);
+    }
   } else if (lds_ok) {
     const size_t lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, false);
     auto k = wf_trace_shadow<true, QUADS, TW>;
@@ -848,8 +924,15 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     a.disc_slot = (unsigned)ccls;
     prof_rays_[ccls] += n;
     WF_CHECK(pmark(stream, ccls, true));
-    if (g_wf_trace_waves == 4) WF_CHECK(launch_closest<4>(sc, cam, a, prim_launch, gen_lds, bvh, n, stream));
-    else WF_CHECK(launch_closest<8>(sc, cam, a, prim_launch, gen_lds, bvh, n, stream));
+    {
+      const int tw = !bvh ? g_wf_trace_waves : prim_launch ? g_tw_primary : g_tw_closest;
+      switch (tw) {
+        case 4: WF_CHECK(launch_closest<4>(sc, cam, a, prim_launch, gen_lds, bvh, n, stream)); break;
+        case 5: WF_CHECK(launch_closest<5>(sc, cam, a, prim_launch, gen_lds, bvh, n, stream)); break;
+        case 6: WF_CHECK(launch_closest<6>(sc, cam, a, prim_launch, gen_lds, bvh, n, stream)); break;
+        default: WF_CHECK(launch_closest<8>(sc, cam, a, prim_launch, gen_lds, bvh, n, stream)); break;
+      }
+    }
     WF_CHECK(pmark(stream, ccls, false));
     // 2. prepare_computations + spawn
     WF_CHECK(pmark(stream, WF_PREP, true));
@@ -869,8 +952,12 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
       a.disc_slot = WF_SHADOW;
       prof_rays_[WF_SHADOW] += a.n_shadow;
       WF_CHECK(pmark(stream, WF_SHADOW, true));
-      if (g_wf_trace_waves == 4) WF_CHECK(launch_shadow_wf<4>(sc, a, gen_lds, bvh, stream));
-      else WF_CHECK(launch_shadow_wf<8>(sc, a, gen_lds, bvh, stream));
+      switch (!bvh ? g_wf_trace_waves : g_tw_shadow) {
+        case 4: WF_CHECK(launch_shadow_wf<4>(sc, a, gen_lds, bvh, stream)); break;
+        case 5: WF_CHECK(launch_shadow_wf<5>(sc, a, gen_lds, bvh, stream)); break;
+        case 6: WF_CHECK(launch_shadow_wf<6>(sc, a, gen_lds, bvh, stream)); break;
+        default: WF_CHECK(launch_shadow_wf<8>(sc, a, gen_lds, bvh, stream)); break;
+      }
       WF_CHECK(pmark(stream, WF_SHADOW, false));
     }
     if (stats) {

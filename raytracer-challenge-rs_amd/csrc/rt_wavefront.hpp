@@ -62,6 +62,8 @@ struct PrimRec {  // primary rays share the origin: per diag sphere (s, o', c)
 
 constexpr int kMaxGen = 66;
 extern int g_wf_trace_waves;  // tuning knob: trace-kernel occupancy (4 or 8 waves/SIMD)
+extern int g_tw_primary, g_tw_closest, g_tw_shadow;  // tuning knobs: BVH trace-kernel occupancy
+extern int g_wf_lane;         // tuning knob: 1 = per-lane BVH traversal for secondary / shadow rays
 extern int g_wf_accel;        // tuning knob: 1 = BVH traversal (when no counters are requested), 0 = exhaustive
 
 struct WfCounters {

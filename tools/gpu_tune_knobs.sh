@@ -1,0 +1,5 @@
+#!/bin/bash
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
+mkdir -p gpurun_out
+timeout -k 10 300 python tools/tune_knobs.py "$@" 2>&1 | grep -v amdgpu.ids | tee gpurun_out/tune_knobs.log

@@ -1,0 +1,40 @@
+"""A/B runtime tuning knobs on the C3 frame in one process, interleaved
+rounds; every variant must reproduce the first variant's image (dev tool).
+Usage: tune_knobs.py lane=0,1 wf_waves=8,4 [--scene c3|c5]"""
+import itertools, os, sys
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "raytracer-challenge-rs_amd")]
+import torch  # noqa
+import rtamd
+from rtamd import scenes
+args = [x for x in sys.argv[1:] if "=" in x]
+scene = "c5" if "--c5" in sys.argv else "c3"
+knobs = [(k, [int(v) for v in vs.split(",")]) for k, vs in (x.split("=") for x in args)]
+if scene == "c5":
+    w, cam, depth = scenes.c5(1024, 1024)
+else:
+    w, cam, depth = scenes.c3()
+w.upload(0)
+buf = torch.empty((cam.vsize, cam.hsize, 3), dtype=torch.float64, device="cuda")
+s = torch.cuda.current_stream().cuda_stream
+combos = list(itertools.product(*[vs for _, vs in knobs]))
+res, ref = {}, None
+for r in range(4):
+    for combo in combos:
+        for (k, _), v in zip(knobs, combo):
+            rtamd._rtamd._tuning_set(k, v)
+        rtamd._rtamd._wf_profile(w, 1, False)
+        for _ in range(3):
+            cam.render_shard_device(w, depth, 8, 0, 1, buf.data_ptr(), s, False)
+        torch.cuda.synchronize()
+        p = rtamd._rtamd._wf_profile(w, 0, True)
+        res.setdefault(combo, []).append((sum(p["ms"].values()), p["ms"], p["tests"], p["boxes"]))
+        chk = buf.cpu().numpy().tobytes()
+        ref = ref or chk
+        assert chk == ref, combo
+for combo, v in res.items():
+    tot, ms, tests, boxes = min(v, key=lambda x: x[0])
+    name = " ".join(f"{k}={c}" for (k, _), c in zip(knobs, combo))
+    print(f"{name}: frame {tot:.3f} ms  " + " ".join(f"{c}={m:.3f}" for c, m in ms.items())
+          + "  tests " + " ".join(f"{c}={t/1e6:.0f}M" for c, t in tests.items())
+          + "  boxes " + " ".join(f"{c}={t/1e6:.0f}M" for c, t in boxes.items()), flush=True)
