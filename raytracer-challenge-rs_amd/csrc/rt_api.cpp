@@ -227,7 +227,8 @@ int rtamd_tuning_set(const char* key, int value) {
     return RT_OK;
   }
   if (key && std::strcmp(key, "lane") == 0) {
-    rtamd::g_wf_lane = value;  // 0 = wave traversal, 1 = per-lane (LDS stack when it fits), 2 = per-lane, scratch stack
+    rtamd::g_wf_lane = value;  // 0 = wave traversal, 1 = per-lane (LDS stack when it fits), 2 = per-lane, scratch
+                               // stack, 5 = per-lane with the scene in LDS when it fits (default)
     return RT_OK;
   }
   if (key && std::strcmp(key, "accel") == 0) {

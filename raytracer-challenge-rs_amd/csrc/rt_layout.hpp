@@ -61,7 +61,7 @@ static_assert(sizeof(BvhNode) == 64, "BvhNode must stay 64 B");
 constexpr int32_t kBvhEmpty = (int32_t)0x80000000;
 constexpr int kBvhLeafMax = 127;
 constexpr int kBvhMaxDepth = 60;  // traversal stack entries per wave
-constexpr int kLaneLdsDepth = 32;  // per-lane traversal: LDS stack when bvh_depth fits
+constexpr int kLaneLdsDepth = 16;  // per-lane traversal: LDS stack when bvh_depth fits
 
 // Intersection ordering key: (object index << 2) | position in the object's
 // local_intersect list (at most 4 entries, cylinder/cone). Equal t resolve by

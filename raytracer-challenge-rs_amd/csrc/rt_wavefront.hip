@@ -26,7 +26,8 @@ constexpr int kTraceBlock = 1024;  // trace kernels: 16 waves, one LDS image per
 // allocator): 8 = two 1024-thread blocks per CU (<= 64 VGPRs), 4 = one.
 int g_wf_trace_waves = 8;  // tuning knob (rtamd_tuning_set("wf_waves", n))
 int g_wf_accel = 1;        // 1 = BVH traversal when counters are not requested, 0 = exhaustive always
-int g_wf_lane = 1;         // 1 = per-lane traversal for secondary / shadow rays, 0 = wave (packet) traversal
+int g_wf_lane = 5;  // secondary / shadow rays: 5 = per-lane, scene + stack in LDS (when they fit), 1 = per-lane
+                    // with an LDS (or scratch) stack, 0 = wave (packet) traversal
 // occupancy (waves per SIMD the register allocator targets) of the BVH trace kernels
 int g_tw_primary = 4, g_tw_closest = 4, g_tw_shadow = 4;
 constexpr int kWfBlock = 256;      // prep / shadow / combine
@@ -405,19 +406,21 @@ __device__ __forceinline__ void bvh_trace(const DevScene& sc, cPrimRec prim, int
 // traversal above.
 // LDS_STACK: the stack lives in LDS, entry k of lane t at lds[k * kTraceBlock + t]
 // (needs bvh_depth <= kLaneLdsDepth); otherwise in private (scratch) memory.
+// `nodes` / `sd` point at the hierarchy and the sphere records in global
+// memory or at the block's LDS copy. `h` arrives initialised (it may already
+// hold the planes' nearest hit, which tightens the culling).
 template <bool SHADOW, bool LDS_STACK>
-__device__ __forceinline__ void lane_trace(const DevScene& sc, V3 o, V3 d, double t_shadow, Hit& h, unsigned& n_disc,
-                                           unsigned& n_tests, unsigned& n_boxes, int* lds) {
-  hit_init(h);
+__device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDiag* sd, bool has_bvh, V3 o, V3 d,
+                                           double t_shadow, Hit& h, unsigned& n_disc, unsigned& n_tests,
+                                           unsigned& n_boxes, int* lds) {
   const V3 inv = v3(slab_inv(d.x), slab_inv(d.y), slab_inv(d.z));
-  const BvhNode* nodes = sc.bvh;
-  const SphereDiag* sd = sc.sph_diag;
   int pstk[LDS_STACK ? 1 : kBvhMaxDepth + 4];
   auto stk = [&](int k) -> int& { if constexpr (LDS_STACK) return lds[k * kTraceBlock]; else return pstk[k]; };
   int sp = 0;
-  int e = 0;  // current entry: internal node index, leaf code, or kBvhEmpty (done)
+  auto pop = [&]() { return sp > 0 ? stk(--sp) : kBvhEmpty; };
+  int e = (SHADOW && h.key >= 0 && h.t < t_shadow) || !has_bvh ? kBvhEmpty : 0;
   while (e != kBvhEmpty) {
-    if (e >= 0) {
+    if (e >= 0) {  // a node visit: both children's boxes, near child first by this lane's direction
       const BvhNode& nd = nodes[e];
       const double t_hi = SHADOW ? t_shadow : h.t;
       const int c0 = nd.child[0], c1 = nd.child[1];
@@ -426,18 +429,13 @@ __device__ __forceinline__ void lane_trace(const DevScene& sc, V3 o, V3 d, doubl
       n_boxes += 2;
       if (h0 && h1) {
         const int axis = nd.axis;
-        const double dax = axis == 0 ? d.x : axis == 1 ? d.y : d.z;
-        const bool flip = dax < 0.0;
+        const bool flip = (axis == 0 ? d.x : axis == 1 ? d.y : d.z) < 0.0;
         stk(sp++) = flip ? c0 : c1;
         e = flip ? c1 : c0;
-      } else if (h0) {
-        e = c0;
-      } else if (h1) {
-        e = c1;
       } else {
-        e = sp > 0 ? stk(--sp) : kBvhEmpty;
+        e = h0 ? c0 : h1 ? c1 : pop();
       }
-    } else {
+    } else {  // a leaf: its spheres
       const int code = -(e + 1);
       const int first = code >> 7, cnt = code & 127;
       for (int k = first; k < first + cnt; ++k) {
@@ -447,26 +445,64 @@ __device__ __forceinline__ void lane_trace(const DevScene& sc, V3 o, V3 d, doubl
                             [&] { return (int)r.meta; }, h, n_disc);
       }
       n_tests += (unsigned)cnt;
-      if (SHADOW && h.key >= 0 && h.t < t_shadow) break;  // this lane is shadowed
-      e = sp > 0 ? stk(--sp) : kBvhEmpty;
+      if (SHADOW && h.key >= 0 && h.t < t_shadow) break;  // shadowed: done
+      e = pop();
     }
   }
 }
 
-// LANE: 0 = wave traversal, 1 = per-lane with a scratch stack, 2 = per-lane with an LDS stack
+// LANE == 5: the block stages the hierarchy and the sphere records in LDS
+// (dynamic shared memory: [stack kLaneLdsDepth x kTraceBlock ints][nodes][spheres]).
+__host__ __device__ inline size_t lane_lds_bytes(int n_bvh, int n_diag) {
+  return (size_t)kLaneLdsDepth * kTraceBlock * 4 + (size_t)n_bvh * sizeof(BvhNode) + (size_t)n_diag * sizeof(SphereDiag);
+}
+struct LaneScene {
+  const BvhNode* nodes;
+  const SphereDiag* sd;
+  int* stack;
+};
+template <int LANE>
+__device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, int* static_stack, unsigned char* dyn) {
+  LaneScene ls{sc.bvh, sc.sph_diag, static_stack};
+  if constexpr (LANE == 5) {
+    int* stack = (int*)dyn;
+    BvhNode* nodes = (BvhNode*)(dyn + (size_t)kLaneLdsDepth * kTraceBlock * 4);
+    SphereDiag* sd = (SphereDiag*)((unsigned char*)nodes + (size_t)sc.n_bvh * sizeof(BvhNode));
+    const uint4* gn = (const uint4*)sc.bvh;
+    uint4* ln = (uint4*)nodes;
+    for (int i = threadIdx.x; i < sc.n_bvh * (int)(sizeof(BvhNode) / 16); i += blockDim.x) ln[i] = gn[i];
+    const uint4* gs = (const uint4*)sc.sph_diag;
+    uint4* ls4 = (uint4*)sd;
+    for (int i = threadIdx.x; i < sc.n_diag * (int)(sizeof(SphereDiag) / 16); i += blockDim.x) ls4[i] = gs[i];
+    __syncthreads();
+    ls.nodes = nodes;
+    ls.sd = sd;
+    ls.stack = stack + threadIdx.x;
+  }
+  return ls;
+}
+
 template <bool PRIMARY, bool QUADS, int LANE, int TW>
 __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest_bvh(DevScene sc, DevCamera cam, WfArgs a) {
-  __shared__ int stack_lds[LANE == 2 ? kLaneLdsDepth * kTraceBlock : (kTraceBlock / 64) * (kBvhMaxDepth + 4)];
-  int* stk = LANE == 2 ? stack_lds + threadIdx.x : stack_lds + (threadIdx.x / 64) * (kBvhMaxDepth + 4);
+  constexpr bool LDS_STACK = LANE >= 2;
+  __shared__ int stack_lds[LANE == 5 ? 1 : LDS_STACK ? kLaneLdsDepth * kTraceBlock : (kTraceBlock / 64) * (kBvhMaxDepth + 4)];
+  extern __shared__ __attribute__((aligned(16))) unsigned char lane_dyn[];
+  int* stk = LDS_STACK ? stack_lds + threadIdx.x : stack_lds + (threadIdx.x / 64) * (kBvhMaxDepth + 4);
+  const LaneScene ls = lane_scene<LANE>(sc, stk, lane_dyn);
   unsigned n_disc = 0, n_tests = 0, n_boxes = 0;
   const unsigned stride = gridDim.x * blockDim.x;
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
     V3 o, d;
     wf_ray(a, cam, i, o, d);
     Hit h;
-    if constexpr (LANE && !PRIMARY) lane_trace<false, LANE == 2>(sc, o, d, 0.0, h, n_disc, n_tests, n_boxes, stk);
-    else bvh_trace<PRIMARY, false>(sc, (cPrimRec)a.prim, stk, o, d, 0.0, h, n_disc, n_tests, n_boxes);
-    trace_rest<false, QUADS>(sc, o, d, h, n_disc);
+    if constexpr (LANE && !PRIMARY) {
+      hit_init(h);
+      trace_rest<false, QUADS>(sc, o, d, h, n_disc);  // planes first: an early nearest hit tightens the culling
+      lane_trace<false, LDS_STACK>(ls.nodes, ls.sd, sc.n_bvh > 0, o, d, 0.0, h, n_disc, n_tests, n_boxes, ls.stack);
+    } else {
+      bvh_trace<PRIMARY, false>(sc, (cPrimRec)a.prim, stk, o, d, 0.0, h, n_disc, n_tests, n_boxes);
+      trace_rest<false, QUADS>(sc, o, d, h, n_disc);
+    }
     hit_finish(h);
     WfHit w;
     w.t = h.t; w.key = h.key; w.c1k = h.c1k; w.c2k = h.c2k; w.hin = h.hin;
@@ -482,8 +518,11 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest_bvh(DevScene
 
 template <bool QUADS, int LANE, int TW>
 __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow_bvh(DevScene sc, WfArgs a) {
-  __shared__ int stack_lds[LANE == 2 ? kLaneLdsDepth * kTraceBlock : (kTraceBlock / 64) * (kBvhMaxDepth + 4)];
-  int* stk = LANE == 2 ? stack_lds + threadIdx.x : stack_lds + (threadIdx.x / 64) * (kBvhMaxDepth + 4);
+  constexpr bool LDS_STACK = LANE >= 2;
+  __shared__ int stack_lds[LANE == 5 ? 1 : LDS_STACK ? kLaneLdsDepth * kTraceBlock : (kTraceBlock / 64) * (kBvhMaxDepth + 4)];
+  extern __shared__ __attribute__((aligned(16))) unsigned char lane_dyn[];
+  int* stk = LDS_STACK ? stack_lds + threadIdx.x : stack_lds + (threadIdx.x / 64) * (kBvhMaxDepth + 4);
+  const LaneScene ls = lane_scene<LANE>(sc, stk, lane_dyn);
   unsigned n_disc = 0, n_tests = 0, n_boxes = 0;
   const unsigned stride = gridDim.x * blockDim.x;
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n_shadow; i += stride) {
@@ -491,9 +530,14 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow_bvh(DevScene 
     const V3 o = v3(s.o[0], s.o[1], s.o[2]);
     const V3 d = v3(s.d[0], s.d[1], s.d[2]);
     Hit h;
-    if constexpr (LANE) lane_trace<true, LANE == 2>(sc, o, d, s.dist, h, n_disc, n_tests, n_boxes, stk);
-    else bvh_trace<false, true>(sc, nullptr, stk, o, d, s.dist, h, n_disc, n_tests, n_boxes);
-    if (__any(!(h.key >= 0 && h.t < s.dist))) trace_rest<true, QUADS>(sc, o, d, h, n_disc);
+    if constexpr (LANE) {
+      hit_init(h);
+      trace_rest<true, QUADS>(sc, o, d, h, n_disc);  // planes first: any hit before the light ends the ray
+      lane_trace<true, LDS_STACK>(ls.nodes, ls.sd, sc.n_bvh > 0, o, d, s.dist, h, n_disc, n_tests, n_boxes, ls.stack);
+    } else {
+      bvh_trace<false, true>(sc, nullptr, stk, o, d, s.dist, h, n_disc, n_tests, n_boxes);
+      if (__any(!(h.key >= 0 && h.t < s.dist))) trace_rest<true, QUADS>(sc, o, d, h, n_disc);
+    }
     hit_finish(h);
     a.sflags[s.slot] = (h.key >= 0 && h.t < s.dist) ? 1 : 0;
   }
@@ -717,8 +761,8 @@ hipError_t Wavefront::last_profile(WfProfile* out) {
   }
   if (pframes_ > 1)
     for (int c = 0; c < WF_NCLASS; ++c) out->ms[c] /= (double)pframes_;
-  WfCounters hc;
-  WF_CHECK(hipMemcpy(&hc, d_cnt_, sizeof hc, hipMemcpyDeviceToHost));
+  WfCounters hc{};
+  if (d_cnt_) WF_CHECK(hipMemcpy(&hc, d_cnt_, sizeof hc, hipMemcpyDeviceToHost));  // nothing rendered yet: zeros
   for (int c = 0; c < 3; ++c) {
     out->rays[c] = prof_rays_[c];
     out->disc[c] = (double)hc.disc[c];
@@ -792,7 +836,12 @@ static hipError_t launch_closest_q(const DevScene& sc, const DevCamera& cam, con
     if (primary) {
       auto k = wf_trace_closest_bvh<true, QUADS, 0, TW>;
       hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
-    } else if (g_wf_lane == 1 && sc.bvh_depth <= kLaneLdsDepth) {
+    } else if (g_wf_lane == 5 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc.n_bvh, sc.n_diag) <= kWfLdsLimit) {
+      const size_t lds = lane_lds_bytes(sc.n_bvh, sc.n_diag);
+      auto k = wf_trace_closest_bvh<false, QUADS, 5, TW>;
+      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, lds, n)), dim3(kTraceBlock), lds, stream, sc, cam, a);
+    } else if (g_wf_lane && g_wf_lane != 2 && sc.bvh_depth <= kLaneLdsDepth) {
       auto k = wf_trace_closest_bvh<false, QUADS, 2, TW>;
       hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
     } else if (g_wf_lane) {
@@ -828,7 +877,12 @@ static hipError_t launch_closest(const DevScene& sc, const DevCamera& cam, const
 template <bool QUADS, int TW>
 static hipError_t launch_shadow_q(const DevScene& sc, const WfArgs& a, bool lds_ok, bool bvh, hipStream_t stream) {
   if (bvh) {
-    if (g_wf_lane == 1 && sc.bvh_depth <= kLaneLdsDepth) {
+    if (g_wf_lane == 5 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc.n_bvh, sc.n_diag) <= kWfLdsLimit) {
+      const size_t lds = lane_lds_bytes(sc.n_bvh, sc.n_diag);
+      auto k = wf_trace_shadow_bvh<QUADS, 5, TW>;
+      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, lds, a.n_shadow)), dim3(kTraceBlock), lds, stream, sc, a);
+    } else if (g_wf_lane && g_wf_lane != 2 && sc.bvh_depth <= kLaneLdsDepth) {
       auto k = wf_trace_shadow_bvh<QUADS, 2, TW>;
       hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, 0, a.n_shadow)), dim3(kTraceBlock), 0, stream, sc, a);
     } else if (g_wf_lane) {

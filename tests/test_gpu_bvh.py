@@ -139,3 +139,17 @@ def test_accel_knob_off_matches(rt):
     finally:
         rt._rtamd._tuning_set("accel", 1)
     assert a.to_numpy().tobytes() == b.to_numpy().tobytes()
+
+
+@pytest.mark.parametrize("lane", [0, 1, 2, 5])
+def test_traversal_variants_bitwise(rt, lane):
+    """Every traversal variant (wave / per-lane with LDS or scratch stack /
+    per-lane with the scene staged in LDS) gives the exhaustive frame."""
+    w, cam, depth = _glass_cluster(rt, n=250, seed=21, inside=False)
+    exact, _ = cam.render(w, depth, want_stats=True)
+    rt._rtamd._tuning_set("lane", lane)
+    try:
+        fast, _ = cam.render(w, depth, want_stats=False)
+    finally:
+        rt._rtamd._tuning_set("lane", 5)
+    assert fast.to_numpy().tobytes() == exact.to_numpy().tobytes()

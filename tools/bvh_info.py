@@ -1,0 +1,14 @@
+import os, sys
+sys.path[:0] = ['/root/repo', '/root/repo/raytracer-challenge-rs_amd']
+import torch, rtamd
+from rtamd import scenes
+for lf in (1, 2, 4, 8):
+    rtamd._rtamd._tuning_set("bvh_leaf", lf)
+    w, cam, depth = scenes.c3()
+    w.upload(0)
+    p = rtamd._rtamd._wf_profile(w, -1, True)
+    print("leaf", lf, "nodes", p["n_bvh_nodes"], "depth", p["bvh_depth"], flush=True)
+w, cam, depth = scenes.c5(256, 256)
+w.upload(0)
+p = rtamd._rtamd._wf_profile(w, -1, True)
+print("c5 nodes", p["n_bvh_nodes"], "depth", p["bvh_depth"])
