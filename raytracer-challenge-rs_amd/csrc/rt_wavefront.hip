@@ -145,6 +145,24 @@ __device__ __forceinline__ void wf_ray(const WfArgs& a, const DevCamera& cam, un
   }
 }
 
+// Shadow ray j of a generation: World::is_shadowed(comps.over_point, light)
+// (world.rs:95-105) of hit node j / L and light j % L, built from the node's
+// over point exactly as the reference builds it (v = light - point,
+// distance = |v|, direction = v.normalize()). slot = node * L + light.
+__device__ __forceinline__ void shadow_ray(const DevScene& sc, const WfArgs& a, unsigned j, V3& o, V3& d,
+                                           double& dist, unsigned& slot) {
+  const unsigned L = (unsigned)sc.n_lights;
+  const unsigned q = j / L, l = j - q * L;
+  const int node = a.shadow_nodes[q];
+  const WfNode& nd = a.nodes[node];
+  o = v3(nd.over[0], nd.over[1], nd.over[2]);
+  cLightRec Lr = (cLightRec)sc.lights + l;
+  const V3 v = vsub(v3(Lr->pos[0], Lr->pos[1], Lr->pos[2]), o);
+  dist = sqrt(v.x * v.x + v.y * v.y + v.z * v.z);  // magnitude (vector.rs:21-23)
+  d = vnormalize(v);
+  slot = (unsigned)node * L + l;
+}
+
 // ------------------------------------------------------------ primary records
 // Per diagonal sphere: s (inverse diagonal), o' = s*o + t for the camera origin
 // o, and c = o'.o' - 1 — the same operations the general test performs, so the
@@ -311,13 +329,14 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow(DevScene sc, 
   if constexpr (USE_LDS) lv = wf_lds_stage<false>(sc, nullptr, lds_raw);
   const unsigned stride = gridDim.x * blockDim.x;
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n_shadow; i += stride) {
-    const WfShadow s = a.shadows[i];
-    const V3 o = v3(s.o[0], s.o[1], s.o[2]);
-    const V3 d = v3(s.d[0], s.d[1], s.d[2]);
+    V3 o, d;
+    double dist;
+    unsigned slot;
+    shadow_ray(sc, a, i, o, d, dist, slot);
     Hit h;
     if constexpr (USE_LDS) wf_trace_lds<false, true, QUADS>(sc, lv, o, d, h, n_disc);
     else trace<true>(sc, o, d, h, n_disc);
-    a.sflags[s.slot] = (h.key >= 0 && h.t < s.dist) ? 1 : 0;
+    a.sflags[slot] = (h.key >= 0 && h.t < dist) ? 1 : 0;
   }
   const unsigned long long s = wave_sum(n_disc);
   if (lane_id() == 0 && s) atomicAdd(&a.cnt->disc[a.disc_slot], s);
@@ -526,20 +545,21 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow_bvh(DevScene 
   unsigned n_disc = 0, n_tests = 0, n_boxes = 0;
   const unsigned stride = gridDim.x * blockDim.x;
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n_shadow; i += stride) {
-    const WfShadow s = a.shadows[i];
-    const V3 o = v3(s.o[0], s.o[1], s.o[2]);
-    const V3 d = v3(s.d[0], s.d[1], s.d[2]);
+    V3 o, d;
+    double dist;
+    unsigned slot;
+    shadow_ray(sc, a, i, o, d, dist, slot);
     Hit h;
     if constexpr (LANE) {
       hit_init(h);
       trace_rest<true, QUADS>(sc, o, d, h, n_disc);  // planes first: any hit before the light ends the ray
-      lane_trace<true, LDS_STACK>(ls.nodes, ls.sd, sc.n_bvh > 0, o, d, s.dist, h, n_disc, n_tests, n_boxes, ls.stack);
+      lane_trace<true, LDS_STACK>(ls.nodes, ls.sd, sc.n_bvh > 0, o, d, dist, h, n_disc, n_tests, n_boxes, ls.stack);
     } else {
-      bvh_trace<false, true>(sc, nullptr, stk, o, d, s.dist, h, n_disc, n_tests, n_boxes);
-      if (__any(!(h.key >= 0 && h.t < s.dist))) trace_rest<true, QUADS>(sc, o, d, h, n_disc);
+      bvh_trace<false, true>(sc, nullptr, stk, o, d, dist, h, n_disc, n_tests, n_boxes);
+      if (__any(!(h.key >= 0 && h.t < dist))) trace_rest<true, QUADS>(sc, o, d, h, n_disc);
     }
     hit_finish(h);
-    a.sflags[s.slot] = (h.key >= 0 && h.t < s.dist) ? 1 : 0;
+    a.sflags[slot] = (h.key >= 0 && h.t < dist) ? 1 : 0;
   }
   const unsigned long long sd = wave_sum(n_disc), st = wave_sum(n_tests), sb = wave_sum(n_boxes);
   if (lane_id() == 0) {
@@ -553,7 +573,6 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow_bvh(DevScene 
 __global__ __launch_bounds__(kWfBlock) void wf_prep(DevScene sc, DevCamera cam, WfArgs a) {
   const unsigned stride = gridDim.x * blockDim.x;
   const unsigned L = (unsigned)sc.n_lights;
-  cLightRec lights = (cLightRec)sc.lights;
   const unsigned remaining = a.max_depth - a.g;
   // every lane of a wave runs the same number of iterations (appends are convergent)
   const unsigned n_iter = (a.n + stride - 1) / stride;
@@ -592,7 +611,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_prep(DevScene sc, DevCamera cam, 
     // shadow rays: one per light, in light order (world.rs:41-56)
     unsigned sbase, rbase, fbase;
     block_append(&a.cnt->n_shadow[a.g], L, hit && L > 0, &a.cnt->n_rays[a.g + 1], want_refl, want_refr, sbase, rbase,
-                 fbase);
+                 fbase);  // n_shadow counts shadow rays (hits x lights); the list holds the hit nodes
     if (!valid) continue;
     WfNode nd;
     nd.obj = -1; nd.child_refl = -1; nd.child_refr = -1; nd.pad = 0;
@@ -602,18 +621,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_prep(DevScene sc, DevCamera cam, 
       nd.normal[0] = c.normal.x; nd.normal[1] = c.normal.y; nd.normal[2] = c.normal.z;
       // shade_hit's Schlick factor (world.rs:62-64), same inputs as the reference's call
       nd.schlick = (m->reflective > 0.0 && m->transparency > 0.0) ? schlick(c.eyev, c.normal, c.n1, c.n2) : 0.0;
-      for (unsigned l = 0; l < L; ++l) {
-        cLightRec Lr = lights + l;
-        const V3 v = vsub(v3(Lr->pos[0], Lr->pos[1], Lr->pos[2]), c.over);
-        WfShadow s;
-        s.dist = sqrt(v.x * v.x + v.y * v.y + v.z * v.z);  // magnitude (vector.rs:21-23)
-        const V3 dir = vnormalize(v);
-        s.o[0] = c.over.x; s.o[1] = c.over.y; s.o[2] = c.over.z;
-        s.d[0] = dir.x; s.d[1] = dir.y; s.d[2] = dir.z;
-        s.slot = (int)(i * L + l);
-        s.pad = 0;
-        a.shadows[sbase + l] = s;
-      }
+      if (L > 0) a.shadow_nodes[sbase / L] = (int32_t)i;  // its shadow rays are built by the shadow trace
       if (want_refl && rbase < a.cap_next) {
         const V3 rv = vreflect(d, c.normal);  // comps.reflectv (intersection.rs:101)
         WfRay r;
@@ -725,7 +733,7 @@ __global__ void wf_count_kinds(WfArgs a) {
 Wavefront::~Wavefront() {
   for (auto& g : gens_) {
     (void)hipFree(g.rays); (void)hipFree(g.hits); (void)hipFree(g.nodes); (void)hipFree(g.colors);
-    (void)hipFree(g.shadows); (void)hipFree(g.sflags);
+    (void)hipFree(g.shadow_nodes); (void)hipFree(g.sflags);
   }
   if (d_cnt_) (void)hipFree(d_cnt_);
   if (d_prim_) (void)hipFree(d_prim_);
@@ -792,10 +800,10 @@ hipError_t Wavefront::ensure_gen(size_t g, size_t rays, size_t n_lights) {
   }
   const size_t need_sh = std::max<size_t>(b.cap_rays * n_lights, 1);
   if (b.cap_shadows < need_sh) {
-    (void)hipFree(b.shadows); (void)hipFree(b.sflags);
-    b.shadows = nullptr; b.sflags = nullptr;
+    (void)hipFree(b.shadow_nodes); (void)hipFree(b.sflags);
+    b.shadow_nodes = nullptr; b.sflags = nullptr;
     b.cap_shadows = 0;
-    WF_CHECK(hipMalloc(&b.shadows, need_sh * sizeof(WfShadow)));
+    WF_CHECK(hipMalloc(&b.shadow_nodes, std::max<size_t>(b.cap_rays, 1) * sizeof(int32_t)));
     WF_CHECK(hipMalloc(&b.sflags, need_sh));
     b.cap_shadows = need_sh;
   }
@@ -959,7 +967,7 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     WF_CHECK(ensure_gen(g + 1, cap_next, L));
     WfArgs a{};
     WfGenBuf& B = gens_[g];
-    a.rays = B.rays; a.hits = B.hits; a.nodes = B.nodes; a.shadows = B.shadows; a.sflags = B.sflags;
+    a.rays = B.rays; a.hits = B.hits; a.nodes = B.nodes; a.shadow_nodes = B.shadow_nodes; a.sflags = B.sflags;
     a.colors = (g == 0 && !averaged) ? d_out : B.colors;
     a.aa = aa;
     a.rows = n0 / aa / (cam.hsize ? cam.hsize : 1);

@@ -46,13 +46,6 @@ struct WfNode {  // 72 B: what shade_hit needs from prepare_computations
   int32_t child_refr;
   int32_t pad;
 };
-struct WfShadow {  // 64 B
-  double o[3];
-  double d[3];
-  double dist;
-  int32_t slot;  // node * n_lights + light
-  int32_t pad;
-};
 struct PrimRec {  // primary rays share the origin: per diag sphere (s, o', c)
   double s[3];
   double op[3];
@@ -80,7 +73,7 @@ struct WfGenBuf {
   WfHit* hits = nullptr;
   WfNode* nodes = nullptr;
   double* colors = nullptr;
-  WfShadow* shadows = nullptr;
+  int32_t* shadow_nodes = nullptr;  // hit nodes of the generation (each casts one shadow ray per light)
   uint8_t* sflags = nullptr;
   size_t cap_rays = 0, cap_shadows = 0;
 };
@@ -91,7 +84,7 @@ struct WfArgs {
   WfHit* hits;
   WfNode* nodes;
   double* colors;       // colors_g (g >= 1) or the output (g == 0)
-  WfShadow* shadows;
+  int32_t* shadow_nodes;  // hit node indices; shadow ray j = (node j / L, light j % L)
   uint8_t* sflags;
   WfRay* next_rays;     // rays_{g+1}
   const double* child_colors;  // colors_{g+1}
