@@ -29,7 +29,8 @@ using namespace rtamd;
 namespace {
 
 thread_local std::string g_err;
-int g_bvh_leaf = 4;  // BVH leaf size at scene creation (tuning knob "bvh_leaf")
+int g_bvh_leaf = 4;     // BVH leaf size at scene creation (tuning knob "bvh_leaf")
+int g_bvh_ct = 100;     // SAH node-visit cost in percent of a sphere test (tuning knob "bvh_ct")
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -235,6 +236,11 @@ int rtamd_tuning_set(const char* key, int value) {
     rtamd::g_wf_accel = value != 0;
     return RT_OK;
   }
+  if (key && std::strcmp(key, "bvh_ct") == 0) {
+    if (value < 1 || value > 10000) return fail(RT_ERR_INVALID_ARGUMENT, "bvh_ct must be in [1, 10000]");
+    g_bvh_ct = value;
+    return RT_OK;
+  }
   if (key && std::strcmp(key, "bvh_leaf") == 0) {
     if (value < 1 || value > kBvhLeafMax) return fail(RT_ERR_INVALID_ARGUMENT, "bvh_leaf must be in [1, 127]");
     g_bvh_leaf = value;
@@ -371,7 +377,7 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   // exact-culling hierarchy over the diagonal spheres (reorders `diag`; keys
   // come from `meta`, so the order changes no result)
   int bvh_depth = 0;
-  std::vector<BvhNode> bvh = build_sphere_bvh(diag, g_bvh_leaf, &bvh_depth);
+  std::vector<BvhNode> bvh = build_sphere_bvh(diag, g_bvh_leaf, &bvh_depth, g_bvh_ct / 100.0);
   std::vector<LightRec> lrec(n_lights);
   for (size_t i = 0; i < n_lights; ++i)
     for (int c = 0; c < 3; ++c) { lrec[i].pos[c] = lights[i].position[c]; lrec[i].intensity[c] = lights[i].intensity[c]; }

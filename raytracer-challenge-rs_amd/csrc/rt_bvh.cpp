@@ -5,8 +5,8 @@
 // the group's box, group.rs:108-188; AABB slab test bounding_box.rs:95-136).
 // This builder plays that role for the flattened world, with two changes
 // that matter on the GPU:
-//   * binned-SAH splits over the sphere centroids (a wave traverses the tree
-//     together, so the cost of a node is the union over 64 rays), and
+//   * binned-SAH splits over the sphere centroids (32 bins, all three axes),
+//     and
 //   * every box is padded outward, so the traversal never culls a sphere the
 //     exhaustive loop would have hit: culling is exact by construction
 //     (DESIGN.md "Exact culling").
@@ -77,8 +77,9 @@ struct Builder {
   std::vector<double> cen;  // 3 per sphere
   std::vector<BvhNode> nodes;
   int leaf_size;
+  double trav_cost;  // SAH cost of a node visit relative to one sphere test
 
-  static constexpr int kBins = 16;
+  static constexpr int kBins = 32;
 
   // Returns the child code for spheres [b, e) at `depth`.
   int32_t build(int b, int e, int depth, Box* out_box) {
@@ -96,34 +97,44 @@ struct Builder {
       if (cb.hi[a] - cb.lo[a] > ext) { ext = cb.hi[a] - cb.lo[a]; axis = a; }
     int mid = -1;
     if (ext > 0 && depth < kBvhMaxDepth - 24) {
-      // binned SAH along the widest centroid axis
-      Box bin_box[kBins];
-      int bin_n[kBins] = {0};
-      auto bin_of = [&](int i) {
-        int k = (int)((cen[3 * i + axis] - cb.lo[axis]) / ext * kBins);
-        return std::min(std::max(k, 0), kBins - 1);
-      };
-      for (int i = b; i < e; ++i) {
-        const int k = bin_of(i);
-        ++bin_n[k];
-        bin_box[k].grow(box[i]);
-      }
+      // binned SAH over the three centroid axes: split cost C_t * A + sum(A_side * n_side)
       double best = INFINITY;
-      int best_k = -1;
-      for (int k = 1; k < kBins; ++k) {
-        Box l, r;
-        int nl = 0, nr = 0;
-        for (int j = 0; j < k; ++j) { if (bin_n[j]) { l.grow(bin_box[j]); nl += bin_n[j]; } }
-        for (int j = k; j < kBins; ++j) { if (bin_n[j]) { r.grow(bin_box[j]); nr += bin_n[j]; } }
-        if (!nl || !nr) continue;
-        const double c = l.area() * nl + r.area() * nr;
-        if (c < best) { best = c; best_k = k; }
+      int best_k = -1, best_axis = axis;
+      for (int ax = 0; ax < 3; ++ax) {
+        const double ex = cb.hi[ax] - cb.lo[ax];
+        if (!(ex > 0)) continue;
+        Box bin_box[kBins];
+        int bin_n[kBins] = {0};
+        for (int i = b; i < e; ++i) {
+          const int k = bin_index(i, ax, cb.lo[ax], ex);
+          ++bin_n[k];
+          bin_box[k].grow(box[i]);
+        }
+        Box right[kBins];
+        int nright[kBins + 1] = {0};
+        for (int k = kBins - 1; k >= 1; --k) {
+          right[k] = k + 1 < kBins ? right[k + 1] : Box{};
+          if (bin_n[k]) right[k].grow(bin_box[k]);
+          nright[k] = nright[k + 1] + bin_n[k];
+        }
+        Box l;
+        int nl = 0;
+        for (int k = 1; k < kBins; ++k) {
+          if (bin_n[k - 1]) { l.grow(bin_box[k - 1]); nl += bin_n[k - 1]; }
+          const int nr = nright[k];
+          if (!nl || !nr) continue;
+          const double c = l.area() * nl + right[k].area() * nr;
+          if (c < best) { best = c; best_k = k; best_axis = ax; }
+        }
       }
       if (best_k > 0) {
-        // leaf if splitting does not pay (traversal cost ~ one sphere test)
+        // leaf when splitting does not pay
         const double leaf_cost = bb.area() * n;
-        if (n <= kBvhLeafMax && best + bb.area() >= leaf_cost) return leaf(b, n);
-        mid = partition(b, e, [&](int i) { return bin_of(i) < best_k; });
+        if (n <= kBvhLeafMax && trav_cost * bb.area() + best >= leaf_cost) return leaf(b, n);
+        axis = best_axis;
+        ext = cb.hi[axis] - cb.lo[axis];
+        const double lo = cb.lo[axis];
+        mid = partition(b, e, [&](int i) { return bin_index(i, axis, lo, ext) < best_k; });
       }
     }
     if (mid <= b || mid >= e) {  // degenerate centroids or depth guard: median split
@@ -147,6 +158,10 @@ struct Builder {
   }
 
   int32_t leaf(int b, int n) { return -(1 + ((b << 7) | n)); }
+  int bin_index(int i, int ax, double lo, double ex) const {
+    const int k = (int)((cen[3 * i + ax] - lo) / ex * kBins);
+    return std::min(std::max(k, 0), kBins - 1);
+  }
 
   template <typename Pred>
   int partition(int b, int e, Pred left) {
@@ -194,7 +209,7 @@ static int tree_depth(const std::vector<BvhNode>& nodes, int32_t e) {
   return 1 + std::max(tree_depth(nodes, nodes[e].child[0]), tree_depth(nodes, nodes[e].child[1]));
 }
 
-std::vector<BvhNode> build_sphere_bvh(std::vector<SphereDiag>& spheres, int leaf_size, int* depth) {
+std::vector<BvhNode> build_sphere_bvh(std::vector<SphereDiag>& spheres, int leaf_size, int* depth, double trav_cost) {
   if (depth) *depth = 0;
   std::vector<BvhNode> out;
   const int n = (int)spheres.size();
@@ -202,7 +217,7 @@ std::vector<BvhNode> build_sphere_bvh(std::vector<SphereDiag>& spheres, int leaf
   // the leaf code stores the first index in 24 bits
   if (n >= (1 << 24)) return out;
   leaf_size = std::max(1, std::min(leaf_size, kBvhLeafMax));
-  Builder bd{spheres, {}, {}, {}, leaf_size};
+  Builder bd{spheres, {}, {}, {}, leaf_size, trav_cost};
   bd.box.resize(n);
   bd.cen.resize(3 * n);
   for (int i = 0; i < n; ++i) {

@@ -14,6 +14,8 @@ namespace rtamd {
 // empty when there are no spheres.
 // `depth` receives the most far children a near-first traversal keeps
 // pending (the number of internal nodes on the longest root-leaf path).
-std::vector<BvhNode> build_sphere_bvh(std::vector<SphereDiag>& spheres, int leaf_size, int* depth = nullptr);
+// `trav_cost`: SAH cost of a node visit relative to one sphere test.
+std::vector<BvhNode> build_sphere_bvh(std::vector<SphereDiag>& spheres, int leaf_size, int* depth = nullptr,
+                                      double trav_cost = 1.0);
 
 }  // namespace rtamd

@@ -438,7 +438,14 @@ __device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDia
   int sp = 0;
   auto pop = [&]() { return sp > 0 ? stk(--sp) : kBvhEmpty; };
   int e = (SHADOW && h.key >= 0 && h.t < t_shadow) || !has_bvh ? kBvhEmpty : 0;
+#ifdef RTAMD_DIAG
+  unsigned it = 0;  // diagnostic build: loop iterations of this lane vs the wave's
+  const unsigned n_tests0 = n_tests, n_boxes0 = n_boxes;
+#endif
   while (e != kBvhEmpty) {
+#ifdef RTAMD_DIAG
+    ++it;
+#endif
     if (e >= 0) {  // a node visit: both children's boxes, near child first by this lane's direction
       const BvhNode& nd = nodes[e];
       const double t_hi = SHADOW ? t_shadow : h.t;
@@ -468,6 +475,13 @@ __device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDia
       e = pop();
     }
   }
+#ifdef RTAMD_DIAG
+  // diagnostic build: tests = this lane's loop iterations, boxes = the wave's (max over its lanes)
+  unsigned mx = it;
+  for (int off = 32; off > 0; off >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, off, 64));
+  n_tests = n_tests0 + it;
+  n_boxes = n_boxes0 + mx;
+#endif
 }
 
 // LANE == 5: the block stages the hierarchy and the sphere records in LDS

@@ -10,11 +10,17 @@ from rtamd import scenes
 args = [x for x in sys.argv[1:] if "=" in x]
 scene = "c5" if "--c5" in sys.argv else "c3"
 knobs = [(k, [int(v) for v in vs.split(",")]) for k, vs in (x.split("=") for x in args)]
-if scene == "c5":
-    w, cam, depth = scenes.c5(1024, 1024)
-else:
-    w, cam, depth = scenes.c3()
-w.upload(0)
+SCENE_KNOBS = ("bvh_leaf", "bvh_ct")  # applied at scene creation: one world per value
+
+
+def make_world():
+    if scene == "c5":
+        return scenes.c5(1024, 1024)
+    return scenes.c3()
+
+
+worlds = {}
+w, cam, depth = make_world()
 buf = torch.empty((cam.vsize, cam.hsize, 3), dtype=torch.float64, device="cuda")
 s = torch.cuda.current_stream().cuda_stream
 combos = list(itertools.product(*[vs for _, vs in knobs]))
@@ -23,6 +29,11 @@ for r in range(4):
     for combo in combos:
         for (k, _), v in zip(knobs, combo):
             rtamd._rtamd._tuning_set(k, v)
+        skey = tuple(v for (k, _), v in zip(knobs, combo) if k in SCENE_KNOBS)
+        if skey not in worlds:
+            worlds[skey] = make_world()[0]
+            worlds[skey].upload(0)
+        w = worlds[skey]
         rtamd._rtamd._wf_profile(w, 1, False)
         for _ in range(3):
             cam.render_shard_device(w, depth, 8, 0, 1, buf.data_ptr(), s, False)
