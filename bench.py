@@ -236,8 +236,8 @@ def roofline(prof, W, H, a, n, ref_work, frame_ms):
     if os.path.exists(a.pmc_summary):
         try:
             pm = json.load(open(a.pmc_summary))
-            if (pm.get("width"), pm.get("height"), pm.get("spheres"), pm.get("n_gpus"),
-                    pm.get("kernel_class")) == (W, H, a.spheres, n, dom):
+            if (pm.get("width"), pm.get("height"), pm.get("spheres"), pm.get("n_gpus"), pm.get("kernel_class"),
+                    pm.get("traversal")) == (W, H, a.spheres, n, dom, "bvh" if prof["bvh"] else "exhaustive"):
                 traffic, traffic_src = pm.get("hbm_bytes_per_frame"), os.path.relpath(a.pmc_summary, REPO)
         except Exception:
             pass

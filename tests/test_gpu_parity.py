@@ -195,6 +195,22 @@ def test_c3_full_size_sampled_rows(rt, oracle):
     _compare_frame(rt, oracle, w, cam, depth, rows=rows)
 
 
+def test_c5_sampled_rows(rt, oracle):
+    """C5 (4 planes + 9996 spheres, 2 lights, depth 8) at 384x384 on the GPU;
+    oracle on a few rows (10k-object intersection lists on the CPU)."""
+    from rtamd import scenes
+    w, cam, depth = scenes.c5(384, 384)
+    _compare_frame(rt, oracle, w, cam, depth, rows=[0, 150, 191, 300])
+
+
+def test_c5_fast_path_bitwise(rt):
+    from rtamd import scenes
+    w, cam, depth = scenes.c5(256, 256)
+    fast, _ = cam.render(w, depth, want_stats=False)
+    exact, _ = cam.render(w, depth, want_stats=True)
+    assert fast.to_numpy().tobytes() == exact.to_numpy().tobytes()
+
+
 def test_shards_reassemble_bitwise(rt):
     """Interleaved row-block shards (the multi-GPU partition) rendered one at a
     time into device buffers reassemble into the single-launch frame exactly."""

@@ -16,4 +16,4 @@ run p3 --pmc SQC_DCACHE_HITS SQC_DCACHE_MISSES SQC_DCACHE_REQ SQ_ACTIVE_INST_SCA
 run p4 --pmc FETCH_SIZE && \
 run p5 --pmc WRITE_SIZE && \
 run p6 --pmc TCC_HIT_sum TCC_MISS_sum && \
-python tools/pmc_summary.py $OUT/pmc_summary.json --dominant closest $OUT/p1 $OUT/p2 $OUT/p3 $OUT/p4 $OUT/p5 $OUT/p6 > /dev/null && echo "summary ok" | tee -a $OUT/steps.log
+python tools/pmc_summary.py $OUT/pmc_summary.json --dominant closest --traversal ${TRAVERSAL:-bvh} $OUT/p1 $OUT/p2 $OUT/p3 $OUT/p4 $OUT/p5 $OUT/p6 > /dev/null && echo "summary ok" | tee -a $OUT/steps.log

@@ -44,6 +44,7 @@ ap.add_argument("--height", type=int, default=1080)
 ap.add_argument("--spheres", type=int, default=1000)
 ap.add_argument("--n-gpus", type=int, default=1)
 ap.add_argument("--dominant", default="closest")
+ap.add_argument("--traversal", default="bvh", help="bvh (fast path) or exhaustive")
 a = ap.parse_args()
 
 tot = collections.defaultdict(lambda: collections.defaultdict(float))
@@ -61,7 +62,7 @@ for d in a.dirs:
             tot[c][r["Counter_Name"]] += float(r["Counter_Value"])
         frames[f] = len(seen)
 nf = max(frames.values()) if frames else 0
-res = {"width": a.width, "height": a.height, "spheres": a.spheres, "n_gpus": a.n_gpus,
+res = {"width": a.width, "height": a.height, "spheres": a.spheres, "n_gpus": a.n_gpus, "traversal": a.traversal,
        "frames_per_pass": nf, "per_frame": {}}
 for c, cs in tot.items():
     pf = {k: v / max(nf, 1) for k, v in cs.items()}
