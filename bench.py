@@ -127,14 +127,19 @@ def main():
     if a.exhaustive:
         rtamd._rtamd._tuning_set("accel", 0)
     W, H, B = cam.hsize, cam.vsize, a.row_block
-    fa = FrameAssembler(H, W, B, rank, n, dev)  # interleaved row blocks + one RCCL gather
+    # interleaved row blocks + one RCCL gather per frame; two shard slots so that
+    # frame s's gather overlaps frame s+1's render (rtamd.distributed.FrameAssembler)
+    fa = FrameAssembler(H, W, B, rank, n, dev, slots=2)
     assert len(fa.rows) == rtamd.shard_rows(H, B, rank, n)
     shard = fa.shard
     stream = torch.cuda.current_stream()
+    frame_no = [0]
 
     def step():
-        cam.render_shard_device(world, depth, B, rank, n, shard.data_ptr(), stream.cuda_stream, False)
-        fa.assemble()  # n == 1: the shard buffer already is the row-major canvas
+        s = frame_no[0]
+        cam.render_shard_device(world, depth, B, rank, n, fa.slot(s).data_ptr(), stream.cuda_stream, False)
+        fa.submit(s)  # n == 1: the shard buffer already is the row-major canvas
+        frame_no[0] = s + 1
 
     # exact work counters of one frame (deterministic), from a counted warm-up launch
     # (this first launch also sizes the wavefront queues of this camera/shard)
@@ -151,6 +156,7 @@ def main():
                 + SURVEY_OPS_ROOTS * float(counts[6]))
     for _ in range(a.warmup):
         step()
+    fa.flush()
     torch.cuda.synchronize()
 
     # Timed region. The library records HIP events around every kernel launch
@@ -162,6 +168,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
+    fa.flush()  # the last frame's gather + un-interleave are inside the timed region
     torch.cuda.synchronize()
     if n > 1:
         dist.barrier()

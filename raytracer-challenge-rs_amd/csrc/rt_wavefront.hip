@@ -368,6 +368,18 @@ __device__ __forceinline__ bool slab_hit(P lo, P hi, V3 o, V3 inv, double t_hi) 
   const double tmax = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmax(z0, z1));
   return tmin <= tmax && tmax >= 0.0 && tmin <= t_hi;
 }
+// Same test, also returning the entry distance (child ordering only: the
+// culling decision is the one above).
+template <typename P>
+__device__ __forceinline__ bool slab_hit(P lo, P hi, V3 o, V3 inv, double t_hi, double& t_in) {
+  const double x0 = ((double)lo[0] - o.x) * inv.x, x1 = ((double)hi[0] - o.x) * inv.x;
+  const double y0 = ((double)lo[1] - o.y) * inv.y, y1 = ((double)hi[1] - o.y) * inv.y;
+  const double z0 = ((double)lo[2] - o.z) * inv.z, z1 = ((double)hi[2] - o.z) * inv.z;
+  const double tmin = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmin(z0, z1));
+  const double tmax = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmax(z0, z1));
+  t_in = tmin;
+  return tmin <= tmax && tmax >= 0.0 && tmin <= t_hi;
+}
 
 template <bool PRIMARY, bool SHADOW>
 __device__ __forceinline__ void bvh_trace(const DevScene& sc, cPrimRec prim, int* stk, V3 o, V3 d, double t_shadow,
@@ -446,16 +458,16 @@ __device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDia
 #ifdef RTAMD_DIAG
     ++it;
 #endif
-    if (e >= 0) {  // a node visit: both children's boxes, near child first by this lane's direction
+    if (e >= 0) {  // a node visit: both children's boxes, the one entered first visited first
       const BvhNode& nd = nodes[e];
       const double t_hi = SHADOW ? t_shadow : h.t;
       const int c0 = nd.child[0], c1 = nd.child[1];
-      const bool h0 = slab_hit(nd.lo[0], nd.hi[0], o, inv, t_hi);
-      const bool h1 = c1 != kBvhEmpty && slab_hit(nd.lo[1], nd.hi[1], o, inv, t_hi);
+      double t0, t1;
+      const bool h0 = slab_hit(nd.lo[0], nd.hi[0], o, inv, t_hi, t0);
+      const bool h1 = c1 != kBvhEmpty && slab_hit(nd.lo[1], nd.hi[1], o, inv, t_hi, t1);
       n_boxes += 2;
       if (h0 && h1) {
-        const int axis = nd.axis;
-        const bool flip = (axis == 0 ? d.x : axis == 1 ? d.y : d.z) < 0.0;
+        const bool flip = t1 < t0;
         stk(sp++) = flip ? c0 : c1;
         e = flip ? c1 : c0;
       } else {

@@ -19,17 +19,28 @@ def shard_row_ids(height, row_block, shard, n_shards):
 
 
 class FrameAssembler:
-    """Shard buffers + the gather/un-interleave step of one (H, W) frame."""
+    """Shard buffers + the gather/un-interleave step of one (H, W) frame.
 
-    def __init__(self, height, width, row_block, rank, n_shards, device, dtype=torch.float64):
+    `slots` > 1 pipelines consecutive frames: frame s renders into shard slot
+    s % slots, `submit(s)` issues its gather asynchronously and only then
+    completes frame s-1 (wait + un-interleave), so the gather of one frame
+    runs (on RCCL's stream) while the next frame renders. Stream order keeps
+    it safe: a slot's shard is rendered again only after the stream has
+    waited on that slot's previous gather, and a slot's gather list is
+    overwritten only by a gather issued after the un-interleave that read it.
+    """
+
+    def __init__(self, height, width, row_block, rank, n_shards, device, dtype=torch.float64, slots=1):
         self.H, self.W, self.B = height, width, row_block
         self.rank, self.n = rank, n_shards
         self.rows = shard_row_ids(height, row_block, rank, n_shards)
         self.max_rows = max(len(shard_row_ids(height, row_block, s, n_shards)) for s in range(n_shards))
         # padded so that every rank sends the same element count
-        self.shard = torch.zeros((self.max_rows, width, 3), dtype=dtype, device=device)
+        self.shards = [torch.zeros((self.max_rows, width, 3), dtype=dtype, device=device) for _ in range(slots)]
+        self.shard = self.shards[0]
+        self._pending = None  # (work, slot) of the last submitted, not yet completed frame
         if rank == 0:
-            self.gathered = [torch.empty_like(self.shard) for _ in range(n_shards)]
+            self.gathered = [[torch.empty_like(self.shard) for _ in range(n_shards)] for _ in range(slots)]
             self.canvas = torch.empty((height, width, 3), dtype=dtype, device=device)
             src, dst = [], []
             for s in range(n_shards):
@@ -39,13 +50,52 @@ class FrameAssembler:
             self.src_idx = torch.tensor(src, device=device)
             self.dst_idx = torch.tensor(dst, device=device)
 
+    def slot(self, step):
+        """Shard buffer frame `step` renders into."""
+        return self.shards[step % len(self.shards)]
+
+    def _gather(self, slot, group, async_op):
+        return dist.gather(self.shards[slot], self.gathered[slot] if self.rank == 0 else None, dst=0,
+                           group=group, async_op=async_op)
+
+    def _unweave(self, slot):
+        self.canvas.index_copy_(0, self.dst_idx, torch.cat(self.gathered[slot]).index_select(0, self.src_idx))
+        return self.canvas
+
     def assemble(self, group=None):
         """Gather all shards to rank 0; returns the (H, W, 3) canvas on rank 0,
         None elsewhere. With one shard the shard buffer already is the canvas."""
         if self.n == 1:
             return self.shard[: self.H]
-        dist.gather(self.shard, self.gathered if self.rank == 0 else None, dst=0, group=group)
+        self._gather(0, group, False)
         if self.rank != 0:
             return None
-        self.canvas.index_copy_(0, self.dst_idx, torch.cat(self.gathered).index_select(0, self.src_idx))
-        return self.canvas
+        return self._unweave(0)
+
+    def submit(self, step, group=None):
+        """Issue frame `step`'s gather, then complete frame step-1. Returns
+        frame step-1's canvas on rank 0 (None elsewhere or if there is none),
+        valid until the next submit."""
+        if self.n == 1:
+            prev, self._pending = self._pending, (None, step % len(self.shards))
+            return None if prev is None else self.shards[prev[1]][: self.H]
+        work = self._gather(step % len(self.shards), group, True)
+        done = self._complete()
+        self._pending = (work, step % len(self.shards))
+        return done
+
+    def flush(self):
+        """Complete the last submitted frame; its canvas on rank 0."""
+        if self.n == 1:
+            prev, self._pending = self._pending, None
+            return None if prev is None else self.shards[prev[1]][: self.H]
+        done = self._complete()
+        self._pending = None
+        return done
+
+    def _complete(self):
+        if self._pending is None:
+            return None
+        work, slot = self._pending
+        work.wait()  # NCCL: the current stream waits on the gather (the host does not block)
+        return self._unweave(slot) if self.rank == 0 else None

@@ -57,6 +57,60 @@ def test_gloo_frame_assembly(tmp_path, world_size, row_block):
     assert np.array_equal(got, ref)
 
 
+def _pipeline_worker(rank, world_size, port, row_block, n_frames, out_path):
+    """Frame f is golden + f; frames go through the 2-slot pipeline."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world_size)
+    try:
+        from rtamd.distributed import FrameAssembler
+        ref = torch.from_numpy(np.load(os.path.join(HERE, "golden", "c3_64x36_s200.npz"))["canvas"])
+        H, W = ref.shape[:2]
+        fa = FrameAssembler(H, W, row_block, rank, world_size, torch.device("cpu"), slots=2)
+        done = []
+        for f in range(n_frames):
+            buf = fa.slot(f)
+            buf.fill_(-1.0)
+            buf[: len(fa.rows)] = ref[fa.rows] + f
+            c = fa.submit(f)
+            if f == 0 or rank != 0:
+                assert c is None
+            else:
+                done.append(c.clone())
+        c = fa.flush()
+        if rank == 0:
+            done.append(c.clone())
+            np.save(out_path, torch.stack(done).numpy())
+        else:
+            assert c is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world_size,row_block", [(2, 8), (3, 5)])
+def test_gloo_pipelined_frames(tmp_path, world_size, row_block):
+    """The 2-slot pipeline bench.py runs at N>1: every frame comes out whole
+    and in order, one submit behind."""
+    out = str(tmp_path / "frames.npy")
+    mp.spawn(_pipeline_worker, args=(world_size, _free_port(), row_block, 5, out), nprocs=world_size, join=True)
+    got = np.load(out)
+    ref = np.load(os.path.join(HERE, "golden", "c3_64x36_s200.npz"))["canvas"]
+    assert got.shape == (5,) + ref.shape
+    for f in range(5):
+        assert np.array_equal(got[f], ref + f), f
+
+
+def test_single_shard_pipeline():
+    from rtamd.distributed import FrameAssembler
+    fa = FrameAssembler(10, 4, 8, 0, 1, torch.device("cpu"), slots=2)
+    outs = []
+    for f in range(3):
+        fa.slot(f).fill_(f)
+        c = fa.submit(f)
+        outs.append(None if c is None else float(c[0, 0, 0]))
+    outs.append(float(fa.flush()[9, 3, 2]))
+    assert outs == [None, 0.0, 1.0, 2.0]
+
+
 def test_shard_rows_partition(rt):
     from rtamd.distributed import shard_row_ids
     for H, B, n in [(1080, 8, 8), (1080, 8, 3), (37, 5, 4), (4, 8, 8), (1, 1, 2)]:
