@@ -29,8 +29,8 @@ using namespace rtamd;
 namespace {
 
 thread_local std::string g_err;
-int g_bvh_leaf = 4;     // BVH leaf size at scene creation (tuning knob "bvh_leaf")
-int g_bvh_ct = 100;     // SAH node-visit cost in percent of a sphere test (tuning knob "bvh_ct")
+int g_bvh_leaf = 2;     // BVH leaf size at scene creation (tuning knob "bvh_leaf")
+int g_bvh_ct = 70;      // SAH node-visit cost in percent of a sphere test (tuning knob "bvh_ct")
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -197,7 +197,8 @@ int rtamd_wf_profile(const rt_scene* cs, int enable, double out[25]) {
   if (!cs) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
   rt_scene* s = const_cast<rt_scene*>(cs);
   std::lock_guard<std::mutex> lk(s->mu);
-  if (enable >= 0) s->wf.set_profiling(enable != 0);
+  // enable: 0 off, 1 every kernel class, >= 2: (class mask << 1) | 1 (bench.py times one class)
+  if (enable >= 0) s->wf.set_profiling(enable != 0, enable > 1 ? (enable >> 1) : (1 << WF_NCLASS) - 1);
   if (out) {
     RT_HIP(hipSetDevice(s->device));
     WfProfile p;

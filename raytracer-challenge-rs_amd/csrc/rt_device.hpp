@@ -380,6 +380,18 @@ __device__ __forceinline__ double schlick(V3 eyev, V3 normal, double n1, double 
   return r0 + (1.0 - r0) * x5;
 }
 
+// `v % 2.0 == 0.0` (Rust's f64 `%` is fmod) for an integer-valued or
+// non-finite v, without the fmod loop: binary64 values of magnitude >= 2^53
+// are even integers, below that the integer conversion is exact.
+__device__ __forceinline__ bool fmod2_is_zero(double v) {
+  if (!(fabs(v) < 0x1p53)) return !isnan(v) && !isinf(v);
+  return (((long long)v) & 1) == 0;
+}
+
+// componentwise select (a select between whole structs becomes a scratch
+// copy indexed by the condition)
+__device__ __forceinline__ V3 vsel(bool c, V3 a, V3 b) { return v3(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z); }
+
 // Pattern::color_at_shape (pattern/mod.rs:39-49) and the five kinds.
 __device__ __forceinline__ V3 pattern_color(const ShadeRec& s, V3 world_point) {
   const V3 op = m34_point(s.inv, world_point);
@@ -390,7 +402,7 @@ __device__ __forceinline__ V3 pattern_color(const ShadeRec& s, V3 world_point) {
     case 0:  // test_pattern.rs:7-9
       return pp;
     case 1:  // stripe.rs:14-20
-      return fmod(floor(pp.x), 2.0) == 0.0 ? a : b;
+      return vsel(fmod2_is_zero(floor(pp.x)), a, b);
     case 2: {  // gradient.rs:14-18
       const V3 distance = vsub(b, a);
       const double fraction = pp.x - floor(pp.x);
@@ -398,7 +410,7 @@ __device__ __forceinline__ V3 pattern_color(const ShadeRec& s, V3 world_point) {
     }
     case 3: {  // ring.rs:14-21
       const double distance = floor(sqrt(pp.x * pp.x + pp.z * pp.z));
-      return fmod(distance, 2.0) == 0.0 ? a : b;
+      return vsel(fmod2_is_zero(distance), a, b);
     }
     default: {  // checkers.rs:14-21: `as isize` (saturating) then % 2
       const double distance = floor(pp.x) + floor(pp.y) + floor(pp.z);
@@ -406,8 +418,8 @@ __device__ __forceinline__ V3 pattern_color(const ShadeRec& s, V3 world_point) {
       if (isnan(distance)) even = true;                          // NaN as isize = 0
       else if (distance >= 9223372036854775808.0) even = false;  // isize::MAX is odd
       else if (distance < -9223372036854775808.0) even = true;   // isize::MIN is even
-      else even = fmod(distance, 2.0) == 0.0;                   // exact integer parity
-      return even ? a : b;
+      else even = fmod2_is_zero(distance);                      // exact integer parity
+      return vsel(even, a, b);
     }
   }
 }

@@ -10,6 +10,7 @@
 // operations, so bit-identical) and each primary sphere test drops from 28 to
 // 16 f64 operations.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cstring>
@@ -354,39 +355,68 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow(DevScene sc, 
 typedef const RT_CONST BvhNode* cBvhNode;
 typedef const RT_CONST PrimRec* cPrimRec;
 
-__device__ __forceinline__ double slab_inv(double d) {
-  // 1/d, with a huge finite value for d == 0 (no NaN from 0 * inf)
-  return d == 0.0 ? copysign(1e300, d) : 1.0 / d;
+// The per-lane traversal's slab test runs in binary32 on an interval that is
+// widened to contain the exact (real-arithmetic) one; DESIGN.md §5.2 has the
+// error bound. Per ray and axis: inv = 1/d, and the plane constants
+// c = o*inv -/+ delta with delta = 2^-20 |inv| (M + |o|), where M bounds every
+// box coordinate on that axis (the root's children); the computed entry
+// (exit) distance fma(corner, inv, -c) then never exceeds (falls short of)
+// the exact one: its rounding error is below 2^-23 |inv| (M + |o|) = delta/8.
+// An axis whose direction is (nearly) zero or whose origin is huge / NaN is
+// not used for culling at all (interval (-inf, +inf)).
+struct SlabRay {
+  float inv[3], c_lo[3], c_hi[3];
+};
+__device__ __forceinline__ SlabRay slab_ray(V3 o, V3 d, const float* M) {
+  SlabRay r;
+  const double oa[3] = {o.x, o.y, o.z}, da[3] = {d.x, d.y, d.z};
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    if (fabs(da[a]) >= 0x1p-60 && fabs(oa[a]) <= 0x1p60 && M[a] <= 0x1p60f) {  // NaN fails
+      const double inv = 1.0 / da[a];
+      const double oinv = oa[a] * inv;
+      const double delta = 0x1p-20 * fabs(inv) * ((double)M[a] + fabs(oa[a]));
+      const float on = (float)(oinv + delta), of = (float)(oinv - delta);
+      r.inv[a] = (float)inv;
+      r.c_lo[a] = inv >= 0.0 ? on : of;  // the lo plane is the entry plane when inv >= 0
+      r.c_hi[a] = inv >= 0.0 ? of : on;
+    } else {
+      r.inv[a] = 0.0f;
+      r.c_lo[a] = INFINITY;
+      r.c_hi[a] = -INFINITY;
+    }
+  }
+  return r;
 }
+// binary32 upper bound of a non-negative binary64 distance
+__device__ __forceinline__ float f32_up(double x) {
+  const float f = (float)x;
+  return (double)f < x ? __int_as_float(__float_as_int(f) + 1) : f;
+}
+// max(entry, 0) <= min(exit, t_hi): the ray may meet the box within [0, t_hi]
+// (t_hi >= 0). `t_in` = the widened entry distance (child ordering only).
 template <typename P>  // P: constant-address (scalar loads) or generic (per-lane loads) float pointer
-__device__ __forceinline__ bool slab_hit(P lo, P hi, V3 o, V3 inv, double t_hi) {
-  // binary32 box corners widened exactly to binary64; the test runs in binary64
-  const double x0 = ((double)lo[0] - o.x) * inv.x, x1 = ((double)hi[0] - o.x) * inv.x;
-  const double y0 = ((double)lo[1] - o.y) * inv.y, y1 = ((double)hi[1] - o.y) * inv.y;
-  const double z0 = ((double)lo[2] - o.z) * inv.z, z1 = ((double)hi[2] - o.z) * inv.z;
-  const double tmin = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmin(z0, z1));
-  const double tmax = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmax(z0, z1));
-  return tmin <= tmax && tmax >= 0.0 && tmin <= t_hi;
-}
-// Same test, also returning the entry distance (child ordering only: the
-// culling decision is the one above).
-template <typename P>
-__device__ __forceinline__ bool slab_hit(P lo, P hi, V3 o, V3 inv, double t_hi, double& t_in) {
-  const double x0 = ((double)lo[0] - o.x) * inv.x, x1 = ((double)hi[0] - o.x) * inv.x;
-  const double y0 = ((double)lo[1] - o.y) * inv.y, y1 = ((double)hi[1] - o.y) * inv.y;
-  const double z0 = ((double)lo[2] - o.z) * inv.z, z1 = ((double)hi[2] - o.z) * inv.z;
-  const double tmin = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmin(z0, z1));
-  const double tmax = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmax(z0, z1));
+__device__ __forceinline__ bool slab_hit32(P lo, P hi, const SlabRay& r, float t_hi, float& t_in) {
+  const float x0 = fmaf(lo[0], r.inv[0], -r.c_lo[0]), x1 = fmaf(hi[0], r.inv[0], -r.c_hi[0]);
+  const float y0 = fmaf(lo[1], r.inv[1], -r.c_lo[1]), y1 = fmaf(hi[1], r.inv[1], -r.c_hi[1]);
+  const float z0 = fmaf(lo[2], r.inv[2], -r.c_lo[2]), z1 = fmaf(hi[2], r.inv[2], -r.c_hi[2]);
+  const float tmin = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), 0.0f));
+  const float tmax = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), t_hi));
   t_in = tmin;
-  return tmin <= tmax && tmax >= 0.0 && tmin <= t_hi;
+  return tmin <= tmax;
 }
 
 template <bool PRIMARY, bool SHADOW>
 __device__ __forceinline__ void bvh_trace(const DevScene& sc, cPrimRec prim, int* stk, V3 o, V3 d, double t_shadow,
                                           Hit& h, unsigned& n_disc, unsigned& n_tests, unsigned& n_boxes) {
   hit_init(h);
-  const V3 inv = v3(slab_inv(d.x), slab_inv(d.y), slab_inv(d.z));
   const cBvhNode nodes = (cBvhNode)sc.bvh;
+  float M[3];
+  for (int a = 0; a < 3; ++a)
+    M[a] = fmaxf(fmaxf(fabsf(nodes->lo[0][a]), fabsf(nodes->hi[0][a])),
+                 fmaxf(fabsf(nodes->lo[1][a]), fabsf(nodes->hi[1][a])));
+  const SlabRay sr = slab_ray(o, d, M);
+  const float t_sh = SHADOW ? f32_up(t_shadow) : 0.0f;
   const cSphereDiag sd = (cSphereDiag)sc.sph_diag;
   int sp = 1;
   stk[0] = 0;
@@ -413,10 +443,11 @@ __device__ __forceinline__ void bvh_trace(const DevScene& sc, cPrimRec prim, int
       continue;
     }
     const cBvhNode nd = nodes + e;
-    const double t_hi = SHADOW ? t_shadow : h.t;
+    const float t_hi = SHADOW ? t_sh : f32_up(h.t);
     const int c0 = nd->child[0], c1 = nd->child[1];
-    const bool h0 = slab_hit(nd->lo[0], nd->hi[0], o, inv, t_hi);
-    const bool h1 = c1 != kBvhEmpty && slab_hit(nd->lo[1], nd->hi[1], o, inv, t_hi);
+    float t0, t1;
+    const bool h0 = slab_hit32(nd->lo[0], nd->hi[0], sr, t_hi, t0);
+    const bool h1 = c1 != kBvhEmpty && slab_hit32(nd->lo[1], nd->hi[1], sr, t_hi, t1);
     n_boxes += 2;
     const bool any0 = __any(h0), any1 = __any(h1);
     // push the far child first so the near one (by the lead lane's direction) pops first
@@ -441,10 +472,11 @@ __device__ __forceinline__ void bvh_trace(const DevScene& sc, cPrimRec prim, int
 // memory or at the block's LDS copy. `h` arrives initialised (it may already
 // hold the planes' nearest hit, which tightens the culling).
 template <bool SHADOW, bool LDS_STACK>
-__device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDiag* sd, bool has_bvh, V3 o, V3 d,
-                                           double t_shadow, Hit& h, unsigned& n_disc, unsigned& n_tests,
+__device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDiag* sd, const float* M, bool has_bvh,
+                                           V3 o, V3 d, double t_shadow, Hit& h, unsigned& n_disc, unsigned& n_tests,
                                            unsigned& n_boxes, int* lds) {
-  const V3 inv = v3(slab_inv(d.x), slab_inv(d.y), slab_inv(d.z));
+  const SlabRay sr = slab_ray(o, d, M);
+  float t_hi = f32_up(SHADOW ? t_shadow : h.t);
   int pstk[LDS_STACK ? 1 : kBvhMaxDepth + 4];
   auto stk = [&](int k) -> int& { if constexpr (LDS_STACK) return lds[k * kTraceBlock]; else return pstk[k]; };
   int sp = 0;
@@ -460,11 +492,10 @@ __device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDia
 #endif
     if (e >= 0) {  // a node visit: both children's boxes, the one entered first visited first
       const BvhNode& nd = nodes[e];
-      const double t_hi = SHADOW ? t_shadow : h.t;
       const int c0 = nd.child[0], c1 = nd.child[1];
-      double t0, t1;
-      const bool h0 = slab_hit(nd.lo[0], nd.hi[0], o, inv, t_hi, t0);
-      const bool h1 = c1 != kBvhEmpty && slab_hit(nd.lo[1], nd.hi[1], o, inv, t_hi, t1);
+      float t0, t1;
+      const bool h0 = slab_hit32(nd.lo[0], nd.hi[0], sr, t_hi, t0);
+      const bool h1 = c1 != kBvhEmpty && slab_hit32(nd.lo[1], nd.hi[1], sr, t_hi, t1);
       n_boxes += 2;
       if (h0 && h1) {
         const bool flip = t1 < t0;
@@ -483,7 +514,11 @@ __device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDia
                             [&] { return (int)r.meta; }, h, n_disc);
       }
       n_tests += (unsigned)cnt;
-      if (SHADOW && h.key >= 0 && h.t < t_shadow) break;  // shadowed: done
+      if constexpr (SHADOW) {
+        if (h.key >= 0 && h.t < t_shadow) break;  // shadowed: done
+      } else {
+        t_hi = f32_up(h.t);
+      }
       e = pop();
     }
   }
@@ -497,21 +532,24 @@ __device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDia
 }
 
 // LANE == 5: the block stages the hierarchy and the sphere records in LDS
-// (dynamic shared memory: [stack kLaneLdsDepth x kTraceBlock ints][nodes][spheres]).
-__host__ __device__ inline size_t lane_lds_bytes(int n_bvh, int n_diag) {
-  return (size_t)kLaneLdsDepth * kTraceBlock * 4 + (size_t)n_bvh * sizeof(BvhNode) + (size_t)n_diag * sizeof(SphereDiag);
+// (dynamic shared memory: [stack bvh_depth x kTraceBlock ints][nodes][spheres];
+// a lane pushes at most one entry per tree level).
+__host__ __device__ inline size_t lane_stack_bytes(int depth) { return (size_t)(depth > 0 ? depth : 1) * kTraceBlock * 4; }
+__host__ __device__ inline size_t lane_lds_bytes(const DevScene& sc) {
+  return lane_stack_bytes(sc.bvh_depth) + (size_t)sc.n_bvh * sizeof(BvhNode) + (size_t)sc.n_diag * sizeof(SphereDiag);
 }
 struct LaneScene {
   const BvhNode* nodes;
   const SphereDiag* sd;
   int* stack;
+  float M[3];  // bound on |box coordinate| per axis (slab_ray)
 };
 template <int LANE>
 __device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, int* static_stack, unsigned char* dyn) {
   LaneScene ls{sc.bvh, sc.sph_diag, static_stack};
   if constexpr (LANE == 5) {
     int* stack = (int*)dyn;
-    BvhNode* nodes = (BvhNode*)(dyn + (size_t)kLaneLdsDepth * kTraceBlock * 4);
+    BvhNode* nodes = (BvhNode*)(dyn + lane_stack_bytes(sc.bvh_depth));
     SphereDiag* sd = (SphereDiag*)((unsigned char*)nodes + (size_t)sc.n_bvh * sizeof(BvhNode));
     const uint4* gn = (const uint4*)sc.bvh;
     uint4* ln = (uint4*)nodes;
@@ -523,6 +561,14 @@ __device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, int* static_
     ls.nodes = nodes;
     ls.sd = sd;
     ls.stack = stack + threadIdx.x;
+  }
+  for (int a = 0; a < 3; ++a) {
+    float m = 0.0f;
+    if (sc.n_bvh > 0) {  // the root's two child boxes contain every box below them
+      const BvhNode& r = ls.nodes[0];
+      m = fmaxf(fmaxf(fabsf(r.lo[0][a]), fabsf(r.hi[0][a])), fmaxf(fabsf(r.lo[1][a]), fabsf(r.hi[1][a])));
+    }
+    ls.M[a] = m;
   }
   return ls;
 }
@@ -543,7 +589,7 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest_bvh(DevScene
     if constexpr (LANE && !PRIMARY) {
       hit_init(h);
       trace_rest<false, QUADS>(sc, o, d, h, n_disc);  // planes first: an early nearest hit tightens the culling
-      lane_trace<false, LDS_STACK>(ls.nodes, ls.sd, sc.n_bvh > 0, o, d, 0.0, h, n_disc, n_tests, n_boxes, ls.stack);
+      lane_trace<false, LDS_STACK>(ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, n_disc, n_tests, n_boxes, ls.stack);
     } else {
       bvh_trace<PRIMARY, false>(sc, (cPrimRec)a.prim, stk, o, d, 0.0, h, n_disc, n_tests, n_boxes);
       trace_rest<false, QUADS>(sc, o, d, h, n_disc);
@@ -579,7 +625,7 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow_bvh(DevScene 
     if constexpr (LANE) {
       hit_init(h);
       trace_rest<true, QUADS>(sc, o, d, h, n_disc);  // planes first: any hit before the light ends the ray
-      lane_trace<true, LDS_STACK>(ls.nodes, ls.sd, sc.n_bvh > 0, o, d, dist, h, n_disc, n_tests, n_boxes, ls.stack);
+      lane_trace<true, LDS_STACK>(ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, dist, h, n_disc, n_tests, n_boxes, ls.stack);
     } else {
       bvh_trace<false, true>(sc, nullptr, stk, o, d, dist, h, n_disc, n_tests, n_boxes);
       if (__any(!(h.key >= 0 && h.t < dist))) trace_rest<true, QUADS>(sc, o, d, h, n_disc);
@@ -756,6 +802,13 @@ __global__ void wf_count_kinds(WfArgs a) {
 }
 
 // ---------------------------------------------------------- host side
+// Per-launch profiling: while a kernel class is being timed (Wavefront::pmark)
+// its launch carries the start/stop events in the dispatch itself
+// (hipExtLaunchKernel, WF_LAUNCH), so no event packets sit between the kernels
+// and a profiled frame runs like an unprofiled one.
+static thread_local hipEvent_t t_ev_start = nullptr, t_ev_stop = nullptr;
+static thread_local int t_ev_used = 0;
+
 Wavefront::~Wavefront() {
   for (auto& g : gens_) {
     (void)hipFree(g.rays); (void)hipFree(g.hits); (void)hipFree(g.nodes); (void)hipFree(g.colors);
@@ -769,19 +822,25 @@ Wavefront::~Wavefront() {
 }
 
 hipError_t Wavefront::pmark(hipStream_t s, int cls, bool begin) {
-  if (!profiling_) return hipSuccess;
-  const size_t idx = 2 * pn_ + (begin ? 0 : 1);
-  while (pev_.size() <= idx) {
-    hipEvent_t e;
-    WF_CHECK(hipEventCreate(&e));
-    pev_.push_back(e);
-  }
+  (void)s;
+  if (!profiling_ || !(pmask_ & (1 << cls))) return hipSuccess;
   if (begin) {
+    const size_t idx = 2 * pn_;
+    while (pev_.size() <= idx + 1) {
+      hipEvent_t e;
+      WF_CHECK(hipEventCreate(&e));
+      pev_.push_back(e);
+    }
     if (pcls_.size() <= pn_) pcls_.resize(pn_ + 1);
     pcls_[pn_] = cls;
+    t_ev_start = pev_[idx];
+    t_ev_stop = pev_[idx + 1];
+    t_ev_used = 0;
+  } else {
+    t_ev_start = t_ev_stop = nullptr;
+    if (t_ev_used != 1) return hipErrorInvalidValue;  // a timed class is exactly one launch
+    ++pn_;
   }
-  WF_CHECK(hipEventRecord(pev_[idx], s));
-  if (!begin) ++pn_;
   return hipSuccess;
 }
 
@@ -863,41 +922,52 @@ static int occupancy_grid(K kern, int block, size_t lds, unsigned n) {
 
 static constexpr size_t kWfLdsLimit = 160 * 1024 - 1024;
 
+// Per-launch profiling: see t_ev_start.
+#define WF_LAUNCH(kern, grid, block, lds, stream, ...)                                                  \
+  do {                                                                                                 \
+    if (t_ev_start) {                                                                                  \
+      hipExtLaunchKernelGGL(kern, grid, block, lds, stream, t_ev_start, t_ev_stop, 0, __VA_ARGS__);    \
+      ++t_ev_used;                                                                                     \
+    } else {                                                                                           \
+      hipLaunchKernelGGL(kern, grid, block, lds, stream, __VA_ARGS__);                                 \
+    }                                                                                                  \
+  } while (0)
+
 template <bool QUADS, int TW>
 static hipError_t launch_closest_q(const DevScene& sc, const DevCamera& cam, const WfArgs& a, bool primary,
                                    bool lds_ok, bool bvh, unsigned n, hipStream_t stream) {
   if (bvh) {
     if (primary) {
       auto k = wf_trace_closest_bvh<true, QUADS, 0, TW>;
-      hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
-    } else if (g_wf_lane == 5 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc.n_bvh, sc.n_diag) <= kWfLdsLimit) {
-      const size_t lds = lane_lds_bytes(sc.n_bvh, sc.n_diag);
+      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
+    } else if (g_wf_lane == 5 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc) <= kWfLdsLimit) {
+      const size_t lds = lane_lds_bytes(sc);
       auto k = wf_trace_closest_bvh<false, QUADS, 5, TW>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, lds, n)), dim3(kTraceBlock), lds, stream, sc, cam, a);
+      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, n)), dim3(kTraceBlock), lds, stream, sc, cam, a);
     } else if (g_wf_lane && g_wf_lane != 2 && sc.bvh_depth <= kLaneLdsDepth) {
       auto k = wf_trace_closest_bvh<false, QUADS, 2, TW>;
-      hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
+      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
     } else if (g_wf_lane) {
       auto k = wf_trace_closest_bvh<false, QUADS, 1, TW>;
-      hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
+      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
     } else {
       auto k = wf_trace_closest_bvh<false, QUADS, 0, TW>;
-      hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
+      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
     }
   } else if (primary) {
     const size_t lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, true);
     auto k = wf_trace_closest<true, true, QUADS, TW>;
     WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, lds, n)), dim3(kTraceBlock), lds, stream, sc, cam, a);
+    WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, n)), dim3(kTraceBlock), lds, stream, sc, cam, a);
   } else if (lds_ok) {
     const size_t lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, false);
     auto k = wf_trace_closest<true, false, QUADS, TW>;
     WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, lds, n)), dim3(kTraceBlock), lds, stream, sc, cam, a);
+    WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, n)), dim3(kTraceBlock), lds, stream, sc, cam, a);
   } else {
     auto k = wf_trace_closest<false, false, QUADS, TW>;
-    hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
+    WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
   }
   return hipGetLastError();
 }
@@ -911,29 +981,29 @@ static hipError_t launch_closest(const DevScene& sc, const DevCamera& cam, const
 template <bool QUADS, int TW>
 static hipError_t launch_shadow_q(const DevScene& sc, const WfArgs& a, bool lds_ok, bool bvh, hipStream_t stream) {
   if (bvh) {
-    if (g_wf_lane == 5 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc.n_bvh, sc.n_diag) <= kWfLdsLimit) {
-      const size_t lds = lane_lds_bytes(sc.n_bvh, sc.n_diag);
+    if (g_wf_lane == 5 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc) <= kWfLdsLimit) {
+      const size_t lds = lane_lds_bytes(sc);
       auto k = wf_trace_shadow_bvh<QUADS, 5, TW>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, lds, a.n_shadow)), dim3(kTraceBlock), lds, stream, sc, a);
+      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, a.n_shadow)), dim3(kTraceBlock), lds, stream, sc, a);
     } else if (g_wf_lane && g_wf_lane != 2 && sc.bvh_depth <= kLaneLdsDepth) {
       auto k = wf_trace_shadow_bvh<QUADS, 2, TW>;
-      hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, 0, a.n_shadow)), dim3(kTraceBlock), 0, stream, sc, a);
+      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, a.n_shadow)), dim3(kTraceBlock), 0, stream, sc, a);
     } else if (g_wf_lane) {
       auto k = wf_trace_shadow_bvh<QUADS, 1, TW>;
-      hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, 0, a.n_shadow)), dim3(kTraceBlock), 0, stream, sc, a);
+      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, a.n_shadow)), dim3(kTraceBlock), 0, stream, sc, a);
     } else {
       auto k = wf_trace_shadow_bvh<QUADS, 0, TW>;
-      hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, 0, a.n_shadow)), dim3(kTraceBlock), 0, stream, sc, a);
+      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, a.n_shadow)), dim3(kTraceBlock), 0, stream, sc, a);
     }
   } else if (lds_ok) {
     const size_t lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, false);
     auto k = wf_trace_shadow<true, QUADS, TW>;
     WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, lds, a.n_shadow)), dim3(kTraceBlock), lds, stream, sc, a);
+    WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, a.n_shadow)), dim3(kTraceBlock), lds, stream, sc, a);
   } else {
     auto k = wf_trace_shadow<false, QUADS, TW>;
-    hipLaunchKernelGGL(k, dim3(occupancy_grid(k, kTraceBlock, 0, a.n_shadow)), dim3(kTraceBlock), 0, stream, sc, a);
+    WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, a.n_shadow)), dim3(kTraceBlock), 0, stream, sc, a);
   }
   return hipGetLastError();
 }
@@ -976,10 +1046,10 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
   last_bvh_ = bvh;
   const bool use_prim = camera_mode && (prim_lds || bvh) && sc.n_diag > 0;
   if (use_prim) {
-    hipLaunchKernelGGL(wf_prim_prep, dim3((sc.n_diag + 4 + 255) / 256), dim3(256), 0, stream, sc, cam, d_prim_);
+    WF_LAUNCH(wf_prim_prep, dim3((sc.n_diag + 4 + 255) / 256), dim3(256), 0, stream, sc, cam, d_prim_);
     WF_CHECK(hipGetLastError());
   }
-  WF_CHECK(hipEventRecord(ev0_, stream));
+  if (ms_kernel) WF_CHECK(hipEventRecord(ev0_, stream));
   if (profiling_) ++pframes_;
   prof_rays_[0] = prof_rays_[1] = prof_rays_[2] = 0;
   unsigned last = 0;
@@ -1024,7 +1094,7 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     WF_CHECK(pmark(stream, ccls, false));
     // 2. prepare_computations + spawn
     WF_CHECK(pmark(stream, WF_PREP, true));
-    hipLaunchKernelGGL(wf_prep, dim3(occupancy_grid(wf_prep, kWfBlock, 0, n)), dim3(kWfBlock), 0, stream, sc, cam, a);
+    WF_LAUNCH(wf_prep, dim3(occupancy_grid(wf_prep, kWfBlock, 0, n)), dim3(kWfBlock), 0, stream, sc, cam, a);
     WF_CHECK(hipGetLastError());
     WF_CHECK(pmark(stream, WF_PREP, false));
     if (!calibrated) {
@@ -1049,7 +1119,7 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
       WF_CHECK(pmark(stream, WF_SHADOW, false));
     }
     if (stats) {
-      hipLaunchKernelGGL(wf_count_kinds, dim3(occupancy_grid(wf_count_kinds, 256, 0, n)), dim3(256), 0, stream, a);
+      WF_LAUNCH(wf_count_kinds, dim3(occupancy_grid(wf_count_kinds, 256, 0, n)), dim3(256), 0, stream, a);
       WF_CHECK(hipGetLastError());
     }
   }
@@ -1067,7 +1137,7 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     a.camera_mode = camera_mode ? 1u : 0u;
     a.row_block = row_block; a.shard = shard; a.n_shards = n_shards;
     WF_CHECK(pmark(stream, WF_COMBINE, true));
-    hipLaunchKernelGGL(wf_combine, dim3(occupancy_grid(wf_combine, kWfBlock, 0, a.n)), dim3(kWfBlock), 0, stream, sc,
+    WF_LAUNCH(wf_combine, dim3(occupancy_grid(wf_combine, kWfBlock, 0, a.n)), dim3(kWfBlock), 0, stream, sc,
                        cam, a);
     WF_CHECK(hipGetLastError());
     WF_CHECK(pmark(stream, WF_COMBINE, false));
@@ -1077,12 +1147,12 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     WF_CHECK(pmark(stream, WF_COMBINE, true));
     WfArgs a{};
     a.aa = aa; a.rows = n_pix / cam.hsize;
-    hipLaunchKernelGGL(wf_average, dim3(occupancy_grid(wf_average, kWfBlock, 0, n_pix)), dim3(kWfBlock), 0, stream,
+    WF_LAUNCH(wf_average, dim3(occupancy_grid(wf_average, kWfBlock, 0, n_pix)), dim3(kWfBlock), 0, stream,
                        a, cam.hsize, gens_[0].colors, n_pix, d_out);
     WF_CHECK(hipGetLastError());
     WF_CHECK(pmark(stream, WF_COMBINE, false));
   }
-  WF_CHECK(hipEventRecord(ev1_, stream));
+  if (ms_kernel) WF_CHECK(hipEventRecord(ev1_, stream));
   if (!calibrated && !signature.empty()) cache_[signature] = counts;
   if (stats || ms_kernel) {
     WF_CHECK(hipStreamSynchronize(stream));

@@ -115,9 +115,11 @@ struct WfProfile {
 class Wavefront {
  public:
   ~Wavefront();
-  // Profiling mode: HIP events around every launch, per kernel class.
-  void set_profiling(bool on) {
+  // Profiling mode: start/stop events carried by every launch of the kernel
+  // classes in `class_mask` (bit WF_*), summed per class.
+  void set_profiling(bool on, int class_mask = (1 << WF_NCLASS) - 1) {
     profiling_ = on;
+    pmask_ = class_mask;
     if (on) { pn_ = 0; pframes_ = 0; }
   }
   // Per-class times averaged over the frames rendered since profiling was
@@ -147,6 +149,7 @@ class Wavefront {
   std::map<std::string, Counts> cache_;
   bool last_bvh_ = false;
   bool profiling_ = false;
+  int pmask_ = (1 << WF_NCLASS) - 1;
   std::vector<hipEvent_t> pev_;        // event pool (pairs)
   std::vector<int> pcls_;              // class of each recorded pair
   size_t pn_ = 0;                      // pairs recorded since profiling was enabled

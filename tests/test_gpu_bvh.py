@@ -112,6 +112,52 @@ def test_bvh_color_at_batch_random_rays(rt):
         assert fast.tobytes() == exact.tobytes(), depth
 
 
+@pytest.mark.parametrize("offset", [0.0, 1e5, -3e7])
+def test_bvh_binary32_slabs_far_and_axis_rays(rt, offset):
+    """The per-lane traversal's binary32 slab test (DESIGN.md §5.2 error
+    bound): a cluster far from the origin, rays from just outside it with
+    direction components exactly 0, grazing rays tangent to spheres, and
+    origins on box faces, all bitwise equal to the exhaustive loop."""
+    rng = np.random.default_rng(int(abs(offset)) % 997 + 3)
+    w = rt.World()
+    centres, radii = [], []
+    for i in range(300):
+        r = float(rng.uniform(0.05, 0.6))
+        c = rng.uniform(-4, 4, 3) + offset
+        s = rt.glass_sphere() if i % 4 == 0 else rt.Sphere()
+        s.set_transform(rt.translation(*c) * rt.scaling(r, r, r))
+        s.material.reflective = 0.5
+        w.add_object(s)
+        centres.append(c)
+        radii.append(r)
+    w.add_light(rt.PointLight(rt.Point(offset - 10, offset + 10, offset - 10), rt.Color(1, 1, 1)))
+    rays = []
+    for c, r in zip(centres[:200], radii[:200]):
+        for ax in range(3):
+            o = np.array(c, dtype=np.float64)
+            o[ax] -= 6.0
+            d = np.zeros(3)
+            d[ax] = 1.0
+            rays.append(np.hstack([o, d]))                          # axis ray through the centre
+            o2 = o.copy()
+            o2[(ax + 1) % 3] += r                                     # tangent (grazing) axis ray
+            rays.append(np.hstack([o2, d]))
+            o3 = o.copy()
+            o3[(ax + 1) % 3] += r * (1 + 1e-12)                     # just outside the tangent
+            rays.append(np.hstack([o3, d]))
+    o = np.array(centres)[rng.integers(0, 300, 4000)] + rng.normal(scale=1.0, size=(4000, 3))
+    d = rng.normal(size=(4000, 3))
+    d[::3, 0] = 0.0                                                  # zero components
+    d[1::3, 1:] = 0.0
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.vstack([np.array(rays), np.hstack([o, d])])
+    for depth in (0, 3):
+        fast, _ = w.color_at_batch(rays, depth, want_stats=False)
+        exact, _ = w.color_at_batch(rays, depth, want_stats=True)
+        assert fast.tobytes() == exact.tobytes(), depth
+    assert rt._rtamd._wf_profile(w, -1, True)["n_bvh_nodes"] > 0
+
+
 def test_bvh_shard_device_bitwise(rt):
     import torch
     from rtamd import scenes

@@ -39,13 +39,15 @@ for r in range(4):
             cam.render_shard_device(w, depth, 8, 0, 1, buf.data_ptr(), s, False)
         torch.cuda.synchronize()
         p = rtamd._rtamd._wf_profile(w, 0, True)
-        res.setdefault(combo, []).append((sum(p["ms"].values()), p["ms"], p["tests"], p["boxes"]))
+        lds = (max(int(p["bvh_depth"]), 1) * 4096 + 64 * p["n_bvh_nodes"] + 64 * p["n_diag"]) / 1024
+        res.setdefault(combo, []).append((sum(p["ms"].values()), p["ms"], p["tests"], p["boxes"],
+                                          f"nodes {p['n_bvh_nodes']} depth {p['bvh_depth']} lane-LDS {lds:.0f}KB"))
         chk = buf.cpu().numpy().tobytes()
         ref = ref or chk
         assert chk == ref, combo
 for combo, v in res.items():
-    tot, ms, tests, boxes = min(v, key=lambda x: x[0])
+    tot, ms, tests, boxes, info = min(v, key=lambda x: x[0])
     name = " ".join(f"{k}={c}" for (k, _), c in zip(knobs, combo))
     print(f"{name}: frame {tot:.3f} ms  " + " ".join(f"{c}={m:.3f}" for c, m in ms.items())
           + "  tests " + " ".join(f"{c}={t/1e6:.0f}M" for c, t in tests.items())
-          + "  boxes " + " ".join(f"{c}={t/1e6:.0f}M" for c, t in boxes.items()), flush=True)
+          + "  boxes " + " ".join(f"{c}={t/1e6:.0f}M" for c, t in boxes.items()) + "  " + info, flush=True)
