@@ -388,11 +388,10 @@ __device__ __forceinline__ SlabRay slab_ray(V3 o, V3 d, const float* M) {
   }
   return r;
 }
-// binary32 upper bound of a non-negative binary64 distance
-__device__ __forceinline__ float f32_up(double x) {
-  const float f = (float)x;
-  return (double)f < x ? __int_as_float(__float_as_int(f) + 1) : f;
-}
+// binary32 upper bound of a non-negative binary64 distance: RN(x) is within
+// 2^-23 of x relative to it, and RN(f * (1 + 2^-22)) > f * (1 + 2^-23)
+// (0 and inf map to themselves).
+__device__ __forceinline__ float f32_up(double x) { return (float)x * (1.0f + 0x1p-22f); }
 // max(entry, 0) <= min(exit, t_hi): the ray may meet the box within [0, t_hi]
 // (t_hi >= 0). `t_in` = the widened entry distance (child ordering only).
 template <typename P>  // P: constant-address (scalar loads) or generic (per-lane loads) float pointer
@@ -491,11 +490,17 @@ __device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDia
     ++it;
 #endif
     if (e >= 0) {  // a node visit: both children's boxes, the one entered first visited first
-      const BvhNode& nd = nodes[e];
-      const int c0 = nd.child[0], c1 = nd.child[1];
+      // the whole 64-B node in four 16-B loads: lo[0], lo[1], hi[0], hi[1], child[2], axis, pad
+      const uint4* np = reinterpret_cast<const uint4*>(nodes + e);
+      const uint4 q0 = np[0], q1 = np[1], q2 = np[2], q3 = np[3];
+      const float lo0[3] = {__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z)};
+      const float lo1[3] = {__uint_as_float(q0.w), __uint_as_float(q1.x), __uint_as_float(q1.y)};
+      const float hi0[3] = {__uint_as_float(q1.z), __uint_as_float(q1.w), __uint_as_float(q2.x)};
+      const float hi1[3] = {__uint_as_float(q2.y), __uint_as_float(q2.z), __uint_as_float(q2.w)};
+      const int c0 = (int)q3.x, c1 = (int)q3.y;
       float t0, t1;
-      const bool h0 = slab_hit32(nd.lo[0], nd.hi[0], sr, t_hi, t0);
-      const bool h1 = c1 != kBvhEmpty && slab_hit32(nd.lo[1], nd.hi[1], sr, t_hi, t1);
+      const bool h0 = slab_hit32(lo0, hi0, sr, t_hi, t0);
+      const bool h1 = slab_hit32(lo1, hi1, sr, t_hi, t1) & (c1 != kBvhEmpty);
       n_boxes += 2;
       if (h0 && h1) {
         const bool flip = t1 < t0;
