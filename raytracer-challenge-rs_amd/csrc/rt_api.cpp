@@ -233,6 +233,10 @@ int rtamd_tuning_set(const char* key, int value) {
                                // stack, 5 = per-lane with the scene in LDS when it fits (default)
     return RT_OK;
   }
+  if (key && std::strcmp(key, "skip_shadow") == 0) {
+    rtamd::g_wf_skip_shadow = value != 0;
+    return RT_OK;
+  }
   if (key && std::strcmp(key, "accel") == 0) {
     rtamd::g_wf_accel = value != 0;
     return RT_OK;

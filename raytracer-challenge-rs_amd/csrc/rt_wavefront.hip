@@ -27,8 +27,9 @@ constexpr int kTraceBlock = 1024;  // trace kernels: 16 waves, one LDS image per
 // allocator): 8 = two 1024-thread blocks per CU (<= 64 VGPRs), 4 = one.
 int g_wf_trace_waves = 8;  // tuning knob (rtamd_tuning_set("wf_waves", n))
 int g_wf_accel = 1;        // 1 = BVH traversal when counters are not requested, 0 = exhaustive always
-int g_wf_lane = 5;  // secondary / shadow rays: 5 = per-lane, scene + stack in LDS (when they fit), 1 = per-lane
-                    // with an LDS (or scratch) stack, 0 = wave (packet) traversal
+int g_wf_lane = 5;  // secondary / shadow rays: 5 = per-lane, scene + stack in LDS (when they fit), 6 = nodes +
+                    // stack in LDS, 1 = per-lane with an LDS (or scratch) stack, 0 = wave (packet) traversal
+int g_wf_skip_shadow = 1;  // fast path: leave out shadow rays that cannot change the colour
 // occupancy (waves per SIMD the register allocator targets) of the BVH trace kernels
 int g_tw_primary = 4, g_tw_closest = 4, g_tw_shadow = 4;
 constexpr int kWfBlock = 256;      // prep / shadow / combine
@@ -88,18 +89,24 @@ __device__ __forceinline__ void gen0_pixel(const WfArgs& a, uint32_t hsize, uint
 
 // Block-aggregated queue appends for wf_prep (one atomic per counter per
 // block instead of per wave: the counters are single hot addresses).
-// Called by every thread of the block (it synchronises). Lanes with want_s
-// get `per_s` consecutive shadow slots, lanes with want_r / want_f one ray
-// slot each in the next generation (reflected rays of the block first).
-__device__ __forceinline__ void block_append(unsigned* shadow_ctr, unsigned per_s, bool want_s, unsigned* ray_ctr,
-                                             bool want_r, bool want_f, unsigned& so, unsigned& ro, unsigned& fo) {
+// Called by every thread of the block (it synchronises). A lane gets `n_s`
+// consecutive shadow slots, and with want_r / want_f one ray slot each in the
+// next generation (reflected rays of the block first).
+__device__ __forceinline__ void block_append(unsigned* shadow_ctr, unsigned n_s, unsigned* ray_ctr, bool want_r,
+                                             bool want_f, unsigned& so, unsigned& ro, unsigned& fo) {
   __shared__ unsigned s_cnt[kWfBlock / 64][3];
   __shared__ unsigned s_base[3];
   const unsigned lane = lane_id(), wave = threadIdx.x / 64;
-  const unsigned long long ms = __ballot(want_s), mr = __ballot(want_r), mf = __ballot(want_f);
+  const unsigned long long mr = __ballot(want_r), mf = __ballot(want_f);
   const unsigned long long below = (1ull << lane) - 1ull;
+  unsigned incl = n_s;  // inclusive prefix of the shadow counts over the wave
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned t = (unsigned)__shfl_up((int)incl, off, 64);
+    if ((int)lane >= off) incl += t;
+  }
+  if (lane == 63) s_cnt[wave][0] = incl;
   if (lane == 0) {
-    s_cnt[wave][0] = (unsigned)__popcll(ms) * per_s;
     s_cnt[wave][1] = (unsigned)__popcll(mr);
     s_cnt[wave][2] = (unsigned)__popcll(mf);
   }
@@ -118,7 +125,7 @@ __device__ __forceinline__ void block_append(unsigned* shadow_ctr, unsigned per_
     s_base[2] = rb + t[1];
   }
   __syncthreads();
-  so = s_base[0] + s_cnt[wave][0] + (unsigned)__popcll(ms & below) * per_s;
+  so = s_base[0] + s_cnt[wave][0] + (incl - n_s);
   ro = s_base[1] + s_cnt[wave][1] + (unsigned)__popcll(mr & below);
   fo = s_base[2] + s_cnt[wave][2] + (unsigned)__popcll(mf & below);
   __syncthreads();  // s_cnt / s_base are reused by the next call
@@ -147,21 +154,37 @@ __device__ __forceinline__ void wf_ray(const WfArgs& a, const DevCamera& cam, un
 }
 
 // Shadow ray j of a generation: World::is_shadowed(comps.over_point, light)
-// (world.rs:95-105) of hit node j / L and light j % L, built from the node's
-// over point exactly as the reference builds it (v = light - point,
-// distance = |v|, direction = v.normalize()). slot = node * L + light.
+// (world.rs:95-105) for shadow slot a.shadow_nodes[j] = node * L + light,
+// built from the node's over point exactly as the reference builds it
+// (v = light - point, distance = |v|, direction = v.normalize()).
 __device__ __forceinline__ void shadow_ray(const DevScene& sc, const WfArgs& a, unsigned j, V3& o, V3& d,
                                            double& dist, unsigned& slot) {
   const unsigned L = (unsigned)sc.n_lights;
-  const unsigned q = j / L, l = j - q * L;
-  const int node = a.shadow_nodes[q];
+  slot = (unsigned)a.shadow_nodes[j];
+  const unsigned node = L == 1 ? slot : slot / L, l = slot - node * L;
   const WfNode& nd = a.nodes[node];
   o = v3(nd.over[0], nd.over[1], nd.over[2]);
   cLightRec Lr = (cLightRec)sc.lights + l;
   const V3 v = vsub(v3(Lr->pos[0], Lr->pos[1], Lr->pos[2]), o);
   dist = sqrt(v.x * v.x + v.y * v.y + v.z * v.z);  // magnitude (vector.rs:21-23)
   d = vnormalize(v);
-  slot = (unsigned)node * L + l;
+}
+
+// A shadow ray whose answer cannot change the colour (DESIGN.md "Skipped
+// shadow rays"): with the light behind the surface, lighting() returns
+// `ambient` in shadow and `ambient + 0 + 0` in light (material.rs:23-87),
+// bit-identical unless a component of ambient is -0 or NaN. Evaluated with
+// the operations lighting() itself performs; patterned materials are never
+// skipped (their colour is only known in wf_combine).
+__device__ __forceinline__ bool shadow_irrelevant(const ShadeRec& m, cLightRec L, V3 over, V3 normal) {
+  if (m.pattern_kind >= 0) return false;
+  const V3 lightv = vnormalize(vsub(v3(L->pos[0], L->pos[1], L->pos[2]), over));
+  if (!(vdot(lightv, normal) < 0.0)) return false;
+  const V3 effective_color = vmul(v3(m.color[0], m.color[1], m.color[2]),
+                                  v3(L->intensity[0], L->intensity[1], L->intensity[2]));
+  const V3 ambient = vscale(effective_color, m.ambient);
+  auto plain = [](double x) { return x == x && !(x == 0.0 && signbit(x)); };
+  return plain(ambient.x) && plain(ambient.y) && plain(ambient.z);
 }
 
 // ------------------------------------------------------------ primary records
@@ -540,8 +563,9 @@ __device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDia
 // (dynamic shared memory: [stack bvh_depth x kTraceBlock ints][nodes][spheres];
 // a lane pushes at most one entry per tree level).
 __host__ __device__ inline size_t lane_stack_bytes(int depth) { return (size_t)(depth > 0 ? depth : 1) * kTraceBlock * 4; }
-__host__ __device__ inline size_t lane_lds_bytes(const DevScene& sc) {
-  return lane_stack_bytes(sc.bvh_depth) + (size_t)sc.n_bvh * sizeof(BvhNode) + (size_t)sc.n_diag * sizeof(SphereDiag);
+__host__ __device__ inline size_t lane_lds_bytes(const DevScene& sc, bool spheres = true) {
+  return lane_stack_bytes(sc.bvh_depth) + (size_t)sc.n_bvh * sizeof(BvhNode) +
+         (spheres ? (size_t)sc.n_diag * sizeof(SphereDiag) : 0);
 }
 struct LaneScene {
   const BvhNode* nodes;
@@ -552,19 +576,21 @@ struct LaneScene {
 template <int LANE>
 __device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, int* static_stack, unsigned char* dyn) {
   LaneScene ls{sc.bvh, sc.sph_diag, static_stack};
-  if constexpr (LANE == 5) {
+  if constexpr (LANE == 5 || LANE == 6) {  // 6: the sphere records stay in global memory
     int* stack = (int*)dyn;
     BvhNode* nodes = (BvhNode*)(dyn + lane_stack_bytes(sc.bvh_depth));
-    SphereDiag* sd = (SphereDiag*)((unsigned char*)nodes + (size_t)sc.n_bvh * sizeof(BvhNode));
     const uint4* gn = (const uint4*)sc.bvh;
     uint4* ln = (uint4*)nodes;
     for (int i = threadIdx.x; i < sc.n_bvh * (int)(sizeof(BvhNode) / 16); i += blockDim.x) ln[i] = gn[i];
-    const uint4* gs = (const uint4*)sc.sph_diag;
-    uint4* ls4 = (uint4*)sd;
-    for (int i = threadIdx.x; i < sc.n_diag * (int)(sizeof(SphereDiag) / 16); i += blockDim.x) ls4[i] = gs[i];
+    if constexpr (LANE == 5) {
+      SphereDiag* sd = (SphereDiag*)((unsigned char*)nodes + (size_t)sc.n_bvh * sizeof(BvhNode));
+      const uint4* gs = (const uint4*)sc.sph_diag;
+      uint4* ls4 = (uint4*)sd;
+      for (int i = threadIdx.x; i < sc.n_diag * (int)(sizeof(SphereDiag) / 16); i += blockDim.x) ls4[i] = gs[i];
+      ls.sd = sd;
+    }
     __syncthreads();
     ls.nodes = nodes;
-    ls.sd = sd;
     ls.stack = stack + threadIdx.x;
   }
   for (int a = 0; a < 3; ++a) {
@@ -581,7 +607,7 @@ __device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, int* static_
 template <bool PRIMARY, bool QUADS, int LANE, int TW>
 __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest_bvh(DevScene sc, DevCamera cam, WfArgs a) {
   constexpr bool LDS_STACK = LANE >= 2;
-  __shared__ int stack_lds[LANE == 5 ? 1 : LDS_STACK ? kLaneLdsDepth * kTraceBlock : (kTraceBlock / 64) * (kBvhMaxDepth + 4)];
+  __shared__ int stack_lds[LANE >= 5 ? 1 : LDS_STACK ? kLaneLdsDepth * kTraceBlock : (kTraceBlock / 64) * (kBvhMaxDepth + 4)];
   extern __shared__ __attribute__((aligned(16))) unsigned char lane_dyn[];
   int* stk = LDS_STACK ? stack_lds + threadIdx.x : stack_lds + (threadIdx.x / 64) * (kBvhMaxDepth + 4);
   const LaneScene ls = lane_scene<LANE>(sc, stk, lane_dyn);
@@ -615,7 +641,7 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest_bvh(DevScene
 template <bool QUADS, int LANE, int TW>
 __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow_bvh(DevScene sc, WfArgs a) {
   constexpr bool LDS_STACK = LANE >= 2;
-  __shared__ int stack_lds[LANE == 5 ? 1 : LDS_STACK ? kLaneLdsDepth * kTraceBlock : (kTraceBlock / 64) * (kBvhMaxDepth + 4)];
+  __shared__ int stack_lds[LANE >= 5 ? 1 : LDS_STACK ? kLaneLdsDepth * kTraceBlock : (kTraceBlock / 64) * (kBvhMaxDepth + 4)];
   extern __shared__ __attribute__((aligned(16))) unsigned char lane_dyn[];
   int* stk = LDS_STACK ? stack_lds + threadIdx.x : stack_lds + (threadIdx.x / 64) * (kBvhMaxDepth + 4);
   const LaneScene ls = lane_scene<LANE>(sc, stk, lane_dyn);
@@ -685,10 +711,19 @@ __global__ __launch_bounds__(kWfBlock) void wf_prep(DevScene sc, DevCamera cam, 
         }
       }
     }
-    // shadow rays: one per light, in light order (world.rs:41-56)
+    // shadow rays: one per light (world.rs:41-56); the fast path leaves out the
+    // ones whose answer cannot change the colour (their flag is written here)
+    unsigned n_s = 0, skip = 0;
+    if (hit) {
+      for (unsigned l = 0; l < L; ++l) {
+        if (a.skip_shadow && l < 32 && shadow_irrelevant(*m, (cLightRec)sc.lights + l, c.over, c.normal))
+          skip |= 1u << l;
+        else
+          ++n_s;
+      }
+    }
     unsigned sbase, rbase, fbase;
-    block_append(&a.cnt->n_shadow[a.g], L, hit && L > 0, &a.cnt->n_rays[a.g + 1], want_refl, want_refr, sbase, rbase,
-                 fbase);  // n_shadow counts shadow rays (hits x lights); the list holds the hit nodes
+    block_append(&a.cnt->n_shadow[a.g], n_s, &a.cnt->n_rays[a.g + 1], want_refl, want_refr, sbase, rbase, fbase);
     if (!valid) continue;
     WfNode nd;
     nd.obj = -1; nd.child_refl = -1; nd.child_refr = -1; nd.pad = 0;
@@ -698,7 +733,10 @@ __global__ __launch_bounds__(kWfBlock) void wf_prep(DevScene sc, DevCamera cam, 
       nd.normal[0] = c.normal.x; nd.normal[1] = c.normal.y; nd.normal[2] = c.normal.z;
       // shade_hit's Schlick factor (world.rs:62-64), same inputs as the reference's call
       nd.schlick = (m->reflective > 0.0 && m->transparency > 0.0) ? schlick(c.eyev, c.normal, c.n1, c.n2) : 0.0;
-      if (L > 0) a.shadow_nodes[sbase / L] = (int32_t)i;  // its shadow rays are built by the shadow trace
+      for (unsigned l = 0; l < L; ++l) {  // its shadow rays are built by the shadow trace
+        if (l < 32 && (skip >> l & 1u)) a.sflags[i * L + l] = 0;
+        else a.shadow_nodes[sbase++] = (int32_t)(i * L + l);
+      }
       if (want_refl && rbase < a.cap_next) {
         const V3 rv = vreflect(d, c.normal);  // comps.reflectv (intersection.rs:101)
         WfRay r;
@@ -893,7 +931,7 @@ hipError_t Wavefront::ensure_gen(size_t g, size_t rays, size_t n_lights) {
     (void)hipFree(b.shadow_nodes); (void)hipFree(b.sflags);
     b.shadow_nodes = nullptr; b.sflags = nullptr;
     b.cap_shadows = 0;
-    WF_CHECK(hipMalloc(&b.shadow_nodes, std::max<size_t>(b.cap_rays, 1) * sizeof(int32_t)));
+    WF_CHECK(hipMalloc(&b.shadow_nodes, need_sh * sizeof(int32_t)));
     WF_CHECK(hipMalloc(&b.sflags, need_sh));
     b.cap_shadows = need_sh;
   }
@@ -945,7 +983,12 @@ static hipError_t launch_closest_q(const DevScene& sc, const DevCamera& cam, con
     if (primary) {
       auto k = wf_trace_closest_bvh<true, QUADS, 0, TW>;
       WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
-    } else if (g_wf_lane == 5 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc) <= kWfLdsLimit) {
+    } else if (g_wf_lane == 6 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc, false) <= kWfLdsLimit) {
+      const size_t lds = lane_lds_bytes(sc, false);
+      auto k = wf_trace_closest_bvh<false, QUADS, 6, TW>;
+      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, n)), dim3(kTraceBlock), lds, stream, sc, cam, a);
+    } else if (g_wf_lane >= 5 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc) <= kWfLdsLimit) {
       const size_t lds = lane_lds_bytes(sc);
       auto k = wf_trace_closest_bvh<false, QUADS, 5, TW>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -986,7 +1029,12 @@ static hipError_t launch_closest(const DevScene& sc, const DevCamera& cam, const
 template <bool QUADS, int TW>
 static hipError_t launch_shadow_q(const DevScene& sc, const WfArgs& a, bool lds_ok, bool bvh, hipStream_t stream) {
   if (bvh) {
-    if (g_wf_lane == 5 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc) <= kWfLdsLimit) {
+    if (g_wf_lane == 6 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc, false) <= kWfLdsLimit) {
+      const size_t lds = lane_lds_bytes(sc, false);
+      auto k = wf_trace_shadow_bvh<QUADS, 6, TW>;
+      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, a.n_shadow)), dim3(kTraceBlock), lds, stream, sc, a);
+    } else if (g_wf_lane >= 5 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc) <= kWfLdsLimit) {
       const size_t lds = lane_lds_bytes(sc);
       auto k = wf_trace_shadow_bvh<QUADS, 5, TW>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -1029,7 +1077,12 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
   const bool averaged = aa > 1;
   WF_CHECK(ensure_misc((size_t)sc.n_diag));
   const unsigned L = (unsigned)sc.n_lights;
-  auto it = signature.empty() ? cache_.end() : cache_.find(signature);
+  // BVH traversal (and skipped shadow rays) unless the exact exhaustive counters are requested
+  const bool bvh = g_wf_accel != 0 && stats == nullptr && sc.n_bvh > 0;
+  const bool skip_shadow = stats == nullptr && g_wf_skip_shadow != 0;
+  // the shadow-ray counts differ between the two modes
+  const std::string key = signature.empty() ? signature : signature + (skip_shadow ? 'S' : 'A');
+  auto it = key.empty() ? cache_.end() : cache_.find(key);
   const bool calibrated = it != cache_.end();
   Counts counts;
   if (calibrated) counts = it->second;
@@ -1046,8 +1099,6 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
   }
   const bool prim_lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, true) <= kWfLdsLimit;
   const bool gen_lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, false) <= kWfLdsLimit;
-  // BVH traversal unless the exact exhaustive counters are requested
-  const bool bvh = g_wf_accel != 0 && stats == nullptr && sc.n_bvh > 0;
   last_bvh_ = bvh;
   const bool use_prim = camera_mode && (prim_lds || bvh) && sc.n_diag > 0;
   if (use_prim) {
@@ -1081,6 +1132,7 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     a.g = g; a.max_depth = max_depth;
     a.camera_mode = camera_mode ? 1u : 0u;
     a.row_block = row_block; a.shard = shard; a.n_shards = n_shards;
+    a.skip_shadow = skip_shadow ? 1u : 0u;
     // 1. closest hit
     const bool prim_launch = g == 0 && use_prim;
     const int ccls = prim_launch ? WF_PRIMARY : WF_CLOSEST;
@@ -1158,7 +1210,7 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     WF_CHECK(pmark(stream, WF_COMBINE, false));
   }
   if (ms_kernel) WF_CHECK(hipEventRecord(ev1_, stream));
-  if (!calibrated && !signature.empty()) cache_[signature] = counts;
+  if (!calibrated && !key.empty()) cache_[key] = counts;
   if (stats || ms_kernel) {
     WF_CHECK(hipStreamSynchronize(stream));
     if (ms_kernel) WF_CHECK(hipEventElapsedTime(ms_kernel, ev0_, ev1_));

@@ -58,6 +58,7 @@ extern int g_wf_trace_waves;  // tuning knob: trace-kernel occupancy (4 or 8 wav
 extern int g_tw_primary, g_tw_closest, g_tw_shadow;  // tuning knobs: BVH trace-kernel occupancy
 extern int g_wf_lane;         // tuning knob: 1 = per-lane BVH traversal for secondary / shadow rays
 extern int g_wf_accel;        // tuning knob: 1 = BVH traversal (when no counters are requested), 0 = exhaustive
+extern int g_wf_skip_shadow;  // tuning knob: 1 = the fast path leaves out shadow rays that cannot change the colour
 
 struct WfCounters {
   unsigned n_rays[kMaxGen];    // appended rays per generation (index g+1 filled by prep(g))
@@ -84,7 +85,7 @@ struct WfArgs {
   WfHit* hits;
   WfNode* nodes;
   double* colors;       // colors_g (g >= 1) or the output (g == 0)
-  int32_t* shadow_nodes;  // hit node indices; shadow ray j = (node j / L, light j % L)
+  int32_t* shadow_nodes;  // shadow slots: shadow ray j = slot node * L + light
   uint8_t* sflags;
   WfRay* next_rays;     // rays_{g+1}
   const double* child_colors;  // colors_{g+1}
@@ -99,6 +100,7 @@ struct WfArgs {
   unsigned disc_slot;   // WfCounters::disc index of this trace launch
   unsigned aa;          // AA samples per pixel (generation 0 in camera mode)
   unsigned rows;        // local rows of the camera shard (generation-0 tiling)
+  unsigned skip_shadow; // leave out shadow rays that cannot change the colour (fast path)
 };
 
 // Per-kernel-class timing of the last frame (profiling mode only).

@@ -27,7 +27,7 @@ def _both(rt, w, cam, depth, aa=1):
     return fast.to_numpy(), exact.to_numpy(), st
 
 
-def _glass_cluster(rt, n=300, seed=7, inside=True):
+def _glass_cluster(rt, n=300, seed=7, inside=True, neg_zero=False):
     """Overlapping glass and mirror spheres (containers several deep), and a
     camera that may sit inside one of them."""
     rng = np.random.default_rng(seed)
@@ -43,6 +43,8 @@ def _glass_cluster(rt, n=300, seed=7, inside=True):
         s.material.refractive_index = 1.0 + rng.uniform(0, 1.5)
         s.material.reflective = rng.uniform(0, 0.9)
         s.material.color = rt.Color(*rng.uniform(0, 1, 3))
+        if neg_zero and i % 2:
+            s.material.color = rt.Color(-0.0, 0.5, -0.0)
         w.add_object(s)
     w.add_light(rt.PointLight(rt.Point(-10, 10, -10), rt.Color(1, 1, 1)))
     cam = rt.Camera(96, 64, PI / 2.5)
@@ -187,7 +189,31 @@ def test_accel_knob_off_matches(rt):
     assert a.to_numpy().tobytes() == b.to_numpy().tobytes()
 
 
-@pytest.mark.parametrize("lane", [0, 1, 2, 5])
+@pytest.mark.parametrize("neg_zero", [False, True])
+def test_skipped_shadow_rays_bitwise(rt, neg_zero):
+    """The fast path leaves out shadow rays whose answer cannot change the
+    colour (light behind the surface, DESIGN.md "Skipped shadow rays"). The
+    frame must stay bitwise equal to the exhaustive one, also with -0.0 colour
+    components (where ambient and ambient + 0 + 0 differ, so nothing may be
+    skipped), and fewer shadow rays must actually be traced."""
+    w, cam, depth = _glass_cluster(rt, n=200, seed=31, inside=False, neg_zero=neg_zero)
+    exact, st = cam.render(w, depth, want_stats=True)
+    rt._rtamd._wf_profile(w, 1, False)
+    fast, _ = cam.render(w, depth, want_stats=False)
+    traced = rt._rtamd._wf_profile(w, 0, True)["rays"]["shadow"]
+    assert fast.to_numpy().tobytes() == exact.to_numpy().tobytes()
+    assert traced < st["rays_shadow"]
+    rt._rtamd._tuning_set("skip_shadow", 0)
+    try:
+        rt._rtamd._wf_profile(w, 1, False)
+        full, _ = cam.render(w, depth, want_stats=False)
+        assert rt._rtamd._wf_profile(w, 0, True)["rays"]["shadow"] == st["rays_shadow"]
+    finally:
+        rt._rtamd._tuning_set("skip_shadow", 1)
+    assert full.to_numpy().tobytes() == exact.to_numpy().tobytes()
+
+
+@pytest.mark.parametrize("lane", [0, 1, 2, 5, 6])
 def test_traversal_variants_bitwise(rt, lane):
     """Every traversal variant (wave / per-lane with LDS or scratch stack /
     per-lane with the scene staged in LDS) gives the exhaustive frame."""
