@@ -27,8 +27,10 @@ constexpr int kTraceBlock = 1024;  // trace kernels: 16 waves, one LDS image per
 // allocator): 8 = two 1024-thread blocks per CU (<= 64 VGPRs), 4 = one.
 int g_wf_trace_waves = 8;  // tuning knob (rtamd_tuning_set("wf_waves", n))
 int g_wf_accel = 1;        // 1 = BVH traversal when counters are not requested, 0 = exhaustive always
-int g_wf_lane = 5;  // secondary / shadow rays: 5 = per-lane, scene + stack in LDS (when they fit), 6 = nodes +
-                    // stack in LDS, 1 = per-lane with an LDS (or scratch) stack, 0 = wave (packet) traversal
+int g_wf_lane = 7;  // secondary / shadow rays: 7 = per-lane with leaves batched across the wave, scene + stack
+                    // in LDS (when they fit; else 3 = the same with only the stack in LDS), 5 = per-lane, scene
+                    // + stack in LDS, 6 = nodes + stack in LDS, 1 = per-lane with an LDS (or scratch) stack,
+                    // 0 = wave (packet) traversal
 int g_wf_skip_shadow = 1;  // fast path: leave out shadow rays that cannot change the colour
 // occupancy (waves per SIMD the register allocator targets) of the BVH trace kernels
 int g_tw_primary = 4, g_tw_closest = 4, g_tw_shadow = 4;
@@ -493,7 +495,7 @@ __device__ __forceinline__ void bvh_trace(const DevScene& sc, cPrimRec prim, int
 // `nodes` / `sd` point at the hierarchy and the sphere records in global
 // memory or at the block's LDS copy. `h` arrives initialised (it may already
 // hold the planes' nearest hit, which tightens the culling).
-template <bool SHADOW, bool LDS_STACK>
+template <bool SHADOW, bool LDS_STACK, bool WW = false>
 __device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDiag* sd, const float* M, bool has_bvh,
                                            V3 o, V3 d, double t_shadow, Hit& h, unsigned& n_disc, unsigned& n_tests,
                                            unsigned& n_boxes, int* lds) {
@@ -504,6 +506,67 @@ __device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDia
   int sp = 0;
   auto pop = [&]() { return sp > 0 ? stk(--sp) : kBvhEmpty; };
   int e = (SHADOW && h.key >= 0 && h.t < t_shadow) || !has_bvh ? kBvhEmpty : 0;
+  // a node visit: both children's boxes, the one entered first visited first
+  auto visit = [&]() {
+    // the whole 64-B node in four 16-B loads: lo[0], lo[1], hi[0], hi[1], child[2], axis, pad
+    const uint4* np = reinterpret_cast<const uint4*>(nodes + e);
+    const uint4 q0 = np[0], q1 = np[1], q2 = np[2], q3 = np[3];
+    const float lo0[3] = {__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z)};
+    const float lo1[3] = {__uint_as_float(q0.w), __uint_as_float(q1.x), __uint_as_float(q1.y)};
+    const float hi0[3] = {__uint_as_float(q1.z), __uint_as_float(q1.w), __uint_as_float(q2.x)};
+    const float hi1[3] = {__uint_as_float(q2.y), __uint_as_float(q2.z), __uint_as_float(q2.w)};
+    const int c0 = (int)q3.x, c1 = (int)q3.y;
+    float t0, t1;
+    const bool h0 = slab_hit32(lo0, hi0, sr, t_hi, t0);
+    const bool h1 = slab_hit32(lo1, hi1, sr, t_hi, t1) & (c1 != kBvhEmpty);
+    n_boxes += 2;
+    if (h0 && h1) {
+      const bool flip = t1 < t0;
+      stk(sp++) = flip ? c0 : c1;
+      e = flip ? c1 : c0;
+    } else {
+      e = h0 ? c0 : h1 ? c1 : pop();
+    }
+  };
+  // a leaf's spheres; true when a shadow ray is found occluded
+  auto leaf = [&](int code_e) {
+    const int code = -(code_e + 1);
+    const int first = code >> 7, cnt = code & 127;
+    for (int k = first; k < first + cnt; ++k) {
+      const SphereDiag& r = sd[k];
+      const double s0 = r.s[0], s1 = r.s[1], s2 = r.s[2];
+      sphere_test<SHADOW>(s0 * o.x + r.t[0], s1 * o.y + r.t[1], s2 * o.z + r.t[2], s0 * d.x, s1 * d.y, s2 * d.z,
+                          [&] { return (int)r.meta; }, h, n_disc);
+    }
+    n_tests += (unsigned)cnt;
+    if constexpr (SHADOW) {
+      return h.key >= 0 && h.t < t_shadow;
+    } else {
+      t_hi = f32_up(h.t);
+      return false;
+    }
+  };
+  if constexpr (WW) {
+    // Leaves batched across the wave (speculative while-while): a lane meeting
+    // a leaf postpones it and keeps visiting nodes; the node phase ends when no
+    // lane without a postponed leaf has a node left, then all postponed leaves
+    // are tested together. Culling only ever uses the lane's current bound, so
+    // the postponement changes no result.
+    int pl = kBvhEmpty;
+    for (;;) {
+      for (;;) {
+        if (e < 0 && e != kBvhEmpty && pl == kBvhEmpty) { pl = e; e = pop(); }
+        if (!__any(e >= 0 && pl == kBvhEmpty)) break;
+        if (e >= 0) visit();  // lanes holding a leaf keep going (speculative)
+      }
+      if (!__any(pl != kBvhEmpty)) break;
+      if (pl != kBvhEmpty) {
+        if (leaf(pl)) { e = kBvhEmpty; sp = 0; }  // shadowed: done
+        pl = kBvhEmpty;
+      }
+    }
+    return;
+  }
 #ifdef RTAMD_DIAG
   unsigned it = 0;  // diagnostic build: loop iterations of this lane vs the wave's
   const unsigned n_tests0 = n_tests, n_boxes0 = n_boxes;
@@ -512,41 +575,10 @@ __device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDia
 #ifdef RTAMD_DIAG
     ++it;
 #endif
-    if (e >= 0) {  // a node visit: both children's boxes, the one entered first visited first
-      // the whole 64-B node in four 16-B loads: lo[0], lo[1], hi[0], hi[1], child[2], axis, pad
-      const uint4* np = reinterpret_cast<const uint4*>(nodes + e);
-      const uint4 q0 = np[0], q1 = np[1], q2 = np[2], q3 = np[3];
-      const float lo0[3] = {__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z)};
-      const float lo1[3] = {__uint_as_float(q0.w), __uint_as_float(q1.x), __uint_as_float(q1.y)};
-      const float hi0[3] = {__uint_as_float(q1.z), __uint_as_float(q1.w), __uint_as_float(q2.x)};
-      const float hi1[3] = {__uint_as_float(q2.y), __uint_as_float(q2.z), __uint_as_float(q2.w)};
-      const int c0 = (int)q3.x, c1 = (int)q3.y;
-      float t0, t1;
-      const bool h0 = slab_hit32(lo0, hi0, sr, t_hi, t0);
-      const bool h1 = slab_hit32(lo1, hi1, sr, t_hi, t1) & (c1 != kBvhEmpty);
-      n_boxes += 2;
-      if (h0 && h1) {
-        const bool flip = t1 < t0;
-        stk(sp++) = flip ? c0 : c1;
-        e = flip ? c1 : c0;
-      } else {
-        e = h0 ? c0 : h1 ? c1 : pop();
-      }
-    } else {  // a leaf: its spheres
-      const int code = -(e + 1);
-      const int first = code >> 7, cnt = code & 127;
-      for (int k = first; k < first + cnt; ++k) {
-        const SphereDiag& r = sd[k];
-        const double s0 = r.s[0], s1 = r.s[1], s2 = r.s[2];
-        sphere_test<SHADOW>(s0 * o.x + r.t[0], s1 * o.y + r.t[1], s2 * o.z + r.t[2], s0 * d.x, s1 * d.y, s2 * d.z,
-                            [&] { return (int)r.meta; }, h, n_disc);
-      }
-      n_tests += (unsigned)cnt;
-      if constexpr (SHADOW) {
-        if (h.key >= 0 && h.t < t_shadow) break;  // shadowed: done
-      } else {
-        t_hi = f32_up(h.t);
-      }
+    if (e >= 0) {
+      visit();
+    } else {
+      if (leaf(e)) break;  // shadowed: done
       e = pop();
     }
   }
@@ -576,13 +608,13 @@ struct LaneScene {
 template <int LANE>
 __device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, int* static_stack, unsigned char* dyn) {
   LaneScene ls{sc.bvh, sc.sph_diag, static_stack};
-  if constexpr (LANE == 5 || LANE == 6) {  // 6: the sphere records stay in global memory
+  if constexpr (LANE >= 5) {  // 6: the sphere records stay in global memory
     int* stack = (int*)dyn;
     BvhNode* nodes = (BvhNode*)(dyn + lane_stack_bytes(sc.bvh_depth));
     const uint4* gn = (const uint4*)sc.bvh;
     uint4* ln = (uint4*)nodes;
     for (int i = threadIdx.x; i < sc.n_bvh * (int)(sizeof(BvhNode) / 16); i += blockDim.x) ln[i] = gn[i];
-    if constexpr (LANE == 5) {
+    if constexpr (LANE != 6) {
       SphereDiag* sd = (SphereDiag*)((unsigned char*)nodes + (size_t)sc.n_bvh * sizeof(BvhNode));
       const uint4* gs = (const uint4*)sc.sph_diag;
       uint4* ls4 = (uint4*)sd;
@@ -620,7 +652,7 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest_bvh(DevScene
     if constexpr (LANE && !PRIMARY) {
       hit_init(h);
       trace_rest<false, QUADS>(sc, o, d, h, n_disc);  // planes first: an early nearest hit tightens the culling
-      lane_trace<false, LDS_STACK>(ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, n_disc, n_tests, n_boxes, ls.stack);
+      lane_trace<false, LDS_STACK, LANE == 7 || LANE == 3>(ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, n_disc, n_tests, n_boxes, ls.stack);
     } else {
       bvh_trace<PRIMARY, false>(sc, (cPrimRec)a.prim, stk, o, d, 0.0, h, n_disc, n_tests, n_boxes);
       trace_rest<false, QUADS>(sc, o, d, h, n_disc);
@@ -656,7 +688,7 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow_bvh(DevScene 
     if constexpr (LANE) {
       hit_init(h);
       trace_rest<true, QUADS>(sc, o, d, h, n_disc);  // planes first: any hit before the light ends the ray
-      lane_trace<true, LDS_STACK>(ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, dist, h, n_disc, n_tests, n_boxes, ls.stack);
+      lane_trace<true, LDS_STACK, LANE == 7 || LANE == 3>(ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, dist, h, n_disc, n_tests, n_boxes, ls.stack);
     } else {
       bvh_trace<false, true>(sc, nullptr, stk, o, d, dist, h, n_disc, n_tests, n_boxes);
       if (__any(!(h.key >= 0 && h.t < dist))) trace_rest<true, QUADS>(sc, o, d, h, n_disc);
@@ -988,11 +1020,19 @@ static hipError_t launch_closest_q(const DevScene& sc, const DevCamera& cam, con
       auto k = wf_trace_closest_bvh<false, QUADS, 6, TW>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, n)), dim3(kTraceBlock), lds, stream, sc, cam, a);
+    } else if (g_wf_lane == 7 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc) <= kWfLdsLimit) {
+      const size_t lds = lane_lds_bytes(sc);
+      auto k = wf_trace_closest_bvh<false, QUADS, 7, TW>;
+      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, n)), dim3(kTraceBlock), lds, stream, sc, cam, a);
     } else if (g_wf_lane >= 5 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc) <= kWfLdsLimit) {
       const size_t lds = lane_lds_bytes(sc);
       auto k = wf_trace_closest_bvh<false, QUADS, 5, TW>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, n)), dim3(kTraceBlock), lds, stream, sc, cam, a);
+    } else if (g_wf_lane == 7 && sc.bvh_depth <= kLaneLdsDepth) {
+      auto k = wf_trace_closest_bvh<false, QUADS, 3, TW>;
+      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
     } else if (g_wf_lane && g_wf_lane != 2 && sc.bvh_depth <= kLaneLdsDepth) {
       auto k = wf_trace_closest_bvh<false, QUADS, 2, TW>;
       WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
@@ -1034,11 +1074,19 @@ static hipError_t launch_shadow_q(const DevScene& sc, const WfArgs& a, bool lds_
       auto k = wf_trace_shadow_bvh<QUADS, 6, TW>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, a.n_shadow)), dim3(kTraceBlock), lds, stream, sc, a);
+    } else if (g_wf_lane == 7 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc) <= kWfLdsLimit) {
+      const size_t lds = lane_lds_bytes(sc);
+      auto k = wf_trace_shadow_bvh<QUADS, 7, TW>;
+      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, a.n_shadow)), dim3(kTraceBlock), lds, stream, sc, a);
     } else if (g_wf_lane >= 5 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc) <= kWfLdsLimit) {
       const size_t lds = lane_lds_bytes(sc);
       auto k = wf_trace_shadow_bvh<QUADS, 5, TW>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, a.n_shadow)), dim3(kTraceBlock), lds, stream, sc, a);
+    } else if (g_wf_lane == 7 && sc.bvh_depth <= kLaneLdsDepth) {
+      auto k = wf_trace_shadow_bvh<QUADS, 3, TW>;
+      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, a.n_shadow)), dim3(kTraceBlock), 0, stream, sc, a);
     } else if (g_wf_lane && g_wf_lane != 2 && sc.bvh_depth <= kLaneLdsDepth) {
       auto k = wf_trace_shadow_bvh<QUADS, 2, TW>;
       WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, a.n_shadow)), dim3(kTraceBlock), 0, stream, sc, a);

@@ -213,15 +213,18 @@ def test_skipped_shadow_rays_bitwise(rt, neg_zero):
     assert full.to_numpy().tobytes() == exact.to_numpy().tobytes()
 
 
-@pytest.mark.parametrize("lane", [0, 1, 2, 5, 6])
+@pytest.mark.parametrize("lane", [0, 1, 2, 5, 6, 7])
 def test_traversal_variants_bitwise(rt, lane):
     """Every traversal variant (wave / per-lane with LDS or scratch stack /
-    per-lane with the scene staged in LDS) gives the exhaustive frame."""
+    per-lane with the scene or the nodes staged in LDS / per-lane with leaves
+    batched across the wave, the default) gives the exhaustive frame. The
+    scenes above that do not fit in LDS (3000 spheres) run the batched-leaf
+    variant with the scene in global memory."""
     w, cam, depth = _glass_cluster(rt, n=250, seed=21, inside=False)
     exact, _ = cam.render(w, depth, want_stats=True)
     rt._rtamd._tuning_set("lane", lane)
     try:
         fast, _ = cam.render(w, depth, want_stats=False)
     finally:
-        rt._rtamd._tuning_set("lane", 5)
+        rt._rtamd._tuning_set("lane", 7)
     assert fast.to_numpy().tobytes() == exact.to_numpy().tobytes()

@@ -17,3 +17,6 @@ run p4 --pmc FETCH_SIZE && \
 run p5 --pmc WRITE_SIZE && \
 run p6 --pmc TCC_HIT_sum TCC_MISS_sum && \
 python tools/pmc_summary.py $OUT/pmc_summary.json --dominant closest --traversal ${TRAVERSAL:-bvh} $OUT/p1 $OUT/p2 $OUT/p3 $OUT/p4 $OUT/p5 $OUT/p6 > /dev/null && echo "summary ok" | tee -a $OUT/steps.log
+# optional extra counters (LDS use, VALU lane utilisation); kept out of the summary's && chain
+run p7 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS
+run p8 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU
