@@ -89,48 +89,69 @@ __device__ __forceinline__ void gen0_pixel(const WfArgs& a, uint32_t hsize, uint
   lr = r0 + wy;
 }
 
-// Block-aggregated queue appends for wf_prep (one atomic per counter per
-// block instead of per wave: the counters are single hot addresses).
-// Called by every thread of the block (it synchronises). A lane gets `n_s`
-// consecutive shadow slots, and with want_r / want_f one ray slot each in the
-// next generation (reflected rays of the block first).
-__device__ __forceinline__ void block_append(unsigned* shadow_ctr, unsigned n_s, unsigned* ray_ctr, bool want_r,
-                                             bool want_f, unsigned& so, unsigned& ro, unsigned& fo) {
-  __shared__ unsigned s_cnt[kWfBlock / 64][3];
-  __shared__ unsigned s_base[3];
-  const unsigned lane = lane_id(), wave = threadIdx.x / 64;
+// Queue appends without block barriers or hot counters (DESIGN.md "Sharded
+// queues"). The queues of a generation are split into kShards regions of a
+// fixed capacity; wave-iteration q (rays 64q .. 64q+63 of the generation)
+// appends to region (q / kShardGroup) mod kShards with one atomic per queue,
+// on that region's own counter (128 B apart). Groups of kShardGroup adjacent
+// wave-iterations share a region, so neighbouring rays stay neighbours. Every lane of the wave calls it. A lane gets
+// `n_s` consecutive shadow-list slots and one ray slot each for want_r /
+// want_f (returned as absolute slots; ~0u when the region is full, which the
+// capacities rule out).
+__device__ __forceinline__ void shard_append(const WfArgs& a, unsigned q, unsigned n_s, bool want_r, bool want_f,
+                                             unsigned& so, unsigned& ro, unsigned& fo) {
+  const unsigned lane = lane_id();
+  const unsigned s = (q / kShardGroup) % kShards;
   const unsigned long long mr = __ballot(want_r), mf = __ballot(want_f);
   const unsigned long long below = (1ull << lane) - 1ull;
-  unsigned incl = n_s;  // inclusive prefix of the shadow counts over the wave
+  unsigned incl = n_s;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
     const unsigned t = (unsigned)__shfl_up((int)incl, off, 64);
     if ((int)lane >= off) incl += t;
   }
-  if (lane == 63) s_cnt[wave][0] = incl;
+  const unsigned s_tot = (unsigned)__shfl((int)incl, 63, 64);
+  const unsigned nr = (unsigned)__popcll(mr), nf = (unsigned)__popcll(mf);
+  unsigned sb = 0, rb = 0;
   if (lane == 0) {
-    s_cnt[wave][1] = (unsigned)__popcll(mr);
-    s_cnt[wave][2] = (unsigned)__popcll(mf);
+    if (s_tot) sb = atomicAdd(a.sh_cnt + s * kShardStride, s_tot);
+    if (nr + nf) rb = atomicAdd(a.out_cnt + s * kShardStride, nr + nf);
+  }
+  sb = (unsigned)__shfl((int)sb, 0, 64) + (incl - n_s);
+  rb = (unsigned)__shfl((int)rb, 0, 64);
+  const unsigned r_off = rb + (unsigned)__popcll(mr & below), f_off = rb + nr + (unsigned)__popcll(mf & below);
+  so = sb + n_s <= a.sh_cap ? s * a.sh_cap + sb : ~0u;
+  ro = r_off < a.out_cap ? s * a.out_cap + r_off : ~0u;
+  fo = f_off < a.out_cap ? s * a.out_cap + f_off : ~0u;
+}
+
+// Block-wide: the exclusive prefix of a generation's kShards region counts
+// into pre[0..kShards] (LDS), or nullptr for a dense generation. Every thread
+// of the block calls it (it synchronises when cnt != nullptr).
+__device__ __forceinline__ const unsigned* shard_prefix(const unsigned* cnt, unsigned* pre) {
+  if (!cnt) return nullptr;
+  if (threadIdx.x < 64) {
+    const unsigned v = threadIdx.x < kShards ? cnt[threadIdx.x * kShardStride] : 0u;
+    unsigned incl = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const unsigned t = (unsigned)__shfl_up((int)incl, off, 64);
+      if ((int)threadIdx.x >= off) incl += t;
+    }
+    if (threadIdx.x < kShards) pre[threadIdx.x + 1] = incl;
+    if (threadIdx.x == 0) pre[0] = 0;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned t[3] = {0, 0, 0};
-    for (unsigned w = 0; w < kWfBlock / 64; ++w)
-      for (int k = 0; k < 3; ++k) {
-        const unsigned c = s_cnt[w][k];
-        s_cnt[w][k] = t[k];  // exclusive prefix over the block's waves
-        t[k] += c;
-      }
-    s_base[0] = t[0] ? atomicAdd(shadow_ctr, t[0]) : 0u;
-    const unsigned rb = (t[1] + t[2]) ? atomicAdd(ray_ctr, t[1] + t[2]) : 0u;
-    s_base[1] = rb;
-    s_base[2] = rb + t[1];
-  }
-  __syncthreads();
-  so = s_base[0] + s_cnt[wave][0] + (incl - n_s);
-  ro = s_base[1] + s_cnt[wave][1] + (unsigned)__popcll(mr & below);
-  fo = s_base[2] + s_cnt[wave][2] + (unsigned)__popcll(mf & below);
-  __syncthreads();  // s_cnt / s_base are reused by the next call
+  return pre;
+}
+// Slot of the j-th entry of a sharded queue (regions of `cap`), j < pre[kShards].
+__device__ __forceinline__ unsigned shard_slot(const unsigned* pre, unsigned cap, unsigned j) {
+  if (!pre) return j;
+  unsigned lo = 0;
+#pragma unroll
+  for (unsigned step = kShards / 2; step > 0; step >>= 1)
+    if (pre[lo + step] <= j) lo += step;
+  return lo * cap + (j - pre[lo]);
 }
 
 // Root rays of generation 0: sample `smp` of a pixel of the shard
@@ -328,16 +349,19 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest(DevScene sc,
   unsigned n_disc = 0;
   WfLds lv{};
   if constexpr (USE_LDS) lv = wf_lds_stage<PRIMARY>(sc, a.prim, lds_raw);
+  __shared__ unsigned s_pre[kShards + 1];
+  const unsigned* pre = shard_prefix(a.in_cnt, s_pre);
   const unsigned stride = gridDim.x * blockDim.x;
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
+    const unsigned slot = shard_slot(pre, a.in_cap, i);
     V3 o, d;
-    wf_ray(a, cam, i, o, d);
+    wf_ray(a, cam, slot, o, d);
     Hit h;
     if constexpr (USE_LDS) wf_trace_lds<PRIMARY, false, QUADS>(sc, lv, o, d, h, n_disc);
     else trace<false>(sc, o, d, h, n_disc);
     WfHit w;
     w.t = h.t; w.key = h.key; w.c1k = h.c1k; w.c2k = h.c2k; w.hin = h.hin;
-    a.hits[i] = w;
+    a.hits[slot] = w;
   }
   const unsigned long long s = wave_sum(n_disc);
   if (lane_id() == 0 && s) atomicAdd(&a.cnt->disc[a.disc_slot], s);
@@ -353,12 +377,14 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow(DevScene sc, 
   unsigned n_disc = 0;
   WfLds lv{};
   if constexpr (USE_LDS) lv = wf_lds_stage<false>(sc, nullptr, lds_raw);
+  __shared__ unsigned s_pre[kShards + 1];
+  const unsigned* pre = shard_prefix(a.sh_cnt, s_pre);
   const unsigned stride = gridDim.x * blockDim.x;
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n_shadow; i += stride) {
     V3 o, d;
     double dist;
     unsigned slot;
-    shadow_ray(sc, a, i, o, d, dist, slot);
+    shadow_ray(sc, a, shard_slot(pre, a.sh_cap, i), o, d, dist, slot);
     Hit h;
     if constexpr (USE_LDS) wf_trace_lds<false, true, QUADS>(sc, lv, o, d, h, n_disc);
     else trace<true>(sc, o, d, h, n_disc);
@@ -366,6 +392,88 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow(DevScene sc, 
   }
   const unsigned long long s = wave_sum(n_disc);
   if (lane_id() == 0 && s) atomicAdd(&a.cnt->disc[a.disc_slot], s);
+}
+
+// ---------------------------------------------------------- prep (spawn)
+// prepare_computations (intersection.rs:53-105) of ray i's finished hit `h`
+// (stored at `slot`) and the spawn of its shadow, reflected and refracted rays
+// (world.rs:40-134): the hit node, the shadow-list entries and the next
+// generation's rays. Every lane of the wave calls it (shard_append), `valid`
+// false for the padding lanes. wf_prep runs it on the stored hits; the BVH
+// trace kernels run it right after their traversal (no hit queue).
+__device__ __forceinline__ void prep_one(const DevScene& sc, const WfArgs& a, unsigned i, unsigned slot, bool valid,
+                                         V3 o, V3 d, const Hit& h) {
+  const unsigned L = (unsigned)sc.n_lights;
+  const unsigned remaining = a.max_depth - a.g;
+  bool hit = false, want_refl = false, want_refr = false;
+  Comps c{};
+  V3 refr_dir = v3(0, 0, 0);
+  const ShadeRec* m = nullptr;
+  if (valid) {
+    if (h.key >= 0) {
+      c = prepare(sc, o, d, h);
+      hit = true;
+      m = &sc.shade[c.obj];
+      // reflected_color (world.rs:107-114)
+      want_refl = !(req(m->reflective, 0.0) || remaining == 0);
+      // refracted_color (world.rs:116-134)
+      if (!(req(m->transparency, 0.0) || remaining == 0)) {
+        const double n_ratio = c.n1 / c.n2;
+        const double cos_i = vdot(c.eyev, c.normal);
+        const double sin2_t = n_ratio * n_ratio * (1.0 - cos_i * cos_i);
+        if (!(sin2_t > 1.0)) {
+          const double cos_t = sqrt(1.0 - sin2_t);
+          refr_dir = vsub(vscale(c.normal, n_ratio * cos_i - cos_t), vscale(c.eyev, n_ratio));
+          want_refr = true;
+        }
+      }
+    }
+  }
+  // shadow rays: one per light (world.rs:41-56); the fast path leaves out the
+  // ones whose answer cannot change the colour (their flag is written here)
+  unsigned n_s = 0, skip = 0;
+  if (hit) {
+    for (unsigned l = 0; l < L; ++l) {
+      if (a.skip_shadow && l < 32 && shadow_irrelevant(*m, (cLightRec)sc.lights + l, c.over, c.normal))
+        skip |= 1u << l;
+      else
+        ++n_s;
+    }
+  }
+  unsigned sbase, rbase, fbase;
+  shard_append(a, i / 64, n_s, want_refl, want_refr, sbase, rbase, fbase);
+  if (!valid) return;
+  WfNode nd;
+  nd.obj = -1; nd.child_refl = -1; nd.child_refr = -1; nd.pad = 0;
+  if (hit) {
+    nd.obj = c.obj;
+    nd.over[0] = c.over.x; nd.over[1] = c.over.y; nd.over[2] = c.over.z;
+    nd.normal[0] = c.normal.x; nd.normal[1] = c.normal.y; nd.normal[2] = c.normal.z;
+    // shade_hit's Schlick factor (world.rs:62-64), same inputs as the reference's call
+    nd.schlick = (m->reflective > 0.0 && m->transparency > 0.0) ? schlick(c.eyev, c.normal, c.n1, c.n2) : 0.0;
+    for (unsigned l = 0; l < L; ++l) {  // its shadow rays are built by the shadow trace
+      if (l < 32 && (skip >> l & 1u)) a.sflags[slot * L + l] = 0;
+      else if (sbase != ~0u) a.shadow_nodes[sbase++] = (int32_t)(slot * L + l);
+    }
+    if (want_refl && rbase != ~0u) {
+      const V3 rv = vreflect(d, c.normal);  // comps.reflectv (intersection.rs:101)
+      WfRay r;
+      r.o[0] = c.over.x; r.o[1] = c.over.y; r.o[2] = c.over.z;
+      r.d[0] = rv.x; r.d[1] = rv.y; r.d[2] = rv.z;
+      r.pad = 0;
+      a.next_rays[rbase] = r;
+      nd.child_refl = (int)rbase;
+    }
+    if (want_refr && fbase != ~0u) {
+      WfRay r;
+      r.o[0] = c.under.x; r.o[1] = c.under.y; r.o[2] = c.under.z;
+      r.d[0] = refr_dir.x; r.d[1] = refr_dir.y; r.d[2] = refr_dir.z;
+      r.pad = 0;
+      a.next_rays[fbase] = r;
+      nd.child_refr = (int)fbase;
+    }
+  }
+  a.nodes[slot] = nd;
 }
 
 // ------------------------------------------------------------ BVH traversal
@@ -643,24 +751,32 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest_bvh(DevScene
   extern __shared__ __attribute__((aligned(16))) unsigned char lane_dyn[];
   int* stk = LDS_STACK ? stack_lds + threadIdx.x : stack_lds + (threadIdx.x / 64) * (kBvhMaxDepth + 4);
   const LaneScene ls = lane_scene<LANE>(sc, stk, lane_dyn);
+  __shared__ unsigned s_pre[kShards + 1];
+  const unsigned* pre = shard_prefix(a.in_cnt, s_pre);
   unsigned n_disc = 0, n_tests = 0, n_boxes = 0;
   const unsigned stride = gridDim.x * blockDim.x;
-  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
-    V3 o, d;
-    wf_ray(a, cam, i, o, d);
+  // every lane of a wave runs the same number of iterations (prep_one's appends are wave-wide)
+  const unsigned n_iter = (a.n + stride - 1) / stride;
+  unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+  for (unsigned it = 0; it < n_iter; ++it, i += stride) {
+    const bool valid = i < a.n;
+    const unsigned slot = valid ? shard_slot(pre, a.in_cap, i) : 0u;
+    V3 o = v3(0, 0, 0), d = v3(0, 0, 0);
     Hit h;
-    if constexpr (LANE && !PRIMARY) {
-      hit_init(h);
-      trace_rest<false, QUADS>(sc, o, d, h, n_disc);  // planes first: an early nearest hit tightens the culling
-      lane_trace<false, LDS_STACK, LANE == 7 || LANE == 3>(ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, n_disc, n_tests, n_boxes, ls.stack);
-    } else {
-      bvh_trace<PRIMARY, false>(sc, (cPrimRec)a.prim, stk, o, d, 0.0, h, n_disc, n_tests, n_boxes);
-      trace_rest<false, QUADS>(sc, o, d, h, n_disc);
+    hit_init(h);
+    if (valid) {
+      wf_ray(a, cam, slot, o, d);
+      if constexpr (LANE && !PRIMARY) {
+        trace_rest<false, QUADS>(sc, o, d, h, n_disc);  // planes first: an early nearest hit tightens the culling
+        lane_trace<false, LDS_STACK, LANE == 7 || LANE == 3>(ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h,
+                                                             n_disc, n_tests, n_boxes, ls.stack);
+      } else {
+        bvh_trace<PRIMARY, false>(sc, (cPrimRec)a.prim, stk, o, d, 0.0, h, n_disc, n_tests, n_boxes);
+        trace_rest<false, QUADS>(sc, o, d, h, n_disc);
+      }
     }
     hit_finish(h);
-    WfHit w;
-    w.t = h.t; w.key = h.key; w.c1k = h.c1k; w.c2k = h.c2k; w.hin = h.hin;
-    a.hits[i] = w;
+    prep_one(sc, a, i, slot, valid, o, d, h);  // the hit is shaded and spawned right here
   }
   const unsigned long long s = wave_sum(n_disc), st = wave_sum(n_tests), sb = wave_sum(n_boxes);
   if (lane_id() == 0) {
@@ -677,13 +793,15 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow_bvh(DevScene 
   extern __shared__ __attribute__((aligned(16))) unsigned char lane_dyn[];
   int* stk = LDS_STACK ? stack_lds + threadIdx.x : stack_lds + (threadIdx.x / 64) * (kBvhMaxDepth + 4);
   const LaneScene ls = lane_scene<LANE>(sc, stk, lane_dyn);
+  __shared__ unsigned s_pre[kShards + 1];
+  const unsigned* pre = shard_prefix(a.sh_cnt, s_pre);
   unsigned n_disc = 0, n_tests = 0, n_boxes = 0;
   const unsigned stride = gridDim.x * blockDim.x;
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n_shadow; i += stride) {
     V3 o, d;
     double dist;
     unsigned slot;
-    shadow_ray(sc, a, i, o, d, dist, slot);
+    shadow_ray(sc, a, shard_slot(pre, a.sh_cap, i), o, d, dist, slot);
     Hit h;
     if constexpr (LANE) {
       hit_init(h);
@@ -704,90 +822,25 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow_bvh(DevScene 
   }
 }
 
-// ---------------------------------------------------------- prep (spawn)
 __global__ __launch_bounds__(kWfBlock) void wf_prep(DevScene sc, DevCamera cam, WfArgs a) {
+  __shared__ unsigned s_pre[kShards + 1];
+  const unsigned* pre = shard_prefix(a.in_cnt, s_pre);
   const unsigned stride = gridDim.x * blockDim.x;
-  const unsigned L = (unsigned)sc.n_lights;
-  const unsigned remaining = a.max_depth - a.g;
-  // every lane of a wave runs the same number of iterations (appends are convergent)
+  // every lane of a wave runs the same number of iterations (appends are wave-wide)
   const unsigned n_iter = (a.n + stride - 1) / stride;
   unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
   for (unsigned it = 0; it < n_iter; ++it, i += stride) {
     const bool valid = i < a.n;
-    bool hit = false, want_refl = false, want_refr = false;
-    Comps c{};
-    V3 d = v3(0, 0, 0), refr_dir = v3(0, 0, 0);
-    const ShadeRec* m = nullptr;
+    const unsigned slot = valid ? shard_slot(pre, a.in_cap, i) : 0u;
+    V3 o = v3(0, 0, 0), d = v3(0, 0, 0);
+    Hit h;
+    h.key = -1;
     if (valid) {
-      V3 o;
-      wf_ray(a, cam, i, o, d);
-      const WfHit w = a.hits[i];
-      if (w.key >= 0) {
-        Hit h;
-        h.t = w.t; h.key = w.key; h.hin = w.hin; h.c1k = w.c1k; h.c2k = w.c2k; h.c1t = 0; h.c2t = 0;
-        c = prepare(sc, o, d, h);
-        hit = true;
-        m = &sc.shade[c.obj];
-        // reflected_color (world.rs:107-114)
-        want_refl = !(req(m->reflective, 0.0) || remaining == 0);
-        // refracted_color (world.rs:116-134)
-        if (!(req(m->transparency, 0.0) || remaining == 0)) {
-          const double n_ratio = c.n1 / c.n2;
-          const double cos_i = vdot(c.eyev, c.normal);
-          const double sin2_t = n_ratio * n_ratio * (1.0 - cos_i * cos_i);
-          if (!(sin2_t > 1.0)) {
-            const double cos_t = sqrt(1.0 - sin2_t);
-            refr_dir = vsub(vscale(c.normal, n_ratio * cos_i - cos_t), vscale(c.eyev, n_ratio));
-            want_refr = true;
-          }
-        }
-      }
+      wf_ray(a, cam, slot, o, d);
+      const WfHit w = a.hits[slot];
+      h.t = w.t; h.key = w.key; h.hin = w.hin; h.c1k = w.c1k; h.c2k = w.c2k; h.c1t = 0; h.c2t = 0;
     }
-    // shadow rays: one per light (world.rs:41-56); the fast path leaves out the
-    // ones whose answer cannot change the colour (their flag is written here)
-    unsigned n_s = 0, skip = 0;
-    if (hit) {
-      for (unsigned l = 0; l < L; ++l) {
-        if (a.skip_shadow && l < 32 && shadow_irrelevant(*m, (cLightRec)sc.lights + l, c.over, c.normal))
-          skip |= 1u << l;
-        else
-          ++n_s;
-      }
-    }
-    unsigned sbase, rbase, fbase;
-    block_append(&a.cnt->n_shadow[a.g], n_s, &a.cnt->n_rays[a.g + 1], want_refl, want_refr, sbase, rbase, fbase);
-    if (!valid) continue;
-    WfNode nd;
-    nd.obj = -1; nd.child_refl = -1; nd.child_refr = -1; nd.pad = 0;
-    if (hit) {
-      nd.obj = c.obj;
-      nd.over[0] = c.over.x; nd.over[1] = c.over.y; nd.over[2] = c.over.z;
-      nd.normal[0] = c.normal.x; nd.normal[1] = c.normal.y; nd.normal[2] = c.normal.z;
-      // shade_hit's Schlick factor (world.rs:62-64), same inputs as the reference's call
-      nd.schlick = (m->reflective > 0.0 && m->transparency > 0.0) ? schlick(c.eyev, c.normal, c.n1, c.n2) : 0.0;
-      for (unsigned l = 0; l < L; ++l) {  // its shadow rays are built by the shadow trace
-        if (l < 32 && (skip >> l & 1u)) a.sflags[i * L + l] = 0;
-        else a.shadow_nodes[sbase++] = (int32_t)(i * L + l);
-      }
-      if (want_refl && rbase < a.cap_next) {
-        const V3 rv = vreflect(d, c.normal);  // comps.reflectv (intersection.rs:101)
-        WfRay r;
-        r.o[0] = c.over.x; r.o[1] = c.over.y; r.o[2] = c.over.z;
-        r.d[0] = rv.x; r.d[1] = rv.y; r.d[2] = rv.z;
-        r.pad = 0;
-        a.next_rays[rbase] = r;
-        nd.child_refl = (int)rbase;
-      }
-      if (want_refr && fbase < a.cap_next) {
-        WfRay r;
-        r.o[0] = c.under.x; r.o[1] = c.under.y; r.o[2] = c.under.z;
-        r.d[0] = refr_dir.x; r.d[1] = refr_dir.y; r.d[2] = refr_dir.z;
-        r.pad = 0;
-        a.next_rays[fbase] = r;
-        nd.child_refr = (int)fbase;
-      }
-    }
-    a.nodes[i] = nd;
+    prep_one(sc, a, i, slot, valid, o, d, h);
   }
 }
 
@@ -798,19 +851,22 @@ __global__ __launch_bounds__(kWfBlock) void wf_combine(DevScene sc, DevCamera ca
   const unsigned stride = gridDim.x * blockDim.x;
   const unsigned L = (unsigned)sc.n_lights;
   cLightRec lights = (cLightRec)sc.lights;
+  __shared__ unsigned s_pre[kShards + 1];
+  const unsigned* pre = shard_prefix(a.in_cnt, s_pre);
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
-    const WfNode nd = a.nodes[i];
+    const unsigned slot = shard_slot(pre, a.in_cap, i);
+    const WfNode nd = a.nodes[slot];
     V3 color = v3(0.0, 0.0, 0.0);
     if (nd.obj >= 0) {
       V3 o, d;
-      wf_ray(a, cam, i, o, d);
+      wf_ray(a, cam, slot, o, d);
       const ShadeRec& m = sc.shade[nd.obj];
       const V3 over = v3(nd.over[0], nd.over[1], nd.over[2]);
       const V3 normal = v3(nd.normal[0], nd.normal[1], nd.normal[2]);
       const V3 eyev = vneg(d);
       V3 surface = v3(0.0, 0.0, 0.0);  // Sum = fold from (0,0,0) (color.rs:96-103)
       for (unsigned l = 0; l < L; ++l) {
-        const bool shadowed = a.sflags[i * L + l] != 0;
+        const bool shadowed = a.sflags[slot * L + l] != 0;
         surface = vadd(surface, lighting(m, lights + l, over, eyev, normal, shadowed));
       }
       V3 refl = v3(0.0, 0.0, 0.0), refr = v3(0.0, 0.0, 0.0);
@@ -829,7 +885,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_combine(DevScene sc, DevCamera ca
         color = vadd(vadd(surface, refl), refr);
       }
     }
-    size_t oi = i;
+    size_t oi = slot;
     if (a.g == 0 && a.camera_mode && a.aa == 1) {  // generation 0 is tile-ordered: write row-major
       uint32_t x, lr, smp;
       gen0_pixel(a, cam.hsize, i, x, lr, smp);
@@ -864,8 +920,10 @@ __global__ __launch_bounds__(kWfBlock) void wf_average(WfArgs a, unsigned hsize,
 __global__ void wf_count_kinds(WfArgs a) {
   unsigned nrefl = 0, nrefr = 0;
   const unsigned stride = gridDim.x * blockDim.x;
+  __shared__ unsigned s_pre[kShards + 1];
+  const unsigned* pre = shard_prefix(a.in_cnt, s_pre);
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
-    const WfNode nd = a.nodes[i];
+    const WfNode nd = a.nodes[shard_slot(pre, a.in_cap, i)];
     nrefl += nd.child_refl >= 0;
     nrefr += nd.child_refr >= 0;
   }
@@ -890,6 +948,7 @@ Wavefront::~Wavefront() {
     (void)hipFree(g.shadow_nodes); (void)hipFree(g.sflags);
   }
   if (d_cnt_) (void)hipFree(d_cnt_);
+  if (d_shard_) (void)hipFree(d_shard_);
   if (d_prim_) (void)hipFree(d_prim_);
   if (ev0_) (void)hipEventDestroy(ev0_);
   if (ev1_) (void)hipEventDestroy(ev1_);
@@ -943,15 +1002,15 @@ hipError_t Wavefront::last_profile(WfProfile* out) {
 
 // Grow-only per-generation buffers. The shadow queue and the shadow flags are
 // sized rays * n_lights (at most one shadow ray per light per hit).
-hipError_t Wavefront::ensure_gen(size_t g, size_t rays, size_t n_lights) {
+hipError_t Wavefront::ensure_gen(size_t g, size_t slots, size_t n_lights, size_t list_slots) {
   if (gens_.size() <= g) gens_.resize(g + 1);
   WfGenBuf& b = gens_[g];
-  rays = std::max<size_t>(rays, 1);
-  if (b.cap_rays < rays) {
+  slots = std::max<size_t>(slots, 1);
+  if (b.cap_rays < slots) {
     (void)hipFree(b.rays); (void)hipFree(b.hits); (void)hipFree(b.nodes); (void)hipFree(b.colors);
     b.rays = nullptr; b.hits = nullptr; b.nodes = nullptr; b.colors = nullptr;
     b.cap_rays = 0;
-    const size_t cap = rays + rays / 8;
+    const size_t cap = slots + slots / 8;
     WF_CHECK(hipMalloc(&b.rays, cap * sizeof(WfRay)));
     WF_CHECK(hipMalloc(&b.hits, cap * sizeof(WfHit)));
     WF_CHECK(hipMalloc(&b.nodes, cap * sizeof(WfNode)));
@@ -960,18 +1019,27 @@ hipError_t Wavefront::ensure_gen(size_t g, size_t rays, size_t n_lights) {
   }
   const size_t need_sh = std::max<size_t>(b.cap_rays * n_lights, 1);
   if (b.cap_shadows < need_sh) {
-    (void)hipFree(b.shadow_nodes); (void)hipFree(b.sflags);
-    b.shadow_nodes = nullptr; b.sflags = nullptr;
+    (void)hipFree(b.sflags);
+    b.sflags = nullptr;
     b.cap_shadows = 0;
-    WF_CHECK(hipMalloc(&b.shadow_nodes, need_sh * sizeof(int32_t)));
     WF_CHECK(hipMalloc(&b.sflags, need_sh));
     b.cap_shadows = need_sh;
+  }
+  list_slots = std::max<size_t>(list_slots, 1);
+  if (b.cap_list < list_slots) {
+    (void)hipFree(b.shadow_nodes);
+    b.shadow_nodes = nullptr;
+    b.cap_list = 0;
+    const size_t cap = list_slots + list_slots / 8;
+    WF_CHECK(hipMalloc(&b.shadow_nodes, cap * sizeof(int32_t)));
+    b.cap_list = cap;
   }
   return hipSuccess;
 }
 
 hipError_t Wavefront::ensure_misc(size_t n_diag) {
   if (!d_cnt_) WF_CHECK(hipMalloc(&d_cnt_, sizeof(WfCounters)));
+  if (!d_shard_) WF_CHECK(hipMalloc(&d_shard_, (size_t)kMaxGen * 2 * kShards * kShardStride * sizeof(unsigned)));
   if (!ev0_) WF_CHECK(hipEventCreate(&ev0_));
   if (!ev1_) WF_CHECK(hipEventCreate(&ev1_));
   if (prim_cap_ < n_diag + 4) {
@@ -1139,7 +1207,9 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
   counts.rays[0] = n0;
 
   WF_CHECK(hipMemsetAsync(d_cnt_, 0, sizeof(WfCounters), stream));
-  WF_CHECK(ensure_gen(0, n0, L));
+  WF_CHECK(hipMemsetAsync(d_shard_, 0, (size_t)(max_depth + 2) * 2 * kShards * kShardStride * sizeof(unsigned),
+                          stream));
+  WF_CHECK(ensure_gen(0, n0, L, 0));
   if (!camera_mode) {
     // batch rays: n0 x 6 doubles -> WfRay queue of generation 0
     WF_CHECK(hipMemcpy2DAsync(gens_[0].rays, sizeof(WfRay), d_in_rays, 6 * sizeof(double), 6 * sizeof(double), n0,
@@ -1157,14 +1227,20 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
   if (profiling_) ++pframes_;
   prof_rays_[0] = prof_rays_[1] = prof_rays_[2] = 0;
   unsigned last = 0;
+  // per-region capacity of each generation's sharded arrays (generation 0 is dense)
+  std::vector<unsigned> caps(max_depth + 2, 0);
   for (unsigned g = 0; g <= max_depth; ++g) {
     const unsigned n = counts.rays[g];
     if (n == 0) break;
     last = g;
-    // capacity of the next generation: exact when calibrated, else the bound 2n
-    const size_t cap_next = calibrated ? counts.rays[g + 1] : (g < max_depth ? 2ull * n : 0ull);
-    WF_CHECK(ensure_gen(g, n, L));
-    WF_CHECK(ensure_gen(g + 1, cap_next, L));
+    // wave-iteration q of this generation appends to region (q / kShardGroup) mod kShards: a
+    // region receives at most `per` wave-iterations, each spawning <= 128 rays and <= 64 L shadow rays
+    const unsigned groups = ((n + 63) / 64 + kShardGroup - 1) / kShardGroup;
+    const unsigned per = kShardGroup * ((groups + kShards - 1) / kShards);
+    const unsigned out_cap = g < max_depth ? 128u * per : 0u, sh_cap = 64u * L * per;
+    caps[g + 1] = out_cap;
+    WF_CHECK(ensure_gen(g, g == 0 ? n : (size_t)kShards * caps[g], L, (size_t)kShards * sh_cap));
+    WF_CHECK(ensure_gen(g + 1, (size_t)kShards * out_cap, L, 0));
     WfArgs a{};
     WfGenBuf& B = gens_[g];
     a.rays = B.rays; a.hits = B.hits; a.nodes = B.nodes; a.shadow_nodes = B.shadow_nodes; a.sflags = B.sflags;
@@ -1176,7 +1252,12 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     a.cnt = d_cnt_;
     a.prim = d_prim_;
     a.n = n;
-    a.cap_next = (unsigned)cap_next;
+    a.in_cnt = g == 0 ? nullptr : shard_cnt(g, 0);
+    a.in_cap = caps[g];
+    a.out_cnt = shard_cnt(g + 1, 0);
+    a.out_cap = out_cap;
+    a.sh_cnt = shard_cnt(g, 1);
+    a.sh_cap = sh_cap;
     a.g = g; a.max_depth = max_depth;
     a.camera_mode = camera_mode ? 1u : 0u;
     a.row_block = row_block; a.shard = shard; a.n_shards = n_shards;
@@ -1197,17 +1278,26 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
       }
     }
     WF_CHECK(pmark(stream, ccls, false));
-    // 2. prepare_computations + spawn
-    WF_CHECK(pmark(stream, WF_PREP, true));
-    WF_LAUNCH(wf_prep, dim3(occupancy_grid(wf_prep, kWfBlock, 0, n)), dim3(kWfBlock), 0, stream, sc, cam, a);
-    WF_CHECK(hipGetLastError());
-    WF_CHECK(pmark(stream, WF_PREP, false));
+    // 2. prepare_computations + spawn (the BVH trace kernels do it themselves)
+    if (!bvh) {
+      WF_CHECK(pmark(stream, WF_PREP, true));
+      WF_LAUNCH(wf_prep, dim3(occupancy_grid(wf_prep, kWfBlock, 0, n)), dim3(kWfBlock), 0, stream, sc, cam, a);
+      WF_CHECK(hipGetLastError());
+      WF_CHECK(pmark(stream, WF_PREP, false));
+    }
     if (!calibrated) {
-      WfCounters hc;
-      WF_CHECK(hipMemcpyAsync(&hc, d_cnt_, sizeof hc, hipMemcpyDeviceToHost, stream));
+      std::vector<unsigned> hr((size_t)kShards * kShardStride), hs(hr.size());
+      WF_CHECK(hipMemcpyAsync(hr.data(), shard_cnt(g + 1, 0), hr.size() * sizeof(unsigned), hipMemcpyDeviceToHost,
+                              stream));
+      WF_CHECK(hipMemcpyAsync(hs.data(), shard_cnt(g, 1), hs.size() * sizeof(unsigned), hipMemcpyDeviceToHost, stream));
       WF_CHECK(hipStreamSynchronize(stream));
-      counts.rays[g + 1] = g < max_depth ? hc.n_rays[g + 1] : 0;
-      counts.shadows[g] = hc.n_shadow[g];
+      unsigned nr = 0, ns = 0;
+      for (int k = 0; k < kShards; ++k) {
+        nr += hr[(size_t)k * kShardStride];
+        ns += hs[(size_t)k * kShardStride];
+      }
+      counts.rays[g + 1] = g < max_depth ? nr : 0;
+      counts.shadows[g] = ns;
     }
     a.n_shadow = counts.shadows[g];
     // 3. shadow rays
@@ -1238,6 +1328,8 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     a.rows = n0 / aa / (cam.hsize ? cam.hsize : 1);
     a.child_colors = gens_[g + 1].colors;
     a.n = counts.rays[g];
+    a.in_cnt = g == 0 ? nullptr : shard_cnt((unsigned)g, 0);
+    a.in_cap = caps[g];
     a.g = (unsigned)g; a.max_depth = max_depth;
     a.camera_mode = camera_mode ? 1u : 0u;
     a.row_block = row_block; a.shard = shard; a.n_shards = n_shards;

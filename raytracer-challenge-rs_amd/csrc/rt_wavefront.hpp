@@ -29,7 +29,13 @@
 
 namespace rtamd {
 
-struct WfRay {  // 64 B
+// Sharded generation queues (DESIGN.md "Sharded queues"): kShards regions per
+// queue, counters kShardStride uints (128 B) apart.
+constexpr int kShards = 64;
+constexpr int kShardStride = 32;
+constexpr int kShardGroup = 16;  // consecutive wave-iterations sharing a region (one block's worth)
+
+struct WfRay {  // 56 B
   double o[3];
   double d[3];
   int64_t pad;
@@ -61,8 +67,6 @@ extern int g_wf_accel;        // tuning knob: 1 = BVH traversal (when no counter
 extern int g_wf_skip_shadow;  // tuning knob: 1 = the fast path leaves out shadow rays that cannot change the colour
 
 struct WfCounters {
-  unsigned n_rays[kMaxGen];    // appended rays per generation (index g+1 filled by prep(g))
-  unsigned n_shadow[kMaxGen];  // shadow rays per generation
   unsigned n_refl[kMaxGen], n_refr[kMaxGen];
   unsigned long long disc[3];  // disc >= 0 tests: [0] primary closest, [1] closest, [2] shadow
   unsigned long long tests[3];  // BVH mode: sphere tests executed (lanes x spheres), per trace class
@@ -74,9 +78,9 @@ struct WfGenBuf {
   WfHit* hits = nullptr;
   WfNode* nodes = nullptr;
   double* colors = nullptr;
-  int32_t* shadow_nodes = nullptr;  // hit nodes of the generation (each casts one shadow ray per light)
-  uint8_t* sflags = nullptr;
-  size_t cap_rays = 0, cap_shadows = 0;
+  int32_t* shadow_nodes = nullptr;  // shadow list of the generation (node slot * L + light, sharded)
+  uint8_t* sflags = nullptr;         // per node slot and light
+  size_t cap_rays = 0, cap_shadows = 0, cap_list = 0;
 };
 
 // Kernel arguments for one generation.
@@ -85,7 +89,7 @@ struct WfArgs {
   WfHit* hits;
   WfNode* nodes;
   double* colors;       // colors_g (g >= 1) or the output (g == 0)
-  int32_t* shadow_nodes;  // shadow slots: shadow ray j = slot node * L + light
+  int32_t* shadow_nodes;  // shadow list of this generation: entries node slot * L + light
   uint8_t* sflags;
   WfRay* next_rays;     // rays_{g+1}
   const double* child_colors;  // colors_{g+1}
@@ -93,7 +97,6 @@ struct WfArgs {
   const PrimRec* prim;  // per-frame primary records (camera mode, g == 0)
   unsigned n;           // rays in this generation
   unsigned n_shadow;    // shadow rays in this generation
-  unsigned cap_next;    // capacity of rays_{g+1}
   unsigned g, max_depth;
   unsigned camera_mode; // g == 0 rays come from the camera (1) or from `rays` (0)
   unsigned row_block, shard, n_shards;
@@ -101,6 +104,14 @@ struct WfArgs {
   unsigned aa;          // AA samples per pixel (generation 0 in camera mode)
   unsigned rows;        // local rows of the camera shard (generation-0 tiling)
   unsigned skip_shadow; // leave out shadow rays that cannot change the colour (fast path)
+  // sharded queues: this generation's rays (in_cnt == nullptr: dense, slot = index),
+  // the next generation's rays and this generation's shadow list
+  const unsigned* in_cnt;
+  unsigned in_cap;      // per-region capacity of this generation's arrays
+  unsigned* out_cnt;
+  unsigned out_cap;     // per-region capacity of the next generation's arrays
+  unsigned* sh_cnt;
+  unsigned sh_cap;      // per-region capacity of the shadow list
 };
 
 // Per-kernel-class timing of the last frame (profiling mode only).
@@ -138,10 +149,13 @@ class Wavefront {
                     DevStats* stats, float* ms_kernel);
 
  private:
-  hipError_t ensure_gen(size_t g, size_t rays, size_t n_lights);
+  hipError_t ensure_gen(size_t g, size_t slots, size_t n_lights, size_t list_slots);
   hipError_t ensure_misc(size_t n_diag);
+  // shard counters: generation g's rays (q = 0) / shadow list (q = 1)
+  unsigned* shard_cnt(unsigned g, unsigned q) { return d_shard_ + ((size_t)g * 2 + q) * kShards * kShardStride; }
   std::vector<WfGenBuf> gens_;
   WfCounters* d_cnt_ = nullptr;
+  unsigned* d_shard_ = nullptr;  // kMaxGen x 2 x kShards counters, kShardStride apart
   PrimRec* d_prim_ = nullptr;
   size_t prim_cap_ = 0;
   hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
