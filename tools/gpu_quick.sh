@@ -3,7 +3,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "gpu tests rc=$rc"; tail -15 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "gpu tests rc=$rc"; tail -15 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 200 python bench.py --no-cpu-baseline $* > gpurun_out/bench.json 2> gpurun_out/bench.err; rc=$?; echo "bench rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/bench.err; exit $rc; }
 python -c "
 import json; d=json.load(open('gpurun_out/bench.json')); r=d['roofline']
