@@ -192,8 +192,8 @@ const char* rt_last_error(void) { return g_err.c_str(); }
 // of the wavefront pipeline. enable: 1 = on, 0 = off, -1 = just read. out[16]:
 // ms[5] (primary, closest, shadow, prep, combine), rays[3], disc[3],
 // n_diag, n_gen, n_planes, n_lights, n_quads, tests[3], boxes[3], bvh,
-// n_bvh_nodes, bvh_depth.
-int rtamd_wf_profile(const rt_scene* cs, int enable, double out[25]) {
+// n_bvh_nodes, bvh_depth, n_bvh4_nodes, bvh4_stack.
+int rtamd_wf_profile(const rt_scene* cs, int enable, double out[27]) {
   if (!cs) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
   rt_scene* s = const_cast<rt_scene*>(cs);
   std::lock_guard<std::mutex> lk(s->mu);
@@ -214,6 +214,8 @@ int rtamd_wf_profile(const rt_scene* cs, int enable, double out[25]) {
     out[22] = p.bvh;
     out[23] = s->dev.n_bvh;
     out[24] = s->dev.bvh_depth;
+    out[25] = s->dev.n_bvh4;
+    out[26] = s->dev.bvh4_stack;
   }
   return RT_OK;
 }
@@ -231,6 +233,10 @@ int rtamd_tuning_set(const char* key, int value) {
   if (key && std::strcmp(key, "lane") == 0) {
     rtamd::g_wf_lane = value;  // 0 = wave traversal, 1 = per-lane (LDS stack when it fits), 2 = per-lane, scratch
                                // stack, 5 = per-lane with the scene in LDS when it fits (default)
+    return RT_OK;
+  }
+  if (key && std::strcmp(key, "refill") == 0) {
+    rtamd::g_wf_refill = value;
     return RT_OK;
   }
   if (key && std::strcmp(key, "skip_shadow") == 0) {
@@ -383,6 +389,9 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   // come from `meta`, so the order changes no result)
   int bvh_depth = 0;
   std::vector<BvhNode> bvh = build_sphere_bvh(diag, g_bvh_leaf, &bvh_depth, g_bvh_ct / 100.0);
+  int bvh4_stack = 0;
+  bool bvh4_code16 = false;
+  std::vector<BvhNode4> bvh4 = collapse_bvh4(bvh, &bvh4_stack, &bvh4_code16);
   std::vector<LightRec> lrec(n_lights);
   for (size_t i = 0; i < n_lights; ++i)
     for (int c = 0; c < 3; ++c) { lrec[i].pos[c] = lights[i].position[c]; lrec[i].intensity[c] = lights[i].intensity[c]; }
@@ -395,7 +404,8 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   const size_t o_pl = align(o_gen + (gen.size() + 1) * sizeof(SphereGen));
   const size_t o_qd = align(o_pl + (planes.size() + 1) * sizeof(PlaneRec));
   const size_t o_bv = align(o_qd + (quads.size() + 1) * sizeof(QuadRec));
-  const size_t o_sh = align(o_bv + (bvh.size() + 1) * sizeof(BvhNode));
+  const size_t o_b4 = align(o_bv + (bvh.size() + 1) * sizeof(BvhNode));
+  const size_t o_sh = align(o_b4 + (bvh4.size() + 1) * sizeof(BvhNode4));
   const size_t o_li = align(o_sh + shade.size() * sizeof(ShadeRec));
   const size_t total = align(o_li + lrec.size() * sizeof(LightRec)) + 256;
   std::vector<unsigned char> host(total, 0);
@@ -404,6 +414,7 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   if (!planes.empty()) std::memcpy(&host[o_pl], planes.data(), planes.size() * sizeof(PlaneRec));
   if (!quads.empty()) std::memcpy(&host[o_qd], quads.data(), quads.size() * sizeof(QuadRec));
   if (!bvh.empty()) std::memcpy(&host[o_bv], bvh.data(), bvh.size() * sizeof(BvhNode));
+  if (!bvh4.empty()) std::memcpy(&host[o_b4], bvh4.data(), bvh4.size() * sizeof(BvhNode4));
   if (!shade.empty()) std::memcpy(&host[o_sh], shade.data(), shade.size() * sizeof(ShadeRec));
   if (!lrec.empty()) std::memcpy(&host[o_li], lrec.data(), lrec.size() * sizeof(LightRec));
 
@@ -430,6 +441,10 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   s->dev.bvh = bvh.empty() ? nullptr : (const BvhNode*)(b + o_bv);
   s->dev.n_bvh = (int32_t)bvh.size();
   s->dev.bvh_depth = bvh_depth;
+  s->dev.bvh4 = bvh4.empty() ? nullptr : (const BvhNode4*)(b + o_b4);
+  s->dev.n_bvh4 = (int32_t)bvh4.size();
+  s->dev.bvh4_stack = bvh4_stack;
+  s->dev.bvh4_code16 = bvh4_code16 ? 1 : 0;
   s->dev.shade = (const ShadeRec*)(b + o_sh);
   s->dev.lights = (const LightRec*)(b + o_li);
   s->dev.n_diag = (int32_t)diag.size();

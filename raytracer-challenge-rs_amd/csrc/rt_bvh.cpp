@@ -238,4 +238,95 @@ std::vector<BvhNode> build_sphere_bvh(std::vector<SphereDiag>& spheres, int leaf
   return bd.nodes;
 }
 
+namespace {
+struct Slot4 {
+  int32_t code;
+  float lo[3], hi[3];
+  double area() const {
+    const double dx = (double)hi[0] - lo[0], dy = (double)hi[1] - lo[1], dz = (double)hi[2] - lo[2];
+    return 2.0 * (dx * dy + dy * dz + dz * dx);
+  }
+};
+
+struct Collapser {
+  const std::vector<BvhNode>& bin;
+  std::vector<BvhNode4> out;
+  bool code16 = true;
+
+  static Slot4 child_slot(const BvhNode& n, int k) {
+    Slot4 s;
+    s.code = n.child[k];
+    for (int a = 0; a < 3; ++a) { s.lo[a] = n.lo[k][a]; s.hi[a] = n.hi[k][a]; }
+    return s;
+  }
+  // four-wide node for binary node `e`; returns its index and the pending-entry need below it
+  int32_t make(int32_t e, int* need) {
+    std::vector<Slot4> kids;
+    for (int k = 0; k < 2; ++k)
+      if (bin[e].child[k] != kBvhEmpty) kids.push_back(child_slot(bin[e], k));
+    while (kids.size() < 4) {
+      int best = -1;
+      double ba = -1.0;
+      for (int i = 0; i < (int)kids.size(); ++i)
+        if (kids[i].code >= 0 && kids[i].area() > ba) { ba = kids[i].area(); best = i; }
+      if (best < 0) break;
+      const BvhNode& n = bin[kids[best].code];
+      std::vector<Slot4> rep;
+      for (int k = 0; k < 2; ++k)
+        if (n.child[k] != kBvhEmpty) rep.push_back(child_slot(n, k));
+      if (kids.size() - 1 + rep.size() > 4) break;
+      kids.erase(kids.begin() + best);
+      kids.insert(kids.begin() + best, rep.begin(), rep.end());
+    }
+    const int32_t idx = (int32_t)out.size();
+    out.emplace_back();
+    int below = 0;
+    int32_t codes[4];
+    for (int i = 0; i < 4; ++i) {
+      codes[i] = kBvhEmpty;
+      if (i >= (int)kids.size()) continue;
+      codes[i] = kids[i].code;
+      if (kids[i].code >= 0) {
+        int nb = 0;
+        codes[i] = make(kids[i].code, &nb);
+        below = std::max(below, nb);
+      }
+    }
+    BvhNode4& nd = out[idx];
+    std::memset(&nd, 0, sizeof nd);
+    for (int i = 0; i < 4; ++i) {
+      nd.child[i] = codes[i];
+      nd.code[i] = (uint16_t)kBvh4Empty;
+      if (codes[i] >= 0) {
+        if (codes[i] < 0x8000) nd.code[i] = (uint16_t)codes[i];
+        else code16 = false;
+      } else if (codes[i] != kBvhEmpty) {
+        const int code = -(codes[i] + 1), first = code >> 7, cnt = code & 127;
+        if (cnt >= 1 && cnt <= 8 && first + cnt < 0xFFF) nd.code[i] = (uint16_t)(0x8000 | (cnt - 1) << 12 | first);
+        else code16 = false;
+      }
+      for (int a = 0; a < 3; ++a) {
+        nd.lo[a][i] = i < (int)kids.size() ? kids[i].lo[a] : 0.0f;
+        nd.hi[a][i] = i < (int)kids.size() ? kids[i].hi[a] : 0.0f;
+      }
+    }
+    *need = (int)kids.size() - 1 + below;
+    return idx;
+  }
+};
+}  // namespace
+
+std::vector<BvhNode4> collapse_bvh4(const std::vector<BvhNode>& bin, int* stack, bool* code16) {
+  if (stack) *stack = 0;
+  if (code16) *code16 = false;
+  if (bin.empty()) return {};
+  Collapser c{bin, {}};
+  c.out.reserve(bin.size());
+  int need = 0;
+  c.make(0, &need);
+  if (stack) *stack = need;
+  if (code16) *code16 = c.code16;
+  return c.out;
+}
+
 }  // namespace rtamd

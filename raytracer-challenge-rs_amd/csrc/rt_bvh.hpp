@@ -18,4 +18,13 @@ namespace rtamd {
 std::vector<BvhNode> build_sphere_bvh(std::vector<SphereDiag>& spheres, int leaf_size, int* depth = nullptr,
                                       double trav_cost = 1.0);
 
+// Collapses the binary hierarchy into four-wide nodes (root = 0): each node
+// repeatedly opens its largest-area internal child until it holds four
+// children. Boxes and leaf codes are copied unchanged, so the four-wide
+// traversal culls exactly what the binary one may cull. `stack` receives the
+// most entries a nearest-first traversal keeps pending (on a root-leaf path,
+// the sum of (children - 1) over its nodes). `code16` tells whether every
+// child fits BvhNode4::code.
+std::vector<BvhNode4> collapse_bvh4(const std::vector<BvhNode>& bin, int* stack = nullptr, bool* code16 = nullptr);
+
 }  // namespace rtamd

@@ -58,6 +58,22 @@ struct alignas(64) BvhNode {
   int32_t axis, pad;
 };
 static_assert(sizeof(BvhNode) == 64, "BvhNode must stay 64 B");
+// Four-wide node, collapsed from the binary hierarchy (rt_bvh.cpp): the four
+// children's boxes (the binary nodes' binary32 boxes, copied unchanged) laid
+// out per coordinate, so one lane reads what it needs in seven 16-B loads and
+// tests the four boxes with independent instruction streams. `code` is the
+// traversal's 16-bit child code: an internal node index (< 0x8000), a leaf
+// 0x8000 | (count - 1) << 12 | first (count <= 8, first + count < 0xFFF), or
+// kBvh4Empty; valid when DevScene::bvh4_code16 is set. `child` keeps the
+// binary hierarchy's 32-bit codes (internal index / leaf code / kBvhEmpty).
+struct alignas(128) BvhNode4 {
+  float lo[3][4], hi[3][4];  // lo[axis][child]
+  uint16_t code[4];
+  int32_t child[4];
+  int32_t pad[2];
+};
+constexpr int kBvh4Empty = 0xFFFF;
+static_assert(sizeof(BvhNode4) == 128, "BvhNode4 must stay 128 B");
 constexpr int32_t kBvhEmpty = (int32_t)0x80000000;
 constexpr int kBvhLeafMax = 127;
 constexpr int kBvhMaxDepth = 60;  // traversal stack entries per wave
@@ -100,6 +116,10 @@ struct DevScene {
   int32_t n_quads;
   int32_t n_bvh;
   int32_t bvh_depth;  // most far children pending on a traversal stack
+  const BvhNode4* bvh4;  // the same hierarchy, four-wide (nullptr when the scene has no BVH)
+  int32_t n_bvh4;
+  int32_t bvh4_stack;  // most children a nearest-first four-wide traversal keeps pending
+  int32_t bvh4_code16;  // 1 when every BvhNode4::code is valid (scenes of < 4088 diagonal spheres)
 };
 
 struct DevCamera {

@@ -32,6 +32,7 @@ int g_wf_lane = 7;  // secondary / shadow rays: 7 = per-lane with leaves batched
                     // + stack in LDS, 6 = nodes + stack in LDS, 1 = per-lane with an LDS (or scratch) stack,
                     // 0 = wave (packet) traversal
 int g_wf_skip_shadow = 1;  // fast path: leave out shadow rays that cannot change the colour
+int g_wf_refill = 0;       // 1 = lanes take a new ray as soon as theirs is done (DESIGN.md "Lane refill")
 // occupancy (waves per SIMD the register allocator targets) of the BVH trace kernels
 int g_tw_primary = 4, g_tw_closest = 4, g_tw_shadow = 4;
 constexpr int kWfBlock = 256;      // prep / shadow / combine
@@ -603,10 +604,40 @@ __device__ __forceinline__ void bvh_trace(const DevScene& sc, cPrimRec prim, int
 // `nodes` / `sd` point at the hierarchy and the sphere records in global
 // memory or at the block's LDS copy. `h` arrives initialised (it may already
 // hold the planes' nearest hit, which tightens the culling).
-template <bool SHADOW, bool LDS_STACK, bool WW = false>
+// SOA: the LDS image stores chunk k (16 B) of node / sphere record i at
+// chunk array k, element i (LANE == 9), so the lanes' random record reads
+// spread over all LDS banks instead of the few a 64-B record stride reaches.
+template <bool SOA>
+__device__ __forceinline__ void node_chunks(const BvhNode* nodes, int ns, int e, uint4& q0, uint4& q1, uint4& q2,
+                                            uint4& q3) {
+  const uint4* b = reinterpret_cast<const uint4*>(nodes);
+  if constexpr (SOA) {
+    q0 = b[e]; q1 = b[e + ns]; q2 = b[e + 2 * ns]; q3 = b[e + 3 * ns];
+  } else {
+    q0 = b[4 * e]; q1 = b[4 * e + 1]; q2 = b[4 * e + 2]; q3 = b[4 * e + 3];
+  }
+}
+template <bool SHADOW, bool SOA>
+__device__ __forceinline__ void leaf_sphere_test(const SphereDiag* sd, int nsph, int k, V3 o, V3 d, Hit& h,
+                                                 unsigned& n_disc) {
+  if constexpr (SOA) {
+    const double2* b = reinterpret_cast<const double2*>(sd);
+    const double2 c0 = b[k], c1 = b[k + nsph], c2 = b[k + 2 * nsph];
+    const double s0 = c0.x, s1 = c0.y, s2 = c1.x;
+    sphere_test<SHADOW>(s0 * o.x + c1.y, s1 * o.y + c2.x, s2 * o.z + c2.y, s0 * d.x, s1 * d.y, s2 * d.z,
+                        [&] { return reinterpret_cast<const int*>(b + 3 * nsph + k)[0]; }, h, n_disc);
+  } else {
+    const SphereDiag& r = sd[k];
+    const double s0 = r.s[0], s1 = r.s[1], s2 = r.s[2];
+    sphere_test<SHADOW>(s0 * o.x + r.t[0], s1 * o.y + r.t[1], s2 * o.z + r.t[2], s0 * d.x, s1 * d.y, s2 * d.z,
+                        [&] { return (int)r.meta; }, h, n_disc);
+  }
+}
+
+template <bool SHADOW, bool LDS_STACK, bool WW = false, bool SOA = false>
 __device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDiag* sd, const float* M, bool has_bvh,
                                            V3 o, V3 d, double t_shadow, Hit& h, unsigned& n_disc, unsigned& n_tests,
-                                           unsigned& n_boxes, int* lds) {
+                                           unsigned& n_boxes, int* lds, int ns = 0, int nsph = 0) {
   const SlabRay sr = slab_ray(o, d, M);
   float t_hi = f32_up(SHADOW ? t_shadow : h.t);
   int pstk[LDS_STACK ? 1 : kBvhMaxDepth + 4];
@@ -617,8 +648,8 @@ __device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDia
   // a node visit: both children's boxes, the one entered first visited first
   auto visit = [&]() {
     // the whole 64-B node in four 16-B loads: lo[0], lo[1], hi[0], hi[1], child[2], axis, pad
-    const uint4* np = reinterpret_cast<const uint4*>(nodes + e);
-    const uint4 q0 = np[0], q1 = np[1], q2 = np[2], q3 = np[3];
+    uint4 q0, q1, q2, q3;
+    node_chunks<SOA>(nodes, ns, e, q0, q1, q2, q3);
     const float lo0[3] = {__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z)};
     const float lo1[3] = {__uint_as_float(q0.w), __uint_as_float(q1.x), __uint_as_float(q1.y)};
     const float hi0[3] = {__uint_as_float(q1.z), __uint_as_float(q1.w), __uint_as_float(q2.x)};
@@ -640,12 +671,7 @@ __device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDia
   auto leaf = [&](int code_e) {
     const int code = -(code_e + 1);
     const int first = code >> 7, cnt = code & 127;
-    for (int k = first; k < first + cnt; ++k) {
-      const SphereDiag& r = sd[k];
-      const double s0 = r.s[0], s1 = r.s[1], s2 = r.s[2];
-      sphere_test<SHADOW>(s0 * o.x + r.t[0], s1 * o.y + r.t[1], s2 * o.z + r.t[2], s0 * d.x, s1 * d.y, s2 * d.z,
-                          [&] { return (int)r.meta; }, h, n_disc);
-    }
+    for (int k = first; k < first + cnt; ++k) leaf_sphere_test<SHADOW, SOA>(sd, nsph, k, o, d, h, n_disc);
     n_tests += (unsigned)cnt;
     if constexpr (SHADOW) {
       return h.key >= 0 && h.t < t_shadow;
@@ -699,6 +725,99 @@ __device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDia
 #endif
 }
 
+// Four-wide per-lane traversal (LANE == 8): the same culling rule over the
+// collapsed hierarchy (BvhNode4; its boxes are the binary nodes' boxes, so
+// the exactness argument carries over unchanged). A visit tests the four
+// child boxes as independent instruction streams, continues into the hit
+// child entered first and pushes the other hit children farthest first, so
+// a ray makes about half the dependent node loads of the binary walk. The
+// stack holds 16-bit child codes in LDS (entry k of lane t at
+// stk[k * kTraceBlock]); its top stays in a register, so a pop returns at
+// once and the LDS read of the next entry overlaps the next node's loads.
+// Leaves are batched across the wave (speculative while-while), as in
+// lane_trace<..., WW>.
+template <bool SHADOW>
+__device__ __forceinline__ void lane_trace4(const BvhNode4* nodes, const SphereDiag* sd, const float* M, bool has_bvh,
+                                            V3 o, V3 d, double t_shadow, Hit& h, unsigned& n_disc, unsigned& n_tests,
+                                            unsigned& n_boxes, unsigned short* stk) {
+  const SlabRay sr = slab_ray(o, d, M);
+  float t_hi = f32_up(SHADOW ? t_shadow : h.t);
+  constexpr int E = kBvh4Empty;
+  int sp = 0, top = E;
+  auto push = [&](int v) {
+    if (top != E) stk[(sp++) * kTraceBlock] = (unsigned short)top;
+    top = v;
+  };
+  auto pop = [&]() {
+    const int r = top;
+    top = sp > 0 ? (int)stk[(--sp) * kTraceBlock] : E;
+    return r;
+  };
+  int e = (SHADOW && h.key >= 0 && h.t < t_shadow) || !has_bvh ? E : 0;
+  auto visit = [&]() {
+    const uint4* np = reinterpret_cast<const uint4*>(nodes + e);
+    uint4 q[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) q[k] = np[k];
+    const float* f = reinterpret_cast<const float*>(q);  // lo[3][4] at 0, hi[3][4] at 12
+    const unsigned cw[2] = {q[6].x, q[6].y};
+    float dist[4];
+    int code[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      code[k] = (int)((cw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
+      const float lo[3] = {f[k], f[4 + k], f[8 + k]};
+      const float hi[3] = {f[12 + k], f[16 + k], f[20 + k]};
+      float tk;
+      const bool hk = slab_hit32(lo, hi, sr, t_hi, tk) & (code[k] != E);
+      dist[k] = hk ? tk : INFINITY;
+    }
+    n_boxes += 4;
+    // sort the four (distance, code) pairs ascending; misses (inf) sink to the end
+    auto cas = [&](int i, int j) {
+      const bool sw = dist[j] < dist[i];
+      const float di = dist[i], dj = dist[j];
+      const int ci = code[i], cj = code[j];
+      dist[i] = sw ? dj : di; dist[j] = sw ? di : dj;
+      code[i] = sw ? cj : ci; code[j] = sw ? ci : cj;
+    };
+    cas(0, 1); cas(2, 3); cas(0, 2); cas(1, 3); cas(1, 2);
+    if (dist[3] != INFINITY) push(code[3]);
+    if (dist[2] != INFINITY) push(code[2]);
+    if (dist[1] != INFINITY) push(code[1]);
+    e = dist[0] != INFINITY ? code[0] : pop();
+  };
+  auto leaf = [&](int c) {
+    const int first = c & 0xFFF, cnt = ((c >> 12) & 7) + 1;
+    for (int k = first; k < first + cnt; ++k) {
+      const SphereDiag& r = sd[k];
+      const double s0 = r.s[0], s1 = r.s[1], s2 = r.s[2];
+      sphere_test<SHADOW>(s0 * o.x + r.t[0], s1 * o.y + r.t[1], s2 * o.z + r.t[2], s0 * d.x, s1 * d.y, s2 * d.z,
+                          [&] { return (int)r.meta; }, h, n_disc);
+    }
+    n_tests += (unsigned)cnt;
+    if constexpr (SHADOW) {
+      return h.key >= 0 && h.t < t_shadow;
+    } else {
+      t_hi = f32_up(h.t);
+      return false;
+    }
+  };
+  int pl = E;
+  for (;;) {
+    for (;;) {
+      if (e != E && e >= 0x8000 && pl == E) { pl = e; e = pop(); }
+      if (!__any(e < 0x8000 && pl == E)) break;
+      if (e < 0x8000) visit();  // lanes holding a leaf keep going (speculative)
+    }
+    if (!__any(pl != E)) break;
+    if (pl != E) {
+      if (leaf(pl)) { e = E; sp = 0; top = E; }  // shadowed: done
+      pl = E;
+    }
+  }
+}
+
 // LANE == 5: the block stages the hierarchy and the sphere records in LDS
 // (dynamic shared memory: [stack bvh_depth x kTraceBlock ints][nodes][spheres];
 // a lane pushes at most one entry per tree level).
@@ -707,26 +826,63 @@ __host__ __device__ inline size_t lane_lds_bytes(const DevScene& sc, bool sphere
   return lane_stack_bytes(sc.bvh_depth) + (size_t)sc.n_bvh * sizeof(BvhNode) +
          (spheres ? (size_t)sc.n_diag * sizeof(SphereDiag) : 0);
 }
+// LANE == 8: [16-bit stack bvh4_stack x kTraceBlock][four-wide nodes][spheres]
+__host__ __device__ inline size_t lane4_stack_bytes(const DevScene& sc) {
+  return ((size_t)(sc.bvh4_stack > 0 ? sc.bvh4_stack : 1) * kTraceBlock * 2 + 127) & ~(size_t)127;
+}
+__host__ __device__ inline size_t lane4_lds_bytes(const DevScene& sc) {
+  return lane4_stack_bytes(sc) + (size_t)sc.n_bvh4 * sizeof(BvhNode4) + (size_t)sc.n_diag * sizeof(SphereDiag);
+}
 struct LaneScene {
   const BvhNode* nodes;
   const SphereDiag* sd;
   int* stack;
   float M[3];  // bound on |box coordinate| per axis (slab_ray)
+  const BvhNode4* nodes4;
+  unsigned short* stack16;
 };
 template <int LANE>
 __device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, int* static_stack, unsigned char* dyn) {
   LaneScene ls{sc.bvh, sc.sph_diag, static_stack};
+  if constexpr (LANE == 8) {
+    unsigned short* stack = (unsigned short*)dyn;
+    BvhNode4* nodes = (BvhNode4*)(dyn + lane4_stack_bytes(sc));
+    SphereDiag* sdl = (SphereDiag*)((unsigned char*)nodes + (size_t)sc.n_bvh4 * sizeof(BvhNode4));
+    const uint4* gn = (const uint4*)sc.bvh4;
+    uint4* ln = (uint4*)nodes;
+    for (int i = threadIdx.x; i < sc.n_bvh4 * (int)(sizeof(BvhNode4) / 16); i += blockDim.x) ln[i] = gn[i];
+    const uint4* gs = (const uint4*)sc.sph_diag;
+    uint4* ls4 = (uint4*)sdl;
+    for (int i = threadIdx.x; i < sc.n_diag * (int)(sizeof(SphereDiag) / 16); i += blockDim.x) ls4[i] = gs[i];
+    __syncthreads();
+    ls.nodes4 = nodes;
+    ls.sd = sdl;
+    ls.stack16 = stack + threadIdx.x;
+    for (int a = 0; a < 3; ++a) {
+      float m = 0.0f;
+      if (sc.n_bvh4 > 0) {  // the root's child boxes contain every box below them
+        const BvhNode4& r = nodes[0];
+        for (int k = 0; k < 4; ++k)
+          if (r.code[k] != kBvh4Empty) m = fmaxf(m, fmaxf(fabsf(r.lo[a][k]), fabsf(r.hi[a][k])));
+      }
+      ls.M[a] = m;
+    }
+    return ls;
+  }
   if constexpr (LANE >= 5) {  // 6: the sphere records stay in global memory
     int* stack = (int*)dyn;
     BvhNode* nodes = (BvhNode*)(dyn + lane_stack_bytes(sc.bvh_depth));
     const uint4* gn = (const uint4*)sc.bvh;
     uint4* ln = (uint4*)nodes;
-    for (int i = threadIdx.x; i < sc.n_bvh * (int)(sizeof(BvhNode) / 16); i += blockDim.x) ln[i] = gn[i];
+    // LANE 9: chunk k of record i at k * n + i (node_chunks<true>)
+    for (int i = threadIdx.x; i < sc.n_bvh * (int)(sizeof(BvhNode) / 16); i += blockDim.x)
+      ln[LANE == 9 ? (i & 3) * sc.n_bvh + (i >> 2) : i] = gn[i];
     if constexpr (LANE != 6) {
       SphereDiag* sd = (SphereDiag*)((unsigned char*)nodes + (size_t)sc.n_bvh * sizeof(BvhNode));
       const uint4* gs = (const uint4*)sc.sph_diag;
       uint4* ls4 = (uint4*)sd;
-      for (int i = threadIdx.x; i < sc.n_diag * (int)(sizeof(SphereDiag) / 16); i += blockDim.x) ls4[i] = gs[i];
+      for (int i = threadIdx.x; i < sc.n_diag * (int)(sizeof(SphereDiag) / 16); i += blockDim.x)
+        ls4[LANE == 9 ? (i & 3) * sc.n_diag + (i >> 2) : i] = gs[i];
       ls.sd = sd;
     }
     __syncthreads();
@@ -736,7 +892,10 @@ __device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, int* static_
   for (int a = 0; a < 3; ++a) {
     float m = 0.0f;
     if (sc.n_bvh > 0) {  // the root's two child boxes contain every box below them
-      const BvhNode& r = ls.nodes[0];
+      uint4 q[4];
+      node_chunks<LANE == 9>(ls.nodes, sc.n_bvh, 0, q[0], q[1], q[2], q[3]);
+      BvhNode r;
+      memcpy(&r, q, sizeof r);
       m = fmaxf(fmaxf(fabsf(r.lo[0][a]), fabsf(r.hi[0][a])), fmaxf(fabsf(r.lo[1][a]), fabsf(r.hi[1][a])));
     }
     ls.M[a] = m;
@@ -766,10 +925,13 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest_bvh(DevScene
     hit_init(h);
     if (valid) {
       wf_ray(a, cam, slot, o, d);
-      if constexpr (LANE && !PRIMARY) {
+      if constexpr (LANE == 8 && !PRIMARY) {
         trace_rest<false, QUADS>(sc, o, d, h, n_disc);  // planes first: an early nearest hit tightens the culling
-        lane_trace<false, LDS_STACK, LANE == 7 || LANE == 3>(ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h,
-                                                             n_disc, n_tests, n_boxes, ls.stack);
+        lane_trace4<false>(ls.nodes4, ls.sd, ls.M, sc.n_bvh4 > 0, o, d, 0.0, h, n_disc, n_tests, n_boxes, ls.stack16);
+      } else if constexpr (LANE && !PRIMARY) {
+        trace_rest<false, QUADS>(sc, o, d, h, n_disc);  // planes first: an early nearest hit tightens the culling
+        lane_trace<false, LDS_STACK, LANE == 7 || LANE == 3 || LANE == 9, LANE == 9>(
+            ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, n_disc, n_tests, n_boxes, ls.stack, sc.n_bvh, sc.n_diag);
       } else {
         bvh_trace<PRIMARY, false>(sc, (cPrimRec)a.prim, stk, o, d, 0.0, h, n_disc, n_tests, n_boxes);
         trace_rest<false, QUADS>(sc, o, d, h, n_disc);
@@ -803,16 +965,127 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow_bvh(DevScene 
     unsigned slot;
     shadow_ray(sc, a, shard_slot(pre, a.sh_cap, i), o, d, dist, slot);
     Hit h;
-    if constexpr (LANE) {
+    if constexpr (LANE == 8) {
       hit_init(h);
       trace_rest<true, QUADS>(sc, o, d, h, n_disc);  // planes first: any hit before the light ends the ray
-      lane_trace<true, LDS_STACK, LANE == 7 || LANE == 3>(ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, dist, h, n_disc, n_tests, n_boxes, ls.stack);
+      lane_trace4<true>(ls.nodes4, ls.sd, ls.M, sc.n_bvh4 > 0, o, d, dist, h, n_disc, n_tests, n_boxes, ls.stack16);
+    } else if constexpr (LANE) {
+      hit_init(h);
+      trace_rest<true, QUADS>(sc, o, d, h, n_disc);  // planes first: any hit before the light ends the ray
+      lane_trace<true, LDS_STACK, LANE == 7 || LANE == 3 || LANE == 9, LANE == 9>(
+          ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, dist, h, n_disc, n_tests, n_boxes, ls.stack, sc.n_bvh, sc.n_diag);
     } else {
       bvh_trace<false, true>(sc, nullptr, stk, o, d, dist, h, n_disc, n_tests, n_boxes);
       if (__any(!(h.key >= 0 && h.t < dist))) trace_rest<true, QUADS>(sc, o, d, h, n_disc);
     }
     hit_finish(h);
     a.sflags[slot] = (h.key >= 0 && h.t < dist) ? 1 : 0;
+  }
+  const unsigned long long sd = wave_sum(n_disc), st = wave_sum(n_tests), sb = wave_sum(n_boxes);
+  if (lane_id() == 0) {
+    if (sd) atomicAdd(&a.cnt->disc[a.disc_slot], sd);
+    if (st) atomicAdd(&a.cnt->tests[a.disc_slot], st);
+    if (sb) atomicAdd(&a.cnt->boxes[a.disc_slot], sb);
+  }
+}
+
+// Shadow rays with lane refill (DESIGN.md "Lane refill"): the per-lane
+// traversal of lane_trace<true, true, true> (binary nodes, sphere records and
+// stack in LDS, leaves batched across the wave), but a lane whose ray is
+// finished takes the next ray of its wave's range at once instead of idling
+// until the wave's longest ray is done. Each wave owns a contiguous range of
+// the shadow list (neighbouring rays stay together); a refill happens after a
+// leaf round once at least kRefillMin lanes are idle (or none is busy).
+// Results are per ray and independent of when a ray runs, so the flags are
+// those of lane_trace.
+constexpr int kRefillMin = 16;
+template <bool QUADS, int LANE, int TW>
+__global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow_refill(DevScene sc, WfArgs a) {
+  constexpr bool SOA = LANE == 9;
+  __shared__ int stack_lds[1];
+  extern __shared__ __attribute__((aligned(16))) unsigned char lane_dyn[];
+  const LaneScene ls = lane_scene<LANE>(sc, stack_lds, lane_dyn);
+  __shared__ unsigned s_pre[kShards + 1];
+  const unsigned* pre = shard_prefix(a.sh_cnt, s_pre);
+  unsigned n_disc = 0, n_tests = 0, n_boxes = 0;
+  const unsigned waves = gridDim.x * (blockDim.x / 64);
+  const unsigned wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+  const unsigned per = (a.n_shadow + waves - 1) / waves;
+  unsigned next = min(wave * per, a.n_shadow);
+  const unsigned end = min(next + per, a.n_shadow);
+  const unsigned lane = lane_id();
+  const unsigned long long below = (1ull << lane) - 1ull;
+  int* const stk = ls.stack;
+  const bool has_bvh = sc.n_bvh > 0;
+  // lane state
+  bool active = false;
+  V3 o = v3(0, 0, 0), d = v3(0, 0, 0);
+  double dist = 0.0;
+  unsigned slot = 0;
+  Hit h;
+  hit_init(h);
+  SlabRay sr{};
+  float t_hi = 0.0f;
+  int e = kBvhEmpty, pl = kBvhEmpty, sp = 0;
+  auto pop = [&]() { return sp > 0 ? stk[(--sp) * kTraceBlock] : kBvhEmpty; };
+  for (;;) {
+    // refill idle lanes from the wave's range
+    const unsigned long long idle = __ballot(!active);
+    const unsigned n_idle = (unsigned)__popcll(idle);
+    if (next < end && (n_idle >= kRefillMin || n_idle == 64u)) {
+      const unsigned j = next + (unsigned)__popcll(idle & below);
+      next = min(next + n_idle, end);
+      if (!active && j < end) {
+        shadow_ray(sc, a, shard_slot(pre, a.sh_cap, j), o, d, dist, slot);
+        hit_init(h);
+        trace_rest<true, QUADS>(sc, o, d, h, n_disc);  // planes first: any hit before the light ends the ray
+        sr = slab_ray(o, d, ls.M);
+        t_hi = f32_up(dist);
+        sp = 0;
+        pl = kBvhEmpty;
+        e = (h.key >= 0 && h.t < dist) || !has_bvh ? kBvhEmpty : 0;
+        active = true;
+      }
+    }
+    if (!__any(active)) break;
+    // node phase: lanes meeting a leaf postpone it and keep visiting nodes
+    for (;;) {
+      if (e < 0 && e != kBvhEmpty && pl == kBvhEmpty) { pl = e; e = pop(); }
+      if (!__any(e >= 0 && pl == kBvhEmpty)) break;
+      if (e >= 0) {
+        uint4 q0, q1, q2, q3;
+        node_chunks<SOA>(ls.nodes, sc.n_bvh, e, q0, q1, q2, q3);
+        const float lo0[3] = {__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z)};
+        const float lo1[3] = {__uint_as_float(q0.w), __uint_as_float(q1.x), __uint_as_float(q1.y)};
+        const float hi0[3] = {__uint_as_float(q1.z), __uint_as_float(q1.w), __uint_as_float(q2.x)};
+        const float hi1[3] = {__uint_as_float(q2.y), __uint_as_float(q2.z), __uint_as_float(q2.w)};
+        const int c0 = (int)q3.x, c1 = (int)q3.y;
+        float t0, t1;
+        const bool h0 = slab_hit32(lo0, hi0, sr, t_hi, t0);
+        const bool h1 = slab_hit32(lo1, hi1, sr, t_hi, t1) & (c1 != kBvhEmpty);
+        n_boxes += 2;
+        if (h0 && h1) {
+          const bool flip = t1 < t0;
+          stk[(sp++) * kTraceBlock] = flip ? c0 : c1;
+          e = flip ? c1 : c0;
+        } else {
+          e = h0 ? c0 : h1 ? c1 : pop();
+        }
+      }
+    }
+    // leaf round
+    if (pl != kBvhEmpty) {
+      const int code = -(pl + 1);
+      const int first = code >> 7, cnt = code & 127;
+      for (int k = first; k < first + cnt; ++k) leaf_sphere_test<true, SOA>(ls.sd, sc.n_diag, k, o, d, h, n_disc);
+      n_tests += (unsigned)cnt;
+      if (h.key >= 0 && h.t < dist) { e = kBvhEmpty; sp = 0; }  // shadowed: done
+      pl = kBvhEmpty;
+    }
+    if (active && e == kBvhEmpty && pl == kBvhEmpty) {
+      a.sflags[slot] = (h.key >= 0 && h.t < dist) ? 1 : 0;
+      active = false;
+    }
   }
   const unsigned long long sd = wave_sum(n_disc), st = wave_sum(n_tests), sb = wave_sum(n_boxes);
   if (lane_id() == 0) {
@@ -1064,6 +1337,10 @@ static int occupancy_grid(K kern, int block, size_t lds, unsigned n) {
 }
 
 static constexpr size_t kWfLdsLimit = 160 * 1024 - 1024;
+// the four-wide traversal runs when its 16-bit codes are valid and the block's LDS image fits
+static bool lane4_ok(const DevScene& sc) {
+  return sc.n_bvh4 > 0 && sc.bvh4_code16 && lane4_lds_bytes(sc) <= kWfLdsLimit;
+}
 
 // Per-launch profiling: see t_ev_start.
 #define WF_LAUNCH(kern, grid, block, lds, stream, ...)                                                  \
@@ -1083,14 +1360,20 @@ static hipError_t launch_closest_q(const DevScene& sc, const DevCamera& cam, con
     if (primary) {
       auto k = wf_trace_closest_bvh<true, QUADS, 0, TW>;
       WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
+    } else if (g_wf_lane == 8 && lane4_ok(sc)) {
+      const size_t lds = lane4_lds_bytes(sc);
+      auto k = wf_trace_closest_bvh<false, QUADS, 8, TW>;
+      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, n)), dim3(kTraceBlock), lds, stream, sc, cam, a);
     } else if (g_wf_lane == 6 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc, false) <= kWfLdsLimit) {
       const size_t lds = lane_lds_bytes(sc, false);
       auto k = wf_trace_closest_bvh<false, QUADS, 6, TW>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, n)), dim3(kTraceBlock), lds, stream, sc, cam, a);
-    } else if (g_wf_lane == 7 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc) <= kWfLdsLimit) {
+    } else if ((g_wf_lane == 7 || g_wf_lane == 9) && sc.bvh_depth <= kLaneLdsDepth &&
+               lane_lds_bytes(sc) <= kWfLdsLimit) {
       const size_t lds = lane_lds_bytes(sc);
-      auto k = wf_trace_closest_bvh<false, QUADS, 7, TW>;
+      auto k = g_wf_lane == 9 ? wf_trace_closest_bvh<false, QUADS, 9, TW> : wf_trace_closest_bvh<false, QUADS, 7, TW>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, n)), dim3(kTraceBlock), lds, stream, sc, cam, a);
     } else if (g_wf_lane >= 5 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc) <= kWfLdsLimit) {
@@ -1098,7 +1381,7 @@ static hipError_t launch_closest_q(const DevScene& sc, const DevCamera& cam, con
       auto k = wf_trace_closest_bvh<false, QUADS, 5, TW>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, n)), dim3(kTraceBlock), lds, stream, sc, cam, a);
-    } else if (g_wf_lane == 7 && sc.bvh_depth <= kLaneLdsDepth) {
+    } else if ((g_wf_lane == 7 || g_wf_lane == 9) && sc.bvh_depth <= kLaneLdsDepth) {
       auto k = wf_trace_closest_bvh<false, QUADS, 3, TW>;
       WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
     } else if (g_wf_lane && g_wf_lane != 2 && sc.bvh_depth <= kLaneLdsDepth) {
@@ -1137,14 +1420,26 @@ static hipError_t launch_closest(const DevScene& sc, const DevCamera& cam, const
 template <bool QUADS, int TW>
 static hipError_t launch_shadow_q(const DevScene& sc, const WfArgs& a, bool lds_ok, bool bvh, hipStream_t stream) {
   if (bvh) {
-    if (g_wf_lane == 6 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc, false) <= kWfLdsLimit) {
+    if (g_wf_refill && (g_wf_lane == 7 || g_wf_lane == 9) && sc.bvh_depth <= kLaneLdsDepth &&
+        lane_lds_bytes(sc) <= kWfLdsLimit) {
+      const size_t lds = lane_lds_bytes(sc);
+      auto k = g_wf_lane == 9 ? wf_trace_shadow_refill<QUADS, 9, TW> : wf_trace_shadow_refill<QUADS, 7, TW>;
+      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, a.n_shadow)), dim3(kTraceBlock), lds, stream, sc, a);
+    } else if (g_wf_lane == 8 && lane4_ok(sc)) {
+      const size_t lds = lane4_lds_bytes(sc);
+      auto k = wf_trace_shadow_bvh<QUADS, 8, TW>;
+      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, a.n_shadow)), dim3(kTraceBlock), lds, stream, sc, a);
+    } else if (g_wf_lane == 6 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc, false) <= kWfLdsLimit) {
       const size_t lds = lane_lds_bytes(sc, false);
       auto k = wf_trace_shadow_bvh<QUADS, 6, TW>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, a.n_shadow)), dim3(kTraceBlock), lds, stream, sc, a);
-    } else if (g_wf_lane == 7 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc) <= kWfLdsLimit) {
+    } else if ((g_wf_lane == 7 || g_wf_lane == 9) && sc.bvh_depth <= kLaneLdsDepth &&
+               lane_lds_bytes(sc) <= kWfLdsLimit) {
       const size_t lds = lane_lds_bytes(sc);
-      auto k = wf_trace_shadow_bvh<QUADS, 7, TW>;
+      auto k = g_wf_lane == 9 ? wf_trace_shadow_bvh<QUADS, 9, TW> : wf_trace_shadow_bvh<QUADS, 7, TW>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, a.n_shadow)), dim3(kTraceBlock), lds, stream, sc, a);
     } else if (g_wf_lane >= 5 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc) <= kWfLdsLimit) {
@@ -1152,7 +1447,7 @@ static hipError_t launch_shadow_q(const DevScene& sc, const WfArgs& a, bool lds_
       auto k = wf_trace_shadow_bvh<QUADS, 5, TW>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, a.n_shadow)), dim3(kTraceBlock), lds, stream, sc, a);
-    } else if (g_wf_lane == 7 && sc.bvh_depth <= kLaneLdsDepth) {
+    } else if ((g_wf_lane == 7 || g_wf_lane == 9) && sc.bvh_depth <= kLaneLdsDepth) {
       auto k = wf_trace_shadow_bvh<QUADS, 3, TW>;
       WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, a.n_shadow)), dim3(kTraceBlock), 0, stream, sc, a);
     } else if (g_wf_lane && g_wf_lane != 2 && sc.bvh_depth <= kLaneLdsDepth) {

@@ -64,6 +64,7 @@ extern int g_wf_trace_waves;  // tuning knob: trace-kernel occupancy (4 or 8 wav
 extern int g_tw_primary, g_tw_closest, g_tw_shadow;  // tuning knobs: BVH trace-kernel occupancy
 extern int g_wf_lane;         // tuning knob: 1 = per-lane BVH traversal for secondary / shadow rays
 extern int g_wf_accel;        // tuning knob: 1 = BVH traversal (when no counters are requested), 0 = exhaustive
+extern int g_wf_refill;       // tuning knob: 1 = lane refill in the per-lane trace kernels
 extern int g_wf_skip_shadow;  // tuning knob: 1 = the fast path leaves out shadow rays that cannot change the colour
 
 struct WfCounters {

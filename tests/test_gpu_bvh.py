@@ -213,7 +213,7 @@ def test_skipped_shadow_rays_bitwise(rt, neg_zero):
     assert full.to_numpy().tobytes() == exact.to_numpy().tobytes()
 
 
-@pytest.mark.parametrize("lane", [0, 1, 2, 5, 6, 7])
+@pytest.mark.parametrize("lane", [0, 1, 2, 5, 6, 7, 8, 9])
 def test_traversal_variants_bitwise(rt, lane):
     """Every traversal variant (wave / per-lane with LDS or scratch stack /
     per-lane with the scene or the nodes staged in LDS / per-lane with leaves
@@ -227,4 +227,19 @@ def test_traversal_variants_bitwise(rt, lane):
         fast, _ = cam.render(w, depth, want_stats=False)
     finally:
         rt._rtamd._tuning_set("lane", 7)
+    assert fast.to_numpy().tobytes() == exact.to_numpy().tobytes()
+
+
+@pytest.mark.parametrize("inside", [False, True])
+def test_lane_refill_bitwise(rt, inside):
+    """Lane refill (a lane takes its wave's next ray as soon as its own is
+    done) changes only when a ray is traced, never its result: the frame
+    equals the exhaustive frame, also with the camera inside nested glass."""
+    w, cam, depth = _glass_cluster(rt, n=250, seed=23, inside=inside)
+    exact, _ = cam.render(w, depth, want_stats=True)
+    rt._rtamd._tuning_set("refill", 1)
+    try:
+        fast, _ = cam.render(w, depth, want_stats=False)
+    finally:
+        rt._rtamd._tuning_set("refill", 0)
     assert fast.to_numpy().tobytes() == exact.to_numpy().tobytes()

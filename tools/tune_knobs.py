@@ -1,6 +1,7 @@
 """A/B runtime tuning knobs on the C3 frame in one process, interleaved
 rounds; every variant must reproduce the first variant's image (dev tool).
-Usage: tune_knobs.py lane=0,1 wf_waves=8,4 [--scene c3|c5]"""
+Usage: tune_knobs.py lane=0,1 wf_waves=8,4 [--c5] [--no-check]
+(--no-check: timing experiments whose images differ, e.g. exp=0,1)"""
 import itertools, os, sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "raytracer-challenge-rs_amd")]
@@ -44,7 +45,7 @@ for r in range(4):
                                           f"nodes {p['n_bvh_nodes']} depth {p['bvh_depth']} lane-LDS {lds:.0f}KB"))
         chk = buf.cpu().numpy().tobytes()
         ref = ref or chk
-        assert chk == ref, combo
+        assert chk == ref or "--no-check" in sys.argv, combo
 for combo, v in res.items():
     tot, ms, tests, boxes, info = min(v, key=lambda x: x[0])
     name = " ".join(f"{k}={c}" for (k, _), c in zip(knobs, combo))
