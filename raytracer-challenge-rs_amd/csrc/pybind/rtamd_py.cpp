@@ -38,7 +38,7 @@ static py::array_t<double> check_rays(py::array_t<double, py::array::c_style | p
 }
 
 extern "C" int rtamd_tuning_set(const char* key, int value);
-extern "C" int rtamd_wf_profile(const rt_scene* s, int enable, double out[27]);
+extern "C" int rtamd_wf_profile(const rt_scene* s, int enable, double out[29]);
 
 PYBIND11_MODULE(_rtamd, m) {
   m.doc() = "MI355X-native render path of raytracer-challenge-rs (host API over the C-ABI)";
@@ -379,7 +379,7 @@ PYBIND11_MODULE(_rtamd, m) {
       }, py::arg("max_depth") = 5)
       .def("render_to", &SceneParser::render_to, py::arg("path"), py::arg("max_depth") = 5);
   m.def("_wf_profile", [](const World& w, int enable, bool read) {
-    double o[27] = {0};
+    double o[29] = {0};
     check(rtamd_wf_profile(w.scene(), enable, read ? o : nullptr), "wf_profile");
     py::dict d;
     if (read) {
@@ -394,6 +394,7 @@ PYBIND11_MODULE(_rtamd, m) {
       for (int i = 0; i < 3; ++i) { tests[cls[i]] = o[16 + i]; boxes[cls[i]] = o[19 + i]; }
       d["tests"] = tests; d["boxes"] = boxes; d["bvh"] = (bool)o[22]; d["n_bvh_nodes"] = o[23]; d["bvh_depth"] = o[24];
       d["n_bvh4_nodes"] = o[25]; d["bvh4_stack"] = o[26];
+      d["lb_res"] = o[27]; d["lb_items"] = o[28];
     }
     return d;
   }, py::arg("world"), py::arg("enable") = -1, py::arg("read") = true);

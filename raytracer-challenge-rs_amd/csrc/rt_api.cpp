@@ -31,6 +31,7 @@ namespace {
 thread_local std::string g_err;
 int g_bvh_leaf = 2;     // BVH leaf size at scene creation (tuning knob "bvh_leaf")
 int g_bvh_ct = 70;      // SAH node-visit cost in percent of a sphere test (tuning knob "bvh_ct")
+int g_lb_res = 128;     // light-buffer cells per cube-map face edge at scene creation, 0 = none ("lb_res")
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -192,8 +193,8 @@ const char* rt_last_error(void) { return g_err.c_str(); }
 // of the wavefront pipeline. enable: 1 = on, 0 = off, -1 = just read. out[16]:
 // ms[5] (primary, closest, shadow, prep, combine), rays[3], disc[3],
 // n_diag, n_gen, n_planes, n_lights, n_quads, tests[3], boxes[3], bvh,
-// n_bvh_nodes, bvh_depth, n_bvh4_nodes, bvh4_stack.
-int rtamd_wf_profile(const rt_scene* cs, int enable, double out[27]) {
+// n_bvh_nodes, bvh_depth, n_bvh4_nodes, bvh4_stack, lb_res, lb_items.
+int rtamd_wf_profile(const rt_scene* cs, int enable, double out[29]) {
   if (!cs) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
   rt_scene* s = const_cast<rt_scene*>(cs);
   std::lock_guard<std::mutex> lk(s->mu);
@@ -216,6 +217,8 @@ int rtamd_wf_profile(const rt_scene* cs, int enable, double out[27]) {
     out[24] = s->dev.bvh_depth;
     out[25] = s->dev.n_bvh4;
     out[26] = s->dev.bvh4_stack;
+    out[27] = s->dev.lb_cells ? s->dev.lb_res : 0;
+    out[28] = s->dev.lb_cells ? s->dev.lb_n_items : 0;
   }
   return RT_OK;
 }
@@ -233,6 +236,15 @@ int rtamd_tuning_set(const char* key, int value) {
   if (key && std::strcmp(key, "lane") == 0) {
     rtamd::g_wf_lane = value;  // 0 = wave traversal, 1 = per-lane (LDS stack when it fits), 2 = per-lane, scratch
                                // stack, 5 = per-lane with the scene in LDS when it fits (default)
+    return RT_OK;
+  }
+  if (key && std::strcmp(key, "lb_res") == 0) {
+    if (value < 0 || value > 512) return fail(RT_ERR_INVALID_ARGUMENT, "lb_res must be in [0, 512]");
+    g_lb_res = value;
+    return RT_OK;
+  }
+  if (key && std::strcmp(key, "shadow_lb") == 0) {
+    rtamd::g_wf_shadow_lb = value != 0;
     return RT_OK;
   }
   if (key && std::strcmp(key, "refill") == 0) {
@@ -395,6 +407,10 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   std::vector<LightRec> lrec(n_lights);
   for (size_t i = 0; i < n_lights; ++i)
     for (int c = 0; c < 3; ++c) { lrec[i].pos[c] = lights[i].position[c]; lrec[i].intensity[c] = lights[i].intensity[c]; }
+  // light buffers over the (reordered) diagonal spheres: the shadow rays' cell lists
+  LightBuffer lb;
+  if (!diag.empty() && n_lights > 0 && n_lights <= (size_t)kLbMaxLights && g_lb_res > 0)
+    lb = build_light_buffer(diag, lrec, g_lb_res);
 
   // ---- one blob, 64-B aligned sections
   auto align = [](size_t x) { return (x + 255) & ~(size_t)255; };
@@ -407,7 +423,11 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   const size_t o_b4 = align(o_bv + (bvh.size() + 1) * sizeof(BvhNode));
   const size_t o_sh = align(o_b4 + (bvh4.size() + 1) * sizeof(BvhNode4));
   const size_t o_li = align(o_sh + shade.size() * sizeof(ShadeRec));
-  const size_t total = align(o_li + lrec.size() * sizeof(LightRec)) + 256;
+  const size_t o_lc = align(o_li + lrec.size() * sizeof(LightRec));
+  const size_t o_lv = align(o_lc + lb.cells.size() * sizeof(LbCell));
+  const size_t o_ld = align(o_lv + (lb.ov.size() + 1) * sizeof(uint16_t));
+  const size_t o_ll = align(o_ld + lb.delta.size() * sizeof(float));
+  const size_t total = align(o_ll + lb.limit.size() * sizeof(float)) + 256;
   std::vector<unsigned char> host(total, 0);
   if (!diag.empty()) std::memcpy(&host[o_diag], diag.data(), diag.size() * sizeof(SphereDiag));
   if (!gen.empty()) std::memcpy(&host[o_gen], gen.data(), gen.size() * sizeof(SphereGen));
@@ -417,6 +437,12 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   if (!bvh4.empty()) std::memcpy(&host[o_b4], bvh4.data(), bvh4.size() * sizeof(BvhNode4));
   if (!shade.empty()) std::memcpy(&host[o_sh], shade.data(), shade.size() * sizeof(ShadeRec));
   if (!lrec.empty()) std::memcpy(&host[o_li], lrec.data(), lrec.size() * sizeof(LightRec));
+  if (!lb.cells.empty()) {
+    std::memcpy(&host[o_lc], lb.cells.data(), lb.cells.size() * sizeof(LbCell));
+    if (!lb.ov.empty()) std::memcpy(&host[o_lv], lb.ov.data(), lb.ov.size() * sizeof(uint16_t));
+    std::memcpy(&host[o_ld], lb.delta.data(), lb.delta.size() * sizeof(float));
+    std::memcpy(&host[o_ll], lb.limit.data(), lb.limit.size() * sizeof(float));
+  }
 
   rt_scene* s = new rt_scene();
   s->device = device;
@@ -445,6 +471,12 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   s->dev.n_bvh4 = (int32_t)bvh4.size();
   s->dev.bvh4_stack = bvh4_stack;
   s->dev.bvh4_code16 = bvh4_code16 ? 1 : 0;
+  s->dev.lb_cells = lb.cells.empty() ? nullptr : (const LbCell*)(b + o_lc);
+  s->dev.lb_ov = (const uint16_t*)(b + o_lv);
+  s->dev.lb_delta = (const float*)(b + o_ld);
+  s->dev.lb_limit = (const float*)(b + o_ll);
+  s->dev.lb_res = lb.res;
+  s->dev.lb_n_items = (int32_t)std::min<size_t>(lb.n_items, 0x7FFFFFFF);
   s->dev.shade = (const ShadeRec*)(b + o_sh);
   s->dev.lights = (const LightRec*)(b + o_li);
   s->dev.n_diag = (int32_t)diag.size();

@@ -13,6 +13,7 @@
 #include "rt_bvh.hpp"
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstring>
 #include <limits>
@@ -327,6 +328,127 @@ std::vector<BvhNode4> collapse_bvh4(const std::vector<BvhNode>& bin, int* stack,
   if (stack) *stack = need;
   if (code16) *code16 = c.code16;
   return c.out;
+}
+
+// ------------------------------------------------------------ light buffer
+// See rt_layout.hpp (LbCell) and DESIGN.md "Light buffer" for the argument.
+// Margins: the query (binary32, from the binary64 shadow-ray vector) lands
+// within ~1e-6 (cube-map coordinate units) of the exact direction of any
+// root point at distance >= r0 from the light while |light - o| <= 2^24 r0;
+// the pyramid of a face is relaxed by kLbEta and every coordinate range is
+// widened by kLbMargin, both 1e-5.
+namespace {
+constexpr double kLbEta = 1e-5, kLbMargin = 1e-5;
+
+// distance from the origin to the box, 0 when it contains the origin
+double box_dist0(const double* lo, const double* hi) {
+  double s = 0.0;
+  for (int a = 0; a < 3; ++a) {
+    const double g = lo[a] > 0.0 ? lo[a] : hi[a] < 0.0 ? -hi[a] : 0.0;
+    s += g * g;
+  }
+  return std::sqrt(s);
+}
+double min_abs(double lo, double hi) { return lo > 0.0 ? lo : hi < 0.0 ? -hi : 0.0; }
+int lb_cell_index(double x, int R) {  // x in [-1, 1]
+  const int i = (int)std::floor((x + 1.0) * 0.5 * R);
+  return std::max(0, std::min(R - 1, i));
+}
+}  // namespace
+
+LightBuffer build_light_buffer(const std::vector<SphereDiag>& sph, const std::vector<LightRec>& lights, int R) {
+  LightBuffer lb;
+  const int n = (int)sph.size();
+  if (n == 0 || n >= 0xFFFF || R < 1 || lights.empty()) return lb;
+  lb.res = R;
+  const size_t per = (size_t)6 * R * R;
+  lb.cells.assign(lights.size() * per, LbCell{0, 0, 0, 0});
+  lb.delta.assign(lights.size() * (size_t)n, 0.0f);
+  lb.limit.assign(lights.size(), -1.0f);
+  std::vector<std::array<double, 6>> rel(n);
+  std::vector<double> delta(n);
+  std::vector<char> finite(n), caster(n), near(n);
+  std::vector<std::array<int, 4>> rect;  // per record and face: i_lo, i_hi, j_lo, j_hi (i_lo < 0: none)
+  std::vector<std::vector<uint16_t>> lists(per);
+  for (size_t l = 0; l < lights.size(); ++l) {
+    const double* L = lights[l].pos;
+    if (!(std::isfinite(L[0]) && std::isfinite(L[1]) && std::isfinite(L[2]))) continue;  // limit -1: exhaustive
+    double dmax = 0.0;
+    for (int i = 0; i < n; ++i) {
+      caster[i] = (sph[i].meta & 1) != 0;
+      const Box b = sphere_box(sph[i]);
+      bool fin = true;
+      for (int a = 0; a < 3; ++a) {
+        rel[i][a] = b.lo[a] - L[a];
+        rel[i][3 + a] = b.hi[a] - L[a];
+        fin = fin && std::isfinite(rel[i][a]) && std::isfinite(rel[i][3 + a]);
+      }
+      finite[i] = fin;
+      delta[i] = fin ? box_dist0(&rel[i][0], &rel[i][3]) * (1.0 - 1e-9) : 0.0;
+      if (caster[i] && fin) dmax = std::max(dmax, delta[i]);
+      lb.delta[l * n + i] = f32_down(delta[i]);
+    }
+    // records whose box comes within 1e-3 of the farthest box's distance are
+    // listed in every cell; r0 = the nearest of the others
+    const double r_near = 1e-3 * dmax;
+    double r0 = INFINITY;
+    for (int i = 0; i < n; ++i) {
+      near[i] = 0;
+      if (!caster[i]) continue;
+      near[i] = !finite[i] || delta[i] < r_near || delta[i] == 0.0;
+      if (!near[i]) r0 = std::min(r0, delta[i]);
+    }
+    lb.limit[l] = std::isfinite(r0) ? f32_down(std::min(0x1p24 * r0, 1e30)) : 1e30f;
+    auto face_rect = [&](int i, int f, int* r) {
+      r[0] = -1;
+      const int a = f >> 1, bx = (a + 1) % 3, cx = (a + 2) % 3;
+      const double s = (f & 1) ? -1.0 : 1.0;
+      const double* lo = &rel[i][0];
+      const double* hi = &rel[i][3];
+      const double A_lo = s > 0 ? lo[a] : -hi[a], A_hi = s > 0 ? hi[a] : -lo[a];
+      if (!(A_hi > 0.0)) return;
+      const double a_min = std::max(A_lo, std::max(min_abs(lo[bx], hi[bx]), min_abs(lo[cx], hi[cx])) / (1.0 + kLbEta));
+      if (a_min > A_hi) return;
+      double u_lo = -1.0, u_hi = 1.0, v_lo = -1.0, v_hi = 1.0;
+      if (a_min > 0.0) {
+        u_lo = std::min(lo[bx] / a_min, lo[bx] / A_hi) - kLbMargin;
+        u_hi = std::max(hi[bx] / a_min, hi[bx] / A_hi) + kLbMargin;
+        v_lo = std::min(lo[cx] / a_min, lo[cx] / A_hi) - kLbMargin;
+        v_hi = std::max(hi[cx] / a_min, hi[cx] / A_hi) + kLbMargin;
+      }
+      r[0] = lb_cell_index(std::max(-1.0, std::min(1.0, u_lo)), R);
+      r[1] = lb_cell_index(std::max(-1.0, std::min(1.0, u_hi)), R);
+      r[2] = lb_cell_index(std::max(-1.0, std::min(1.0, v_lo)), R);
+      r[3] = lb_cell_index(std::max(-1.0, std::min(1.0, v_hi)), R);
+    };
+    for (auto& v : lists) v.clear();
+    for (int i = 0; i < n; ++i) {
+      if (!caster[i]) continue;
+      for (int f = 0; f < 6; ++f) {
+        int r[4];
+        if (near[i]) { r[0] = 0; r[1] = R - 1; r[2] = 0; r[3] = R - 1; }
+        else face_rect(i, f, r);
+        if (r[0] < 0) continue;
+        for (int j = r[2]; j <= r[3]; ++j)
+          for (int k = r[0]; k <= r[1]; ++k) lists[(size_t)f * R * R + (size_t)j * R + k].push_back((uint16_t)i);
+      }
+    }
+    const float* dl = &lb.delta[l * n];
+    for (size_t c = 0; c < per; ++c) {
+      std::vector<uint16_t>& v = lists[c];
+      std::sort(v.begin(), v.end(), [&](uint16_t x, uint16_t y) { return dl[x] < dl[y] || (dl[x] == dl[y] && x < y); });
+      uint16_t in[kLbInline] = {0, 0, 0, 0, 0};
+      for (size_t k = 0; k < v.size() && k < (size_t)kLbInline; ++k) in[k] = v[k];
+      LbCell& cell = lb.cells[l * per + c];
+      cell.w0 = (uint32_t)std::min<size_t>(v.size(), 0xFFFF) | (uint32_t)in[0] << 16;
+      cell.w1 = in[1] | (uint32_t)in[2] << 16;
+      cell.w2 = in[3] | (uint32_t)in[4] << 16;
+      cell.ov = (uint32_t)lb.ov.size();
+      for (size_t k = kLbInline; k < v.size(); ++k) lb.ov.push_back(v[k]);
+      lb.n_items += v.size();
+    }
+  }
+  return lb;
 }
 
 }  // namespace rtamd

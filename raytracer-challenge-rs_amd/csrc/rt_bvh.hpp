@@ -1,5 +1,6 @@
 // rt_bvh.hpp — host-side BVH over the SphereDiag records (see rt_layout.hpp).
 #pragma once
+#include <stddef.h>
 #include <vector>
 
 #include "rt_layout.hpp"
@@ -26,5 +27,18 @@ std::vector<BvhNode> build_sphere_bvh(std::vector<SphereDiag>& spheres, int leaf
 // the sum of (children - 1) over its nodes). `code16` tells whether every
 // child fits BvhNode4::code.
 std::vector<BvhNode4> collapse_bvh4(const std::vector<BvhNode>& bin, int* stack = nullptr, bool* code16 = nullptr);
+
+// Light buffer over the shadow-casting records, one cube map of R x R cells
+// per face per light (rt_layout.hpp LbCell; DESIGN.md "Light buffer").
+// Empty (cells.size() == 0) when there are no records, or 65535 or more.
+struct LightBuffer {
+  int res = 0;
+  size_t n_items = 0;
+  std::vector<LbCell> cells;    // n_lights * 6R^2
+  std::vector<uint16_t> ov;     // list entries past the inline ones
+  std::vector<float> delta;     // n_lights * n_records
+  std::vector<float> limit;     // per light
+};
+LightBuffer build_light_buffer(const std::vector<SphereDiag>& spheres, const std::vector<LightRec>& lights, int R);
 
 }  // namespace rtamd

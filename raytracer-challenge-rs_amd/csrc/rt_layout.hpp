@@ -79,6 +79,33 @@ constexpr int kBvhLeafMax = 127;
 constexpr int kBvhMaxDepth = 60;  // traversal stack entries per wave
 constexpr int kLaneLdsDepth = 16;  // per-lane traversal: LDS stack when bvh_depth fits
 
+// Light buffer (Haines & Greenberg 1986, made exact): per point light, a
+// cube map of directions around the light (6 faces x R x R cells). Cell c of
+// light l lists every shadow-casting SphereDiag record whose padded box may
+// hold a point whose direction from the light falls in the cell (rt_bvh.cpp
+// build_light_buffer: a conservative projection with margins far above the
+// query's rounding), ordered by lb_delta[l * n_diag + idx], a binary32 lower
+// bound on the distance from the light to the record's box. A shadow ray from
+// o is blocked only by a sphere with a root point q on the segment
+// [o, light), and every such q lies in that sphere's box in the cell of
+// direction o - light (DESIGN.md "Light buffer"), so testing that cell's
+// list up to delta > |light - o| answers is_shadowed exactly. Records whose
+// box comes near the light are listed in every cell. The answer is valid
+// while |light - o| <= lb_limit[l]; farther origins take the exhaustive loop.
+//
+// One 16-B record per cell holds the list's first kLbInline 16-bit indices,
+// so a ray makes one dependent global load for its cell; longer lists
+// continue in lb_ov[ov ..].
+constexpr int kLbMaxLights = 16;
+constexpr int kLbInline = 5;
+struct alignas(16) LbCell {
+  uint32_t w0;  // count (low 16) | idx0 (high 16)
+  uint32_t w1;  // idx1 | idx2 << 16
+  uint32_t w2;  // idx3 | idx4 << 16
+  uint32_t ov;  // entries kLbInline.. at lb_ov[ov ..]
+};
+static_assert(sizeof(LbCell) == 16, "LbCell must stay 16 B");
+
 // Intersection ordering key: (object index << 2) | position in the object's
 // local_intersect list (at most 4 entries, cylinder/cone). Equal t resolve by
 // this key exactly like the reference's stable sort (intersection.rs:108-116).
@@ -120,6 +147,12 @@ struct DevScene {
   int32_t n_bvh4;
   int32_t bvh4_stack;  // most children a nearest-first four-wide traversal keeps pending
   int32_t bvh4_code16;  // 1 when every BvhNode4::code is valid (scenes of < 4088 diagonal spheres)
+  const LbCell* lb_cells;  // light buffer: n_lights * 6R^2 cells, nullptr when not built
+  const uint16_t* lb_ov;
+  const float* lb_delta;   // n_lights * n_diag
+  const float* lb_limit;   // per light
+  int32_t lb_res;          // R
+  int32_t lb_n_items;
 };
 
 struct DevCamera {

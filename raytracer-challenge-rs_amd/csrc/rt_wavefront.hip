@@ -32,10 +32,12 @@ int g_wf_lane = 7;  // secondary / shadow rays: 7 = per-lane with leaves batched
                     // + stack in LDS, 6 = nodes + stack in LDS, 1 = per-lane with an LDS (or scratch) stack,
                     // 0 = wave (packet) traversal
 int g_wf_skip_shadow = 1;  // fast path: leave out shadow rays that cannot change the colour
+int g_wf_shadow_lb = 1;    // 1 = shadow rays through the light buffer (DESIGN.md "Light buffer")
 int g_wf_refill = 0;       // 1 = lanes take a new ray as soon as theirs is done (DESIGN.md "Lane refill")
 // occupancy (waves per SIMD the register allocator targets) of the BVH trace kernels
 int g_tw_primary = 4, g_tw_closest = 4, g_tw_shadow = 4;
 constexpr int kWfBlock = 256;      // prep / shadow / combine
+constexpr int kLbWaves = 8;        // light-buffer shadow kernel: two 1024-thread blocks per CU
 
 #define WF_CHECK(x)                        \
   do {                                     \
@@ -44,6 +46,13 @@ constexpr int kWfBlock = 256;      // prep / shadow / combine
   } while (0)
 
 __device__ __forceinline__ unsigned lane_id() { return __lane_id(); }
+
+// The calling wave's row of the work counters (WfCounters): lane 0 adds the
+// wave's totals there.
+__device__ __forceinline__ WfWorkRow* work_row(WfCounters* c) {
+  const unsigned w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  return c->work + (w & (kWorkRows - 1));
+}
 
 // Wave-aggregated queue append: every active lane calls it (convergent);
 // lanes with want=true get consecutive slots (in lane order) of `per` entries.
@@ -182,10 +191,11 @@ __device__ __forceinline__ void wf_ray(const WfArgs& a, const DevCamera& cam, un
 // built from the node's over point exactly as the reference builds it
 // (v = light - point, distance = |v|, direction = v.normalize()).
 __device__ __forceinline__ void shadow_ray(const DevScene& sc, const WfArgs& a, unsigned j, V3& o, V3& d,
-                                           double& dist, unsigned& slot) {
+                                           double& dist, unsigned& slot, unsigned* light = nullptr) {
   const unsigned L = (unsigned)sc.n_lights;
   slot = (unsigned)a.shadow_nodes[j];
   const unsigned node = L == 1 ? slot : slot / L, l = slot - node * L;
+  if (light) *light = l;
   const WfNode& nd = a.nodes[node];
   o = v3(nd.over[0], nd.over[1], nd.over[2]);
   cLightRec Lr = (cLightRec)sc.lights + l;
@@ -365,7 +375,7 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest(DevScene sc,
     a.hits[slot] = w;
   }
   const unsigned long long s = wave_sum(n_disc);
-  if (lane_id() == 0 && s) atomicAdd(&a.cnt->disc[a.disc_slot], s);
+  if (lane_id() == 0 && s) atomicAdd(&work_row(a.cnt)->disc[a.disc_slot], s);
 }
 
 // World::is_shadowed (world.rs:95-105): shadowed iff some shadow-casting
@@ -392,7 +402,7 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow(DevScene sc, 
     a.sflags[slot] = (h.key >= 0 && h.t < dist) ? 1 : 0;
   }
   const unsigned long long s = wave_sum(n_disc);
-  if (lane_id() == 0 && s) atomicAdd(&a.cnt->disc[a.disc_slot], s);
+  if (lane_id() == 0 && s) atomicAdd(&work_row(a.cnt)->disc[a.disc_slot], s);
 }
 
 // ---------------------------------------------------------- prep (spawn)
@@ -942,9 +952,9 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest_bvh(DevScene
   }
   const unsigned long long s = wave_sum(n_disc), st = wave_sum(n_tests), sb = wave_sum(n_boxes);
   if (lane_id() == 0) {
-    if (s) atomicAdd(&a.cnt->disc[a.disc_slot], s);
-    if (st) atomicAdd(&a.cnt->tests[a.disc_slot], st);
-    if (sb) atomicAdd(&a.cnt->boxes[a.disc_slot], sb);
+    if (s) atomicAdd(&work_row(a.cnt)->disc[a.disc_slot], s);
+    if (st) atomicAdd(&work_row(a.cnt)->tests[a.disc_slot], st);
+    if (sb) atomicAdd(&work_row(a.cnt)->boxes[a.disc_slot], sb);
   }
 }
 
@@ -983,9 +993,9 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow_bvh(DevScene 
   }
   const unsigned long long sd = wave_sum(n_disc), st = wave_sum(n_tests), sb = wave_sum(n_boxes);
   if (lane_id() == 0) {
-    if (sd) atomicAdd(&a.cnt->disc[a.disc_slot], sd);
-    if (st) atomicAdd(&a.cnt->tests[a.disc_slot], st);
-    if (sb) atomicAdd(&a.cnt->boxes[a.disc_slot], sb);
+    if (sd) atomicAdd(&work_row(a.cnt)->disc[a.disc_slot], sd);
+    if (st) atomicAdd(&work_row(a.cnt)->tests[a.disc_slot], st);
+    if (sb) atomicAdd(&work_row(a.cnt)->boxes[a.disc_slot], sb);
   }
 }
 
@@ -1089,9 +1099,101 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow_refill(DevSce
   }
   const unsigned long long sd = wave_sum(n_disc), st = wave_sum(n_tests), sb = wave_sum(n_boxes);
   if (lane_id() == 0) {
-    if (sd) atomicAdd(&a.cnt->disc[a.disc_slot], sd);
-    if (st) atomicAdd(&a.cnt->tests[a.disc_slot], st);
-    if (sb) atomicAdd(&a.cnt->boxes[a.disc_slot], sb);
+    if (sd) atomicAdd(&work_row(a.cnt)->disc[a.disc_slot], sd);
+    if (st) atomicAdd(&work_row(a.cnt)->tests[a.disc_slot], st);
+    if (sb) atomicAdd(&work_row(a.cnt)->boxes[a.disc_slot], sb);
+  }
+}
+
+// Shadow rays through the light buffer (DESIGN.md "Light buffer"): the
+// planes / general records first, exhaustively (as in every trace kernel),
+// then the cube-map cell of direction o - light lists every diagonal sphere
+// that can block the ray, nearest box first; the walk stops at the first
+// blocker or at the first box farther from the light than the origin. One
+// 16-B load brings the cell's first kLbInline entries. A ray whose origin is
+// beyond the light's validity radius (or non-finite) tests every sphere. The
+// sphere records and the per-light box distances are staged in LDS when they
+// fit.
+__host__ __device__ inline size_t lb_lds_bytes(const DevScene& sc) {
+  return (size_t)sc.n_diag * sizeof(SphereDiag) + (((size_t)sc.n_lights * sc.n_diag * sizeof(float) + 15) & ~(size_t)15);
+}
+template <bool QUADS, bool LDS, int TW>
+__global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow_lb(DevScene sc, WfArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lane_dyn[];
+  const SphereDiag* sd = sc.sph_diag;
+  const float* delta = sc.lb_delta;
+  if constexpr (LDS) {
+    const uint4* gs = (const uint4*)sc.sph_diag;
+    uint4* ls4 = (uint4*)lane_dyn;
+    const int n_rec = sc.n_diag * (int)(sizeof(SphereDiag) / 16);
+    for (int i = threadIdx.x; i < n_rec; i += blockDim.x) ls4[i] = gs[i];
+    float* ld = (float*)(lane_dyn + (size_t)sc.n_diag * sizeof(SphereDiag));
+    for (int i = threadIdx.x; i < sc.n_lights * sc.n_diag; i += blockDim.x) ld[i] = sc.lb_delta[i];
+    sd = (const SphereDiag*)lane_dyn;  // shard_prefix (or the barrier below) synchronises the block
+    delta = ld;
+  }
+  __shared__ unsigned s_pre[kShards + 1];
+  const unsigned* pre = shard_prefix(a.sh_cnt, s_pre);
+  if (!pre) __syncthreads();
+  unsigned n_disc = 0, n_tests = 0;
+  const int R = sc.lb_res;
+  const unsigned per_light = 6u * (unsigned)R * (unsigned)R;
+  const float half_r = 0.5f * (float)R;
+  const unsigned stride = gridDim.x * blockDim.x;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n_shadow; i += stride) {
+    V3 o, d;
+    double dist;
+    unsigned slot, l;
+    shadow_ray(sc, a, shard_slot(pre, a.sh_cap, i), o, d, dist, slot, &l);
+    Hit h;
+    hit_init(h);
+    trace_rest<true, QUADS>(sc, o, d, h, n_disc);  // planes first: any hit before the light ends the ray
+    if (!(h.key >= 0 && h.t < dist)) {
+      cLightRec Lr = (cLightRec)sc.lights + l;
+      if (dist <= (double)sc.lb_limit[l] && dist >= 1e-30) {
+        // w = o - light (= -(light - o) bit for bit), in binary32
+        const float wx = (float)(o.x - Lr->pos[0]), wy = (float)(o.y - Lr->pos[1]), wz = (float)(o.z - Lr->pos[2]);
+        const float ax = fabsf(wx), ay = fabsf(wy), az = fabsf(wz);
+        unsigned f;
+        float wa, wb, wc;
+        if (ax >= ay && ax >= az) { f = wx < 0.0f ? 1u : 0u; wa = ax; wb = wy; wc = wz; }
+        else if (ay >= az) { f = wy < 0.0f ? 3u : 2u; wa = ay; wb = wz; wc = wx; }
+        else { f = wz < 0.0f ? 5u : 4u; wa = az; wb = wx; wc = wy; }
+        const float u = fminf(fmaxf(wb / wa, -1.0f), 1.0f), v = fminf(fmaxf(wc / wa, -1.0f), 1.0f);
+        const unsigned iu = (unsigned)min((int)((u + 1.0f) * half_r), R - 1);
+        const unsigned iv = (unsigned)min((int)((v + 1.0f) * half_r), R - 1);
+        const LbCell c = sc.lb_cells[l * per_light + (f * (unsigned)R + iv) * (unsigned)R + iu];
+        const unsigned cnt = c.w0 & 0xFFFFu;
+        // the inline entries as a queue of 16-bit indices: idx0..idx3 in q, idx4 in c.w2 >> 16
+        unsigned long long q = (unsigned long long)(c.w0 >> 16) | (unsigned long long)c.w1 << 16 |
+                               (unsigned long long)(c.w2 & 0xFFFFu) << 48;
+        const float* dl = delta + (size_t)l * sc.n_diag;
+        const float dist_up = f32_up(dist);
+        for (unsigned k = 0; k < cnt; ++k) {
+          unsigned idx;
+          if (k < 4u) { idx = (unsigned)(q & 0xFFFFu); q >>= 16; }
+          else if (k == 4u) idx = c.w2 >> 16;
+          else idx = sc.lb_ov[c.ov + k - (unsigned)kLbInline];
+          if (dl[idx] > dist_up) break;  // this box and all after it lie beyond the origin
+          leaf_sphere_test<true, false>(sd, 0, (int)idx, o, d, h, n_disc);
+          ++n_tests;
+          if (h.key >= 0 && h.t < dist) break;
+        }
+      } else {
+        for (int k = 0; k < sc.n_diag; ++k) {
+          leaf_sphere_test<true, false>(sd, 0, k, o, d, h, n_disc);
+          ++n_tests;
+          if (h.key >= 0 && h.t < dist) break;
+        }
+      }
+    }
+    hit_finish(h);
+    a.sflags[slot] = (h.key >= 0 && h.t < dist) ? 1 : 0;
+  }
+  const unsigned long long sdc = wave_sum(n_disc), st = wave_sum(n_tests);
+  if (lane_id() == 0) {
+    if (sdc) atomicAdd(&work_row(a.cnt)->disc[a.disc_slot], sdc);
+    if (st) atomicAdd(&work_row(a.cnt)->tests[a.disc_slot], st);
   }
 }
 
@@ -1265,9 +1367,9 @@ hipError_t Wavefront::last_profile(WfProfile* out) {
   if (d_cnt_) WF_CHECK(hipMemcpy(&hc, d_cnt_, sizeof hc, hipMemcpyDeviceToHost));  // nothing rendered yet: zeros
   for (int c = 0; c < 3; ++c) {
     out->rays[c] = prof_rays_[c];
-    out->disc[c] = (double)hc.disc[c];
-    out->tests[c] = (double)hc.tests[c];
-    out->boxes[c] = (double)hc.boxes[c];
+    out->disc[c] = (double)hc.disc(c);
+    out->tests[c] = (double)hc.tests(c);
+    out->boxes[c] = (double)hc.boxes(c);
   }
   out->bvh = last_bvh_ ? 1 : 0;
   return hipSuccess;
@@ -1419,7 +1521,17 @@ static hipError_t launch_closest(const DevScene& sc, const DevCamera& cam, const
 
 template <bool QUADS, int TW>
 static hipError_t launch_shadow_q(const DevScene& sc, const WfArgs& a, bool lds_ok, bool bvh, hipStream_t stream) {
-  if (bvh) {
+  if (bvh && g_wf_shadow_lb && sc.lb_cells) {
+    const size_t lds = lb_lds_bytes(sc);
+    if (lds <= kWfLdsLimit) {
+      auto k = wf_trace_shadow_lb<QUADS, true, QUADS ? 4 : kLbWaves>;
+      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, a.n_shadow)), dim3(kTraceBlock), lds, stream, sc, a);
+    } else {
+      auto k = wf_trace_shadow_lb<QUADS, false, QUADS ? 4 : kLbWaves>;
+      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, a.n_shadow)), dim3(kTraceBlock), 0, stream, sc, a);
+    }
+  } else if (bvh) {
     if (g_wf_refill && (g_wf_lane == 7 || g_wf_lane == 9) && sc.bvh_depth <= kLaneLdsDepth &&
         lane_lds_bytes(sc) <= kWfLdsLimit) {
       const size_t lds = lane_lds_bytes(sc);
@@ -1666,7 +1778,7 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     s.sphere_tests = (rays + shadows) * (unsigned long long)(sc.n_diag + sc.n_gen);
     s.plane_tests = (rays + shadows) * (unsigned long long)sc.n_planes;
     s.other_tests = (rays + shadows) * (unsigned long long)sc.n_quads;
-    s.sphere_disc_ge0 = hc.disc[0] + hc.disc[1] + hc.disc[2];
+    s.sphere_disc_ge0 = hc.disc(0) + hc.disc(1) + hc.disc(2);
     *stats = s;
   }
   return hipSuccess;

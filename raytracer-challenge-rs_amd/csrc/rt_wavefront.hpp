@@ -64,14 +64,38 @@ extern int g_wf_trace_waves;  // tuning knob: trace-kernel occupancy (4 or 8 wav
 extern int g_tw_primary, g_tw_closest, g_tw_shadow;  // tuning knobs: BVH trace-kernel occupancy
 extern int g_wf_lane;         // tuning knob: 1 = per-lane BVH traversal for secondary / shadow rays
 extern int g_wf_accel;        // tuning knob: 1 = BVH traversal (when no counters are requested), 0 = exhaustive
+extern int g_wf_shadow_lb;    // tuning knob: 1 = shadow rays through the light buffer when the scene has one
 extern int g_wf_refill;       // tuning knob: 1 = lane refill in the per-lane trace kernels
 extern int g_wf_skip_shadow;  // tuning knob: 1 = the fast path leaves out shadow rays that cannot change the colour
 
-struct WfCounters {
-  unsigned n_refl[kMaxGen], n_refr[kMaxGen];
-  unsigned long long disc[3];  // disc >= 0 tests: [0] primary closest, [1] closest, [2] shadow
+// Work counters of the trace kernels, one row per wave slot (wave id mod
+// kWorkRows, rows 128 B apart): thousands of waves ending together would
+// otherwise queue on one address (one L2 atomic at a time), which cost the
+// short light-buffer launches most of their time. The host sums the rows.
+constexpr int kWorkRows = 256;
+struct alignas(128) WfWorkRow {
+  unsigned long long disc[3];   // disc >= 0 tests: [0] primary closest, [1] closest, [2] shadow
   unsigned long long tests[3];  // BVH mode: sphere tests executed (lanes x spheres), per trace class
   unsigned long long boxes[3];  // BVH mode: child-box tests executed (lanes x boxes)
+};
+struct WfCounters {
+  unsigned n_refl[kMaxGen], n_refr[kMaxGen];
+  WfWorkRow work[kWorkRows];
+  unsigned long long disc(int c) const {
+    unsigned long long t = 0;
+    for (int r = 0; r < kWorkRows; ++r) t += work[r].disc[c];
+    return t;
+  }
+  unsigned long long tests(int c) const {
+    unsigned long long t = 0;
+    for (int r = 0; r < kWorkRows; ++r) t += work[r].tests[c];
+    return t;
+  }
+  unsigned long long boxes(int c) const {
+    unsigned long long t = 0;
+    for (int r = 0; r < kWorkRows; ++r) t += work[r].boxes[c];
+    return t;
+  }
 };
 
 struct WfGenBuf {

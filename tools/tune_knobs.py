@@ -11,7 +11,7 @@ from rtamd import scenes
 args = [x for x in sys.argv[1:] if "=" in x]
 scene = "c5" if "--c5" in sys.argv else "c3"
 knobs = [(k, [int(v) for v in vs.split(",")]) for k, vs in (x.split("=") for x in args)]
-SCENE_KNOBS = ("bvh_leaf", "bvh_ct")  # applied at scene creation: one world per value
+SCENE_KNOBS = ("bvh_leaf", "bvh_ct", "lb_res")  # applied at scene creation: one world per value
 
 
 def make_world():
@@ -42,7 +42,7 @@ for r in range(4):
         p = rtamd._rtamd._wf_profile(w, 0, True)
         lds = (max(int(p["bvh_depth"]), 1) * 4096 + 64 * p["n_bvh_nodes"] + 64 * p["n_diag"]) / 1024
         res.setdefault(combo, []).append((sum(p["ms"].values()), p["ms"], p["tests"], p["boxes"],
-                                          f"nodes {p['n_bvh_nodes']} depth {p['bvh_depth']} lane-LDS {lds:.0f}KB"))
+                                          f"lb {p['lb_res']:.0f}/{p['lb_items']:.0f} nodes {p['n_bvh_nodes']} depth {p['bvh_depth']} lane-LDS {lds:.0f}KB"))
         chk = buf.cpu().numpy().tobytes()
         ref = ref or chk
         assert chk == ref or "--no-check" in sys.argv, combo
