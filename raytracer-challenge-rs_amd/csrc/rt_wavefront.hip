@@ -37,7 +37,7 @@ int g_wf_refill = 0;       // 1 = lanes take a new ray as soon as theirs is done
 // occupancy (waves per SIMD the register allocator targets) of the BVH trace kernels
 int g_tw_primary = 4, g_tw_closest = 4, g_tw_shadow = 4;
 constexpr int kWfBlock = 256;      // prep / shadow / combine
-constexpr int kLbWaves = 8;        // light-buffer shadow kernel: two 1024-thread blocks per CU
+constexpr int kLbWaves = 4;        // light-buffer shadow kernel (lighting() needs > 64 VGPRs)
 
 #define WF_CHECK(x)                        \
   do {                                     \
@@ -196,12 +196,25 @@ __device__ __forceinline__ void shadow_ray(const DevScene& sc, const WfArgs& a, 
   slot = (unsigned)a.shadow_nodes[j];
   const unsigned node = L == 1 ? slot : slot / L, l = slot - node * L;
   if (light) *light = l;
-  const WfNode& nd = a.nodes[node];
-  o = v3(nd.over[0], nd.over[1], nd.over[2]);
+  const double* ov = a.geo[node].over;
+  o = v3(ov[0], ov[1], ov[2]);
   cLightRec Lr = (cLightRec)sc.lights + l;
   const V3 v = vsub(v3(Lr->pos[0], Lr->pos[1], Lr->pos[2]), o);
   dist = sqrt(v.x * v.x + v.y * v.y + v.z * v.z);  // magnitude (vector.rs:21-23)
   d = vnormalize(v);
+}
+
+// The outcome of shadow ray `slot` (= node slot * L + light): lighting() of
+// the hit with that light (material.rs:38-82), in shadow or not, as the
+// reference's shade_hit evaluates it (world.rs:41-56).
+__device__ __forceinline__ void shadow_result(const DevScene& sc, const WfArgs& a, unsigned slot, bool shadowed) {
+  const unsigned L = (unsigned)sc.n_lights;
+  const unsigned node = L == 1 ? slot : slot / L, l = slot - node * L;
+  const WfGeo& g = a.geo[node];
+  const V3 c = lighting(sc.shade[g.obj], (cLightRec)sc.lights + l, v3(g.over[0], g.over[1], g.over[2]),
+                        v3(g.eyev[0], g.eyev[1], g.eyev[2]), v3(g.normal[0], g.normal[1], g.normal[2]), shadowed);
+  double* dst = a.surf + (size_t)slot * 3;
+  dst[0] = c.x; dst[1] = c.y; dst[2] = c.z;
 }
 
 // A shadow ray whose answer cannot change the colour (DESIGN.md "Skipped
@@ -209,14 +222,14 @@ __device__ __forceinline__ void shadow_ray(const DevScene& sc, const WfArgs& a, 
 // `ambient` in shadow and `ambient + 0 + 0` in light (material.rs:23-87),
 // bit-identical unless a component of ambient is -0 or NaN. Evaluated with
 // the operations lighting() itself performs; patterned materials are never
-// skipped (their colour is only known in wf_combine).
-__device__ __forceinline__ bool shadow_irrelevant(const ShadeRec& m, cLightRec L, V3 over, V3 normal) {
+// skipped. Returns whether it is, and that ambient value.
+__device__ __forceinline__ bool shadow_irrelevant(const ShadeRec& m, cLightRec L, V3 over, V3 normal, V3& ambient) {
   if (m.pattern_kind >= 0) return false;
   const V3 lightv = vnormalize(vsub(v3(L->pos[0], L->pos[1], L->pos[2]), over));
   if (!(vdot(lightv, normal) < 0.0)) return false;
   const V3 effective_color = vmul(v3(m.color[0], m.color[1], m.color[2]),
                                   v3(L->intensity[0], L->intensity[1], L->intensity[2]));
-  const V3 ambient = vscale(effective_color, m.ambient);
+  ambient = vscale(effective_color, m.ambient);
   auto plain = [](double x) { return x == x && !(x == 0.0 && signbit(x)); };
   return plain(ambient.x) && plain(ambient.y) && plain(ambient.z);
 }
@@ -399,7 +412,7 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow(DevScene sc, 
     Hit h;
     if constexpr (USE_LDS) wf_trace_lds<false, true, QUADS>(sc, lv, o, d, h, n_disc);
     else trace<true>(sc, o, d, h, n_disc);
-    a.sflags[slot] = (h.key >= 0 && h.t < dist) ? 1 : 0;
+    shadow_result(sc, a, slot, h.key >= 0 && h.t < dist);
   }
   const unsigned long long s = wave_sum(n_disc);
   if (lane_id() == 0 && s) atomicAdd(&work_row(a.cnt)->disc[a.disc_slot], s);
@@ -441,31 +454,40 @@ __device__ __forceinline__ void prep_one(const DevScene& sc, const WfArgs& a, un
     }
   }
   // shadow rays: one per light (world.rs:41-56); the fast path leaves out the
-  // ones whose answer cannot change the colour (their flag is written here)
+  // ones whose answer cannot change the colour, and their lighting() value
+  // (the ambient term) is written here; the shadow trace writes the others
   unsigned n_s = 0, skip = 0;
   if (hit) {
     for (unsigned l = 0; l < L; ++l) {
-      if (a.skip_shadow && l < 32 && shadow_irrelevant(*m, (cLightRec)sc.lights + l, c.over, c.normal))
+      V3 amb;
+      if (a.skip_shadow && l < 32 && shadow_irrelevant(*m, (cLightRec)sc.lights + l, c.over, c.normal, amb)) {
         skip |= 1u << l;
-      else
+        double* sp = a.surf + ((size_t)slot * L + l) * 3;
+        sp[0] = amb.x; sp[1] = amb.y; sp[2] = amb.z;
+      } else {
         ++n_s;
+      }
     }
   }
   unsigned sbase, rbase, fbase;
   shard_append(a, i / 64, n_s, want_refl, want_refr, sbase, rbase, fbase);
   if (!valid) return;
   WfNode nd;
-  nd.obj = -1; nd.child_refl = -1; nd.child_refr = -1; nd.pad = 0;
+  nd.obj = -1; nd.child_refl = -1; nd.child_refr = -1; nd.pad = 0; nd.schlick = 0.0;
   if (hit) {
     nd.obj = c.obj;
-    nd.over[0] = c.over.x; nd.over[1] = c.over.y; nd.over[2] = c.over.z;
-    nd.normal[0] = c.normal.x; nd.normal[1] = c.normal.y; nd.normal[2] = c.normal.z;
+    if (n_s) {
+      WfGeo gm;
+      gm.over[0] = c.over.x; gm.over[1] = c.over.y; gm.over[2] = c.over.z;
+      gm.normal[0] = c.normal.x; gm.normal[1] = c.normal.y; gm.normal[2] = c.normal.z;
+      gm.eyev[0] = c.eyev.x; gm.eyev[1] = c.eyev.y; gm.eyev[2] = c.eyev.z;
+      gm.obj = c.obj; gm.pad = 0;
+      a.geo[slot] = gm;
+    }
     // shade_hit's Schlick factor (world.rs:62-64), same inputs as the reference's call
     nd.schlick = (m->reflective > 0.0 && m->transparency > 0.0) ? schlick(c.eyev, c.normal, c.n1, c.n2) : 0.0;
-    for (unsigned l = 0; l < L; ++l) {  // its shadow rays are built by the shadow trace
-      if (l < 32 && (skip >> l & 1u)) a.sflags[slot * L + l] = 0;
-      else if (sbase != ~0u) a.shadow_nodes[sbase++] = (int32_t)(slot * L + l);
-    }
+    for (unsigned l = 0; l < L; ++l)  // its shadow rays are built by the shadow trace
+      if (!(l < 32 && (skip >> l & 1u)) && sbase != ~0u) a.shadow_nodes[sbase++] = (int32_t)(slot * L + l);
     if (want_refl && rbase != ~0u) {
       const V3 rv = vreflect(d, c.normal);  // comps.reflectv (intersection.rs:101)
       WfRay r;
@@ -989,7 +1011,7 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow_bvh(DevScene 
       if (__any(!(h.key >= 0 && h.t < dist))) trace_rest<true, QUADS>(sc, o, d, h, n_disc);
     }
     hit_finish(h);
-    a.sflags[slot] = (h.key >= 0 && h.t < dist) ? 1 : 0;
+    shadow_result(sc, a, slot, h.key >= 0 && h.t < dist);
   }
   const unsigned long long sd = wave_sum(n_disc), st = wave_sum(n_tests), sb = wave_sum(n_boxes);
   if (lane_id() == 0) {
@@ -1093,7 +1115,7 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow_refill(DevSce
       pl = kBvhEmpty;
     }
     if (active && e == kBvhEmpty && pl == kBvhEmpty) {
-      a.sflags[slot] = (h.key >= 0 && h.t < dist) ? 1 : 0;
+      shadow_result(sc, a, slot, h.key >= 0 && h.t < dist);
       active = false;
     }
   }
@@ -1188,7 +1210,7 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow_lb(DevScene s
       }
     }
     hit_finish(h);
-    a.sflags[slot] = (h.key >= 0 && h.t < dist) ? 1 : 0;
+    shadow_result(sc, a, slot, h.key >= 0 && h.t < dist);
   }
   const unsigned long long sdc = wave_sum(n_disc), st = wave_sum(n_tests);
   if (lane_id() == 0) {
@@ -1225,7 +1247,6 @@ __global__ __launch_bounds__(kWfBlock) void wf_prep(DevScene sc, DevCamera cam, 
 __global__ __launch_bounds__(kWfBlock) void wf_combine(DevScene sc, DevCamera cam, WfArgs a) {
   const unsigned stride = gridDim.x * blockDim.x;
   const unsigned L = (unsigned)sc.n_lights;
-  cLightRec lights = (cLightRec)sc.lights;
   __shared__ unsigned s_pre[kShards + 1];
   const unsigned* pre = shard_prefix(a.in_cnt, s_pre);
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
@@ -1233,16 +1254,11 @@ __global__ __launch_bounds__(kWfBlock) void wf_combine(DevScene sc, DevCamera ca
     const WfNode nd = a.nodes[slot];
     V3 color = v3(0.0, 0.0, 0.0);
     if (nd.obj >= 0) {
-      V3 o, d;
-      wf_ray(a, cam, slot, o, d);
       const ShadeRec& m = sc.shade[nd.obj];
-      const V3 over = v3(nd.over[0], nd.over[1], nd.over[2]);
-      const V3 normal = v3(nd.normal[0], nd.normal[1], nd.normal[2]);
-      const V3 eyev = vneg(d);
       V3 surface = v3(0.0, 0.0, 0.0);  // Sum = fold from (0,0,0) (color.rs:96-103)
       for (unsigned l = 0; l < L; ++l) {
-        const bool shadowed = a.sflags[slot * L + l] != 0;
-        surface = vadd(surface, lighting(m, lights + l, over, eyev, normal, shadowed));
+        const double* sp = a.surf + ((size_t)slot * L + l) * 3;
+        surface = vadd(surface, v3(sp[0], sp[1], sp[2]));
       }
       V3 refl = v3(0.0, 0.0, 0.0), refr = v3(0.0, 0.0, 0.0);
       if (nd.child_refl >= 0) {
@@ -1320,7 +1336,7 @@ static thread_local int t_ev_used = 0;
 Wavefront::~Wavefront() {
   for (auto& g : gens_) {
     (void)hipFree(g.rays); (void)hipFree(g.hits); (void)hipFree(g.nodes); (void)hipFree(g.colors);
-    (void)hipFree(g.shadow_nodes); (void)hipFree(g.sflags);
+    (void)hipFree(g.shadow_nodes); (void)hipFree(g.geo); (void)hipFree(g.surf);
   }
   if (d_cnt_) (void)hipFree(d_cnt_);
   if (d_shard_) (void)hipFree(d_shard_);
@@ -1383,21 +1399,23 @@ hipError_t Wavefront::ensure_gen(size_t g, size_t slots, size_t n_lights, size_t
   slots = std::max<size_t>(slots, 1);
   if (b.cap_rays < slots) {
     (void)hipFree(b.rays); (void)hipFree(b.hits); (void)hipFree(b.nodes); (void)hipFree(b.colors);
-    b.rays = nullptr; b.hits = nullptr; b.nodes = nullptr; b.colors = nullptr;
+    (void)hipFree(b.geo);
+    b.rays = nullptr; b.hits = nullptr; b.nodes = nullptr; b.colors = nullptr; b.geo = nullptr;
     b.cap_rays = 0;
     const size_t cap = slots + slots / 8;
     WF_CHECK(hipMalloc(&b.rays, cap * sizeof(WfRay)));
     WF_CHECK(hipMalloc(&b.hits, cap * sizeof(WfHit)));
     WF_CHECK(hipMalloc(&b.nodes, cap * sizeof(WfNode)));
     WF_CHECK(hipMalloc(&b.colors, cap * 3 * sizeof(double)));
+    WF_CHECK(hipMalloc(&b.geo, cap * sizeof(WfGeo)));
     b.cap_rays = cap;
   }
   const size_t need_sh = std::max<size_t>(b.cap_rays * n_lights, 1);
   if (b.cap_shadows < need_sh) {
-    (void)hipFree(b.sflags);
-    b.sflags = nullptr;
+    (void)hipFree(b.surf);
+    b.surf = nullptr;
     b.cap_shadows = 0;
-    WF_CHECK(hipMalloc(&b.sflags, need_sh));
+    WF_CHECK(hipMalloc(&b.surf, need_sh * 3 * sizeof(double)));
     b.cap_shadows = need_sh;
   }
   list_slots = std::max<size_t>(list_slots, 1);
@@ -1524,11 +1542,11 @@ static hipError_t launch_shadow_q(const DevScene& sc, const WfArgs& a, bool lds_
   if (bvh && g_wf_shadow_lb && sc.lb_cells) {
     const size_t lds = lb_lds_bytes(sc);
     if (lds <= kWfLdsLimit) {
-      auto k = wf_trace_shadow_lb<QUADS, true, QUADS ? 4 : kLbWaves>;
+      auto k = wf_trace_shadow_lb<QUADS, true, kLbWaves>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, a.n_shadow)), dim3(kTraceBlock), lds, stream, sc, a);
     } else {
-      auto k = wf_trace_shadow_lb<QUADS, false, QUADS ? 4 : kLbWaves>;
+      auto k = wf_trace_shadow_lb<QUADS, false, kLbWaves>;
       WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, a.n_shadow)), dim3(kTraceBlock), 0, stream, sc, a);
     }
   } else if (bvh) {
@@ -1650,7 +1668,8 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     WF_CHECK(ensure_gen(g + 1, (size_t)kShards * out_cap, L, 0));
     WfArgs a{};
     WfGenBuf& B = gens_[g];
-    a.rays = B.rays; a.hits = B.hits; a.nodes = B.nodes; a.shadow_nodes = B.shadow_nodes; a.sflags = B.sflags;
+    a.rays = B.rays; a.hits = B.hits; a.nodes = B.nodes; a.shadow_nodes = B.shadow_nodes;
+    a.geo = B.geo; a.surf = B.surf;
     a.colors = (g == 0 && !averaged) ? d_out : B.colors;
     a.aa = aa;
     a.rows = n0 / aa / (cam.hsize ? cam.hsize : 1);
@@ -1729,7 +1748,7 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
   for (int g = (int)last; g >= 0; --g) {
     WfArgs a{};
     WfGenBuf& B = gens_[g];
-    a.rays = B.rays; a.nodes = B.nodes; a.sflags = B.sflags;
+    a.rays = B.rays; a.nodes = B.nodes; a.surf = B.surf;
     a.colors = (g == 0 && !averaged) ? d_out : B.colors;
     a.aa = aa;
     a.rows = n0 / aa / (cam.hsize ? cam.hsize : 1);

@@ -44,8 +44,7 @@ struct WfHit {  // 24 B: nearest hit + containers top-2 (rt_device.hpp Hit)
   double t;
   int32_t key, c1k, c2k, hin;
 };
-struct WfNode {  // 72 B: what shade_hit needs from prepare_computations
-  double over[3], normal[3];
+struct WfNode {  // 24 B: what shade_hit needs besides the lighting (which prep_one evaluates)
   double schlick;      // Computations::schlick (only read when reflective && transparent)
   int32_t obj;         // -1 = miss
   int32_t child_refl;  // index into rays_{g+1}, -1 = none (black)
@@ -98,13 +97,19 @@ struct WfCounters {
   }
 };
 
+struct WfGeo {  // 80 B: the lighting() inputs of a hit (comps.over_point, normalv, eyev)
+  double over[3], normal[3], eyev[3];
+  int32_t obj;
+  int32_t pad;
+};
 struct WfGenBuf {
   WfRay* rays = nullptr;
   WfHit* hits = nullptr;
   WfNode* nodes = nullptr;
   double* colors = nullptr;
   int32_t* shadow_nodes = nullptr;  // shadow list of the generation (node slot * L + light, sharded)
-  uint8_t* sflags = nullptr;         // per node slot and light
+  WfGeo* geo = nullptr;              // per node slot: what the shadow trace needs to evaluate lighting()
+  double* surf = nullptr;            // lighting() per node slot and light (3 doubles)
   size_t cap_rays = 0, cap_shadows = 0, cap_list = 0;
 };
 
@@ -115,7 +120,9 @@ struct WfArgs {
   WfNode* nodes;
   double* colors;       // colors_g (g >= 1) or the output (g == 0)
   int32_t* shadow_nodes;  // shadow list of this generation: entries node slot * L + light
-  uint8_t* sflags;
+  WfGeo* geo;           // per node slot: over point, normal, eye vector, object
+  double* surf;         // per node slot * L + light: lighting() (written by prep_one when the light needs
+                        // no shadow ray, else by the shadow trace)
   WfRay* next_rays;     // rays_{g+1}
   const double* child_colors;  // colors_{g+1}
   WfCounters* cnt;
