@@ -67,8 +67,11 @@ def parse():
     p.add_argument("--spheres", type=int, default=1000)
     p.add_argument("--depth", type=int, default=5)
     p.add_argument("--row-block", type=int, default=8)
+    p.add_argument("--inflight", type=int, default=3,
+                   help="frames in flight: consecutive frames render on this many streams (own workspaces)")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget for the CPU baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--knob", action="append", default=[], help="library tuning knob k=v (dev; see rt_api.cpp)")
     p.add_argument("--exhaustive", action="store_true",
                    help="disable the exact-culling BVH: every ray tests every shape (the reference's loop)")
     p.add_argument("--pmc-summary", default=os.path.join(REPO, "profiles", "r01_pmc_summary.json"),
@@ -122,6 +125,9 @@ def main():
     if n > 1:
         dist.init_process_group("nccl", device_id=dev)
 
+    for kv in a.knob:
+        k, v = kv.split("=")
+        rtamd._rtamd._tuning_set(k, int(v))
     world, cam, depth = scenes.c3(a.width, a.height, a.spheres)
     if a.depth != depth:
         depth = a.depth
@@ -131,16 +137,39 @@ def main():
     W, H, B = cam.hsize, cam.vsize, a.row_block
     # interleaved row blocks + one RCCL gather per frame; two shard slots so that
     # frame s's gather overlaps frame s+1's render (rtamd.distributed.FrameAssembler)
-    fa = FrameAssembler(H, W, B, rank, n, dev, slots=2)
+    # F frames in flight: frame s renders on stream s % F (the library keeps one
+    # workspace per stream, so the renders overlap on the device) into shard
+    # slot s % (F + 1); the assembler (gather + un-interleave) runs on the
+    # current stream after that frame's render. A slot is rendered again only
+    # after the assembler has completed its previous frame (free_ev).
+    F = max(1, a.inflight)
+    fa = FrameAssembler(H, W, B, rank, n, dev, slots=F + 1 if F > 1 else 2)
     assert len(fa.rows) == rtamd.shard_rows(H, B, rank, n)
     shard = fa.shard
     stream = torch.cuda.current_stream()
+    # frame s renders on rstreams[s % F]; rstreams[0] is the current stream. With frames
+    # in flight the library's shadow side stream is off (the frames are the concurrency,
+    # and every extra stream competes for the GPU's few hardware queues).
+    rstreams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(F - 1)]
+    if F > 1:
+        rtamd._rtamd._tuning_set("shadow_stream", 0)
+    free_ev = [None] * len(fa.shards)
     frame_no = [0]
 
     def step():
         s = frame_no[0]
-        cam.render_shard_device(world, depth, B, rank, n, fa.slot(s).data_ptr(), stream.cuda_stream, False)
+        rs = rstreams[s % F]
+        slot = s % len(fa.shards)
+        if rs is not stream and free_ev[slot] is not None:
+            rs.wait_event(free_ev[slot])
+        cam.render_shard_device(world, depth, B, rank, n, fa.slot(s).data_ptr(), rs.cuda_stream, False)
+        if rs is not stream:
+            stream.wait_stream(rs)
         fa.submit(s)  # n == 1: the shard buffer already is the row-major canvas
+        if F > 1 and s > 0:  # frame s-1 is complete once the current stream gets here
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            free_ev[(s - 1) % len(fa.shards)] = ev
         frame_no[0] = s + 1
 
     # exact work counters of one frame (deterministic), from a counted warm-up launch
@@ -212,8 +241,9 @@ def main():
                             f"1 light, reflect+refract depth {depth}",
                 "width": W, "height": H, "spheres": a.spheres, "depth": depth,
                 "rays_per_frame": int(rays_per_frame),
-                "parallelism": f"{n} GPUs, one process each: interleaved {B}-row blocks, RCCL gather to rank 0"
-                               if n > 1 else "1 GPU: wavefront pipeline",
+                "parallelism": (f"{n} GPUs, one process each: interleaved {B}-row blocks, RCCL gather to rank 0"
+                                if n > 1 else "1 GPU: wavefront pipeline") + f"; {F} frames in flight",
+                "frames_in_flight": F,
             },
             "roofline": roofline(prof, breakdown, W, H, a, n, ref_work, elapsed / a.steps * 1e3),
         }

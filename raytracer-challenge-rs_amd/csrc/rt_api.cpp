@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -57,9 +58,57 @@ struct rt_scene {
   double* d_in = nullptr;       // cached input for batch entry points
   size_t in_cap = 0;
   hipStream_t stream = nullptr;
-  std::mutex mu;  // one call at a time per scene (shared workspace)
-  Wavefront wf;   // wavefront pipeline workspace (queues grow on demand)
+  std::mutex mu;  // one host call at a time per scene (the workspace pool)
+  // Wavefront workspaces (queues grow on demand), one per stream in use, at
+  // most kMaxWorkspaces: renders issued on different streams run concurrently
+  // on the device (frames in flight). A workspace taken over by
+  // another stream is reused in stream order: the new stream first waits on
+  // the event recorded after the workspace's last render.
+  struct WfSlot {
+    std::unique_ptr<Wavefront> wf;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    unsigned long long tick = 0;
+  };
+  static constexpr size_t kMaxWorkspaces = 8;
+  std::vector<WfSlot> wfs;
+  unsigned long long tick = 0;
+  WfSlot* last_wf = nullptr;
+  bool prof_on = false;
+  int prof_mask = (1 << WF_NCLASS) - 1;
   int n_objects = 0, n_lights = 0;
+  ~rt_scene() {
+    for (WfSlot& w : wfs)
+      if (w.done) (void)hipEventDestroy(w.done);
+  }
+  // the workspace for a render on `st` (stream-ordered after its previous user)
+  hipError_t acquire(hipStream_t st, WfSlot** out) {
+    WfSlot* pick = nullptr;
+    for (WfSlot& w : wfs)
+      if (w.stream == st) pick = &w;
+    if (!pick && wfs.size() < kMaxWorkspaces) {
+      wfs.reserve(kMaxWorkspaces);  // slot addresses stay valid
+      wfs.emplace_back();
+      pick = &wfs.back();
+      pick->wf = std::make_unique<Wavefront>();
+      hipError_t e = hipEventCreateWithFlags(&pick->done, hipEventDisableTiming);
+      if (e != hipSuccess) return e;
+      if (prof_on) pick->wf->set_profiling(true, prof_mask);
+      pick->stream = st;
+    }
+    if (!pick) {  // take over the least recently used workspace
+      pick = &wfs[0];
+      for (WfSlot& w : wfs)
+        if (w.tick < pick->tick) pick = &w;
+      hipError_t e = hipStreamWaitEvent(st, pick->done, 0);
+      if (e != hipSuccess) return e;
+      pick->stream = st;
+    }
+    pick->tick = ++tick;
+    last_wf = pick;
+    *out = pick;
+    return hipSuccess;
+  }
 };
 
 namespace {
@@ -164,8 +213,12 @@ int run_render(rt_scene* s, const DevCamera& cam, const double* d_rays, uint32_t
     const uint32_t p[6] = {n_tasks, aa, max_depth, row_block, shard, n_shards};
     sig.append((const char*)p, sizeof p);
   }
-  hipError_t e = s->wf.render(s->dev, cam, d_rays == nullptr, d_rays, n_tasks, aa, max_depth, row_block, shard,
-                              n_shards, d_out, stream, sig, stats_out, ms_out);
+  rt_scene::WfSlot* w = nullptr;
+  hipError_t e = s->acquire(stream, &w);
+  if (e == hipSuccess)
+    e = w->wf->render(s->dev, cam, d_rays == nullptr, d_rays, n_tasks, aa, max_depth, row_block, shard, n_shards,
+                      d_out, stream, sig, stats_out, ms_out, s->wfs.size() == 1);
+  if (e == hipSuccess) e = hipEventRecord(w->done, stream);
   if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("wavefront render: ") + hipGetErrorString(e));
   return RT_OK;
 }
@@ -199,11 +252,27 @@ int rtamd_wf_profile(const rt_scene* cs, int enable, double out[29]) {
   rt_scene* s = const_cast<rt_scene*>(cs);
   std::lock_guard<std::mutex> lk(s->mu);
   // enable: 0 off, 1 every kernel class, >= 2: (class mask << 1) | 1 (bench.py times one class)
-  if (enable >= 0) s->wf.set_profiling(enable != 0, enable > 1 ? (enable >> 1) : (1 << WF_NCLASS) - 1);
+  if (enable >= 0) {
+    s->prof_on = enable != 0;
+    s->prof_mask = enable > 1 ? (enable >> 1) : (1 << WF_NCLASS) - 1;
+    for (rt_scene::WfSlot& w : s->wfs) w.wf->set_profiling(s->prof_on, s->prof_mask);
+  }
   if (out) {
     RT_HIP(hipSetDevice(s->device));
-    WfProfile p;
-    RT_HIP(s->wf.last_profile(&p));
+    // class times: averaged over every frame profiled on any workspace; the
+    // counters: the last frame
+    WfProfile p{};
+    double ms_sum[WF_NCLASS] = {};
+    size_t frames = 0;
+    for (rt_scene::WfSlot& w : s->wfs) {
+      WfProfile q;
+      RT_HIP(w.wf->last_profile(&q));
+      const size_t f = w.wf->profiled_frames();
+      for (int c = 0; c < WF_NCLASS; ++c) ms_sum[c] += q.ms[c] * (double)(f > 1 ? f : 1);
+      frames += f > 1 ? f : (f == 1 ? 1 : 0);
+      if (&w == s->last_wf) p = q;
+    }
+    for (int c = 0; c < WF_NCLASS; ++c) p.ms[c] = frames ? ms_sum[c] / (double)frames : 0.0;
     for (int i = 0; i < 5; ++i) out[i] = p.ms[i];
     for (int i = 0; i < 3; ++i) { out[5 + i] = p.rays[i]; out[8 + i] = p.disc[i]; }
     out[11] = s->dev.n_diag; out[12] = s->dev.n_gen; out[13] = s->dev.n_planes;
@@ -249,6 +318,20 @@ int rtamd_tuning_set(const char* key, int value) {
   }
   if (key && std::strcmp(key, "refill") == 0) {
     rtamd::g_wf_refill = value;
+    return RT_OK;
+  }
+  if (key && std::strcmp(key, "shadow_stream") == 0) {
+    if (value < 0 || value > 2) return fail(RT_ERR_INVALID_ARGUMENT, "shadow_stream must be 0, 1 or 2");
+    rtamd::g_wf_shadow_stream = value;
+    return RT_OK;
+  }
+  if (key && std::strcmp(key, "adaptive_block") == 0) {
+    rtamd::g_wf_adaptive_block = value != 0;
+    return RT_OK;
+  }
+  if (key && std::strcmp(key, "refill_min") == 0) {
+    if (value < 1 || value > 64) return fail(RT_ERR_INVALID_ARGUMENT, "refill_min must be in [1, 64]");
+    rtamd::g_wf_refill_min = value;
     return RT_OK;
   }
   if (key && std::strcmp(key, "skip_shadow") == 0) {
@@ -401,6 +484,7 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   // come from `meta`, so the order changes no result)
   int bvh_depth = 0;
   std::vector<BvhNode> bvh = build_sphere_bvh(diag, g_bvh_leaf, &bvh_depth, g_bvh_ct / 100.0);
+  const bool bvh_code16 = !bvh.empty() && fill_code16(bvh);
   int bvh4_stack = 0;
   bool bvh4_code16 = false;
   std::vector<BvhNode4> bvh4 = collapse_bvh4(bvh, &bvh4_stack, &bvh4_code16);
@@ -467,6 +551,7 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   s->dev.bvh = bvh.empty() ? nullptr : (const BvhNode*)(b + o_bv);
   s->dev.n_bvh = (int32_t)bvh.size();
   s->dev.bvh_depth = bvh_depth;
+  s->dev.bvh_code16 = bvh_code16 ? 1 : 0;
   s->dev.bvh4 = bvh4.empty() ? nullptr : (const BvhNode4*)(b + o_b4);
   s->dev.n_bvh4 = (int32_t)bvh4.size();
   s->dev.bvh4_stack = bvh4_stack;

@@ -330,6 +330,28 @@ std::vector<BvhNode4> collapse_bvh4(const std::vector<BvhNode>& bin, int* stack,
   return c.out;
 }
 
+namespace {
+// BvhNode4::code encoding of a binary child code; false when it does not fit
+bool to_code16(int32_t c, uint16_t* out) {
+  if (c == kBvhEmpty) { *out = (uint16_t)kBvh4Empty; return true; }
+  if (c >= 0) { *out = (uint16_t)c; return c < 0x8000; }
+  const int code = -(c + 1), first = code >> 7, cnt = code & 127;
+  *out = (uint16_t)(0x8000 | (cnt - 1) << 12 | first);
+  return cnt >= 1 && cnt <= 8 && first + cnt < 0xFFF;
+}
+}  // namespace
+
+bool fill_code16(std::vector<BvhNode>& bin) {
+  bool ok = bin.size() < 0x8000;
+  for (BvhNode& n : bin) {
+    uint16_t c0 = 0, c1 = 0;
+    ok = to_code16(n.child[0], &c0) && ok;
+    ok = to_code16(n.child[1], &c1) && ok;
+    n.code16 = (uint32_t)c0 | (uint32_t)c1 << 16;
+  }
+  return ok;
+}
+
 // ------------------------------------------------------------ light buffer
 // See rt_layout.hpp (LbCell) and DESIGN.md "Light buffer" for the argument.
 // Margins: the query (binary32, from the binary64 shadow-ray vector) lands

@@ -28,6 +28,10 @@ std::vector<BvhNode> build_sphere_bvh(std::vector<SphereDiag>& spheres, int leaf
 // child fits BvhNode4::code.
 std::vector<BvhNode4> collapse_bvh4(const std::vector<BvhNode>& bin, int* stack = nullptr, bool* code16 = nullptr);
 
+// Fills BvhNode::code16 of every node; returns whether every child fits the
+// 16-bit code (else the 16-bit traversal is not used).
+bool fill_code16(std::vector<BvhNode>& bin);
+
 // Light buffer over the shadow-casting records, one cube map of R x R cells
 // per face per light (rt_layout.hpp LbCell; DESIGN.md "Light buffer").
 // Empty (cells.size() == 0) when there are no records, or 65535 or more.

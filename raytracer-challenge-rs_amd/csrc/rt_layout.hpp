@@ -51,11 +51,14 @@ static_assert(sizeof(QuadRec) == 128, "QuadRec must stay 128 B");
 // boxes (the slab test itself runs in binary64, so culling stays
 // conservative). A child is an internal node index (>= 0), a leaf code
 // -(1 + (first << 7 | count)) over the (reordered) SphereDiag array, or
-// kBvhEmpty.
+// kBvhEmpty. `code16` holds both children again as 16-bit codes (child 0 in
+// the low half; the encoding of BvhNode4::code), valid when
+// DevScene::bvh_code16 is set.
 struct alignas(64) BvhNode {
   float lo[2][3], hi[2][3];
   int32_t child[2];
-  int32_t axis, pad;
+  int32_t axis;
+  uint32_t code16;
 };
 static_assert(sizeof(BvhNode) == 64, "BvhNode must stay 64 B");
 // Four-wide node, collapsed from the binary hierarchy (rt_bvh.cpp): the four
@@ -143,6 +146,7 @@ struct DevScene {
   int32_t n_quads;
   int32_t n_bvh;
   int32_t bvh_depth;  // most far children pending on a traversal stack
+  int32_t bvh_code16;  // 1 when every BvhNode::code16 is valid (< 0x8000 nodes, leaves of <= 8 below 0xFFF)
   const BvhNode4* bvh4;  // the same hierarchy, four-wide (nullptr when the scene has no BVH)
   int32_t n_bvh4;
   int32_t bvh4_stack;  // most children a nearest-first four-wide traversal keeps pending

@@ -33,7 +33,9 @@ int g_wf_lane = 7;  // secondary / shadow rays: 7 = per-lane with leaves batched
                     // 0 = wave (packet) traversal
 int g_wf_skip_shadow = 1;  // fast path: leave out shadow rays that cannot change the colour
 int g_wf_shadow_lb = 1;    // 1 = shadow rays through the light buffer (DESIGN.md "Light buffer")
-int g_wf_refill = 0;       // 1 = lanes take a new ray as soon as theirs is done (DESIGN.md "Lane refill")
+int g_wf_refill = 0;       // 1 = lanes take a new ray as soon as theirs is done (DESIGN.md "Lane refill");
+                           // LANE 12 = the same for the closest-hit rays of generations >= 1
+int g_wf_refill_min = 16;
 // occupancy (waves per SIMD the register allocator targets) of the BVH trace kernels
 int g_tw_primary = 4, g_tw_closest = 4, g_tw_shadow = 4;
 constexpr int kWfBlock = 256;      // prep / shadow / combine
@@ -850,6 +852,81 @@ __device__ __forceinline__ void lane_trace4(const BvhNode4* nodes, const SphereD
   }
 }
 
+// Per-lane traversal on 16-bit child codes (LANE == 10 / 11; BvhNode::code16,
+// needs DevScene::bvh_code16): the same visit order, culling rule and
+// leaves batched across the wave as lane_trace<..., WW>, with a stack of
+// 16-bit entries in LDS (entry k of lane t at stk[k * kTraceBlock]) whose top
+// stays in a register, so a pop returns at once and the LDS read of the next
+// entry overlaps the next node's loads. Half the stack bytes of the 32-bit
+// walk: with the sphere records in global memory (LANE 10) a block's LDS
+// image fits twice in a CU.
+template <bool SHADOW>
+__device__ __forceinline__ void lane_trace16(const BvhNode* nodes, const SphereDiag* sd, const float* M, bool has_bvh,
+                                             V3 o, V3 d, double t_shadow, Hit& h, unsigned& n_disc, unsigned& n_tests,
+                                             unsigned& n_boxes, unsigned short* stk) {
+  const SlabRay sr = slab_ray(o, d, M);
+  float t_hi = f32_up(SHADOW ? t_shadow : h.t);
+  constexpr unsigned E = (unsigned)kBvh4Empty;
+  int sp = 0;
+  unsigned top = E;
+  auto push = [&](unsigned v) {
+    if (top != E) stk[(sp++) * kTraceBlock] = (unsigned short)top;
+    top = v;
+  };
+  auto pop = [&]() {
+    const unsigned r = top;
+    top = sp > 0 ? (unsigned)stk[(--sp) * kTraceBlock] : E;
+    return r;
+  };
+  unsigned e = (SHADOW && h.key >= 0 && h.t < t_shadow) || !has_bvh ? E : 0u;
+  auto visit = [&]() {
+    // the two boxes in three 16-B loads, the codes in one 4-B load
+    const uint4* np = reinterpret_cast<const uint4*>(nodes + e);
+    const uint4 q0 = np[0], q1 = np[1], q2 = np[2];
+    const unsigned cc = nodes[e].code16;
+    const float lo0[3] = {__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z)};
+    const float lo1[3] = {__uint_as_float(q0.w), __uint_as_float(q1.x), __uint_as_float(q1.y)};
+    const float hi0[3] = {__uint_as_float(q1.z), __uint_as_float(q1.w), __uint_as_float(q2.x)};
+    const float hi1[3] = {__uint_as_float(q2.y), __uint_as_float(q2.z), __uint_as_float(q2.w)};
+    const unsigned c0 = cc & 0xFFFFu, c1 = cc >> 16;
+    float t0, t1;
+    const bool h0 = slab_hit32(lo0, hi0, sr, t_hi, t0);
+    const bool h1 = slab_hit32(lo1, hi1, sr, t_hi, t1) & (c1 != E);
+    n_boxes += 2;
+    if (h0 && h1) {
+      const bool flip = t1 < t0;
+      push(flip ? c0 : c1);
+      e = flip ? c1 : c0;
+    } else {
+      e = h0 ? c0 : h1 ? c1 : pop();
+    }
+  };
+  auto leaf = [&](unsigned c) {
+    const int first = (int)(c & 0xFFFu), cnt = (int)((c >> 12) & 7u) + 1;
+    for (int k = first; k < first + cnt; ++k) leaf_sphere_test<SHADOW, false>(sd, 0, k, o, d, h, n_disc);
+    n_tests += (unsigned)cnt;
+    if constexpr (SHADOW) {
+      return h.key >= 0 && h.t < t_shadow;
+    } else {
+      t_hi = f32_up(h.t);
+      return false;
+    }
+  };
+  unsigned pl = E;
+  for (;;) {
+    for (;;) {
+      if (e != E && e >= 0x8000u && pl == E) { pl = e; e = pop(); }
+      if (!__any(e < 0x8000u && pl == E)) break;
+      if (e < 0x8000u) visit();  // lanes holding a leaf keep going (speculative)
+    }
+    if (!__any(pl != E)) break;
+    if (pl != E) {
+      if (leaf(pl)) { e = E; sp = 0; top = E; }  // shadowed: done
+      pl = E;
+    }
+  }
+}
+
 // LANE == 5: the block stages the hierarchy and the sphere records in LDS
 // (dynamic shared memory: [stack bvh_depth x kTraceBlock ints][nodes][spheres];
 // a lane pushes at most one entry per tree level).
@@ -864,6 +941,13 @@ __host__ __device__ inline size_t lane4_stack_bytes(const DevScene& sc) {
 }
 __host__ __device__ inline size_t lane4_lds_bytes(const DevScene& sc) {
   return lane4_stack_bytes(sc) + (size_t)sc.n_bvh4 * sizeof(BvhNode4) + (size_t)sc.n_diag * sizeof(SphereDiag);
+}
+// LANE 10 / 11: [16-bit stack bvh_depth x kTraceBlock][binary nodes][spheres (11 only)]
+__host__ __device__ inline size_t lane16_stack_bytes(const DevScene& sc) {
+  return ((size_t)(sc.bvh_depth > 0 ? sc.bvh_depth : 1) * kTraceBlock * 2 + 127) & ~(size_t)127;
+}
+__host__ __device__ inline size_t lane16_lds_bytes(const DevScene& sc, bool spheres) {
+  return lane16_stack_bytes(sc) + (size_t)sc.n_bvh * sizeof(BvhNode) + (spheres ? (size_t)sc.n_diag * sizeof(SphereDiag) : 0);
 }
 struct LaneScene {
   const BvhNode* nodes;
@@ -901,7 +985,23 @@ __device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, int* static_
     }
     return ls;
   }
-  if constexpr (LANE >= 5) {  // 6: the sphere records stay in global memory
+  if constexpr (LANE == 10 || LANE == 11) {  // 10: the sphere records stay in global memory
+    unsigned short* stack = (unsigned short*)dyn;
+    BvhNode* nodes = (BvhNode*)(dyn + lane16_stack_bytes(sc));
+    const uint4* gn = (const uint4*)sc.bvh;
+    uint4* ln = (uint4*)nodes;
+    for (int i = threadIdx.x; i < sc.n_bvh * (int)(sizeof(BvhNode) / 16); i += blockDim.x) ln[i] = gn[i];
+    if constexpr (LANE == 11) {
+      SphereDiag* sdl = (SphereDiag*)((unsigned char*)nodes + (size_t)sc.n_bvh * sizeof(BvhNode));
+      const uint4* gs = (const uint4*)sc.sph_diag;
+      uint4* ls4 = (uint4*)sdl;
+      for (int i = threadIdx.x; i < sc.n_diag * (int)(sizeof(SphereDiag) / 16); i += blockDim.x) ls4[i] = gs[i];
+      ls.sd = sdl;
+    }
+    __syncthreads();
+    ls.nodes = nodes;
+    ls.stack16 = stack + threadIdx.x;
+  } else if constexpr (LANE >= 5) {  // 6: the sphere records stay in global memory
     int* stack = (int*)dyn;
     BvhNode* nodes = (BvhNode*)(dyn + lane_stack_bytes(sc.bvh_depth));
     const uint4* gn = (const uint4*)sc.bvh;
@@ -937,6 +1037,12 @@ __device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, int* static_
 
 template <bool PRIMARY, bool QUADS, int LANE, int TW>
 __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest_bvh(DevScene sc, DevCamera cam, WfArgs a) {
+#ifdef RTAMD_PHASE
+  // phase-timing build (dev): shader cycles per wave of LDS staging (disc),
+  // traversal (tests) and shading + spawn (boxes), summed over the waves
+  const unsigned long long ph0 = __builtin_amdgcn_s_memtime();
+  unsigned long long ph_stage = 0, ph_trav = 0, ph_prep = 0;
+#endif
   constexpr bool LDS_STACK = LANE >= 2;
   __shared__ int stack_lds[LANE >= 5 ? 1 : LDS_STACK ? kLaneLdsDepth * kTraceBlock : (kTraceBlock / 64) * (kBvhMaxDepth + 4)];
   extern __shared__ __attribute__((aligned(16))) unsigned char lane_dyn[];
@@ -949,7 +1055,13 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest_bvh(DevScene
   // every lane of a wave runs the same number of iterations (prep_one's appends are wave-wide)
   const unsigned n_iter = (a.n + stride - 1) / stride;
   unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+#ifdef RTAMD_PHASE
+  ph_stage = __builtin_amdgcn_s_memtime() - ph0;
+#endif
   for (unsigned it = 0; it < n_iter; ++it, i += stride) {
+#ifdef RTAMD_PHASE
+    const unsigned long long pa = __builtin_amdgcn_s_memtime();
+#endif
     const bool valid = i < a.n;
     const unsigned slot = valid ? shard_slot(pre, a.in_cap, i) : 0u;
     V3 o = v3(0, 0, 0), d = v3(0, 0, 0);
@@ -957,7 +1069,10 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest_bvh(DevScene
     hit_init(h);
     if (valid) {
       wf_ray(a, cam, slot, o, d);
-      if constexpr (LANE == 8 && !PRIMARY) {
+      if constexpr ((LANE == 10 || LANE == 11) && !PRIMARY) {
+        trace_rest<false, QUADS>(sc, o, d, h, n_disc);  // planes first: an early nearest hit tightens the culling
+        lane_trace16<false>(ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, n_disc, n_tests, n_boxes, ls.stack16);
+      } else if constexpr (LANE == 8 && !PRIMARY) {
         trace_rest<false, QUADS>(sc, o, d, h, n_disc);  // planes first: an early nearest hit tightens the culling
         lane_trace4<false>(ls.nodes4, ls.sd, ls.M, sc.n_bvh4 > 0, o, d, 0.0, h, n_disc, n_tests, n_boxes, ls.stack16);
       } else if constexpr (LANE && !PRIMARY) {
@@ -970,8 +1085,23 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest_bvh(DevScene
       }
     }
     hit_finish(h);
+#ifdef RTAMD_PHASE
+    const unsigned long long pb = __builtin_amdgcn_s_memtime();
+    ph_trav += pb - pa;
+#endif
     prep_one(sc, a, i, slot, valid, o, d, h);  // the hit is shaded and spawned right here
+#ifdef RTAMD_PHASE
+    ph_prep += __builtin_amdgcn_s_memtime() - pb;
+#endif
   }
+#ifdef RTAMD_PHASE
+  if (lane_id() == 0) {
+    atomicAdd(&work_row(a.cnt)->disc[a.disc_slot], ph_stage);
+    atomicAdd(&work_row(a.cnt)->tests[a.disc_slot], ph_trav);
+    atomicAdd(&work_row(a.cnt)->boxes[a.disc_slot], ph_prep);
+  }
+  return;
+#endif
   const unsigned long long s = wave_sum(n_disc), st = wave_sum(n_tests), sb = wave_sum(n_boxes);
   if (lane_id() == 0) {
     if (s) atomicAdd(&work_row(a.cnt)->disc[a.disc_slot], s);
@@ -1122,6 +1252,114 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow_refill(DevSce
   const unsigned long long sd = wave_sum(n_disc), st = wave_sum(n_tests), sb = wave_sum(n_boxes);
   if (lane_id() == 0) {
     if (sd) atomicAdd(&work_row(a.cnt)->disc[a.disc_slot], sd);
+    if (st) atomicAdd(&work_row(a.cnt)->tests[a.disc_slot], st);
+    if (sb) atomicAdd(&work_row(a.cnt)->boxes[a.disc_slot], sb);
+  }
+}
+
+// Closest-hit rays with lane refill (LANE == 12, DESIGN.md "Lane refill"):
+// the per-lane traversal of lane_trace<false, true, true> (binary nodes,
+// sphere records and stack in LDS, leaves batched across the wave), but a
+// lane whose ray is finished takes the next ray of its wave's range at once
+// instead of idling until the wave's longest ray is done. The hit goes to the
+// hit queue; wf_prep shades it and spawns the children (prep_one needs whole
+// waves, which a refilling wave does not have). Each wave owns a contiguous
+// range of the generation; a refill happens after a leaf round once at least
+// a.refill_min lanes are idle (or none is busy). A ray's hit does not depend
+// on when or where it is traced, so the hits are those of lane_trace.
+template <bool QUADS, int TW>
+__global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest_refill(DevScene sc, DevCamera cam, WfArgs a) {
+  __shared__ int stack_lds[1];
+  extern __shared__ __attribute__((aligned(16))) unsigned char lane_dyn[];
+  const LaneScene ls = lane_scene<7>(sc, stack_lds, lane_dyn);
+  __shared__ unsigned s_pre[kShards + 1];
+  const unsigned* pre = shard_prefix(a.in_cnt, s_pre);
+  unsigned n_disc = 0, n_tests = 0, n_boxes = 0;
+  const unsigned waves = gridDim.x * (blockDim.x / 64);
+  const unsigned wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+  const unsigned per = (a.n + waves - 1) / waves;
+  unsigned next = min(wave * per, a.n);
+  const unsigned end = min(next + per, a.n);
+  const unsigned lane = lane_id();
+  const unsigned long long below = (1ull << lane) - 1ull;
+  int* const stk = ls.stack;
+  const bool has_bvh = sc.n_bvh > 0;
+  const unsigned rmin = a.refill_min;
+  bool active = false;
+  V3 o = v3(0, 0, 0), d = v3(0, 0, 0);
+  unsigned slot = 0;
+  Hit h;
+  hit_init(h);
+  SlabRay sr{};
+  float t_hi = 0.0f;
+  int e = kBvhEmpty, pl = kBvhEmpty, sp = 0;
+  auto pop = [&]() { return sp > 0 ? stk[(--sp) * kTraceBlock] : kBvhEmpty; };
+  for (;;) {
+    // refill idle lanes from the wave's range
+    const unsigned long long idle = __ballot(!active);
+    const unsigned n_idle = (unsigned)__popcll(idle);
+    if (next < end && (n_idle >= rmin || n_idle == 64u)) {
+      const unsigned j = next + (unsigned)__popcll(idle & below);
+      next = min(next + n_idle, end);
+      if (!active && j < end) {
+        slot = shard_slot(pre, a.in_cap, j);
+        wf_ray(a, cam, slot, o, d);
+        hit_init(h);
+        trace_rest<false, QUADS>(sc, o, d, h, n_disc);  // planes first: an early nearest hit tightens the culling
+        sr = slab_ray(o, d, ls.M);
+        t_hi = f32_up(h.t);
+        sp = 0;
+        pl = kBvhEmpty;
+        e = has_bvh ? 0 : kBvhEmpty;
+        active = true;
+      }
+    }
+    if (!__any(active)) break;
+    // node phase: lanes meeting a leaf postpone it and keep visiting nodes
+    for (;;) {
+      if (e < 0 && e != kBvhEmpty && pl == kBvhEmpty) { pl = e; e = pop(); }
+      if (!__any(e >= 0 && pl == kBvhEmpty)) break;
+      if (e >= 0) {
+        uint4 q0, q1, q2, q3;
+        node_chunks<false>(ls.nodes, sc.n_bvh, e, q0, q1, q2, q3);
+        const float lo0[3] = {__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z)};
+        const float lo1[3] = {__uint_as_float(q0.w), __uint_as_float(q1.x), __uint_as_float(q1.y)};
+        const float hi0[3] = {__uint_as_float(q1.z), __uint_as_float(q1.w), __uint_as_float(q2.x)};
+        const float hi1[3] = {__uint_as_float(q2.y), __uint_as_float(q2.z), __uint_as_float(q2.w)};
+        const int c0 = (int)q3.x, c1 = (int)q3.y;
+        float t0, t1;
+        const bool h0 = slab_hit32(lo0, hi0, sr, t_hi, t0);
+        const bool h1 = slab_hit32(lo1, hi1, sr, t_hi, t1) & (c1 != kBvhEmpty);
+        n_boxes += 2;
+        if (h0 && h1) {
+          const bool flip = t1 < t0;
+          stk[(sp++) * kTraceBlock] = flip ? c0 : c1;
+          e = flip ? c1 : c0;
+        } else {
+          e = h0 ? c0 : h1 ? c1 : pop();
+        }
+      }
+    }
+    // leaf round
+    if (pl != kBvhEmpty) {
+      const int code = -(pl + 1);
+      const int first = code >> 7, cnt = code & 127;
+      for (int k = first; k < first + cnt; ++k) leaf_sphere_test<false, false>(ls.sd, sc.n_diag, k, o, d, h, n_disc);
+      n_tests += (unsigned)cnt;
+      t_hi = f32_up(h.t);
+      pl = kBvhEmpty;
+    }
+    if (active && e == kBvhEmpty && pl == kBvhEmpty) {
+      hit_finish(h);
+      WfHit w;
+      w.t = h.t; w.key = h.key; w.c1k = h.c1k; w.c2k = h.c2k; w.hin = h.hin;
+      a.hits[slot] = w;
+      active = false;
+    }
+  }
+  const unsigned long long s = wave_sum(n_disc), st = wave_sum(n_tests), sb = wave_sum(n_boxes);
+  if (lane_id() == 0) {
+    if (s) atomicAdd(&work_row(a.cnt)->disc[a.disc_slot], s);
     if (st) atomicAdd(&work_row(a.cnt)->tests[a.disc_slot], st);
     if (sb) atomicAdd(&work_row(a.cnt)->boxes[a.disc_slot], sb);
   }
@@ -1343,6 +1581,10 @@ Wavefront::~Wavefront() {
   if (d_prim_) (void)hipFree(d_prim_);
   if (ev0_) (void)hipEventDestroy(ev0_);
   if (ev1_) (void)hipEventDestroy(ev1_);
+  for (hipEvent_t e : fork_ev_)
+    if (e) (void)hipEventDestroy(e);
+  if (join_ev_) (void)hipEventDestroy(join_ev_);
+  if (side_) (void)hipStreamDestroy(side_);
   for (hipEvent_t e : pev_) (void)hipEventDestroy(e);
 }
 
@@ -1430,6 +1672,26 @@ hipError_t Wavefront::ensure_gen(size_t g, size_t slots, size_t n_lights, size_t
   return hipSuccess;
 }
 
+// The shadow stream of the current device (recreated if the device changed).
+hipError_t Wavefront::ensure_side() {
+  int dev = 0;
+  WF_CHECK(hipGetDevice(&dev));
+  if (side_ && side_dev_ == dev) return hipSuccess;
+  if (side_) {
+    WF_CHECK(hipStreamSynchronize(side_));
+    (void)hipStreamDestroy(side_);
+    for (hipEvent_t& e : fork_ev_)
+      if (e) { (void)hipEventDestroy(e); e = nullptr; }
+    if (join_ev_) { (void)hipEventDestroy(join_ev_); join_ev_ = nullptr; }
+    side_ = nullptr;
+  }
+  WF_CHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+  for (hipEvent_t& e : fork_ev_) WF_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  WF_CHECK(hipEventCreateWithFlags(&join_ev_, hipEventDisableTiming));
+  side_dev_ = dev;
+  return hipSuccess;
+}
+
 hipError_t Wavefront::ensure_misc(size_t n_diag) {
   if (!d_cnt_) WF_CHECK(hipMalloc(&d_cnt_, sizeof(WfCounters)));
   if (!d_shard_) WF_CHECK(hipMalloc(&d_shard_, (size_t)kMaxGen * 2 * kShards * kShardStride * sizeof(unsigned)));
@@ -1457,6 +1719,28 @@ static int occupancy_grid(K kern, int block, size_t lds, unsigned n) {
 }
 
 static constexpr size_t kWfLdsLimit = 160 * 1024 - 1024;
+
+// Threads per block of a trace launch over n rays. A trace block holds one CU
+// (its LDS image), so a launch of fewer than (CUs x kTraceBlock) rays would
+// leave CUs idle with full-size blocks: such launches spread their rays over
+// every CU instead, in blocks of a multiple of 64 threads (small shards of a
+// multi-GPU frame, the deep generations). The kernels index their LDS stacks
+// with the kTraceBlock stride and loop over gridDim x blockDim, so any block
+// size up to kTraceBlock gives the same results.
+int g_wf_adaptive_block = 0;  // tuning knob ("adaptive_block"); frames in flight fill idle CUs better
+int g_wf_shadow_stream = 1;   // tuning knob ("shadow_stream"): 0 off, 1 when the frame renders alone, 2 always
+static int trace_block(unsigned n) {
+  if (!g_wf_adaptive_block) return kTraceBlock;
+  static int n_cu = 0;
+  if (n_cu == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (n_cu < 1) n_cu = 1;
+  }
+  const unsigned per = ((n + (unsigned)n_cu - 1) / (unsigned)n_cu + 63u) & ~63u;
+  return (int)std::min<unsigned>(std::max<unsigned>(per, 64u), (unsigned)kTraceBlock);
+}
 // the four-wide traversal runs when its 16-bit codes are valid and the block's LDS image fits
 static bool lane4_ok(const DevScene& sc) {
   return sc.n_bvh4 > 0 && sc.bvh4_code16 && lane4_lds_bytes(sc) <= kWfLdsLimit;
@@ -1476,57 +1760,69 @@ static bool lane4_ok(const DevScene& sc) {
 template <bool QUADS, int TW>
 static hipError_t launch_closest_q(const DevScene& sc, const DevCamera& cam, const WfArgs& a, bool primary,
                                    bool lds_ok, bool bvh, unsigned n, hipStream_t stream) {
+  const int tb = trace_block(n);
   if (bvh) {
     if (primary) {
       auto k = wf_trace_closest_bvh<true, QUADS, 0, TW>;
-      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
+      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, n)), dim3(tb), 0, stream, sc, cam, a);
+    } else if (g_wf_lane == 12 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc) <= kWfLdsLimit) {
+      const size_t lds = lane_lds_bytes(sc);
+      auto k = wf_trace_closest_refill<QUADS, TW>;
+      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, n)), dim3(tb), lds, stream, sc, cam, a);
+    } else if ((g_wf_lane == 10 || g_wf_lane == 11) && sc.bvh_code16 && sc.bvh_depth <= kLaneLdsDepth &&
+               lane16_lds_bytes(sc, g_wf_lane == 11) <= kWfLdsLimit) {
+      const size_t lds = lane16_lds_bytes(sc, g_wf_lane == 11);
+      auto k = g_wf_lane == 11 ? wf_trace_closest_bvh<false, QUADS, 11, TW> : wf_trace_closest_bvh<false, QUADS, 10, TW>;
+      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, n)), dim3(tb), lds, stream, sc, cam, a);
     } else if (g_wf_lane == 8 && lane4_ok(sc)) {
       const size_t lds = lane4_lds_bytes(sc);
       auto k = wf_trace_closest_bvh<false, QUADS, 8, TW>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, n)), dim3(kTraceBlock), lds, stream, sc, cam, a);
+      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, n)), dim3(tb), lds, stream, sc, cam, a);
     } else if (g_wf_lane == 6 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc, false) <= kWfLdsLimit) {
       const size_t lds = lane_lds_bytes(sc, false);
       auto k = wf_trace_closest_bvh<false, QUADS, 6, TW>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, n)), dim3(kTraceBlock), lds, stream, sc, cam, a);
+      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, n)), dim3(tb), lds, stream, sc, cam, a);
     } else if ((g_wf_lane == 7 || g_wf_lane == 9) && sc.bvh_depth <= kLaneLdsDepth &&
                lane_lds_bytes(sc) <= kWfLdsLimit) {
       const size_t lds = lane_lds_bytes(sc);
       auto k = g_wf_lane == 9 ? wf_trace_closest_bvh<false, QUADS, 9, TW> : wf_trace_closest_bvh<false, QUADS, 7, TW>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, n)), dim3(kTraceBlock), lds, stream, sc, cam, a);
+      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, n)), dim3(tb), lds, stream, sc, cam, a);
     } else if (g_wf_lane >= 5 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc) <= kWfLdsLimit) {
       const size_t lds = lane_lds_bytes(sc);
       auto k = wf_trace_closest_bvh<false, QUADS, 5, TW>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, n)), dim3(kTraceBlock), lds, stream, sc, cam, a);
+      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, n)), dim3(tb), lds, stream, sc, cam, a);
     } else if ((g_wf_lane == 7 || g_wf_lane == 9) && sc.bvh_depth <= kLaneLdsDepth) {
       auto k = wf_trace_closest_bvh<false, QUADS, 3, TW>;
-      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
+      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, n)), dim3(tb), 0, stream, sc, cam, a);
     } else if (g_wf_lane && g_wf_lane != 2 && sc.bvh_depth <= kLaneLdsDepth) {
       auto k = wf_trace_closest_bvh<false, QUADS, 2, TW>;
-      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
+      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, n)), dim3(tb), 0, stream, sc, cam, a);
     } else if (g_wf_lane) {
       auto k = wf_trace_closest_bvh<false, QUADS, 1, TW>;
-      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
+      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, n)), dim3(tb), 0, stream, sc, cam, a);
     } else {
       auto k = wf_trace_closest_bvh<false, QUADS, 0, TW>;
-      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
+      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, n)), dim3(tb), 0, stream, sc, cam, a);
     }
   } else if (primary) {
     const size_t lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, true);
     auto k = wf_trace_closest<true, true, QUADS, TW>;
     WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, n)), dim3(kTraceBlock), lds, stream, sc, cam, a);
+    WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, n)), dim3(tb), lds, stream, sc, cam, a);
   } else if (lds_ok) {
     const size_t lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, false);
     auto k = wf_trace_closest<true, false, QUADS, TW>;
     WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, n)), dim3(kTraceBlock), lds, stream, sc, cam, a);
+    WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, n)), dim3(tb), lds, stream, sc, cam, a);
   } else {
     auto k = wf_trace_closest<false, false, QUADS, TW>;
-    WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, n)), dim3(kTraceBlock), 0, stream, sc, cam, a);
+    WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, n)), dim3(tb), 0, stream, sc, cam, a);
   }
   return hipGetLastError();
 }
@@ -1539,15 +1835,16 @@ static hipError_t launch_closest(const DevScene& sc, const DevCamera& cam, const
 
 template <bool QUADS, int TW>
 static hipError_t launch_shadow_q(const DevScene& sc, const WfArgs& a, bool lds_ok, bool bvh, hipStream_t stream) {
+  const int tb = trace_block(a.n_shadow);
   if (bvh && g_wf_shadow_lb && sc.lb_cells) {
     const size_t lds = lb_lds_bytes(sc);
     if (lds <= kWfLdsLimit) {
       auto k = wf_trace_shadow_lb<QUADS, true, kLbWaves>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, a.n_shadow)), dim3(kTraceBlock), lds, stream, sc, a);
+      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, a.n_shadow)), dim3(tb), lds, stream, sc, a);
     } else {
       auto k = wf_trace_shadow_lb<QUADS, false, kLbWaves>;
-      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, a.n_shadow)), dim3(kTraceBlock), 0, stream, sc, a);
+      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, a.n_shadow)), dim3(tb), 0, stream, sc, a);
     }
   } else if (bvh) {
     if (g_wf_refill && (g_wf_lane == 7 || g_wf_lane == 9) && sc.bvh_depth <= kLaneLdsDepth &&
@@ -1555,49 +1852,49 @@ static hipError_t launch_shadow_q(const DevScene& sc, const WfArgs& a, bool lds_
       const size_t lds = lane_lds_bytes(sc);
       auto k = g_wf_lane == 9 ? wf_trace_shadow_refill<QUADS, 9, TW> : wf_trace_shadow_refill<QUADS, 7, TW>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, a.n_shadow)), dim3(kTraceBlock), lds, stream, sc, a);
+      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, a.n_shadow)), dim3(tb), lds, stream, sc, a);
     } else if (g_wf_lane == 8 && lane4_ok(sc)) {
       const size_t lds = lane4_lds_bytes(sc);
       auto k = wf_trace_shadow_bvh<QUADS, 8, TW>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, a.n_shadow)), dim3(kTraceBlock), lds, stream, sc, a);
+      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, a.n_shadow)), dim3(tb), lds, stream, sc, a);
     } else if (g_wf_lane == 6 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc, false) <= kWfLdsLimit) {
       const size_t lds = lane_lds_bytes(sc, false);
       auto k = wf_trace_shadow_bvh<QUADS, 6, TW>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, a.n_shadow)), dim3(kTraceBlock), lds, stream, sc, a);
+      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, a.n_shadow)), dim3(tb), lds, stream, sc, a);
     } else if ((g_wf_lane == 7 || g_wf_lane == 9) && sc.bvh_depth <= kLaneLdsDepth &&
                lane_lds_bytes(sc) <= kWfLdsLimit) {
       const size_t lds = lane_lds_bytes(sc);
       auto k = g_wf_lane == 9 ? wf_trace_shadow_bvh<QUADS, 9, TW> : wf_trace_shadow_bvh<QUADS, 7, TW>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, a.n_shadow)), dim3(kTraceBlock), lds, stream, sc, a);
+      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, a.n_shadow)), dim3(tb), lds, stream, sc, a);
     } else if (g_wf_lane >= 5 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc) <= kWfLdsLimit) {
       const size_t lds = lane_lds_bytes(sc);
       auto k = wf_trace_shadow_bvh<QUADS, 5, TW>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, a.n_shadow)), dim3(kTraceBlock), lds, stream, sc, a);
+      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, a.n_shadow)), dim3(tb), lds, stream, sc, a);
     } else if ((g_wf_lane == 7 || g_wf_lane == 9) && sc.bvh_depth <= kLaneLdsDepth) {
       auto k = wf_trace_shadow_bvh<QUADS, 3, TW>;
-      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, a.n_shadow)), dim3(kTraceBlock), 0, stream, sc, a);
+      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, a.n_shadow)), dim3(tb), 0, stream, sc, a);
     } else if (g_wf_lane && g_wf_lane != 2 && sc.bvh_depth <= kLaneLdsDepth) {
       auto k = wf_trace_shadow_bvh<QUADS, 2, TW>;
-      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, a.n_shadow)), dim3(kTraceBlock), 0, stream, sc, a);
+      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, a.n_shadow)), dim3(tb), 0, stream, sc, a);
     } else if (g_wf_lane) {
       auto k = wf_trace_shadow_bvh<QUADS, 1, TW>;
-      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, a.n_shadow)), dim3(kTraceBlock), 0, stream, sc, a);
+      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, a.n_shadow)), dim3(tb), 0, stream, sc, a);
     } else {
       auto k = wf_trace_shadow_bvh<QUADS, 0, TW>;
-      WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, a.n_shadow)), dim3(kTraceBlock), 0, stream, sc, a);
+      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, a.n_shadow)), dim3(tb), 0, stream, sc, a);
     }
   } else if (lds_ok) {
     const size_t lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, false);
     auto k = wf_trace_shadow<true, QUADS, TW>;
     WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, lds, a.n_shadow)), dim3(kTraceBlock), lds, stream, sc, a);
+    WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, a.n_shadow)), dim3(tb), lds, stream, sc, a);
   } else {
     auto k = wf_trace_shadow<false, QUADS, TW>;
-    WF_LAUNCH(k, dim3(occupancy_grid(k, kTraceBlock, 0, a.n_shadow)), dim3(kTraceBlock), 0, stream, sc, a);
+    WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, a.n_shadow)), dim3(tb), 0, stream, sc, a);
   }
   return hipGetLastError();
 }
@@ -1610,7 +1907,7 @@ static hipError_t launch_shadow_wf(const DevScene& sc, const WfArgs& a, bool lds
 hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool camera_mode, const double* d_in_rays,
                              unsigned n0, unsigned aa, unsigned max_depth, unsigned row_block, unsigned shard,
                              unsigned n_shards, double* d_out, hipStream_t stream, const std::string& signature,
-                             DevStats* stats, float* ms_kernel) {
+                             DevStats* stats, float* ms_kernel, bool solo) {
   if (max_depth + 2 > (unsigned)kMaxGen) return hipErrorInvalidValue;
   if (aa == 0 || aa > 16 || (aa & (aa - 1)) != 0 || (!camera_mode && aa != 1) || n0 % aa != 0)
     return hipErrorInvalidValue;
@@ -1644,10 +1941,21 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
   const bool gen_lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, false) <= kWfLdsLimit;
   last_bvh_ = bvh;
   const bool use_prim = camera_mode && (prim_lds || bvh) && sc.n_diag > 0;
+  // the closest-hit refill kernel (LANE 12) leaves prepare_computations to wf_prep
+  const bool split_prep = bvh && g_wf_lane == 12 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc) <= kWfLdsLimit;
   if (use_prim) {
     WF_LAUNCH(wf_prim_prep, dim3((sc.n_diag + 4 + 255) / 256), dim3(256), 0, stream, sc, cam, d_prim_);
     WF_CHECK(hipGetLastError());
   }
+  // Shadow traces of generation g depend only on closest(g), like closest(g+1):
+  // they run on the side stream, forked after closest(g) and joined before the
+  // combine pass (DESIGN.md "Shadow stream").
+  hipStream_t sh_stream = stream;
+  if (g_wf_shadow_stream == 2 || (g_wf_shadow_stream == 1 && solo)) {
+    WF_CHECK(ensure_side());
+    sh_stream = side_;
+  }
+  bool forked = false;
   if (ms_kernel) WF_CHECK(hipEventRecord(ev0_, stream));
   if (profiling_) ++pframes_;
   prof_rays_[0] = prof_rays_[1] = prof_rays_[2] = 0;
@@ -1688,6 +1996,7 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     a.camera_mode = camera_mode ? 1u : 0u;
     a.row_block = row_block; a.shard = shard; a.n_shards = n_shards;
     a.skip_shadow = skip_shadow ? 1u : 0u;
+    a.refill_min = (unsigned)g_wf_refill_min;
     // 1. closest hit
     const bool prim_launch = g == 0 && use_prim;
     const int ccls = prim_launch ? WF_PRIMARY : WF_CLOSEST;
@@ -1704,8 +2013,8 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
       }
     }
     WF_CHECK(pmark(stream, ccls, false));
-    // 2. prepare_computations + spawn (the BVH trace kernels do it themselves)
-    if (!bvh) {
+    // 2. prepare_computations + spawn (the BVH trace kernels do it themselves, except the refill one)
+    if (!bvh || (split_prep && !prim_launch)) {
       WF_CHECK(pmark(stream, WF_PREP, true));
       WF_LAUNCH(wf_prep, dim3(occupancy_grid(wf_prep, kWfBlock, 0, n)), dim3(kWfBlock), 0, stream, sc, cam, a);
       WF_CHECK(hipGetLastError());
@@ -1730,19 +2039,28 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     if (a.n_shadow) {
       a.disc_slot = WF_SHADOW;
       prof_rays_[WF_SHADOW] += a.n_shadow;
-      WF_CHECK(pmark(stream, WF_SHADOW, true));
-      switch (!bvh ? g_wf_trace_waves : g_tw_shadow) {
-        case 4: WF_CHECK(launch_shadow_wf<4>(sc, a, gen_lds, bvh, stream)); break;
-        case 5: WF_CHECK(launch_shadow_wf<5>(sc, a, gen_lds, bvh, stream)); break;
-        case 6: WF_CHECK(launch_shadow_wf<6>(sc, a, gen_lds, bvh, stream)); break;
-        default: WF_CHECK(launch_shadow_wf<8>(sc, a, gen_lds, bvh, stream)); break;
+      if (sh_stream != stream) {
+        WF_CHECK(hipEventRecord(fork_ev_[g], stream));
+        WF_CHECK(hipStreamWaitEvent(sh_stream, fork_ev_[g], 0));
+        forked = true;
       }
-      WF_CHECK(pmark(stream, WF_SHADOW, false));
+      WF_CHECK(pmark(sh_stream, WF_SHADOW, true));
+      switch (!bvh ? g_wf_trace_waves : g_tw_shadow) {
+        case 4: WF_CHECK(launch_shadow_wf<4>(sc, a, gen_lds, bvh, sh_stream)); break;
+        case 5: WF_CHECK(launch_shadow_wf<5>(sc, a, gen_lds, bvh, sh_stream)); break;
+        case 6: WF_CHECK(launch_shadow_wf<6>(sc, a, gen_lds, bvh, sh_stream)); break;
+        default: WF_CHECK(launch_shadow_wf<8>(sc, a, gen_lds, bvh, sh_stream)); break;
+      }
+      WF_CHECK(pmark(sh_stream, WF_SHADOW, false));
     }
     if (stats) {
       WF_LAUNCH(wf_count_kinds, dim3(occupancy_grid(wf_count_kinds, 256, 0, n)), dim3(256), 0, stream, a);
       WF_CHECK(hipGetLastError());
     }
+  }
+  if (forked) {  // join: the combine pass reads every generation's lighting terms
+    WF_CHECK(hipEventRecord(join_ev_, sh_stream));
+    WF_CHECK(hipStreamWaitEvent(stream, join_ev_, 0));
   }
   // 4. combine, deepest generation first
   for (int g = (int)last; g >= 0; --g) {

@@ -65,6 +65,9 @@ extern int g_wf_lane;         // tuning knob: 1 = per-lane BVH traversal for sec
 extern int g_wf_accel;        // tuning knob: 1 = BVH traversal (when no counters are requested), 0 = exhaustive
 extern int g_wf_shadow_lb;    // tuning knob: 1 = shadow rays through the light buffer when the scene has one
 extern int g_wf_refill;       // tuning knob: 1 = lane refill in the per-lane trace kernels
+extern int g_wf_shadow_stream;   // tuning knob: 1 = shadow traces on a second stream, overlapping the next generation
+extern int g_wf_adaptive_block;  // tuning knob: 1 = small trace launches spread over every CU (smaller blocks)
+extern int g_wf_refill_min;   // tuning knob: idle lanes that trigger a refill (closest-hit refill kernel)
 extern int g_wf_skip_shadow;  // tuning knob: 1 = the fast path leaves out shadow rays that cannot change the colour
 
 // Work counters of the trace kernels, one row per wave slot (wave id mod
@@ -144,6 +147,7 @@ struct WfArgs {
   unsigned out_cap;     // per-region capacity of the next generation's arrays
   unsigned* sh_cnt;
   unsigned sh_cap;      // per-region capacity of the shadow list
+  unsigned refill_min;  // lane refill: idle lanes that trigger a refill (wf_trace_closest_refill)
 };
 
 // Per-kernel-class timing of the last frame (profiling mode only).
@@ -167,6 +171,7 @@ class Wavefront {
     pmask_ = class_mask;
     if (on) { pn_ = 0; pframes_ = 0; }
   }
+  size_t profiled_frames() const { return pframes_; }
   // Per-class times averaged over the frames rendered since profiling was
   // enabled; rays / disc counts of the last frame (synchronises).
   hipError_t last_profile(WfProfile* out);
@@ -174,11 +179,12 @@ class Wavefront {
   // rays) into `out` (n0/aa*3 doubles, device; AA samples are averaged like
   // Color::average). Counts of a signature seen before are reused (fully
   // asynchronous); otherwise each generation is sized by a synchronous count
-  // read-back. stats (host) may be null.
+  // read-back. stats (host) may be null. `solo`: no other workspace renders
+  // concurrently (then the shadow traces take the side stream).
   hipError_t render(const DevScene& sc, const DevCamera& cam, bool camera_mode, const double* d_in_rays,
                     unsigned n0, unsigned aa, unsigned max_depth, unsigned row_block, unsigned shard,
                     unsigned n_shards, double* d_out, hipStream_t stream, const std::string& signature,
-                    DevStats* stats, float* ms_kernel);
+                    DevStats* stats, float* ms_kernel, bool solo = true);
 
  private:
   hipError_t ensure_gen(size_t g, size_t slots, size_t n_lights, size_t list_slots);
@@ -191,6 +197,13 @@ class Wavefront {
   PrimRec* d_prim_ = nullptr;
   size_t prim_cap_ = 0;
   hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
+  // shadow traces run on a second stream (DESIGN.md "Shadow stream"): fork
+  // event per generation (recorded after its closest-hit launch), one join
+  hipStream_t side_ = nullptr;
+  int side_dev_ = -1;
+  hipEvent_t fork_ev_[kMaxGen] = {};
+  hipEvent_t join_ev_ = nullptr;
+  hipError_t ensure_side();
   struct Counts {
     std::vector<unsigned> rays, shadows;
   };

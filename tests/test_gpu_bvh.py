@@ -213,20 +213,24 @@ def test_skipped_shadow_rays_bitwise(rt, neg_zero):
     assert full.to_numpy().tobytes() == exact.to_numpy().tobytes()
 
 
-@pytest.mark.parametrize("lane", [0, 1, 2, 5, 6, 7, 8, 9])
-def test_traversal_variants_bitwise(rt, lane):
+@pytest.mark.parametrize("lane,tw", [(0, 4), (1, 4), (2, 4), (5, 4), (6, 4), (7, 4), (8, 4), (9, 4), (10, 4), (10, 8), (11, 4), (12, 4)])
+def test_traversal_variants_bitwise(rt, lane, tw):
     """Every traversal variant (wave / per-lane with LDS or scratch stack /
     per-lane with the scene or the nodes staged in LDS / per-lane with leaves
-    batched across the wave, the default) gives the exhaustive frame. The
+    batched across the wave, the default / 16-bit child codes with the stack
+    top in a register, at 4 and 8 waves per SIMD / closest-hit lane refill with
+    the spawn in wf_prep) gives the exhaustive frame. The
     scenes above that do not fit in LDS (3000 spheres) run the batched-leaf
     variant with the scene in global memory."""
     w, cam, depth = _glass_cluster(rt, n=250, seed=21, inside=False)
     exact, _ = cam.render(w, depth, want_stats=True)
     rt._rtamd._tuning_set("lane", lane)
+    rt._rtamd._tuning_set("tw_closest", tw)
     try:
         fast, _ = cam.render(w, depth, want_stats=False)
     finally:
         rt._rtamd._tuning_set("lane", 7)
+        rt._rtamd._tuning_set("tw_closest", 4)
     assert fast.to_numpy().tobytes() == exact.to_numpy().tobytes()
 
 
@@ -243,3 +247,31 @@ def test_lane_refill_bitwise(rt, inside):
     finally:
         rt._rtamd._tuning_set("refill", 0)
     assert fast.to_numpy().tobytes() == exact.to_numpy().tobytes()
+
+
+@pytest.mark.parametrize("n_streams", [2, 10])
+def test_frames_in_flight_bitwise(rt, n_streams):
+    """Frames rendered concurrently on several streams (one workspace per
+    stream; with 10 streams, more than the pool's 8 workspaces, so workspaces
+    change hands in stream order) all equal the exhaustive frame, for the
+    whole frame and for an 8-way shard, with the shadow-stream fork/join and
+    small-launch block sizing on."""
+    import torch
+    from rtamd import scenes
+    w, cam, depth = scenes.c3(240, 136, n_spheres=600)
+    full, _ = cam.render(w, depth, want_stats=True)
+    full = full.to_numpy()
+    rows8 = [y for y in range(cam.vsize) if (y // 8) % 8 == 5]
+    streams = [torch.cuda.Stream() for _ in range(n_streams)]
+    frames = 3 * n_streams
+    bufs = [torch.full((cam.vsize, cam.hsize, 3), -1.0, dtype=torch.float64, device="cuda") for _ in range(frames)]
+    sh = [torch.full((len(rows8), cam.hsize, 3), -1.0, dtype=torch.float64, device="cuda") for _ in range(frames)]
+    torch.cuda.synchronize()
+    for f in range(frames):
+        st = streams[f % n_streams].cuda_stream
+        cam.render_shard_device(w, depth, 8, 0, 1, bufs[f].data_ptr(), st, False)
+        cam.render_shard_device(w, depth, 8, 5, 8, sh[f].data_ptr(), st, False)
+    torch.cuda.synchronize()
+    for f in range(frames):
+        assert bufs[f].cpu().numpy().tobytes() == full.tobytes(), f
+        assert sh[f].cpu().numpy().tobytes() == full[rows8].tobytes(), f

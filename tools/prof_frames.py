@@ -19,14 +19,27 @@ ap.add_argument("--width", type=int, default=1920)
 ap.add_argument("--height", type=int, default=1080)
 ap.add_argument("--spheres", type=int, default=1000)
 ap.add_argument("--exhaustive", action="store_true")
+ap.add_argument("--inflight", type=int, default=3, help="frames in flight (streams), as bench.py")
+ap.add_argument("--shard", default="0/1", help="render rank r of an n-way row split: r/n (dev)")
+ap.add_argument("--knob", action="append", default=[], help="tuning knob k=v (dev)")
 a = ap.parse_args()
+for kv in a.knob:
+    k, v = kv.split("=")
+    rtamd._rtamd._tuning_set(k, int(v))
 w, cam, depth = scenes.c3(a.width, a.height, a.spheres)
 w.upload(0)
 if a.exhaustive:
     rtamd._rtamd._tuning_set("accel", 0)
-buf = torch.empty((a.height, a.width, 3), dtype=torch.float64, device="cuda")
-s = torch.cuda.current_stream().cuda_stream
-for _ in range(a.frames):
-    cam.render_shard_device(w, depth, 8, 0, 1, buf.data_ptr(), s, False)
+r, n = (int(x) for x in a.shard.split("/"))
+rows = rtamd.shard_rows(a.height, 8, r, n)
+F = max(1, a.inflight)
+if F > 1:
+    rtamd._rtamd._tuning_set("shadow_stream", 0)  # as bench.py
+bufs = [torch.empty((rows, a.width, 3), dtype=torch.float64, device="cuda") for _ in range(F)]
+streams = [torch.cuda.Stream() for _ in range(F)] if F > 1 else [torch.cuda.current_stream()]
+torch.cuda.synchronize()
+for f in range(a.frames):
+    cam.render_shard_device(w, depth, 8, r, n, bufs[f % F].data_ptr(), streams[f % F].cuda_stream, False)
+buf = bufs[0]
 torch.cuda.synchronize()
 print("frames", a.frames, "checksum", float(buf.sum()))

@@ -1,0 +1,60 @@
+"""Per-GPU frame time of one shard of the bench workload at N = 1, 2, 4, 8
+(dev tool): renders rank r's interleaved row blocks of an N-way split on the
+one local GPU, so the render part of the multi-GPU scaling curve can be read
+without N GPUs (the RCCL gather is not included). Prints, per N, the mean
+frame time over the ranks and the worst rank, and the per-class breakdown of
+rank 0. Usage: shard_time.py [--frames K] [--knob k=v ...]"""
+import argparse
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "raytracer-challenge-rs_amd")]
+import torch  # noqa: E402
+
+import rtamd  # noqa: E402
+from rtamd import scenes  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--frames", type=int, default=20)
+ap.add_argument("--row-block", type=int, default=8)
+ap.add_argument("--knob", action="append", default=[])
+ap.add_argument("--ns", default="1,2,4,8")
+ap.add_argument("--inflight", type=int, default=3)
+a = ap.parse_args()
+for kv in a.knob:
+    k, v = kv.split("=")
+    rtamd._rtamd._tuning_set(k, int(v))
+w, cam, depth = scenes.c3()
+w.upload(0)
+H, W, B = cam.vsize, cam.hsize, a.row_block
+s = torch.cuda.current_stream().cuda_stream
+base = None
+for n in [int(x) for x in a.ns.split(",")]:
+    times = []
+    for r in range(n):
+        rows = rtamd.shard_rows(H, B, r, n)
+        F = max(1, a.inflight)
+        if F > 1:
+            rtamd._rtamd._tuning_set("shadow_stream", 0)  # as bench.py
+        bufs = [torch.empty((rows, W, 3), dtype=torch.float64, device="cuda") for _ in range(F)]
+        sts = [torch.cuda.Stream() for _ in range(F)] if F > 1 else [torch.cuda.current_stream()]
+        torch.cuda.synchronize()
+        for f in range(3 * F):
+            cam.render_shard_device(w, depth, B, r, n, bufs[f % F].data_ptr(), sts[f % F].cuda_stream, False)
+        torch.cuda.synchronize()
+        if r == 0:
+            rtamd._rtamd._wf_profile(w, 1, False)
+        t0 = time.perf_counter()
+        for f in range(a.frames):
+            cam.render_shard_device(w, depth, B, r, n, bufs[f % F].data_ptr(), sts[f % F].cuda_stream, False)
+        torch.cuda.synchronize()
+        times.append((time.perf_counter() - t0) / a.frames * 1e3)
+        if r == 0:
+            p = rtamd._rtamd._wf_profile(w, 0, True)
+            cls = " ".join(f"{c}={m:.3f}" for c, m in p["ms"].items())
+    mean, worst = sum(times) / n, max(times)
+    base = base or worst
+    print(f"N={n}: per-GPU frame mean {mean:.3f} ms, worst rank {worst:.3f} ms -> render speedup {base / worst:.2f}x"
+          f"  (rank 0 classes, profiled pass: {cls})", flush=True)
