@@ -7,7 +7,11 @@ of primary + reflection + refraction + shadow rays (each one a
 `World::intersect`, world.rs:71,101). With N GPUs (one process per GPU,
 launched by torch.distributed.run) the frame is split into interleaved 8-row
 blocks, each rank renders its rows into HBM, and the canvas is assembled on
-rank 0 with one RCCL gather (strong scaling: the frame is fixed).
+rank 0 with one RCCL gather (strong scaling: the frame is fixed). F frames
+are in flight (--inflight, default 3): consecutive frames render on F streams,
+each with its own library workspace, so one frame's short, latency-bound
+deep generations overlap the next frame's work; every frame is complete,
+gathered and assembled inside the timed region.
 
 The scene is uploaded before timing (inputs resident in HBM). The timed
 region holds exactly K steps bracketed by barrier + synchronize; the
@@ -15,8 +19,9 @@ reported time is the max over ranks.
 
 Printed JSON line (rank 0): metric/value/unit per BASELINE.json, plus
   roofline      f64 VALU roofline of the dominant trace-kernel class of the
-                wavefront pipeline; kernel time from HIP events the library
-                records on the launch stream inside the timed region
+                wavefront pipeline; kernel time from HIP events carried by its
+                launches in a serialized pass of the same K frames (one stream,
+                kernels alone on the GPU, as in the rocprofv3 kernel trace)
   cpu_baseline  the C oracle (a port of the reference algorithm) on a bounded
                 row sample on this host's cores (N=1, rank 0 only)
 """
@@ -60,8 +65,8 @@ SURVEY_OPS_SPHERE, SURVEY_OPS_PLANE, SURVEY_OPS_ROOTS = 57, 34, 6
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=30)
+    p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--width", type=int, default=1920)
     p.add_argument("--height", type=int, default=1080)
     p.add_argument("--spheres", type=int, default=1000)
@@ -190,11 +195,8 @@ def main():
     fa.flush()
     torch.cuda.synchronize()
 
-    # Timed region. The library times every launch of the dominant kernel class
-    # (secondary-ray closest-hit traversal) with start/stop events carried by the
-    # launch itself on the launch stream (hipExtLaunchKernel); the other classes
-    # run untimed here and are timed in the breakdown pass below.
-    rtamd._rtamd._wf_profile(world, (1 << (1 + WF_CLOSEST)) | 1, False)
+    # Timed region: K frames, F in flight, no profiling events.
+    rtamd._rtamd._wf_profile(world, 0, False)
     if n > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -207,15 +209,18 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    prof = rtamd._rtamd._wf_profile(world, 0, True)
-    # Breakdown pass (outside the timed region): the same K frames with every
-    # kernel class timed, for the per-class table.
+    # Serialized pass (outside the timed region): the same K frames one after the
+    # other on one stream, every launch carrying its own start/stop HIP events
+    # (hipExtLaunchKernel), for the roofline's per-launch kernel time and the
+    # per-class table. With frames in flight the timed region overlaps kernels of
+    # different frames, so a launch's duration there includes the CUs it waited
+    # for; here each kernel runs alone, as in the rocprofv3 kernel trace.
     rtamd._rtamd._wf_profile(world, 1, False)
     for _ in range(a.steps):
-        step()
-    fa.flush()
+        cam.render_shard_device(world, depth, B, rank, n, shard.data_ptr(), stream.cuda_stream, False)
     torch.cuda.synchronize()
     breakdown = rtamd._rtamd._wf_profile(world, 0, True)
+    prof = breakdown
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if n > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -257,7 +262,7 @@ def main():
 def roofline(prof, breakdown, W, H, a, n, ref_work, frame_ms):
     """f64 VALU roofline of the dominant trace-kernel class (its launches in
     one frame on rank 0). Its time comes from the launch-carried HIP events of
-    the timed region (`prof`); the per-class table from the breakdown pass."""
+    the serialized pass (`prof` = `breakdown`), like the per-class table."""
     nd, ng, npl = prof["n_diag"], prof["n_gen"], prof["n_planes"]
     per_sphere = {"primary": OPS_SPHERE_PRIMARY, "closest": OPS_SPHERE_DIAG, "shadow": OPS_SPHERE_DIAG}
 
@@ -276,10 +281,7 @@ def roofline(prof, breakdown, W, H, a, n, ref_work, frame_ms):
     for c in ("prep", "combine"):
         kernels[c] = {"ms_per_frame": round(breakdown["ms"][c], 4)}
     dom = max(("primary", "closest", "shadow"), key=lambda c: breakdown["ms"][c])
-    # the dominant class's time from the timed region (falls back to the breakdown
-    # pass if another class dominates this workload)
-    kernel_ms, ms_src = (prof["ms"][dom], "timed region") if prof["ms"][dom] > 0 else \
-        (breakdown["ms"][dom], "breakdown pass")
+    kernel_ms, ms_src = breakdown["ms"][dom], "serialized pass: launch-carried HIP events, one stream"
     if kernel_ms <= 0:  # megakernel variant selected (RTAMD_WAVES=1): no per-class events
         return {"bound": "valu_f64", "kernel": None, "achieved": None, "peak": PEAK_F64_VALU_TFLOPS,
                 "unit": "TFLOP/s", "frac": None, "traffic": None}

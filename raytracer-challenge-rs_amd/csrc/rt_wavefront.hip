@@ -927,6 +927,23 @@ __device__ __forceinline__ void lane_trace16(const BvhNode* nodes, const SphereD
   }
 }
 
+// Block-wide copy of n 16-B chunks from global memory into LDS with eight
+// loads in flight per thread (one load-wait-store per chunk left the staging
+// latency-bound: ~9K cycles per block for the C3 scene). Every thread of the
+// block calls it; the caller synchronises.
+__device__ __forceinline__ void stage_lds(uint4* dst, const uint4* src, int n) {
+  const int bd = (int)blockDim.x;
+  int i = (int)threadIdx.x;
+  for (; i + 7 * bd < n; i += 8 * bd) {
+    uint4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = src[i + k * bd];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dst[i + k * bd] = v[k];
+  }
+  for (; i < n; i += bd) dst[i] = src[i];
+}
+
 // LANE == 5: the block stages the hierarchy and the sphere records in LDS
 // (dynamic shared memory: [stack bvh_depth x kTraceBlock ints][nodes][spheres];
 // a lane pushes at most one entry per tree level).
@@ -966,10 +983,10 @@ __device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, int* static_
     SphereDiag* sdl = (SphereDiag*)((unsigned char*)nodes + (size_t)sc.n_bvh4 * sizeof(BvhNode4));
     const uint4* gn = (const uint4*)sc.bvh4;
     uint4* ln = (uint4*)nodes;
-    for (int i = threadIdx.x; i < sc.n_bvh4 * (int)(sizeof(BvhNode4) / 16); i += blockDim.x) ln[i] = gn[i];
+    stage_lds(ln, gn, sc.n_bvh4 * (int)(sizeof(BvhNode4) / 16));
     const uint4* gs = (const uint4*)sc.sph_diag;
     uint4* ls4 = (uint4*)sdl;
-    for (int i = threadIdx.x; i < sc.n_diag * (int)(sizeof(SphereDiag) / 16); i += blockDim.x) ls4[i] = gs[i];
+    stage_lds(ls4, gs, sc.n_diag * (int)(sizeof(SphereDiag) / 16));
     __syncthreads();
     ls.nodes4 = nodes;
     ls.sd = sdl;
@@ -990,12 +1007,12 @@ __device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, int* static_
     BvhNode* nodes = (BvhNode*)(dyn + lane16_stack_bytes(sc));
     const uint4* gn = (const uint4*)sc.bvh;
     uint4* ln = (uint4*)nodes;
-    for (int i = threadIdx.x; i < sc.n_bvh * (int)(sizeof(BvhNode) / 16); i += blockDim.x) ln[i] = gn[i];
+    stage_lds(ln, gn, sc.n_bvh * (int)(sizeof(BvhNode) / 16));
     if constexpr (LANE == 11) {
       SphereDiag* sdl = (SphereDiag*)((unsigned char*)nodes + (size_t)sc.n_bvh * sizeof(BvhNode));
       const uint4* gs = (const uint4*)sc.sph_diag;
       uint4* ls4 = (uint4*)sdl;
-      for (int i = threadIdx.x; i < sc.n_diag * (int)(sizeof(SphereDiag) / 16); i += blockDim.x) ls4[i] = gs[i];
+      stage_lds(ls4, gs, sc.n_diag * (int)(sizeof(SphereDiag) / 16));
       ls.sd = sdl;
     }
     __syncthreads();
@@ -1007,14 +1024,22 @@ __device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, int* static_
     const uint4* gn = (const uint4*)sc.bvh;
     uint4* ln = (uint4*)nodes;
     // LANE 9: chunk k of record i at k * n + i (node_chunks<true>)
-    for (int i = threadIdx.x; i < sc.n_bvh * (int)(sizeof(BvhNode) / 16); i += blockDim.x)
-      ln[LANE == 9 ? (i & 3) * sc.n_bvh + (i >> 2) : i] = gn[i];
+    if constexpr (LANE == 9) {
+      for (int i = threadIdx.x; i < sc.n_bvh * (int)(sizeof(BvhNode) / 16); i += blockDim.x)
+        ln[(i & 3) * sc.n_bvh + (i >> 2)] = gn[i];
+    } else {
+      stage_lds(ln, gn, sc.n_bvh * (int)(sizeof(BvhNode) / 16));
+    }
     if constexpr (LANE != 6) {
       SphereDiag* sd = (SphereDiag*)((unsigned char*)nodes + (size_t)sc.n_bvh * sizeof(BvhNode));
       const uint4* gs = (const uint4*)sc.sph_diag;
       uint4* ls4 = (uint4*)sd;
-      for (int i = threadIdx.x; i < sc.n_diag * (int)(sizeof(SphereDiag) / 16); i += blockDim.x)
-        ls4[LANE == 9 ? (i & 3) * sc.n_diag + (i >> 2) : i] = gs[i];
+      if constexpr (LANE == 9) {
+        for (int i = threadIdx.x; i < sc.n_diag * (int)(sizeof(SphereDiag) / 16); i += blockDim.x)
+          ls4[(i & 3) * sc.n_diag + (i >> 2)] = gs[i];
+      } else {
+        stage_lds(ls4, gs, sc.n_diag * (int)(sizeof(SphereDiag) / 16));
+      }
       ls.sd = sd;
     }
     __syncthreads();
@@ -1386,7 +1411,7 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow_lb(DevScene s
     const uint4* gs = (const uint4*)sc.sph_diag;
     uint4* ls4 = (uint4*)lane_dyn;
     const int n_rec = sc.n_diag * (int)(sizeof(SphereDiag) / 16);
-    for (int i = threadIdx.x; i < n_rec; i += blockDim.x) ls4[i] = gs[i];
+    stage_lds(ls4, gs, n_rec);
     float* ld = (float*)(lane_dyn + (size_t)sc.n_diag * sizeof(SphereDiag));
     for (int i = threadIdx.x; i < sc.n_lights * sc.n_diag; i += blockDim.x) ld[i] = sc.lb_delta[i];
     sd = (const SphereDiag*)lane_dyn;  // shard_prefix (or the barrier below) synchronises the block

@@ -6,8 +6,8 @@ of a shared canvas (camera.rs:157-172). Here the frame is split into blocks of
 rule as `rt_shard_rows` / `rt_render_shard_device`, include/rt_render.h), so
 dense and empty regions spread evenly. Each rank renders its rows into a
 device buffer padded to the largest shard; ONE gather (RCCL on GPUs, gloo in
-the CPU tests) brings the shards to rank 0, which un-interleaves them into the
-row-major canvas with one index_copy. No other exchange exists.
+the CPU tests) brings the shards to rank 0, into one contiguous buffer, which
+rank 0 un-interleaves into the row-major canvas with one index_select. No other exchange exists.
 """
 import torch
 import torch.distributed as dist
@@ -40,15 +40,19 @@ class FrameAssembler:
         self.shard = self.shards[0]
         self._pending = None  # (work, slot) of the last submitted, not yet completed frame
         if rank == 0:
-            self.gathered = [[torch.empty_like(self.shard) for _ in range(n_shards)] for _ in range(slots)]
+            # each slot's gather lands in ONE contiguous (n * max_rows, W, 3) buffer (the
+            # list handed to the gather is views of it), and the un-interleave is a single
+            # index_select through the inverse row map: canvas row y <- buffer row src[y]
+            self.gather_buf = [torch.empty((n_shards * self.max_rows, width, 3), dtype=dtype, device=device)
+                               for _ in range(slots)]
+            self.gathered = [[b[s * self.max_rows:(s + 1) * self.max_rows] for s in range(n_shards)]
+                             for b in self.gather_buf]
             self.canvas = torch.empty((height, width, 3), dtype=dtype, device=device)
-            src, dst = [], []
+            inv = [0] * height
             for s in range(n_shards):
-                rows_s = shard_row_ids(height, row_block, s, n_shards)
-                src += [s * self.max_rows + i for i in range(len(rows_s))]
-                dst += rows_s
-            self.src_idx = torch.tensor(src, device=device)
-            self.dst_idx = torch.tensor(dst, device=device)
+                for i, y in enumerate(shard_row_ids(height, row_block, s, n_shards)):
+                    inv[y] = s * self.max_rows + i
+            self.inv_idx = torch.tensor(inv, device=device)
 
     def slot(self, step):
         """Shard buffer frame `step` renders into."""
@@ -59,7 +63,7 @@ class FrameAssembler:
                            group=group, async_op=async_op)
 
     def _unweave(self, slot):
-        self.canvas.index_copy_(0, self.dst_idx, torch.cat(self.gathered[slot]).index_select(0, self.src_idx))
+        torch.index_select(self.gather_buf[slot], 0, self.inv_idx, out=self.canvas)
         return self.canvas
 
     def assemble(self, group=None):

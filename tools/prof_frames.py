@@ -19,7 +19,7 @@ ap.add_argument("--width", type=int, default=1920)
 ap.add_argument("--height", type=int, default=1080)
 ap.add_argument("--spheres", type=int, default=1000)
 ap.add_argument("--exhaustive", action="store_true")
-ap.add_argument("--inflight", type=int, default=3, help="frames in flight (streams), as bench.py")
+ap.add_argument("--inflight", type=int, default=1, help="frames in flight (streams); 1 = serialized, as bench.py's roofline pass")
 ap.add_argument("--shard", default="0/1", help="render rank r of an n-way row split: r/n (dev)")
 ap.add_argument("--knob", action="append", default=[], help="tuning knob k=v (dev)")
 a = ap.parse_args()
@@ -33,8 +33,7 @@ if a.exhaustive:
 r, n = (int(x) for x in a.shard.split("/"))
 rows = rtamd.shard_rows(a.height, 8, r, n)
 F = max(1, a.inflight)
-if F > 1:
-    rtamd._rtamd._tuning_set("shadow_stream", 0)  # as bench.py
+rtamd._rtamd._tuning_set("shadow_stream", 0)  # as bench.py (its serialized roofline pass: one stream)
 bufs = [torch.empty((rows, a.width, 3), dtype=torch.float64, device="cuda") for _ in range(F)]
 streams = [torch.cuda.Stream() for _ in range(F)] if F > 1 else [torch.cuda.current_stream()]
 torch.cuda.synchronize()

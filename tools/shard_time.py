@@ -22,6 +22,7 @@ ap.add_argument("--row-block", type=int, default=8)
 ap.add_argument("--knob", action="append", default=[])
 ap.add_argument("--ns", default="1,2,4,8")
 ap.add_argument("--inflight", type=int, default=3)
+ap.add_argument("--ranks", action="store_true", help="print every rank's time")
 a = ap.parse_args()
 for kv in a.knob:
     k, v = kv.split("=")
@@ -56,5 +57,7 @@ for n in [int(x) for x in a.ns.split(",")]:
             cls = " ".join(f"{c}={m:.3f}" for c, m in p["ms"].items())
     mean, worst = sum(times) / n, max(times)
     base = base or worst
+    if "--ranks" in sys.argv:
+        print("   per rank ms:", " ".join(f"{t:.3f}" for t in times))
     print(f"N={n}: per-GPU frame mean {mean:.3f} ms, worst rank {worst:.3f} ms -> render speedup {base / worst:.2f}x"
           f"  (rank 0 classes, profiled pass: {cls})", flush=True)
