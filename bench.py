@@ -72,10 +72,13 @@ def parse():
     p.add_argument("--spheres", type=int, default=1000)
     p.add_argument("--depth", type=int, default=5)
     p.add_argument("--row-block", type=int, default=8)
-    p.add_argument("--inflight", type=int, default=3,
+    p.add_argument("--inflight", type=int, default=4,
                    help="frames in flight: consecutive frames render on this many streams (own workspaces)")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget for the CPU baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--stream-kind", default="auto", choices=["auto", "cumask", "raw", "torch"],
+                   help="render streams: library-made with a hardware queue each (cumask), library-made plain "
+                        "(raw), torch; auto = cumask on 1 GPU, raw with N GPUs")
     p.add_argument("--knob", action="append", default=[], help="library tuning knob k=v (dev; see rt_api.cpp)")
     p.add_argument("--exhaustive", action="store_true",
                    help="disable the exact-culling BVH: every ray tests every shape (the reference's loop)")
@@ -143,20 +146,27 @@ def main():
     # interleaved row blocks + one RCCL gather per frame; two shard slots so that
     # frame s's gather overlaps frame s+1's render (rtamd.distributed.FrameAssembler)
     # F frames in flight: frame s renders on stream s % F (the library keeps one
-    # workspace per stream, so the renders overlap on the device) into shard
-    # slot s % (F + 1); the assembler (gather + un-interleave) runs on the
-    # current stream after that frame's render. A slot is rendered again only
-    # after the assembler has completed its previous frame (free_ev).
+    # workspace per stream, so the renders overlap on the device).
+    # - 1 GPU: into canvas slot s % F. The streams never wait on each other (stream
+    #   order alone protects a slot), so they are streams with a hardware queue each
+    #   (rtamd.render_stream(); any cross-stream wait on such a stream costs ~1 ms).
+    # - N GPUs: into shard slot s % (F + 1); the assembler (gather + un-interleave)
+    #   runs on the current stream after that frame's render, and a slot is rendered
+    #   again only after the assembler has completed its previous frame (free_ev).
+    #   The gather needs those cross-stream waits, so the render streams are plain.
     F = max(1, a.inflight)
-    fa = FrameAssembler(H, W, B, rank, n, dev, slots=F + 1 if F > 1 else 2)
+    fa = FrameAssembler(H, W, B, rank, n, dev, slots=F if n == 1 else (F + 1 if F > 1 else 2))
     assert len(fa.rows) == rtamd.shard_rows(H, B, rank, n)
     shard = fa.shard
     stream = torch.cuda.current_stream()
-    # frame s renders on rstreams[s % F]; rstreams[0] is the current stream. With frames
-    # in flight the library's shadow side stream is off (the frames are the concurrency,
-    # and every extra stream competes for the GPU's few hardware queues).
-    rstreams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(F - 1)]
-    if F > 1:
+    kind = a.stream_kind if a.stream_kind != "auto" else ("cumask" if n == 1 else "raw")
+    if F == 1:
+        rstreams = [stream]
+    elif kind == "torch":
+        rstreams = [torch.cuda.Stream(device=dev) for _ in range(F)]
+    else:
+        rstreams = [rtamd.render_stream(kind == "cumask") for _ in range(F)]
+    if F > 1:  # the frames are the concurrency: no shadow side stream
         rtamd._rtamd._tuning_set("shadow_stream", 0)
     free_ev = [None] * len(fa.shards)
     frame_no = [0]
@@ -164,13 +174,18 @@ def main():
     def step():
         s = frame_no[0]
         rs = rstreams[s % F]
+        if n == 1:
+            cam.render_shard_device(world, depth, B, rank, n, fa.slot(s).data_ptr(), rs.cuda_stream, False)
+            fa.submit(s)  # the shard buffer already is the row-major canvas
+            frame_no[0] = s + 1
+            return
         slot = s % len(fa.shards)
         if rs is not stream and free_ev[slot] is not None:
             rs.wait_event(free_ev[slot])
         cam.render_shard_device(world, depth, B, rank, n, fa.slot(s).data_ptr(), rs.cuda_stream, False)
         if rs is not stream:
             stream.wait_stream(rs)
-        fa.submit(s)  # n == 1: the shard buffer already is the row-major canvas
+        fa.submit(s)
         if F > 1 and s > 0:  # frame s-1 is complete once the current stream gets here
             ev = torch.cuda.Event()
             ev.record(stream)
@@ -249,6 +264,7 @@ def main():
                 "parallelism": (f"{n} GPUs, one process each: interleaved {B}-row blocks, RCCL gather to rank 0"
                                 if n > 1 else "1 GPU: wavefront pipeline") + f"; {F} frames in flight",
                 "frames_in_flight": F,
+                "render_streams": kind if F > 1 else "current",
             },
             "roofline": roofline(prof, breakdown, W, H, a, n, ref_work, elapsed / a.steps * 1e3),
         }

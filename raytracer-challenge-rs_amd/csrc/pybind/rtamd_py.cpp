@@ -38,6 +38,7 @@ static py::array_t<double> check_rays(py::array_t<double, py::array::c_style | p
 }
 
 extern "C" int rtamd_tuning_set(const char* key, int value);
+extern "C" int rtamd_stream_create(int cu_masked, void** out);
 extern "C" int rtamd_wf_profile(const rt_scene* s, int enable, double out[29]);
 
 PYBIND11_MODULE(_rtamd, m) {
@@ -399,4 +400,9 @@ PYBIND11_MODULE(_rtamd, m) {
     return d;
   }, py::arg("world"), py::arg("enable") = -1, py::arg("read") = true);
   m.def("_tuning_set", [](const std::string& k, int v) { check(rtamd_tuning_set(k.c_str(), v), "tuning"); });
+  m.def("_stream_create", [](bool cu_masked) {
+    void* st = nullptr;
+    check(rtamd_stream_create(cu_masked ? 1 : 0, &st), "stream");
+    return (uintptr_t)st;
+  });
 }

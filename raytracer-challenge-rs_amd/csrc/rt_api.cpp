@@ -359,6 +359,25 @@ int rtamd_tuning_set(const char* key, int value) {
   }
   return fail(RT_ERR_INVALID_ARGUMENT, "unknown tuning key");
 }
+// Development hook (not in the public ABI): a non-blocking stream on the
+// current device; cu_masked = 1 creates it through hipExtStreamCreateWithCUMask
+// with every CU enabled (the runtime gives such a stream a hardware queue of
+// its own instead of sharing one of the GPU_MAX_HW_QUEUES).
+int rtamd_stream_create(int cu_masked, void** out) {
+  if (!out) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
+  hipStream_t st = nullptr;
+  if (cu_masked) {
+    int dev = 0, n_cu = 0;
+    RT_HIP(hipGetDevice(&dev));
+    RT_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+    std::vector<uint32_t> mask((size_t)(n_cu + 31) / 32, 0xFFFFFFFFu);
+    RT_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
+  } else {
+    RT_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  }
+  *out = st;
+  return RT_OK;
+}
 int rt_abi_version(void) { return RT_ABI_VERSION; }
 
 int rt_device_count(void) {

@@ -37,3 +37,13 @@ from ._rtamd import RtError, EPSILON  # noqa: E402
 
 LIB_PATH = _os.path.join(_os.path.dirname(_here), "lib", "librtamd.so")
 MAX_RECURSION_DEPTH = 5  # reference world.rs:16
+
+
+def render_stream(dedicated_queue=True):
+    """A torch stream for rendering frames concurrently (frames in flight,
+    DESIGN.md §5.4): created by the library through
+    hipExtStreamCreateWithCUMask with every CU enabled, which gives it a
+    hardware queue of its own. Plain streams share the GPU's few hardware
+    queues (GPU_MAX_HW_QUEUES), and two frames whose streams share a queue
+    serialise. Lives as long as the process."""
+    return _torch.cuda.ExternalStream(_rtamd._stream_create(bool(dedicated_queue)))

@@ -21,7 +21,9 @@ ap.add_argument("--frames", type=int, default=20)
 ap.add_argument("--row-block", type=int, default=8)
 ap.add_argument("--knob", action="append", default=[])
 ap.add_argument("--ns", default="1,2,4,8")
-ap.add_argument("--inflight", type=int, default=3)
+ap.add_argument("--inflight", type=int, default=4)
+ap.add_argument("--streams", default="cumask", choices=["torch", "once", "raw", "cumask"],
+                help="torch: new torch streams per rank; once: torch streams made once; raw / cumask: library-made streams (cumask: hipExtStreamCreateWithCUMask), made once")
 ap.add_argument("--ranks", action="store_true", help="print every rank's time")
 a = ap.parse_args()
 for kv in a.knob:
@@ -32,6 +34,13 @@ w.upload(0)
 H, W, B = cam.vsize, cam.hsize, a.row_block
 s = torch.cuda.current_stream().cuda_stream
 base = None
+_F = max(1, a.inflight)
+if a.streams == "once":
+    _made = [torch.cuda.Stream() for _ in range(_F)]
+elif a.streams in ("raw", "cumask"):
+    _made = [torch.cuda.ExternalStream(rtamd._rtamd._stream_create(a.streams == "cumask")) for _ in range(_F)]
+else:
+    _made = None
 for n in [int(x) for x in a.ns.split(",")]:
     times = []
     for r in range(n):
@@ -40,7 +49,7 @@ for n in [int(x) for x in a.ns.split(",")]:
         if F > 1:
             rtamd._rtamd._tuning_set("shadow_stream", 0)  # as bench.py
         bufs = [torch.empty((rows, W, 3), dtype=torch.float64, device="cuda") for _ in range(F)]
-        sts = [torch.cuda.Stream() for _ in range(F)] if F > 1 else [torch.cuda.current_stream()]
+        sts = _made or ([torch.cuda.Stream() for _ in range(F)] if F > 1 else [torch.cuda.current_stream()])
         torch.cuda.synchronize()
         for f in range(3 * F):
             cam.render_shard_device(w, depth, B, r, n, bufs[f % F].data_ptr(), sts[f % F].cuda_stream, False)
