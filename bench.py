@@ -34,6 +34,13 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [REPO, os.path.join(REPO, "raytracer-challenge-rs_amd")]
 
+# Frames in flight render on several streams (--inflight): give the process
+# enough hardware queues that they do not share one (HIP's default is 4; the
+# current stream, the render streams and RCCL's stream each want their own).
+# Read by the HIP runtime at initialisation, so before torch is imported.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
 import torch  # noqa: E402  (load torch's HIP runtime first: see rtamd/__init__.py)
 import torch.distributed as dist  # noqa: E402
 
@@ -76,9 +83,8 @@ def parse():
                    help="frames in flight: consecutive frames render on this many streams (own workspaces)")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget for the CPU baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--stream-kind", default="auto", choices=["auto", "cumask", "raw", "torch"],
-                   help="render streams: library-made with a hardware queue each (cumask), library-made plain "
-                        "(raw), torch; auto = cumask on 1 GPU, raw with N GPUs")
+    p.add_argument("--stream-kind", default="raw", choices=["cumask", "raw", "torch"],
+                   help="render streams: library-made plain (raw), library-made CU-masked (cumask), torch")
     p.add_argument("--knob", action="append", default=[], help="library tuning knob k=v (dev; see rt_api.cpp)")
     p.add_argument("--exhaustive", action="store_true",
                    help="disable the exact-culling BVH: every ray tests every shape (the reference's loop)")
@@ -148,18 +154,19 @@ def main():
     # F frames in flight: frame s renders on stream s % F (the library keeps one
     # workspace per stream, so the renders overlap on the device).
     # - 1 GPU: into canvas slot s % F. The streams never wait on each other (stream
-    #   order alone protects a slot), so they are streams with a hardware queue each
-    #   (rtamd.render_stream(); any cross-stream wait on such a stream costs ~1 ms).
+    #   order alone protects a slot).
     # - N GPUs: into shard slot s % (F + 1); the assembler (gather + un-interleave)
     #   runs on the current stream after that frame's render, and a slot is rendered
     #   again only after the assembler has completed its previous frame (free_ev).
-    #   The gather needs those cross-stream waits, so the render streams are plain.
+    # The render streams are plain streams, each on its own hardware queue
+    # (GPU_MAX_HW_QUEUES above); CU-masked streams (--stream-kind cumask) also get
+    # their own queue, but any cross-stream wait on them costs ~1 ms.
     F = max(1, a.inflight)
     fa = FrameAssembler(H, W, B, rank, n, dev, slots=F if n == 1 else (F + 1 if F > 1 else 2))
     assert len(fa.rows) == rtamd.shard_rows(H, B, rank, n)
     shard = fa.shard
     stream = torch.cuda.current_stream()
-    kind = a.stream_kind if a.stream_kind != "auto" else ("cumask" if n == 1 else "raw")
+    kind = a.stream_kind
     if F == 1:
         rstreams = [stream]
     elif kind == "torch":
