@@ -8,7 +8,7 @@ of primary + reflection + refraction + shadow rays (each one a
 launched by torch.distributed.run) the frame is split into interleaved 8-row
 blocks, each rank renders its rows into HBM, and the canvas is assembled on
 rank 0 with one RCCL gather (strong scaling: the frame is fixed). F frames
-are in flight (--inflight, default 3): consecutive frames render on F streams,
+are in flight (--inflight, default 4 for C3): consecutive frames render on F streams,
 each with its own library workspace, so one frame's short, latency-bound
 deep generations overlap the next frame's work; every frame is complete,
 gathered and assembled inside the timed region.
@@ -50,6 +50,7 @@ from rtamd.distributed import FrameAssembler  # noqa: E402
 
 WF_CLOSEST = 1  # kernel class index (csrc/rt_wavefront.hpp WfClass)
 METRIC = "Mrays/s (primary+secondary) on 1920×1080/1000-sphere/depth-5; 1→8 GPU scaling"
+METRIC_C5 = "Mrays/s (primary+secondary) on 4096×4096/10000-shape/depth-8 (C5)"
 PEAK_F64_VALU_TFLOPS = 39.3  # 256 CU x 64 f64 lanes/clk x 2.4 GHz, non-fused add/mul (MI355X_MICROARCH.md)
 
 # Algorithmic f64 operations per unit of work (DESIGN.md "Roofline"): the
@@ -74,12 +75,15 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=30)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--width", type=int, default=1920)
-    p.add_argument("--height", type=int, default=1080)
-    p.add_argument("--spheres", type=int, default=1000)
-    p.add_argument("--depth", type=int, default=5)
+    p.add_argument("--config", default="c3", choices=["c3", "c5"],
+                   help="c3: the headline workload (default); c5: 4096x4096, 4 planes + 9996 spheres, 2 lights, "
+                        "depth 8 (SURVEY.md §8d C5; sizes below override)")
+    p.add_argument("--width", type=int, default=None)
+    p.add_argument("--height", type=int, default=None)
+    p.add_argument("--spheres", type=int, default=None)
+    p.add_argument("--depth", type=int, default=None)
     p.add_argument("--row-block", type=int, default=8)
-    p.add_argument("--inflight", type=int, default=4,
+    p.add_argument("--inflight", type=int, default=None,
                    help="frames in flight: consecutive frames render on this many streams (own workspaces)")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget for the CPU baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -142,8 +146,10 @@ def main():
     for kv in a.knob:
         k, v = kv.split("=")
         rtamd._rtamd._tuning_set(k, int(v))
-    world, cam, depth = scenes.c3(a.width, a.height, a.spheres)
-    if a.depth != depth:
+    dflt = {"c3": (1920, 1080, 1000), "c5": (4096, 4096, 9996)}[a.config]
+    a.width, a.height, a.spheres = a.width or dflt[0], a.height or dflt[1], a.spheres or dflt[2]
+    world, cam, depth = getattr(scenes, a.config)(a.width, a.height, a.spheres)
+    if a.depth is not None:
         depth = a.depth
     world.upload(local_rank)  # flatten + upload: outside the timed region
     if a.exhaustive:
@@ -161,7 +167,9 @@ def main():
     # The render streams are plain streams, each on its own hardware queue
     # (GPU_MAX_HW_QUEUES above); CU-masked streams (--stream-kind cumask) also get
     # their own queue, but any cross-stream wait on them costs ~1 ms.
-    F = max(1, a.inflight)
+    # default: 4 frames in flight for C3; one for C5, whose wavefront workspace
+    # (16.8 M primary rays, depth 8) takes tens of GB per frame
+    F = max(1, a.inflight if a.inflight is not None else (4 if a.config == "c3" else 1))
     fa = FrameAssembler(H, W, B, rank, n, dev, slots=F if n == 1 else (F + 1 if F > 1 else 2))
     assert len(fa.rows) == rtamd.shard_rows(H, B, rank, n)
     shard = fa.shard
@@ -251,7 +259,7 @@ def main():
     if rank == 0:
         value = rays_per_frame * a.steps / elapsed / 1e6
         out = {
-            "metric": METRIC,
+            "metric": METRIC if a.config == "c3" else METRIC_C5,
             "value": round(value, 3),
             "unit": "Mrays/s",
             "n_gpus": n,
@@ -264,8 +272,10 @@ def main():
             "dtype": "f64",
             "data": "synthetic",
             "config": {
-                "workload": f"c3: {W}x{H}, floor plane + {a.spheres} random spheres (splitmix64 seed 0x5EED0003), "
-                            f"1 light, reflect+refract depth {depth}",
+                "workload": (f"c3: {W}x{H}, floor plane + {a.spheres} random spheres (splitmix64 seed 0x5EED0003), "
+                             f"1 light, reflect+refract depth {depth}") if a.config == "c3" else
+                            (f"c5: {W}x{H}, 4 planes + {a.spheres} random spheres (splitmix64 seed 0x5EED0005), "
+                             f"2 lights, reflect+refract depth {depth}"),
                 "width": W, "height": H, "spheres": a.spheres, "depth": depth,
                 "rays_per_frame": int(rays_per_frame),
                 "parallelism": (f"{n} GPUs, one process each: interleaved {B}-row blocks, RCCL gather to rank 0"
@@ -310,13 +320,21 @@ def roofline(prof, breakdown, W, H, a, n, ref_work, frame_ms):
                 "unit": "TFLOP/s", "frac": None, "traffic": None}
     ops = class_ops(dom)
     achieved = ops / (kernel_ms * 1e-3) / 1e12
-    traffic, traffic_src = None, None
+    traffic, traffic_src, counters = None, None, None
     if os.path.exists(a.pmc_summary):
         try:
             pm = json.load(open(a.pmc_summary))
             if (pm.get("width"), pm.get("height"), pm.get("spheres"), pm.get("n_gpus"), pm.get("kernel_class"),
                     pm.get("traversal")) == (W, H, a.spheres, n, dom, "bvh" if prof["bvh"] else "exhaustive"):
                 traffic, traffic_src = pm.get("hbm_bytes_per_frame"), os.path.relpath(a.pmc_summary, REPO)
+                c = pm["per_frame"][dom]
+                # SQ_ACTIVE_INST_VALU counts quad-cycles summed over the SIMDs; GRBM_GUI_ACTIVE
+                # is summed over the 8 XCDs (MI355X: 256 CUs x 4 SIMDs)
+                simd_cycles = c["GRBM_GUI_ACTIVE"] / 8.0 * 1024.0
+                counters = {"valu_busy": round(4.0 * c["SQ_ACTIVE_INST_VALU"] / simd_cycles, 3),
+                            "f64_valu_insts_per_frame": c["SQ_INSTS_VALU_ADD_F64"] + c["SQ_INSTS_VALU_MUL_F64"]
+                            + c["SQ_INSTS_VALU_FMA_F64"] + c["SQ_INSTS_VALU_TRANS_F64"],
+                            "valu_insts_per_frame": c["SQ_INSTS_VALU"]}
         except Exception:
             pass
     return {
@@ -336,6 +354,7 @@ def roofline(prof, breakdown, W, H, a, n, ref_work, frame_ms):
         "traversal": "bvh" if prof["bvh"] else "exhaustive",
         "reference_work_tflops": round(ref_work / (frame_ms * 1e-3) / 1e12, 3),
         "traffic_source": traffic_src,
+        "pmc": counters,
         "kernels": kernels,
     }
 
