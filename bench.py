@@ -89,6 +89,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--stream-kind", default="raw", choices=["cumask", "raw", "torch"],
                    help="render streams: library-made plain (raw), library-made CU-masked (cumask), torch")
+    p.add_argument("--event-path", action="store_true",
+                   help="dev: on one GPU, run the N-GPU frame pipeline (shard slots, cross-stream events)")
     p.add_argument("--knob", action="append", default=[], help="library tuning knob k=v (dev; see rt_api.cpp)")
     p.add_argument("--exhaustive", action="store_true",
                    help="disable the exact-culling BVH: every ray tests every shape (the reference's loop)")
@@ -170,7 +172,8 @@ def main():
     # default: 4 frames in flight for C3; one for C5, whose wavefront workspace
     # (16.8 M primary rays, depth 8) takes tens of GB per frame
     F = max(1, a.inflight if a.inflight is not None else (4 if a.config == "c3" else 1))
-    fa = FrameAssembler(H, W, B, rank, n, dev, slots=F if n == 1 else (F + 1 if F > 1 else 2))
+    events = n > 1 or a.event_path
+    fa = FrameAssembler(H, W, B, rank, n, dev, slots=F if not events else (F + 1 if F > 1 else 2))
     assert len(fa.rows) == rtamd.shard_rows(H, B, rank, n)
     shard = fa.shard
     stream = torch.cuda.current_stream()
@@ -189,7 +192,7 @@ def main():
     def step():
         s = frame_no[0]
         rs = rstreams[s % F]
-        if n == 1:
+        if not events:
             cam.render_shard_device(world, depth, B, rank, n, fa.slot(s).data_ptr(), rs.cuda_stream, False)
             fa.submit(s)  # the shard buffer already is the row-major canvas
             frame_no[0] = s + 1
