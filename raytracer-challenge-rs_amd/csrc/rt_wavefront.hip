@@ -1402,19 +1402,32 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest_refill(DevSc
 __host__ __device__ inline size_t lb_lds_bytes(const DevScene& sc) {
   return (size_t)sc.n_diag * sizeof(SphereDiag) + (((size_t)sc.n_lights * sc.n_diag * sizeof(float) + 15) & ~(size_t)15);
 }
-template <bool QUADS, bool LDS, int TW>
+// LDS: 1 = sphere records and box distances staged in LDS, 2 = only the box
+// distances (scenes whose records do not fit, e.g. C5), 0 = neither.
+template <bool QUADS, int LDS, int TW>
 __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow_lb(DevScene sc, WfArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lane_dyn[];
   const SphereDiag* sd = sc.sph_diag;
   const float* delta = sc.lb_delta;
-  if constexpr (LDS) {
+  if constexpr (LDS == 1) {
     const uint4* gs = (const uint4*)sc.sph_diag;
     uint4* ls4 = (uint4*)lane_dyn;
     const int n_rec = sc.n_diag * (int)(sizeof(SphereDiag) / 16);
     stage_lds(ls4, gs, n_rec);
-    float* ld = (float*)(lane_dyn + (size_t)sc.n_diag * sizeof(SphereDiag));
-    for (int i = threadIdx.x; i < sc.n_lights * sc.n_diag; i += blockDim.x) ld[i] = sc.lb_delta[i];
     sd = (const SphereDiag*)lane_dyn;  // shard_prefix (or the barrier below) synchronises the block
+  }
+  if constexpr (LDS != 0) {
+    float* ld = (float*)(lane_dyn + (LDS == 1 ? (size_t)sc.n_diag * sizeof(SphereDiag) : 0));
+    const int nd = sc.n_lights * sc.n_diag, bd = (int)blockDim.x;
+    int i = (int)threadIdx.x;
+    for (; i + 7 * bd < nd; i += 8 * bd) {  // eight loads in flight per thread
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = sc.lb_delta[i + k * bd];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) ld[i + k * bd] = v[k];
+    }
+    for (; i < nd; i += bd) ld[i] = sc.lb_delta[i];
     delta = ld;
   }
   __shared__ unsigned s_pre[kShards + 1];
@@ -1863,12 +1876,17 @@ static hipError_t launch_shadow_q(const DevScene& sc, const WfArgs& a, bool lds_
   const int tb = trace_block(a.n_shadow);
   if (bvh && g_wf_shadow_lb && sc.lb_cells) {
     const size_t lds = lb_lds_bytes(sc);
+    const size_t lds_d = lb_lds_bytes(sc) - (size_t)sc.n_diag * sizeof(SphereDiag);  // the distances alone
     if (lds <= kWfLdsLimit) {
-      auto k = wf_trace_shadow_lb<QUADS, true, kLbWaves>;
+      auto k = wf_trace_shadow_lb<QUADS, 1, kLbWaves>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, a.n_shadow)), dim3(tb), lds, stream, sc, a);
+    } else if (lds_d <= kWfLdsLimit) {
+      auto k = wf_trace_shadow_lb<QUADS, 2, kLbWaves>;
+      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_d));
+      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds_d, a.n_shadow)), dim3(tb), lds_d, stream, sc, a);
     } else {
-      auto k = wf_trace_shadow_lb<QUADS, false, kLbWaves>;
+      auto k = wf_trace_shadow_lb<QUADS, 0, kLbWaves>;
       WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, a.n_shadow)), dim3(tb), 0, stream, sc, a);
     }
   } else if (bvh) {
