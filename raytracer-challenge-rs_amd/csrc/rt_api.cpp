@@ -304,7 +304,8 @@ int rtamd_tuning_set(const char* key, int value) {
   }
   if (key && std::strcmp(key, "lane") == 0) {
     rtamd::g_wf_lane = value;  // 0 = wave traversal, 1 = per-lane (LDS stack when it fits), 2 = per-lane, scratch
-                               // stack, 5 = per-lane with the scene in LDS when it fits (default)
+                               // stack, 5 = per-lane with the scene in LDS when it fits, 7 = 5 with leaves batched
+                               // across the wave, 14 = 7 over the pair node layout (default); see rt_wavefront.hip
     return RT_OK;
   }
   if (key && std::strcmp(key, "lb_res") == 0) {

@@ -27,7 +27,9 @@ constexpr int kTraceBlock = 1024;  // trace kernels: 16 waves, one LDS image per
 // allocator): 8 = two 1024-thread blocks per CU (<= 64 VGPRs), 4 = one.
 int g_wf_trace_waves = 8;  // tuning knob (rtamd_tuning_set("wf_waves", n))
 int g_wf_accel = 1;        // 1 = BVH traversal when counters are not requested, 0 = exhaustive always
-int g_wf_lane = 7;  // secondary / shadow rays: 7 = per-lane with leaves batched across the wave, scene + stack
+int g_wf_lane = 14;  // secondary rays: 14 = 7 over the pair layout (lane_trace_pair, packed binary32 FMAs);
+                    // shadow rays without a light buffer and scenes that do not fit in LDS take 7's path.
+                    // 7 = per-lane with leaves batched across the wave, scene + stack
                     // in LDS (when they fit; else 3 = the same with only the stack in LDS), 5 = per-lane, scene
                     // + stack in LDS, 6 = nodes + stack in LDS, 1 = per-lane with an LDS (or scratch) stack,
                     // 0 = wave (packet) traversal
@@ -927,6 +929,109 @@ __device__ __forceinline__ void lane_trace16(const BvhNode* nodes, const SphereD
   }
 }
 
+// Per-lane traversal over the pair layout (LANE == 14): the block's LDS copy
+// of each binary node stores, per axis, the two children's lower bounds as
+// one 8-B pair and their upper bounds as the next pair (lo0 lo1 hi0 hi1 per
+// axis, then the child codes). Which face a ray enters on an axis follows the
+// sign of its direction there, so each lane computes once the byte offsets of
+// its entry and exit pairs and loads them directly: one packed binary32 FMA
+// gives both children's entry (or exit) distances on an axis, and no per-axis
+// min/max is needed to tell entry from exit. The entry and exit values are the
+// ones lane_trace computes (entry = fma(entry face, inv, -on), exit =
+// fma(exit face, inv, -of), where lane_trace's min/max picks exactly them), so
+// the culling and the visit order are the same bit for bit. Leaves are
+// batched across the wave as in lane_trace<..., WW>.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+template <bool SHADOW>
+__device__ __forceinline__ void lane_trace_pair(const unsigned char* nodes, const SphereDiag* sd, const float* M,
+                                                bool has_bvh, V3 o, V3 d, double t_shadow, Hit& h, unsigned& n_disc,
+                                                unsigned& n_tests, unsigned& n_boxes, int* lds) {
+  float inv[3], on[3], of[3];
+  int ent[3], ext[3];
+  {
+    const double oa[3] = {o.x, o.y, o.z}, da[3] = {d.x, d.y, d.z};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      bool neg = false;
+      if (fabs(da[a]) >= 0x1p-60 && fabs(oa[a]) <= 0x1p60 && M[a] <= 0x1p60f) {  // as slab_ray; NaN fails
+        const double iv = 1.0 / da[a];
+        const double oinv = oa[a] * iv;
+        const double delta = 0x1p-20 * fabs(iv) * ((double)M[a] + fabs(oa[a]));
+        inv[a] = (float)iv;
+        on[a] = (float)(oinv + delta);
+        of[a] = (float)(oinv - delta);
+        neg = !(iv >= 0.0);
+      } else {
+        inv[a] = 0.0f;
+        on[a] = INFINITY;
+        of[a] = -INFINITY;
+      }
+      ent[a] = 16 * a + (neg ? 8 : 0);
+      ext[a] = ent[a] ^ 8;
+    }
+  }
+  // keep the six offsets in registers (the compiler would otherwise recompute
+  // the exit offsets in every visit)
+#pragma unroll
+  for (int a = 0; a < 3; ++a) asm volatile("" : "+v"(ent[a]), "+v"(ext[a]));
+  float t_hi = f32_up(SHADOW ? t_shadow : h.t);
+  auto stk = [&](int k) -> int& { return lds[k * kTraceBlock]; };
+  int sp = 0;
+  auto pop = [&]() { return sp > 0 ? stk(--sp) : kBvhEmpty; };
+  int e = (SHADOW && h.key >= 0 && h.t < t_shadow) || !has_bvh ? kBvhEmpty : 0;
+  auto visit = [&]() {
+    const unsigned char* nb = nodes + (size_t)e * 64;
+    const f32x2 ex = *(const f32x2*)(nb + ent[0]), ey = *(const f32x2*)(nb + ent[1]), ez = *(const f32x2*)(nb + ent[2]);
+    const f32x2 xx = *(const f32x2*)(nb + ext[0]), xy = *(const f32x2*)(nb + ext[1]), xz = *(const f32x2*)(nb + ext[2]);
+    const int2 cc = *(const int2*)(nb + 48);
+    const f32x2 tx0 = __builtin_elementwise_fma(ex, (f32x2)(inv[0]), (f32x2)(-on[0]));
+    const f32x2 ty0 = __builtin_elementwise_fma(ey, (f32x2)(inv[1]), (f32x2)(-on[1]));
+    const f32x2 tz0 = __builtin_elementwise_fma(ez, (f32x2)(inv[2]), (f32x2)(-on[2]));
+    const f32x2 tx1 = __builtin_elementwise_fma(xx, (f32x2)(inv[0]), (f32x2)(-of[0]));
+    const f32x2 ty1 = __builtin_elementwise_fma(xy, (f32x2)(inv[1]), (f32x2)(-of[1]));
+    const f32x2 tz1 = __builtin_elementwise_fma(xz, (f32x2)(inv[2]), (f32x2)(-of[2]));
+    const float t0 = fmaxf(fmaxf(tx0.x, ty0.x), fmaxf(tz0.x, 0.0f));
+    const float t1 = fmaxf(fmaxf(tx0.y, ty0.y), fmaxf(tz0.y, 0.0f));
+    const float u0 = fminf(fminf(tx1.x, ty1.x), fminf(tz1.x, t_hi));
+    const float u1 = fminf(fminf(tx1.y, ty1.y), fminf(tz1.y, t_hi));
+    const bool h0 = t0 <= u0;
+    const bool h1 = (t1 <= u1) & (cc.y != kBvhEmpty);
+    n_boxes += 2;
+    if (h0 && h1) {
+      const bool flip = t1 < t0;
+      stk(sp++) = flip ? cc.x : cc.y;
+      e = flip ? cc.y : cc.x;
+    } else {
+      e = h0 ? cc.x : h1 ? cc.y : pop();
+    }
+  };
+  auto leaf = [&](int code_e) {
+    const int code = -(code_e + 1);
+    const int first = code >> 7, cnt = code & 127;
+    for (int k = first; k < first + cnt; ++k) leaf_sphere_test<SHADOW, false>(sd, 0, k, o, d, h, n_disc);
+    n_tests += (unsigned)cnt;
+    if constexpr (SHADOW) {
+      return h.key >= 0 && h.t < t_shadow;
+    } else {
+      t_hi = f32_up(h.t);
+      return false;
+    }
+  };
+  int pl = kBvhEmpty;
+  for (;;) {
+    for (;;) {
+      if (e < 0 && e != kBvhEmpty && pl == kBvhEmpty) { pl = e; e = pop(); }
+      if (!__any(e >= 0 && pl == kBvhEmpty)) break;
+      if (e >= 0) visit();  // lanes holding a leaf keep going (speculative)
+    }
+    if (!__any(pl != kBvhEmpty)) break;
+    if (pl != kBvhEmpty) {
+      if (leaf(pl)) { e = kBvhEmpty; sp = 0; }  // shadowed: done
+      pl = kBvhEmpty;
+    }
+  }
+}
+
 // Block-wide copy of n 16-B chunks from global memory into LDS with eight
 // loads in flight per thread (one load-wait-store per chunk left the staging
 // latency-bound: ~9K cycles per block for the C3 scene). Every thread of the
@@ -1018,6 +1123,33 @@ __device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, int* static_
     __syncthreads();
     ls.nodes = nodes;
     ls.stack16 = stack + threadIdx.x;
+  } else if constexpr (LANE == 14) {  // pair layout (lane_trace_pair) + sphere records
+    int* stack = (int*)dyn;
+    unsigned char* nodes = dyn + lane_stack_bytes(sc.bvh_depth);
+    for (int i = threadIdx.x; i < sc.n_bvh; i += blockDim.x) {
+      const BvhNode& g = sc.bvh[i];
+      float* q = (float*)(nodes + (size_t)i * 64);
+      for (int a = 0; a < 3; ++a) {
+        q[4 * a] = g.lo[0][a]; q[4 * a + 1] = g.lo[1][a]; q[4 * a + 2] = g.hi[0][a]; q[4 * a + 3] = g.hi[1][a];
+      }
+      int* c = (int*)(q + 12);
+      c[0] = g.child[0]; c[1] = g.child[1]; c[2] = g.axis; c[3] = 0;
+    }
+    SphereDiag* sdl = (SphereDiag*)(nodes + (size_t)sc.n_bvh * sizeof(BvhNode));
+    stage_lds((uint4*)sdl, (const uint4*)sc.sph_diag, sc.n_diag * (int)(sizeof(SphereDiag) / 16));
+    __syncthreads();
+    ls.nodes = (const BvhNode*)nodes;  // pair layout: read only by lane_trace_pair
+    ls.sd = sdl;
+    ls.stack = stack + threadIdx.x;
+    for (int a = 0; a < 3; ++a) {  // from the hierarchy in global memory (binary layout)
+      float m = 0.0f;
+      if (sc.n_bvh > 0) {
+        const BvhNode& r = sc.bvh[0];
+        m = fmaxf(fmaxf(fabsf(r.lo[0][a]), fabsf(r.hi[0][a])), fmaxf(fabsf(r.lo[1][a]), fabsf(r.hi[1][a])));
+      }
+      ls.M[a] = m;
+    }
+    return ls;
   } else if constexpr (LANE >= 5) {  // 6: the sphere records stay in global memory
     int* stack = (int*)dyn;
     BvhNode* nodes = (BvhNode*)(dyn + lane_stack_bytes(sc.bvh_depth));
@@ -1094,7 +1226,11 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest_bvh(DevScene
     hit_init(h);
     if (valid) {
       wf_ray(a, cam, slot, o, d);
-      if constexpr ((LANE == 10 || LANE == 11) && !PRIMARY) {
+      if constexpr (LANE == 14 && !PRIMARY) {
+        trace_rest<false, QUADS>(sc, o, d, h, n_disc);  // planes first: an early nearest hit tightens the culling
+        lane_trace_pair<false>((const unsigned char*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, n_disc,
+                               n_tests, n_boxes, ls.stack);
+      } else if constexpr ((LANE == 10 || LANE == 11) && !PRIMARY) {
         trace_rest<false, QUADS>(sc, o, d, h, n_disc);  // planes first: an early nearest hit tightens the culling
         lane_trace16<false>(ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, n_disc, n_tests, n_boxes, ls.stack16);
       } else if constexpr (LANE == 8 && !PRIMARY) {
@@ -1803,6 +1939,11 @@ static hipError_t launch_closest_q(const DevScene& sc, const DevCamera& cam, con
     if (primary) {
       auto k = wf_trace_closest_bvh<true, QUADS, 0, TW>;
       WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, n)), dim3(tb), 0, stream, sc, cam, a);
+    } else if (g_wf_lane == 14 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc) <= kWfLdsLimit) {
+      const size_t lds = lane_lds_bytes(sc);
+      auto k = wf_trace_closest_bvh<false, QUADS, 14, TW>;
+      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, n)), dim3(tb), lds, stream, sc, cam, a);
     } else if (g_wf_lane == 12 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc) <= kWfLdsLimit) {
       const size_t lds = lane_lds_bytes(sc);
       auto k = wf_trace_closest_refill<QUADS, TW>;
@@ -1824,7 +1965,7 @@ static hipError_t launch_closest_q(const DevScene& sc, const DevCamera& cam, con
       auto k = wf_trace_closest_bvh<false, QUADS, 6, TW>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, n)), dim3(tb), lds, stream, sc, cam, a);
-    } else if ((g_wf_lane == 7 || g_wf_lane == 9) && sc.bvh_depth <= kLaneLdsDepth &&
+    } else if ((g_wf_lane == 7 || g_wf_lane == 9 || g_wf_lane == 14) && sc.bvh_depth <= kLaneLdsDepth &&
                lane_lds_bytes(sc) <= kWfLdsLimit) {
       const size_t lds = lane_lds_bytes(sc);
       auto k = g_wf_lane == 9 ? wf_trace_closest_bvh<false, QUADS, 9, TW> : wf_trace_closest_bvh<false, QUADS, 7, TW>;
@@ -1835,7 +1976,7 @@ static hipError_t launch_closest_q(const DevScene& sc, const DevCamera& cam, con
       auto k = wf_trace_closest_bvh<false, QUADS, 5, TW>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, n)), dim3(tb), lds, stream, sc, cam, a);
-    } else if ((g_wf_lane == 7 || g_wf_lane == 9) && sc.bvh_depth <= kLaneLdsDepth) {
+    } else if ((g_wf_lane == 7 || g_wf_lane == 9 || g_wf_lane == 14) && sc.bvh_depth <= kLaneLdsDepth) {
       auto k = wf_trace_closest_bvh<false, QUADS, 3, TW>;
       WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, n)), dim3(tb), 0, stream, sc, cam, a);
     } else if (g_wf_lane && g_wf_lane != 2 && sc.bvh_depth <= kLaneLdsDepth) {
@@ -1890,7 +2031,7 @@ static hipError_t launch_shadow_q(const DevScene& sc, const WfArgs& a, bool lds_
       WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, a.n_shadow)), dim3(tb), 0, stream, sc, a);
     }
   } else if (bvh) {
-    if (g_wf_refill && (g_wf_lane == 7 || g_wf_lane == 9) && sc.bvh_depth <= kLaneLdsDepth &&
+    if (g_wf_refill && (g_wf_lane == 7 || g_wf_lane == 9 || g_wf_lane == 14) && sc.bvh_depth <= kLaneLdsDepth &&
         lane_lds_bytes(sc) <= kWfLdsLimit) {
       const size_t lds = lane_lds_bytes(sc);
       auto k = g_wf_lane == 9 ? wf_trace_shadow_refill<QUADS, 9, TW> : wf_trace_shadow_refill<QUADS, 7, TW>;
@@ -1906,7 +2047,7 @@ static hipError_t launch_shadow_q(const DevScene& sc, const WfArgs& a, bool lds_
       auto k = wf_trace_shadow_bvh<QUADS, 6, TW>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, a.n_shadow)), dim3(tb), lds, stream, sc, a);
-    } else if ((g_wf_lane == 7 || g_wf_lane == 9) && sc.bvh_depth <= kLaneLdsDepth &&
+    } else if ((g_wf_lane == 7 || g_wf_lane == 9 || g_wf_lane == 14) && sc.bvh_depth <= kLaneLdsDepth &&
                lane_lds_bytes(sc) <= kWfLdsLimit) {
       const size_t lds = lane_lds_bytes(sc);
       auto k = g_wf_lane == 9 ? wf_trace_shadow_bvh<QUADS, 9, TW> : wf_trace_shadow_bvh<QUADS, 7, TW>;
@@ -1917,7 +2058,7 @@ static hipError_t launch_shadow_q(const DevScene& sc, const WfArgs& a, bool lds_
       auto k = wf_trace_shadow_bvh<QUADS, 5, TW>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, a.n_shadow)), dim3(tb), lds, stream, sc, a);
-    } else if ((g_wf_lane == 7 || g_wf_lane == 9) && sc.bvh_depth <= kLaneLdsDepth) {
+    } else if ((g_wf_lane == 7 || g_wf_lane == 9 || g_wf_lane == 14) && sc.bvh_depth <= kLaneLdsDepth) {
       auto k = wf_trace_shadow_bvh<QUADS, 3, TW>;
       WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, a.n_shadow)), dim3(tb), 0, stream, sc, a);
     } else if (g_wf_lane && g_wf_lane != 2 && sc.bvh_depth <= kLaneLdsDepth) {

@@ -213,7 +213,7 @@ def test_skipped_shadow_rays_bitwise(rt, neg_zero):
     assert full.to_numpy().tobytes() == exact.to_numpy().tobytes()
 
 
-@pytest.mark.parametrize("lane,tw", [(0, 4), (1, 4), (2, 4), (5, 4), (6, 4), (7, 4), (8, 4), (9, 4), (10, 4), (10, 8), (11, 4), (12, 4)])
+@pytest.mark.parametrize("lane,tw", [(0, 4), (1, 4), (2, 4), (5, 4), (6, 4), (7, 4), (8, 4), (9, 4), (10, 4), (10, 8), (11, 4), (12, 4), (14, 4)])
 def test_traversal_variants_bitwise(rt, lane, tw):
     """Every traversal variant (wave / per-lane with LDS or scratch stack /
     per-lane with the scene or the nodes staged in LDS / per-lane with leaves
@@ -229,7 +229,7 @@ def test_traversal_variants_bitwise(rt, lane, tw):
     try:
         fast, _ = cam.render(w, depth, want_stats=False)
     finally:
-        rt._rtamd._tuning_set("lane", 7)
+        rt._rtamd._tuning_set("lane", 14)
         rt._rtamd._tuning_set("tw_closest", 4)
     assert fast.to_numpy().tobytes() == exact.to_numpy().tobytes()
 
