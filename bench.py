@@ -89,6 +89,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--stream-kind", default="raw", choices=["cumask", "raw", "torch"],
                    help="render streams: library-made plain (raw), library-made CU-masked (cumask), torch")
+    p.add_argument("--verify", action="store_true",
+                   help="dev: check the last assembled frame against a one-GPU render of the whole frame")
+    p.add_argument("--dist-backend", default="nccl", help="dev: torch.distributed backend (nccl = RCCL)")
     p.add_argument("--event-path", action="store_true",
                    help="dev: on one GPU, run the N-GPU frame pipeline (shard slots, cross-stream events)")
     p.add_argument("--knob", action="append", default=[], help="library tuning knob k=v (dev; see rt_api.cpp)")
@@ -143,7 +146,10 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if n > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:  # dev rehearsal of the N-rank pipeline, e.g. 2 ranks sharing one GPU
+            dist.init_process_group(a.dist_backend)
 
     for kv in a.knob:
         k, v = kv.split("=")
@@ -236,7 +242,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
-    fa.flush()  # the last frame's gather + un-interleave are inside the timed region
+    last = fa.flush()  # the last frame's gather + un-interleave are inside the timed region
     torch.cuda.synchronize()
     if n > 1:
         dist.barrier()
@@ -254,6 +260,14 @@ def main():
     torch.cuda.synchronize()
     breakdown = rtamd._rtamd._wf_profile(world, 0, True)
     prof = breakdown
+    if a.verify and rank == 0:  # dev: the assembled last frame equals a one-GPU render of the whole frame
+        whole = torch.empty((H, W, 3), dtype=torch.float64, device=dev)
+        cam.render_shard_device(world, depth, B, 0, 1, whole.data_ptr(), stream.cuda_stream, False)
+        torch.cuda.synchronize()
+        same = last is not None and bool(torch.equal(last, whole))
+        print(f"verify: assembled frame {'==' if same else '!='} whole-frame render", file=sys.stderr, flush=True)
+        if not same:
+            raise SystemExit("verify failed: the assembled frame differs from the whole-frame render")
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if n > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
