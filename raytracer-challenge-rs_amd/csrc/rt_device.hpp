@@ -425,13 +425,15 @@ __device__ __forceinline__ V3 pattern_color(const ShadeRec& s, V3 world_point) {
 }
 
 // Material::lighting (material.rs:38-82)
+// `lightv` = (light.position - point).normalize(), which the caller may
+// already hold: the shadow ray from `point` to the light has exactly that
+// direction (same operands, same operations), so the shadow trace passes it.
 __device__ __forceinline__ V3 lighting(const ShadeRec& m, cLightRec L, V3 point, V3 eyev, V3 normal,
-                                       bool in_shadow) {
+                                       bool in_shadow, V3 lightv) {
   const V3 color = m.pattern_kind >= 0 ? pattern_color(m, point)
                                        : v3(m.color[0], m.color[1], m.color[2]);
   const V3 intensity = v3(L->intensity[0], L->intensity[1], L->intensity[2]);
   const V3 effective_color = vmul(color, intensity);
-  const V3 lightv = vnormalize(vsub(v3(L->pos[0], L->pos[1], L->pos[2]), point));
   const V3 ambient = vscale(effective_color, m.ambient);
   if (in_shadow) return ambient;
   const double light_dot_normal = vdot(lightv, normal);
@@ -446,6 +448,11 @@ __device__ __forceinline__ V3 lighting(const ShadeRec& m, cLightRec L, V3 point,
     }
   }
   return vadd(vadd(ambient, diffuse), specular);
+}
+__device__ __forceinline__ V3 lighting(const ShadeRec& m, cLightRec L, V3 point, V3 eyev, V3 normal,
+                                       bool in_shadow) {
+  return lighting(m, L, point, eyev, normal, in_shadow,
+                  vnormalize(vsub(v3(L->pos[0], L->pos[1], L->pos[2]), point)));
 }
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {

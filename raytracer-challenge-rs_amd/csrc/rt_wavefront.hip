@@ -211,12 +211,15 @@ __device__ __forceinline__ void shadow_ray(const DevScene& sc, const WfArgs& a, 
 // The outcome of shadow ray `slot` (= node slot * L + light): lighting() of
 // the hit with that light (material.rs:38-82), in shadow or not, as the
 // reference's shade_hit evaluates it (world.rs:41-56).
-__device__ __forceinline__ void shadow_result(const DevScene& sc, const WfArgs& a, unsigned slot, bool shadowed) {
+// `over` and `lightv` are the shadow ray's origin and direction (shadow_ray):
+// the over point and the light vector lighting() would recompute.
+__device__ __forceinline__ void shadow_result(const DevScene& sc, const WfArgs& a, unsigned slot, bool shadowed,
+                                              V3 over, V3 lightv) {
   const unsigned L = (unsigned)sc.n_lights;
   const unsigned node = L == 1 ? slot : slot / L, l = slot - node * L;
   const WfGeo& g = a.geo[node];
-  const V3 c = lighting(sc.shade[g.obj], (cLightRec)sc.lights + l, v3(g.over[0], g.over[1], g.over[2]),
-                        v3(g.eyev[0], g.eyev[1], g.eyev[2]), v3(g.normal[0], g.normal[1], g.normal[2]), shadowed);
+  const V3 c = lighting(sc.shade[g.obj], (cLightRec)sc.lights + l, over, v3(g.eyev[0], g.eyev[1], g.eyev[2]),
+                        v3(g.normal[0], g.normal[1], g.normal[2]), shadowed, lightv);
   double* dst = a.surf + (size_t)slot * 3;
   dst[0] = c.x; dst[1] = c.y; dst[2] = c.z;
 }
@@ -416,7 +419,7 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow(DevScene sc, 
     Hit h;
     if constexpr (USE_LDS) wf_trace_lds<false, true, QUADS>(sc, lv, o, d, h, n_disc);
     else trace<true>(sc, o, d, h, n_disc);
-    shadow_result(sc, a, slot, h.key >= 0 && h.t < dist);
+    shadow_result(sc, a, slot, h.key >= 0 && h.t < dist, o, d);
   }
   const unsigned long long s = wave_sum(n_disc);
   if (lane_id() == 0 && s) atomicAdd(&work_row(a.cnt)->disc[a.disc_slot], s);
@@ -1302,7 +1305,7 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow_bvh(DevScene 
       if (__any(!(h.key >= 0 && h.t < dist))) trace_rest<true, QUADS>(sc, o, d, h, n_disc);
     }
     hit_finish(h);
-    shadow_result(sc, a, slot, h.key >= 0 && h.t < dist);
+    shadow_result(sc, a, slot, h.key >= 0 && h.t < dist, o, d);
   }
   const unsigned long long sd = wave_sum(n_disc), st = wave_sum(n_tests), sb = wave_sum(n_boxes);
   if (lane_id() == 0) {
@@ -1406,7 +1409,7 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow_refill(DevSce
       pl = kBvhEmpty;
     }
     if (active && e == kBvhEmpty && pl == kBvhEmpty) {
-      shadow_result(sc, a, slot, h.key >= 0 && h.t < dist);
+      shadow_result(sc, a, slot, h.key >= 0 && h.t < dist, o, d);
       active = false;
     }
   }
@@ -1622,7 +1625,7 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow_lb(DevScene s
       }
     }
     hit_finish(h);
-    shadow_result(sc, a, slot, h.key >= 0 && h.t < dist);
+    shadow_result(sc, a, slot, h.key >= 0 && h.t < dist, o, d);
   }
   const unsigned long long sdc = wave_sum(n_disc), st = wave_sum(n_tests);
   if (lane_id() == 0) {
