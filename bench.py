@@ -38,15 +38,17 @@ sys.path[:0] = [REPO, os.path.join(REPO, "raytracer-challenge-rs_amd")]
 # enough hardware queues that they do not share one (HIP's default is 4; the
 # current stream, the render streams and RCCL's stream each want their own).
 # Read by the HIP runtime at initialisation, so before torch is imported.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+# With N GPUs each render stream also has its process group's RCCL stream.
+_queues = 8 if int(os.environ.get("WORLD_SIZE", "1") or 1) == 1 else 16
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < _queues:
+    os.environ["GPU_MAX_HW_QUEUES"] = str(_queues)
 
 import torch  # noqa: E402  (load torch's HIP runtime first: see rtamd/__init__.py)
 import torch.distributed as dist  # noqa: E402
 
 import rtamd  # noqa: E402
 from rtamd import scenes  # noqa: E402
-from rtamd.distributed import FrameAssembler  # noqa: E402
+from rtamd.distributed import FrameAssembler, StreamFrameAssembler  # noqa: E402
 
 WF_CLOSEST = 1  # kernel class index (csrc/rt_wavefront.hpp WfClass)
 METRIC = "Mrays/s (primary+secondary) on 1920×1080/1000-sphere/depth-5; 1→8 GPU scaling"
@@ -89,9 +91,13 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--stream-kind", default="raw", choices=["cumask", "raw", "torch"],
                    help="render streams: library-made plain (raw), library-made CU-masked (cumask), torch")
+    p.add_argument("--fake-shard", default=None,
+                   help="dev: r/n renders only rank r's rows of an n-way split on this one process (no gather)")
     p.add_argument("--verify", action="store_true",
                    help="dev: check the last assembled frame against a one-GPU render of the whole frame")
     p.add_argument("--dist-backend", default="nccl", help="dev: torch.distributed backend (nccl = RCCL)")
+    p.add_argument("--assembler", default="stream", choices=["stream", "main"],
+                   help="N GPUs: per-stream gather + un-interleave (stream) or on the current stream (main, dev)")
     p.add_argument("--event-path", action="store_true",
                    help="dev: on one GPU, run the N-GPU frame pipeline (shard slots, cross-stream events)")
     p.add_argument("--knob", action="append", default=[], help="library tuning knob k=v (dev; see rt_api.cpp)")
@@ -143,6 +149,9 @@ def main():
     if a.gpus != world_size and world_size > 1:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world_size}; using WORLD_SIZE", file=sys.stderr)
     n = world_size
+    srank, sn = rank, n  # the shard this process renders
+    if a.fake_shard:
+        srank, sn = (int(x) for x in a.fake_shard.split("/"))
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if n > 1:
@@ -163,25 +172,22 @@ def main():
     if a.exhaustive:
         rtamd._rtamd._tuning_set("accel", 0)
     W, H, B = cam.hsize, cam.vsize, a.row_block
-    # interleaved row blocks + one RCCL gather per frame; two shard slots so that
-    # frame s's gather overlaps frame s+1's render (rtamd.distributed.FrameAssembler)
     # F frames in flight: frame s renders on stream s % F (the library keeps one
     # workspace per stream, so the renders overlap on the device).
-    # - 1 GPU: into canvas slot s % F. The streams never wait on each other (stream
-    #   order alone protects a slot).
-    # - N GPUs: into shard slot s % (F + 1); the assembler (gather + un-interleave)
-    #   runs on the current stream after that frame's render, and a slot is rendered
-    #   again only after the assembler has completed its previous frame (free_ev).
+    # - 1 GPU: into canvas slot s % F; stream order alone protects a slot.
+    # - N GPUs (default "stream" assembler): each render stream owns a shard slot, a
+    #   gather buffer, a canvas and a process group, and a frame's render, RCCL
+    #   gather and rank 0's un-interleave all queue behind its own stream, so frames
+    #   on different streams never wait on each other (StreamFrameAssembler).
+    # - "main" assembler (dev): gather and un-interleave on the current stream,
+    #   coupled to the render streams by events (FrameAssembler; 0.30 instead of
+    #   0.18 ms per 8-way shard frame, measured with --fake-shard --event-path).
     # The render streams are plain streams, each on its own hardware queue
     # (GPU_MAX_HW_QUEUES above); CU-masked streams (--stream-kind cumask) also get
     # their own queue, but any cross-stream wait on them costs ~1 ms.
     # default: 4 frames in flight for C3; one for C5, whose wavefront workspace
     # (16.8 M primary rays, depth 8) takes tens of GB per frame
     F = max(1, a.inflight if a.inflight is not None else (4 if a.config == "c3" else 1))
-    events = n > 1 or a.event_path
-    fa = FrameAssembler(H, W, B, rank, n, dev, slots=F if not events else (F + 1 if F > 1 else 2))
-    assert len(fa.rows) == rtamd.shard_rows(H, B, rank, n)
-    shard = fa.shard
     stream = torch.cuda.current_stream()
     kind = a.stream_kind
     if F == 1:
@@ -192,6 +198,16 @@ def main():
         rstreams = [rtamd.render_stream(kind == "cumask") for _ in range(F)]
     if F > 1:  # the frames are the concurrency: no shadow side stream
         rtamd._rtamd._tuning_set("shadow_stream", 0)
+    per_stream = n > 1 and a.assembler == "stream"
+    events = not per_stream and (n > 1 or a.event_path)
+    if per_stream:
+        groups = [dist.new_group(list(range(n))) for _ in range(F)]
+        fa = StreamFrameAssembler(H, W, B, rank, n, dev, streams=rstreams if F > 1 else None, groups=groups,
+                                  slots=F)
+    else:
+        fa = FrameAssembler(H, W, B, rank, n, dev, slots=F if not events else (F + 1 if F > 1 else 2))
+    assert len(fa.rows) == rtamd.shard_rows(H, B, rank, n)
+    shard = fa.shard
     free_ev = [None] * len(fa.shards)
     frame_no = [0]
 
@@ -199,14 +215,14 @@ def main():
         s = frame_no[0]
         rs = rstreams[s % F]
         if not events:
-            cam.render_shard_device(world, depth, B, rank, n, fa.slot(s).data_ptr(), rs.cuda_stream, False)
-            fa.submit(s)  # the shard buffer already is the row-major canvas
+            cam.render_shard_device(world, depth, B, srank, sn, fa.slot(s).data_ptr(), rs.cuda_stream, False)
+            fa.submit(s)  # 1 GPU: the shard buffer already is the row-major canvas
             frame_no[0] = s + 1
             return
         slot = s % len(fa.shards)
         if rs is not stream and free_ev[slot] is not None:
             rs.wait_event(free_ev[slot])
-        cam.render_shard_device(world, depth, B, rank, n, fa.slot(s).data_ptr(), rs.cuda_stream, False)
+        cam.render_shard_device(world, depth, B, srank, sn, fa.slot(s).data_ptr(), rs.cuda_stream, False)
         if rs is not stream:
             stream.wait_stream(rs)
         fa.submit(s)
@@ -218,7 +234,7 @@ def main():
 
     # exact work counters of one frame (deterministic), from a counted warm-up launch
     # (this first launch also sizes the wavefront queues of this camera/shard)
-    st = cam.render_shard_device(world, depth, B, rank, n, shard.data_ptr(), stream.cuda_stream, True)
+    st = cam.render_shard_device(world, depth, B, srank, sn, shard.data_ptr(), stream.cuda_stream, True)
     counts = torch.tensor([st["rays_primary"], st["rays_reflect"], st["rays_refract"], st["rays_shadow"],
                            st["sphere_tests"], st["plane_tests"], st["sphere_disc_ge0"]],
                           dtype=torch.float64, device=dev)
@@ -256,7 +272,7 @@ def main():
     # for; here each kernel runs alone, as in the rocprofv3 kernel trace.
     rtamd._rtamd._wf_profile(world, 1, False)
     for _ in range(a.steps):
-        cam.render_shard_device(world, depth, B, rank, n, shard.data_ptr(), stream.cuda_stream, False)
+        cam.render_shard_device(world, depth, B, srank, sn, shard.data_ptr(), stream.cuda_stream, False)
     torch.cuda.synchronize()
     breakdown = rtamd._rtamd._wf_profile(world, 0, True)
     prof = breakdown

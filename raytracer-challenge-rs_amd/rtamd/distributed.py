@@ -103,3 +103,81 @@ class FrameAssembler:
         work, slot = self._pending
         work.wait()  # NCCL: the current stream waits on the gather (the host does not block)
         return self._unweave(slot) if self.rank == 0 else None
+
+
+class StreamFrameAssembler:
+    """Frame assembly with frames in flight and no cross-stream coupling.
+
+    Frames render on F streams (frame s on stream s % F). Each stream owns a
+    shard slot, a gather buffer and (on rank 0) a canvas, and a process group
+    of its own, so a frame's render, its gather (RCCL on that group's stream,
+    fenced against the render stream both ways) and rank 0's un-interleave
+    all run in order behind that one stream. Frames on different streams
+    never wait on each other, and slot reuse (frame s + F) is ordered by the
+    stream itself. The un-interleave is one index_select through the inverse
+    row map (as in FrameAssembler). `streams=None` runs on the current stream
+    (CPU tests with gloo).
+    """
+
+    def __init__(self, height, width, row_block, rank, n_shards, device, streams=None, groups=None,
+                 dtype=torch.float64, slots=1):
+        self.H, self.W, self.B = height, width, row_block
+        self.rank, self.n = rank, n_shards
+        self.streams = streams
+        self.F = len(streams) if streams else max(1, slots)
+        self.groups = groups if groups is not None else [None] * self.F
+        self.rows = shard_row_ids(height, row_block, rank, n_shards)
+        self.max_rows = max(len(shard_row_ids(height, row_block, s, n_shards)) for s in range(n_shards))
+        self.shards = [torch.zeros((self.max_rows, width, 3), dtype=dtype, device=device) for _ in range(self.F)]
+        self.shard = self.shards[0]
+        self._last = None
+        if rank == 0 and n_shards > 1:
+            self.gather_buf = [torch.empty((n_shards * self.max_rows, width, 3), dtype=dtype, device=device)
+                               for _ in range(self.F)]
+            self.gathered = [[b[s * self.max_rows:(s + 1) * self.max_rows] for s in range(n_shards)]
+                             for b in self.gather_buf]
+            self.canvas = [torch.empty((height, width, 3), dtype=dtype, device=device) for _ in range(self.F)]
+            inv = [0] * height
+            for s in range(n_shards):
+                for i, y in enumerate(shard_row_ids(height, row_block, s, n_shards)):
+                    inv[y] = s * self.max_rows + i
+            self.inv_idx = torch.tensor(inv, device=device)
+
+    def slot(self, step):
+        """Shard buffer frame `step` renders into (on stream step % F)."""
+        return self.shards[step % self.F]
+
+    def stream(self, step):
+        return self.streams[step % self.F] if self.streams else None
+
+    def submit(self, step):
+        """Gather and assemble frame `step`, queued behind its render on its
+        stream; returns its canvas on rank 0 (valid until frame step + F is
+        submitted), None elsewhere."""
+        k = step % self.F
+        if self.n == 1:
+            self._last = self.shards[k][: self.H]
+            return self._last
+        ctx = torch.cuda.stream(self.streams[k]) if self.streams else _nullctx()
+        with ctx:
+            work = dist.gather(self.shards[k], self.gathered[k] if self.rank == 0 else None, dst=0,
+                               group=self.groups[k], async_op=True)
+            work.wait()  # the frame's stream waits on its gather (the host does not block)
+            if self.rank != 0:
+                self._last = None
+                return None
+            torch.index_select(self.gather_buf[k], 0, self.inv_idx, out=self.canvas[k])
+            self._last = self.canvas[k]
+            return self._last
+
+    def flush(self):
+        """The last submitted frame's canvas on rank 0 (everything is already queued)."""
+        return self._last
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False

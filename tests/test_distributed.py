@@ -117,3 +117,46 @@ def test_shard_rows_partition(rt):
         rows = [shard_row_ids(H, B, s, n) for s in range(n)]
         assert sorted(sum(rows, [])) == list(range(H))
         assert [len(r) for r in rows] == [rt.shard_rows(H, B, s, n) for s in range(n)]
+
+
+def _stream_worker(rank, world_size, port, row_block, n_frames, n_slots, out_path):
+    """StreamFrameAssembler (bench.py's N>1 path): frame f is golden + f, one
+    process group per slot; every submit returns frame f assembled."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world_size)
+    try:
+        from rtamd.distributed import StreamFrameAssembler
+        ref = torch.from_numpy(np.load(os.path.join(HERE, "golden", "c3_64x36_s200.npz"))["canvas"])
+        H, W = ref.shape[:2]
+        groups = [dist.new_group(list(range(world_size))) for _ in range(n_slots)]
+        fa = StreamFrameAssembler(H, W, row_block, rank, world_size, torch.device("cpu"), groups=groups,
+                                  slots=n_slots)
+        done = []
+        for f in range(n_frames):
+            buf = fa.slot(f)
+            buf.fill_(-1.0)
+            buf[: len(fa.rows)] = ref[fa.rows] + f
+            c = fa.submit(f)
+            if rank == 0:
+                done.append(c.clone())
+            else:
+                assert c is None
+        if rank == 0:
+            assert fa.flush() is not None
+            np.save(out_path, torch.stack(done).numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world_size,row_block,n_slots", [(2, 8, 4), (3, 5, 3)])
+def test_gloo_stream_assembler(tmp_path, world_size, row_block, n_slots):
+    """The per-stream assembler of bench.py's N>1 path (one slot, gather buffer,
+    canvas and process group per render stream): every frame comes out whole."""
+    out = str(tmp_path / "frames.npy")
+    mp.spawn(_stream_worker, args=(world_size, _free_port(), row_block, 6, n_slots, out), nprocs=world_size,
+             join=True)
+    got = np.load(out)
+    ref = np.load(os.path.join(HERE, "golden", "c3_64x36_s200.npz"))["canvas"]
+    assert got.shape == (6,) + ref.shape
+    for f in range(6):
+        assert np.array_equal(got[f], ref + f), f
