@@ -38,7 +38,7 @@ sys.path[:0] = [REPO, os.path.join(REPO, "raytracer-challenge-rs_amd")]
 # enough hardware queues that they do not share one (HIP's default is 4; the
 # current stream, the render streams and RCCL's stream each want their own).
 # Read by the HIP runtime at initialisation, so before torch is imported.
-# With N GPUs each render stream also has its process group's RCCL stream.
+# With N GPUs each render stream may also have a process group's RCCL stream.
 _queues = 8 if int(os.environ.get("WORLD_SIZE", "1") or 1) == 1 else 16
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < _queues:
     os.environ["GPU_MAX_HW_QUEUES"] = str(_queues)
@@ -48,7 +48,7 @@ import torch.distributed as dist  # noqa: E402
 
 import rtamd  # noqa: E402
 from rtamd import scenes  # noqa: E402
-from rtamd.distributed import FrameAssembler, StreamFrameAssembler  # noqa: E402
+from rtamd.distributed import FrameAssembler, RcclStreamAssembler, StreamFrameAssembler  # noqa: E402
 
 WF_CLOSEST = 1  # kernel class index (csrc/rt_wavefront.hpp WfClass)
 METRIC = "Mrays/s (primary+secondary) on 1920×1080/1000-sphere/depth-5; 1→8 GPU scaling"
@@ -96,8 +96,12 @@ def parse():
     p.add_argument("--verify", action="store_true",
                    help="dev: check the last assembled frame against a one-GPU render of the whole frame")
     p.add_argument("--dist-backend", default="nccl", help="dev: torch.distributed backend (nccl = RCCL)")
-    p.add_argument("--assembler", default="stream", choices=["stream", "main"],
-                   help="N GPUs: per-stream gather + un-interleave (stream) or on the current stream (main, dev)")
+    p.add_argument("--assembler", default="rccl", choices=["rccl", "stream", "main"],
+                   help="N GPUs: gathers enqueued by the library on each render stream (rccl), per-stream "
+                        "torch process groups (stream), or assembly on the current stream (main, dev)")
+    p.add_argument("--emulate-gather", action="store_true",
+                   help="dev, 1 GPU: per render stream, a side stream standing in for its RCCL stream copies the "
+                        "shard (fenced both ways, as the N-GPU stream assembler), then the un-interleave runs")
     p.add_argument("--event-path", action="store_true",
                    help="dev: on one GPU, run the N-GPU frame pipeline (shard slots, cross-stream events)")
     p.add_argument("--knob", action="append", default=[], help="library tuning knob k=v (dev; see rt_api.cpp)")
@@ -198,9 +202,19 @@ def main():
         rstreams = [rtamd.render_stream(kind == "cumask") for _ in range(F)]
     if F > 1:  # the frames are the concurrency: no shadow side stream
         rtamd._rtamd._tuning_set("shadow_stream", 0)
-    per_stream = n > 1 and a.assembler == "stream"
+    per_stream = n > 1 and a.assembler in ("stream", "rccl")
     events = not per_stream and (n > 1 or a.event_path)
-    if per_stream:
+    fa = None
+    if n > 1 and a.assembler == "rccl" and F > 1:
+        try:
+            fa = RcclStreamAssembler(H, W, B, rank, n, dev, streams=rstreams)
+        except Exception as e:  # fall back to the torch process groups
+            print(f"warning: RCCL stream assembler unavailable ({e}); using per-stream process groups",
+                  file=sys.stderr, flush=True)
+            fa = None
+    if fa is not None:
+        pass
+    elif per_stream:
         groups = [dist.new_group(list(range(n))) for _ in range(F)]
         fa = StreamFrameAssembler(H, W, B, rank, n, dev, streams=rstreams if F > 1 else None, groups=groups,
                                   slots=F)
@@ -211,11 +225,26 @@ def main():
     free_ev = [None] * len(fa.shards)
     frame_no = [0]
 
+    if a.emulate_gather:
+        gstreams = [torch.cuda.Stream(device=dev) for _ in range(F)]
+        gbufs = [torch.empty_like(fa.slot(k)) for k in range(F)]
+        canv = [torch.empty_like(fa.slot(k)) for k in range(F)]
+        perm = torch.randperm(fa.slot(0).shape[0], device=dev)
+
     def step():
         s = frame_no[0]
         rs = rstreams[s % F]
         if not events:
             cam.render_shard_device(world, depth, B, srank, sn, fa.slot(s).data_ptr(), rs.cuda_stream, False)
+            if a.emulate_gather:
+                k = s % F
+                gs = gstreams[k]
+                gs.wait_stream(rs)
+                with torch.cuda.stream(gs):
+                    gbufs[k].copy_(fa.slot(s))
+                rs.wait_stream(gs)
+                with torch.cuda.stream(rs):
+                    torch.index_select(gbufs[k], 0, perm, out=canv[k])
             fa.submit(s)  # 1 GPU: the shard buffer already is the row-major canvas
             frame_no[0] = s + 1
             return

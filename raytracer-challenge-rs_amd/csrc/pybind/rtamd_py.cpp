@@ -39,6 +39,10 @@ static py::array_t<double> check_rays(py::array_t<double, py::array::c_style | p
 
 extern "C" int rtamd_tuning_set(const char* key, int value);
 extern "C" int rtamd_stream_create(int cu_masked, void** out);
+extern "C" int rtamd_nccl_unique_id(unsigned char* out, size_t size);
+extern "C" int rtamd_nccl_comm_init(int nranks, const unsigned char* id, size_t size, int rank, int device, void** comm);
+extern "C" int rtamd_nccl_gather_f64(const double* send, double* recv, size_t count, int root, void* comm, void* stream);
+extern "C" int rtamd_nccl_comm_destroy(void* comm);
 extern "C" int rtamd_wf_profile(const rt_scene* s, int enable, double out[29]);
 
 PYBIND11_MODULE(_rtamd, m) {
@@ -400,6 +404,24 @@ PYBIND11_MODULE(_rtamd, m) {
     return d;
   }, py::arg("world"), py::arg("enable") = -1, py::arg("read") = true);
   m.def("_tuning_set", [](const std::string& k, int v) { check(rtamd_tuning_set(k.c_str(), v), "tuning"); });
+  m.def("_nccl_unique_id", []() {
+    std::string id(128, '\0');
+    check(rtamd_nccl_unique_id((unsigned char*)&id[0], id.size()), "nccl unique id");
+    return py::bytes(id);
+  });
+  m.def("_nccl_comm_init", [](int nranks, py::bytes id, int rank, int device) {
+    std::string s = id;
+    void* comm = nullptr;
+    {
+      py::gil_scoped_release nogil;
+      check(rtamd_nccl_comm_init(nranks, (const unsigned char*)s.data(), s.size(), rank, device, &comm), "nccl comm init");
+    }
+    return (uintptr_t)comm;
+  });
+  m.def("_nccl_gather_f64", [](uintptr_t send, uintptr_t recv, size_t count, int root, uintptr_t comm, uintptr_t stream) {
+    check(rtamd_nccl_gather_f64((const double*)send, (double*)recv, count, root, (void*)comm, (void*)stream), "nccl gather");
+  });
+  m.def("_nccl_comm_destroy", [](uintptr_t comm) { check(rtamd_nccl_comm_destroy((void*)comm), "nccl comm destroy"); });
   m.def("_stream_create", [](bool cu_masked) {
     void* st = nullptr;
     check(rtamd_stream_create(cu_masked ? 1 : 0, &st), "stream");

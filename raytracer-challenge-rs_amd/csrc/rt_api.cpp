@@ -379,6 +379,38 @@ int rtamd_stream_create(int cu_masked, void** out) {
   *out = st;
   return RT_OK;
 }
+// Development/benchmark hooks (not in the public ABI): an RCCL communicator
+// per render stream for multi-process frame assembly, so that a frame's
+// gather is enqueued on the stream that rendered it (no cross-stream event;
+// bench.py, rtamd.distributed.RcclStreamAssembler).
+int rtamd_nccl_unique_id(unsigned char* out, size_t size) {
+  if (!out || size < sizeof(ncclUniqueId)) return fail(RT_ERR_INVALID_ARGUMENT, "unique id buffer too small");
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return fail(RT_ERR_RCCL, "ncclGetUniqueId");
+  std::memcpy(out, &id, sizeof id);
+  return RT_OK;
+}
+int rtamd_nccl_comm_init(int nranks, const unsigned char* id, size_t size, int rank, int device, void** comm) {
+  if (!id || !comm || size < sizeof(ncclUniqueId) || nranks < 1 || rank < 0 || rank >= nranks)
+    return fail(RT_ERR_INVALID_ARGUMENT, "bad communicator arguments");
+  RT_HIP(hipSetDevice(device));
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof uid);
+  ncclComm_t c = nullptr;
+  if (ncclCommInitRank(&c, nranks, uid, rank) != ncclSuccess) return fail(RT_ERR_RCCL, "ncclCommInitRank");
+  *comm = c;
+  return RT_OK;
+}
+int rtamd_nccl_gather_f64(const double* send, double* recv, size_t count, int root, void* comm, void* stream) {
+  if (!send || !comm) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
+  if (ncclGather(send, recv, count, ncclDouble, root, (ncclComm_t)comm, (hipStream_t)stream) != ncclSuccess)
+    return fail(RT_ERR_RCCL, "ncclGather");
+  return RT_OK;
+}
+int rtamd_nccl_comm_destroy(void* comm) {
+  if (comm && ncclCommDestroy((ncclComm_t)comm) != ncclSuccess) return fail(RT_ERR_RCCL, "ncclCommDestroy");
+  return RT_OK;
+}
 int rt_abi_version(void) { return RT_ABI_VERSION; }
 
 int rt_device_count(void) {

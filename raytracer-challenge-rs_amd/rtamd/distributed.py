@@ -181,3 +181,52 @@ class _nullctx:
 
     def __exit__(self, *exc):
         return False
+
+
+class RcclStreamAssembler(StreamFrameAssembler):
+    """StreamFrameAssembler whose gathers are RCCL collectives the library
+    enqueues directly on each frame's render stream (one communicator per
+    render stream, rtamd._rtamd._nccl_*): a frame's render, gather and rank
+    0's un-interleave are consecutive work of ONE stream, with no
+    cross-stream event at all. Cross-stream fences (a render stream and a
+    process group's own RCCL stream waiting on each other) cost ~0.17 ms per
+    frame on an 8-way shard (`bench.py --fake-shard 0/8 --emulate-gather`),
+    which is the whole frame again. The communicators' unique ids travel over
+    the default process group."""
+
+    def __init__(self, height, width, row_block, rank, n_shards, device, streams, dtype=torch.float64):
+        super().__init__(height, width, row_block, rank, n_shards, device, streams=streams,
+                         groups=[None] * len(streams), dtype=dtype)
+        from . import _rtamd
+        self._lib = _rtamd
+        dev_index = device.index if device.index is not None else torch.cuda.current_device()
+        self.comms = []
+        for _ in range(self.F):
+            uid = torch.zeros(128, dtype=torch.uint8, device=device)
+            if rank == 0:
+                uid.copy_(torch.frombuffer(bytearray(_rtamd._nccl_unique_id()), dtype=torch.uint8))
+            dist.broadcast(uid, src=0)
+            self.comms.append(_rtamd._nccl_comm_init(n_shards, bytes(uid.cpu().numpy().tobytes()), rank,
+                                                     dev_index))
+
+    def submit(self, step):
+        k = step % self.F
+        if self.n == 1:
+            self._last = self.shards[k][: self.H]
+            return self._last
+        st = self.streams[k]
+        recv = self.gather_buf[k].data_ptr() if self.rank == 0 else 0
+        self._lib._nccl_gather_f64(self.shards[k].data_ptr(), recv, self.shards[k].numel(), 0, self.comms[k],
+                                   st.cuda_stream)
+        if self.rank != 0:
+            self._last = None
+            return None
+        with torch.cuda.stream(st):
+            torch.index_select(self.gather_buf[k], 0, self.inv_idx, out=self.canvas[k])
+        self._last = self.canvas[k]
+        return self._last
+
+    def close(self):
+        for c in self.comms:
+            self._lib._nccl_comm_destroy(c)
+        self.comms = []

@@ -361,3 +361,20 @@ def test_bad_aa_rejected(rt):
     buf = torch.empty((4, 4, 3), dtype=torch.float64, device="cuda")
     with pytest.raises(rt.RtError, match="aa_samples"):
         c.render_shard_device(w, 5, 8, 0, 1, buf.data_ptr(), 0, False, aa_samples=3)
+
+
+def test_rccl_stream_gather_hooks(rt):
+    """The library's per-stream RCCL hooks (bench.py's N-GPU assembler):
+    a one-rank communicator gathers a buffer on a render stream."""
+    import torch
+    comm = rt._rtamd._nccl_comm_init(1, rt._rtamd._nccl_unique_id(), 0, 0)
+    try:
+        st = rt.render_stream(False)
+        send = torch.arange(3000, dtype=torch.float64, device="cuda")
+        recv = torch.full_like(send, -1.0)
+        torch.cuda.synchronize()
+        rt._rtamd._nccl_gather_f64(send.data_ptr(), recv.data_ptr(), send.numel(), 0, comm, st.cuda_stream)
+        torch.cuda.synchronize()
+        assert torch.equal(send, recv)
+    finally:
+        rt._rtamd._nccl_comm_destroy(comm)
