@@ -351,6 +351,9 @@ def main():
             out["cpu_baseline"] = cpu_baseline(world, cam, depth, a.cpu_seconds)
         print(json.dumps(out), flush=True)
     if n > 1:
+        torch.cuda.synchronize()
+        if hasattr(fa, "close"):
+            fa.close()  # the per-stream RCCL communicators
         dist.destroy_process_group()
 
 
