@@ -344,6 +344,7 @@ def main():
                                 if n > 1 else "1 GPU: wavefront pipeline") + f"; {F} frames in flight",
                 "frames_in_flight": F,
                 "render_streams": kind if F > 1 else "current",
+                "assembler": type(fa).__name__ if n > 1 else None,
             },
             "roofline": roofline(prof, breakdown, W, H, a, n, ref_work, elapsed / a.steps * 1e3),
         }
