@@ -202,12 +202,20 @@ class RcclStreamAssembler(StreamFrameAssembler):
         dev_index = device.index if device.index is not None else torch.cuda.current_device()
         self.comms = []
         for _ in range(self.F):
-            uid = torch.zeros(128, dtype=torch.uint8, device=device)
+            # byte 0: rank 0 could make an id (1) or not (0); every rank reads the same
+            # flag, so a failure sends every rank to the caller's fallback together
+            msg = torch.zeros(129, dtype=torch.uint8, device=device)
             if rank == 0:
-                uid.copy_(torch.frombuffer(bytearray(_rtamd._nccl_unique_id()), dtype=torch.uint8))
-            dist.broadcast(uid, src=0)
-            self.comms.append(_rtamd._nccl_comm_init(n_shards, bytes(uid.cpu().numpy().tobytes()), rank,
-                                                     dev_index))
+                try:
+                    msg[1:].copy_(torch.frombuffer(bytearray(_rtamd._nccl_unique_id()), dtype=torch.uint8))
+                    msg[0] = 1
+                except Exception:  # pragma: no cover - environment dependent
+                    msg[0] = 0
+            dist.broadcast(msg, src=0)
+            host = msg.cpu().numpy().tobytes()
+            if host[0] != 1:
+                raise RuntimeError("rank 0 could not create an RCCL unique id")
+            self.comms.append(_rtamd._nccl_comm_init(n_shards, host[1:], rank, dev_index))
 
     def submit(self, step):
         k = step % self.F
