@@ -979,8 +979,11 @@ __device__ __forceinline__ void lane_trace_pair(const unsigned char* nodes, cons
   for (int a = 0; a < 3; ++a) asm volatile("" : "+v"(ent[a]), "+v"(ext[a]));
   float t_hi = f32_up(SHADOW ? t_shadow : h.t);
   auto stk = [&](int k) -> int& { return lds[k * kTraceBlock]; };
-  int sp = 0;
-  auto pop = [&]() { return sp > 0 ? stk(--sp) : kBvhEmpty; };
+  // entry 0 is a sentinel (kBvhEmpty): a pop needs no emptiness test, and a
+  // lane that pops it is done and pops no more (the stack holds bvh_depth + 1)
+  stk(0) = kBvhEmpty;
+  int sp = 1;
+  auto pop = [&]() { return stk(--sp); };
   int e = (SHADOW && h.key >= 0 && h.t < t_shadow) || !has_bvh ? kBvhEmpty : 0;
   auto visit = [&]() {
     const unsigned char* nb = nodes + (size_t)e * 64;
@@ -1029,7 +1032,7 @@ __device__ __forceinline__ void lane_trace_pair(const unsigned char* nodes, cons
     }
     if (!__any(pl != kBvhEmpty)) break;
     if (pl != kBvhEmpty) {
-      if (leaf(pl)) { e = kBvhEmpty; sp = 0; }  // shadowed: done
+      if (leaf(pl)) { e = kBvhEmpty; sp = 1; }  // shadowed: done
       pl = kBvhEmpty;
     }
   }
@@ -1128,7 +1131,7 @@ __device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, int* static_
     ls.stack16 = stack + threadIdx.x;
   } else if constexpr (LANE == 14) {  // pair layout (lane_trace_pair) + sphere records
     int* stack = (int*)dyn;
-    unsigned char* nodes = dyn + lane_stack_bytes(sc.bvh_depth);
+    unsigned char* nodes = dyn + lane_stack_bytes(sc.bvh_depth + 1);  // + the sentinel entry
     for (int i = threadIdx.x; i < sc.n_bvh; i += blockDim.x) {
       const BvhNode& g = sc.bvh[i];
       float* q = (float*)(nodes + (size_t)i * 64);
@@ -1942,8 +1945,9 @@ static hipError_t launch_closest_q(const DevScene& sc, const DevCamera& cam, con
     if (primary) {
       auto k = wf_trace_closest_bvh<true, QUADS, 0, TW>;
       WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, n)), dim3(tb), 0, stream, sc, cam, a);
-    } else if (g_wf_lane == 14 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc) <= kWfLdsLimit) {
-      const size_t lds = lane_lds_bytes(sc);
+    } else if (g_wf_lane == 14 && sc.bvh_depth <= kLaneLdsDepth &&
+               lane_lds_bytes(sc) + lane_stack_bytes(1) <= kWfLdsLimit) {
+      const size_t lds = lane_lds_bytes(sc) + lane_stack_bytes(1);
       auto k = wf_trace_closest_bvh<false, QUADS, 14, TW>;
       WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, n)), dim3(tb), lds, stream, sc, cam, a);
