@@ -26,6 +26,7 @@ ap.add_argument("--ns", default="1,2,4,8")
 ap.add_argument("--inflight", type=int, default=4)
 ap.add_argument("--streams", default="raw", choices=["torch", "once", "raw", "cumask"],
                 help="torch: new torch streams per rank; once: torch streams made once; raw / cumask: library-made streams (cumask: hipExtStreamCreateWithCUMask), made once")
+ap.add_argument("--reverse", action="store_true", help="measure the ranks last to first")
 ap.add_argument("--ranks", action="store_true", help="print every rank's time")
 a = ap.parse_args()
 for kv in a.knob:
@@ -44,8 +45,10 @@ elif a.streams in ("raw", "cumask"):
 else:
     _made = None
 for n in [int(x) for x in a.ns.split(",")]:
-    times = []
-    for r in range(n):
+
+    order = list(range(n))[::-1] if a.reverse else list(range(n))
+    times = [0.0] * n
+    for r in order:
         rows = rtamd.shard_rows(H, B, r, n)
         F = max(1, a.inflight)
         if F > 1:
@@ -56,14 +59,16 @@ for n in [int(x) for x in a.ns.split(",")]:
         for f in range(3 * F):
             cam.render_shard_device(w, depth, B, r, n, bufs[f % F].data_ptr(), sts[f % F].cuda_stream, False)
         torch.cuda.synchronize()
-        if r == 0:
-            rtamd._rtamd._wf_profile(w, 1, False)
         t0 = time.perf_counter()
         for f in range(a.frames):
             cam.render_shard_device(w, depth, B, r, n, bufs[f % F].data_ptr(), sts[f % F].cuda_stream, False)
         torch.cuda.synchronize()
-        times.append((time.perf_counter() - t0) / a.frames * 1e3)
-        if r == 0:
+        times[r] = (time.perf_counter() - t0) / a.frames * 1e3
+        if r == 0:  # per-class times from a separate profiled pass (events would slow the timed frames)
+            rtamd._rtamd._wf_profile(w, 1, False)
+            for f in range(min(a.frames, 20)):
+                cam.render_shard_device(w, depth, B, r, n, bufs[f % F].data_ptr(), sts[f % F].cuda_stream, False)
+            torch.cuda.synchronize()
             p = rtamd._rtamd._wf_profile(w, 0, True)
             cls = " ".join(f"{c}={m:.3f}" for c, m in p["ms"].items())
     mean, worst = sum(times) / n, max(times)
