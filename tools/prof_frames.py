@@ -19,6 +19,7 @@ ap.add_argument("--width", type=int, default=1920)
 ap.add_argument("--height", type=int, default=1080)
 ap.add_argument("--spheres", type=int, default=1000)
 ap.add_argument("--exhaustive", action="store_true")
+ap.add_argument("--config", default="c3", choices=["c3", "c5"])
 ap.add_argument("--inflight", type=int, default=1, help="frames in flight (streams); 1 = serialized, as bench.py's roofline pass")
 ap.add_argument("--shard", default="0/1", help="render rank r of an n-way row split: r/n (dev)")
 ap.add_argument("--knob", action="append", default=[], help="tuning knob k=v (dev)")
@@ -26,7 +27,7 @@ a = ap.parse_args()
 for kv in a.knob:
     k, v = kv.split("=")
     rtamd._rtamd._tuning_set(k, int(v))
-w, cam, depth = scenes.c3(a.width, a.height, a.spheres)
+w, cam, depth = scenes.c3(a.width, a.height, a.spheres) if a.config == "c3" else scenes.c5(a.width, a.height, a.spheres)
 w.upload(0)
 if a.exhaustive:
     rtamd._rtamd._tuning_set("accel", 0)
