@@ -249,20 +249,23 @@ def test_lane_refill_bitwise(rt, inside):
     assert fast.to_numpy().tobytes() == exact.to_numpy().tobytes()
 
 
-@pytest.mark.parametrize("n_streams", [2, 10])
-def test_frames_in_flight_bitwise(rt, n_streams):
+@pytest.mark.parametrize("n_streams,kind", [(2, "torch"), (10, "torch"), (4, "plain"), (4, "dedicated")])
+def test_frames_in_flight_bitwise(rt, n_streams, kind):
     """Frames rendered concurrently on several streams (one workspace per
     stream; with 10 streams, more than the pool's 8 workspaces, so workspaces
     change hands in stream order) all equal the exhaustive frame, for the
-    whole frame and for an 8-way shard, with the shadow-stream fork/join and
-    small-launch block sizing on."""
+    whole frame and for an 8-way shard, on torch streams and on the
+    library's render streams (rtamd.render_stream, plain and CU-masked)."""
     import torch
     from rtamd import scenes
     w, cam, depth = scenes.c3(240, 136, n_spheres=600)
     full, _ = cam.render(w, depth, want_stats=True)
     full = full.to_numpy()
     rows8 = [y for y in range(cam.vsize) if (y // 8) % 8 == 5]
-    streams = [torch.cuda.Stream() for _ in range(n_streams)]
+    if kind == "torch":
+        streams = [torch.cuda.Stream() for _ in range(n_streams)]
+    else:  # rtamd.render_stream: library-made plain or CU-masked (own hardware queue) streams
+        streams = [rt.render_stream(kind == "dedicated") for _ in range(n_streams)]
     frames = 3 * n_streams
     bufs = [torch.full((cam.vsize, cam.hsize, 3), -1.0, dtype=torch.float64, device="cuda") for _ in range(frames)]
     sh = [torch.full((len(rows8), cam.hsize, 3), -1.0, dtype=torch.float64, device="cuda") for _ in range(frames)]
