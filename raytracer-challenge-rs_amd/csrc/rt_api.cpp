@@ -32,7 +32,7 @@ namespace {
 thread_local std::string g_err;
 int g_bvh_leaf = 2;     // BVH leaf size at scene creation (tuning knob "bvh_leaf")
 int g_bvh_ct = 70;      // SAH node-visit cost in percent of a sphere test (tuning knob "bvh_ct")
-int g_lb_res = 128;     // light-buffer cells per cube-map face edge at scene creation, 0 = none ("lb_res")
+int g_lb_res = 256;     // light-buffer cells per cube-map face edge at scene creation, 0 = none ("lb_res")
 
 int fail(int code, const std::string& msg) {
   g_err = msg;

@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 PI = math.pi
 
 
-def _three(rt, make, lb_res=128):
+def _three(rt, make, lb_res=256):
     rt._rtamd._tuning_set("lb_res", lb_res)
     try:
         w, cam, depth = make(rt)
@@ -33,7 +33,7 @@ def _three(rt, make, lb_res=128):
         exact, _ = cam.render(w, depth, want_stats=True)
         p = rt._rtamd._wf_profile(prof_world, -1, True)
     finally:
-        rt._rtamd._tuning_set("lb_res", 128)
+        rt._rtamd._tuning_set("lb_res", 256)
     return fast.to_numpy(), bvh.to_numpy(), exact.to_numpy(), p
 
 
@@ -61,7 +61,7 @@ def _cluster(rt, light, n=300, seed=7, cam_from=(0, 2, -9), cam_to=(0, 1, 2), sh
     return w, cam, 5
 
 
-@pytest.mark.parametrize("lb_res", [1, 3, 16, 128, 512])
+@pytest.mark.parametrize("lb_res", [1, 3, 16, 128, 256, 512])
 def test_lightbuf_c3_any_resolution(rt, lb_res):
     from rtamd import scenes
     fast, bvh, exact, p = _three(rt, lambda rt: scenes.c3(192, 108), lb_res)
@@ -147,4 +147,4 @@ def test_lightbuf_color_at_batch_random_rays(rt):
             assert fast.tobytes() == exact.tobytes(), depth
         assert rt._rtamd._wf_profile(w, -1, True)["lb_res"] == 64
     finally:
-        rt._rtamd._tuning_set("lb_res", 128)
+        rt._rtamd._tuning_set("lb_res", 256)
