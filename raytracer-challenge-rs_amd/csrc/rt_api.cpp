@@ -330,6 +330,10 @@ int rtamd_tuning_set(const char* key, int value) {
     rtamd::g_wf_adaptive_block = value != 0;
     return RT_OK;
   }
+  if (key && std::strcmp(key, "prim_lane") == 0) {
+    rtamd::g_wf_prim_lane = value != 0;
+    return RT_OK;
+  }
   if (key && std::strcmp(key, "refill_min") == 0) {
     if (value < 1 || value > 64) return fail(RT_ERR_INVALID_ARGUMENT, "refill_min must be in [1, 64]");
     rtamd::g_wf_refill_min = value;

@@ -38,6 +38,7 @@ int g_wf_shadow_lb = 1;    // 1 = shadow rays through the light buffer (DESIGN.m
 int g_wf_refill = 0;       // 1 = lanes take a new ray as soon as theirs is done (DESIGN.md "Lane refill");
                            // LANE 12 = the same for the closest-hit rays of generations >= 1
 int g_wf_refill_min = 16;
+int g_wf_prim_lane = 0;  // tuning knob ("prim_lane"): 1 = primary rays take the per-lane pair traversal too
 // occupancy (waves per SIMD the register allocator targets) of the BVH trace kernels
 int g_tw_primary = 4, g_tw_closest = 4, g_tw_shadow = 4;
 constexpr int kWfBlock = 256;      // prep / shadow / combine
@@ -1232,7 +1233,7 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest_bvh(DevScene
     hit_init(h);
     if (valid) {
       wf_ray(a, cam, slot, o, d);
-      if constexpr (LANE == 14 && !PRIMARY) {
+      if constexpr (LANE == 14) {  // also primary rays (g_wf_prim_lane)
         trace_rest<false, QUADS>(sc, o, d, h, n_disc);  // planes first: an early nearest hit tightens the culling
         lane_trace_pair<false>((const unsigned char*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, n_disc,
                                n_tests, n_boxes, ls.stack);
@@ -1942,7 +1943,13 @@ static hipError_t launch_closest_q(const DevScene& sc, const DevCamera& cam, con
                                    bool lds_ok, bool bvh, unsigned n, hipStream_t stream) {
   const int tb = trace_block(n);
   if (bvh) {
-    if (primary) {
+    if (primary && g_wf_prim_lane && sc.bvh_depth + 1 <= kLaneLdsDepth &&
+        lane_lds_bytes(sc) + lane_stack_bytes(1) <= kWfLdsLimit) {
+      const size_t lds = lane_lds_bytes(sc) + lane_stack_bytes(1);
+      auto k = wf_trace_closest_bvh<true, QUADS, 14, TW>;
+      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, n)), dim3(tb), lds, stream, sc, cam, a);
+    } else if (primary) {
       auto k = wf_trace_closest_bvh<true, QUADS, 0, TW>;
       WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, n)), dim3(tb), 0, stream, sc, cam, a);
     } else if (g_wf_lane == 14 && sc.bvh_depth <= kLaneLdsDepth &&

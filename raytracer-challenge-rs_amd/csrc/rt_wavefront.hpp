@@ -67,7 +67,8 @@ extern int g_wf_shadow_lb;    // tuning knob: 1 = shadow rays through the light 
 extern int g_wf_refill;       // tuning knob: 1 = lane refill in the per-lane trace kernels
 extern int g_wf_shadow_stream;   // tuning knob: 1 = shadow traces on a second stream, overlapping the next generation
 extern int g_wf_adaptive_block;  // tuning knob: 1 = small trace launches spread over every CU (smaller blocks)
-extern int g_wf_refill_min;   // tuning knob: idle lanes that trigger a refill (closest-hit refill kernel)
+extern int g_wf_refill_min;
+extern int g_wf_prim_lane;     // tuning knob: 1 = primary rays take the per-lane pair traversal   // tuning knob: idle lanes that trigger a refill (closest-hit refill kernel)
 extern int g_wf_skip_shadow;  // tuning knob: 1 = the fast path leaves out shadow rays that cannot change the colour
 
 // Work counters of the trace kernels, one row per wave slot (wave id mod

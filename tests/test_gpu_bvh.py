@@ -278,3 +278,16 @@ def test_frames_in_flight_bitwise(rt, n_streams, kind):
     for f in range(frames):
         assert bufs[f].cpu().numpy().tobytes() == full.tobytes(), f
         assert sh[f].cpu().numpy().tobytes() == full[rows8].tobytes(), f
+
+
+def test_primary_per_lane_knob_bitwise(rt):
+    """Primary rays through the per-lane pair traversal (knob prim_lane) give
+    the exhaustive frame, like the default wave (packet) traversal."""
+    w, cam, depth = _glass_cluster(rt, n=250, seed=23, inside=False)
+    exact, _ = cam.render(w, depth, want_stats=True)
+    rt._rtamd._tuning_set("prim_lane", 1)
+    try:
+        fast, _ = cam.render(w, depth, want_stats=False)
+    finally:
+        rt._rtamd._tuning_set("prim_lane", 0)
+    assert fast.to_numpy().tobytes() == exact.to_numpy().tobytes()
