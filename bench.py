@@ -245,7 +245,7 @@ def main():
                 rs.wait_stream(gs)
                 with torch.cuda.stream(rs):
                     torch.index_select(gbufs[k], 0, perm, out=canv[k])
-            fa.submit(s)  # 1 GPU: the shard buffer already is the row-major canvas
+            fa.submit(s)  # 1 GPU: the slot is the canvas; N GPUs: gather + un-interleave on this frame's stream
             frame_no[0] = s + 1
             return
         slot = s % len(fa.shards)
