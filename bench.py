@@ -34,14 +34,57 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [REPO, os.path.join(REPO, "raytracer-challenge-rs_amd")]
 
+
+def _launch_ranks():
+    """`python bench.py --gpus N` (N > 1) outside a torch.distributed launcher:
+    start the N ranks ourselves, one fresh process per GPU, through
+    torch.distributed.run (the driver's own command line for N > 1), and exit
+    with its status. Runs before anything touches the GPU (the parent only
+    counts devices, which does not initialise HIP) and never re-execs itself.
+    Mirrors render_multithreaded owning its workers (camera.rs:150-217)."""
+    import socket
+    import subprocess
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--dry-launch", action="store_true")
+    a, _ = ap.parse_known_args()
+    if "WORLD_SIZE" in os.environ:
+        ws = int(os.environ["WORLD_SIZE"])
+        if a.gpus != ws:
+            sys.exit(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={ws} ranks")
+        return
+    import torch
+    visible = torch.cuda.device_count()  # counts devices without initialising HIP
+    if a.gpus > visible and not a.dry_launch:
+        sys.exit(f"bench.py: --gpus {a.gpus} but only {visible} GPU(s) are visible")
+    if a.gpus <= 1:
+        return
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
+
+
 # Frames in flight render on several streams (--inflight): give the process
 # enough hardware queues that they do not share one (HIP's default is 4; the
 # current stream, the render streams and RCCL's stream each want their own).
-# Read by the HIP runtime at initialisation, so before torch is imported.
+# Read by the HIP runtime at initialisation, so before torch is imported (and
+# before _launch_ranks counts the devices).
 # With N GPUs each render stream may also have a process group's RCCL stream.
 _queues = 8 if int(os.environ.get("WORLD_SIZE", "1") or 1) == 1 else 16
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < _queues:
     os.environ["GPU_MAX_HW_QUEUES"] = str(_queues)
+
+if __name__ == "__main__":
+    _launch_ranks()
+
+if "--dry-launch" in sys.argv and __name__ == "__main__":  # dev/test: report the rank layout, touch no GPU
+    print(json.dumps({"dry_launch": True, "rank": int(os.environ.get("RANK", "0")),
+                      "world_size": int(os.environ.get("WORLD_SIZE", "1")),
+                      "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}), flush=True)
+    sys.exit(0)
 
 import torch  # noqa: E402  (load torch's HIP runtime first: see rtamd/__init__.py)
 import torch.distributed as dist  # noqa: E402
@@ -107,46 +150,106 @@ def parse():
     p.add_argument("--knob", action="append", default=[], help="library tuning knob k=v (dev; see rt_api.cpp)")
     p.add_argument("--exhaustive", action="store_true",
                    help="disable the exact-culling BVH: every ray tests every shape (the reference's loop)")
-    p.add_argument("--pmc-summary", default=os.path.join(REPO, "profiles", "r01_pmc_summary.json"),
-                   help="HBM traffic per launch measured by rocprofv3 --pmc for this workload")
+    p.add_argument("--pmc-summary", default=None,
+                   help="HBM traffic per launch measured by rocprofv3 --pmc for this workload "
+                        "(default: the newest profiles/r*_pmc_summary*.json that matches it)")
+    p.add_argument("--no-verify-frames", action="store_true",
+                   help="dev: skip the bitwise check of the last timed frame against the exhaustive frame")
+    p.add_argument("--no-end-to-end", action="store_true",
+                   help="dev: skip the host-canvas + PPM timing of the drop-in entry point")
+    p.add_argument("--dry-launch", action="store_true",
+                   help="test: each rank prints its RANK/WORLD_SIZE and exits without touching a GPU")
     return p.parse_args()
 
 
+def host_cores():
+    """CPUs this process may use: its affinity set, capped by a cgroup CPU quota
+    (cpu.max) when one is set. `os.cpu_count()` is the whole machine."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(world, cam, depth, budget_s):
-    """Oracle (C port of the reference algorithm, threads in row blocks like
-    render_multithreaded) on evenly spaced rows, sized to ~budget_s."""
+    """Oracle (C port of the reference algorithm: full intersection list + sort
+    + containers walk, recursive color_at) on evenly spaced rows, threads in
+    contiguous row blocks like render_multithreaded (camera.rs:157-172): on
+    every core this process may use, and on one core. Each sample is sized to
+    ~budget_s (the one-core sample to a third of it)."""
     from oracle import pyoracle
     ow = pyoracle.OracleWorld.from_world(world)
-    nthreads = max(1, min(16, os.cpu_count() or 1))
     desc = cam.desc_bytes()
+    H = cam.vsize
 
-    def run(rows):
+    def run(rows, nthreads):
         t0 = time.perf_counter()
         _, st = ow.render_rows(desc, depth, rows, nthreads)
         dt = time.perf_counter() - t0
         return dt, st["rays_primary"] + st["rays_reflect"] + st["rays_refract"] + st["rays_shadow"]
 
-    H = cam.vsize
-    # calibrate: one row per thread, spread over the frame
-    probe = [int((i + 0.5) * H / nthreads) for i in range(nthreads)]
-    t_probe, r_probe = run(probe)
-    if t_probe >= 0.5 * budget_s:  # slow rows (C5): the probe already is the sample
-        rows, dt, rays = probe, t_probe, r_probe
-        stride = max(1, H // len(probe))
-    else:
-        n_rows = int(max(1, min(H, nthreads * budget_s / max(t_probe, 1e-6))))
+    def sample(nthreads, budget):
+        # calibrate: one row per thread, spread over the frame
+        probe = sorted({int((i + 0.5) * H / nthreads) for i in range(min(nthreads, H))})
+        t_probe, r_probe = run(probe, nthreads)
+        if t_probe >= 0.5 * budget:  # slow rows (C5): the probe already is the sample
+            return probe, t_probe, r_probe, max(1, H // len(probe))
+        n_rows = int(max(1, min(H, len(probe) * budget / max(t_probe, 1e-6))))
         stride = max(1, H // n_rows)
         rows = list(range(stride // 2, H, stride))
-        dt, rays = run(rows)
+        dt, rays = run(rows, nthreads)
+        return rows, dt, rays, stride
+
+    nthreads = host_cores()
+    rows, dt, rays, stride = sample(nthreads, budget_s)
+    rows1, dt1, rays1, stride1 = sample(1, budget_s / 3)
     return {
         "value": rays / dt / 1e6,
         "unit": "Mrays/s",
         "cores": nthreads,
         "kind": "port",
+        "cpu_model": cpu_model(),
+        "cpus_on_host": os.cpu_count(),
+        "single_core": {"value": rays1 / dt1 / 1e6, "unit": "Mrays/s", "cores": 1,
+                        "sample": f"{len(rows1)} of {H} rows (every {stride1}th), {rays1} rays in {dt1:.2f}s"},
         "sample": f"{len(rows)} of {H} rows (every {stride}th), {rays} rays in {dt:.2f}s; "
                   f"C restatement of the reference algorithm (oracle/rt_oracle.c: full intersection list + "
-                  f"sort + containers walk, recursion depth {depth}), {nthreads} threads in row blocks",
+                  f"sort + containers walk, recursion depth {depth}), {nthreads} threads in row blocks "
+                  f"(every CPU this process may use: affinity set, cgroup quota)",
     }
+
+
+def end_to_end(world, cam, depth, frames=3):
+    """The drop-in entry point as a caller sees it: `rt_render` (Camera::render,
+    camera.rs:133-148: device render + the canvas copied to a host buffer) and
+    `rt_canvas_to_ppm` (image/ppm.rs:24-51), per frame, one frame at a time."""
+    cam.render(world, depth, want_stats=False)  # calibrates the scene's own workspace
+    t0 = time.perf_counter()
+    for _ in range(frames):
+        canvas, _ = cam.render(world, depth, want_stats=False)
+    t_render = (time.perf_counter() - t0) / frames
+    arr = canvas.to_numpy()
+    t0 = time.perf_counter()
+    ppm = rtamd.canvas_to_ppm(arr)
+    t_ppm = time.perf_counter() - t0
+    return {"ms_render_to_host": round(t_render * 1e3, 3), "ms_canvas_to_ppm": round(t_ppm * 1e3, 3),
+            "ppm_bytes": len(ppm), "frames": frames,
+            "note": "rt_render (device render + 50 MB device-to-host copy of the f64 canvas, one frame at a time) "
+                    "and rt_canvas_to_ppm on the host; not the headline value"}
 
 
 def main():
@@ -154,8 +257,8 @@ def main():
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if a.gpus != world_size and world_size > 1:
-        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world_size}; using WORLD_SIZE", file=sys.stderr)
+    if a.gpus != world_size:  # _launch_ranks starts N ranks for --gpus N; never fall back silently
+        sys.exit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE {world_size}")
     n = world_size
     srank, sn = rank, n  # the shard this process renders
     if a.fake_shard:
@@ -267,7 +370,11 @@ def main():
 
     # exact work counters of one frame (deterministic), from a counted warm-up launch
     # (this first launch also sizes the wavefront queues of this camera/shard)
-    st = cam.render_shard_device(world, depth, B, srank, sn, shard.data_ptr(), stream.cuda_stream, True)
+    st = cam.render_shard_device(world, depth, B, srank, sn, shard.data_ptr(), stream.cuda_stream, True,
+                                 exhaustive=True)
+    assert st["exhaustive"]
+    # the exhaustive frame (the reference's every-shape loop) that the timed fast-path frames must equal
+    ref_shard = shard.clone()
     counts = torch.tensor([st["rays_primary"], st["rays_reflect"], st["rays_refract"], st["rays_shadow"],
                            st["sphere_tests"], st["plane_tests"], st["sphere_disc_ge0"]],
                           dtype=torch.float64, device=dev)
@@ -304,6 +411,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    # Parity of the timed frames (outside the timed region): the last frame each
+    # rank rendered, and rank 0's assembled canvas, must equal the exhaustive frame
+    # bit for bit (camera.rs:133-148 renders every pixel with the every-shape loop).
+    parity = None if a.no_verify_frames else verify_frames(fa, last, ref_shard, frame_no[0] - 1, n, rank, H)
     # Serialized pass (outside the timed region): the same K frames one after the
     # other on one stream, every launch carrying its own start/stop HIP events
     # (hipExtLaunchKernel), for the roofline's per-launch kernel time and the
@@ -324,6 +435,17 @@ def main():
         print(f"verify: assembled frame {'==' if same else '!='} whole-frame render", file=sys.stderr, flush=True)
         if not same:
             raise SystemExit("verify failed: the assembled frame differs from the whole-frame render")
+    # the fast path's own counters (what the kernels traced), one frame
+    fst = cam.render_shard_device(world, depth, B, srank, sn, shard.data_ptr(), stream.cuda_stream, True,
+                                  exhaustive=False)
+    traced = torch.tensor([fst["rays_primary"] + fst["rays_reflect"] + fst["rays_refract"] + fst["rays_shadow_traced"],
+                           fst["sphere_tests_executed"], fst["box_tests_executed"],
+                           fst["rays_primary"] + fst["rays_reflect"] + fst["rays_refract"] + fst["rays_shadow"]],
+                          dtype=torch.float64, device=dev)
+    if n > 1:
+        dist.all_reduce(traced)
+    assert float(traced[3]) == rays_per_frame, "fast-path reference ray count differs from the exhaustive count"
+    traced_rays = float(traced[0])
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if n > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -358,15 +480,63 @@ def main():
                 "assembler": type(fa).__name__ if n > 1 else None,
             },
             "roofline": roofline(prof, breakdown, W, H, a, n, ref_work, elapsed / a.steps * 1e3),
+            "traced_rays_per_frame": int(traced_rays),
+            "traced_mrays_per_s": round(traced_rays * a.steps / elapsed / 1e6, 3),
+            "rays_note": "value counts the reference's rays (one per World::intersect call, world.rs:71,101), "
+                         "including shadow rays the fast path provably need not trace; traced_* counts what the "
+                         "kernels traced",
+            "parity": parity,
         }
+        if n == 1 and not a.no_end_to_end:
+            out["end_to_end"] = end_to_end(world, cam, depth)
         if n == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(world, cam, depth, a.cpu_seconds)
         print(json.dumps(out), flush=True)
+    if parity is not None and not parity["ok"]:
+        raise SystemExit("bench.py: the timed frames differ from the exhaustive frame")
     if n > 1:
         torch.cuda.synchronize()
         if hasattr(fa, "close"):
             fa.close()  # the per-stream RCCL communicators
         dist.destroy_process_group()
+
+
+def verify_frames(fa, last, ref_shard, last_step, n, rank, H):
+    """Bitwise parity of the benchmarked frames: every rank's last rendered
+    shard equals its exhaustive shard, and rank 0's last assembled canvas equals
+    the exhaustive shards gathered and un-interleaved the same way. Collective."""
+    own = bool(torch.equal(fa.slot(last_step), ref_shard))
+    canvas_ok = True
+    if n == 1:
+        canvas_ok = last is not None and bool(torch.equal(last, ref_shard[:H]))
+    else:
+        bufs = [torch.empty_like(ref_shard) for _ in range(n)] if rank == 0 else None
+        dist.gather(ref_shard, bufs, dst=0)
+        if rank == 0:
+            ref_canvas = torch.index_select(torch.cat(bufs), 0, fa.inv_idx)
+            canvas_ok = last is not None and bool(torch.equal(last, ref_canvas))
+    ok = torch.tensor([1.0 if (own and canvas_ok) else 0.0], dtype=torch.float64, device=ref_shard.device)
+    if n > 1:
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    return {"vs_exhaustive": "bitwise", "ok": bool(ok[0] == 1.0),
+            "checked": "last timed frame: every rank's shard and rank 0's assembled canvas vs the exhaustive "
+                       "(every-shape loop) frame rendered before timing"}
+
+
+def pmc_summary_path(a, W, H, n):
+    """The newest committed PMC summary measured on this workload."""
+    if a.pmc_summary:
+        return a.pmc_summary
+    import glob
+    cands = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary*.json")), reverse=True)
+    for c in cands:
+        try:
+            pm = json.load(open(c))
+        except (OSError, ValueError):
+            continue
+        if (pm.get("width"), pm.get("height"), pm.get("spheres"), pm.get("n_gpus")) == (W, H, a.spheres, n):
+            return c
+    return ""
 
 
 def roofline(prof, breakdown, W, H, a, n, ref_work, frame_ms):
@@ -397,8 +567,15 @@ def roofline(prof, breakdown, W, H, a, n, ref_work, frame_ms):
                 "unit": "TFLOP/s", "frac": None, "traffic": None}
     ops = class_ops(dom)
     achieved = ops / (kernel_ms * 1e-3) / 1e12
+    # SURVEY.md §8(d)'s pricing of the same executed tests: 57 per sphere test, 34 per
+    # plane test, +6 per disc >= 0 (the reference's general 4x4 path; boxes unpriced)
+    survey_ops = (SURVEY_OPS_SPHERE * (prof["tests"][dom] + prof["rays"][dom] * ng)
+                  + SURVEY_OPS_PLANE * prof["rays"][dom] * npl + SURVEY_OPS_ROOTS * prof["disc"][dom])
+    achieved_survey = survey_ops / (kernel_ms * 1e-3) / 1e12
     traffic, traffic_src, counters = None, None, None
-    if os.path.exists(a.pmc_summary):
+    pmc_path = pmc_summary_path(a, W, H, n)
+    if pmc_path and os.path.exists(pmc_path):
+        a.pmc_summary = pmc_path
         try:
             pm = json.load(open(a.pmc_summary))
             if (pm.get("width"), pm.get("height"), pm.get("spheres"), pm.get("n_gpus"), pm.get("kernel_class"),
@@ -421,6 +598,10 @@ def roofline(prof, breakdown, W, H, a, n, ref_work, frame_ms):
         "peak": PEAK_F64_VALU_TFLOPS,
         "unit": "TFLOP/s",
         "frac": round(achieved / PEAK_F64_VALU_TFLOPS, 4),
+        "achieved_survey": round(achieved_survey, 3),
+        "frac_survey": round(achieved_survey / PEAK_F64_VALU_TFLOPS, 4),
+        "survey_pricing": "SURVEY.md §8(d): 57 f64 ops per executed sphere test, 34 per plane test, +6 per "
+                          "disc >= 0; box tests unpriced",
         "traffic": traffic,
         "kernel_ms": round(kernel_ms, 4),
         "kernel_ms_source": ms_src,

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 /* ---- status codes ------------------------------------------------------ */
 enum {
@@ -108,8 +108,20 @@ typedef struct rt_camera_desc {
   double inverse[16]; /* Camera::transform_inverse */
 } rt_camera_desc;
 
-/* Exact work counters. One "ray" = one `World::intersect` invocation
- * (world.rs:71 for radiance rays, world.rs:101 for shadow rays). */
+/* Work counters of one render call. One "ray" = one `World::intersect`
+ * invocation of the reference (world.rs:71 for radiance rays, world.rs:101
+ * for shadow rays); the `rays_*` and `*_tests` fields count the REFERENCE's
+ * work and are exact on every path. The renders always run the fast path
+ * (exact-culling BVH, shadow rays that cannot change a colour left out)
+ * unless RT_RENDER_EXHAUSTIVE is passed to an `_ex` entry point; asking for
+ * stats never changes the algorithm.
+ *   sphere_tests / plane_tests / other_tests: the reference's loop tests
+ *     every shape for every ray (world.rs:31-38), so these are rays x shapes.
+ *   sphere_disc_ge0: sphere tests with disc >= 0 in the reference's loop.
+ *     Only the exhaustive loop evaluates every one: RT_STATS_NOT_COUNTED on
+ *     the fast path.
+ *   *_traced / *_executed (ABI 3): what the kernels actually did. */
+#define RT_STATS_NOT_COUNTED UINT64_MAX
 typedef struct rt_stats {
   uint64_t rays_primary;
   uint64_t rays_reflect;
@@ -121,7 +133,21 @@ typedef struct rt_stats {
   uint64_t other_tests; /* Cube / Cylinder / Cone local_intersect calls */
   double ms_kernel; /* device time of the render kernel(s), HIP events */
   double ms_total;  /* wall time of the call */
+  /* ABI 3 */
+  uint64_t rays_shadow_traced;    /* shadow rays the kernels traced (<= rays_shadow) */
+  uint64_t sphere_tests_executed; /* sphere tests the kernels executed (after culling) */
+  uint64_t box_tests_executed;    /* BVH child-box tests executed */
+  uint32_t exhaustive;            /* 1: rendered by the reference's every-shape loop */
+  uint32_t _pad;
 } rt_stats;
+
+/* Flags of the `_ex` render entry points. */
+enum {
+  /* Run the reference's every-shape loop (world.rs:31-38) instead of the
+   * exact-culling fast path: same image bit for bit, every counter exact
+   * (incl. sphere_disc_ge0), ~15x slower. For parity checks and counting. */
+  RT_RENDER_EXHAUSTIVE = 1
+};
 
 typedef struct rt_scene rt_scene; /* opaque: device-resident flattened World */
 
@@ -164,6 +190,11 @@ int rt_render_aa(const rt_scene* scene, const rt_camera_desc* camera,
                  uint32_t max_depth, uint32_t aa_samples, double* out_rgb,
                  rt_stats* stats);
 
+/* rt_render_aa with `flags` (RT_RENDER_*). */
+int rt_render_ex(const rt_scene* scene, const rt_camera_desc* camera,
+                 uint32_t max_depth, uint32_t aa_samples, uint32_t flags,
+                 double* out_rgb, rt_stats* stats);
+
 /* Device-resident shard render (used by multi-GPU and the benchmark).
  * Renders the rows y with (y / row_block) % n_shards == shard, in increasing
  * y order, into `d_out_rgb` (a DEVICE buffer on the scene's device holding
@@ -179,6 +210,13 @@ int rt_render_shard_device(const rt_scene* scene, const rt_camera_desc* camera,
                            uint32_t shard, uint32_t n_shards,
                            double* d_out_rgb, void* stream, rt_stats* stats);
 
+/* rt_render_shard_device with `flags` (RT_RENDER_*). */
+int rt_render_shard_device_ex(const rt_scene* scene, const rt_camera_desc* camera,
+                              uint32_t max_depth, uint32_t aa_samples,
+                              uint32_t row_block, uint32_t shard, uint32_t n_shards,
+                              uint32_t flags, double* d_out_rgb, void* stream,
+                              rt_stats* stats);
+
 /* Number of rows shard `shard` of `n_shards` owns (for sizing buffers). */
 uint32_t rt_shard_rows(uint32_t vsize, uint32_t row_block, uint32_t shard,
                        uint32_t n_shards);
@@ -187,6 +225,11 @@ uint32_t rt_shard_rows(uint32_t vsize, uint32_t row_block, uint32_t shard,
  * rays: n*6 doubles (origin xyz, direction xyz); out_rgb: n*3 doubles (host). */
 int rt_color_at_batch(const rt_scene* scene, const double* rays, size_t n,
                       uint32_t remaining, double* out_rgb, rt_stats* stats);
+
+/* rt_color_at_batch with `flags` (RT_RENDER_*). */
+int rt_color_at_batch_ex(const rt_scene* scene, const double* rays, size_t n,
+                         uint32_t remaining, uint32_t flags, double* out_rgb,
+                         rt_stats* stats);
 
 /* `World::is_shadowed(point, light)` (world.rs:95-105) for a batch of points
  * against light index `light`. out: n uint8 (1 = shadowed). */

@@ -23,10 +23,16 @@ class Stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in (
         "rays_primary", "rays_reflect", "rays_refract", "rays_shadow",
         "sphere_tests", "plane_tests", "sphere_disc_ge0", "other_tests")] + [
-        ("ms_kernel", ctypes.c_double), ("ms_total", ctypes.c_double)]
+        ("ms_kernel", ctypes.c_double), ("ms_total", ctypes.c_double)] + [
+        # ABI 3 (include/rt_render.h): what a GPU render executed; the oracle leaves them 0
+        (n, ctypes.c_uint64) for n in ("rays_shadow_traced", "sphere_tests_executed", "box_tests_executed")] + [
+        ("exhaustive", ctypes.c_uint32), ("_pad", ctypes.c_uint32)]
+    # the reference's work counters (what the oracle counts)
+    REFERENCE = ("rays_primary", "rays_reflect", "rays_refract", "rays_shadow",
+                 "sphere_tests", "plane_tests", "sphere_disc_ge0", "other_tests")
 
     def as_dict(self):
-        return {n: getattr(self, n) for n, _ in self._fields_ if not n.startswith("ms_")}
+        return {n: getattr(self, n) for n in self.REFERENCE}
 
 
 def build():

@@ -300,15 +300,17 @@ class Camera {
     return Ray(origin, (pixel - origin).normalize());
   }
   // camera.rs:133-148: the drop-in. `max_depth` = MAX_RECURSION_DEPTH (5).
-  Canvas render(const World& world, unsigned max_depth = 5, rt_stats* stats = nullptr) const {
+  // `flags`: RT_RENDER_EXHAUSTIVE runs the reference's every-shape loop (exact counters).
+  Canvas render(const World& world, unsigned max_depth = 5, rt_stats* stats = nullptr, uint32_t flags = 0) const {
     Canvas c(desc_.hsize, desc_.vsize);
-    check(rt_render(world.scene(), &desc_, max_depth, c.data(), stats), "rt_render");
+    check(rt_render_ex(world.scene(), &desc_, max_depth, 1, flags, c.data(), stats), "rt_render");
     return c;
   }
   // camera.rs:150-214: average of `rays_for_pixel` per pixel (render_opts.aa_samples).
-  Canvas render_multithreaded(const World& world, unsigned max_depth = 5, rt_stats* stats = nullptr) const {
+  Canvas render_multithreaded(const World& world, unsigned max_depth = 5, rt_stats* stats = nullptr,
+                              uint32_t flags = 0) const {
     Canvas c(desc_.hsize, desc_.vsize);
-    check(rt_render_aa(world.scene(), &desc_, max_depth, (uint32_t)render_opts.samples, c.data(), stats),
+    check(rt_render_ex(world.scene(), &desc_, max_depth, (uint32_t)render_opts.samples, flags, c.data(), stats),
           "rt_render_aa");
     return c;
   }

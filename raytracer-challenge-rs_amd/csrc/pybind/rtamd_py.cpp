@@ -21,11 +21,24 @@ static py::dict stats_dict(const rt_stats& s) {
   d["rays_shadow"] = s.rays_shadow;
   d["sphere_tests"] = s.sphere_tests;
   d["plane_tests"] = s.plane_tests;
-  d["sphere_disc_ge0"] = s.sphere_disc_ge0;
+  // None on the fast path: only the exhaustive loop evaluates every sphere test
+  if (s.sphere_disc_ge0 == RT_STATS_NOT_COUNTED) d["sphere_disc_ge0"] = py::none();
+  else d["sphere_disc_ge0"] = s.sphere_disc_ge0;
   d["other_tests"] = s.other_tests;
   d["ms_kernel"] = s.ms_kernel;
   d["ms_total"] = s.ms_total;
+  d["rays_shadow_traced"] = s.rays_shadow_traced;
+  d["sphere_tests_executed"] = s.sphere_tests_executed;
+  d["box_tests_executed"] = s.box_tests_executed;
+  d["exhaustive"] = (bool)s.exhaustive;
   return d;
+}
+
+// The `exhaustive` keyword of the render bindings: None follows want_stats (the
+// counted reference loop, whose counters the tests compare with the oracle's).
+static uint32_t render_flags(bool want_stats, const py::object& exhaustive) {
+  const bool ex = exhaustive.is_none() ? want_stats : exhaustive.cast<bool>();
+  return ex ? (uint32_t)RT_RENDER_EXHAUSTIVE : 0u;
 }
 
 static py::bytes pod_bytes(const void* p, size_t n) { return py::bytes((const char*)p, n); }
@@ -40,7 +53,9 @@ static py::array_t<double> check_rays(py::array_t<double, py::array::c_style | p
 extern "C" int rtamd_tuning_set(const char* key, int value);
 extern "C" int rtamd_stream_create(int cu_masked, void** out);
 extern "C" int rtamd_nccl_unique_id(unsigned char* out, size_t size);
-extern "C" int rtamd_nccl_comm_init(int nranks, const unsigned char* id, size_t size, int rank, int device, void** comm);
+extern "C" int rtamd_nccl_comm_init(int nranks, const unsigned char* id, size_t size, int rank, int device,
+                                    int timeout_ms, void** comm);
+extern "C" int rtamd_nccl_comm_abort(void* comm);
 extern "C" int rtamd_nccl_gather_f64(const double* send, double* recv, size_t count, int root, void* comm, void* stream);
 extern "C" int rtamd_nccl_comm_destroy(void* comm);
 extern "C" int rtamd_wf_profile(const rt_scene* s, int enable, double out[29]);
@@ -267,18 +282,20 @@ PYBIND11_MODULE(_rtamd, m) {
         return pod_bytes(l.data(), l.size() * sizeof(rt_light_desc));
       })
       .def("color_at_batch", [](const World& w, py::array_t<double, py::array::c_style | py::array::forcecast> rays,
-                                unsigned remaining, bool want_stats) {
+                                unsigned remaining, bool want_stats, py::object exhaustive) {
         check_rays(rays, 6);
         const size_t n = (size_t)rays.shape(0);
         py::array_t<double> out({(py::ssize_t)n, (py::ssize_t)3});
         rt_stats st{};
+        const uint32_t flags = render_flags(want_stats, exhaustive);
         {
           py::gil_scoped_release nogil;
-          check(rt_color_at_batch(w.scene(), rays.data(), n, remaining, out.mutable_data(), want_stats ? &st : nullptr),
+          check(rt_color_at_batch_ex(w.scene(), rays.data(), n, remaining, flags, out.mutable_data(),
+                                     want_stats ? &st : nullptr),
                 "rt_color_at_batch");
         }
         return py::make_tuple(out, stats_dict(st));
-      }, py::arg("rays"), py::arg("remaining") = 5, py::arg("want_stats") = true)
+      }, py::arg("rays"), py::arg("remaining") = 5, py::arg("want_stats") = true, py::arg("exhaustive") = py::none())
       .def("hit_batch", [](const World& w, py::array_t<double, py::array::c_style | py::array::forcecast> rays) {
         check_rays(rays, 6);
         const size_t n = (size_t)rays.shape(0);
@@ -305,40 +322,47 @@ PYBIND11_MODULE(_rtamd, m) {
       .def_property_readonly("field_of_view", &Camera::field_of_view)
       .def("ray_for_pixel", &Camera::ray_for_pixel)
       .def("desc_bytes", [](const Camera& c) { return pod_bytes(&c.desc(), sizeof(rt_camera_desc)); })
-      // want_stats: exact (exhaustive) counters; False runs the fast path (BVH traversal)
-      .def("render", [](const Camera& c, const World& w, unsigned max_depth, bool want_stats) {
+      // want_stats: return the counters. exhaustive: run the reference's every-shape loop
+      // (RT_RENDER_EXHAUSTIVE: exact sphere_disc_ge0 too); None = the same as want_stats, so
+      // render(w) is the counted reference loop and render(w, want_stats=False) the fast path
+      .def("render", [](const Camera& c, const World& w, unsigned max_depth, bool want_stats, py::object exhaustive) {
         rt_stats st{};
         Canvas* out;
+        const uint32_t flags = render_flags(want_stats, exhaustive);
         {
           py::gil_scoped_release nogil;
-          out = new Canvas(c.render(w, max_depth, want_stats ? &st : nullptr));
+          out = new Canvas(c.render(w, max_depth, want_stats ? &st : nullptr, flags));
         }
         return py::make_tuple(std::unique_ptr<Canvas>(out), stats_dict(st));
-      }, py::arg("world"), py::arg("max_depth") = 5, py::arg("want_stats") = true)
+      }, py::arg("world"), py::arg("max_depth") = 5, py::arg("want_stats") = true, py::arg("exhaustive") = py::none())
       .def_readwrite("render_opts", &Camera::render_opts, py::return_value_policy::reference_internal)
-      .def("render_multithreaded", [](const Camera& c, const World& w, unsigned max_depth, bool want_stats) {
+      .def("render_multithreaded", [](const Camera& c, const World& w, unsigned max_depth, bool want_stats,
+                                      py::object exhaustive) {
         rt_stats st{};
         Canvas* out;
+        const uint32_t flags = render_flags(want_stats, exhaustive);
         {
           py::gil_scoped_release nogil;
-          out = new Canvas(c.render_multithreaded(w, max_depth, want_stats ? &st : nullptr));
+          out = new Canvas(c.render_multithreaded(w, max_depth, want_stats ? &st : nullptr, flags));
         }
         return py::make_tuple(std::unique_ptr<Canvas>(out), stats_dict(st));
-      }, py::arg("world"), py::arg("max_depth") = 5, py::arg("want_stats") = true)
+      }, py::arg("world"), py::arg("max_depth") = 5, py::arg("want_stats") = true, py::arg("exhaustive") = py::none())
       .def("render_shard_device", [](const Camera& c, const World& w, unsigned max_depth, unsigned row_block,
                                      unsigned shard, unsigned n_shards, uintptr_t d_out, uintptr_t stream,
-                                     bool want_stats, unsigned aa_samples) {
+                                     bool want_stats, unsigned aa_samples, py::object exhaustive) {
         rt_stats st{};
         int rc;
+        const uint32_t flags = render_flags(want_stats, exhaustive);
         {
           py::gil_scoped_release nogil;
-          rc = rt_render_shard_device(w.scene(), &c.desc(), max_depth, aa_samples, row_block, shard, n_shards,
-                                      (double*)d_out, (void*)stream, want_stats ? &st : nullptr);
+          rc = rt_render_shard_device_ex(w.scene(), &c.desc(), max_depth, aa_samples, row_block, shard, n_shards,
+                                         flags, (double*)d_out, (void*)stream, want_stats ? &st : nullptr);
         }
         check(rc, "rt_render_shard_device");
         return stats_dict(st);
       }, py::arg("world"), py::arg("max_depth"), py::arg("row_block"), py::arg("shard"), py::arg("n_shards"),
-         py::arg("d_out"), py::arg("stream") = 0, py::arg("want_stats") = false, py::arg("aa_samples") = 1)
+         py::arg("d_out"), py::arg("stream") = 0, py::arg("want_stats") = false, py::arg("aa_samples") = 1,
+         py::arg("exhaustive") = py::none())
       .def("render_multi", [](const Camera& c, std::vector<World*> worlds, unsigned max_depth, unsigned row_block,
                               unsigned aa_samples) {
         std::vector<rt_scene*> sc;
@@ -409,15 +433,18 @@ PYBIND11_MODULE(_rtamd, m) {
     check(rtamd_nccl_unique_id((unsigned char*)&id[0], id.size()), "nccl unique id");
     return py::bytes(id);
   });
-  m.def("_nccl_comm_init", [](int nranks, py::bytes id, int rank, int device) {
+  m.def("_nccl_comm_init", [](int nranks, py::bytes id, int rank, int device, int timeout_ms) {
     std::string s = id;
     void* comm = nullptr;
+    int rc;
     {
       py::gil_scoped_release nogil;
-      check(rtamd_nccl_comm_init(nranks, (const unsigned char*)s.data(), s.size(), rank, device, &comm), "nccl comm init");
+      rc = rtamd_nccl_comm_init(nranks, (const unsigned char*)s.data(), s.size(), rank, device, timeout_ms, &comm);
     }
+    check(rc, "nccl comm init");
     return (uintptr_t)comm;
-  });
+  }, py::arg("nranks"), py::arg("id"), py::arg("rank"), py::arg("device"), py::arg("timeout_ms") = 60000);
+  m.def("_nccl_comm_abort", [](uintptr_t comm) { check(rtamd_nccl_comm_abort((void*)comm), "nccl comm abort"); });
   m.def("_nccl_gather_f64", [](uintptr_t send, uintptr_t recv, size_t count, int root, uintptr_t comm, uintptr_t stream) {
     check(rtamd_nccl_gather_f64((const double*)send, (double*)recv, count, root, (void*)comm, (void*)stream), "nccl gather");
   });

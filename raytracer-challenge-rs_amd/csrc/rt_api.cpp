@@ -16,6 +16,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rt_render.h"
@@ -75,6 +76,26 @@ struct rt_scene {
   unsigned long long tick = 0;
   WfSlot* last_wf = nullptr;
   bool prof_on = false;
+  // rt_render_multi's communicators and buffers, cached on scenes[0]
+  struct MultiCache {
+    std::vector<rt_scene*> scenes;
+    std::vector<ncclComm_t> comms;
+    std::vector<double*> send;
+    std::vector<size_t> send_cap;
+    double* recv = nullptr;  // on device 0
+    size_t recv_cap = 0;
+    void release() {
+      for (size_t i = 0; i < send.size(); ++i) {
+        (void)hipSetDevice((int)i);
+        if (send[i]) (void)hipFree(send[i]);
+        if (i < comms.size() && comms[i]) (void)ncclCommDestroy(comms[i]);
+      }
+      (void)hipSetDevice(0);
+      if (recv) (void)hipFree(recv);
+      *this = MultiCache{};
+    }
+  } multi;
+  std::mutex multi_mu;
   int prof_mask = (1 << WF_NCLASS) - 1;
   int n_objects = 0, n_lights = 0;
   ~rt_scene() {
@@ -196,15 +217,33 @@ bool valid_aa(uint32_t aa) { return aa == 1 || aa == 2 || aa == 4 || aa == 8 || 
 // wavefront pipeline. `n_tasks` root rays = pixels x aa (camera) or rays
 // (batch). `stats_out`, when given, receives the exact counters and
 // `ms_out` the kernel time (both synchronise).
+// A workspace whose device-side queue check failed (Wavefront::fault) fails
+// the call that finds it; the check raised it for an earlier, asynchronous
+// frame. The calibration is dropped, so the next frame recalibrates.
+int check_faults(rt_scene* s) {
+  for (rt_scene::WfSlot& w : s->wfs)
+    if (w.wf->fault()) {
+      w.wf->clear_fault();
+      return fail(RT_ERR_HIP, "wavefront queue check: a generation's ray count differed from its calibrated "
+                              "launch size in an earlier frame (rays may be missing from that frame)");
+    }
+  return RT_OK;
+}
+
 int run_render(rt_scene* s, const DevCamera& cam, const double* d_rays, uint32_t n_tasks, uint32_t aa,
                uint32_t max_depth, uint32_t row_block, uint32_t shard, uint32_t n_shards, double* d_out,
-               hipStream_t stream, DevStats* stats_out = nullptr, float* ms_out = nullptr) {
+               hipStream_t stream, DevStats* stats_out = nullptr, float* ms_out = nullptr, uint32_t flags = 0,
+               rt_scene::WfSlot** used = nullptr) {
   if (max_depth > (uint32_t)kMaxDepth)
     return fail(RT_ERR_INVALID_ARGUMENT, "max_depth > " + std::to_string(kMaxDepth));
   if (!valid_aa(aa)) return fail(RT_ERR_INVALID_ARGUMENT, "aa_samples must be 1, 2, 4, 8 or 16");
+  if (flags & ~(uint32_t)RT_RENDER_EXHAUSTIVE) return fail(RT_ERR_INVALID_ARGUMENT, "unknown render flags");
+  int rc = check_faults(s);
+  if (rc != RT_OK) return rc;
   if (n_tasks == 0) {
     if (stats_out) *stats_out = DevStats{};
     if (ms_out) *ms_out = 0.f;
+    if (used) *used = nullptr;
     return RT_OK;
   }
   std::string sig;
@@ -215,15 +254,23 @@ int run_render(rt_scene* s, const DevCamera& cam, const double* d_rays, uint32_t
   }
   rt_scene::WfSlot* w = nullptr;
   hipError_t e = s->acquire(stream, &w);
+  const unsigned wf_flags = ((flags & RT_RENDER_EXHAUSTIVE) ? WF_EXHAUSTIVE : 0u) | (used ? WF_COUNT : 0u);
   if (e == hipSuccess)
     e = w->wf->render(s->dev, cam, d_rays == nullptr, d_rays, n_tasks, aa, max_depth, row_block, shard, n_shards,
-                      d_out, stream, sig, stats_out, ms_out, s->wfs.size() == 1);
+                      d_out, stream, sig, stats_out, ms_out, s->wfs.size() == 1, wf_flags);
   if (e == hipSuccess) e = hipEventRecord(w->done, stream);
   if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("wavefront render: ") + hipGetErrorString(e));
+  if (used) *used = w;
+  if (stats_out || ms_out) return check_faults(s);  // synchronised: this frame's check has run
   return RT_OK;
 }
 
 void fill_stats(rt_stats* st, const DevStats& ds, float ms_kernel, double ms_total) {
+  std::memset(st, 0, sizeof *st);
+  st->rays_shadow_traced = ds.rays_shadow_traced;
+  st->sphere_tests_executed = ds.sphere_tests_executed;
+  st->box_tests_executed = ds.box_tests_executed;
+  st->exhaustive = ds.exhaustive;
   st->rays_primary = ds.rays_primary;
   st->rays_reflect = ds.rays_reflect;
   st->rays_refract = ds.rays_refract;
@@ -343,6 +390,10 @@ int rtamd_tuning_set(const char* key, int value) {
     rtamd::g_wf_skip_shadow = value != 0;
     return RT_OK;
   }
+  if (key && std::strcmp(key, "corrupt_calibration") == 0) {  // test hook: exercises the queue check
+    rtamd::Wavefront::g_corrupt_calibration = value != 0;
+    return RT_OK;
+  }
   if (key && std::strcmp(key, "accel") == 0) {
     rtamd::g_wf_accel = value != 0;
     return RT_OK;
@@ -394,25 +445,55 @@ int rtamd_nccl_unique_id(unsigned char* out, size_t size) {
   std::memcpy(out, &id, sizeof id);
   return RT_OK;
 }
-int rtamd_nccl_comm_init(int nranks, const unsigned char* id, size_t size, int rank, int device, void** comm) {
-  if (!id || !comm || size < sizeof(ncclUniqueId) || nranks < 1 || rank < 0 || rank >= nranks)
+// The communicator is created non-blocking and waited for at most `timeout_ms`,
+// so a rank whose peers failed before joining does not hang: it aborts the
+// half-made communicator and returns RT_ERR_RCCL, and the caller's agreement
+// step (RcclStreamAssembler) sends every rank to the fallback together.
+namespace {
+ncclResult_t nccl_wait(ncclComm_t c, ncclResult_t r, int timeout_ms) {
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+  while (r == ncclInProgress) {
+    if (std::chrono::steady_clock::now() > deadline) return ncclInProgress;
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+    if (ncclCommGetAsyncError(c, &r) != ncclSuccess) return ncclInternalError;
+  }
+  return r;
+}
+}  // namespace
+int rtamd_nccl_comm_init(int nranks, const unsigned char* id, size_t size, int rank, int device, int timeout_ms,
+                         void** comm) {
+  if (!id || !comm || size < sizeof(ncclUniqueId) || nranks < 1 || rank < 0 || rank >= nranks || timeout_ms < 1)
     return fail(RT_ERR_INVALID_ARGUMENT, "bad communicator arguments");
+  *comm = nullptr;
   RT_HIP(hipSetDevice(device));
   ncclUniqueId uid;
   std::memcpy(&uid, id, sizeof uid);
   ncclComm_t c = nullptr;
-  if (ncclCommInitRank(&c, nranks, uid, rank) != ncclSuccess) return fail(RT_ERR_RCCL, "ncclCommInitRank");
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
+  ncclResult_t r = ncclCommInitRankConfig(&c, nranks, uid, rank, &cfg);
+  if (c && (r == ncclSuccess || r == ncclInProgress)) r = nccl_wait(c, r, timeout_ms);
+  if (r != ncclSuccess) {
+    if (c) (void)ncclCommAbort(c);
+    return fail(RT_ERR_RCCL, r == ncclInProgress ? "ncclCommInitRankConfig: timed out" : "ncclCommInitRankConfig");
+  }
   *comm = c;
   return RT_OK;
 }
 int rtamd_nccl_gather_f64(const double* send, double* recv, size_t count, int root, void* comm, void* stream) {
   if (!send || !comm) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
-  if (ncclGather(send, recv, count, ncclDouble, root, (ncclComm_t)comm, (hipStream_t)stream) != ncclSuccess)
-    return fail(RT_ERR_RCCL, "ncclGather");
+  ncclResult_t r = ncclGather(send, recv, count, ncclDouble, root, (ncclComm_t)comm, (hipStream_t)stream);
+  // a non-blocking communicator may still be connecting: the enqueue completes in the background
+  if (r == ncclInProgress) r = nccl_wait((ncclComm_t)comm, r, 120000);
+  if (r != ncclSuccess) return fail(RT_ERR_RCCL, "ncclGather");
   return RT_OK;
 }
 int rtamd_nccl_comm_destroy(void* comm) {
   if (comm && ncclCommDestroy((ncclComm_t)comm) != ncclSuccess) return fail(RT_ERR_RCCL, "ncclCommDestroy");
+  return RT_OK;
+}
+int rtamd_nccl_comm_abort(void* comm) {
+  if (comm && ncclCommAbort((ncclComm_t)comm) != ncclSuccess) return fail(RT_ERR_RCCL, "ncclCommAbort");
   return RT_OK;
 }
 int rt_abi_version(void) { return RT_ABI_VERSION; }
@@ -636,6 +717,8 @@ void rt_scene_destroy(rt_scene* s) {
   if (!s) return;
   (void)hipSetDevice(s->device);
   if (s->stream) (void)hipStreamSynchronize(s->stream);
+  s->multi.release();
+  (void)hipSetDevice(s->device);
   if (s->d_blob) (void)hipFree(s->d_blob);
   if (s->d_out) (void)hipFree(s->d_out);
   if (s->d_in) (void)hipFree(s->d_in);
@@ -656,6 +739,13 @@ uint32_t rt_shard_rows(uint32_t vsize, uint32_t row_block, uint32_t shard, uint3
 int rt_render_shard_device(const rt_scene* scene, const rt_camera_desc* camera, uint32_t max_depth,
                            uint32_t aa_samples, uint32_t row_block, uint32_t shard, uint32_t n_shards,
                            double* d_out_rgb, void* stream, rt_stats* stats) {
+  return rt_render_shard_device_ex(scene, camera, max_depth, aa_samples, row_block, shard, n_shards, 0, d_out_rgb,
+                                   stream, stats);
+}
+
+int rt_render_shard_device_ex(const rt_scene* scene, const rt_camera_desc* camera, uint32_t max_depth,
+                              uint32_t aa_samples, uint32_t row_block, uint32_t shard, uint32_t n_shards,
+                              uint32_t flags, double* d_out_rgb, void* stream, rt_stats* stats) {
   if (!scene || !camera || !d_out_rgb) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
   if (row_block == 0 || n_shards == 0 || shard >= n_shards)
     return fail(RT_ERR_INVALID_ARGUMENT, "bad shard specification");
@@ -671,7 +761,7 @@ int rt_render_shard_device(const rt_scene* scene, const rt_camera_desc* camera, 
   DevStats ds{};
   float ms = 0.f;
   int rc = run_render(s, to_dev_camera(*camera), nullptr, (uint32_t)n_tasks, aa_samples, max_depth, row_block, shard,
-                      n_shards, d_out_rgb, st, stats ? &ds : nullptr, stats ? &ms : nullptr);
+                      n_shards, d_out_rgb, st, stats ? &ds : nullptr, stats ? &ms : nullptr, flags);
   if (rc != RT_OK) return rc;
   if (stats)
     fill_stats(stats, ds, ms, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
@@ -680,6 +770,11 @@ int rt_render_shard_device(const rt_scene* scene, const rt_camera_desc* camera, 
 
 int rt_render_aa(const rt_scene* scene, const rt_camera_desc* camera, uint32_t max_depth, uint32_t aa_samples,
                  double* out_rgb, rt_stats* stats) {
+  return rt_render_ex(scene, camera, max_depth, aa_samples, 0, out_rgb, stats);
+}
+
+int rt_render_ex(const rt_scene* scene, const rt_camera_desc* camera, uint32_t max_depth, uint32_t aa_samples,
+                 uint32_t flags, double* out_rgb, rt_stats* stats) {
   if (!scene || !camera || !out_rgb) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
   if (camera->hsize == 0 || camera->vsize == 0) return fail(RT_ERR_INVALID_ARGUMENT, "empty camera");
   if (!valid_aa(aa_samples)) return fail(RT_ERR_INVALID_ARGUMENT, "aa_samples must be 1, 2, 4, 8 or 16");
@@ -694,10 +789,11 @@ int rt_render_aa(const rt_scene* scene, const rt_camera_desc* camera, uint32_t m
   DevStats ds{};
   float ms = 0.f;
   rc = run_render(s, to_dev_camera(*camera), nullptr, (uint32_t)(n_pix * aa_samples), aa_samples, max_depth,
-                  camera->vsize, 0, 1, s->d_out, s->stream, stats ? &ds : nullptr, &ms);
+                  camera->vsize, 0, 1, s->d_out, s->stream, stats ? &ds : nullptr, &ms, flags);
   if (rc != RT_OK) return rc;
   RT_HIP(hipMemcpyAsync(out_rgb, s->d_out, n_pix * 3 * sizeof(double), hipMemcpyDeviceToHost, s->stream));
   RT_HIP(hipStreamSynchronize(s->stream));
+  if ((rc = check_faults(s)) != RT_OK) return rc;
   if (stats)
     fill_stats(stats, ds, ms, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
   return RT_OK;
@@ -710,6 +806,11 @@ int rt_render(const rt_scene* scene, const rt_camera_desc* camera, uint32_t max_
 
 int rt_color_at_batch(const rt_scene* scene, const double* rays, size_t n, uint32_t remaining,
                       double* out_rgb, rt_stats* stats) {
+  return rt_color_at_batch_ex(scene, rays, n, remaining, 0, out_rgb, stats);
+}
+
+int rt_color_at_batch_ex(const rt_scene* scene, const double* rays, size_t n, uint32_t remaining, uint32_t flags,
+                         double* out_rgb, rt_stats* stats) {
   if (!scene || (n && (!rays || !out_rgb))) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
   if (n >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "batch too large");
   rt_scene* s = const_cast<rt_scene*>(scene);
@@ -725,7 +826,7 @@ int rt_color_at_batch(const rt_scene* scene, const double* rays, size_t n, uint3
   DevStats ds{};
   float ms = 0.f;
   rc = run_render(s, cam, s->d_in, (uint32_t)n, 1, remaining, 1, 0, 1, s->d_out, s->stream, stats ? &ds : nullptr,
-                  &ms);
+                  &ms, flags);
   if (rc != RT_OK) return rc;
   if (n) RT_HIP(hipMemcpyAsync(out_rgb, s->d_out, n * 3 * sizeof(double), hipMemcpyDeviceToHost, s->stream));
   RT_HIP(hipStreamSynchronize(s->stream));
@@ -772,12 +873,16 @@ int rt_hit_batch(const rt_scene* scene, const double* rays, size_t n, double* ou
   return RT_OK;
 }
 
-// Single-process multi-GPU render: interleaved row blocks, one RCCL gather.
+// Single-process multi-GPU render (the GPU form of `render_multithreaded`,
+// camera.rs:150-217): interleaved row blocks, one RCCL gather to device 0.
+// The communicators and device buffers are cached on scenes[0] across calls
+// (rt_scene::MultiCache) and rebuilt only when the scene set changes.
 int rt_render_multi(rt_scene* const* scenes, int n_devices, const rt_camera_desc* camera,
                     uint32_t max_depth, uint32_t aa_samples, uint32_t row_block, double* out_rgb,
                     rt_stats* stats) {
   if (!scenes || n_devices < 1 || !camera || !out_rgb || row_block == 0)
     return fail(RT_ERR_INVALID_ARGUMENT, "bad arguments");
+  if (camera->hsize == 0 || camera->vsize == 0) return fail(RT_ERR_INVALID_ARGUMENT, "empty camera");
   if (!valid_aa(aa_samples)) return fail(RT_ERR_INVALID_ARGUMENT, "aa_samples must be 1, 2, 4, 8 or 16");
   for (int i = 0; i < n_devices; ++i)
     if (!scenes[i] || scenes[i]->device != i)
@@ -786,98 +891,99 @@ int rt_render_multi(rt_scene* const* scenes, int n_devices, const rt_camera_desc
   const uint32_t W = camera->hsize, H = camera->vsize;
   uint32_t max_rows = 0;
   for (int i = 0; i < n_devices; ++i) max_rows = std::max(max_rows, rt_shard_rows(H, row_block, i, n_devices));
+  if ((uint64_t)max_rows * W * aa_samples >= (1ull << 31))
+    return fail(RT_ERR_INVALID_ARGUMENT, "shard too large for one launch");
   const size_t per = (size_t)max_rows * W * 3;  // padded per-rank element count
-  std::vector<double*> send(n_devices, nullptr);
-  double* recv = nullptr;
-  std::vector<ncclComm_t> comms(n_devices);
-  std::vector<int> devs(n_devices);
-  for (int i = 0; i < n_devices; ++i) devs[i] = i;
-  int rc = RT_OK;
-  bool comm_ok = false;
-  std::vector<rt_stats> st(n_devices);
-  auto body = [&]() -> int {
-    for (int i = 0; i < n_devices; ++i) {
-      RT_HIP(hipSetDevice(i));
-      RT_HIP(hipMalloc(&send[i], std::max<size_t>(per, 1) * sizeof(double)));
-      RT_HIP(hipMemsetAsync(send[i], 0, std::max<size_t>(per, 1) * sizeof(double), scenes[i]->stream));
-    }
-    RT_HIP(hipSetDevice(0));
-    RT_HIP(hipMalloc(&recv, std::max<size_t>(per * n_devices, 1) * sizeof(double)));
+  rt_scene* s0 = scenes[0];
+  std::lock_guard<std::mutex> mlk(s0->multi_mu);
+  rt_scene::MultiCache& mc = s0->multi;
+  const std::vector<rt_scene*> want(scenes, scenes + n_devices);
+  if (mc.scenes != want) {
+    mc.release();
+    mc.scenes = want;
+    mc.send.assign(n_devices, nullptr);
+    mc.send_cap.assign(n_devices, 0);
     if (n_devices > 1) {
-      if (ncclCommInitAll(comms.data(), n_devices, devs.data()) != ncclSuccess)
+      std::vector<int> devs(n_devices);
+      for (int i = 0; i < n_devices; ++i) devs[i] = i;
+      mc.comms.assign(n_devices, nullptr);
+      if (ncclCommInitAll(mc.comms.data(), n_devices, devs.data()) != ncclSuccess) {
+        mc.comms.clear();
+        mc.scenes.clear();
         return fail(RT_ERR_RCCL, "ncclCommInitAll failed");
-      comm_ok = true;
+      }
     }
+  }
+  for (int i = 0; i < n_devices; ++i) {
+    RT_HIP(hipSetDevice(i));
+    int rc = ensure_dev_buffer(&mc.send[i], &mc.send_cap[i], per);
+    if (rc != RT_OK) return rc;
+  }
+  RT_HIP(hipSetDevice(0));
+  int rc = ensure_dev_buffer(&mc.recv, &mc.recv_cap, per * n_devices);
+  if (rc != RT_OK) return rc;
+  // every device renders its shard (asynchronously, each on its scene's stream)
+  std::vector<rt_scene::WfSlot*> used(n_devices, nullptr);
+  for (int i = 0; i < n_devices; ++i) {
+    RT_HIP(hipSetDevice(i));
+    std::lock_guard<std::mutex> lk(scenes[i]->mu);
+    const uint32_t rows = rt_shard_rows(H, row_block, i, n_devices);
+    rc = run_render(scenes[i], to_dev_camera(*camera), nullptr, rows * W * aa_samples, aa_samples, max_depth,
+                    row_block, i, n_devices, mc.send[i], scenes[i]->stream, nullptr, nullptr, 0,
+                    stats ? &used[i] : nullptr);
+    if (rc != RT_OK) return rc;
+  }
+  if (n_devices > 1) {
+    if (ncclGroupStart() != ncclSuccess) return fail(RT_ERR_RCCL, "ncclGroupStart");
+    for (int i = 0; i < n_devices; ++i)
+      if (ncclGather(mc.send[i], i == 0 ? mc.recv : nullptr, per, ncclDouble, 0, mc.comms[i], scenes[i]->stream) !=
+          ncclSuccess) {
+        (void)ncclGroupEnd();
+        return fail(RT_ERR_RCCL, "ncclGather");
+      }
+    if (ncclGroupEnd() != ncclSuccess) return fail(RT_ERR_RCCL, "ncclGroupEnd");
+  } else {
+    RT_HIP(hipMemcpyAsync(mc.recv, mc.send[0], per * sizeof(double), hipMemcpyDeviceToDevice, scenes[0]->stream));
+  }
+  // device 0 holds every shard, rank-major: copy each row block straight into its canvas rows
+  RT_HIP(hipSetDevice(0));
+  for (int i = 0; i < n_devices; ++i) {
+    uint32_t lr = 0;
+    for (uint32_t blk = (uint32_t)i; (uint64_t)blk * row_block < H; blk += (uint32_t)n_devices) {
+      const uint32_t y0 = blk * row_block, nr = std::min(row_block, H - y0);
+      RT_HIP(hipMemcpyAsync(out_rgb + (size_t)y0 * W * 3, mc.recv + (size_t)i * per + (size_t)lr * W * 3,
+                            (size_t)nr * W * 3 * sizeof(double), hipMemcpyDeviceToHost, scenes[0]->stream));
+      lr += nr;
+    }
+  }
+  for (int i = 0; i < n_devices; ++i) {
+    RT_HIP(hipSetDevice(i));
+    RT_HIP(hipStreamSynchronize(scenes[i]->stream));
+  }
+  for (int i = 0; i < n_devices; ++i)
+    if ((rc = check_faults(scenes[i])) != RT_OK) return rc;
+  if (stats) {
+    std::memset(stats, 0, sizeof *stats);
     for (int i = 0; i < n_devices; ++i) {
+      if (!used[i]) continue;  // an empty shard
       RT_HIP(hipSetDevice(i));
       std::lock_guard<std::mutex> lk(scenes[i]->mu);
-      const uint32_t rows = rt_shard_rows(H, row_block, i, n_devices);
-      int r = run_render(scenes[i], to_dev_camera(*camera), nullptr, rows * W * aa_samples, aa_samples, max_depth,
-                         row_block, i, n_devices, send[i], scenes[i]->stream);
-      if (r != RT_OK) return r;
-    }
-    if (n_devices > 1) {
-      if (ncclGroupStart() != ncclSuccess) return fail(RT_ERR_RCCL, "ncclGroupStart");
-      for (int i = 0; i < n_devices; ++i) {
-        if (ncclGather(send[i], i == 0 ? recv : nullptr, per, ncclDouble, 0, comms[i], scenes[i]->stream) !=
-            ncclSuccess)
-          return fail(RT_ERR_RCCL, "ncclGather");
-      }
-      if (ncclGroupEnd() != ncclSuccess) return fail(RT_ERR_RCCL, "ncclGroupEnd");
-    } else {
-      RT_HIP(hipMemcpyAsync(recv, send[0], per * sizeof(double), hipMemcpyDeviceToDevice, scenes[0]->stream));
-    }
-    for (int i = 0; i < n_devices; ++i) {
-      RT_HIP(hipSetDevice(i));
-      RT_HIP(hipStreamSynchronize(scenes[i]->stream));
-    }
-    // exact counters: one more counted render per device (same deterministic work)
-    if (stats) {
-      for (int i = 0; i < n_devices; ++i) {
-        RT_HIP(hipSetDevice(i));
-        std::lock_guard<std::mutex> lk(scenes[i]->mu);
-        const uint32_t rows = rt_shard_rows(H, row_block, i, n_devices);
-        DevStats ds{};
-        float ms = 0.f;
-        int r = run_render(scenes[i], to_dev_camera(*camera), nullptr, rows * W * aa_samples, aa_samples, max_depth,
-                           row_block, i, n_devices, send[i], scenes[i]->stream, &ds, &ms);
-        if (r != RT_OK) return r;
-        fill_stats(&st[i], ds, ms, 0.0);
-      }
-    }
-    // un-interleave rank-major rows into the canvas
-    std::vector<double> host(per * n_devices);
-    RT_HIP(hipSetDevice(0));
-    RT_HIP(hipMemcpy(host.data(), recv, host.size() * sizeof(double), hipMemcpyDeviceToHost));
-    for (int i = 0; i < n_devices; ++i) {
-      uint32_t lr = 0;
-      for (uint32_t blk = i; (uint64_t)blk * row_block < H; blk += n_devices)
-        for (uint32_t y = blk * row_block; y < std::min(H, (blk + 1) * row_block); ++y, ++lr)
-          std::memcpy(out_rgb + (size_t)y * W * 3, host.data() + (size_t)i * per + (size_t)lr * W * 3,
-                      (size_t)W * 3 * sizeof(double));
-    }
-    return RT_OK;
-  };
-  rc = body();
-  for (int i = 0; i < n_devices; ++i) {
-    (void)hipSetDevice(i);
-    if (send[i]) (void)hipFree(send[i]);
-    if (comm_ok) ncclCommDestroy(comms[i]);
-  }
-  (void)hipSetDevice(0);
-  if (recv) (void)hipFree(recv);
-  if (rc == RT_OK && stats) {
-    std::memset(stats, 0, sizeof *stats);
-    for (auto& x : st) {
+      DevStats ds{};
+      RT_HIP(used[i]->wf->read_stats(&ds));
+      rt_stats x;
+      fill_stats(&x, ds, 0.f, 0.0);
       stats->rays_primary += x.rays_primary; stats->rays_reflect += x.rays_reflect;
       stats->rays_refract += x.rays_refract; stats->rays_shadow += x.rays_shadow;
       stats->sphere_tests += x.sphere_tests; stats->plane_tests += x.plane_tests;
-      stats->sphere_disc_ge0 += x.sphere_disc_ge0; stats->other_tests += x.other_tests;
-      stats->ms_kernel = std::max(stats->ms_kernel, x.ms_kernel);
+      stats->other_tests += x.other_tests;
+      stats->sphere_disc_ge0 = x.sphere_disc_ge0;  // RT_STATS_NOT_COUNTED: the fast path
+      stats->rays_shadow_traced += x.rays_shadow_traced;
+      stats->sphere_tests_executed += x.sphere_tests_executed;
+      stats->box_tests_executed += x.box_tests_executed;
     }
     stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
-  return rc;
+  return RT_OK;
 }
 
 }  // extern "C"

@@ -165,10 +165,12 @@ struct DevCamera {
   uint32_t hsize, vsize;
 };
 
-// Counters accumulated by the kernels (order = rt_stats prefix).
+// Counters of one render (order = rt_stats prefix, then its ABI-3 fields).
 struct DevStats {
   unsigned long long rays_primary, rays_reflect, rays_refract, rays_shadow;
   unsigned long long sphere_tests, plane_tests, sphere_disc_ge0, other_tests;
+  unsigned long long rays_shadow_traced, sphere_tests_executed, box_tests_executed;
+  unsigned exhaustive;  // sphere_disc_ge0 is exact (every sphere tested for every reference ray)
 };
 
 }  // namespace rtamd

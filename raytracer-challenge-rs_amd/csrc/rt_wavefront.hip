@@ -1728,7 +1728,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_average(WfArgs a, unsigned hsize,
 
 // Reflected / refracted ray counts per generation (stats only).
 __global__ void wf_count_kinds(WfArgs a) {
-  unsigned nrefl = 0, nrefr = 0;
+  unsigned nrefl = 0, nrefr = 0, nhit = 0;
   const unsigned stride = gridDim.x * blockDim.x;
   __shared__ unsigned s_pre[kShards + 1];
   const unsigned* pre = shard_prefix(a.in_cnt, s_pre);
@@ -1736,11 +1736,37 @@ __global__ void wf_count_kinds(WfArgs a) {
     const WfNode nd = a.nodes[shard_slot(pre, a.in_cap, i)];
     nrefl += nd.child_refl >= 0;
     nrefr += nd.child_refr >= 0;
+    nhit += nd.obj >= 0;  // shade_hit runs: one is_shadowed per light (world.rs:41-56)
   }
-  const unsigned long long s1 = wave_sum(nrefl), s2 = wave_sum(nrefr);
+  const unsigned long long s1 = wave_sum(nrefl), s2 = wave_sum(nrefr), s3 = wave_sum(nhit);
   if (lane_id() == 0) {
     if (s1) atomicAdd(&a.cnt->n_refl[a.g], (unsigned)s1);
     if (s2) atomicAdd(&a.cnt->n_refr[a.g], (unsigned)s2);
+    if (s3) atomicAdd(&a.cnt->n_hit[a.g], (unsigned)s3);
+  }
+}
+
+// Device-side check of a calibrated frame: every generation's queue counts
+// (the sharded region counters the trace kernels appended to) must equal the
+// launch sizes the host took from its calibration cache. A mismatch would mean
+// rays were left untraced; it raises the host-mapped fault flag, which the
+// library reports as RT_ERR_HIP on the next call (Wavefront::fault).
+struct WfCheckArgs {
+  unsigned n_gen;              // generations 0 .. n_gen-1 were launched
+  unsigned rays[kMaxGen];      // expected ray count of generation g (g >= 1)
+  unsigned shadows[kMaxGen];   // expected shadow-list length of generation g
+};
+__global__ void wf_check_counts(const unsigned* shard_base, WfCheckArgs c, int* fault) {
+  for (unsigned g = threadIdx.x; g <= c.n_gen && g < (unsigned)kMaxGen; g += blockDim.x) {
+    const unsigned* r = shard_base + ((size_t)g * 2 + 0) * kShards * kShardStride;
+    const unsigned* q = shard_base + ((size_t)g * 2 + 1) * kShards * kShardStride;
+    unsigned nr = 0, ns = 0;
+    for (int k = 0; k < kShards; ++k) {
+      nr += r[k * kShardStride];
+      ns += q[k * kShardStride];
+    }
+    const bool bad = (g >= 1 && nr != c.rays[g]) || (g < c.n_gen && ns != c.shadows[g]);
+    if (bad) *fault = 1;
   }
 }
 
@@ -1760,6 +1786,7 @@ Wavefront::~Wavefront() {
   if (d_cnt_) (void)hipFree(d_cnt_);
   if (d_shard_) (void)hipFree(d_shard_);
   if (d_prim_) (void)hipFree(d_prim_);
+  if (h_fault_) (void)hipHostFree(h_fault_);
   if (ev0_) (void)hipEventDestroy(ev0_);
   if (ev1_) (void)hipEventDestroy(ev1_);
   for (hipEvent_t e : fork_ev_)
@@ -1875,6 +1902,11 @@ hipError_t Wavefront::ensure_side() {
 
 hipError_t Wavefront::ensure_misc(size_t n_diag) {
   if (!d_cnt_) WF_CHECK(hipMalloc(&d_cnt_, sizeof(WfCounters)));
+  if (!h_fault_) {
+    WF_CHECK(hipHostMalloc((void**)&h_fault_, sizeof(int), hipHostMallocMapped));
+    *(volatile int*)h_fault_ = 0;
+    WF_CHECK(hipHostGetDevicePointer((void**)&d_fault_, h_fault_, 0));
+  }
   if (!d_shard_) WF_CHECK(hipMalloc(&d_shard_, (size_t)kMaxGen * 2 * kShards * kShardStride * sizeof(unsigned)));
   if (!ev0_) WF_CHECK(hipEventCreate(&ev0_));
   if (!ev1_) WF_CHECK(hipEventCreate(&ev1_));
@@ -2102,10 +2134,12 @@ static hipError_t launch_shadow_wf(const DevScene& sc, const WfArgs& a, bool lds
                         : launch_shadow_q<false, TW>(sc, a, lds_ok, bvh, stream);
 }
 
+int Wavefront::g_corrupt_calibration = 0;
+
 hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool camera_mode, const double* d_in_rays,
                              unsigned n0, unsigned aa, unsigned max_depth, unsigned row_block, unsigned shard,
                              unsigned n_shards, double* d_out, hipStream_t stream, const std::string& signature,
-                             DevStats* stats, float* ms_kernel, bool solo) {
+                             DevStats* stats, float* ms_kernel, bool solo, unsigned flags) {
   if (max_depth + 2 > (unsigned)kMaxGen) return hipErrorInvalidValue;
   if (aa == 0 || aa > 16 || (aa & (aa - 1)) != 0 || (!camera_mode && aa != 1) || n0 % aa != 0)
     return hipErrorInvalidValue;
@@ -2113,15 +2147,19 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
   const bool averaged = aa > 1;
   WF_CHECK(ensure_misc((size_t)sc.n_diag));
   const unsigned L = (unsigned)sc.n_lights;
-  // BVH traversal (and skipped shadow rays) unless the exact exhaustive counters are requested
-  const bool bvh = g_wf_accel != 0 && stats == nullptr && sc.n_bvh > 0;
-  const bool skip_shadow = stats == nullptr && g_wf_skip_shadow != 0;
+  // BVH traversal and skipped shadow rays unless the reference's every-shape loop is asked
+  // for; counting (stats) never changes the algorithm
+  const bool exhaustive = (flags & WF_EXHAUSTIVE) != 0;
+  const bool count = stats != nullptr || (flags & WF_COUNT) != 0;
+  const bool bvh = g_wf_accel != 0 && !exhaustive && sc.n_bvh > 0;
+  const bool skip_shadow = !exhaustive && g_wf_skip_shadow != 0;
   // the shadow-ray counts differ between the two modes
   const std::string key = signature.empty() ? signature : signature + (skip_shadow ? 'S' : 'A');
   auto it = key.empty() ? cache_.end() : cache_.find(key);
   const bool calibrated = it != cache_.end();
   Counts counts;
   if (calibrated) counts = it->second;
+  if (calibrated && g_corrupt_calibration && counts.rays.size() > 1 && counts.rays[1] > 0) --counts.rays[1];
   counts.rays.resize(max_depth + 2, 0);
   counts.shadows.resize(max_depth + 2, 0);
   counts.rays[0] = n0;
@@ -2251,10 +2289,20 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
       }
       WF_CHECK(pmark(sh_stream, WF_SHADOW, false));
     }
-    if (stats) {
+    if (count) {
       WF_LAUNCH(wf_count_kinds, dim3(occupancy_grid(wf_count_kinds, 256, 0, n)), dim3(256), 0, stream, a);
       WF_CHECK(hipGetLastError());
     }
+  }
+  if (calibrated) {  // the queues must hold exactly what was launched
+    WfCheckArgs ck{};
+    ck.n_gen = last + 1;
+    for (unsigned g = 0; g <= last + 1 && g < (unsigned)kMaxGen; ++g) {
+      ck.rays[g] = g < counts.rays.size() ? counts.rays[g] : 0;
+      ck.shadows[g] = g < counts.shadows.size() ? counts.shadows[g] : 0;
+    }
+    WF_LAUNCH(wf_check_counts, dim3(1), dim3(64), 0, stream, d_shard_, ck, d_fault_);
+    WF_CHECK(hipGetLastError());
   }
   if (forked) {  // join: the combine pass reads every generation's lighting terms
     WF_CHECK(hipEventRecord(join_ev_, sh_stream));
@@ -2297,25 +2345,48 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     WF_CHECK(hipStreamSynchronize(stream));
     if (ms_kernel) WF_CHECK(hipEventElapsedTime(ms_kernel, ev0_, ev1_));
   }
-  if (stats) {
-    WfCounters hc;
-    WF_CHECK(hipMemcpy(&hc, d_cnt_, sizeof hc, hipMemcpyDeviceToHost));
-    DevStats s{};
-    unsigned long long rays = 0, shadows = 0;
-    for (unsigned g = 0; g <= last; ++g) {
-      rays += counts.rays[g];
-      shadows += counts.shadows[g];
-      s.rays_reflect += hc.n_refl[g];
-      s.rays_refract += hc.n_refr[g];
-    }
-    s.rays_primary = n0;
-    s.rays_shadow = shadows;
-    s.sphere_tests = (rays + shadows) * (unsigned long long)(sc.n_diag + sc.n_gen);
-    s.plane_tests = (rays + shadows) * (unsigned long long)sc.n_planes;
-    s.other_tests = (rays + shadows) * (unsigned long long)sc.n_quads;
-    s.sphere_disc_ge0 = hc.disc(0) + hc.disc(1) + hc.disc(2);
-    *stats = s;
+  lr_.counts = counts;
+  lr_.last = last; lr_.L = L; lr_.n0 = n0;
+  lr_.counted = count; lr_.exact_disc = !bvh && !skip_shadow; lr_.bvh = bvh;
+  lr_.n_diag = (unsigned long long)sc.n_diag; lr_.n_gen = (unsigned long long)sc.n_gen;
+  lr_.n_planes = (unsigned long long)sc.n_planes; lr_.n_quads = (unsigned long long)sc.n_quads;
+  lr_.stream = stream;
+  if (stats) WF_CHECK(read_stats(stats));
+  return hipSuccess;
+}
+
+hipError_t Wavefront::read_stats(DevStats* out) {
+  *out = DevStats{};
+  if (!lr_.counted || !d_cnt_) return hipErrorInvalidValue;
+  WF_CHECK(hipStreamSynchronize(lr_.stream));
+  WfCounters hc;
+  WF_CHECK(hipMemcpy(&hc, d_cnt_, sizeof hc, hipMemcpyDeviceToHost));
+  DevStats s{};
+  unsigned long long rays = 0, hits = 0, traced_shadows = 0;
+  for (unsigned g = 0; g <= lr_.last && g < lr_.counts.rays.size(); ++g) {
+    rays += lr_.counts.rays[g];
+    traced_shadows += lr_.counts.shadows[g];
+    hits += hc.n_hit[g];
+    s.rays_reflect += hc.n_refl[g];
+    s.rays_refract += hc.n_refr[g];
   }
+  // the reference's work: every hit runs is_shadowed once per light (world.rs:41-56), and
+  // World::intersect tests every shape for every ray (world.rs:31-38)
+  const unsigned long long shadows = hits * (unsigned long long)lr_.L;
+  s.rays_primary = lr_.n0;
+  s.rays_shadow = shadows;
+  s.sphere_tests = (rays + shadows) * (lr_.n_diag + lr_.n_gen);
+  s.plane_tests = (rays + shadows) * lr_.n_planes;
+  s.other_tests = (rays + shadows) * lr_.n_quads;
+  s.sphere_disc_ge0 = lr_.exact_disc ? hc.disc(0) + hc.disc(1) + hc.disc(2) : ~0ull;
+  s.exhaustive = lr_.exact_disc ? 1u : 0u;
+  // what the kernels did
+  s.rays_shadow_traced = traced_shadows;
+  const unsigned long long traced = rays + traced_shadows;
+  s.sphere_tests_executed = lr_.bvh ? hc.tests(0) + hc.tests(1) + hc.tests(2) + traced * lr_.n_gen
+                                    : traced * (lr_.n_diag + lr_.n_gen);
+  s.box_tests_executed = hc.boxes(0) + hc.boxes(1) + hc.boxes(2);
+  *out = s;
   return hipSuccess;
 }
 

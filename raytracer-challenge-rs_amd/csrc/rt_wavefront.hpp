@@ -59,6 +59,7 @@ struct PrimRec {  // primary rays share the origin: per diag sphere (s, o', c)
 };
 
 constexpr int kMaxGen = 66;
+enum WfFlags : unsigned { WF_EXHAUSTIVE = 1u, WF_COUNT = 2u };
 extern int g_wf_trace_waves;  // tuning knob: trace-kernel occupancy (4 or 8 waves/SIMD)
 extern int g_tw_primary, g_tw_closest, g_tw_shadow;  // tuning knobs: BVH trace-kernel occupancy
 extern int g_wf_lane;         // tuning knob: 1 = per-lane BVH traversal for secondary / shadow rays
@@ -82,7 +83,7 @@ struct alignas(128) WfWorkRow {
   unsigned long long boxes[3];  // BVH mode: child-box tests executed (lanes x boxes)
 };
 struct WfCounters {
-  unsigned n_refl[kMaxGen], n_refr[kMaxGen];
+  unsigned n_refl[kMaxGen], n_refr[kMaxGen], n_hit[kMaxGen];
   WfWorkRow work[kWorkRows];
   unsigned long long disc(int c) const {
     unsigned long long t = 0;
@@ -182,10 +183,26 @@ class Wavefront {
   // asynchronous); otherwise each generation is sized by a synchronous count
   // read-back. stats (host) may be null. `solo`: no other workspace renders
   // concurrently (then the shadow traces take the side stream).
+  // `flags`: WF_EXHAUSTIVE runs the reference's every-shape loop (exact
+  // sphere_disc_ge0); WF_COUNT counts the reference's rays of this render
+  // (read later by read_stats). A non-null `stats` implies WF_COUNT and
+  // synchronises to fill it.
   hipError_t render(const DevScene& sc, const DevCamera& cam, bool camera_mode, const double* d_in_rays,
                     unsigned n0, unsigned aa, unsigned max_depth, unsigned row_block, unsigned shard,
                     unsigned n_shards, double* d_out, hipStream_t stream, const std::string& signature,
-                    DevStats* stats, float* ms_kernel, bool solo = true);
+                    DevStats* stats, float* ms_kernel, bool solo = true, unsigned flags = 0);
+  // The counters of the last render (rendered with WF_COUNT); synchronises its stream.
+  hipError_t read_stats(DevStats* out);
+  // A generation's actual queue count differed from the calibrated launch size
+  // (a device-side check of every calibrated frame, wf_check_counts). Sticky
+  // until clear_fault(), which also drops the calibration.
+  bool fault() const { return h_fault_ && *(volatile int*)h_fault_ != 0; }
+  void clear_fault() {
+    if (h_fault_) *(volatile int*)h_fault_ = 0;
+    cache_.clear();
+  }
+  // test hook: perturb calibrated launch sizes (generation 1 launched with one ray fewer)
+  static int g_corrupt_calibration;
 
  private:
   hipError_t ensure_gen(size_t g, size_t slots, size_t n_lights, size_t list_slots);
@@ -209,6 +226,15 @@ class Wavefront {
     std::vector<unsigned> rays, shadows;
   };
   std::map<std::string, Counts> cache_;
+  int* h_fault_ = nullptr;  // host-mapped flag written by wf_check_counts
+  int* d_fault_ = nullptr;  // its device address
+  struct LastRender {       // what read_stats needs of the last render
+    Counts counts;
+    unsigned last = 0, L = 0, n0 = 0;
+    bool counted = false, exact_disc = false, bvh = false;
+    unsigned long long n_diag = 0, n_gen = 0, n_planes = 0, n_quads = 0;
+    hipStream_t stream = nullptr;
+  } lr_;
   bool last_bvh_ = false;
   bool profiling_ = false;
   int pmask_ = (1 << WF_NCLASS) - 1;

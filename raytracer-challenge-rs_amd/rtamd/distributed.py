@@ -192,47 +192,87 @@ class RcclStreamAssembler(StreamFrameAssembler):
     process group's own RCCL stream waiting on each other) cost ~0.17 ms per
     frame on an 8-way shard (`bench.py --fake-shard 0/8 --emulate-gather`),
     which is the whole frame again. The communicators' unique ids travel over
-    the default process group."""
+    the default process group.
 
-    def __init__(self, height, width, row_block, rank, n_shards, device, streams, dtype=torch.float64):
+    Creation is all-or-nothing across ranks: after each communicator every
+    rank contributes its success to a MIN all-reduce over the default group
+    (the library creates communicators non-blocking with a timeout, so a rank
+    whose peers failed does not hang in the init). If any rank failed, every
+    rank aborts what it created and raises together, so all ranks take the
+    caller's fallback in step. `lib` (tests) replaces the library hooks;
+    `streams` entries may be None (CPU tests: the current stream)."""
+
+    def __init__(self, height, width, row_block, rank, n_shards, device, streams, dtype=torch.float64, lib=None,
+                 timeout_ms=60000):
         super().__init__(height, width, row_block, rank, n_shards, device, streams=streams,
                          groups=[None] * len(streams), dtype=dtype)
-        from . import _rtamd
-        self._lib = _rtamd
-        dev_index = device.index if device.index is not None else torch.cuda.current_device()
+        if lib is None:
+            from . import _rtamd as lib
+        self._lib = lib
+        if device.type == "cuda":
+            dev_index = device.index if device.index is not None else torch.cuda.current_device()
+        else:
+            dev_index = 0
         self.comms = []
-        for _ in range(self.F):
-            # byte 0: rank 0 could make an id (1) or not (0); every rank reads the same
-            # flag, so a failure sends every rank to the caller's fallback together
-            msg = torch.zeros(129, dtype=torch.uint8, device=device)
-            if rank == 0:
+        try:
+            for _ in range(self.F):
+                # byte 0: rank 0 could make an id (1) or not (0); every rank reads the same flag
+                msg = torch.zeros(129, dtype=torch.uint8, device=device)
+                if rank == 0:
+                    try:
+                        msg[1:].copy_(torch.frombuffer(bytearray(lib._nccl_unique_id()), dtype=torch.uint8))
+                        msg[0] = 1
+                    except Exception:  # pragma: no cover - environment dependent
+                        msg[0] = 0
+                dist.broadcast(msg, src=0)
+                host = msg.cpu().numpy().tobytes()
+                if host[0] != 1:
+                    raise RuntimeError("rank 0 could not create an RCCL unique id")
+                comm, err = None, None
                 try:
-                    msg[1:].copy_(torch.frombuffer(bytearray(_rtamd._nccl_unique_id()), dtype=torch.uint8))
-                    msg[0] = 1
-                except Exception:  # pragma: no cover - environment dependent
-                    msg[0] = 0
-            dist.broadcast(msg, src=0)
-            host = msg.cpu().numpy().tobytes()
-            if host[0] != 1:
-                raise RuntimeError("rank 0 could not create an RCCL unique id")
-            self.comms.append(_rtamd._nccl_comm_init(n_shards, host[1:], rank, dev_index))
+                    comm = lib._nccl_comm_init(n_shards, host[1:], rank, dev_index, timeout_ms)
+                except Exception as e:
+                    err = e
+                if comm is not None:
+                    self.comms.append(comm)
+                ok = torch.tensor([1 if comm is not None else 0], dtype=torch.int32, device=device)
+                dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+                if int(ok[0]) != 1:
+                    raise RuntimeError(f"RCCL communicator creation failed on some rank"
+                                       f"{f' (here: {err})' if err is not None else ''}")
+        except Exception:
+            self.abort()
+            raise
+
+    def _stream_handle(self, k):
+        st = self.streams[k]
+        return (st.cuda_stream if st is not None else 0), st
 
     def submit(self, step):
         k = step % self.F
         if self.n == 1:
             self._last = self.shards[k][: self.H]
             return self._last
-        st = self.streams[k]
+        handle, st = self._stream_handle(k)
         recv = self.gather_buf[k].data_ptr() if self.rank == 0 else 0
         self._lib._nccl_gather_f64(self.shards[k].data_ptr(), recv, self.shards[k].numel(), 0, self.comms[k],
-                                   st.cuda_stream)
+                                   handle)
         if self.rank != 0:
             self._last = None
             return None
-        with torch.cuda.stream(st):
+        with (torch.cuda.stream(st) if st is not None else _nullctx()):
             torch.index_select(self.gather_buf[k], 0, self.inv_idx, out=self.canvas[k])
         self._last = self.canvas[k]
         return self._last
+
+    def abort(self):
+        """Tear the communicators down without waiting on peers (failure path)."""
+        for c in self.comms:
+            try:
+                self._lib._nccl_comm_abort(c)
+            except Exception:  # pragma: no cover - best effort
+                pass
+        self.comms = []
 
     def close(self):
         for c in self.comms:

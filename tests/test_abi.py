@@ -24,7 +24,8 @@ def test_header_declares_the_boundary():
     for must in ("rt_scene_create", "rt_scene_destroy", "rt_render", "rt_render_shard_device",
                  "rt_render_multi", "rt_color_at_batch", "rt_is_shadowed_batch", "rt_hit_batch",
                  "rt_canvas_to_ppm", "rt_quantize_u8", "rt_matrix_inverse", "rt_camera_init",
-                 "rt_last_error", "rt_abi_version", "rt_device_count", "rt_shard_rows", "rt_render_aa"):
+                 "rt_last_error", "rt_abi_version", "rt_device_count", "rt_shard_rows", "rt_render_aa",
+                 "rt_render_ex", "rt_render_shard_device_ex", "rt_color_at_batch_ex"):
         assert must in names
 
 
@@ -36,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_shard_rows():
     lib = ctypes.CDLL(LIB)
-    assert lib.rt_abi_version() == 2
+    assert lib.rt_abi_version() == 3
     f = lib.rt_shard_rows
     f.restype = ctypes.c_uint32
     f.argtypes = [ctypes.c_uint32] * 4
@@ -60,7 +61,7 @@ def test_descriptor_layout_matches_oracle(rt, oracle):
     L = oracle.lib()
     assert len(rt.Sphere().desc_bytes()) == L.oracle_sizeof_shape_desc() == 680
     assert len(rt.Camera(4, 3, 1.0).desc_bytes()) == L.oracle_sizeof_camera_desc() == 160
-    assert L.oracle_sizeof_stats() == ctypes.sizeof(oracle.Stats) == 8 * 8 + 2 * 8
+    assert L.oracle_sizeof_stats() == ctypes.sizeof(oracle.Stats) == 8 * 8 + 2 * 8 + 3 * 8 + 2 * 4
 
 
 def test_cylinders_differing_only_in_bounds_are_not_duplicates(rt):

@@ -160,3 +160,111 @@ def test_gloo_stream_assembler(tmp_path, world_size, row_block, n_slots):
     assert got.shape == (6,) + ref.shape
     for f in range(6):
         assert np.array_equal(got[f], ref + f), f
+
+
+class _FakeRccl:
+    """Stands in for the library's RCCL hooks (rtamd._rtamd._nccl_*) on CPU:
+    ids are bytes, communicators are integers, the gather runs over gloo on the
+    tensors the pointers name. `fail_at` = (rank, k): that rank's k-th
+    communicator init raises, as a failing ncclCommInitRankConfig would."""
+
+    def __init__(self, rank, fail_at=None):
+        self.rank, self.fail_at = rank, fail_at
+        self.made, self.aborted, self.destroyed, self.gathers = [], [], [], []
+        self.tensors = {}  # data_ptr -> tensor (set by the test once the assembler exists)
+
+    def _nccl_unique_id(self):
+        return bytes(range(128))
+
+    def _nccl_comm_init(self, nranks, uid, rank, dev, timeout_ms):
+        assert uid == bytes(range(128)) and rank == self.rank and timeout_ms > 0
+        k = len(self.made) + len(self.aborted)
+        if self.fail_at == (rank, k):
+            raise RuntimeError("injected ncclCommInitRankConfig failure")
+        c = 1000 * (rank + 1) + k
+        self.made.append(c)
+        return c
+
+    def _nccl_comm_abort(self, c):
+        self.aborted.append(c)
+
+    def _nccl_comm_destroy(self, c):
+        self.destroyed.append(c)
+
+    def _nccl_gather_f64(self, send, recv, count, root, comm, stream):
+        self.gathers.append((send, comm, stream))
+        src = self.tensors[send]
+        assert src.numel() == count and root == 0
+        if self.rank == 0:
+            dst = self.tensors[recv]
+            dist.gather(src, list(dst.chunk(dist.get_world_size())), dst=0)
+        else:
+            dist.gather(src, None, dst=0)
+
+
+def _rccl_assembler_worker(rank, world_size, port, fail_at, n_frames, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world_size)
+    try:
+        from rtamd.distributed import RcclStreamAssembler
+        ref = torch.from_numpy(np.load(os.path.join(HERE, "golden", "c3_64x36_s200.npz"))["canvas"])
+        H, W = ref.shape[:2]
+        lib = _FakeRccl(rank, fail_at)
+        F = 3
+        if fail_at is not None:
+            with pytest.raises(RuntimeError, match="failed on some rank"):
+                RcclStreamAssembler(H, W, 8, rank, world_size, torch.device("cpu"), streams=[None] * F, lib=lib)
+            # every rank fell back together and left nothing behind
+            assert sorted(lib.aborted) == sorted(lib.made) and not lib.destroyed
+            assert len(lib.made) == fail_at[1] + (0 if rank == fail_at[0] else 1)
+            dist.barrier()  # the default group still works: nobody is stuck in an init
+            np.save(out_path + f".{rank}", np.array([len(lib.made)]))
+            return
+        fa = RcclStreamAssembler(H, W, 8, rank, world_size, torch.device("cpu"), streams=[None] * F, lib=lib)
+        assert fa.comms == [1000 * (rank + 1) + k for k in range(F)]
+        for t in fa.shards:
+            lib.tensors[t.data_ptr()] = t
+        if rank == 0:
+            for t in fa.gather_buf:
+                lib.tensors[t.data_ptr()] = t
+        done = []
+        for f in range(n_frames):
+            buf = fa.slot(f)
+            buf.fill_(-1.0)
+            buf[: len(fa.rows)] = ref[fa.rows] + f
+            c = fa.submit(f)
+            # frame f gathers slot f % F over communicator f % F
+            assert lib.gathers[-1][:2] == (fa.shards[f % F].data_ptr(), fa.comms[f % F])
+            if rank == 0:
+                done.append(c.clone())
+            else:
+                assert c is None
+        fa.close()
+        assert lib.destroyed == [1000 * (rank + 1) + k for k in range(F)] and not lib.aborted
+        if rank == 0:
+            np.save(out_path, torch.stack(done).numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_rccl_stream_assembler_frames(tmp_path):
+    """bench.py's default N>1 assembler (one library communicator per render
+    stream): id broadcast, per-slot communicators, frame f through slot and
+    communicator f % F, every frame assembled whole."""
+    out = str(tmp_path / "frames.npy")
+    mp.spawn(_rccl_assembler_worker, args=(2, _free_port(), None, 7, out), nprocs=2, join=True)
+    got = np.load(out)
+    ref = np.load(os.path.join(HERE, "golden", "c3_64x36_s200.npz"))["canvas"]
+    for f in range(7):
+        assert np.array_equal(got[f], ref + f), f
+
+
+@pytest.mark.parametrize("fail_at", [(1, 1), (0, 0), (1, 2)])
+def test_gloo_rccl_stream_assembler_fallback_agreement(tmp_path, fail_at):
+    """One rank's communicator init fails: every rank raises together (no rank
+    left blocked in an init or a collective) and aborts what it created."""
+    out = str(tmp_path / "made.npy")
+    mp.spawn(_rccl_assembler_worker, args=(2, _free_port(), fail_at, 0, out), nprocs=2, join=True)
+    for r in range(2):
+        made = int(np.load(out + f".{r}.npy")[0])
+        assert made == fail_at[1] + (0 if r == fail_at[0] else 1)

@@ -1,0 +1,146 @@
+"""The benchmarked fast path at full size, the fast path's counters, the
+boundary's multi-device entry point and the device-side queue check.
+
+bench.py times the fast path (exact-culling BVH, light buffer, shadow rays
+that cannot change a colour left out) on the full 1920x1080 C3 frame and the
+4096x4096 C5 frame. These tests require those frames to equal the
+reference's every-shape loop (RT_RENDER_EXHAUSTIVE) bit for bit, and the fast
+frame to match the oracle on sampled rows (camera.rs:133-148).
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+NTHREADS = max(1, min(16, os.cpu_count() or 1))
+RAY_KEYS = ("rays_primary", "rays_reflect", "rays_refract", "rays_shadow", "sphere_tests", "plane_tests",
+            "other_tests")
+
+
+def _device_frame(cam, w, depth, exhaustive, stream=None):
+    import torch
+    buf = torch.empty((cam.vsize, cam.hsize, 3), dtype=torch.float64, device="cuda")
+    st = cam.render_shard_device(w, depth, 8, 0, 1, buf.data_ptr(),
+                                 (stream or torch.cuda.current_stream()).cuda_stream, True, exhaustive=exhaustive)
+    torch.cuda.synchronize()
+    return buf, st
+
+
+def test_c3_full_frame_fast_equals_exhaustive(rt, oracle):
+    """C3 at 1920x1080 (the headline frame): fast == exhaustive bitwise, the
+    fast frame vs the oracle on sampled rows, and the fast path's counters."""
+    import torch
+    from rtamd import scenes
+    w, cam, depth = scenes.c3()
+    exact, se = _device_frame(cam, w, depth, True)
+    fast, sf = _device_frame(cam, w, depth, False)
+    assert torch.equal(fast, exact)
+    assert se["exhaustive"] and not sf["exhaustive"]
+    for k in RAY_KEYS:  # the reference's work, exact on both paths
+        assert sf[k] == se[k], k
+    assert sf["sphere_disc_ge0"] is None and se["sphere_disc_ge0"] > 0
+    assert se["rays_shadow_traced"] == se["rays_shadow"]
+    assert 0 < sf["rays_shadow_traced"] < sf["rays_shadow"]
+    assert sf["sphere_tests_executed"] < se["sphere_tests_executed"] / 50
+    assert sf["box_tests_executed"] > 0 and se["box_tests_executed"] == 0
+    rows = [3, 262, 540, 811, 1076]
+    ref, _ = oracle.OracleWorld.from_world(w).render_rows(cam.desc_bytes(), depth, rows, NTHREADS)
+    got = fast.cpu().numpy()[rows]
+    assert np.abs(got - ref).max() <= TOL
+    assert rt.canvas_to_ppm(got) == oracle.canvas_to_ppm(ref)
+
+
+def test_c3_full_frame_frames_in_flight_equal(rt):
+    """bench.py's timed configuration: 4 frames in flight on 4 render streams
+    (each its own workspace, calibrated launch sizes), every frame bitwise equal
+    to the exhaustive frame."""
+    import torch
+    from rtamd import scenes
+    w, cam, depth = scenes.c3()
+    exact, _ = _device_frame(cam, w, depth, True)
+    streams = [rt.render_stream(False) for _ in range(4)]
+    bufs = [torch.empty_like(exact) for _ in streams]
+    for f in range(12):
+        k = f % 4
+        bufs[k].fill_(-1.0)
+        torch.cuda.current_stream().synchronize()
+        cam.render_shard_device(w, depth, 8, 0, 1, bufs[k].data_ptr(), streams[k].cuda_stream, False)
+    torch.cuda.synchronize()
+    for b in bufs:
+        assert torch.equal(b, exact)
+
+
+def test_c5_full_frame_fast_equals_exhaustive(rt):
+    """C5 at its full 4096x4096 (4 planes + 9996 spheres, 2 lights, depth 8)."""
+    import torch
+    from rtamd import scenes
+    w, cam, depth = scenes.c5()
+    exact, se = _device_frame(cam, w, depth, True)
+    fast, sf = _device_frame(cam, w, depth, False)
+    assert torch.equal(fast, exact)
+    for k in RAY_KEYS:
+        assert sf[k] == se[k], k
+    del exact, fast
+    torch.cuda.empty_cache()
+
+
+def test_host_render_stats_from_fast_path(rt, oracle):
+    """rt_render with stats runs the fast path (asking for counters never
+    changes the algorithm); the reference ray counts still equal the oracle's."""
+    from rtamd import scenes
+    w, cam, depth = scenes.c3(160, 90, n_spheres=300)
+    fast, sf = cam.render(w, depth, want_stats=True, exhaustive=False)
+    exact, se = cam.render(w, depth, want_stats=True)
+    assert fast.to_numpy().tobytes() == exact.to_numpy().tobytes()
+    _, rst = oracle.OracleWorld.from_world(w).render(cam.desc_bytes(), depth, nthreads=NTHREADS)
+    for k in RAY_KEYS:
+        assert sf[k] == rst[k] == se[k], k
+    assert se["sphere_disc_ge0"] == rst["sphere_disc_ge0"] and sf["sphere_disc_ge0"] is None
+
+
+def test_render_multi_one_device_equals_render(rt):
+    """rt_render_multi (render_multithreaded across devices, camera.rs:150) with
+    n_devices = 1: bitwise equal to rt_render / rt_render_aa, on repeated calls
+    (cached buffers), for AA and odd row blocks."""
+    from rtamd import scenes
+    w, cam, depth = scenes.c3(200, 113, n_spheres=300)
+    ref, _ = cam.render(w, depth, want_stats=False)
+    for row_block in (8, 3, 113):
+        got, st = cam.render_multi([w], depth, row_block)
+        assert got.to_numpy().tobytes() == ref.to_numpy().tobytes()
+        assert st["rays_primary"] == 200 * 113 and st["sphere_disc_ge0"] is None
+    _, se = cam.render(w, depth)
+    for k in RAY_KEYS:
+        assert st[k] == se[k], k
+    cam.render_opts.aa_samples(rt.AASamples.X4)
+    ref4, _ = cam.render_multithreaded(w, depth, want_stats=False)
+    got4, st4 = cam.render_multi([w], depth, 8, 4)
+    assert got4.to_numpy().tobytes() == ref4.to_numpy().tobytes()
+    assert st4["rays_primary"] == 4 * 200 * 113
+
+
+def test_queue_check_reports_miscalibration(rt):
+    """A calibrated frame whose queue counts differ from its launch sizes (here
+    forced by a test hook that launches generation 1 one ray short) fails the
+    next call with RT_ERR_HIP instead of silently dropping rays; the library
+    then recalibrates."""
+    import torch
+    from rtamd import scenes
+    w, cam, depth = scenes.c3(96, 54, n_spheres=200)
+    exact, _ = _device_frame(cam, w, depth, True)
+    st = rt.render_stream(False)
+    buf = torch.empty_like(exact)
+    cam.render_shard_device(w, depth, 8, 0, 1, buf.data_ptr(), st.cuda_stream, False)  # calibrates
+    rt._rtamd._tuning_set("corrupt_calibration", 1)
+    try:
+        cam.render_shard_device(w, depth, 8, 0, 1, buf.data_ptr(), st.cuda_stream, False)
+        torch.cuda.synchronize()
+    finally:
+        rt._rtamd._tuning_set("corrupt_calibration", 0)
+    with pytest.raises(rt.RtError, match="queue check"):
+        cam.render_shard_device(w, depth, 8, 0, 1, buf.data_ptr(), st.cuda_stream, False)
+    cam.render_shard_device(w, depth, 8, 0, 1, buf.data_ptr(), st.cuda_stream, False)  # recalibrates
+    torch.cuda.synchronize()
+    assert torch.equal(buf, exact)
