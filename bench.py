@@ -546,11 +546,19 @@ def roofline(prof, breakdown, W, H, a, n, ref_work, frame_ms):
     nd, ng, npl = prof["n_diag"], prof["n_gen"], prof["n_planes"]
     per_sphere = {"primary": OPS_SPHERE_PRIMARY, "closest": OPS_SPHERE_DIAG, "shadow": OPS_SPHERE_DIAG}
 
+    fused = bool(prof.get("fused"))
+    sh_in_r, sh_in_t = prof.get("shadow_rays_in", {}), prof.get("shadow_tests_in", {})
+
     def class_ops(c):
         # executed work: diag-sphere tests (every sphere per ray when exhaustive, the
         # visited leaves' spheres under the BVH), child-box tests, the rest exhaustively
-        return (prof["tests"][c] * per_sphere[c] + OPS_BOX * prof["boxes"][c]
-                + prof["rays"][c] * (OPS_SPHERE_GEN * ng + OPS_PLANE * npl) + OPS_ROOTS * prof["disc"][c])
+        ops = (prof["tests"][c] * per_sphere[c] + OPS_BOX * prof["boxes"][c]
+               + prof["rays"][c] * (OPS_SPHERE_GEN * ng + OPS_PLANE * npl) + OPS_ROOTS * prof["disc"][c])
+        if fused and c in ("primary", "closest"):
+            # the fused launches also trace their hits' shadow rays (light buffer: sphere tests only)
+            ops += (OPS_SPHERE_DIAG * sh_in_t.get(c, 0.0)
+                    + sh_in_r.get(c, 0.0) * (OPS_SPHERE_GEN * ng + OPS_PLANE * npl))
+        return ops
     kernels = {}
     for c in ("primary", "closest", "shadow"):
         ms_c = breakdown["ms"][c]
@@ -558,6 +566,11 @@ def roofline(prof, breakdown, W, H, a, n, ref_work, frame_ms):
         kernels[c] = {"ms_per_frame": round(ms_c, 4), "rays": int(prof["rays"][c]),
                       "sphere_tests": int(prof["tests"][c]), "box_tests": int(prof["boxes"][c]),
                       "tflops": round(ops_c / (ms_c * 1e-3) / 1e12, 3) if ms_c > 0 else None}
+        if fused and c in ("primary", "closest"):
+            kernels[c]["shadow_rays_inside"] = int(sh_in_r.get(c, 0.0))
+            kernels[c]["shadow_sphere_tests_inside"] = int(sh_in_t.get(c, 0.0))
+    if fused:
+        kernels["shadow"]["note"] = "traced inside the fused primary / closest-hit launches (no launch of its own)"
     for c in ("prep", "combine"):
         kernels[c] = {"ms_per_frame": round(breakdown["ms"][c], 4)}
     dom = max(("primary", "closest", "shadow"), key=lambda c: breakdown["ms"][c])
@@ -571,6 +584,9 @@ def roofline(prof, breakdown, W, H, a, n, ref_work, frame_ms):
     # plane test, +6 per disc >= 0 (the reference's general 4x4 path; boxes unpriced)
     survey_ops = (SURVEY_OPS_SPHERE * (prof["tests"][dom] + prof["rays"][dom] * ng)
                   + SURVEY_OPS_PLANE * prof["rays"][dom] * npl + SURVEY_OPS_ROOTS * prof["disc"][dom])
+    if fused and dom in ("primary", "closest"):
+        survey_ops += (SURVEY_OPS_SPHERE * (sh_in_t.get(dom, 0.0) + sh_in_r.get(dom, 0.0) * ng)
+                       + SURVEY_OPS_PLANE * sh_in_r.get(dom, 0.0) * npl)
     achieved_survey = survey_ops / (kernel_ms * 1e-3) / 1e12
     traffic, traffic_src, counters = None, None, None
     pmc_path = pmc_summary_path(a, W, H, n)
@@ -593,7 +609,8 @@ def roofline(prof, breakdown, W, H, a, n, ref_work, frame_ms):
             pass
     return {
         "bound": "valu_f64",
-        "kernel": f"wf_trace_{dom}: its launches in one frame",
+        "kernel": (f"wf_trace_fused ({dom} launches: closest hit + shading + shadow rays + spawn) in one frame"
+                   if fused else f"wf_trace_{dom}: its launches in one frame"),
         "achieved": round(achieved, 3),
         "peak": PEAK_F64_VALU_TFLOPS,
         "unit": "TFLOP/s",

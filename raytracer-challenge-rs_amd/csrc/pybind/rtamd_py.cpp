@@ -58,7 +58,7 @@ extern "C" int rtamd_nccl_comm_init(int nranks, const unsigned char* id, size_t 
 extern "C" int rtamd_nccl_comm_abort(void* comm);
 extern "C" int rtamd_nccl_gather_f64(const double* send, double* recv, size_t count, int root, void* comm, void* stream);
 extern "C" int rtamd_nccl_comm_destroy(void* comm);
-extern "C" int rtamd_wf_profile(const rt_scene* s, int enable, double out[29]);
+extern "C" int rtamd_wf_profile(const rt_scene* s, int enable, double out[34]);
 
 PYBIND11_MODULE(_rtamd, m) {
   m.doc() = "MI355X-native render path of raytracer-challenge-rs (host API over the C-ABI)";
@@ -408,7 +408,7 @@ PYBIND11_MODULE(_rtamd, m) {
       }, py::arg("max_depth") = 5)
       .def("render_to", &SceneParser::render_to, py::arg("path"), py::arg("max_depth") = 5);
   m.def("_wf_profile", [](const World& w, int enable, bool read) {
-    double o[29] = {0};
+    double o[34] = {0};
     check(rtamd_wf_profile(w.scene(), enable, read ? o : nullptr), "wf_profile");
     py::dict d;
     if (read) {
@@ -422,8 +422,10 @@ PYBIND11_MODULE(_rtamd, m) {
       py::dict tests, boxes;
       for (int i = 0; i < 3; ++i) { tests[cls[i]] = o[16 + i]; boxes[cls[i]] = o[19 + i]; }
       d["tests"] = tests; d["boxes"] = boxes; d["bvh"] = (bool)o[22]; d["n_bvh_nodes"] = o[23]; d["bvh_depth"] = o[24];
-      d["n_bvh4_nodes"] = o[25]; d["bvh4_stack"] = o[26];
       d["lb_res"] = o[27]; d["lb_items"] = o[28];
+      py::dict shr, sht;
+      shr["primary"] = o[29]; shr["closest"] = o[30]; sht["primary"] = o[31]; sht["closest"] = o[32];
+      d["shadow_rays_in"] = shr; d["shadow_tests_in"] = sht; d["fused"] = (bool)o[33];
     }
     return d;
   }, py::arg("world"), py::arg("enable") = -1, py::arg("read") = true);

@@ -293,8 +293,9 @@ const char* rt_last_error(void) { return g_err.c_str(); }
 // of the wavefront pipeline. enable: 1 = on, 0 = off, -1 = just read. out[16]:
 // ms[5] (primary, closest, shadow, prep, combine), rays[3], disc[3],
 // n_diag, n_gen, n_planes, n_lights, n_quads, tests[3], boxes[3], bvh,
-// n_bvh_nodes, bvh_depth, n_bvh4_nodes, bvh4_stack, lb_res, lb_items.
-int rtamd_wf_profile(const rt_scene* cs, int enable, double out[29]) {
+// n_bvh_nodes, bvh_depth, (2 unused), lb_res, lb_items, sh_rays[2], sh_tests[2]
+// (shadow rays / sphere tests inside the fused primary / secondary launches), fused.
+int rtamd_wf_profile(const rt_scene* cs, int enable, double out[34]) {
   if (!cs) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
   rt_scene* s = const_cast<rt_scene*>(cs);
   std::lock_guard<std::mutex> lk(s->mu);
@@ -331,30 +332,18 @@ int rtamd_wf_profile(const rt_scene* cs, int enable, double out[29]) {
     out[22] = p.bvh;
     out[23] = s->dev.n_bvh;
     out[24] = s->dev.bvh_depth;
-    out[25] = s->dev.n_bvh4;
-    out[26] = s->dev.bvh4_stack;
+    out[25] = 0;
+    out[26] = 0;
     out[27] = s->dev.lb_cells ? s->dev.lb_res : 0;
     out[28] = s->dev.lb_cells ? s->dev.lb_n_items : 0;
+    for (int i = 0; i < 2; ++i) { out[29 + i] = p.sh_rays[i]; out[31 + i] = p.sh_tests[i]; }
+    out[33] = p.fused;
   }
   return RT_OK;
 }
 
 // Development-only tuning hook (not declared in include/rt_render.h).
 int rtamd_tuning_set(const char* key, int value) {
-  int* tw = !key ? nullptr : std::strcmp(key, "tw_primary") == 0 ? &rtamd::g_tw_primary
-                           : std::strcmp(key, "tw_closest") == 0 ? &rtamd::g_tw_closest
-                           : std::strcmp(key, "tw_shadow") == 0  ? &rtamd::g_tw_shadow : nullptr;
-  if (tw) {
-    if (value != 4 && value != 5 && value != 6 && value != 8) return fail(RT_ERR_INVALID_ARGUMENT, "waves must be 4, 5, 6 or 8");
-    *tw = value;
-    return RT_OK;
-  }
-  if (key && std::strcmp(key, "lane") == 0) {
-    rtamd::g_wf_lane = value;  // 0 = wave traversal, 1 = per-lane (LDS stack when it fits), 2 = per-lane, scratch
-                               // stack, 5 = per-lane with the scene in LDS when it fits, 7 = 5 with leaves batched
-                               // across the wave, 14 = 7 over the pair node layout (default); see rt_wavefront.hip
-    return RT_OK;
-  }
   if (key && std::strcmp(key, "lb_res") == 0) {
     if (value < 0 || value > 512) return fail(RT_ERR_INVALID_ARGUMENT, "lb_res must be in [0, 512]");
     g_lb_res = value;
@@ -364,8 +353,9 @@ int rtamd_tuning_set(const char* key, int value) {
     rtamd::g_wf_shadow_lb = value != 0;
     return RT_OK;
   }
-  if (key && std::strcmp(key, "refill") == 0) {
-    rtamd::g_wf_refill = value;
+  if (key && std::strcmp(key, "image") == 0) {
+    if (value != 0 && value != 1 && value != 3) return fail(RT_ERR_INVALID_ARGUMENT, "image must be 0, 1 or 3");
+    rtamd::g_wf_image = value;
     return RT_OK;
   }
   if (key && std::strcmp(key, "shadow_stream") == 0) {
@@ -375,15 +365,6 @@ int rtamd_tuning_set(const char* key, int value) {
   }
   if (key && std::strcmp(key, "adaptive_block") == 0) {
     rtamd::g_wf_adaptive_block = value != 0;
-    return RT_OK;
-  }
-  if (key && std::strcmp(key, "prim_lane") == 0) {
-    rtamd::g_wf_prim_lane = value != 0;
-    return RT_OK;
-  }
-  if (key && std::strcmp(key, "refill_min") == 0) {
-    if (value < 1 || value > 64) return fail(RT_ERR_INVALID_ARGUMENT, "refill_min must be in [1, 64]");
-    rtamd::g_wf_refill_min = value;
     return RT_OK;
   }
   if (key && std::strcmp(key, "skip_shadow") == 0) {
@@ -406,11 +387,6 @@ int rtamd_tuning_set(const char* key, int value) {
   if (key && std::strcmp(key, "bvh_leaf") == 0) {
     if (value < 1 || value > kBvhLeafMax) return fail(RT_ERR_INVALID_ARGUMENT, "bvh_leaf must be in [1, 127]");
     g_bvh_leaf = value;
-    return RT_OK;
-  }
-  if (key && std::strcmp(key, "wf_waves") == 0) {
-    if (value != 4 && value != 8) return fail(RT_ERR_INVALID_ARGUMENT, "wf_waves must be 4 or 8");
-    rtamd::g_wf_trace_waves = value;
     return RT_OK;
   }
   return fail(RT_ERR_INVALID_ARGUMENT, "unknown tuning key");

@@ -424,6 +424,11 @@ __device__ __forceinline__ V3 pattern_color(const ShadeRec& s, V3 world_point) {
   }
 }
 
+// f64::powf of the specular term (OCML pow). Out of line: inlined into the
+// fused trace kernels, its polynomial constants were hoisted out of the ray
+// loop into VGPRs and spilled across the BVH traversal.
+__device__ __attribute__((noinline)) double spec_pow(double x, double y) { return pow(x, y); }
+
 // Material::lighting (material.rs:38-82)
 // `lightv` = (light.position - point).normalize(), which the caller may
 // already hold: the shadow ray from `point` to the light has exactly that
@@ -443,7 +448,7 @@ __device__ __forceinline__ V3 lighting(const ShadeRec& m, cLightRec L, V3 point,
     const V3 reflectv = vreflect(vneg(lightv), normal);
     const double reflect_dot_eye = vdot(reflectv, eyev);
     if (!(reflect_dot_eye <= 0.0)) {
-      const double factor = pow(reflect_dot_eye, m.shininess);
+      const double factor = spec_pow(reflect_dot_eye, m.shininess);
       specular = vscale(vscale(intensity, m.specular), factor);
     }
   }

@@ -23,26 +23,12 @@
 namespace rtamd {
 
 constexpr int kTraceBlock = 1024;  // trace kernels: 16 waves, one LDS image per block
-// Occupancy of the trace kernels (min waves per SIMD for the register
-// allocator): 8 = two 1024-thread blocks per CU (<= 64 VGPRs), 4 = one.
-int g_wf_trace_waves = 8;  // tuning knob (rtamd_tuning_set("wf_waves", n))
-int g_wf_accel = 1;        // 1 = BVH traversal when counters are not requested, 0 = exhaustive always
-int g_wf_lane = 14;  // secondary rays: 14 = 7 over the pair layout (lane_trace_pair, packed binary32 FMAs);
-                    // shadow rays without a light buffer and scenes that do not fit in LDS take 7's path.
-                    // 7 = per-lane with leaves batched across the wave, scene + stack
-                    // in LDS (when they fit; else 3 = the same with only the stack in LDS), 5 = per-lane, scene
-                    // + stack in LDS, 6 = nodes + stack in LDS, 1 = per-lane with an LDS (or scratch) stack,
-                    // 0 = wave (packet) traversal
+int g_wf_accel = 1;        // 1 = BVH traversal (fused generations) unless the exhaustive loop is asked for
 int g_wf_skip_shadow = 1;  // fast path: leave out shadow rays that cannot change the colour
 int g_wf_shadow_lb = 1;    // 1 = shadow rays through the light buffer (DESIGN.md "Light buffer")
-int g_wf_refill = 0;       // 1 = lanes take a new ray as soon as theirs is done (DESIGN.md "Lane refill");
-                           // LANE 12 = the same for the closest-hit rays of generations >= 1
-int g_wf_refill_min = 16;
-int g_wf_prim_lane = 0;  // tuning knob ("prim_lane"): 1 = primary rays take the per-lane pair traversal too
-// occupancy (waves per SIMD the register allocator targets) of the BVH trace kernels
-int g_tw_primary = 4, g_tw_closest = 4, g_tw_shadow = 4;
+int g_wf_image = 0;        // tuning knob ("image", tests): 0 = the fused kernels pick their scene image,
+                           // 3 / 1 = force the global-memory image with an LDS / scratch stack
 constexpr int kWfBlock = 256;      // prep / shadow / combine
-constexpr int kLbWaves = 4;        // light-buffer shadow kernel (lighting() needs > 64 VGPRs)
 
 #define WF_CHECK(x)                        \
   do {                                     \
@@ -634,50 +620,32 @@ __device__ __forceinline__ void bvh_trace(const DevScene& sc, cPrimRec prim, int
   }
 }
 
-// Per-lane traversal for incoherent rays (secondary and shadow generations):
-// every lane walks the BVH on its own (near child first by its own direction,
-// a private stack), so a wave pays for the longest path instead of the union
-// of 64 paths. Same culling rule and the same exactness argument as the wave
-// traversal above.
+// Per-lane traversal for incoherent rays (secondary and shadow generations)
+// over the binary node layout in global memory (scenes whose image does not
+// fit in LDS): every lane walks the BVH on its own (near child first by its
+// own direction, a private stack), so a wave pays for the longest path
+// instead of the union of 64 paths. Same culling rule and the same exactness
+// argument as the wave traversal above.
 // LDS_STACK: the stack lives in LDS, entry k of lane t at lds[k * kTraceBlock + t]
 // (needs bvh_depth <= kLaneLdsDepth); otherwise in private (scratch) memory.
-// `nodes` / `sd` point at the hierarchy and the sphere records in global
-// memory or at the block's LDS copy. `h` arrives initialised (it may already
-// hold the planes' nearest hit, which tightens the culling).
-// SOA: the LDS image stores chunk k (16 B) of node / sphere record i at
-// chunk array k, element i (LANE == 9), so the lanes' random record reads
-// spread over all LDS banks instead of the few a 64-B record stride reaches.
-template <bool SOA>
-__device__ __forceinline__ void node_chunks(const BvhNode* nodes, int ns, int e, uint4& q0, uint4& q1, uint4& q2,
-                                            uint4& q3) {
+// `h` arrives initialised (it may already hold the planes' nearest hit, which
+// tightens the culling).
+__device__ __forceinline__ void node_chunks(const BvhNode* nodes, int e, uint4& q0, uint4& q1, uint4& q2, uint4& q3) {
   const uint4* b = reinterpret_cast<const uint4*>(nodes);
-  if constexpr (SOA) {
-    q0 = b[e]; q1 = b[e + ns]; q2 = b[e + 2 * ns]; q3 = b[e + 3 * ns];
-  } else {
-    q0 = b[4 * e]; q1 = b[4 * e + 1]; q2 = b[4 * e + 2]; q3 = b[4 * e + 3];
-  }
+  q0 = b[4 * e]; q1 = b[4 * e + 1]; q2 = b[4 * e + 2]; q3 = b[4 * e + 3];
 }
-template <bool SHADOW, bool SOA>
-__device__ __forceinline__ void leaf_sphere_test(const SphereDiag* sd, int nsph, int k, V3 o, V3 d, Hit& h,
-                                                 unsigned& n_disc) {
-  if constexpr (SOA) {
-    const double2* b = reinterpret_cast<const double2*>(sd);
-    const double2 c0 = b[k], c1 = b[k + nsph], c2 = b[k + 2 * nsph];
-    const double s0 = c0.x, s1 = c0.y, s2 = c1.x;
-    sphere_test<SHADOW>(s0 * o.x + c1.y, s1 * o.y + c2.x, s2 * o.z + c2.y, s0 * d.x, s1 * d.y, s2 * d.z,
-                        [&] { return reinterpret_cast<const int*>(b + 3 * nsph + k)[0]; }, h, n_disc);
-  } else {
-    const SphereDiag& r = sd[k];
-    const double s0 = r.s[0], s1 = r.s[1], s2 = r.s[2];
-    sphere_test<SHADOW>(s0 * o.x + r.t[0], s1 * o.y + r.t[1], s2 * o.z + r.t[2], s0 * d.x, s1 * d.y, s2 * d.z,
-                        [&] { return (int)r.meta; }, h, n_disc);
-  }
+template <bool SHADOW>
+__device__ __forceinline__ void leaf_sphere_test(const SphereDiag* sd, int k, V3 o, V3 d, Hit& h, unsigned& n_disc) {
+  const SphereDiag& r = sd[k];
+  const double s0 = r.s[0], s1 = r.s[1], s2 = r.s[2];
+  sphere_test<SHADOW>(s0 * o.x + r.t[0], s1 * o.y + r.t[1], s2 * o.z + r.t[2], s0 * d.x, s1 * d.y, s2 * d.z,
+                      [&] { return (int)r.meta; }, h, n_disc);
 }
 
-template <bool SHADOW, bool LDS_STACK, bool WW = false, bool SOA = false>
+template <bool SHADOW, bool LDS_STACK>
 __device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDiag* sd, const float* M, bool has_bvh,
                                            V3 o, V3 d, double t_shadow, Hit& h, unsigned& n_disc, unsigned& n_tests,
-                                           unsigned& n_boxes, int* lds, int ns = 0, int nsph = 0) {
+                                           unsigned& n_boxes, int* lds) {
   const SlabRay sr = slab_ray(o, d, M);
   float t_hi = f32_up(SHADOW ? t_shadow : h.t);
   int pstk[LDS_STACK ? 1 : kBvhMaxDepth + 4];
@@ -689,7 +657,7 @@ __device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDia
   auto visit = [&]() {
     // the whole 64-B node in four 16-B loads: lo[0], lo[1], hi[0], hi[1], child[2], axis, pad
     uint4 q0, q1, q2, q3;
-    node_chunks<SOA>(nodes, ns, e, q0, q1, q2, q3);
+    node_chunks(nodes, e, q0, q1, q2, q3);
     const float lo0[3] = {__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z)};
     const float lo1[3] = {__uint_as_float(q0.w), __uint_as_float(q1.x), __uint_as_float(q1.y)};
     const float hi0[3] = {__uint_as_float(q1.z), __uint_as_float(q1.w), __uint_as_float(q2.x)};
@@ -711,7 +679,7 @@ __device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDia
   auto leaf = [&](int code_e) {
     const int code = -(code_e + 1);
     const int first = code >> 7, cnt = code & 127;
-    for (int k = first; k < first + cnt; ++k) leaf_sphere_test<SHADOW, SOA>(sd, nsph, k, o, d, h, n_disc);
+    for (int k = first; k < first + cnt; ++k) leaf_sphere_test<SHADOW>(sd, k, o, d, h, n_disc);
     n_tests += (unsigned)cnt;
     if constexpr (SHADOW) {
       return h.key >= 0 && h.t < t_shadow;
@@ -720,219 +688,25 @@ __device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDia
       return false;
     }
   };
-  if constexpr (WW) {
-    // Leaves batched across the wave (speculative while-while): a lane meeting
-    // a leaf postpones it and keeps visiting nodes; the node phase ends when no
-    // lane without a postponed leaf has a node left, then all postponed leaves
-    // are tested together. Culling only ever uses the lane's current bound, so
-    // the postponement changes no result.
-    int pl = kBvhEmpty;
-    for (;;) {
-      for (;;) {
-        if (e < 0 && e != kBvhEmpty && pl == kBvhEmpty) { pl = e; e = pop(); }
-        if (!__any(e >= 0 && pl == kBvhEmpty)) break;
-        if (e >= 0) visit();  // lanes holding a leaf keep going (speculative)
-      }
-      if (!__any(pl != kBvhEmpty)) break;
-      if (pl != kBvhEmpty) {
-        if (leaf(pl)) { e = kBvhEmpty; sp = 0; }  // shadowed: done
-        pl = kBvhEmpty;
-      }
-    }
-    return;
-  }
-#ifdef RTAMD_DIAG
-  unsigned it = 0;  // diagnostic build: loop iterations of this lane vs the wave's
-  const unsigned n_tests0 = n_tests, n_boxes0 = n_boxes;
-#endif
-  while (e != kBvhEmpty) {
-#ifdef RTAMD_DIAG
-    ++it;
-#endif
-    if (e >= 0) {
-      visit();
-    } else {
-      if (leaf(e)) break;  // shadowed: done
-      e = pop();
-    }
-  }
-#ifdef RTAMD_DIAG
-  // diagnostic build: tests = this lane's loop iterations, boxes = the wave's (max over its lanes)
-  unsigned mx = it;
-  for (int off = 32; off > 0; off >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, off, 64));
-  n_tests = n_tests0 + it;
-  n_boxes = n_boxes0 + mx;
-#endif
-}
-
-// Four-wide per-lane traversal (LANE == 8): the same culling rule over the
-// collapsed hierarchy (BvhNode4; its boxes are the binary nodes' boxes, so
-// the exactness argument carries over unchanged). A visit tests the four
-// child boxes as independent instruction streams, continues into the hit
-// child entered first and pushes the other hit children farthest first, so
-// a ray makes about half the dependent node loads of the binary walk. The
-// stack holds 16-bit child codes in LDS (entry k of lane t at
-// stk[k * kTraceBlock]); its top stays in a register, so a pop returns at
-// once and the LDS read of the next entry overlaps the next node's loads.
-// Leaves are batched across the wave (speculative while-while), as in
-// lane_trace<..., WW>.
-template <bool SHADOW>
-__device__ __forceinline__ void lane_trace4(const BvhNode4* nodes, const SphereDiag* sd, const float* M, bool has_bvh,
-                                            V3 o, V3 d, double t_shadow, Hit& h, unsigned& n_disc, unsigned& n_tests,
-                                            unsigned& n_boxes, unsigned short* stk) {
-  const SlabRay sr = slab_ray(o, d, M);
-  float t_hi = f32_up(SHADOW ? t_shadow : h.t);
-  constexpr int E = kBvh4Empty;
-  int sp = 0, top = E;
-  auto push = [&](int v) {
-    if (top != E) stk[(sp++) * kTraceBlock] = (unsigned short)top;
-    top = v;
-  };
-  auto pop = [&]() {
-    const int r = top;
-    top = sp > 0 ? (int)stk[(--sp) * kTraceBlock] : E;
-    return r;
-  };
-  int e = (SHADOW && h.key >= 0 && h.t < t_shadow) || !has_bvh ? E : 0;
-  auto visit = [&]() {
-    const uint4* np = reinterpret_cast<const uint4*>(nodes + e);
-    uint4 q[7];
-#pragma unroll
-    for (int k = 0; k < 7; ++k) q[k] = np[k];
-    const float* f = reinterpret_cast<const float*>(q);  // lo[3][4] at 0, hi[3][4] at 12
-    const unsigned cw[2] = {q[6].x, q[6].y};
-    float dist[4];
-    int code[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      code[k] = (int)((cw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
-      const float lo[3] = {f[k], f[4 + k], f[8 + k]};
-      const float hi[3] = {f[12 + k], f[16 + k], f[20 + k]};
-      float tk;
-      const bool hk = slab_hit32(lo, hi, sr, t_hi, tk) & (code[k] != E);
-      dist[k] = hk ? tk : INFINITY;
-    }
-    n_boxes += 4;
-    // sort the four (distance, code) pairs ascending; misses (inf) sink to the end
-    auto cas = [&](int i, int j) {
-      const bool sw = dist[j] < dist[i];
-      const float di = dist[i], dj = dist[j];
-      const int ci = code[i], cj = code[j];
-      dist[i] = sw ? dj : di; dist[j] = sw ? di : dj;
-      code[i] = sw ? cj : ci; code[j] = sw ? ci : cj;
-    };
-    cas(0, 1); cas(2, 3); cas(0, 2); cas(1, 3); cas(1, 2);
-    if (dist[3] != INFINITY) push(code[3]);
-    if (dist[2] != INFINITY) push(code[2]);
-    if (dist[1] != INFINITY) push(code[1]);
-    e = dist[0] != INFINITY ? code[0] : pop();
-  };
-  auto leaf = [&](int c) {
-    const int first = c & 0xFFF, cnt = ((c >> 12) & 7) + 1;
-    for (int k = first; k < first + cnt; ++k) {
-      const SphereDiag& r = sd[k];
-      const double s0 = r.s[0], s1 = r.s[1], s2 = r.s[2];
-      sphere_test<SHADOW>(s0 * o.x + r.t[0], s1 * o.y + r.t[1], s2 * o.z + r.t[2], s0 * d.x, s1 * d.y, s2 * d.z,
-                          [&] { return (int)r.meta; }, h, n_disc);
-    }
-    n_tests += (unsigned)cnt;
-    if constexpr (SHADOW) {
-      return h.key >= 0 && h.t < t_shadow;
-    } else {
-      t_hi = f32_up(h.t);
-      return false;
-    }
-  };
-  int pl = E;
+  // Leaves batched across the wave (speculative while-while): a lane meeting
+  // a leaf postpones it and keeps visiting nodes; the node phase ends when no
+  // lane without a postponed leaf has a node left, then all postponed leaves
+  // are tested together. Culling only ever uses the lane's current bound, so
+  // the postponement changes no result.
+  int pl = kBvhEmpty;
   for (;;) {
     for (;;) {
-      if (e != E && e >= 0x8000 && pl == E) { pl = e; e = pop(); }
-      if (!__any(e < 0x8000 && pl == E)) break;
-      if (e < 0x8000) visit();  // lanes holding a leaf keep going (speculative)
+      if (e < 0 && e != kBvhEmpty && pl == kBvhEmpty) { pl = e; e = pop(); }
+      if (!__any(e >= 0 && pl == kBvhEmpty)) break;
+      if (e >= 0) visit();  // lanes holding a leaf keep going (speculative)
     }
-    if (!__any(pl != E)) break;
-    if (pl != E) {
-      if (leaf(pl)) { e = E; sp = 0; top = E; }  // shadowed: done
-      pl = E;
-    }
-  }
-}
-
-// Per-lane traversal on 16-bit child codes (LANE == 10 / 11; BvhNode::code16,
-// needs DevScene::bvh_code16): the same visit order, culling rule and
-// leaves batched across the wave as lane_trace<..., WW>, with a stack of
-// 16-bit entries in LDS (entry k of lane t at stk[k * kTraceBlock]) whose top
-// stays in a register, so a pop returns at once and the LDS read of the next
-// entry overlaps the next node's loads. Half the stack bytes of the 32-bit
-// walk: with the sphere records in global memory (LANE 10) a block's LDS
-// image fits twice in a CU.
-template <bool SHADOW>
-__device__ __forceinline__ void lane_trace16(const BvhNode* nodes, const SphereDiag* sd, const float* M, bool has_bvh,
-                                             V3 o, V3 d, double t_shadow, Hit& h, unsigned& n_disc, unsigned& n_tests,
-                                             unsigned& n_boxes, unsigned short* stk) {
-  const SlabRay sr = slab_ray(o, d, M);
-  float t_hi = f32_up(SHADOW ? t_shadow : h.t);
-  constexpr unsigned E = (unsigned)kBvh4Empty;
-  int sp = 0;
-  unsigned top = E;
-  auto push = [&](unsigned v) {
-    if (top != E) stk[(sp++) * kTraceBlock] = (unsigned short)top;
-    top = v;
-  };
-  auto pop = [&]() {
-    const unsigned r = top;
-    top = sp > 0 ? (unsigned)stk[(--sp) * kTraceBlock] : E;
-    return r;
-  };
-  unsigned e = (SHADOW && h.key >= 0 && h.t < t_shadow) || !has_bvh ? E : 0u;
-  auto visit = [&]() {
-    // the two boxes in three 16-B loads, the codes in one 4-B load
-    const uint4* np = reinterpret_cast<const uint4*>(nodes + e);
-    const uint4 q0 = np[0], q1 = np[1], q2 = np[2];
-    const unsigned cc = nodes[e].code16;
-    const float lo0[3] = {__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z)};
-    const float lo1[3] = {__uint_as_float(q0.w), __uint_as_float(q1.x), __uint_as_float(q1.y)};
-    const float hi0[3] = {__uint_as_float(q1.z), __uint_as_float(q1.w), __uint_as_float(q2.x)};
-    const float hi1[3] = {__uint_as_float(q2.y), __uint_as_float(q2.z), __uint_as_float(q2.w)};
-    const unsigned c0 = cc & 0xFFFFu, c1 = cc >> 16;
-    float t0, t1;
-    const bool h0 = slab_hit32(lo0, hi0, sr, t_hi, t0);
-    const bool h1 = slab_hit32(lo1, hi1, sr, t_hi, t1) & (c1 != E);
-    n_boxes += 2;
-    if (h0 && h1) {
-      const bool flip = t1 < t0;
-      push(flip ? c0 : c1);
-      e = flip ? c1 : c0;
-    } else {
-      e = h0 ? c0 : h1 ? c1 : pop();
-    }
-  };
-  auto leaf = [&](unsigned c) {
-    const int first = (int)(c & 0xFFFu), cnt = (int)((c >> 12) & 7u) + 1;
-    for (int k = first; k < first + cnt; ++k) leaf_sphere_test<SHADOW, false>(sd, 0, k, o, d, h, n_disc);
-    n_tests += (unsigned)cnt;
-    if constexpr (SHADOW) {
-      return h.key >= 0 && h.t < t_shadow;
-    } else {
-      t_hi = f32_up(h.t);
-      return false;
-    }
-  };
-  unsigned pl = E;
-  for (;;) {
-    for (;;) {
-      if (e != E && e >= 0x8000u && pl == E) { pl = e; e = pop(); }
-      if (!__any(e < 0x8000u && pl == E)) break;
-      if (e < 0x8000u) visit();  // lanes holding a leaf keep going (speculative)
-    }
-    if (!__any(pl != E)) break;
-    if (pl != E) {
-      if (leaf(pl)) { e = E; sp = 0; top = E; }  // shadowed: done
-      pl = E;
+    if (!__any(pl != kBvhEmpty)) break;
+    if (pl != kBvhEmpty) {
+      if (leaf(pl)) { e = kBvhEmpty; sp = 0; }  // shadowed: done
+      pl = kBvhEmpty;
     }
   }
 }
-
 // Per-lane traversal over the pair layout (LANE == 14): the block's LDS copy
 // of each binary node stores, per axis, the two children's lower bounds as
 // one 8-B pair and their upper bounds as the next pair (lo0 lo1 hi0 hi1 per
@@ -1015,7 +789,7 @@ __device__ __forceinline__ void lane_trace_pair(const unsigned char* nodes, cons
   auto leaf = [&](int code_e) {
     const int code = -(code_e + 1);
     const int first = code >> 7, cnt = code & 127;
-    for (int k = first; k < first + cnt; ++k) leaf_sphere_test<SHADOW, false>(sd, 0, k, o, d, h, n_disc);
+    for (int k = first; k < first + cnt; ++k) leaf_sphere_test<SHADOW>(sd, k, o, d, h, n_disc);
     n_tests += (unsigned)cnt;
     if constexpr (SHADOW) {
       return h.key >= 0 && h.t < t_shadow;
@@ -1056,167 +830,319 @@ __device__ __forceinline__ void stage_lds(uint4* dst, const uint4* src, int n) {
   for (; i < n; i += bd) dst[i] = src[i];
 }
 
-// LANE == 5: the block stages the hierarchy and the sphere records in LDS
-// (dynamic shared memory: [stack bvh_depth x kTraceBlock ints][nodes][spheres];
-// a lane pushes at most one entry per tree level).
+// ------------------------------------------------------------ fused trace kernels
+// The fast path (BVH) evaluates a whole generation in ONE launch per
+// generation (DESIGN.md "Fused generations"): closest hit, prepare_computations,
+// the child-ray spawn, every light's shadow ray and lighting(), and, for a
+// node without children (a miss, a diffuse surface, the last generation), its
+// final colour. Only nodes with a reflected or refracted child are queued
+// (ParentRec) for wf_combine_parents, which runs once the children's colours
+// exist. Scene images of the kernels (LANE):
+//   14: pair-layout nodes + sphere records + per-lane stack in LDS (the default)
+//    3: nodes and records in global memory, per-lane stack in LDS
+//    1: nodes and records in global memory, per-lane stack in scratch (trees
+//       deeper than kLaneLdsDepth)
+//    0: primary rays, wave (packet) traversal over global nodes (one LDS stack
+//       per wave); the sphere records are staged in LDS for the shadow rays
+//       when they fit
+// The per-light box distances of the light buffer are staged in LDS when they
+// fit beside the image (WfArgs::lds_flags).
 __host__ __device__ inline size_t lane_stack_bytes(int depth) { return (size_t)(depth > 0 ? depth : 1) * kTraceBlock * 4; }
-__host__ __device__ inline size_t lane_lds_bytes(const DevScene& sc, bool spheres = true) {
-  return lane_stack_bytes(sc.bvh_depth) + (size_t)sc.n_bvh * sizeof(BvhNode) +
-         (spheres ? (size_t)sc.n_diag * sizeof(SphereDiag) : 0);
+__host__ __device__ inline size_t sph_lds_bytes(const DevScene& sc) { return (size_t)sc.n_diag * sizeof(SphereDiag); }
+__host__ __device__ inline size_t delta_lds_bytes(const DevScene& sc) {
+  return sc.lb_cells ? (((size_t)sc.n_lights * sc.n_diag * sizeof(float) + 15) & ~(size_t)15) : 0;
 }
-// LANE == 8: [16-bit stack bvh4_stack x kTraceBlock][four-wide nodes][spheres]
-__host__ __device__ inline size_t lane4_stack_bytes(const DevScene& sc) {
-  return ((size_t)(sc.bvh4_stack > 0 ? sc.bvh4_stack : 1) * kTraceBlock * 2 + 127) & ~(size_t)127;
+// LANE 14: [stack (bvh_depth + 1 with the sentinel) x kTraceBlock][pair nodes][sphere records]
+__host__ __device__ inline size_t pair_lds_bytes(const DevScene& sc) {
+  return lane_stack_bytes(sc.bvh_depth + 1) + (size_t)sc.n_bvh * sizeof(BvhNode) + sph_lds_bytes(sc);
 }
-__host__ __device__ inline size_t lane4_lds_bytes(const DevScene& sc) {
-  return lane4_stack_bytes(sc) + (size_t)sc.n_bvh4 * sizeof(BvhNode4) + (size_t)sc.n_diag * sizeof(SphereDiag);
-}
-// LANE 10 / 11: [16-bit stack bvh_depth x kTraceBlock][binary nodes][spheres (11 only)]
-__host__ __device__ inline size_t lane16_stack_bytes(const DevScene& sc) {
-  return ((size_t)(sc.bvh_depth > 0 ? sc.bvh_depth : 1) * kTraceBlock * 2 + 127) & ~(size_t)127;
-}
-__host__ __device__ inline size_t lane16_lds_bytes(const DevScene& sc, bool spheres) {
-  return lane16_stack_bytes(sc) + (size_t)sc.n_bvh * sizeof(BvhNode) + (spheres ? (size_t)sc.n_diag * sizeof(SphereDiag) : 0);
-}
+constexpr unsigned kLdsSpheres = 1u, kLdsDeltas = 2u;  // WfArgs::lds_flags (LANE 0: records; all: distances)
+
 struct LaneScene {
-  const BvhNode* nodes;
-  const SphereDiag* sd;
-  int* stack;
-  float M[3];  // bound on |box coordinate| per axis (slab_ray)
-  const BvhNode4* nodes4;
-  unsigned short* stack16;
+  const unsigned char* nodes;  // pair layout in LDS (14) or BvhNode[] in global memory
+  const SphereDiag* sd;        // sphere records (LDS or global)
+  const float* delta;          // light buffer: per-light box distances (LDS or global)
+  int* stack;                  // per-lane LDS stack (14, 3) or the wave's stack (0)
+  float M[3];                  // bound on |box coordinate| per axis (slab_ray)
 };
 template <int LANE>
-__device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, int* static_stack, unsigned char* dyn) {
-  LaneScene ls{sc.bvh, sc.sph_diag, static_stack};
-  if constexpr (LANE == 8) {
-    unsigned short* stack = (unsigned short*)dyn;
-    BvhNode4* nodes = (BvhNode4*)(dyn + lane4_stack_bytes(sc));
-    SphereDiag* sdl = (SphereDiag*)((unsigned char*)nodes + (size_t)sc.n_bvh4 * sizeof(BvhNode4));
-    const uint4* gn = (const uint4*)sc.bvh4;
-    uint4* ln = (uint4*)nodes;
-    stage_lds(ln, gn, sc.n_bvh4 * (int)(sizeof(BvhNode4) / 16));
-    const uint4* gs = (const uint4*)sc.sph_diag;
-    uint4* ls4 = (uint4*)sdl;
-    stage_lds(ls4, gs, sc.n_diag * (int)(sizeof(SphereDiag) / 16));
-    __syncthreads();
-    ls.nodes4 = nodes;
-    ls.sd = sdl;
-    ls.stack16 = stack + threadIdx.x;
-    for (int a = 0; a < 3; ++a) {
-      float m = 0.0f;
-      if (sc.n_bvh4 > 0) {  // the root's child boxes contain every box below them
-        const BvhNode4& r = nodes[0];
-        for (int k = 0; k < 4; ++k)
-          if (r.code[k] != kBvh4Empty) m = fmaxf(m, fmaxf(fabsf(r.lo[a][k]), fabsf(r.hi[a][k])));
-      }
-      ls.M[a] = m;
-    }
-    return ls;
-  }
-  if constexpr (LANE == 10 || LANE == 11) {  // 10: the sphere records stay in global memory
-    unsigned short* stack = (unsigned short*)dyn;
-    BvhNode* nodes = (BvhNode*)(dyn + lane16_stack_bytes(sc));
-    const uint4* gn = (const uint4*)sc.bvh;
-    uint4* ln = (uint4*)nodes;
-    stage_lds(ln, gn, sc.n_bvh * (int)(sizeof(BvhNode) / 16));
-    if constexpr (LANE == 11) {
-      SphereDiag* sdl = (SphereDiag*)((unsigned char*)nodes + (size_t)sc.n_bvh * sizeof(BvhNode));
-      const uint4* gs = (const uint4*)sc.sph_diag;
-      uint4* ls4 = (uint4*)sdl;
-      stage_lds(ls4, gs, sc.n_diag * (int)(sizeof(SphereDiag) / 16));
-      ls.sd = sdl;
-    }
-    __syncthreads();
-    ls.nodes = nodes;
-    ls.stack16 = stack + threadIdx.x;
-  } else if constexpr (LANE == 14) {  // pair layout (lane_trace_pair) + sphere records
-    int* stack = (int*)dyn;
-    unsigned char* nodes = dyn + lane_stack_bytes(sc.bvh_depth + 1);  // + the sentinel entry
+__device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, const WfArgs& a, int* static_stack,
+                                                unsigned char* dyn) {
+  LaneScene ls{(const unsigned char*)sc.bvh, sc.sph_diag, sc.lb_delta, static_stack, {0.f, 0.f, 0.f}};
+  unsigned char* p = dyn;
+  if constexpr (LANE == 14) {
+    // pair layout: per axis, the two children's lower bounds form one 8-B pair
+    // and their upper bounds the next (lane_trace_pair)
+    ls.stack = (int*)dyn + threadIdx.x;
+    p += lane_stack_bytes(sc.bvh_depth + 1);
     for (int i = threadIdx.x; i < sc.n_bvh; i += blockDim.x) {
       const BvhNode& g = sc.bvh[i];
-      float* q = (float*)(nodes + (size_t)i * 64);
-      for (int a = 0; a < 3; ++a) {
-        q[4 * a] = g.lo[0][a]; q[4 * a + 1] = g.lo[1][a]; q[4 * a + 2] = g.hi[0][a]; q[4 * a + 3] = g.hi[1][a];
+      float* q = (float*)(p + (size_t)i * 64);
+      for (int ax = 0; ax < 3; ++ax) {
+        q[4 * ax] = g.lo[0][ax]; q[4 * ax + 1] = g.lo[1][ax]; q[4 * ax + 2] = g.hi[0][ax]; q[4 * ax + 3] = g.hi[1][ax];
       }
       int* c = (int*)(q + 12);
       c[0] = g.child[0]; c[1] = g.child[1]; c[2] = g.axis; c[3] = 0;
     }
-    SphereDiag* sdl = (SphereDiag*)(nodes + (size_t)sc.n_bvh * sizeof(BvhNode));
-    stage_lds((uint4*)sdl, (const uint4*)sc.sph_diag, sc.n_diag * (int)(sizeof(SphereDiag) / 16));
-    __syncthreads();
-    ls.nodes = (const BvhNode*)nodes;  // pair layout: read only by lane_trace_pair
-    ls.sd = sdl;
-    ls.stack = stack + threadIdx.x;
-    for (int a = 0; a < 3; ++a) {  // from the hierarchy in global memory (binary layout)
-      float m = 0.0f;
-      if (sc.n_bvh > 0) {
-        const BvhNode& r = sc.bvh[0];
-        m = fmaxf(fmaxf(fabsf(r.lo[0][a]), fabsf(r.hi[0][a])), fmaxf(fabsf(r.lo[1][a]), fabsf(r.hi[1][a])));
-      }
-      ls.M[a] = m;
-    }
-    return ls;
-  } else if constexpr (LANE >= 5) {  // 6: the sphere records stay in global memory
-    int* stack = (int*)dyn;
-    BvhNode* nodes = (BvhNode*)(dyn + lane_stack_bytes(sc.bvh_depth));
-    const uint4* gn = (const uint4*)sc.bvh;
-    uint4* ln = (uint4*)nodes;
-    // LANE 9: chunk k of record i at k * n + i (node_chunks<true>)
-    if constexpr (LANE == 9) {
-      for (int i = threadIdx.x; i < sc.n_bvh * (int)(sizeof(BvhNode) / 16); i += blockDim.x)
-        ln[(i & 3) * sc.n_bvh + (i >> 2)] = gn[i];
-    } else {
-      stage_lds(ln, gn, sc.n_bvh * (int)(sizeof(BvhNode) / 16));
-    }
-    if constexpr (LANE != 6) {
-      SphereDiag* sd = (SphereDiag*)((unsigned char*)nodes + (size_t)sc.n_bvh * sizeof(BvhNode));
-      const uint4* gs = (const uint4*)sc.sph_diag;
-      uint4* ls4 = (uint4*)sd;
-      if constexpr (LANE == 9) {
-        for (int i = threadIdx.x; i < sc.n_diag * (int)(sizeof(SphereDiag) / 16); i += blockDim.x)
-          ls4[(i & 3) * sc.n_diag + (i >> 2)] = gs[i];
-      } else {
-        stage_lds(ls4, gs, sc.n_diag * (int)(sizeof(SphereDiag) / 16));
-      }
-      ls.sd = sd;
-    }
-    __syncthreads();
-    ls.nodes = nodes;
-    ls.stack = stack + threadIdx.x;
+    ls.nodes = p;
+    p += (size_t)sc.n_bvh * sizeof(BvhNode);
   }
-  for (int a = 0; a < 3; ++a) {
-    float m = 0.0f;
-    if (sc.n_bvh > 0) {  // the root's two child boxes contain every box below them
-      uint4 q[4];
-      node_chunks<LANE == 9>(ls.nodes, sc.n_bvh, 0, q[0], q[1], q[2], q[3]);
-      BvhNode r;
-      memcpy(&r, q, sizeof r);
-      m = fmaxf(fmaxf(fabsf(r.lo[0][a]), fabsf(r.hi[0][a])), fmaxf(fabsf(r.lo[1][a]), fabsf(r.hi[1][a])));
+  if (LANE == 14 || (LANE == 0 && (a.lds_flags & kLdsSpheres))) {
+    stage_lds((uint4*)p, (const uint4*)sc.sph_diag, sc.n_diag * (int)(sizeof(SphereDiag) / 16));
+    ls.sd = (const SphereDiag*)p;
+    p += sph_lds_bytes(sc);
+  }
+  if (a.lds_flags & kLdsDeltas) {
+    float* ld = (float*)p;
+    const int nd = sc.n_lights * sc.n_diag, bd = (int)blockDim.x;
+    int i = (int)threadIdx.x;
+    for (; i + 7 * bd < nd; i += 8 * bd) {  // eight loads in flight per thread
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = sc.lb_delta[i + k * bd];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) ld[i + k * bd] = v[k];
     }
-    ls.M[a] = m;
+    for (; i < nd; i += bd) ld[i] = sc.lb_delta[i];
+    ls.delta = ld;
+  }
+  __syncthreads();
+  for (int ax = 0; ax < 3; ++ax) {  // the root's two child boxes contain every box below them
+    float m = 0.0f;
+    if (sc.n_bvh > 0) {
+      const BvhNode& r = sc.bvh[0];
+      m = fmaxf(fmaxf(fabsf(r.lo[0][ax]), fabsf(r.hi[0][ax])), fmaxf(fabsf(r.lo[1][ax]), fabsf(r.hi[1][ax])));
+    }
+    ls.M[ax] = m;
   }
   return ls;
 }
 
-template <bool PRIMARY, bool QUADS, int LANE, int TW>
-__global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest_bvh(DevScene sc, DevCamera cam, WfArgs a) {
+// World::is_shadowed for the diagonal spheres through the light buffer
+// (DESIGN.md "Light buffer"): the cube-map cell of direction o - light lists
+// every sphere that can block the ray, nearest box first; the walk stops at
+// the first blocker or at the first box farther from the light than the
+// origin. One 16-B load brings the cell's first kLbInline entries. An origin
+// beyond the light's validity radius (or non-finite) tests every sphere.
+__device__ __forceinline__ void lb_walk(const DevScene& sc, const SphereDiag* sd, const float* delta, unsigned l,
+                                        V3 o, V3 d, double dist, Hit& h, unsigned& n_disc, unsigned& n_tests) {
+  cLightRec Lr = (cLightRec)sc.lights + l;
+  if (dist <= (double)sc.lb_limit[l] && dist >= 1e-30) {
+    const int R = sc.lb_res;
+    const unsigned per_light = 6u * (unsigned)R * (unsigned)R;
+    const float half_r = 0.5f * (float)R;
+    // w = o - light (= -(light - o) bit for bit), in binary32
+    const float wx = (float)(o.x - Lr->pos[0]), wy = (float)(o.y - Lr->pos[1]), wz = (float)(o.z - Lr->pos[2]);
+    const float ax = fabsf(wx), ay = fabsf(wy), az = fabsf(wz);
+    unsigned f;
+    float wa, wb, wc;
+    if (ax >= ay && ax >= az) { f = wx < 0.0f ? 1u : 0u; wa = ax; wb = wy; wc = wz; }
+    else if (ay >= az) { f = wy < 0.0f ? 3u : 2u; wa = ay; wb = wz; wc = wx; }
+    else { f = wz < 0.0f ? 5u : 4u; wa = az; wb = wx; wc = wy; }
+    const float u = fminf(fmaxf(wb / wa, -1.0f), 1.0f), v = fminf(fmaxf(wc / wa, -1.0f), 1.0f);
+    const unsigned iu = (unsigned)min((int)((u + 1.0f) * half_r), R - 1);
+    const unsigned iv = (unsigned)min((int)((v + 1.0f) * half_r), R - 1);
+    const LbCell c = sc.lb_cells[l * per_light + (f * (unsigned)R + iv) * (unsigned)R + iu];
+    const unsigned cnt = c.w0 & 0xFFFFu;
+    // the inline entries as a queue of 16-bit indices: idx0..idx3 in q, idx4 in c.w2 >> 16
+    unsigned long long q = (unsigned long long)(c.w0 >> 16) | (unsigned long long)c.w1 << 16 |
+                           (unsigned long long)(c.w2 & 0xFFFFu) << 48;
+    const float* dl = delta + (size_t)l * sc.n_diag;
+    const float dist_up = f32_up(dist);
+    for (unsigned k = 0; k < cnt; ++k) {
+      unsigned idx;
+      if (k < 4u) { idx = (unsigned)(q & 0xFFFFu); q >>= 16; }
+      else if (k == 4u) idx = c.w2 >> 16;
+      else idx = sc.lb_ov[c.ov + k - (unsigned)kLbInline];
+      if (dl[idx] > dist_up) break;  // this box and all after it lie beyond the origin
+      leaf_sphere_test<true>(sd, (int)idx, o, d, h, n_disc);
+      ++n_tests;
+      if (h.key >= 0 && h.t < dist) break;
+    }
+  } else {
+    for (int k = 0; k < sc.n_diag; ++k) {
+      leaf_sphere_test<true>(sd, k, o, d, h, n_disc);
+      ++n_tests;
+      if (h.key >= 0 && h.t < dist) break;
+    }
+  }
+}
+
+// World::is_shadowed (world.rs:95-105) of the ray from `o` towards light `l`
+// (direction d, distance dist): the records outside the BVH first (any hit
+// before the light ends the ray), then the light buffer, or the BVH of the
+// kernel's image when the scene has no light buffer.
+template <int LANE, bool QUADS>
+__device__ __forceinline__ bool shadow_trace(const DevScene& sc, const WfArgs& a, const LaneScene& ls, unsigned l,
+                                             V3 o, V3 d, double dist, unsigned& n_disc, unsigned& n_tests,
+                                             unsigned& n_boxes) {
+  Hit h;
+  hit_init(h);
+  trace_rest<true, QUADS>(sc, o, d, h, n_disc);
+  if (!(h.key >= 0 && h.t < dist)) {
+    if (a.use_lb) {
+      lb_walk(sc, ls.sd, ls.delta, l, o, d, dist, h, n_disc, n_tests);
+    } else if constexpr (LANE == 14) {
+      lane_trace_pair<true>(ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, dist, h, n_disc, n_tests, n_boxes, ls.stack);
+    } else if constexpr (LANE == 0) {
+      Hit hb;  // the wave traversal starts from an empty hit; any blocker is an answer
+      bvh_trace<false, true>(sc, nullptr, ls.stack, o, d, dist, hb, n_disc, n_tests, n_boxes);
+      if (hb.key >= 0 && hb.key != 0x7fffffff && hb.t < dist) h = hb;
+    } else {
+      lane_trace<true, LANE == 3>((const BvhNode*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, dist, h, n_disc,
+                                  n_tests, n_boxes, ls.stack);
+    }
+  }
+  hit_finish(h);
+  return h.key >= 0 && h.t < dist;
+}
+
+// World::shade_hit's combination (world.rs:58-67) of the surface term and the
+// reflected / refracted colours, with the reference's expression.
+__device__ __forceinline__ V3 shade_color(const ShadeRec& m, V3 surface, V3 refl, V3 refr, double schlick_r) {
+  if (m.reflective > 0.0 && m.transparency > 0.0)
+    return vadd(vadd(surface, vscale(refl, schlick_r)), vscale(refr, 1.0 - schlick_r));
+  return vadd(vadd(surface, refl), refr);
+}
+
+// Where generation g's colour of ray `slot` goes: generation 0 of a camera
+// render without AA is tile-ordered, and its colours are written row-major
+// into the output.
+__device__ __forceinline__ double* color_dst(const WfArgs& a, const DevCamera& cam, unsigned slot) {
+  size_t oi = slot;
+  if (a.g == 0 && a.camera_mode && a.aa == 1) {
+    uint32_t x, lr, smp;
+    gen0_pixel(a, cam.hsize, slot, x, lr, smp);
+    oi = (size_t)lr * cam.hsize + x;
+  }
+  return a.colors + oi * 3;
+}
+
+// Per-lane tallies of a fused trace kernel (summed per wave at the end).
+struct FusedTally {
+  unsigned disc = 0, tests = 0, boxes = 0;           // closest-hit work
+  unsigned sh_disc = 0, sh_tests = 0, sh_boxes = 0;  // shadow-ray work
+  unsigned sh_rays = 0;                              // shadow rays traced
+  unsigned hits = 0, refl = 0, refr = 0;             // counted launches: shade_hit runs, children spawned
+};
+
+// Everything after the closest hit of ray `slot` (index i of the generation):
+// prepare_computations (intersection.rs:53-105), the reflected / refracted
+// children (world.rs:107-134), shade_hit's lighting over the lights in order
+// (world.rs:40-56: one is_shadowed per light, a left fold from black), then
+// either the final colour (no children) or a ParentRec. Every lane of the wave
+// calls it (shard_append), `valid` false for the padding lanes.
+template <int LANE, bool QUADS>
+__device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera& cam, const WfArgs& a,
+                                            const LaneScene& ls, unsigned i, unsigned slot, bool valid, V3 o, V3 d,
+                                            const Hit& h, FusedTally& t) {
+  const unsigned L = (unsigned)sc.n_lights;
+  const unsigned remaining = a.max_depth - a.g;
+  bool hit = false, want_refl = false, want_refr = false;
+  Comps c{};
+  V3 refr_dir = v3(0, 0, 0);
+  const ShadeRec* m = nullptr;
+  if (valid && h.key >= 0) {
+    c = prepare(sc, o, d, h);
+    hit = true;
+    m = &sc.shade[c.obj];
+    // reflected_color (world.rs:107-114)
+    want_refl = !(req(m->reflective, 0.0) || remaining == 0);
+    // refracted_color (world.rs:116-134)
+    if (!(req(m->transparency, 0.0) || remaining == 0)) {
+      const double n_ratio = c.n1 / c.n2;
+      const double cos_i = vdot(c.eyev, c.normal);
+      const double sin2_t = n_ratio * n_ratio * (1.0 - cos_i * cos_i);
+      if (!(sin2_t > 1.0)) {
+        const double cos_t = sqrt(1.0 - sin2_t);
+        refr_dir = vsub(vscale(c.normal, n_ratio * cos_i - cos_t), vscale(c.eyev, n_ratio));
+        want_refr = true;
+      }
+    }
+  }
+  const bool parent = want_refl || want_refr;
+  unsigned pbase, rbase, fbase;
+  shard_append(a, i / 64, parent ? 1u : 0u, want_refl, want_refr, pbase, rbase, fbase);
+  if (!valid) return;
+  t.hits += hit; t.refl += want_refl; t.refr += want_refr;
+  double* dst = color_dst(a, cam, slot);
+  if (!hit) {  // color_at: a miss is black (world.rs:74-75)
+    dst[0] = 0.0; dst[1] = 0.0; dst[2] = 0.0;
+    return;
+  }
+  int child_refl = -1, child_refr = -1;
+  if (want_refl && rbase != ~0u) {
+    const V3 rv = vreflect(d, c.normal);  // comps.reflectv (intersection.rs:101)
+    WfRay r;
+    r.o[0] = c.over.x; r.o[1] = c.over.y; r.o[2] = c.over.z;
+    r.d[0] = rv.x; r.d[1] = rv.y; r.d[2] = rv.z;
+    r.pad = 0;
+    a.next_rays[rbase] = r;
+    child_refl = (int)rbase;
+  }
+  if (want_refr && fbase != ~0u) {
+    WfRay r;
+    r.o[0] = c.under.x; r.o[1] = c.under.y; r.o[2] = c.under.z;
+    r.d[0] = refr_dir.x; r.d[1] = refr_dir.y; r.d[2] = refr_dir.z;
+    r.pad = 0;
+    a.next_rays[fbase] = r;
+    child_refr = (int)fbase;
+  }
+  // shade_hit's Schlick factor (world.rs:62-64), same inputs as the reference's call
+  const double schlick_r =
+      (m->reflective > 0.0 && m->transparency > 0.0) ? schlick(c.eyev, c.normal, c.n1, c.n2) : 0.0;
+  // surface = Sum over the lights of lighting(..., is_shadowed(over_point, light))
+  V3 surface = v3(0.0, 0.0, 0.0);  // fold from (0,0,0) (color.rs:96-103)
+  for (unsigned l = 0; l < L; ++l) {
+    cLightRec Lr = (cLightRec)sc.lights + l;
+    V3 term;
+    if (a.skip_shadow && shadow_irrelevant(*m, Lr, c.over, c.normal, term)) {
+      // the light is behind the surface: lighting() is the ambient term either way
+    } else {
+      // the shadow ray exactly as World::is_shadowed builds it (world.rs:95-105)
+      const V3 v = vsub(v3(Lr->pos[0], Lr->pos[1], Lr->pos[2]), c.over);
+      const double dist = sqrt(v.x * v.x + v.y * v.y + v.z * v.z);  // magnitude (vector.rs:21-23)
+      const V3 sdir = vnormalize(v);
+      const bool shadowed = shadow_trace<LANE, QUADS>(sc, a, ls, l, c.over, sdir, dist, t.sh_disc, t.sh_tests,
+                                                      t.sh_boxes);
+      ++t.sh_rays;
+      term = lighting(*m, Lr, c.over, c.eyev, c.normal, shadowed, sdir);
+    }
+    surface = vadd(surface, term);
+  }
+  if (child_refl >= 0 || child_refr >= 0) {  // the children's colours come later (wf_combine_parents)
+    ParentRec pr;
+    pr.surface[0] = surface.x; pr.surface[1] = surface.y; pr.surface[2] = surface.z;
+    pr.schlick = schlick_r;
+    pr.slot = slot; pr.obj = c.obj; pr.child_refl = child_refl; pr.child_refr = child_refr;
+    if (pbase != ~0u) a.parents[pbase] = pr;
+    return;
+  }
+  const V3 zero = v3(0.0, 0.0, 0.0);  // reflected / refracted colour: black (world.rs:108-109, 117-118)
+  const V3 col = shade_color(*m, surface, zero, zero, schlick_r);
+  dst[0] = col.x; dst[1] = col.y; dst[2] = col.z;
+}
+
+// One generation of the fast path (see above). PRIMARY: generation 0 of a
+// camera render (wave traversal with the shared-origin primary records).
+template <bool PRIMARY, bool QUADS, int LANE>
+__global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, DevCamera cam, WfArgs a) {
 #ifdef RTAMD_PHASE
   // phase-timing build (dev): shader cycles per wave of LDS staging (disc),
-  // traversal (tests) and shading + spawn (boxes), summed over the waves
+  // traversal (tests) and shading + shadow rays + spawn (boxes), summed over the waves
   const unsigned long long ph0 = __builtin_amdgcn_s_memtime();
   unsigned long long ph_stage = 0, ph_trav = 0, ph_prep = 0;
 #endif
-  constexpr bool LDS_STACK = LANE >= 2;
-  __shared__ int stack_lds[LANE >= 5 ? 1 : LDS_STACK ? kLaneLdsDepth * kTraceBlock : (kTraceBlock / 64) * (kBvhMaxDepth + 4)];
+  __shared__ int stack_lds[LANE == 3 ? kLaneLdsDepth * kTraceBlock
+                           : LANE == 0 ? (kTraceBlock / 64) * (kBvhMaxDepth + 4) : 1];
   extern __shared__ __attribute__((aligned(16))) unsigned char lane_dyn[];
-  int* stk = LDS_STACK ? stack_lds + threadIdx.x : stack_lds + (threadIdx.x / 64) * (kBvhMaxDepth + 4);
-  const LaneScene ls = lane_scene<LANE>(sc, stk, lane_dyn);
+  int* stk = LANE == 0 ? stack_lds + (threadIdx.x / 64) * (kBvhMaxDepth + 4) : stack_lds + threadIdx.x;
+  const LaneScene ls = lane_scene<LANE>(sc, a, stk, lane_dyn);
   __shared__ unsigned s_pre[kShards + 1];
   const unsigned* pre = shard_prefix(a.in_cnt, s_pre);
-  unsigned n_disc = 0, n_tests = 0, n_boxes = 0;
+  FusedTally t;
   const unsigned stride = gridDim.x * blockDim.x;
-  // every lane of a wave runs the same number of iterations (prep_one's appends are wave-wide)
+  // every lane of a wave runs the same number of iterations (the appends are wave-wide)
   const unsigned n_iter = (a.n + stride - 1) / stride;
   unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
 #ifdef RTAMD_PHASE
@@ -1233,23 +1159,17 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest_bvh(DevScene
     hit_init(h);
     if (valid) {
       wf_ray(a, cam, slot, o, d);
-      if constexpr (LANE == 14) {  // also primary rays (g_wf_prim_lane)
-        trace_rest<false, QUADS>(sc, o, d, h, n_disc);  // planes first: an early nearest hit tightens the culling
-        lane_trace_pair<false>((const unsigned char*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, n_disc,
-                               n_tests, n_boxes, ls.stack);
-      } else if constexpr ((LANE == 10 || LANE == 11) && !PRIMARY) {
-        trace_rest<false, QUADS>(sc, o, d, h, n_disc);  // planes first: an early nearest hit tightens the culling
-        lane_trace16<false>(ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, n_disc, n_tests, n_boxes, ls.stack16);
-      } else if constexpr (LANE == 8 && !PRIMARY) {
-        trace_rest<false, QUADS>(sc, o, d, h, n_disc);  // planes first: an early nearest hit tightens the culling
-        lane_trace4<false>(ls.nodes4, ls.sd, ls.M, sc.n_bvh4 > 0, o, d, 0.0, h, n_disc, n_tests, n_boxes, ls.stack16);
-      } else if constexpr (LANE && !PRIMARY) {
-        trace_rest<false, QUADS>(sc, o, d, h, n_disc);  // planes first: an early nearest hit tightens the culling
-        lane_trace<false, LDS_STACK, LANE == 7 || LANE == 3 || LANE == 9, LANE == 9>(
-            ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, n_disc, n_tests, n_boxes, ls.stack, sc.n_bvh, sc.n_diag);
+      if constexpr (LANE == 0) {
+        bvh_trace<PRIMARY, false>(sc, (cPrimRec)a.prim, stk, o, d, 0.0, h, t.disc, t.tests, t.boxes);
+        trace_rest<false, QUADS>(sc, o, d, h, t.disc);
       } else {
-        bvh_trace<PRIMARY, false>(sc, (cPrimRec)a.prim, stk, o, d, 0.0, h, n_disc, n_tests, n_boxes);
-        trace_rest<false, QUADS>(sc, o, d, h, n_disc);
+        trace_rest<false, QUADS>(sc, o, d, h, t.disc);  // planes first: an early nearest hit tightens the culling
+        if constexpr (LANE == 14)
+          lane_trace_pair<false>(ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, t.disc, t.tests, t.boxes,
+                                 ls.stack);
+        else
+          lane_trace<false, LANE == 3>((const BvhNode*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, t.disc,
+                                       t.tests, t.boxes, ls.stack);
       }
     }
     hit_finish(h);
@@ -1257,7 +1177,7 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest_bvh(DevScene
     const unsigned long long pb = __builtin_amdgcn_s_memtime();
     ph_trav += pb - pa;
 #endif
-    prep_one(sc, a, i, slot, valid, o, d, h);  // the hit is shaded and spawned right here
+    shade_fused<LANE, QUADS>(sc, cam, a, ls, i, slot, valid, o, d, h, t);
 #ifdef RTAMD_PHASE
     ph_prep += __builtin_amdgcn_s_memtime() - pb;
 #endif
@@ -1270,374 +1190,28 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest_bvh(DevScene
   }
   return;
 #endif
-  const unsigned long long s = wave_sum(n_disc), st = wave_sum(n_tests), sb = wave_sum(n_boxes);
+  const unsigned long long s = wave_sum(t.disc), st = wave_sum(t.tests), sb = wave_sum(t.boxes);
+  const unsigned long long hs = wave_sum(t.sh_disc), hst = wave_sum(t.sh_tests), hsb = wave_sum(t.sh_boxes);
+  const unsigned long long hr = wave_sum(t.sh_rays);
   if (lane_id() == 0) {
-    if (s) atomicAdd(&work_row(a.cnt)->disc[a.disc_slot], s);
-    if (st) atomicAdd(&work_row(a.cnt)->tests[a.disc_slot], st);
-    if (sb) atomicAdd(&work_row(a.cnt)->boxes[a.disc_slot], sb);
+    WfWorkRow* w = work_row(a.cnt);
+    if (s) atomicAdd(&w->disc[a.disc_slot], s);
+    if (st) atomicAdd(&w->tests[a.disc_slot], st);
+    if (sb) atomicAdd(&w->boxes[a.disc_slot], sb);
+    if (hs) atomicAdd(&w->disc[WF_SHADOW], hs);
+    if (hst) { atomicAdd(&w->tests[WF_SHADOW], hst); atomicAdd(&w->sh_tests[a.disc_slot], hst); }
+    if (hsb) atomicAdd(&w->boxes[WF_SHADOW], hsb);
+    if (hr) atomicAdd(&w->sh_rays[a.disc_slot], hr);
+  }
+  if (a.count) {  // counted launch: shade_hit runs and children per generation (read_stats)
+    const unsigned long long n1 = wave_sum(t.hits), n2 = wave_sum(t.refl), n3 = wave_sum(t.refr);
+    if (lane_id() == 0) {
+      if (n1) atomicAdd(&a.cnt->n_hit[a.g], (unsigned)n1);
+      if (n2) atomicAdd(&a.cnt->n_refl[a.g], (unsigned)n2);
+      if (n3) atomicAdd(&a.cnt->n_refr[a.g], (unsigned)n3);
+    }
   }
 }
-
-template <bool QUADS, int LANE, int TW>
-__global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow_bvh(DevScene sc, WfArgs a) {
-  constexpr bool LDS_STACK = LANE >= 2;
-  __shared__ int stack_lds[LANE >= 5 ? 1 : LDS_STACK ? kLaneLdsDepth * kTraceBlock : (kTraceBlock / 64) * (kBvhMaxDepth + 4)];
-  extern __shared__ __attribute__((aligned(16))) unsigned char lane_dyn[];
-  int* stk = LDS_STACK ? stack_lds + threadIdx.x : stack_lds + (threadIdx.x / 64) * (kBvhMaxDepth + 4);
-  const LaneScene ls = lane_scene<LANE>(sc, stk, lane_dyn);
-  __shared__ unsigned s_pre[kShards + 1];
-  const unsigned* pre = shard_prefix(a.sh_cnt, s_pre);
-  unsigned n_disc = 0, n_tests = 0, n_boxes = 0;
-  const unsigned stride = gridDim.x * blockDim.x;
-  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n_shadow; i += stride) {
-    V3 o, d;
-    double dist;
-    unsigned slot;
-    shadow_ray(sc, a, shard_slot(pre, a.sh_cap, i), o, d, dist, slot);
-    Hit h;
-    if constexpr (LANE == 8) {
-      hit_init(h);
-      trace_rest<true, QUADS>(sc, o, d, h, n_disc);  // planes first: any hit before the light ends the ray
-      lane_trace4<true>(ls.nodes4, ls.sd, ls.M, sc.n_bvh4 > 0, o, d, dist, h, n_disc, n_tests, n_boxes, ls.stack16);
-    } else if constexpr (LANE) {
-      hit_init(h);
-      trace_rest<true, QUADS>(sc, o, d, h, n_disc);  // planes first: any hit before the light ends the ray
-      lane_trace<true, LDS_STACK, LANE == 7 || LANE == 3 || LANE == 9, LANE == 9>(
-          ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, dist, h, n_disc, n_tests, n_boxes, ls.stack, sc.n_bvh, sc.n_diag);
-    } else {
-      bvh_trace<false, true>(sc, nullptr, stk, o, d, dist, h, n_disc, n_tests, n_boxes);
-      if (__any(!(h.key >= 0 && h.t < dist))) trace_rest<true, QUADS>(sc, o, d, h, n_disc);
-    }
-    hit_finish(h);
-    shadow_result(sc, a, slot, h.key >= 0 && h.t < dist, o, d);
-  }
-  const unsigned long long sd = wave_sum(n_disc), st = wave_sum(n_tests), sb = wave_sum(n_boxes);
-  if (lane_id() == 0) {
-    if (sd) atomicAdd(&work_row(a.cnt)->disc[a.disc_slot], sd);
-    if (st) atomicAdd(&work_row(a.cnt)->tests[a.disc_slot], st);
-    if (sb) atomicAdd(&work_row(a.cnt)->boxes[a.disc_slot], sb);
-  }
-}
-
-// Shadow rays with lane refill (DESIGN.md "Lane refill"): the per-lane
-// traversal of lane_trace<true, true, true> (binary nodes, sphere records and
-// stack in LDS, leaves batched across the wave), but a lane whose ray is
-// finished takes the next ray of its wave's range at once instead of idling
-// until the wave's longest ray is done. Each wave owns a contiguous range of
-// the shadow list (neighbouring rays stay together); a refill happens after a
-// leaf round once at least kRefillMin lanes are idle (or none is busy).
-// Results are per ray and independent of when a ray runs, so the flags are
-// those of lane_trace.
-constexpr int kRefillMin = 16;
-template <bool QUADS, int LANE, int TW>
-__global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow_refill(DevScene sc, WfArgs a) {
-  constexpr bool SOA = LANE == 9;
-  __shared__ int stack_lds[1];
-  extern __shared__ __attribute__((aligned(16))) unsigned char lane_dyn[];
-  const LaneScene ls = lane_scene<LANE>(sc, stack_lds, lane_dyn);
-  __shared__ unsigned s_pre[kShards + 1];
-  const unsigned* pre = shard_prefix(a.sh_cnt, s_pre);
-  unsigned n_disc = 0, n_tests = 0, n_boxes = 0;
-  const unsigned waves = gridDim.x * (blockDim.x / 64);
-  const unsigned wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
-  const unsigned per = (a.n_shadow + waves - 1) / waves;
-  unsigned next = min(wave * per, a.n_shadow);
-  const unsigned end = min(next + per, a.n_shadow);
-  const unsigned lane = lane_id();
-  const unsigned long long below = (1ull << lane) - 1ull;
-  int* const stk = ls.stack;
-  const bool has_bvh = sc.n_bvh > 0;
-  // lane state
-  bool active = false;
-  V3 o = v3(0, 0, 0), d = v3(0, 0, 0);
-  double dist = 0.0;
-  unsigned slot = 0;
-  Hit h;
-  hit_init(h);
-  SlabRay sr{};
-  float t_hi = 0.0f;
-  int e = kBvhEmpty, pl = kBvhEmpty, sp = 0;
-  auto pop = [&]() { return sp > 0 ? stk[(--sp) * kTraceBlock] : kBvhEmpty; };
-  for (;;) {
-    // refill idle lanes from the wave's range
-    const unsigned long long idle = __ballot(!active);
-    const unsigned n_idle = (unsigned)__popcll(idle);
-    if (next < end && (n_idle >= kRefillMin || n_idle == 64u)) {
-      const unsigned j = next + (unsigned)__popcll(idle & below);
-      next = min(next + n_idle, end);
-      if (!active && j < end) {
-        shadow_ray(sc, a, shard_slot(pre, a.sh_cap, j), o, d, dist, slot);
-        hit_init(h);
-        trace_rest<true, QUADS>(sc, o, d, h, n_disc);  // planes first: any hit before the light ends the ray
-        sr = slab_ray(o, d, ls.M);
-        t_hi = f32_up(dist);
-        sp = 0;
-        pl = kBvhEmpty;
-        e = (h.key >= 0 && h.t < dist) || !has_bvh ? kBvhEmpty : 0;
-        active = true;
-      }
-    }
-    if (!__any(active)) break;
-    // node phase: lanes meeting a leaf postpone it and keep visiting nodes
-    for (;;) {
-      if (e < 0 && e != kBvhEmpty && pl == kBvhEmpty) { pl = e; e = pop(); }
-      if (!__any(e >= 0 && pl == kBvhEmpty)) break;
-      if (e >= 0) {
-        uint4 q0, q1, q2, q3;
-        node_chunks<SOA>(ls.nodes, sc.n_bvh, e, q0, q1, q2, q3);
-        const float lo0[3] = {__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z)};
-        const float lo1[3] = {__uint_as_float(q0.w), __uint_as_float(q1.x), __uint_as_float(q1.y)};
-        const float hi0[3] = {__uint_as_float(q1.z), __uint_as_float(q1.w), __uint_as_float(q2.x)};
-        const float hi1[3] = {__uint_as_float(q2.y), __uint_as_float(q2.z), __uint_as_float(q2.w)};
-        const int c0 = (int)q3.x, c1 = (int)q3.y;
-        float t0, t1;
-        const bool h0 = slab_hit32(lo0, hi0, sr, t_hi, t0);
-        const bool h1 = slab_hit32(lo1, hi1, sr, t_hi, t1) & (c1 != kBvhEmpty);
-        n_boxes += 2;
-        if (h0 && h1) {
-          const bool flip = t1 < t0;
-          stk[(sp++) * kTraceBlock] = flip ? c0 : c1;
-          e = flip ? c1 : c0;
-        } else {
-          e = h0 ? c0 : h1 ? c1 : pop();
-        }
-      }
-    }
-    // leaf round
-    if (pl != kBvhEmpty) {
-      const int code = -(pl + 1);
-      const int first = code >> 7, cnt = code & 127;
-      for (int k = first; k < first + cnt; ++k) leaf_sphere_test<true, SOA>(ls.sd, sc.n_diag, k, o, d, h, n_disc);
-      n_tests += (unsigned)cnt;
-      if (h.key >= 0 && h.t < dist) { e = kBvhEmpty; sp = 0; }  // shadowed: done
-      pl = kBvhEmpty;
-    }
-    if (active && e == kBvhEmpty && pl == kBvhEmpty) {
-      shadow_result(sc, a, slot, h.key >= 0 && h.t < dist, o, d);
-      active = false;
-    }
-  }
-  const unsigned long long sd = wave_sum(n_disc), st = wave_sum(n_tests), sb = wave_sum(n_boxes);
-  if (lane_id() == 0) {
-    if (sd) atomicAdd(&work_row(a.cnt)->disc[a.disc_slot], sd);
-    if (st) atomicAdd(&work_row(a.cnt)->tests[a.disc_slot], st);
-    if (sb) atomicAdd(&work_row(a.cnt)->boxes[a.disc_slot], sb);
-  }
-}
-
-// Closest-hit rays with lane refill (LANE == 12, DESIGN.md "Lane refill"):
-// the per-lane traversal of lane_trace<false, true, true> (binary nodes,
-// sphere records and stack in LDS, leaves batched across the wave), but a
-// lane whose ray is finished takes the next ray of its wave's range at once
-// instead of idling until the wave's longest ray is done. The hit goes to the
-// hit queue; wf_prep shades it and spawns the children (prep_one needs whole
-// waves, which a refilling wave does not have). Each wave owns a contiguous
-// range of the generation; a refill happens after a leaf round once at least
-// a.refill_min lanes are idle (or none is busy). A ray's hit does not depend
-// on when or where it is traced, so the hits are those of lane_trace.
-template <bool QUADS, int TW>
-__global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest_refill(DevScene sc, DevCamera cam, WfArgs a) {
-  __shared__ int stack_lds[1];
-  extern __shared__ __attribute__((aligned(16))) unsigned char lane_dyn[];
-  const LaneScene ls = lane_scene<7>(sc, stack_lds, lane_dyn);
-  __shared__ unsigned s_pre[kShards + 1];
-  const unsigned* pre = shard_prefix(a.in_cnt, s_pre);
-  unsigned n_disc = 0, n_tests = 0, n_boxes = 0;
-  const unsigned waves = gridDim.x * (blockDim.x / 64);
-  const unsigned wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
-  const unsigned per = (a.n + waves - 1) / waves;
-  unsigned next = min(wave * per, a.n);
-  const unsigned end = min(next + per, a.n);
-  const unsigned lane = lane_id();
-  const unsigned long long below = (1ull << lane) - 1ull;
-  int* const stk = ls.stack;
-  const bool has_bvh = sc.n_bvh > 0;
-  const unsigned rmin = a.refill_min;
-  bool active = false;
-  V3 o = v3(0, 0, 0), d = v3(0, 0, 0);
-  unsigned slot = 0;
-  Hit h;
-  hit_init(h);
-  SlabRay sr{};
-  float t_hi = 0.0f;
-  int e = kBvhEmpty, pl = kBvhEmpty, sp = 0;
-  auto pop = [&]() { return sp > 0 ? stk[(--sp) * kTraceBlock] : kBvhEmpty; };
-  for (;;) {
-    // refill idle lanes from the wave's range
-    const unsigned long long idle = __ballot(!active);
-    const unsigned n_idle = (unsigned)__popcll(idle);
-    if (next < end && (n_idle >= rmin || n_idle == 64u)) {
-      const unsigned j = next + (unsigned)__popcll(idle & below);
-      next = min(next + n_idle, end);
-      if (!active && j < end) {
-        slot = shard_slot(pre, a.in_cap, j);
-        wf_ray(a, cam, slot, o, d);
-        hit_init(h);
-        trace_rest<false, QUADS>(sc, o, d, h, n_disc);  // planes first: an early nearest hit tightens the culling
-        sr = slab_ray(o, d, ls.M);
-        t_hi = f32_up(h.t);
-        sp = 0;
-        pl = kBvhEmpty;
-        e = has_bvh ? 0 : kBvhEmpty;
-        active = true;
-      }
-    }
-    if (!__any(active)) break;
-    // node phase: lanes meeting a leaf postpone it and keep visiting nodes
-    for (;;) {
-      if (e < 0 && e != kBvhEmpty && pl == kBvhEmpty) { pl = e; e = pop(); }
-      if (!__any(e >= 0 && pl == kBvhEmpty)) break;
-      if (e >= 0) {
-        uint4 q0, q1, q2, q3;
-        node_chunks<false>(ls.nodes, sc.n_bvh, e, q0, q1, q2, q3);
-        const float lo0[3] = {__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z)};
-        const float lo1[3] = {__uint_as_float(q0.w), __uint_as_float(q1.x), __uint_as_float(q1.y)};
-        const float hi0[3] = {__uint_as_float(q1.z), __uint_as_float(q1.w), __uint_as_float(q2.x)};
-        const float hi1[3] = {__uint_as_float(q2.y), __uint_as_float(q2.z), __uint_as_float(q2.w)};
-        const int c0 = (int)q3.x, c1 = (int)q3.y;
-        float t0, t1;
-        const bool h0 = slab_hit32(lo0, hi0, sr, t_hi, t0);
-        const bool h1 = slab_hit32(lo1, hi1, sr, t_hi, t1) & (c1 != kBvhEmpty);
-        n_boxes += 2;
-        if (h0 && h1) {
-          const bool flip = t1 < t0;
-          stk[(sp++) * kTraceBlock] = flip ? c0 : c1;
-          e = flip ? c1 : c0;
-        } else {
-          e = h0 ? c0 : h1 ? c1 : pop();
-        }
-      }
-    }
-    // leaf round
-    if (pl != kBvhEmpty) {
-      const int code = -(pl + 1);
-      const int first = code >> 7, cnt = code & 127;
-      for (int k = first; k < first + cnt; ++k) leaf_sphere_test<false, false>(ls.sd, sc.n_diag, k, o, d, h, n_disc);
-      n_tests += (unsigned)cnt;
-      t_hi = f32_up(h.t);
-      pl = kBvhEmpty;
-    }
-    if (active && e == kBvhEmpty && pl == kBvhEmpty) {
-      hit_finish(h);
-      WfHit w;
-      w.t = h.t; w.key = h.key; w.c1k = h.c1k; w.c2k = h.c2k; w.hin = h.hin;
-      a.hits[slot] = w;
-      active = false;
-    }
-  }
-  const unsigned long long s = wave_sum(n_disc), st = wave_sum(n_tests), sb = wave_sum(n_boxes);
-  if (lane_id() == 0) {
-    if (s) atomicAdd(&work_row(a.cnt)->disc[a.disc_slot], s);
-    if (st) atomicAdd(&work_row(a.cnt)->tests[a.disc_slot], st);
-    if (sb) atomicAdd(&work_row(a.cnt)->boxes[a.disc_slot], sb);
-  }
-}
-
-// Shadow rays through the light buffer (DESIGN.md "Light buffer"): the
-// planes / general records first, exhaustively (as in every trace kernel),
-// then the cube-map cell of direction o - light lists every diagonal sphere
-// that can block the ray, nearest box first; the walk stops at the first
-// blocker or at the first box farther from the light than the origin. One
-// 16-B load brings the cell's first kLbInline entries. A ray whose origin is
-// beyond the light's validity radius (or non-finite) tests every sphere. The
-// sphere records and the per-light box distances are staged in LDS when they
-// fit.
-__host__ __device__ inline size_t lb_lds_bytes(const DevScene& sc) {
-  return (size_t)sc.n_diag * sizeof(SphereDiag) + (((size_t)sc.n_lights * sc.n_diag * sizeof(float) + 15) & ~(size_t)15);
-}
-// LDS: 1 = sphere records and box distances staged in LDS, 2 = only the box
-// distances (scenes whose records do not fit, e.g. C5), 0 = neither.
-template <bool QUADS, int LDS, int TW>
-__global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow_lb(DevScene sc, WfArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char lane_dyn[];
-  const SphereDiag* sd = sc.sph_diag;
-  const float* delta = sc.lb_delta;
-  if constexpr (LDS == 1) {
-    const uint4* gs = (const uint4*)sc.sph_diag;
-    uint4* ls4 = (uint4*)lane_dyn;
-    const int n_rec = sc.n_diag * (int)(sizeof(SphereDiag) / 16);
-    stage_lds(ls4, gs, n_rec);
-    sd = (const SphereDiag*)lane_dyn;  // shard_prefix (or the barrier below) synchronises the block
-  }
-  if constexpr (LDS != 0) {
-    float* ld = (float*)(lane_dyn + (LDS == 1 ? (size_t)sc.n_diag * sizeof(SphereDiag) : 0));
-    const int nd = sc.n_lights * sc.n_diag, bd = (int)blockDim.x;
-    int i = (int)threadIdx.x;
-    for (; i + 7 * bd < nd; i += 8 * bd) {  // eight loads in flight per thread
-      float v[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = sc.lb_delta[i + k * bd];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) ld[i + k * bd] = v[k];
-    }
-    for (; i < nd; i += bd) ld[i] = sc.lb_delta[i];
-    delta = ld;
-  }
-  __shared__ unsigned s_pre[kShards + 1];
-  const unsigned* pre = shard_prefix(a.sh_cnt, s_pre);
-  if (!pre) __syncthreads();
-  unsigned n_disc = 0, n_tests = 0;
-  const int R = sc.lb_res;
-  const unsigned per_light = 6u * (unsigned)R * (unsigned)R;
-  const float half_r = 0.5f * (float)R;
-  const unsigned stride = gridDim.x * blockDim.x;
-  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n_shadow; i += stride) {
-    V3 o, d;
-    double dist;
-    unsigned slot, l;
-    shadow_ray(sc, a, shard_slot(pre, a.sh_cap, i), o, d, dist, slot, &l);
-    Hit h;
-    hit_init(h);
-    trace_rest<true, QUADS>(sc, o, d, h, n_disc);  // planes first: any hit before the light ends the ray
-    if (!(h.key >= 0 && h.t < dist)) {
-      cLightRec Lr = (cLightRec)sc.lights + l;
-      if (dist <= (double)sc.lb_limit[l] && dist >= 1e-30) {
-        // w = o - light (= -(light - o) bit for bit), in binary32
-        const float wx = (float)(o.x - Lr->pos[0]), wy = (float)(o.y - Lr->pos[1]), wz = (float)(o.z - Lr->pos[2]);
-        const float ax = fabsf(wx), ay = fabsf(wy), az = fabsf(wz);
-        unsigned f;
-        float wa, wb, wc;
-        if (ax >= ay && ax >= az) { f = wx < 0.0f ? 1u : 0u; wa = ax; wb = wy; wc = wz; }
-        else if (ay >= az) { f = wy < 0.0f ? 3u : 2u; wa = ay; wb = wz; wc = wx; }
-        else { f = wz < 0.0f ? 5u : 4u; wa = az; wb = wx; wc = wy; }
-        const float u = fminf(fmaxf(wb / wa, -1.0f), 1.0f), v = fminf(fmaxf(wc / wa, -1.0f), 1.0f);
-        const unsigned iu = (unsigned)min((int)((u + 1.0f) * half_r), R - 1);
-        const unsigned iv = (unsigned)min((int)((v + 1.0f) * half_r), R - 1);
-        const LbCell c = sc.lb_cells[l * per_light + (f * (unsigned)R + iv) * (unsigned)R + iu];
-        const unsigned cnt = c.w0 & 0xFFFFu;
-        // the inline entries as a queue of 16-bit indices: idx0..idx3 in q, idx4 in c.w2 >> 16
-        unsigned long long q = (unsigned long long)(c.w0 >> 16) | (unsigned long long)c.w1 << 16 |
-                               (unsigned long long)(c.w2 & 0xFFFFu) << 48;
-        const float* dl = delta + (size_t)l * sc.n_diag;
-        const float dist_up = f32_up(dist);
-        for (unsigned k = 0; k < cnt; ++k) {
-          unsigned idx;
-          if (k < 4u) { idx = (unsigned)(q & 0xFFFFu); q >>= 16; }
-          else if (k == 4u) idx = c.w2 >> 16;
-          else idx = sc.lb_ov[c.ov + k - (unsigned)kLbInline];
-          if (dl[idx] > dist_up) break;  // this box and all after it lie beyond the origin
-          leaf_sphere_test<true, false>(sd, 0, (int)idx, o, d, h, n_disc);
-          ++n_tests;
-          if (h.key >= 0 && h.t < dist) break;
-        }
-      } else {
-        for (int k = 0; k < sc.n_diag; ++k) {
-          leaf_sphere_test<true, false>(sd, 0, k, o, d, h, n_disc);
-          ++n_tests;
-          if (h.key >= 0 && h.t < dist) break;
-        }
-      }
-    }
-    hit_finish(h);
-    shadow_result(sc, a, slot, h.key >= 0 && h.t < dist, o, d);
-  }
-  const unsigned long long sdc = wave_sum(n_disc), st = wave_sum(n_tests);
-  if (lane_id() == 0) {
-    if (sdc) atomicAdd(&work_row(a.cnt)->disc[a.disc_slot], sdc);
-    if (st) atomicAdd(&work_row(a.cnt)->tests[a.disc_slot], st);
-  }
-}
-
 __global__ __launch_bounds__(kWfBlock) void wf_prep(DevScene sc, DevCamera cam, WfArgs a) {
   __shared__ unsigned s_pre[kShards + 1];
   const unsigned* pre = shard_prefix(a.in_cnt, s_pre);
@@ -1703,6 +1277,32 @@ __global__ __launch_bounds__(kWfBlock) void wf_combine(DevScene sc, DevCamera ca
     }
     double* out = a.colors + oi * 3;
     out[0] = color.x; out[1] = color.y; out[2] = color.z;
+  }
+}
+
+// The fast path's combine (DESIGN.md "Fused generations"): shade_hit of every
+// node of generation g that has a reflected or refracted child, from its
+// ParentRec (surface term, Schlick factor) and the children's colours, which
+// generation g+1 wrote (directly or through this pass).
+__global__ __launch_bounds__(kWfBlock) void wf_combine_parents(DevScene sc, DevCamera cam, WfArgs a) {
+  const unsigned stride = gridDim.x * blockDim.x;
+  __shared__ unsigned s_pre[kShards + 1];
+  const unsigned* pre = shard_prefix(a.sh_cnt, s_pre);
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
+    const ParentRec p = a.parents[shard_slot(pre, a.sh_cap, i)];
+    const ShadeRec& m = sc.shade[p.obj];
+    V3 refl = v3(0.0, 0.0, 0.0), refr = v3(0.0, 0.0, 0.0);
+    if (p.child_refl >= 0) {
+      const double* cc = a.child_colors + (size_t)p.child_refl * 3;
+      refl = vscale(v3(cc[0], cc[1], cc[2]), m.reflective);  // world.rs:113
+    }
+    if (p.child_refr >= 0) {
+      const double* cc = a.child_colors + (size_t)p.child_refr * 3;
+      refr = vscale(v3(cc[0], cc[1], cc[2]), m.transparency);  // world.rs:133
+    }
+    const V3 col = shade_color(m, v3(p.surface[0], p.surface[1], p.surface[2]), refl, refr, p.schlick);
+    double* out = color_dst(a, cam, p.slot);
+    out[0] = col.x; out[1] = col.y; out[2] = col.z;
   }
 }
 
@@ -1781,7 +1381,7 @@ static thread_local int t_ev_used = 0;
 Wavefront::~Wavefront() {
   for (auto& g : gens_) {
     (void)hipFree(g.rays); (void)hipFree(g.hits); (void)hipFree(g.nodes); (void)hipFree(g.colors);
-    (void)hipFree(g.shadow_nodes); (void)hipFree(g.geo); (void)hipFree(g.surf);
+    (void)hipFree(g.shadow_nodes); (void)hipFree(g.geo); (void)hipFree(g.surf); (void)hipFree(g.parents);
   }
   if (d_cnt_) (void)hipFree(d_cnt_);
   if (d_shard_) (void)hipFree(d_shard_);
@@ -1837,46 +1437,46 @@ hipError_t Wavefront::last_profile(WfProfile* out) {
     out->tests[c] = (double)hc.tests(c);
     out->boxes[c] = (double)hc.boxes(c);
   }
+  for (int c = 0; c < 2; ++c) {
+    out->sh_rays[c] = (double)hc.sh_rays(c);
+    out->sh_tests[c] = (double)hc.sh_tests(c);
+  }
+  if (last_fused_) out->rays[WF_SHADOW] = out->sh_rays[0] + out->sh_rays[1];  // traced inside the fused launches
   out->bvh = last_bvh_ ? 1 : 0;
+  out->fused = last_fused_ ? 1 : 0;
   return hipSuccess;
 }
 
-// Grow-only per-generation buffers. The shadow queue and the shadow flags are
-// sized rays * n_lights (at most one shadow ray per light per hit).
-hipError_t Wavefront::ensure_gen(size_t g, size_t slots, size_t n_lights, size_t list_slots) {
+// Grow-only per-generation buffers (12.5 % headroom on each reallocation).
+// The fast path needs the rays, the colours and the parents list; the
+// exhaustive pipeline the hits, nodes, hit geometry, lighting terms
+// (slots x n_lights) and the shadow list.
+template <typename T>
+static hipError_t grow(T*& p, size_t& cap, size_t need) {
+  need = std::max<size_t>(need, 1);
+  if (cap >= need) return hipSuccess;
+  (void)hipFree(p);
+  p = nullptr;
+  cap = 0;
+  const size_t n = need + need / 8;
+  WF_CHECK(hipMalloc(&p, n * sizeof(T)));
+  cap = n;
+  return hipSuccess;
+}
+hipError_t Wavefront::ensure_gen(size_t g, size_t slots, size_t n_lights, size_t list_slots, bool fused) {
   if (gens_.size() <= g) gens_.resize(g + 1);
   WfGenBuf& b = gens_[g];
-  slots = std::max<size_t>(slots, 1);
-  if (b.cap_rays < slots) {
-    (void)hipFree(b.rays); (void)hipFree(b.hits); (void)hipFree(b.nodes); (void)hipFree(b.colors);
-    (void)hipFree(b.geo);
-    b.rays = nullptr; b.hits = nullptr; b.nodes = nullptr; b.colors = nullptr; b.geo = nullptr;
-    b.cap_rays = 0;
-    const size_t cap = slots + slots / 8;
-    WF_CHECK(hipMalloc(&b.rays, cap * sizeof(WfRay)));
-    WF_CHECK(hipMalloc(&b.hits, cap * sizeof(WfHit)));
-    WF_CHECK(hipMalloc(&b.nodes, cap * sizeof(WfNode)));
-    WF_CHECK(hipMalloc(&b.colors, cap * 3 * sizeof(double)));
-    WF_CHECK(hipMalloc(&b.geo, cap * sizeof(WfGeo)));
-    b.cap_rays = cap;
+  WF_CHECK(grow(b.rays, b.cap_rays, slots));
+  WF_CHECK(grow(b.colors, b.cap_colors, slots * 3));
+  if (fused) {
+    WF_CHECK(grow(b.parents, b.cap_parents, list_slots));
+    return hipSuccess;
   }
-  const size_t need_sh = std::max<size_t>(b.cap_rays * n_lights, 1);
-  if (b.cap_shadows < need_sh) {
-    (void)hipFree(b.surf);
-    b.surf = nullptr;
-    b.cap_shadows = 0;
-    WF_CHECK(hipMalloc(&b.surf, need_sh * 3 * sizeof(double)));
-    b.cap_shadows = need_sh;
-  }
-  list_slots = std::max<size_t>(list_slots, 1);
-  if (b.cap_list < list_slots) {
-    (void)hipFree(b.shadow_nodes);
-    b.shadow_nodes = nullptr;
-    b.cap_list = 0;
-    const size_t cap = list_slots + list_slots / 8;
-    WF_CHECK(hipMalloc(&b.shadow_nodes, cap * sizeof(int32_t)));
-    b.cap_list = cap;
-  }
+  WF_CHECK(grow(b.hits, b.cap_hits, slots));
+  WF_CHECK(grow(b.nodes, b.cap_nodes, slots));
+  WF_CHECK(grow(b.geo, b.cap_geo, slots));
+  WF_CHECK(grow(b.surf, b.cap_surf, slots * std::max<size_t>(n_lights, 1) * 3));
+  WF_CHECK(grow(b.shadow_nodes, b.cap_list, list_slots));
   return hipSuccess;
 }
 
@@ -1941,7 +1541,8 @@ static constexpr size_t kWfLdsLimit = 160 * 1024 - 1024;
 // with the kTraceBlock stride and loop over gridDim x blockDim, so any block
 // size up to kTraceBlock gives the same results.
 int g_wf_adaptive_block = 0;  // tuning knob ("adaptive_block"); frames in flight fill idle CUs better
-int g_wf_shadow_stream = 1;   // tuning knob ("shadow_stream"): 0 off, 1 when the frame renders alone, 2 always
+int g_wf_shadow_stream = 1;   // tuning knob ("shadow_stream", exhaustive pipeline): 0 off, 1 when the frame
+                              // renders alone, 2 always
 static int trace_block(unsigned n) {
   if (!g_wf_adaptive_block) return kTraceBlock;
   static int n_cu = 0;
@@ -1953,10 +1554,6 @@ static int trace_block(unsigned n) {
   }
   const unsigned per = ((n + (unsigned)n_cu - 1) / (unsigned)n_cu + 63u) & ~63u;
   return (int)std::min<unsigned>(std::max<unsigned>(per, 64u), (unsigned)kTraceBlock);
-}
-// the four-wide traversal runs when its 16-bit codes are valid and the block's LDS image fits
-static bool lane4_ok(const DevScene& sc) {
-  return sc.n_bvh4 > 0 && sc.bvh4_code16 && lane4_lds_bytes(sc) <= kWfLdsLimit;
 }
 
 // Per-launch profiling: see t_ev_start.
@@ -1970,168 +1567,73 @@ static bool lane4_ok(const DevScene& sc) {
     }                                                                                                  \
   } while (0)
 
-template <bool QUADS, int TW>
-static hipError_t launch_closest_q(const DevScene& sc, const DevCamera& cam, const WfArgs& a, bool primary,
-                                   bool lds_ok, bool bvh, unsigned n, hipStream_t stream) {
-  const int tb = trace_block(n);
-  if (bvh) {
-    if (primary && g_wf_prim_lane && sc.bvh_depth + 1 <= kLaneLdsDepth &&
-        lane_lds_bytes(sc) + lane_stack_bytes(1) <= kWfLdsLimit) {
-      const size_t lds = lane_lds_bytes(sc) + lane_stack_bytes(1);
-      auto k = wf_trace_closest_bvh<true, QUADS, 14, TW>;
-      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, n)), dim3(tb), lds, stream, sc, cam, a);
-    } else if (primary) {
-      auto k = wf_trace_closest_bvh<true, QUADS, 0, TW>;
-      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, n)), dim3(tb), 0, stream, sc, cam, a);
-    } else if (g_wf_lane == 14 && sc.bvh_depth <= kLaneLdsDepth &&
-               lane_lds_bytes(sc) + lane_stack_bytes(1) <= kWfLdsLimit) {
-      const size_t lds = lane_lds_bytes(sc) + lane_stack_bytes(1);
-      auto k = wf_trace_closest_bvh<false, QUADS, 14, TW>;
-      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, n)), dim3(tb), lds, stream, sc, cam, a);
-    } else if (g_wf_lane == 12 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc) <= kWfLdsLimit) {
-      const size_t lds = lane_lds_bytes(sc);
-      auto k = wf_trace_closest_refill<QUADS, TW>;
-      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, n)), dim3(tb), lds, stream, sc, cam, a);
-    } else if ((g_wf_lane == 10 || g_wf_lane == 11) && sc.bvh_code16 && sc.bvh_depth <= kLaneLdsDepth &&
-               lane16_lds_bytes(sc, g_wf_lane == 11) <= kWfLdsLimit) {
-      const size_t lds = lane16_lds_bytes(sc, g_wf_lane == 11);
-      auto k = g_wf_lane == 11 ? wf_trace_closest_bvh<false, QUADS, 11, TW> : wf_trace_closest_bvh<false, QUADS, 10, TW>;
-      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, n)), dim3(tb), lds, stream, sc, cam, a);
-    } else if (g_wf_lane == 8 && lane4_ok(sc)) {
-      const size_t lds = lane4_lds_bytes(sc);
-      auto k = wf_trace_closest_bvh<false, QUADS, 8, TW>;
-      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, n)), dim3(tb), lds, stream, sc, cam, a);
-    } else if (g_wf_lane == 6 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc, false) <= kWfLdsLimit) {
-      const size_t lds = lane_lds_bytes(sc, false);
-      auto k = wf_trace_closest_bvh<false, QUADS, 6, TW>;
-      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, n)), dim3(tb), lds, stream, sc, cam, a);
-    } else if ((g_wf_lane == 7 || g_wf_lane == 9 || g_wf_lane == 14) && sc.bvh_depth <= kLaneLdsDepth &&
-               lane_lds_bytes(sc) <= kWfLdsLimit) {
-      const size_t lds = lane_lds_bytes(sc);
-      auto k = g_wf_lane == 9 ? wf_trace_closest_bvh<false, QUADS, 9, TW> : wf_trace_closest_bvh<false, QUADS, 7, TW>;
-      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, n)), dim3(tb), lds, stream, sc, cam, a);
-    } else if (g_wf_lane >= 5 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc) <= kWfLdsLimit) {
-      const size_t lds = lane_lds_bytes(sc);
-      auto k = wf_trace_closest_bvh<false, QUADS, 5, TW>;
-      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, n)), dim3(tb), lds, stream, sc, cam, a);
-    } else if ((g_wf_lane == 7 || g_wf_lane == 9 || g_wf_lane == 14) && sc.bvh_depth <= kLaneLdsDepth) {
-      auto k = wf_trace_closest_bvh<false, QUADS, 3, TW>;
-      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, n)), dim3(tb), 0, stream, sc, cam, a);
-    } else if (g_wf_lane && g_wf_lane != 2 && sc.bvh_depth <= kLaneLdsDepth) {
-      auto k = wf_trace_closest_bvh<false, QUADS, 2, TW>;
-      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, n)), dim3(tb), 0, stream, sc, cam, a);
-    } else if (g_wf_lane) {
-      auto k = wf_trace_closest_bvh<false, QUADS, 1, TW>;
-      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, n)), dim3(tb), 0, stream, sc, cam, a);
-    } else {
-      auto k = wf_trace_closest_bvh<false, QUADS, 0, TW>;
-      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, n)), dim3(tb), 0, stream, sc, cam, a);
-    }
-  } else if (primary) {
-    const size_t lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, true);
-    auto k = wf_trace_closest<true, true, QUADS, TW>;
-    WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, n)), dim3(tb), lds, stream, sc, cam, a);
-  } else if (lds_ok) {
-    const size_t lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, false);
-    auto k = wf_trace_closest<true, false, QUADS, TW>;
-    WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, n)), dim3(tb), lds, stream, sc, cam, a);
-  } else {
-    auto k = wf_trace_closest<false, false, QUADS, TW>;
-    WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, n)), dim3(tb), 0, stream, sc, cam, a);
-  }
+template <typename K>
+static hipError_t launch_lds(K kern, size_t lds, unsigned n, hipStream_t stream, const DevScene& sc,
+                             const DevCamera& cam, const WfArgs& a, int block) {
+  if (lds > 0) WF_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  WF_LAUNCH(kern, dim3(occupancy_grid(kern, block, lds, n)), dim3(block), lds, stream, sc, cam, a);
   return hipGetLastError();
 }
-template <int TW>
-static hipError_t launch_closest(const DevScene& sc, const DevCamera& cam, const WfArgs& a, bool primary, bool lds_ok,
-                                 bool bvh, unsigned n, hipStream_t stream) {
-  return sc.n_quads > 0 ? launch_closest_q<true, TW>(sc, cam, a, primary, lds_ok, bvh, n, stream)
-                        : launch_closest_q<false, TW>(sc, cam, a, primary, lds_ok, bvh, n, stream);
-}
 
-template <bool QUADS, int TW>
-static hipError_t launch_shadow_q(const DevScene& sc, const WfArgs& a, bool lds_ok, bool bvh, hipStream_t stream) {
+// ---- the exhaustive pipeline (counted launches: the reference's every-shape loop)
+template <bool QUADS>
+static hipError_t launch_closest_exh(const DevScene& sc, const DevCamera& cam, const WfArgs& a, bool primary,
+                                     bool lds_ok, unsigned n, hipStream_t stream) {
+  const int tb = trace_block(n);
+  if (primary)
+    return launch_lds(wf_trace_closest<true, true, QUADS, 8>, wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, true),
+                      n, stream, sc, cam, a, tb);
+  if (lds_ok)
+    return launch_lds(wf_trace_closest<true, false, QUADS, 8>, wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, false),
+                      n, stream, sc, cam, a, tb);
+  return launch_lds(wf_trace_closest<false, false, QUADS, 8>, 0, n, stream, sc, cam, a, tb);
+}
+template <bool QUADS>
+static hipError_t launch_shadow_exh(const DevScene& sc, const WfArgs& a, bool lds_ok, hipStream_t stream) {
   const int tb = trace_block(a.n_shadow);
-  if (bvh && g_wf_shadow_lb && sc.lb_cells) {
-    const size_t lds = lb_lds_bytes(sc);
-    const size_t lds_d = lb_lds_bytes(sc) - (size_t)sc.n_diag * sizeof(SphereDiag);  // the distances alone
-    if (lds <= kWfLdsLimit) {
-      auto k = wf_trace_shadow_lb<QUADS, 1, kLbWaves>;
-      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, a.n_shadow)), dim3(tb), lds, stream, sc, a);
-    } else if (lds_d <= kWfLdsLimit) {
-      auto k = wf_trace_shadow_lb<QUADS, 2, kLbWaves>;
-      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_d));
-      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds_d, a.n_shadow)), dim3(tb), lds_d, stream, sc, a);
-    } else {
-      auto k = wf_trace_shadow_lb<QUADS, 0, kLbWaves>;
-      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, a.n_shadow)), dim3(tb), 0, stream, sc, a);
-    }
-  } else if (bvh) {
-    if (g_wf_refill && (g_wf_lane == 7 || g_wf_lane == 9 || g_wf_lane == 14) && sc.bvh_depth <= kLaneLdsDepth &&
-        lane_lds_bytes(sc) <= kWfLdsLimit) {
-      const size_t lds = lane_lds_bytes(sc);
-      auto k = g_wf_lane == 9 ? wf_trace_shadow_refill<QUADS, 9, TW> : wf_trace_shadow_refill<QUADS, 7, TW>;
-      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, a.n_shadow)), dim3(tb), lds, stream, sc, a);
-    } else if (g_wf_lane == 8 && lane4_ok(sc)) {
-      const size_t lds = lane4_lds_bytes(sc);
-      auto k = wf_trace_shadow_bvh<QUADS, 8, TW>;
-      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, a.n_shadow)), dim3(tb), lds, stream, sc, a);
-    } else if (g_wf_lane == 6 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc, false) <= kWfLdsLimit) {
-      const size_t lds = lane_lds_bytes(sc, false);
-      auto k = wf_trace_shadow_bvh<QUADS, 6, TW>;
-      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, a.n_shadow)), dim3(tb), lds, stream, sc, a);
-    } else if ((g_wf_lane == 7 || g_wf_lane == 9 || g_wf_lane == 14) && sc.bvh_depth <= kLaneLdsDepth &&
-               lane_lds_bytes(sc) <= kWfLdsLimit) {
-      const size_t lds = lane_lds_bytes(sc);
-      auto k = g_wf_lane == 9 ? wf_trace_shadow_bvh<QUADS, 9, TW> : wf_trace_shadow_bvh<QUADS, 7, TW>;
-      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, a.n_shadow)), dim3(tb), lds, stream, sc, a);
-    } else if (g_wf_lane >= 5 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc) <= kWfLdsLimit) {
-      const size_t lds = lane_lds_bytes(sc);
-      auto k = wf_trace_shadow_bvh<QUADS, 5, TW>;
-      WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, a.n_shadow)), dim3(tb), lds, stream, sc, a);
-    } else if ((g_wf_lane == 7 || g_wf_lane == 9 || g_wf_lane == 14) && sc.bvh_depth <= kLaneLdsDepth) {
-      auto k = wf_trace_shadow_bvh<QUADS, 3, TW>;
-      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, a.n_shadow)), dim3(tb), 0, stream, sc, a);
-    } else if (g_wf_lane && g_wf_lane != 2 && sc.bvh_depth <= kLaneLdsDepth) {
-      auto k = wf_trace_shadow_bvh<QUADS, 2, TW>;
-      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, a.n_shadow)), dim3(tb), 0, stream, sc, a);
-    } else if (g_wf_lane) {
-      auto k = wf_trace_shadow_bvh<QUADS, 1, TW>;
-      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, a.n_shadow)), dim3(tb), 0, stream, sc, a);
-    } else {
-      auto k = wf_trace_shadow_bvh<QUADS, 0, TW>;
-      WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, a.n_shadow)), dim3(tb), 0, stream, sc, a);
-    }
-  } else if (lds_ok) {
+  if (lds_ok) {
     const size_t lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, false);
-    auto k = wf_trace_shadow<true, QUADS, TW>;
+    auto k = wf_trace_shadow<true, QUADS, 8>;
     WF_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     WF_LAUNCH(k, dim3(occupancy_grid(k, tb, lds, a.n_shadow)), dim3(tb), lds, stream, sc, a);
   } else {
-    auto k = wf_trace_shadow<false, QUADS, TW>;
+    auto k = wf_trace_shadow<false, QUADS, 8>;
     WF_LAUNCH(k, dim3(occupancy_grid(k, tb, 0, a.n_shadow)), dim3(tb), 0, stream, sc, a);
   }
   return hipGetLastError();
 }
-template <int TW>
-static hipError_t launch_shadow_wf(const DevScene& sc, const WfArgs& a, bool lds_ok, bool bvh, hipStream_t stream) {
-  return sc.n_quads > 0 ? launch_shadow_q<true, TW>(sc, a, lds_ok, bvh, stream)
-                        : launch_shadow_q<false, TW>(sc, a, lds_ok, bvh, stream);
+
+// ---- the fast path: one fused launch per generation (image choice: see lane_scene)
+template <bool QUADS>
+static hipError_t launch_fused_q(const DevScene& sc, const DevCamera& cam, WfArgs a, bool primary, unsigned n,
+                                 hipStream_t stream) {
+  const int tb = trace_block(n);
+  const size_t dl = a.use_lb ? delta_lds_bytes(sc) : 0;
+  size_t dyn = 0;
+  a.lds_flags = 0;
+  if (primary) {
+    const size_t room = kWfLdsLimit - (size_t)(kTraceBlock / 64) * (kBvhMaxDepth + 4) * 4;
+    if (sph_lds_bytes(sc) <= room) { a.lds_flags |= kLdsSpheres; dyn += sph_lds_bytes(sc); }
+    if (dl && dyn + dl <= room) { a.lds_flags |= kLdsDeltas; dyn += dl; }
+    return launch_lds(wf_trace_fused<true, QUADS, 0>, dyn, n, stream, sc, cam, a, tb);
+  }
+  if (g_wf_image == 0 && pair_lds_bytes(sc) <= kWfLdsLimit) {
+    dyn = pair_lds_bytes(sc);
+    if (dl && dyn + dl <= kWfLdsLimit) { a.lds_flags |= kLdsDeltas; dyn += dl; }
+    return launch_lds(wf_trace_fused<false, QUADS, 14>, dyn, n, stream, sc, cam, a, tb);
+  }
+  if (g_wf_image != 1 && sc.bvh_depth <= kLaneLdsDepth) {
+    const size_t room = kWfLdsLimit - (size_t)kLaneLdsDepth * kTraceBlock * 4;
+    if (dl && dl <= room) { a.lds_flags |= kLdsDeltas; dyn = dl; }
+    return launch_lds(wf_trace_fused<false, QUADS, 3>, dyn, n, stream, sc, cam, a, tb);
+  }
+  if (dl && dl <= kWfLdsLimit) { a.lds_flags |= kLdsDeltas; dyn = dl; }
+  return launch_lds(wf_trace_fused<false, QUADS, 1>, dyn, n, stream, sc, cam, a, tb);
+}
+static hipError_t launch_fused(const DevScene& sc, const DevCamera& cam, const WfArgs& a, bool primary, unsigned n,
+                               hipStream_t stream) {
+  return sc.n_quads > 0 ? launch_fused_q<true>(sc, cam, a, primary, n, stream)
+                        : launch_fused_q<false>(sc, cam, a, primary, n, stream);
 }
 
 int Wavefront::g_corrupt_calibration = 0;
@@ -2147,14 +1649,16 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
   const bool averaged = aa > 1;
   WF_CHECK(ensure_misc((size_t)sc.n_diag));
   const unsigned L = (unsigned)sc.n_lights;
-  // BVH traversal and skipped shadow rays unless the reference's every-shape loop is asked
-  // for; counting (stats) never changes the algorithm
+  // BVH traversal (fused generations) and skipped shadow rays unless the
+  // reference's every-shape loop is asked for; counting (stats) never changes the algorithm
   const bool exhaustive = (flags & WF_EXHAUSTIVE) != 0;
   const bool count = stats != nullptr || (flags & WF_COUNT) != 0;
   const bool bvh = g_wf_accel != 0 && !exhaustive && sc.n_bvh > 0;
+  const bool fused = bvh;
   const bool skip_shadow = !exhaustive && g_wf_skip_shadow != 0;
-  // the shadow-ray counts differ between the two modes
-  const std::string key = signature.empty() ? signature : signature + (skip_shadow ? 'S' : 'A');
+  // the shadow-ray counts differ between the two modes; the fused pipeline's
+  // second queue per generation holds its parents instead of shadow rays
+  const std::string key = signature.empty() ? signature : signature + (skip_shadow ? 'S' : 'A') + (fused ? 'F' : 'E');
   auto it = key.empty() ? cache_.end() : cache_.find(key);
   const bool calibrated = it != cache_.end();
   Counts counts;
@@ -2167,7 +1671,7 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
   WF_CHECK(hipMemsetAsync(d_cnt_, 0, sizeof(WfCounters), stream));
   WF_CHECK(hipMemsetAsync(d_shard_, 0, (size_t)(max_depth + 2) * 2 * kShards * kShardStride * sizeof(unsigned),
                           stream));
-  WF_CHECK(ensure_gen(0, n0, L, 0));
+  WF_CHECK(ensure_gen(0, n0, L, 0, fused));
   if (!camera_mode) {
     // batch rays: n0 x 6 doubles -> WfRay queue of generation 0
     WF_CHECK(hipMemcpy2DAsync(gens_[0].rays, sizeof(WfRay), d_in_rays, 6 * sizeof(double), 6 * sizeof(double), n0,
@@ -2176,18 +1680,17 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
   const bool prim_lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, true) <= kWfLdsLimit;
   const bool gen_lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, false) <= kWfLdsLimit;
   last_bvh_ = bvh;
+  last_fused_ = fused;
   const bool use_prim = camera_mode && (prim_lds || bvh) && sc.n_diag > 0;
-  // the closest-hit refill kernel (LANE 12) leaves prepare_computations to wf_prep
-  const bool split_prep = bvh && g_wf_lane == 12 && sc.bvh_depth <= kLaneLdsDepth && lane_lds_bytes(sc) <= kWfLdsLimit;
   if (use_prim) {
     WF_LAUNCH(wf_prim_prep, dim3((sc.n_diag + 4 + 255) / 256), dim3(256), 0, stream, sc, cam, d_prim_);
     WF_CHECK(hipGetLastError());
   }
-  // Shadow traces of generation g depend only on closest(g), like closest(g+1):
-  // they run on the side stream, forked after closest(g) and joined before the
-  // combine pass (DESIGN.md "Shadow stream").
+  // Exhaustive pipeline: shadow traces of generation g depend only on
+  // closest(g), like closest(g+1); they run on the side stream, forked after
+  // closest(g) and joined before the combine pass (DESIGN.md "Shadow stream").
   hipStream_t sh_stream = stream;
-  if (g_wf_shadow_stream == 2 || (g_wf_shadow_stream == 1 && solo)) {
+  if (!fused && (g_wf_shadow_stream == 2 || (g_wf_shadow_stream == 1 && solo))) {
     WF_CHECK(ensure_side());
     sh_stream = side_;
   }
@@ -2196,24 +1699,27 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
   if (profiling_) ++pframes_;
   prof_rays_[0] = prof_rays_[1] = prof_rays_[2] = 0;
   unsigned last = 0;
-  // per-region capacity of each generation's sharded arrays (generation 0 is dense)
-  std::vector<unsigned> caps(max_depth + 2, 0);
+  // per-region capacity of each generation's sharded arrays (generation 0 is
+  // dense) and of its second queue (shadow list, or the fused path's parents)
+  std::vector<unsigned> caps(max_depth + 2, 0), list_caps(max_depth + 2, 0);
   for (unsigned g = 0; g <= max_depth; ++g) {
     const unsigned n = counts.rays[g];
     if (n == 0) break;
     last = g;
     // wave-iteration q of this generation appends to region (q / kShardGroup) mod kShards: a
-    // region receives at most `per` wave-iterations, each spawning <= 128 rays and <= 64 L shadow rays
+    // region receives at most `per` wave-iterations, each spawning <= 128 rays and <= 64 L shadow
+    // rays (<= 64 parents)
     const unsigned groups = ((n + 63) / 64 + kShardGroup - 1) / kShardGroup;
     const unsigned per = kShardGroup * ((groups + kShards - 1) / kShards);
-    const unsigned out_cap = g < max_depth ? 128u * per : 0u, sh_cap = 64u * L * per;
+    const unsigned out_cap = g < max_depth ? 128u * per : 0u, sh_cap = (fused ? 64u : 64u * L) * per;
     caps[g + 1] = out_cap;
-    WF_CHECK(ensure_gen(g, g == 0 ? n : (size_t)kShards * caps[g], L, (size_t)kShards * sh_cap));
-    WF_CHECK(ensure_gen(g + 1, (size_t)kShards * out_cap, L, 0));
+    list_caps[g] = sh_cap;
+    WF_CHECK(ensure_gen(g, g == 0 ? n : (size_t)kShards * caps[g], L, (size_t)kShards * sh_cap, fused));
+    WF_CHECK(ensure_gen(g + 1, (size_t)kShards * out_cap, L, 0, fused));
     WfArgs a{};
     WfGenBuf& B = gens_[g];
     a.rays = B.rays; a.hits = B.hits; a.nodes = B.nodes; a.shadow_nodes = B.shadow_nodes;
-    a.geo = B.geo; a.surf = B.surf;
+    a.geo = B.geo; a.surf = B.surf; a.parents = B.parents;
     a.colors = (g == 0 && !averaged) ? d_out : B.colors;
     a.aa = aa;
     a.rows = n0 / aa / (cam.hsize ? cam.hsize : 1);
@@ -2232,25 +1738,24 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     a.camera_mode = camera_mode ? 1u : 0u;
     a.row_block = row_block; a.shard = shard; a.n_shards = n_shards;
     a.skip_shadow = skip_shadow ? 1u : 0u;
-    a.refill_min = (unsigned)g_wf_refill_min;
-    // 1. closest hit
+    a.count = count ? 1u : 0u;
+    a.use_lb = (g_wf_shadow_lb && sc.lb_cells) ? 1u : 0u;
+    // 1. closest hit (fused: with the shading, the shadow rays and the spawn)
     const bool prim_launch = g == 0 && use_prim;
     const int ccls = prim_launch ? WF_PRIMARY : WF_CLOSEST;
     a.disc_slot = (unsigned)ccls;
     prof_rays_[ccls] += n;
     WF_CHECK(pmark(stream, ccls, true));
-    {
-      const int tw = !bvh ? g_wf_trace_waves : prim_launch ? g_tw_primary : g_tw_closest;
-      switch (tw) {
-        case 4: WF_CHECK(launch_closest<4>(sc, cam, a, prim_launch, gen_lds, bvh, n, stream)); break;
-        case 5: WF_CHECK(launch_closest<5>(sc, cam, a, prim_launch, gen_lds, bvh, n, stream)); break;
-        case 6: WF_CHECK(launch_closest<6>(sc, cam, a, prim_launch, gen_lds, bvh, n, stream)); break;
-        default: WF_CHECK(launch_closest<8>(sc, cam, a, prim_launch, gen_lds, bvh, n, stream)); break;
-      }
+    if (fused) {
+      WF_CHECK(launch_fused(sc, cam, a, prim_launch, n, stream));
+    } else if (sc.n_quads > 0) {
+      WF_CHECK(launch_closest_exh<true>(sc, cam, a, prim_launch, gen_lds, n, stream));
+    } else {
+      WF_CHECK(launch_closest_exh<false>(sc, cam, a, prim_launch, gen_lds, n, stream));
     }
     WF_CHECK(pmark(stream, ccls, false));
-    // 2. prepare_computations + spawn (the BVH trace kernels do it themselves, except the refill one)
-    if (!bvh || (split_prep && !prim_launch)) {
+    // 2. prepare_computations + spawn (exhaustive pipeline)
+    if (!fused) {
       WF_CHECK(pmark(stream, WF_PREP, true));
       WF_LAUNCH(wf_prep, dim3(occupancy_grid(wf_prep, kWfBlock, 0, n)), dim3(kWfBlock), 0, stream, sc, cam, a);
       WF_CHECK(hipGetLastError());
@@ -2270,8 +1775,9 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
       counts.rays[g + 1] = g < max_depth ? nr : 0;
       counts.shadows[g] = ns;
     }
+    if (fused) continue;
     a.n_shadow = counts.shadows[g];
-    // 3. shadow rays
+    // 3. shadow rays (exhaustive pipeline)
     if (a.n_shadow) {
       a.disc_slot = WF_SHADOW;
       prof_rays_[WF_SHADOW] += a.n_shadow;
@@ -2281,12 +1787,8 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
         forked = true;
       }
       WF_CHECK(pmark(sh_stream, WF_SHADOW, true));
-      switch (!bvh ? g_wf_trace_waves : g_tw_shadow) {
-        case 4: WF_CHECK(launch_shadow_wf<4>(sc, a, gen_lds, bvh, sh_stream)); break;
-        case 5: WF_CHECK(launch_shadow_wf<5>(sc, a, gen_lds, bvh, sh_stream)); break;
-        case 6: WF_CHECK(launch_shadow_wf<6>(sc, a, gen_lds, bvh, sh_stream)); break;
-        default: WF_CHECK(launch_shadow_wf<8>(sc, a, gen_lds, bvh, sh_stream)); break;
-      }
+      if (sc.n_quads > 0) WF_CHECK(launch_shadow_exh<true>(sc, a, gen_lds, sh_stream));
+      else WF_CHECK(launch_shadow_exh<false>(sc, a, gen_lds, sh_stream));
       WF_CHECK(pmark(sh_stream, WF_SHADOW, false));
     }
     if (count) {
@@ -2308,24 +1810,32 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     WF_CHECK(hipEventRecord(join_ev_, sh_stream));
     WF_CHECK(hipStreamWaitEvent(stream, join_ev_, 0));
   }
-  // 4. combine, deepest generation first
+  // 4. combine, deepest generation first (fused: only the nodes with children)
   for (int g = (int)last; g >= 0; --g) {
     WfArgs a{};
     WfGenBuf& B = gens_[g];
-    a.rays = B.rays; a.nodes = B.nodes; a.surf = B.surf;
+    a.rays = B.rays; a.nodes = B.nodes; a.surf = B.surf; a.parents = B.parents;
     a.colors = (g == 0 && !averaged) ? d_out : B.colors;
     a.aa = aa;
     a.rows = n0 / aa / (cam.hsize ? cam.hsize : 1);
     a.child_colors = gens_[g + 1].colors;
-    a.n = counts.rays[g];
+    a.n = fused ? counts.shadows[g] : counts.rays[g];
     a.in_cnt = g == 0 ? nullptr : shard_cnt((unsigned)g, 0);
     a.in_cap = caps[g];
+    a.sh_cnt = shard_cnt((unsigned)g, 1);
+    a.sh_cap = list_caps[g];
     a.g = (unsigned)g; a.max_depth = max_depth;
     a.camera_mode = camera_mode ? 1u : 0u;
     a.row_block = row_block; a.shard = shard; a.n_shards = n_shards;
+    if (a.n == 0) continue;
     WF_CHECK(pmark(stream, WF_COMBINE, true));
-    WF_LAUNCH(wf_combine, dim3(occupancy_grid(wf_combine, kWfBlock, 0, a.n)), dim3(kWfBlock), 0, stream, sc,
-                       cam, a);
+    if (fused) {
+      WF_LAUNCH(wf_combine_parents, dim3(occupancy_grid(wf_combine_parents, kWfBlock, 0, a.n)), dim3(kWfBlock), 0,
+                stream, sc, cam, a);
+    } else {
+      WF_LAUNCH(wf_combine, dim3(occupancy_grid(wf_combine, kWfBlock, 0, a.n)), dim3(kWfBlock), 0, stream, sc,
+                cam, a);
+    }
     WF_CHECK(hipGetLastError());
     WF_CHECK(pmark(stream, WF_COMBINE, false));
   }
@@ -2347,7 +1857,7 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
   }
   lr_.counts = counts;
   lr_.last = last; lr_.L = L; lr_.n0 = n0;
-  lr_.counted = count; lr_.exact_disc = !bvh && !skip_shadow; lr_.bvh = bvh;
+  lr_.counted = count; lr_.exact_disc = !bvh && !skip_shadow; lr_.bvh = bvh; lr_.fused = fused;
   lr_.n_diag = (unsigned long long)sc.n_diag; lr_.n_gen = (unsigned long long)sc.n_gen;
   lr_.n_planes = (unsigned long long)sc.n_planes; lr_.n_quads = (unsigned long long)sc.n_quads;
   lr_.stream = stream;
@@ -2365,11 +1875,12 @@ hipError_t Wavefront::read_stats(DevStats* out) {
   unsigned long long rays = 0, hits = 0, traced_shadows = 0;
   for (unsigned g = 0; g <= lr_.last && g < lr_.counts.rays.size(); ++g) {
     rays += lr_.counts.rays[g];
-    traced_shadows += lr_.counts.shadows[g];
+    if (!lr_.fused) traced_shadows += lr_.counts.shadows[g];
     hits += hc.n_hit[g];
     s.rays_reflect += hc.n_refl[g];
     s.rays_refract += hc.n_refr[g];
   }
+  if (lr_.fused) traced_shadows = hc.sh_rays(0) + hc.sh_rays(1);
   // the reference's work: every hit runs is_shadowed once per light (world.rs:41-56), and
   // World::intersect tests every shape for every ray (world.rs:31-38)
   const unsigned long long shadows = hits * (unsigned long long)lr_.L;

@@ -1,15 +1,27 @@
 // rt_wavefront.hpp — host side of the wavefront render pipeline.
 //
 // The recursion tree of `World::color_at` (world.rs:70-81) is evaluated one
-// GENERATION (recursion depth) at a time over flat ray queues:
+// GENERATION (recursion depth) at a time over flat ray queues.
 //
-//   for g = 0 .. max_depth:                       (radiance rays of depth g)
+// Fast path (BVH; DESIGN.md "Fused generations"), one launch per generation:
+//   for g = 0 .. max_depth:
+//     trace_fused(g)   World::intersect + hit, prepare_computations, the
+//                      reflected / refracted children -> rays_{g+1}, every
+//                      light's is_shadowed + lighting (world.rs:40-56), and
+//                      the final colour of each node without children
+//                      -> colors_g; nodes with children -> parents_g
+//   for g = max_depth .. 0:
+//     combine_parents(g)  shade_hit's sum with the children's colours
+//                         (world.rs:58-67)                     -> colors_g
+//
+// Exhaustive pipeline (the reference's every-shape loop; counted launches):
+//   for g = 0 .. max_depth:
 //     trace_closest(g)  World::intersect + hit          -> hits_g
 //     prep(g)           prepare_computations; spawn the shadow rays
 //                       (is_shadowed, world.rs:95-105) and the reflected /
 //                       refracted children (world.rs:107-134)   -> nodes_g,
 //                       shadow queue S_g, rays_{g+1}
-//     trace_shadow(g)   any-hit test of S_g                     -> flags_g
+//     trace_shadow(g)   any-hit test of S_g + lighting()        -> surf_g
 //   for g = max_depth .. 0:
 //     combine(g)        lighting over lights (left fold) + children colours,
 //                       Schlick or plain sum (world.rs:40-68)   -> colors_g
@@ -51,6 +63,16 @@ struct WfNode {  // 24 B: what shade_hit needs besides the lighting (which prep_
   int32_t child_refr;
   int32_t pad;
 };
+// A fast-path node with children (48 B): its surface term (the lighting sum
+// over the lights), Schlick factor, colour slot and children (wf_combine_parents).
+struct ParentRec {
+  double surface[3];
+  double schlick;      // Computations::schlick (only read when reflective && transparent)
+  uint32_t slot;       // the node's slot in generation g (its colour's place)
+  int32_t obj;
+  int32_t child_refl;  // index into rays_{g+1}, -1 = none (black)
+  int32_t child_refr;
+};
 struct PrimRec {  // primary rays share the origin: per diag sphere (s, o', c)
   double s[3];
   double op[3];
@@ -60,16 +82,11 @@ struct PrimRec {  // primary rays share the origin: per diag sphere (s, o', c)
 
 constexpr int kMaxGen = 66;
 enum WfFlags : unsigned { WF_EXHAUSTIVE = 1u, WF_COUNT = 2u };
-extern int g_wf_trace_waves;  // tuning knob: trace-kernel occupancy (4 or 8 waves/SIMD)
-extern int g_tw_primary, g_tw_closest, g_tw_shadow;  // tuning knobs: BVH trace-kernel occupancy
-extern int g_wf_lane;         // tuning knob: 1 = per-lane BVH traversal for secondary / shadow rays
-extern int g_wf_accel;        // tuning knob: 1 = BVH traversal (when no counters are requested), 0 = exhaustive
+extern int g_wf_accel;        // tuning knob: 1 = BVH traversal (when the exhaustive loop is not asked for)
 extern int g_wf_shadow_lb;    // tuning knob: 1 = shadow rays through the light buffer when the scene has one
-extern int g_wf_refill;       // tuning knob: 1 = lane refill in the per-lane trace kernels
-extern int g_wf_shadow_stream;   // tuning knob: 1 = shadow traces on a second stream, overlapping the next generation
+extern int g_wf_image;        // tuning knob: 0 = automatic scene image of the fused kernels, 3 / 1 = global memory
+extern int g_wf_shadow_stream;   // tuning knob: 1 = exhaustive shadow traces on a second stream
 extern int g_wf_adaptive_block;  // tuning knob: 1 = small trace launches spread over every CU (smaller blocks)
-extern int g_wf_refill_min;
-extern int g_wf_prim_lane;     // tuning knob: 1 = primary rays take the per-lane pair traversal   // tuning knob: idle lanes that trigger a refill (closest-hit refill kernel)
 extern int g_wf_skip_shadow;  // tuning knob: 1 = the fast path leaves out shadow rays that cannot change the colour
 
 // Work counters of the trace kernels, one row per wave slot (wave id mod
@@ -81,6 +98,8 @@ struct alignas(128) WfWorkRow {
   unsigned long long disc[3];   // disc >= 0 tests: [0] primary closest, [1] closest, [2] shadow
   unsigned long long tests[3];  // BVH mode: sphere tests executed (lanes x spheres), per trace class
   unsigned long long boxes[3];  // BVH mode: child-box tests executed (lanes x boxes)
+  unsigned long long sh_rays[2];   // fused kernels: shadow rays traced, [0] primary / [1] secondary launches
+  unsigned long long sh_tests[2];  // fused kernels: shadow sphere tests executed, per launch class
 };
 struct WfCounters {
   unsigned n_refl[kMaxGen], n_refr[kMaxGen], n_hit[kMaxGen];
@@ -100,6 +119,16 @@ struct WfCounters {
     for (int r = 0; r < kWorkRows; ++r) t += work[r].boxes[c];
     return t;
   }
+  unsigned long long sh_rays(int c) const {
+    unsigned long long t = 0;
+    for (int r = 0; r < kWorkRows; ++r) t += work[r].sh_rays[c];
+    return t;
+  }
+  unsigned long long sh_tests(int c) const {
+    unsigned long long t = 0;
+    for (int r = 0; r < kWorkRows; ++r) t += work[r].sh_tests[c];
+    return t;
+  }
 };
 
 struct WfGeo {  // 80 B: the lighting() inputs of a hit (comps.over_point, normalv, eyev)
@@ -107,15 +136,17 @@ struct WfGeo {  // 80 B: the lighting() inputs of a hit (comps.over_point, norma
   int32_t obj;
   int32_t pad;
 };
-struct WfGenBuf {
+struct WfGenBuf {  // grow-only; the fast path allocates rays, colors and parents only
   WfRay* rays = nullptr;
+  double* colors = nullptr;
+  ParentRec* parents = nullptr;     // fast path: nodes with children (sharded)
   WfHit* hits = nullptr;
   WfNode* nodes = nullptr;
-  double* colors = nullptr;
   int32_t* shadow_nodes = nullptr;  // shadow list of the generation (node slot * L + light, sharded)
   WfGeo* geo = nullptr;              // per node slot: what the shadow trace needs to evaluate lighting()
   double* surf = nullptr;            // lighting() per node slot and light (3 doubles)
-  size_t cap_rays = 0, cap_shadows = 0, cap_list = 0;
+  size_t cap_rays = 0, cap_colors = 0, cap_parents = 0, cap_hits = 0, cap_nodes = 0, cap_list = 0, cap_geo = 0,
+         cap_surf = 0;
 };
 
 // Kernel arguments for one generation.
@@ -128,6 +159,7 @@ struct WfArgs {
   WfGeo* geo;           // per node slot: over point, normal, eye vector, object
   double* surf;         // per node slot * L + light: lighting() (written by prep_one when the light needs
                         // no shadow ray, else by the shadow trace)
+  ParentRec* parents;   // fast path: this generation's nodes with children (sharded like the shadow list)
   WfRay* next_rays;     // rays_{g+1}
   const double* child_colors;  // colors_{g+1}
   WfCounters* cnt;
@@ -148,8 +180,10 @@ struct WfArgs {
   unsigned* out_cnt;
   unsigned out_cap;     // per-region capacity of the next generation's arrays
   unsigned* sh_cnt;
-  unsigned sh_cap;      // per-region capacity of the shadow list
-  unsigned refill_min;  // lane refill: idle lanes that trigger a refill (wf_trace_closest_refill)
+  unsigned sh_cap;      // per-region capacity of the shadow list (fast path: of the parents)
+  unsigned count;       // counted launch: tally shade_hit runs and children (fast path)
+  unsigned use_lb;      // fast path: shadow rays through the light buffer
+  unsigned lds_flags;   // fast path: what the trace kernel stages in LDS (kLdsSpheres | kLdsDeltas)
 };
 
 // Per-kernel-class timing of the last frame (profiling mode only).
@@ -160,7 +194,9 @@ struct WfProfile {
   double disc[3];   // disc >= 0 tests per trace class
   double tests[3];  // sphere tests executed per trace class (exhaustive: rays x n_diag)
   double boxes[3];  // BVH child-box tests executed per trace class (0 when exhaustive)
+  double sh_rays[2], sh_tests[2];  // fused frames: shadow rays / sphere tests inside the primary / secondary launches
   int bvh;          // the last frame traversed the BVH
+  int fused;        // the last frame ran the fused pipeline
 };
 
 class Wavefront {
@@ -205,7 +241,7 @@ class Wavefront {
   static int g_corrupt_calibration;
 
  private:
-  hipError_t ensure_gen(size_t g, size_t slots, size_t n_lights, size_t list_slots);
+  hipError_t ensure_gen(size_t g, size_t slots, size_t n_lights, size_t list_slots, bool fused);
   hipError_t ensure_misc(size_t n_diag);
   // shard counters: generation g's rays (q = 0) / shadow list (q = 1)
   unsigned* shard_cnt(unsigned g, unsigned q) { return d_shard_ + ((size_t)g * 2 + q) * kShards * kShardStride; }
@@ -231,11 +267,11 @@ class Wavefront {
   struct LastRender {       // what read_stats needs of the last render
     Counts counts;
     unsigned last = 0, L = 0, n0 = 0;
-    bool counted = false, exact_disc = false, bvh = false;
+    bool counted = false, exact_disc = false, bvh = false, fused = false;
     unsigned long long n_diag = 0, n_gen = 0, n_planes = 0, n_quads = 0;
     hipStream_t stream = nullptr;
   } lr_;
-  bool last_bvh_ = false;
+  bool last_bvh_ = false, last_fused_ = false;
   bool profiling_ = false;
   int pmask_ = (1 << WF_NCLASS) - 1;
   std::vector<hipEvent_t> pev_;        // event pool (pairs)

@@ -213,39 +213,24 @@ def test_skipped_shadow_rays_bitwise(rt, neg_zero):
     assert full.to_numpy().tobytes() == exact.to_numpy().tobytes()
 
 
-@pytest.mark.parametrize("lane,tw", [(0, 4), (1, 4), (2, 4), (5, 4), (6, 4), (7, 4), (8, 4), (9, 4), (10, 4), (10, 8), (11, 4), (12, 4), (14, 4)])
-def test_traversal_variants_bitwise(rt, lane, tw):
-    """Every traversal variant (wave / per-lane with LDS or scratch stack /
-    per-lane with the scene or the nodes staged in LDS / per-lane with leaves
-    batched across the wave, the default / 16-bit child codes with the stack
-    top in a register, at 4 and 8 waves per SIMD / closest-hit lane refill with
-    the spawn in wf_prep) gives the exhaustive frame. The
-    scenes above that do not fit in LDS (3000 spheres) run the batched-leaf
-    variant with the scene in global memory."""
+@pytest.mark.parametrize("image,shadow_lb", [(0, 1), (0, 0), (3, 1), (3, 0), (1, 1), (1, 0)])
+def test_fused_images_bitwise(rt, image, shadow_lb):
+    """Every scene image of the fused trace kernels (pair layout in LDS, the
+    default / nodes and records in global memory with an LDS stack / with a
+    scratch stack), with shadow rays through the light buffer or through the
+    BVH (the primary launch then takes the wave traversal), gives the
+    exhaustive frame. The scenes above that do not fit in LDS (3000 spheres)
+    run image 3 on their own."""
     w, cam, depth = _glass_cluster(rt, n=250, seed=21, inside=False)
     exact, _ = cam.render(w, depth, want_stats=True)
-    rt._rtamd._tuning_set("lane", lane)
-    rt._rtamd._tuning_set("tw_closest", tw)
+    rt._rtamd._tuning_set("image", image)
+    rt._rtamd._tuning_set("shadow_lb", shadow_lb)
     try:
         fast, _ = cam.render(w, depth, want_stats=False)
+        assert rt._rtamd._wf_profile(w, -1, True)["fused"]
     finally:
-        rt._rtamd._tuning_set("lane", 14)
-        rt._rtamd._tuning_set("tw_closest", 4)
-    assert fast.to_numpy().tobytes() == exact.to_numpy().tobytes()
-
-
-@pytest.mark.parametrize("inside", [False, True])
-def test_lane_refill_bitwise(rt, inside):
-    """Lane refill (a lane takes its wave's next ray as soon as its own is
-    done) changes only when a ray is traced, never its result: the frame
-    equals the exhaustive frame, also with the camera inside nested glass."""
-    w, cam, depth = _glass_cluster(rt, n=250, seed=23, inside=inside)
-    exact, _ = cam.render(w, depth, want_stats=True)
-    rt._rtamd._tuning_set("refill", 1)
-    try:
-        fast, _ = cam.render(w, depth, want_stats=False)
-    finally:
-        rt._rtamd._tuning_set("refill", 0)
+        rt._rtamd._tuning_set("image", 0)
+        rt._rtamd._tuning_set("shadow_lb", 1)
     assert fast.to_numpy().tobytes() == exact.to_numpy().tobytes()
 
 
@@ -278,16 +263,3 @@ def test_frames_in_flight_bitwise(rt, n_streams, kind):
     for f in range(frames):
         assert bufs[f].cpu().numpy().tobytes() == full.tobytes(), f
         assert sh[f].cpu().numpy().tobytes() == full[rows8].tobytes(), f
-
-
-def test_primary_per_lane_knob_bitwise(rt):
-    """Primary rays through the per-lane pair traversal (knob prim_lane) give
-    the exhaustive frame, like the default wave (packet) traversal."""
-    w, cam, depth = _glass_cluster(rt, n=250, seed=23, inside=False)
-    exact, _ = cam.render(w, depth, want_stats=True)
-    rt._rtamd._tuning_set("prim_lane", 1)
-    try:
-        fast, _ = cam.render(w, depth, want_stats=False)
-    finally:
-        rt._rtamd._tuning_set("prim_lane", 0)
-    assert fast.to_numpy().tobytes() == exact.to_numpy().tobytes()

@@ -21,6 +21,8 @@ def _targs(n, name):
 def klass(n):
     """Kernel class of a demangled name: primary / closest / shadow / prep /
     combine / frame (wf_prim_prep: one per rendered frame)."""
+    if "wf_trace_fused<" in n:  # fused generation: closest hit + shading + shadow rays + spawn
+        return "primary" if _targs(n, "wf_trace_fused")[0] == "true" else "closest"
     if "wf_trace_closest_bvh<" in n:
         return "primary" if _targs(n, "wf_trace_closest_bvh")[0] == "true" else "closest"
     if "wf_trace_closest<" in n:
@@ -29,7 +31,7 @@ def klass(n):
         return "shadow"
     if "wf_prep(" in n:
         return "prep"
-    if "wf_combine(" in n or "wf_average(" in n:
+    if "wf_combine(" in n or "wf_combine_parents(" in n or "wf_average(" in n:
         return "combine"
     if "wf_prim_prep(" in n:
         return "frame"
