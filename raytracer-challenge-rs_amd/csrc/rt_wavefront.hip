@@ -217,9 +217,9 @@ __device__ __forceinline__ void shadow_result(const DevScene& sc, const WfArgs& 
 // bit-identical unless a component of ambient is -0 or NaN. Evaluated with
 // the operations lighting() itself performs; patterned materials are never
 // skipped. Returns whether it is, and that ambient value.
-__device__ __forceinline__ bool shadow_irrelevant(const ShadeRec& m, cLightRec L, V3 over, V3 normal, V3& ambient) {
+// `lightv` = (light.position - over).normalize(), the shadow ray's direction.
+__device__ __forceinline__ bool shadow_irrelevant(const ShadeRec& m, cLightRec L, V3 lightv, V3 normal, V3& ambient) {
   if (m.pattern_kind >= 0) return false;
-  const V3 lightv = vnormalize(vsub(v3(L->pos[0], L->pos[1], L->pos[2]), over));
   if (!(vdot(lightv, normal) < 0.0)) return false;
   const V3 effective_color = vmul(v3(m.color[0], m.color[1], m.color[2]),
                                   v3(L->intensity[0], L->intensity[1], L->intensity[2]));
@@ -454,7 +454,9 @@ __device__ __forceinline__ void prep_one(const DevScene& sc, const WfArgs& a, un
   if (hit) {
     for (unsigned l = 0; l < L; ++l) {
       V3 amb;
-      if (a.skip_shadow && l < 32 && shadow_irrelevant(*m, (cLightRec)sc.lights + l, c.over, c.normal, amb)) {
+      cLightRec Lr = (cLightRec)sc.lights + l;
+      if (a.skip_shadow && l < 32 &&
+          shadow_irrelevant(*m, Lr, vnormalize(vsub(v3(Lr->pos[0], Lr->pos[1], Lr->pos[2]), c.over)), c.normal, amb)) {
         skip |= 1u << l;
         double* sp = a.surf + ((size_t)slot * L + l) * 3;
         sp[0] = amb.x; sp[1] = amb.y; sp[2] = amb.z;
@@ -1095,14 +1097,15 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
   V3 surface = v3(0.0, 0.0, 0.0);  // fold from (0,0,0) (color.rs:96-103)
   for (unsigned l = 0; l < L; ++l) {
     cLightRec Lr = (cLightRec)sc.lights + l;
+    // the shadow ray exactly as World::is_shadowed builds it (world.rs:95-105); its
+    // direction is also lighting()'s light vector (same operands, same operations)
+    const V3 v = vsub(v3(Lr->pos[0], Lr->pos[1], Lr->pos[2]), c.over);
+    const double dist = sqrt(v.x * v.x + v.y * v.y + v.z * v.z);  // magnitude (vector.rs:21-23)
+    const V3 sdir = v3(v.x / dist, v.y / dist, v.z / dist);       // normalize (vector.rs:25-28)
     V3 term;
-    if (a.skip_shadow && shadow_irrelevant(*m, Lr, c.over, c.normal, term)) {
+    if (a.skip_shadow && shadow_irrelevant(*m, Lr, sdir, c.normal, term)) {
       // the light is behind the surface: lighting() is the ambient term either way
     } else {
-      // the shadow ray exactly as World::is_shadowed builds it (world.rs:95-105)
-      const V3 v = vsub(v3(Lr->pos[0], Lr->pos[1], Lr->pos[2]), c.over);
-      const double dist = sqrt(v.x * v.x + v.y * v.y + v.z * v.z);  // magnitude (vector.rs:21-23)
-      const V3 sdir = vnormalize(v);
       const bool shadowed = shadow_trace<LANE, QUADS>(sc, a, ls, l, c.over, sdir, dist, t.sh_disc, t.sh_tests,
                                                       t.sh_boxes);
       ++t.sh_rays;
