@@ -422,6 +422,7 @@ PYBIND11_MODULE(_rtamd, m) {
       py::dict tests, boxes;
       for (int i = 0; i < 3; ++i) { tests[cls[i]] = o[16 + i]; boxes[cls[i]] = o[19 + i]; }
       d["tests"] = tests; d["boxes"] = boxes; d["bvh"] = (bool)o[22]; d["n_bvh_nodes"] = o[23]; d["bvh_depth"] = o[24];
+      d["n_obvh_nodes"] = o[25]; d["n_other_culled"] = o[26];
       d["lb_res"] = o[27]; d["lb_items"] = o[28];
       py::dict shr, sht;
       shr["primary"] = o[29]; shr["closest"] = o[30]; sht["primary"] = o[31]; sht["closest"] = o[32];

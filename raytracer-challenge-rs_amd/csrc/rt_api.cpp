@@ -293,7 +293,7 @@ const char* rt_last_error(void) { return g_err.c_str(); }
 // of the wavefront pipeline. enable: 1 = on, 0 = off, -1 = just read. out[16]:
 // ms[5] (primary, closest, shadow, prep, combine), rays[3], disc[3],
 // n_diag, n_gen, n_planes, n_lights, n_quads, tests[3], boxes[3], bvh,
-// n_bvh_nodes, bvh_depth, (2 unused), lb_res, lb_items, sh_rays[2], sh_tests[2]
+// n_bvh_nodes, bvh_depth, n_obvh_nodes, n_other_culled, lb_res, lb_items, sh_rays[2], sh_tests[2]
 // (shadow rays / sphere tests inside the fused primary / secondary launches), fused.
 int rtamd_wf_profile(const rt_scene* cs, int enable, double out[34]) {
   if (!cs) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
@@ -332,8 +332,8 @@ int rtamd_wf_profile(const rt_scene* cs, int enable, double out[34]) {
     out[22] = p.bvh;
     out[23] = s->dev.n_bvh;
     out[24] = s->dev.bvh_depth;
-    out[25] = 0;
-    out[26] = 0;
+    out[25] = s->dev.n_obvh;
+    out[26] = s->dev.n_orec;
     out[27] = s->dev.lb_cells ? s->dev.lb_res : 0;
     out[28] = s->dev.lb_cells ? s->dev.lb_n_items : 0;
     for (int i = 0; i < 2; ++i) { out[29 + i] = p.sh_rays[i]; out[31 + i] = p.sh_tests[i]; }
@@ -597,10 +597,39 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   // come from `meta`, so the order changes no result)
   int bvh_depth = 0;
   std::vector<BvhNode> bvh = build_sphere_bvh(diag, g_bvh_leaf, &bvh_depth, g_bvh_ct / 100.0);
-  const bool bvh_code16 = !bvh.empty() && fill_code16(bvh);
-  int bvh4_stack = 0;
-  bool bvh4_code16 = false;
-  std::vector<BvhNode4> bvh4 = collapse_bvh4(bvh, &bvh4_stack, &bvh4_code16);
+  // ... and over the other bounded records (general spheres, cubes, cylinders
+  // with finite caps); the rest stays exhaustive on the fast path too
+  std::vector<OtherRec> orec;
+  std::vector<SphereGen> fx_gen;
+  std::vector<QuadRec> fx_quads;
+  double blo[3], bhi[3];
+  for (const SphereGen& g : gen) {
+    OtherRec r{};
+    for (int e = 0; e < 12; ++e) r.m[e] = g.m[e];
+    r.kind = 0;
+    r.meta = (int32_t)g.meta;
+    if (other_box(r, blo, bhi)) orec.push_back(r);
+    else fx_gen.push_back(g);
+  }
+  for (const QuadRec& q : quads) {
+    if (other_box(q, blo, bhi)) orec.push_back(q);
+    else fx_quads.push_back(q);
+  }
+  int obvh_depth = 0;
+  std::vector<BvhNode> obvh = build_other_bvh(orec, g_bvh_leaf, &obvh_depth, g_bvh_ct / 100.0);
+  if (obvh.empty()) {  // (only when there are no records, or more than the leaf codes can index)
+    for (const OtherRec& r : orec) {
+      if (r.kind == 0) {
+        SphereGen g{};
+        for (int e = 0; e < 12; ++e) g.m[e] = r.m[e];
+        g.meta = r.meta;
+        fx_gen.push_back(g);
+      } else {
+        fx_quads.push_back(r);
+      }
+    }
+    orec.clear();
+  }
   std::vector<LightRec> lrec(n_lights);
   for (size_t i = 0; i < n_lights; ++i)
     for (int c = 0; c < 3; ++c) { lrec[i].pos[c] = lights[i].position[c]; lrec[i].intensity[c] = lights[i].intensity[c]; }
@@ -617,8 +646,11 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   const size_t o_pl = align(o_gen + (gen.size() + 1) * sizeof(SphereGen));
   const size_t o_qd = align(o_pl + (planes.size() + 1) * sizeof(PlaneRec));
   const size_t o_bv = align(o_qd + (quads.size() + 1) * sizeof(QuadRec));
-  const size_t o_b4 = align(o_bv + (bvh.size() + 1) * sizeof(BvhNode));
-  const size_t o_sh = align(o_b4 + (bvh4.size() + 1) * sizeof(BvhNode4));
+  const size_t o_ob = align(o_bv + (bvh.size() + 1) * sizeof(BvhNode));
+  const size_t o_or = align(o_ob + (obvh.size() + 1) * sizeof(BvhNode));
+  const size_t o_fg = align(o_or + (orec.size() + 1) * sizeof(OtherRec));
+  const size_t o_fq = align(o_fg + (fx_gen.size() + 1) * sizeof(SphereGen));
+  const size_t o_sh = align(o_fq + (fx_quads.size() + 1) * sizeof(QuadRec));
   const size_t o_li = align(o_sh + shade.size() * sizeof(ShadeRec));
   const size_t o_lc = align(o_li + lrec.size() * sizeof(LightRec));
   const size_t o_lv = align(o_lc + lb.cells.size() * sizeof(LbCell));
@@ -631,7 +663,10 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   if (!planes.empty()) std::memcpy(&host[o_pl], planes.data(), planes.size() * sizeof(PlaneRec));
   if (!quads.empty()) std::memcpy(&host[o_qd], quads.data(), quads.size() * sizeof(QuadRec));
   if (!bvh.empty()) std::memcpy(&host[o_bv], bvh.data(), bvh.size() * sizeof(BvhNode));
-  if (!bvh4.empty()) std::memcpy(&host[o_b4], bvh4.data(), bvh4.size() * sizeof(BvhNode4));
+  if (!obvh.empty()) std::memcpy(&host[o_ob], obvh.data(), obvh.size() * sizeof(BvhNode));
+  if (!orec.empty()) std::memcpy(&host[o_or], orec.data(), orec.size() * sizeof(OtherRec));
+  if (!fx_gen.empty()) std::memcpy(&host[o_fg], fx_gen.data(), fx_gen.size() * sizeof(SphereGen));
+  if (!fx_quads.empty()) std::memcpy(&host[o_fq], fx_quads.data(), fx_quads.size() * sizeof(QuadRec));
   if (!shade.empty()) std::memcpy(&host[o_sh], shade.data(), shade.size() * sizeof(ShadeRec));
   if (!lrec.empty()) std::memcpy(&host[o_li], lrec.data(), lrec.size() * sizeof(LightRec));
   if (!lb.cells.empty()) {
@@ -664,11 +699,15 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   s->dev.bvh = bvh.empty() ? nullptr : (const BvhNode*)(b + o_bv);
   s->dev.n_bvh = (int32_t)bvh.size();
   s->dev.bvh_depth = bvh_depth;
-  s->dev.bvh_code16 = bvh_code16 ? 1 : 0;
-  s->dev.bvh4 = bvh4.empty() ? nullptr : (const BvhNode4*)(b + o_b4);
-  s->dev.n_bvh4 = (int32_t)bvh4.size();
-  s->dev.bvh4_stack = bvh4_stack;
-  s->dev.bvh4_code16 = bvh4_code16 ? 1 : 0;
+  s->dev.obvh = obvh.empty() ? nullptr : (const BvhNode*)(b + o_ob);
+  s->dev.orec = (const OtherRec*)(b + o_or);
+  s->dev.n_obvh = (int32_t)obvh.size();
+  s->dev.obvh_depth = obvh_depth;
+  s->dev.n_orec = (int32_t)orec.size();
+  s->dev.fx_gen = (const SphereGen*)(b + o_fg);
+  s->dev.fx_quads = (const QuadRec*)(b + o_fq);
+  s->dev.n_fx_gen = (int32_t)fx_gen.size();
+  s->dev.n_fx_quads = (int32_t)fx_quads.size();
   s->dev.lb_cells = lb.cells.empty() ? nullptr : (const LbCell*)(b + o_lc);
   s->dev.lb_ov = (const uint16_t*)(b + o_lv);
   s->dev.lb_delta = (const float*)(b + o_ld);

@@ -1,13 +1,13 @@
-// rt_bvh.cpp — host-side BVH over the SphereDiag records.
+// rt_bvh.cpp — host-side BVHs over the flattened world's bounded records.
 //
 // The reference accelerates only through `Group` (bounding-box early-out,
 // group.rs:50-70) and `Group::divide` (split the children by the halves of
 // the group's box, group.rs:108-188; AABB slab test bounding_box.rs:95-136).
 // This builder plays that role for the flattened world, with two changes
 // that matter on the GPU:
-//   * binned-SAH splits over the sphere centroids (32 bins, all three axes),
+//   * binned-SAH splits over the record centroids (32 bins, all three axes),
 //     and
-//   * every box is padded outward, so the traversal never culls a sphere the
+//   * every box is padded outward, so the traversal never culls a record the
 //     exhaustive loop would have hit: culling is exact by construction
 //     (DESIGN.md "Exact culling").
 #include "rt_bvh.hpp"
@@ -43,19 +43,22 @@ struct Box {
   }
 };
 
+// Padding of a record's box: 1e-6 of its size and position (far above the
+// rounding of any root computed from the record; DESIGN.md "Exact culling").
+void pad_axis(double lo, double hi, double* out_lo, double* out_hi) {
+  const double pad = 1e-6 * ((hi - lo) + std::fabs(lo) + std::fabs(hi)) + 1e-9;
+  *out_lo = lo - pad;
+  *out_hi = hi + pad;
+}
+
 // World-space extent of the record's unit sphere: the stored inverse maps
 // p -> s*p + t per axis, and |s*p + t| <= 1 means p in [(-1-t)/s, (1-t)/s].
-// Padded by 1e-6 of the box's size and position (far above the rounding of
-// any root computed from the record).
 Box sphere_box(const SphereDiag& r) {
   Box b;
   for (int a = 0; a < 3; ++a) {
     const double p0 = (-1.0 - r.t[a]) / r.s[a];
     const double p1 = (1.0 - r.t[a]) / r.s[a];
-    double lo = std::min(p0, p1), hi = std::max(p0, p1);
-    const double pad = 1e-6 * ((hi - lo) + std::fabs(lo) + std::fabs(hi)) + 1e-9;
-    b.lo[a] = lo - pad;
-    b.hi[a] = hi + pad;
+    pad_axis(std::min(p0, p1), std::max(p0, p1), &b.lo[a], &b.hi[a]);
   }
   return b;
 }
@@ -72,17 +75,19 @@ float f32_up(double x) {
   return f;
 }
 
+// Binned-SAH builder over item boxes; produces the node array and the leaf
+// order of the items (`order[k]` = original index of the k-th leaf item).
 struct Builder {
-  std::vector<SphereDiag>& sph;
+  std::vector<int> order;
   std::vector<Box> box;
-  std::vector<double> cen;  // 3 per sphere
+  std::vector<double> cen;  // 3 per item
   std::vector<BvhNode> nodes;
   int leaf_size;
-  double trav_cost;  // SAH cost of a node visit relative to one sphere test
+  double trav_cost;  // SAH cost of a node visit relative to one record test
 
   static constexpr int kBins = 32;
 
-  // Returns the child code for spheres [b, e) at `depth`.
+  // Returns the child code for items [b, e) at `depth`.
   int32_t build(int b, int e, int depth, Box* out_box) {
     Box bb, cb;
     for (int i = b; i < e; ++i) {
@@ -182,48 +187,49 @@ struct Builder {
     std::sort(idx.begin(), idx.end(), [&](int x, int y) {
       return cen[3 * x + axis] < cen[3 * y + axis] || (cen[3 * x + axis] == cen[3 * y + axis] && x < y);
     });
-    std::vector<SphereDiag> s2;
+    std::vector<int> o2;
     std::vector<Box> b2;
     std::vector<double> c2;
     for (int i : idx) {
-      s2.push_back(sph[i]);
+      o2.push_back(order[i]);
       b2.push_back(box[i]);
       c2.insert(c2.end(), &cen[3 * i], &cen[3 * i] + 3);
     }
     for (int i = b; i < e; ++i) {
-      sph[i] = s2[i - b];
+      order[i] = o2[i - b];
       box[i] = b2[i - b];
       std::memcpy(&cen[3 * i], &c2[3 * (i - b)], 3 * sizeof(double));
     }
   }
   void swap_items(int i, int j) {
-    std::swap(sph[i], sph[j]);
+    std::swap(order[i], order[j]);
     std::swap(box[i], box[j]);
     for (int a = 0; a < 3; ++a) std::swap(cen[3 * i + a], cen[3 * j + a]);
   }
 };
 
-}  // namespace
-
-static int tree_depth(const std::vector<BvhNode>& nodes, int32_t e) {
+int tree_depth(const std::vector<BvhNode>& nodes, int32_t e) {
   if (e < 0) return 0;
   return 1 + std::max(tree_depth(nodes, nodes[e].child[0]), tree_depth(nodes, nodes[e].child[1]));
 }
 
-std::vector<BvhNode> build_sphere_bvh(std::vector<SphereDiag>& spheres, int leaf_size, int* depth, double trav_cost) {
+// The hierarchy over `boxes`; `order` receives the leaf order of the items.
+std::vector<BvhNode> build_over_boxes(const std::vector<Box>& boxes, int leaf_size, double trav_cost, int* depth,
+                                      std::vector<int>* order) {
   if (depth) *depth = 0;
+  order->clear();
   std::vector<BvhNode> out;
-  const int n = (int)spheres.size();
+  const int n = (int)boxes.size();
   if (n == 0) return out;
   // the leaf code stores the first index in 24 bits
   if (n >= (1 << 24)) return out;
   leaf_size = std::max(1, std::min(leaf_size, kBvhLeafMax));
-  Builder bd{spheres, {}, {}, {}, leaf_size, trav_cost};
-  bd.box.resize(n);
+  Builder bd{{}, boxes, {}, {}, leaf_size, trav_cost};
+  bd.order.resize(n);
   bd.cen.resize(3 * n);
   for (int i = 0; i < n; ++i) {
-    bd.box[i] = sphere_box(spheres[i]);
-    for (int a = 0; a < 3; ++a) bd.cen[3 * i + a] = 0.5 * (bd.box[i].lo[a] + bd.box[i].hi[a]);
+    bd.order[i] = i;
+    for (int a = 0; a < 3; ++a) bd.cen[3 * i + a] = 0.5 * (boxes[i].lo[a] + boxes[i].hi[a]);
   }
   bd.nodes.reserve(2 * n / std::max(1, leaf_size) + 2);
   Box all;
@@ -236,120 +242,93 @@ std::vector<BvhNode> build_sphere_bvh(std::vector<SphereDiag>& spheres, int leaf
     bd.nodes.assign(1, r);
   }
   if (depth) *depth = tree_depth(bd.nodes, 0);  // kBvhEmpty < 0 counts as a leaf
+  *order = bd.order;
   return bd.nodes;
 }
 
-namespace {
-struct Slot4 {
-  int32_t code;
-  float lo[3], hi[3];
-  double area() const {
-    const double dx = (double)hi[0] - lo[0], dy = (double)hi[1] - lo[1], dz = (double)hi[2] - lo[2];
-    return 2.0 * (dx * dy + dy * dz + dz * dx);
-  }
-};
-
-struct Collapser {
-  const std::vector<BvhNode>& bin;
-  std::vector<BvhNode4> out;
-  bool code16 = true;
-
-  static Slot4 child_slot(const BvhNode& n, int k) {
-    Slot4 s;
-    s.code = n.child[k];
-    for (int a = 0; a < 3; ++a) { s.lo[a] = n.lo[k][a]; s.hi[a] = n.hi[k][a]; }
-    return s;
-  }
-  // four-wide node for binary node `e`; returns its index and the pending-entry need below it
-  int32_t make(int32_t e, int* need) {
-    std::vector<Slot4> kids;
-    for (int k = 0; k < 2; ++k)
-      if (bin[e].child[k] != kBvhEmpty) kids.push_back(child_slot(bin[e], k));
-    while (kids.size() < 4) {
-      int best = -1;
-      double ba = -1.0;
-      for (int i = 0; i < (int)kids.size(); ++i)
-        if (kids[i].code >= 0 && kids[i].area() > ba) { ba = kids[i].area(); best = i; }
-      if (best < 0) break;
-      const BvhNode& n = bin[kids[best].code];
-      std::vector<Slot4> rep;
-      for (int k = 0; k < 2; ++k)
-        if (n.child[k] != kBvhEmpty) rep.push_back(child_slot(n, k));
-      if (kids.size() - 1 + rep.size() > 4) break;
-      kids.erase(kids.begin() + best);
-      kids.insert(kids.begin() + best, rep.begin(), rep.end());
-    }
-    const int32_t idx = (int32_t)out.size();
-    out.emplace_back();
-    int below = 0;
-    int32_t codes[4];
-    for (int i = 0; i < 4; ++i) {
-      codes[i] = kBvhEmpty;
-      if (i >= (int)kids.size()) continue;
-      codes[i] = kids[i].code;
-      if (kids[i].code >= 0) {
-        int nb = 0;
-        codes[i] = make(kids[i].code, &nb);
-        below = std::max(below, nb);
-      }
-    }
-    BvhNode4& nd = out[idx];
-    std::memset(&nd, 0, sizeof nd);
-    for (int i = 0; i < 4; ++i) {
-      nd.child[i] = codes[i];
-      nd.code[i] = (uint16_t)kBvh4Empty;
-      if (codes[i] >= 0) {
-        if (codes[i] < 0x8000) nd.code[i] = (uint16_t)codes[i];
-        else code16 = false;
-      } else if (codes[i] != kBvhEmpty) {
-        const int code = -(codes[i] + 1), first = code >> 7, cnt = code & 127;
-        if (cnt >= 1 && cnt <= 8 && first + cnt < 0xFFF) nd.code[i] = (uint16_t)(0x8000 | (cnt - 1) << 12 | first);
-        else code16 = false;
-      }
-      for (int a = 0; a < 3; ++a) {
-        nd.lo[a][i] = i < (int)kids.size() ? kids[i].lo[a] : 0.0f;
-        nd.hi[a][i] = i < (int)kids.size() ? kids[i].hi[a] : 0.0f;
-      }
-    }
-    *need = (int)kids.size() - 1 + below;
-    return idx;
-  }
-};
-}  // namespace
-
-std::vector<BvhNode4> collapse_bvh4(const std::vector<BvhNode>& bin, int* stack, bool* code16) {
-  if (stack) *stack = 0;
-  if (code16) *code16 = false;
-  if (bin.empty()) return {};
-  Collapser c{bin, {}};
-  c.out.reserve(bin.size());
-  int need = 0;
-  c.make(0, &need);
-  if (stack) *stack = need;
-  if (code16) *code16 = c.code16;
-  return c.out;
+template <typename R>
+void apply_order(std::vector<R>& items, const std::vector<int>& order) {
+  std::vector<R> out;
+  out.reserve(order.size());
+  for (int i : order) out.push_back(items[i]);
+  items.swap(out);
 }
 
-namespace {
-// BvhNode4::code encoding of a binary child code; false when it does not fit
-bool to_code16(int32_t c, uint16_t* out) {
-  if (c == kBvhEmpty) { *out = (uint16_t)kBvh4Empty; return true; }
-  if (c >= 0) { *out = (uint16_t)c; return c < 0x8000; }
-  const int code = -(c + 1), first = code >> 7, cnt = code & 127;
-  *out = (uint16_t)(0x8000 | (cnt - 1) << 12 | first);
-  return cnt >= 1 && cnt <= 8 && first + cnt < 0xFFF;
+// A = the 3x3 part of an inverse (rows 0-2), F = A^-1 by cofactors; returns
+// |A|_inf * |F|_inf (the condition number), or +inf when A is singular.
+double invert3(const double* m, double F[3][3]) {
+  const double a[3][3] = {{m[0], m[1], m[2]}, {m[4], m[5], m[6]}, {m[8], m[9], m[10]}};
+  const double c00 = a[1][1] * a[2][2] - a[1][2] * a[2][1];
+  const double c01 = a[1][2] * a[2][0] - a[1][0] * a[2][2];
+  const double c02 = a[1][0] * a[2][1] - a[1][1] * a[2][0];
+  const double det = a[0][0] * c00 + a[0][1] * c01 + a[0][2] * c02;
+  if (!(std::fabs(det) > 0.0) || !std::isfinite(det)) return INFINITY;
+  F[0][0] = c00 / det;
+  F[1][0] = c01 / det;
+  F[2][0] = c02 / det;
+  F[0][1] = (a[0][2] * a[2][1] - a[0][1] * a[2][2]) / det;
+  F[1][1] = (a[0][0] * a[2][2] - a[0][2] * a[2][0]) / det;
+  F[2][1] = (a[0][1] * a[2][0] - a[0][0] * a[2][1]) / det;
+  F[0][2] = (a[0][1] * a[1][2] - a[0][2] * a[1][1]) / det;
+  F[1][2] = (a[0][2] * a[1][0] - a[0][0] * a[1][2]) / det;
+  F[2][2] = (a[0][0] * a[1][1] - a[0][1] * a[1][0]) / det;
+  double na = 0.0, nf = 0.0;
+  for (int r = 0; r < 3; ++r) {
+    na = std::max(na, std::fabs(a[r][0]) + std::fabs(a[r][1]) + std::fabs(a[r][2]));
+    nf = std::max(nf, std::fabs(F[r][0]) + std::fabs(F[r][1]) + std::fabs(F[r][2]));
+  }
+  const double k = na * nf;
+  return std::isfinite(k) ? k : INFINITY;
 }
+
 }  // namespace
 
-bool fill_code16(std::vector<BvhNode>& bin) {
-  bool ok = bin.size() < 0x8000;
-  for (BvhNode& n : bin) {
-    uint16_t c0 = 0, c1 = 0;
-    ok = to_code16(n.child[0], &c0) && ok;
-    ok = to_code16(n.child[1], &c1) && ok;
-    n.code16 = (uint32_t)c0 | (uint32_t)c1 << 16;
+std::vector<BvhNode> build_sphere_bvh(std::vector<SphereDiag>& spheres, int leaf_size, int* depth, double trav_cost) {
+  std::vector<Box> boxes(spheres.size());
+  for (size_t i = 0; i < spheres.size(); ++i) boxes[i] = sphere_box(spheres[i]);
+  std::vector<int> order;
+  std::vector<BvhNode> nodes = build_over_boxes(boxes, leaf_size, trav_cost, depth, &order);
+  if (!nodes.empty()) apply_order(spheres, order);
+  return nodes;
+}
+
+bool other_box(const OtherRec& r, double lo[3], double hi[3]) {
+  // cones stay exhaustive: their a ~ 0 branch pushes t = -c / 2.0 * b
+  // (cone.rs:104), a root that need not lie on the cone at all
+  if (r.kind != 0 && r.kind != 2 && r.kind != 3) return false;
+  double L[3] = {-1.0, -1.0, -1.0}, U[3] = {1.0, 1.0, 1.0};
+  if (r.kind == 3) {  // cylinder: bounded only with finite caps' planes
+    if (!std::isfinite(r.minimum) || !std::isfinite(r.maximum) || !(r.minimum <= r.maximum)) return false;
+    L[1] = r.minimum;
+    U[1] = r.maximum;
   }
-  return ok;
+  double F[3][3];
+  const double cond = invert3(r.m, F);
+  if (!(cond <= 1e6)) return false;  // too ill-conditioned for the padding argument
+  const double b[3] = {r.m[3], r.m[7], r.m[11]};
+  for (int i = 0; i < 3; ++i) {
+    // world point p = F (q - b) for a local point q of the record's region
+    double c = 0.0, h = 0.0;
+    for (int j = 0; j < 3; ++j) {
+      c += F[i][j] * (0.5 * (L[j] + U[j]) - b[j]);
+      h += r.kind == 0 ? F[i][j] * F[i][j] : std::fabs(F[i][j]) * 0.5 * (U[j] - L[j]);
+    }
+    if (r.kind == 0) h = std::sqrt(h);  // the ellipsoid's extent along axis i
+    h *= 1.0 + 1e-12;                   // the rounding of F, c and h themselves
+    if (!std::isfinite(c) || !std::isfinite(h)) return false;
+    pad_axis(c - h, c + h, &lo[i], &hi[i]);
+  }
+  return true;
+}
+
+std::vector<BvhNode> build_other_bvh(std::vector<OtherRec>& recs, int leaf_size, int* depth, double trav_cost) {
+  std::vector<Box> boxes(recs.size());
+  for (size_t i = 0; i < recs.size(); ++i)
+    if (!other_box(recs[i], boxes[i].lo, boxes[i].hi)) return {};  // the caller passes bounded records only
+  std::vector<int> order;
+  std::vector<BvhNode> nodes = build_over_boxes(boxes, leaf_size, trav_cost, depth, &order);
+  if (!nodes.empty()) apply_order(recs, order);
+  return nodes;
 }
 
 // ------------------------------------------------------------ light buffer

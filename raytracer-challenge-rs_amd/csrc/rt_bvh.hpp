@@ -1,4 +1,4 @@
-// rt_bvh.hpp — host-side BVH over the SphereDiag records (see rt_layout.hpp).
+// rt_bvh.hpp — host-side BVHs over the bounded records and the light buffer (see rt_layout.hpp).
 #pragma once
 #include <stddef.h>
 #include <vector>
@@ -19,18 +19,15 @@ namespace rtamd {
 std::vector<BvhNode> build_sphere_bvh(std::vector<SphereDiag>& spheres, int leaf_size, int* depth = nullptr,
                                       double trav_cost = 1.0);
 
-// Collapses the binary hierarchy into four-wide nodes (root = 0): each node
-// repeatedly opens its largest-area internal child until it holds four
-// children. Boxes and leaf codes are copied unchanged, so the four-wide
-// traversal culls exactly what the binary one may cull. `stack` receives the
-// most entries a nearest-first traversal keeps pending (on a root-leaf path,
-// the sum of (children - 1) over its nodes). `code16` tells whether every
-// child fits BvhNode4::code.
-std::vector<BvhNode4> collapse_bvh4(const std::vector<BvhNode>& bin, int* stack = nullptr, bool* code16 = nullptr);
-
-// Fills BvhNode::code16 of every node; returns whether every child fits the
-// 16-bit code (else the 16-bit traversal is not used).
-bool fill_code16(std::vector<BvhNode>& bin);
+// The other bounded records (general-transform spheres, cubes, cylinders
+// with finite caps; rt_layout.hpp OtherRec): other_box gives the padded
+// world box of one (false when the record must stay exhaustive: a cone, an
+// open-ended cylinder, an ill-conditioned transform). build_other_bvh builds
+// the hierarchy over records that all have one (reordered in place into leaf
+// order); empty when there are none.
+bool other_box(const OtherRec& r, double lo[3], double hi[3]);
+std::vector<BvhNode> build_other_bvh(std::vector<OtherRec>& recs, int leaf_size, int* depth = nullptr,
+                                     double trav_cost = 1.0);
 
 // Light buffer over the shadow-casting records, one cube map of R x R cells
 // per face per light (rt_layout.hpp LbCell; DESIGN.md "Light buffer").

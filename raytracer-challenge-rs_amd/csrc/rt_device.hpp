@@ -223,8 +223,8 @@ __device__ __forceinline__ int quad_local_intersect(int kind, double mn, double 
 // Shape::intersect (geometry/mod.rs:46-49) of one QuadRec, folded into `h`:
 // the nearest t >= 0 of the object's list competes by (t, key); an object
 // with an odd number of t < 0 is a container, ordered by its last one.
-template <bool SHADOW>
-__device__ __forceinline__ void quad_test(cQuadRec q, V3 o, V3 d, Hit& h) {
+template <bool SHADOW, typename QP>  // QP: constant-address (wave-uniform) or generic record pointer
+__device__ __forceinline__ void quad_test(QP q, V3 o, V3 d, Hit& h) {
   const V3 lo = v3(q->m[0] * o.x + q->m[1] * o.y + q->m[2] * o.z + q->m[3],
                    q->m[4] * o.x + q->m[5] * o.y + q->m[6] * o.z + q->m[7],
                    q->m[8] * o.x + q->m[9] * o.y + q->m[10] * o.z + q->m[11]);
@@ -256,10 +256,13 @@ __device__ __forceinline__ void quad_test(cQuadRec q, V3 o, V3 d, Hit& h) {
 // cubes / cylinders / cones), tested exhaustively from global memory.
 // QUADS = false compiles the solids out (kernel variants for scenes without
 // them keep the sphere loops' register allocation, hence their occupancy).
-template <bool SHADOW, bool QUADS = true>
+// FAST: the fast path's remainder (the records outside both hierarchies;
+// the other bounded records are traversed by other_trace).
+template <bool SHADOW, bool QUADS = true, bool FAST = false>
 __device__ __forceinline__ void trace_rest(const DevScene& sc, V3 o, V3 d, Hit& h, unsigned& n_disc) {
-  cSphereGen sg = (cSphereGen)sc.sph_gen;
-  for (int j = 0; j < sc.n_gen; ++j) {
+  cSphereGen sg = (cSphereGen)(FAST ? sc.fx_gen : sc.sph_gen);
+  const int n_gen = FAST ? sc.n_fx_gen : sc.n_gen;
+  for (int j = 0; j < n_gen; ++j) {
     double m[12];
 #pragma unroll
     for (int e = 0; e < 12; ++e) m[e] = sg[j].m[e];
@@ -275,8 +278,25 @@ __device__ __forceinline__ void trace_rest(const DevScene& sc, V3 o, V3 d, Hit& 
     plane_test<SHADOW>(oy, dy, (int)pl[j].meta, h);
   }
   if constexpr (QUADS) {
-    cQuadRec qr = (cQuadRec)sc.quads;
-    for (int j = 0; j < sc.n_quads; ++j) quad_test<SHADOW>(qr + j, o, d, h);
+    cQuadRec qr = (cQuadRec)(FAST ? sc.fx_quads : sc.quads);
+    const int n_quads = FAST ? sc.n_fx_quads : sc.n_quads;
+    for (int j = 0; j < n_quads; ++j) quad_test<SHADOW>(qr + j, o, d, h);
+  }
+}
+
+// One culled other record (rt_layout.hpp OtherRec) with exactly the
+// operations of the exhaustive loops above: a general sphere as trace_rest's
+// general records, a solid as quad_test.
+template <bool SHADOW>
+__device__ __forceinline__ void other_test(const OtherRec* q, V3 o, V3 d, Hit& h, unsigned& n_disc) {
+  if (q->kind == 0) {
+    const double* m = q->m;
+    const V3 lo = m34_point(m, o);
+    const V3 ld = v3(m[0] * d.x + m[1] * d.y + m[2] * d.z, m[4] * d.x + m[5] * d.y + m[6] * d.z,
+                     m[8] * d.x + m[9] * d.y + m[10] * d.z);
+    sphere_test<SHADOW>(lo.x, lo.y, lo.z, ld.x, ld.y, ld.z, [&] { return (int)q->meta; }, h, n_disc);
+  } else {
+    quad_test<SHADOW>(q, o, d, h);
   }
 }
 

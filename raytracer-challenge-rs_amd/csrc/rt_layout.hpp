@@ -44,39 +44,25 @@ struct alignas(64) QuadRec {  // cube.rs / cylinder.rs / cone.rs
 };
 static_assert(sizeof(QuadRec) == 128, "QuadRec must stay 128 B");
 
-// Bounding-volume hierarchy over the SphereDiag records (built on the host,
-// rt_bvh.cpp). Binary nodes carry both children's boxes, so one 64-B load
-// (one s_load_dwordx16 for a wave, four 16-B loads for a lane) decides both
-// children. Boxes are binary32 rounded OUTWARD from the padded binary64
-// boxes (the slab test itself runs in binary64, so culling stays
-// conservative). A child is an internal node index (>= 0), a leaf code
-// -(1 + (first << 7 | count)) over the (reordered) SphereDiag array, or
-// kBvhEmpty. `code16` holds both children again as 16-bit codes (child 0 in
-// the low half; the encoding of BvhNode4::code), valid when
-// DevScene::bvh_code16 is set.
+// Bounding-volume hierarchies (built on the host, rt_bvh.cpp): one over the
+// SphereDiag records, one over the other bounded records (OtherRec: general-
+// transform spheres, cubes, bounded cylinders). Binary nodes carry both
+// children's boxes, so one 64-B load (one s_load_dwordx16 for a wave, four
+// 16-B loads for a lane) decides both children. Boxes are binary32 rounded
+// OUTWARD from the padded binary64 boxes, so culling stays conservative
+// (DESIGN.md "Exact culling"). A child is an internal node index (>= 0), a
+// leaf code -(1 + (first << 7 | count)) over the (reordered) record array,
+// or kBvhEmpty.
 struct alignas(64) BvhNode {
   float lo[2][3], hi[2][3];
   int32_t child[2];
   int32_t axis;
-  uint32_t code16;
+  uint32_t pad;
 };
 static_assert(sizeof(BvhNode) == 64, "BvhNode must stay 64 B");
-// Four-wide node, collapsed from the binary hierarchy (rt_bvh.cpp): the four
-// children's boxes (the binary nodes' binary32 boxes, copied unchanged) laid
-// out per coordinate, so one lane reads what it needs in seven 16-B loads and
-// tests the four boxes with independent instruction streams. `code` is the
-// traversal's 16-bit child code: an internal node index (< 0x8000), a leaf
-// 0x8000 | (count - 1) << 12 | first (count <= 8, first + count < 0xFFF), or
-// kBvh4Empty; valid when DevScene::bvh4_code16 is set. `child` keeps the
-// binary hierarchy's 32-bit codes (internal index / leaf code / kBvhEmpty).
-struct alignas(128) BvhNode4 {
-  float lo[3][4], hi[3][4];  // lo[axis][child]
-  uint16_t code[4];
-  int32_t child[4];
-  int32_t pad[2];
-};
-constexpr int kBvh4Empty = 0xFFFF;
-static_assert(sizeof(BvhNode4) == 128, "BvhNode4 must stay 128 B");
+// A culled record other than a diagonal sphere: the QuadRec layout, with
+// kind 0 = sphere under a general inverse (rows 0-2 in m).
+typedef QuadRec OtherRec;
 constexpr int32_t kBvhEmpty = (int32_t)0x80000000;
 constexpr int kBvhLeafMax = 127;
 constexpr int kBvhMaxDepth = 60;  // traversal stack entries per wave
@@ -146,11 +132,14 @@ struct DevScene {
   int32_t n_quads;
   int32_t n_bvh;
   int32_t bvh_depth;  // most far children pending on a traversal stack
-  int32_t bvh_code16;  // 1 when every BvhNode::code16 is valid (< 0x8000 nodes, leaves of <= 8 below 0xFFF)
-  const BvhNode4* bvh4;  // the same hierarchy, four-wide (nullptr when the scene has no BVH)
-  int32_t n_bvh4;
-  int32_t bvh4_stack;  // most children a nearest-first four-wide traversal keeps pending
-  int32_t bvh4_code16;  // 1 when every BvhNode4::code is valid (scenes of < 4088 diagonal spheres)
+  // fast path: the hierarchy over the other bounded records, and what stays
+  // outside every hierarchy (tested exhaustively, with the planes)
+  const BvhNode* obvh;      // nullptr when there are no culled other records
+  const OtherRec* orec;     // in obvh leaf order
+  int32_t n_obvh, obvh_depth, n_orec;
+  const SphereGen* fx_gen;  // general spheres outside the obvh
+  const QuadRec* fx_quads;  // cubes / cylinders / cones outside the obvh
+  int32_t n_fx_gen, n_fx_quads;
   const LbCell* lb_cells;  // light buffer: n_lights * 6R^2 cells, nullptr when not built
   const uint16_t* lb_ov;
   const float* lb_delta;   // n_lights * n_diag

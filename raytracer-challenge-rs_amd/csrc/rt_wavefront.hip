@@ -832,6 +832,52 @@ __device__ __forceinline__ void stage_lds(uint4* dst, const uint4* src, int n) {
   for (; i < n; i += bd) dst[i] = src[i];
 }
 
+// Per-lane traversal of the hierarchy over the other bounded records
+// (general-transform spheres, cubes, cylinders with finite caps; global
+// memory, private stack): the same culling rule and exactness argument as the
+// sphere hierarchy (DESIGN.md "Exact culling"). Scenes made of diagonal
+// spheres and planes (C3, C5) have no such hierarchy.
+template <bool SHADOW>
+__device__ __forceinline__ void other_trace(const DevScene& sc, V3 o, V3 d, double t_shadow, Hit& h,
+                                            unsigned& n_disc, unsigned& n_tests, unsigned& n_boxes) {
+  if (sc.n_obvh == 0 || (SHADOW && h.key >= 0 && h.t < t_shadow)) return;
+  const BvhNode* nodes = sc.obvh;
+  float M[3];
+  for (int ax = 0; ax < 3; ++ax)  // the root's two child boxes contain every box below them
+    M[ax] = fmaxf(fmaxf(fabsf(nodes[0].lo[0][ax]), fabsf(nodes[0].hi[0][ax])),
+                  fmaxf(fabsf(nodes[0].lo[1][ax]), fabsf(nodes[0].hi[1][ax])));
+  const SlabRay sr = slab_ray(o, d, M);
+  float t_hi = f32_up(SHADOW ? t_shadow : h.t);
+  int stk[kBvhMaxDepth + 4];
+  int sp = 0, e = 0;
+  while (e != kBvhEmpty) {
+    if (e >= 0) {
+      const BvhNode& nd = nodes[e];
+      float t0 = 0.0f, t1 = 0.0f;
+      const bool h0 = slab_hit32(nd.lo[0], nd.hi[0], sr, t_hi, t0);
+      const bool h1 = nd.child[1] != kBvhEmpty && slab_hit32(nd.lo[1], nd.hi[1], sr, t_hi, t1);
+      n_boxes += 2;
+      if (h0 && h1) {
+        const bool flip = t1 < t0;
+        stk[sp++] = flip ? nd.child[0] : nd.child[1];
+        e = flip ? nd.child[1] : nd.child[0];
+      } else {
+        e = h0 ? nd.child[0] : h1 ? nd.child[1] : (sp > 0 ? stk[--sp] : kBvhEmpty);
+      }
+    } else {
+      const int code = -(e + 1), first = code >> 7, cnt = code & 127;
+      for (int k = first; k < first + cnt; ++k) other_test<SHADOW>(sc.orec + k, o, d, h, n_disc);
+      n_tests += (unsigned)cnt;
+      if constexpr (SHADOW) {
+        if (h.key >= 0 && h.t < t_shadow) return;  // shadowed: done
+      } else {
+        t_hi = f32_up(h.t);
+      }
+      e = sp > 0 ? stk[--sp] : kBvhEmpty;
+    }
+  }
+}
+
 // ------------------------------------------------------------ fused trace kernels
 // The fast path (BVH) evaluates a whole generation in ONE launch per
 // generation (DESIGN.md "Fused generations"): closest hit, prepare_computations,
@@ -980,7 +1026,8 @@ __device__ __forceinline__ bool shadow_trace(const DevScene& sc, const WfArgs& a
                                              unsigned& n_boxes) {
   Hit h;
   hit_init(h);
-  trace_rest<true, QUADS>(sc, o, d, h, n_disc);
+  trace_rest<true, QUADS, true>(sc, o, d, h, n_disc);
+  if constexpr (QUADS) other_trace<true>(sc, o, d, dist, h, n_disc, n_tests, n_boxes);
   if (!(h.key >= 0 && h.t < dist)) {
     if (a.use_lb) {
       lb_walk(sc, ls.sd, ls.delta, l, o, d, dist, h, n_disc, n_tests);
@@ -1164,9 +1211,12 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
       wf_ray(a, cam, slot, o, d);
       if constexpr (LANE == 0) {
         bvh_trace<PRIMARY, false>(sc, (cPrimRec)a.prim, stk, o, d, 0.0, h, t.disc, t.tests, t.boxes);
-        trace_rest<false, QUADS>(sc, o, d, h, t.disc);
+        trace_rest<false, QUADS, true>(sc, o, d, h, t.disc);
+        if constexpr (QUADS) other_trace<false>(sc, o, d, 0.0, h, t.disc, t.tests, t.boxes);
       } else {
-        trace_rest<false, QUADS>(sc, o, d, h, t.disc);  // planes first: an early nearest hit tightens the culling
+        // planes and the other records first: an early nearest hit tightens the culling
+        trace_rest<false, QUADS, true>(sc, o, d, h, t.disc);
+        if constexpr (QUADS) other_trace<false>(sc, o, d, 0.0, h, t.disc, t.tests, t.boxes);
         if constexpr (LANE == 14)
           lane_trace_pair<false>(ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, t.disc, t.tests, t.boxes,
                                  ls.stack);
@@ -1635,8 +1685,9 @@ static hipError_t launch_fused_q(const DevScene& sc, const DevCamera& cam, WfArg
 }
 static hipError_t launch_fused(const DevScene& sc, const DevCamera& cam, const WfArgs& a, bool primary, unsigned n,
                                hipStream_t stream) {
-  return sc.n_quads > 0 ? launch_fused_q<true>(sc, cam, a, primary, n, stream)
-                        : launch_fused_q<false>(sc, cam, a, primary, n, stream);
+  // QUADS: solids outside the hierarchies, or the hierarchy over the other records
+  return sc.n_fx_quads > 0 || sc.n_obvh > 0 ? launch_fused_q<true>(sc, cam, a, primary, n, stream)
+                                            : launch_fused_q<false>(sc, cam, a, primary, n, stream);
 }
 
 int Wavefront::g_corrupt_calibration = 0;
@@ -1656,7 +1707,7 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
   // reference's every-shape loop is asked for; counting (stats) never changes the algorithm
   const bool exhaustive = (flags & WF_EXHAUSTIVE) != 0;
   const bool count = stats != nullptr || (flags & WF_COUNT) != 0;
-  const bool bvh = g_wf_accel != 0 && !exhaustive && sc.n_bvh > 0;
+  const bool bvh = g_wf_accel != 0 && !exhaustive && (sc.n_bvh > 0 || sc.n_obvh > 0);
   const bool fused = bvh;
   const bool skip_shadow = !exhaustive && g_wf_skip_shadow != 0;
   // the shadow-ray counts differ between the two modes; the fused pipeline's

@@ -263,3 +263,110 @@ def test_frames_in_flight_bitwise(rt, n_streams, kind):
     for f in range(frames):
         assert bufs[f].cpu().numpy().tobytes() == full.tobytes(), f
         assert sh[f].cpu().numpy().tobytes() == full[rows8].tobytes(), f
+
+
+def _general_field(rt, n=360, seed=17):
+    """Every shape kind under general transforms (rotated, sheared, scaled):
+    spheres, cubes, closed and open bounded cylinders (culled by the other
+    records' hierarchy), cones and an open-ended cylinder (exhaustive), a
+    few diagonal spheres, glass and mirrors nested in each other."""
+    rng = np.random.default_rng(seed)
+    w = rt.World()
+    floor = rt.Plane()
+    floor.material.reflective = 0.25
+    w.add_object(floor)
+    pole = rt.Cylinder()  # infinite: stays exhaustive
+    pole.set_transform(rt.translation(4.5, 0, 4.5) * rt.scaling(0.2, 1.0, 0.2))
+    w.add_object(pole)
+    for i in range(n):
+        k = i % 6
+        if k in (0, 1):
+            s = rt.glass_sphere() if i % 4 == 0 else rt.Sphere()
+        elif k == 2:
+            s = rt.Cube()
+        elif k == 3:
+            lo = float(rng.uniform(-1.0, 0.0))
+            s = rt.Cylinder(lo, lo + float(rng.uniform(0.2, 1.5)), bool(i % 2))
+        elif k == 4:
+            s = rt.Cone(float(rng.uniform(-1.0, -0.2)), float(rng.uniform(0.0, 0.8)), True)
+        else:
+            s = rt.Sphere()
+        r = float(rng.uniform(0.15, 0.5))
+        c = rng.uniform([-4, r, -4], [4, 3, 4])
+        if k == 5:  # diagonal (translation . scaling): the sphere hierarchy
+            tf = rt.translation(*c) * rt.scaling(r, r * 0.8, r * 1.2)
+        else:
+            tf = (rt.translation(*c) * rt.rotation_y(float(rng.uniform(0, 6.3)))
+                  * rt.rotation_x(float(rng.uniform(0, 6.3)))
+                  * rt.shearing(*[float(x) for x in rng.uniform(-0.3, 0.3, 6)]) * rt.scaling(r, r * 0.7, r * 1.1))
+        s.set_transform(tf)
+        s.material.color = rt.Color(*rng.uniform(0, 1, 3))
+        if i % 3 == 1:
+            s.material.transparency = 0.8
+            s.material.refractive_index = float(1.0 + rng.uniform(0, 1.2))
+            s.material.reflective = 0.5
+        elif i % 3 == 2:
+            s.material.reflective = float(rng.uniform(0.2, 0.9))
+        w.add_object(s)
+    w.add_light(rt.PointLight(rt.Point(-10, 10, -10), rt.Color(1, 1, 1)))
+    return w
+
+
+@pytest.mark.parametrize("frm", [(0, 2.5, -9), (0.0, 1.2, 0.0), (-2.0, 1.5, -1.0)])
+def test_other_records_hierarchy_bitwise(rt, frm):
+    """General-transform spheres, cubes and bounded cylinders are culled by a
+    hierarchy of their own (Group::divide's role, group.rs:108-188, over
+    padded world boxes of the transformed shapes); the frames stay bitwise
+    equal to the exhaustive loop, from outside and from inside the field."""
+    w = _general_field(rt)
+    cam = rt.Camera(128, 96, PI / 2.5)
+    cam.set_transform(rt.view_transform(rt.Point(*frm), rt.Point(0, 1, 2), rt.Vector(0, 1, 0)))
+    fast, exact, st = _both(rt, w, cam, 6)
+    p = rt._rtamd._wf_profile(w, -1, True)
+    assert p["n_other_culled"] > 200 and p["n_obvh_nodes"] > 0
+    assert fast.tobytes() == exact.tobytes()
+
+
+def test_other_records_hierarchy_random_rays(rt):
+    """color_at from random origins (inside solids too) and directions, with
+    axis-aligned and grazing directions, at several depths."""
+    w = _general_field(rt, n=240, seed=5)
+    rng = np.random.default_rng(9)
+    o = rng.uniform([-4.5, -0.5, -4.5], [4.5, 3.5, 4.5], size=(16000, 3))
+    d = rng.normal(size=(16000, 3))
+    d[::5, 1:] = 0.0
+    d[1::5, ::2] = 0.0
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.hstack([o, d])
+    for depth in (0, 2, 5):
+        fast, _ = w.color_at_batch(rays, depth, want_stats=False)
+        exact, _ = w.color_at_batch(rays, depth, want_stats=True)
+        assert fast.tobytes() == exact.tobytes(), depth
+
+
+def test_other_records_only_scene_takes_fast_path(rt):
+    """A scene without diagonal spheres (only general solids) still takes the
+    fast path through the other records' hierarchy, and culls: it executes
+    far fewer record tests than the reference's loop."""
+    rng = np.random.default_rng(4)
+    w = rt.World()
+    w.add_object(rt.Plane())
+    for i in range(300):
+        s = rt.Cube() if i % 2 else rt.Sphere()
+        c = rng.uniform([-6, 0.3, -6], [6, 3, 6])
+        s.set_transform(rt.translation(*c) * rt.rotation_y(float(rng.uniform(0, 3))) * rt.scaling(0.3, 0.2, 0.25))
+        s.material.reflective = 0.4
+        w.add_object(s)
+    w.add_light(rt.PointLight(rt.Point(-10, 10, -10), rt.Color(1, 1, 1)))
+    cam = rt.Camera(96, 64, PI / 3)
+    cam.set_transform(rt.view_transform(rt.Point(0, 4, -12), rt.Point(0, 1, 0), rt.Vector(0, 1, 0)))
+    exact, st = cam.render(w, 5, want_stats=True)
+    rt._rtamd._wf_profile(w, 1, False)
+    fast, fst = cam.render(w, 5, want_stats=False)
+    p = rt._rtamd._wf_profile(w, 0, True)
+    assert p["bvh"] and p["fused"]
+    assert fast.to_numpy().tobytes() == exact.to_numpy().tobytes()
+    # executed record tests (closest-hit + shadow) against the reference's every-shape loop
+    executed = sum(p["tests"].values())
+    reference = (st["rays_primary"] + st["rays_reflect"] + st["rays_refract"] + st["rays_shadow"]) * 300
+    assert executed < reference / 10
