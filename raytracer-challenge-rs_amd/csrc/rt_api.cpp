@@ -358,6 +358,7 @@ int rtamd_tuning_set(const char* key, int value) {
     rtamd::g_wf_image = value;
     return RT_OK;
   }
+
   if (key && std::strcmp(key, "shadow_stream") == 0) {
     if (value < 0 || value > 2) return fail(RT_ERR_INVALID_ARGUMENT, "shadow_stream must be 0, 1 or 2");
     rtamd::g_wf_shadow_stream = value;
@@ -597,6 +598,7 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   // come from `meta`, so the order changes no result)
   int bvh_depth = 0;
   std::vector<BvhNode> bvh = build_sphere_bvh(diag, g_bvh_leaf, &bvh_depth, g_bvh_ct / 100.0);
+  const std::vector<BvhPair> bvh_pair = pair_layout(bvh);
   // ... and over the other bounded records (general spheres, cubes, cylinders
   // with finite caps); the rest stays exhaustive on the fast path too
   std::vector<OtherRec> orec;
@@ -646,7 +648,8 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   const size_t o_pl = align(o_gen + (gen.size() + 1) * sizeof(SphereGen));
   const size_t o_qd = align(o_pl + (planes.size() + 1) * sizeof(PlaneRec));
   const size_t o_bv = align(o_qd + (quads.size() + 1) * sizeof(QuadRec));
-  const size_t o_ob = align(o_bv + (bvh.size() + 1) * sizeof(BvhNode));
+  const size_t o_bp = align(o_bv + (bvh.size() + 1) * sizeof(BvhNode));
+  const size_t o_ob = align(o_bp + (bvh_pair.size() + 1) * sizeof(BvhPair));
   const size_t o_or = align(o_ob + (obvh.size() + 1) * sizeof(BvhNode));
   const size_t o_fg = align(o_or + (orec.size() + 1) * sizeof(OtherRec));
   const size_t o_fq = align(o_fg + (fx_gen.size() + 1) * sizeof(SphereGen));
@@ -663,6 +666,7 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   if (!planes.empty()) std::memcpy(&host[o_pl], planes.data(), planes.size() * sizeof(PlaneRec));
   if (!quads.empty()) std::memcpy(&host[o_qd], quads.data(), quads.size() * sizeof(QuadRec));
   if (!bvh.empty()) std::memcpy(&host[o_bv], bvh.data(), bvh.size() * sizeof(BvhNode));
+  if (!bvh_pair.empty()) std::memcpy(&host[o_bp], bvh_pair.data(), bvh_pair.size() * sizeof(BvhPair));
   if (!obvh.empty()) std::memcpy(&host[o_ob], obvh.data(), obvh.size() * sizeof(BvhNode));
   if (!orec.empty()) std::memcpy(&host[o_or], orec.data(), orec.size() * sizeof(OtherRec));
   if (!fx_gen.empty()) std::memcpy(&host[o_fg], fx_gen.data(), fx_gen.size() * sizeof(SphereGen));
@@ -697,6 +701,7 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   s->dev.planes = (const PlaneRec*)(b + o_pl);
   s->dev.quads = (const QuadRec*)(b + o_qd);
   s->dev.bvh = bvh.empty() ? nullptr : (const BvhNode*)(b + o_bv);
+  s->dev.bvh_pair = bvh.empty() ? nullptr : (const BvhPair*)(b + o_bp);
   s->dev.n_bvh = (int32_t)bvh.size();
   s->dev.bvh_depth = bvh_depth;
   s->dev.obvh = obvh.empty() ? nullptr : (const BvhNode*)(b + o_ob);

@@ -292,6 +292,19 @@ std::vector<BvhNode> build_sphere_bvh(std::vector<SphereDiag>& spheres, int leaf
   return nodes;
 }
 
+std::vector<BvhPair> pair_layout(const std::vector<BvhNode>& nodes) {
+  std::vector<BvhPair> out(nodes.size());
+  for (size_t i = 0; i < nodes.size(); ++i) {
+    const BvhNode& g = nodes[i];
+    BvhPair& q = out[i];
+    for (int a = 0; a < 3; ++a) {
+      q.b[4 * a] = g.lo[0][a]; q.b[4 * a + 1] = g.lo[1][a]; q.b[4 * a + 2] = g.hi[0][a]; q.b[4 * a + 3] = g.hi[1][a];
+    }
+    q.child[0] = g.child[0]; q.child[1] = g.child[1]; q.axis = g.axis; q.pad = 0;
+  }
+  return out;
+}
+
 bool other_box(const OtherRec& r, double lo[3], double hi[3]) {
   // cones stay exhaustive: their a ~ 0 branch pushes t = -c / 2.0 * b
   // (cone.rs:104), a root that need not lie on the cone at all

@@ -19,6 +19,9 @@ namespace rtamd {
 std::vector<BvhNode> build_sphere_bvh(std::vector<SphereDiag>& spheres, int leaf_size, int* depth = nullptr,
                                       double trav_cost = 1.0);
 
+// The nodes in the pair layout of the per-lane traversal (rt_layout.hpp BvhPair).
+std::vector<BvhPair> pair_layout(const std::vector<BvhNode>& nodes);
+
 // The other bounded records (general-transform spheres, cubes, cylinders
 // with finite caps; rt_layout.hpp OtherRec): other_box gives the padded
 // world box of one (false when the record must stay exhaustive: a cone, an

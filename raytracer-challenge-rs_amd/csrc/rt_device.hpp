@@ -468,8 +468,18 @@ __device__ __forceinline__ V3 lighting(const ShadeRec& m, cLightRec L, V3 point,
     const V3 reflectv = vreflect(vneg(lightv), normal);
     const double reflect_dot_eye = vdot(reflectv, eyev);
     if (!(reflect_dot_eye <= 0.0)) {
-      const double factor = spec_pow(reflect_dot_eye, m.shininess);
-      specular = vscale(vscale(intensity, m.specular), factor);
+      // A material without specular (e.g. the C3/C5 floors): (I * 0) * f equals
+      // I * 0 bit for bit whenever f = pow(x, y) is finite and not -0, which holds
+      // for 0 < x <= 1 and 0 <= y < inf (f in [0, 1]); then pow need not run.
+      const bool no_spec = m.specular == 0.0 && reflect_dot_eye <= 1.0 && m.shininess >= 0.0 &&
+                           m.shininess < INFINITY && fabs(intensity.x) < INFINITY &&
+                           fabs(intensity.y) < INFINITY && fabs(intensity.z) < INFINITY;
+      if (no_spec) {
+        specular = vscale(intensity, m.specular);
+      } else {
+        const double factor = spec_pow(reflect_dot_eye, m.shininess);
+        specular = vscale(vscale(intensity, m.specular), factor);
+      }
     }
   }
   return vadd(vadd(ambient, diffuse), specular);

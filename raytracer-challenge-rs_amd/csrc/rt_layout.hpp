@@ -60,6 +60,17 @@ struct alignas(64) BvhNode {
   uint32_t pad;
 };
 static_assert(sizeof(BvhNode) == 64, "BvhNode must stay 64 B");
+// The same node in the pair layout the per-lane traversal reads
+// (lane_trace_pair): per axis a, b[4a..4a+3] = lo[0][a], lo[1][a], hi[0][a],
+// hi[1][a], so the two children's entry (or exit) planes on an axis are one
+// 8-B pair, chosen by the sign of the ray's direction.
+struct alignas(64) BvhPair {
+  float b[12];
+  int32_t child[2];
+  int32_t axis;
+  uint32_t pad;
+};
+static_assert(sizeof(BvhPair) == 64, "BvhPair must stay 64 B");
 // A culled record other than a diagonal sphere: the QuadRec layout, with
 // kind 0 = sphere under a general inverse (rows 0-2 in m).
 typedef QuadRec OtherRec;
@@ -128,6 +139,7 @@ struct DevScene {
   const LightRec* lights;
   const QuadRec* quads;
   const BvhNode* bvh;  // nullptr when the scene has no BVH
+  const BvhPair* bvh_pair;  // the same nodes in the pair layout
   int32_t n_diag, n_gen, n_planes, n_objects, n_lights;
   int32_t n_quads;
   int32_t n_bvh;

@@ -919,21 +919,13 @@ __device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, const WfArgs
   LaneScene ls{(const unsigned char*)sc.bvh, sc.sph_diag, sc.lb_delta, static_stack, {0.f, 0.f, 0.f}};
   unsigned char* p = dyn;
   if constexpr (LANE == 14) {
-    // pair layout: per axis, the two children's lower bounds form one 8-B pair
-    // and their upper bounds the next (lane_trace_pair)
+    // pair layout (BvhPair): per axis, the two children's lower bounds form one
+    // 8-B pair and their upper bounds the next (lane_trace_pair)
     ls.stack = (int*)dyn + threadIdx.x;
     p += lane_stack_bytes(sc.bvh_depth + 1);
-    for (int i = threadIdx.x; i < sc.n_bvh; i += blockDim.x) {
-      const BvhNode& g = sc.bvh[i];
-      float* q = (float*)(p + (size_t)i * 64);
-      for (int ax = 0; ax < 3; ++ax) {
-        q[4 * ax] = g.lo[0][ax]; q[4 * ax + 1] = g.lo[1][ax]; q[4 * ax + 2] = g.hi[0][ax]; q[4 * ax + 3] = g.hi[1][ax];
-      }
-      int* c = (int*)(q + 12);
-      c[0] = g.child[0]; c[1] = g.child[1]; c[2] = g.axis; c[3] = 0;
-    }
+    stage_lds((uint4*)p, (const uint4*)sc.bvh_pair, sc.n_bvh * (int)(sizeof(BvhPair) / 16));
     ls.nodes = p;
-    p += (size_t)sc.n_bvh * sizeof(BvhNode);
+    p += (size_t)sc.n_bvh * sizeof(BvhPair);
   }
   if (LANE == 14 || (LANE == 0 && (a.lds_flags & kLdsSpheres))) {
     stage_lds((uint4*)p, (const uint4*)sc.sph_diag, sc.n_diag * (int)(sizeof(SphereDiag) / 16));
@@ -1153,8 +1145,12 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
     if (a.skip_shadow && shadow_irrelevant(*m, Lr, sdir, c.normal, term)) {
       // the light is behind the surface: lighting() is the ambient term either way
     } else {
+#ifdef RTAMD_EXP_NOSHADOW  // experiment build (dev, wrong images): the cost of the shadow rays
+      const bool shadowed = false;
+#else
       const bool shadowed = shadow_trace<LANE, QUADS>(sc, a, ls, l, c.over, sdir, dist, t.sh_disc, t.sh_tests,
                                                       t.sh_boxes);
+#endif
       ++t.sh_rays;
       term = lighting(*m, Lr, c.over, c.eyev, c.normal, shadowed, sdir);
     }
