@@ -232,20 +232,31 @@ __device__ __forceinline__ bool shadow_irrelevant(const ShadeRec& m, cLightRec L
 // Per diagonal sphere: s (inverse diagonal), o' = s*o + t for the camera origin
 // o, and c = o'.o' - 1 — the same operations the general test performs, so the
 // values are bit-identical to what each primary ray would compute.
-__global__ void wf_prim_prep(DevScene sc, DevCamera cam, PrimRec* prim) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= sc.n_diag + 4) return;
-  PrimRec p{};
-  if (j < sc.n_diag) {
-    const V3 o = m34_point(cam.inv, v3(0.0, 0.0, 0.0));  // camera.rs:65
-    const SphereDiag& r = sc.sph_diag[j];
-    p.s[0] = r.s[0]; p.s[1] = r.s[1]; p.s[2] = r.s[2];
-    p.op[0] = r.s[0] * o.x + r.t[0];
-    p.op[1] = r.s[1] * o.y + r.t[1];
-    p.op[2] = r.s[2] * o.z + r.t[2];
-    p.c = p.op[0] * p.op[0] + p.op[1] * p.op[1] + p.op[2] * p.op[2] - 1.0;
+// The frame's first launch: zero the work counters and the queue counters of
+// this workspace (n_a and n_b 16-B words) and, for a camera frame, write the
+// primary records (wf_prim_prep's computation). One launch instead of two
+// fills and a kernel.
+__global__ void wf_frame_init(DevScene sc, DevCamera cam, PrimRec* prim, unsigned do_prim, uint4* zero_a,
+                              unsigned n_a, uint4* zero_b, unsigned n_b) {
+  const unsigned stride = gridDim.x * blockDim.x;
+  const unsigned i0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+  for (unsigned i = i0; i < n_a; i += stride) zero_a[i] = z;
+  for (unsigned i = i0; i < n_b; i += stride) zero_b[i] = z;
+  if (!do_prim) return;
+  const V3 o = m34_point(cam.inv, v3(0.0, 0.0, 0.0));  // camera.rs:65
+  for (unsigned j = i0; j < (unsigned)sc.n_diag + 4; j += stride) {
+    PrimRec p{};
+    if (j < (unsigned)sc.n_diag) {
+      const SphereDiag& r = sc.sph_diag[j];
+      p.s[0] = r.s[0]; p.s[1] = r.s[1]; p.s[2] = r.s[2];
+      p.op[0] = r.s[0] * o.x + r.t[0];
+      p.op[1] = r.s[1] * o.y + r.t[1];
+      p.op[2] = r.s[2] * o.z + r.t[2];
+      p.c = p.op[0] * p.op[0] + p.op[1] * p.op[1] + p.op[2] * p.op[2] - 1.0;
+    }
+    prim[j] = p;  // j >= n_diag: zero padding records
   }
-  prim[j] = p;  // j >= n_diag: zero padding records
 }
 
 // LDS image for the trace kernels: [diag or prim records][gen][planes][metas]
@@ -1283,6 +1294,30 @@ __global__ __launch_bounds__(kWfBlock) void wf_prep(DevScene sc, DevCamera cam, 
   }
 }
 
+// Device-side check of a calibrated frame: every generation's queue counts
+// (the sharded region counters the trace kernels appended to) must equal the
+// launch sizes the host took from its calibration cache. A mismatch would mean
+// rays were left untraced; it raises the host-mapped fault flag, which the
+// library reports as RT_ERR_HIP on the next call (Wavefront::fault).
+struct WfCheckArgs {
+  unsigned n_gen;              // generations 0 .. n_gen-1 were launched
+  unsigned rays[kMaxGen];      // expected ray count of generation g (g >= 1)
+  unsigned shadows[kMaxGen];   // expected shadow-list length of generation g
+};
+// one wave (threads 0..63 of a block)
+__device__ __forceinline__ void check_counts_wave(const unsigned* shard_base, const WfCheckArgs& c, int* fault) {
+  for (unsigned g = threadIdx.x; g <= c.n_gen && g < (unsigned)kMaxGen; g += 64) {
+    const unsigned* r = shard_base + ((size_t)g * 2 + 0) * kShards * kShardStride;
+    const unsigned* q = shard_base + ((size_t)g * 2 + 1) * kShards * kShardStride;
+    unsigned nr = 0, ns = 0;
+    for (int k = 0; k < kShards; ++k) {
+      nr += r[k * kShardStride];
+      ns += q[k * kShardStride];
+    }
+    const bool bad = (g >= 1 && nr != c.rays[g]) || (g < c.n_gen && ns != c.shadows[g]);
+    if (bad) *fault = 1;
+  }
+}
 // ---------------------------------------------------------- combine
 // World::shade_hit (world.rs:40-68) from the node, the shadow flags and the
 // children's colours; color_at miss -> black (world.rs:74-75).
@@ -1333,7 +1368,12 @@ __global__ __launch_bounds__(kWfBlock) void wf_combine(DevScene sc, DevCamera ca
 // node of generation g that has a reflected or refracted child, from its
 // ParentRec (surface term, Schlick factor) and the children's colours, which
 // generation g+1 wrote (directly or through this pass).
-__global__ __launch_bounds__(kWfBlock) void wf_combine_parents(DevScene sc, DevCamera cam, WfArgs a) {
+__global__ __launch_bounds__(kWfBlock) void wf_combine_parents(DevScene sc, DevCamera cam, WfArgs a,
+                                                                WfCheckArgs ck, const unsigned* shard_base,
+                                                                int* fault) {
+  // the first combine launch of a calibrated frame also runs the queue check
+  // (wf_check_counts): every trace launch of the frame precedes it
+  if (fault && blockIdx.x == 0 && threadIdx.x < 64) check_counts_wave(shard_base, ck, fault);
   const unsigned stride = gridDim.x * blockDim.x;
   __shared__ unsigned s_pre[kShards + 1];
   const unsigned* pre = shard_prefix(a.sh_cnt, s_pre);
@@ -1395,28 +1435,9 @@ __global__ void wf_count_kinds(WfArgs a) {
   }
 }
 
-// Device-side check of a calibrated frame: every generation's queue counts
-// (the sharded region counters the trace kernels appended to) must equal the
-// launch sizes the host took from its calibration cache. A mismatch would mean
-// rays were left untraced; it raises the host-mapped fault flag, which the
-// library reports as RT_ERR_HIP on the next call (Wavefront::fault).
-struct WfCheckArgs {
-  unsigned n_gen;              // generations 0 .. n_gen-1 were launched
-  unsigned rays[kMaxGen];      // expected ray count of generation g (g >= 1)
-  unsigned shadows[kMaxGen];   // expected shadow-list length of generation g
-};
+// the check alone (frames without a parents combine, the exhaustive pipeline)
 __global__ void wf_check_counts(const unsigned* shard_base, WfCheckArgs c, int* fault) {
-  for (unsigned g = threadIdx.x; g <= c.n_gen && g < (unsigned)kMaxGen; g += blockDim.x) {
-    const unsigned* r = shard_base + ((size_t)g * 2 + 0) * kShards * kShardStride;
-    const unsigned* q = shard_base + ((size_t)g * 2 + 1) * kShards * kShardStride;
-    unsigned nr = 0, ns = 0;
-    for (int k = 0; k < kShards; ++k) {
-      nr += r[k * kShardStride];
-      ns += q[k * kShardStride];
-    }
-    const bool bad = (g >= 1 && nr != c.rays[g]) || (g < c.n_gen && ns != c.shadows[g]);
-    if (bad) *fault = 1;
-  }
+  if (threadIdx.x < 64) check_counts_wave(shard_base, c, fault);
 }
 
 // ---------------------------------------------------------- host side
@@ -1718,9 +1739,7 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
   counts.shadows.resize(max_depth + 2, 0);
   counts.rays[0] = n0;
 
-  WF_CHECK(hipMemsetAsync(d_cnt_, 0, sizeof(WfCounters), stream));
-  WF_CHECK(hipMemsetAsync(d_shard_, 0, (size_t)(max_depth + 2) * 2 * kShards * kShardStride * sizeof(unsigned),
-                          stream));
+
   WF_CHECK(ensure_gen(0, n0, L, 0, fused));
   if (!camera_mode) {
     // batch rays: n0 x 6 doubles -> WfRay queue of generation 0
@@ -1732,8 +1751,13 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
   last_bvh_ = bvh;
   last_fused_ = fused;
   const bool use_prim = camera_mode && (prim_lds || bvh) && sc.n_diag > 0;
-  if (use_prim) {
-    WF_LAUNCH(wf_prim_prep, dim3((sc.n_diag + 4 + 255) / 256), dim3(256), 0, stream, sc, cam, d_prim_);
+  {  // counters zeroed and the primary records written by one launch
+    static_assert(sizeof(WfCounters) % 16 == 0, "WfCounters is zeroed in 16-B words");
+    const unsigned n_a = (unsigned)(sizeof(WfCounters) / 16);
+    const unsigned n_b = (unsigned)((size_t)(max_depth + 2) * 2 * kShards * kShardStride * sizeof(unsigned) / 16);
+    const unsigned work = std::max<unsigned>(std::max(n_a, n_b), use_prim ? (unsigned)sc.n_diag + 4 : 0u);
+    WF_LAUNCH(wf_frame_init, dim3(std::min<unsigned>((work + 255) / 256, 256u)), dim3(256), 0, stream, sc, cam,
+              d_prim_, use_prim ? 1u : 0u, (uint4*)d_cnt_, n_a, (uint4*)d_shard_, n_b);
     WF_CHECK(hipGetLastError());
   }
   // Exhaustive pipeline: shadow traces of generation g depend only on
@@ -1846,15 +1870,16 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
       WF_CHECK(hipGetLastError());
     }
   }
-  if (calibrated) {  // the queues must hold exactly what was launched
-    WfCheckArgs ck{};
+  // the queues must hold exactly what was launched (calibrated frames): checked
+  // by the first parents combine, or by a launch of its own
+  WfCheckArgs ck{};
+  bool check_pending = calibrated;
+  if (calibrated) {
     ck.n_gen = last + 1;
     for (unsigned g = 0; g <= last + 1 && g < (unsigned)kMaxGen; ++g) {
       ck.rays[g] = g < counts.rays.size() ? counts.rays[g] : 0;
       ck.shadows[g] = g < counts.shadows.size() ? counts.shadows[g] : 0;
     }
-    WF_LAUNCH(wf_check_counts, dim3(1), dim3(64), 0, stream, d_shard_, ck, d_fault_);
-    WF_CHECK(hipGetLastError());
   }
   if (forked) {  // join: the combine pass reads every generation's lighting terms
     WF_CHECK(hipEventRecord(join_ev_, sh_stream));
@@ -1881,13 +1906,18 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     WF_CHECK(pmark(stream, WF_COMBINE, true));
     if (fused) {
       WF_LAUNCH(wf_combine_parents, dim3(occupancy_grid(wf_combine_parents, kWfBlock, 0, a.n)), dim3(kWfBlock), 0,
-                stream, sc, cam, a);
+                stream, sc, cam, a, ck, d_shard_, check_pending ? d_fault_ : nullptr);
+      check_pending = false;
     } else {
       WF_LAUNCH(wf_combine, dim3(occupancy_grid(wf_combine, kWfBlock, 0, a.n)), dim3(kWfBlock), 0, stream, sc,
                 cam, a);
     }
     WF_CHECK(hipGetLastError());
     WF_CHECK(pmark(stream, WF_COMBINE, false));
+  }
+  if (check_pending) {
+    WF_LAUNCH(wf_check_counts, dim3(1), dim3(64), 0, stream, d_shard_, ck, d_fault_);
+    WF_CHECK(hipGetLastError());
   }
   if (averaged) {
     const unsigned n_pix = n0 / aa;

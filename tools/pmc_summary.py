@@ -4,7 +4,7 @@ Usage: pmc_summary.py OUT.json [--width W --height H --spheres S --n-gpus N
        --dominant CLASS] DIR [DIR ...]
 Each DIR holds one --pmc pass (*_counter_collection.csv). Counters are summed
 over all dispatches of a kernel class and divided by the number of frames
-(= wf_prim_prep dispatches, one per rendered frame), i.e. per-FRAME values of
+(= wf_frame_init dispatches, one per rendered frame), i.e. per-FRAME values of
 that class's launches — the same unit as bench.py's roofline.
 
 HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE (KiB) under-reports a
@@ -20,7 +20,7 @@ def _targs(n, name):
 
 def klass(n):
     """Kernel class of a demangled name: primary / closest / shadow / prep /
-    combine / frame (wf_prim_prep: one per rendered frame)."""
+    combine / frame (wf_frame_init: one per rendered frame)."""
     if "wf_trace_fused<" in n:  # fused generation: closest hit + shading + shadow rays + spawn
         return "primary" if _targs(n, "wf_trace_fused")[0] == "true" else "closest"
     if "wf_trace_closest_bvh<" in n:
@@ -33,7 +33,7 @@ def klass(n):
         return "prep"
     if "wf_combine(" in n or "wf_combine_parents(" in n or "wf_average(" in n:
         return "combine"
-    if "wf_prim_prep(" in n:
+    if "wf_frame_init(" in n or "wf_prim_prep(" in n:
         return "frame"
     return None
 

@@ -1,6 +1,6 @@
 """Render N frames of the bench workload on the fast path only (no counted
 frame), for rocprofv3 kernel-trace / PMC passes (dev tool). Per-frame
-figures = totals / N (tools/pmc_summary.py divides by the wf_prim_prep
+figures = totals / N (tools/pmc_summary.py divides by the wf_frame_init
 count, one per frame)."""
 import argparse
 import os
