@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 /* ---- status codes ------------------------------------------------------ */
 enum {
@@ -264,6 +264,25 @@ int rt_render_multi(rt_scene* const* scenes, int n_devices,
  * with out == NULL) is returned. No terminating NUL is written. */
 int rt_canvas_to_ppm(const double* rgb, uint32_t width, uint32_t height,
                      char* out, size_t cap, size_t* out_len);
+
+/* `canvas_to_ppm` (image/ppm.rs:24-51) of a DEVICE canvas (rows x width x 3
+ * f64, row-major, as rt_render_shard_device writes it) into DEVICE memory
+ * `d_out` (cap bytes), on `stream` (NULL = the default stream). The bytes are
+ * those rt_canvas_to_ppm writes. *out_len receives the text's length (d_out ==
+ * NULL: the length only); a buffer of 12 * width * height + height + 32 bytes
+ * always suffices. Returns after the text is complete. width <= 12288. */
+int rt_canvas_to_ppm_device(const double* d_rgb, uint32_t width, uint32_t height,
+                            char* d_out, size_t cap, size_t* out_len, void* stream);
+
+/* `canvas_to_ppm(&camera.render(&world))` (camera.rs:133-148 then
+ * image/ppm.rs:24-51; the render_scene / demo-binary output path) in one call:
+ * the frame is rendered, encoded on the device and only the PPM text crosses
+ * to the host buffer `out` (cap bytes). *out_len receives the text's length;
+ * out == NULL asks for the length only (the frame is still rendered), and a
+ * too-small cap returns RT_ERR_BUFFER_TOO_SMALL. hsize <= 12288. */
+int rt_render_ppm(const rt_scene* scene, const rt_camera_desc* camera,
+                  uint32_t max_depth, uint32_t aa_samples, char* out, size_t cap,
+                  size_t* out_len, rt_stats* stats);
 
 /* `scale_color_component` (image/ppm.rs:73-75) over n values. */
 int rt_quantize_u8(const double* values, size_t n, uint8_t* out);

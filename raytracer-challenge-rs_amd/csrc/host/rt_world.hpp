@@ -314,6 +314,18 @@ class Camera {
           "rt_render_aa");
     return c;
   }
+  // canvas_to_ppm(&self.render(world)) (camera.rs:133-148, image/ppm.rs:24-51), encoded
+  // on the device; aa_samples > 1 renders as render_multithreaded does.
+  std::string render_ppm(const World& world, unsigned max_depth = 5, unsigned aa_samples = 1,
+                         rt_stats* stats = nullptr) const {
+    const size_t bound = 32 + (size_t)12 * desc_.hsize * desc_.vsize + desc_.vsize;
+    std::string s(bound, '\0');
+    size_t len = 0;
+    check(rt_render_ppm(world.scene(), &desc_, max_depth, aa_samples, &s[0], s.size(), &len, stats),
+          "rt_render_ppm");
+    s.resize(len);
+    return s;
+  }
   RenderOpts render_opts;
 
  private:

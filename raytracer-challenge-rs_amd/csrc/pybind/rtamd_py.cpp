@@ -249,6 +249,18 @@ PYBIND11_MODULE(_rtamd, m) {
     check(rt_canvas_to_ppm(rgb.data(), w, h, &s[0], len, &len), "rt_canvas_to_ppm");
     return py::bytes(s);
   });
+  // canvas_to_ppm of a device canvas into a device buffer (pointers as integers, e.g.
+  // torch tensors' data_ptr()); returns the text's length
+  m.def("canvas_to_ppm_device", [](uintptr_t d_rgb, uint32_t w, uint32_t h, uintptr_t d_out, size_t cap,
+                                   uintptr_t stream) {
+    size_t len = 0;
+    {
+      py::gil_scoped_release nogil;
+      check(rt_canvas_to_ppm_device((const double*)d_rgb, w, h, (char*)d_out, cap, &len, (void*)stream),
+            "rt_canvas_to_ppm_device");
+    }
+    return len;
+  }, py::arg("d_rgb"), py::arg("width"), py::arg("height"), py::arg("d_out"), py::arg("cap"), py::arg("stream") = 0);
   m.def("quantize_u8", [](py::array_t<double, py::array::c_style | py::array::forcecast> v) {
     py::array_t<uint8_t> o(v.size());
     check(rt_quantize_u8(v.data(), (size_t)v.size(), o.mutable_data()), "rt_quantize_u8");
@@ -335,6 +347,15 @@ PYBIND11_MODULE(_rtamd, m) {
         }
         return py::make_tuple(std::unique_ptr<Canvas>(out), stats_dict(st));
       }, py::arg("world"), py::arg("max_depth") = 5, py::arg("want_stats") = true, py::arg("exhaustive") = py::none())
+      .def("render_ppm", [](const Camera& c, const World& w, unsigned max_depth, unsigned aa_samples, bool want_stats) {
+        rt_stats st{};
+        std::string out;
+        {
+          py::gil_scoped_release nogil;
+          out = c.render_ppm(w, max_depth, aa_samples, want_stats ? &st : nullptr);
+        }
+        return py::make_tuple(py::bytes(out), stats_dict(st));
+      }, py::arg("world"), py::arg("max_depth") = 5, py::arg("aa_samples") = 1, py::arg("want_stats") = false)
       .def_readwrite("render_opts", &Camera::render_opts, py::return_value_policy::reference_internal)
       .def("render_multithreaded", [](const Camera& c, const World& w, unsigned max_depth, bool want_stats,
                                       py::object exhaustive) {

@@ -24,6 +24,7 @@
 #include "rt_bvh.hpp"
 #include "rt_kernels.hpp"
 #include "rt_layout.hpp"
+#include "rt_ppm_dev.hpp"
 #include "rt_wavefront.hpp"
 
 using namespace rtamd;
@@ -58,6 +59,14 @@ struct rt_scene {
   size_t out_cap = 0;           // doubles
   double* d_in = nullptr;       // cached input for batch entry points
   size_t in_cap = 0;
+  // rt_render_ppm: the device PPM text and its row lengths / offsets
+  char* d_ppm = nullptr;
+  size_t ppm_cap = 0;
+  void* d_ppm_rows = nullptr;
+  size_t ppm_rows_cap = 0;  // rows
+  // device-to-host copies into caller memory go through two pinned chunks
+  void* h_stage[2] = {nullptr, nullptr};
+  hipEvent_t stage_ev[2] = {nullptr, nullptr};
   hipStream_t stream = nullptr;
   std::mutex mu;  // one host call at a time per scene (the workspace pool)
   // Wavefront workspaces (queues grow on demand), one per stream in use, at
@@ -101,6 +110,10 @@ struct rt_scene {
   ~rt_scene() {
     for (WfSlot& w : wfs)
       if (w.done) (void)hipEventDestroy(w.done);
+    for (int k = 0; k < 2; ++k) {
+      if (h_stage[k]) (void)hipHostFree(h_stage[k]);
+      if (stage_ev[k]) (void)hipEventDestroy(stage_ev[k]);
+    }
   }
   // the workspace for a render on `st` (stream-ordered after its previous user)
   hipError_t acquire(hipStream_t st, WfSlot** out) {
@@ -198,6 +211,45 @@ int ensure_dev_buffer(double** buf, size_t* cap, size_t need) {
   RT_HIP(hipMalloc(buf, std::max<size_t>(need, 1) * sizeof(double)));
   *cap = need;
   return RT_OK;
+}
+
+// Device-to-host copy of n bytes into caller (pageable) memory, stream-ordered
+// after the work already on `st`: chunks land in two pinned buffers by DMA
+// while the host copies the previous chunk out (a pageable hipMemcpy of a
+// 50 MB canvas stages through the runtime at a few GB/s). Synchronous.
+constexpr size_t kStageChunk = (size_t)8 << 20;
+int copy_to_host(rt_scene* s, void* dst, const void* src, size_t n, hipStream_t st) {
+  if (n == 0) return RT_OK;
+  for (int k = 0; k < 2; ++k) {
+    if (!s->h_stage[k]) RT_HIP(hipHostMalloc(&s->h_stage[k], kStageChunk, hipHostMallocDefault));
+    if (!s->stage_ev[k]) RT_HIP(hipEventCreateWithFlags(&s->stage_ev[k], hipEventDisableTiming));
+  }
+  const size_t n_chunks = (n + kStageChunk - 1) / kStageChunk;
+  auto len = [&](size_t c) { return std::min(kStageChunk, n - c * kStageChunk); };
+  auto drain = [&](size_t c) -> int {
+    RT_HIP(hipEventSynchronize(s->stage_ev[c & 1]));
+    std::memcpy((char*)dst + c * kStageChunk, s->h_stage[c & 1], len(c));
+    return RT_OK;
+  };
+  for (size_t c = 0; c < n_chunks; ++c) {
+    if (c >= 2) {
+      int rc = drain(c - 2);
+      if (rc != RT_OK) return rc;
+    }
+    RT_HIP(hipMemcpyAsync(s->h_stage[c & 1], (const char*)src + c * kStageChunk, len(c), hipMemcpyDeviceToHost, st));
+    RT_HIP(hipEventRecord(s->stage_ev[c & 1], st));
+  }
+  for (size_t c = n_chunks >= 2 ? n_chunks - 2 : 0; c < n_chunks; ++c) {
+    int rc = drain(c);
+    if (rc != RT_OK) return rc;
+  }
+  return RT_OK;
+}
+
+PpmHeader ppm_header(uint32_t w, uint32_t h) {  // image/ppm.rs:53-63
+  PpmHeader hd{};
+  hd.n = (unsigned)std::snprintf(hd.s, sizeof hd.s, "P3\n%u %u\n255\n", w, h);
+  return hd;
 }
 
 DevCamera to_dev_camera(const rt_camera_desc& c) {
@@ -742,6 +794,8 @@ void rt_scene_destroy(rt_scene* s) {
   if (s->d_blob) (void)hipFree(s->d_blob);
   if (s->d_out) (void)hipFree(s->d_out);
   if (s->d_in) (void)hipFree(s->d_in);
+  if (s->d_ppm) (void)hipFree(s->d_ppm);
+  if (s->d_ppm_rows) (void)hipFree(s->d_ppm_rows);
   if (s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
 }
@@ -811,11 +865,90 @@ int rt_render_ex(const rt_scene* scene, const rt_camera_desc* camera, uint32_t m
   rc = run_render(s, to_dev_camera(*camera), nullptr, (uint32_t)(n_pix * aa_samples), aa_samples, max_depth,
                   camera->vsize, 0, 1, s->d_out, s->stream, stats ? &ds : nullptr, &ms, flags);
   if (rc != RT_OK) return rc;
-  RT_HIP(hipMemcpyAsync(out_rgb, s->d_out, n_pix * 3 * sizeof(double), hipMemcpyDeviceToHost, s->stream));
-  RT_HIP(hipStreamSynchronize(s->stream));
+  if ((rc = copy_to_host(s, out_rgb, s->d_out, n_pix * 3 * sizeof(double), s->stream)) != RT_OK) return rc;
   if ((rc = check_faults(s)) != RT_OK) return rc;
   if (stats)
     fill_stats(stats, ds, ms, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+  return RT_OK;
+}
+
+int rt_render_ppm(const rt_scene* scene, const rt_camera_desc* camera, uint32_t max_depth, uint32_t aa_samples,
+                  char* out, size_t cap, size_t* out_len, rt_stats* stats) {
+  if (!scene || !camera || !out_len) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
+  if (camera->hsize == 0 || camera->vsize == 0) return fail(RT_ERR_INVALID_ARGUMENT, "empty camera");
+  if (!valid_aa(aa_samples)) return fail(RT_ERR_INVALID_ARGUMENT, "aa_samples must be 1, 2, 4, 8 or 16");
+  if (camera->hsize > kPpmMaxWidth)
+    return fail(RT_ERR_INVALID_ARGUMENT, "canvas wider than the device PPM encoder's row (use rt_canvas_to_ppm)");
+  rt_scene* s = const_cast<rt_scene*>(scene);
+  std::lock_guard<std::mutex> lk(s->mu);
+  auto t0 = std::chrono::steady_clock::now();
+  RT_HIP(hipSetDevice(s->device));
+  const uint32_t W = camera->hsize, H = camera->vsize;
+  const uint64_t n_pix = (uint64_t)W * H;
+  if (n_pix * aa_samples >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "canvas too large for one launch");
+  int rc = ensure_dev_buffer(&s->d_out, &s->out_cap, n_pix * 3);
+  if (rc != RT_OK) return rc;
+  const PpmHeader hd = ppm_header(W, H);
+  const size_t bound = hd.n + (size_t)12 * n_pix + H;  // <= 4 bytes per component, one '\n' per row
+  if (s->ppm_cap < bound) {
+    if (s->d_ppm) (void)hipFree(s->d_ppm);
+    s->d_ppm = nullptr;
+    s->ppm_cap = 0;
+    RT_HIP(hipMalloc(&s->d_ppm, bound));
+    s->ppm_cap = bound;
+  }
+  if (s->ppm_rows_cap < H) {
+    if (s->d_ppm_rows) (void)hipFree(s->d_ppm_rows);
+    s->d_ppm_rows = nullptr;
+    s->ppm_rows_cap = 0;
+    RT_HIP(hipMalloc(&s->d_ppm_rows, (size_t)H * 4 + ((size_t)H + 1) * 8 + 8));
+    s->ppm_rows_cap = H;
+  }
+  unsigned long long* d_off = (unsigned long long*)(((uintptr_t)s->d_ppm_rows + (size_t)H * 4 + 7) & ~(uintptr_t)7);
+  DevStats ds{};
+  float ms = 0.f;
+  rc = run_render(s, to_dev_camera(*camera), nullptr, (uint32_t)(n_pix * aa_samples), aa_samples, max_depth, H, 0,
+                  1, s->d_out, s->stream, stats ? &ds : nullptr, stats ? &ms : nullptr, 0);
+  if (rc != RT_OK) return rc;
+  RT_HIP(ppm_encode_device(s->d_out, W, H, s->d_ppm, s->ppm_cap, (unsigned*)s->d_ppm_rows, d_off, hd, s->stream));
+  unsigned long long body = 0;
+  RT_HIP(hipMemcpyAsync(&body, d_off + H, sizeof body, hipMemcpyDeviceToHost, s->stream));
+  RT_HIP(hipStreamSynchronize(s->stream));
+  if ((rc = check_faults(s)) != RT_OK) return rc;
+  *out_len = hd.n + (size_t)body;
+  if (out) {
+    if (cap < *out_len) return fail(RT_ERR_BUFFER_TOO_SMALL, "PPM buffer too small");
+    if ((rc = copy_to_host(s, out, s->d_ppm, *out_len, s->stream)) != RT_OK) return rc;
+  }
+  if (stats)
+    fill_stats(stats, ds, ms, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+  return RT_OK;
+}
+
+int rt_canvas_to_ppm_device(const double* d_rgb, uint32_t width, uint32_t height, char* d_out, size_t cap,
+                            size_t* out_len, void* stream) {
+  if (!out_len || (width && height && !d_rgb)) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
+  if (width > kPpmMaxWidth)
+    return fail(RT_ERR_INVALID_ARGUMENT, "canvas wider than the device PPM encoder's row (use rt_canvas_to_ppm)");
+  const PpmHeader hd = ppm_header(width, height);
+  if (height == 0) {  // the header alone (ppm.rs:24-27)
+    *out_len = hd.n;
+    if (d_out && cap >= hd.n) RT_HIP(hipMemcpyAsync(d_out, hd.s, hd.n, hipMemcpyHostToDevice, (hipStream_t)stream));
+    RT_HIP(hipStreamSynchronize((hipStream_t)stream));
+    return d_out && cap < hd.n ? fail(RT_ERR_BUFFER_TOO_SMALL, "PPM buffer too small") : RT_OK;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  void* rows = nullptr;
+  RT_HIP(hipMallocAsync(&rows, (size_t)height * 4 + ((size_t)height + 1) * 8 + 8, st));
+  unsigned long long* d_off = (unsigned long long*)(((uintptr_t)rows + (size_t)height * 4 + 7) & ~(uintptr_t)7);
+  hipError_t e = ppm_encode_device(d_rgb, width, height, d_out, cap, (unsigned*)rows, d_off, hd, st);
+  unsigned long long body = 0;
+  if (e == hipSuccess) e = hipMemcpyAsync(&body, d_off + height, sizeof body, hipMemcpyDeviceToHost, st);
+  (void)hipFreeAsync(rows, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("rt_canvas_to_ppm_device: ") + hipGetErrorString(e));
+  *out_len = hd.n + (size_t)body;
+  if (d_out && cap < *out_len) return fail(RT_ERR_BUFFER_TOO_SMALL, "PPM buffer too small");
   return RT_OK;
 }
 

@@ -118,6 +118,12 @@ __device__ __forceinline__ void shard_append(const WfArgs& a, unsigned q, unsign
     if (s_tot) sb = atomicAdd(a.sh_cnt + s * kShardStride, s_tot);
     if (nr + nf) rb = atomicAdd(a.out_cnt + s * kShardStride, nr + nf);
   }
+#ifdef RTAMD_EXP_ATOM2  // experiment (dev): a second, dependent round trip of returning atomics
+  if (lane == 0) {
+    const unsigned z = atomicAdd(a.out_cnt + s * kShardStride + 1 + (sb & 1u), 0u);
+    rb += (z == 0xFFFFFFFFu) ? 1u : 0u;
+  }
+#endif
   sb = (unsigned)__shfl((int)sb, 0, 64) + (incl - n_s);
   rb = (unsigned)__shfl((int)rb, 0, 64);
   const unsigned r_off = rb + (unsigned)__popcll(mr & below), f_off = rb + nr + (unsigned)__popcll(mf & below);
@@ -1076,7 +1082,15 @@ struct FusedTally {
   unsigned sh_disc = 0, sh_tests = 0, sh_boxes = 0;  // shadow-ray work
   unsigned sh_rays = 0;                              // shadow rays traced
   unsigned hits = 0, refl = 0, refr = 0;             // counted launches: shade_hit runs, children spawned
+#ifdef RTAMD_PHASE
+  unsigned long long ph[5] = {0, 0, 0, 0, 0};  // phase build: prepare, append, spawn, lights, final writes
+#endif
 };
+#ifdef RTAMD_PHASE
+#define PH_MARK(k) do { const unsigned long long pn_ = __builtin_amdgcn_s_memtime(); t.ph[k] += pn_ - ph_last; ph_last = pn_; } while (0)
+#else
+#define PH_MARK(k) do { } while (0)
+#endif
 
 // Everything after the closest hit of ray `slot` (index i of the generation):
 // prepare_computations (intersection.rs:53-105), the reflected / refracted
@@ -1090,6 +1104,9 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
                                             const Hit& h, FusedTally& t) {
   const unsigned L = (unsigned)sc.n_lights;
   const unsigned remaining = a.max_depth - a.g;
+#ifdef RTAMD_PHASE
+  unsigned long long ph_last = __builtin_amdgcn_s_memtime();
+#endif
   bool hit = false, want_refl = false, want_refr = false;
   Comps c{};
   V3 refr_dir = v3(0, 0, 0);
@@ -1114,7 +1131,9 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
   }
   const bool parent = want_refl || want_refr;
   unsigned pbase, rbase, fbase;
+  PH_MARK(0);
   shard_append(a, i / 64, parent ? 1u : 0u, want_refl, want_refr, pbase, rbase, fbase);
+  PH_MARK(1);
   if (!valid) return;
   t.hits += hit; t.refl += want_refl; t.refr += want_refr;
   double* dst = color_dst(a, cam, slot);
@@ -1145,6 +1164,7 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
       (m->reflective > 0.0 && m->transparency > 0.0) ? schlick(c.eyev, c.normal, c.n1, c.n2) : 0.0;
   // surface = Sum over the lights of lighting(..., is_shadowed(over_point, light))
   V3 surface = v3(0.0, 0.0, 0.0);  // fold from (0,0,0) (color.rs:96-103)
+  PH_MARK(2);
   for (unsigned l = 0; l < L; ++l) {
     cLightRec Lr = (cLightRec)sc.lights + l;
     // the shadow ray exactly as World::is_shadowed builds it (world.rs:95-105); its
@@ -1167,17 +1187,20 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
     }
     surface = vadd(surface, term);
   }
+  PH_MARK(3);
   if (child_refl >= 0 || child_refr >= 0) {  // the children's colours come later (wf_combine_parents)
     ParentRec pr;
     pr.surface[0] = surface.x; pr.surface[1] = surface.y; pr.surface[2] = surface.z;
     pr.schlick = schlick_r;
     pr.slot = slot; pr.obj = c.obj; pr.child_refl = child_refl; pr.child_refr = child_refr;
     if (pbase != ~0u) a.parents[pbase] = pr;
+    PH_MARK(4);
     return;
   }
   const V3 zero = v3(0.0, 0.0, 0.0);  // reflected / refracted colour: black (world.rs:108-109, 117-118)
   const V3 col = shade_color(*m, surface, zero, zero, schlick_r);
   dst[0] = col.x; dst[1] = col.y; dst[2] = col.z;
+  PH_MARK(4);
 }
 
 // One generation of the fast path (see above). PRIMARY: generation 0 of a
@@ -1230,6 +1253,20 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
         else
           lane_trace<false, LANE == 3>((const BvhNode*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, t.disc,
                                        t.tests, t.boxes, ls.stack);
+#ifdef RTAMD_EXP_TRAV2  // experiment (dev): the traversal a second time (its marginal cost)
+        {
+          Hit h2;
+          hit_init(h2);
+          trace_rest<false, QUADS, true>(sc, o, d, h2, t.disc);
+          if constexpr (LANE == 14)
+            lane_trace_pair<false>(ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h2, t.disc, t.tests, t.boxes,
+                                   ls.stack);
+          else
+            lane_trace<false, LANE == 3>((const BvhNode*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h2, t.disc,
+                                         t.tests, t.boxes, ls.stack);
+          if (h2.key != h.key) a.colors[0] = 1e300;
+        }
+#endif
       }
     }
     hit_finish(h);
@@ -1247,6 +1284,13 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
     atomicAdd(&work_row(a.cnt)->disc[a.disc_slot], ph_stage);
     atomicAdd(&work_row(a.cnt)->tests[a.disc_slot], ph_trav);
     atomicAdd(&work_row(a.cnt)->boxes[a.disc_slot], ph_prep);
+    if (a.disc_slot == WF_CLOSEST) {  // sub-phases of the shading (lane 0's view)
+      atomicAdd(&work_row(a.cnt)->disc[WF_SHADOW], t.ph[0]);
+      atomicAdd(&work_row(a.cnt)->tests[WF_SHADOW], t.ph[1]);
+      atomicAdd(&work_row(a.cnt)->boxes[WF_SHADOW], t.ph[2]);
+      atomicAdd(&work_row(a.cnt)->sh_tests[0], t.ph[3]);
+      atomicAdd(&work_row(a.cnt)->sh_rays[0], t.ph[4]);
+    }
   }
   return;
 #endif

@@ -25,7 +25,8 @@ def test_header_declares_the_boundary():
                  "rt_render_multi", "rt_color_at_batch", "rt_is_shadowed_batch", "rt_hit_batch",
                  "rt_canvas_to_ppm", "rt_quantize_u8", "rt_matrix_inverse", "rt_camera_init",
                  "rt_last_error", "rt_abi_version", "rt_device_count", "rt_shard_rows", "rt_render_aa",
-                 "rt_render_ex", "rt_render_shard_device_ex", "rt_color_at_batch_ex"):
+                 "rt_render_ex", "rt_render_shard_device_ex", "rt_color_at_batch_ex", "rt_render_ppm",
+                 "rt_canvas_to_ppm_device"):
         assert must in names
 
 
@@ -37,7 +38,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_shard_rows():
     lib = ctypes.CDLL(LIB)
-    assert lib.rt_abi_version() == 3
+    assert lib.rt_abi_version() == 4
     f = lib.rt_shard_rows
     f.restype = ctypes.c_uint32
     f.argtypes = [ctypes.c_uint32] * 4
