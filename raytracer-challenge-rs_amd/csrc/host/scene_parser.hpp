@@ -83,11 +83,14 @@ class SceneParser {
     return scene_.camera->render(*w, max_depth, stats);
   }
   // lib.rs:267-284 writes a PNG; this front-end writes the PPM (image/ppm.rs)
+  // (rendered and encoded on the device: rt_render_ppm; bytes = render(...).to_ppm())
   void render_to(const std::string& path, unsigned max_depth = 5) const {
-    Canvas c = render(max_depth);
+    if (!scene_.camera) throw SceneParserError("missing required key `camera`");
+    auto w = build_world();
+    const std::string ppm = scene_.camera->hsize() <= 12288 ? scene_.camera->render_ppm(*w, max_depth)
+                                                            : scene_.camera->render(*w, max_depth).to_ppm();
     std::ofstream f(path, std::ios::binary);
     if (!f) throw SceneParserError("cannot write `" + path + "`");
-    const std::string ppm = c.to_ppm();
     f.write(ppm.data(), (std::streamsize)ppm.size());
   }
 
