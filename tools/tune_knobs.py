@@ -1,6 +1,6 @@
 """A/B runtime tuning knobs on the C3 frame in one process, interleaved
 rounds; every variant must reproduce the first variant's image (dev tool).
-Usage: tune_knobs.py lane=0,1 wf_waves=8,4 [--c5] [--no-check]
+Usage: tune_knobs.py bvh_leaf=2,3 lb_res=128,256 [--c5] [--no-check]  (knobs: rtamd_tuning_set in rt_api.cpp)
 (--no-check: timing experiments whose images differ, e.g. exp=0,1)"""
 import itertools, os, sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
