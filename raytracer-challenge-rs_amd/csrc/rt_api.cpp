@@ -226,9 +226,24 @@ int copy_to_host(rt_scene* s, void* dst, const void* src, size_t n, hipStream_t 
   }
   const size_t n_chunks = (n + kStageChunk - 1) / kStageChunk;
   auto len = [&](size_t c) { return std::min(kStageChunk, n - c * kStageChunk); };
+  // the host side of a chunk is copied out by a few threads (one thread's memcpy into
+  // pageable memory runs well below the DMA rate)
+  const unsigned n_threads = std::max(1u, std::min(4u, std::thread::hardware_concurrency() / 2));
   auto drain = [&](size_t c) -> int {
     RT_HIP(hipEventSynchronize(s->stage_ev[c & 1]));
-    std::memcpy((char*)dst + c * kStageChunk, s->h_stage[c & 1], len(c));
+    char* d = (char*)dst + c * kStageChunk;
+    const char* src_h = (const char*)s->h_stage[c & 1];
+    const size_t n_c = len(c);
+    if (n_threads == 1 || n_c < ((size_t)1 << 20)) {
+      std::memcpy(d, src_h, n_c);
+      return RT_OK;
+    }
+    const size_t part = ((n_c + n_threads - 1) / n_threads + 4095) & ~(size_t)4095;
+    std::vector<std::thread> pool;
+    for (unsigned t = 1; t < n_threads && t * part < n_c; ++t)
+      pool.emplace_back([=] { std::memcpy(d + t * part, src_h + t * part, std::min(part, n_c - t * part)); });
+    std::memcpy(d, src_h, std::min(part, n_c));
+    for (std::thread& th : pool) th.join();
     return RT_OK;
   };
   for (size_t c = 0; c < n_chunks; ++c) {

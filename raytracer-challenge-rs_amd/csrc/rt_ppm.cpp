@@ -3,6 +3,9 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
+#include <vector>
+#include <algorithm>
 
 #include "../../include/rt_render.h"
 
@@ -36,44 +39,86 @@ int rt_quantize_u8(const double* values, size_t n, uint8_t* out) {
 
 // image/ppm.rs:24-63. Tokens are appended to the current line; before each
 // token, if line.len() + token.len() > 70 the line is flushed with its
-// trailing spaces trimmed (`trim_end`). Each canvas row ends the line.
+// trailing spaces trimmed (`trim_end`), and each canvas row ends the line.
+// Every token but the row's last is followed by exactly one space, and a flush
+// turns that one space into '\n', so a row's text is its tokens joined by one
+// separator byte each plus the final '\n' (its length does not depend on the
+// breaks), and the breaks are found afterwards: with the line starting at byte
+// ls, the last space at or before byte ls + 70 becomes '\n' whenever the row's
+// last token ends beyond ls + 70 (rt_ppm_dev.hip uses the same two facts).
+// Rows are encoded in parallel.
+}  // extern "C"
+
+namespace {
+
+size_t ppm_row_len(const double* row, uint32_t w) {
+  if (w == 0) return 1;
+  size_t n = 0;
+  for (size_t k = 0; k < (size_t)3 * w; ++k) {
+    const unsigned q = scale_color_component(row[k]);
+    n += (q >= 100 ? 3 : q >= 10 ? 2 : 1) + 1;
+  }
+  return n;
+}
+
+void ppm_row_write(const double* row, uint32_t w, char* out) {
+  char* p = out;
+  for (size_t k = 0; k < (size_t)3 * w; ++k) {
+    p += utoa3(scale_color_component(row[k]), p);
+    *p++ = (k + 1 == (size_t)3 * w) ? '\n' : ' ';
+  }
+  if (w == 0) *p++ = '\n';
+  const size_t len = (size_t)(p - out);
+  size_t ls = 0;
+  while (ls + 70 < len - 1) {
+    size_t q = ls + 70;
+    while (out[q] != ' ') --q;
+    out[q] = '\n';
+    ls = q + 1;
+  }
+}
+
+// f(r0, r1) over the rows, split across a few threads for large canvases.
+template <typename F>
+void for_rows(uint32_t height, size_t work, F f) {
+  unsigned t = std::thread::hardware_concurrency();
+  t = std::max(1u, std::min(t, 8u));
+  if (work < ((size_t)1 << 18) || t == 1 || height < 2 * t) {
+    f(0u, height);
+    return;
+  }
+  std::vector<std::thread> pool;
+  const uint32_t per = (height + t - 1) / t;
+  for (unsigned k = 1; k < t && k * per < height; ++k)
+    pool.emplace_back([=] { f(k * per, std::min(height, (k + 1) * per)); });
+  f(0u, std::min(height, per));
+  for (std::thread& th : pool) th.join();
+}
+
+}  // namespace
+
+extern "C" {
+
 int rt_canvas_to_ppm(const double* rgb, uint32_t width, uint32_t height, char* out, size_t cap,
                      size_t* out_len) {
   if (!out_len || (width && height && !rgb)) return RT_ERR_INVALID_ARGUMENT;
-  size_t len = 0;
-  auto emit = [&](const char* s, size_t n) {
-    if (out && len + n <= cap) std::memcpy(out + len, s, n);
-    len += n;
-  };
   char hdr[64];
-  int hn = std::snprintf(hdr, sizeof hdr, "P3\n%u %u\n255\n", width, height);
-  emit(hdr, (size_t)hn);
-  char line[96];
-  for (uint32_t j = 0; j < height; ++j) {
-    size_t ll = 0;
-    for (uint32_t i = 0; i < width; ++i) {
-      const double* px = rgb + ((size_t)j * width + i) * 3;
-      for (int idx = 0; idx < 3; ++idx) {
-        char tok[4];
-        const int tn = utoa3(scale_color_component(px[idx]), tok);
-        if (ll + (size_t)tn > 70) {
-          size_t tl = ll;
-          while (tl > 0 && line[tl - 1] == ' ') --tl;
-          emit(line, tl);
-          emit("\n", 1);
-          ll = 0;
-        }
-        std::memcpy(line + ll, tok, (size_t)tn);
-        ll += (size_t)tn;
-        if (idx < 2) line[ll++] = ' ';
-      }
-      if (i + 1 < width) line[ll++] = ' ';
-    }
-    emit(line, ll);
-    emit("\n", 1);
-  }
+  const size_t hn = (size_t)std::snprintf(hdr, sizeof hdr, "P3\n%u %u\n255\n", width, height);
+  const size_t row_doubles = (size_t)width * 3;
+  std::vector<size_t> off((size_t)height + 1, 0);
+  for_rows(height, row_doubles * height, [&](uint32_t r0, uint32_t r1) {
+    for (uint32_t j = r0; j < r1; ++j) off[j + 1] = ppm_row_len(rgb + j * row_doubles, width);
+  });
+  off[0] = hn;
+  for (uint32_t j = 0; j < height; ++j) off[j + 1] += off[j];
+  const size_t len = off[height];
   *out_len = len;
-  if (out && len > cap) return RT_ERR_BUFFER_TOO_SMALL;
+  if (!out) return RT_OK;
+  if (len > cap) return RT_ERR_BUFFER_TOO_SMALL;
+  std::memcpy(out, hdr, hn);
+  for_rows(height, row_doubles * height, [&](uint32_t r0, uint32_t r1) {
+    for (uint32_t j = r0; j < r1; ++j) ppm_row_write(rgb + j * row_doubles, width, out + off[j]);
+  });
   return RT_OK;
 }
 
