@@ -36,3 +36,14 @@ def test_ppm_bytes_match_oracle(rt, oracle):
             img.flat[::17] = 0.1  # exact .5 ties after scaling
             img.flat[::29] = np.nan
         assert rt.canvas_to_ppm(img) == oracle.canvas_to_ppm(img)
+
+
+def test_ppm_row_parallel_writer_matches_oracle(rt, oracle):
+    """Canvases large enough for the row-parallel host writer (threads over
+    row ranges; every token's position computed before the breaks are walked)."""
+    rng = np.random.default_rng(11)
+    vals = np.array([0.0, 1 / 255, 9 / 255, 10 / 255, 99 / 255, 100 / 255, 1.0, 0.5 / 255, np.nan, -1.0, 2.0])
+    for (h, w) in [(300, 301), (97, 1024), (1000, 71)]:
+        img = rng.choice(vals, size=(h, w, 3))
+        img[::3] = rng.uniform(-0.2, 1.3, size=img[::3].shape)
+        assert rt.canvas_to_ppm(img) == oracle.canvas_to_ppm(img)
