@@ -101,7 +101,12 @@ struct alignas(128) WfWorkRow {
   unsigned long long sh_rays[2];   // fused kernels: shadow rays traced, [0] primary / [1] secondary launches
   unsigned long long sh_tests[2];  // fused kernels: shadow sphere tests executed, per launch class
 };
+// Fused launches hand out their rays in chunks of 64 (one wave-iteration) from
+// per-XCD counters, kChunkClasses per generation, each on a 128-B line.
+constexpr int kChunkClasses = 8;
+constexpr int kChunkStride = 32;
 struct WfCounters {
+  unsigned chunk[kMaxGen * kChunkClasses * kChunkStride];
   unsigned n_refl[kMaxGen], n_refr[kMaxGen], n_hit[kMaxGen];
   WfWorkRow work[kWorkRows];
   unsigned long long disc(int c) const {
