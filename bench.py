@@ -8,7 +8,7 @@ of primary + reflection + refraction + shadow rays (each one a
 launched by torch.distributed.run) the frame is split into interleaved 8-row
 blocks, each rank renders its rows into HBM, and the canvas is assembled on
 rank 0 with one RCCL gather (strong scaling: the frame is fixed). F frames
-are in flight (--inflight, default 4 for C3, 2 for C5): consecutive frames render on F streams,
+are in flight (--inflight, default 4 for C3, 1 for C5): consecutive frames render on F streams,
 each with its own library workspace, so one frame's short, latency-bound
 deep generations overlap the next frame's work; every frame is complete,
 gathered and assembled inside the timed region.
@@ -307,7 +307,7 @@ def main():
     # their own queue, but any cross-stream wait on them costs ~1 ms.
     # default: 4 frames in flight for C3; one for C5, whose wavefront workspace
     # (16.8 M primary rays, depth 8) takes tens of GB per frame
-    F = max(1, a.inflight if a.inflight is not None else (4 if a.config == "c3" else 2))
+    F = max(1, a.inflight if a.inflight is not None else (4 if a.config == "c3" else 1))
     stream = torch.cuda.current_stream()
     kind = a.stream_kind
     if F == 1:
