@@ -118,12 +118,6 @@ __device__ __forceinline__ void shard_append(const WfArgs& a, unsigned q, unsign
     if (s_tot) sb = atomicAdd(a.sh_cnt + s * kShardStride, s_tot);
     if (nr + nf) rb = atomicAdd(a.out_cnt + s * kShardStride, nr + nf);
   }
-#ifdef RTAMD_EXP_ATOM2  // experiment (dev): a second, dependent round trip of returning atomics
-  if (lane == 0) {
-    const unsigned z = atomicAdd(a.out_cnt + s * kShardStride + 1 + (sb & 1u), 0u);
-    rb += (z == 0xFFFFFFFFu) ? 1u : 0u;
-  }
-#endif
   sb = (unsigned)__shfl((int)sb, 0, 64) + (incl - n_s);
   rb = (unsigned)__shfl((int)rb, 0, 64);
   const unsigned r_off = rb + (unsigned)__popcll(mr & below), f_off = rb + nr + (unsigned)__popcll(mf & below);
