@@ -420,6 +420,14 @@ int rtamd_tuning_set(const char* key, int value) {
     rtamd::g_wf_shadow_lb = value != 0;
     return RT_OK;
   }
+  if (key && std::strcmp(key, "treelet") == 0) {
+    rtamd::g_wf_treelet = value != 0;
+    return RT_OK;
+  }
+  if (key && std::strcmp(key, "treelet_deltas") == 0) {
+    rtamd::g_wf_treelet_deltas = value != 0;
+    return RT_OK;
+  }
   if (key && std::strcmp(key, "image") == 0) {
     if (value != 0 && value != 1 && value != 3) return fail(RT_ERR_INVALID_ARGUMENT, "image must be 0, 1 or 3");
     rtamd::g_wf_image = value;

@@ -213,6 +213,46 @@ int tree_depth(const std::vector<BvhNode>& nodes, int32_t e) {
   return 1 + std::max(tree_depth(nodes, nodes[e].child[0]), tree_depth(nodes, nodes[e].child[1]));
 }
 
+// The nodes renumbered for the treelet: the first kTreeletNodes in
+// breadth-first order (root 0, then each level in turn), so that a prefix of
+// the array is the top of the hierarchy (the global-memory image stages such a
+// prefix in LDS), then each remaining subtree in depth-first order (its nodes
+// contiguous, for the L2). The numbering changes neither the boxes nor the
+// child order, so no traversal result changes.
+constexpr size_t kTreeletNodes = 1536;
+std::vector<BvhNode> treelet_order(const std::vector<BvhNode>& in) {
+  if (in.empty()) return in;
+  std::vector<int> order;
+  order.reserve(in.size());
+  std::vector<int> queue{0};
+  size_t h = 0;
+  for (; h < queue.size() && order.size() < kTreeletNodes; ++h) {
+    order.push_back(queue[h]);
+    for (int c = 0; c < 2; ++c)
+      if (in[queue[h]].child[c] >= 0) queue.push_back(in[queue[h]].child[c]);
+  }
+  std::vector<int> stack;
+  for (; h < queue.size(); ++h) {  // the frontier's subtrees, depth-first
+    stack.assign(1, queue[h]);
+    while (!stack.empty()) {
+      const int e = stack.back();
+      stack.pop_back();
+      order.push_back(e);
+      for (int c = 1; c >= 0; --c)
+        if (in[e].child[c] >= 0) stack.push_back(in[e].child[c]);
+    }
+  }
+  std::vector<int32_t> remap(in.size(), -1);
+  for (size_t i = 0; i < order.size(); ++i) remap[order[i]] = (int32_t)i;
+  std::vector<BvhNode> out(order.size());
+  for (size_t i = 0; i < order.size(); ++i) {
+    out[i] = in[order[i]];
+    for (int c = 0; c < 2; ++c)
+      if (out[i].child[c] >= 0) out[i].child[c] = remap[out[i].child[c]];
+  }
+  return out;
+}
+
 // The hierarchy over `boxes`; `order` receives the leaf order of the items.
 std::vector<BvhNode> build_over_boxes(const std::vector<Box>& boxes, int leaf_size, double trav_cost, int* depth,
                                       std::vector<int>* order) {
@@ -243,7 +283,7 @@ std::vector<BvhNode> build_over_boxes(const std::vector<Box>& boxes, int leaf_si
   }
   if (depth) *depth = tree_depth(bd.nodes, 0);  // kBvhEmpty < 0 counts as a leaf
   *order = bd.order;
-  return bd.nodes;
+  return treelet_order(bd.nodes);
 }
 
 template <typename R>

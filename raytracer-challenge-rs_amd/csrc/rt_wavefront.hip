@@ -28,6 +28,8 @@ int g_wf_skip_shadow = 1;  // fast path: leave out shadow rays that cannot chang
 int g_wf_shadow_lb = 1;    // 1 = shadow rays through the light buffer (DESIGN.md "Light buffer")
 int g_wf_image = 0;        // tuning knob ("image", tests): 0 = the fused kernels pick their scene image,
                            // 3 / 1 = force the global-memory image with an LDS / scratch stack
+int g_wf_treelet = 1;         // tuning knob ("treelet"): the global-memory image's top nodes in LDS
+int g_wf_treelet_deltas = 0;  // tuning knob ("treelet_deltas"): the light buffer's distances staged first
 constexpr int kWfBlock = 256;      // prep / shadow / combine
 
 #define WF_CHECK(x)                        \
@@ -655,10 +657,13 @@ __device__ __forceinline__ void leaf_sphere_test(const SphereDiag* sd, int k, V3
                       [&] { return (int)r.meta; }, h, n_disc);
 }
 
+// With a treelet (the global-memory image), the first n_top nodes (breadth-first:
+// the top levels) are read from their LDS copy `top`, the rest from `nodes`.
 template <bool SHADOW, bool LDS_STACK>
 __device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDiag* sd, const float* M, bool has_bvh,
                                            V3 o, V3 d, double t_shadow, Hit& h, unsigned& n_disc, unsigned& n_tests,
-                                           unsigned& n_boxes, int* lds) {
+                                           unsigned& n_boxes, int* lds, const BvhNode* top = nullptr,
+                                           int n_top = 0) {
   const SlabRay sr = slab_ray(o, d, M);
   float t_hi = f32_up(SHADOW ? t_shadow : h.t);
   int pstk[LDS_STACK ? 1 : kBvhMaxDepth + 4];
@@ -669,8 +674,20 @@ __device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDia
   // a node visit: both children's boxes, the one entered first visited first
   auto visit = [&]() {
     // the whole 64-B node in four 16-B loads: lo[0], lo[1], hi[0], hi[1], child[2], axis, pad
-    uint4 q0, q1, q2, q3;
-    node_chunks(nodes, e, q0, q1, q2, q3);
+    // (explicit address spaces: the two paths stay LDS and global loads)
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 r0, r1, r2, r3;
+    if (e < n_top) {
+      typedef __attribute__((address_space(3))) const u32x4 lq;
+      lq* b = (lq*)(top + e);
+      r0 = b[0]; r1 = b[1]; r2 = b[2]; r3 = b[3];
+    } else {
+      typedef __attribute__((address_space(1))) const u32x4 gq;
+      gq* b = (gq*)(nodes + e);
+      r0 = b[0]; r1 = b[1]; r2 = b[2]; r3 = b[3];
+    }
+    const uint4 q0 = make_uint4(r0.x, r0.y, r0.z, r0.w), q1 = make_uint4(r1.x, r1.y, r1.z, r1.w);
+    const uint4 q2 = make_uint4(r2.x, r2.y, r2.z, r2.w), q3 = make_uint4(r3.x, r3.y, r3.z, r3.w);
     const float lo0[3] = {__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z)};
     const float lo1[3] = {__uint_as_float(q0.w), __uint_as_float(q1.x), __uint_as_float(q1.y)};
     const float hi0[3] = {__uint_as_float(q1.z), __uint_as_float(q1.w), __uint_as_float(q2.x)};
@@ -923,11 +940,13 @@ struct LaneScene {
   const float* delta;          // light buffer: per-light box distances (LDS or global)
   int* stack;                  // per-lane LDS stack (14, 3) or the wave's stack (0)
   float M[3];                  // bound on |box coordinate| per axis (slab_ray)
+  const BvhNode* top;          // 3: the LDS copy of the first n_top nodes
+  int n_top;
 };
 template <int LANE>
 __device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, const WfArgs& a, int* static_stack,
                                                 unsigned char* dyn) {
-  LaneScene ls{(const unsigned char*)sc.bvh, sc.sph_diag, sc.lb_delta, static_stack, {0.f, 0.f, 0.f}};
+  LaneScene ls{(const unsigned char*)sc.bvh, sc.sph_diag, sc.lb_delta, static_stack, {0.f, 0.f, 0.f}, nullptr, 0};
   unsigned char* p = dyn;
   if constexpr (LANE == 14) {
     // pair layout (BvhPair): per axis, the two children's lower bounds form one
@@ -942,6 +961,12 @@ __device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, const WfArgs
     stage_lds((uint4*)p, (const uint4*)sc.sph_diag, sc.n_diag * (int)(sizeof(SphereDiag) / 16));
     ls.sd = (const SphereDiag*)p;
     p += sph_lds_bytes(sc);
+  }
+  if (LANE == 3 && a.n_top > 0) {  // the treelet: after the distances when those are staged
+    unsigned char* q = p + ((a.lds_flags & kLdsDeltas) ? delta_lds_bytes(sc) : 0);
+    stage_lds((uint4*)q, (const uint4*)sc.bvh, (int)a.n_top * (int)(sizeof(BvhNode) / 16));
+    ls.top = (const BvhNode*)q;
+    ls.n_top = (int)a.n_top;
   }
   if (a.lds_flags & kLdsDeltas) {
     float* ld = (float*)p;
@@ -1042,7 +1067,7 @@ __device__ __forceinline__ bool shadow_trace(const DevScene& sc, const WfArgs& a
       if (hb.key >= 0 && hb.key != 0x7fffffff && hb.t < dist) h = hb;
     } else {
       lane_trace<true, LANE == 3>((const BvhNode*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, dist, h, n_disc,
-                                  n_tests, n_boxes, ls.stack);
+                                  n_tests, n_boxes, ls.stack, ls.top, ls.n_top);
     }
   }
   hit_finish(h);
@@ -1272,7 +1297,7 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
                                  ls.stack);
         else
           lane_trace<false, LANE == 3>((const BvhNode*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, t.disc,
-                                       t.tests, t.boxes, ls.stack);
+                                       t.tests, t.boxes, ls.stack, ls.top, ls.n_top);
 #ifdef RTAMD_EXP_TRAV2  // experiment (dev): the traversal a second time (its marginal cost)
         {
           Hit h2;
@@ -1759,7 +1784,13 @@ static hipError_t launch_fused_q(const DevScene& sc, const DevCamera& cam, WfArg
   }
   if (g_wf_image != 1 && sc.bvh_depth <= kLaneLdsDepth) {
     const size_t room = kWfLdsLimit - (size_t)kLaneLdsDepth * kTraceBlock * 4;
-    if (dl && dl <= room) { a.lds_flags |= kLdsDeltas; dyn = dl; }
+    // the room left beside the stack: the light buffer's distances and/or a treelet
+    const bool deltas = dl && dl <= room && (!g_wf_treelet || g_wf_treelet_deltas);
+    if (deltas) { a.lds_flags |= kLdsDeltas; dyn = dl; }
+    if (g_wf_treelet) {
+      a.n_top = (unsigned)std::min<size_t>((size_t)sc.n_bvh, (room - dyn) / sizeof(BvhNode));
+      dyn += (size_t)a.n_top * sizeof(BvhNode);
+    }
     return launch_lds(wf_trace_fused<false, QUADS, 3>, dyn, n, stream, sc, cam, a, tb);
   }
   if (dl && dl <= kWfLdsLimit) { a.lds_flags |= kLdsDeltas; dyn = dl; }

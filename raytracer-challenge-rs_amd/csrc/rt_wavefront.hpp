@@ -85,6 +85,8 @@ enum WfFlags : unsigned { WF_EXHAUSTIVE = 1u, WF_COUNT = 2u };
 extern int g_wf_accel;        // tuning knob: 1 = BVH traversal (when the exhaustive loop is not asked for)
 extern int g_wf_shadow_lb;    // tuning knob: 1 = shadow rays through the light buffer when the scene has one
 extern int g_wf_image;        // tuning knob: 0 = automatic scene image of the fused kernels, 3 / 1 = global memory
+extern int g_wf_treelet;         // tuning knob: the global-memory image stages a treelet in LDS
+extern int g_wf_treelet_deltas;  // tuning knob: ... after the light buffer's distances (when they fit)
 extern int g_wf_shadow_stream;   // tuning knob: 1 = exhaustive shadow traces on a second stream
 extern int g_wf_adaptive_block;  // tuning knob: 1 = small trace launches spread over every CU (smaller blocks)
 extern int g_wf_skip_shadow;  // tuning knob: 1 = the fast path leaves out shadow rays that cannot change the colour
@@ -189,6 +191,7 @@ struct WfArgs {
   unsigned count;       // counted launch: tally shade_hit runs and children (fast path)
   unsigned use_lb;      // fast path: shadow rays through the light buffer
   unsigned lds_flags;   // fast path: what the trace kernel stages in LDS (kLdsSpheres | kLdsDeltas)
+  unsigned n_top;       // fast path, global-memory image: the first n_top (breadth-first) nodes are in LDS
 };
 
 // Per-kernel-class timing of the last frame (profiling mode only).
