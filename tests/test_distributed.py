@@ -1,4 +1,4 @@
-"""Multi-rank frame assembly on CPU (gloo), world_size 2 and 3.
+"""Multi-rank frame assembly on CPU (gloo), world_size 2, 3 and 8.
 
 Each rank renders ONLY its interleaved row blocks (rtamd.distributed, the same
 layout as rt_render_shard_device) — here with the oracle, since this container
@@ -47,7 +47,7 @@ def _worker(rank, world_size, port, row_block, out_path):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world_size,row_block", [(2, 8), (3, 5), (2, 64)])
+@pytest.mark.parametrize("world_size,row_block", [(2, 8), (3, 5), (2, 64), (8, 4)])
 def test_gloo_frame_assembly(tmp_path, world_size, row_block):
     out = str(tmp_path / "canvas.npy")
     mp.spawn(_worker, args=(world_size, _free_port(), row_block, out), nprocs=world_size, join=True)
