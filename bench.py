@@ -434,7 +434,12 @@ def main():
     for _ in range(a.steps):
         cam.render_shard_device(world, depth, B, srank, sn, shard.data_ptr(), stream.cuda_stream, False)
     torch.cuda.synchronize()
-    breakdown = rtamd._rtamd._wf_profile(world, 0, True)
+    rtamd._rtamd._wf_profile(world, 0, False)
+    # the fast path's own counters (what the kernels executed and traced), one counted
+    # frame on the same workspace: the timed and profiled kernels do not count
+    fst = cam.render_shard_device(world, depth, B, srank, sn, shard.data_ptr(), stream.cuda_stream, True,
+                                  exhaustive=False)
+    breakdown = rtamd._rtamd._wf_profile(world, -1, True)  # class times of the profiled frames, counters of the counted one
     prof = breakdown
     if a.verify and rank == 0:  # dev: the assembled last frame equals a one-GPU render of the whole frame
         whole = torch.empty((H, W, 3), dtype=torch.float64, device=dev)
@@ -444,9 +449,6 @@ def main():
         print(f"verify: assembled frame {'==' if same else '!='} whole-frame render", file=sys.stderr, flush=True)
         if not same:
             raise SystemExit("verify failed: the assembled frame differs from the whole-frame render")
-    # the fast path's own counters (what the kernels traced), one frame
-    fst = cam.render_shard_device(world, depth, B, srank, sn, shard.data_ptr(), stream.cuda_stream, True,
-                                  exhaustive=False)
     traced = torch.tensor([fst["rays_primary"] + fst["rays_reflect"] + fst["rays_refract"] + fst["rays_shadow_traced"],
                            fst["sphere_tests_executed"], fst["box_tests_executed"],
                            fst["rays_primary"] + fst["rays_reflect"] + fst["rays_refract"] + fst["rays_shadow"]],

@@ -75,9 +75,10 @@ def test_bvh_frames_bitwise_equal_exhaustive(rt, name):
 def test_bvh_is_the_fast_path(rt):
     from rtamd import scenes
     w, cam, depth = scenes.c3(64, 36, n_spheres=200)
-    rt._rtamd._wf_profile(w, 1, False)
     cam.render(w, depth, want_stats=False)
-    p = rt._rtamd._wf_profile(w, 0, True)
+    assert rt._rtamd._wf_profile(w, -1, True)["bvh"]
+    cam.render(w, depth, want_stats=True, exhaustive=False)  # the fast path, counting its work
+    p = rt._rtamd._wf_profile(w, -1, True)
     assert p["bvh"] and 0 < p["tests"]["primary"] < p["rays"]["primary"] * 200
     cam.render(w, depth, want_stats=True)
     assert not rt._rtamd._wf_profile(w, -1, True)["bvh"]
@@ -198,16 +199,16 @@ def test_skipped_shadow_rays_bitwise(rt, neg_zero):
     skipped), and fewer shadow rays must actually be traced."""
     w, cam, depth = _glass_cluster(rt, n=200, seed=31, inside=False, neg_zero=neg_zero)
     exact, st = cam.render(w, depth, want_stats=True)
-    rt._rtamd._wf_profile(w, 1, False)
     fast, _ = cam.render(w, depth, want_stats=False)
-    traced = rt._rtamd._wf_profile(w, 0, True)["rays"]["shadow"]
+    counted, sf = cam.render(w, depth, want_stats=True, exhaustive=False)  # the fast path, counting
     assert fast.to_numpy().tobytes() == exact.to_numpy().tobytes()
-    assert traced < st["rays_shadow"]
+    assert counted.to_numpy().tobytes() == exact.to_numpy().tobytes()
+    assert 0 < sf["rays_shadow_traced"] < st["rays_shadow"]
     rt._rtamd._tuning_set("skip_shadow", 0)
     try:
-        rt._rtamd._wf_profile(w, 1, False)
         full, _ = cam.render(w, depth, want_stats=False)
-        assert rt._rtamd._wf_profile(w, 0, True)["rays"]["shadow"] == st["rays_shadow"]
+        _, sa = cam.render(w, depth, want_stats=True, exhaustive=False)
+        assert sa["rays_shadow_traced"] == st["rays_shadow"]
     finally:
         rt._rtamd._tuning_set("skip_shadow", 1)
     assert full.to_numpy().tobytes() == exact.to_numpy().tobytes()
@@ -361,9 +362,8 @@ def test_other_records_only_scene_takes_fast_path(rt):
     cam = rt.Camera(96, 64, PI / 3)
     cam.set_transform(rt.view_transform(rt.Point(0, 4, -12), rt.Point(0, 1, 0), rt.Vector(0, 1, 0)))
     exact, st = cam.render(w, 5, want_stats=True)
-    rt._rtamd._wf_profile(w, 1, False)
-    fast, fst = cam.render(w, 5, want_stats=False)
-    p = rt._rtamd._wf_profile(w, 0, True)
+    fast, fst = cam.render(w, 5, want_stats=True, exhaustive=False)  # the fast path, counting its work
+    p = rt._rtamd._wf_profile(w, -1, True)
     assert p["bvh"] and p["fused"]
     assert fast.to_numpy().tobytes() == exact.to_numpy().tobytes()
     # executed record tests (closest-hit + shadow) against the reference's every-shape loop

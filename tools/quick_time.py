@@ -61,7 +61,9 @@ rtamd._rtamd._wf_profile(w, 1, False)
 for f in range(min(a.frames, 5)):
     cam.render_shard_device(w, depth, 8, r, n, bufs[0].data_ptr(), s0, False)
 torch.cuda.synchronize()
-p = rtamd._rtamd._wf_profile(w, 0, True)
+rtamd._rtamd._wf_profile(w, 0, False)
+cam.render_shard_device(w, depth, 8, r, n, bufs[0].data_ptr(), s0, True, exhaustive=False)  # counted: the work tallies
+p = rtamd._rtamd._wf_profile(w, -1, True)
 print(json.dumps({"tag": a.tag, "config": a.config, "shard": a.shard, "knobs": a.knob, "inflight": F,
                   "ms_per_frame": round(ms, 4), "mrays_per_s": round(ref_rays / ms / 1e3, 1),
                   "ref_rays": ref_rays, "traced_shadow": st["rays_shadow_traced"], "upload_s": round(t_up, 2),
