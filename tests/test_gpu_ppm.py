@@ -94,3 +94,17 @@ def test_render_ppm_aa_and_c5_slice(rt):
     canvas, _ = cam.render(w, depth, want_stats=False)
     ppm, _ = cam.render_ppm(w, depth)
     assert ppm == _as_bytes(rt.canvas_to_ppm(canvas.to_numpy()))
+
+
+def test_device_ppm_empty_canvases(rt, oracle):
+    """Zero width (every row is "\\n", ppm.rs:47-48) and zero height (the header
+    alone), as the host writer and the oracle produce them."""
+    import torch
+    for h, w in [(3, 0), (0, 4), (0, 0)]:
+        img = np.zeros((h, w, 3))
+        d = torch.zeros(max(1, h * w * 3), dtype=torch.float64, device="cuda")
+        cap = 12 * w * h + h + 32
+        out = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+        n = rt._rtamd.canvas_to_ppm_device(d.data_ptr(), w, h, out.data_ptr(), cap, 0)
+        got = out[:n].cpu().numpy().tobytes()
+        assert got == _as_bytes(oracle.canvas_to_ppm(img)) == _as_bytes(rt.canvas_to_ppm(img)), (h, w)
