@@ -91,7 +91,7 @@ import torch.distributed as dist  # noqa: E402
 
 import rtamd  # noqa: E402
 from rtamd import scenes  # noqa: E402
-from rtamd.distributed import FrameAssembler, RcclStreamAssembler, StreamFrameAssembler  # noqa: E402
+from rtamd.distributed import FrameAssembler, RcclStreamAssembler, StreamFrameAssembler, shard_of  # noqa: E402
 
 WF_CLOSEST = 1  # kernel class index (csrc/rt_wavefront.hpp WfClass)
 METRIC = "Mrays/s (primary+secondary) on 1920×1080/1000-sphere/depth-5; 1→8 GPU scaling"
@@ -269,7 +269,7 @@ def main():
     if a.gpus != world_size:  # _launch_ranks starts N ranks for --gpus N; never fall back silently
         sys.exit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE {world_size}")
     n = world_size
-    srank, sn = rank, n  # the shard this process renders
+    srank, sn = shard_of(rank, n), n  # the shard this process renders (rank 0 assembles: the smallest)
     if a.fake_shard:
         srank, sn = (int(x) for x in a.fake_shard.split("/"))
     torch.cuda.set_device(local_rank)
@@ -336,7 +336,7 @@ def main():
                                   slots=F)
     else:
         fa = FrameAssembler(H, W, B, rank, n, dev, slots=F if not events else (F + 1 if F > 1 else 2))
-    assert len(fa.rows) == rtamd.shard_rows(H, B, rank, n)
+    assert len(fa.rows) == rtamd.shard_rows(H, B, srank, n)
     shard = fa.shard
     free_ev = [None] * len(fa.shards)
     frame_no = [0]

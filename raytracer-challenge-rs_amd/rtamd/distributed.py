@@ -2,8 +2,9 @@
 
 The reference parallelises `render_multithreaded` over contiguous row blocks
 of a shared canvas (camera.rs:157-172). Here the frame is split into blocks of
-`row_block` rows dealt round-robin to the ranks (block b -> rank b mod N, same
-rule as `rt_shard_rows` / `rt_render_shard_device`, include/rt_render.h), so
+`row_block` rows dealt round-robin to the shards (block b -> shard b mod N, same
+rule as `rt_shard_rows` / `rt_render_shard_device`, include/rt_render.h; rank r
+renders shard N-1-r, `shard_of`), so
 dense and empty regions spread evenly. Each rank renders its rows into a
 device buffer padded to the largest shard; ONE gather (RCCL on GPUs, gloo in
 the CPU tests) brings the shards to rank 0, into one contiguous buffer, which
@@ -11,6 +12,14 @@ rank 0 un-interleaves into the row-major canvas with one index_select. No other 
 """
 import torch
 import torch.distributed as dist
+
+
+def shard_of(rank, n_shards):
+    """The shard rank `rank` renders: ranks take the shards in reverse, so
+    that rank 0, which also receives and assembles every frame, renders the
+    last shard, the one with the fewest rows when the row blocks do not divide
+    evenly (C3 at 8 GPUs: 135 blocks, 16 for rank 0 and 17 for the others)."""
+    return n_shards - 1 - rank
 
 
 def shard_row_ids(height, row_block, shard, n_shards):
@@ -33,7 +42,8 @@ class FrameAssembler:
     def __init__(self, height, width, row_block, rank, n_shards, device, dtype=torch.float64, slots=1):
         self.H, self.W, self.B = height, width, row_block
         self.rank, self.n = rank, n_shards
-        self.rows = shard_row_ids(height, row_block, rank, n_shards)
+        self.shard_index = shard_of(rank, n_shards)
+        self.rows = shard_row_ids(height, row_block, self.shard_index, n_shards)
         self.max_rows = max(len(shard_row_ids(height, row_block, s, n_shards)) for s in range(n_shards))
         # padded so that every rank sends the same element count
         self.shards = [torch.zeros((self.max_rows, width, 3), dtype=dtype, device=device) for _ in range(slots)]
@@ -49,8 +59,8 @@ class FrameAssembler:
                              for b in self.gather_buf]
             self.canvas = torch.empty((height, width, 3), dtype=dtype, device=device)
             inv = [0] * height
-            for s in range(n_shards):
-                for i, y in enumerate(shard_row_ids(height, row_block, s, n_shards)):
+            for s in range(n_shards):  # gather position s holds rank s's shard
+                for i, y in enumerate(shard_row_ids(height, row_block, shard_of(s, n_shards), n_shards)):
                     inv[y] = s * self.max_rows + i
             self.inv_idx = torch.tensor(inv, device=device)
 
@@ -126,7 +136,8 @@ class StreamFrameAssembler:
         self.streams = streams
         self.F = len(streams) if streams else max(1, slots)
         self.groups = groups if groups is not None else [None] * self.F
-        self.rows = shard_row_ids(height, row_block, rank, n_shards)
+        self.shard_index = shard_of(rank, n_shards)
+        self.rows = shard_row_ids(height, row_block, self.shard_index, n_shards)
         self.max_rows = max(len(shard_row_ids(height, row_block, s, n_shards)) for s in range(n_shards))
         self.shards = [torch.zeros((self.max_rows, width, 3), dtype=dtype, device=device) for _ in range(self.F)]
         self.shard = self.shards[0]
@@ -138,8 +149,8 @@ class StreamFrameAssembler:
                              for b in self.gather_buf]
             self.canvas = [torch.empty((height, width, 3), dtype=dtype, device=device) for _ in range(self.F)]
             inv = [0] * height
-            for s in range(n_shards):
-                for i, y in enumerate(shard_row_ids(height, row_block, s, n_shards)):
+            for s in range(n_shards):  # gather position s holds rank s's shard
+                for i, y in enumerate(shard_row_ids(height, row_block, shard_of(s, n_shards), n_shards)):
                     inv[y] = s * self.max_rows + i
             self.inv_idx = torch.tensor(inv, device=device)
 

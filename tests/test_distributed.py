@@ -35,7 +35,7 @@ def _worker(rank, world_size, port, row_block, out_path):
         w, cam, depth = golden_cases.scene(rtamd, "c3", {"width": 64, "height": 36, "n_spheres": 200})
         H, W = cam.vsize, cam.hsize
         fa = FrameAssembler(H, W, row_block, rank, world_size, torch.device("cpu"))
-        assert len(fa.rows) == rtamd.shard_rows(H, row_block, rank, world_size)
+        assert len(fa.rows) == rtamd.shard_rows(H, row_block, world_size - 1 - rank, world_size)
         part, _ = pyoracle.OracleWorld.from_world(w).render_rows(cam.desc_bytes(), depth, fa.rows, 2)
         fa.shard[: len(fa.rows)] = torch.from_numpy(part)
         canvas = fa.assemble()
