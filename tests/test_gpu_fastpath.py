@@ -72,6 +72,29 @@ def test_c3_full_frame_frames_in_flight_equal(rt):
         assert torch.equal(b, exact)
 
 
+def test_c3_full_frame_aa_and_zoo_fast_equal_exhaustive(rt):
+    """render_multithreaded X4 (camera.rs:150-253) at the full 1920x1080 of C3,
+    and the feature zoo (every pattern, rotated / sheared solids, nested glass,
+    a shadowless object, two lights) at 1920x1080: fast == exhaustive bitwise."""
+    import torch
+    from rtamd import scenes
+    w, cam, depth = scenes.c3()
+    for flags in (True, False):
+        buf = torch.empty((cam.vsize, cam.hsize, 3), dtype=torch.float64, device="cuda")
+        cam.render_shard_device(w, depth, 8, 0, 1, buf.data_ptr(), torch.cuda.current_stream().cuda_stream, True,
+                                exhaustive=flags, aa_samples=4)
+        torch.cuda.synchronize()
+        if flags:
+            exact = buf
+        else:
+            assert torch.equal(buf, exact)
+    del exact, buf
+    w, cam, depth = scenes.zoo(1920, 1080)
+    exact, _ = _device_frame(cam, w, depth, True)
+    fast, _ = _device_frame(cam, w, depth, False)
+    assert torch.equal(fast, exact)
+
+
 def test_c5_full_frame_fast_equals_exhaustive(rt):
     """C5 at its full 4096x4096 (4 planes + 9996 spheres, 2 lights, depth 8)."""
     import torch
