@@ -240,8 +240,14 @@ int copy_to_host(rt_scene* s, void* dst, const void* src, size_t n, hipStream_t 
     }
     const size_t part = ((n_c + n_threads - 1) / n_threads + 4095) & ~(size_t)4095;
     std::vector<std::thread> pool;
-    for (unsigned t = 1; t < n_threads && t * part < n_c; ++t)
-      pool.emplace_back([=] { std::memcpy(d + t * part, src_h + t * part, std::min(part, n_c - t * part)); });
+    unsigned t = 1;
+    try {  // nothing may throw across the C ABI: a thread that cannot start is copied here
+      for (; t < n_threads && t * part < n_c; ++t)
+        pool.emplace_back([=] { std::memcpy(d + t * part, src_h + t * part, std::min(part, n_c - t * part)); });
+    } catch (...) {
+    }
+    for (unsigned u = t; u < n_threads && u * part < n_c; ++u)
+      std::memcpy(d + u * part, src_h + u * part, std::min(part, n_c - u * part));
     std::memcpy(d, src_h, std::min(part, n_c));
     for (std::thread& th : pool) th.join();
     return RT_OK;

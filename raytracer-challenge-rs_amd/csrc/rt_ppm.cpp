@@ -89,8 +89,13 @@ void for_rows(uint32_t height, size_t work, F f) {
   }
   std::vector<std::thread> pool;
   const uint32_t per = (height + t - 1) / t;
-  for (unsigned k = 1; k < t && k * per < height; ++k)
-    pool.emplace_back([=] { f(k * per, std::min(height, (k + 1) * per)); });
+  unsigned k = 1;
+  try {  // nothing may throw across the C ABI: row ranges whose thread cannot start run here
+    for (; k < t && k * per < height; ++k)
+      pool.emplace_back([=] { f(k * per, std::min(height, (k + 1) * per)); });
+  } catch (...) {
+  }
+  for (unsigned u = k; u < t && u * per < height; ++u) f(u * per, std::min(height, (u + 1) * per));
   f(0u, std::min(height, per));
   for (std::thread& th : pool) th.join();
 }
@@ -105,7 +110,12 @@ int rt_canvas_to_ppm(const double* rgb, uint32_t width, uint32_t height, char* o
   char hdr[64];
   const size_t hn = (size_t)std::snprintf(hdr, sizeof hdr, "P3\n%u %u\n255\n", width, height);
   const size_t row_doubles = (size_t)width * 3;
-  std::vector<size_t> off((size_t)height + 1, 0);
+  std::vector<size_t> off;
+  try {
+    off.assign((size_t)height + 1, 0);
+  } catch (...) {
+    return RT_ERR_INVALID_ARGUMENT;  // no memory for the row offsets
+  }
   for_rows(height, row_doubles * height, [&](uint32_t r0, uint32_t r1) {
     for (uint32_t j = r0; j < r1; ++j) off[j + 1] = ppm_row_len(rgb + j * row_doubles, width);
   });
