@@ -40,7 +40,8 @@ enum {
   RT_ERR_DUPLICATE_SHAPES = -5, /* structurally-equal shapes: see DESIGN.md */
   RT_ERR_NOT_INVERTIBLE = -6,   /* Matrix::inverse assert, matrix.rs:139 */
   RT_ERR_BUFFER_TOO_SMALL = -7,
-  RT_ERR_NO_DEVICE = -8
+  RT_ERR_NO_DEVICE = -8,
+  RT_ERR_HOST = -9 /* host-side failure (e.g. out of host memory); no exception crosses the ABI */
 };
 
 /* ---- shape kinds / pattern kinds ---------------------------------------- */

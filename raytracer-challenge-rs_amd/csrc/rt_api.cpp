@@ -8,6 +8,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <exception>
+#include <new>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -39,6 +41,25 @@ int g_lb_res = 256;     // light-buffer cells per cube-map face edge at scene cr
 int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
+}
+
+// Nothing may throw across the C ABI (the Rust side maps codes to
+// errors, an unwinding C++ exception would abort the caller): every int entry
+// point runs its body through guarded().
+template <typename F>
+int guarded(F&& body) noexcept {
+  try {
+    return body();
+  } catch (const std::bad_alloc&) {
+    g_err = "out of memory";  // short: no allocation
+    return RT_ERR_HOST;
+  } catch (const std::exception& e) {
+    try { g_err = e.what(); } catch (...) { g_err.clear(); }
+    return RT_ERR_HOST;
+  } catch (...) {
+    g_err = "host error";
+    return RT_ERR_HOST;
+  }
 }
 
 #define RT_HIP(call)                                                                   \
@@ -557,23 +578,28 @@ int rtamd_nccl_comm_abort(void* comm) {
 int rt_abi_version(void) { return RT_ABI_VERSION; }
 
 int rt_device_count(void) {
+  return guarded([&]() -> int {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
   return n;
+  });
 }
 
 int rt_matrix_inverse(const double m[16], double out[16]) {
+  return guarded([&]() -> int {
   if (!m || !out) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
   rt::Matrix a = rt::Matrix::from_slice(4, 4, m);
   if (!a.is_invertible()) return fail(RT_ERR_NOT_INVERTIBLE, "matrix is not invertible (matrix.rs:139)");
   rt::Matrix inv = a.inverse();
   std::memcpy(out, inv.data(), 16 * sizeof(double));
   return RT_OK;
+  });
 }
 
 // camera.rs:33-55 (+ set_transform :128-131)
 int rt_camera_init(uint32_t hsize, uint32_t vsize, double field_of_view, const double transform[16],
                    rt_camera_desc* out) {
+  return guarded([&]() -> int {
   if (!out || hsize == 0 || vsize == 0) return fail(RT_ERR_INVALID_ARGUMENT, "bad camera size");
   const double half_view = std::tan(field_of_view / 2.0);
   const double aspect = (double)hsize / (double)vsize;
@@ -598,10 +624,12 @@ int rt_camera_init(uint32_t hsize, uint32_t vsize, double field_of_view, const d
     std::memcpy(out->inverse, id.data(), sizeof out->inverse);
   }
   return RT_OK;
+  });
 }
 
 int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light_desc* lights,
                     size_t n_lights, int device, rt_scene** out) {
+  return guarded([&]() -> int {
   if (!out || (n_shapes && !shapes) || (n_lights && !lights))
     return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
   *out = nullptr;
@@ -812,6 +840,7 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   s->n_lights = (int)n_lights;
   *out = s;
   return RT_OK;
+  });
 }
 
 void rt_scene_destroy(rt_scene* s) {
@@ -842,13 +871,16 @@ uint32_t rt_shard_rows(uint32_t vsize, uint32_t row_block, uint32_t shard, uint3
 int rt_render_shard_device(const rt_scene* scene, const rt_camera_desc* camera, uint32_t max_depth,
                            uint32_t aa_samples, uint32_t row_block, uint32_t shard, uint32_t n_shards,
                            double* d_out_rgb, void* stream, rt_stats* stats) {
+  return guarded([&]() -> int {
   return rt_render_shard_device_ex(scene, camera, max_depth, aa_samples, row_block, shard, n_shards, 0, d_out_rgb,
                                    stream, stats);
+  });
 }
 
 int rt_render_shard_device_ex(const rt_scene* scene, const rt_camera_desc* camera, uint32_t max_depth,
                               uint32_t aa_samples, uint32_t row_block, uint32_t shard, uint32_t n_shards,
                               uint32_t flags, double* d_out_rgb, void* stream, rt_stats* stats) {
+  return guarded([&]() -> int {
   if (!scene || !camera || !d_out_rgb) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
   if (row_block == 0 || n_shards == 0 || shard >= n_shards)
     return fail(RT_ERR_INVALID_ARGUMENT, "bad shard specification");
@@ -869,15 +901,19 @@ int rt_render_shard_device_ex(const rt_scene* scene, const rt_camera_desc* camer
   if (stats)
     fill_stats(stats, ds, ms, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
   return RT_OK;
+  });
 }
 
 int rt_render_aa(const rt_scene* scene, const rt_camera_desc* camera, uint32_t max_depth, uint32_t aa_samples,
                  double* out_rgb, rt_stats* stats) {
+  return guarded([&]() -> int {
   return rt_render_ex(scene, camera, max_depth, aa_samples, 0, out_rgb, stats);
+  });
 }
 
 int rt_render_ex(const rt_scene* scene, const rt_camera_desc* camera, uint32_t max_depth, uint32_t aa_samples,
                  uint32_t flags, double* out_rgb, rt_stats* stats) {
+  return guarded([&]() -> int {
   if (!scene || !camera || !out_rgb) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
   if (camera->hsize == 0 || camera->vsize == 0) return fail(RT_ERR_INVALID_ARGUMENT, "empty camera");
   if (!valid_aa(aa_samples)) return fail(RT_ERR_INVALID_ARGUMENT, "aa_samples must be 1, 2, 4, 8 or 16");
@@ -899,10 +935,12 @@ int rt_render_ex(const rt_scene* scene, const rt_camera_desc* camera, uint32_t m
   if (stats)
     fill_stats(stats, ds, ms, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
   return RT_OK;
+  });
 }
 
 int rt_render_ppm(const rt_scene* scene, const rt_camera_desc* camera, uint32_t max_depth, uint32_t aa_samples,
                   char* out, size_t cap, size_t* out_len, rt_stats* stats) {
+  return guarded([&]() -> int {
   if (!scene || !camera || !out_len) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
   if (camera->hsize == 0 || camera->vsize == 0) return fail(RT_ERR_INVALID_ARGUMENT, "empty camera");
   if (!valid_aa(aa_samples)) return fail(RT_ERR_INVALID_ARGUMENT, "aa_samples must be 1, 2, 4, 8 or 16");
@@ -952,10 +990,12 @@ int rt_render_ppm(const rt_scene* scene, const rt_camera_desc* camera, uint32_t 
   if (stats)
     fill_stats(stats, ds, ms, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
   return RT_OK;
+  });
 }
 
 int rt_canvas_to_ppm_device(const double* d_rgb, uint32_t width, uint32_t height, char* d_out, size_t cap,
                             size_t* out_len, void* stream) {
+  return guarded([&]() -> int {
   if (!out_len || (width && height && !d_rgb)) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
   if (width > kPpmMaxWidth)
     return fail(RT_ERR_INVALID_ARGUMENT, "canvas wider than the device PPM encoder's row (use rt_canvas_to_ppm)");
@@ -979,20 +1019,26 @@ int rt_canvas_to_ppm_device(const double* d_rgb, uint32_t width, uint32_t height
   *out_len = hd.n + (size_t)body;
   if (d_out && cap < *out_len) return fail(RT_ERR_BUFFER_TOO_SMALL, "PPM buffer too small");
   return RT_OK;
+  });
 }
 
 int rt_render(const rt_scene* scene, const rt_camera_desc* camera, uint32_t max_depth, double* out_rgb,
               rt_stats* stats) {
+  return guarded([&]() -> int {
   return rt_render_aa(scene, camera, max_depth, 1, out_rgb, stats);
+  });
 }
 
 int rt_color_at_batch(const rt_scene* scene, const double* rays, size_t n, uint32_t remaining,
                       double* out_rgb, rt_stats* stats) {
+  return guarded([&]() -> int {
   return rt_color_at_batch_ex(scene, rays, n, remaining, 0, out_rgb, stats);
+  });
 }
 
 int rt_color_at_batch_ex(const rt_scene* scene, const double* rays, size_t n, uint32_t remaining, uint32_t flags,
                          double* out_rgb, rt_stats* stats) {
+  return guarded([&]() -> int {
   if (!scene || (n && (!rays || !out_rgb))) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
   if (n >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "batch too large");
   rt_scene* s = const_cast<rt_scene*>(scene);
@@ -1015,10 +1061,12 @@ int rt_color_at_batch_ex(const rt_scene* scene, const double* rays, size_t n, ui
   if (stats)
     fill_stats(stats, ds, ms, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
   return RT_OK;
+  });
 }
 
 int rt_is_shadowed_batch(const rt_scene* scene, const double* points, size_t n, uint32_t light,
                          uint8_t* out) {
+  return guarded([&]() -> int {
   if (!scene || (n && (!points || !out))) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
   rt_scene* s = const_cast<rt_scene*>(scene);
   if ((int)light >= s->n_lights) return fail(RT_ERR_INVALID_ARGUMENT, "light index out of range");
@@ -1035,9 +1083,11 @@ int rt_is_shadowed_batch(const rt_scene* scene, const double* points, size_t n, 
   RT_HIP(hipMemcpyAsync(out, s->d_out, n, hipMemcpyDeviceToHost, s->stream));
   RT_HIP(hipStreamSynchronize(s->stream));
   return RT_OK;
+  });
 }
 
 int rt_hit_batch(const rt_scene* scene, const double* rays, size_t n, double* out24) {
+  return guarded([&]() -> int {
   if (!scene || (n && (!rays || !out24))) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
   if (n >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "batch too large");
   rt_scene* s = const_cast<rt_scene*>(scene);
@@ -1053,6 +1103,7 @@ int rt_hit_batch(const rt_scene* scene, const double* rays, size_t n, double* ou
   RT_HIP(hipMemcpyAsync(out24, s->d_out, n * 24 * sizeof(double), hipMemcpyDeviceToHost, s->stream));
   RT_HIP(hipStreamSynchronize(s->stream));
   return RT_OK;
+  });
 }
 
 // Single-process multi-GPU render (the GPU form of `render_multithreaded`,
@@ -1062,6 +1113,7 @@ int rt_hit_batch(const rt_scene* scene, const double* rays, size_t n, double* ou
 int rt_render_multi(rt_scene* const* scenes, int n_devices, const rt_camera_desc* camera,
                     uint32_t max_depth, uint32_t aa_samples, uint32_t row_block, double* out_rgb,
                     rt_stats* stats) {
+  return guarded([&]() -> int {
   if (!scenes || n_devices < 1 || !camera || !out_rgb || row_block == 0)
     return fail(RT_ERR_INVALID_ARGUMENT, "bad arguments");
   if (camera->hsize == 0 || camera->vsize == 0) return fail(RT_ERR_INVALID_ARGUMENT, "empty camera");
@@ -1166,6 +1218,7 @@ int rt_render_multi(rt_scene* const* scenes, int n_devices, const rt_camera_desc
     stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
   return RT_OK;
+  });
 }
 
 }  // extern "C"
