@@ -127,7 +127,19 @@ inline Shape Cone(double minimum = -std::numeric_limits<double>::infinity(),
 // canvas.rs:8-52 + image/ppm.rs
 class Canvas {
  public:
-  Canvas(size_t w, size_t h) : w_(w), h_(h), px_(w * h * 3, 0.0) {}
+  Canvas(size_t w, size_t h) : w_(w), h_(h), px_(new double[w * h * 3]()) {}  // black (raytracer/src/canvas.rs:16)
+  // Storage the caller overwrites entirely (a render writes every pixel): no
+  // zero pass, so the pages are first touched by the copy from the device.
+  struct Uninit {};
+  Canvas(size_t w, size_t h, Uninit) : w_(w), h_(h), px_(new double[w * h * 3]) {}
+  Canvas(const Canvas& o) : w_(o.w_), h_(o.h_), px_(new double[o.w_ * o.h_ * 3]) {
+    std::memcpy(px_.get(), o.px_.get(), w_ * h_ * 3 * sizeof(double));
+  }
+  Canvas(Canvas&&) noexcept = default;
+  Canvas& operator=(Canvas o) noexcept {
+    w_ = o.w_; h_ = o.h_; px_.swap(o.px_);
+    return *this;
+  }
   size_t width() const { return w_; }
   size_t height() const { return h_; }
   Color get_pixel(size_t x, size_t y) const {
@@ -138,13 +150,13 @@ class Canvas {
     double* p = &px_[idx(x, y)];
     p[0] = c.red; p[1] = c.green; p[2] = c.blue;
   }
-  double* data() { return px_.data(); }
-  const double* data() const { return px_.data(); }
+  double* data() { return px_.get(); }
+  const double* data() const { return px_.get(); }
   std::string to_ppm() const {  // canvas_to_ppm (image/ppm.rs:24-51)
     size_t len = 0;
-    check(rt_canvas_to_ppm(px_.data(), (uint32_t)w_, (uint32_t)h_, nullptr, 0, &len), "rt_canvas_to_ppm");
+    check(rt_canvas_to_ppm(px_.get(), (uint32_t)w_, (uint32_t)h_, nullptr, 0, &len), "rt_canvas_to_ppm");
     std::string s(len, '\0');
-    check(rt_canvas_to_ppm(px_.data(), (uint32_t)w_, (uint32_t)h_, &s[0], len, &len), "rt_canvas_to_ppm");
+    check(rt_canvas_to_ppm(px_.get(), (uint32_t)w_, (uint32_t)h_, &s[0], len, &len), "rt_canvas_to_ppm");
     return s;
   }
 
@@ -154,7 +166,7 @@ class Canvas {
     return (y * w_ + x) * 3;
   }
   size_t w_, h_;
-  std::vector<double> px_;
+  std::unique_ptr<double[]> px_;
 };
 
 inline rt_shape_desc to_desc(const Shape& s) {
@@ -302,14 +314,14 @@ class Camera {
   // camera.rs:133-148: the drop-in. `max_depth` = MAX_RECURSION_DEPTH (5).
   // `flags`: RT_RENDER_EXHAUSTIVE runs the reference's every-shape loop (exact counters).
   Canvas render(const World& world, unsigned max_depth = 5, rt_stats* stats = nullptr, uint32_t flags = 0) const {
-    Canvas c(desc_.hsize, desc_.vsize);
+    Canvas c(desc_.hsize, desc_.vsize, Canvas::Uninit{});
     check(rt_render_ex(world.scene(), &desc_, max_depth, 1, flags, c.data(), stats), "rt_render");
     return c;
   }
   // camera.rs:150-214: average of `rays_for_pixel` per pixel (render_opts.aa_samples).
   Canvas render_multithreaded(const World& world, unsigned max_depth = 5, rt_stats* stats = nullptr,
                               uint32_t flags = 0) const {
-    Canvas c(desc_.hsize, desc_.vsize);
+    Canvas c(desc_.hsize, desc_.vsize, Canvas::Uninit{});
     check(rt_render_ex(world.scene(), &desc_, max_depth, (uint32_t)render_opts.samples, flags, c.data(), stats),
           "rt_render_aa");
     return c;
