@@ -1255,22 +1255,29 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
   // the next chunk, so the launch ends with the last chunk, not with the
   // slowest wave of a static split (an LDS image holds its CU until every wave
   // of its block is done): C3 1.098 -> 1.013 ms/frame. The next chunk is asked
-  // for when the current one starts. A launch with fewer than three chunks per
-  // wave (an 8-way shard's generations) strides over them statically, with no
-  // atomics (there the dynamic form cost 5 %: the first chunks' atomics all
-  // arrive at once and balancing one or two chunks per wave gains nothing).
+  // for when the current one starts. A launch with one to three chunks per
+  // wave (the deep generations; most generations of a 2-way shard) gives each
+  // wave its first chunk statically (chunk = wave index, no atomic to wait
+  // for) and hands out the rest, W + x + X k, from the class counters: a
+  // 2-way shard 0.554 -> 0.540 ms/frame; the same form for the large launches
+  // cost 1.5 % on C3 (their chunks then leave the class-interleaved order).
+  // A launch with at most one chunk per wave (an 8-way shard's deep
+  // generations) strides over them statically, with no atomics.
   // Every lane of a wave works on the same chunk (the
   // appends are wave-wide); the chunk index is the wave-iteration index the
   // appends' regions and capacities are defined by.
   const unsigned n_chunks = (a.n + 63u) / 64u;
   const unsigned waves_per_block = blockDim.x / 64u;
   const unsigned W = gridDim.x * waves_per_block;
-  const bool dyn = n_chunks >= 3u * W;
+  const bool dyn_all = n_chunks >= 3u * W;            // every chunk from the counters
+  const bool dyn_tail = !dyn_all && n_chunks > W;     // the first chunk static, the rest from the counters
+  const bool dyn = dyn_all || dyn_tail;
   const unsigned X = gridDim.x < (unsigned)kChunkClasses ? gridDim.x : (unsigned)kChunkClasses;
   const unsigned cls = blockIdx.x % X;
   unsigned* ctr = a.cnt->chunk + ((size_t)a.g * kChunkClasses + cls) * kChunkStride;
+  const unsigned c_base = dyn_all ? cls : W + cls;  // the class's k-th counter chunk: c_base + X k
   unsigned c = blockIdx.x * waves_per_block + threadIdx.x / 64u;
-  if (dyn) {
+  if (dyn_all) {
     unsigned k0 = 0;
     if (lane_id() == 0) k0 = atomicAdd(ctr, 1u);
     c = cls + X * (unsigned)__shfl((int)k0, 0, 64);
@@ -1331,7 +1338,7 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
 #ifdef RTAMD_PHASE
     ph_prep += __builtin_amdgcn_s_memtime() - pb;
 #endif
-    c = dyn ? cls + X * (unsigned)__shfl((int)k_next, 0, 64) : c + W;
+    c = dyn ? c_base + X * (unsigned)__shfl((int)k_next, 0, 64) : c + W;
   }
 #ifdef RTAMD_PHASE
   if (lane_id() == 0) {
