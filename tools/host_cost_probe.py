@@ -14,7 +14,7 @@ w, cam, depth = scenes.c3()
 w.upload(0)
 F = 4
 sts = [rtamd.render_stream(False) for _ in range(F)]
-for sh in ((0, 1), (0, 8)):
+for sh in ((0, 1), (0, 8), (0, 64)):
     rows = rtamd.shard_rows(cam.vsize, 8, sh[0], sh[1])
     bufs = [torch.empty((rows, cam.hsize, 3), dtype=torch.float64, device="cuda") for _ in range(F)]
     for f in range(3 * F):
