@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4
+#define RT_ABI_VERSION 5
 
 /* ---- status codes ------------------------------------------------------ */
 enum {
@@ -204,7 +204,10 @@ int rt_render_ex(const rt_scene* scene, const rt_camera_desc* camera,
  * there (torch's current stream is often the null stream).
  * Asynchronous unless `stats` is non-NULL (then it synchronises to read the
  * counters). `n_shards == 1` renders the whole frame. `aa_samples` as in
- * rt_render_aa (1 = `Camera::render`). */
+ * rt_render_aa (1 = `Camera::render`).
+ * Deferred errors: an asynchronous call returns before its frame has run, so
+ * a device-side failure of that frame (see rt_scene_check) is reported by the
+ * next call on the scene, or by rt_scene_check. */
 int rt_render_shard_device(const rt_scene* scene, const rt_camera_desc* camera,
                            uint32_t max_depth, uint32_t aa_samples,
                            uint32_t row_block,
@@ -292,6 +295,22 @@ int rt_quantize_u8(const double* values, size_t n, uint8_t* out);
 const char* rt_last_error(void);
 int rt_abi_version(void);
 int rt_device_count(void);
+
+/* Sizes of the ABI structs as this library was built (ABI 5). A foreign
+ * binding (INTEGRATION.md's Rust `#[repr(C)]` mirrors) asserts its own
+ * `size_of` against these before its first call: rt_stats is filled in full
+ * (sizeof(rt_stats) bytes) by every entry point that takes one. */
+size_t rt_sizeof_shape_desc(void);  /* 680 */
+size_t rt_sizeof_camera_desc(void); /* 160 */
+size_t rt_sizeof_stats(void);       /* 112 */
+
+/* Waits for every render issued on `scene` (on any stream) and reports any
+ * frame the library found incomplete after the fact: an asynchronous render
+ * (rt_render_shard_device[_ex] without stats) is checked on the device, and a
+ * failed check surfaces as RT_ERR_HIP from the NEXT call on the scene, or from
+ * this one. Callers that render asynchronously call it after their last frame
+ * to learn about every frame. RT_OK when all frames were complete. */
+int rt_scene_check(const rt_scene* scene);
 
 #ifdef __cplusplus
 }

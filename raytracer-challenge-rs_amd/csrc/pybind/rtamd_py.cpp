@@ -283,6 +283,10 @@ PYBIND11_MODULE(_rtamd, m) {
       .def("object", &World::object, py::return_value_policy::reference_internal)
       .def("light", &World::light, py::return_value_policy::reference_internal)
       .def("upload", [](const World& w, int device) { w.scene(device); }, py::arg("device") = 0)
+      .def("check", [](const World& w) {  // rt_scene_check: every frame issued on the scene was complete
+        py::gil_scoped_release nogil;
+        check(rt_scene_check(w.scene()), "rt_scene_check");
+      })
       .def("color_at", &World::color_at, py::arg("ray"), py::arg("remaining") = 5)
       .def("is_shadowed", &World::is_shadowed)
       .def("descs_bytes", [](const World& w) {

@@ -71,6 +71,17 @@ int guarded(F&& body) noexcept {
 
 }  // namespace
 
+// rt_last_error's text for entry points in other translation units (rt_ppm.cpp);
+// internal to the library (hidden), not part of the ABI.
+extern "C" __attribute__((visibility("hidden"))) int rtamd_fail(int code, const char* msg) noexcept {
+  try {
+    g_err = msg ? msg : "";
+  } catch (...) {
+    g_err.clear();
+  }
+  return code;
+}
+
 struct rt_scene {
   int device = 0;
   DevScene dev{};
@@ -114,11 +125,14 @@ struct rt_scene {
     std::vector<size_t> send_cap;
     double* recv = nullptr;  // on device 0
     size_t recv_cap = 0;
+    std::vector<hipEvent_t> ev0, ev1;  // per device: around its shard render (stats->ms_kernel)
     void release() {
       for (size_t i = 0; i < send.size(); ++i) {
         (void)hipSetDevice((int)i);
         if (send[i]) (void)hipFree(send[i]);
         if (i < comms.size() && comms[i]) (void)ncclCommDestroy(comms[i]);
+        if (i < ev0.size() && ev0[i]) (void)hipEventDestroy(ev0[i]);
+        if (i < ev1.size() && ev1[i]) (void)hipEventDestroy(ev1[i]);
       }
       (void)hipSetDevice(0);
       if (recv) (void)hipFree(recv);
@@ -576,6 +590,23 @@ int rtamd_nccl_comm_abort(void* comm) {
   return RT_OK;
 }
 int rt_abi_version(void) { return RT_ABI_VERSION; }
+size_t rt_sizeof_shape_desc(void) { return sizeof(rt_shape_desc); }
+size_t rt_sizeof_camera_desc(void) { return sizeof(rt_camera_desc); }
+size_t rt_sizeof_stats(void) { return sizeof(rt_stats); }
+static_assert(sizeof(rt_shape_desc) == 680 && sizeof(rt_camera_desc) == 160 && sizeof(rt_stats) == 112,
+              "ABI struct sizes (include/rt_render.h, INTEGRATION.md)");
+
+int rt_scene_check(const rt_scene* scene) {
+  return guarded([&]() -> int {
+  if (!scene) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
+  rt_scene* s = const_cast<rt_scene*>(scene);
+  std::lock_guard<std::mutex> lk(s->mu);
+  RT_HIP(hipSetDevice(s->device));
+  for (rt_scene::WfSlot& w : s->wfs)
+    if (w.done) RT_HIP(hipEventSynchronize(w.done));  // the workspace's last render (and its check) has run
+  return check_faults(s);
+  });
+}
 
 int rt_device_count(void) {
   return guarded([&]() -> int {
@@ -1148,10 +1179,14 @@ int rt_render_multi(rt_scene* const* scenes, int n_devices, const rt_camera_desc
       }
     }
   }
+  mc.ev0.resize(n_devices, nullptr);
+  mc.ev1.resize(n_devices, nullptr);
   for (int i = 0; i < n_devices; ++i) {
     RT_HIP(hipSetDevice(i));
     int rc = ensure_dev_buffer(&mc.send[i], &mc.send_cap[i], per);
     if (rc != RT_OK) return rc;
+    if (!mc.ev0[i]) RT_HIP(hipEventCreate(&mc.ev0[i]));
+    if (!mc.ev1[i]) RT_HIP(hipEventCreate(&mc.ev1[i]));
   }
   RT_HIP(hipSetDevice(0));
   int rc = ensure_dev_buffer(&mc.recv, &mc.recv_cap, per * n_devices);
@@ -1162,10 +1197,12 @@ int rt_render_multi(rt_scene* const* scenes, int n_devices, const rt_camera_desc
     RT_HIP(hipSetDevice(i));
     std::lock_guard<std::mutex> lk(scenes[i]->mu);
     const uint32_t rows = rt_shard_rows(H, row_block, i, n_devices);
+    if (stats) RT_HIP(hipEventRecord(mc.ev0[i], scenes[i]->stream));
     rc = run_render(scenes[i], to_dev_camera(*camera), nullptr, rows * W * aa_samples, aa_samples, max_depth,
                     row_block, i, n_devices, mc.send[i], scenes[i]->stream, nullptr, nullptr, 0,
                     stats ? &used[i] : nullptr);
     if (rc != RT_OK) return rc;
+    if (stats) RT_HIP(hipEventRecord(mc.ev1[i], scenes[i]->stream));
   }
   if (n_devices > 1) {
     if (ncclGroupStart() != ncclSuccess) return fail(RT_ERR_RCCL, "ncclGroupStart");
@@ -1214,6 +1251,9 @@ int rt_render_multi(rt_scene* const* scenes, int n_devices, const rt_camera_desc
       stats->rays_shadow_traced += x.rays_shadow_traced;
       stats->sphere_tests_executed += x.sphere_tests_executed;
       stats->box_tests_executed += x.box_tests_executed;
+      float ms = 0.f;  // ms_kernel: the slowest device's shard render (HIP events around it)
+      RT_HIP(hipEventElapsedTime(&ms, mc.ev0[i], mc.ev1[i]));
+      stats->ms_kernel = std::max(stats->ms_kernel, (double)ms);
     }
     stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }

@@ -350,7 +350,13 @@ bool other_box(const OtherRec& r, double lo[3], double hi[3]) {
   // (cone.rs:104), a root that need not lie on the cone at all
   if (r.kind != 0 && r.kind != 2 && r.kind != 3) return false;
   double L[3] = {-1.0, -1.0, -1.0}, U[3] = {1.0, 1.0, 1.0};
-  if (r.kind == 3) {  // cylinder: bounded only with finite caps' planes
+  if (r.kind == 3) {  // cylinder: culled only when closed, with finite caps' planes
+    // An OPEN tube stays exhaustive: the culling argument needs "an odd number of
+    // t < 0 roots => the origin lies inside the box" (DESIGN.md §5.2), true for
+    // closed convex solids only. A backward line can cross one wall of an open
+    // tube within [min, max] and leave through the open end, so the tube is a
+    // `containers` entry (intersection.rs:63-90) for a ray that never meets its box.
+    if (!r.closed) return false;
     if (!std::isfinite(r.minimum) || !std::isfinite(r.maximum) || !(r.minimum <= r.maximum)) return false;
     L[1] = r.minimum;
     U[1] = r.maximum;

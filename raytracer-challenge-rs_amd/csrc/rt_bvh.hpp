@@ -22,10 +22,10 @@ std::vector<BvhNode> build_sphere_bvh(std::vector<SphereDiag>& spheres, int leaf
 // The nodes in the pair layout of the per-lane traversal (rt_layout.hpp BvhPair).
 std::vector<BvhPair> pair_layout(const std::vector<BvhNode>& nodes);
 
-// The other bounded records (general-transform spheres, cubes, cylinders
-// with finite caps; rt_layout.hpp OtherRec): other_box gives the padded
-// world box of one (false when the record must stay exhaustive: a cone, an
-// open-ended cylinder, an ill-conditioned transform). build_other_bvh builds
+// The other bounded records (general-transform spheres, cubes, closed
+// cylinders with finite caps; rt_layout.hpp OtherRec): other_box gives the
+// padded world box of one (false when the record must stay exhaustive: a
+// cone, an open or unbounded cylinder, an ill-conditioned transform). build_other_bvh builds
 // the hierarchy over records that all have one (reordered in place into leaf
 // order); empty when there are none.
 bool other_box(const OtherRec& r, double lo[3], double hi[3]);

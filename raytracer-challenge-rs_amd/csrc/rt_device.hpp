@@ -447,11 +447,7 @@ __device__ __forceinline__ V3 pattern_color(const ShadeRec& s, V3 world_point) {
 // f64::powf of the specular term (OCML pow). Out of line: inlined into the
 // fused trace kernels, its polynomial constants were hoisted out of the ray
 // loop into VGPRs and spilled across the BVH traversal.
-#ifdef RTAMD_EXP_NOPOW  // experiment (dev, wrong images): the cost of pow
-__device__ __attribute__((noinline)) double spec_pow(double x, double y) { return x * y; }
-#else
 __device__ __attribute__((noinline)) double spec_pow(double x, double y) { return pow(x, y); }
-#endif
 
 // Material::lighting (material.rs:38-82)
 // `lightv` = (light.position - point).normalize(), which the caller may

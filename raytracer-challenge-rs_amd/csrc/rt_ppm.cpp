@@ -31,8 +31,10 @@ inline int utoa3(unsigned v, char* out) {  // v <= 255
 
 extern "C" {
 
+int rtamd_fail(int code, const char* msg) noexcept;  // rt_api.cpp
+
 int rt_quantize_u8(const double* values, size_t n, uint8_t* out) {
-  if (n && (!values || !out)) return RT_ERR_INVALID_ARGUMENT;
+  if (n && (!values || !out)) return rtamd_fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
   for (size_t i = 0; i < n; ++i) out[i] = (uint8_t)scale_color_component(values[i]);
   return RT_OK;
 }
@@ -106,15 +108,15 @@ extern "C" {
 
 int rt_canvas_to_ppm(const double* rgb, uint32_t width, uint32_t height, char* out, size_t cap,
                      size_t* out_len) {
-  if (!out_len || (width && height && !rgb)) return RT_ERR_INVALID_ARGUMENT;
+  if (!out_len || (width && height && !rgb)) return rtamd_fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
   char hdr[64];
   const size_t hn = (size_t)std::snprintf(hdr, sizeof hdr, "P3\n%u %u\n255\n", width, height);
   const size_t row_doubles = (size_t)width * 3;
   std::vector<size_t> off;
   try {
     off.assign((size_t)height + 1, 0);
-  } catch (...) {
-    return RT_ERR_INVALID_ARGUMENT;  // no memory for the row offsets
+  } catch (...) {  // nothing may throw across the C ABI (as guarded() in rt_api.cpp)
+    return rtamd_fail(RT_ERR_HOST, "out of memory (PPM row offsets)");
   }
   for_rows(height, row_doubles * height, [&](uint32_t r0, uint32_t r1) {
     for (uint32_t j = r0; j < r1; ++j) off[j + 1] = ppm_row_len(rgb + j * row_doubles, width);
@@ -124,7 +126,7 @@ int rt_canvas_to_ppm(const double* rgb, uint32_t width, uint32_t height, char* o
   const size_t len = off[height];
   *out_len = len;
   if (!out) return RT_OK;
-  if (len > cap) return RT_ERR_BUFFER_TOO_SMALL;
+  if (len > cap) return rtamd_fail(RT_ERR_BUFFER_TOO_SMALL, "PPM buffer too small");
   std::memcpy(out, hdr, hn);
   for_rows(height, row_doubles * height, [&](uint32_t r0, uint32_t r1) {
     for (uint32_t j = r0; j < r1; ++j) ppm_row_write(rgb + j * row_doubles, width, out + off[j]);

@@ -1112,15 +1112,7 @@ struct FusedTally {
   unsigned sh_disc = 0, sh_tests = 0, sh_boxes = 0;  // shadow-ray work
   unsigned sh_rays = 0;                              // shadow rays traced
   unsigned hits = 0, refl = 0, refr = 0;             // counted launches: shade_hit runs, children spawned
-#ifdef RTAMD_PHASE
-  unsigned long long ph[5] = {0, 0, 0, 0, 0};  // phase build: prepare, append, spawn, lights, final writes
-#endif
 };
-#ifdef RTAMD_PHASE
-#define PH_MARK(k) do { const unsigned long long pn_ = __builtin_amdgcn_s_memtime(); t.ph[k] += pn_ - ph_last; ph_last = pn_; } while (0)
-#else
-#define PH_MARK(k) do { } while (0)
-#endif
 
 // Everything after the closest hit of ray `slot` (index i of the generation):
 // prepare_computations (intersection.rs:53-105), the reflected / refracted
@@ -1134,9 +1126,6 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
                                             const Hit& h, FusedTally& t) {
   const unsigned L = (unsigned)sc.n_lights;
   const unsigned remaining = a.max_depth - a.g;
-#ifdef RTAMD_PHASE
-  unsigned long long ph_last = __builtin_amdgcn_s_memtime();
-#endif
   bool hit = false, want_refl = false, want_refr = false;
   Comps c{};
   V3 refr_dir = v3(0, 0, 0);
@@ -1161,9 +1150,7 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
   }
   const bool parent = want_refl || want_refr;
   unsigned pbase, rbase, fbase;
-  PH_MARK(0);
   shard_append(a, i / 64, parent ? 1u : 0u, want_refl, want_refr, pbase, rbase, fbase);
-  PH_MARK(1);
   if (!valid) return;
   t.hits += hit; t.refl += want_refl; t.refr += want_refr;
   double* dst = color_dst(a, cam, slot);
@@ -1185,7 +1172,6 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
       (m->reflective > 0.0 && m->transparency > 0.0) ? schlick(c.eyev, c.normal, c.n1, c.n2) : 0.0;
   // surface = Sum over the lights of lighting(..., is_shadowed(over_point, light))
   V3 surface = v3(0.0, 0.0, 0.0);  // fold from (0,0,0) (color.rs:96-103)
-  PH_MARK(2);
   for (unsigned l = 0; l < L; ++l) {
     cLightRec Lr = (cLightRec)sc.lights + l;
     // the shadow ray exactly as World::is_shadowed builds it (world.rs:95-105); its
@@ -1197,18 +1183,13 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
     if (a.skip_shadow && shadow_irrelevant(*m, Lr, sdir, c.normal, term)) {
       // the light is behind the surface: lighting() is the ambient term either way
     } else {
-#ifdef RTAMD_EXP_NOSHADOW  // experiment build (dev, wrong images): the cost of the shadow rays
-      const bool shadowed = false;
-#else
       const bool shadowed = shadow_trace<LANE, QUADS>(sc, a, ls, l, c.over, sdir, dist, t.sh_disc, t.sh_tests,
                                                       t.sh_boxes);
-#endif
       ++t.sh_rays;
       term = lighting(*m, Lr, c.over, c.eyev, c.normal, shadowed, sdir);
     }
     surface = vadd(surface, term);
   }
-  PH_MARK(3);
   if (child_refl >= 0 || child_refr >= 0) {  // the children's colours come later (wf_combine_parents)
     if (pbase != ~0u) {
       ParentRec* pr = a.parents + pbase;
@@ -1217,13 +1198,11 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
       i32x4 tail = {(int)slot, c.obj, child_refl, child_refr};
       __builtin_nontemporal_store(tail, (i32x4*)&pr->slot);
     }
-    PH_MARK(4);
     return;
   }
   const V3 zero = v3(0.0, 0.0, 0.0);  // reflected / refracted colour: black (world.rs:108-109, 117-118)
   const V3 col = shade_color(*m, surface, zero, zero, schlick_r);
   st_d(dst, col.x); st_d(dst + 1, col.y); st_d(dst + 2, col.z);
-  PH_MARK(4);
 }
 
 // One generation of the fast path (see above). PRIMARY: generation 0 of a
@@ -1234,12 +1213,6 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
 // 1.021 -> 0.964 ms/frame, an 8-way shard 0.204 -> 0.184 ms.
 template <bool PRIMARY, bool QUADS, int LANE, bool TALLY>
 __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, DevCamera cam, WfArgs a) {
-#ifdef RTAMD_PHASE
-  // phase-timing build (dev): shader cycles per wave of LDS staging (disc),
-  // traversal (tests) and shading + shadow rays + spawn (boxes), summed over the waves
-  const unsigned long long ph0 = __builtin_amdgcn_s_memtime();
-  unsigned long long ph_stage = 0, ph_trav = 0, ph_prep = 0;
-#endif
   __shared__ int stack_lds[LANE == 3 ? kLaneLdsDepth * kTraceBlock
                            : LANE == 0 ? (kTraceBlock / 64) * (kBvhMaxDepth + 4) : 1];
   extern __shared__ __attribute__((aligned(16))) unsigned char lane_dyn[];
@@ -1282,13 +1255,7 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
     if (lane_id() == 0) k0 = atomicAdd(ctr, 1u);
     c = cls + X * (unsigned)__shfl((int)k0, 0, 64);
   }
-#ifdef RTAMD_PHASE
-  ph_stage = __builtin_amdgcn_s_memtime() - ph0;
-#endif
   while (c < n_chunks) {
-#ifdef RTAMD_PHASE
-    const unsigned long long pa = __builtin_amdgcn_s_memtime();
-#endif
     unsigned k_next = 0;
     if (dyn && lane_id() == 0) k_next = atomicAdd(ctr, 1u);
     const unsigned i = c * 64u + lane_id();
@@ -1313,48 +1280,12 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
         else
           lane_trace<false, LANE == 3>((const BvhNode*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, t.disc,
                                        t.tests, t.boxes, ls.stack, ls.top, ls.n_top);
-#ifdef RTAMD_EXP_TRAV2  // experiment (dev): the traversal a second time (its marginal cost)
-        {
-          Hit h2;
-          hit_init(h2);
-          trace_rest<false, QUADS, true>(sc, o, d, h2, t.disc);
-          if constexpr (LANE == 14)
-            lane_trace_pair<false>(ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h2, t.disc, t.tests, t.boxes,
-                                   ls.stack);
-          else
-            lane_trace<false, LANE == 3>((const BvhNode*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h2, t.disc,
-                                         t.tests, t.boxes, ls.stack);
-          if (h2.key != h.key) a.colors[0] = 1e300;
-        }
-#endif
       }
     }
     hit_finish(h);
-#ifdef RTAMD_PHASE
-    const unsigned long long pb = __builtin_amdgcn_s_memtime();
-    ph_trav += pb - pa;
-#endif
     shade_fused<LANE, QUADS>(sc, cam, a, ls, i, slot, valid, o, d, h, t);
-#ifdef RTAMD_PHASE
-    ph_prep += __builtin_amdgcn_s_memtime() - pb;
-#endif
     c = dyn ? c_base + X * (unsigned)__shfl((int)k_next, 0, 64) : c + W;
   }
-#ifdef RTAMD_PHASE
-  if (lane_id() == 0) {
-    atomicAdd(&work_row(a.cnt)->disc[a.disc_slot], ph_stage);
-    atomicAdd(&work_row(a.cnt)->tests[a.disc_slot], ph_trav);
-    atomicAdd(&work_row(a.cnt)->boxes[a.disc_slot], ph_prep);
-    if (a.disc_slot == WF_CLOSEST) {  // sub-phases of the shading (lane 0's view)
-      atomicAdd(&work_row(a.cnt)->disc[WF_SHADOW], t.ph[0]);
-      atomicAdd(&work_row(a.cnt)->tests[WF_SHADOW], t.ph[1]);
-      atomicAdd(&work_row(a.cnt)->boxes[WF_SHADOW], t.ph[2]);
-      atomicAdd(&work_row(a.cnt)->sh_tests[0], t.ph[3]);
-      atomicAdd(&work_row(a.cnt)->sh_rays[0], t.ph[4]);
-    }
-  }
-  return;
-#endif
   if constexpr (!TALLY) return;
   const unsigned long long s = wave_sum(t.disc), st = wave_sum(t.tests), sb = wave_sum(t.boxes);
   const unsigned long long hs = wave_sum(t.sh_disc), hst = wave_sum(t.sh_tests), hsb = wave_sum(t.sh_boxes);

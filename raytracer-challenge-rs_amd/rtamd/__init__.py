@@ -39,11 +39,14 @@ LIB_PATH = _os.path.join(_os.path.dirname(_here), "lib", "librtamd.so")
 MAX_RECURSION_DEPTH = 5  # reference world.rs:16
 
 
-def render_stream(dedicated_queue=True):
+def render_stream(dedicated_queue=False):
     """A torch stream for rendering frames concurrently (frames in flight,
-    DESIGN.md §5.4): created by the library through
-    hipExtStreamCreateWithCUMask with every CU enabled, which gives it a
-    hardware queue of its own. Plain streams share the GPU's few hardware
-    queues (GPU_MAX_HW_QUEUES), and two frames whose streams share a queue
-    serialise. Lives as long as the process."""
+    DESIGN.md §5.4), made by the library: by default a plain non-blocking
+    stream (it takes one of the process's GPU_MAX_HW_QUEUES hardware queues;
+    raise that variable before HIP initialises when rendering on several).
+    dedicated_queue=True makes it through hipExtStreamCreateWithCUMask with
+    every CU enabled, which gives it a hardware queue of its own, but every
+    cross-stream event wait involving such a stream costs ~1 ms (DESIGN.md
+    §5.4), so use it only for frames that never wait on another stream.
+    Lives as long as the process."""
     return _torch.cuda.ExternalStream(_rtamd._stream_create(bool(dedicated_queue)))

@@ -4,7 +4,7 @@
 The reference holds no golden images (`renders/` is
 git-ignored and the Rust crate cannot be built here), so whole-frame goldens
 come from the C oracle (oracle/rt_oracle.c), which is itself pinned by the
-reference's 49 known-answer tests (tests/test_oracle_kat.py). The fixtures
+reference's 67 known-answer tests (tests/test_oracle_kat.py). The fixtures
 freeze the oracle's output so that (1) a change to the oracle is caught on CPU
 and (2) the GPU path is checked against files, not only against a live oracle.
 

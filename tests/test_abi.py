@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_shard_rows():
     lib = ctypes.CDLL(LIB)
-    assert lib.rt_abi_version() == 4
+    assert lib.rt_abi_version() == 5
     f = lib.rt_shard_rows
     f.restype = ctypes.c_uint32
     f.argtypes = [ctypes.c_uint32] * 4

@@ -345,6 +345,50 @@ def test_other_records_hierarchy_random_rays(rt):
         assert fast.tobytes() == exact.tobytes(), depth
 
 
+def test_open_glass_tubes_stay_containers(rt):
+    """Open finite glass tubes (refractive index 1.5, so n1/n2 sees them):
+    a ray whose origin lies outside a tube's box can have its backward line
+    cross exactly one wall inside [min, max] and leave through the open end,
+    which makes the tube a `containers` entry (intersection.rs:63-90) for a
+    ray that never meets the box. Such tubes stay exhaustive on the fast path;
+    fast == exhaustive bitwise on crafted and random rays."""
+    rng = np.random.default_rng(13)
+    w = rt.World()
+    w.add_object(rt.Plane())
+    tubes = []
+    for i in range(40):
+        t = rt.Cylinder(0.0, 1.0, False)
+        c = rng.uniform([-5, 0, -5], [5, 2, 5])
+        t.set_transform(rt.translation(*c) * rt.rotation_z(float(rng.uniform(-0.4, 0.4))) * rt.scaling(0.5, 1.2, 0.5))
+        t.material.transparency = 0.9
+        t.material.reflective = 0.3
+        t.material.refractive_index = 1.5
+        w.add_object(t)
+        tubes.append(c)
+    for i in range(60):  # glass spheres ahead of the rays: their n1 shows a wrong container
+        s = rt.glass_sphere()
+        r = float(rng.uniform(0.2, 0.5))
+        s.set_transform(rt.translation(*rng.uniform([-6, r, -6], [6, 3, 6])) * rt.scaling(r, r, r))
+        s.material.refractive_index = 2.0
+        w.add_object(s)
+    w.add_light(rt.PointLight(rt.Point(-10, 10, -10), rt.Color(1, 1, 1)))
+    rays = []
+    for c in tubes:  # origin beside the tube, above its top; backward line: one wall, then out the open end
+        for k in range(8):
+            o = np.array(c) + np.array([1.5 + 0.3 * k, 2.2 + 0.2 * k, 0.05 * k])
+            d = np.array([0.6, 0.5 + 0.05 * k, 0.1 * (k - 4)])
+            rays.append(np.hstack([o, d / np.linalg.norm(d)]))
+    o = rng.uniform([-6, -0.5, -6], [6, 3.5, 6], size=(12000, 3))
+    d = rng.normal(size=(12000, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.vstack([np.array(rays), np.hstack([o, d])])
+    for depth in (0, 1, 4):
+        fast, _ = w.color_at_batch(rays, depth, want_stats=False)
+        exact, _ = w.color_at_batch(rays, depth, want_stats=True)
+        assert fast.tobytes() == exact.tobytes(), depth
+    assert rt._rtamd._wf_profile(w, -1, True)["n_other_culled"] == 0  # open tubes are never culled
+
+
 def test_other_records_only_scene_takes_fast_path(rt):
     """A scene without diagonal spheres (only general solids) still takes the
     fast path through the other records' hierarchy, and culls: it executes
