@@ -290,7 +290,7 @@ def main():
         depth = a.depth
     world.upload(local_rank)  # flatten + upload: outside the timed region
     if a.exhaustive:
-        rtamd._rtamd._tuning_set("accel", 0)
+        world.tune("accel", 0)
     W, H, B = cam.hsize, cam.vsize, a.row_block
     # F frames in flight: frame s renders on stream s % F (the library keeps one
     # workspace per stream, so the renders overlap on the device).
@@ -317,7 +317,7 @@ def main():
     else:
         rstreams = [rtamd.render_stream(kind == "cumask") for _ in range(F)]
     if F > 1:  # the frames are the concurrency: no shadow side stream
-        rtamd._rtamd._tuning_set("shadow_stream", 0)
+        world.tune("shadow_stream", 0)
     per_stream = n > 1 and a.assembler in ("stream", "rccl")
     events = not per_stream and (n > 1 or a.event_path)
     fa = None
@@ -551,13 +551,20 @@ def pmc_summary_path(a, W, H, n):
 
 
 def roofline(prof, breakdown, W, H, a, n, ref_work, frame_ms):
-    """f64 VALU roofline of the dominant trace-kernel class (its launches in
-    one frame on rank 0). Its time comes from the launch-carried HIP events of
-    the serialized pass (`prof` = `breakdown`), like the per-class table."""
+    """f64 VALU roofline of the dominant kernel (its launches in one frame on
+    rank 0). Its time comes from the launch-carried HIP events of the
+    serialized pass (`prof` = `breakdown`), like the per-class table. With the
+    persistent frame kernel (the default fast path) that kernel is the whole
+    frame: one launch per frame doing every depth's rays, their shadow rays and
+    the combine, so its executed work is every class's."""
     nd, ng, npl = prof["n_diag"], prof["n_gen"], prof["n_planes"]
-    per_sphere = {"primary": OPS_SPHERE_PRIMARY, "closest": OPS_SPHERE_DIAG, "shadow": OPS_SPHERE_DIAG}
-
     fused = bool(prof.get("fused"))
+    persist = bool(prof.get("persist"))
+    # the persistent kernel traces root rays per lane like every other ray (28 ops per
+    # diagonal sphere test); the generation pipeline's primary launch uses the
+    # shared-origin records (16)
+    per_sphere = {"primary": OPS_SPHERE_DIAG if persist else OPS_SPHERE_PRIMARY, "closest": OPS_SPHERE_DIAG,
+                  "shadow": OPS_SPHERE_DIAG}
     sh_in_r, sh_in_t = prof.get("shadow_rays_in", {}), prof.get("shadow_tests_in", {})
 
     def class_ops(c):
@@ -570,6 +577,16 @@ def roofline(prof, breakdown, W, H, a, n, ref_work, frame_ms):
             ops += (OPS_SPHERE_DIAG * sh_in_t.get(c, 0.0)
                     + sh_in_r.get(c, 0.0) * (OPS_SPHERE_GEN * ng + OPS_PLANE * npl))
         return ops
+
+    def class_survey_ops(c):
+        # SURVEY.md §8(d)'s pricing of the same executed tests: 57 per sphere test, 34 per
+        # plane test, +6 per disc >= 0 (the reference's general 4x4 path; boxes unpriced)
+        ops = (SURVEY_OPS_SPHERE * (prof["tests"][c] + prof["rays"][c] * ng)
+               + SURVEY_OPS_PLANE * prof["rays"][c] * npl + SURVEY_OPS_ROOTS * prof["disc"][c])
+        if fused and c in ("primary", "closest"):
+            ops += (SURVEY_OPS_SPHERE * (sh_in_t.get(c, 0.0) + sh_in_r.get(c, 0.0) * ng)
+                    + SURVEY_OPS_PLANE * sh_in_r.get(c, 0.0) * npl)
+        return ops
     kernels = {}
     for c in ("primary", "closest", "shadow"):
         ms_c = breakdown["ms"][c]
@@ -581,23 +598,37 @@ def roofline(prof, breakdown, W, H, a, n, ref_work, frame_ms):
             kernels[c]["shadow_rays_inside"] = int(sh_in_r.get(c, 0.0))
             kernels[c]["shadow_sphere_tests_inside"] = int(sh_in_t.get(c, 0.0))
     if fused:
-        kernels["shadow"]["note"] = "traced inside the fused primary / closest-hit launches (no launch of its own)"
+        kernels["shadow"]["note"] = "traced inside the fast-path launches (no launch of its own)"
     for c in ("prep", "combine"):
         kernels[c] = {"ms_per_frame": round(breakdown["ms"][c], 4)}
-    dom = max(("primary", "closest", "shadow"), key=lambda c: breakdown["ms"][c])
-    kernel_ms, ms_src = breakdown["ms"][dom], "serialized pass: launch-carried HIP events, one stream"
-    if kernel_ms <= 0:  # megakernel variant selected (RTAMD_WAVES=1): no per-class events
+    ms_src = "serialized pass: launch-carried HIP events, one stream"
+    if persist:
+        dom = "persist"
+        kernel_ms = breakdown["ms"]["closest"]  # the one launch per frame (rt_persist.hip ps_render)
+        ops = class_ops("primary") + class_ops("closest")
+        survey_ops = class_survey_ops("primary") + class_survey_ops("closest")
+        kernels = {"persist": {"ms_per_frame": round(kernel_ms, 4),
+                               "rays": int(prof["rays"]["primary"] + prof["rays"]["closest"]),
+                               "root_rays": int(prof["rays"]["primary"]), "child_rays": int(prof["rays"]["closest"]),
+                               "sphere_tests": int(prof["tests"]["primary"] + prof["tests"]["closest"]),
+                               "box_tests": int(prof["boxes"]["primary"] + prof["boxes"]["closest"]),
+                               "shadow_rays_inside": int(sh_in_r.get("primary", 0.0) + sh_in_r.get("closest", 0.0)),
+                               "tflops": round(ops / (kernel_ms * 1e-3) / 1e12, 3) if kernel_ms > 0 else None},
+                   "combine": {"ms_per_frame": round(breakdown["ms"]["combine"], 4),
+                               "note": "AA averaging only: shade_hit's combine runs inside ps_render"}}
+        kname = ("ps_render (rt_persist.hip): one launch per frame, every recursion depth's rays with their "
+                 "shading, shadow rays and shade_hit combine")
+    else:
+        dom = max(("primary", "closest", "shadow"), key=lambda c: breakdown["ms"][c])
+        kernel_ms = breakdown["ms"][dom]
+        ops = class_ops(dom)
+        survey_ops = class_survey_ops(dom)
+        kname = (f"wf_trace_fused ({dom} launches: closest hit + shading + shadow rays + spawn) in one frame"
+                 if fused else f"wf_trace_{dom}: its launches in one frame")
+    if kernel_ms <= 0:
         return {"bound": "valu_f64", "kernel": None, "achieved": None, "peak": PEAK_F64_VALU_TFLOPS,
                 "unit": "TFLOP/s", "frac": None, "traffic": None}
-    ops = class_ops(dom)
     achieved = ops / (kernel_ms * 1e-3) / 1e12
-    # SURVEY.md §8(d)'s pricing of the same executed tests: 57 per sphere test, 34 per
-    # plane test, +6 per disc >= 0 (the reference's general 4x4 path; boxes unpriced)
-    survey_ops = (SURVEY_OPS_SPHERE * (prof["tests"][dom] + prof["rays"][dom] * ng)
-                  + SURVEY_OPS_PLANE * prof["rays"][dom] * npl + SURVEY_OPS_ROOTS * prof["disc"][dom])
-    if fused and dom in ("primary", "closest"):
-        survey_ops += (SURVEY_OPS_SPHERE * (sh_in_t.get(dom, 0.0) + sh_in_r.get(dom, 0.0) * ng)
-                       + SURVEY_OPS_PLANE * sh_in_r.get(dom, 0.0) * npl)
     achieved_survey = survey_ops / (kernel_ms * 1e-3) / 1e12
     traffic, traffic_src, counters = None, None, None
     pmc_path = pmc_summary_path(a, W, H, n)
@@ -615,13 +646,13 @@ def roofline(prof, breakdown, W, H, a, n, ref_work, frame_ms):
                 counters = {"valu_busy": round(4.0 * c["SQ_ACTIVE_INST_VALU"] / simd_cycles, 3),
                             "f64_valu_insts_per_frame": c["SQ_INSTS_VALU_ADD_F64"] + c["SQ_INSTS_VALU_MUL_F64"]
                             + c["SQ_INSTS_VALU_FMA_F64"] + c["SQ_INSTS_VALU_TRANS_F64"],
-                            "valu_insts_per_frame": c["SQ_INSTS_VALU"]}
+                            "valu_insts_per_frame": c["SQ_INSTS_VALU"],
+                            "build": pm.get("build")}
         except Exception:
             pass
     return {
         "bound": "valu_f64",
-        "kernel": (f"wf_trace_fused ({dom} launches: closest hit + shading + shadow rays + spawn) in one frame"
-                   if fused else f"wf_trace_{dom}: its launches in one frame"),
+        "kernel": kname,
         "achieved": round(achieved, 3),
         "peak": PEAK_F64_VALU_TFLOPS,
         "unit": "TFLOP/s",
@@ -633,10 +664,12 @@ def roofline(prof, breakdown, W, H, a, n, ref_work, frame_ms):
         "traffic": traffic,
         "kernel_ms": round(kernel_ms, 4),
         "kernel_ms_source": ms_src,
+        "kernel_regime": "serialized (one frame at a time); the timed region keeps frames in flight, so its "
+                         "per-frame time (ms_per_step) can be below kernel_ms",
         "ops_per_frame": ops,
-        "per_unit": f"{OPS_SPHERE_DIAG} f64 ops per sphere test ({OPS_SPHERE_PRIMARY} for primary rays), "
-                    f"{OPS_BOX} per BVH box test, {OPS_PLANE} per plane test, {OPS_ROOTS} per root pair "
-                    f"(DESIGN.md 'Roofline'); executed tests counted on the device",
+        "per_unit": f"{OPS_SPHERE_DIAG} f64 ops per sphere test ({OPS_SPHERE_PRIMARY} for the generation "
+                    f"pipeline's primary rays), {OPS_BOX} per BVH box test, {OPS_PLANE} per plane test, "
+                    f"{OPS_ROOTS} per root pair (DESIGN.md 'Roofline'); executed tests counted on the device",
         "traversal": "bvh" if prof["bvh"] else "exhaustive",
         "reference_work_tflops": round(ref_work / (frame_ms * 1e-3) / 1e12, 3),
         "traffic_source": traffic_src,

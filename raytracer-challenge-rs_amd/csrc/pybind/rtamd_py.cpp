@@ -58,7 +58,8 @@ extern "C" int rtamd_nccl_comm_init(int nranks, const unsigned char* id, size_t 
 extern "C" int rtamd_nccl_comm_abort(void* comm);
 extern "C" int rtamd_nccl_gather_f64(const double* send, double* recv, size_t count, int root, void* comm, void* stream);
 extern "C" int rtamd_nccl_comm_destroy(void* comm);
-extern "C" int rtamd_wf_profile(const rt_scene* s, int enable, double out[34]);
+extern "C" int rtamd_wf_profile(const rt_scene* s, int enable, double out[35]);
+extern "C" int rtamd_scene_tuning_set(const rt_scene* s, const char* key, int value);
 
 PYBIND11_MODULE(_rtamd, m) {
   m.doc() = "MI355X-native render path of raytracer-challenge-rs (host API over the C-ABI)";
@@ -283,6 +284,9 @@ PYBIND11_MODULE(_rtamd, m) {
       .def("object", &World::object, py::return_value_policy::reference_internal)
       .def("light", &World::light, py::return_value_policy::reference_internal)
       .def("upload", [](const World& w, int device) { w.scene(device); }, py::arg("device") = 0)
+      .def("tune", [](const World& w, const std::string& k, int v) {  // this scene's render-time knob (dev)
+        check(rtamd_scene_tuning_set(w.scene(), k.c_str(), v), "tuning");
+      })
       .def("check", [](const World& w) {  // rt_scene_check: every frame issued on the scene was complete
         py::gil_scoped_release nogil;
         check(rt_scene_check(w.scene()), "rt_scene_check");
@@ -433,7 +437,7 @@ PYBIND11_MODULE(_rtamd, m) {
       }, py::arg("max_depth") = 5)
       .def("render_to", &SceneParser::render_to, py::arg("path"), py::arg("max_depth") = 5);
   m.def("_wf_profile", [](const World& w, int enable, bool read) {
-    double o[34] = {0};
+    double o[35] = {0};
     check(rtamd_wf_profile(w.scene(), enable, read ? o : nullptr), "wf_profile");
     py::dict d;
     if (read) {
@@ -452,6 +456,7 @@ PYBIND11_MODULE(_rtamd, m) {
       py::dict shr, sht;
       shr["primary"] = o[29]; shr["closest"] = o[30]; sht["primary"] = o[31]; sht["closest"] = o[32];
       d["shadow_rays_in"] = shr; d["shadow_tests_in"] = sht; d["fused"] = (bool)o[33];
+      d["persist"] = (bool)o[34];
     }
     return d;
   }, py::arg("world"), py::arg("enable") = -1, py::arg("read") = true);

@@ -37,6 +37,9 @@ thread_local std::string g_err;
 int g_bvh_leaf = 2;     // BVH leaf size at scene creation (tuning knob "bvh_leaf")
 int g_bvh_ct = 70;      // SAH node-visit cost in percent of a sphere test (tuning knob "bvh_ct")
 int g_lb_res = 256;     // light-buffer cells per cube-map face edge at scene creation, 0 = none ("lb_res")
+// render-time tuning copied into every scene at its creation (rt_scene::tune)
+std::mutex g_tune_mu;
+WfTuning g_tune_defaults;
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -142,6 +145,7 @@ struct rt_scene {
   std::mutex multi_mu;
   int prof_mask = (1 << WF_NCLASS) - 1;
   int n_objects = 0, n_lights = 0;
+  WfTuning tune;  // this scene's render-time tuning (read under `mu` by every render)
   ~rt_scene() {
     for (WfSlot& w : wfs)
       if (w.done) (void)hipEventDestroy(w.done);
@@ -330,10 +334,13 @@ bool valid_aa(uint32_t aa) { return aa == 1 || aa == 2 || aa == 4 || aa == 8 || 
 // frame. The calibration is dropped, so the next frame recalibrates.
 int check_faults(rt_scene* s) {
   for (rt_scene::WfSlot& w : s->wfs)
-    if (w.wf->fault()) {
+    if (const int f = w.wf->fault()) {
       w.wf->clear_fault();
-      return fail(RT_ERR_HIP, "wavefront queue check: a generation's ray count differed from its calibrated "
-                              "launch size in an earlier frame (rays may be missing from that frame)");
+      if (f == 1)
+        return fail(RT_ERR_HIP, "wavefront queue check: a generation's ray count differed from its calibrated "
+                                "launch size in an earlier frame (rays may be missing from that frame)");
+      return fail(RT_ERR_HIP, "persistent frame kernel: a wait exceeded its time bound in an earlier frame (that "
+                              "frame was abandoned incomplete)");
     }
   return RT_OK;
 }
@@ -365,7 +372,7 @@ int run_render(rt_scene* s, const DevCamera& cam, const double* d_rays, uint32_t
   const unsigned wf_flags = ((flags & RT_RENDER_EXHAUSTIVE) ? WF_EXHAUSTIVE : 0u) | (used ? WF_COUNT : 0u);
   if (e == hipSuccess)
     e = w->wf->render(s->dev, cam, d_rays == nullptr, d_rays, n_tasks, aa, max_depth, row_block, shard, n_shards,
-                      d_out, stream, sig, stats_out, ms_out, s->wfs.size() == 1, wf_flags);
+                      d_out, stream, sig, stats_out, ms_out, s->tune, s->wfs.size() == 1, wf_flags);
   if (e == hipSuccess) e = hipEventRecord(w->done, stream);
   if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("wavefront render: ") + hipGetErrorString(e));
   if (used) *used = w;
@@ -402,8 +409,8 @@ const char* rt_last_error(void) { return g_err.c_str(); }
 // ms[5] (primary, closest, shadow, prep, combine), rays[3], disc[3],
 // n_diag, n_gen, n_planes, n_lights, n_quads, tests[3], boxes[3], bvh,
 // n_bvh_nodes, bvh_depth, n_obvh_nodes, n_other_culled, lb_res, lb_items, sh_rays[2], sh_tests[2]
-// (shadow rays / sphere tests inside the fused primary / secondary launches), fused.
-int rtamd_wf_profile(const rt_scene* cs, int enable, double out[34]) {
+// (shadow rays / sphere tests inside the fused primary / secondary launches), fused, persist.
+int rtamd_wf_profile(const rt_scene* cs, int enable, double out[35]) {
   if (!cs) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
   rt_scene* s = const_cast<rt_scene*>(cs);
   std::lock_guard<std::mutex> lk(s->mu);
@@ -446,54 +453,20 @@ int rtamd_wf_profile(const rt_scene* cs, int enable, double out[34]) {
     out[28] = s->dev.lb_cells ? s->dev.lb_n_items : 0;
     for (int i = 0; i < 2; ++i) { out[29 + i] = p.sh_rays[i]; out[31 + i] = p.sh_tests[i]; }
     out[33] = p.fused;
+    out[34] = p.persist;
   }
   return RT_OK;
 }
 
-// Development-only tuning hook (not declared in include/rt_render.h).
+// Development-only tuning hooks (not declared in include/rt_render.h).
+// rtamd_tuning_set: the scene-creation knobs (lb_res, bvh_leaf, bvh_ct) and
+// the render-time defaults copied into scenes created afterwards;
+// rtamd_scene_tuning_set: one scene's render-time knobs (WfTuning).
 int rtamd_tuning_set(const char* key, int value) {
+  return guarded([&]() -> int {
   if (key && std::strcmp(key, "lb_res") == 0) {
     if (value < 0 || value > 512) return fail(RT_ERR_INVALID_ARGUMENT, "lb_res must be in [0, 512]");
     g_lb_res = value;
-    return RT_OK;
-  }
-  if (key && std::strcmp(key, "shadow_lb") == 0) {
-    rtamd::g_wf_shadow_lb = value != 0;
-    return RT_OK;
-  }
-  if (key && std::strcmp(key, "treelet") == 0) {
-    rtamd::g_wf_treelet = value != 0;
-    return RT_OK;
-  }
-  if (key && std::strcmp(key, "treelet_deltas") == 0) {
-    rtamd::g_wf_treelet_deltas = value != 0;
-    return RT_OK;
-  }
-  if (key && std::strcmp(key, "image") == 0) {
-    if (value != 0 && value != 1 && value != 3) return fail(RT_ERR_INVALID_ARGUMENT, "image must be 0, 1 or 3");
-    rtamd::g_wf_image = value;
-    return RT_OK;
-  }
-
-  if (key && std::strcmp(key, "shadow_stream") == 0) {
-    if (value < 0 || value > 2) return fail(RT_ERR_INVALID_ARGUMENT, "shadow_stream must be 0, 1 or 2");
-    rtamd::g_wf_shadow_stream = value;
-    return RT_OK;
-  }
-  if (key && std::strcmp(key, "adaptive_block") == 0) {
-    rtamd::g_wf_adaptive_block = value != 0;
-    return RT_OK;
-  }
-  if (key && std::strcmp(key, "skip_shadow") == 0) {
-    rtamd::g_wf_skip_shadow = value != 0;
-    return RT_OK;
-  }
-  if (key && std::strcmp(key, "corrupt_calibration") == 0) {  // test hook: exercises the queue check
-    rtamd::Wavefront::g_corrupt_calibration = value != 0;
-    return RT_OK;
-  }
-  if (key && std::strcmp(key, "accel") == 0) {
-    rtamd::g_wf_accel = value != 0;
     return RT_OK;
   }
   if (key && std::strcmp(key, "bvh_ct") == 0) {
@@ -506,7 +479,24 @@ int rtamd_tuning_set(const char* key, int value) {
     g_bvh_leaf = value;
     return RT_OK;
   }
-  return fail(RT_ERR_INVALID_ARGUMENT, "unknown tuning key");
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  const int r = wf_tuning_apply(g_tune_defaults, key, value);
+  if (r < 0) return fail(RT_ERR_INVALID_ARGUMENT, std::string("bad value for tuning key ") + key);
+  if (r == 0) return fail(RT_ERR_INVALID_ARGUMENT, "unknown tuning key");
+  return RT_OK;
+  });
+}
+int rtamd_scene_tuning_set(const rt_scene* scene, const char* key, int value) {
+  return guarded([&]() -> int {
+  if (!scene) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
+  rt_scene* s = const_cast<rt_scene*>(scene);
+  std::lock_guard<std::mutex> lk(s->mu);
+  const int r = wf_tuning_apply(s->tune, key, value);
+  if (r < 0) return fail(RT_ERR_INVALID_ARGUMENT, std::string("bad value for tuning key ") + (key ? key : ""));
+  if (r == 0) return fail(RT_ERR_INVALID_ARGUMENT, "unknown render-time tuning key (scene-creation keys: "
+                                                   "rtamd_tuning_set before the scene is created)");
+  return RT_OK;
+  });
 }
 // Development hook (not in the public ABI): a non-blocking stream on the
 // current device; cu_masked = 1 creates it through hipExtStreamCreateWithCUMask
@@ -822,6 +812,10 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
 
   rt_scene* s = new rt_scene();
   s->device = device;
+  {
+    std::lock_guard<std::mutex> tlk(g_tune_mu);
+    s->tune = g_tune_defaults;
+  }
   auto cleanup = [&](int rc) {
     rt_scene_destroy(s);
     return rc;

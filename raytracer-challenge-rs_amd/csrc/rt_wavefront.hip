@@ -16,21 +16,37 @@
 #include <cstring>
 
 #include "rt_device.hpp"
+#include "rt_trace.hpp"
 #include "rt_wavefront.hpp"
 
 #pragma clang fp contract(off)
 
 namespace rtamd {
 
-constexpr int kTraceBlock = 1024;  // trace kernels: 16 waves, one LDS image per block
-int g_wf_accel = 1;        // 1 = BVH traversal (fused generations) unless the exhaustive loop is asked for
-int g_wf_skip_shadow = 1;  // fast path: leave out shadow rays that cannot change the colour
-int g_wf_shadow_lb = 1;    // 1 = shadow rays through the light buffer (DESIGN.md "Light buffer")
-int g_wf_image = 0;        // tuning knob ("image", tests): 0 = the fused kernels pick their scene image,
-                           // 3 / 1 = force the global-memory image with an LDS / scratch stack
-int g_wf_treelet = 1;         // tuning knob ("treelet"): the global-memory image's top nodes in LDS
-int g_wf_treelet_deltas = 0;  // tuning knob ("treelet_deltas"): the light buffer's distances staged first
 constexpr int kWfBlock = 256;      // prep / shadow / combine
+
+int wf_tuning_apply(WfTuning& t, const char* key, int value) {
+  struct Knob {
+    const char* name;
+    int WfTuning::*field;
+    int lo, hi;
+  };
+  static const Knob knobs[] = {
+      {"accel", &WfTuning::accel, 0, 1},           {"persist", &WfTuning::persist, 0, 1},
+      {"skip_shadow", &WfTuning::skip_shadow, 0, 1}, {"shadow_lb", &WfTuning::shadow_lb, 0, 1},
+      {"image", &WfTuning::image, 0, 3},           {"treelet", &WfTuning::treelet, 0, 1},
+      {"treelet_deltas", &WfTuning::treelet_deltas, 0, 1}, {"shadow_stream", &WfTuning::shadow_stream, 0, 2},
+      {"adaptive_block", &WfTuning::adaptive_block, 0, 1},
+      {"corrupt_calibration", &WfTuning::corrupt_calibration, 0, 1}};
+  if (!key) return 0;
+  for (const Knob& k : knobs) {
+    if (std::strcmp(key, k.name) != 0) continue;
+    if (value < k.lo || value > k.hi || (k.field == &WfTuning::image && value == 2)) return -1;
+    t.*(k.field) = value;
+    return 1;
+  }
+  return 0;
+}
 
 #define WF_CHECK(x)                        \
   do {                                     \
@@ -38,7 +54,6 @@ constexpr int kWfBlock = 256;      // prep / shadow / combine
     if (_e != hipSuccess) return _e;       \
   } while (0)
 
-__device__ __forceinline__ unsigned lane_id() { return __lane_id(); }
 
 // The calling wave's row of the work counters (WfCounters): lane 0 adds the
 // wave's totals there.
@@ -60,37 +75,7 @@ __device__ __forceinline__ unsigned wave_append(unsigned* counter, bool want, un
   return base + rank * per;
 }
 
-// AA sample offsets of Camera::get_offsets (camera.rs:92-126), per count
-// 1, 2, 4, 8, 16 at offsets 0, 1, 3, 7, 15 of the table.
-__constant__ double kAaOffsets[31][2] = {
-    {0.5, 0.5},
-    {0.25, 0.5}, {0.75, 0.5},
-    {0.25, 0.25}, {0.75, 0.25}, {0.25, 0.75}, {0.75, 0.75},
-    {0.25, 0.25}, {0.5, 0.25}, {0.75, 0.25}, {0.25, 0.5}, {0.75, 0.5}, {0.25, 0.75}, {0.5, 0.75}, {0.75, 0.75},
-    {0.125, 0.125}, {0.375, 0.125}, {0.625, 0.125}, {0.875, 0.125},
-    {0.125, 0.375}, {0.375, 0.375}, {0.625, 0.375}, {0.875, 0.375},
-    {0.125, 0.625}, {0.375, 0.625}, {0.625, 0.625}, {0.875, 0.625},
-    {0.125, 0.875}, {0.375, 0.875}, {0.625, 0.875}, {0.875, 0.875}};
 
-// Generation-0 ray order of a camera shard: the shard's local rows in bands
-// of 8, each band in tiles of 8 columns, AA samples innermost, so one wave
-// holds an 8x8 pixel tile (coherent rays for the BVH traversal). Returns the
-// pixel (x, local row) and the sample index of ray i.
-__device__ __forceinline__ void gen0_pixel(const WfArgs& a, uint32_t hsize, uint32_t i, uint32_t& x, uint32_t& lr,
-                                           uint32_t& smp) {
-  const uint32_t p = i / a.aa;
-  smp = i - p * a.aa;
-  const uint32_t band = p / (8u * hsize);
-  const uint32_t r0 = band * 8u;
-  const uint32_t R = min(8u, a.rows - r0);
-  const uint32_t j = p - band * 8u * hsize;
-  const uint32_t t = j / (8u * R);
-  const uint32_t w = min(8u, hsize - 8u * t);
-  const uint32_t within = j - t * 8u * R;
-  const uint32_t wy = within / w;
-  x = 8u * t + (within - wy * w);
-  lr = r0 + wy;
-}
 
 // Queue appends without block barriers or hot counters (DESIGN.md "Sharded
 // queues"). The queues of a generation are split into kShards regions of a
@@ -163,7 +148,7 @@ __device__ __forceinline__ unsigned shard_slot(const unsigned* pre, unsigned cap
 __device__ __forceinline__ void wf_ray(const WfArgs& a, const DevCamera& cam, unsigned i, V3& o, V3& d) {
   if (a.g == 0 && a.camera_mode) {
     uint32_t x, lr, smp;
-    gen0_pixel(a, cam.hsize, i, x, lr, smp);
+    gen0_pixel(a.aa, a.rows, cam.hsize, i, x, lr, smp);
     const uint32_t blk = lr / a.row_block, off = lr - blk * a.row_block;
     const uint32_t y = (blk * a.n_shards + a.shard) * a.row_block + off;
     if (a.aa == 1) {
@@ -213,22 +198,6 @@ __device__ __forceinline__ void shadow_result(const DevScene& sc, const WfArgs& 
   dst[0] = c.x; dst[1] = c.y; dst[2] = c.z;
 }
 
-// A shadow ray whose answer cannot change the colour (DESIGN.md "Skipped
-// shadow rays"): with the light behind the surface, lighting() returns
-// `ambient` in shadow and `ambient + 0 + 0` in light (material.rs:23-87),
-// bit-identical unless a component of ambient is -0 or NaN. Evaluated with
-// the operations lighting() itself performs; patterned materials are never
-// skipped. Returns whether it is, and that ambient value.
-// `lightv` = (light.position - over).normalize(), the shadow ray's direction.
-__device__ __forceinline__ bool shadow_irrelevant(const ShadeRec& m, cLightRec L, V3 lightv, V3 normal, V3& ambient) {
-  if (m.pattern_kind >= 0) return false;
-  if (!(vdot(lightv, normal) < 0.0)) return false;
-  const V3 effective_color = vmul(v3(m.color[0], m.color[1], m.color[2]),
-                                  v3(L->intensity[0], L->intensity[1], L->intensity[2]));
-  ambient = vscale(effective_color, m.ambient);
-  auto plain = [](double x) { return x == x && !(x == 0.0 && signbit(x)); };
-  return plain(ambient.x) && plain(ambient.y) && plain(ambient.z);
-}
 
 // ------------------------------------------------------------ primary records
 // Per diagonal sphere: s (inverse diagonal), o' = s*o + t for the camera origin
@@ -518,394 +487,6 @@ __device__ __forceinline__ void prep_one(const DevScene& sc, const WfArgs& a, un
   a.nodes[slot] = nd;
 }
 
-// ------------------------------------------------------------ BVH traversal
-// Exact culling (DESIGN.md "Exact culling"): the wave traverses the sphere
-// BVH together (wave-uniform stack in LDS, wave-uniform 64-B node loads) and
-// skips a child only when NO lane's ray meets its padded box within
-// [0, t_hi] (t_hi = the lane's current nearest hit, or the light distance for
-// shadow rays). A sphere the exhaustive loop would hit always lies in a box
-// that passes, and the per-lane results are order-independent minima, so the
-// results are bit-identical to the exhaustive loop. Lanes whose rays miss a
-// visited leaf still test its spheres (harmless: exhaustive work).
-typedef const RT_CONST BvhNode* cBvhNode;
-typedef const RT_CONST PrimRec* cPrimRec;
-
-// The per-lane traversal's slab test runs in binary32 on an interval that is
-// widened to contain the exact (real-arithmetic) one; DESIGN.md §5.2 has the
-// error bound. Per ray and axis: inv = 1/d, and the plane constants
-// c = o*inv -/+ delta with delta = 2^-20 |inv| (M + |o|), where M bounds every
-// box coordinate on that axis (the root's children); the computed entry
-// (exit) distance fma(corner, inv, -c) then never exceeds (falls short of)
-// the exact one: its rounding error is below 2^-23 |inv| (M + |o|) = delta/8.
-// An axis whose direction is (nearly) zero or whose origin is huge / NaN is
-// not used for culling at all (interval (-inf, +inf)).
-struct SlabRay {
-  float inv[3], c_lo[3], c_hi[3];
-};
-__device__ __forceinline__ SlabRay slab_ray(V3 o, V3 d, const float* M) {
-  SlabRay r;
-  const double oa[3] = {o.x, o.y, o.z}, da[3] = {d.x, d.y, d.z};
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    if (fabs(da[a]) >= 0x1p-60 && fabs(oa[a]) <= 0x1p60 && M[a] <= 0x1p60f) {  // NaN fails
-      const double inv = 1.0 / da[a];
-      const double oinv = oa[a] * inv;
-      const double delta = 0x1p-20 * fabs(inv) * ((double)M[a] + fabs(oa[a]));
-      const float on = (float)(oinv + delta), of = (float)(oinv - delta);
-      r.inv[a] = (float)inv;
-      r.c_lo[a] = inv >= 0.0 ? on : of;  // the lo plane is the entry plane when inv >= 0
-      r.c_hi[a] = inv >= 0.0 ? of : on;
-    } else {
-      r.inv[a] = 0.0f;
-      r.c_lo[a] = INFINITY;
-      r.c_hi[a] = -INFINITY;
-    }
-  }
-  return r;
-}
-// binary32 upper bound of a non-negative binary64 distance: RN(x) is within
-// 2^-23 of x relative to it, and RN(f * (1 + 2^-22)) > f * (1 + 2^-23)
-// (0 and inf map to themselves).
-__device__ __forceinline__ float f32_up(double x) { return (float)x * (1.0f + 0x1p-22f); }
-// max(entry, 0) <= min(exit, t_hi): the ray may meet the box within [0, t_hi]
-// (t_hi >= 0). `t_in` = the widened entry distance (child ordering only).
-template <typename P>  // P: constant-address (scalar loads) or generic (per-lane loads) float pointer
-__device__ __forceinline__ bool slab_hit32(P lo, P hi, const SlabRay& r, float t_hi, float& t_in) {
-  const float x0 = fmaf(lo[0], r.inv[0], -r.c_lo[0]), x1 = fmaf(hi[0], r.inv[0], -r.c_hi[0]);
-  const float y0 = fmaf(lo[1], r.inv[1], -r.c_lo[1]), y1 = fmaf(hi[1], r.inv[1], -r.c_hi[1]);
-  const float z0 = fmaf(lo[2], r.inv[2], -r.c_lo[2]), z1 = fmaf(hi[2], r.inv[2], -r.c_hi[2]);
-  const float tmin = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), 0.0f));
-  const float tmax = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), t_hi));
-  t_in = tmin;
-  return tmin <= tmax;
-}
-
-template <bool PRIMARY, bool SHADOW>
-__device__ __forceinline__ void bvh_trace(const DevScene& sc, cPrimRec prim, int* stk, V3 o, V3 d, double t_shadow,
-                                          Hit& h, unsigned& n_disc, unsigned& n_tests, unsigned& n_boxes) {
-  hit_init(h);
-  const cBvhNode nodes = (cBvhNode)sc.bvh;
-  float M[3];
-  for (int a = 0; a < 3; ++a)
-    M[a] = fmaxf(fmaxf(fabsf(nodes->lo[0][a]), fabsf(nodes->hi[0][a])),
-                 fmaxf(fabsf(nodes->lo[1][a]), fabsf(nodes->hi[1][a])));
-  const SlabRay sr = slab_ray(o, d, M);
-  const float t_sh = SHADOW ? f32_up(t_shadow) : 0.0f;
-  const cSphereDiag sd = (cSphereDiag)sc.sph_diag;
-  int sp = 1;
-  stk[0] = 0;
-  while (sp > 0) {
-    --sp;
-    const int e = __builtin_amdgcn_readfirstlane(stk[sp]);
-    if (e < 0) {  // leaf: first << 7 | count
-      const int code = -(e + 1);
-      const int first = code >> 7, cnt = code & 127;
-      for (int k = first; k < first + cnt; ++k) {
-        if constexpr (PRIMARY) {
-          const cPrimRec r = prim + k;
-          const double dx = r->s[0] * d.x, dy = r->s[1] * d.y, dz = r->s[2] * d.z;
-          sphere_adc<false>(dx * dx + dy * dy + dz * dz, dx * r->op[0] + dy * r->op[1] + dz * r->op[2], r->c,
-                            [&] { return (int)sd[k].meta; }, h, n_disc);
-        } else {
-          diag_test<SHADOW>(sd + k, o, d, h, n_disc);
-        }
-      }
-      n_tests += (unsigned)cnt;
-      if constexpr (SHADOW) {
-        if (!__any(!(h.key >= 0 && h.t < t_shadow))) break;  // every lane is shadowed
-      }
-      continue;
-    }
-    const cBvhNode nd = nodes + e;
-    const float t_hi = SHADOW ? t_sh : f32_up(h.t);
-    const int c0 = nd->child[0], c1 = nd->child[1];
-    float t0, t1;
-    const bool h0 = slab_hit32(nd->lo[0], nd->hi[0], sr, t_hi, t0);
-    const bool h1 = c1 != kBvhEmpty && slab_hit32(nd->lo[1], nd->hi[1], sr, t_hi, t1);
-    n_boxes += 2;
-    const bool any0 = __any(h0), any1 = __any(h1);
-    // push the far child first so the near one (by the lead lane's direction) pops first
-    const int axis = nd->axis;
-    const double dax = axis == 0 ? d.x : axis == 1 ? d.y : d.z;
-    const bool flip = __builtin_amdgcn_readfirstlane(dax < 0.0 ? 1 : 0) != 0;
-    const int near_c = flip ? c1 : c0, far_c = flip ? c0 : c1;
-    const bool near_hit = flip ? any1 : any0, far_hit = flip ? any0 : any1;
-    if (far_hit) stk[sp++] = far_c;
-    if (near_hit) stk[sp++] = near_c;
-  }
-}
-
-// Per-lane traversal for incoherent rays (secondary and shadow generations)
-// over the binary node layout in global memory (scenes whose image does not
-// fit in LDS): every lane walks the BVH on its own (near child first by its
-// own direction, a private stack), so a wave pays for the longest path
-// instead of the union of 64 paths. Same culling rule and the same exactness
-// argument as the wave traversal above.
-// LDS_STACK: the stack lives in LDS, entry k of lane t at lds[k * kTraceBlock + t]
-// (needs bvh_depth <= kLaneLdsDepth); otherwise in private (scratch) memory.
-// `h` arrives initialised (it may already hold the planes' nearest hit, which
-// tightens the culling).
-__device__ __forceinline__ void node_chunks(const BvhNode* nodes, int e, uint4& q0, uint4& q1, uint4& q2, uint4& q3) {
-  const uint4* b = reinterpret_cast<const uint4*>(nodes);
-  q0 = b[4 * e]; q1 = b[4 * e + 1]; q2 = b[4 * e + 2]; q3 = b[4 * e + 3];
-}
-template <bool SHADOW>
-__device__ __forceinline__ void leaf_sphere_test(const SphereDiag* sd, int k, V3 o, V3 d, Hit& h, unsigned& n_disc) {
-  const SphereDiag& r = sd[k];
-  const double s0 = r.s[0], s1 = r.s[1], s2 = r.s[2];
-  sphere_test<SHADOW>(s0 * o.x + r.t[0], s1 * o.y + r.t[1], s2 * o.z + r.t[2], s0 * d.x, s1 * d.y, s2 * d.z,
-                      [&] { return (int)r.meta; }, h, n_disc);
-}
-
-// With a treelet (the global-memory image), the first n_top nodes (breadth-first:
-// the top levels) are read from their LDS copy `top`, the rest from `nodes`.
-template <bool SHADOW, bool LDS_STACK>
-__device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDiag* sd, const float* M, bool has_bvh,
-                                           V3 o, V3 d, double t_shadow, Hit& h, unsigned& n_disc, unsigned& n_tests,
-                                           unsigned& n_boxes, int* lds, const BvhNode* top = nullptr,
-                                           int n_top = 0) {
-  const SlabRay sr = slab_ray(o, d, M);
-  float t_hi = f32_up(SHADOW ? t_shadow : h.t);
-  int pstk[LDS_STACK ? 1 : kBvhMaxDepth + 4];
-  auto stk = [&](int k) -> int& { if constexpr (LDS_STACK) return lds[k * kTraceBlock]; else return pstk[k]; };
-  int sp = 0;
-  auto pop = [&]() { return sp > 0 ? stk(--sp) : kBvhEmpty; };
-  int e = (SHADOW && h.key >= 0 && h.t < t_shadow) || !has_bvh ? kBvhEmpty : 0;
-  // a node visit: both children's boxes, the one entered first visited first
-  auto visit = [&]() {
-    // the whole 64-B node in four 16-B loads: lo[0], lo[1], hi[0], hi[1], child[2], axis, pad
-    // (explicit address spaces: the two paths stay LDS and global loads)
-    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-    u32x4 r0, r1, r2, r3;
-    if (e < n_top) {
-      typedef __attribute__((address_space(3))) const u32x4 lq;
-      lq* b = (lq*)(top + e);
-      r0 = b[0]; r1 = b[1]; r2 = b[2]; r3 = b[3];
-    } else {
-      typedef __attribute__((address_space(1))) const u32x4 gq;
-      gq* b = (gq*)(nodes + e);
-      r0 = b[0]; r1 = b[1]; r2 = b[2]; r3 = b[3];
-    }
-    const uint4 q0 = make_uint4(r0.x, r0.y, r0.z, r0.w), q1 = make_uint4(r1.x, r1.y, r1.z, r1.w);
-    const uint4 q2 = make_uint4(r2.x, r2.y, r2.z, r2.w), q3 = make_uint4(r3.x, r3.y, r3.z, r3.w);
-    const float lo0[3] = {__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z)};
-    const float lo1[3] = {__uint_as_float(q0.w), __uint_as_float(q1.x), __uint_as_float(q1.y)};
-    const float hi0[3] = {__uint_as_float(q1.z), __uint_as_float(q1.w), __uint_as_float(q2.x)};
-    const float hi1[3] = {__uint_as_float(q2.y), __uint_as_float(q2.z), __uint_as_float(q2.w)};
-    const int c0 = (int)q3.x, c1 = (int)q3.y;
-    float t0, t1;
-    const bool h0 = slab_hit32(lo0, hi0, sr, t_hi, t0);
-    const bool h1 = slab_hit32(lo1, hi1, sr, t_hi, t1) & (c1 != kBvhEmpty);
-    n_boxes += 2;
-    if (h0 && h1) {
-      const bool flip = t1 < t0;
-      stk(sp++) = flip ? c0 : c1;
-      e = flip ? c1 : c0;
-    } else {
-      e = h0 ? c0 : h1 ? c1 : pop();
-    }
-  };
-  // a leaf's spheres; true when a shadow ray is found occluded
-  auto leaf = [&](int code_e) {
-    const int code = -(code_e + 1);
-    const int first = code >> 7, cnt = code & 127;
-    for (int k = first; k < first + cnt; ++k) leaf_sphere_test<SHADOW>(sd, k, o, d, h, n_disc);
-    n_tests += (unsigned)cnt;
-    if constexpr (SHADOW) {
-      return h.key >= 0 && h.t < t_shadow;
-    } else {
-      t_hi = f32_up(h.t);
-      return false;
-    }
-  };
-  // Leaves batched across the wave (speculative while-while): a lane meeting
-  // a leaf postpones it and keeps visiting nodes; the node phase ends when no
-  // lane without a postponed leaf has a node left, then all postponed leaves
-  // are tested together. Culling only ever uses the lane's current bound, so
-  // the postponement changes no result.
-  int pl = kBvhEmpty;
-  for (;;) {
-    for (;;) {
-      if (e < 0 && e != kBvhEmpty && pl == kBvhEmpty) { pl = e; e = pop(); }
-      if (!__any(e >= 0 && pl == kBvhEmpty)) break;
-      if (e >= 0) visit();  // lanes holding a leaf keep going (speculative)
-    }
-    if (!__any(pl != kBvhEmpty)) break;
-    if (pl != kBvhEmpty) {
-      if (leaf(pl)) { e = kBvhEmpty; sp = 0; }  // shadowed: done
-      pl = kBvhEmpty;
-    }
-  }
-}
-// Per-lane traversal over the pair layout (LANE == 14): the block's LDS copy
-// of each binary node stores, per axis, the two children's lower bounds as
-// one 8-B pair and their upper bounds as the next pair (lo0 lo1 hi0 hi1 per
-// axis, then the child codes). Which face a ray enters on an axis follows the
-// sign of its direction there, so each lane computes once the byte offsets of
-// its entry and exit pairs and loads them directly: one packed binary32 FMA
-// gives both children's entry (or exit) distances on an axis, and no per-axis
-// min/max is needed to tell entry from exit. The entry and exit values are the
-// ones lane_trace computes (entry = fma(entry face, inv, -on), exit =
-// fma(exit face, inv, -of), where lane_trace's min/max picks exactly them), so
-// the culling and the visit order are the same bit for bit. Leaves are
-// batched across the wave as in lane_trace<..., WW>.
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-template <bool SHADOW>
-__device__ __forceinline__ void lane_trace_pair(const unsigned char* nodes, const SphereDiag* sd, const float* M,
-                                                bool has_bvh, V3 o, V3 d, double t_shadow, Hit& h, unsigned& n_disc,
-                                                unsigned& n_tests, unsigned& n_boxes, int* lds) {
-  float inv[3], on[3], of[3];
-  int ent[3], ext[3];
-  {
-    const double oa[3] = {o.x, o.y, o.z}, da[3] = {d.x, d.y, d.z};
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      bool neg = false;
-      if (fabs(da[a]) >= 0x1p-60 && fabs(oa[a]) <= 0x1p60 && M[a] <= 0x1p60f) {  // as slab_ray; NaN fails
-        const double iv = 1.0 / da[a];
-        const double oinv = oa[a] * iv;
-        const double delta = 0x1p-20 * fabs(iv) * ((double)M[a] + fabs(oa[a]));
-        inv[a] = (float)iv;
-        on[a] = (float)(oinv + delta);
-        of[a] = (float)(oinv - delta);
-        neg = !(iv >= 0.0);
-      } else {
-        inv[a] = 0.0f;
-        on[a] = INFINITY;
-        of[a] = -INFINITY;
-      }
-      ent[a] = 16 * a + (neg ? 8 : 0);
-      ext[a] = ent[a] ^ 8;
-    }
-  }
-  // keep the six offsets in registers (the compiler would otherwise recompute
-  // the exit offsets in every visit)
-#pragma unroll
-  for (int a = 0; a < 3; ++a) asm volatile("" : "+v"(ent[a]), "+v"(ext[a]));
-  float t_hi = f32_up(SHADOW ? t_shadow : h.t);
-  auto stk = [&](int k) -> int& { return lds[k * kTraceBlock]; };
-  // entry 0 is a sentinel (kBvhEmpty): a pop needs no emptiness test, and a
-  // lane that pops it is done and pops no more (the stack holds bvh_depth + 1)
-  stk(0) = kBvhEmpty;
-  int sp = 1;
-  auto pop = [&]() { return stk(--sp); };
-  int e = (SHADOW && h.key >= 0 && h.t < t_shadow) || !has_bvh ? kBvhEmpty : 0;
-  auto visit = [&]() {
-    const unsigned char* nb = nodes + (size_t)e * 64;
-    const f32x2 ex = *(const f32x2*)(nb + ent[0]), ey = *(const f32x2*)(nb + ent[1]), ez = *(const f32x2*)(nb + ent[2]);
-    const f32x2 xx = *(const f32x2*)(nb + ext[0]), xy = *(const f32x2*)(nb + ext[1]), xz = *(const f32x2*)(nb + ext[2]);
-    const int2 cc = *(const int2*)(nb + 48);
-    const f32x2 tx0 = __builtin_elementwise_fma(ex, (f32x2)(inv[0]), (f32x2)(-on[0]));
-    const f32x2 ty0 = __builtin_elementwise_fma(ey, (f32x2)(inv[1]), (f32x2)(-on[1]));
-    const f32x2 tz0 = __builtin_elementwise_fma(ez, (f32x2)(inv[2]), (f32x2)(-on[2]));
-    const f32x2 tx1 = __builtin_elementwise_fma(xx, (f32x2)(inv[0]), (f32x2)(-of[0]));
-    const f32x2 ty1 = __builtin_elementwise_fma(xy, (f32x2)(inv[1]), (f32x2)(-of[1]));
-    const f32x2 tz1 = __builtin_elementwise_fma(xz, (f32x2)(inv[2]), (f32x2)(-of[2]));
-    const float t0 = fmaxf(fmaxf(tx0.x, ty0.x), fmaxf(tz0.x, 0.0f));
-    const float t1 = fmaxf(fmaxf(tx0.y, ty0.y), fmaxf(tz0.y, 0.0f));
-    const float u0 = fminf(fminf(tx1.x, ty1.x), fminf(tz1.x, t_hi));
-    const float u1 = fminf(fminf(tx1.y, ty1.y), fminf(tz1.y, t_hi));
-    const bool h0 = t0 <= u0;
-    const bool h1 = (t1 <= u1) & (cc.y != kBvhEmpty);
-    n_boxes += 2;
-    if (h0 && h1) {
-      const bool flip = t1 < t0;
-      stk(sp++) = flip ? cc.x : cc.y;
-      e = flip ? cc.y : cc.x;
-    } else {
-      e = h0 ? cc.x : h1 ? cc.y : pop();
-    }
-  };
-  auto leaf = [&](int code_e) {
-    const int code = -(code_e + 1);
-    const int first = code >> 7, cnt = code & 127;
-    for (int k = first; k < first + cnt; ++k) leaf_sphere_test<SHADOW>(sd, k, o, d, h, n_disc);
-    n_tests += (unsigned)cnt;
-    if constexpr (SHADOW) {
-      return h.key >= 0 && h.t < t_shadow;
-    } else {
-      t_hi = f32_up(h.t);
-      return false;
-    }
-  };
-  int pl = kBvhEmpty;
-  for (;;) {
-    for (;;) {
-      if (e < 0 && e != kBvhEmpty && pl == kBvhEmpty) { pl = e; e = pop(); }
-      if (!__any(e >= 0 && pl == kBvhEmpty)) break;
-      if (e >= 0) visit();  // lanes holding a leaf keep going (speculative)
-    }
-    if (!__any(pl != kBvhEmpty)) break;
-    if (pl != kBvhEmpty) {
-      if (leaf(pl)) { e = kBvhEmpty; sp = 1; }  // shadowed: done
-      pl = kBvhEmpty;
-    }
-  }
-}
-
-// Block-wide copy of n 16-B chunks from global memory into LDS with eight
-// loads in flight per thread (one load-wait-store per chunk left the staging
-// latency-bound: ~9K cycles per block for the C3 scene). Every thread of the
-// block calls it; the caller synchronises.
-__device__ __forceinline__ void stage_lds(uint4* dst, const uint4* src, int n) {
-  const int bd = (int)blockDim.x;
-  int i = (int)threadIdx.x;
-  for (; i + 7 * bd < n; i += 8 * bd) {
-    uint4 v[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = src[i + k * bd];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) dst[i + k * bd] = v[k];
-  }
-  for (; i < n; i += bd) dst[i] = src[i];
-}
-
-// Per-lane traversal of the hierarchy over the other bounded records
-// (general-transform spheres, cubes, cylinders with finite caps; global
-// memory, private stack): the same culling rule and exactness argument as the
-// sphere hierarchy (DESIGN.md "Exact culling"). Scenes made of diagonal
-// spheres and planes (C3, C5) have no such hierarchy.
-template <bool SHADOW>
-__device__ __forceinline__ void other_trace(const DevScene& sc, V3 o, V3 d, double t_shadow, Hit& h,
-                                            unsigned& n_disc, unsigned& n_tests, unsigned& n_boxes) {
-  if (sc.n_obvh == 0 || (SHADOW && h.key >= 0 && h.t < t_shadow)) return;
-  const BvhNode* nodes = sc.obvh;
-  float M[3];
-  for (int ax = 0; ax < 3; ++ax)  // the root's two child boxes contain every box below them
-    M[ax] = fmaxf(fmaxf(fabsf(nodes[0].lo[0][ax]), fabsf(nodes[0].hi[0][ax])),
-                  fmaxf(fabsf(nodes[0].lo[1][ax]), fabsf(nodes[0].hi[1][ax])));
-  const SlabRay sr = slab_ray(o, d, M);
-  float t_hi = f32_up(SHADOW ? t_shadow : h.t);
-  int stk[kBvhMaxDepth + 4];
-  int sp = 0, e = 0;
-  while (e != kBvhEmpty) {
-    if (e >= 0) {
-      const BvhNode& nd = nodes[e];
-      float t0 = 0.0f, t1 = 0.0f;
-      const bool h0 = slab_hit32(nd.lo[0], nd.hi[0], sr, t_hi, t0);
-      const bool h1 = nd.child[1] != kBvhEmpty && slab_hit32(nd.lo[1], nd.hi[1], sr, t_hi, t1);
-      n_boxes += 2;
-      if (h0 && h1) {
-        const bool flip = t1 < t0;
-        stk[sp++] = flip ? nd.child[0] : nd.child[1];
-        e = flip ? nd.child[1] : nd.child[0];
-      } else {
-        e = h0 ? nd.child[0] : h1 ? nd.child[1] : (sp > 0 ? stk[--sp] : kBvhEmpty);
-      }
-    } else {
-      const int code = -(e + 1), first = code >> 7, cnt = code & 127;
-      for (int k = first; k < first + cnt; ++k) other_test<SHADOW>(sc.orec + k, o, d, h, n_disc);
-      n_tests += (unsigned)cnt;
-      if constexpr (SHADOW) {
-        if (h.key >= 0 && h.t < t_shadow) return;  // shadowed: done
-      } else {
-        t_hi = f32_up(h.t);
-      }
-      e = sp > 0 ? stk[--sp] : kBvhEmpty;
-    }
-  }
-}
-
 // ------------------------------------------------------------ fused trace kernels
 // The fast path (BVH) evaluates a whole generation in ONE launch per
 // generation (DESIGN.md "Fused generations"): closest hit, prepare_computations,
@@ -923,165 +504,6 @@ __device__ __forceinline__ void other_trace(const DevScene& sc, V3 o, V3 d, doub
 //       when they fit
 // The per-light box distances of the light buffer are staged in LDS when they
 // fit beside the image (WfArgs::lds_flags).
-__host__ __device__ inline size_t lane_stack_bytes(int depth) { return (size_t)(depth > 0 ? depth : 1) * kTraceBlock * 4; }
-__host__ __device__ inline size_t sph_lds_bytes(const DevScene& sc) { return (size_t)sc.n_diag * sizeof(SphereDiag); }
-__host__ __device__ inline size_t delta_lds_bytes(const DevScene& sc) {
-  return sc.lb_cells ? (((size_t)sc.n_lights * sc.n_diag * sizeof(float) + 15) & ~(size_t)15) : 0;
-}
-// LANE 14: [stack (bvh_depth + 1 with the sentinel) x kTraceBlock][pair nodes][sphere records]
-__host__ __device__ inline size_t pair_lds_bytes(const DevScene& sc) {
-  return lane_stack_bytes(sc.bvh_depth + 1) + (size_t)sc.n_bvh * sizeof(BvhNode) + sph_lds_bytes(sc);
-}
-constexpr unsigned kLdsSpheres = 1u, kLdsDeltas = 2u;  // WfArgs::lds_flags (LANE 0: records; all: distances)
-
-struct LaneScene {
-  const unsigned char* nodes;  // pair layout in LDS (14) or BvhNode[] in global memory
-  const SphereDiag* sd;        // sphere records (LDS or global)
-  const float* delta;          // light buffer: per-light box distances (LDS or global)
-  int* stack;                  // per-lane LDS stack (14, 3) or the wave's stack (0)
-  float M[3];                  // bound on |box coordinate| per axis (slab_ray)
-  const BvhNode* top;          // 3: the LDS copy of the first n_top nodes
-  int n_top;
-};
-template <int LANE>
-__device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, const WfArgs& a, int* static_stack,
-                                                unsigned char* dyn) {
-  LaneScene ls{(const unsigned char*)sc.bvh, sc.sph_diag, sc.lb_delta, static_stack, {0.f, 0.f, 0.f}, nullptr, 0};
-  unsigned char* p = dyn;
-  if constexpr (LANE == 14) {
-    // pair layout (BvhPair): per axis, the two children's lower bounds form one
-    // 8-B pair and their upper bounds the next (lane_trace_pair)
-    ls.stack = (int*)dyn + threadIdx.x;
-    p += lane_stack_bytes(sc.bvh_depth + 1);
-    stage_lds((uint4*)p, (const uint4*)sc.bvh_pair, sc.n_bvh * (int)(sizeof(BvhPair) / 16));
-    ls.nodes = p;
-    p += (size_t)sc.n_bvh * sizeof(BvhPair);
-  }
-  if (LANE == 14 || (LANE == 0 && (a.lds_flags & kLdsSpheres))) {
-    stage_lds((uint4*)p, (const uint4*)sc.sph_diag, sc.n_diag * (int)(sizeof(SphereDiag) / 16));
-    ls.sd = (const SphereDiag*)p;
-    p += sph_lds_bytes(sc);
-  }
-  if (LANE == 3 && a.n_top > 0) {  // the treelet: after the distances when those are staged
-    unsigned char* q = p + ((a.lds_flags & kLdsDeltas) ? delta_lds_bytes(sc) : 0);
-    stage_lds((uint4*)q, (const uint4*)sc.bvh, (int)a.n_top * (int)(sizeof(BvhNode) / 16));
-    ls.top = (const BvhNode*)q;
-    ls.n_top = (int)a.n_top;
-  }
-  if (a.lds_flags & kLdsDeltas) {
-    float* ld = (float*)p;
-    const int nd = sc.n_lights * sc.n_diag, bd = (int)blockDim.x;
-    int i = (int)threadIdx.x;
-    for (; i + 7 * bd < nd; i += 8 * bd) {  // eight loads in flight per thread
-      float v[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = sc.lb_delta[i + k * bd];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) ld[i + k * bd] = v[k];
-    }
-    for (; i < nd; i += bd) ld[i] = sc.lb_delta[i];
-    ls.delta = ld;
-  }
-  __syncthreads();
-  for (int ax = 0; ax < 3; ++ax) {  // the root's two child boxes contain every box below them
-    float m = 0.0f;
-    if (sc.n_bvh > 0) {
-      const BvhNode& r = sc.bvh[0];
-      m = fmaxf(fmaxf(fabsf(r.lo[0][ax]), fabsf(r.hi[0][ax])), fmaxf(fabsf(r.lo[1][ax]), fabsf(r.hi[1][ax])));
-    }
-    ls.M[ax] = m;
-  }
-  return ls;
-}
-
-// World::is_shadowed for the diagonal spheres through the light buffer
-// (DESIGN.md "Light buffer"): the cube-map cell of direction o - light lists
-// every sphere that can block the ray, nearest box first; the walk stops at
-// the first blocker or at the first box farther from the light than the
-// origin. One 16-B load brings the cell's first kLbInline entries. An origin
-// beyond the light's validity radius (or non-finite) tests every sphere.
-__device__ __forceinline__ void lb_walk(const DevScene& sc, const SphereDiag* sd, const float* delta, unsigned l,
-                                        V3 o, V3 d, double dist, Hit& h, unsigned& n_disc, unsigned& n_tests) {
-  cLightRec Lr = (cLightRec)sc.lights + l;
-  if (dist <= (double)sc.lb_limit[l] && dist >= 1e-30) {
-    const int R = sc.lb_res;
-    const unsigned per_light = 6u * (unsigned)R * (unsigned)R;
-    const float half_r = 0.5f * (float)R;
-    // w = o - light (= -(light - o) bit for bit), in binary32
-    const float wx = (float)(o.x - Lr->pos[0]), wy = (float)(o.y - Lr->pos[1]), wz = (float)(o.z - Lr->pos[2]);
-    const float ax = fabsf(wx), ay = fabsf(wy), az = fabsf(wz);
-    unsigned f;
-    float wa, wb, wc;
-    if (ax >= ay && ax >= az) { f = wx < 0.0f ? 1u : 0u; wa = ax; wb = wy; wc = wz; }
-    else if (ay >= az) { f = wy < 0.0f ? 3u : 2u; wa = ay; wb = wz; wc = wx; }
-    else { f = wz < 0.0f ? 5u : 4u; wa = az; wb = wx; wc = wy; }
-    const float u = fminf(fmaxf(wb / wa, -1.0f), 1.0f), v = fminf(fmaxf(wc / wa, -1.0f), 1.0f);
-    const unsigned iu = (unsigned)min((int)((u + 1.0f) * half_r), R - 1);
-    const unsigned iv = (unsigned)min((int)((v + 1.0f) * half_r), R - 1);
-    const LbCell c = sc.lb_cells[l * per_light + (f * (unsigned)R + iv) * (unsigned)R + iu];
-    const unsigned cnt = c.w0 & 0xFFFFu;
-    // the inline entries as a queue of 16-bit indices: idx0..idx3 in q, idx4 in c.w2 >> 16
-    unsigned long long q = (unsigned long long)(c.w0 >> 16) | (unsigned long long)c.w1 << 16 |
-                           (unsigned long long)(c.w2 & 0xFFFFu) << 48;
-    const float* dl = delta + (size_t)l * sc.n_diag;
-    const float dist_up = f32_up(dist);
-    for (unsigned k = 0; k < cnt; ++k) {
-      unsigned idx;
-      if (k < 4u) { idx = (unsigned)(q & 0xFFFFu); q >>= 16; }
-      else if (k == 4u) idx = c.w2 >> 16;
-      else idx = sc.lb_ov[c.ov + k - (unsigned)kLbInline];
-      if (dl[idx] > dist_up) break;  // this box and all after it lie beyond the origin
-      leaf_sphere_test<true>(sd, (int)idx, o, d, h, n_disc);
-      ++n_tests;
-      if (h.key >= 0 && h.t < dist) break;
-    }
-  } else {
-    for (int k = 0; k < sc.n_diag; ++k) {
-      leaf_sphere_test<true>(sd, k, o, d, h, n_disc);
-      ++n_tests;
-      if (h.key >= 0 && h.t < dist) break;
-    }
-  }
-}
-
-// World::is_shadowed (world.rs:95-105) of the ray from `o` towards light `l`
-// (direction d, distance dist): the records outside the BVH first (any hit
-// before the light ends the ray), then the light buffer, or the BVH of the
-// kernel's image when the scene has no light buffer.
-template <int LANE, bool QUADS>
-__device__ __forceinline__ bool shadow_trace(const DevScene& sc, const WfArgs& a, const LaneScene& ls, unsigned l,
-                                             V3 o, V3 d, double dist, unsigned& n_disc, unsigned& n_tests,
-                                             unsigned& n_boxes) {
-  Hit h;
-  hit_init(h);
-  trace_rest<true, QUADS, true>(sc, o, d, h, n_disc);
-  if constexpr (QUADS) other_trace<true>(sc, o, d, dist, h, n_disc, n_tests, n_boxes);
-  if (!(h.key >= 0 && h.t < dist)) {
-    if (a.use_lb) {
-      lb_walk(sc, ls.sd, ls.delta, l, o, d, dist, h, n_disc, n_tests);
-    } else if constexpr (LANE == 14) {
-      lane_trace_pair<true>(ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, dist, h, n_disc, n_tests, n_boxes, ls.stack);
-    } else if constexpr (LANE == 0) {
-      Hit hb;  // the wave traversal starts from an empty hit; any blocker is an answer
-      bvh_trace<false, true>(sc, nullptr, ls.stack, o, d, dist, hb, n_disc, n_tests, n_boxes);
-      if (hb.key >= 0 && hb.key != 0x7fffffff && hb.t < dist) h = hb;
-    } else {
-      lane_trace<true, LANE == 3>((const BvhNode*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, dist, h, n_disc,
-                                  n_tests, n_boxes, ls.stack, ls.top, ls.n_top);
-    }
-  }
-  hit_finish(h);
-  return h.key >= 0 && h.t < dist;
-}
-
-// World::shade_hit's combination (world.rs:58-67) of the surface term and the
-// reflected / refracted colours, with the reference's expression.
-__device__ __forceinline__ V3 shade_color(const ShadeRec& m, V3 surface, V3 refl, V3 refr, double schlick_r) {
-  if (m.reflective > 0.0 && m.transparency > 0.0)
-    return vadd(vadd(surface, vscale(refl, schlick_r)), vscale(refr, 1.0 - schlick_r));
-  return vadd(vadd(surface, refl), refr);
-}
-
 // Where generation g's colour of ray `slot` goes: generation 0 of a camera
 // render without AA is tile-ordered, and its colours are written row-major
 // into the output.
@@ -1089,18 +511,12 @@ __device__ __forceinline__ double* color_dst(const WfArgs& a, const DevCamera& c
   size_t oi = slot;
   if (a.g == 0 && a.camera_mode && a.aa == 1) {
     uint32_t x, lr, smp;
-    gen0_pixel(a, cam.hsize, slot, x, lr, smp);
+    gen0_pixel(a.aa, a.rows, cam.hsize, slot, x, lr, smp);
     oi = (size_t)lr * cam.hsize + x;
   }
   return a.colors + oi * 3;
 }
 
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-// Streaming loads and stores of the fused kernels: rays, parents and colours
-// are written once and read once by a later launch, so they are marked
-// non-temporal and leave the L2 to the scene (C3 0.947 -> 0.929 ms, C5 60.0
-// -> 58.8 ms per frame). The same marking in wf_combine_parents cost 2 %.
-__device__ __forceinline__ void st_d(double* p, double v) { __builtin_nontemporal_store(v, p); }
 __device__ __forceinline__ void st_ray(WfRay* p, V3 o, V3 d) {
   st_d(&p->o[0], o.x); st_d(&p->o[1], o.y); st_d(&p->o[2], o.z);
   st_d(&p->d[0], d.x); st_d(&p->d[1], d.y); st_d(&p->d[2], d.z);
@@ -1183,7 +599,7 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
     if (a.skip_shadow && shadow_irrelevant(*m, Lr, sdir, c.normal, term)) {
       // the light is behind the surface: lighting() is the ambient term either way
     } else {
-      const bool shadowed = shadow_trace<LANE, QUADS>(sc, a, ls, l, c.over, sdir, dist, t.sh_disc, t.sh_tests,
+      const bool shadowed = shadow_trace<LANE, QUADS>(sc, a.use_lb, ls, l, c.over, sdir, dist, t.sh_disc, t.sh_tests,
                                                       t.sh_boxes);
       ++t.sh_rays;
       term = lighting(*m, Lr, c.over, c.eyev, c.normal, shadowed, sdir);
@@ -1217,7 +633,7 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
                            : LANE == 0 ? (kTraceBlock / 64) * (kBvhMaxDepth + 4) : 1];
   extern __shared__ __attribute__((aligned(16))) unsigned char lane_dyn[];
   int* stk = LANE == 0 ? stack_lds + (threadIdx.x / 64) * (kBvhMaxDepth + 4) : stack_lds + threadIdx.x;
-  const LaneScene ls = lane_scene<LANE>(sc, a, stk, lane_dyn);
+  const LaneScene ls = lane_scene<LANE>(sc, a.lds_flags, a.n_top, stk, lane_dyn);
   __shared__ unsigned s_pre[kShards + 1];
   const unsigned* pre = shard_prefix(a.in_cnt, s_pre);
   FusedTally t;
@@ -1393,7 +809,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_combine(DevScene sc, DevCamera ca
     size_t oi = slot;
     if (a.g == 0 && a.camera_mode && a.aa == 1) {  // generation 0 is tile-ordered: write row-major
       uint32_t x, lr, smp;
-      gen0_pixel(a, cam.hsize, i, x, lr, smp);
+      gen0_pixel(a.aa, a.rows, cam.hsize, i, x, lr, smp);
       oi = (size_t)lr * cam.hsize + x;
     }
     double* out = a.colors + oi * 3;
@@ -1446,7 +862,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_average(WfArgs a, unsigned hsize,
     }
     const V3 avg = vscale(sum, 1.0 / (double)aa);
     uint32_t x, lr, smp;
-    gen0_pixel(a, hsize, p * aa, x, lr, smp);
+    gen0_pixel(a.aa, a.rows, hsize, p * aa, x, lr, smp);
     double* o = out + ((size_t)lr * hsize + x) * 3;
     o[0] = avg.x; o[1] = avg.y; o[2] = avg.z;
   }
@@ -1493,6 +909,9 @@ Wavefront::~Wavefront() {
   if (d_cnt_) (void)hipFree(d_cnt_);
   if (d_shard_) (void)hipFree(d_shard_);
   if (d_prim_) (void)hipFree(d_prim_);
+  if (ps_rings_) (void)hipFree(ps_rings_);
+  if (ps_parents_) (void)hipFree(ps_parents_);
+  if (ps_ctr_) (void)hipFree(ps_ctr_);
   if (h_fault_) (void)hipHostFree(h_fault_);
   if (ev0_) (void)hipEventDestroy(ev0_);
   if (ev1_) (void)hipEventDestroy(ev1_);
@@ -1549,8 +968,15 @@ hipError_t Wavefront::last_profile(WfProfile* out) {
     out->sh_tests[c] = (double)hc.sh_tests(c);
   }
   if (last_fused_) out->rays[WF_SHADOW] = out->sh_rays[0] + out->sh_rays[1];  // traced inside the fused launches
+  if (last_persist_) {  // one launch: the root rays and, from a counted frame, the children per depth
+    out->rays[WF_PRIMARY] = (double)lr_.n0;
+    double kids = 0.0;
+    for (int g = 0; g < kMaxGen; ++g) kids += (double)hc.n_refl[g] + (double)hc.n_refr[g];
+    out->rays[WF_CLOSEST] = kids;
+  }
   out->bvh = last_bvh_ ? 1 : 0;
   out->fused = last_fused_ ? 1 : 0;
+  out->persist = last_persist_ ? 1 : 0;
   return hipSuccess;
 }
 
@@ -1647,11 +1073,9 @@ static constexpr size_t kWfLdsLimit = 160 * 1024 - 1024;
 // multi-GPU frame, the deep generations). The kernels index their LDS stacks
 // with the kTraceBlock stride and loop over gridDim x blockDim, so any block
 // size up to kTraceBlock gives the same results.
-int g_wf_adaptive_block = 0;  // tuning knob ("adaptive_block"); frames in flight fill idle CUs better
-int g_wf_shadow_stream = 1;   // tuning knob ("shadow_stream", exhaustive pipeline): 0 off, 1 when the frame
-                              // renders alone, 2 always
-static int trace_block(unsigned n) {
-  if (!g_wf_adaptive_block) return kTraceBlock;
+// (WfTuning::adaptive_block; frames in flight fill idle CUs better without it)
+static int trace_block(unsigned n, int adaptive) {
+  if (!adaptive) return kTraceBlock;
   static int n_cu = 0;
   if (n_cu == 0) {
     int dev = 0;
@@ -1685,8 +1109,8 @@ static hipError_t launch_lds(K kern, size_t lds, unsigned n, hipStream_t stream,
 // ---- the exhaustive pipeline (counted launches: the reference's every-shape loop)
 template <bool QUADS>
 static hipError_t launch_closest_exh(const DevScene& sc, const DevCamera& cam, const WfArgs& a, bool primary,
-                                     bool lds_ok, unsigned n, hipStream_t stream) {
-  const int tb = trace_block(n);
+                                     bool lds_ok, unsigned n, hipStream_t stream, const WfTuning& tn) {
+  const int tb = trace_block(n, tn.adaptive_block);
   if (primary)
     return launch_lds(wf_trace_closest<true, true, QUADS, 8>, wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, true),
                       n, stream, sc, cam, a, tb);
@@ -1696,8 +1120,9 @@ static hipError_t launch_closest_exh(const DevScene& sc, const DevCamera& cam, c
   return launch_lds(wf_trace_closest<false, false, QUADS, 8>, 0, n, stream, sc, cam, a, tb);
 }
 template <bool QUADS>
-static hipError_t launch_shadow_exh(const DevScene& sc, const WfArgs& a, bool lds_ok, hipStream_t stream) {
-  const int tb = trace_block(a.n_shadow);
+static hipError_t launch_shadow_exh(const DevScene& sc, const WfArgs& a, bool lds_ok, hipStream_t stream,
+                                    const WfTuning& tn) {
+  const int tb = trace_block(a.n_shadow, tn.adaptive_block);
   if (lds_ok) {
     const size_t lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, false);
     auto k = wf_trace_shadow<true, QUADS, 8>;
@@ -1713,8 +1138,8 @@ static hipError_t launch_shadow_exh(const DevScene& sc, const WfArgs& a, bool ld
 // ---- the fast path: one fused launch per generation (image choice: see lane_scene)
 template <bool QUADS, bool TALLY>
 static hipError_t launch_fused_q(const DevScene& sc, const DevCamera& cam, WfArgs a, bool primary, unsigned n,
-                                 hipStream_t stream) {
-  const int tb = trace_block(n);
+                                 hipStream_t stream, const WfTuning& tn) {
+  const int tb = trace_block(n, tn.adaptive_block);
   const size_t dl = a.use_lb ? delta_lds_bytes(sc) : 0;
   size_t dyn = 0;
   a.lds_flags = 0;
@@ -1724,17 +1149,17 @@ static hipError_t launch_fused_q(const DevScene& sc, const DevCamera& cam, WfArg
     if (dl && dyn + dl <= room) { a.lds_flags |= kLdsDeltas; dyn += dl; }
     return launch_lds(wf_trace_fused<true, QUADS, 0, TALLY>, dyn, n, stream, sc, cam, a, tb);
   }
-  if (g_wf_image == 0 && pair_lds_bytes(sc) <= kWfLdsLimit) {
+  if (tn.image == 0 && pair_lds_bytes(sc) <= kWfLdsLimit) {
     dyn = pair_lds_bytes(sc);
     if (dl && dyn + dl <= kWfLdsLimit) { a.lds_flags |= kLdsDeltas; dyn += dl; }
     return launch_lds(wf_trace_fused<false, QUADS, 14, TALLY>, dyn, n, stream, sc, cam, a, tb);
   }
-  if (g_wf_image != 1 && sc.bvh_depth <= kLaneLdsDepth) {
+  if (tn.image != 1 && sc.bvh_depth <= kLaneLdsDepth) {
     const size_t room = kWfLdsLimit - (size_t)kLaneLdsDepth * kTraceBlock * 4;
     // the room left beside the stack: the light buffer's distances and/or a treelet
-    const bool deltas = dl && dl <= room && (!g_wf_treelet || g_wf_treelet_deltas);
+    const bool deltas = dl && dl <= room && (!tn.treelet || tn.treelet_deltas);
     if (deltas) { a.lds_flags |= kLdsDeltas; dyn = dl; }
-    if (g_wf_treelet) {
+    if (tn.treelet) {
       a.n_top = (unsigned)std::min<size_t>((size_t)sc.n_bvh, (room - dyn) / sizeof(BvhNode));
       dyn += (size_t)a.n_top * sizeof(BvhNode);
     }
@@ -1744,22 +1169,20 @@ static hipError_t launch_fused_q(const DevScene& sc, const DevCamera& cam, WfArg
   return launch_lds(wf_trace_fused<false, QUADS, 1, TALLY>, dyn, n, stream, sc, cam, a, tb);
 }
 static hipError_t launch_fused(const DevScene& sc, const DevCamera& cam, const WfArgs& a, bool primary, unsigned n,
-                               hipStream_t stream, bool tally) {
+                               hipStream_t stream, bool tally, const WfTuning& tn) {
   // QUADS: solids outside the hierarchies, or the hierarchy over the other records
   const bool quads = sc.n_fx_quads > 0 || sc.n_obvh > 0;
   if (tally)
-    return quads ? launch_fused_q<true, true>(sc, cam, a, primary, n, stream)
-                 : launch_fused_q<false, true>(sc, cam, a, primary, n, stream);
-  return quads ? launch_fused_q<true, false>(sc, cam, a, primary, n, stream)
-               : launch_fused_q<false, false>(sc, cam, a, primary, n, stream);
+    return quads ? launch_fused_q<true, true>(sc, cam, a, primary, n, stream, tn)
+                 : launch_fused_q<false, true>(sc, cam, a, primary, n, stream, tn);
+  return quads ? launch_fused_q<true, false>(sc, cam, a, primary, n, stream, tn)
+               : launch_fused_q<false, false>(sc, cam, a, primary, n, stream, tn);
 }
-
-int Wavefront::g_corrupt_calibration = 0;
 
 hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool camera_mode, const double* d_in_rays,
                              unsigned n0, unsigned aa, unsigned max_depth, unsigned row_block, unsigned shard,
                              unsigned n_shards, double* d_out, hipStream_t stream, const std::string& signature,
-                             DevStats* stats, float* ms_kernel, bool solo, unsigned flags) {
+                             DevStats* stats, float* ms_kernel, const WfTuning& tn, bool solo, unsigned flags) {
   if (max_depth + 2 > (unsigned)kMaxGen) return hipErrorInvalidValue;
   if (aa == 0 || aa > 16 || (aa & (aa - 1)) != 0 || (!camera_mode && aa != 1) || n0 % aa != 0)
     return hipErrorInvalidValue;
@@ -1771,9 +1194,15 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
   // reference's every-shape loop is asked for; counting (stats) never changes the algorithm
   const bool exhaustive = (flags & WF_EXHAUSTIVE) != 0;
   const bool count = stats != nullptr || (flags & WF_COUNT) != 0;
-  const bool bvh = g_wf_accel != 0 && !exhaustive && (sc.n_bvh > 0 || sc.n_obvh > 0);
+  const bool bvh = tn.accel != 0 && !exhaustive && (sc.n_bvh > 0 || sc.n_obvh > 0);
   const bool fused = bvh;
-  const bool skip_shadow = !exhaustive && g_wf_skip_shadow != 0;
+  const bool skip_shadow = !exhaustive && tn.skip_shadow != 0;
+  // the fast path: one persistent launch per render (rt_persist.hip), for
+  // recursion depths whose heap-addressed trees it can hold
+  if (bvh && tn.persist && max_depth <= kPsMaxDepth)
+    return render_persist(sc, cam, camera_mode, d_in_rays, n0, aa, max_depth, row_block, shard, n_shards, d_out,
+                          stream, stats, ms_kernel, count, tn);
+  last_persist_ = false;
   // the shadow-ray counts differ between the two modes; the fused pipeline's
   // second queue per generation holds its parents instead of shadow rays
   const std::string key = signature.empty() ? signature : signature + (skip_shadow ? 'S' : 'A') + (fused ? 'F' : 'E');
@@ -1781,7 +1210,7 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
   const bool calibrated = it != cache_.end();
   Counts counts;
   if (calibrated) counts = it->second;
-  if (calibrated && g_corrupt_calibration && counts.rays.size() > 1 && counts.rays[1] > 0) --counts.rays[1];
+  if (calibrated && tn.corrupt_calibration && counts.rays.size() > 1 && counts.rays[1] > 0) --counts.rays[1];
   counts.rays.resize(max_depth + 2, 0);
   counts.shadows.resize(max_depth + 2, 0);
   counts.rays[0] = n0;
@@ -1811,7 +1240,7 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
   // closest(g), like closest(g+1); they run on the side stream, forked after
   // closest(g) and joined before the combine pass (DESIGN.md "Shadow stream").
   hipStream_t sh_stream = stream;
-  if (!fused && (g_wf_shadow_stream == 2 || (g_wf_shadow_stream == 1 && solo))) {
+  if (!fused && (tn.shadow_stream == 2 || (tn.shadow_stream == 1 && solo))) {
     WF_CHECK(ensure_side());
     sh_stream = side_;
   }
@@ -1860,7 +1289,7 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     a.row_block = row_block; a.shard = shard; a.n_shards = n_shards;
     a.skip_shadow = skip_shadow ? 1u : 0u;
     a.count = count ? 1u : 0u;
-    a.use_lb = (g_wf_shadow_lb && sc.lb_cells) ? 1u : 0u;
+    a.use_lb = (tn.shadow_lb && sc.lb_cells) ? 1u : 0u;
     // 1. closest hit (fused: with the shading, the shadow rays and the spawn)
     const bool prim_launch = g == 0 && use_prim;
     const int ccls = prim_launch ? WF_PRIMARY : WF_CLOSEST;
@@ -1868,11 +1297,11 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     prof_rays_[ccls] += n;
     WF_CHECK(pmark(stream, ccls, true));
     if (fused) {
-      WF_CHECK(launch_fused(sc, cam, a, prim_launch, n, stream, count));
+      WF_CHECK(launch_fused(sc, cam, a, prim_launch, n, stream, count, tn));
     } else if (sc.n_quads > 0) {
-      WF_CHECK(launch_closest_exh<true>(sc, cam, a, prim_launch, gen_lds, n, stream));
+      WF_CHECK(launch_closest_exh<true>(sc, cam, a, prim_launch, gen_lds, n, stream, tn));
     } else {
-      WF_CHECK(launch_closest_exh<false>(sc, cam, a, prim_launch, gen_lds, n, stream));
+      WF_CHECK(launch_closest_exh<false>(sc, cam, a, prim_launch, gen_lds, n, stream, tn));
     }
     WF_CHECK(pmark(stream, ccls, false));
     // 2. prepare_computations + spawn (exhaustive pipeline)
@@ -1908,8 +1337,8 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
         forked = true;
       }
       WF_CHECK(pmark(sh_stream, WF_SHADOW, true));
-      if (sc.n_quads > 0) WF_CHECK(launch_shadow_exh<true>(sc, a, gen_lds, sh_stream));
-      else WF_CHECK(launch_shadow_exh<false>(sc, a, gen_lds, sh_stream));
+      if (sc.n_quads > 0) WF_CHECK(launch_shadow_exh<true>(sc, a, gen_lds, sh_stream, tn));
+      else WF_CHECK(launch_shadow_exh<false>(sc, a, gen_lds, sh_stream, tn));
       WF_CHECK(pmark(sh_stream, WF_SHADOW, false));
     }
     if (count) {
@@ -1985,6 +1414,124 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
   lr_.counts = counts;
   lr_.last = last; lr_.L = L; lr_.n0 = n0;
   lr_.counted = count; lr_.exact_disc = !bvh && !skip_shadow; lr_.bvh = bvh; lr_.fused = fused;
+  lr_.persist = false;
+  lr_.n_diag = (unsigned long long)sc.n_diag; lr_.n_gen = (unsigned long long)sc.n_gen;
+  lr_.n_planes = (unsigned long long)sc.n_planes; lr_.n_quads = (unsigned long long)sc.n_quads;
+  lr_.stream = stream;
+  if (stats) WF_CHECK(read_stats(stats));
+  return hipSuccess;
+}
+
+// The persistent frame kernel (rt_persist.hpp): one launch renders every
+// recursion depth and folds shade_hit's combine into the children's
+// delivery. Its trees are addressed by position (PsParent per heap node of a
+// root's recursion tree), sized here from the depth.
+hipError_t Wavefront::render_persist(const DevScene& sc, const DevCamera& cam, bool camera_mode,
+                                     const double* d_in_rays, unsigned n0, unsigned aa, unsigned max_depth,
+                                     unsigned row_block, unsigned shard, unsigned n_shards, double* d_out,
+                                     hipStream_t stream, DevStats* stats, float* ms_kernel, bool count,
+                                     const WfTuning& tn) {
+  const bool averaged = aa > 1;
+  const unsigned L = (unsigned)sc.n_lights;
+  WF_CHECK(ensure_misc((size_t)sc.n_diag));
+  if (!ps_ctr_) {  // zero once: every launch leaves its counters zeroed for the next one (ps_render)
+    WF_CHECK(hipMalloc(&ps_ctr_, sizeof(PsCounters)));
+    WF_CHECK(hipMemsetAsync(ps_ctr_, 0, sizeof(PsCounters), stream));
+  }
+  int dev = 0, n_cu = 0;
+  WF_CHECK(hipGetDevice(&dev));
+  WF_CHECK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+  n_cu = std::max(n_cu, 1);
+  // one workgroup per CU (the LDS image); small renders take fewer (two camera chunks each)
+  const unsigned n_chunks = (n0 + 63u) / 64u;
+  const unsigned grid = std::max(1u, std::min((unsigned)n_cu, (n_chunks + 1u) / 2u));
+  // heap-addressed trees: 2^d - 1 nodes per root may have children, at most 2^d
+  // rays of one root are queued or traced at once (an antichain of its tree)
+  const unsigned n_int = (1u << max_depth) - 1u;
+  const size_t leaves = (size_t)1 << max_depth;
+  const size_t per_tree = 64 * ((size_t)n_int * sizeof(PsParent) + leaves * sizeof(PsRay));
+  const unsigned trees =
+      (unsigned)std::min<size_t>(kPsMaxTrees, std::max<size_t>(4, kPsBudget / ((size_t)n_cu * per_tree)));
+  const size_t q_cap = (size_t)trees * 64 * leaves + kPsSpare;
+  WF_CHECK(grow(ps_rings_, ps_rings_cap_, (size_t)grid * q_cap));
+  WF_CHECK(grow(ps_parents_, ps_parents_cap_, std::max<size_t>(1, (size_t)grid * trees * 64 * n_int)));
+  if (averaged) WF_CHECK(ensure_gen(0, n0, L, 0, true));
+  // the scene image (as the generation pipeline's fused kernels)
+  constexpr size_t limit = kWfLdsLimit - kPsSchedBytes;
+  const bool use_lb = tn.shadow_lb && sc.lb_cells;
+  const size_t dl = use_lb ? delta_lds_bytes(sc) : 0;
+  PsArgs a{};
+  size_t dyn = 0;
+  int image = 1;
+  if (tn.image == 0 && pair_lds_bytes(sc) <= limit) {
+    image = 14;
+    dyn = pair_lds_bytes(sc);
+    if (dl && dyn + dl <= limit) { a.lds_flags |= kLdsDeltas; dyn += dl; }
+  } else if (tn.image != 1 && sc.bvh_depth <= kLaneLdsDepth) {
+    image = 3;
+    const size_t room = limit - (size_t)kLaneLdsDepth * kTraceBlock * 4;
+    if (dl && dl <= room && (!tn.treelet || tn.treelet_deltas)) { a.lds_flags |= kLdsDeltas; dyn = dl; }
+    if (tn.treelet) {
+      a.n_top = (unsigned)std::min<size_t>((size_t)sc.n_bvh, (room - dyn) / sizeof(BvhNode));
+      dyn += (size_t)a.n_top * sizeof(BvhNode);
+    }
+  } else if (dl && dl <= limit) {
+    a.lds_flags |= kLdsDeltas;
+    dyn = dl;
+  }
+  a.rings = ps_rings_;
+  a.parents = ps_parents_;
+  a.ctr = ps_ctr_;
+  a.cnt = d_cnt_;
+  a.out = averaged ? gens_[0].colors : d_out;
+  a.in_rays = d_in_rays;
+  a.fault = d_fault_;
+  a.q_cap = (unsigned)q_cap;
+  a.n_int = n_int;
+  a.trees = trees;
+  a.n0 = n0;
+  a.max_depth = max_depth;
+  a.camera_mode = camera_mode ? 1u : 0u;
+  a.aa = aa;
+  a.rows = n0 / aa / (cam.hsize ? cam.hsize : 1);
+  a.row_block = row_block; a.shard = shard; a.n_shards = n_shards;
+  a.use_lb = use_lb ? 1u : 0u;
+  a.skip_shadow = tn.skip_shadow ? 1u : 0u;
+  a.count = count ? 1u : 0u;
+  if (count) WF_CHECK(hipMemsetAsync(d_cnt_, 0, sizeof(WfCounters), stream));
+  if (ms_kernel) WF_CHECK(hipEventRecord(ev0_, stream));
+  if (profiling_) ++pframes_;
+  prof_rays_[0] = prof_rays_[1] = prof_rays_[2] = 0;
+  prof_rays_[WF_PRIMARY] = n0;
+  const bool quads = sc.n_fx_quads > 0 || sc.n_obvh > 0;
+  WF_CHECK(pmark(stream, WF_CLOSEST, true));
+  hipEvent_t e0 = t_ev_start, e1 = t_ev_stop;
+  if (e0) ++t_ev_used;
+  if (image == 14) WF_CHECK(ps_launch_lds(sc, cam, a, quads, count, grid, dyn, stream, e0, e1));
+  else WF_CHECK(ps_launch_global(sc, cam, a, image, quads, count, grid, dyn, stream, e0, e1));
+  WF_CHECK(pmark(stream, WF_CLOSEST, false));
+  if (averaged) {  // Color::average of each pixel's samples (color.rs:26-33)
+    const unsigned n_pix = n0 / aa;
+    WF_CHECK(pmark(stream, WF_COMBINE, true));
+    WfArgs wa{};
+    wa.aa = aa;
+    wa.rows = n_pix / cam.hsize;
+    WF_LAUNCH(wf_average, dim3(occupancy_grid(wf_average, kWfBlock, 0, n_pix)), dim3(kWfBlock), 0, stream, wa,
+              cam.hsize, gens_[0].colors, n_pix, d_out);
+    WF_CHECK(hipGetLastError());
+    WF_CHECK(pmark(stream, WF_COMBINE, false));
+  }
+  if (ms_kernel) WF_CHECK(hipEventRecord(ev1_, stream));
+  if (stats || ms_kernel) {
+    WF_CHECK(hipStreamSynchronize(stream));
+    if (ms_kernel) WF_CHECK(hipEventElapsedTime(ms_kernel, ev0_, ev1_));
+  }
+  last_bvh_ = true;
+  last_fused_ = true;
+  last_persist_ = true;
+  lr_.counts = Counts{};
+  lr_.last = max_depth; lr_.L = L; lr_.n0 = n0;
+  lr_.counted = count; lr_.exact_disc = false; lr_.bvh = true; lr_.fused = true; lr_.persist = true;
   lr_.n_diag = (unsigned long long)sc.n_diag; lr_.n_gen = (unsigned long long)sc.n_gen;
   lr_.n_planes = (unsigned long long)sc.n_planes; lr_.n_quads = (unsigned long long)sc.n_quads;
   lr_.stream = stream;
@@ -2000,7 +1547,16 @@ hipError_t Wavefront::read_stats(DevStats* out) {
   WF_CHECK(hipMemcpy(&hc, d_cnt_, sizeof hc, hipMemcpyDeviceToHost));
   DevStats s{};
   unsigned long long rays = 0, hits = 0, traced_shadows = 0;
-  for (unsigned g = 0; g <= lr_.last && g < lr_.counts.rays.size(); ++g) {
+  if (lr_.persist) {  // one launch: the rays per depth come from its tallies
+    rays = lr_.n0;
+    for (unsigned g = 0; g <= lr_.last && g < (unsigned)kMaxGen; ++g) {
+      rays += (unsigned long long)hc.n_refl[g] + hc.n_refr[g];
+      hits += hc.n_hit[g];
+      s.rays_reflect += hc.n_refl[g];
+      s.rays_refract += hc.n_refr[g];
+    }
+  }
+  for (unsigned g = 0; !lr_.persist && g <= lr_.last && g < lr_.counts.rays.size(); ++g) {
     rays += lr_.counts.rays[g];
     if (!lr_.fused) traced_shadows += lr_.counts.shadows[g];
     hits += hc.n_hit[g];

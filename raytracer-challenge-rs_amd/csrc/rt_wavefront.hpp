@@ -38,6 +38,7 @@
 #include <vector>
 
 #include "rt_layout.hpp"
+#include "rt_persist.hpp"
 
 namespace rtamd {
 
@@ -82,14 +83,25 @@ struct PrimRec {  // primary rays share the origin: per diag sphere (s, o', c)
 
 constexpr int kMaxGen = 66;
 enum WfFlags : unsigned { WF_EXHAUSTIVE = 1u, WF_COUNT = 2u };
-extern int g_wf_accel;        // tuning knob: 1 = BVH traversal (when the exhaustive loop is not asked for)
-extern int g_wf_shadow_lb;    // tuning knob: 1 = shadow rays through the light buffer when the scene has one
-extern int g_wf_image;        // tuning knob: 0 = automatic scene image of the fused kernels, 3 / 1 = global memory
-extern int g_wf_treelet;         // tuning knob: the global-memory image stages a treelet in LDS
-extern int g_wf_treelet_deltas;  // tuning knob: ... after the light buffer's distances (when they fit)
-extern int g_wf_shadow_stream;   // tuning knob: 1 = exhaustive shadow traces on a second stream
-extern int g_wf_adaptive_block;  // tuning knob: 1 = small trace launches spread over every CU (smaller blocks)
-extern int g_wf_skip_shadow;  // tuning knob: 1 = the fast path leaves out shadow rays that cannot change the colour
+
+// Render-time tuning of a scene (rt_scene::tune, copied from the process
+// defaults when the scene is created; rtamd_scene_tuning_set changes one
+// scene's). Every render reads its scene's values under the scene's lock, so
+// concurrent renders of different scenes never see each other's settings.
+struct WfTuning {
+  int accel = 1;           // 1 = exact-culling BVH fast path (unless the exhaustive loop is asked for)
+  int persist = 1;         // 1 = the persistent frame kernel (rt_persist.hip) when max_depth <= kPsMaxDepth
+  int skip_shadow = 1;     // 1 = the fast path leaves out shadow rays that cannot change the colour
+  int shadow_lb = 1;       // 1 = shadow rays through the light buffer when the scene has one
+  int image = 0;           // 0 = automatic scene image of the fast-path kernels, 3 / 1 = global memory
+  int treelet = 1;         // the global-memory image stages a treelet in LDS
+  int treelet_deltas = 0;  // ... after the light buffer's distances (when they fit)
+  int shadow_stream = 1;   // exhaustive pipeline: 1 = shadow traces on a second stream when rendering alone
+  int adaptive_block = 0;  // generation pipeline: 1 = small trace launches spread over every CU
+  int corrupt_calibration = 0;  // test hook: generation 1 of a calibrated frame launched one ray short
+};
+// Applies `key` = `value` to `t`: 1 = applied, 0 = not a render-time key, -1 = bad value.
+int wf_tuning_apply(WfTuning& t, const char* key, int value);
 
 // Work counters of the trace kernels, one row per wave slot (wave id mod
 // kWorkRows, rows 128 B apart): thousands of waves ending together would
@@ -205,6 +217,7 @@ struct WfProfile {
   double sh_rays[2], sh_tests[2];  // fused frames: shadow rays / sphere tests inside the primary / secondary launches
   int bvh;          // the last frame traversed the BVH
   int fused;        // the last frame ran the fused pipeline
+  int persist;      // the last frame ran the persistent frame kernel (one launch; its time is the closest class)
 };
 
 class Wavefront {
@@ -234,21 +247,29 @@ class Wavefront {
   hipError_t render(const DevScene& sc, const DevCamera& cam, bool camera_mode, const double* d_in_rays,
                     unsigned n0, unsigned aa, unsigned max_depth, unsigned row_block, unsigned shard,
                     unsigned n_shards, double* d_out, hipStream_t stream, const std::string& signature,
-                    DevStats* stats, float* ms_kernel, bool solo = true, unsigned flags = 0);
+                    DevStats* stats, float* ms_kernel, const WfTuning& tn, bool solo = true, unsigned flags = 0);
   // The counters of the last render (rendered with WF_COUNT); synchronises its stream.
   hipError_t read_stats(DevStats* out);
   // A generation's actual queue count differed from the calibrated launch size
   // (a device-side check of every calibrated frame, wf_check_counts). Sticky
   // until clear_fault(), which also drops the calibration.
-  bool fault() const { return h_fault_ && *(volatile int*)h_fault_ != 0; }
+  // 1: queue check (generation pipeline); 2 / 3: a wait of the persistent
+  // frame kernel exceeded its time bound (rt_persist.hip)
+  int fault() const { return h_fault_ ? *(volatile int*)h_fault_ : 0; }
   void clear_fault() {
     if (h_fault_) *(volatile int*)h_fault_ = 0;
     cache_.clear();
   }
-  // test hook: perturb calibrated launch sizes (generation 1 launched with one ray fewer)
-  static int g_corrupt_calibration;
-
  private:
+  // the persistent frame kernel (rt_persist.hip): one launch per render
+  hipError_t render_persist(const DevScene& sc, const DevCamera& cam, bool camera_mode, const double* d_in_rays,
+                            unsigned n0, unsigned aa, unsigned max_depth, unsigned row_block, unsigned shard,
+                            unsigned n_shards, double* d_out, hipStream_t stream, DevStats* stats, float* ms_kernel,
+                            bool count, const WfTuning& tn);
+  PsRay* ps_rings_ = nullptr;
+  PsParent* ps_parents_ = nullptr;
+  PsCounters* ps_ctr_ = nullptr;
+  size_t ps_rings_cap_ = 0, ps_parents_cap_ = 0;  // records
   hipError_t ensure_gen(size_t g, size_t slots, size_t n_lights, size_t list_slots, bool fused);
   hipError_t ensure_misc(size_t n_diag);
   // shard counters: generation g's rays (q = 0) / shadow list (q = 1)
@@ -275,11 +296,11 @@ class Wavefront {
   struct LastRender {       // what read_stats needs of the last render
     Counts counts;
     unsigned last = 0, L = 0, n0 = 0;
-    bool counted = false, exact_disc = false, bvh = false, fused = false;
+    bool counted = false, exact_disc = false, bvh = false, fused = false, persist = false;
     unsigned long long n_diag = 0, n_gen = 0, n_planes = 0, n_quads = 0;
     hipStream_t stream = nullptr;
   } lr_;
-  bool last_bvh_ = false, last_fused_ = false;
+  bool last_bvh_ = false, last_fused_ = false, last_persist_ = false;
   bool profiling_ = false;
   int pmask_ = (1 << WF_NCLASS) - 1;
   std::vector<hipEvent_t> pev_;        // event pool (pairs)

@@ -181,12 +181,12 @@ def test_accel_knob_off_matches(rt):
     from rtamd import scenes
     w, cam, depth = scenes.zoo(80, 60)
     a, _ = cam.render(w, depth, want_stats=False)
-    rt._rtamd._tuning_set("accel", 0)
+    w.tune("accel", 0)
     try:
         b, _ = cam.render(w, depth, want_stats=False)
         assert not rt._rtamd._wf_profile(w, -1, True)["bvh"]
     finally:
-        rt._rtamd._tuning_set("accel", 1)
+        w.tune("accel", 1)
     assert a.to_numpy().tobytes() == b.to_numpy().tobytes()
 
 
@@ -204,34 +204,39 @@ def test_skipped_shadow_rays_bitwise(rt, neg_zero):
     assert fast.to_numpy().tobytes() == exact.to_numpy().tobytes()
     assert counted.to_numpy().tobytes() == exact.to_numpy().tobytes()
     assert 0 < sf["rays_shadow_traced"] < st["rays_shadow"]
-    rt._rtamd._tuning_set("skip_shadow", 0)
+    w.tune("skip_shadow", 0)
     try:
         full, _ = cam.render(w, depth, want_stats=False)
         _, sa = cam.render(w, depth, want_stats=True, exhaustive=False)
         assert sa["rays_shadow_traced"] == st["rays_shadow"]
     finally:
-        rt._rtamd._tuning_set("skip_shadow", 1)
+        w.tune("skip_shadow", 1)
     assert full.to_numpy().tobytes() == exact.to_numpy().tobytes()
 
 
+@pytest.mark.parametrize("persist", [1, 0])
 @pytest.mark.parametrize("image,shadow_lb", [(0, 1), (0, 0), (3, 1), (3, 0), (1, 1), (1, 0)])
-def test_fused_images_bitwise(rt, image, shadow_lb):
-    """Every scene image of the fused trace kernels (pair layout in LDS, the
+def test_fused_images_bitwise(rt, image, shadow_lb, persist):
+    """Every scene image of the fast-path kernels (pair layout in LDS, the
     default / nodes and records in global memory with an LDS stack / with a
     scratch stack), with shadow rays through the light buffer or through the
-    BVH (the primary launch then takes the wave traversal), gives the
-    exhaustive frame. The scenes above that do not fit in LDS (3000 spheres)
-    run image 3 on their own."""
+    BVH, on the persistent frame kernel and on the generation pipeline (whose
+    primary launch then takes the wave traversal), gives the exhaustive frame.
+    The scenes above that do not fit in LDS (3000 spheres) run image 3 on
+    their own."""
     w, cam, depth = _glass_cluster(rt, n=250, seed=21, inside=False)
     exact, _ = cam.render(w, depth, want_stats=True)
-    rt._rtamd._tuning_set("image", image)
-    rt._rtamd._tuning_set("shadow_lb", shadow_lb)
+    w.tune("image", image)
+    w.tune("shadow_lb", shadow_lb)
+    w.tune("persist", persist)
     try:
         fast, _ = cam.render(w, depth, want_stats=False)
-        assert rt._rtamd._wf_profile(w, -1, True)["fused"]
+        p = rt._rtamd._wf_profile(w, -1, True)
+        assert p["fused"] and p["persist"] == bool(persist)
     finally:
-        rt._rtamd._tuning_set("image", 0)
-        rt._rtamd._tuning_set("shadow_lb", 1)
+        w.tune("image", 0)
+        w.tune("shadow_lb", 1)
+        w.tune("persist", 1)
     assert fast.to_numpy().tobytes() == exact.to_numpy().tobytes()
 
 

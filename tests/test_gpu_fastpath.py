@@ -144,26 +144,34 @@ def test_render_multi_one_device_equals_render(rt):
     assert st4["rays_primary"] == 4 * 200 * 113
 
 
-def test_queue_check_reports_miscalibration(rt):
-    """A calibrated frame whose queue counts differ from its launch sizes (here
-    forced by a test hook that launches generation 1 one ray short) fails the
-    next call with RT_ERR_HIP instead of silently dropping rays; the library
-    then recalibrates."""
+@pytest.mark.parametrize("via_check", [False, True])
+def test_queue_check_reports_miscalibration(rt, via_check):
+    """The generation pipeline (persist off): a calibrated frame whose queue
+    counts differ from its launch sizes (here forced by a test hook that
+    launches generation 1 one ray short) fails the next call, or
+    rt_scene_check, with RT_ERR_HIP instead of silently dropping rays; the
+    library then recalibrates."""
     import torch
     from rtamd import scenes
     w, cam, depth = scenes.c3(96, 54, n_spheres=200)
     exact, _ = _device_frame(cam, w, depth, True)
+    w.tune("persist", 0)
     st = rt.render_stream(False)
     buf = torch.empty_like(exact)
     cam.render_shard_device(w, depth, 8, 0, 1, buf.data_ptr(), st.cuda_stream, False)  # calibrates
-    rt._rtamd._tuning_set("corrupt_calibration", 1)
+    w.tune("corrupt_calibration", 1)
     try:
         cam.render_shard_device(w, depth, 8, 0, 1, buf.data_ptr(), st.cuda_stream, False)
         torch.cuda.synchronize()
     finally:
-        rt._rtamd._tuning_set("corrupt_calibration", 0)
+        w.tune("corrupt_calibration", 0)
     with pytest.raises(rt.RtError, match="queue check"):
-        cam.render_shard_device(w, depth, 8, 0, 1, buf.data_ptr(), st.cuda_stream, False)
+        if via_check:
+            w.check()
+        else:
+            cam.render_shard_device(w, depth, 8, 0, 1, buf.data_ptr(), st.cuda_stream, False)
     cam.render_shard_device(w, depth, 8, 0, 1, buf.data_ptr(), st.cuda_stream, False)  # recalibrates
     torch.cuda.synchronize()
+    w.check()
+    w.tune("persist", 1)
     assert torch.equal(buf, exact)

@@ -25,11 +25,11 @@ def _three(rt, make, lb_res=256):
         w, cam, depth = make(rt)
         prof_world = w
         fast, _ = cam.render(w, depth, want_stats=False)
-        rt._rtamd._tuning_set("shadow_lb", 0)
+        w.tune("shadow_lb", 0)
         try:
             bvh, _ = cam.render(w, depth, want_stats=False)
         finally:
-            rt._rtamd._tuning_set("shadow_lb", 1)
+            w.tune("shadow_lb", 1)
         exact, _ = cam.render(w, depth, want_stats=True)
         p = rt._rtamd._wf_profile(prof_world, -1, True)
     finally:

@@ -21,6 +21,8 @@ def _targs(n, name):
 def klass(n):
     """Kernel class of a demangled name: primary / closest / shadow / prep /
     combine / frame (wf_frame_init: one per rendered frame)."""
+    if "ps_render<" in n:  # the persistent frame kernel: the whole frame in one launch
+        return "persist"
     if "wf_trace_fused<" in n:  # fused generation: closest hit + shading + shadow rays + spawn
         return "primary" if _targs(n, "wf_trace_fused")[0] == "true" else "closest"
     if "wf_trace_closest_bvh<" in n:
@@ -47,6 +49,7 @@ ap.add_argument("--spheres", type=int, default=1000)
 ap.add_argument("--n-gpus", type=int, default=1)
 ap.add_argument("--dominant", default="closest")
 ap.add_argument("--traversal", default="bvh", help="bvh (fast path) or exhaustive")
+ap.add_argument("--build", default=None, help="the build the passes profiled (git describe / tag)")
 a = ap.parse_args()
 
 tot = collections.defaultdict(lambda: collections.defaultdict(float))
@@ -58,14 +61,15 @@ for d in a.dirs:
             c = klass(r["Kernel_Name"])
             if c is None:
                 continue
-            if c == "frame":
+            if c in ("frame", "persist"):  # one frame_init or one ps_render dispatch per rendered frame
                 seen.add(r["Dispatch_Id"])
+            if c == "frame":
                 continue
             tot[c][r["Counter_Name"]] += float(r["Counter_Value"])
         frames[f] = len(seen)
 nf = max(frames.values()) if frames else 0
 res = {"width": a.width, "height": a.height, "spheres": a.spheres, "n_gpus": a.n_gpus, "traversal": a.traversal,
-       "frames_per_pass": nf, "per_frame": {}}
+       "frames_per_pass": nf, "per_frame": {}, "build": a.build}
 for c, cs in tot.items():
     pf = {k: v / max(nf, 1) for k, v in cs.items()}
     if "FETCH_SIZE" in pf or "WRITE_SIZE" in pf:

@@ -30,11 +30,11 @@ for kv in a.knob:
 w, cam, depth = scenes.c3(a.width, a.height, a.spheres) if a.config == "c3" else scenes.c5(a.width, a.height, a.spheres)
 w.upload(0)
 if a.exhaustive:
-    rtamd._rtamd._tuning_set("accel", 0)
+    w.tune("accel", 0)
 r, n = (int(x) for x in a.shard.split("/"))
 rows = rtamd.shard_rows(a.height, 8, r, n)
 F = max(1, a.inflight)
-rtamd._rtamd._tuning_set("shadow_stream", 0)  # as bench.py (its serialized roofline pass: one stream)
+w.tune("shadow_stream", 0)  # as bench.py (its serialized roofline pass: one stream)
 bufs = [torch.empty((rows, a.width, 3), dtype=torch.float64, device="cuda") for _ in range(F)]
 streams = [torch.cuda.Stream() for _ in range(F)] if F > 1 else [torch.cuda.current_stream()]
 torch.cuda.synchronize()

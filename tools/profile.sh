@@ -25,6 +25,7 @@ run p3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_L
 run p4 --pmc FETCH_SIZE && \
 run p5 --pmc WRITE_SIZE && \
 run p6 --pmc TCC_HIT_sum TCC_MISS_sum && \
-python tools/pmc_summary.py "$OUT/pmc_summary.json" --dominant "${DOMINANT:-closest}" --traversal "${TRAVERSAL:-bvh}" \
+python tools/pmc_summary.py "$OUT/pmc_summary.json" --dominant "${DOMINANT:-persist}" --traversal "${TRAVERSAL:-bvh}" \
+  --build "$(cat BUILD_ID 2>/dev/null || echo unknown)" \
   $SUMMARY_ARGS "$OUT"/p1 "$OUT"/p2 "$OUT"/p3 "$OUT"/p4 "$OUT"/p5 "$OUT"/p6 > /dev/null && \
   echo "summary ok" | tee -a "$OUT/steps.log"

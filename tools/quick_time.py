@@ -43,7 +43,7 @@ t_up = time.perf_counter() - t0
 F = a.inflight or (4 if a.config == "c3" else 1)
 r, n = (int(x) for x in a.shard.split("/"))
 rows = rtamd.shard_rows(H, 8, r, n)
-rtamd._rtamd._tuning_set("shadow_stream", 0)
+w.tune("shadow_stream", 0)
 streams = [rtamd.render_stream(False) for _ in range(F)] if F > 1 else [torch.cuda.current_stream()]
 bufs = [torch.empty((rows, W, 3), dtype=torch.float64, device="cuda") for _ in range(F)]
 s0 = torch.cuda.current_stream().cuda_stream

@@ -52,7 +52,7 @@ for n in [int(x) for x in a.ns.split(",")]:
         rows = rtamd.shard_rows(H, B, r, n)
         F = max(1, a.inflight)
         if F > 1:
-            rtamd._rtamd._tuning_set("shadow_stream", 0)  # as bench.py
+            w.tune("shadow_stream", 0)  # as bench.py
         bufs = [torch.empty((rows, W, 3), dtype=torch.float64, device="cuda") for _ in range(F)]
         sts = _made or ([torch.cuda.Stream() for _ in range(F)] if F > 1 else [torch.cuda.current_stream()])
         torch.cuda.synchronize()
