@@ -339,8 +339,10 @@ int check_faults(rt_scene* s) {
       if (f == 1)
         return fail(RT_ERR_HIP, "wavefront queue check: a generation's ray count differed from its calibrated "
                                 "launch size in an earlier frame (rays may be missing from that frame)");
+      std::string d;
+      for (int k = 1; k < 24; ++k) d += (k > 1 ? "," : "") + std::to_string(w.wf->fault_word(k));
       return fail(RT_ERR_HIP, "persistent frame kernel: a wait exceeded its time bound in an earlier frame (that "
-                              "frame was abandoned incomplete)");
+                              "frame was abandoned incomplete; code " + std::to_string(f) + ": " + d + ")");
     }
   return RT_OK;
 }

@@ -51,6 +51,20 @@ __device__ __forceinline__ void ps_st2(void* p, double x, double y) {
 }
 __device__ __forceinline__ ps_d2 ps_ld2(const void* p) { return __builtin_nontemporal_load((const ps_d2*)p); }
 
+// A wait exceeded its time bound: record what this wave saw (host-mapped,
+// read back in the library's error text), then the code (word 0).
+__device__ __noinline__ void ps_fault(const PsArgs& a, const PsSched& S, int code, unsigned it,
+                                      unsigned long long dt) {
+  volatile int* f = a.fault;
+  f[1] = (int)blockIdx.x; f[2] = (int)(threadIdx.x >> 6);
+  f[3] = (int)S.head; f[4] = (int)S.tail; f[5] = (int)S.commit; f[6] = (int)S.busy;
+  f[7] = (int)S.roots_done; f[8] = (int)S.tree_free; f[9] = (int)S.cls_done;
+  f[10] = (int)it; f[11] = (int)(dt & 0xFFFFFFFFull); f[12] = (int)(dt >> 32);
+  for (int k = 0; k < 8; ++k) f[13 + k] = S.live[k];
+  f[21] = (int)gridDim.x; f[22] = (int)a.trees; f[23] = (int)a.q_cap;
+  f[0] = code;
+}
+
 // The next camera chunk for this workgroup: class counters first its own
 // (blocks are dealt round-robin to the XCDs), then the others'.
 __device__ __forceinline__ unsigned ps_next_chunk(PsSched& S, const PsArgs& a, unsigned n_chunks) {
@@ -128,7 +142,7 @@ __device__ void ps_acquire(PsSched& S, const PsArgs& a, unsigned n_chunks, unsig
       if (it == 0) {
         t0 = now;
       } else if (now - t0 > kPsWaitTicks) {
-        *(volatile int*)a.fault = 2;
+        ps_fault(a, S, 2, it, now - t0);
         kind = PS_EXIT;
         return;
       }
@@ -379,7 +393,7 @@ __global__ __launch_bounds__(kTraceBlock, 4) void ps_render(DevScene sc, DevCame
             if (it == 0) {
               t0 = now;
             } else if (now - t0 > kPsWaitTicks) {
-              *(volatile int*)a.fault = 3;
+              ps_fault(a, S, 3, it, now - t0);
               break;
             }
           }

@@ -1036,8 +1036,8 @@ hipError_t Wavefront::ensure_side() {
 hipError_t Wavefront::ensure_misc(size_t n_diag) {
   if (!d_cnt_) WF_CHECK(hipMalloc(&d_cnt_, sizeof(WfCounters)));
   if (!h_fault_) {
-    WF_CHECK(hipHostMalloc((void**)&h_fault_, sizeof(int), hipHostMallocMapped));
-    *(volatile int*)h_fault_ = 0;
+    WF_CHECK(hipHostMalloc((void**)&h_fault_, kFaultWords * sizeof(int), hipHostMallocMapped));
+    for (int k = 0; k < kFaultWords; ++k) ((volatile int*)h_fault_)[k] = 0;
     WF_CHECK(hipHostGetDevicePointer((void**)&d_fault_, h_fault_, 0));
   }
   if (!d_shard_) WF_CHECK(hipMalloc(&d_shard_, (size_t)kMaxGen * 2 * kShards * kShardStride * sizeof(unsigned)));

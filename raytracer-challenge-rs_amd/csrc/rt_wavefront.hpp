@@ -256,6 +256,9 @@ class Wavefront {
   // 1: queue check (generation pipeline); 2 / 3: a wait of the persistent
   // frame kernel exceeded its time bound (rt_persist.hip)
   int fault() const { return h_fault_ ? *(volatile int*)h_fault_ : 0; }
+  // words 1.. of the fault record: what the faulting wave saw (rt_persist.hip ps_fault)
+  static constexpr int kFaultWords = 32;
+  int fault_word(int k) const { return h_fault_ && k < kFaultWords ? ((volatile int*)h_fault_)[k] : 0; }
   void clear_fault() {
     if (h_fault_) *(volatile int*)h_fault_ = 0;
     cache_.clear();
