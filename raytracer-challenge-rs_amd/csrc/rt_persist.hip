@@ -88,6 +88,7 @@ __device__ __forceinline__ unsigned ps_next_chunk(PsSched& S, const PsArgs& a, u
 __device__ void ps_acquire(PsSched& S, const PsArgs& a, unsigned n_chunks, unsigned& kind, unsigned& base,
                            unsigned& take, unsigned& tree) {
   unsigned long long t0 = 0;
+  unsigned waits = 0;
   for (unsigned it = 0;; ++it) {
     atomicAdd(&S.busy, 1u);
     unsigned h = ps_ld(&S.head), c = ps_ld(&S.commit);
@@ -137,9 +138,9 @@ __device__ void ps_acquire(PsSched& S, const PsArgs& a, unsigned n_chunks, unsig
       kind = PS_EXIT;
       return;
     }
-    if ((it & 63u) == 0u) {
+    if ((waits++ & 63u) == 0u) {  // the clock starts at this wave's first wait (not at a lost CAS)
       const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-      if (it == 0) {
+      if (waits == 1u) {
         t0 = now;
       } else if (now - t0 > kPsWaitTicks) {
         ps_fault(a, S, 2, it, now - t0);
