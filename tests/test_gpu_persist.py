@@ -119,12 +119,11 @@ def test_persist_back_to_back_and_shards(rt):
     for b in bufs:
         cam.render_shard_device(w, depth, 8, 0, 1, b.data_ptr(), st, False)
     streams = [rt.render_stream() for _ in range(4)]
-    shards = []
+    shards = [torch.full((rt.shard_rows(cam.vsize, 8, s, 8), cam.hsize, 3), -1.0, dtype=torch.float64, device="cuda")
+              for s in range(8)]
+    torch.cuda.synchronize()  # the fills (current stream) before the renders (other streams)
     for s in range(8):
-        rows = rt.shard_rows(cam.vsize, 8, s, 8)
-        buf = torch.full((rows, cam.hsize, 3), -1.0, dtype=torch.float64, device="cuda")
-        cam.render_shard_device(w, depth, 8, s, 8, buf.data_ptr(), streams[s % 4].cuda_stream, False)
-        shards.append(buf)
+        cam.render_shard_device(w, depth, 8, s, 8, shards[s].data_ptr(), streams[s % 4].cuda_stream, False)
     torch.cuda.synchronize()
     w.check()
     for b in bufs:
