@@ -124,7 +124,8 @@ __device__ void ps_acquire(PsSched& S, const PsArgs& a, unsigned n_chunks, unsig
     }
     h = ps_ld(&S.head);
     c = ps_ld(&S.commit);
-    if (c != h) {
+    // policy 1: fewer than 64 queued rays only when no other wave can add to them
+    if (c != h && (a.policy == 0u || ps_ld(&S.roots_done) || ps_ld(&S.busy) <= 1u)) {
       const unsigned n = min(64u, c - h);
       if (atomicCAS(&S.head, h, h + n) == h) {
         kind = PS_QUEUED; base = h; take = n;
@@ -236,6 +237,12 @@ struct PsTally {
   unsigned disc = 0, tests = 0, boxes = 0;
   unsigned sh_disc = 0, sh_tests = 0, sh_boxes = 0, sh_rays = 0;
 };
+// shader clock (counted launches only: where a wave's time goes)
+template <bool TALLY>
+__device__ __forceinline__ unsigned long long ps_clock() {
+  if constexpr (TALLY) return __builtin_amdgcn_s_memtime();
+  return 0ull;
+}
 
 // One frame. LANE: the scene image (rt_trace.hpp lane_scene: 14 = pair
 // layout in LDS, 3 = global nodes with an LDS stack and treelet, 1 = global
@@ -260,9 +267,11 @@ __global__ __launch_bounds__(kTraceBlock, 4) void ps_render(DevScene sc, DevCame
   PsTally tl;
   for (;;) {
     unsigned kind = 0, base = 0, take = 0, tree = 0;
+    const unsigned long long c0 = ps_clock<TALLY>();
     if (lane == 0) ps_acquire(S, a, n_chunks, kind, base, take, tree);
     kind = (unsigned)__shfl((int)kind, 0, 64);
     if (kind == PS_EXIT) break;
+    const unsigned long long c1 = ps_clock<TALLY>();
     base = (unsigned)__shfl((int)base, 0, 64);
     take = (unsigned)__shfl((int)take, 0, 64);
     tree = (unsigned)__shfl((int)tree, 0, 64);
@@ -299,6 +308,7 @@ __global__ __launch_bounds__(kTraceBlock, 4) void ps_render(DevScene sc, DevCame
                                      tl.tests, tl.boxes, ls.stack, ls.top, ls.n_top);
     }
     hit_finish(h);
+    const unsigned long long c2 = ps_clock<TALLY>();
     // ---- color_at's shading (world.rs:70-81, 40-68): prepare_computations,
     // the children, every light's shadow ray and lighting()
     const unsigned g = 31u - (unsigned)__clz((int)(node + 1u));  // depth of heap node `node`
@@ -403,6 +413,7 @@ __global__ __launch_bounds__(kTraceBlock, 4) void ps_render(DevScene sc, DevCame
         __hip_atomic_store(&S.commit, rb + nr + nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
+    const unsigned long long c3 = ps_clock<TALLY>();
     // ---- nodes without children: their colour is final
     if (valid && nk == 0u) {
       V3 col = v3(0.0, 0.0, 0.0);  // a miss is black (world.rs:74-75)
@@ -418,6 +429,7 @@ __global__ __launch_bounds__(kTraceBlock, 4) void ps_render(DevScene sc, DevCame
       if (left == 0) atomicOr(&S.tree_free, 1u << t);
     }
     if constexpr (TALLY) {  // counted launch: executed work per class, shade_hit runs and children per depth
+      const unsigned long long c4 = ps_clock<TALLY>();
       const unsigned cls = kind == PS_ROOTS ? (unsigned)WF_PRIMARY : (unsigned)WF_CLOSEST;
       const unsigned long long s = wave_sum(tl.disc), st = wave_sum(tl.tests), sb = wave_sum(tl.boxes);
       const unsigned long long hs = wave_sum(tl.sh_disc), hst = wave_sum(tl.sh_tests), hsb = wave_sum(tl.sh_boxes);
@@ -431,6 +443,13 @@ __global__ __launch_bounds__(kTraceBlock, 4) void ps_render(DevScene sc, DevCame
         if (hst) { atomicAdd(&w->tests[WF_SHADOW], hst); atomicAdd(&w->sh_tests[cls], hst); }
         if (hsb) atomicAdd(&w->boxes[WF_SHADOW], hsb);
         if (hr) atomicAdd(&w->sh_rays[cls], hr);
+        const unsigned q = kind == PS_ROOTS ? 0u : 1u;
+        atomicAdd(&w->ps_items[q], 1ull);
+        atomicAdd(&w->ps_lanes[q], (unsigned long long)take);
+        atomicAdd(&w->ps_cycles[0], c1 - c0);
+        atomicAdd(&w->ps_cycles[1], c2 - c1);
+        atomicAdd(&w->ps_cycles[2], c3 - c2);
+        atomicAdd(&w->ps_cycles[3], c4 - c3);
       }
       tl = PsTally{};
       if (a.count && valid) {

@@ -88,6 +88,7 @@ struct PsArgs {
   unsigned n0, max_depth;
   unsigned camera_mode, aa, rows, row_block, shard, n_shards;
   unsigned use_lb, lds_flags, n_top, skip_shadow, count;
+  unsigned policy;  // WfTuning::ps_policy: 0 = queued rays before an idle wave; 1 = a partial chunk only when no other wave can add to it
 };
 
 // Launchers (rt_persist.hip, one object per image class): the LDS image

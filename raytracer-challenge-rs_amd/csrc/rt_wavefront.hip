@@ -37,7 +37,9 @@ int wf_tuning_apply(WfTuning& t, const char* key, int value) {
       {"image", &WfTuning::image, 0, 3},           {"treelet", &WfTuning::treelet, 0, 1},
       {"treelet_deltas", &WfTuning::treelet_deltas, 0, 1}, {"shadow_stream", &WfTuning::shadow_stream, 0, 2},
       {"adaptive_block", &WfTuning::adaptive_block, 0, 1},
-      {"corrupt_calibration", &WfTuning::corrupt_calibration, 0, 1}};
+      {"corrupt_calibration", &WfTuning::corrupt_calibration, 0, 1},
+      {"ps_trees", &WfTuning::ps_trees, 0, 32},     {"ps_policy", &WfTuning::ps_policy, 0, 1},
+      {"ps_grid", &WfTuning::ps_grid, 0, 4096}};
   if (!key) return 0;
   for (const Knob& k : knobs) {
     if (std::strcmp(key, k.name) != 0) continue;
@@ -968,6 +970,8 @@ hipError_t Wavefront::last_profile(WfProfile* out) {
     out->sh_tests[c] = (double)hc.sh_tests(c);
   }
   if (last_fused_) out->rays[WF_SHADOW] = out->sh_rays[0] + out->sh_rays[1];  // traced inside the fused launches
+  for (int c = 0; c < 2; ++c) { out->ps_items[c] = (double)hc.ps_items(c); out->ps_lanes[c] = (double)hc.ps_lanes(c); }
+  for (int c = 0; c < 4; ++c) out->ps_cycles[c] = (double)hc.ps_cycles(c);
   if (last_persist_) {  // one launch: the root rays and, from a counted frame, the children per depth
     out->rays[WF_PRIMARY] = (double)lr_.n0;
     double kids = 0.0;
@@ -1444,14 +1448,16 @@ hipError_t Wavefront::render_persist(const DevScene& sc, const DevCamera& cam, b
   n_cu = std::max(n_cu, 1);
   // one workgroup per CU (the LDS image); small renders take fewer (two camera chunks each)
   const unsigned n_chunks = (n0 + 63u) / 64u;
-  const unsigned grid = std::max(1u, std::min((unsigned)n_cu, (n_chunks + 1u) / 2u));
+  unsigned grid = std::max(1u, std::min((unsigned)n_cu, (n_chunks + 1u) / 2u));
+  if (tn.ps_grid > 0) grid = std::min((unsigned)tn.ps_grid, std::max(1u, n_chunks));
   // heap-addressed trees: 2^d - 1 nodes per root may have children, at most 2^d
   // rays of one root are queued or traced at once (an antichain of its tree)
   const unsigned n_int = (1u << max_depth) - 1u;
   const size_t leaves = (size_t)1 << max_depth;
   const size_t per_tree = 64 * ((size_t)n_int * sizeof(PsParent) + leaves * sizeof(PsRay));
-  const unsigned trees =
+  unsigned trees =
       (unsigned)std::min<size_t>(kPsMaxTrees, std::max<size_t>(4, kPsBudget / ((size_t)n_cu * per_tree)));
+  if (tn.ps_trees > 0) trees = (unsigned)tn.ps_trees;
   const size_t q_cap = (size_t)trees * 64 * leaves + kPsSpare;
   WF_CHECK(grow(ps_rings_, ps_rings_cap_, (size_t)grid * q_cap));
   WF_CHECK(grow(ps_parents_, ps_parents_cap_, std::max<size_t>(1, (size_t)grid * trees * 64 * n_int)));
@@ -1498,6 +1504,7 @@ hipError_t Wavefront::render_persist(const DevScene& sc, const DevCamera& cam, b
   a.use_lb = use_lb ? 1u : 0u;
   a.skip_shadow = tn.skip_shadow ? 1u : 0u;
   a.count = count ? 1u : 0u;
+  a.policy = (unsigned)tn.ps_policy;
   if (count) WF_CHECK(hipMemsetAsync(d_cnt_, 0, sizeof(WfCounters), stream));
   if (ms_kernel) WF_CHECK(hipEventRecord(ev0_, stream));
   if (profiling_) ++pframes_;

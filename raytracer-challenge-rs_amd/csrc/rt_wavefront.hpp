@@ -99,6 +99,9 @@ struct WfTuning {
   int shadow_stream = 1;   // exhaustive pipeline: 1 = shadow traces on a second stream when rendering alone
   int adaptive_block = 0;  // generation pipeline: 1 = small trace launches spread over every CU
   int corrupt_calibration = 0;  // test hook: generation 1 of a calibrated frame launched one ray short
+  int ps_trees = 0;        // persistent kernel: tree slots per workgroup (0 = from the memory budget, at most 32)
+  int ps_policy = 0;       // persistent kernel: when a wave takes fewer than 64 queued rays (PsArgs::policy)
+  int ps_grid = 0;         // persistent kernel: workgroups (0 = one per CU, fewer for small renders)
 };
 // Applies `key` = `value` to `t`: 1 = applied, 0 = not a render-time key, -1 = bad value.
 int wf_tuning_apply(WfTuning& t, const char* key, int value);
@@ -114,6 +117,10 @@ struct alignas(128) WfWorkRow {
   unsigned long long boxes[3];  // BVH mode: child-box tests executed (lanes x boxes)
   unsigned long long sh_rays[2];   // fused kernels: shadow rays traced, [0] primary / [1] secondary launches
   unsigned long long sh_tests[2];  // fused kernels: shadow sphere tests executed, per launch class
+  // persistent kernel (counted launches): its work items and where its waves' time goes
+  unsigned long long ps_items[2];   // chunks taken: [0] camera chunks, [1] queued-ray chunks
+  unsigned long long ps_lanes[2];   // rays in them (lane use of the items = lanes / (64 x items))
+  unsigned long long ps_cycles[4];  // shader clocks: [0] getting work, [1] trace, [2] shading + spawn, [3] delivery
 };
 // Fused launches hand out their rays in chunks of 64 (one wave-iteration) from
 // per-XCD counters, kChunkClasses per generation, each on a 128-B line.
@@ -141,6 +148,21 @@ struct WfCounters {
   unsigned long long sh_rays(int c) const {
     unsigned long long t = 0;
     for (int r = 0; r < kWorkRows; ++r) t += work[r].sh_rays[c];
+    return t;
+  }
+  unsigned long long ps_items(int c) const {
+    unsigned long long t = 0;
+    for (int r = 0; r < kWorkRows; ++r) t += work[r].ps_items[c];
+    return t;
+  }
+  unsigned long long ps_lanes(int c) const {
+    unsigned long long t = 0;
+    for (int r = 0; r < kWorkRows; ++r) t += work[r].ps_lanes[c];
+    return t;
+  }
+  unsigned long long ps_cycles(int c) const {
+    unsigned long long t = 0;
+    for (int r = 0; r < kWorkRows; ++r) t += work[r].ps_cycles[c];
     return t;
   }
   unsigned long long sh_tests(int c) const {
@@ -218,6 +240,7 @@ struct WfProfile {
   int bvh;          // the last frame traversed the BVH
   int fused;        // the last frame ran the fused pipeline
   int persist;      // the last frame ran the persistent frame kernel (one launch; its time is the closest class)
+  double ps_items[2], ps_lanes[2], ps_cycles[4];  // persistent kernel, counted frame (WfWorkRow)
 };
 
 class Wavefront {
