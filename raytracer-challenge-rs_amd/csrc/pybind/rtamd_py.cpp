@@ -58,7 +58,7 @@ extern "C" int rtamd_nccl_comm_init(int nranks, const unsigned char* id, size_t 
 extern "C" int rtamd_nccl_comm_abort(void* comm);
 extern "C" int rtamd_nccl_gather_f64(const double* send, double* recv, size_t count, int root, void* comm, void* stream);
 extern "C" int rtamd_nccl_comm_destroy(void* comm);
-extern "C" int rtamd_wf_profile(const rt_scene* s, int enable, double out[43]);
+extern "C" int rtamd_wf_profile(const rt_scene* s, int enable, double out[45]);
 extern "C" int rtamd_scene_tuning_set(const rt_scene* s, const char* key, int value);
 
 PYBIND11_MODULE(_rtamd, m) {
@@ -437,7 +437,7 @@ PYBIND11_MODULE(_rtamd, m) {
       }, py::arg("max_depth") = 5)
       .def("render_to", &SceneParser::render_to, py::arg("path"), py::arg("max_depth") = 5);
   m.def("_wf_profile", [](const World& w, int enable, bool read) {
-    double o[43] = {0};
+    double o[45] = {0};
     check(rtamd_wf_profile(w.scene(), enable, read ? o : nullptr), "wf_profile");
     py::dict d;
     if (read) {
@@ -460,7 +460,7 @@ PYBIND11_MODULE(_rtamd, m) {
       py::dict ps;
       ps["items_roots"] = o[35]; ps["items_queued"] = o[36]; ps["lanes_roots"] = o[37]; ps["lanes_queued"] = o[38];
       ps["cycles_acquire"] = o[39]; ps["cycles_trace"] = o[40]; ps["cycles_shade"] = o[41];
-      ps["cycles_deliver"] = o[42];
+      ps["cycles_spawn"] = o[42]; ps["cycles_combine"] = o[43];
       d["ps"] = ps;
     }
     return d;

@@ -412,8 +412,8 @@ const char* rt_last_error(void) { return g_err.c_str(); }
 // n_diag, n_gen, n_planes, n_lights, n_quads, tests[3], boxes[3], bvh,
 // n_bvh_nodes, bvh_depth, n_obvh_nodes, n_other_culled, lb_res, lb_items, sh_rays[2], sh_tests[2]
 // (shadow rays / sphere tests inside the fused primary / secondary launches), fused, persist,
-// persistent kernel items[2], lanes[2], cycles[4] (counted frames).
-int rtamd_wf_profile(const rt_scene* cs, int enable, double out[43]) {
+// persistent kernel items[2], lanes[2], cycles[6] (counted frames).
+int rtamd_wf_profile(const rt_scene* cs, int enable, double out[45]) {
   if (!cs) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
   rt_scene* s = const_cast<rt_scene*>(cs);
   std::lock_guard<std::mutex> lk(s->mu);
@@ -458,7 +458,7 @@ int rtamd_wf_profile(const rt_scene* cs, int enable, double out[43]) {
     out[33] = p.fused;
     out[34] = p.persist;
     for (int i = 0; i < 2; ++i) { out[35 + i] = p.ps_items[i]; out[37 + i] = p.ps_lanes[i]; }
-    for (int i = 0; i < 4; ++i) out[39 + i] = p.ps_cycles[i];
+    for (int i = 0; i < 6; ++i) out[39 + i] = p.ps_cycles[i];
   }
   return RT_OK;
 }

@@ -34,6 +34,7 @@ struct PsSched {
   unsigned pad;
   int live[kPsMaxTrees];         // rays of tree t not yet finished (queued, being traced, or published)
   unsigned root0[kPsMaxTrees];   // root index of tree t's first ray (its camera chunk * 64)
+  unsigned lvl[kPsMaxTrees][kPsMaxDepth];  // nodes with children of tree t per depth (its level lists)
 };
 static_assert(sizeof(PsSched) <= kPsSchedBytes, "PsSched exceeds its LDS budget (rt_persist.hpp)");
 
@@ -185,52 +186,50 @@ __device__ __forceinline__ double* ps_root_dst(const PsArgs& a, const DevCamera&
   return a.out + oi * 3;
 }
 
-// The colour `col` of heap node `n` of root ray (t, px) is final: hand it to
-// the parent's record. The child that arrives last at a parent evaluates
-// shade_hit's combination for it (world.rs:58-67; the reflected colour is
+// Tree t is finished (every ray of its 64 roots has been traced and every
+// node without children has written its colour into its parent's record):
+// evaluate shade_hit's combination (world.rs:58-67; the reflected colour is
 // color_at(reflect ray) * reflective, world.rs:113, the refracted one
-// * transparency, world.rs:133) and continues upward; the root's colour is
-// written to the output.
-__device__ __forceinline__ void ps_deliver(const DevScene& sc, const PsArgs& a, const DevCamera& cam,
-                                           PsParent* par, const PsSched& S, unsigned t, unsigned px, unsigned n,
-                                           V3 col) {
-  while (n != 0u) {
-    const unsigned pn = (n - 1u) >> 1;
-    const bool refr_side = ((n - 1u) & 1u) != 0u;
-    PsParent* P = par + ((size_t)t * 64u + px) * a.n_int + pn;
-    double* dst = refr_side ? P->refr : P->refl;
-    ps_st2(dst, col.x, col.y);
-    __builtin_nontemporal_store(col.z, dst + 2);
-    ps_drain();
-    const unsigned before =
-        __hip_atomic_fetch_sub(&P->pending, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (before != 1u) return;  // the sibling has not delivered yet: it continues from here
-    const ps_d2 s01 = ps_ld2(P->surface), s2k = ps_ld2(&P->surface[2]);
-    const ps_u4 tl = __builtin_nontemporal_load((const ps_u4*)&P->obj);
-    const ShadeRec& m = sc.shade[(int)tl.x];
-    V3 refl = v3(0.0, 0.0, 0.0), refr = v3(0.0, 0.0, 0.0);
-    if (tl.y & 1u) {
-      V3 cc = col;
-      if (refr_side) {
+// * transparency, world.rs:133) for its nodes with children, deepest level
+// first, one node per lane; a level's colours go into the next level's
+// records (or, at the roots, the output) before that level is read.
+// Run by one whole wave.
+__device__ __forceinline__ void ps_combine_tree(const DevScene& sc, const PsArgs& a, const DevCamera& cam,
+                                                PsParent* par, const uint16_t* lists, PsSched& S, unsigned t) {
+  const unsigned lane = lane_id();
+  for (int g = (int)a.max_depth - 1; g >= 0; --g) {
+    const unsigned cnt = S.lvl[t][g];
+    const uint16_t* lst = lists + ((size_t)t * (64u * a.n_int) + 64u * ((1u << g) - 1u));
+    for (unsigned i = lane; i < cnt; i += 64u) {
+      const unsigned e = __builtin_nontemporal_load(lst + i);
+      const unsigned px = e >> 10, node = e & 1023u;
+      const PsParent* P = par + ((size_t)t * 64u + px) * a.n_int + node;
+      const ps_d2 s01 = ps_ld2(P->surface), s2k = ps_ld2(&P->surface[2]);
+      const ps_u4 tl = __builtin_nontemporal_load((const ps_u4*)&P->obj);
+      const ShadeRec& m = sc.shade[(int)tl.x];
+      V3 refl = v3(0.0, 0.0, 0.0), refr = v3(0.0, 0.0, 0.0);
+      if (tl.y & 1u) {
         const ps_d2 q = ps_ld2(P->refl);
-        cc = v3(q.x, q.y, __builtin_nontemporal_load(&P->refl[2]));
+        refl = vscale(v3(q.x, q.y, __builtin_nontemporal_load(&P->refl[2])), m.reflective);
       }
-      refl = vscale(cc, m.reflective);
-    }
-    if (tl.y & 2u) {
-      V3 cc = col;
-      if (!refr_side) {
+      if (tl.y & 2u) {
         const ps_d2 q = ps_ld2(P->refr);
-        cc = v3(q.x, q.y, __builtin_nontemporal_load(&P->refr[2]));
+        refr = vscale(v3(q.x, q.y, __builtin_nontemporal_load(&P->refr[2])), m.transparency);
       }
-      refr = vscale(cc, m.transparency);
+      const V3 col = shade_color(m, v3(s01.x, s01.y, s2k.x), refl, refr, s2k.y);
+      double* dst;
+      if (node == 0u) {
+        dst = ps_root_dst(a, cam, S.root0[t] + px);
+      } else {
+        PsParent* Q = par + ((size_t)t * 64u + px) * a.n_int + ((node - 1u) >> 1);
+        dst = ((node - 1u) & 1u) ? Q->refr : Q->refl;
+      }
+      ps_st2(dst, col.x, col.y);
+      __builtin_nontemporal_store(col.z, dst + 2);
     }
-    col = shade_color(m, v3(s01.x, s01.y, s2k.x), refl, refr, s2k.y);
-    n = pn;
+    ps_drain();  // this level's colours are in the L2 before the next level reads them
   }
-  double* out = ps_root_dst(a, cam, S.root0[t] + px);
-  ps_st2(out, col.x, col.y);
-  __builtin_nontemporal_store(col.z, out + 2);
+  if (lane < kPsMaxDepth) S.lvl[t][lane] = 0u;
 }
 
 struct PsTally {
@@ -257,12 +256,14 @@ __global__ __launch_bounds__(kTraceBlock, 4) void ps_render(DevScene sc, DevCame
     S.roots_done = 0u; S.cls_done = 0u;
     S.tree_free = a.trees >= 32u ? 0xFFFFFFFFu : (1u << a.trees) - 1u;
   }
+  for (unsigned k = threadIdx.x; k < kPsMaxTrees * kPsMaxDepth; k += blockDim.x) (&S.lvl[0][0])[k] = 0u;
   const LaneScene ls = lane_scene<LANE>(sc, a.lds_flags, a.n_top, stack_lds + threadIdx.x, lane_dyn);
   const unsigned lane = lane_id();
   const unsigned n_chunks = (a.n0 + 63u) / 64u;
   const unsigned L = (unsigned)sc.n_lights;
   PsRay* ring = a.rings + (size_t)blockIdx.x * a.q_cap;
   PsParent* par = a.parents + (size_t)blockIdx.x * a.trees * 64u * a.n_int;
+  uint16_t* lists = a.lists + (size_t)blockIdx.x * a.trees * 64u * a.n_int;
   WfCounters* cnt = (WfCounters*)a.cnt;
   PsTally tl;
   for (;;) {
@@ -359,6 +360,7 @@ __global__ __launch_bounds__(kTraceBlock, 4) void ps_render(DevScene sc, DevCame
         surface = vadd(surface, term);
       }
     }
+    const unsigned long long c3 = ps_clock<TALLY>();
     // ---- the children: appended to the ring (one reservation per wave),
     // published once every lane's records are in the L2
     const unsigned long long mr = __ballot(want_refl), mf = __ballot(want_refr);
@@ -369,12 +371,15 @@ __global__ __launch_bounds__(kTraceBlock, 4) void ps_render(DevScene sc, DevCame
       rb = (unsigned)__shfl((int)rb, 0, 64);
     }
     const unsigned nk = (want_refl ? 1u : 0u) + (want_refr ? 1u : 0u);
-    if (nk) {
+    if (nk) {  // a node with children: its record, its entry in the tree's level list, the child rays
       PsParent* P = par + ((size_t)t * 64u + px) * a.n_int + node;
       ps_st2(P->surface, surface.x, surface.y);
       ps_st2(&P->surface[2], surface.z, schlick_r);
       const ps_u4 tail = {(unsigned)c.obj, (want_refl ? 1u : 0u) | (want_refr ? 2u : 0u), nk, 0u};
       __builtin_nontemporal_store(tail, (ps_u4*)&P->obj);
+      const unsigned li = atomicAdd(&S.lvl[t][g], 1u);
+      __builtin_nontemporal_store((uint16_t)((px << 10) | node),
+                                  lists + ((size_t)t * (64u * a.n_int) + 64u * ((1u << g) - 1u) + li));
       const unsigned long long below = (1ull << lane) - 1ull;
       if (want_refl) {  // comps.reflectv (intersection.rs:101) from the over point
         PsRay* r = ring + (rb + (unsigned)__popcll(mr & below)) % a.q_cap;
@@ -393,43 +398,54 @@ __global__ __launch_bounds__(kTraceBlock, 4) void ps_render(DevScene sc, DevCame
       }
       // the tree gains its children before they become visible (never reaches 0 here)
       atomicAdd(&S.live[t], (int)nk - 1);
-    }
-    if (nr + nf) {
-      ps_drain();
-      if (lane == 0) {  // publish in reservation order
-        unsigned long long t0 = 0;
-        for (unsigned it = 0; ps_ld(&S.commit) != rb; ++it) {
-          if ((it & 63u) == 0u) {
-            const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-            if (it == 0) {
-              t0 = now;
-            } else if (now - t0 > kPsWaitTicks) {
-              ps_fault(a, S, 3, it, now - t0);
-              break;
-            }
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-        __hip_atomic_store(&S.commit, rb + nr + nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-    }
-    const unsigned long long c3 = ps_clock<TALLY>();
-    // ---- nodes without children: their colour is final
-    if (valid && nk == 0u) {
+    } else if (valid) {  // a node without children: its colour is final (color_at, world.rs:70-81)
       V3 col = v3(0.0, 0.0, 0.0);  // a miss is black (world.rs:74-75)
       if (hit) {
         const V3 zero = v3(0.0, 0.0, 0.0);  // reflected / refracted colour: black (world.rs:108-109, 117-118)
         col = shade_color(*m, surface, zero, zero, schlick_r);
       }
-      ps_deliver(sc, a, cam, par, S, t, px, node, col);
+      double* dst;
+      if (node == 0u) {
+        dst = ps_root_dst(a, cam, S.root0[t] + px);
+      } else {  // into its parent's record, for the tree's combine
+        PsParent* Q = par + ((size_t)t * 64u + px) * a.n_int + ((node - 1u) >> 1);
+        dst = ((node - 1u) & 1u) ? Q->refr : Q->refl;
+      }
+      ps_st2(dst, col.x, col.y);
+      __builtin_nontemporal_store(col.z, dst + 2);
     }
-    ps_drain();
-    if (valid && nk == 0u) {
-      const int left = atomicAdd(&S.live[t], -1) - 1;
-      if (left == 0) atomicOr(&S.tree_free, 1u << t);
+    ps_drain();  // every record, ring entry and colour of this chunk is in the L2
+    if (nr + nf && lane == 0) {  // publish in reservation order
+      unsigned long long t0 = 0;
+      for (unsigned it = 0; ps_ld(&S.commit) != rb; ++it) {
+        if ((it & 63u) == 0u) {
+          const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+          if (it == 0) {
+            t0 = now;
+          } else if (now - t0 > kPsWaitTicks) {
+            ps_fault(a, S, 3, it, now - t0);
+            break;
+          }
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __hip_atomic_store(&S.commit, rb + nr + nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+    const unsigned long long c4 = ps_clock<TALLY>();
+    // ---- a node without children finishes its ray; the lane that finishes a
+    // tree's last ray hands the tree to this wave's combine
+    bool done_tree = false;
+    if (valid && nk == 0u) done_tree = atomicAdd(&S.live[t], -1) == 1;
+    unsigned long long md = __ballot(done_tree);
+    while (md) {
+      const int src = __ffsll((long long)md) - 1;
+      const unsigned tt = (unsigned)__shfl((int)t, src, 64);
+      ps_combine_tree(sc, a, cam, par, lists, S, tt);
+      if (lane == 0) atomicOr(&S.tree_free, 1u << tt);
+      md &= md - 1ull;
+    }
+    const unsigned long long c5 = ps_clock<TALLY>();
     if constexpr (TALLY) {  // counted launch: executed work per class, shade_hit runs and children per depth
-      const unsigned long long c4 = ps_clock<TALLY>();
       const unsigned cls = kind == PS_ROOTS ? (unsigned)WF_PRIMARY : (unsigned)WF_CLOSEST;
       const unsigned long long s = wave_sum(tl.disc), st = wave_sum(tl.tests), sb = wave_sum(tl.boxes);
       const unsigned long long hs = wave_sum(tl.sh_disc), hst = wave_sum(tl.sh_tests), hsb = wave_sum(tl.sh_boxes);
@@ -450,6 +466,7 @@ __global__ __launch_bounds__(kTraceBlock, 4) void ps_render(DevScene sc, DevCame
         atomicAdd(&w->ps_cycles[1], c2 - c1);
         atomicAdd(&w->ps_cycles[2], c3 - c2);
         atomicAdd(&w->ps_cycles[3], c4 - c3);
+        atomicAdd(&w->ps_cycles[4], c5 - c4);
       }
       tl = PsTally{};
       if (a.count && valid) {

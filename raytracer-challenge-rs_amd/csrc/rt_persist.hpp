@@ -9,11 +9,12 @@
 //   - up to 64 queued child rays from the workgroup's own ring.
 // A wave traces its 64 rays (closest hit, prepare_computations, every light's
 // shadow ray and lighting()), appends the reflected / refracted children to
-// the ring, and writes a PsParent record for every node with children. A node
-// without children knows its colour at once; it hands it to its parent's
-// record, and the child that arrives LAST at a parent (an atomic countdown)
-// evaluates shade_hit's expression (world.rs:58-67) for the parent and carries
-// on upward, to the root, whose colour goes to the canvas.
+// the ring, and writes a PsParent record (and an entry in the tree's list of
+// that depth) for every node with children. A node without children knows its
+// colour at once and writes it into its parent's record. The wave whose ray
+// finishes a tree (an LDS count of the tree's unfinished rays) evaluates
+// shade_hit's expression (world.rs:58-67) for the tree's nodes with children,
+// deepest depth first, and writes the roots' colours to the canvas.
 //
 // Every hand-off stays inside one workgroup (one CU): ring slots and parent
 // records are written with non-temporal stores (kept in the XCD's L2), made
@@ -37,7 +38,7 @@ namespace rtamd {
 constexpr unsigned kPsMaxDepth = 8;      // heap node ids of depth <= 8 fit 10 bits
 constexpr unsigned kPsMaxTrees = 32;     // tree slots per workgroup (one LDS bitmask)
 constexpr unsigned kPsSpare = 1024;      // ring slots claimed but not yet read (16 waves x 64)
-constexpr size_t kPsSchedBytes = 512;    // LDS of the scheduler state (PsSched), beside the scene image
+constexpr size_t kPsSchedBytes = 1536;   // LDS of the scheduler state (PsSched), beside the scene image
 // device memory of a workspace's trees (parents + rings) at the largest grid:
 // sets the tree slots per workgroup for deep recursion (C5, depth 8: 14)
 constexpr size_t kPsBudget = (size_t)12 << 30;
@@ -59,7 +60,7 @@ struct alignas(128) PsParent {  // 128 B (one L2 line): a node with children
   double pad1;
   int32_t obj;
   uint32_t kids;     // bit 0: reflected child, bit 1: refracted child
-  uint32_t pending;  // children still to deliver (atomic countdown)
+  uint32_t n_kids;
   uint32_t pad2[5];
 };
 static_assert(sizeof(PsParent) == 128, "PsParent must stay 128 B");
@@ -79,6 +80,7 @@ struct PsCounters {
 struct PsArgs {
   PsRay* rings;        // grid x q_cap
   PsParent* parents;   // grid x trees x 64 x n_int
+  uint16_t* lists;     // grid x trees x 64 x n_int: per tree and depth, (root << 10 | node) of its nodes with children
   PsCounters* ctr;
   void* cnt;           // WfCounters (counted launches)
   double* out;         // camera, aa == 1: the shard canvas (row-major); else root colours by root index

@@ -914,6 +914,7 @@ Wavefront::~Wavefront() {
   if (ps_rings_) (void)hipFree(ps_rings_);
   if (ps_parents_) (void)hipFree(ps_parents_);
   if (ps_ctr_) (void)hipFree(ps_ctr_);
+  if (ps_lists_) (void)hipFree(ps_lists_);
   if (h_fault_) (void)hipHostFree(h_fault_);
   if (ev0_) (void)hipEventDestroy(ev0_);
   if (ev1_) (void)hipEventDestroy(ev1_);
@@ -971,7 +972,7 @@ hipError_t Wavefront::last_profile(WfProfile* out) {
   }
   if (last_fused_) out->rays[WF_SHADOW] = out->sh_rays[0] + out->sh_rays[1];  // traced inside the fused launches
   for (int c = 0; c < 2; ++c) { out->ps_items[c] = (double)hc.ps_items(c); out->ps_lanes[c] = (double)hc.ps_lanes(c); }
-  for (int c = 0; c < 4; ++c) out->ps_cycles[c] = (double)hc.ps_cycles(c);
+  for (int c = 0; c < 6; ++c) out->ps_cycles[c] = (double)hc.ps_cycles(c);
   if (last_persist_) {  // one launch: the root rays and, from a counted frame, the children per depth
     out->rays[WF_PRIMARY] = (double)lr_.n0;
     double kids = 0.0;
@@ -1461,6 +1462,7 @@ hipError_t Wavefront::render_persist(const DevScene& sc, const DevCamera& cam, b
   const size_t q_cap = (size_t)trees * 64 * leaves + kPsSpare;
   WF_CHECK(grow(ps_rings_, ps_rings_cap_, (size_t)grid * q_cap));
   WF_CHECK(grow(ps_parents_, ps_parents_cap_, std::max<size_t>(1, (size_t)grid * trees * 64 * n_int)));
+  WF_CHECK(grow(ps_lists_, ps_lists_cap_, std::max<size_t>(1, (size_t)grid * trees * 64 * n_int)));
   if (averaged) WF_CHECK(ensure_gen(0, n0, L, 0, true));
   // the scene image (as the generation pipeline's fused kernels)
   constexpr size_t limit = kWfLdsLimit - kPsSchedBytes;
@@ -1487,6 +1489,7 @@ hipError_t Wavefront::render_persist(const DevScene& sc, const DevCamera& cam, b
   }
   a.rings = ps_rings_;
   a.parents = ps_parents_;
+  a.lists = ps_lists_;
   a.ctr = ps_ctr_;
   a.cnt = d_cnt_;
   a.out = averaged ? gens_[0].colors : d_out;

@@ -120,7 +120,8 @@ struct alignas(128) WfWorkRow {
   // persistent kernel (counted launches): its work items and where its waves' time goes
   unsigned long long ps_items[2];   // chunks taken: [0] camera chunks, [1] queued-ray chunks
   unsigned long long ps_lanes[2];   // rays in them (lane use of the items = lanes / (64 x items))
-  unsigned long long ps_cycles[4];  // shader clocks: [0] getting work, [1] trace, [2] shading + spawn, [3] delivery
+  unsigned long long ps_cycles[6];  // shader clocks: [0] getting work, [1] trace, [2] shading, [3] spawn + publish,
+                                    // [4] tree combine
 };
 // Fused launches hand out their rays in chunks of 64 (one wave-iteration) from
 // per-XCD counters, kChunkClasses per generation, each on a 128-B line.
@@ -240,7 +241,7 @@ struct WfProfile {
   int bvh;          // the last frame traversed the BVH
   int fused;        // the last frame ran the fused pipeline
   int persist;      // the last frame ran the persistent frame kernel (one launch; its time is the closest class)
-  double ps_items[2], ps_lanes[2], ps_cycles[4];  // persistent kernel, counted frame (WfWorkRow)
+  double ps_items[2], ps_lanes[2], ps_cycles[6];  // persistent kernel, counted frame (WfWorkRow)
 };
 
 class Wavefront {
@@ -295,7 +296,8 @@ class Wavefront {
   PsRay* ps_rings_ = nullptr;
   PsParent* ps_parents_ = nullptr;
   PsCounters* ps_ctr_ = nullptr;
-  size_t ps_rings_cap_ = 0, ps_parents_cap_ = 0;  // records
+  uint16_t* ps_lists_ = nullptr;
+  size_t ps_rings_cap_ = 0, ps_parents_cap_ = 0, ps_lists_cap_ = 0;  // records
   hipError_t ensure_gen(size_t g, size_t slots, size_t n_lights, size_t list_slots, bool fused);
   hipError_t ensure_misc(size_t n_diag);
   // shard counters: generation g's rays (q = 0) / shadow list (q = 1)

@@ -61,7 +61,7 @@ for st in a.sets:
     cam.render_shard_device(w, depth, 8, r, n, bufs[0].data_ptr(), cur.cuda_stream, True, exhaustive=False)
     p = rtamd._rtamd._wf_profile(w, -1, True)
     ps = p["ps"]
-    cyc = sum(ps[k] for k in ("cycles_acquire", "cycles_trace", "cycles_shade", "cycles_deliver")) or 1.0
+    cyc = sum(v for k, v in ps.items() if k.startswith("cycles_")) or 1.0
     out = {"knobs": knobs, "ms_inflight": round(ms_f, 4), "ms_serial": round(ms_1, 4), "bitwise": ok,
            "persist": p["persist"],
            "lane_use_roots": round(ps["lanes_roots"] / max(1.0, 64 * ps["items_roots"]), 3),
