@@ -6,6 +6,10 @@
 // `prepare_computations` all run on the GPU through the ABI; this header only
 // builds and flattens the scene (host-side, like the reference's setup code).
 #pragma once
+#include <sys/mman.h>
+
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <memory>
@@ -125,14 +129,38 @@ inline Shape Cone(double minimum = -std::numeric_limits<double>::infinity(),
 }
 
 // canvas.rs:8-52 + image/ppm.rs
+// Pixel storage of a Canvas. Frames of 2 MiB and more sit on 2-MiB aligned
+// memory marked for transparent huge pages, so the first touch of a fresh
+// 50-MB canvas (the device-to-host copy of `render`) takes tens of page
+// faults instead of ~12 000.
+struct PixelFree {
+  void operator()(double* p) const noexcept { std::free(p); }
+};
+using PixelPtr = std::unique_ptr<double[], PixelFree>;
+inline PixelPtr alloc_pixels(size_t n) {
+  const size_t bytes = std::max<size_t>(n, 1) * sizeof(double);
+  constexpr size_t kHuge = (size_t)2 << 20;
+  void* p = nullptr;
+  if (bytes >= kHuge) {
+    if (posix_memalign(&p, kHuge, (bytes + kHuge - 1) / kHuge * kHuge) != 0) p = nullptr;
+    if (p) (void)madvise(p, (bytes + kHuge - 1) / kHuge * kHuge, MADV_HUGEPAGE);
+  } else {
+    p = std::malloc(bytes);
+  }
+  if (!p) throw std::bad_alloc();
+  return PixelPtr((double*)p);
+}
+
 class Canvas {
  public:
-  Canvas(size_t w, size_t h) : w_(w), h_(h), px_(new double[w * h * 3]()) {}  // black (raytracer/src/canvas.rs:16)
+  Canvas(size_t w, size_t h) : w_(w), h_(h), px_(alloc_pixels(w * h * 3)) {  // black (raytracer/src/canvas.rs:16)
+    std::memset(px_.get(), 0, w * h * 3 * sizeof(double));
+  }
   // Storage the caller overwrites entirely (a render writes every pixel): no
   // zero pass, so the pages are first touched by the copy from the device.
   struct Uninit {};
-  Canvas(size_t w, size_t h, Uninit) : w_(w), h_(h), px_(new double[w * h * 3]) {}
-  Canvas(const Canvas& o) : w_(o.w_), h_(o.h_), px_(new double[o.w_ * o.h_ * 3]) {
+  Canvas(size_t w, size_t h, Uninit) : w_(w), h_(h), px_(alloc_pixels(w * h * 3)) {}
+  Canvas(const Canvas& o) : w_(o.w_), h_(o.h_), px_(alloc_pixels(o.w_ * o.h_ * 3)) {
     std::memcpy(px_.get(), o.px_.get(), w_ * h_ * 3 * sizeof(double));
   }
   Canvas(Canvas&&) noexcept = default;
@@ -166,7 +194,7 @@ class Canvas {
     return (y * w_ + x) * 3;
   }
   size_t w_, h_;
-  std::unique_ptr<double[]> px_;
+  PixelPtr px_;
 };
 
 inline rt_shape_desc to_desc(const Shape& s) {

@@ -259,6 +259,21 @@ int ensure_dev_buffer(double** buf, size_t* cap, size_t need) {
 constexpr size_t kStageChunk = (size_t)8 << 20;
 int copy_to_host(rt_scene* s, void* dst, const void* src, size_t n, hipStream_t st) {
   if (n == 0) return RT_OK;
+  // Large copies: pin the caller's pages for this call and let the DMA engine
+  // write them directly (one pass over the bytes instead of DMA + host memcpy).
+  // The registration never outlives the call, so the caller may free or reuse
+  // the buffer at once; a buffer that cannot be registered takes the chunks.
+  if (n >= ((size_t)4 << 20) && s->tune.d2h == 1) {
+    if (hipHostRegister(dst, n, hipHostRegisterDefault) == hipSuccess) {
+      hipError_t e = hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, st);
+      if (e == hipSuccess) e = hipStreamSynchronize(st);
+      const hipError_t u = hipHostUnregister(dst);
+      if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("device-to-host copy: ") + hipGetErrorString(e));
+      if (u != hipSuccess) return fail(RT_ERR_HIP, std::string("hipHostUnregister: ") + hipGetErrorString(u));
+      return RT_OK;
+    }
+    (void)hipGetLastError();  // not registrable (e.g. already pinned memory): the staging chunks below
+  }
   for (int k = 0; k < 2; ++k) {
     if (!s->h_stage[k]) RT_HIP(hipHostMalloc(&s->h_stage[k], kStageChunk, hipHostMallocDefault));
     if (!s->stage_ev[k]) RT_HIP(hipEventCreateWithFlags(&s->stage_ev[k], hipEventDisableTiming));

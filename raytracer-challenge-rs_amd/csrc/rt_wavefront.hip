@@ -39,7 +39,7 @@ int wf_tuning_apply(WfTuning& t, const char* key, int value) {
       {"adaptive_block", &WfTuning::adaptive_block, 0, 1},
       {"corrupt_calibration", &WfTuning::corrupt_calibration, 0, 1},
       {"ps_trees", &WfTuning::ps_trees, 0, 32},     {"ps_policy", &WfTuning::ps_policy, 0, 1},
-      {"ps_grid", &WfTuning::ps_grid, 0, 4096}};
+      {"ps_grid", &WfTuning::ps_grid, 0, 4096},     {"d2h", &WfTuning::d2h, 0, 1}};
   if (!key) return 0;
   for (const Knob& k : knobs) {
     if (std::strcmp(key, k.name) != 0) continue;

@@ -102,6 +102,7 @@ struct WfTuning {
   int ps_trees = 0;        // persistent kernel: tree slots per workgroup (0 = from the memory budget, at most 32)
   int ps_policy = 0;       // persistent kernel: when a wave takes fewer than 64 queued rays (PsArgs::policy)
   int ps_grid = 0;         // persistent kernel: workgroups (0 = one per CU, fewer for small renders)
+  int d2h = 1;             // host-canvas copies: 1 = pin the caller's buffer for the call and DMA into it, 0 = pinned chunks
 };
 // Applies `key` = `value` to `t`: 1 = applied, 0 = not a render-time key, -1 = bad value.
 int wf_tuning_apply(WfTuning& t, const char* key, int value);
