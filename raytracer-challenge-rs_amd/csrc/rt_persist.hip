@@ -54,15 +54,16 @@ __device__ __forceinline__ ps_d2 ps_ld2(const void* p) { return __builtin_nontem
 
 // A wait exceeded its time bound: record what this wave saw (host-mapped,
 // read back in the library's error text), then the code (word 0).
-__device__ __noinline__ void ps_fault(const PsArgs& a, const PsSched& S, int code, unsigned it,
-                                      unsigned long long dt) {
-  volatile int* f = a.fault;
+// (Everything by value: a reference to the kernel's arguments would put them in scratch.)
+__device__ __noinline__ void ps_fault(int* fault, unsigned trees, unsigned q_cap, const PsSched& S, int code,
+                                      unsigned it, unsigned long long dt) {
+  volatile int* f = fault;
   f[1] = (int)blockIdx.x; f[2] = (int)(threadIdx.x >> 6);
   f[3] = (int)S.head; f[4] = (int)S.tail; f[5] = (int)S.commit; f[6] = (int)S.busy;
   f[7] = (int)S.roots_done; f[8] = (int)S.tree_free; f[9] = (int)S.cls_done;
   f[10] = (int)it; f[11] = (int)(dt & 0xFFFFFFFFull); f[12] = (int)(dt >> 32);
   for (int k = 0; k < 8; ++k) f[13 + k] = S.live[k];
-  f[21] = (int)gridDim.x; f[22] = (int)a.trees; f[23] = (int)a.q_cap;
+  f[21] = (int)gridDim.x; f[22] = (int)trees; f[23] = (int)q_cap;
   f[0] = code;
 }
 
@@ -145,7 +146,7 @@ __device__ void ps_acquire(PsSched& S, const PsArgs& a, unsigned n_chunks, unsig
       if (waits == 1u) {
         t0 = now;
       } else if (now - t0 > kPsWaitTicks) {
-        ps_fault(a, S, 2, it, now - t0);
+        ps_fault(a.fault, a.trees, a.q_cap, S, 2, it, now - t0);
         kind = PS_EXIT;
         return;
       }
@@ -270,12 +271,12 @@ __global__ __launch_bounds__(kTraceBlock, 4) void ps_render(DevScene sc, DevCame
     unsigned kind = 0, base = 0, take = 0, tree = 0;
     const unsigned long long c0 = ps_clock<TALLY>();
     if (lane == 0) ps_acquire(S, a, n_chunks, kind, base, take, tree);
-    kind = (unsigned)__shfl((int)kind, 0, 64);
+    kind = (unsigned)__builtin_amdgcn_readfirstlane((int)kind);  // lane 0's answer, wave-uniform
     if (kind == PS_EXIT) break;
     const unsigned long long c1 = ps_clock<TALLY>();
-    base = (unsigned)__shfl((int)base, 0, 64);
-    take = (unsigned)__shfl((int)take, 0, 64);
-    tree = (unsigned)__shfl((int)tree, 0, 64);
+    base = (unsigned)__builtin_amdgcn_readfirstlane((int)base);  // lane 0's answer, wave-uniform
+    take = (unsigned)__builtin_amdgcn_readfirstlane((int)take);  // lane 0's answer, wave-uniform
+    tree = (unsigned)__builtin_amdgcn_readfirstlane((int)tree);  // lane 0's answer, wave-uniform
     // ---- this lane's ray: a camera (or batch) root, or a queued child
     const bool valid = lane < take;
     unsigned t = tree, px = lane, node = 0;
@@ -311,51 +312,59 @@ __global__ __launch_bounds__(kTraceBlock, 4) void ps_render(DevScene sc, DevCame
     hit_finish(h);
     const unsigned long long c2 = ps_clock<TALLY>();
     // ---- color_at's shading (world.rs:70-81, 40-68): prepare_computations,
-    // the children, every light's shadow ray and lighting()
+    // the children, every light's shadow ray and lighting(). Only what the
+    // lights loop and the spawn need stays live across the shadow traces; the
+    // under point, reflect vector and refracted direction are formed after it
+    // from the same operands with the same operations (the same bits).
     const unsigned g = 31u - (unsigned)__clz((int)(node + 1u));  // depth of heap node `node`
     const unsigned remaining = a.max_depth - g;
     bool hit = false, want_refl = false, want_refr = false;
-    Comps c{};
-    V3 refr_dir = v3(0.0, 0.0, 0.0);
+    V3 point = v3(0.0, 0.0, 0.0), normal = v3(0.0, 0.0, 0.0), over = v3(0.0, 0.0, 0.0);
+    double n_ratio = 0.0, k_refr = 0.0, schlick_r = 0.0;
+    int obj = 0;
     const ShadeRec* m = nullptr;
     if (valid && h.key >= 0) {
-      c = prepare(sc, o, d, h);
+      const Comps c = prepare(sc, o, d, h);
       hit = true;
+      obj = c.obj;
+      point = c.point;
+      normal = c.normal;
+      over = c.over;
       m = &sc.shade[c.obj];
       // reflected_color (world.rs:107-114)
       want_refl = !(req(m->reflective, 0.0) || remaining == 0);
       // refracted_color (world.rs:116-134)
       if (!(req(m->transparency, 0.0) || remaining == 0)) {
-        const double n_ratio = c.n1 / c.n2;
+        n_ratio = c.n1 / c.n2;
         const double cos_i = vdot(c.eyev, c.normal);
         const double sin2_t = n_ratio * n_ratio * (1.0 - cos_i * cos_i);
         if (!(sin2_t > 1.0)) {
           const double cos_t = sqrt(1.0 - sin2_t);
-          refr_dir = vsub(vscale(c.normal, n_ratio * cos_i - cos_t), vscale(c.eyev, n_ratio));
+          k_refr = n_ratio * cos_i - cos_t;
           want_refr = true;
         }
       }
-    }
-    double schlick_r = 0.0;
-    V3 surface = v3(0.0, 0.0, 0.0);  // fold from (0,0,0) (color.rs:96-103)
-    if (hit) {
       // shade_hit's Schlick factor (world.rs:62-64), same inputs as the reference's call
       schlick_r = (m->reflective > 0.0 && m->transparency > 0.0) ? schlick(c.eyev, c.normal, c.n1, c.n2) : 0.0;
+    }
+    V3 surface = v3(0.0, 0.0, 0.0);  // fold from (0,0,0) (color.rs:96-103)
+    if (hit) {
+      const V3 eyev = vneg(d);  // comps.eyev (intersection.rs:56)
       for (unsigned l = 0; l < L; ++l) {
         cLightRec Lr = (cLightRec)sc.lights + l;
         // the shadow ray exactly as World::is_shadowed builds it (world.rs:95-105); its
         // direction is also lighting()'s light vector (same operands, same operations)
-        const V3 v = vsub(v3(Lr->pos[0], Lr->pos[1], Lr->pos[2]), c.over);
+        const V3 v = vsub(v3(Lr->pos[0], Lr->pos[1], Lr->pos[2]), over);
         const double dist = sqrt(v.x * v.x + v.y * v.y + v.z * v.z);  // magnitude (vector.rs:21-23)
         const V3 sdir = v3(v.x / dist, v.y / dist, v.z / dist);       // normalize (vector.rs:25-28)
         V3 term;
-        if (a.skip_shadow && shadow_irrelevant(*m, Lr, sdir, c.normal, term)) {
+        if (a.skip_shadow && shadow_irrelevant(*m, Lr, sdir, normal, term)) {
           // the light is behind the surface: lighting() is the ambient term either way
         } else {
-          const bool shadowed = shadow_trace<LANE, QUADS>(sc, a.use_lb, ls, l, c.over, sdir, dist, tl.sh_disc,
+          const bool shadowed = shadow_trace<LANE, QUADS>(sc, a.use_lb, ls, l, over, sdir, dist, tl.sh_disc,
                                                           tl.sh_tests, tl.sh_boxes);
           ++tl.sh_rays;
-          term = lighting(*m, Lr, c.over, c.eyev, c.normal, shadowed, sdir);
+          term = lighting(*m, Lr, over, eyev, normal, shadowed, sdir);
         }
         surface = vadd(surface, term);
       }
@@ -368,14 +377,14 @@ __global__ __launch_bounds__(kTraceBlock, 4) void ps_render(DevScene sc, DevCame
     unsigned rb = 0;
     if (nr + nf) {
       if (lane == 0) rb = atomicAdd(&S.tail, nr + nf);
-      rb = (unsigned)__shfl((int)rb, 0, 64);
+      rb = (unsigned)__builtin_amdgcn_readfirstlane((int)rb);
     }
     const unsigned nk = (want_refl ? 1u : 0u) + (want_refr ? 1u : 0u);
     if (nk) {  // a node with children: its record, its entry in the tree's level list, the child rays
       PsParent* P = par + ((size_t)t * 64u + px) * a.n_int + node;
       ps_st2(P->surface, surface.x, surface.y);
       ps_st2(&P->surface[2], surface.z, schlick_r);
-      const ps_u4 tail = {(unsigned)c.obj, (want_refl ? 1u : 0u) | (want_refr ? 2u : 0u), nk, 0u};
+      const ps_u4 tail = {(unsigned)obj, (want_refl ? 1u : 0u) | (want_refr ? 2u : 0u), nk, 0u};
       __builtin_nontemporal_store(tail, (ps_u4*)&P->obj);
       const unsigned li = atomicAdd(&S.lvl[t][g], 1u);
       __builtin_nontemporal_store((uint16_t)((px << 10) | node),
@@ -383,16 +392,18 @@ __global__ __launch_bounds__(kTraceBlock, 4) void ps_render(DevScene sc, DevCame
       const unsigned long long below = (1ull << lane) - 1ull;
       if (want_refl) {  // comps.reflectv (intersection.rs:101) from the over point
         PsRay* r = ring + (rb + (unsigned)__popcll(mr & below)) % a.q_cap;
-        const V3 rv = vreflect(d, c.normal);
-        ps_st2(&r->o[0], c.over.x, c.over.y);
-        ps_st2(&r->o[2], c.over.z, rv.x);
+        const V3 rv = vreflect(d, normal);
+        ps_st2(&r->o[0], over.x, over.y);
+        ps_st2(&r->o[2], over.z, rv.x);
         ps_st2(&r->d[1], rv.y, rv.z);
         __builtin_nontemporal_store((t << 16) | (px << 10) | (2u * node + 1u), &r->id);
       }
-      if (want_refr) {  // refracted_color's ray from the under point (world.rs:129-131)
+      if (want_refr) {  // refracted_color's ray from the under point (world.rs:122-131, intersection.rs:103)
         PsRay* r = ring + (rb + nr + (unsigned)__popcll(mf & below)) % a.q_cap;
-        ps_st2(&r->o[0], c.under.x, c.under.y);
-        ps_st2(&r->o[2], c.under.z, refr_dir.x);
+        const V3 under = vsub(point, vscale(normal, kEpsilon));
+        const V3 refr_dir = vsub(vscale(normal, k_refr), vscale(vneg(d), n_ratio));
+        ps_st2(&r->o[0], under.x, under.y);
+        ps_st2(&r->o[2], under.z, refr_dir.x);
         ps_st2(&r->d[1], refr_dir.y, refr_dir.z);
         __builtin_nontemporal_store((t << 16) | (px << 10) | (2u * node + 2u), &r->id);
       }
@@ -423,7 +434,7 @@ __global__ __launch_bounds__(kTraceBlock, 4) void ps_render(DevScene sc, DevCame
           if (it == 0) {
             t0 = now;
           } else if (now - t0 > kPsWaitTicks) {
-            ps_fault(a, S, 3, it, now - t0);
+            ps_fault(a.fault, a.trees, a.q_cap, S, 3, it, now - t0);
             break;
           }
         }
