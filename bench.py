@@ -8,10 +8,12 @@ of primary + reflection + refraction + shadow rays (each one a
 launched by torch.distributed.run) the frame is split into interleaved 8-row
 blocks, each rank renders its rows into HBM, and the canvas is assembled on
 rank 0 with one RCCL gather (strong scaling: the frame is fixed). F frames
-are in flight (--inflight, default 4 for C3, 1 for C5): consecutive frames render on F streams,
-each with its own library workspace, so one frame's short, latency-bound
-deep generations overlap the next frame's work; every frame is complete,
-gathered and assembled inside the timed region.
+are rendered in batches of NB (--batch, default 8 for C3, 1 for C5: one
+rt_render_frames_device call renders NB frames, every launch of the pipeline
+carrying all of them) on F streams (--inflight, default 4 for C3, 1 for C5),
+each with its own library workspace, so one batch's short, latency-bound deep
+generations overlap the next batch's work; every frame is complete, gathered
+(one gather per batch) and assembled inside the timed region.
 
 The scene is uploaded before timing (inputs resident in HBM). The timed
 region holds exactly K steps bracketed by barrier + synchronize; the
@@ -128,6 +130,8 @@ def parse():
     p.add_argument("--spheres", type=int, default=None)
     p.add_argument("--depth", type=int, default=None)
     p.add_argument("--row-block", type=int, default=8)
+    p.add_argument("--batch", type=int, default=None,
+                   help="frames per render call (rt_render_frames_device, <= 8; default 8 for C3, 1 for C5)")
     p.add_argument("--inflight", type=int, default=None,
                    help="frames in flight: consecutive frames render on this many streams (own workspaces)")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget for the CPU baseline sample")
@@ -308,6 +312,7 @@ def main():
     # default: 4 frames in flight for C3; one for C5, whose wavefront workspace
     # (16.8 M primary rays, depth 8) takes tens of GB per frame
     F = max(1, a.inflight if a.inflight is not None else (4 if a.config == "c3" else 1))
+    NB = max(1, min(8, a.batch if a.batch is not None else (8 if a.config == "c3" else 1)))
     stream = torch.cuda.current_stream()
     kind = a.stream_kind
     if F == 1:
@@ -320,10 +325,12 @@ def main():
         world.tune("shadow_stream", 0)
     per_stream = n > 1 and a.assembler in ("stream", "rccl")
     events = not per_stream and (n > 1 or a.event_path)
+    if events:
+        NB = 1  # the event-coupled dev path assembles frame by frame
     fa = None
     if n > 1 and a.assembler == "rccl" and F > 1:
         try:
-            fa = RcclStreamAssembler(H, W, B, rank, n, dev, streams=rstreams)
+            fa = RcclStreamAssembler(H, W, B, rank, n, dev, streams=rstreams, batch=NB)
         except Exception as e:  # fall back to the torch process groups
             print(f"warning: RCCL stream assembler unavailable ({e}); using per-stream process groups",
                   file=sys.stderr, flush=True)
@@ -333,13 +340,14 @@ def main():
     elif per_stream:
         groups = [dist.new_group(list(range(n))) for _ in range(F)]
         fa = StreamFrameAssembler(H, W, B, rank, n, dev, streams=rstreams if F > 1 else None, groups=groups,
-                                  slots=F)
+                                  slots=F, batch=NB)
     else:
-        fa = FrameAssembler(H, W, B, rank, n, dev, slots=F if not events else (F + 1 if F > 1 else 2))
+        fa = FrameAssembler(H, W, B, rank, n, dev, slots=F * NB if not events else (F + 1 if F > 1 else 2))
     assert len(fa.rows) == rtamd.shard_rows(H, B, srank, n)
     shard = fa.shard
     free_ev = [None] * len(fa.shards)
     frame_no = [0]
+    last_frame = [0]
 
     if a.emulate_gather:
         gstreams = [torch.cuda.Stream(device=dev) for _ in range(F)]
@@ -347,11 +355,19 @@ def main():
         canv = [torch.empty_like(fa.slot(k)) for k in range(F)]
         perm = torch.randperm(fa.slot(0).shape[0], device=dev)
 
-    def step():
+    def step(nf=None, assemble=True):
+        """Render the next batch (nf <= NB frames, default NB) and queue its
+        assembly; frame numbers advance by whole batches, so batch b always
+        uses stream b % F and its own slots."""
         s = frame_no[0]
-        rs = rstreams[s % F]
         if not events:
-            cam.render_shard_device(world, depth, B, srank, sn, fa.slot(s).data_ptr(), rs.cuda_stream, False)
+            nf = NB if nf is None else nf
+            rs = rstreams[(s // NB) % F]
+            if NB == 1:
+                cam.render_shard_device(world, depth, B, srank, sn, fa.slot(s).data_ptr(), rs.cuda_stream, False)
+            else:
+                rtamd.render_frames_device(world, [cam] * nf, depth, B, srank, sn,
+                                           [fa.slot(s + j).data_ptr() for j in range(nf)], rs.cuda_stream)
             if a.emulate_gather:
                 k = s % F
                 gs = gstreams[k]
@@ -361,9 +377,14 @@ def main():
                 rs.wait_stream(gs)
                 with torch.cuda.stream(rs):
                     torch.index_select(gbufs[k], 0, perm, out=canv[k])
-            fa.submit(s)  # 1 GPU: the slot is the canvas; N GPUs: gather + un-interleave on this frame's stream
-            frame_no[0] = s + 1
+            if assemble:
+                # 1 GPU: the slots are the canvases; N GPUs: one gather + un-interleave per batch, on its stream
+                for j in range(nf):
+                    submit(fa, s + j, j == nf - 1)
+            frame_no[0] = s + NB
+            last_frame[0] = s + nf - 1
             return
+        rs = rstreams[s % F]
         slot = s % len(fa.shards)
         if rs is not stream and free_ev[slot] is not None:
             rs.wait_event(free_ev[slot])
@@ -376,6 +397,14 @@ def main():
             ev.record(stream)
             free_ev[(s - 1) % len(fa.shards)] = ev
         frame_no[0] = s + 1
+        last_frame[0] = s
+
+    def run_frames(k, assemble=True):
+        """k frames: whole batches, then one partial batch."""
+        for _ in range(k // NB):
+            step(assemble=assemble)
+        if k % NB:
+            step(k % NB, assemble=assemble)
 
     # exact work counters of one frame (deterministic), from a counted warm-up launch
     # (this first launch also sizes the wavefront queues of this camera/shard)
@@ -397,12 +426,15 @@ def main():
     # setup: one frame on each render stream sizes and calibrates that stream's
     # workspace (its first frame reads the queue counts back synchronously), so the
     # timed region never meets a first frame whatever --warmup is
+    # (with batches: a whole batch, and the timed region's partial batch size, on every stream)
     for _ in range(F):
         step()
+    if a.steps % NB:
+        for _ in range(F):
+            step(a.steps % NB)
     fa.flush()
     torch.cuda.synchronize()
-    for _ in range(a.warmup):
-        step()
+    run_frames(a.warmup)
     fa.flush()
     torch.cuda.synchronize()
 
@@ -412,8 +444,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
+    run_frames(a.steps)
     last = fa.flush()  # the last frame's gather + un-interleave are inside the timed region
     torch.cuda.synchronize()
     if n > 1:
@@ -423,7 +454,12 @@ def main():
     # Parity of the timed frames (outside the timed region): the last frame each
     # rank rendered, and rank 0's assembled canvas, must equal the exhaustive frame
     # bit for bit (camera.rs:133-148 renders every pixel with the every-shape loop).
-    parity = None if a.no_verify_frames else verify_frames(fa, last, ref_shard, frame_no[0] - 1, n, rank, H)
+    parity = None if a.no_verify_frames else verify_frames(fa, last, ref_shard, last_frame[0], n, rank, H)
+    # Where an N-rank frame's time goes (outside the timed region, same streams and
+    # batches): the renders alone, and the assembly (gathers + un-interleave) alone
+    split = None
+    if n > 1:
+        split = phase_split(a, n, rank, dev, run_frames, fa, F, NB)
     # Serialized pass (outside the timed region): the same K frames one after the
     # other on one stream, every launch carrying its own start/stop HIP events
     # (hipExtLaunchKernel), for the roofline's per-launch kernel time and the
@@ -485,8 +521,11 @@ def main():
                 "width": W, "height": H, "spheres": a.spheres, "depth": depth,
                 "rays_per_frame": int(rays_per_frame),
                 "parallelism": (f"{n} GPUs, one process each: interleaved {B}-row blocks, RCCL gather to rank 0"
-                                if n > 1 else "1 GPU: wavefront pipeline") + f"; {F} frames in flight",
-                "frames_in_flight": F,
+                                if n > 1 else "1 GPU: wavefront pipeline") +
+                               f"; batches of {NB} frames on {F} streams",
+                "frames_in_flight": F * NB,
+                "batch": NB,
+                "render_streams_n": F,
                 "render_streams": kind if F > 1 else "current",
                 "assembler": type(fa).__name__ if n > 1 else None,
             },
@@ -498,6 +537,8 @@ def main():
                          "kernels traced",
             "parity": parity,
         }
+        if split is not None:
+            out["per_rank"] = split
         if n == 1 and not a.no_end_to_end:
             out["end_to_end"] = end_to_end(world, cam, depth)
         if n == 1 and not a.no_cpu_baseline:
@@ -510,6 +551,44 @@ def main():
         if hasattr(fa, "close"):
             fa.close()  # the per-stream RCCL communicators
         dist.destroy_process_group()
+
+
+def submit(fa, step, end):
+    """Frame `step` is rendered (`end`: the last of its batch)."""
+    if isinstance(fa, StreamFrameAssembler):
+        fa.submit(step, end=end)
+    else:
+        fa.submit(step)
+
+
+def phase_split(a, n, rank, dev, run_frames, fa, F, NB):
+    """Per-rank frame time of the renders alone and of the assembly alone
+    (gathers + rank 0's un-interleave of the same batches), each over K frames
+    with a barrier on both sides; collective. Gathered to rank 0."""
+    def timed(fn):
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / a.steps * 1e3
+    render_ms = timed(lambda: run_frames(a.steps, assemble=False))
+
+    def gathers():
+        for s in range(0, a.steps, NB):
+            nf = min(NB, a.steps - s)
+            for j in range(nf):
+                submit(fa, s + j, j == nf - 1)
+        fa.flush()
+    gather_ms = timed(gathers)
+    t = torch.tensor([render_ms, gather_ms], dtype=torch.float64, device=dev)
+    allt = [torch.empty_like(t) for _ in range(n)] if rank == 0 else None
+    dist.gather(t, allt, dst=0)
+    if rank != 0:
+        return None
+    return {"render_ms": [round(float(x[0]), 4) for x in allt], "assemble_ms": [round(float(x[1]), 4) for x in allt],
+            "note": "per rank, per frame, outside the timed region: the renders alone and the assembly alone "
+                    "(one gather per batch + rank 0's un-interleave), same streams and batches"}
 
 
 def verify_frames(fa, last, ref_shard, last_step, n, rank, H):

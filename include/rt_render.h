@@ -221,6 +221,23 @@ int rt_render_shard_device_ex(const rt_scene* scene, const rt_camera_desc* camer
                               uint32_t flags, double* d_out_rgb, void* stream,
                               rt_stats* stats);
 
+/* `Camera::render` (camera.rs:133-148) of `n_frames` cameras sharing hsize and
+ * vsize (the frames of an animation, or the steady state of a frame loop)
+ * over the same world: frame f's shard (as rt_render_shard_device) goes to the
+ * DEVICE buffer d_out_rgb[f]. Each frame equals its rt_render_shard_device
+ * render bit for bit; the frames are rendered together, up to 8 per pass of
+ * the pipeline (one launch per recursion generation carries all of them), so
+ * small frames and shards pay the per-pass cost once. Asynchronous on
+ * `stream` unless `stats` is non-NULL: then the frames are rendered one by
+ * one and the counters summed over them. Deferred errors as
+ * rt_render_shard_device. */
+int rt_render_frames_device(const rt_scene* scene, const rt_camera_desc* cameras,
+                            uint32_t n_frames, uint32_t max_depth,
+                            uint32_t aa_samples, uint32_t row_block,
+                            uint32_t shard, uint32_t n_shards,
+                            double* const* d_out_rgb, void* stream,
+                            rt_stats* stats);
+
 /* Number of rows shard `shard` of `n_shards` owns (for sizing buffers). */
 uint32_t rt_shard_rows(uint32_t vsize, uint32_t row_block, uint32_t shard,
                        uint32_t n_shards);

@@ -365,7 +365,7 @@ int check_faults(rt_scene* s) {
 int run_render(rt_scene* s, const DevCamera& cam, const double* d_rays, uint32_t n_tasks, uint32_t aa,
                uint32_t max_depth, uint32_t row_block, uint32_t shard, uint32_t n_shards, double* d_out,
                hipStream_t stream, DevStats* stats_out = nullptr, float* ms_out = nullptr, uint32_t flags = 0,
-               rt_scene::WfSlot** used = nullptr) {
+               rt_scene::WfSlot** used = nullptr, const FrameTable* batch = nullptr, unsigned n_frames = 1) {
   if (max_depth > (uint32_t)kMaxDepth)
     return fail(RT_ERR_INVALID_ARGUMENT, "max_depth > " + std::to_string(kMaxDepth));
   if (!valid_aa(aa)) return fail(RT_ERR_INVALID_ARGUMENT, "aa_samples must be 1, 2, 4, 8 or 16");
@@ -381,15 +381,16 @@ int run_render(rt_scene* s, const DevCamera& cam, const double* d_rays, uint32_t
   std::string sig;
   if (!d_rays) {  // camera renders are deterministic per (camera, shard, depth, aa)
     sig.assign((const char*)&cam, sizeof cam);
-    const uint32_t p[6] = {n_tasks, aa, max_depth, row_block, shard, n_shards};
+    const uint32_t p[7] = {n_tasks, aa, max_depth, row_block, shard, n_shards, n_frames};
     sig.append((const char*)p, sizeof p);
+    for (unsigned f = 1; f < n_frames; ++f) sig.append((const char*)&batch->cam[f], sizeof(DevCamera));
   }
   rt_scene::WfSlot* w = nullptr;
   hipError_t e = s->acquire(stream, &w);
   const unsigned wf_flags = ((flags & RT_RENDER_EXHAUSTIVE) ? WF_EXHAUSTIVE : 0u) | (used ? WF_COUNT : 0u);
   if (e == hipSuccess)
     e = w->wf->render(s->dev, cam, d_rays == nullptr, d_rays, n_tasks, aa, max_depth, row_block, shard, n_shards,
-                      d_out, stream, sig, stats_out, ms_out, s->tune, s->wfs.size() == 1, wf_flags);
+                      d_out, stream, sig, stats_out, ms_out, s->tune, s->wfs.size() == 1, wf_flags, batch, n_frames);
   if (e == hipSuccess) e = hipEventRecord(w->done, stream);
   if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("wavefront render: ") + hipGetErrorString(e));
   if (used) *used = w;
@@ -945,6 +946,71 @@ int rt_render_shard_device_ex(const rt_scene* scene, const rt_camera_desc* camer
   if (rc != RT_OK) return rc;
   if (stats)
     fill_stats(stats, ds, ms, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+  return RT_OK;
+  });
+}
+
+int rt_render_frames_device(const rt_scene* scene, const rt_camera_desc* cameras, uint32_t n_frames,
+                            uint32_t max_depth, uint32_t aa_samples, uint32_t row_block, uint32_t shard,
+                            uint32_t n_shards, double* const* d_out_rgb, void* stream, rt_stats* stats) {
+  return guarded([&]() -> int {
+  if (!scene || (n_frames && (!cameras || !d_out_rgb))) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
+  if (row_block == 0 || n_shards == 0 || shard >= n_shards)
+    return fail(RT_ERR_INVALID_ARGUMENT, "bad shard specification");
+  if (!valid_aa(aa_samples)) return fail(RT_ERR_INVALID_ARGUMENT, "aa_samples must be 1, 2, 4, 8 or 16");
+  for (uint32_t f = 0; f < n_frames; ++f) {
+    if (!d_out_rgb[f]) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
+    if (cameras[f].hsize == 0 || cameras[f].vsize == 0) return fail(RT_ERR_INVALID_ARGUMENT, "empty camera");
+    if (cameras[f].hsize != cameras[0].hsize || cameras[f].vsize != cameras[0].vsize)
+      return fail(RT_ERR_INVALID_ARGUMENT, "the frames of a batch must share hsize and vsize");
+  }
+  if (n_frames == 0) {
+    if (stats) std::memset(stats, 0, sizeof *stats);
+    return RT_OK;
+  }
+  rt_scene* s = const_cast<rt_scene*>(scene);
+  std::lock_guard<std::mutex> lk(s->mu);
+  auto t0 = std::chrono::steady_clock::now();
+  RT_HIP(hipSetDevice(s->device));
+  const uint32_t rows = rt_shard_rows(cameras[0].vsize, row_block, shard, n_shards);
+  const uint64_t per = (uint64_t)rows * cameras[0].hsize * aa_samples;
+  const uint64_t padded = (per + 63) & ~(uint64_t)63;
+  if (padded * std::min<uint32_t>(n_frames, kMaxFrames) >= (1ull << 31))
+    return fail(RT_ERR_INVALID_ARGUMENT, "batch too large");
+  hipStream_t st = (hipStream_t)stream;
+  // one pass of the generation pipeline per group of kMaxFrames frames; a
+  // render that cannot batch (counted, or a scene without the fast path's
+  // hierarchies) goes frame by frame, with the counters summed
+  const bool batch = !stats && s->tune.accel != 0 && (s->dev.n_bvh > 0 || s->dev.n_obvh > 0) && per > 0;
+  DevStats sum{};
+  float ms_sum = 0.f;
+  for (uint32_t f0 = 0; f0 < n_frames;) {
+    const uint32_t nf = batch ? std::min<uint32_t>(kMaxFrames, n_frames - f0) : 1u;
+    FrameTable tab{};
+    for (uint32_t f = 0; f < nf; ++f) {
+      tab.cam[f] = to_dev_camera(cameras[f0 + f]);
+      tab.out[f] = d_out_rgb[f0 + f];
+    }
+    DevStats ds{};
+    float ms = 0.f;
+    int rc = run_render(s, tab.cam[0], nullptr, (uint32_t)per, aa_samples, max_depth, row_block, shard, n_shards,
+                        tab.out[0], st, stats ? &ds : nullptr, stats ? &ms : nullptr, 0, nullptr,
+                        nf > 1 ? &tab : nullptr, nf);
+    if (rc != RT_OK) return rc;
+    if (stats) {
+      sum.rays_primary += ds.rays_primary; sum.rays_reflect += ds.rays_reflect;
+      sum.rays_refract += ds.rays_refract; sum.rays_shadow += ds.rays_shadow;
+      sum.rays_shadow_traced += ds.rays_shadow_traced; sum.sphere_tests += ds.sphere_tests;
+      sum.plane_tests += ds.plane_tests; sum.other_tests += ds.other_tests;
+      sum.sphere_tests_executed += ds.sphere_tests_executed; sum.box_tests_executed += ds.box_tests_executed;
+      sum.exhaustive = ds.exhaustive;
+      sum.sphere_disc_ge0 = ds.exhaustive ? sum.sphere_disc_ge0 + ds.sphere_disc_ge0 : ds.sphere_disc_ge0;
+      ms_sum += ms;
+    }
+    f0 += nf;
+  }
+  if (stats)
+    fill_stats(stats, sum, ms_sum, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
   return RT_OK;
   });
 }

@@ -144,20 +144,35 @@ __device__ __forceinline__ unsigned shard_slot(const unsigned* pre, unsigned cap
   return lo * cap + (j - pre[lo]);
 }
 
+// The frame of generation-0 slot i of a batch (FrameTable) and the slot
+// within that frame.
+__device__ __forceinline__ unsigned frame_of(const WfArgs& a, unsigned i, unsigned& li) {
+  if (a.n_frames <= 1) {
+    li = i;
+    return 0u;
+  }
+  const unsigned f = i / a.frame_rays;
+  li = i - f * a.frame_rays;
+  return f;
+}
+
 // Root rays of generation 0: sample `smp` of a pixel of the shard
-// (camera.rs:57-69 / 71-90), or an explicit ray; deeper generations read
-// their queue.
+// (camera.rs:57-69 / 71-90) of the slot's frame, or an explicit ray; deeper
+// generations read their queue.
 __device__ __forceinline__ void wf_ray(const WfArgs& a, const DevCamera& cam, unsigned i, V3& o, V3& d) {
   if (a.g == 0 && a.camera_mode) {
+    unsigned li;
+    const unsigned f = frame_of(a, i, li);
+    const DevCamera& cf = a.n_frames > 1 ? a.frames->cam[f] : cam;
     uint32_t x, lr, smp;
-    gen0_pixel(a.aa, a.rows, cam.hsize, i, x, lr, smp);
+    gen0_pixel(a.aa, a.rows, cf.hsize, li, x, lr, smp);
     const uint32_t blk = lr / a.row_block, off = lr - blk * a.row_block;
     const uint32_t y = (blk * a.n_shards + a.shard) * a.row_block + off;
     if (a.aa == 1) {
-      ray_for_pixel(cam, x, y, o, d);
+      ray_for_pixel(cf, x, y, o, d);
     } else {
       const double* ofs = kAaOffsets[a.aa - 1 + smp];
-      ray_for_pixel(cam, x, y, o, d, ofs[0], ofs[1]);
+      ray_for_pixel(cf, x, y, o, d, ofs[0], ofs[1]);
     }
   } else {
     const WfRay& r = a.rays[i];
@@ -209,16 +224,28 @@ __device__ __forceinline__ void shadow_result(const DevScene& sc, const WfArgs& 
 // this workspace (n_a and n_b 16-B words) and, for a camera frame, write the
 // primary records (wf_prim_prep's computation). One launch instead of two
 // fills and a kernel.
+// A batch of frames (n_frames > 1) also writes the batch's FrameTable, passed
+// by value (so the host may reuse its copy at once), to the workspace's
+// device copy that the pass's later launches read, and one set of primary
+// records per frame (frame f's at prim + f * (n_diag + 4)).
 __global__ void wf_frame_init(DevScene sc, DevCamera cam, PrimRec* prim, unsigned do_prim, uint4* zero_a,
-                              unsigned n_a, uint4* zero_b, unsigned n_b) {
+                              unsigned n_a, uint4* zero_b, unsigned n_b, FrameTable tab, FrameTable* tab_dev,
+                              unsigned n_frames) {
   const unsigned stride = gridDim.x * blockDim.x;
   const unsigned i0 = blockIdx.x * blockDim.x + threadIdx.x;
   const uint4 z = make_uint4(0u, 0u, 0u, 0u);
   for (unsigned i = i0; i < n_a; i += stride) zero_a[i] = z;
   for (unsigned i = i0; i < n_b; i += stride) zero_b[i] = z;
+  if (n_frames > 1) {
+    const unsigned* src = (const unsigned*)&tab;
+    unsigned* dst = (unsigned*)tab_dev;
+    for (unsigned i = i0; i < (unsigned)(sizeof(FrameTable) / 4); i += stride) dst[i] = src[i];
+  }
   if (!do_prim) return;
-  const V3 o = m34_point(cam.inv, v3(0.0, 0.0, 0.0));  // camera.rs:65
-  for (unsigned j = i0; j < (unsigned)sc.n_diag + 4; j += stride) {
+  const unsigned per = (unsigned)sc.n_diag + 4;
+  for (unsigned jj = i0; jj < per * n_frames; jj += stride) {
+    const unsigned f = jj / per, j = jj - f * per;
+    const V3 o = m34_point(n_frames > 1 ? tab.cam[f].inv : cam.inv, v3(0.0, 0.0, 0.0));  // camera.rs:65
     PrimRec p{};
     if (j < (unsigned)sc.n_diag) {
       const SphereDiag& r = sc.sph_diag[j];
@@ -228,7 +255,7 @@ __global__ void wf_frame_init(DevScene sc, DevCamera cam, PrimRec* prim, unsigne
       p.op[2] = r.s[2] * o.z + r.t[2];
       p.c = p.op[0] * p.op[0] + p.op[1] * p.op[1] + p.op[2] * p.op[2] - 1.0;
     }
-    prim[j] = p;  // j >= n_diag: zero padding records
+    prim[jj] = p;  // j >= n_diag: zero padding records
   }
 }
 
@@ -512,9 +539,12 @@ __device__ __forceinline__ void prep_one(const DevScene& sc, const WfArgs& a, un
 __device__ __forceinline__ double* color_dst(const WfArgs& a, const DevCamera& cam, unsigned slot) {
   size_t oi = slot;
   if (a.g == 0 && a.camera_mode && a.aa == 1) {
+    unsigned li;
+    const unsigned f = frame_of(a, slot, li);
     uint32_t x, lr, smp;
-    gen0_pixel(a.aa, a.rows, cam.hsize, slot, x, lr, smp);
+    gen0_pixel(1u, a.rows, cam.hsize, li, x, lr, smp);
     oi = (size_t)lr * cam.hsize + x;
+    if (a.n_frames > 1) return a.frames->out[f] + oi * 3;
   }
   return a.colors + oi * 3;
 }
@@ -677,7 +707,8 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
     unsigned k_next = 0;
     if (dyn && lane_id() == 0) k_next = atomicAdd(ctr, 1u);
     const unsigned i = c * 64u + lane_id();
-    const bool valid = i < a.n;
+    // a batch's generation 0: the padding slots after each frame's root rays hold no ray
+    const bool valid = i < a.n && (a.g != 0 || a.n_frames <= 1 || i % a.frame_rays < a.frame_real);
     const unsigned slot = valid ? shard_slot(pre, a.in_cap, i) : 0u;
     V3 o = v3(0, 0, 0), d = v3(0, 0, 0);
     Hit h;
@@ -685,7 +716,10 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
     if (valid) {
       wf_ray(a, cam, slot, o, d);
       if constexpr (LANE == 0) {
-        bvh_trace<PRIMARY, false>(sc, (cPrimRec)a.prim, stk, o, d, 0.0, h, t.disc, t.tests, t.boxes);
+        // the chunk's frame (chunks never mix frames): its shared-origin primary records
+        const unsigned pf = a.n_frames > 1 ? (c * 64u) / a.frame_rays : 0u;
+        bvh_trace<PRIMARY, false>(sc, (cPrimRec)(a.prim + (size_t)pf * ((unsigned)sc.n_diag + 4)), stk, o, d, 0.0, h,
+                                  t.disc, t.tests, t.boxes);
         trace_rest<false, QUADS, true>(sc, o, d, h, t.disc);
         if constexpr (QUADS) other_trace<false>(sc, o, d, 0.0, h, t.disc, t.tests, t.boxes);
       } else {
@@ -851,21 +885,25 @@ __global__ __launch_bounds__(kWfBlock) void wf_combine_parents(DevScene sc, DevC
 }
 
 // Color::average (color.rs:26-33) of the AA samples of each pixel: a left
-// fold from black, then * (1 / n); written row-major.
+// fold from black, then * (1 / n); written row-major (a batch: into each
+// frame's canvas, its samples at that frame's generation-0 slots).
 __global__ __launch_bounds__(kWfBlock) void wf_average(WfArgs a, unsigned hsize, const double* colors, unsigned n_pix,
                                                        double* out) {
   const unsigned stride = gridDim.x * blockDim.x;
   const unsigned aa = a.aa;
+  const unsigned pix_frame = a.n_frames > 1 ? a.frame_real / aa : n_pix;
   for (unsigned p = blockIdx.x * blockDim.x + threadIdx.x; p < n_pix; p += stride) {
+    const unsigned f = p / pix_frame, lp = p - f * pix_frame;
+    const size_t s0 = (size_t)f * (a.n_frames > 1 ? a.frame_rays : 0u) + (size_t)lp * aa;
     V3 sum = v3(0.0, 0.0, 0.0);
     for (unsigned s = 0; s < aa; ++s) {
-      const double* c = colors + ((size_t)p * aa + s) * 3;
+      const double* c = colors + (s0 + s) * 3;
       sum = vadd(sum, v3(c[0], c[1], c[2]));
     }
     const V3 avg = vscale(sum, 1.0 / (double)aa);
     uint32_t x, lr, smp;
-    gen0_pixel(a.aa, a.rows, hsize, p * aa, x, lr, smp);
-    double* o = out + ((size_t)lr * hsize + x) * 3;
+    gen0_pixel(a.aa, a.rows, hsize, lp * aa, x, lr, smp);
+    double* o = (a.n_frames > 1 ? a.frames->out[f] : out) + ((size_t)lr * hsize + x) * 3;
     o[0] = avg.x; o[1] = avg.y; o[2] = avg.z;
   }
 }
@@ -911,6 +949,7 @@ Wavefront::~Wavefront() {
   if (d_cnt_) (void)hipFree(d_cnt_);
   if (d_shard_) (void)hipFree(d_shard_);
   if (d_prim_) (void)hipFree(d_prim_);
+  if (d_frames_) (void)hipFree(d_frames_);
   if (ps_rings_) (void)hipFree(ps_rings_);
   if (ps_parents_) (void)hipFree(ps_parents_);
   if (ps_ctr_) (void)hipFree(ps_ctr_);
@@ -1038,7 +1077,7 @@ hipError_t Wavefront::ensure_side() {
   return hipSuccess;
 }
 
-hipError_t Wavefront::ensure_misc(size_t n_diag) {
+hipError_t Wavefront::ensure_misc(size_t n_diag, unsigned n_frames) {
   if (!d_cnt_) WF_CHECK(hipMalloc(&d_cnt_, sizeof(WfCounters)));
   if (!h_fault_) {
     WF_CHECK(hipHostMalloc((void**)&h_fault_, kFaultWords * sizeof(int), hipHostMallocMapped));
@@ -1048,11 +1087,13 @@ hipError_t Wavefront::ensure_misc(size_t n_diag) {
   if (!d_shard_) WF_CHECK(hipMalloc(&d_shard_, (size_t)kMaxGen * 2 * kShards * kShardStride * sizeof(unsigned)));
   if (!ev0_) WF_CHECK(hipEventCreate(&ev0_));
   if (!ev1_) WF_CHECK(hipEventCreate(&ev1_));
-  if (prim_cap_ < n_diag + 4) {
+  if (n_frames > 1 && !d_frames_) WF_CHECK(hipMalloc(&d_frames_, sizeof(FrameTable)));
+  const size_t np = (n_diag + 4) * n_frames;  // one set of primary records per frame of a batch
+  if (prim_cap_ < np) {
     if (d_prim_) (void)hipFree(d_prim_);
     d_prim_ = nullptr;
-    WF_CHECK(hipMalloc(&d_prim_, (n_diag + 4) * sizeof(PrimRec)));
-    prim_cap_ = n_diag + 4;
+    WF_CHECK(hipMalloc(&d_prim_, np * sizeof(PrimRec)));
+    prim_cap_ = np;
   }
   return hipSuccess;
 }
@@ -1187,13 +1228,15 @@ static hipError_t launch_fused(const DevScene& sc, const DevCamera& cam, const W
 hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool camera_mode, const double* d_in_rays,
                              unsigned n0, unsigned aa, unsigned max_depth, unsigned row_block, unsigned shard,
                              unsigned n_shards, double* d_out, hipStream_t stream, const std::string& signature,
-                             DevStats* stats, float* ms_kernel, const WfTuning& tn, bool solo, unsigned flags) {
+                             DevStats* stats, float* ms_kernel, const WfTuning& tn, bool solo, unsigned flags,
+                             const FrameTable* batch, unsigned n_frames) {
   if (max_depth + 2 > (unsigned)kMaxGen) return hipErrorInvalidValue;
   if (aa == 0 || aa > 16 || (aa & (aa - 1)) != 0 || (!camera_mode && aa != 1) || n0 % aa != 0)
     return hipErrorInvalidValue;
+  if (n_frames == 0 || n_frames > kMaxFrames || (n_frames > 1 && !batch)) return hipErrorInvalidValue;
   // with AA the root colours are averaged into d_out by wf_average
   const bool averaged = aa > 1;
-  WF_CHECK(ensure_misc((size_t)sc.n_diag));
+  WF_CHECK(ensure_misc((size_t)sc.n_diag, n_frames));
   const unsigned L = (unsigned)sc.n_lights;
   // BVH traversal (fused generations) and skipped shadow rays unless the
   // reference's every-shape loop is asked for; counting (stats) never changes the algorithm
@@ -1202,9 +1245,16 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
   const bool bvh = tn.accel != 0 && !exhaustive && (sc.n_bvh > 0 || sc.n_obvh > 0);
   const bool fused = bvh;
   const bool skip_shadow = !exhaustive && tn.skip_shadow != 0;
+  // a batch of frames: the fast path's generations over every frame's root
+  // rays (uncounted camera renders only; the caller renders others one by one)
+  const unsigned frame_real = n0;
+  if (n_frames > 1) {
+    if (!camera_mode || !fused || count || n0 == 0) return hipErrorInvalidValue;
+    n0 = n_frames * ((n0 + 63u) & ~63u);
+  }
   // the fast path: one persistent launch per render (rt_persist.hip), for
   // recursion depths whose heap-addressed trees it can hold
-  if (bvh && tn.persist && max_depth <= kPsMaxDepth)
+  if (bvh && tn.persist && max_depth <= kPsMaxDepth && n_frames == 1)
     return render_persist(sc, cam, camera_mode, d_in_rays, n0, aa, max_depth, row_block, shard, n_shards, d_out,
                           stream, stats, ms_kernel, count, tn);
   last_persist_ = false;
@@ -1236,9 +1286,11 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     static_assert(sizeof(WfCounters) % 16 == 0, "WfCounters is zeroed in 16-B words");
     const unsigned n_a = (unsigned)(sizeof(WfCounters) / 16);
     const unsigned n_b = (unsigned)((size_t)(max_depth + 2) * 2 * kShards * kShardStride * sizeof(unsigned) / 16);
-    const unsigned work = std::max<unsigned>(std::max(n_a, n_b), use_prim ? (unsigned)sc.n_diag + 4 : 0u);
+    const unsigned work = std::max<unsigned>(std::max(n_a, n_b), use_prim ? n_frames * ((unsigned)sc.n_diag + 4) : 0u);
+    const FrameTable none{};
     WF_LAUNCH(wf_frame_init, dim3(std::min<unsigned>((work + 255) / 256, 256u)), dim3(256), 0, stream, sc, cam,
-              d_prim_, use_prim ? 1u : 0u, (uint4*)d_cnt_, n_a, (uint4*)d_shard_, n_b);
+              d_prim_, use_prim ? 1u : 0u, (uint4*)d_cnt_, n_a, (uint4*)d_shard_, n_b, n_frames > 1 ? *batch : none,
+              d_frames_, n_frames);
     WF_CHECK(hipGetLastError());
   }
   // Exhaustive pipeline: shadow traces of generation g depend only on
@@ -1277,7 +1329,8 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     a.geo = B.geo; a.surf = B.surf; a.parents = B.parents;
     a.colors = (g == 0 && !averaged) ? d_out : B.colors;
     a.aa = aa;
-    a.rows = n0 / aa / (cam.hsize ? cam.hsize : 1);
+    a.rows = frame_real / aa / (cam.hsize ? cam.hsize : 1);
+    a.n_frames = n_frames; a.frame_rays = n0 / n_frames; a.frame_real = frame_real; a.frames = d_frames_;
     a.next_rays = gens_[g + 1].rays;
     a.child_colors = gens_[g + 1].colors;
     a.cnt = d_cnt_;
@@ -1373,7 +1426,8 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     a.rays = B.rays; a.nodes = B.nodes; a.surf = B.surf; a.parents = B.parents;
     a.colors = (g == 0 && !averaged) ? d_out : B.colors;
     a.aa = aa;
-    a.rows = n0 / aa / (cam.hsize ? cam.hsize : 1);
+    a.rows = frame_real / aa / (cam.hsize ? cam.hsize : 1);
+    a.n_frames = n_frames; a.frame_rays = n0 / n_frames; a.frame_real = frame_real; a.frames = d_frames_;
     a.child_colors = gens_[g + 1].colors;
     a.n = fused ? counts.shadows[g] : counts.rays[g];
     a.in_cnt = g == 0 ? nullptr : shard_cnt((unsigned)g, 0);
@@ -1401,10 +1455,11 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     WF_CHECK(hipGetLastError());
   }
   if (averaged) {
-    const unsigned n_pix = n0 / aa;
+    const unsigned n_pix = n_frames * (frame_real / aa);
     WF_CHECK(pmark(stream, WF_COMBINE, true));
     WfArgs a{};
-    a.aa = aa; a.rows = n_pix / cam.hsize;
+    a.aa = aa; a.rows = frame_real / aa / cam.hsize;
+    a.n_frames = n_frames; a.frame_rays = n0 / n_frames; a.frame_real = frame_real; a.frames = d_frames_;
     WF_LAUNCH(wf_average, dim3(occupancy_grid(wf_average, kWfBlock, 0, n_pix)), dim3(kWfBlock), 0, stream,
                        a, cam.hsize, gens_[0].colors, n_pix, d_out);
     WF_CHECK(hipGetLastError());

@@ -90,7 +90,8 @@ enum WfFlags : unsigned { WF_EXHAUSTIVE = 1u, WF_COUNT = 2u };
 // concurrent renders of different scenes never see each other's settings.
 struct WfTuning {
   int accel = 1;           // 1 = exact-culling BVH fast path (unless the exhaustive loop is asked for)
-  int persist = 1;         // 1 = the persistent frame kernel (rt_persist.hip) when max_depth <= kPsMaxDepth
+  int persist = 0;         // 1 = the persistent frame kernel (rt_persist.hip) when max_depth <= kPsMaxDepth
+                           //     (opt-in: measured ~2x slower than the generation pipeline)
   int skip_shadow = 1;     // 1 = the fast path leaves out shadow rays that cannot change the colour
   int shadow_lb = 1;       // 1 = shadow rays through the light buffer when the scene has one
   int image = 0;           // 0 = automatic scene image of the fast-path kernels, 3 / 1 = global memory
@@ -192,6 +193,18 @@ struct WfGenBuf {  // grow-only; the fast path allocates rays, colors and parent
          cap_surf = 0;
 };
 
+// A batch of frames rendered by one pass of the generation pipeline (camera
+// mode): every generation's launch carries the rays of all of them, so a
+// small frame (a multi-GPU shard) still fills the GPU and the chain of
+// dependent launches is paid once per batch. Frame f's root rays are slots
+// [f * frame_rays, f * frame_rays + frame_real) of generation 0 (frame_rays
+// padded to whole 64-ray chunks, so a chunk never mixes two cameras).
+constexpr unsigned kMaxFrames = 8;
+struct FrameTable {
+  DevCamera cam[kMaxFrames];
+  double* out[kMaxFrames];  // device canvases (the shard's rows, row-major)
+};
+
 // Kernel arguments for one generation.
 struct WfArgs {
   WfRay* rays;          // rays_g (g >= 1 or batch mode)
@@ -228,6 +241,9 @@ struct WfArgs {
   unsigned use_lb;      // fast path: shadow rays through the light buffer
   unsigned lds_flags;   // fast path: what the trace kernel stages in LDS (kLdsSpheres | kLdsDeltas)
   unsigned n_top;       // fast path, global-memory image: the first n_top (breadth-first) nodes are in LDS
+  unsigned n_frames;    // camera mode: frames in this pass (1: cam / colors; > 1: `frames`)
+  unsigned frame_rays, frame_real;  // n_frames > 1: generation-0 slots per frame, root rays per frame
+  const FrameTable* frames;         // n_frames > 1: the device copy of the batch's cameras and canvases
 };
 
 // Per-kernel-class timing of the last frame (profiling mode only).
@@ -272,7 +288,8 @@ class Wavefront {
   hipError_t render(const DevScene& sc, const DevCamera& cam, bool camera_mode, const double* d_in_rays,
                     unsigned n0, unsigned aa, unsigned max_depth, unsigned row_block, unsigned shard,
                     unsigned n_shards, double* d_out, hipStream_t stream, const std::string& signature,
-                    DevStats* stats, float* ms_kernel, const WfTuning& tn, bool solo = true, unsigned flags = 0);
+                    DevStats* stats, float* ms_kernel, const WfTuning& tn, bool solo = true, unsigned flags = 0,
+                    const FrameTable* batch = nullptr, unsigned n_frames = 1);
   // The counters of the last render (rendered with WF_COUNT); synchronises its stream.
   hipError_t read_stats(DevStats* out);
   // A generation's actual queue count differed from the calibrated launch size
@@ -300,7 +317,7 @@ class Wavefront {
   uint16_t* ps_lists_ = nullptr;
   size_t ps_rings_cap_ = 0, ps_parents_cap_ = 0, ps_lists_cap_ = 0;  // records
   hipError_t ensure_gen(size_t g, size_t slots, size_t n_lights, size_t list_slots, bool fused);
-  hipError_t ensure_misc(size_t n_diag);
+  hipError_t ensure_misc(size_t n_diag, unsigned n_frames = 1);
   // shard counters: generation g's rays (q = 0) / shadow list (q = 1)
   unsigned* shard_cnt(unsigned g, unsigned q) { return d_shard_ + ((size_t)g * 2 + q) * kShards * kShardStride; }
   std::vector<WfGenBuf> gens_;
@@ -308,6 +325,7 @@ class Wavefront {
   unsigned* d_shard_ = nullptr;  // kMaxGen x 2 x kShards counters, kShardStride apart
   PrimRec* d_prim_ = nullptr;
   size_t prim_cap_ = 0;
+  FrameTable* d_frames_ = nullptr;  // the current batch's table (written by wf_frame_init)
   hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
   // shadow traces run on a second stream (DESIGN.md "Shadow stream"): fork
   // event per generation (recorded after its closest-hit launch), one join

@@ -118,68 +118,91 @@ class FrameAssembler:
 class StreamFrameAssembler:
     """Frame assembly with frames in flight and no cross-stream coupling.
 
-    Frames render on F streams (frame s on stream s % F). Each stream owns a
-    shard slot, a gather buffer and (on rank 0) a canvas, and a process group
-    of its own, so a frame's render, its gather (RCCL on that group's stream,
-    fenced against the render stream both ways) and rank 0's un-interleave
-    all run in order behind that one stream. Frames on different streams
-    never wait on each other, and slot reuse (frame s + F) is ordered by the
-    stream itself. The un-interleave is one index_select through the inverse
-    row map (as in FrameAssembler). `streams=None` runs on the current stream
-    (CPU tests with gloo).
+    Frames render on F streams in batches of `batch` frames (one
+    rt_render_frames_device call; batch 1 = one frame per call): frame s is
+    frame s % batch of batch s // batch, on stream (s // batch) % F. Each
+    stream owns the shard slots of one batch (contiguous), a gather buffer and
+    (on rank 0) a canvas per frame of the batch, and a process group of its
+    own, so a batch's render, its ONE gather (RCCL on that group's stream,
+    fenced against the render stream both ways) and rank 0's un-interleave all
+    run in order behind that one stream. Batches on different streams never
+    wait on each other, and slot reuse (batch + F) is ordered by the stream
+    itself. The un-interleave is one index_select through the inverse row map
+    (as in FrameAssembler). `streams=None` runs on the current stream (CPU
+    tests with gloo).
     """
 
     def __init__(self, height, width, row_block, rank, n_shards, device, streams=None, groups=None,
-                 dtype=torch.float64, slots=1):
+                 dtype=torch.float64, slots=1, batch=1):
         self.H, self.W, self.B = height, width, row_block
         self.rank, self.n = rank, n_shards
         self.streams = streams
         self.F = len(streams) if streams else max(1, slots)
+        self.NB = max(1, batch)
         self.groups = groups if groups is not None else [None] * self.F
         self.shard_index = shard_of(rank, n_shards)
         self.rows = shard_row_ids(height, row_block, self.shard_index, n_shards)
         self.max_rows = max(len(shard_row_ids(height, row_block, s, n_shards)) for s in range(n_shards))
-        self.shards = [torch.zeros((self.max_rows, width, 3), dtype=dtype, device=device) for _ in range(self.F)]
-        self.shard = self.shards[0]
+        # stream k's batch: NB padded shard slots, back to back (one gather sends them all)
+        self.shards = [torch.zeros((self.NB * self.max_rows, width, 3), dtype=dtype, device=device)
+                       for _ in range(self.F)]
+        self.shard = self.shards[0][: self.max_rows]
         self._last = None
         if rank == 0 and n_shards > 1:
-            self.gather_buf = [torch.empty((n_shards * self.max_rows, width, 3), dtype=dtype, device=device)
+            per = self.NB * self.max_rows  # rows rank s sends
+            self.gather_buf = [torch.empty((n_shards * per, width, 3), dtype=dtype, device=device)
                                for _ in range(self.F)]
-            self.gathered = [[b[s * self.max_rows:(s + 1) * self.max_rows] for s in range(n_shards)]
-                             for b in self.gather_buf]
-            self.canvas = [torch.empty((height, width, 3), dtype=dtype, device=device) for _ in range(self.F)]
-            inv = [0] * height
-            for s in range(n_shards):  # gather position s holds rank s's shard
+            self.gathered = [[b[s * per:(s + 1) * per] for s in range(n_shards)] for b in self.gather_buf]
+            self.canvas = [torch.empty((self.NB * height, width, 3), dtype=dtype, device=device)
+                           for _ in range(self.F)]
+            one, inv = [0] * height, [0] * (self.NB * height)
+            for s in range(n_shards):  # gather position s holds rank s's shard slots
                 for i, y in enumerate(shard_row_ids(height, row_block, shard_of(s, n_shards), n_shards)):
-                    inv[y] = s * self.max_rows + i
-            self.inv_idx = torch.tensor(inv, device=device)
+                    one[y] = s * self.max_rows + i  # one frame's gather (no batch)
+                    for j in range(self.NB):  # canvas j, row y <- rank s's slot j, row i
+                        inv[j * height + y] = s * per + j * self.max_rows + i
+            self.inv_idx = torch.tensor(one, device=device)
+            self.inv_batch = torch.tensor(inv, device=device)
+
+    def _k(self, step):
+        return (step // self.NB) % self.F
 
     def slot(self, step):
-        """Shard buffer frame `step` renders into (on stream step % F)."""
-        return self.shards[step % self.F]
+        """Shard buffer frame `step` renders into (on stream (step // batch) % F)."""
+        j = step % self.NB
+        return self.shards[self._k(step)][j * self.max_rows:(j + 1) * self.max_rows]
 
     def stream(self, step):
-        return self.streams[step % self.F] if self.streams else None
+        return self.streams[self._k(step)] if self.streams else None
 
-    def submit(self, step):
-        """Gather and assemble frame `step`, queued behind its render on its
-        stream; returns its canvas on rank 0 (valid until frame step + F is
-        submitted), None elsewhere."""
-        k = step % self.F
+    def submit(self, step, end=None):
+        """Frame `step` is rendered. At the end of its batch (`end`, default:
+        the batch's last frame) gather and assemble the batch, queued behind
+        its render on its stream; returns frame step's canvas on rank 0 (valid
+        until batch step // batch + F is submitted), None elsewhere or before
+        the batch's end."""
+        k, j = self._k(step), step % self.NB
         if self.n == 1:
-            self._last = self.shards[k][: self.H]
+            self._last = self.slot(step)[: self.H]
             return self._last
+        if end is None:
+            end = j == self.NB - 1
+        if not end:
+            return None
         ctx = torch.cuda.stream(self.streams[k]) if self.streams else _nullctx()
         with ctx:
-            work = dist.gather(self.shards[k], self.gathered[k] if self.rank == 0 else None, dst=0,
-                               group=self.groups[k], async_op=True)
-            work.wait()  # the frame's stream waits on its gather (the host does not block)
+            self._gather(k)
             if self.rank != 0:
                 self._last = None
                 return None
-            torch.index_select(self.gather_buf[k], 0, self.inv_idx, out=self.canvas[k])
-            self._last = self.canvas[k]
+            torch.index_select(self.gather_buf[k], 0, self.inv_batch, out=self.canvas[k])
+            self._last = self.canvas[k][j * self.H:(j + 1) * self.H]
             return self._last
+
+    def _gather(self, k):
+        work = dist.gather(self.shards[k], self.gathered[k] if self.rank == 0 else None, dst=0,
+                           group=self.groups[k], async_op=True)
+        work.wait()  # the batch's stream waits on its gather (the host does not block)
 
     def flush(self):
         """The last submitted frame's canvas on rank 0 (everything is already queued)."""
@@ -214,9 +237,9 @@ class RcclStreamAssembler(StreamFrameAssembler):
     `streams` entries may be None (CPU tests: the current stream)."""
 
     def __init__(self, height, width, row_block, rank, n_shards, device, streams, dtype=torch.float64, lib=None,
-                 timeout_ms=60000):
+                 timeout_ms=60000, batch=1):
         super().__init__(height, width, row_block, rank, n_shards, device, streams=streams,
-                         groups=[None] * len(streams), dtype=dtype)
+                         groups=[None] * len(streams), dtype=dtype, batch=batch)
         if lib is None:
             from . import _rtamd as lib
         self._lib = lib
@@ -259,22 +282,17 @@ class RcclStreamAssembler(StreamFrameAssembler):
         st = self.streams[k]
         return (st.cuda_stream if st is not None else 0), st
 
-    def submit(self, step):
-        k = step % self.F
-        if self.n == 1:
-            self._last = self.shards[k][: self.H]
-            return self._last
-        handle, st = self._stream_handle(k)
+    def submit(self, step, end=None):
+        k = self._k(step)
+        if self.n == 1 or self.streams[k] is None:
+            return super().submit(step, end)
+        with torch.cuda.stream(self.streams[k]):  # index_select on the render stream, behind the gather
+            return super().submit(step, end)
+
+    def _gather(self, k):
+        handle, _ = self._stream_handle(k)
         recv = self.gather_buf[k].data_ptr() if self.rank == 0 else 0
-        self._lib._nccl_gather_f64(self.shards[k].data_ptr(), recv, self.shards[k].numel(), 0, self.comms[k],
-                                   handle)
-        if self.rank != 0:
-            self._last = None
-            return None
-        with (torch.cuda.stream(st) if st is not None else _nullctx()):
-            torch.index_select(self.gather_buf[k], 0, self.inv_idx, out=self.canvas[k])
-        self._last = self.canvas[k]
-        return self._last
+        self._lib._nccl_gather_f64(self.shards[k].data_ptr(), recv, self.shards[k].numel(), 0, self.comms[k], handle)
 
     def abort(self):
         """Tear the communicators down without waiting on peers (failure path)."""

@@ -119,9 +119,21 @@ def test_shard_rows_partition(rt):
         assert [len(r) for r in rows] == [rt.shard_rows(H, B, s, n) for s in range(n)]
 
 
-def _stream_worker(rank, world_size, port, row_block, n_frames, n_slots, out_path):
+def _batch_done(fa, f, batch, n_frames, c, done):
+    """Rank 0's canvases of the batch that frame f ends (if it ends one)."""
+    if f % batch != batch - 1 and f != n_frames - 1:
+        assert c is None
+        return
+    k = (f // batch) % fa.F
+    for g in range(f - f % batch, f + 1):
+        done.append(fa.canvas[k][(g % batch) * fa.H:(g % batch + 1) * fa.H].clone())
+    assert torch.equal(c, done[-1])
+
+
+def _stream_worker(rank, world_size, port, row_block, n_frames, n_slots, out_path, batch=1):
     """StreamFrameAssembler (bench.py's N>1 path): frame f is golden + f, one
-    process group per slot; every submit returns frame f assembled."""
+    process group per slot; every submit returns frame f assembled (batch > 1:
+    every batch's last submit gathers and assembles the batch)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world_size)
     try:
@@ -130,12 +142,19 @@ def _stream_worker(rank, world_size, port, row_block, n_frames, n_slots, out_pat
         H, W = ref.shape[:2]
         groups = [dist.new_group(list(range(world_size))) for _ in range(n_slots)]
         fa = StreamFrameAssembler(H, W, row_block, rank, world_size, torch.device("cpu"), groups=groups,
-                                  slots=n_slots)
+                                  slots=n_slots, batch=batch)
         done = []
         for f in range(n_frames):
             buf = fa.slot(f)
             buf.fill_(-1.0)
             buf[: len(fa.rows)] = ref[fa.rows] + f
+            if batch > 1:
+                c = fa.submit(f, end=f % batch == batch - 1 or f == n_frames - 1)
+                if rank == 0:
+                    _batch_done(fa, f, batch, n_frames, c, done)
+                else:
+                    assert c is None
+                continue
             c = fa.submit(f)
             if rank == 0:
                 done.append(c.clone())
@@ -159,6 +178,20 @@ def test_gloo_stream_assembler(tmp_path, world_size, row_block, n_slots):
     ref = np.load(os.path.join(HERE, "golden", "c3_64x36_s200.npz"))["canvas"]
     assert got.shape == (6,) + ref.shape
     for f in range(6):
+        assert np.array_equal(got[f], ref + f), f
+
+
+@pytest.mark.parametrize("world_size,row_block,n_slots,batch", [(2, 8, 2, 4), (3, 5, 3, 3)])
+def test_gloo_stream_assembler_batches(tmp_path, world_size, row_block, n_slots, batch):
+    """Batches of frames (bench.py --batch: one render call and ONE gather per
+    batch): 11 frames, the last batch partial, every frame comes out whole."""
+    out = str(tmp_path / "frames.npy")
+    mp.spawn(_stream_worker, args=(world_size, _free_port(), row_block, 11, n_slots, out, batch), nprocs=world_size,
+             join=True)
+    got = np.load(out)
+    ref = np.load(os.path.join(HERE, "golden", "c3_64x36_s200.npz"))["canvas"]
+    assert got.shape == (11,) + ref.shape
+    for f in range(11):
         assert np.array_equal(got[f], ref + f), f
 
 
@@ -202,7 +235,7 @@ class _FakeRccl:
             dist.gather(src, None, dst=0)
 
 
-def _rccl_assembler_worker(rank, world_size, port, fail_at, n_frames, out_path):
+def _rccl_assembler_worker(rank, world_size, port, fail_at, n_frames, out_path, batch=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world_size)
     try:
@@ -220,7 +253,8 @@ def _rccl_assembler_worker(rank, world_size, port, fail_at, n_frames, out_path):
             dist.barrier()  # the default group still works: nobody is stuck in an init
             np.save(out_path + f".{rank}", np.array([len(lib.made)]))
             return
-        fa = RcclStreamAssembler(H, W, 8, rank, world_size, torch.device("cpu"), streams=[None] * F, lib=lib)
+        fa = RcclStreamAssembler(H, W, 8, rank, world_size, torch.device("cpu"), streams=[None] * F, lib=lib,
+                                 batch=batch)
         assert fa.comms == [1000 * (rank + 1) + k for k in range(F)]
         for t in fa.shards:
             lib.tensors[t.data_ptr()] = t
@@ -232,6 +266,20 @@ def _rccl_assembler_worker(rank, world_size, port, fail_at, n_frames, out_path):
             buf = fa.slot(f)
             buf.fill_(-1.0)
             buf[: len(fa.rows)] = ref[fa.rows] + f
+            if batch > 1:
+                n_before = len(lib.gathers)
+                end = f % batch == batch - 1 or f == n_frames - 1
+                c = fa.submit(f, end=end)
+                # one gather per batch, of the batch's slots, over communicator (f // batch) % F
+                assert len(lib.gathers) == n_before + (1 if end else 0)
+                if end:
+                    k = (f // batch) % F
+                    assert lib.gathers[-1][:2] == (fa.shards[k].data_ptr(), fa.comms[k])
+                if rank == 0:
+                    _batch_done(fa, f, batch, n_frames, c, done)
+                else:
+                    assert c is None
+                continue
             c = fa.submit(f)
             # frame f gathers slot f % F over communicator f % F
             assert lib.gathers[-1][:2] == (fa.shards[f % F].data_ptr(), fa.comms[f % F])
@@ -256,6 +304,17 @@ def test_gloo_rccl_stream_assembler_frames(tmp_path):
     got = np.load(out)
     ref = np.load(os.path.join(HERE, "golden", "c3_64x36_s200.npz"))["canvas"]
     for f in range(7):
+        assert np.array_equal(got[f], ref + f), f
+
+
+def test_gloo_rccl_stream_assembler_batches(tmp_path):
+    """The RCCL assembler with batches: one library gather per batch."""
+    out = str(tmp_path / "frames.npy")
+    mp.spawn(_rccl_assembler_worker, args=(2, _free_port(), None, 13, out, 4), nprocs=2, join=True)
+    got = np.load(out)
+    ref = np.load(os.path.join(HERE, "golden", "c3_64x36_s200.npz"))["canvas"]
+    assert got.shape == (13,) + ref.shape
+    for f in range(13):
         assert np.array_equal(got[f], ref + f), f
 
 

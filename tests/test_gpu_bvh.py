@@ -236,7 +236,7 @@ def test_fused_images_bitwise(rt, image, shadow_lb, persist):
     finally:
         w.tune("image", 0)
         w.tune("shadow_lb", 1)
-        w.tune("persist", 1)
+        w.tune("persist", 0)
     assert fast.to_numpy().tobytes() == exact.to_numpy().tobytes()
 
 

@@ -173,5 +173,4 @@ def test_queue_check_reports_miscalibration(rt, via_check):
     cam.render_shard_device(w, depth, 8, 0, 1, buf.data_ptr(), st.cuda_stream, False)  # recalibrates
     torch.cuda.synchronize()
     w.check()
-    w.tune("persist", 1)
     assert torch.equal(buf, exact)

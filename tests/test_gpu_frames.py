@@ -1,0 +1,123 @@
+"""Batches of frames (rt_render_frames_device, DESIGN.md §5.8 "Frame
+batches"): up to 8 cameras share each launch of the generation pipeline.
+Every frame of a batch must equal the same camera's rt_render_shard_device
+frame bit for bit (itself checked against the exhaustive frame and the
+oracle elsewhere), for whole frames and shards, with and without AA, ragged
+frame sizes (root rays not a multiple of 64), more frames than one pass
+holds, and scenes the batch cannot take (rendered frame by frame)."""
+import math
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+PI = math.pi
+
+
+def _cameras(rt, n, w, h):
+    cams = []
+    for k in range(n):
+        c = rt.Camera(w, h, PI / 3.0)
+        a = 2 * PI * k / max(n, 1)
+        c.set_transform(rt.view_transform(rt.Point(12 * math.sin(a), 3 + 0.3 * k, -12 * math.cos(a)),
+                                          rt.Point(0, 1, 5), rt.Vector(0, 1, 0)))
+        cams.append(c)
+    return cams
+
+
+def _check(rt, w, cams, depth, row_block, shard, n_shards, aa=1):
+    import torch
+    rows = rt.shard_rows(cams[0].vsize, row_block, shard, n_shards)
+    bat = [torch.full((rows, cams[0].hsize, 3), -1.0, dtype=torch.float64, device="cuda") for _ in cams]
+    one = [torch.full_like(b, -2.0) for b in bat]
+    torch.cuda.synchronize()
+    st = torch.cuda.current_stream().cuda_stream
+    rt.render_frames_device(w, cams, depth, row_block, shard, n_shards, [b.data_ptr() for b in bat], st, False, aa)
+    for c, b in zip(cams, one):
+        c.render_shard_device(w, depth, row_block, shard, n_shards, b.data_ptr(), st, False, aa)
+    torch.cuda.synchronize()
+    w.check()
+    for k, (b, o) in enumerate(zip(bat, one)):
+        assert torch.equal(b, o), k
+
+
+@pytest.mark.parametrize("n", [2, 8, 11])
+def test_frames_whole_bitwise(rt, n):
+    from rtamd import scenes
+    w, _, depth = scenes.c3(96, 54, n_spheres=400)
+    _check(rt, w, _cameras(rt, n, 96, 54), depth, 8, 0, 1)
+
+
+@pytest.mark.parametrize("shard", [0, 3, 7])
+def test_frames_shards_bitwise(rt, shard):
+    from rtamd import scenes
+    w, _, depth = scenes.c3(200, 113, n_spheres=600)
+    _check(rt, w, _cameras(rt, 5, 200, 113), depth, 8, shard, 8)
+
+
+@pytest.mark.parametrize("aa", [2, 4])
+def test_frames_aa_bitwise(rt, aa):
+    from rtamd import scenes
+    w, _, depth = scenes.c3(37, 23, n_spheres=300)  # ragged: 37*23*aa root rays per frame
+    _check(rt, w, _cameras(rt, 6, 37, 23), depth, 8, 1, 2, aa)
+
+
+@pytest.mark.parametrize("hw", [(1, 1), (7, 3), (65, 1)])
+def test_frames_tiny(rt, hw):
+    from rtamd import scenes
+    w, _, depth = scenes.c3(8, 8, n_spheres=100)
+    _check(rt, w, _cameras(rt, 3, *hw), depth, 8, 0, 1)
+
+
+def test_frames_zoo_and_deep(rt):
+    """Every shape kind and pattern (the other-shape hierarchy) and deep recursion."""
+    from rtamd import scenes
+    w, cam, _ = scenes.zoo(64, 48)
+    cams = _cameras(rt, 4, 64, 48)
+    _check(rt, w, cams, 5, 8, 0, 1)
+    _check(rt, w, cams, 12, 8, 0, 1)
+
+
+def test_frames_unbatchable_scene(rt):
+    """A scene without the fast path's hierarchies (planes only) is rendered
+    frame by frame by the same call."""
+    w = rt.World()
+    fl = rt.Plane()
+    fl.material.reflective = 0.5
+    w.add_object(fl)
+    wall = rt.Plane()
+    wall.set_transform(rt.translation(0, 0, 10) * rt.rotation_x(PI / 2))
+    w.add_object(wall)
+    w.add_light(rt.PointLight(rt.Point(-10, 10, -10), rt.Color(1, 1, 1)))
+    _check(rt, w, _cameras(rt, 3, 40, 30), 5, 8, 0, 1)
+
+
+def test_frames_stats_sum(rt):
+    """With stats the frames are counted one by one and the counters summed."""
+    import torch
+    from rtamd import scenes
+    w, _, depth = scenes.c3(64, 36, n_spheres=200)
+    cams = _cameras(rt, 3, 64, 36)
+    bufs = [torch.empty((36, 64, 3), dtype=torch.float64, device="cuda") for _ in cams]
+    st = rt.render_frames_device(w, cams, depth, 8, 0, 1, [b.data_ptr() for b in bufs], 0, True)
+    tot = {}
+    for c in cams:
+        _, s = c.render(w, depth, want_stats=True, exhaustive=False)
+        for k in ("rays_primary", "rays_reflect", "rays_refract", "rays_shadow", "sphere_tests", "plane_tests"):
+            tot[k] = tot.get(k, 0) + s[k]
+    for k, v in tot.items():
+        assert st[k] == v, k
+
+
+def test_frames_errors(rt):
+    import torch
+    from rtamd import scenes
+    w, _, depth = scenes.c3(16, 16, n_spheres=10)
+    b = torch.empty((16, 16, 3), dtype=torch.float64, device="cuda")
+    with pytest.raises(rt.RtError):  # sizes differ
+        rt.render_frames_device(w, [rt.Camera(16, 16, 1.0), rt.Camera(16, 8, 1.0)], depth, 8, 0, 1,
+                                [b.data_ptr(), b.data_ptr()])
+    with pytest.raises(rt.RtError):
+        rt.render_frames_device(w, [rt.Camera(16, 16, 1.0)], depth, 8, 1, 1, [b.data_ptr()])
+    with pytest.raises(rt.RtError):
+        rt.render_frames_device(w, [rt.Camera(16, 16, 1.0)], depth, 8, 0, 1, [b.data_ptr()], 0, False, 3)
+    rt.render_frames_device(w, [], depth, 8, 0, 1, [])  # nothing to render

@@ -1,9 +1,10 @@
 """The persistent frame kernel (rt_persist.hip, DESIGN.md §5.1 "Persistent
 frames"): one launch renders every recursion depth, with shade_hit's combine
 folded into the children's delivery (an atomic countdown per parent record).
-It is the default fast path for max_depth <= 8; every frame here must equal
-the exhaustive frame (the reference's every-shape loop, itself checked against
-the oracle) bit for bit, and its counters must equal the reference's."""
+It is an opt-in fast path (WfTuning::persist) for max_depth <= 8; every frame
+here must equal the exhaustive frame (the reference's every-shape loop, itself
+checked against the oracle) bit for bit, and its counters must equal the
+reference's."""
 import math
 
 import numpy as np
@@ -28,6 +29,7 @@ def _glass(rt, n=200, seed=7, inside=False):
         s.material.color = rt.Color(*rng.uniform(0, 1, 3))
         w.add_object(s)
     w.add_light(rt.PointLight(rt.Point(-10, 10, -10), rt.Color(1, 1, 1)))
+    w.tune("persist", 1)
     cam = rt.Camera(80, 56, PI / 2.5)
     frm = (0.2, 1.1, -0.4) if inside else (0, 2, -9)
     cam.set_transform(rt.view_transform(rt.Point(*frm), rt.Point(0, 1, 2), rt.Vector(0, 1, 0)))
@@ -51,6 +53,7 @@ def test_persist_scenes_bitwise(rt, name):
     w, cam, depth = {"c3": lambda: scenes.c3(192, 108), "zoo": lambda: scenes.zoo(120, 90),
                      "solids": lambda: scenes.solids(120, 90),
                      "first_scene": lambda: scenes.first_scene(160, 90)}[name]()
+    w.tune("persist", 1)
     fast, _ = cam.render(w, depth, want_stats=False)
     assert rt._rtamd._wf_profile(w, -1, True)["persist"]
     exact, _ = cam.render(w, depth, want_stats=True)
@@ -112,6 +115,7 @@ def test_persist_back_to_back_and_shards(rt):
     import torch
     from rtamd import scenes
     w, cam, depth = scenes.c3(240, 136, n_spheres=600)
+    w.tune("persist", 1)
     full, _ = cam.render(w, depth, want_stats=True)
     full = torch.from_numpy(full.to_numpy()).cuda()
     st = torch.cuda.current_stream().cuda_stream
@@ -134,7 +138,7 @@ def test_persist_back_to_back_and_shards(rt):
 
 
 def test_persist_off_matches(rt):
-    """The generation pipeline (persist off) renders the same frame."""
+    """The generation pipeline (persist off, the default) renders the same frame."""
     w, cam = _glass(rt, n=200, seed=17)
     a, _ = cam.render(w, 6, want_stats=False)
     w.tune("persist", 0)

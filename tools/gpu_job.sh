@@ -8,6 +8,8 @@
 #   benchq     bench.py without the CPU baseline / end-to-end (quick)
 #   c5         bench.py --config c5 --steps 3 --warmup 1 (no CPU baseline)
 #   shard      tools/shard_time.py --ns 1,2,4,8
+#   shardb     the same with 8-frame batches (rt_render_frames_device)
+#   tsel       pytest -m gpu of the files in $TESTS
 #   trace      rocprofv3 --kernel-trace --stats of the timed bench regime
 #   trace_c5   the same for C5
 #   pmc        tools/profile.sh TAG (kernel trace + PMC passes of 5 serialized frames)
@@ -37,6 +39,8 @@ for s in "$@"; do
     benchq) step benchq 400 python bench.py --no-cpu-baseline --no-end-to-end || exit 1; grep '^{' "$OUT/benchq.log" > "$OUT/benchq.json" ;;
     c5) step c5 600 python bench.py --config c5 --steps 3 --warmup 1 --no-cpu-baseline --no-end-to-end || exit 1 ;;
     shard) step shard 600 python tools/shard_time.py --ns 1,2,4,8 --frames 100 --ranks || exit 1 ;;
+    shardb) step shardb 600 python tools/shard_time.py --ns 1,2,4,8 --frames 160 --batch 8 --ranks || exit 1 ;;
+    tsel) step tsel 600 python -u -m pytest $TESTS -m gpu -x -v --timeout 240 --timeout-method thread -p no:cacheprovider || exit 1 ;;
     trace) step trace 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o trace --output-format csv -- \
              python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-end-to-end || exit 1 ;;
     trace_c5) step trace_c5 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace_c5" -o trace_c5 --output-format csv -- \

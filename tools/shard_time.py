@@ -3,7 +3,8 @@
 one local GPU, so the render part of the multi-GPU scaling curve can be read
 without N GPUs (the RCCL gather is not included). Prints, per N, the mean
 frame time over the ranks and the worst rank, and the per-class breakdown of
-rank 0. Usage: shard_time.py [--frames K] [--knob k=v ...]"""
+rank 0. --batch B renders B frames per call (rt_render_frames_device; the
+frame count stays K). Usage: shard_time.py [--frames K] [--batch B] [--knob k=v ...]"""
 import argparse
 import os
 import sys
@@ -28,6 +29,7 @@ ap.add_argument("--streams", default="raw", choices=["torch", "once", "raw", "cu
                 help="torch: new torch streams per rank; once: torch streams made once; raw / cumask: library-made streams (cumask: hipExtStreamCreateWithCUMask), made once")
 ap.add_argument("--reverse", action="store_true", help="measure the ranks last to first")
 ap.add_argument("--ranks", action="store_true", help="print every rank's time")
+ap.add_argument("--batch", type=int, default=1)
 a = ap.parse_args()
 for kv in a.knob:
     k, v = kv.split("=")
@@ -53,21 +55,31 @@ for n in [int(x) for x in a.ns.split(",")]:
         F = max(1, a.inflight)
         if F > 1:
             w.tune("shadow_stream", 0)  # as bench.py
-        bufs = [torch.empty((rows, W, 3), dtype=torch.float64, device="cuda") for _ in range(F)]
+        NB = max(1, a.batch)
+        bufs = [torch.empty((rows, W, 3), dtype=torch.float64, device="cuda") for _ in range(F * NB)]
         sts = _made or ([torch.cuda.Stream() for _ in range(F)] if F > 1 else [torch.cuda.current_stream()])
+
+        def one(f):
+            if NB == 1:
+                cam.render_shard_device(w, depth, B, r, n, bufs[f % F].data_ptr(), sts[f % F].cuda_stream, False)
+            else:
+                k = f % F
+                rtamd.render_frames_device(w, [cam] * NB, depth, B, r, n,
+                                           [b.data_ptr() for b in bufs[k * NB:(k + 1) * NB]], sts[k].cuda_stream)
         torch.cuda.synchronize()
         for f in range(3 * F):
-            cam.render_shard_device(w, depth, B, r, n, bufs[f % F].data_ptr(), sts[f % F].cuda_stream, False)
+            one(f)
         torch.cuda.synchronize()
+        calls = max(1, a.frames // NB)
         t0 = time.perf_counter()
-        for f in range(a.frames):
-            cam.render_shard_device(w, depth, B, r, n, bufs[f % F].data_ptr(), sts[f % F].cuda_stream, False)
+        for f in range(calls):
+            one(f)
         torch.cuda.synchronize()
-        times[r] = (time.perf_counter() - t0) / a.frames * 1e3
+        times[r] = (time.perf_counter() - t0) / (calls * NB) * 1e3
         if r == 0:  # per-class times from a separate profiled pass (events would slow the timed frames)
             rtamd._rtamd._wf_profile(w, 1, False)
-            for f in range(min(a.frames, 20)):
-                cam.render_shard_device(w, depth, B, r, n, bufs[f % F].data_ptr(), sts[f % F].cuda_stream, False)
+            for f in range(min(calls, 20)):
+                one(f)
             torch.cuda.synchronize()
             p = rtamd._rtamd._wf_profile(w, 0, True)
             cls = " ".join(f"{c}={m:.3f}" for c, m in p["ms"].items())
