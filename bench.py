@@ -8,7 +8,7 @@ of primary + reflection + refraction + shadow rays (each one a
 launched by torch.distributed.run) the frame is split into interleaved 8-row
 blocks, each rank renders its rows into HBM, and the canvas is assembled on
 rank 0 with one RCCL gather (strong scaling: the frame is fixed). F frames
-are rendered in batches of NB (--batch, default 8 for C3, 1 for C5: one
+are rendered in batches of NB (--batch, default for C3 8 on 1-2 GPUs and 16 on 4+, 1 for C5: one
 rt_render_frames_device call renders NB frames, every launch of the pipeline
 carrying all of them) on F streams (--inflight, default 4 for C3, 1 for C5),
 each with its own library workspace, so one batch's short, latency-bound deep
@@ -131,7 +131,8 @@ def parse():
     p.add_argument("--depth", type=int, default=None)
     p.add_argument("--row-block", type=int, default=8)
     p.add_argument("--batch", type=int, default=None,
-                   help="frames per render call (rt_render_frames_device, <= 8; default 8 for C3, 1 for C5)")
+                   help="frames per render call (rt_render_frames_device, <= 16; default for C3 8 on 1-2 GPUs, "
+                        "16 on 4+; 1 for C5)")
     p.add_argument("--inflight", type=int, default=None,
                    help="frames in flight: consecutive frames render on this many streams (own workspaces)")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget for the CPU baseline sample")
@@ -312,7 +313,8 @@ def main():
     # default: 4 frames in flight for C3; one for C5, whose wavefront workspace
     # (16.8 M primary rays, depth 8) takes tens of GB per frame
     F = max(1, a.inflight if a.inflight is not None else (4 if a.config == "c3" else 1))
-    NB = max(1, min(8, a.batch if a.batch is not None else (8 if a.config == "c3" else 1)))
+    # (C3: 8 frames per pass on 1-2 GPUs, 16 on the smaller shards of 4+; C5's frame fills the GPU alone)
+    NB = max(1, min(16, a.batch if a.batch is not None else ((8 if n < 4 else 16) if a.config == "c3" else 1)))
     stream = torch.cuda.current_stream()
     kind = a.stream_kind
     if F == 1:

@@ -225,7 +225,7 @@ int rt_render_shard_device_ex(const rt_scene* scene, const rt_camera_desc* camer
  * vsize (the frames of an animation, or the steady state of a frame loop)
  * over the same world: frame f's shard (as rt_render_shard_device) goes to the
  * DEVICE buffer d_out_rgb[f]. Each frame equals its rt_render_shard_device
- * render bit for bit; the frames are rendered together, up to 8 per pass of
+ * render bit for bit; the frames are rendered together, up to 16 per pass of
  * the pipeline (one launch per recursion generation carries all of them), so
  * small frames and shards pay the per-pass cost once. Asynchronous on
  * `stream` unless `stats` is non-NULL: then the frames are rendered one by
@@ -307,6 +307,18 @@ int rt_render_ppm(const rt_scene* scene, const rt_camera_desc* camera,
 
 /* `scale_color_component` (image/ppm.rs:73-75) over n values. */
 int rt_quantize_u8(const double* values, size_t n, uint8_t* out);
+
+/* ---- host buffers ------------------------------------------------------------ */
+
+/* Page-locked host memory for the outputs of the host-buffer entry points
+ * (rt_render, rt_render_aa, rt_render_ex, rt_color_at_batch, ...): the device
+ * writes such a buffer directly at the full link rate, where a pageable buffer
+ * is pinned for the duration of each call (or staged). A Canvas that lives for
+ * many frames (or a pool of them) keeps its pixels here. Released blocks are
+ * pooled (up to 1 GiB) and handed out again for requests of about their size.
+ * NULL on failure (rt_last_error). */
+void* rt_host_buffer_alloc(size_t bytes);
+void rt_host_buffer_free(void* p);
 
 /* ---- diagnostics ----------------------------------------------------------- */
 const char* rt_last_error(void);

@@ -133,14 +133,24 @@ inline Shape Cone(double minimum = -std::numeric_limits<double>::infinity(),
 // memory marked for transparent huge pages, so the first touch of a fresh
 // 50-MB canvas (the device-to-host copy of `render`) takes tens of page
 // faults instead of ~12 000.
+// A render's output canvas (Uninit) of 4 MiB and more takes a pinned block
+// from the library's pool (rt_host_buffer_alloc), which the device writes
+// directly at the link rate; blocks return to the pool with the canvas.
 struct PixelFree {
-  void operator()(double* p) const noexcept { std::free(p); }
+  bool pinned = false;
+  void operator()(double* p) const noexcept {
+    if (pinned) rt_host_buffer_free(p);
+    else std::free(p);
+  }
 };
 using PixelPtr = std::unique_ptr<double[], PixelFree>;
-inline PixelPtr alloc_pixels(size_t n) {
+inline PixelPtr alloc_pixels(size_t n, bool pinned = false) {
   const size_t bytes = std::max<size_t>(n, 1) * sizeof(double);
   constexpr size_t kHuge = (size_t)2 << 20;
   void* p = nullptr;
+  if (pinned && bytes >= 2 * kHuge) {
+    if (void* q = rt_host_buffer_alloc(bytes)) return PixelPtr((double*)q, PixelFree{true});
+  }
   if (bytes >= kHuge) {
     if (posix_memalign(&p, kHuge, (bytes + kHuge - 1) / kHuge * kHuge) != 0) p = nullptr;
     if (p) (void)madvise(p, (bytes + kHuge - 1) / kHuge * kHuge, MADV_HUGEPAGE);
@@ -159,7 +169,7 @@ class Canvas {
   // Storage the caller overwrites entirely (a render writes every pixel): no
   // zero pass, so the pages are first touched by the copy from the device.
   struct Uninit {};
-  Canvas(size_t w, size_t h, Uninit) : w_(w), h_(h), px_(alloc_pixels(w * h * 3)) {}
+  Canvas(size_t w, size_t h, Uninit) : w_(w), h_(h), px_(alloc_pixels(w * h * 3, true)) {}
   Canvas(const Canvas& o) : w_(o.w_), h_(o.h_), px_(alloc_pixels(o.w_ * o.h_ * 3)) {
     std::memcpy(px_.get(), o.px_.get(), w_ * h_ * 3 * sizeof(double));
   }
@@ -181,10 +191,10 @@ class Canvas {
   double* data() { return px_.get(); }
   const double* data() const { return px_.get(); }
   std::string to_ppm() const {  // canvas_to_ppm (image/ppm.rs:24-51)
-    size_t len = 0;
-    check(rt_canvas_to_ppm(px_.get(), (uint32_t)w_, (uint32_t)h_, nullptr, 0, &len), "rt_canvas_to_ppm");
-    std::string s(len, '\0');
-    check(rt_canvas_to_ppm(px_.get(), (uint32_t)w_, (uint32_t)h_, &s[0], len, &len), "rt_canvas_to_ppm");
+    size_t len = 0;  // one pass into the bound (12 bytes per pixel, a newline per row, the header)
+    std::string s((size_t)12 * w_ * h_ + h_ + 32, '\0');
+    check(rt_canvas_to_ppm(px_.get(), (uint32_t)w_, (uint32_t)h_, &s[0], s.size(), &len), "rt_canvas_to_ppm");
+    s.resize(len);
     return s;
   }
 

@@ -245,10 +245,22 @@ PYBIND11_MODULE(_rtamd, m) {
     if (rgb.ndim() != 3 || rgb.shape(2) != 3) throw std::invalid_argument("expected (h, w, 3)");
     size_t len = 0;
     const uint32_t h = (uint32_t)rgb.shape(0), w = (uint32_t)rgb.shape(1);
-    check(rt_canvas_to_ppm(rgb.data(), w, h, nullptr, 0, &len), "rt_canvas_to_ppm");
-    std::string s(len, '\0');
-    check(rt_canvas_to_ppm(rgb.data(), w, h, &s[0], len, &len), "rt_canvas_to_ppm");
-    return py::bytes(s);
+    // one pass into a bytes object of the bound (12 bytes per pixel at most, + a newline per
+    // row + the header), shrunk to the text afterwards: the pages past it are never touched
+    const size_t bound = (size_t)12 * w * h + h + 32;
+    PyObject* obj = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)bound);
+    if (!obj) throw py::error_already_set();
+    int rc;
+    {
+      py::gil_scoped_release nogil;
+      rc = rt_canvas_to_ppm(rgb.data(), w, h, PyBytes_AS_STRING(obj), bound, &len);
+    }
+    if (rc != RT_OK) {
+      Py_DECREF(obj);
+      check(rc, "rt_canvas_to_ppm");
+    }
+    if (_PyBytes_Resize(&obj, (Py_ssize_t)len) != 0) throw py::error_already_set();
+    return py::reinterpret_steal<py::bytes>(obj);
   });
   // canvas_to_ppm of a device canvas into a device buffer (pointers as integers, e.g.
   // torch tensors' data_ptr()); returns the text's length

@@ -41,6 +41,22 @@ int g_lb_res = 256;     // light-buffer cells per cube-map face edge at scene cr
 std::mutex g_tune_mu;
 WfTuning g_tune_defaults;
 
+// Pinned host buffers (rt_host_buffer_alloc): page-locked blocks the DMA
+// engine writes at the full link rate, kept in a small pool on release so a
+// frame loop's canvases reuse the same pages (no registration, no page faults).
+// The pool is never torn down (the HIP runtime may be gone at process exit).
+std::mutex g_pin_mu;
+std::vector<std::pair<void*, size_t>> g_pin_live, g_pin_free;
+size_t g_pin_free_bytes = 0;
+constexpr size_t kPinPoolBytes = (size_t)1 << 30;
+
+bool pinned_block(const void* p, size_t n) {
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  for (const auto& b : g_pin_live)
+    if ((const char*)p >= (const char*)b.first && (const char*)p + n <= (const char*)b.first + b.second) return true;
+  return false;
+}
+
 int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
@@ -259,6 +275,11 @@ int ensure_dev_buffer(double** buf, size_t* cap, size_t need) {
 constexpr size_t kStageChunk = (size_t)8 << 20;
 int copy_to_host(rt_scene* s, void* dst, const void* src, size_t n, hipStream_t st) {
   if (n == 0) return RT_OK;
+  if (pinned_block(dst, n)) {  // an rt_host_buffer_alloc block: the DMA engine writes it directly
+    RT_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, st));
+    RT_HIP(hipStreamSynchronize(st));
+    return RT_OK;
+  }
   // Large copies: pin the caller's pages for this call and let the DMA engine
   // write them directly (one pass over the bytes instead of DMA + host memcpy).
   // The registration never outlives the call, so the caller may free or reuse
@@ -606,6 +627,55 @@ size_t rt_sizeof_camera_desc(void) { return sizeof(rt_camera_desc); }
 size_t rt_sizeof_stats(void) { return sizeof(rt_stats); }
 static_assert(sizeof(rt_shape_desc) == 680 && sizeof(rt_camera_desc) == 160 && sizeof(rt_stats) == 112,
               "ABI struct sizes (include/rt_render.h, INTEGRATION.md)");
+
+void* rt_host_buffer_alloc(size_t bytes) {
+  if (bytes == 0) {
+    g_err = "rt_host_buffer_alloc: zero bytes";
+    return nullptr;
+  }
+  try {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    for (size_t i = 0; i < g_pin_free.size(); ++i)
+      if (g_pin_free[i].second >= bytes && g_pin_free[i].second <= bytes + bytes / 4) {  // a close fit
+        const auto b = g_pin_free[i];
+        g_pin_free.erase(g_pin_free.begin() + (long)i);
+        g_pin_free_bytes -= b.second;
+        g_pin_live.push_back(b);
+        return b.first;
+      }
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess || !p) {
+      (void)hipGetLastError();
+      g_err = "rt_host_buffer_alloc: hipHostMalloc failed";
+      return nullptr;
+    }
+    g_pin_live.emplace_back(p, bytes);
+    return p;
+  } catch (...) {
+    g_err = "out of memory";
+    return nullptr;
+  }
+}
+
+void rt_host_buffer_free(void* p) {
+  if (!p) return;
+  try {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    for (size_t i = 0; i < g_pin_live.size(); ++i)
+      if (g_pin_live[i].first == p) {
+        const auto b = g_pin_live[i];
+        g_pin_live.erase(g_pin_live.begin() + (long)i);
+        if (g_pin_free_bytes + b.second <= kPinPoolBytes) {
+          g_pin_free.push_back(b);
+          g_pin_free_bytes += b.second;
+        } else {
+          (void)hipHostFree(b.first);
+        }
+        return;
+      }
+  } catch (...) {
+  }
+}
 
 int rt_scene_check(const rt_scene* scene) {
   return guarded([&]() -> int {

@@ -13,19 +13,33 @@ namespace {
 
 // image/ppm.rs:73-75: `(value * 255.0).round() as u8` — C round() is half away
 // from zero like f64::round; the `as u8` cast saturates and maps NaN to 0.
+// round(s) for 0 < s < 254.5 without a libm call: the truncating conversion
+// is exact there, and so is s - trunc(s), so `frac >= 0.5` is round's
+// half-away-from-zero rule exactly.
 inline unsigned scale_color_component(double v) {
-  const double s = std::round(v * 255.0);
-  if (!(s > 0.0)) return 0;
-  if (s >= 255.0) return 255;
-  return (unsigned)s;
+  const double s = v * 255.0;
+  if (!(s >= 0.5)) return 0;  // also NaN (as u8: 0) and everything that rounds to <= 0
+  if (s >= 254.5) return 255;
+  const unsigned i = (unsigned)s;
+  return i + (s - (double)i >= 0.5 ? 1u : 0u);
 }
 
-inline int utoa3(unsigned v, char* out) {  // v <= 255
-  if (v >= 100) { out[0] = char('0' + v / 100); out[1] = char('0' + (v / 10) % 10); out[2] = char('0' + v % 10); return 3; }
-  if (v >= 10) { out[0] = char('0' + v / 10); out[1] = char('0' + v % 10); return 2; }
-  out[0] = char('0' + v);
-  return 1;
-}
+// "0".."255" as up to three digit bytes, with the token length in byte 3
+struct DigitTable {
+  uint32_t t[256];
+  DigitTable() {
+    for (unsigned v = 0; v < 256; ++v) {
+      char b[4] = {0, 0, 0, 0};
+      const int n = v >= 100 ? 3 : v >= 10 ? 2 : 1;
+      for (int k = n - 1, x = (int)v; k >= 0; --k, x /= 10) b[k] = char('0' + x % 10);
+      b[3] = (char)n;
+      std::memcpy(&t[v], b, 4);
+    }
+  }
+};
+const DigitTable kDigits;
+
+inline unsigned tok_len(unsigned q) { return kDigits.t[q] >> 24; }
 
 }  // namespace
 
@@ -56,20 +70,29 @@ namespace {
 size_t ppm_row_len(const double* row, uint32_t w) {
   if (w == 0) return 1;
   size_t n = 0;
-  for (size_t k = 0; k < (size_t)3 * w; ++k) {
-    const unsigned q = scale_color_component(row[k]);
-    n += (q >= 100 ? 3 : q >= 10 ? 2 : 1) + 1;
-  }
+  for (size_t k = 0; k < (size_t)3 * w; ++k) n += tok_len(scale_color_component(row[k])) + 1;
   return n;
 }
 
 void ppm_row_write(const double* row, uint32_t w, char* out) {
   char* p = out;
-  for (size_t k = 0; k < (size_t)3 * w; ++k) {
-    p += utoa3(scale_color_component(row[k]), p);
-    *p++ = (k + 1 == (size_t)3 * w) ? '\n' : ' ';
+  const size_t n = (size_t)3 * w;
+  for (size_t k = 0; k + 1 < n; ++k) {
+    // 4-byte store: the digits, then the separator over the length byte (the
+    // row's bytes are exactly its tokens + separators, so this stays inside it)
+    const uint32_t d = kDigits.t[scale_color_component(row[k])];
+    const unsigned len = d >> 24;
+    std::memcpy(p, &d, 4);
+    p[len] = ' ';
+    p += len + 1;
   }
-  if (w == 0) *p++ = '\n';
+  if (n) {  // the last token: byte by byte (the store above could pass the row's end)
+    const uint32_t d = kDigits.t[scale_color_component(row[n - 1])];
+    const unsigned len = d >> 24;
+    for (unsigned k = 0; k < len; ++k) p[k] = (char)(d >> (8 * k));
+    p += len;
+  }
+  *p++ = '\n';
   const size_t len = (size_t)(p - out);
   size_t ls = 0;
   while (ls + 70 < len - 1) {

@@ -199,7 +199,7 @@ struct WfGenBuf {  // grow-only; the fast path allocates rays, colors and parent
 // dependent launches is paid once per batch. Frame f's root rays are slots
 // [f * frame_rays, f * frame_rays + frame_real) of generation 0 (frame_rays
 // padded to whole 64-ray chunks, so a chunk never mixes two cameras).
-constexpr unsigned kMaxFrames = 8;
+constexpr unsigned kMaxFrames = 16;
 struct FrameTable {
   DevCamera cam[kMaxFrames];
   double* out[kMaxFrames];  // device canvases (the shard's rows, row-major)

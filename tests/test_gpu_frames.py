@@ -1,5 +1,5 @@
 """Batches of frames (rt_render_frames_device, DESIGN.md §5.8 "Frame
-batches"): up to 8 cameras share each launch of the generation pipeline.
+batches"): up to 16 cameras share each launch of the generation pipeline.
 Every frame of a batch must equal the same camera's rt_render_shard_device
 frame bit for bit (itself checked against the exhaustive frame and the
 oracle elsewhere), for whole frames and shards, with and without AA, ragged
@@ -40,7 +40,7 @@ def _check(rt, w, cams, depth, row_block, shard, n_shards, aa=1):
         assert torch.equal(b, o), k
 
 
-@pytest.mark.parametrize("n", [2, 8, 11])
+@pytest.mark.parametrize("n", [2, 16, 19])
 def test_frames_whole_bitwise(rt, n):
     from rtamd import scenes
     w, _, depth = scenes.c3(96, 54, n_spheres=400)
