@@ -462,16 +462,25 @@ def main():
     split = None
     if n > 1:
         split = phase_split(a, n, rank, dev, run_frames, fa, F, NB)
-    # Serialized pass (outside the timed region): the same K frames one after the
+    # Serialized pass (outside the timed region): the same K frames in the same
+    # batches (the benched launches: NB frames per launch), one batch after the
     # other on one stream, every launch carrying its own start/stop HIP events
     # (hipExtLaunchKernel), for the roofline's per-launch kernel time and the
-    # per-class table. With frames in flight the timed region overlaps kernels of
-    # different frames, so a launch's duration there includes the CUs it waited
-    # for; here each kernel runs alone, as in the rocprofv3 kernel trace.
+    # per-class table (per frame: a batch's time / NB). With batches in flight the
+    # timed region overlaps kernels of different batches, so a launch's duration
+    # there includes the CUs it waited for; here each kernel runs alone, as in the
+    # rocprofv3 kernel trace.
+    sbufs = [torch.empty_like(shard) for _ in range(NB)] if NB > 1 else [shard]
     rtamd._rtamd._wf_profile(world, 1, False)
-    for _ in range(a.steps):
-        cam.render_shard_device(world, depth, B, srank, sn, shard.data_ptr(), stream.cuda_stream, False)
+    for s0 in range(0, a.steps, NB):
+        nf = min(NB, a.steps - s0)
+        if NB == 1:
+            cam.render_shard_device(world, depth, B, srank, sn, shard.data_ptr(), stream.cuda_stream, False)
+        else:
+            rtamd.render_frames_device(world, [cam] * nf, depth, B, srank, sn, [b.data_ptr() for b in sbufs[:nf]],
+                                       stream.cuda_stream)
     torch.cuda.synchronize()
+    del sbufs
     rtamd._rtamd._wf_profile(world, 0, False)
     # the fast path's own counters (what the kernels executed and traced), one counted
     # frame on the same workspace: the timed and profiled kernels do not count
@@ -531,7 +540,7 @@ def main():
                 "render_streams": kind if F > 1 else "current",
                 "assembler": type(fa).__name__ if n > 1 else None,
             },
-            "roofline": roofline(prof, breakdown, W, H, a, n, ref_work, elapsed / a.steps * 1e3),
+            "roofline": roofline(prof, breakdown, W, H, a, n, ref_work, elapsed / a.steps * 1e3, NB),
             "traced_rays_per_frame": int(traced_rays),
             "traced_mrays_per_s": round(traced_rays * a.steps / elapsed / 1e6, 3),
             "rays_note": "value counts the reference's rays (one per World::intersect call, world.rs:71,101), "
@@ -631,13 +640,14 @@ def pmc_summary_path(a, W, H, n):
     return ""
 
 
-def roofline(prof, breakdown, W, H, a, n, ref_work, frame_ms):
-    """f64 VALU roofline of the dominant kernel (its launches in one frame on
-    rank 0). Its time comes from the launch-carried HIP events of the
-    serialized pass (`prof` = `breakdown`), like the per-class table. With the
-    persistent frame kernel (the default fast path) that kernel is the whole
-    frame: one launch per frame doing every depth's rays, their shadow rays and
-    the combine, so its executed work is every class's."""
+def roofline(prof, breakdown, W, H, a, n, ref_work, frame_ms, nb=1):
+    """f64 VALU roofline of the dominant kernel (its launches per frame on
+    rank 0; with batches, a batch's launches / nb). Its time comes from the
+    launch-carried HIP events of the serialized pass (`prof` = `breakdown`),
+    like the per-class table. With the opt-in persistent frame kernel
+    (knob persist=1) that kernel is the whole frame: one launch per frame
+    doing every depth's rays, their shadow rays and the combine, so its
+    executed work is every class's."""
     nd, ng, npl = prof["n_diag"], prof["n_gen"], prof["n_planes"]
     fused = bool(prof.get("fused"))
     persist = bool(prof.get("persist"))
@@ -682,7 +692,7 @@ def roofline(prof, breakdown, W, H, a, n, ref_work, frame_ms):
         kernels["shadow"]["note"] = "traced inside the fast-path launches (no launch of its own)"
     for c in ("prep", "combine"):
         kernels[c] = {"ms_per_frame": round(breakdown["ms"][c], 4)}
-    ms_src = "serialized pass: launch-carried HIP events, one stream"
+    ms_src = "serialized pass: launch-carried HIP events, one stream, the benched batches"
     if persist:
         dom = "persist"
         kernel_ms = breakdown["ms"]["closest"]  # the one launch per frame (rt_persist.hip ps_render)
@@ -745,8 +755,9 @@ def roofline(prof, breakdown, W, H, a, n, ref_work, frame_ms):
         "traffic": traffic,
         "kernel_ms": round(kernel_ms, 4),
         "kernel_ms_source": ms_src,
-        "kernel_regime": "serialized (one frame at a time); the timed region keeps frames in flight, so its "
-                         "per-frame time (ms_per_step) can be below kernel_ms",
+        "kernel_regime": (f"serialized: one batch of {nb} frames at a time (the benched launches, each carrying "
+                          f"{nb} frames), time per frame = the batch's / {nb}; the timed region keeps several "
+                          "batches in flight, so its per-frame time (ms_per_step) can be below kernel_ms"),
         "ops_per_frame": ops,
         "per_unit": f"{OPS_SPHERE_DIAG} f64 ops per sphere test ({OPS_SPHERE_PRIMARY} for the generation "
                     f"pipeline's primary rays), {OPS_BOX} per BVH box test, {OPS_PLANE} per plane test, "

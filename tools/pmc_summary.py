@@ -4,8 +4,9 @@ Usage: pmc_summary.py OUT.json [--width W --height H --spheres S --n-gpus N
        --dominant CLASS] DIR [DIR ...]
 Each DIR holds one --pmc pass (*_counter_collection.csv). Counters are summed
 over all dispatches of a kernel class and divided by the number of frames
-(= wf_frame_init dispatches, one per rendered frame), i.e. per-FRAME values of
-that class's launches — the same unit as bench.py's roofline.
+(= wf_frame_init dispatches, one per render call, x --batch frames per call),
+i.e. per-FRAME values of that class's launches — the same unit as bench.py's
+roofline.
 
 HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE (KiB) under-reports a
 wide coalesced stream by 2x on gfx950, so hbm_read = 2 * FETCH_SIZE * 1024 is
@@ -50,6 +51,7 @@ ap.add_argument("--n-gpus", type=int, default=1)
 ap.add_argument("--dominant", default="closest")
 ap.add_argument("--traversal", default="bvh", help="bvh (fast path) or exhaustive")
 ap.add_argument("--build", default=None, help="the build the passes profiled (git describe / tag)")
+ap.add_argument("--batch", type=int, default=1, help="frames per render call (rt_render_frames_device)")
 a = ap.parse_args()
 
 tot = collections.defaultdict(lambda: collections.defaultdict(float))
@@ -67,9 +69,9 @@ for d in a.dirs:
                 continue
             tot[c][r["Counter_Name"]] += float(r["Counter_Value"])
         frames[f] = len(seen)
-nf = max(frames.values()) if frames else 0
+nf = (max(frames.values()) if frames else 0) * max(1, a.batch)
 res = {"width": a.width, "height": a.height, "spheres": a.spheres, "n_gpus": a.n_gpus, "traversal": a.traversal,
-       "frames_per_pass": nf, "per_frame": {}, "build": a.build}
+       "frames_per_pass": nf, "batch": max(1, a.batch), "per_frame": {}, "build": a.build}
 for c, cs in tot.items():
     pf = {k: v / max(nf, 1) for k, v in cs.items()}
     if "FETCH_SIZE" in pf or "WRITE_SIZE" in pf:

@@ -2,13 +2,15 @@
 # Profile the bench workload on the GPU box: rocprofv3 kernel-trace stats, then
 # PMC passes (one counter group per run, never combined with sys/runtime
 # traces), summarised per kernel class and per frame by tools/pmc_summary.py.
-# Usage: bash tools/profile.sh TAG [tools/prof_frames.py args]
+# Usage: [BATCH=B] bash tools/profile.sh TAG [tools/prof_frames.py args]
+#        BATCH (default 8): frames per render call, as bench.py renders them
 #        SUMMARY_ARGS="--width 4096 --height 4096 --spheres 9996" for a non-C3 workload.
 # Output: gpurun_out/prof_TAG/ (copy kernel_stats / pmc_summary into profiles/).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 TAG=${1:-r02}; shift
-ARGS="--frames 5 $*"
+BATCH=${BATCH:-8}
+ARGS="--frames $((5 * BATCH)) --batch $BATCH $*"
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -25,7 +27,7 @@ run p3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_L
 run p4 --pmc FETCH_SIZE && \
 run p5 --pmc WRITE_SIZE && \
 run p6 --pmc TCC_HIT_sum TCC_MISS_sum && \
-python tools/pmc_summary.py "$OUT/pmc_summary.json" --dominant "${DOMINANT:-persist}" --traversal "${TRAVERSAL:-bvh}" \
+python tools/pmc_summary.py "$OUT/pmc_summary.json" --dominant "${DOMINANT:-closest}" --batch "$BATCH" --traversal "${TRAVERSAL:-bvh}" \
   --build "$(cat BUILD_ID 2>/dev/null || echo unknown)" \
   $SUMMARY_ARGS "$OUT"/p1 "$OUT"/p2 "$OUT"/p3 "$OUT"/p4 "$OUT"/p5 "$OUT"/p6 > /dev/null && \
   echo "summary ok" | tee -a "$OUT/steps.log"
