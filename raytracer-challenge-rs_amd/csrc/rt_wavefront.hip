@@ -1565,7 +1565,7 @@ hipError_t Wavefront::render_persist(const DevScene& sc, const DevCamera& cam, b
   a.policy = (unsigned)tn.ps_policy;
   if (count) WF_CHECK(hipMemsetAsync(d_cnt_, 0, sizeof(WfCounters), stream));
   if (ms_kernel) WF_CHECK(hipEventRecord(ev0_, stream));
-  if (profiling_) pframes_ += n_frames;  // class times are reported per frame
+  if (profiling_) ++pframes_;
   prof_rays_[0] = prof_rays_[1] = prof_rays_[2] = 0;
   prof_rays_[WF_PRIMARY] = n0;
   const bool quads = sc.n_fx_quads > 0 || sc.n_obvh > 0;
