@@ -23,8 +23,9 @@
 
 namespace rtamd {
 
-constexpr int kWfBlock = 256;      // prep / shadow / combine
+[[maybe_unused]] constexpr int kWfBlock = 256;  // prep / shadow / combine
 
+#ifndef RT_WF_GLOBAL_TU  // (the global-image TU: kernels and their launcher only)
 int wf_tuning_apply(WfTuning& t, const char* key, int value) {
   struct Knob {
     const char* name;
@@ -49,6 +50,7 @@ int wf_tuning_apply(WfTuning& t, const char* key, int value) {
   }
   return 0;
 }
+#endif
 
 #define WF_CHECK(x)                        \
   do {                                     \
@@ -224,6 +226,7 @@ __device__ __forceinline__ void shadow_result(const DevScene& sc, const WfArgs& 
 // this workspace (n_a and n_b 16-B words) and, for a camera frame, write the
 // primary records (wf_prim_prep's computation). One launch instead of two
 // fills and a kernel.
+#ifndef RT_WF_GLOBAL_TU
 // A batch of frames (n_frames > 1) also writes the batch's FrameTable, passed
 // by value (so the host may reuse its copy at once), to the workspace's
 // device copy that the pass's later launches read, and one set of primary
@@ -258,6 +261,7 @@ __global__ void wf_frame_init(DevScene sc, DevCamera cam, PrimRec* prim, unsigne
     prim[jj] = p;  // j >= n_diag: zero padding records
   }
 }
+#endif
 
 // LDS image for the trace kernels: [diag or prim records][gen][planes][metas]
 struct WfLds {
@@ -761,6 +765,7 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
     }
   }
 }
+#ifndef RT_WF_GLOBAL_TU
 __global__ __launch_bounds__(kWfBlock) void wf_prep(DevScene sc, DevCamera cam, WfArgs a) {
   __shared__ unsigned s_pre[kShards + 1];
   const unsigned* pre = shard_prefix(a.in_cnt, s_pre);
@@ -1181,6 +1186,14 @@ static hipError_t launch_shadow_exh(const DevScene& sc, const WfArgs& a, bool ld
   return hipGetLastError();
 }
 
+// the global-memory images' launches live in their own code object (rt_wavefront_glb.o)
+static hipError_t launch_global(int lane, bool quads, bool tally, const DevScene& sc, const DevCamera& cam,
+                                const WfArgs& a, size_t dyn, unsigned n, hipStream_t stream, int block) {
+  const hipError_t e = wf_launch_global(lane, quads, tally, sc, cam, a, dyn, n, stream, block, t_ev_start, t_ev_stop);
+  if (t_ev_start) ++t_ev_used;
+  return e;
+}
+
 // ---- the fast path: one fused launch per generation (image choice: see lane_scene)
 template <bool QUADS, bool TALLY>
 static hipError_t launch_fused_q(const DevScene& sc, const DevCamera& cam, WfArgs a, bool primary, unsigned n,
@@ -1209,10 +1222,10 @@ static hipError_t launch_fused_q(const DevScene& sc, const DevCamera& cam, WfArg
       a.n_top = (unsigned)std::min<size_t>((size_t)sc.n_bvh, (room - dyn) / sizeof(BvhNode));
       dyn += (size_t)a.n_top * sizeof(BvhNode);
     }
-    return launch_lds(wf_trace_fused<false, QUADS, 3, TALLY>, dyn, n, stream, sc, cam, a, tb);
+    return launch_global(3, QUADS, TALLY, sc, cam, a, dyn, n, stream, tb);
   }
   if (dl && dl <= kWfLdsLimit) { a.lds_flags |= kLdsDeltas; dyn = dl; }
-  return launch_lds(wf_trace_fused<false, QUADS, 1, TALLY>, dyn, n, stream, sc, cam, a, tb);
+  return launch_global(1, QUADS, TALLY, sc, cam, a, dyn, n, stream, tb);
 }
 static hipError_t launch_fused(const DevScene& sc, const DevCamera& cam, const WfArgs& a, bool primary, unsigned n,
                                hipStream_t stream, bool tally, const WfTuning& tn) {
@@ -1649,4 +1662,47 @@ hipError_t Wavefront::read_stats(DevStats* out) {
   return hipSuccess;
 }
 
+#else  // RT_WF_GLOBAL_TU
+// The fast path's launches over the global-memory scene images (LANE 3: the
+// treelet and the stack in LDS; LANE 1: the stack in LDS). This TU is the
+// same source compiled a second time with -DRT_WF_GLOBAL_TU and without the
+// AMDGPU register-pressure trackers (Makefile: rt_wavefront_glb.o), which
+// help the LDS image (C3) and cost the global images (C5) ~2 %.
+template <typename K>
+static int occupancy_grid(K kern, int block, size_t lds, unsigned n) {
+  int dev = 0, n_cu = 0, per_cu = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, block, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+  long long want = ((long long)n + block - 1) / block;
+  long long cap = (long long)n_cu * per_cu;
+  long long g = std::min(want, cap);
+  return (int)std::max(g, 1LL);
+}
+template <bool QUADS, int LANE, bool TALLY>
+static hipError_t launch_glb(const DevScene& sc, const DevCamera& cam, const WfArgs& a, size_t dyn, unsigned n,
+                             hipStream_t stream, int block, hipEvent_t e0, hipEvent_t e1) {
+  auto kern = wf_trace_fused<false, QUADS, LANE, TALLY>;
+  if (dyn > 0) WF_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
+  const dim3 grid(occupancy_grid(kern, block, dyn, n));
+  if (e0) hipExtLaunchKernelGGL(kern, grid, dim3(block), dyn, stream, e0, e1, 0, sc, cam, a);
+  else hipLaunchKernelGGL(kern, grid, dim3(block), dyn, stream, sc, cam, a);
+  return hipGetLastError();
+}
+hipError_t wf_launch_global(int lane, bool quads, bool tally, const DevScene& sc, const DevCamera& cam,
+                            const WfArgs& a, size_t dyn, unsigned n, hipStream_t stream, int block, hipEvent_t e0,
+                            hipEvent_t e1) {
+  if (lane == 3) {
+    if (quads) return tally ? launch_glb<true, 3, true>(sc, cam, a, dyn, n, stream, block, e0, e1)
+                            : launch_glb<true, 3, false>(sc, cam, a, dyn, n, stream, block, e0, e1);
+    return tally ? launch_glb<false, 3, true>(sc, cam, a, dyn, n, stream, block, e0, e1)
+                 : launch_glb<false, 3, false>(sc, cam, a, dyn, n, stream, block, e0, e1);
+  }
+  if (lane != 1) return hipErrorInvalidValue;
+  if (quads) return tally ? launch_glb<true, 1, true>(sc, cam, a, dyn, n, stream, block, e0, e1)
+                          : launch_glb<true, 1, false>(sc, cam, a, dyn, n, stream, block, e0, e1);
+  return tally ? launch_glb<false, 1, true>(sc, cam, a, dyn, n, stream, block, e0, e1)
+               : launch_glb<false, 1, false>(sc, cam, a, dyn, n, stream, block, e0, e1);
+}
+#endif  // RT_WF_GLOBAL_TU
 }  // namespace rtamd

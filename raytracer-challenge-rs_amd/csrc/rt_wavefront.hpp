@@ -108,6 +108,15 @@ struct WfTuning {
 // Applies `key` = `value` to `t`: 1 = applied, 0 = not a render-time key, -1 = bad value.
 int wf_tuning_apply(WfTuning& t, const char* key, int value);
 
+// The fast path's launch over a global-memory scene image (lane 3 or 1) of
+// one generation: compiled into its own code object (rt_wavefront.hip built
+// with -DRT_WF_GLOBAL_TU). e0/e1: launch-carried profiling events, or null.
+struct DevCamera;
+struct WfArgs;
+hipError_t wf_launch_global(int lane, bool quads, bool tally, const DevScene& sc, const DevCamera& cam,
+                            const WfArgs& a, size_t dyn, unsigned n, hipStream_t stream, int block, hipEvent_t e0,
+                            hipEvent_t e1);
+
 // Work counters of the trace kernels, one row per wave slot (wave id mod
 // kWorkRows, rows 128 B apart): thousands of waves ending together would
 // otherwise queue on one address (one L2 atomic at a time), which cost the
