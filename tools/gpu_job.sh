@@ -46,7 +46,7 @@ for s in "$@"; do
     trace_c5) step trace_c5 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace_c5" -o trace_c5 --output-format csv -- \
              python bench.py --config c5 --steps 3 --warmup 1 --no-cpu-baseline --no-end-to-end || exit 1 ;;
     pmc) step pmc 900 bash tools/profile.sh "$TAG" || exit 1 ;;
-    pmc_c5) BATCH=1 SUMMARY_ARGS="--width 4096 --height 4096 --spheres 9996" step pmc_c5 900 bash tools/profile.sh "${TAG}_c5" --config c5 || exit 1 ;;
+    pmc_c5) BATCH=1 SUMMARY_ARGS="--width 4096 --height 4096 --spheres 9996" step pmc_c5 900 bash tools/profile.sh "${TAG}_c5" --config c5 --width 4096 --height 4096 --spheres 9996 || exit 1 ;;
     quick) step quick 600 python tools/quick_time.py || exit 1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
