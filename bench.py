@@ -453,6 +453,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    # every asynchronous frame's device-side check (rt_scene_check): a frame left
+    # incomplete raises here instead of passing unnoticed
+    world.check()
     # Parity of the timed frames (outside the timed region): the last frame each
     # rank rendered, and rank 0's assembled canvas, must equal the exhaustive frame
     # bit for bit (camera.rs:133-148 renders every pixel with the every-shape loop).
