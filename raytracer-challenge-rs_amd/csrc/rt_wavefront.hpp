@@ -91,7 +91,7 @@ enum WfFlags : unsigned { WF_EXHAUSTIVE = 1u, WF_COUNT = 2u };
 struct WfTuning {
   int accel = 1;           // 1 = exact-culling BVH fast path (unless the exhaustive loop is asked for)
   int persist = 0;         // 1 = the persistent frame kernel (rt_persist.hip) when max_depth <= kPsMaxDepth
-                           //     (opt-in: measured ~2x slower than the generation pipeline, DESIGN.md §5.7)
+                           //     (opt-in: measured ~2x slower than the generation pipeline, DESIGN.md §5.8)
   int skip_shadow = 1;     // 1 = the fast path leaves out shadow rays that cannot change the colour
   int shadow_lb = 1;       // 1 = shadow rays through the light buffer when the scene has one
   int image = 0;           // 0 = automatic scene image of the fast-path kernels, 3 / 1 = global memory
