@@ -226,7 +226,8 @@ int rt_render_shard_device_ex(const rt_scene* scene, const rt_camera_desc* camer
  * over the same world: frame f's shard (as rt_render_shard_device) goes to the
  * DEVICE buffer d_out_rgb[f]. Each frame equals its rt_render_shard_device
  * render bit for bit; the frames are rendered together, up to 16 per pass of
- * the pipeline (one launch per recursion generation carries all of them), so
+ * the pipeline and at most 2^25 root rays (pixels x aa_samples) per pass (one
+ * launch per recursion generation carries all of them), so
  * small frames and shards pay the per-pass cost once. Asynchronous on
  * `stream` unless `stats` is non-NULL: then the frames are rendered one by
  * one and the counters summed over them. Deferred errors as

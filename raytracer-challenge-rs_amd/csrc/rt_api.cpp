@@ -1045,8 +1045,7 @@ int rt_render_frames_device(const rt_scene* scene, const rt_camera_desc* cameras
   const uint32_t rows = rt_shard_rows(cameras[0].vsize, row_block, shard, n_shards);
   const uint64_t per = (uint64_t)rows * cameras[0].hsize * aa_samples;
   const uint64_t padded = (per + 63) & ~(uint64_t)63;
-  if (padded * std::min<uint32_t>(n_frames, kMaxFrames) >= (1ull << 31))
-    return fail(RT_ERR_INVALID_ARGUMENT, "batch too large");
+  if (padded >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "shard too large");
   hipStream_t st = (hipStream_t)stream;
   // one pass of the generation pipeline per group of kMaxFrames frames; a
   // render that cannot batch (counted, or a scene without the fast path's
@@ -1054,8 +1053,11 @@ int rt_render_frames_device(const rt_scene* scene, const rt_camera_desc* cameras
   const bool batch = !stats && s->tune.accel != 0 && (s->dev.n_bvh > 0 || s->dev.n_obvh > 0) && per > 0;
   DevStats sum{};
   float ms_sum = 0.f;
+  // a pass holds at most ~2^25 root rays (16 C3 frames; 2 C5 frames), which bounds the
+  // workspace's queues; larger frames gain nothing from sharing launches
+  const uint32_t per_pass = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kMaxFrames, ((uint64_t)1 << 25) / std::max<uint64_t>(padded, 1)));
   for (uint32_t f0 = 0; f0 < n_frames;) {
-    const uint32_t nf = batch ? std::min<uint32_t>(kMaxFrames, n_frames - f0) : 1u;
+    const uint32_t nf = batch ? std::min<uint32_t>(per_pass, n_frames - f0) : 1u;
     FrameTable tab{};
     for (uint32_t f = 0; f < nf; ++f) {
       tab.cam[f] = to_dev_camera(cameras[f0 + f]);

@@ -121,3 +121,11 @@ def test_frames_errors(rt):
     with pytest.raises(rt.RtError):
         rt.render_frames_device(w, [rt.Camera(16, 16, 1.0)], depth, 8, 0, 1, [b.data_ptr()], 0, False, 3)
     rt.render_frames_device(w, [], depth, 8, 0, 1, [])  # nothing to render
+
+
+def test_frames_pass_cap(rt):
+    """A pass holds at most 2^25 root rays: 1024x1024 frames at AA 16 (2^24 root
+    rays each) go two per pass, so 3 frames make a pass of 2 and a pass of 1."""
+    from rtamd import scenes
+    w, _, depth = scenes.c3(1024, 1024, n_spheres=200)
+    _check(rt, w, _cameras(rt, 3, 1024, 1024), depth, 8, 0, 1, aa=16)
