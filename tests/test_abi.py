@@ -95,3 +95,45 @@ def test_no_cpu_fallback_without_gpu(rt):
     c = rt.Camera(11, 11, 1.0)
     with pytest.raises(rt.RtError, match="no HIP device"):
         c.render(w)
+
+
+def _host_buffer_lib():
+    lib = ctypes.CDLL(LIB)
+    lib.rt_host_buffer_alloc.restype = ctypes.c_void_p
+    lib.rt_host_buffer_alloc.argtypes = [ctypes.c_size_t]
+    lib.rt_host_buffer_free.argtypes = [ctypes.c_void_p]
+    lib.rt_last_error.restype = ctypes.c_char_p
+    return lib
+
+
+def test_host_buffer_errors_without_crossing_the_abi():
+    """rt_host_buffer_alloc reports failure as NULL + rt_last_error (zero bytes;
+    no device here); rt_host_buffer_free(NULL) and of a foreign pointer are no-ops."""
+    lib = _host_buffer_lib()
+    assert lib.rt_host_buffer_alloc(0) is None
+    assert b"zero bytes" in lib.rt_last_error()
+    lib.rt_host_buffer_free(None)
+    buf = ctypes.create_string_buffer(64)
+    lib.rt_host_buffer_free(ctypes.addressof(buf))  # not a pool block: ignored
+
+
+@pytest.mark.gpu
+def test_host_buffer_pool_reuse_and_render():
+    """Pinned blocks are pooled: a released block comes back for a request of
+    about its size; a render canvas in pooled pinned memory equals the device frame."""
+    from rtamd import scenes
+    lib = _host_buffer_lib()
+    p = lib.rt_host_buffer_alloc(8 << 20)
+    assert p
+    lib.rt_host_buffer_free(p)
+    q = lib.rt_host_buffer_alloc((8 << 20) - 4096)
+    assert q == p
+    lib.rt_host_buffer_free(q)
+    # a >= 4 MB render canvas takes pooled pinned pixels, written by DMA (rt_api.cpp copy_to_host)
+    import torch
+    w, cam, depth = scenes.c3(1024, 768, n_spheres=300)
+    a, _ = cam.render(w, depth, want_stats=False)
+    d = torch.empty((768, 1024, 3), dtype=torch.float64, device="cuda")
+    cam.render_shard_device(w, depth, 8, 0, 1, d.data_ptr(), 0, False)
+    torch.cuda.synchronize()
+    assert a.to_numpy().tobytes() == d.cpu().numpy().tobytes()
