@@ -84,22 +84,35 @@ __device__ __forceinline__ unsigned wave_append(unsigned* counter, bool want, un
 // Queue appends without block barriers or hot counters (DESIGN.md "Sharded
 // queues"). The queues of a generation are split into kShards regions of a
 // fixed capacity; wave-iteration q (rays 64q .. 64q+63 of the generation)
-// appends to region (q / kShardGroup) mod kShards with one atomic per queue,
-// on that region's own counter (128 B apart). Groups of kShardGroup adjacent
-// wave-iterations share a region, so neighbouring rays stay neighbours. Every lane of the wave calls it. A lane gets
-// `n_s` consecutive shadow-list slots and one ray slot each for want_r /
-// want_f (returned as absolute slots; ~0u when the region is full, which the
+// appends with one atomic per queue on a region's own counter (128 B apart),
+// and groups of kShardGroup adjacent wave-iterations share a region, so
+// neighbouring rays stay neighbours. Every lane of the wave calls it. A lane
+// gets `n_s` consecutive parent-list (shadow-list) slots and one ray slot each
+// for want_r / want_f (absolute slots; ~0u when a region is full, which the
 // capacities rule out).
+//
+// The parent list: region (q / kShardGroup) mod kShards.
+// The next generation's rays are sorted into four classes so that its waves
+// hold rays of one class each (coherent traversal and shading):
+//   reflected rays, cat_r = 0 / 1, and refracted rays, cat_f = 0 / 1 (the
+//   caller's categories: reflections off planes or not; refractions leaving an
+//   object or entering one).
+// Reflected rays use the first half of the regions, refracted rays the second:
+// region (q / kShardGroup) mod (kShards / 2) of the half. Category 0 fills a
+// region from its front (counter word 0), category 1 from its back (counter
+// word 1, slots cap-1, cap-2, ...). The capacity bound is that of one queue per
+// region: a region takes at most 2 `per` wave-iterations (twice the
+// wave-iterations of a kShards mapping) of at most 64 rays of its kind each
+// (one per lane, whatever the category), i.e. 128 `per` = out_cap, front and
+// back together. The reader sees 2 kShards virtual regions (shard_prefix<true>).
+// C5 58.7 -> 51.3 ms/frame, C3 0.852 -> 0.83 ms (kinds, then categories).
 __device__ __forceinline__ void shard_append(const WfArgs& a, unsigned q, unsigned n_s, bool want_r, bool want_f,
-                                             unsigned& so, unsigned& ro, unsigned& fo) {
+                                             unsigned& so, unsigned& ro, unsigned& fo, bool cat_r, bool cat_f) {
   const unsigned lane = lane_id();
   const unsigned s = (q / kShardGroup) % kShards;
-  // Reflected rays go to the first half of the regions, refracted rays to the second, so
-  // the next generation's waves hold one kind each (C5 58.7 -> 55.8 ms/frame, C3 0.852 ->
-  // 0.840). The capacity bound is unchanged: a region takes twice the wave-iterations,
-  // at most 64 rays of its kind from each (one per lane).
-  const unsigned s_r = (q / kShardGroup) % (kShards / 2), s_f = kShards / 2 + s_r;
-  const unsigned long long mr = __ballot(want_r), mf = __ballot(want_f);
+  const unsigned p_r = (q / kShardGroup) % (kShards / 2), p_f = kShards / 2 + p_r;
+  const unsigned long long mr0 = __ballot(want_r && !cat_r), mr1 = __ballot(want_r && cat_r);
+  const unsigned long long mf0 = __ballot(want_f && !cat_f), mf1 = __ballot(want_f && cat_f);
   const unsigned long long below = (1ull << lane) - 1ull;
   unsigned incl = n_s;
 #pragma unroll
@@ -108,50 +121,80 @@ __device__ __forceinline__ void shard_append(const WfArgs& a, unsigned q, unsign
     if ((int)lane >= off) incl += t;
   }
   const unsigned s_tot = (unsigned)__shfl((int)incl, 63, 64);
-  const unsigned nr = (unsigned)__popcll(mr), nf = (unsigned)__popcll(mf);
-  unsigned sb = 0, rb = 0, fb = 0;
+  unsigned sb = 0, b0 = 0, b1 = 0, b2 = 0, b3 = 0;
   if (lane == 0) {
     if (s_tot) sb = atomicAdd(a.sh_cnt + s * kShardStride, s_tot);
-    if (nr) rb = atomicAdd(a.out_cnt + s_r * kShardStride, nr);
-    if (nf) fb = atomicAdd(a.out_cnt + s_f * kShardStride, nf);
+    if (mr0) b0 = atomicAdd(a.out_cnt + p_r * kShardStride, (unsigned)__popcll(mr0));
+    if (mr1) b1 = atomicAdd(a.out_cnt + p_r * kShardStride + 1, (unsigned)__popcll(mr1));
+    if (mf0) b2 = atomicAdd(a.out_cnt + p_f * kShardStride, (unsigned)__popcll(mf0));
+    if (mf1) b3 = atomicAdd(a.out_cnt + p_f * kShardStride + 1, (unsigned)__popcll(mf1));
   }
   sb = (unsigned)__shfl((int)sb, 0, 64) + (incl - n_s);
-  rb = (unsigned)__shfl((int)rb, 0, 64);
-  fb = (unsigned)__shfl((int)fb, 0, 64);
-  const unsigned r_off = rb + (unsigned)__popcll(mr & below), f_off = fb + (unsigned)__popcll(mf & below);
+  b0 = (unsigned)__shfl((int)b0, 0, 64); b1 = (unsigned)__shfl((int)b1, 0, 64);
+  b2 = (unsigned)__shfl((int)b2, 0, 64); b3 = (unsigned)__shfl((int)b3, 0, 64);
+  const unsigned r_off = cat_r ? b1 + (unsigned)__popcll(mr1 & below) : b0 + (unsigned)__popcll(mr0 & below);
+  const unsigned f_off = cat_f ? b3 + (unsigned)__popcll(mf1 & below) : b2 + (unsigned)__popcll(mf0 & below);
+  const unsigned cap = a.out_cap;
   so = sb + n_s <= a.sh_cap ? s * a.sh_cap + sb : ~0u;
-  ro = r_off < a.out_cap ? s_r * a.out_cap + r_off : ~0u;
-  fo = f_off < a.out_cap ? s_f * a.out_cap + f_off : ~0u;
+  ro = r_off < cap ? p_r * cap + (cat_r ? cap - 1u - r_off : r_off) : ~0u;
+  fo = f_off < cap ? p_f * cap + (cat_f ? cap - 1u - f_off : f_off) : ~0u;
 }
 
-// Block-wide: the exclusive prefix of a generation's kShards region counts
-// into pre[0..kShards] (LDS), or nullptr for a dense generation. Every thread
-// of the block calls it (it synchronises when cnt != nullptr).
+// Block-wide: the exclusive prefix of a queue's region counts into LDS, or
+// nullptr for a dense generation. Every thread of the block calls it (it
+// synchronises when cnt != nullptr).
+// DUAL = false: the parent (shadow) list, kShards regions, pre[0..kShards].
+// DUAL = true: a generation's rays, 2 kShards virtual regions v (shard_append:
+// kind half h = v / kShards, end e = (v / (kShards/2)) % 2, region r =
+// v % (kShards/2) of the half), pre[0..2 kShards]: each class's regions are
+// contiguous in the dense order.
+template <bool DUAL>
 __device__ __forceinline__ const unsigned* shard_prefix(const unsigned* cnt, unsigned* pre) {
   if (!cnt) return nullptr;
   if (threadIdx.x < 64) {
-    const unsigned v = threadIdx.x < kShards ? cnt[threadIdx.x * kShardStride] : 0u;
-    unsigned incl = v;
+    const unsigned l = threadIdx.x;
+    unsigned va = 0, vb = 0;
+    if (DUAL) {
+      auto count = [&](unsigned v) {
+        const unsigned h = v / kShards, e = (v / (kShards / 2)) & 1u, r = v % (kShards / 2);
+        return cnt[(h * (kShards / 2) + r) * kShardStride + e];
+      };
+      va = count(2 * l);
+      vb = count(2 * l + 1);
+    } else {
+      va = l < kShards ? cnt[l * kShardStride] : 0u;
+    }
+    unsigned incl = va + vb;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
       const unsigned t = (unsigned)__shfl_up((int)incl, off, 64);
-      if ((int)threadIdx.x >= off) incl += t;
+      if ((int)l >= off) incl += t;
     }
-    if (threadIdx.x < kShards) pre[threadIdx.x + 1] = incl;
-    if (threadIdx.x == 0) pre[0] = 0;
+    if (DUAL) {
+      pre[2 * l + 1] = incl - vb;
+      pre[2 * l + 2] = incl;
+    } else if (l < kShards) {
+      pre[l + 1] = incl;
+    }
+    if (l == 0) pre[0] = 0;
   }
   __syncthreads();
   return pre;
 }
-// Slot of the j-th entry of a sharded queue (regions of `cap`), j < pre[kShards].
+// Slot of the j-th entry of a sharded queue (regions of `cap`), j < the total.
+template <bool DUAL>
 __device__ __forceinline__ unsigned shard_slot(const unsigned* pre, unsigned cap, unsigned j) {
   if (!pre) return j;
   unsigned lo = 0;
 #pragma unroll
-  for (unsigned step = kShards / 2; step > 0; step >>= 1)
+  for (unsigned step = DUAL ? kShards : kShards / 2; step > 0; step >>= 1)
     if (pre[lo + step] <= j) lo += step;
-  return lo * cap + (j - pre[lo]);
+  const unsigned off = j - pre[lo];
+  if (!DUAL) return lo * cap + off;
+  const unsigned h = lo / kShards, e = (lo / (kShards / 2)) & 1u, r = lo % (kShards / 2);
+  return (h * (kShards / 2) + r) * cap + (e ? cap - 1u - off : off);
 }
+constexpr unsigned kPreRays = 2 * kShards + 1, kPreList = kShards + 1;  // LDS prefix sizes
 
 // The frame of generation-0 slot i of a batch (FrameTable) and the slot
 // within that frame.
@@ -389,11 +432,11 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest(DevScene sc,
   unsigned n_disc = 0;
   WfLds lv{};
   if constexpr (USE_LDS) lv = wf_lds_stage<PRIMARY>(sc, a.prim, lds_raw);
-  __shared__ unsigned s_pre[kShards + 1];
-  const unsigned* pre = shard_prefix(a.in_cnt, s_pre);
+  __shared__ unsigned s_pre[kPreRays];
+  const unsigned* pre = shard_prefix<true>(a.in_cnt, s_pre);
   const unsigned stride = gridDim.x * blockDim.x;
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
-    const unsigned slot = shard_slot(pre, a.in_cap, i);
+    const unsigned slot = shard_slot<true>(pre, a.in_cap, i);
     V3 o, d;
     wf_ray(a, cam, slot, o, d);
     Hit h;
@@ -417,14 +460,14 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow(DevScene sc, 
   unsigned n_disc = 0;
   WfLds lv{};
   if constexpr (USE_LDS) lv = wf_lds_stage<false>(sc, nullptr, lds_raw);
-  __shared__ unsigned s_pre[kShards + 1];
-  const unsigned* pre = shard_prefix(a.sh_cnt, s_pre);
+  __shared__ unsigned s_pre[kPreList];
+  const unsigned* pre = shard_prefix<false>(a.sh_cnt, s_pre);
   const unsigned stride = gridDim.x * blockDim.x;
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n_shadow; i += stride) {
     V3 o, d;
     double dist;
     unsigned slot;
-    shadow_ray(sc, a, shard_slot(pre, a.sh_cap, i), o, d, dist, slot);
+    shadow_ray(sc, a, shard_slot<false>(pre, a.sh_cap, i), o, d, dist, slot);
     Hit h;
     if constexpr (USE_LDS) wf_trace_lds<false, true, QUADS>(sc, lv, o, d, h, n_disc);
     else trace<true>(sc, o, d, h, n_disc);
@@ -433,6 +476,15 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow(DevScene sc, 
   const unsigned long long s = wave_sum(n_disc);
   if (lane_id() == 0 && s) atomicAdd(&work_row(a.cnt)->disc[a.disc_slot], s);
 }
+
+// The classes of a node's children in the next generation's queue (shard_append):
+// a reflection off a plane (a mirror image of the incoming rays: coherent) or
+// off anything else; a refraction leaving an object (the hit was from inside)
+// or entering one.
+__device__ __forceinline__ bool ray_class_r(const DevScene& sc, bool hit, const Comps& c) {
+  return hit && sc.shade[c.obj].kind == 1;  // RT_SHAPE_PLANE
+}
+__device__ __forceinline__ bool ray_class_f(bool hit, const Comps& c) { return hit && c.inside; }
 
 // ---------------------------------------------------------- prep (spawn)
 // prepare_computations (intersection.rs:53-105) of ray i's finished hit `h`
@@ -488,7 +540,8 @@ __device__ __forceinline__ void prep_one(const DevScene& sc, const WfArgs& a, un
     }
   }
   unsigned sbase, rbase, fbase;
-  shard_append(a, i / 64, n_s, want_refl, want_refr, sbase, rbase, fbase);
+  shard_append(a, i / 64, n_s, want_refl, want_refr, sbase, rbase, fbase, ray_class_r(sc, hit, c),
+               ray_class_f(hit, c));
   if (!valid) return;
   WfNode nd;
   nd.obj = -1; nd.child_refl = -1; nd.child_refr = -1; nd.pad = 0; nd.schlick = 0.0;
@@ -609,7 +662,8 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
   }
   const bool parent = want_refl || want_refr;
   unsigned pbase, rbase, fbase;
-  shard_append(a, i / 64, parent ? 1u : 0u, want_refl, want_refr, pbase, rbase, fbase);
+  shard_append(a, i / 64, parent ? 1u : 0u, want_refl, want_refr, pbase, rbase, fbase, ray_class_r(sc, hit, c),
+               ray_class_f(hit, c));
   if (!valid) return;
   t.hits += hit; t.refl += want_refl; t.refr += want_refr;
   double* dst = color_dst(a, cam, slot);
@@ -677,8 +731,8 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
   extern __shared__ __attribute__((aligned(16))) unsigned char lane_dyn[];
   int* stk = LANE == 0 ? stack_lds + (threadIdx.x / 64) * (kBvhMaxDepth + 4) : stack_lds + threadIdx.x;
   const LaneScene ls = lane_scene<LANE>(sc, a.lds_flags, a.n_top, stk, lane_dyn);
-  __shared__ unsigned s_pre[kShards + 1];
-  const unsigned* pre = shard_prefix(a.in_cnt, s_pre);
+  __shared__ unsigned s_pre[kPreRays];
+  const unsigned* pre = shard_prefix<true>(a.in_cnt, s_pre);
   FusedTally t;
   // Work distribution: chunk c = rays [64c, 64c + 64), one wave-iteration.
   // A launch with more chunks than waves hands them out dynamically from the
@@ -720,7 +774,7 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
     const unsigned i = c * 64u + lane_id();
     // a batch's generation 0: the padding slots after each frame's root rays hold no ray
     const bool valid = i < a.n && (a.g != 0 || a.n_frames <= 1 || i % a.frame_rays < a.frame_real);
-    const unsigned slot = valid ? shard_slot(pre, a.in_cap, i) : 0u;
+    const unsigned slot = valid ? shard_slot<true>(pre, a.in_cap, i) : 0u;
     V3 o = v3(0, 0, 0), d = v3(0, 0, 0);
     Hit h;
     hit_init(h);
@@ -774,15 +828,15 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
 }
 #ifndef RT_WF_GLOBAL_TU
 __global__ __launch_bounds__(kWfBlock) void wf_prep(DevScene sc, DevCamera cam, WfArgs a) {
-  __shared__ unsigned s_pre[kShards + 1];
-  const unsigned* pre = shard_prefix(a.in_cnt, s_pre);
+  __shared__ unsigned s_pre[kPreRays];
+  const unsigned* pre = shard_prefix<true>(a.in_cnt, s_pre);
   const unsigned stride = gridDim.x * blockDim.x;
   // every lane of a wave runs the same number of iterations (appends are wave-wide)
   const unsigned n_iter = (a.n + stride - 1) / stride;
   unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
   for (unsigned it = 0; it < n_iter; ++it, i += stride) {
     const bool valid = i < a.n;
-    const unsigned slot = valid ? shard_slot(pre, a.in_cap, i) : 0u;
+    const unsigned slot = valid ? shard_slot<true>(pre, a.in_cap, i) : 0u;
     V3 o = v3(0, 0, 0), d = v3(0, 0, 0);
     Hit h;
     h.key = -1;
@@ -812,7 +866,7 @@ __device__ __forceinline__ void check_counts_wave(const unsigned* shard_base, co
     const unsigned* q = shard_base + ((size_t)g * 2 + 1) * kShards * kShardStride;
     unsigned nr = 0, ns = 0;
     for (int k = 0; k < kShards; ++k) {
-      nr += r[k * kShardStride];
+      nr += r[k * kShardStride] + r[k * kShardStride + 1];  // front + back (shard_append)
       ns += q[k * kShardStride];
     }
     const bool bad = (g >= 1 && nr != c.rays[g]) || (g < c.n_gen && ns != c.shadows[g]);
@@ -825,10 +879,10 @@ __device__ __forceinline__ void check_counts_wave(const unsigned* shard_base, co
 __global__ __launch_bounds__(kWfBlock) void wf_combine(DevScene sc, DevCamera cam, WfArgs a) {
   const unsigned stride = gridDim.x * blockDim.x;
   const unsigned L = (unsigned)sc.n_lights;
-  __shared__ unsigned s_pre[kShards + 1];
-  const unsigned* pre = shard_prefix(a.in_cnt, s_pre);
+  __shared__ unsigned s_pre[kPreRays];
+  const unsigned* pre = shard_prefix<true>(a.in_cnt, s_pre);
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
-    const unsigned slot = shard_slot(pre, a.in_cap, i);
+    const unsigned slot = shard_slot<true>(pre, a.in_cap, i);
     const WfNode nd = a.nodes[slot];
     V3 color = v3(0.0, 0.0, 0.0);
     if (nd.obj >= 0) {
@@ -876,10 +930,10 @@ __global__ __launch_bounds__(kWfBlock) void wf_combine_parents(DevScene sc, DevC
   // (wf_check_counts): every trace launch of the frame precedes it
   if (fault && blockIdx.x == 0 && threadIdx.x < 64) check_counts_wave(shard_base, ck, fault);
   const unsigned stride = gridDim.x * blockDim.x;
-  __shared__ unsigned s_pre[kShards + 1];
-  const unsigned* pre = shard_prefix(a.sh_cnt, s_pre);
+  __shared__ unsigned s_pre[kPreList];
+  const unsigned* pre = shard_prefix<false>(a.sh_cnt, s_pre);
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
-    const ParentRec p = a.parents[shard_slot(pre, a.sh_cap, i)];
+    const ParentRec p = a.parents[shard_slot<false>(pre, a.sh_cap, i)];
     const ShadeRec& m = sc.shade[p.obj];
     V3 refl = v3(0.0, 0.0, 0.0), refr = v3(0.0, 0.0, 0.0);
     if (p.child_refl >= 0) {
@@ -924,10 +978,10 @@ __global__ __launch_bounds__(kWfBlock) void wf_average(WfArgs a, unsigned hsize,
 __global__ void wf_count_kinds(WfArgs a) {
   unsigned nrefl = 0, nrefr = 0, nhit = 0;
   const unsigned stride = gridDim.x * blockDim.x;
-  __shared__ unsigned s_pre[kShards + 1];
-  const unsigned* pre = shard_prefix(a.in_cnt, s_pre);
+  __shared__ unsigned s_pre[kPreRays];
+  const unsigned* pre = shard_prefix<true>(a.in_cnt, s_pre);
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
-    const WfNode nd = a.nodes[shard_slot(pre, a.in_cap, i)];
+    const WfNode nd = a.nodes[shard_slot<true>(pre, a.in_cap, i)];
     nrefl += nd.child_refl >= 0;
     nrefr += nd.child_refr >= 0;
     nhit += nd.obj >= 0;  // shade_hit runs: one is_shadowed per light (world.rs:41-56)
@@ -1398,7 +1452,7 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
       WF_CHECK(hipStreamSynchronize(stream));
       unsigned nr = 0, ns = 0;
       for (int k = 0; k < kShards; ++k) {
-        nr += hr[(size_t)k * kShardStride];
+        nr += hr[(size_t)k * kShardStride] + hr[(size_t)k * kShardStride + 1];  // front + back (shard_append)
         ns += hs[(size_t)k * kShardStride];
       }
       counts.rays[g + 1] = g < max_depth ? nr : 0;
