@@ -514,6 +514,8 @@ def main():
 
     if rank == 0:
         value = rays_per_frame * a.steps / elapsed / 1e6
+        gather_desc = ("library RCCL communicators on the render streams" if isinstance(fa, RcclStreamAssembler)
+                       else f"torch.distributed {dist.get_backend() if dist.is_initialized() else ''}".strip())
         out = {
             "metric": METRIC if a.config == "c3" else METRIC_C5,
             "value": round(value, 3),
@@ -534,8 +536,8 @@ def main():
                              f"2 lights, reflect+refract depth {depth}"),
                 "width": W, "height": H, "spheres": a.spheres, "depth": depth,
                 "rays_per_frame": int(rays_per_frame),
-                "parallelism": (f"{n} GPUs, one process each: interleaved {B}-row blocks, RCCL gather to rank 0"
-                                if n > 1 else "1 GPU: wavefront pipeline") +
+                "parallelism": (f"{n} GPUs, one process each: interleaved {B}-row blocks, one gather per batch to "
+                                f"rank 0 ({gather_desc})" if n > 1 else "1 GPU: wavefront pipeline") +
                                f"; batches of {NB} frames on {F} streams",
                 "frames_in_flight": F * NB,
                 "batch": NB,
