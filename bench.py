@@ -120,8 +120,8 @@ SURVEY_OPS_SPHERE, SURVEY_OPS_PLANE, SURVEY_OPS_ROOTS = 57, 34, 6
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=30)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=64)  # whole batches of 8 and 16
+    p.add_argument("--warmup", type=int, default=16)
     p.add_argument("--config", default="c3", choices=["c3", "c5"],
                    help="c3: the headline workload (default); c5: 4096x4096, 4 planes + 9996 spheres, 2 lights, "
                         "depth 8 (SURVEY.md §8d C5; sizes below override)")
