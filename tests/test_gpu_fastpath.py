@@ -174,3 +174,39 @@ def test_queue_check_reports_miscalibration(rt, via_check):
     torch.cuda.synchronize()
     w.check()
     assert torch.equal(buf, exact)
+
+
+@pytest.mark.parametrize("glass", [False, True])
+def test_ray_classes_single_class_generations(rt, glass):
+    """Ray classes (shard_append): between two mirror planes every generation
+    is all plane reflections (the back ends of the reflected half's regions fill
+    alone); with glass spheres between them, refractions entering and leaving
+    join. Deep recursion, fast == exhaustive bitwise, counters equal."""
+    import math
+    w = rt.World()
+    floor = rt.Plane()
+    floor.material.reflective = 1.0
+    floor.material.color = rt.Color(0.2, 0.3, 0.4)
+    w.add_object(floor)
+    ceil = rt.Plane()
+    ceil.set_transform(rt.translation(0, 4, 0))
+    ceil.material.reflective = 0.9
+    w.add_object(ceil)
+    rng = np.random.default_rng(3)
+    for k in range(40 if glass else 0):
+        s = rt.glass_sphere()
+        r = rng.uniform(0.2, 0.6)
+        s.set_transform(rt.translation(*rng.uniform([-6, r, -2], [6, 4 - r, 12])) * rt.scaling(r, r, r))
+        s.material.refractive_index = 1.2 + 0.01 * k
+        s.material.reflective = 0.5
+        w.add_object(s)
+    w.add_light(rt.PointLight(rt.Point(-5, 3.5, -5), rt.Color(1, 1, 1)))
+    cam = rt.Camera(160, 120, math.pi / 2.5)
+    cam.set_transform(rt.view_transform(rt.Point(0, 2, -6), rt.Point(0, 1.2, 4), rt.Vector(0, 1, 0)))
+    exact, se = _device_frame(cam, w, 12, True)
+    fast, sf = _device_frame(cam, w, 12, False)
+    import torch
+    assert torch.equal(fast, exact)
+    for k in RAY_KEYS:
+        assert sf[k] == se[k], k
+    assert sf["rays_reflect"] > 10 * sf["rays_primary"]  # the mirrors keep every ray alive
