@@ -297,20 +297,22 @@ def main():
     if a.exhaustive:
         world.tune("accel", 0)
     W, H, B = cam.hsize, cam.vsize, a.row_block
-    # F frames in flight: frame s renders on stream s % F (the library keeps one
-    # workspace per stream, so the renders overlap on the device).
-    # - 1 GPU: into canvas slot s % F; stream order alone protects a slot.
-    # - N GPUs (default "stream" assembler): each render stream owns a shard slot, a
-    #   gather buffer, a canvas and a process group, and a frame's render, RCCL
-    #   gather and rank 0's un-interleave all queue behind its own stream, so frames
-    #   on different streams never wait on each other (StreamFrameAssembler).
-    # - "main" assembler (dev): gather and un-interleave on the current stream,
-    #   coupled to the render streams by events (FrameAssembler; 0.30 instead of
-    #   0.18 ms per 8-way shard frame, measured with --fake-shard --event-path).
+    # Batches of NB frames (one rt_render_frames_device call: every launch of the
+    # pipeline carries the NB frames) on F streams: batch b renders on
+    # stream b % F (the library keeps one workspace per stream, so the batches overlap
+    # on the device).
+    # - 1 GPU: into canvas slots; stream order alone protects a slot.
+    # - N GPUs (default "rccl" assembler): each render stream owns a batch of shard
+    #   slots, a gather buffer, canvases and an RCCL communicator, and a batch's render,
+    #   its ONE gather and rank 0's un-interleave all queue behind its own stream, so
+    #   batches on different streams never wait on each other (RcclStreamAssembler;
+    #   "stream": the same with torch process groups, StreamFrameAssembler).
+    # - "main" assembler (dev): one frame per call, gather and un-interleave on the
+    #   current stream, coupled to the render streams by events (FrameAssembler).
     # The render streams are plain streams, each on its own hardware queue
     # (GPU_MAX_HW_QUEUES above); CU-masked streams (--stream-kind cumask) also get
     # their own queue, but any cross-stream wait on them costs ~1 ms.
-    # default: 4 frames in flight for C3; one for C5, whose wavefront workspace
+    # default: 4 streams for C3; one for C5, whose wavefront workspace
     # (16.8 M primary rays, depth 8) takes tens of GB per frame
     F = max(1, a.inflight if a.inflight is not None else (4 if a.config == "c3" else 1))
     # (C3: 8 frames per pass on 1-2 GPUs, 16 on the smaller shards of 4+; C5's frame fills the GPU alone)
