@@ -1,5 +1,8 @@
+"""BVH node count and depth of the C3 scene per leaf size, and of C5 (dev
+tool; needs a GPU: the hierarchy is built at upload)."""
 import os, sys
-sys.path[:0] = ['/root/repo', '/root/repo/raytracer-challenge-rs_amd']
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, 'raytracer-challenge-rs_amd')]
 import torch, rtamd
 from rtamd import scenes
 for lf in (1, 2, 4, 8):

@@ -1,4 +1,4 @@
-"""Per-kernel counter totals from gpu_prof_quick.sh output (dev tool).
+"""Per-kernel counter totals of a tools/profile.sh output directory (dev tool).
 Usage: pmc_peek.py DIR [kernel-substring]"""
 import csv, glob, os, sys, collections
 d = sys.argv[1]
