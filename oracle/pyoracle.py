@@ -61,6 +61,9 @@ def _load():
     lib.oracle_render_rows.argtypes = [P, ctypes.c_char_p, U, U, ctypes.POINTER(ctypes.c_uint32), U, U, D,
                                        ctypes.POINTER(Stats)]
     lib.oracle_render_rows.restype = I
+    lib.oracle_render_pixels.argtypes = [P, ctypes.c_char_p, U, U, ctypes.POINTER(ctypes.c_uint32), U, U, D,
+                                         ctypes.POINTER(Stats)]
+    lib.oracle_render_pixels.restype = I
     lib.oracle_canvas_to_ppm.argtypes = [D, U, U, ctypes.c_char_p, S]
     lib.oracle_canvas_to_ppm.restype = S
     lib.oracle_nan_seen.restype = I
@@ -155,6 +158,19 @@ class OracleWorld:
                                  nthreads, _dptr(out), ctypes.byref(st))
         if rc != 0:
             raise ValueError(f"oracle_render_rows rc={rc}")
+        return out, st.as_dict()
+
+    def render_pixels(self, camera_desc, max_depth, xy, nthreads=1, aa_samples=1):
+        """Render the pixels xy = [(x, y), ...] with the reference algorithm
+        (as render_rows). Returns (rgb[len(xy), 3], stats)."""
+        pix = np.ascontiguousarray(np.asarray(xy, dtype=np.uint32).reshape(-1, 2))
+        out = np.zeros((len(pix), 3))
+        st = Stats()
+        rc = lib().oracle_render_pixels(self._w, camera_desc, max_depth, aa_samples,
+                                   pix.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), len(pix),
+                                   nthreads, _dptr(out), ctypes.byref(st))
+        if rc != 0:
+            raise ValueError(f"oracle_render_pixels rc={rc}")
         return out, st.as_dict()
 
     def render(self, camera_desc, max_depth, nthreads=1, aa_samples=1):

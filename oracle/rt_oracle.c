@@ -1013,27 +1013,37 @@ typedef struct {
   ocamera cam;
   uint32_t max_depth, aa;
   const uint32_t* rows;
-  uint32_t i0, i1; /* indices into the row list */
+  const uint32_t* pix; /* oracle_render_pixels: (x, y) pairs instead of rows */
+  uint32_t i0, i1; /* indices into the row (pixel) list */
   double* out;
   rt_stats st;
 } or_job;
 
+static ot3 or_pixel_color(or_job* j, uint32_t x, uint32_t y) {
+  if (j->aa <= 1) { /* Camera::render (camera.rs:141-143) */
+    oray r = or_ray_for_pixel(&j->cam, x, y);
+    return or_color_at(j->w, &r, j->max_depth, &j->st);
+  }
+  /* render_multithreaded (camera.rs:176-185) + Color::average (color.rs:26-33) */
+  oray rays[16];
+  int n = or_rays_for_pixel(&j->cam, x, y, j->aa, rays);
+  ot3 c = or_t3(0, 0, 0);
+  for (int s = 0; s < n; ++s) c = or_add(c, or_color_at(j->w, &rays[s], j->max_depth, &j->st));
+  return or_scale(c, 1.0 / (double)n);
+}
+
 static void* or_render_worker(void* arg) {
   or_job* j = (or_job*)arg;
   for (uint32_t i = j->i0; i < j->i1; ++i) {
+    if (j->pix) {
+      ot3 c = or_pixel_color(j, j->pix[2 * (size_t)i], j->pix[2 * (size_t)i + 1]);
+      double* px = j->out + (size_t)i * 3;
+      px[0] = c.x; px[1] = c.y; px[2] = c.z;
+      continue;
+    }
     uint32_t y = j->rows[i];
     for (uint32_t x = 0; x < j->cam.hsize; ++x) {
-      ot3 c;
-      if (j->aa <= 1) { /* Camera::render (camera.rs:141-143) */
-        oray r = or_ray_for_pixel(&j->cam, x, y);
-        c = or_color_at(j->w, &r, j->max_depth, &j->st);
-      } else { /* render_multithreaded (camera.rs:176-185) + Color::average (color.rs:26-33) */
-        oray rays[16];
-        int n = or_rays_for_pixel(&j->cam, x, y, j->aa, rays);
-        c = or_t3(0, 0, 0);
-        for (int s = 0; s < n; ++s) c = or_add(c, or_color_at(j->w, &rays[s], j->max_depth, &j->st));
-        c = or_scale(c, 1.0 / (double)n);
-      }
+      ot3 c = or_pixel_color(j, x, y);
       double* px = j->out + ((size_t)i * j->cam.hsize + x) * 3;
       px[0] = c.x; px[1] = c.y; px[2] = c.z;
     }
@@ -1041,9 +1051,28 @@ static void* or_render_worker(void* arg) {
   return NULL;
 }
 
+static int or_render_list(const oworld* w, const rt_camera_desc* cam, uint32_t max_depth, uint32_t aa_samples,
+                          const uint32_t* rows, const uint32_t* pix, uint32_t n_rows, uint32_t nthreads,
+                          double* out_rgb, rt_stats* st);
 int oracle_render_rows(const oworld* w, const rt_camera_desc* cam, uint32_t max_depth,
                        uint32_t aa_samples, const uint32_t* rows, uint32_t n_rows, uint32_t nthreads,
                        double* out_rgb, rt_stats* st) {
+  return or_render_list(w, cam, max_depth, aa_samples, rows, NULL, n_rows, nthreads, out_rgb, st);
+}
+/* Pixels (x, y) = pix[2i], pix[2i + 1] of the frame, each as Camera::render
+   (or render_multithreaded) computes it, into out_rgb[i]; the pixel list is
+   split over the threads in contiguous blocks. Sampling a large frame (C5) at
+   scattered pixels costs a fraction of whole rows. */
+int oracle_render_pixels(const oworld* w, const rt_camera_desc* cam, uint32_t max_depth, uint32_t aa_samples,
+                         const uint32_t* pix, uint32_t n_pix, uint32_t nthreads, double* out_rgb, rt_stats* st) {
+  if (!pix && n_pix) return RT_ERR_INVALID_ARGUMENT;
+  for (uint32_t i = 0; i < n_pix; ++i)
+    if (pix[2 * (size_t)i] >= cam->hsize || pix[2 * (size_t)i + 1] >= cam->vsize) return RT_ERR_INVALID_ARGUMENT;
+  return or_render_list(w, cam, max_depth, aa_samples, NULL, pix, n_pix, nthreads, out_rgb, st);
+}
+static int or_render_list(const oworld* w, const rt_camera_desc* cam, uint32_t max_depth, uint32_t aa_samples,
+                          const uint32_t* rows, const uint32_t* pix, uint32_t n_rows, uint32_t nthreads,
+                          double* out_rgb, rt_stats* st) {
   if (!(aa_samples == 1 || aa_samples == 2 || aa_samples == 4 || aa_samples == 8 || aa_samples == 16))
     return RT_ERR_INVALID_ARGUMENT;
   ocamera c;
@@ -1052,7 +1081,7 @@ int oracle_render_rows(const oworld* w, const rt_camera_desc* cam, uint32_t max_
   c.pixel_size = cam->pixel_size; c.half_width = cam->half_width; c.half_height = cam->half_height;
   c.inverse = om_from(4, 4, cam->inverse);
   uint32_t* own = NULL;
-  if (!rows) {
+  if (!rows && !pix) {
     own = (uint32_t*)malloc(sizeof(uint32_t) * (n_rows ? n_rows : 1));
     for (uint32_t i = 0; i < n_rows; ++i) own[i] = i;
     rows = own;
@@ -1064,6 +1093,7 @@ int oracle_render_rows(const oworld* w, const rt_camera_desc* cam, uint32_t max_
   uint32_t per = n_rows / nthreads; /* camera.rs:157, last block takes the rest :169-172 */
   for (uint32_t t = 0; t < nthreads; ++t) {
     jobs[t].w = w; jobs[t].cam = c; jobs[t].max_depth = max_depth; jobs[t].aa = aa_samples; jobs[t].rows = rows;
+    jobs[t].pix = pix;
     jobs[t].i0 = t * per; jobs[t].i1 = (t == nthreads - 1) ? n_rows : (t + 1) * per;
     jobs[t].out = out_rgb;
     if (nthreads == 1) or_render_worker(&jobs[t]);

@@ -200,6 +200,10 @@ void oracle_hit(const oworld* w, const double ray[6], double out24[24]);
 int oracle_render_rows(const oworld* w, const rt_camera_desc* cam, uint32_t max_depth,
                        uint32_t aa_samples, const uint32_t* rows, uint32_t n_rows,
                        uint32_t nthreads, double* out_rgb, rt_stats* st);
+/* The pixels (pix[2i], pix[2i+1]) = (x, y), each as oracle_render_rows
+ * computes it, into out_rgb (n_pix*3); blocks of the list per thread. */
+int oracle_render_pixels(const oworld* w, const rt_camera_desc* cam, uint32_t max_depth, uint32_t aa_samples,
+                         const uint32_t* pix, uint32_t n_pix, uint32_t nthreads, double* out_rgb, rt_stats* st);
 size_t oracle_canvas_to_ppm(const double* rgb, uint32_t w, uint32_t h, char* out, size_t cap);
 int oracle_nan_seen(void);
 

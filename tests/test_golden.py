@@ -47,6 +47,25 @@ def test_oracle_reproduces_golden(rt, oracle, name):
     assert {k: int(st[k]) for k in e["counters"]} == e["counters"]
 
 
+def test_oracle_pixels_equal_rows(rt, oracle):
+    """oracle_render_pixels (scattered samples of a large frame, used by the
+    full-size GPU tests) computes each pixel exactly as oracle_render_rows,
+    plain and with AA X4; out-of-frame pixels are refused."""
+    import numpy as np
+    from rtamd import scenes
+    w, cam, depth = scenes.c3(96, 54, n_spheres=120)
+    ow = oracle.OracleWorld.from_world(w)
+    rng = np.random.default_rng(7)
+    xy = np.stack([rng.integers(0, 96, 300), rng.integers(0, 54, 300)], 1)
+    for aa in (1, 4):
+        full, fst = ow.render_rows(cam.desc_bytes(), depth, list(range(54)), 4, aa_samples=aa)
+        px, pst = ow.render_pixels(cam.desc_bytes(), depth, xy, 4, aa_samples=aa)
+        assert px.tobytes() == full[xy[:, 1], xy[:, 0]].tobytes()
+        assert pst["rays_primary"] == 300 * aa
+    with pytest.raises(ValueError):
+        ow.render_pixels(cam.desc_bytes(), depth, [(96, 0)], 1)
+
+
 def test_kat11_center_pixel():
     # camera.rs:327-337: pixel (5,5) of the 11x11 default-world render
     canvas, _, _ = _load("kat11")

@@ -5,7 +5,10 @@ bench.py times the fast path (exact-culling BVH, light buffer, shadow rays
 that cannot change a colour left out) on the full 1920x1080 C3 frame and the
 4096x4096 C5 frame. These tests require those frames to equal the
 reference's every-shape loop (RT_RENDER_EXHAUSTIVE) bit for bit, and the fast
-frame to match the oracle on sampled rows (camera.rs:133-148).
+frame to match the oracle (camera.rs:133-148) on sampled rows and scattered
+pixels of the full-size frames: 60 whole rows and 4096 pixels of C3, 2048
+pixels of C5, each within the north-star tolerance and with identical PPM
+bytes.
 """
 import os
 
@@ -45,11 +48,25 @@ def test_c3_full_frame_fast_equals_exhaustive(rt, oracle):
     assert 0 < sf["rays_shadow_traced"] < sf["rays_shadow"]
     assert sf["sphere_tests_executed"] < se["sphere_tests_executed"] / 50
     assert sf["box_tests_executed"] > 0 and se["box_tests_executed"] == 0
-    rows = [3, 262, 540, 811, 1076]
-    ref, _ = oracle.OracleWorld.from_world(w).render_rows(cam.desc_bytes(), depth, rows, NTHREADS)
+    rows = list(range(3, 1080, 18))  # 60 rows, every part of the frame
+    ow = oracle.OracleWorld.from_world(w)
+    ref, _ = ow.render_rows(cam.desc_bytes(), depth, rows, NTHREADS)
     got = fast.cpu().numpy()[rows]
     assert np.abs(got - ref).max() <= TOL
     assert rt.canvas_to_ppm(got) == oracle.canvas_to_ppm(ref)
+    _check_pixels(rt, oracle, ow, cam, depth, fast, 4096, seed=3)
+
+
+def _check_pixels(rt, oracle, ow, cam, depth, frame, n, seed):
+    """n scattered pixels of a full-size device frame against the oracle:
+    within TOL, and the same PPM bytes (one row of n pixels)."""
+    rng = np.random.default_rng(seed)
+    xy = np.stack([rng.integers(0, cam.hsize, n), rng.integers(0, cam.vsize, n)], 1)
+    ref, st = ow.render_pixels(cam.desc_bytes(), depth, xy, NTHREADS)
+    got = frame[xy[:, 1], xy[:, 0]].cpu().numpy()
+    assert st["rays_primary"] == n
+    assert np.abs(got - ref).max() <= TOL
+    assert rt.canvas_to_ppm(got[None]) == oracle.canvas_to_ppm(ref[None])
 
 
 def test_c3_full_frame_frames_in_flight_equal(rt):
@@ -95,8 +112,10 @@ def test_c3_full_frame_aa_and_zoo_fast_equal_exhaustive(rt):
     assert torch.equal(fast, exact)
 
 
-def test_c5_full_frame_fast_equals_exhaustive(rt):
-    """C5 at its full 4096x4096 (4 planes + 9996 spheres, 2 lights, depth 8)."""
+def test_c5_full_frame_fast_equals_exhaustive(rt, oracle):
+    """C5 at its full 4096x4096 (4 planes + 9996 spheres, 2 lights, depth 8):
+    fast == exhaustive bitwise, and 2048 scattered pixels of the fast frame vs
+    the oracle."""
     import torch
     from rtamd import scenes
     w, cam, depth = scenes.c5()
@@ -105,7 +124,9 @@ def test_c5_full_frame_fast_equals_exhaustive(rt):
     assert torch.equal(fast, exact)
     for k in RAY_KEYS:
         assert sf[k] == se[k], k
-    del exact, fast
+    del exact
+    _check_pixels(rt, oracle, oracle.OracleWorld.from_world(w), cam, depth, fast, 2048, seed=5)
+    del fast
     torch.cuda.empty_cache()
 
 
