@@ -617,6 +617,7 @@ __device__ __forceinline__ V3 shade_color(const ShadeRec& m, V3 surface, V3 refl
 
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
 // Streaming loads and stores of the fused kernels: rays, parents and colours
 // are written once and read once by a later launch, so they are marked
 // non-temporal and leave the L2 to the scene (C3 0.947 -> 0.929 ms, C5 60.0

@@ -227,9 +227,11 @@ __device__ __forceinline__ void wf_ray(const WfArgs& a, const DevCamera& cam, un
       ray_for_pixel(cf, x, y, o, d, ofs[0], ofs[1]);
     }
   } else {
-    const WfRay& r = a.rays[i];
-    o = v3(__builtin_nontemporal_load(&r.o[0]), __builtin_nontemporal_load(&r.o[1]), __builtin_nontemporal_load(&r.o[2]));
-    d = v3(__builtin_nontemporal_load(&r.d[0]), __builtin_nontemporal_load(&r.d[1]), __builtin_nontemporal_load(&r.d[2]));
+    const f64x2* r = reinterpret_cast<const f64x2*>(a.rays + i);  // 48 B, 16-B aligned
+    const f64x2 r0 = __builtin_nontemporal_load(r), r1 = __builtin_nontemporal_load(r + 1),
+                r2 = __builtin_nontemporal_load(r + 2);
+    o = v3(r0.x, r0.y, r1.x);
+    d = v3(r1.y, r2.x, r2.y);
   }
 }
 
@@ -564,7 +566,6 @@ __device__ __forceinline__ void prep_one(const DevScene& sc, const WfArgs& a, un
       WfRay r;
       r.o[0] = c.over.x; r.o[1] = c.over.y; r.o[2] = c.over.z;
       r.d[0] = rv.x; r.d[1] = rv.y; r.d[2] = rv.z;
-      r.pad = 0;
       a.next_rays[rbase] = r;
       nd.child_refl = (int)rbase;
     }
@@ -572,7 +573,6 @@ __device__ __forceinline__ void prep_one(const DevScene& sc, const WfArgs& a, un
       WfRay r;
       r.o[0] = c.under.x; r.o[1] = c.under.y; r.o[2] = c.under.z;
       r.d[0] = refr_dir.x; r.d[1] = refr_dir.y; r.d[2] = refr_dir.z;
-      r.pad = 0;
       a.next_rays[fbase] = r;
       nd.child_refr = (int)fbase;
     }
@@ -614,8 +614,10 @@ __device__ __forceinline__ double* color_dst(const WfArgs& a, const DevCamera& c
 }
 
 __device__ __forceinline__ void st_ray(WfRay* p, V3 o, V3 d) {
-  st_d(&p->o[0], o.x); st_d(&p->o[1], o.y); st_d(&p->o[2], o.z);
-  st_d(&p->d[0], d.x); st_d(&p->d[1], d.y); st_d(&p->d[2], d.z);
+  f64x2* q = reinterpret_cast<f64x2*>(p);  // 48 B, 16-B aligned
+  __builtin_nontemporal_store((f64x2){o.x, o.y}, q);
+  __builtin_nontemporal_store((f64x2){o.z, d.x}, q + 1);
+  __builtin_nontemporal_store((f64x2){d.y, d.z}, q + 2);
 }
 
 // Per-lane tallies of a fused trace kernel (summed per wave at the end).

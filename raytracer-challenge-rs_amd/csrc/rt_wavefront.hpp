@@ -48,11 +48,11 @@ constexpr int kShards = 64;
 constexpr int kShardStride = 32;
 constexpr int kShardGroup = 16;  // consecutive wave-iterations sharing a region (one block's worth)
 
-struct WfRay {  // 56 B
+struct alignas(16) WfRay {  // 48 B: three 16-B loads / stores per ray
   double o[3];
   double d[3];
-  int64_t pad;
 };
+static_assert(sizeof(WfRay) == 48, "WfRay is origin + direction only");
 struct WfHit {  // 24 B: nearest hit + containers top-2 (rt_device.hpp Hit)
   double t;
   int32_t key, c1k, c2k, hin;
