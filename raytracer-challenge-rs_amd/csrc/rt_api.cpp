@@ -34,7 +34,8 @@ using namespace rtamd;
 namespace {
 
 thread_local std::string g_err;
-int g_bvh_leaf = 2;     // BVH leaf size at scene creation (tuning knob "bvh_leaf")
+int g_bvh_leaf = 0;     // BVH leaf size at scene creation (tuning knob "bvh_leaf"); 0 = automatic: 2, or 1 when
+                        // the LDS image cannot hold the scene (C5: 1024² frame 4.42 -> 4.31 ms; C3 best at 2)
 int g_bvh_ct = 70;      // SAH node-visit cost in percent of a sphere test (tuning knob "bvh_ct")
 int g_lb_res = 256;     // light-buffer cells per cube-map face edge at scene creation, 0 = none ("lb_res")
 // render-time tuning copied into every scene at its creation (rt_scene::tune)
@@ -517,7 +518,7 @@ int rtamd_tuning_set(const char* key, int value) {
     return RT_OK;
   }
   if (key && std::strcmp(key, "bvh_leaf") == 0) {
-    if (value < 1 || value > kBvhLeafMax) return fail(RT_ERR_INVALID_ARGUMENT, "bvh_leaf must be in [1, 127]");
+    if (value < 0 || value > kBvhLeafMax) return fail(RT_ERR_INVALID_ARGUMENT, "bvh_leaf must be in [0, 127]");
     g_bvh_leaf = value;
     return RT_OK;
   }
@@ -818,7 +819,15 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   // exact-culling hierarchy over the diagonal spheres (reorders `diag`; keys
   // come from `meta`, so the order changes no result)
   int bvh_depth = 0;
-  std::vector<BvhNode> bvh = build_sphere_bvh(diag, g_bvh_leaf, &bvh_depth, g_bvh_ct / 100.0);
+  const int leaf = g_bvh_leaf > 0 ? g_bvh_leaf : 2;
+  std::vector<BvhNode> bvh = build_sphere_bvh(diag, leaf, &bvh_depth, g_bvh_ct / 100.0);
+  if (g_bvh_leaf == 0 && !bvh.empty()) {
+    // a scene whose pair image (stack, nodes, sphere records) does not fit in
+    // LDS is traversed from global memory, where single-sphere leaves win
+    const size_t image = (size_t)(bvh_depth + 1) * kFusedBlockThreads * 4 + bvh.size() * sizeof(BvhNode) +
+                         diag.size() * sizeof(SphereDiag);
+    if (image > kFusedLdsLimit) bvh = build_sphere_bvh(diag, 1, &bvh_depth, g_bvh_ct / 100.0);
+  }
   const std::vector<BvhPair> bvh_pair = pair_layout(bvh);
   // ... and over the other bounded records (general spheres, cubes, cylinders
   // with finite caps); the rest stays exhaustive on the fast path too
@@ -839,7 +848,7 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
     else fx_quads.push_back(q);
   }
   int obvh_depth = 0;
-  std::vector<BvhNode> obvh = build_other_bvh(orec, g_bvh_leaf, &obvh_depth, g_bvh_ct / 100.0);
+  std::vector<BvhNode> obvh = build_other_bvh(orec, leaf, &obvh_depth, g_bvh_ct / 100.0);
   if (obvh.empty()) {  // (only when there are no records, or more than the leaf codes can index)
     for (const OtherRec& r : orec) {
       if (r.kind == 0) {

@@ -38,6 +38,7 @@ int wf_tuning_apply(WfTuning& t, const char* key, int value) {
       {"image", &WfTuning::image, 0, 3},           {"treelet", &WfTuning::treelet, 0, 1},
       {"treelet_deltas", &WfTuning::treelet_deltas, 0, 1}, {"shadow_stream", &WfTuning::shadow_stream, 0, 2},
       {"adaptive_block", &WfTuning::adaptive_block, 0, 1},
+      {"prim_lane", &WfTuning::prim_lane, 0, 1},
       {"corrupt_calibration", &WfTuning::corrupt_calibration, 0, 1},
       {"ps_trees", &WfTuning::ps_trees, 0, 32},     {"ps_policy", &WfTuning::ps_policy, 0, 1},
       {"ps_grid", &WfTuning::ps_grid, 0, 4096},     {"d2h", &WfTuning::d2h, 0, 1}};
@@ -1178,7 +1179,8 @@ static int occupancy_grid(K kern, int block, size_t lds, unsigned n) {
   return (int)std::max(g, 1LL);
 }
 
-static constexpr size_t kWfLdsLimit = 160 * 1024 - 1024;
+static constexpr size_t kWfLdsLimit = kFusedLdsLimit;
+static_assert(kFusedBlockThreads == kTraceBlock, "rt_api.cpp sizes the pair image with kFusedBlockThreads");
 
 // Threads per block of a trace launch over n rays. A trace block holds one CU
 // (its LDS image), so a launch of fewer than (CUs x kTraceBlock) rays would
@@ -1265,7 +1267,7 @@ static hipError_t launch_fused_q(const DevScene& sc, const DevCamera& cam, WfArg
   const size_t dl = a.use_lb ? delta_lds_bytes(sc) : 0;
   size_t dyn = 0;
   a.lds_flags = 0;
-  if (primary) {
+  if (primary && !(tn.prim_lane && tn.image == 0 && pair_lds_bytes(sc) <= kWfLdsLimit)) {
     const size_t room = kWfLdsLimit - (size_t)(kTraceBlock / 64) * (kBvhMaxDepth + 4) * 4;
     if (sph_lds_bytes(sc) <= room) { a.lds_flags |= kLdsSpheres; dyn += sph_lds_bytes(sc); }
     if (dl && dyn + dl <= room) { a.lds_flags |= kLdsDeltas; dyn += dl; }

@@ -82,6 +82,9 @@ struct PrimRec {  // primary rays share the origin: per diag sphere (s, o', c)
 };
 
 constexpr int kMaxGen = 66;
+// LDS a fused trace launch may take (of the CU's 160 KB)
+constexpr size_t kFusedLdsLimit = 160 * 1024 - 1024;
+constexpr int kFusedBlockThreads = 1024;  // threads of a fused trace block (kTraceBlock, rt_trace.hpp)
 enum WfFlags : unsigned { WF_EXHAUSTIVE = 1u, WF_COUNT = 2u };
 
 // Render-time tuning of a scene (rt_scene::tune, copied from the process
@@ -99,6 +102,8 @@ struct WfTuning {
   int treelet_deltas = 0;  // ... after the light buffer's distances (when they fit)
   int shadow_stream = 1;   // exhaustive pipeline: 1 = shadow traces on a second stream when rendering alone
   int adaptive_block = 0;  // generation pipeline: 1 = small trace launches spread over every CU
+  int prim_lane = 0;       // fast path: 1 = primary rays by the per-lane pair traversal (LDS image) instead
+                           //     of the wave traversal with shared-origin records
   int corrupt_calibration = 0;  // test hook: generation 1 of a calibrated frame launched one ray short
   int ps_trees = 0;        // persistent kernel: tree slots per workgroup (0 = from the memory budget, at most 32)
   int ps_policy = 0;       // persistent kernel: when a wave takes fewer than 64 queued rays (PsArgs::policy)

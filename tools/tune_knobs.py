@@ -29,12 +29,16 @@ res, ref = {}, None
 for r in range(4):
     for combo in combos:
         for (k, _), v in zip(knobs, combo):
-            rtamd._rtamd._tuning_set(k, v)
+            if k in SCENE_KNOBS:
+                rtamd._rtamd._tuning_set(k, v)
         skey = tuple(v for (k, _), v in zip(knobs, combo) if k in SCENE_KNOBS)
         if skey not in worlds:
             worlds[skey] = make_world()[0]
             worlds[skey].upload(0)
         w = worlds[skey]
+        for (k, _), v in zip(knobs, combo):  # render-time knobs are per scene (WfTuning)
+            if k not in SCENE_KNOBS:
+                w.tune(k, v)
         rtamd._rtamd._wf_profile(w, 1, False)
         for _ in range(3):
             cam.render_shard_device(w, depth, 8, 0, 1, buf.data_ptr(), s, False)
