@@ -231,3 +231,28 @@ def test_ray_classes_single_class_generations(rt, glass):
     for k in RAY_KEYS:
         assert sf[k] == se[k], k
     assert sf["rays_reflect"] > 10 * sf["rays_primary"]  # the mirrors keep every ray alive
+
+
+@pytest.mark.parametrize("knob,value", [("prim_lane", 1)])
+def test_fast_path_variants_bitwise(rt, knob, value):
+    """The fast path's measured variants: primary rays by the
+    per-lane pair traversal over the LDS image instead of the wave traversal.
+    Each frame equals the exhaustive frame bit for bit, alone and
+    in a batch of 3 cameras (root rays not a multiple of 64: padded chunks)."""
+    import torch
+    from rtamd import scenes
+    w, cam, depth = scenes.c3(333, 187)
+    exact, _ = _device_frame(cam, w, depth, True)
+    w.tune(knob, value)
+    try:
+        fast, _ = _device_frame(cam, w, depth, False)
+        assert torch.equal(fast, exact)
+        bufs = [torch.full_like(exact, -1.0) for _ in range(3)]
+        rt.render_frames_device(w, [cam] * 3, depth, 8, 0, 1, [b.data_ptr() for b in bufs],
+                                torch.cuda.current_stream().cuda_stream, False, 1)
+        torch.cuda.synchronize()
+        w.check()
+        for b in bufs:
+            assert torch.equal(b, exact)
+    finally:
+        w.tune(knob, 0)
