@@ -83,9 +83,11 @@ if __name__ == "__main__":
     _launch_ranks()
 
 if "--dry-launch" in sys.argv and __name__ == "__main__":  # dev/test: report the rank layout, touch no GPU
-    print(json.dumps({"dry_launch": True, "rank": int(os.environ.get("RANK", "0")),
-                      "world_size": int(os.environ.get("WORLD_SIZE", "1")),
-                      "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}), flush=True)
+    # one write(2) of the whole line: ranks share the stdout pipe, and a write
+    # below PIPE_BUF is atomic, so two ranks' lines never interleave
+    os.write(1, (json.dumps({"dry_launch": True, "rank": int(os.environ.get("RANK", "0")),
+                             "world_size": int(os.environ.get("WORLD_SIZE", "1")),
+                             "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}) + "\n").encode())
     sys.exit(0)
 
 import torch  # noqa: E402  (load torch's HIP runtime first: see rtamd/__init__.py)

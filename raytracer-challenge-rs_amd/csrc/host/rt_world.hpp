@@ -272,8 +272,13 @@ class World {
     }
     return v;
   }
-  // Device-resident flattened world (uploaded on first use).
-  const rt_scene* scene(int device = 0) const {
+  // Device-resident flattened world (uploaded on first use). `device` < 0:
+  // the scene already uploaded, on whatever device it lives (device 0 when
+  // none is); an explicit ordinal re-uploads when the scene lives elsewhere.
+  // Every render / tuning / check path calls scene() without an ordinal, so a
+  // rank that uploaded to its own GPU keeps rendering there.
+  const rt_scene* scene(int device = -1) const {
+    if (device < 0) device = scene_ ? scene_device_ : 0;
     if (!scene_ || scene_device_ != device) {
       const_cast<World*>(this)->drop();
       auto d = descs();
@@ -285,6 +290,11 @@ class World {
     }
     return scene_;
   }
+  int scene_device() const { return scene_ ? scene_device_ : -1; }
+  const void* scene_handle() const { return scene_; }
+  // test hook: relabel the uploaded scene's device without moving it, so a
+  // one-GPU test can check that no render path re-uploads to device 0
+  void debug_relabel_device(int device) { scene_device_ = device; }
   // world.rs:70-81 on the GPU
   Color color_at(const Ray& r, unsigned remaining) const {
     double ray[6] = {r.origin.x, r.origin.y, r.origin.z, r.direction.x, r.direction.y, r.direction.z};

@@ -296,6 +296,9 @@ PYBIND11_MODULE(_rtamd, m) {
       .def("object", &World::object, py::return_value_policy::reference_internal)
       .def("light", &World::light, py::return_value_policy::reference_internal)
       .def("upload", [](const World& w, int device) { w.scene(device); }, py::arg("device") = 0)
+      .def_property_readonly("scene_device", &World::scene_device)  // -1: not uploaded
+      .def("_scene_handle", [](const World& w) { return (uintptr_t)w.scene_handle(); })
+      .def("_debug_relabel_device", &World::debug_relabel_device)
       .def("tune", [](const World& w, const std::string& k, int v) {  // this scene's render-time knob (dev)
         check(rtamd_scene_tuning_set(w.scene(), k.c_str(), v), "tuning");
       })

@@ -20,12 +20,33 @@ def _run(args, env_extra=None):
                           cwd=REPO)
 
 
+def _objects(stdout):
+    """Every JSON object in the stream, wherever the line breaks fall (each rank
+    writes its line with one write(2), but the parser does not rely on it)."""
+    dec = json.JSONDecoder()
+    i, out = 0, []
+    while True:
+        i = stdout.find("{", i)
+        if i < 0:
+            return out
+        try:
+            d, i = dec.raw_decode(stdout, i)
+            out.append(d)
+        except ValueError:
+            i += 1
+
+
 def _ranks(stdout):
     return sorted((d["rank"], d["world_size"], d["local_rank"])
-                  for d in (json.loads(l) for l in stdout.splitlines() if l.startswith("{")) if d.get("dry_launch"))
+                  for d in _objects(stdout) if isinstance(d, dict) and d.get("dry_launch"))
 
 
-@pytest.mark.parametrize("n", [2, 3])
+def test_objects_parser_handles_interleaving():
+    a, b = json.dumps({"dry_launch": True, "rank": 0}), json.dumps({"dry_launch": True, "rank": 1})
+    assert [d["rank"] for d in _objects(a + b + "\nnoise {x\n" + a)] == [0, 1, 0]
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
 def test_gpus_n_spawns_n_ranks(n):
     r = _run(["--gpus", str(n), "--dry-launch"])
     assert r.returncode == 0, r.stderr[-2000:]

@@ -130,7 +130,21 @@ def _batch_done(fa, f, batch, n_frames, c, done):
     assert torch.equal(c, done[-1])
 
 
-def _stream_worker(rank, world_size, port, row_block, n_frames, n_slots, out_path, batch=1):
+def _ref_canvas(kind):
+    """The frame every test frame is derived from: the golden C3 64x36 frame, or
+    ("c3rows") a synthetic canvas of C3's full height, 1080 rows (135 blocks of 8
+    at 8 ranks: 16 for rank 0, 17 for the others, as bench.py's N=8 run), with
+    every row and column distinct."""
+    if kind == "golden":
+        return torch.from_numpy(np.load(os.path.join(HERE, "golden", "c3_64x36_s200.npz"))["canvas"])
+    H, W = 1080, 6
+    y = torch.arange(H, dtype=torch.float64).view(H, 1, 1)
+    x = torch.arange(W, dtype=torch.float64).view(1, W, 1)
+    c = torch.arange(3, dtype=torch.float64).view(1, 1, 3)
+    return y * 1000.0 + x * 10.0 + c / 4.0
+
+
+def _stream_worker(rank, world_size, port, row_block, n_frames, n_slots, out_path, batch=1, kind="golden"):
     """StreamFrameAssembler (bench.py's N>1 path): frame f is golden + f, one
     process group per slot; every submit returns frame f assembled (batch > 1:
     every batch's last submit gathers and assembles the batch)."""
@@ -138,7 +152,7 @@ def _stream_worker(rank, world_size, port, row_block, n_frames, n_slots, out_pat
     dist.init_process_group("gloo", rank=rank, world_size=world_size)
     try:
         from rtamd.distributed import StreamFrameAssembler
-        ref = torch.from_numpy(np.load(os.path.join(HERE, "golden", "c3_64x36_s200.npz"))["canvas"])
+        ref = _ref_canvas(kind)
         H, W = ref.shape[:2]
         groups = [dist.new_group(list(range(world_size))) for _ in range(n_slots)]
         fa = StreamFrameAssembler(H, W, row_block, rank, world_size, torch.device("cpu"), groups=groups,
@@ -235,15 +249,14 @@ class _FakeRccl:
             dist.gather(src, None, dst=0)
 
 
-def _rccl_assembler_worker(rank, world_size, port, fail_at, n_frames, out_path, batch=1):
+def _rccl_assembler_worker(rank, world_size, port, fail_at, n_frames, out_path, batch=1, kind="golden", F=3):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world_size)
     try:
         from rtamd.distributed import RcclStreamAssembler
-        ref = torch.from_numpy(np.load(os.path.join(HERE, "golden", "c3_64x36_s200.npz"))["canvas"])
+        ref = _ref_canvas(kind)
         H, W = ref.shape[:2]
         lib = _FakeRccl(rank, fail_at)
-        F = 3
         if fail_at is not None:
             with pytest.raises(RuntimeError, match="failed on some rank"):
                 RcclStreamAssembler(H, W, 8, rank, world_size, torch.device("cpu"), streams=[None] * F, lib=lib)
@@ -327,3 +340,35 @@ def test_gloo_rccl_stream_assembler_fallback_agreement(tmp_path, fail_at):
     for r in range(2):
         made = int(np.load(out + f".{r}.npy")[0])
         assert made == fail_at[1] + (0 if r == fail_at[0] else 1)
+
+
+# bench.py's N = 8 run (SCALE at 8 GPUs): batches of 16 frames on 4 render
+# streams (bench.py: NB = 16 for n >= 4, F = 4), 8-row blocks of C3's 1080 rows,
+# K = 64 timed frames after the setup batches; here 69 frames, so the last batch
+# is partial (5 frames) and the slots wrap around the 4 streams more than once.
+@pytest.mark.parametrize("world_size", [4, 8])
+def test_gloo_stream_assembler_bench_n8_config(tmp_path, world_size):
+    out = str(tmp_path / "frames.npy")
+    n_frames = 69
+    mp.spawn(_stream_worker, args=(world_size, _free_port(), 8, n_frames, 4, out, 16, "c3rows"),
+             nprocs=world_size, join=True)
+    got = np.load(out)
+    ref = _ref_canvas("c3rows").numpy()
+    assert got.shape == (n_frames,) + ref.shape
+    for f in range(n_frames):
+        assert np.array_equal(got[f], ref + f), f
+
+
+@pytest.mark.parametrize("world_size", [4, 8])
+def test_gloo_rccl_stream_assembler_bench_n8_config(tmp_path, world_size):
+    """The default N>1 assembler (library communicators, faked) in the same
+    configuration: one gather per batch of 16 over communicator (batch mod 4)."""
+    out = str(tmp_path / "frames.npy")
+    n_frames = 69
+    mp.spawn(_rccl_assembler_worker, args=(world_size, _free_port(), None, n_frames, out, 16, "c3rows", 4),
+             nprocs=world_size, join=True)
+    got = np.load(out)
+    ref = _ref_canvas("c3rows").numpy()
+    assert got.shape == (n_frames,) + ref.shape
+    for f in range(n_frames):
+        assert np.array_equal(got[f], ref + f), f

@@ -108,6 +108,31 @@ def test_frames_stats_sum(rt):
         assert st[k] == v, k
 
 
+def test_bindings_keep_the_uploaded_scene(rt):
+    """tune / check / render_frames_device / render must reuse
+    the scene a rank uploaded to its own device and never re-upload it to
+    device 0. The scene is relabelled as if it lived on GPU 5 (one-GPU box);
+    any path that asked for device 0 would drop and recreate it."""
+    import torch
+    from rtamd import scenes
+    w, cam, depth = scenes.c3(32, 18, n_spheres=50)
+    w.upload(0)
+    h = w._scene_handle()
+    w._debug_relabel_device(5)
+    w.tune("skip_shadow", 1)
+    w.check()
+    b = torch.empty((18, 32, 3), dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    rt.render_frames_device(w, [cam, cam], depth, 8, 0, 1, [b.data_ptr(), b.data_ptr()],
+                            torch.cuda.current_stream().cuda_stream)
+    cam.render_shard_device(w, depth, 8, 0, 1, b.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    w.check()
+    cam.render(w, depth, want_stats=False)
+    assert w._scene_handle() == h and w.scene_device == 5
+    w._debug_relabel_device(0)
+
+
 def test_frames_errors(rt):
     import torch
     from rtamd import scenes
