@@ -164,6 +164,8 @@ def parse():
                    help="dev: skip the bitwise check of the last timed frame against the exhaustive frame")
     p.add_argument("--no-end-to-end", action="store_true",
                    help="dev: skip the host-canvas + PPM timing of the drop-in entry point")
+    p.add_argument("--no-distinct", action="store_true", help="dev: skip the orbiting-camera (distinct cameras) run")
+    p.add_argument("--no-cold", action="store_true", help="dev: skip the cold-start (scene create + first render) run")
     p.add_argument("--dry-launch", action="store_true",
                    help="test: each rank prints its RANK/WORLD_SIZE and exits without touching a GPU")
     return p.parse_args()
@@ -244,7 +246,7 @@ def end_to_end(world, cam, depth, frames=3):
     """The drop-in entry point as a caller sees it: `rt_render` (Camera::render,
     camera.rs:133-148: device render + the canvas copied to a host buffer) and
     `rt_canvas_to_ppm` (image/ppm.rs:24-51), per frame, one frame at a time."""
-    cam.render(world, depth, want_stats=False)  # calibrates the scene's own workspace
+    cam.render(world, depth, want_stats=False)  # allocates the scene's own workspace
     t0 = time.perf_counter()
     for _ in range(frames):
         canvas, _ = cam.render(world, depth, want_stats=False)
@@ -266,6 +268,76 @@ def end_to_end(world, cam, depth, frames=3):
                     "frame at a time), rt_canvas_to_ppm on the host, and rt_render_ppm (render + PPM encoded on "
                     "the device + the text copied to the host: canvas_to_ppm(&camera.render(&world)) in one call, "
                     "bytes checked equal); not the headline value"}
+
+
+def distinct_cameras(world, depth, rstreams, dev, headline, frames=64, nb=8):
+    """An animation over the C3 scene: `frames` cameras along an arc
+    (scenes.c3_orbit), each rendered for the first time, in batches of `nb` on
+    the render streams (batch b on stream b % F, as the headline). Nothing is
+    calibrated per camera: every generation of every frame sizes itself on the
+    device. Mrays/s counts each camera's own reference rays (one counted
+    fast-path render per camera, after timing); the frames left in the
+    buffers (the last batch of every stream) are checked bitwise against
+    their exhaustive frames."""
+    cams = [scenes.c3_orbit(k, frames) for k in range(frames)]
+    H, W = cams[0].vsize, cams[0].hsize
+    F = len(rstreams)
+    bufs = [[torch.empty((H, W, 3), dtype=torch.float64, device=dev) for _ in range(nb)] for _ in range(F)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for b in range(frames // nb):
+        rs = rstreams[b % F]
+        rtamd.render_frames_device(world, cams[b * nb:(b + 1) * nb], depth, 8, 0, 1,
+                                   [x.data_ptr() for x in bufs[b % F]], rs.cuda_stream)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    world.check()  # every frame complete (no arena overflow)
+    ok = True
+    ref = torch.empty((H, W, 3), dtype=torch.float64, device=dev)
+    n_batches = frames // nb
+    for b in range(max(0, n_batches - F), n_batches):
+        for j in range(nb):
+            cams[b * nb + j].render_shard_device(world, depth, 8, 0, 1, ref.data_ptr(),
+                                                 torch.cuda.current_stream().cuda_stream, True, exhaustive=True)
+            torch.cuda.synchronize()
+            ok = ok and bool(torch.equal(ref, bufs[b % F][j]))
+    rays = 0
+    for c in cams[:n_batches * nb]:
+        st = c.render_shard_device(world, depth, 8, 0, 1, ref.data_ptr(), torch.cuda.current_stream().cuda_stream,
+                                   True, exhaustive=False)
+        rays += st["rays_primary"] + st["rays_reflect"] + st["rays_refract"] + st["rays_shadow"]
+    del bufs, ref
+    value = rays / dt / 1e6
+    return {"value": round(value, 3), "unit": "Mrays/s", "frames": n_batches * nb, "batch": nb, "streams": F,
+            "ms_per_frame": round(dt / (n_batches * nb) * 1e3, 4), "vs_headline": round(value / headline, 4),
+            "parity": {"vs_exhaustive": "bitwise", "ok": ok, "frames_checked": min(F, n_batches) * nb},
+            "note": "C3 scene, a new camera every frame (scenes.c3_orbit: a 0.8-rad arc around the look-at point), "
+                    "batches of 8 on the render streams, no per-camera calibration or cache; value = the cameras' "
+                    "own reference rays / wall time"}
+
+
+def cold_start(dev_index):
+    """The first call of a new caller: rt_scene_create (flatten, hierarchies,
+    light buffer, upload) and the first rt_render into a host canvas (render +
+    device-to-host copy) of the C3 scene and camera; rt_scene_create of C5.
+    The host World's construction (the caller's own code) is not timed."""
+    w, cam, depth = scenes.c3()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    w.upload(dev_index)
+    t1 = time.perf_counter()
+    canvas, _ = cam.render(w, depth, want_stats=False)
+    t2 = time.perf_counter()
+    del canvas, w
+    w5, _, _ = scenes.c5()
+    t3 = time.perf_counter()
+    w5.upload(dev_index)
+    t4 = time.perf_counter()
+    del w5
+    return {"c3_scene_create_ms": round((t1 - t0) * 1e3, 3), "c3_first_render_ms": round((t2 - t1) * 1e3, 3),
+            "c3_cold_ms": round((t2 - t0) * 1e3, 3), "c5_scene_create_ms": round((t4 - t3) * 1e3, 3),
+            "note": "rt_scene_create + the first rt_render (device render + canvas to host) of a fresh C3 scene "
+                    "and camera; rt_scene_create of C5 (10000 shapes: BVH, light buffer, upload)"}
 
 
 def main():
@@ -429,10 +501,10 @@ def main():
     # loop): 57 per sphere test, 34 per plane test, +6 per disc >= 0 (exact counters)
     ref_work = (SURVEY_OPS_SPHERE * float(counts[4]) + SURVEY_OPS_PLANE * float(counts[5])
                 + SURVEY_OPS_ROOTS * float(counts[6]))
-    # setup: one frame on each render stream sizes and calibrates that stream's
-    # workspace (its first frame reads the queue counts back synchronously), so the
-    # timed region never meets a first frame whatever --warmup is
-    # (with batches: a whole batch, and the timed region's partial batch size, on every stream)
+    # setup: one batch on each render stream allocates that stream's workspace
+    # (queue arenas, counters), so the timed region never meets a first
+    # allocation whatever --warmup is (with batches: a whole batch, and the timed
+    # region's partial batch size, on every stream)
     for _ in range(F):
         step()
     if a.steps % NB:
@@ -561,6 +633,10 @@ def main():
             out["per_rank"] = split
         if n == 1 and not a.no_end_to_end:
             out["end_to_end"] = end_to_end(world, cam, depth)
+        if n == 1 and a.config == "c3" and not a.no_distinct:
+            out["distinct_cameras"] = distinct_cameras(world, depth, rstreams, dev, value)
+        if n == 1 and not a.no_cold:
+            out["cold_ms"] = cold_start(local_rank)
         if n == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(world, cam, depth, a.cpu_seconds)
         print(json.dumps(out), flush=True)
@@ -653,18 +729,11 @@ def roofline(prof, breakdown, W, H, a, n, ref_work, frame_ms, nb=1):
     """f64 VALU roofline of the dominant kernel (its launches per frame on
     rank 0; with batches, a batch's launches / nb). Its time comes from the
     launch-carried HIP events of the serialized pass (`prof` = `breakdown`),
-    like the per-class table. With the opt-in persistent frame kernel
-    (knob persist=1) that kernel is the whole frame: one launch per frame
-    doing every depth's rays, their shadow rays and the combine, so its
-    executed work is every class's."""
+    like the per-class table."""
     nd, ng, npl = prof["n_diag"], prof["n_gen"], prof["n_planes"]
     fused = bool(prof.get("fused"))
-    persist = bool(prof.get("persist"))
-    # the persistent kernel traces root rays per lane like every other ray (28 ops per
-    # diagonal sphere test); the generation pipeline's primary launch uses the
-    # shared-origin records (16)
-    per_sphere = {"primary": OPS_SPHERE_DIAG if persist else OPS_SPHERE_PRIMARY, "closest": OPS_SPHERE_DIAG,
-                  "shadow": OPS_SPHERE_DIAG}
+    # the generation pipeline's primary launch uses the shared-origin records (16 ops per test)
+    per_sphere = {"primary": OPS_SPHERE_PRIMARY, "closest": OPS_SPHERE_DIAG, "shadow": OPS_SPHERE_DIAG}
     sh_in_r, sh_in_t = prof.get("shadow_rays_in", {}), prof.get("shadow_tests_in", {})
 
     def class_ops(c):
@@ -702,29 +771,12 @@ def roofline(prof, breakdown, W, H, a, n, ref_work, frame_ms, nb=1):
     for c in ("prep", "combine"):
         kernels[c] = {"ms_per_frame": round(breakdown["ms"][c], 4)}
     ms_src = "serialized pass: launch-carried HIP events, one stream, the benched batches"
-    if persist:
-        dom = "persist"
-        kernel_ms = breakdown["ms"]["closest"]  # the one launch per frame (rt_persist.hip ps_render)
-        ops = class_ops("primary") + class_ops("closest")
-        survey_ops = class_survey_ops("primary") + class_survey_ops("closest")
-        kernels = {"persist": {"ms_per_frame": round(kernel_ms, 4),
-                               "rays": int(prof["rays"]["primary"] + prof["rays"]["closest"]),
-                               "root_rays": int(prof["rays"]["primary"]), "child_rays": int(prof["rays"]["closest"]),
-                               "sphere_tests": int(prof["tests"]["primary"] + prof["tests"]["closest"]),
-                               "box_tests": int(prof["boxes"]["primary"] + prof["boxes"]["closest"]),
-                               "shadow_rays_inside": int(sh_in_r.get("primary", 0.0) + sh_in_r.get("closest", 0.0)),
-                               "tflops": round(ops / (kernel_ms * 1e-3) / 1e12, 3) if kernel_ms > 0 else None},
-                   "combine": {"ms_per_frame": round(breakdown["ms"]["combine"], 4),
-                               "note": "AA averaging only: shade_hit's combine runs inside ps_render"}}
-        kname = ("ps_render (rt_persist.hip): one launch per frame, every recursion depth's rays with their "
-                 "shading, shadow rays and shade_hit combine")
-    else:
-        dom = max(("primary", "closest", "shadow"), key=lambda c: breakdown["ms"][c])
-        kernel_ms = breakdown["ms"][dom]
-        ops = class_ops(dom)
-        survey_ops = class_survey_ops(dom)
-        kname = (f"wf_trace_fused ({dom} launches: closest hit + shading + shadow rays + spawn) in one frame"
-                 if fused else f"wf_trace_{dom}: its launches in one frame")
+    dom = max(("primary", "closest", "shadow"), key=lambda c: breakdown["ms"][c])
+    kernel_ms = breakdown["ms"][dom]
+    ops = class_ops(dom)
+    survey_ops = class_survey_ops(dom)
+    kname = (f"wf_trace_fused ({dom} launches: closest hit + shading + shadow rays + spawn) in one frame"
+             if fused else f"wf_trace_{dom}: its launches in one frame")
     if kernel_ms <= 0:
         return {"bound": "valu_f64", "kernel": None, "achieved": None, "peak": PEAK_F64_VALU_TFLOPS,
                 "unit": "TFLOP/s", "frac": None, "traffic": None}

@@ -89,6 +89,31 @@ int guarded(F&& body) noexcept {
       return fail(RT_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(_e));      \
   } while (0)
 
+// The caller's current device survives every entry point (SURVEY §8b:
+// callable from any host thread; a multi-device caller's own choice of device
+// must not change under it): an entry point that selects the scene's device
+// holds a DeviceGuard, which restores the previous device on every return.
+struct DeviceGuard {
+  int prev = -1;
+  hipError_t err = hipSuccess;
+  DeviceGuard() {
+    if (hipGetDevice(&prev) != hipSuccess) {
+      prev = -1;
+      (void)hipGetLastError();
+    }
+  }
+  explicit DeviceGuard(int dev) : DeviceGuard() { err = hipSetDevice(dev); }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+#define RT_DEVICE(dev)                                                                             \
+  DeviceGuard _dev_guard(dev);                                                                     \
+  if (_dev_guard.err != hipSuccess)                                                                \
+    return fail(RT_ERR_HIP, std::string("hipSetDevice: ") + hipGetErrorString(_dev_guard.err))
+
 }  // namespace
 
 // rt_last_error's text for entry points in other translation units (rt_ppm.cpp);
@@ -163,6 +188,7 @@ struct rt_scene {
   int prof_mask = (1 << WF_NCLASS) - 1;
   int n_objects = 0, n_lights = 0;
   WfTuning tune;  // this scene's render-time tuning (read under `mu` by every render)
+  WfSizing sizing;  // the fast path's queue arenas, learned from this scene's frames (under `mu`)
   ~rt_scene() {
     for (WfSlot& w : wfs)
       if (w.done) (void)hipEventDestroy(w.done);
@@ -362,32 +388,37 @@ DevCamera to_dev_camera(const rt_camera_desc& c) {
 
 bool valid_aa(uint32_t aa) { return aa == 1 || aa == 2 || aa == 4 || aa == 8 || aa == 16; }
 
-// Launch one render (camera shard or ray batch) on `stream` through the
-// wavefront pipeline. `n_tasks` root rays = pixels x aa (camera) or rays
-// (batch). `stats_out`, when given, receives the exact counters and
-// `ms_out` the kernel time (both synchronise).
-// A workspace whose device-side queue check failed (Wavefront::fault) fails
-// the call that finds it; the check raised it for an earlier, asynchronous
-// frame. The calibration is dropped, so the next frame recalibrates.
+// A workspace whose fast-path frame overflowed its queue arenas (device-sized
+// generations, Wavefront::take_overflow) fails the call that finds it: that
+// earlier, asynchronous frame is incomplete. The arenas are grown past what
+// the frame asked for, so the next frame fits at least that far.
 int check_faults(rt_scene* s) {
-  for (rt_scene::WfSlot& w : s->wfs)
-    if (const int f = w.wf->fault()) {
-      w.wf->clear_fault();
-      if (f == 1)
-        return fail(RT_ERR_HIP, "wavefront queue check: a generation's ray count differed from its calibrated "
-                                "launch size in an earlier frame (rays may be missing from that frame)");
-      std::string d;
-      for (int k = 1; k < 24; ++k) d += (k > 1 ? "," : "") + std::to_string(w.wf->fault_word(k));
-      return fail(RT_ERR_HIP, "persistent frame kernel: a wait exceeded its time bound in an earlier frame (that "
-                              "frame was abandoned incomplete; code " + std::to_string(f) + ": " + d + ")");
-    }
+  for (rt_scene::WfSlot& w : s->wfs) {
+    if (!w.wf->overflowed()) continue;
+    if (w.done) RT_HIP(hipEventSynchronize(w.done));  // its frames have run (the arenas are about to be reallocated)
+    bool was = false;
+    RT_HIP(w.wf->take_overflow(&was));
+    if (was)
+      return fail(RT_ERR_HIP, "wavefront queue arenas overflowed in an earlier asynchronous frame (that frame is "
+                              "incomplete; the arenas have grown: render it again)");
+  }
   return RT_OK;
 }
 
+// Launch one render (camera shard or ray batch) on `stream` through the
+// wavefront pipeline. `n_tasks` root rays = pixels x aa (camera) or rays
+// (batch). `stats_out`, when given, receives the exact counters and
+// `ms_out` the kernel time (both synchronise). `sync`: the caller waits for
+// this render anyway (a host canvas, the counters): the call synchronises,
+// and a frame that overflowed its queue arenas is rendered again, with the
+// arenas grown, until it fits (every synchronous entry point returns a
+// complete frame). Asynchronous renders report an overflow later
+// (check_faults).
 int run_render(rt_scene* s, const DevCamera& cam, const double* d_rays, uint32_t n_tasks, uint32_t aa,
                uint32_t max_depth, uint32_t row_block, uint32_t shard, uint32_t n_shards, double* d_out,
                hipStream_t stream, DevStats* stats_out = nullptr, float* ms_out = nullptr, uint32_t flags = 0,
-               rt_scene::WfSlot** used = nullptr, const FrameTable* batch = nullptr, unsigned n_frames = 1) {
+               rt_scene::WfSlot** used = nullptr, const FrameTable* batch = nullptr, unsigned n_frames = 1,
+               bool sync = false) {
   if (max_depth > (uint32_t)kMaxDepth)
     return fail(RT_ERR_INVALID_ARGUMENT, "max_depth > " + std::to_string(kMaxDepth));
   if (!valid_aa(aa)) return fail(RT_ERR_INVALID_ARGUMENT, "aa_samples must be 1, 2, 4, 8 or 16");
@@ -400,23 +431,27 @@ int run_render(rt_scene* s, const DevCamera& cam, const double* d_rays, uint32_t
     if (used) *used = nullptr;
     return RT_OK;
   }
-  std::string sig;
-  if (!d_rays) {  // camera renders are deterministic per (camera, shard, depth, aa)
-    sig.assign((const char*)&cam, sizeof cam);
-    const uint32_t p[7] = {n_tasks, aa, max_depth, row_block, shard, n_shards, n_frames};
-    sig.append((const char*)p, sizeof p);
-    for (unsigned f = 1; f < n_frames; ++f) sig.append((const char*)&batch->cam[f], sizeof(DevCamera));
-  }
   rt_scene::WfSlot* w = nullptr;
   hipError_t e = s->acquire(stream, &w);
-  const unsigned wf_flags = ((flags & RT_RENDER_EXHAUSTIVE) ? WF_EXHAUSTIVE : 0u) | (used ? WF_COUNT : 0u);
-  if (e == hipSuccess)
-    e = w->wf->render(s->dev, cam, d_rays == nullptr, d_rays, n_tasks, aa, max_depth, row_block, shard, n_shards,
-                      d_out, stream, sig, stats_out, ms_out, s->tune, s->wfs.size() == 1, wf_flags, batch, n_frames);
-  if (e == hipSuccess) e = hipEventRecord(w->done, stream);
   if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("wavefront render: ") + hipGetErrorString(e));
+  const unsigned wf_flags = ((flags & RT_RENDER_EXHAUSTIVE) ? WF_EXHAUSTIVE : 0u) | (used ? WF_COUNT : 0u);
+  sync = sync || stats_out || ms_out;
+  for (int attempt = 0;; ++attempt) {
+    e = w->wf->render(s->dev, cam, d_rays == nullptr, d_rays, n_tasks, aa, max_depth, row_block, shard, n_shards,
+                      d_out, stream, s->sizing, stats_out, ms_out, s->tune, s->wfs.size() == 1, wf_flags, batch,
+                      n_frames);
+    if (e == hipSuccess) e = hipEventRecord(w->done, stream);
+    if (e == hipSuccess && sync) e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("wavefront render: ") + hipGetErrorString(e));
+    if (!sync) break;
+    w->wf->learn(s->sizing);
+    bool over = false;
+    e = w->wf->take_overflow(&over);
+    if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("wavefront arenas: ") + hipGetErrorString(e));
+    if (!over) break;
+    if (attempt >= 24) return fail(RT_ERR_HIP, "wavefront queue arenas: the frame does not fit");
+  }
   if (used) *used = w;
-  if (stats_out || ms_out) return check_faults(s);  // synchronised: this frame's check has run
   return RT_OK;
 }
 
@@ -449,9 +484,8 @@ const char* rt_last_error(void) { return g_err.c_str(); }
 // ms[5] (primary, closest, shadow, prep, combine), rays[3], disc[3],
 // n_diag, n_gen, n_planes, n_lights, n_quads, tests[3], boxes[3], bvh,
 // n_bvh_nodes, bvh_depth, n_obvh_nodes, n_other_culled, lb_res, lb_items, sh_rays[2], sh_tests[2]
-// (shadow rays / sphere tests inside the fused primary / secondary launches), fused, persist,
-// persistent kernel items[2], lanes[2], cycles[6] (counted frames).
-int rtamd_wf_profile(const rt_scene* cs, int enable, double out[45]) {
+// (shadow rays / sphere tests inside the fused primary / secondary launches), fused.
+int rtamd_wf_profile(const rt_scene* cs, int enable, double out[34]) {
   if (!cs) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
   rt_scene* s = const_cast<rt_scene*>(cs);
   std::lock_guard<std::mutex> lk(s->mu);
@@ -462,7 +496,7 @@ int rtamd_wf_profile(const rt_scene* cs, int enable, double out[45]) {
     for (rt_scene::WfSlot& w : s->wfs) w.wf->set_profiling(s->prof_on, s->prof_mask);
   }
   if (out) {
-    RT_HIP(hipSetDevice(s->device));
+    RT_DEVICE(s->device);
     // class times: averaged over every frame profiled on any workspace; the
     // counters: the last frame
     WfProfile p{};
@@ -494,9 +528,6 @@ int rtamd_wf_profile(const rt_scene* cs, int enable, double out[45]) {
     out[28] = s->dev.lb_cells ? s->dev.lb_n_items : 0;
     for (int i = 0; i < 2; ++i) { out[29 + i] = p.sh_rays[i]; out[31 + i] = p.sh_tests[i]; }
     out[33] = p.fused;
-    out[34] = p.persist;
-    for (int i = 0; i < 2; ++i) { out[35 + i] = p.ps_items[i]; out[37 + i] = p.ps_lanes[i]; }
-    for (int i = 0; i < 6; ++i) out[39 + i] = p.ps_cycles[i];
   }
   return RT_OK;
 }
@@ -591,7 +622,7 @@ int rtamd_nccl_comm_init(int nranks, const unsigned char* id, size_t size, int r
   if (!id || !comm || size < sizeof(ncclUniqueId) || nranks < 1 || rank < 0 || rank >= nranks || timeout_ms < 1)
     return fail(RT_ERR_INVALID_ARGUMENT, "bad communicator arguments");
   *comm = nullptr;
-  RT_HIP(hipSetDevice(device));
+  RT_DEVICE(device);
   ncclUniqueId uid;
   std::memcpy(&uid, id, sizeof uid);
   ncclComm_t c = nullptr;
@@ -683,7 +714,7 @@ int rt_scene_check(const rt_scene* scene) {
   if (!scene) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
   rt_scene* s = const_cast<rt_scene*>(scene);
   std::lock_guard<std::mutex> lk(s->mu);
-  RT_HIP(hipSetDevice(s->device));
+  RT_DEVICE(s->device);
   for (rt_scene::WfSlot& w : s->wfs)
     if (w.done) RT_HIP(hipEventSynchronize(w.done));  // the workspace's last render (and its check) has run
   return check_faults(s);
@@ -912,6 +943,11 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
 
   rt_scene* s = new rt_scene();
   s->device = device;
+  // children per ray at most (WfSizing::branch): the exact bound of the arenas
+  int branch = 0;
+  for (size_t i = 0; i < n_shapes; ++i)
+    branch = std::max(branch, (shapes[i].reflective != 0.0 ? 1 : 0) + (shapes[i].transparency != 0.0 ? 1 : 0));
+  s->sizing.branch = branch;
   {
     std::lock_guard<std::mutex> tlk(g_tune_mu);
     s->tune = g_tune_defaults;
@@ -921,6 +957,7 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
     return rc;
   };
   int rc;
+  DeviceGuard restore;  // the caller's device, whatever happens below
   if ((rc = [&]() -> int {
          RT_HIP(hipSetDevice(device));
          RT_HIP(hipMalloc(&s->d_blob, total));
@@ -970,7 +1007,7 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
 
 void rt_scene_destroy(rt_scene* s) {
   if (!s) return;
-  (void)hipSetDevice(s->device);
+  DeviceGuard restore(s->device);
   if (s->stream) (void)hipStreamSynchronize(s->stream);
   s->multi.release();
   (void)hipSetDevice(s->device);
@@ -1013,7 +1050,7 @@ int rt_render_shard_device_ex(const rt_scene* scene, const rt_camera_desc* camer
   rt_scene* s = const_cast<rt_scene*>(scene);
   std::lock_guard<std::mutex> lk(s->mu);
   auto t0 = std::chrono::steady_clock::now();
-  RT_HIP(hipSetDevice(s->device));
+  RT_DEVICE(s->device);
   const uint32_t rows = rt_shard_rows(camera->vsize, row_block, shard, n_shards);
   const uint64_t n_tasks = (uint64_t)rows * camera->hsize * aa_samples;
   if (n_tasks >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "shard too large");
@@ -1050,7 +1087,7 @@ int rt_render_frames_device(const rt_scene* scene, const rt_camera_desc* cameras
   rt_scene* s = const_cast<rt_scene*>(scene);
   std::lock_guard<std::mutex> lk(s->mu);
   auto t0 = std::chrono::steady_clock::now();
-  RT_HIP(hipSetDevice(s->device));
+  RT_DEVICE(s->device);
   const uint32_t rows = rt_shard_rows(cameras[0].vsize, row_block, shard, n_shards);
   const uint64_t per = (uint64_t)rows * cameras[0].hsize * aa_samples;
   const uint64_t padded = (per + 63) & ~(uint64_t)63;
@@ -1112,7 +1149,7 @@ int rt_render_ex(const rt_scene* scene, const rt_camera_desc* camera, uint32_t m
   rt_scene* s = const_cast<rt_scene*>(scene);
   std::lock_guard<std::mutex> lk(s->mu);
   auto t0 = std::chrono::steady_clock::now();
-  RT_HIP(hipSetDevice(s->device));
+  RT_DEVICE(s->device);
   const uint64_t n_pix = (uint64_t)camera->hsize * camera->vsize;
   if (n_pix * aa_samples >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "canvas too large for one launch");
   int rc = ensure_dev_buffer(&s->d_out, &s->out_cap, n_pix * 3);
@@ -1141,7 +1178,7 @@ int rt_render_ppm(const rt_scene* scene, const rt_camera_desc* camera, uint32_t 
   rt_scene* s = const_cast<rt_scene*>(scene);
   std::lock_guard<std::mutex> lk(s->mu);
   auto t0 = std::chrono::steady_clock::now();
-  RT_HIP(hipSetDevice(s->device));
+  RT_DEVICE(s->device);
   const uint32_t W = camera->hsize, H = camera->vsize;
   const uint64_t n_pix = (uint64_t)W * H;
   if (n_pix * aa_samples >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "canvas too large for one launch");
@@ -1167,7 +1204,7 @@ int rt_render_ppm(const rt_scene* scene, const rt_camera_desc* camera, uint32_t 
   DevStats ds{};
   float ms = 0.f;
   rc = run_render(s, to_dev_camera(*camera), nullptr, (uint32_t)(n_pix * aa_samples), aa_samples, max_depth, H, 0,
-                  1, s->d_out, s->stream, stats ? &ds : nullptr, stats ? &ms : nullptr, 0);
+                  1, s->d_out, s->stream, stats ? &ds : nullptr, stats ? &ms : nullptr, 0, nullptr, nullptr, 1, true);
   if (rc != RT_OK) return rc;
   RT_HIP(ppm_encode_device(s->d_out, W, H, s->d_ppm, s->ppm_cap, (unsigned*)s->d_ppm_rows, d_off, hd, s->stream));
   unsigned long long body = 0;
@@ -1236,7 +1273,7 @@ int rt_color_at_batch_ex(const rt_scene* scene, const double* rays, size_t n, ui
   rt_scene* s = const_cast<rt_scene*>(scene);
   std::lock_guard<std::mutex> lk(s->mu);
   auto t0 = std::chrono::steady_clock::now();
-  RT_HIP(hipSetDevice(s->device));
+  RT_DEVICE(s->device);
   int rc = ensure_dev_buffer(&s->d_in, &s->in_cap, n * 6);
   if (rc != RT_OK) return rc;
   rc = ensure_dev_buffer(&s->d_out, &s->out_cap, n * 3);
@@ -1264,7 +1301,7 @@ int rt_is_shadowed_batch(const rt_scene* scene, const double* points, size_t n, 
   if ((int)light >= s->n_lights) return fail(RT_ERR_INVALID_ARGUMENT, "light index out of range");
   if (n >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "batch too large");
   std::lock_guard<std::mutex> lk(s->mu);
-  RT_HIP(hipSetDevice(s->device));
+  RT_DEVICE(s->device);
   if (n == 0) return RT_OK;
   int rc = ensure_dev_buffer(&s->d_in, &s->in_cap, n * 3);
   if (rc != RT_OK) return rc;
@@ -1284,7 +1321,7 @@ int rt_hit_batch(const rt_scene* scene, const double* rays, size_t n, double* ou
   if (n >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "batch too large");
   rt_scene* s = const_cast<rt_scene*>(scene);
   std::lock_guard<std::mutex> lk(s->mu);
-  RT_HIP(hipSetDevice(s->device));
+  RT_DEVICE(s->device);
   if (n == 0) return RT_OK;
   int rc = ensure_dev_buffer(&s->d_in, &s->in_cap, n * 6);
   if (rc != RT_OK) return rc;
@@ -1314,6 +1351,7 @@ int rt_render_multi(rt_scene* const* scenes, int n_devices, const rt_camera_desc
     if (!scenes[i] || scenes[i]->device != i)
       return fail(RT_ERR_INVALID_ARGUMENT, "scenes[i] must live on device i");
   auto t0 = std::chrono::steady_clock::now();
+  DeviceGuard restore;  // the caller's device (the loops below visit every device)
   const uint32_t W = camera->hsize, H = camera->vsize;
   uint32_t max_rows = 0;
   for (int i = 0; i < n_devices; ++i) max_rows = std::max(max_rows, rt_shard_rows(H, row_block, i, n_devices));
@@ -1354,6 +1392,8 @@ int rt_render_multi(rt_scene* const* scenes, int n_devices, const rt_camera_desc
   if (rc != RT_OK) return rc;
   // every device renders its shard (asynchronously, each on its scene's stream)
   std::vector<rt_scene::WfSlot*> used(n_devices, nullptr);
+  int attempt = 0;
+render_all:
   for (int i = 0; i < n_devices; ++i) {
     RT_HIP(hipSetDevice(i));
     std::lock_guard<std::mutex> lk(scenes[i]->mu);
@@ -1392,8 +1432,22 @@ int rt_render_multi(rt_scene* const* scenes, int n_devices, const rt_camera_desc
     RT_HIP(hipSetDevice(i));
     RT_HIP(hipStreamSynchronize(scenes[i]->stream));
   }
-  for (int i = 0; i < n_devices; ++i)
-    if ((rc = check_faults(scenes[i])) != RT_OK) return rc;
+  // a shard that overflowed its queue arenas: the arenas have grown, render the frame again
+  bool again = false;
+  for (int i = 0; i < n_devices; ++i) {
+    RT_HIP(hipSetDevice(i));
+    std::lock_guard<std::mutex> lk(scenes[i]->mu);
+    for (rt_scene::WfSlot& w : scenes[i]->wfs) {
+      bool was = false;
+      w.wf->learn(scenes[i]->sizing);
+      RT_HIP(w.wf->take_overflow(&was));
+      again = again || was;
+    }
+  }
+  if (again) {
+    if (++attempt > 24) return fail(RT_ERR_HIP, "wavefront queue arenas: the frame does not fit");
+    goto render_all;
+  }
   if (stats) {
     std::memset(stats, 0, sizeof *stats);
     for (int i = 0; i < n_devices; ++i) {

@@ -33,15 +33,12 @@ int wf_tuning_apply(WfTuning& t, const char* key, int value) {
     int lo, hi;
   };
   static const Knob knobs[] = {
-      {"accel", &WfTuning::accel, 0, 1},           {"persist", &WfTuning::persist, 0, 1},
-      {"skip_shadow", &WfTuning::skip_shadow, 0, 1}, {"shadow_lb", &WfTuning::shadow_lb, 0, 1},
-      {"image", &WfTuning::image, 0, 3},           {"treelet", &WfTuning::treelet, 0, 1},
-      {"treelet_deltas", &WfTuning::treelet_deltas, 0, 1}, {"shadow_stream", &WfTuning::shadow_stream, 0, 2},
-      {"adaptive_block", &WfTuning::adaptive_block, 0, 1},
-      {"prim_lane", &WfTuning::prim_lane, 0, 1},
-      {"corrupt_calibration", &WfTuning::corrupt_calibration, 0, 1},
-      {"ps_trees", &WfTuning::ps_trees, 0, 32},     {"ps_policy", &WfTuning::ps_policy, 0, 1},
-      {"ps_grid", &WfTuning::ps_grid, 0, 4096},     {"d2h", &WfTuning::d2h, 0, 1}};
+      {"accel", &WfTuning::accel, 0, 1},           {"skip_shadow", &WfTuning::skip_shadow, 0, 1},
+      {"shadow_lb", &WfTuning::shadow_lb, 0, 1},   {"image", &WfTuning::image, 0, 3},
+      {"treelet", &WfTuning::treelet, 0, 1},       {"treelet_deltas", &WfTuning::treelet_deltas, 0, 1},
+      {"shadow_stream", &WfTuning::shadow_stream, 0, 2}, {"adaptive_block", &WfTuning::adaptive_block, 0, 1},
+      {"prim_lane", &WfTuning::prim_lane, 0, 1},   {"arena_pct", &WfTuning::arena_pct, 1, 100},
+      {"d2h", &WfTuning::d2h, 0, 1}};
   if (!key) return 0;
   for (const Knob& k : knobs) {
     if (std::strcmp(key, k.name) != 0) continue;
@@ -284,12 +281,15 @@ __device__ __forceinline__ void shadow_result(const DevScene& sc, const WfArgs& 
 // by value (so the host may reuse its copy at once), to the workspace's
 // device copy that the pass's later launches read, and one set of primary
 // records per frame (frame f's at prim + f * (n_diag + 4)).
+// A fast-path frame also places generation 0 (WfGenTab, device-sized
+// generations): dense, its colours and parents at the arenas' start.
 __global__ void wf_frame_init(DevScene sc, DevCamera cam, PrimRec* prim, unsigned do_prim, uint4* zero_a,
                               unsigned n_a, uint4* zero_b, unsigned n_b, FrameTable tab, FrameTable* tab_dev,
-                              unsigned n_frames) {
+                              unsigned n_frames, WfGenTab* gtab) {
   const unsigned stride = gridDim.x * blockDim.x;
   const unsigned i0 = blockIdx.x * blockDim.x + threadIdx.x;
   const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+  if (gtab && i0 == 0) gtab[0] = WfGenTab{0u, 0u, 0ull, 0ull};
   for (unsigned i = i0; i < n_a; i += stride) zero_a[i] = z;
   for (unsigned i = i0; i < n_b; i += stride) zero_b[i] = z;
   if (n_frames > 1) {
@@ -621,6 +621,59 @@ __device__ __forceinline__ void st_ray(WfRay* p, V3 o, V3 d) {
   __builtin_nontemporal_store((f64x2){d.y, d.z}, q + 2);
 }
 
+// Device-sized generations (DESIGN.md "Device-sized generations"): the
+// launch of generation g takes its ray count from the queue counters (`pre`,
+// the prefix of its regions; generation 0: the host's count), sizes the
+// regions of generation g+1 and of its own parent list from it exactly as
+// the capacity argument of shard_append needs ("Sharded queues": a region of
+// the next generation takes at most 2 `per` wave-iterations of at most 64 rays
+// of its kind, a parent region at most `per` of at most 64 parents), and
+// places them after generation g's colours and parents in the arenas. Every
+// block computes the same values from the same counters and table entry;
+// block 0 writes them for the later launches (generation g+1 and the
+// combines). A generation whose children or parents do not fit spawns none
+// (out_cap = sh_cap = 0: shard_append then hands out no slot, so nothing is
+// written out of bounds) and raises the workspace's overflow record; the
+// frame is incomplete and the host re-renders it (synchronous calls) or
+// reports it (rt_scene_check). Returns the generation's ray count.
+__device__ __forceinline__ unsigned bind_generation(WfArgs& a, const unsigned* pre) {
+  const unsigned g = a.g;
+  const WfGenTab t = a.gtab[g];
+  const unsigned n = g == 0 ? a.n : (pre ? (unsigned)__builtin_amdgcn_readfirstlane((int)pre[2 * kShards]) : 0u);
+  const unsigned groups = ((n + 63u) / 64u + kShardGroup - 1u) / kShardGroup;
+  const unsigned per = kShardGroup * ((groups + kShards - 1u) / kShards);
+  // the last generation spawns no children, so it has no parents either
+  unsigned out_cap = g < a.max_depth ? 128u * per : 0u, sh_cap = g < a.max_depth ? 64u * per : 0u;
+  const unsigned long long slots = g == 0 ? (unsigned long long)n : (unsigned long long)kShards * t.cap;
+  const unsigned long long c_next = t.color_off + slots;
+  const unsigned long long need_c = c_next + (unsigned long long)kShards * out_cap;
+  const unsigned long long need_p = t.par_off + (unsigned long long)kShards * sh_cap;
+  const unsigned long long need_r = (unsigned long long)kShards * out_cap;
+  const bool fits = need_c <= a.color_cap && need_p <= a.par_cap && need_r <= a.ray_cap;
+  if (!fits) { out_cap = 0u; sh_cap = 0u; }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    a.gsh[g] = sh_cap;
+    a.gtab[g + 1] = WfGenTab{out_cap, 0u, c_next, t.par_off + (unsigned long long)kShards * sh_cap};
+    if (!fits) {  // host-mapped: plain vector stores, the flag last
+      volatile WfHostRec* r = a.hrec;
+      r->need_colors = need_c;
+      r->need_parents = need_p;
+      r->need_rays = need_r;
+      __threadfence_system();
+      r->overflow = 1;
+    }
+  }
+  a.n = n;
+  a.in_cap = t.cap;
+  a.out_cap = out_cap;
+  a.sh_cap = sh_cap;
+  a.rays = a.ray_buf[g & 1u];
+  a.next_rays = a.ray_buf[(g + 1u) & 1u];
+  if (!(g == 0 && a.colors_direct)) a.colors = a.color_base + t.color_off * 3ull;
+  a.parents = a.par_base + t.par_off;
+  return n;
+}
+
 // Per-lane tallies of a fused trace kernel (summed per wave at the end).
 struct FusedTally {
   unsigned disc = 0, tests = 0, boxes = 0;           // closest-hit work
@@ -733,9 +786,13 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
                            : LANE == 0 ? (kTraceBlock / 64) * (kBvhMaxDepth + 4) : 1];
   extern __shared__ __attribute__((aligned(16))) unsigned char lane_dyn[];
   int* stk = LANE == 0 ? stack_lds + (threadIdx.x / 64) * (kBvhMaxDepth + 4) : stack_lds + threadIdx.x;
-  const LaneScene ls = lane_scene<LANE>(sc, a.lds_flags, a.n_top, stk, lane_dyn);
   __shared__ unsigned s_pre[kPreRays];
   const unsigned* pre = shard_prefix<true>(a.in_cnt, s_pre);
+  if (a.dev_sized) bind_generation(a, pre);
+  // a block without a chunk (static split below: its first chunk lies past the
+  // last) leaves before staging the image; the exit is block-uniform
+  if (blockIdx.x * (blockDim.x / 64u) >= (a.n + 63u) / 64u) return;
+  const LaneScene ls = lane_scene<LANE>(sc, a.lds_flags, a.n_top, stk, lane_dyn);
   FusedTally t;
   // Work distribution: chunk c = rays [64c, 64c + 64), one wave-iteration.
   // A launch with more chunks than waves hands them out dynamically from the
@@ -852,30 +909,6 @@ __global__ __launch_bounds__(kWfBlock) void wf_prep(DevScene sc, DevCamera cam, 
   }
 }
 
-// Device-side check of a calibrated frame: every generation's queue counts
-// (the sharded region counters the trace kernels appended to) must equal the
-// launch sizes the host took from its calibration cache. A mismatch would mean
-// rays were left untraced; it raises the host-mapped fault flag, which the
-// library reports as RT_ERR_HIP on the next call (Wavefront::fault).
-struct WfCheckArgs {
-  unsigned n_gen;              // generations 0 .. n_gen-1 were launched
-  unsigned rays[kMaxGen];      // expected ray count of generation g (g >= 1)
-  unsigned shadows[kMaxGen];   // expected shadow-list length of generation g
-};
-// one wave (threads 0..63 of a block)
-__device__ __forceinline__ void check_counts_wave(const unsigned* shard_base, const WfCheckArgs& c, int* fault) {
-  for (unsigned g = threadIdx.x; g <= c.n_gen && g < (unsigned)kMaxGen; g += 64) {
-    const unsigned* r = shard_base + ((size_t)g * 2 + 0) * kShards * kShardStride;
-    const unsigned* q = shard_base + ((size_t)g * 2 + 1) * kShards * kShardStride;
-    unsigned nr = 0, ns = 0;
-    for (int k = 0; k < kShards; ++k) {
-      nr += r[k * kShardStride] + r[k * kShardStride + 1];  // front + back (shard_append)
-      ns += q[k * kShardStride];
-    }
-    const bool bad = (g >= 1 && nr != c.rays[g]) || (g < c.n_gen && ns != c.shadows[g]);
-    if (bad) *fault = 1;
-  }
-}
 // ---------------------------------------------------------- combine
 // World::shade_hit (world.rs:40-68) from the node, the shadow flags and the
 // children's colours; color_at miss -> black (world.rs:74-75).
@@ -925,26 +958,48 @@ __global__ __launch_bounds__(kWfBlock) void wf_combine(DevScene sc, DevCamera ca
 // The fast path's combine (DESIGN.md "Fused generations"): shade_hit of every
 // node of generation g that has a reflected or refracted child, from its
 // ParentRec (surface term, Schlick factor) and the children's colours, which
-// generation g+1 wrote (directly or through this pass).
-__global__ __launch_bounds__(kWfBlock) void wf_combine_parents(DevScene sc, DevCamera cam, WfArgs a,
-                                                                WfCheckArgs ck, const unsigned* shard_base,
-                                                                int* fault) {
-  // the first combine launch of a calibrated frame also runs the queue check
-  // (wf_check_counts): every trace launch of the frame precedes it
-  if (fault && blockIdx.x == 0 && threadIdx.x < 64) check_counts_wave(shard_base, ck, fault);
+// generation g+1 wrote (directly or through this pass). Its parents' count
+// comes from their region counters and their place from the generation table
+// (device-sized generations). Generation 0's pass, the frame's last, also
+// records the frame's ray count per generation in the workspace's host-mapped
+// record (a.out_cnt: generation 1's ray counters), which sizes later frames.
+__global__ __launch_bounds__(kWfBlock) void wf_combine_parents(DevScene sc, DevCamera cam, WfArgs a) {
   const unsigned stride = gridDim.x * blockDim.x;
   __shared__ unsigned s_pre[kPreList];
   const unsigned* pre = shard_prefix<false>(a.sh_cnt, s_pre);
-  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
-    const ParentRec p = a.parents[shard_slot<false>(pre, a.sh_cap, i)];
+  const unsigned n = (unsigned)__builtin_amdgcn_readfirstlane((int)pre[kShards]);
+  const WfGenTab t = a.gtab[a.g];
+  const unsigned sh_cap = a.gsh[a.g];
+  const ParentRec* parents = a.par_base + t.par_off;
+  const double* child_colors = a.color_base + a.gtab[a.g + 1].color_off * 3ull;
+  if (!(a.g == 0 && a.colors_direct)) a.colors = a.color_base + t.color_off * 3ull;
+  if (a.g == 0 && blockIdx.x == 0 && threadIdx.x < 64) {
+    volatile WfHostRec* r = a.hrec;
+    for (unsigned l = threadIdx.x; l <= a.max_depth && l < (unsigned)kMaxGen; l += 64) {
+      unsigned c = a.frame_real * (a.n_frames > 1 ? a.n_frames : 1u);
+      if (l > 0) {
+        const unsigned* q = a.out_cnt + (size_t)(l - 1) * 2 * kShards * kShardStride;
+        c = 0;
+        for (int k = 0; k < kShards; ++k) c += q[k * kShardStride] + q[k * kShardStride + 1];  // front + back
+      }
+      r->counts[l] = c;
+    }
+    if (threadIdx.x == 0) {
+      r->n_real = a.frame_real * (a.n_frames > 1 ? a.n_frames : 1u);
+      r->n_gens = a.max_depth + 1;
+      r->frames = r->frames + 1;
+    }
+  }
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const ParentRec p = parents[shard_slot<false>(pre, sh_cap, i)];
     const ShadeRec& m = sc.shade[p.obj];
     V3 refl = v3(0.0, 0.0, 0.0), refr = v3(0.0, 0.0, 0.0);
     if (p.child_refl >= 0) {
-      const double* cc = a.child_colors + (size_t)p.child_refl * 3;
+      const double* cc = child_colors + (size_t)p.child_refl * 3;
       refl = vscale(v3(cc[0], cc[1], cc[2]), m.reflective);  // world.rs:113
     }
     if (p.child_refr >= 0) {
-      const double* cc = a.child_colors + (size_t)p.child_refr * 3;
+      const double* cc = child_colors + (size_t)p.child_refr * 3;
       refr = vscale(v3(cc[0], cc[1], cc[2]), m.transparency);  // world.rs:133
     }
     const V3 col = shade_color(m, v3(p.surface[0], p.surface[1], p.surface[2]), refl, refr, p.schlick);
@@ -997,11 +1052,6 @@ __global__ void wf_count_kinds(WfArgs a) {
   }
 }
 
-// the check alone (frames without a parents combine, the exhaustive pipeline)
-__global__ void wf_check_counts(const unsigned* shard_base, WfCheckArgs c, int* fault) {
-  if (threadIdx.x < 64) check_counts_wave(shard_base, c, fault);
-}
-
 // ---------------------------------------------------------- host side
 // Per-launch profiling: while a kernel class is being timed (Wavefront::pmark)
 // its launch carries the start/stop events in the dispatch itself
@@ -1013,17 +1063,16 @@ static thread_local int t_ev_used = 0;
 Wavefront::~Wavefront() {
   for (auto& g : gens_) {
     (void)hipFree(g.rays); (void)hipFree(g.hits); (void)hipFree(g.nodes); (void)hipFree(g.colors);
-    (void)hipFree(g.shadow_nodes); (void)hipFree(g.geo); (void)hipFree(g.surf); (void)hipFree(g.parents);
+    (void)hipFree(g.shadow_nodes); (void)hipFree(g.geo); (void)hipFree(g.surf);
   }
+  (void)hipFree(colors_); (void)hipFree(parents_); (void)hipFree(rays_[0]); (void)hipFree(rays_[1]);
+  if (d_gtab_) (void)hipFree(d_gtab_);
+  if (d_gsh_) (void)hipFree(d_gsh_);
   if (d_cnt_) (void)hipFree(d_cnt_);
   if (d_shard_) (void)hipFree(d_shard_);
   if (d_prim_) (void)hipFree(d_prim_);
   if (d_frames_) (void)hipFree(d_frames_);
-  if (ps_rings_) (void)hipFree(ps_rings_);
-  if (ps_parents_) (void)hipFree(ps_parents_);
-  if (ps_ctr_) (void)hipFree(ps_ctr_);
-  if (ps_lists_) (void)hipFree(ps_lists_);
-  if (h_fault_) (void)hipHostFree(h_fault_);
+  if (h_rec_) (void)hipHostFree(h_rec_);
   if (ev0_) (void)hipEventDestroy(ev0_);
   if (ev1_) (void)hipEventDestroy(ev1_);
   for (hipEvent_t e : fork_ev_)
@@ -1074,29 +1123,27 @@ hipError_t Wavefront::last_profile(WfProfile* out) {
     out->tests[c] = (double)hc.tests(c);
     out->boxes[c] = (double)hc.boxes(c);
   }
+  if (last_fused_ && lr_.stream) {  // the fast path's generations sized themselves: their rays from the record
+    std::vector<unsigned> rays;
+    WF_CHECK(last_counts(rays));
+    out->rays[WF_PRIMARY] = rays.empty() ? 0.0 : (double)rays[0];
+    double sec = 0.0;
+    for (size_t g = 1; g < rays.size(); ++g) sec += (double)rays[g];
+    out->rays[WF_CLOSEST] = sec;
+  }
   for (int c = 0; c < 2; ++c) {
     out->sh_rays[c] = (double)hc.sh_rays(c);
     out->sh_tests[c] = (double)hc.sh_tests(c);
   }
   if (last_fused_) out->rays[WF_SHADOW] = out->sh_rays[0] + out->sh_rays[1];  // traced inside the fused launches
-  for (int c = 0; c < 2; ++c) { out->ps_items[c] = (double)hc.ps_items(c); out->ps_lanes[c] = (double)hc.ps_lanes(c); }
-  for (int c = 0; c < 6; ++c) out->ps_cycles[c] = (double)hc.ps_cycles(c);
-  if (last_persist_) {  // one launch: the root rays and, from a counted frame, the children per depth
-    out->rays[WF_PRIMARY] = (double)lr_.n0;
-    double kids = 0.0;
-    for (int g = 0; g < kMaxGen; ++g) kids += (double)hc.n_refl[g] + (double)hc.n_refr[g];
-    out->rays[WF_CLOSEST] = kids;
-  }
   out->bvh = last_bvh_ ? 1 : 0;
   out->fused = last_fused_ ? 1 : 0;
-  out->persist = last_persist_ ? 1 : 0;
   return hipSuccess;
 }
 
-// Grow-only per-generation buffers (12.5 % headroom on each reallocation).
-// The fast path needs the rays, the colours and the parents list; the
-// exhaustive pipeline the hits, nodes, hit geometry, lighting terms
-// (slots x n_lights) and the shadow list.
+// Grow-only per-generation buffers of the exhaustive pipeline (12.5 %
+// headroom on each reallocation): the rays, colours, hits, nodes, hit
+// geometry, lighting terms (slots x n_lights) and the shadow list.
 template <typename T>
 static hipError_t grow(T*& p, size_t& cap, size_t need) {
   need = std::max<size_t>(need, 1);
@@ -1109,20 +1156,87 @@ static hipError_t grow(T*& p, size_t& cap, size_t need) {
   cap = n;
   return hipSuccess;
 }
-hipError_t Wavefront::ensure_gen(size_t g, size_t slots, size_t n_lights, size_t list_slots, bool fused) {
+hipError_t Wavefront::ensure_gen(size_t g, size_t slots, size_t n_lights, size_t list_slots) {
   if (gens_.size() <= g) gens_.resize(g + 1);
   WfGenBuf& b = gens_[g];
   WF_CHECK(grow(b.rays, b.cap_rays, slots));
   WF_CHECK(grow(b.colors, b.cap_colors, slots * 3));
-  if (fused) {
-    WF_CHECK(grow(b.parents, b.cap_parents, list_slots));
-    return hipSuccess;
-  }
   WF_CHECK(grow(b.hits, b.cap_hits, slots));
   WF_CHECK(grow(b.nodes, b.cap_nodes, slots));
   WF_CHECK(grow(b.geo, b.cap_geo, slots));
   WF_CHECK(grow(b.surf, b.cap_surf, slots * std::max<size_t>(n_lights, 1) * 3));
   WF_CHECK(grow(b.shadow_nodes, b.cap_list, list_slots));
+  return hipSuccess;
+}
+
+// The fast path's arenas (device-sized generations): colour slots, parent
+// records, and ray slots per ping-pong buffer. Grow-only (12.5 % headroom),
+// unless `exact` (the arena_pct test hook), which reallocates to the size
+// asked for.
+hipError_t Wavefront::ensure_arenas(unsigned long long colors, unsigned long long parents, unsigned long long rays,
+                                    bool exact) {
+  auto fit = [&](auto*& p, unsigned long long& cap, unsigned long long need, size_t elem, int n_bufs) -> hipError_t {
+    need = std::max<unsigned long long>(need, 1);
+    if (exact ? cap == need : cap >= need) return hipSuccess;
+    const unsigned long long n = exact ? need : need + need / 8;
+    for (int k = 0; k < n_bufs; ++k) {
+      (void)hipFree((&p)[k]);
+      (&p)[k] = nullptr;
+    }
+    cap = 0;
+    for (int k = 0; k < n_bufs; ++k) WF_CHECK(hipMalloc((void**)&(&p)[k], n * elem));
+    cap = n;
+    return hipSuccess;
+  };
+  WF_CHECK(fit(colors_, color_cap_, colors, 3 * sizeof(double), 1));
+  WF_CHECK(fit(parents_, par_cap_, parents, sizeof(ParentRec), 1));
+  WF_CHECK(fit(rays_[0], ray_cap_, rays, sizeof(WfRay), 2));
+  return hipSuccess;
+}
+
+hipError_t Wavefront::take_overflow(bool* was) {
+  *was = false;
+  if (!h_rec_) return hipSuccess;
+  volatile WfHostRec* r = h_rec_;
+  if (!r->overflow) return hipSuccess;
+  *was = true;
+  const unsigned long long nc = r->need_colors, np = r->need_parents, nr = r->need_rays;
+  r->overflow = 0;
+  // at least double whatever fell short: the generations after the overflowing
+  // one never ran, so their needs are unknown
+  auto next = [](unsigned long long cap, unsigned long long need) {
+    return need > cap ? std::max(need + need / 4, 2 * cap) : cap;
+  };
+  return ensure_arenas(next(color_cap_, nc), next(par_cap_, np), next(ray_cap_, nr), false);
+}
+
+void Wavefront::learn(WfSizing& sz) const {
+  if (!h_rec_) return;
+  const volatile WfHostRec* r = h_rec_;
+  if (r->frames == 0) return;
+  const unsigned n0 = r->n_real, ng = std::min<unsigned>((unsigned)r->n_gens, (unsigned)kMaxGen);
+  if (n0 == 0 || ng == 0) return;
+  double sum = 0.0, mx = 0.0;
+  for (unsigned g = 0; g < ng; ++g) {
+    const double c = (double)r->counts[g];
+    if (g + 1 < ng) sum += c;  // the last generation spawns no children
+    mx = std::max(mx, c);
+  }
+  sz.rho = std::max(sz.rho, sum / n0);
+  sz.mu = std::max(sz.mu, mx / n0);
+}
+
+hipError_t Wavefront::last_counts(std::vector<unsigned>& rays) {
+  rays.clear();
+  if (!lr_.fused) {
+    rays = lr_.rays;
+    return hipSuccess;
+  }
+  WF_CHECK(hipStreamSynchronize(lr_.stream));
+  const volatile WfHostRec* r = h_rec_;
+  const unsigned ng = std::min<unsigned>((unsigned)r->n_gens, (unsigned)kMaxGen);
+  for (unsigned g = 0; g < ng; ++g) rays.push_back((unsigned)r->counts[g]);
+  while (rays.size() > 1 && rays.back() == 0) rays.pop_back();
   return hipSuccess;
 }
 
@@ -1148,11 +1262,13 @@ hipError_t Wavefront::ensure_side() {
 
 hipError_t Wavefront::ensure_misc(size_t n_diag, unsigned n_frames) {
   if (!d_cnt_) WF_CHECK(hipMalloc(&d_cnt_, sizeof(WfCounters)));
-  if (!h_fault_) {
-    WF_CHECK(hipHostMalloc((void**)&h_fault_, kFaultWords * sizeof(int), hipHostMallocMapped));
-    for (int k = 0; k < kFaultWords; ++k) ((volatile int*)h_fault_)[k] = 0;
-    WF_CHECK(hipHostGetDevicePointer((void**)&d_fault_, h_fault_, 0));
+  if (!h_rec_) {
+    WF_CHECK(hipHostMalloc((void**)&h_rec_, sizeof(WfHostRec), hipHostMallocMapped));
+    std::memset((void*)h_rec_, 0, sizeof(WfHostRec));
+    WF_CHECK(hipHostGetDevicePointer((void**)&d_rec_, h_rec_, 0));
   }
+  if (!d_gtab_) WF_CHECK(hipMalloc(&d_gtab_, (kMaxGen + 1) * sizeof(WfGenTab)));
+  if (!d_gsh_) WF_CHECK(hipMalloc(&d_gsh_, kMaxGen * sizeof(unsigned)));
   if (!d_shard_) WF_CHECK(hipMalloc(&d_shard_, (size_t)kMaxGen * 2 * kShards * kShardStride * sizeof(unsigned)));
   if (!ev0_) WF_CHECK(hipEventCreate(&ev0_));
   if (!ev1_) WF_CHECK(hipEventCreate(&ev1_));
@@ -1305,17 +1421,14 @@ static hipError_t launch_fused(const DevScene& sc, const DevCamera& cam, const W
 
 hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool camera_mode, const double* d_in_rays,
                              unsigned n0, unsigned aa, unsigned max_depth, unsigned row_block, unsigned shard,
-                             unsigned n_shards, double* d_out, hipStream_t stream, const std::string& signature,
-                             DevStats* stats, float* ms_kernel, const WfTuning& tn, bool solo, unsigned flags,
+                             unsigned n_shards, double* d_out, hipStream_t stream, WfSizing& sz, DevStats* stats,
+                             float* ms_kernel, const WfTuning& tn, bool solo, unsigned flags,
                              const FrameTable* batch, unsigned n_frames) {
   if (max_depth + 2 > (unsigned)kMaxGen) return hipErrorInvalidValue;
   if (aa == 0 || aa > 16 || (aa & (aa - 1)) != 0 || (!camera_mode && aa != 1) || n0 % aa != 0)
     return hipErrorInvalidValue;
   if (n_frames == 0 || n_frames > kMaxFrames || (n_frames > 1 && !batch)) return hipErrorInvalidValue;
-  // with AA the root colours are averaged into d_out by wf_average
-  const bool averaged = aa > 1;
   WF_CHECK(ensure_misc((size_t)sc.n_diag, n_frames));
-  const unsigned L = (unsigned)sc.n_lights;
   // BVH traversal (fused generations) and skipped shadow rays unless the
   // reference's every-shape loop is asked for; counting (stats) never changes the algorithm
   const bool exhaustive = (flags & WF_EXHAUSTIVE) != 0;
@@ -1330,37 +1443,9 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     if (!camera_mode || !fused || count || n0 == 0) return hipErrorInvalidValue;
     n0 = n_frames * ((n0 + 63u) & ~63u);
   }
-  // the fast path: one persistent launch per render (rt_persist.hip), for
-  // recursion depths whose heap-addressed trees it can hold
-  if (bvh && tn.persist && max_depth <= kPsMaxDepth && n_frames == 1)
-    return render_persist(sc, cam, camera_mode, d_in_rays, n0, aa, max_depth, row_block, shard, n_shards, d_out,
-                          stream, stats, ms_kernel, count, tn);
-  last_persist_ = false;
-  // the shadow-ray counts differ between the two modes; the fused pipeline's
-  // second queue per generation holds its parents instead of shadow rays
-  const std::string key = signature.empty() ? signature : signature + (skip_shadow ? 'S' : 'A') + (fused ? 'F' : 'E');
-  auto it = key.empty() ? cache_.end() : cache_.find(key);
-  const bool calibrated = it != cache_.end();
-  Counts counts;
-  if (calibrated) counts = it->second;
-  if (calibrated && tn.corrupt_calibration && counts.rays.size() > 1 && counts.rays[1] > 0) --counts.rays[1];
-  counts.rays.resize(max_depth + 2, 0);
-  counts.shadows.resize(max_depth + 2, 0);
-  counts.rays[0] = n0;
-
-
-  WF_CHECK(ensure_gen(0, n0, L, 0, fused));
-  if (!camera_mode) {
-    // batch rays: n0 x 6 doubles -> WfRay queue of generation 0
-    WF_CHECK(hipMemcpy2DAsync(gens_[0].rays, sizeof(WfRay), d_in_rays, 6 * sizeof(double), 6 * sizeof(double), n0,
-                              hipMemcpyDeviceToDevice, stream));
-  }
-  const bool prim_lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, true) <= kWfLdsLimit;
-  const bool gen_lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, false) <= kWfLdsLimit;
-  last_bvh_ = bvh;
-  last_fused_ = fused;
-  const bool use_prim = camera_mode && (prim_lds || bvh) && sc.n_diag > 0;
-  {  // counters zeroed and the primary records written by one launch
+  const bool use_prim = camera_mode && sc.n_diag > 0 &&
+                        (fused || wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, true) <= kWfLdsLimit);
+  {  // counters zeroed, generation 0 placed and the primary records written by one launch
     static_assert(sizeof(WfCounters) % 16 == 0, "WfCounters is zeroed in 16-B words");
     const unsigned n_a = (unsigned)(sizeof(WfCounters) / 16);
     const unsigned n_b = (unsigned)((size_t)(max_depth + 2) * 2 * kShards * kShardStride * sizeof(unsigned) / 16);
@@ -1368,48 +1453,222 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     const FrameTable none{};
     WF_LAUNCH(wf_frame_init, dim3(std::min<unsigned>((work + 255) / 256, 256u)), dim3(256), 0, stream, sc, cam,
               d_prim_, use_prim ? 1u : 0u, (uint4*)d_cnt_, n_a, (uint4*)d_shard_, n_b, n_frames > 1 ? *batch : none,
-              d_frames_, n_frames);
+              d_frames_, n_frames, fused ? d_gtab_ : (WfGenTab*)nullptr);
     WF_CHECK(hipGetLastError());
   }
-  // Exhaustive pipeline: shadow traces of generation g depend only on
-  // closest(g), like closest(g+1); they run on the side stream, forked after
-  // closest(g) and joined before the combine pass (DESIGN.md "Shadow stream").
+  if (ms_kernel) WF_CHECK(hipEventRecord(ev0_, stream));
+  if (profiling_) pframes_ += n_frames;  // class times are reported per frame
+  prof_rays_[0] = prof_rays_[1] = prof_rays_[2] = 0;
+  last_bvh_ = bvh;
+  last_fused_ = fused;
+  lr_.stream = stream;
+  lr_.fused = fused;
+  if (fused)
+    WF_CHECK(render_fast(sc, cam, camera_mode, d_in_rays, n0, frame_real, aa, max_depth, row_block, shard, n_shards,
+                         d_out, stream, sz, count, skip_shadow, tn, batch, n_frames));
+  else
+    WF_CHECK(render_exhaustive(sc, cam, camera_mode, d_in_rays, n0, aa, max_depth, row_block, shard, n_shards, d_out,
+                               stream, count, skip_shadow, tn, solo));
+  if (ms_kernel) WF_CHECK(hipEventRecord(ev1_, stream));
+  lr_.L = (unsigned)sc.n_lights; lr_.n0 = n0; lr_.max_depth = max_depth;
+  lr_.counted = count; lr_.exact_disc = !bvh && !skip_shadow; lr_.bvh = bvh;
+  lr_.n_diag = (unsigned long long)sc.n_diag; lr_.n_gen = (unsigned long long)sc.n_gen;
+  lr_.n_planes = (unsigned long long)sc.n_planes; lr_.n_quads = (unsigned long long)sc.n_quads;
+  if (stats || ms_kernel) {
+    WF_CHECK(hipStreamSynchronize(stream));
+    if (ms_kernel) WF_CHECK(hipEventElapsedTime(ms_kernel, ev0_, ev1_));
+  }
+  if (stats) WF_CHECK(read_stats(stats));
+  return hipSuccess;
+}
+
+// Slots of generation g+1 that generation g's launch reserves for n_g rays
+// (bind_generation: 64 regions of 128 `per`), and of its parent list.
+static unsigned long long gen_slots(unsigned long long n) {
+  const unsigned long long groups = ((n + 63) / 64 + kShardGroup - 1) / kShardGroup;
+  return (unsigned long long)kShards * 128ull * kShardGroup * ((groups + kShards - 1) / kShards);
+}
+
+// The fast path (DESIGN.md "Device-sized generations"): every launch of the
+// frame is enqueued at once; each generation's launch finds its own ray count
+// on the device. The host only sizes the arenas, from the scene's learned
+// ratios (WfSizing) or, when smaller, from the exact bound of the recursion
+// (every ray spawning `branch` children); a frame that outgrows them is
+// reported through the workspace's overflow record (take_overflow).
+hipError_t Wavefront::render_fast(const DevScene& sc, const DevCamera& cam, bool camera_mode, const double* d_in_rays,
+                                  unsigned n0, unsigned frame_real, unsigned aa, unsigned max_depth,
+                                  unsigned row_block, unsigned shard, unsigned n_shards, double* d_out,
+                                  hipStream_t stream, WfSizing& sz, bool count, bool skip_shadow, const WfTuning& tn,
+                                  const FrameTable* batch, unsigned n_frames) {
+  const bool averaged = aa > 1;
+  const unsigned n_real = frame_real * n_frames;
+  // ---- arena sizes
+  learn(sz);  // this workspace's last recorded frame (a frame still in flight may be stale: a hint only)
+  const unsigned D = max_depth;
+  double c_bound = (double)n0, p_bound = 0.0, r_bound = camera_mode ? 0.0 : (double)n0;
+  {
+    double ng = (double)n0;
+    for (unsigned g = 0; g < D; ++g) {
+      const double s = (double)gen_slots((unsigned long long)std::min(ng, 4.0e9));
+      c_bound += s;
+      p_bound += s / 2.0;
+      r_bound = std::max(r_bound, s);
+      ng = std::min(ng * (double)sz.branch, 4.0e9);
+      if (ng == 0.0) break;
+    }
+  }
+  const double rho = sz.rho > 0.0 ? sz.rho : 8.0, mu = sz.mu > 0.0 ? sz.mu : 2.0;
+  const double min_region = (double)gen_slots(1);  // one wave-iteration's regions: 64 x 128 x kShardGroup
+  const double c_learn = (double)n0 + 2.5 * rho * n_real + min_region * D;
+  const double p_learn = 1.25 * rho * n_real + min_region / 2.0 * D;
+  const double r_learn = std::max(camera_mode ? 0.0 : (double)n0, 2.5 * mu * n_real + min_region);
+  double want_c = std::min(c_bound, c_learn), want_p = std::min(p_bound, p_learn), want_r = std::min(r_bound, r_learn);
+  // the test hook shrinks the arenas once per setting (the re-renders after an
+  // overflow then grow them as usual)
+  const bool squeeze = tn.arena_pct < 100 && tn.arena_pct != squeezed_pct_;
+  squeezed_pct_ = tn.arena_pct;
+  if (squeeze) {
+    want_c = std::max((double)n0, want_c * tn.arena_pct / 100.0);
+    want_p *= tn.arena_pct / 100.0;
+    want_r = std::max(camera_mode ? 0.0 : (double)n0, want_r * tn.arena_pct / 100.0);
+  }
+  WF_CHECK(ensure_arenas((unsigned long long)want_c, (unsigned long long)want_p, (unsigned long long)want_r, squeeze));
+  if (!camera_mode)  // batch rays: n0 x 6 doubles -> generation 0's ray buffer
+    WF_CHECK(hipMemcpy2DAsync(rays_[0], sizeof(WfRay), d_in_rays, 6 * sizeof(double), 6 * sizeof(double), n0,
+                              hipMemcpyDeviceToDevice, stream));
+  WfArgs a{};
+  a.dev_sized = 1;
+  a.colors_direct = averaged ? 0u : 1u;
+  a.gtab = d_gtab_;
+  a.gsh = d_gsh_;
+  a.ray_buf[0] = rays_[0];
+  a.ray_buf[1] = rays_[1];
+  a.color_base = colors_;
+  a.par_base = parents_;
+  a.color_cap = color_cap_;
+  a.par_cap = par_cap_;
+  a.ray_cap = ray_cap_;
+  a.hrec = d_rec_;
+  a.aa = aa;
+  a.rows = frame_real / aa / (cam.hsize ? cam.hsize : 1);
+  a.n_frames = n_frames; a.frame_rays = n0 / n_frames; a.frame_real = frame_real; a.frames = d_frames_;
+  a.cnt = d_cnt_;
+  a.prim = d_prim_;
+  a.max_depth = max_depth;
+  a.camera_mode = camera_mode ? 1u : 0u;
+  a.row_block = row_block; a.shard = shard; a.n_shards = n_shards;
+  a.skip_shadow = skip_shadow ? 1u : 0u;
+  a.count = count ? 1u : 0u;
+  a.use_lb = (tn.shadow_lb && sc.lb_cells) ? 1u : 0u;
+  const bool use_prim = camera_mode && sc.n_diag > 0;
+  // an upper bound on any generation's rays, for the grid of the device-sized
+  // launches (the kernels stride over what they find)
+  const unsigned kAnyRays = 1u << 30;
+  for (unsigned g = 0; g <= max_depth; ++g) {
+    a.g = g;
+    a.colors = d_out;  // generation 0 without AA: the output (bind_generation keeps it)
+    a.n = g == 0 ? n0 : 0u;
+    a.in_cnt = g == 0 ? nullptr : shard_cnt(g, 0);
+    a.out_cnt = shard_cnt(g + 1, 0);
+    a.sh_cnt = shard_cnt(g, 1);
+    const bool prim_launch = g == 0 && use_prim;
+    const int ccls = prim_launch ? WF_PRIMARY : WF_CLOSEST;
+    a.disc_slot = (unsigned)ccls;
+    if (g == 0) prof_rays_[ccls] += n_real;
+    WF_CHECK(pmark(stream, ccls, true));
+    WF_CHECK(launch_fused(sc, cam, a, prim_launch, g == 0 ? n0 : kAnyRays, stream, count, tn));
+    WF_CHECK(pmark(stream, ccls, false));
+  }
+  // combine, deepest generation first (only the nodes with children; the last
+  // generation has none). Generation 0's pass records the frame's counts.
+  static int combine_grid = 0;
+  if (combine_grid == 0) combine_grid = occupancy_grid(wf_combine_parents, kWfBlock, 0, kAnyRays);
+  for (int g = max_depth > 0 ? (int)max_depth - 1 : 0; g >= 0; --g) {
+    a.g = (unsigned)g;
+    a.colors = d_out;
+    a.sh_cnt = shard_cnt((unsigned)g, 1);
+    a.out_cnt = shard_cnt(1, 0);
+    WF_CHECK(pmark(stream, WF_COMBINE, true));
+    WF_LAUNCH(wf_combine_parents, dim3(combine_grid), dim3(kWfBlock), 0, stream, sc, cam, a);
+    WF_CHECK(hipGetLastError());
+    WF_CHECK(pmark(stream, WF_COMBINE, false));
+  }
+  if (averaged) {
+    const unsigned n_pix = n_frames * (frame_real / aa);
+    WF_CHECK(pmark(stream, WF_COMBINE, true));
+    WfArgs v{};
+    v.aa = aa; v.rows = frame_real / aa / cam.hsize;
+    v.n_frames = n_frames; v.frame_rays = n0 / n_frames; v.frame_real = frame_real; v.frames = d_frames_;
+    WF_LAUNCH(wf_average, dim3(occupancy_grid(wf_average, kWfBlock, 0, n_pix)), dim3(kWfBlock), 0, stream, v,
+              cam.hsize, colors_, n_pix, d_out);
+    WF_CHECK(hipGetLastError());
+    WF_CHECK(pmark(stream, WF_COMBINE, false));
+  }
+  (void)batch;
+  lr_.last = max_depth;
+  lr_.rays.clear();
+  lr_.shadows.clear();
+  return hipSuccess;
+}
+
+// The exhaustive pipeline (the reference's every-shape loop, counted renders):
+// each generation's ray and shadow-ray counts are read back before the next
+// launch (synchronous); its buffers are per generation.
+hipError_t Wavefront::render_exhaustive(const DevScene& sc, const DevCamera& cam, bool camera_mode,
+                                        const double* d_in_rays, unsigned n0, unsigned aa, unsigned max_depth,
+                                        unsigned row_block, unsigned shard, unsigned n_shards, double* d_out,
+                                        hipStream_t stream, bool count, bool skip_shadow, const WfTuning& tn,
+                                        bool solo) {
+  const bool averaged = aa > 1;
+  const unsigned L = (unsigned)sc.n_lights;
+  std::vector<unsigned> rays(max_depth + 2, 0), shadows(max_depth + 2, 0);
+  rays[0] = n0;
+  WF_CHECK(ensure_gen(0, n0, L, 0));
+  if (!camera_mode) {
+    // batch rays: n0 x 6 doubles -> WfRay queue of generation 0
+    WF_CHECK(hipMemcpy2DAsync(gens_[0].rays, sizeof(WfRay), d_in_rays, 6 * sizeof(double), 6 * sizeof(double), n0,
+                              hipMemcpyDeviceToDevice, stream));
+  }
+  const bool prim_lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, true) <= kWfLdsLimit;
+  const bool gen_lds = wf_lds_bytes(sc.n_diag, sc.n_gen, sc.n_planes, false) <= kWfLdsLimit;
+  const bool use_prim = camera_mode && prim_lds && sc.n_diag > 0;
+  // Shadow traces of generation g depend only on closest(g), like closest(g+1);
+  // they run on the side stream, forked after closest(g) and joined before the
+  // combine pass (DESIGN.md "Shadow stream").
   hipStream_t sh_stream = stream;
-  if (!fused && (tn.shadow_stream == 2 || (tn.shadow_stream == 1 && solo))) {
+  if (tn.shadow_stream == 2 || (tn.shadow_stream == 1 && solo)) {
     WF_CHECK(ensure_side());
     sh_stream = side_;
   }
   bool forked = false;
-  if (ms_kernel) WF_CHECK(hipEventRecord(ev0_, stream));
-  if (profiling_) pframes_ += n_frames;  // class times are reported per frame
-  prof_rays_[0] = prof_rays_[1] = prof_rays_[2] = 0;
   unsigned last = 0;
   // per-region capacity of each generation's sharded arrays (generation 0 is
-  // dense) and of its second queue (shadow list, or the fused path's parents)
+  // dense) and of its shadow list
   std::vector<unsigned> caps(max_depth + 2, 0), list_caps(max_depth + 2, 0);
   for (unsigned g = 0; g <= max_depth; ++g) {
-    const unsigned n = counts.rays[g];
+    const unsigned n = rays[g];
     if (n == 0) break;
     last = g;
-    // wave-iteration q of this generation appends its parents (shadow rays) to region
-    // (q / kShardGroup) mod kShards, at most `per` wave-iterations of <= 64 parents (64 L
-    // shadow rays) each; its reflected and refracted rays to region (q / kShardGroup) mod
-    // (kShards / 2) of their half, at most 2 `per` wave-iterations of <= 64 rays each (shard_append)
+    // wave-iteration q of this generation appends its shadow rays to region
+    // (q / kShardGroup) mod kShards, at most `per` wave-iterations of <= 64 L
+    // shadow rays each; its reflected and refracted rays to region (q / kShardGroup)
+    // mod (kShards / 2) of their half, at most 2 `per` wave-iterations of <= 64 rays
+    // each (shard_append)
     const unsigned groups = ((n + 63) / 64 + kShardGroup - 1) / kShardGroup;
     const unsigned per = kShardGroup * ((groups + kShards - 1) / kShards);
-    const unsigned out_cap = g < max_depth ? 128u * per : 0u, sh_cap = (fused ? 64u : 64u * L) * per;
+    const unsigned out_cap = g < max_depth ? 128u * per : 0u, sh_cap = 64u * L * per;
     caps[g + 1] = out_cap;
     list_caps[g] = sh_cap;
-    WF_CHECK(ensure_gen(g, g == 0 ? n : (size_t)kShards * caps[g], L, (size_t)kShards * sh_cap, fused));
-    WF_CHECK(ensure_gen(g + 1, (size_t)kShards * out_cap, L, 0, fused));
+    WF_CHECK(ensure_gen(g, g == 0 ? n : (size_t)kShards * caps[g], L, (size_t)kShards * sh_cap));
+    WF_CHECK(ensure_gen(g + 1, (size_t)kShards * out_cap, L, 0));
     WfArgs a{};
     WfGenBuf& B = gens_[g];
     a.rays = B.rays; a.hits = B.hits; a.nodes = B.nodes; a.shadow_nodes = B.shadow_nodes;
-    a.geo = B.geo; a.surf = B.surf; a.parents = B.parents;
+    a.geo = B.geo; a.surf = B.surf;
     a.colors = (g == 0 && !averaged) ? d_out : B.colors;
     a.aa = aa;
-    a.rows = frame_real / aa / (cam.hsize ? cam.hsize : 1);
-    a.n_frames = n_frames; a.frame_rays = n0 / n_frames; a.frame_real = frame_real; a.frames = d_frames_;
+    a.rows = n0 / aa / (cam.hsize ? cam.hsize : 1);
+    a.n_frames = 1; a.frame_rays = n0; a.frame_real = n0;
     a.next_rays = gens_[g + 1].rays;
     a.child_colors = gens_[g + 1].colors;
     a.cnt = d_cnt_;
@@ -1426,29 +1685,21 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
     a.row_block = row_block; a.shard = shard; a.n_shards = n_shards;
     a.skip_shadow = skip_shadow ? 1u : 0u;
     a.count = count ? 1u : 0u;
-    a.use_lb = (tn.shadow_lb && sc.lb_cells) ? 1u : 0u;
-    // 1. closest hit (fused: with the shading, the shadow rays and the spawn)
+    // 1. closest hit
     const bool prim_launch = g == 0 && use_prim;
     const int ccls = prim_launch ? WF_PRIMARY : WF_CLOSEST;
     a.disc_slot = (unsigned)ccls;
     prof_rays_[ccls] += n;
     WF_CHECK(pmark(stream, ccls, true));
-    if (fused) {
-      WF_CHECK(launch_fused(sc, cam, a, prim_launch, n, stream, count, tn));
-    } else if (sc.n_quads > 0) {
-      WF_CHECK(launch_closest_exh<true>(sc, cam, a, prim_launch, gen_lds, n, stream, tn));
-    } else {
-      WF_CHECK(launch_closest_exh<false>(sc, cam, a, prim_launch, gen_lds, n, stream, tn));
-    }
+    if (sc.n_quads > 0) WF_CHECK(launch_closest_exh<true>(sc, cam, a, prim_launch, gen_lds, n, stream, tn));
+    else WF_CHECK(launch_closest_exh<false>(sc, cam, a, prim_launch, gen_lds, n, stream, tn));
     WF_CHECK(pmark(stream, ccls, false));
-    // 2. prepare_computations + spawn (exhaustive pipeline)
-    if (!fused) {
-      WF_CHECK(pmark(stream, WF_PREP, true));
-      WF_LAUNCH(wf_prep, dim3(occupancy_grid(wf_prep, kWfBlock, 0, n)), dim3(kWfBlock), 0, stream, sc, cam, a);
-      WF_CHECK(hipGetLastError());
-      WF_CHECK(pmark(stream, WF_PREP, false));
-    }
-    if (!calibrated) {
+    // 2. prepare_computations + spawn
+    WF_CHECK(pmark(stream, WF_PREP, true));
+    WF_LAUNCH(wf_prep, dim3(occupancy_grid(wf_prep, kWfBlock, 0, n)), dim3(kWfBlock), 0, stream, sc, cam, a);
+    WF_CHECK(hipGetLastError());
+    WF_CHECK(pmark(stream, WF_PREP, false));
+    {  // the next generation's size and this one's shadow list, read back
       std::vector<unsigned> hr((size_t)kShards * kShardStride), hs(hr.size());
       WF_CHECK(hipMemcpyAsync(hr.data(), shard_cnt(g + 1, 0), hr.size() * sizeof(unsigned), hipMemcpyDeviceToHost,
                               stream));
@@ -1459,12 +1710,11 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
         nr += hr[(size_t)k * kShardStride] + hr[(size_t)k * kShardStride + 1];  // front + back (shard_append)
         ns += hs[(size_t)k * kShardStride];
       }
-      counts.rays[g + 1] = g < max_depth ? nr : 0;
-      counts.shadows[g] = ns;
+      rays[g + 1] = g < max_depth ? nr : 0;
+      shadows[g] = ns;
     }
-    if (fused) continue;
-    a.n_shadow = counts.shadows[g];
-    // 3. shadow rays (exhaustive pipeline)
+    a.n_shadow = shadows[g];
+    // 3. shadow rays
     if (a.n_shadow) {
       a.disc_slot = WF_SHADOW;
       prof_rays_[WF_SHADOW] += a.n_shadow;
@@ -1483,203 +1733,46 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
       WF_CHECK(hipGetLastError());
     }
   }
-  // the queues must hold exactly what was launched (calibrated frames): checked
-  // by the first parents combine, or by a launch of its own
-  WfCheckArgs ck{};
-  bool check_pending = calibrated;
-  if (calibrated) {
-    ck.n_gen = last + 1;
-    for (unsigned g = 0; g <= last + 1 && g < (unsigned)kMaxGen; ++g) {
-      ck.rays[g] = g < counts.rays.size() ? counts.rays[g] : 0;
-      ck.shadows[g] = g < counts.shadows.size() ? counts.shadows[g] : 0;
-    }
-  }
   if (forked) {  // join: the combine pass reads every generation's lighting terms
     WF_CHECK(hipEventRecord(join_ev_, sh_stream));
     WF_CHECK(hipStreamWaitEvent(stream, join_ev_, 0));
   }
-  // 4. combine, deepest generation first (fused: only the nodes with children)
+  // 4. combine, deepest generation first
   for (int g = (int)last; g >= 0; --g) {
     WfArgs a{};
     WfGenBuf& B = gens_[g];
-    a.rays = B.rays; a.nodes = B.nodes; a.surf = B.surf; a.parents = B.parents;
+    a.rays = B.rays; a.nodes = B.nodes; a.surf = B.surf;
     a.colors = (g == 0 && !averaged) ? d_out : B.colors;
     a.aa = aa;
-    a.rows = frame_real / aa / (cam.hsize ? cam.hsize : 1);
-    a.n_frames = n_frames; a.frame_rays = n0 / n_frames; a.frame_real = frame_real; a.frames = d_frames_;
+    a.rows = n0 / aa / (cam.hsize ? cam.hsize : 1);
+    a.n_frames = 1; a.frame_rays = n0; a.frame_real = n0;
     a.child_colors = gens_[g + 1].colors;
-    a.n = fused ? counts.shadows[g] : counts.rays[g];
+    a.n = rays[g];
     a.in_cnt = g == 0 ? nullptr : shard_cnt((unsigned)g, 0);
     a.in_cap = caps[g];
-    a.sh_cnt = shard_cnt((unsigned)g, 1);
-    a.sh_cap = list_caps[g];
     a.g = (unsigned)g; a.max_depth = max_depth;
     a.camera_mode = camera_mode ? 1u : 0u;
     a.row_block = row_block; a.shard = shard; a.n_shards = n_shards;
     if (a.n == 0) continue;
     WF_CHECK(pmark(stream, WF_COMBINE, true));
-    if (fused) {
-      WF_LAUNCH(wf_combine_parents, dim3(occupancy_grid(wf_combine_parents, kWfBlock, 0, a.n)), dim3(kWfBlock), 0,
-                stream, sc, cam, a, ck, d_shard_, check_pending ? d_fault_ : nullptr);
-      check_pending = false;
-    } else {
-      WF_LAUNCH(wf_combine, dim3(occupancy_grid(wf_combine, kWfBlock, 0, a.n)), dim3(kWfBlock), 0, stream, sc,
-                cam, a);
-    }
+    WF_LAUNCH(wf_combine, dim3(occupancy_grid(wf_combine, kWfBlock, 0, a.n)), dim3(kWfBlock), 0, stream, sc, cam, a);
     WF_CHECK(hipGetLastError());
     WF_CHECK(pmark(stream, WF_COMBINE, false));
-  }
-  if (check_pending) {
-    WF_LAUNCH(wf_check_counts, dim3(1), dim3(64), 0, stream, d_shard_, ck, d_fault_);
-    WF_CHECK(hipGetLastError());
   }
   if (averaged) {
-    const unsigned n_pix = n_frames * (frame_real / aa);
-    WF_CHECK(pmark(stream, WF_COMBINE, true));
-    WfArgs a{};
-    a.aa = aa; a.rows = frame_real / aa / cam.hsize;
-    a.n_frames = n_frames; a.frame_rays = n0 / n_frames; a.frame_real = frame_real; a.frames = d_frames_;
-    WF_LAUNCH(wf_average, dim3(occupancy_grid(wf_average, kWfBlock, 0, n_pix)), dim3(kWfBlock), 0, stream,
-                       a, cam.hsize, gens_[0].colors, n_pix, d_out);
-    WF_CHECK(hipGetLastError());
-    WF_CHECK(pmark(stream, WF_COMBINE, false));
-  }
-  if (ms_kernel) WF_CHECK(hipEventRecord(ev1_, stream));
-  if (!calibrated && !key.empty()) cache_[key] = counts;
-  if (stats || ms_kernel) {
-    WF_CHECK(hipStreamSynchronize(stream));
-    if (ms_kernel) WF_CHECK(hipEventElapsedTime(ms_kernel, ev0_, ev1_));
-  }
-  lr_.counts = counts;
-  lr_.last = last; lr_.L = L; lr_.n0 = n0;
-  lr_.counted = count; lr_.exact_disc = !bvh && !skip_shadow; lr_.bvh = bvh; lr_.fused = fused;
-  lr_.persist = false;
-  lr_.n_diag = (unsigned long long)sc.n_diag; lr_.n_gen = (unsigned long long)sc.n_gen;
-  lr_.n_planes = (unsigned long long)sc.n_planes; lr_.n_quads = (unsigned long long)sc.n_quads;
-  lr_.stream = stream;
-  if (stats) WF_CHECK(read_stats(stats));
-  return hipSuccess;
-}
-
-// The persistent frame kernel (rt_persist.hpp): one launch renders every
-// recursion depth and folds shade_hit's combine into the children's
-// delivery. Its trees are addressed by position (PsParent per heap node of a
-// root's recursion tree), sized here from the depth.
-hipError_t Wavefront::render_persist(const DevScene& sc, const DevCamera& cam, bool camera_mode,
-                                     const double* d_in_rays, unsigned n0, unsigned aa, unsigned max_depth,
-                                     unsigned row_block, unsigned shard, unsigned n_shards, double* d_out,
-                                     hipStream_t stream, DevStats* stats, float* ms_kernel, bool count,
-                                     const WfTuning& tn) {
-  const bool averaged = aa > 1;
-  const unsigned L = (unsigned)sc.n_lights;
-  WF_CHECK(ensure_misc((size_t)sc.n_diag));
-  if (!ps_ctr_) {  // zero once: every launch leaves its counters zeroed for the next one (ps_render)
-    WF_CHECK(hipMalloc(&ps_ctr_, sizeof(PsCounters)));
-    WF_CHECK(hipMemsetAsync(ps_ctr_, 0, sizeof(PsCounters), stream));
-  }
-  int dev = 0, n_cu = 0;
-  WF_CHECK(hipGetDevice(&dev));
-  WF_CHECK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-  n_cu = std::max(n_cu, 1);
-  // one workgroup per CU (the LDS image); small renders take fewer (two camera chunks each)
-  const unsigned n_chunks = (n0 + 63u) / 64u;
-  unsigned grid = std::max(1u, std::min((unsigned)n_cu, (n_chunks + 1u) / 2u));
-  if (tn.ps_grid > 0) grid = std::min((unsigned)tn.ps_grid, std::max(1u, n_chunks));
-  // heap-addressed trees: 2^d - 1 nodes per root may have children, at most 2^d
-  // rays of one root are queued or traced at once (an antichain of its tree)
-  const unsigned n_int = (1u << max_depth) - 1u;
-  const size_t leaves = (size_t)1 << max_depth;
-  const size_t per_tree = 64 * ((size_t)n_int * sizeof(PsParent) + leaves * sizeof(PsRay));
-  unsigned trees =
-      (unsigned)std::min<size_t>(kPsMaxTrees, std::max<size_t>(4, kPsBudget / ((size_t)n_cu * per_tree)));
-  if (tn.ps_trees > 0) trees = (unsigned)tn.ps_trees;
-  const size_t q_cap = (size_t)trees * 64 * leaves + kPsSpare;
-  WF_CHECK(grow(ps_rings_, ps_rings_cap_, (size_t)grid * q_cap));
-  WF_CHECK(grow(ps_parents_, ps_parents_cap_, std::max<size_t>(1, (size_t)grid * trees * 64 * n_int)));
-  WF_CHECK(grow(ps_lists_, ps_lists_cap_, std::max<size_t>(1, (size_t)grid * trees * 64 * n_int)));
-  if (averaged) WF_CHECK(ensure_gen(0, n0, L, 0, true));
-  // the scene image (as the generation pipeline's fused kernels)
-  constexpr size_t limit = kWfLdsLimit - kPsSchedBytes;
-  const bool use_lb = tn.shadow_lb && sc.lb_cells;
-  const size_t dl = use_lb ? delta_lds_bytes(sc) : 0;
-  PsArgs a{};
-  size_t dyn = 0;
-  int image = 1;
-  if (tn.image == 0 && pair_lds_bytes(sc) <= limit) {
-    image = 14;
-    dyn = pair_lds_bytes(sc);
-    if (dl && dyn + dl <= limit) { a.lds_flags |= kLdsDeltas; dyn += dl; }
-  } else if (tn.image != 1 && sc.bvh_depth <= kLaneLdsDepth) {
-    image = 3;
-    const size_t room = limit - (size_t)kLaneLdsDepth * kTraceBlock * 4;
-    if (dl && dl <= room && (!tn.treelet || tn.treelet_deltas)) { a.lds_flags |= kLdsDeltas; dyn = dl; }
-    if (tn.treelet) {
-      a.n_top = (unsigned)std::min<size_t>((size_t)sc.n_bvh, (room - dyn) / sizeof(BvhNode));
-      dyn += (size_t)a.n_top * sizeof(BvhNode);
-    }
-  } else if (dl && dl <= limit) {
-    a.lds_flags |= kLdsDeltas;
-    dyn = dl;
-  }
-  a.rings = ps_rings_;
-  a.parents = ps_parents_;
-  a.lists = ps_lists_;
-  a.ctr = ps_ctr_;
-  a.cnt = d_cnt_;
-  a.out = averaged ? gens_[0].colors : d_out;
-  a.in_rays = d_in_rays;
-  a.fault = d_fault_;
-  a.q_cap = (unsigned)q_cap;
-  a.n_int = n_int;
-  a.trees = trees;
-  a.n0 = n0;
-  a.max_depth = max_depth;
-  a.camera_mode = camera_mode ? 1u : 0u;
-  a.aa = aa;
-  a.rows = n0 / aa / (cam.hsize ? cam.hsize : 1);
-  a.row_block = row_block; a.shard = shard; a.n_shards = n_shards;
-  a.use_lb = use_lb ? 1u : 0u;
-  a.skip_shadow = tn.skip_shadow ? 1u : 0u;
-  a.count = count ? 1u : 0u;
-  a.policy = (unsigned)tn.ps_policy;
-  if (count) WF_CHECK(hipMemsetAsync(d_cnt_, 0, sizeof(WfCounters), stream));
-  if (ms_kernel) WF_CHECK(hipEventRecord(ev0_, stream));
-  if (profiling_) ++pframes_;
-  prof_rays_[0] = prof_rays_[1] = prof_rays_[2] = 0;
-  prof_rays_[WF_PRIMARY] = n0;
-  const bool quads = sc.n_fx_quads > 0 || sc.n_obvh > 0;
-  WF_CHECK(pmark(stream, WF_CLOSEST, true));
-  hipEvent_t e0 = t_ev_start, e1 = t_ev_stop;
-  if (e0) ++t_ev_used;
-  if (image == 14) WF_CHECK(ps_launch_lds(sc, cam, a, quads, count, grid, dyn, stream, e0, e1));
-  else WF_CHECK(ps_launch_global(sc, cam, a, image, quads, count, grid, dyn, stream, e0, e1));
-  WF_CHECK(pmark(stream, WF_CLOSEST, false));
-  if (averaged) {  // Color::average of each pixel's samples (color.rs:26-33)
     const unsigned n_pix = n0 / aa;
     WF_CHECK(pmark(stream, WF_COMBINE, true));
-    WfArgs wa{};
-    wa.aa = aa;
-    wa.rows = n_pix / cam.hsize;
-    WF_LAUNCH(wf_average, dim3(occupancy_grid(wf_average, kWfBlock, 0, n_pix)), dim3(kWfBlock), 0, stream, wa,
+    WfArgs a{};
+    a.aa = aa; a.rows = n0 / aa / cam.hsize;
+    a.n_frames = 1; a.frame_rays = n0; a.frame_real = n0;
+    WF_LAUNCH(wf_average, dim3(occupancy_grid(wf_average, kWfBlock, 0, n_pix)), dim3(kWfBlock), 0, stream, a,
               cam.hsize, gens_[0].colors, n_pix, d_out);
     WF_CHECK(hipGetLastError());
     WF_CHECK(pmark(stream, WF_COMBINE, false));
   }
-  if (ms_kernel) WF_CHECK(hipEventRecord(ev1_, stream));
-  if (stats || ms_kernel) {
-    WF_CHECK(hipStreamSynchronize(stream));
-    if (ms_kernel) WF_CHECK(hipEventElapsedTime(ms_kernel, ev0_, ev1_));
-  }
-  last_bvh_ = true;
-  last_fused_ = true;
-  last_persist_ = true;
-  lr_.counts = Counts{};
-  lr_.last = max_depth; lr_.L = L; lr_.n0 = n0;
-  lr_.counted = count; lr_.exact_disc = false; lr_.bvh = true; lr_.fused = true; lr_.persist = true;
-  lr_.n_diag = (unsigned long long)sc.n_diag; lr_.n_gen = (unsigned long long)sc.n_gen;
-  lr_.n_planes = (unsigned long long)sc.n_planes; lr_.n_quads = (unsigned long long)sc.n_quads;
-  lr_.stream = stream;
-  if (stats) WF_CHECK(read_stats(stats));
+  lr_.rays = rays;
+  lr_.shadows = shadows;
+  lr_.last = last;
   return hipSuccess;
 }
 
@@ -1689,20 +1782,13 @@ hipError_t Wavefront::read_stats(DevStats* out) {
   WF_CHECK(hipStreamSynchronize(lr_.stream));
   WfCounters hc;
   WF_CHECK(hipMemcpy(&hc, d_cnt_, sizeof hc, hipMemcpyDeviceToHost));
+  std::vector<unsigned> counts;
+  WF_CHECK(last_counts(counts));
   DevStats s{};
   unsigned long long rays = 0, hits = 0, traced_shadows = 0;
-  if (lr_.persist) {  // one launch: the rays per depth come from its tallies
-    rays = lr_.n0;
-    for (unsigned g = 0; g <= lr_.last && g < (unsigned)kMaxGen; ++g) {
-      rays += (unsigned long long)hc.n_refl[g] + hc.n_refr[g];
-      hits += hc.n_hit[g];
-      s.rays_reflect += hc.n_refl[g];
-      s.rays_refract += hc.n_refr[g];
-    }
-  }
-  for (unsigned g = 0; !lr_.persist && g <= lr_.last && g < lr_.counts.rays.size(); ++g) {
-    rays += lr_.counts.rays[g];
-    if (!lr_.fused) traced_shadows += lr_.counts.shadows[g];
+  for (unsigned g = 0; g < counts.size() && g < (unsigned)kMaxGen; ++g) {
+    rays += counts[g];
+    if (!lr_.fused && g < lr_.shadows.size()) traced_shadows += lr_.shadows[g];
     hits += hc.n_hit[g];
     s.rays_reflect += hc.n_refl[g];
     s.rays_refract += hc.n_refr[g];

@@ -33,12 +33,10 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
-#include <map>
 #include <string>
 #include <vector>
 
 #include "rt_layout.hpp"
-#include "rt_persist.hpp"
 
 namespace rtamd {
 
@@ -93,8 +91,6 @@ enum WfFlags : unsigned { WF_EXHAUSTIVE = 1u, WF_COUNT = 2u };
 // concurrent renders of different scenes never see each other's settings.
 struct WfTuning {
   int accel = 1;           // 1 = exact-culling BVH fast path (unless the exhaustive loop is asked for)
-  int persist = 0;         // 1 = the persistent frame kernel (rt_persist.hip) when max_depth <= kPsMaxDepth
-                           //     (opt-in: measured ~2x slower than the generation pipeline)
   int skip_shadow = 1;     // 1 = the fast path leaves out shadow rays that cannot change the colour
   int shadow_lb = 1;       // 1 = shadow rays through the light buffer when the scene has one
   int image = 0;           // 0 = automatic scene image of the fast-path kernels, 3 / 1 = global memory
@@ -104,10 +100,8 @@ struct WfTuning {
   int adaptive_block = 0;  // generation pipeline: 1 = small trace launches spread over every CU
   int prim_lane = 0;       // fast path: 1 = primary rays by the per-lane pair traversal (LDS image) instead
                            //     of the wave traversal with shared-origin records
-  int corrupt_calibration = 0;  // test hook: generation 1 of a calibrated frame launched one ray short
-  int ps_trees = 0;        // persistent kernel: tree slots per workgroup (0 = from the memory budget, at most 32)
-  int ps_policy = 0;       // persistent kernel: when a wave takes fewer than 64 queued rays (PsArgs::policy)
-  int ps_grid = 0;         // persistent kernel: workgroups (0 = one per CU, fewer for small renders)
+  int arena_pct = 100;     // test hook: the fast path's queue arenas sized to this percentage of the hint,
+                           //     shrinking them (< 100: forces overflows, DESIGN.md "Device-sized generations")
   int d2h = 1;             // host-canvas copies: 1 = pin the caller's buffer for the call and DMA into it, 0 = pinned chunks
 };
 // Applies `key` = `value` to `t`: 1 = applied, 0 = not a render-time key, -1 = bad value.
@@ -133,11 +127,6 @@ struct alignas(128) WfWorkRow {
   unsigned long long boxes[3];  // BVH mode: child-box tests executed (lanes x boxes)
   unsigned long long sh_rays[2];   // fused kernels: shadow rays traced, [0] primary / [1] secondary launches
   unsigned long long sh_tests[2];  // fused kernels: shadow sphere tests executed, per launch class
-  // persistent kernel (counted launches): its work items and where its waves' time goes
-  unsigned long long ps_items[2];   // chunks taken: [0] camera chunks, [1] queued-ray chunks
-  unsigned long long ps_lanes[2];   // rays in them (lane use of the items = lanes / (64 x items))
-  unsigned long long ps_cycles[6];  // shader clocks: [0] getting work, [1] trace, [2] shading, [3] spawn + publish,
-                                    // [4] tree combine
 };
 // Fused launches hand out their rays in chunks of 64 (one wave-iteration) from
 // per-XCD counters, kChunkClasses per generation, each on a 128-B line.
@@ -167,21 +156,6 @@ struct WfCounters {
     for (int r = 0; r < kWorkRows; ++r) t += work[r].sh_rays[c];
     return t;
   }
-  unsigned long long ps_items(int c) const {
-    unsigned long long t = 0;
-    for (int r = 0; r < kWorkRows; ++r) t += work[r].ps_items[c];
-    return t;
-  }
-  unsigned long long ps_lanes(int c) const {
-    unsigned long long t = 0;
-    for (int r = 0; r < kWorkRows; ++r) t += work[r].ps_lanes[c];
-    return t;
-  }
-  unsigned long long ps_cycles(int c) const {
-    unsigned long long t = 0;
-    for (int r = 0; r < kWorkRows; ++r) t += work[r].ps_cycles[c];
-    return t;
-  }
   unsigned long long sh_tests(int c) const {
     unsigned long long t = 0;
     for (int r = 0; r < kWorkRows; ++r) t += work[r].sh_tests[c];
@@ -194,17 +168,51 @@ struct WfGeo {  // 80 B: the lighting() inputs of a hit (comps.over_point, norma
   int32_t obj;
   int32_t pad;
 };
-struct WfGenBuf {  // grow-only; the fast path allocates rays, colors and parents only
+struct WfGenBuf {  // grow-only, the exhaustive pipeline's per-generation arrays
   WfRay* rays = nullptr;
   double* colors = nullptr;
-  ParentRec* parents = nullptr;     // fast path: nodes with children (sharded)
   WfHit* hits = nullptr;
   WfNode* nodes = nullptr;
   int32_t* shadow_nodes = nullptr;  // shadow list of the generation (node slot * L + light, sharded)
   WfGeo* geo = nullptr;              // per node slot: what the shadow trace needs to evaluate lighting()
   double* surf = nullptr;            // lighting() per node slot and light (3 doubles)
-  size_t cap_rays = 0, cap_colors = 0, cap_parents = 0, cap_hits = 0, cap_nodes = 0, cap_list = 0, cap_geo = 0,
-         cap_surf = 0;
+  size_t cap_rays = 0, cap_colors = 0, cap_hits = 0, cap_nodes = 0, cap_list = 0, cap_geo = 0, cap_surf = 0;
+};
+
+// Device-sized generations (the fast path; DESIGN.md "Device-sized
+// generations"). The host never learns a generation's ray count before its
+// launch: the launch of generation g reads it from the queue counters, sizes
+// the sharded regions of generation g+1 and of its own parent list from it,
+// and places them in three per-workspace arenas (colours, parent records, and
+// two ping-pong ray buffers). Generation g's place, written by generation
+// g-1's launch (g = 0: by wf_frame_init):
+struct WfGenTab {
+  unsigned cap;                   // per-region capacity of its rays / colours (0: generation 0, dense)
+  unsigned pad;
+  unsigned long long color_off;   // its first colour slot in the colour arena
+  unsigned long long par_off;     // its parent list's first record in the parent arena
+};
+// A generation that does not fit the arenas spawns no children (the frame is
+// then incomplete): its launch raises `overflow` in this host-mapped record of
+// the workspace with what it needed. Every frame's last combine also records
+// the frame's ray count per generation, from which the host sizes the arenas
+// of later frames (WfSizing); nothing waits for it.
+struct WfHostRec {
+  int overflow;
+  int pad[3];
+  unsigned long long need_colors, need_parents, need_rays;  // of the generation that overflowed
+  unsigned long long frames;   // frames recorded (the counts below are the last one's)
+  unsigned n_real;             // root rays (without the padding of a batch)
+  unsigned n_gens;             // generations counted (max_depth + 1)
+  unsigned counts[kMaxGen];    // rays of each generation
+};
+// Arena sizes learned per scene (every workspace of a scene reads and
+// updates them under the scene's lock): per root ray, the most secondary
+// work any frame needed (rho = sum of the ray counts of the generations that
+// may spawn children / root rays; mu = largest generation / root rays).
+struct WfSizing {
+  double rho = 0.0, mu = 0.0;
+  int branch = 2;  // children per ray at most: 0 no reflective or transparent material, 1 never both, 2 otherwise
 };
 
 // A batch of frames rendered by one pass of the generation pipeline (camera
@@ -258,6 +266,17 @@ struct WfArgs {
   unsigned n_frames;    // camera mode: frames in this pass (1: cam / colors; > 1: `frames`)
   unsigned frame_rays, frame_real;  // n_frames > 1: generation-0 slots per frame, root rays per frame
   const FrameTable* frames;         // n_frames > 1: the device copy of the batch's cameras and canvases
+  // device-sized generations (fast path): bind_generation fills n, in_cap,
+  // out_cap, sh_cap, rays, next_rays, colors and parents from the tables
+  unsigned dev_sized;
+  unsigned colors_direct;           // generation 0's colours go to `colors` as given (the output)
+  WfGenTab* gtab;                   // [kMaxGen + 1]
+  unsigned* gsh;                    // [kMaxGen]: per-region capacity of generation g's parent list
+  WfRay* ray_buf[2];                // generation g's rays in ray_buf[g & 1]
+  double* color_base;
+  ParentRec* par_base;
+  unsigned long long color_cap, par_cap, ray_cap;  // colour slots, parent records, ray slots per buffer
+  WfHostRec* hrec;                  // device address of the workspace's host-mapped record
 };
 
 // Per-kernel-class timing of the last frame (profiling mode only).
@@ -271,8 +290,6 @@ struct WfProfile {
   double sh_rays[2], sh_tests[2];  // fused frames: shadow rays / sphere tests inside the primary / secondary launches
   int bvh;          // the last frame traversed the BVH
   int fused;        // the last frame ran the fused pipeline
-  int persist;      // the last frame ran the persistent frame kernel (one launch; its time is the closest class)
-  double ps_items[2], ps_lanes[2], ps_cycles[6];  // persistent kernel, counted frame (WfWorkRow)
 };
 
 class Wavefront {
@@ -291,50 +308,61 @@ class Wavefront {
   hipError_t last_profile(WfProfile* out);
   // Render n0 root rays (camera pixels x `aa` samples of a shard, or explicit
   // rays) into `out` (n0/aa*3 doubles, device; AA samples are averaged like
-  // Color::average). Counts of a signature seen before are reused (fully
-  // asynchronous); otherwise each generation is sized by a synchronous count
-  // read-back. stats (host) may be null. `solo`: no other workspace renders
-  // concurrently (then the shadow traces take the side stream).
+  // Color::average). The fast path (BVH) is fully asynchronous: every
+  // generation sizes itself on the device (WfGenTab); `sz` sizes the arenas.
+  // The exhaustive pipeline (WF_EXHAUSTIVE or a scene without hierarchies)
+  // reads each generation's count back (synchronous). stats (host) may be
+  // null. `solo`: no other workspace renders concurrently (then the
+  // exhaustive shadow traces take the side stream).
   // `flags`: WF_EXHAUSTIVE runs the reference's every-shape loop (exact
   // sphere_disc_ge0); WF_COUNT counts the reference's rays of this render
   // (read later by read_stats). A non-null `stats` implies WF_COUNT and
   // synchronises to fill it.
   hipError_t render(const DevScene& sc, const DevCamera& cam, bool camera_mode, const double* d_in_rays,
                     unsigned n0, unsigned aa, unsigned max_depth, unsigned row_block, unsigned shard,
-                    unsigned n_shards, double* d_out, hipStream_t stream, const std::string& signature,
-                    DevStats* stats, float* ms_kernel, const WfTuning& tn, bool solo = true, unsigned flags = 0,
+                    unsigned n_shards, double* d_out, hipStream_t stream, WfSizing& sz, DevStats* stats,
+                    float* ms_kernel, const WfTuning& tn, bool solo = true, unsigned flags = 0,
                     const FrameTable* batch = nullptr, unsigned n_frames = 1);
   // The counters of the last render (rendered with WF_COUNT); synchronises its stream.
   hipError_t read_stats(DevStats* out);
-  // A generation's actual queue count differed from the calibrated launch size
-  // (a device-side check of every calibrated frame, wf_check_counts). Sticky
-  // until clear_fault(), which also drops the calibration.
-  // 1: queue check (generation pipeline); 2 / 3: a wait of the persistent
-  // frame kernel exceeded its time bound (rt_persist.hip)
-  int fault() const { return h_fault_ ? *(volatile int*)h_fault_ : 0; }
-  // words 1.. of the fault record: what the faulting wave saw (rt_persist.hip ps_fault)
-  static constexpr int kFaultWords = 32;
-  int fault_word(int k) const { return h_fault_ && k < kFaultWords ? ((volatile int*)h_fault_)[k] : 0; }
-  void clear_fault() {
-    if (h_fault_) *(volatile int*)h_fault_ = 0;
-    cache_.clear();
-  }
+  // A fast-path frame of this workspace overflowed its arenas (WfHostRec):
+  // that frame is incomplete. take_overflow() clears the flag and grows the
+  // arenas past what the overflowing generation asked for (the next frame
+  // fits at least that generation); it returns whether the flag was set.
+  // Call it only once the frame has completed (after a synchronisation).
+  bool overflowed() const { return h_rec_ && ((volatile WfHostRec*)h_rec_)->overflow != 0; }
+  hipError_t take_overflow(bool* was);
+  // The learned sizes from this workspace's last recorded frame (non-blocking:
+  // the record of a frame still in flight may be stale).
+  void learn(WfSizing& sz) const;
+
  private:
-  // the persistent frame kernel (rt_persist.hip): one launch per render
-  hipError_t render_persist(const DevScene& sc, const DevCamera& cam, bool camera_mode, const double* d_in_rays,
-                            unsigned n0, unsigned aa, unsigned max_depth, unsigned row_block, unsigned shard,
-                            unsigned n_shards, double* d_out, hipStream_t stream, DevStats* stats, float* ms_kernel,
-                            bool count, const WfTuning& tn);
-  PsRay* ps_rings_ = nullptr;
-  PsParent* ps_parents_ = nullptr;
-  PsCounters* ps_ctr_ = nullptr;
-  uint16_t* ps_lists_ = nullptr;
-  size_t ps_rings_cap_ = 0, ps_parents_cap_ = 0, ps_lists_cap_ = 0;  // records
-  hipError_t ensure_gen(size_t g, size_t slots, size_t n_lights, size_t list_slots, bool fused);
+  hipError_t render_fast(const DevScene& sc, const DevCamera& cam, bool camera_mode, const double* d_in_rays,
+                         unsigned n0, unsigned frame_real, unsigned aa, unsigned max_depth, unsigned row_block,
+                         unsigned shard, unsigned n_shards, double* d_out, hipStream_t stream, WfSizing& sz,
+                         bool count, bool skip_shadow, const WfTuning& tn, const FrameTable* batch,
+                         unsigned n_frames);
+  hipError_t render_exhaustive(const DevScene& sc, const DevCamera& cam, bool camera_mode, const double* d_in_rays,
+                               unsigned n0, unsigned aa, unsigned max_depth, unsigned row_block, unsigned shard,
+                               unsigned n_shards, double* d_out, hipStream_t stream, bool count, bool skip_shadow,
+                               const WfTuning& tn, bool solo);
+  hipError_t ensure_gen(size_t g, size_t slots, size_t n_lights, size_t list_slots);
   hipError_t ensure_misc(size_t n_diag, unsigned n_frames = 1);
+  hipError_t ensure_arenas(unsigned long long colors, unsigned long long parents, unsigned long long rays,
+                           bool exact);
   // shard counters: generation g's rays (q = 0) / shadow list (q = 1)
   unsigned* shard_cnt(unsigned g, unsigned q) { return d_shard_ + ((size_t)g * 2 + q) * kShards * kShardStride; }
   std::vector<WfGenBuf> gens_;
+  // the fast path's arenas (grow-only; arena_pct < 100 shrinks them, a test hook)
+  double* colors_ = nullptr;
+  ParentRec* parents_ = nullptr;
+  WfRay* rays_[2] = {nullptr, nullptr};
+  unsigned long long color_cap_ = 0, par_cap_ = 0, ray_cap_ = 0;
+  int squeezed_pct_ = 100;  // the arena_pct the arenas were last shrunk to
+  WfGenTab* d_gtab_ = nullptr;
+  unsigned* d_gsh_ = nullptr;
+  WfHostRec* h_rec_ = nullptr;  // host-mapped (hipHostMallocMapped)
+  WfHostRec* d_rec_ = nullptr;  // its device address
   WfCounters* d_cnt_ = nullptr;
   unsigned* d_shard_ = nullptr;  // kMaxGen x 2 x kShards counters, kShardStride apart
   PrimRec* d_prim_ = nullptr;
@@ -348,20 +376,16 @@ class Wavefront {
   hipEvent_t fork_ev_[kMaxGen] = {};
   hipEvent_t join_ev_ = nullptr;
   hipError_t ensure_side();
-  struct Counts {
-    std::vector<unsigned> rays, shadows;
-  };
-  std::map<std::string, Counts> cache_;
-  int* h_fault_ = nullptr;  // host-mapped flag written by wf_check_counts
-  int* d_fault_ = nullptr;  // its device address
   struct LastRender {       // what read_stats needs of the last render
-    Counts counts;
-    unsigned last = 0, L = 0, n0 = 0;
-    bool counted = false, exact_disc = false, bvh = false, fused = false, persist = false;
+    std::vector<unsigned> rays, shadows;  // exhaustive pipeline: counts per generation (read back)
+    unsigned last = 0, L = 0, n0 = 0, max_depth = 0;
+    bool counted = false, exact_disc = false, bvh = false, fused = false;
     unsigned long long n_diag = 0, n_gen = 0, n_planes = 0, n_quads = 0;
     hipStream_t stream = nullptr;
   } lr_;
-  bool last_bvh_ = false, last_fused_ = false, last_persist_ = false;
+  // generation counts of the last render (fast path: from the host-mapped record; synchronises)
+  hipError_t last_counts(std::vector<unsigned>& rays);
+  bool last_bvh_ = false, last_fused_ = false;
   bool profiling_ = false;
   int pmask_ = (1 << WF_NCLASS) - 1;
   std::vector<hipEvent_t> pev_;        // event pool (pairs)

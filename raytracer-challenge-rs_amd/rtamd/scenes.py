@@ -129,6 +129,15 @@ def c3(width=1920, height=1080, n_spheres=1000, seed=0x5EED0003):
     return w, _camera(width, height, PI / 3.0, (0, 3, -12), (0, 1, 5)), 5
 
 
+def c3_orbit(k, n=64, width=1920, height=1080, arc=0.8):
+    """Camera k of n along an arc of `arc` radians around C3's look-at point
+    (0, 1, 5), at C3's distance (17) and height: the moving camera of an
+    animation over the C3 scene (frame k = 0 .. n-1; the middle one is close to
+    C3's own camera)."""
+    a = -arc / 2.0 + arc * k / max(n - 1, 1)
+    return _camera(width, height, PI / 3.0, (17.0 * math.sin(a), 3.0, 5.0 - 17.0 * math.cos(a)), (0, 1, 5))
+
+
 def c5(width=4096, height=4096, n_spheres=9996, seed=0x5EED0005):
     """C5: room of 4 planes (reflect-refract.yml:55-104 style) + spheres, 2 lights, depth 8."""
     rng = SplitMix64(seed)

@@ -71,8 +71,8 @@ def _check_pixels(rt, oracle, ow, cam, depth, frame, n, seed):
 
 def test_c3_full_frame_frames_in_flight_equal(rt):
     """bench.py's timed configuration: 4 frames in flight on 4 render streams
-    (each its own workspace, calibrated launch sizes), every frame bitwise equal
-    to the exhaustive frame."""
+    (each its own workspace, device-sized generations), every frame bitwise
+    equal to the exhaustive frame."""
     import torch
     from rtamd import scenes
     w, cam, depth = scenes.c3()
@@ -165,36 +165,69 @@ def test_render_multi_one_device_equals_render(rt):
     assert st4["rays_primary"] == 4 * 200 * 113
 
 
-@pytest.mark.parametrize("via_check", [False, True])
-def test_queue_check_reports_miscalibration(rt, via_check):
-    """The generation pipeline (persist off): a calibrated frame whose queue
-    counts differ from its launch sizes (here forced by a test hook that
-    launches generation 1 one ray short) fails the next call, or
-    rt_scene_check, with RT_ERR_HIP instead of silently dropping rays; the
-    library then recalibrates."""
+def test_arena_overflow_sync_rerenders_async_reports(rt):
+    """Device-sized generations: the queue arenas are sized from a
+    hint, and a generation that does not fit spawns no children and raises the
+    workspace's overflow record. Forced here by shrinking the arenas to 2 % of
+    the hint (test hook arena_pct):
+    - a synchronous render (rt_render to a host canvas) notices it, grows the
+      arenas and renders again: its frame is complete;
+    - an asynchronous render (rt_render_shard_device) leaves an incomplete
+      frame, which rt_scene_check (or the next call) reports; the arenas have
+      grown, so the next frame is complete."""
     import torch
     from rtamd import scenes
     w, cam, depth = scenes.c3(96, 54, n_spheres=200)
     exact, _ = _device_frame(cam, w, depth, True)
-    w.tune("persist", 0)
+    w.tune("arena_pct", 2)
+    try:
+        host, _ = cam.render(w, depth, want_stats=False)
+    finally:
+        w.tune("arena_pct", 100)
+    assert host.to_numpy().tobytes() == exact.cpu().numpy().tobytes()
     st = rt.render_stream(False)
     buf = torch.empty_like(exact)
-    cam.render_shard_device(w, depth, 8, 0, 1, buf.data_ptr(), st.cuda_stream, False)  # calibrates
-    w.tune("corrupt_calibration", 1)
+    w.tune("arena_pct", 2)
     try:
         cam.render_shard_device(w, depth, 8, 0, 1, buf.data_ptr(), st.cuda_stream, False)
         torch.cuda.synchronize()
     finally:
-        w.tune("corrupt_calibration", 0)
-    with pytest.raises(rt.RtError, match="queue check"):
-        if via_check:
-            w.check()
-        else:
-            cam.render_shard_device(w, depth, 8, 0, 1, buf.data_ptr(), st.cuda_stream, False)
-    cam.render_shard_device(w, depth, 8, 0, 1, buf.data_ptr(), st.cuda_stream, False)  # recalibrates
+        w.tune("arena_pct", 100)
+    assert not torch.equal(buf, exact)  # incomplete: the children of an overflowing generation were dropped
+    with pytest.raises(rt.RtError, match="overflow"):
+        w.check()
+    cam.render_shard_device(w, depth, 8, 0, 1, buf.data_ptr(), st.cuda_stream, False)
     torch.cuda.synchronize()
     w.check()
     assert torch.equal(buf, exact)
+
+
+def test_first_seen_cameras_async_bitwise(rt):
+    """A fresh scene, 8 distinct cameras per batch on 4 streams, no render
+    before: every call is asynchronous from its first frame (no calibration,
+    device-sized generations) and every frame equals its exhaustive frame."""
+    import math
+    import torch
+    from rtamd import scenes
+    w, cam0, depth = scenes.c3(320, 180, n_spheres=600)
+    cams = []
+    for k in range(32):
+        c = rt.Camera(320, 180, math.pi / 3.0)
+        a = 2 * math.pi * k / 32
+        c.set_transform(rt.view_transform(rt.Point(14 * math.sin(a), 2.5 + 0.1 * k, -14 * math.cos(a)),
+                                          rt.Point(0, 1, 0), rt.Vector(0, 1, 0)))
+        cams.append(c)
+    streams = [rt.render_stream(False) for _ in range(4)]
+    bufs = [torch.full((180, 320, 3), -1.0, dtype=torch.float64, device="cuda") for _ in cams]
+    torch.cuda.synchronize()
+    for b in range(4):
+        rt.render_frames_device(w, cams[8 * b:8 * b + 8], depth, 8, 0, 1, [x.data_ptr() for x in bufs[8 * b:8 * b + 8]],
+                                streams[b].cuda_stream)
+    torch.cuda.synchronize()
+    w.check()
+    for k, c in enumerate(cams):
+        exact, _ = _device_frame(c, w, depth, True)
+        assert torch.equal(bufs[k], exact), k
 
 
 @pytest.mark.parametrize("glass", [False, True])

@@ -22,8 +22,6 @@ def _targs(n, name):
 def klass(n):
     """Kernel class of a demangled name: primary / closest / shadow / prep /
     combine / frame (wf_frame_init: one per rendered frame)."""
-    if "ps_render<" in n:  # the persistent frame kernel: the whole frame in one launch
-        return "persist"
     if "wf_trace_fused<" in n:  # fused generation: closest hit + shading + shadow rays + spawn
         return "primary" if _targs(n, "wf_trace_fused")[0] == "true" else "closest"
     if "wf_trace_closest_bvh<" in n:
@@ -63,7 +61,7 @@ for d in a.dirs:
             c = klass(r["Kernel_Name"])
             if c is None:
                 continue
-            if c in ("frame", "persist"):  # one frame_init or one ps_render dispatch per rendered frame
+            if c == "frame":  # one frame_init dispatch per rendered frame (batch)
                 seen.add(r["Dispatch_Id"])
             if c == "frame":
                 continue
