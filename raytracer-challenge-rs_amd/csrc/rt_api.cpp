@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -132,33 +133,46 @@ struct rt_scene {
   DevScene dev{};
   // device allocations
   void* d_blob = nullptr;       // trace + shade + light records
-  double* d_out = nullptr;      // cached output for host-buffer entry points
-  size_t out_cap = 0;           // doubles
-  double* d_in = nullptr;       // cached input for batch entry points
-  size_t in_cap = 0;
-  // rt_render_ppm: the device PPM text and its row lengths / offsets
-  char* d_ppm = nullptr;
-  size_t ppm_cap = 0;
-  void* d_ppm_rows = nullptr;
-  size_t ppm_rows_cap = 0;  // rows
-  // device-to-host copies into caller memory go through two pinned chunks
-  void* h_stage[2] = {nullptr, nullptr};
-  hipEvent_t stage_ev[2] = {nullptr, nullptr};
-  hipStream_t stream = nullptr;
-  std::mutex mu;  // one host call at a time per scene (the workspace pool)
+  hipStream_t stream = nullptr;  // rt_render_multi's stream on this device
+  // Host-buffer entry points (rt_render*, rt_render_ppm, the batch calls) run
+  // in a context of their own, taken from this pool for the call: a private
+  // stream, device buffers for the input and output, and the pinned chunks of
+  // the device-to-host copy. The scene's lock is held only while a call takes
+  // or returns a context and while it enqueues work; its waits on the device
+  // and its copies to the host run unlocked, so threads rendering one scene
+  // overlap (each on its own stream and workspace).
+  struct HostCtx {
+    hipStream_t stream = nullptr;
+    double* d_out = nullptr;  // output (doubles)
+    size_t out_cap = 0;
+    double* d_in = nullptr;   // batch input
+    size_t in_cap = 0;
+    char* d_ppm = nullptr;    // rt_render_ppm: the text and its row lengths / offsets
+    size_t ppm_cap = 0;
+    void* d_ppm_rows = nullptr;
+    size_t ppm_rows_cap = 0;  // rows
+    void* h_stage[2] = {nullptr, nullptr};  // device-to-host copies into caller memory: two pinned chunks
+    hipEvent_t stage_ev[2] = {nullptr, nullptr};
+    bool busy = false;
+  };
+  std::deque<HostCtx> ctxs;  // deque: a context's address survives the pool's growth
+  std::mutex mu;  // the workspace and context pools, tuning, sizing (held only to enqueue)
   // Wavefront workspaces (queues grow on demand), one per stream in use, at
-  // most kMaxWorkspaces: renders issued on different streams run concurrently
-  // on the device (frames in flight). A workspace taken over by
-  // another stream is reused in stream order: the new stream first waits on
-  // the event recorded after the workspace's last render.
+  // most kMaxWorkspaces unpinned: renders issued on different streams run
+  // concurrently on the device (frames in flight). A workspace
+  // taken over by another stream is reused in stream order: the new stream
+  // first waits on the event recorded after the workspace's last render. A
+  // synchronous call pins its workspace until it has read it back (its
+  // counters, its overflow record), so no other stream takes it over meanwhile.
   struct WfSlot {
     std::unique_ptr<Wavefront> wf;
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
     unsigned long long tick = 0;
+    int pins = 0;
   };
   static constexpr size_t kMaxWorkspaces = 8;
-  std::vector<WfSlot> wfs;
+  std::deque<WfSlot> wfs;
   unsigned long long tick = 0;
   WfSlot* last_wf = nullptr;
   bool prof_on = false;
@@ -192,18 +206,45 @@ struct rt_scene {
   ~rt_scene() {
     for (WfSlot& w : wfs)
       if (w.done) (void)hipEventDestroy(w.done);
-    for (int k = 0; k < 2; ++k) {
-      if (h_stage[k]) (void)hipHostFree(h_stage[k]);
-      if (stage_ev[k]) (void)hipEventDestroy(stage_ev[k]);
+    for (HostCtx& c : ctxs) {
+      if (c.stream) {
+        (void)hipStreamSynchronize(c.stream);
+        (void)hipStreamDestroy(c.stream);
+      }
+      (void)hipFree(c.d_out); (void)hipFree(c.d_in); (void)hipFree(c.d_ppm); (void)hipFree(c.d_ppm_rows);
+      for (int k = 0; k < 2; ++k) {
+        if (c.h_stage[k]) (void)hipHostFree(c.h_stage[k]);
+        if (c.stage_ev[k]) (void)hipEventDestroy(c.stage_ev[k]);
+      }
     }
+  }
+  // A host context for one call (under `mu`); returned by release_ctx.
+  hipError_t take_ctx(HostCtx** out) {
+    for (HostCtx& c : ctxs)
+      if (!c.busy) {
+        c.busy = true;
+        *out = &c;
+        return hipSuccess;
+      }
+    ctxs.emplace_back();
+    HostCtx& c = ctxs.back();
+    const hipError_t e = hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      ctxs.pop_back();
+      return e;
+    }
+    c.busy = true;
+    *out = &c;
+    return hipSuccess;
   }
   // the workspace for a render on `st` (stream-ordered after its previous user)
   hipError_t acquire(hipStream_t st, WfSlot** out) {
     WfSlot* pick = nullptr;
     for (WfSlot& w : wfs)
       if (w.stream == st) pick = &w;
-    if (!pick && wfs.size() < kMaxWorkspaces) {
-      wfs.reserve(kMaxWorkspaces);  // slot addresses stay valid
+    size_t unpinned = 0;
+    for (WfSlot& w : wfs) unpinned += w.pins == 0;
+    if (!pick && (wfs.size() < kMaxWorkspaces || unpinned == 0)) {
       wfs.emplace_back();
       pick = &wfs.back();
       pick->wf = std::make_unique<Wavefront>();
@@ -212,10 +253,9 @@ struct rt_scene {
       if (prof_on) pick->wf->set_profiling(true, prof_mask);
       pick->stream = st;
     }
-    if (!pick) {  // take over the least recently used workspace
-      pick = &wfs[0];
+    if (!pick) {  // take over the least recently used workspace that no call holds
       for (WfSlot& w : wfs)
-        if (w.tick < pick->tick) pick = &w;
+        if (w.pins == 0 && (!pick || w.tick < pick->tick)) pick = &w;
       hipError_t e = hipStreamWaitEvent(st, pick->done, 0);
       if (e != hipSuccess) return e;
       pick->stream = st;
@@ -300,7 +340,7 @@ int ensure_dev_buffer(double** buf, size_t* cap, size_t need) {
 // while the host copies the previous chunk out (a pageable hipMemcpy of a
 // 50 MB canvas stages through the runtime at a few GB/s). Synchronous.
 constexpr size_t kStageChunk = (size_t)8 << 20;
-int copy_to_host(rt_scene* s, void* dst, const void* src, size_t n, hipStream_t st) {
+int copy_to_host(rt_scene::HostCtx* s, int d2h, void* dst, const void* src, size_t n, hipStream_t st) {
   if (n == 0) return RT_OK;
   if (pinned_block(dst, n)) {  // an rt_host_buffer_alloc block: the DMA engine writes it directly
     RT_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, st));
@@ -311,7 +351,7 @@ int copy_to_host(rt_scene* s, void* dst, const void* src, size_t n, hipStream_t 
   // write them directly (one pass over the bytes instead of DMA + host memcpy).
   // The registration never outlives the call, so the caller may free or reuse
   // the buffer at once; a buffer that cannot be registered takes the chunks.
-  if (n >= ((size_t)4 << 20) && s->tune.d2h == 1) {
+  if (n >= ((size_t)4 << 20) && d2h == 1) {
     if (hipHostRegister(dst, n, hipHostRegisterDefault) == hipSuccess) {
       hipError_t e = hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, st);
       if (e == hipSuccess) e = hipStreamSynchronize(st);
@@ -394,7 +434,7 @@ bool valid_aa(uint32_t aa) { return aa == 1 || aa == 2 || aa == 4 || aa == 8 || 
 // the frame asked for, so the next frame fits at least that far.
 int check_faults(rt_scene* s) {
   for (rt_scene::WfSlot& w : s->wfs) {
-    if (!w.wf->overflowed()) continue;
+    if (w.pins || !w.wf->overflowed()) continue;  // a pinned workspace's own call handles its frame
     if (w.done) RT_HIP(hipEventSynchronize(w.done));  // its frames have run (the arenas are about to be reallocated)
     bool was = false;
     RT_HIP(w.wf->take_overflow(&was));
@@ -408,17 +448,18 @@ int check_faults(rt_scene* s) {
 // Launch one render (camera shard or ray batch) on `stream` through the
 // wavefront pipeline. `n_tasks` root rays = pixels x aa (camera) or rays
 // (batch). `stats_out`, when given, receives the exact counters and
-// `ms_out` the kernel time (both synchronise). `sync`: the caller waits for
-// this render anyway (a host canvas, the counters): the call synchronises,
-// and a frame that overflowed its queue arenas is rendered again, with the
-// arenas grown, until it fits (every synchronous entry point returns a
-// complete frame). Asynchronous renders report an overflow later
-// (check_faults).
+// `ms_out` the kernel time. `sync`: the caller waits for this render anyway
+// (a host canvas, the counters): the call waits for it, and a frame that
+// overflowed its queue arenas is rendered again, with the arenas grown,
+// until it fits (every synchronous entry point returns a complete frame).
+// Asynchronous renders report an overflow later (check_faults). With `lk`
+// (the scene's lock, held on entry and on return) the waits run unlocked;
+// the workspace stays pinned to this call meanwhile.
 int run_render(rt_scene* s, const DevCamera& cam, const double* d_rays, uint32_t n_tasks, uint32_t aa,
                uint32_t max_depth, uint32_t row_block, uint32_t shard, uint32_t n_shards, double* d_out,
                hipStream_t stream, DevStats* stats_out = nullptr, float* ms_out = nullptr, uint32_t flags = 0,
                rt_scene::WfSlot** used = nullptr, const FrameTable* batch = nullptr, unsigned n_frames = 1,
-               bool sync = false) {
+               bool sync = false, std::unique_lock<std::mutex>* lk = nullptr) {
   if (max_depth > (uint32_t)kMaxDepth)
     return fail(RT_ERR_INVALID_ARGUMENT, "max_depth > " + std::to_string(kMaxDepth));
   if (!valid_aa(aa)) return fail(RT_ERR_INVALID_ARGUMENT, "aa_samples must be 1, 2, 4, 8 or 16");
@@ -434,16 +475,28 @@ int run_render(rt_scene* s, const DevCamera& cam, const double* d_rays, uint32_t
   rt_scene::WfSlot* w = nullptr;
   hipError_t e = s->acquire(stream, &w);
   if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("wavefront render: ") + hipGetErrorString(e));
-  const unsigned wf_flags = ((flags & RT_RENDER_EXHAUSTIVE) ? WF_EXHAUSTIVE : 0u) | (used ? WF_COUNT : 0u);
+  const unsigned wf_flags = ((flags & RT_RENDER_EXHAUSTIVE) ? WF_EXHAUSTIVE : 0u) |
+                            ((used || stats_out) ? WF_COUNT : 0u) | (ms_out ? WF_TIME : 0u);
   sync = sync || stats_out || ms_out;
+  struct Pin {  // the workspace is this call's until it returns
+    rt_scene::WfSlot* w;
+    bool on;
+    ~Pin() {
+      if (on) --w->pins;
+    }
+  } pin{w, sync};
+  if (sync) ++w->pins;
   for (int attempt = 0;; ++attempt) {
     e = w->wf->render(s->dev, cam, d_rays == nullptr, d_rays, n_tasks, aa, max_depth, row_block, shard, n_shards,
-                      d_out, stream, s->sizing, stats_out, ms_out, s->tune, s->wfs.size() == 1, wf_flags, batch,
+                      d_out, stream, s->sizing, nullptr, nullptr, s->tune, s->wfs.size() == 1, wf_flags, batch,
                       n_frames);
     if (e == hipSuccess) e = hipEventRecord(w->done, stream);
-    if (e == hipSuccess && sync) e = hipStreamSynchronize(stream);
     if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("wavefront render: ") + hipGetErrorString(e));
     if (!sync) break;
+    if (lk) lk->unlock();
+    e = hipStreamSynchronize(stream);
+    if (lk) lk->lock();
+    if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("wavefront render: ") + hipGetErrorString(e));
     w->wf->learn(s->sizing);
     bool over = false;
     e = w->wf->take_overflow(&over);
@@ -451,9 +504,29 @@ int run_render(rt_scene* s, const DevCamera& cam, const double* d_rays, uint32_t
     if (!over) break;
     if (attempt >= 24) return fail(RT_ERR_HIP, "wavefront queue arenas: the frame does not fit");
   }
+  if (stats_out) RT_HIP(w->wf->read_stats(stats_out));
+  if (ms_out) RT_HIP(w->wf->kernel_ms(ms_out));
   if (used) *used = w;
   return RT_OK;
 }
+
+// A host context for the duration of one entry point (rt_scene::HostCtx),
+// returned to the pool under the scene's lock.
+struct CtxLease {
+  rt_scene* s;
+  std::unique_lock<std::mutex>& lk;
+  rt_scene::HostCtx* c = nullptr;
+  ~CtxLease() {
+    if (!c) return;
+    if (!lk.owns_lock()) lk.lock();
+    c->busy = false;
+  }
+};
+#define RT_TAKE_CTX(lease)                                                           \
+  do {                                                                               \
+    const hipError_t _e = (lease).s->take_ctx(&(lease).c);                           \
+    if (_e != hipSuccess) return fail(RT_ERR_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(_e)); \
+  } while (0)
 
 void fill_stats(rt_stats* st, const DevStats& ds, float ms_kernel, double ms_total) {
   std::memset(st, 0, sizeof *st);
@@ -1012,12 +1085,8 @@ void rt_scene_destroy(rt_scene* s) {
   s->multi.release();
   (void)hipSetDevice(s->device);
   if (s->d_blob) (void)hipFree(s->d_blob);
-  if (s->d_out) (void)hipFree(s->d_out);
-  if (s->d_in) (void)hipFree(s->d_in);
-  if (s->d_ppm) (void)hipFree(s->d_ppm);
-  if (s->d_ppm_rows) (void)hipFree(s->d_ppm_rows);
   if (s->stream) (void)hipStreamDestroy(s->stream);
-  delete s;
+  delete s;  // the host contexts and workspaces release their memory (on the scene's device)
 }
 
 uint32_t rt_shard_rows(uint32_t vsize, uint32_t row_block, uint32_t shard, uint32_t n_shards) {
@@ -1048,7 +1117,7 @@ int rt_render_shard_device_ex(const rt_scene* scene, const rt_camera_desc* camer
     return fail(RT_ERR_INVALID_ARGUMENT, "bad shard specification");
   if (camera->hsize == 0 || camera->vsize == 0) return fail(RT_ERR_INVALID_ARGUMENT, "empty camera");
   rt_scene* s = const_cast<rt_scene*>(scene);
-  std::lock_guard<std::mutex> lk(s->mu);
+  std::unique_lock<std::mutex> lk(s->mu);
   auto t0 = std::chrono::steady_clock::now();
   RT_DEVICE(s->device);
   const uint32_t rows = rt_shard_rows(camera->vsize, row_block, shard, n_shards);
@@ -1058,7 +1127,8 @@ int rt_render_shard_device_ex(const rt_scene* scene, const rt_camera_desc* camer
   DevStats ds{};
   float ms = 0.f;
   int rc = run_render(s, to_dev_camera(*camera), nullptr, (uint32_t)n_tasks, aa_samples, max_depth, row_block, shard,
-                      n_shards, d_out_rgb, st, stats ? &ds : nullptr, stats ? &ms : nullptr, flags);
+                      n_shards, d_out_rgb, st, stats ? &ds : nullptr, stats ? &ms : nullptr, flags, nullptr, nullptr,
+                      1, false, &lk);
   if (rc != RT_OK) return rc;
   if (stats)
     fill_stats(stats, ds, ms, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
@@ -1085,7 +1155,7 @@ int rt_render_frames_device(const rt_scene* scene, const rt_camera_desc* cameras
     return RT_OK;
   }
   rt_scene* s = const_cast<rt_scene*>(scene);
-  std::lock_guard<std::mutex> lk(s->mu);
+  std::unique_lock<std::mutex> lk(s->mu);
   auto t0 = std::chrono::steady_clock::now();
   RT_DEVICE(s->device);
   const uint32_t rows = rt_shard_rows(cameras[0].vsize, row_block, shard, n_shards);
@@ -1113,7 +1183,7 @@ int rt_render_frames_device(const rt_scene* scene, const rt_camera_desc* cameras
     float ms = 0.f;
     int rc = run_render(s, tab.cam[0], nullptr, (uint32_t)per, aa_samples, max_depth, row_block, shard, n_shards,
                         tab.out[0], st, stats ? &ds : nullptr, stats ? &ms : nullptr, 0, nullptr,
-                        nf > 1 ? &tab : nullptr, nf);
+                        nf > 1 ? &tab : nullptr, nf, false, &lk);
     if (rc != RT_OK) return rc;
     if (stats) {
       sum.rays_primary += ds.rays_primary; sum.rays_reflect += ds.rays_reflect;
@@ -1147,20 +1217,25 @@ int rt_render_ex(const rt_scene* scene, const rt_camera_desc* camera, uint32_t m
   if (camera->hsize == 0 || camera->vsize == 0) return fail(RT_ERR_INVALID_ARGUMENT, "empty camera");
   if (!valid_aa(aa_samples)) return fail(RT_ERR_INVALID_ARGUMENT, "aa_samples must be 1, 2, 4, 8 or 16");
   rt_scene* s = const_cast<rt_scene*>(scene);
-  std::lock_guard<std::mutex> lk(s->mu);
+  std::unique_lock<std::mutex> lk(s->mu);
   auto t0 = std::chrono::steady_clock::now();
   RT_DEVICE(s->device);
   const uint64_t n_pix = (uint64_t)camera->hsize * camera->vsize;
   if (n_pix * aa_samples >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "canvas too large for one launch");
-  int rc = ensure_dev_buffer(&s->d_out, &s->out_cap, n_pix * 3);
+  CtxLease cx{s, lk};
+  RT_TAKE_CTX(cx);
+  int rc = ensure_dev_buffer(&cx.c->d_out, &cx.c->out_cap, n_pix * 3);
   if (rc != RT_OK) return rc;
   DevStats ds{};
   float ms = 0.f;
   rc = run_render(s, to_dev_camera(*camera), nullptr, (uint32_t)(n_pix * aa_samples), aa_samples, max_depth,
-                  camera->vsize, 0, 1, s->d_out, s->stream, stats ? &ds : nullptr, &ms, flags);
+                  camera->vsize, 0, 1, cx.c->d_out, cx.c->stream, stats ? &ds : nullptr, &ms, flags, nullptr, nullptr,
+                  1, true, &lk);
   if (rc != RT_OK) return rc;
-  if ((rc = copy_to_host(s, out_rgb, s->d_out, n_pix * 3 * sizeof(double), s->stream)) != RT_OK) return rc;
-  if ((rc = check_faults(s)) != RT_OK) return rc;
+  const int d2h = s->tune.d2h;
+  lk.unlock();  // the copy to the caller's canvas runs unlocked (the context is this call's)
+  if ((rc = copy_to_host(cx.c, d2h, out_rgb, cx.c->d_out, n_pix * 3 * sizeof(double), cx.c->stream)) != RT_OK)
+    return rc;
   if (stats)
     fill_stats(stats, ds, ms, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
   return RT_OK;
@@ -1176,45 +1251,50 @@ int rt_render_ppm(const rt_scene* scene, const rt_camera_desc* camera, uint32_t 
   if (camera->hsize > kPpmMaxWidth)
     return fail(RT_ERR_INVALID_ARGUMENT, "canvas wider than the device PPM encoder's row (use rt_canvas_to_ppm)");
   rt_scene* s = const_cast<rt_scene*>(scene);
-  std::lock_guard<std::mutex> lk(s->mu);
+  std::unique_lock<std::mutex> lk(s->mu);
   auto t0 = std::chrono::steady_clock::now();
   RT_DEVICE(s->device);
   const uint32_t W = camera->hsize, H = camera->vsize;
   const uint64_t n_pix = (uint64_t)W * H;
   if (n_pix * aa_samples >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "canvas too large for one launch");
-  int rc = ensure_dev_buffer(&s->d_out, &s->out_cap, n_pix * 3);
+  CtxLease cx{s, lk};
+  RT_TAKE_CTX(cx);
+  rt_scene::HostCtx* c = cx.c;
+  int rc = ensure_dev_buffer(&c->d_out, &c->out_cap, n_pix * 3);
   if (rc != RT_OK) return rc;
   const PpmHeader hd = ppm_header(W, H);
   const size_t bound = hd.n + (size_t)12 * n_pix + H;  // <= 4 bytes per component, one '\n' per row
-  if (s->ppm_cap < bound) {
-    if (s->d_ppm) (void)hipFree(s->d_ppm);
-    s->d_ppm = nullptr;
-    s->ppm_cap = 0;
-    RT_HIP(hipMalloc(&s->d_ppm, bound));
-    s->ppm_cap = bound;
+  if (c->ppm_cap < bound) {
+    if (c->d_ppm) (void)hipFree(c->d_ppm);
+    c->d_ppm = nullptr;
+    c->ppm_cap = 0;
+    RT_HIP(hipMalloc(&c->d_ppm, bound));
+    c->ppm_cap = bound;
   }
-  if (s->ppm_rows_cap < H) {
-    if (s->d_ppm_rows) (void)hipFree(s->d_ppm_rows);
-    s->d_ppm_rows = nullptr;
-    s->ppm_rows_cap = 0;
-    RT_HIP(hipMalloc(&s->d_ppm_rows, (size_t)H * 4 + ((size_t)H + 1) * 8 + 8));
-    s->ppm_rows_cap = H;
+  if (c->ppm_rows_cap < H) {
+    if (c->d_ppm_rows) (void)hipFree(c->d_ppm_rows);
+    c->d_ppm_rows = nullptr;
+    c->ppm_rows_cap = 0;
+    RT_HIP(hipMalloc(&c->d_ppm_rows, (size_t)H * 4 + ((size_t)H + 1) * 8 + 8));
+    c->ppm_rows_cap = H;
   }
-  unsigned long long* d_off = (unsigned long long*)(((uintptr_t)s->d_ppm_rows + (size_t)H * 4 + 7) & ~(uintptr_t)7);
+  unsigned long long* d_off = (unsigned long long*)(((uintptr_t)c->d_ppm_rows + (size_t)H * 4 + 7) & ~(uintptr_t)7);
   DevStats ds{};
   float ms = 0.f;
   rc = run_render(s, to_dev_camera(*camera), nullptr, (uint32_t)(n_pix * aa_samples), aa_samples, max_depth, H, 0,
-                  1, s->d_out, s->stream, stats ? &ds : nullptr, stats ? &ms : nullptr, 0, nullptr, nullptr, 1, true);
+                  1, c->d_out, c->stream, stats ? &ds : nullptr, stats ? &ms : nullptr, 0, nullptr, nullptr, 1, true,
+                  &lk);
   if (rc != RT_OK) return rc;
-  RT_HIP(ppm_encode_device(s->d_out, W, H, s->d_ppm, s->ppm_cap, (unsigned*)s->d_ppm_rows, d_off, hd, s->stream));
+  const int d2h = s->tune.d2h;
+  lk.unlock();
+  RT_HIP(ppm_encode_device(c->d_out, W, H, c->d_ppm, c->ppm_cap, (unsigned*)c->d_ppm_rows, d_off, hd, c->stream));
   unsigned long long body = 0;
-  RT_HIP(hipMemcpyAsync(&body, d_off + H, sizeof body, hipMemcpyDeviceToHost, s->stream));
-  RT_HIP(hipStreamSynchronize(s->stream));
-  if ((rc = check_faults(s)) != RT_OK) return rc;
+  RT_HIP(hipMemcpyAsync(&body, d_off + H, sizeof body, hipMemcpyDeviceToHost, c->stream));
+  RT_HIP(hipStreamSynchronize(c->stream));
   *out_len = hd.n + (size_t)body;
   if (out) {
     if (cap < *out_len) return fail(RT_ERR_BUFFER_TOO_SMALL, "PPM buffer too small");
-    if ((rc = copy_to_host(s, out, s->d_ppm, *out_len, s->stream)) != RT_OK) return rc;
+    if ((rc = copy_to_host(c, d2h, out, c->d_ppm, *out_len, c->stream)) != RT_OK) return rc;
   }
   if (stats)
     fill_stats(stats, ds, ms, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
@@ -1271,22 +1351,26 @@ int rt_color_at_batch_ex(const rt_scene* scene, const double* rays, size_t n, ui
   if (!scene || (n && (!rays || !out_rgb))) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
   if (n >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "batch too large");
   rt_scene* s = const_cast<rt_scene*>(scene);
-  std::lock_guard<std::mutex> lk(s->mu);
+  std::unique_lock<std::mutex> lk(s->mu);
   auto t0 = std::chrono::steady_clock::now();
   RT_DEVICE(s->device);
-  int rc = ensure_dev_buffer(&s->d_in, &s->in_cap, n * 6);
+  CtxLease cx{s, lk};
+  RT_TAKE_CTX(cx);
+  rt_scene::HostCtx* c = cx.c;
+  int rc = ensure_dev_buffer(&c->d_in, &c->in_cap, n * 6);
   if (rc != RT_OK) return rc;
-  rc = ensure_dev_buffer(&s->d_out, &s->out_cap, n * 3);
+  rc = ensure_dev_buffer(&c->d_out, &c->out_cap, n * 3);
   if (rc != RT_OK) return rc;
-  if (n) RT_HIP(hipMemcpyAsync(s->d_in, rays, n * 6 * sizeof(double), hipMemcpyHostToDevice, s->stream));
+  if (n) RT_HIP(hipMemcpyAsync(c->d_in, rays, n * 6 * sizeof(double), hipMemcpyHostToDevice, c->stream));
   DevCamera cam{};
   DevStats ds{};
   float ms = 0.f;
-  rc = run_render(s, cam, s->d_in, (uint32_t)n, 1, remaining, 1, 0, 1, s->d_out, s->stream, stats ? &ds : nullptr,
-                  &ms, flags);
+  rc = run_render(s, cam, c->d_in, (uint32_t)n, 1, remaining, 1, 0, 1, c->d_out, c->stream, stats ? &ds : nullptr,
+                  &ms, flags, nullptr, nullptr, 1, true, &lk);
   if (rc != RT_OK) return rc;
-  if (n) RT_HIP(hipMemcpyAsync(out_rgb, s->d_out, n * 3 * sizeof(double), hipMemcpyDeviceToHost, s->stream));
-  RT_HIP(hipStreamSynchronize(s->stream));
+  lk.unlock();
+  if (n) RT_HIP(hipMemcpyAsync(out_rgb, c->d_out, n * 3 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  RT_HIP(hipStreamSynchronize(c->stream));
   if (stats)
     fill_stats(stats, ds, ms, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
   return RT_OK;
@@ -1300,17 +1384,21 @@ int rt_is_shadowed_batch(const rt_scene* scene, const double* points, size_t n, 
   rt_scene* s = const_cast<rt_scene*>(scene);
   if ((int)light >= s->n_lights) return fail(RT_ERR_INVALID_ARGUMENT, "light index out of range");
   if (n >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "batch too large");
-  std::lock_guard<std::mutex> lk(s->mu);
+  std::unique_lock<std::mutex> lk(s->mu);
   RT_DEVICE(s->device);
   if (n == 0) return RT_OK;
-  int rc = ensure_dev_buffer(&s->d_in, &s->in_cap, n * 3);
+  CtxLease cx{s, lk};
+  RT_TAKE_CTX(cx);
+  rt_scene::HostCtx* c = cx.c;
+  lk.unlock();  // the context is this call's: nothing below touches shared state
+  int rc = ensure_dev_buffer(&c->d_in, &c->in_cap, n * 3);
   if (rc != RT_OK) return rc;
-  rc = ensure_dev_buffer(&s->d_out, &s->out_cap, (n + 7) / 8);
+  rc = ensure_dev_buffer(&c->d_out, &c->out_cap, (n + 7) / 8);
   if (rc != RT_OK) return rc;
-  RT_HIP(hipMemcpyAsync(s->d_in, points, n * 3 * sizeof(double), hipMemcpyHostToDevice, s->stream));
-  RT_HIP(launch_shadow(s->dev, s->d_in, (int)n, (int)light, (uint8_t*)s->d_out, s->stream));
-  RT_HIP(hipMemcpyAsync(out, s->d_out, n, hipMemcpyDeviceToHost, s->stream));
-  RT_HIP(hipStreamSynchronize(s->stream));
+  RT_HIP(hipMemcpyAsync(c->d_in, points, n * 3 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  RT_HIP(launch_shadow(s->dev, c->d_in, (int)n, (int)light, (uint8_t*)c->d_out, c->stream));
+  RT_HIP(hipMemcpyAsync(out, c->d_out, n, hipMemcpyDeviceToHost, c->stream));
+  RT_HIP(hipStreamSynchronize(c->stream));
   return RT_OK;
   });
 }
@@ -1320,17 +1408,21 @@ int rt_hit_batch(const rt_scene* scene, const double* rays, size_t n, double* ou
   if (!scene || (n && (!rays || !out24))) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
   if (n >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "batch too large");
   rt_scene* s = const_cast<rt_scene*>(scene);
-  std::lock_guard<std::mutex> lk(s->mu);
+  std::unique_lock<std::mutex> lk(s->mu);
   RT_DEVICE(s->device);
   if (n == 0) return RT_OK;
-  int rc = ensure_dev_buffer(&s->d_in, &s->in_cap, n * 6);
+  CtxLease cx{s, lk};
+  RT_TAKE_CTX(cx);
+  rt_scene::HostCtx* c = cx.c;
+  lk.unlock();
+  int rc = ensure_dev_buffer(&c->d_in, &c->in_cap, n * 6);
   if (rc != RT_OK) return rc;
-  rc = ensure_dev_buffer(&s->d_out, &s->out_cap, n * 24);
+  rc = ensure_dev_buffer(&c->d_out, &c->out_cap, n * 24);
   if (rc != RT_OK) return rc;
-  RT_HIP(hipMemcpyAsync(s->d_in, rays, n * 6 * sizeof(double), hipMemcpyHostToDevice, s->stream));
-  RT_HIP(launch_hit(s->dev, s->d_in, (int)n, s->d_out, s->stream));
-  RT_HIP(hipMemcpyAsync(out24, s->d_out, n * 24 * sizeof(double), hipMemcpyDeviceToHost, s->stream));
-  RT_HIP(hipStreamSynchronize(s->stream));
+  RT_HIP(hipMemcpyAsync(c->d_in, rays, n * 6 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  RT_HIP(launch_hit(s->dev, c->d_in, (int)n, c->d_out, c->stream));
+  RT_HIP(hipMemcpyAsync(out24, c->d_out, n * 24 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  RT_HIP(hipStreamSynchronize(c->stream));
   return RT_OK;
   });
 }

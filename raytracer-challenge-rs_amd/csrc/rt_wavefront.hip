@@ -639,7 +639,11 @@ __device__ __forceinline__ void st_ray(WfRay* p, V3 o, V3 d) {
 __device__ __forceinline__ unsigned bind_generation(WfArgs& a, const unsigned* pre) {
   const unsigned g = a.g;
   const WfGenTab t = a.gtab[g];
-  const unsigned n = g == 0 ? a.n : (pre ? (unsigned)__builtin_amdgcn_readfirstlane((int)pre[2 * kShards]) : 0u);
+  // (the region counters count every child asked for, also those a full
+  // region refused: a generation placed with no room (cap 0, after an
+  // overflow) has no rays)
+  const unsigned n = g == 0 ? a.n
+                            : (pre && t.cap ? (unsigned)__builtin_amdgcn_readfirstlane((int)pre[2 * kShards]) : 0u);
   const unsigned groups = ((n + 63u) / 64u + kShardGroup - 1u) / kShardGroup;
   const unsigned per = kShardGroup * ((groups + kShards - 1u) / kShards);
   // the last generation spawns no children, so it has no parents either
@@ -967,9 +971,10 @@ __global__ __launch_bounds__(kWfBlock) void wf_combine_parents(DevScene sc, DevC
   const unsigned stride = gridDim.x * blockDim.x;
   __shared__ unsigned s_pre[kPreList];
   const unsigned* pre = shard_prefix<false>(a.sh_cnt, s_pre);
-  const unsigned n = (unsigned)__builtin_amdgcn_readfirstlane((int)pre[kShards]);
   const WfGenTab t = a.gtab[a.g];
   const unsigned sh_cap = a.gsh[a.g];
+  // (no room for the parents after an overflow: the counters hold what was asked for)
+  const unsigned n = sh_cap ? (unsigned)__builtin_amdgcn_readfirstlane((int)pre[kShards]) : 0u;
   const ParentRec* parents = a.par_base + t.par_off;
   const double* child_colors = a.color_base + a.gtab[a.g + 1].color_off * 3ull;
   if (!(a.g == 0 && a.colors_direct)) a.colors = a.color_base + t.color_off * 3ull;
@@ -1456,7 +1461,8 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
               d_frames_, n_frames, fused ? d_gtab_ : (WfGenTab*)nullptr);
     WF_CHECK(hipGetLastError());
   }
-  if (ms_kernel) WF_CHECK(hipEventRecord(ev0_, stream));
+  const bool timed = ms_kernel != nullptr || (flags & WF_TIME) != 0;
+  if (timed) WF_CHECK(hipEventRecord(ev0_, stream));
   if (profiling_) pframes_ += n_frames;  // class times are reported per frame
   prof_rays_[0] = prof_rays_[1] = prof_rays_[2] = 0;
   last_bvh_ = bvh;
@@ -1469,7 +1475,7 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
   else
     WF_CHECK(render_exhaustive(sc, cam, camera_mode, d_in_rays, n0, aa, max_depth, row_block, shard, n_shards, d_out,
                                stream, count, skip_shadow, tn, solo));
-  if (ms_kernel) WF_CHECK(hipEventRecord(ev1_, stream));
+  if (timed) WF_CHECK(hipEventRecord(ev1_, stream));
   lr_.L = (unsigned)sc.n_lights; lr_.n0 = n0; lr_.max_depth = max_depth;
   lr_.counted = count; lr_.exact_disc = !bvh && !skip_shadow; lr_.bvh = bvh;
   lr_.n_diag = (unsigned long long)sc.n_diag; lr_.n_gen = (unsigned long long)sc.n_gen;

@@ -83,7 +83,7 @@ constexpr int kMaxGen = 66;
 // LDS a fused trace launch may take (of the CU's 160 KB)
 constexpr size_t kFusedLdsLimit = 160 * 1024 - 1024;
 constexpr int kFusedBlockThreads = 1024;  // threads of a fused trace block (kTraceBlock, rt_trace.hpp)
-enum WfFlags : unsigned { WF_EXHAUSTIVE = 1u, WF_COUNT = 2u };
+enum WfFlags : unsigned { WF_EXHAUSTIVE = 1u, WF_COUNT = 2u, WF_TIME = 4u };  // WF_TIME: events around the render (kernel_ms)
 
 // Render-time tuning of a scene (rt_scene::tune, copied from the process
 // defaults when the scene is created; rtamd_scene_tuning_set changes one
@@ -325,6 +325,8 @@ class Wavefront {
                     const FrameTable* batch = nullptr, unsigned n_frames = 1);
   // The counters of the last render (rendered with WF_COUNT); synchronises its stream.
   hipError_t read_stats(DevStats* out);
+  // Device time of the last render rendered with WF_TIME (after it completed).
+  hipError_t kernel_ms(float* ms) { return hipEventElapsedTime(ms, ev0_, ev1_); }
   // A fast-path frame of this workspace overflowed its arenas (WfHostRec):
   // that frame is incomplete. take_overflow() clears the flag and grows the
   // arenas past what the overflowing generation asked for (the next frame
