@@ -17,6 +17,22 @@
  *     the message is available from rt_last_error() on the calling thread.
  *     The library never aborts across the ABI (the reference panics instead:
  *     raytracer/src/geometry/intersection.rs:113, matrix.rs:139, canvas.rs:45-46).
+ *
+ * Threads and devices (callable from any host thread)
+ *   - Every entry point may be called from any host thread, on one scene or
+ *     on several at once. An rt_scene's lock is held only while a call
+ *     enqueues its work: the synchronous entry points (the host-buffer calls
+ *     rt_render*, rt_render_ppm, rt_color_at_batch*, rt_is_shadowed_batch,
+ *     rt_hit_batch, and any call given a non-NULL `stats`) wait for the device
+ *     and copy their results without it, each in a context (stream, device
+ *     buffers) of its own, so threads rendering one scene overlap on the GPU.
+ *   - Asynchronous calls (rt_render_shard_device[_ex], rt_render_frames_device
+ *     without stats) never wait on the host: every recursion generation of the
+ *     frame sizes itself on the device, for a new camera as for a repeated one.
+ *     Work issued on one stream runs in issue order; different streams overlap.
+ *   - Every entry point that selects a scene's device restores the caller's
+ *     current HIP device before it returns, on success and on failure.
+ *   - rt_last_error() is per thread.
  */
 #ifndef RT_RENDER_H
 #define RT_RENDER_H
@@ -203,7 +219,8 @@ int rt_render_ex(const rt_scene* scene, const rt_camera_desc* camera,
  * default (null) stream, so the work is ordered with the caller's other work
  * there (torch's current stream is often the null stream).
  * Asynchronous unless `stats` is non-NULL (then it synchronises to read the
- * counters). `n_shards == 1` renders the whole frame. `aa_samples` as in
+ * counters): the host enqueues the whole frame without waiting, whatever the
+ * camera. `n_shards == 1` renders the whole frame. `aa_samples` as in
  * rt_render_aa (1 = `Camera::render`).
  * Deferred errors: an asynchronous call returns before its frame has run, so
  * a device-side failure of that frame (see rt_scene_check) is reported by the
@@ -335,11 +352,15 @@ size_t rt_sizeof_camera_desc(void); /* 160 */
 size_t rt_sizeof_stats(void);       /* 112 */
 
 /* Waits for every render issued on `scene` (on any stream) and reports any
- * frame the library found incomplete after the fact: an asynchronous render
- * (rt_render_shard_device[_ex] without stats) is checked on the device, and a
- * failed check surfaces as RT_ERR_HIP from the NEXT call on the scene, or from
- * this one. Callers that render asynchronously call it after their last frame
- * to learn about every frame. RT_OK when all frames were complete. */
+ * frame the library found incomplete after the fact. The wavefront queues of
+ * an asynchronous render live in per-workspace arenas sized from the frames
+ * the scene has rendered (DESIGN.md "Device-sized generations"); a frame
+ * whose recursion outgrows them is detected on the device, left incomplete,
+ * and reported as RT_ERR_HIP by the NEXT call on the scene, or by this one,
+ * after the arenas have grown (render that frame again). Synchronous calls
+ * never report it: they grow the arenas and render again themselves. Callers
+ * that render asynchronously call it after their last frame to learn about
+ * every frame. RT_OK when all frames were complete. */
 int rt_scene_check(const rt_scene* scene);
 
 #ifdef __cplusplus
