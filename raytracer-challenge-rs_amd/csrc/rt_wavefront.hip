@@ -671,12 +671,21 @@ __device__ __forceinline__ unsigned bind_generation(WfArgs& a, const unsigned* p
   a.in_cap = t.cap;
   a.out_cap = out_cap;
   a.sh_cap = sh_cap;
-  a.rays = a.ray_buf[g & 1u];
-  a.next_rays = a.ray_buf[(g + 1u) & 1u];
+  // (constant indices: a dynamic index would keep the whole argument block in scratch)
+  WfRay* const rb0 = a.ray_buf[0];
+  WfRay* const rb1 = a.ray_buf[1];
+  a.rays = (g & 1u) ? rb1 : rb0;
+  a.next_rays = (g & 1u) ? rb0 : rb1;
   if (!(g == 0 && a.colors_direct)) a.colors = a.color_base + t.color_off * 3ull;
   a.parents = a.par_base + t.par_off;
   return n;
 }
+
+// Phase-cost experiments (dev builds only, -DRTAMD_EXP_DUP_*: a phase runs a
+// second time on opaque copies of its inputs, its result sunk; the frame is
+// unchanged and the added time is the phase's cost). tools/exp_time.sh.
+__device__ __forceinline__ void exp_opaque(double& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void exp_sink(double x) { asm volatile("" ::"v"(x)); }
 
 // Per-lane tallies of a fused trace kernel (summed per wave at the end).
 struct FusedTally {
@@ -704,6 +713,14 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
   const ShadeRec* m = nullptr;
   if (valid && h.key >= 0) {
     c = prepare(sc, o, d, h);
+#ifdef RTAMD_EXP_DUP_PREP
+    {
+      V3 o2 = o;
+      exp_opaque(o2.x);
+      const Comps c2 = prepare(sc, o2, d, h);
+      exp_sink(c2.over.x + c2.normal.y + c2.n1);
+    }
+#endif
     hit = true;
     m = &sc.shade[c.obj];
     // reflected_color (world.rs:107-114)
@@ -758,8 +775,24 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
     } else {
       const bool shadowed = shadow_trace<LANE, QUADS>(sc, a.use_lb, ls, l, c.over, sdir, dist, t.sh_disc, t.sh_tests,
                                                       t.sh_boxes);
+#ifdef RTAMD_EXP_DUP_SHADOW
+      {
+        V3 o2 = c.over;
+        exp_opaque(o2.x);
+        unsigned u0 = 0, u1 = 0, u2 = 0;
+        exp_sink(shadow_trace<LANE, QUADS>(sc, a.use_lb, ls, l, o2, sdir, dist, u0, u1, u2) ? 1.0 : 0.0);
+      }
+#endif
       ++t.sh_rays;
       term = lighting(*m, Lr, c.over, c.eyev, c.normal, shadowed, sdir);
+#ifdef RTAMD_EXP_DUP_LIGHT
+      {
+        V3 o2 = c.over;
+        exp_opaque(o2.x);
+        const V3 t2 = lighting(*m, Lr, o2, c.eyev, c.normal, shadowed, sdir);
+        exp_sink(t2.x + t2.y + t2.z);
+      }
+#endif
     }
     surface = vadd(surface, term);
   }
@@ -858,6 +891,17 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
         if constexpr (LANE == 14)
           lane_trace_pair<false>(ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, t.disc, t.tests, t.boxes,
                                  ls.stack);
+#ifdef RTAMD_EXP_DUP_TRAV
+        if constexpr (LANE == 14) {
+          Hit h2;
+          hit_init(h2);
+          V3 o2 = o;
+          exp_opaque(o2.x);
+          unsigned u0 = 0, u1 = 0, u2 = 0;
+          lane_trace_pair<false>(ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o2, d, 0.0, h2, u0, u1, u2, ls.stack);
+          exp_sink(h2.t);
+        }
+#endif
         else
           lane_trace<false, LANE == 3>((const BvhNode*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, t.disc,
                                        t.tests, t.boxes, ls.stack, ls.top, ls.n_top);
