@@ -209,8 +209,11 @@ __device__ __forceinline__ unsigned frame_of(const WfArgs& a, unsigned i, unsign
 // Root rays of generation 0: sample `smp` of a pixel of the shard
 // (camera.rs:57-69 / 71-90) of the slot's frame, or an explicit ray; deeper
 // generations read their queue.
+// CAM = false: a launch that never reads camera rays (generations >= 1, or
+// explicit rays), compiled without the camera path and its registers.
+template <bool CAM = true>
 __device__ __forceinline__ void wf_ray(const WfArgs& a, const DevCamera& cam, unsigned i, V3& o, V3& d) {
-  if (a.g == 0 && a.camera_mode) {
+  if (CAM && a.g == 0 && a.camera_mode) {
     unsigned li;
     const unsigned f = frame_of(a, i, li);
     const DevCamera& cf = a.n_frames > 1 ? a.frames->cam[f] : cam;
@@ -601,9 +604,10 @@ __device__ __forceinline__ void prep_one(const DevScene& sc, const WfArgs& a, un
 // Where generation g's colour of ray `slot` goes: generation 0 of a camera
 // render without AA is tile-ordered, and its colours are written row-major
 // into the output.
+template <bool CAM = true>
 __device__ __forceinline__ double* color_dst(const WfArgs& a, const DevCamera& cam, unsigned slot) {
   size_t oi = slot;
-  if (a.g == 0 && a.camera_mode && a.aa == 1) {
+  if (CAM && a.g == 0 && a.camera_mode && a.aa == 1) {
     unsigned li;
     const unsigned f = frame_of(a, slot, li);
     uint32_t x, lr, smp;
@@ -701,7 +705,7 @@ struct FusedTally {
 // (world.rs:40-56: one is_shadowed per light, a left fold from black), then
 // either the final colour (no children) or a ParentRec. Every lane of the wave
 // calls it (shard_append), `valid` false for the padding lanes.
-template <int LANE, bool QUADS>
+template <int LANE, bool QUADS, bool CAM>
 __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera& cam, const WfArgs& a,
                                             const LaneScene& ls, unsigned i, unsigned slot, bool valid, V3 o, V3 d,
                                             const Hit& h, FusedTally& t) {
@@ -743,7 +747,7 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
                ray_class_f(hit, c));
   if (!valid) return;
   t.hits += hit; t.refl += want_refl; t.refr += want_refr;
-  double* dst = color_dst(a, cam, slot);
+  double* dst = color_dst<CAM>(a, cam, slot);
   if (!hit) {  // color_at: a miss is black (world.rs:74-75)
     st_d(dst, 0.0); st_d(dst + 1, 0.0); st_d(dst + 2, 0.0);
     return;
@@ -817,7 +821,8 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
 // for). Every other frame (the timed ones, the profiled ones) skips the
 // per-visit and per-test counting and the wave-end atomics altogether: C3
 // 1.021 -> 0.964 ms/frame, an 8-way shard 0.204 -> 0.184 ms.
-template <bool PRIMARY, bool QUADS, int LANE, bool TALLY>
+// CAM: the launch may read camera rays (generation 0 of a camera render).
+template <bool PRIMARY, bool QUADS, int LANE, bool TALLY, bool CAM = PRIMARY>
 __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, DevCamera cam, WfArgs a) {
   __shared__ int stack_lds[LANE == 3 ? kLaneLdsDepth * kTraceBlock
                            : LANE == 0 ? (kTraceBlock / 64) * (kBvhMaxDepth + 4) : 1];
@@ -876,7 +881,7 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
     Hit h;
     hit_init(h);
     if (valid) {
-      wf_ray(a, cam, slot, o, d);
+      wf_ray<CAM>(a, cam, slot, o, d);
       if constexpr (LANE == 0) {
         // the chunk's frame (chunks never mix frames): its shared-origin primary records
         const unsigned pf = a.n_frames > 1 ? (c * 64u) / a.frame_rays : 0u;
@@ -908,7 +913,7 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
       }
     }
     hit_finish(h);
-    shade_fused<LANE, QUADS>(sc, cam, a, ls, i, slot, valid, o, d, h, t);
+    shade_fused<LANE, QUADS, CAM>(sc, cam, a, ls, i, slot, valid, o, d, h, t);
     c = dyn ? c_base + X * (unsigned)__shfl((int)k_next, 0, 64) : c + W;
   }
   if constexpr (!TALLY) return;
@@ -1417,9 +1422,11 @@ static hipError_t launch_shadow_exh(const DevScene& sc, const WfArgs& a, bool ld
 }
 
 // the global-memory images' launches live in their own code object (rt_wavefront_glb.o)
-static hipError_t launch_global(int lane, bool quads, bool tally, const DevScene& sc, const DevCamera& cam,
-                                const WfArgs& a, size_t dyn, unsigned n, hipStream_t stream, int block) {
-  const hipError_t e = wf_launch_global(lane, quads, tally, sc, cam, a, dyn, n, stream, block, t_ev_start, t_ev_stop);
+static hipError_t launch_global(int lane, bool quads, bool tally, bool cam_rays, const DevScene& sc,
+                                const DevCamera& cam, const WfArgs& a, size_t dyn, unsigned n, hipStream_t stream,
+                                int block) {
+  const hipError_t e =
+      wf_launch_global(lane, quads, tally, cam_rays, sc, cam, a, dyn, n, stream, block, t_ev_start, t_ev_stop);
   if (t_ev_start) ++t_ev_used;
   return e;
 }
@@ -1438,10 +1445,12 @@ static hipError_t launch_fused_q(const DevScene& sc, const DevCamera& cam, WfArg
     if (dl && dyn + dl <= room) { a.lds_flags |= kLdsDeltas; dyn += dl; }
     return launch_lds(wf_trace_fused<true, QUADS, 0, TALLY>, dyn, n, stream, sc, cam, a, tb);
   }
+  const bool cam_rays = a.g == 0 && a.camera_mode;  // only generation 0 of a camera render reads camera rays
   if (tn.image == 0 && pair_lds_bytes(sc) <= kWfLdsLimit) {
     dyn = pair_lds_bytes(sc);
     if (dl && dyn + dl <= kWfLdsLimit) { a.lds_flags |= kLdsDeltas; dyn += dl; }
-    return launch_lds(wf_trace_fused<false, QUADS, 14, TALLY>, dyn, n, stream, sc, cam, a, tb);
+    return cam_rays ? launch_lds(wf_trace_fused<false, QUADS, 14, TALLY, true>, dyn, n, stream, sc, cam, a, tb)
+                    : launch_lds(wf_trace_fused<false, QUADS, 14, TALLY, false>, dyn, n, stream, sc, cam, a, tb);
   }
   if (tn.image != 1 && sc.bvh_depth <= kLaneLdsDepth) {
     const size_t room = kWfLdsLimit - (size_t)kLaneLdsDepth * kTraceBlock * 4;
@@ -1452,10 +1461,10 @@ static hipError_t launch_fused_q(const DevScene& sc, const DevCamera& cam, WfArg
       a.n_top = (unsigned)std::min<size_t>((size_t)sc.n_bvh, (room - dyn) / sizeof(BvhNode));
       dyn += (size_t)a.n_top * sizeof(BvhNode);
     }
-    return launch_global(3, QUADS, TALLY, sc, cam, a, dyn, n, stream, tb);
+    return launch_global(3, QUADS, TALLY, cam_rays, sc, cam, a, dyn, n, stream, tb);
   }
   if (dl && dl <= kWfLdsLimit) { a.lds_flags |= kLdsDeltas; dyn = dl; }
-  return launch_global(1, QUADS, TALLY, sc, cam, a, dyn, n, stream, tb);
+  return launch_global(1, QUADS, TALLY, cam_rays, sc, cam, a, dyn, n, stream, tb);
 }
 static hipError_t launch_fused(const DevScene& sc, const DevCamera& cam, const WfArgs& a, bool primary, unsigned n,
                                hipStream_t stream, bool tally, const WfTuning& tn) {
@@ -1881,30 +1890,35 @@ static int occupancy_grid(K kern, int block, size_t lds, unsigned n) {
   long long g = std::min(want, cap);
   return (int)std::max(g, 1LL);
 }
-template <bool QUADS, int LANE, bool TALLY>
+template <bool QUADS, int LANE, bool TALLY, bool CAM>
 static hipError_t launch_glb(const DevScene& sc, const DevCamera& cam, const WfArgs& a, size_t dyn, unsigned n,
                              hipStream_t stream, int block, hipEvent_t e0, hipEvent_t e1) {
-  auto kern = wf_trace_fused<false, QUADS, LANE, TALLY>;
+  auto kern = wf_trace_fused<false, QUADS, LANE, TALLY, CAM>;
   if (dyn > 0) WF_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
   const dim3 grid(occupancy_grid(kern, block, dyn, n));
   if (e0) hipExtLaunchKernelGGL(kern, grid, dim3(block), dyn, stream, e0, e1, 0, sc, cam, a);
   else hipLaunchKernelGGL(kern, grid, dim3(block), dyn, stream, sc, cam, a);
   return hipGetLastError();
 }
-hipError_t wf_launch_global(int lane, bool quads, bool tally, const DevScene& sc, const DevCamera& cam,
+template <int LANE>
+static hipError_t launch_glb_lane(bool quads, bool tally, bool cam_rays, const DevScene& sc, const DevCamera& cam,
+                                  const WfArgs& a, size_t dyn, unsigned n, hipStream_t stream, int block, hipEvent_t e0,
+                                  hipEvent_t e1) {
+#define RT_GLB(Q, T, C) launch_glb<Q, LANE, T, C>(sc, cam, a, dyn, n, stream, block, e0, e1)
+  if (cam_rays) {
+    if (quads) return tally ? RT_GLB(true, true, true) : RT_GLB(true, false, true);
+    return tally ? RT_GLB(false, true, true) : RT_GLB(false, false, true);
+  }
+  if (quads) return tally ? RT_GLB(true, true, false) : RT_GLB(true, false, false);
+  return tally ? RT_GLB(false, true, false) : RT_GLB(false, false, false);
+#undef RT_GLB
+}
+hipError_t wf_launch_global(int lane, bool quads, bool tally, bool cam_rays, const DevScene& sc, const DevCamera& cam,
                             const WfArgs& a, size_t dyn, unsigned n, hipStream_t stream, int block, hipEvent_t e0,
                             hipEvent_t e1) {
-  if (lane == 3) {
-    if (quads) return tally ? launch_glb<true, 3, true>(sc, cam, a, dyn, n, stream, block, e0, e1)
-                            : launch_glb<true, 3, false>(sc, cam, a, dyn, n, stream, block, e0, e1);
-    return tally ? launch_glb<false, 3, true>(sc, cam, a, dyn, n, stream, block, e0, e1)
-                 : launch_glb<false, 3, false>(sc, cam, a, dyn, n, stream, block, e0, e1);
-  }
-  if (lane != 1) return hipErrorInvalidValue;
-  if (quads) return tally ? launch_glb<true, 1, true>(sc, cam, a, dyn, n, stream, block, e0, e1)
-                          : launch_glb<true, 1, false>(sc, cam, a, dyn, n, stream, block, e0, e1);
-  return tally ? launch_glb<false, 1, true>(sc, cam, a, dyn, n, stream, block, e0, e1)
-               : launch_glb<false, 1, false>(sc, cam, a, dyn, n, stream, block, e0, e1);
+  if (lane == 3) return launch_glb_lane<3>(quads, tally, cam_rays, sc, cam, a, dyn, n, stream, block, e0, e1);
+  if (lane == 1) return launch_glb_lane<1>(quads, tally, cam_rays, sc, cam, a, dyn, n, stream, block, e0, e1);
+  return hipErrorInvalidValue;
 }
 #endif  // RT_WF_GLOBAL_TU
 }  // namespace rtamd

@@ -112,7 +112,7 @@ int wf_tuning_apply(WfTuning& t, const char* key, int value);
 // with -DRT_WF_GLOBAL_TU). e0/e1: launch-carried profiling events, or null.
 struct DevCamera;
 struct WfArgs;
-hipError_t wf_launch_global(int lane, bool quads, bool tally, const DevScene& sc, const DevCamera& cam,
+hipError_t wf_launch_global(int lane, bool quads, bool tally, bool cam_rays, const DevScene& sc, const DevCamera& cam,
                             const WfArgs& a, size_t dyn, unsigned n, hipStream_t stream, int block, hipEvent_t e0,
                             hipEvent_t e1);
 
