@@ -1045,7 +1045,7 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   s->dev.planes = (const PlaneRec*)(b + o_pl);
   s->dev.quads = (const QuadRec*)(b + o_qd);
   s->dev.bvh = bvh.empty() ? nullptr : (const BvhNode*)(b + o_bv);
-  s->dev.bvh_pair = bvh.empty() ? nullptr : (const BvhPair*)(b + o_bp);
+  s->dev.bvh_pair = bvh_pair.empty() ? nullptr : (const BvhPair*)(b + o_bp);
   s->dev.n_bvh = (int32_t)bvh.size();
   s->dev.bvh_depth = bvh_depth;
   s->dev.obvh = obvh.empty() ? nullptr : (const BvhNode*)(b + o_ob);

@@ -333,6 +333,18 @@ std::vector<BvhNode> build_sphere_bvh(std::vector<SphereDiag>& spheres, int leaf
 }
 
 std::vector<BvhPair> pair_layout(const std::vector<BvhNode>& nodes) {
+  // the 16-bit child codes of the pair image (rt_layout.hpp BvhPair)
+  auto code16 = [](int32_t c, bool* ok) -> int32_t {
+    if (c == kBvhEmpty) return 0xFFFF;
+    if (c >= 0) {
+      if (c >= 0x8000) *ok = false;
+      return c;
+    }
+    const int code = -(c + 1), first = code >> 7, cnt = code & 127;
+    if (first >= 4095 || cnt < 1 || cnt > 8) *ok = false;
+    return 0x8000 | (first << 3) | (cnt - 1);
+  };
+  bool ok = true;
   std::vector<BvhPair> out(nodes.size());
   for (size_t i = 0; i < nodes.size(); ++i) {
     const BvhNode& g = nodes[i];
@@ -340,8 +352,12 @@ std::vector<BvhPair> pair_layout(const std::vector<BvhNode>& nodes) {
     for (int a = 0; a < 3; ++a) {
       q.b[4 * a] = g.lo[0][a]; q.b[4 * a + 1] = g.lo[1][a]; q.b[4 * a + 2] = g.hi[0][a]; q.b[4 * a + 3] = g.hi[1][a];
     }
-    q.child[0] = g.child[0]; q.child[1] = g.child[1]; q.axis = g.axis; q.pad = 0;
+    q.child[0] = code16(g.child[0], &ok);
+    q.child[1] = code16(g.child[1], &ok);
+    q.axis = g.axis;
+    q.pad = 0;
   }
+  if (!ok) out.clear();  // not encodable: no pair image (the fast path reads the binary nodes from global memory)
   return out;
 }
 

@@ -63,7 +63,10 @@ static_assert(sizeof(BvhNode) == 64, "BvhNode must stay 64 B");
 // The same node in the pair layout the per-lane traversal reads
 // (lane_trace_pair): per axis a, b[4a..4a+3] = lo[0][a], lo[1][a], hi[0][a],
 // hi[1][a], so the two children's entry (or exit) planes on an axis are one
-// 8-B pair, chosen by the sign of the ray's direction.
+// 8-B pair, chosen by the sign of the ray's direction. Its child codes are
+// 16-bit, so the traversal's LDS stack is too: a node index below 0x8000, a
+// leaf 0x8000 | first << 3 | (count - 1) (first < 4095, count <= 8), 0xFFFF
+// empty. A hierarchy that does not fit these codes has no pair image.
 struct alignas(64) BvhPair {
   float b[12];
   int32_t child[2];

@@ -205,6 +205,19 @@ __device__ __forceinline__ void leaf_sphere_test(const SphereDiag* sd, int k, V3
   sphere_test<SHADOW>(s0 * o.x + r.t[0], s1 * o.y + r.t[1], s2 * o.z + r.t[2], s0 * d.x, s1 * d.y, s2 * d.z,
                       [&] { return (int)r.meta; }, h, n_disc);
 }
+// The pair image's LDS copy of the sphere records (lane_scene, LANE 14): 48 B
+// per record (s[3], t[3]) and the metas apart, 52 B instead of 64.
+struct Sph48 {
+  const double* r;   // 6 doubles per record
+  const int* meta;
+};
+template <bool SHADOW>
+__device__ __forceinline__ void leaf_sphere_test(Sph48 sd, int k, V3 o, V3 d, Hit& h, unsigned& n_disc) {
+  const double* r = sd.r + 6 * k;
+  const double s0 = r[0], s1 = r[1], s2 = r[2];
+  sphere_test<SHADOW>(s0 * o.x + r[3], s1 * o.y + r[4], s2 * o.z + r[5], s0 * d.x, s1 * d.y, s2 * d.z,
+                      [&] { return sd.meta[k]; }, h, n_disc);
+}
 
 // With a treelet (the global-memory image), the first n_top nodes (breadth-first:
 // the top levels) are read from their LDS copy `top`, the rest from `nodes`.
@@ -298,11 +311,15 @@ __device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDia
 // fma(exit face, inv, -of), where lane_trace's min/max picks exactly them), so
 // the culling and the visit order are the same bit for bit. Leaves are
 // batched across the wave as in lane_trace<..., WW>.
+// The pair image's child codes are 16-bit (rt_layout.hpp BvhPair: a node
+// index below 0x8000, a leaf 0x8000 | first << 3 | (count - 1), 0xFFFF
+// empty), so the per-lane LDS stack holds 16-bit entries.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+constexpr int kPairEmpty = 0xFFFF;
 template <bool SHADOW>
-__device__ __forceinline__ void lane_trace_pair(const unsigned char* nodes, const SphereDiag* sd, const float* M,
+__device__ __forceinline__ void lane_trace_pair(const unsigned char* nodes, Sph48 sd, const float* M,
                                                 bool has_bvh, V3 o, V3 d, double t_shadow, Hit& h, unsigned& n_disc,
-                                                unsigned& n_tests, unsigned& n_boxes, int* lds) {
+                                                unsigned& n_tests, unsigned& n_boxes, uint16_t* lds) {
   float inv[3], on[3], of[3];
   int ent[3], ext[3];
   {
@@ -332,13 +349,13 @@ __device__ __forceinline__ void lane_trace_pair(const unsigned char* nodes, cons
 #pragma unroll
   for (int a = 0; a < 3; ++a) asm volatile("" : "+v"(ent[a]), "+v"(ext[a]));
   float t_hi = f32_up(SHADOW ? t_shadow : h.t);
-  auto stk = [&](int k) -> int& { return lds[k * kTraceBlock]; };
-  // entry 0 is a sentinel (kBvhEmpty): a pop needs no emptiness test, and a
+  auto stk = [&](int k) -> uint16_t& { return lds[k * kTraceBlock]; };
+  // entry 0 is a sentinel (kPairEmpty): a pop needs no emptiness test, and a
   // lane that pops it is done and pops no more (the stack holds bvh_depth + 1)
-  stk(0) = kBvhEmpty;
+  stk(0) = (uint16_t)kPairEmpty;
   int sp = 1;
-  auto pop = [&]() { return stk(--sp); };
-  int e = (SHADOW && h.key >= 0 && h.t < t_shadow) || !has_bvh ? kBvhEmpty : 0;
+  auto pop = [&]() { return (int)stk(--sp); };
+  int e = (SHADOW && h.key >= 0 && h.t < t_shadow) || !has_bvh ? kPairEmpty : 0;
   auto visit = [&]() {
     const unsigned char* nb = nodes + (size_t)e * 64;
     const f32x2 ex = *(const f32x2*)(nb + ent[0]), ey = *(const f32x2*)(nb + ent[1]), ez = *(const f32x2*)(nb + ent[2]);
@@ -355,19 +372,18 @@ __device__ __forceinline__ void lane_trace_pair(const unsigned char* nodes, cons
     const float u0 = fminf(fminf(tx1.x, ty1.x), fminf(tz1.x, t_hi));
     const float u1 = fminf(fminf(tx1.y, ty1.y), fminf(tz1.y, t_hi));
     const bool h0 = t0 <= u0;
-    const bool h1 = (t1 <= u1) & (cc.y != kBvhEmpty);
+    const bool h1 = (t1 <= u1) & (cc.y != kPairEmpty);
     n_boxes += 2;
     if (h0 && h1) {
       const bool flip = t1 < t0;
-      stk(sp++) = flip ? cc.x : cc.y;
+      stk(sp++) = (uint16_t)(flip ? cc.x : cc.y);
       e = flip ? cc.y : cc.x;
     } else {
       e = h0 ? cc.x : h1 ? cc.y : pop();
     }
   };
-  auto leaf = [&](int code_e) {
-    const int code = -(code_e + 1);
-    const int first = code >> 7, cnt = code & 127;
+  auto leaf = [&](int code) {
+    const int first = (code >> 3) & 0xFFF, cnt = (code & 7) + 1;
     for (int k = first; k < first + cnt; ++k) leaf_sphere_test<SHADOW>(sd, k, o, d, h, n_disc);
     n_tests += (unsigned)cnt;
     if constexpr (SHADOW) {
@@ -377,17 +393,17 @@ __device__ __forceinline__ void lane_trace_pair(const unsigned char* nodes, cons
       return false;
     }
   };
-  int pl = kBvhEmpty;
+  int pl = kPairEmpty;
   for (;;) {
     for (;;) {
-      if (e < 0 && e != kBvhEmpty && pl == kBvhEmpty) { pl = e; e = pop(); }
-      if (!__any(e >= 0 && pl == kBvhEmpty)) break;
-      if (e >= 0) visit();  // lanes holding a leaf keep going (speculative)
+      if (e >= 0x8000 && e != kPairEmpty && pl == kPairEmpty) { pl = e; e = pop(); }
+      if (!__any(e < 0x8000 && pl == kPairEmpty)) break;
+      if (e < 0x8000) visit();  // lanes holding a leaf keep going (speculative)
     }
-    if (!__any(pl != kBvhEmpty)) break;
-    if (pl != kBvhEmpty) {
-      if (leaf(pl)) { e = kBvhEmpty; sp = 1; }  // shadowed: done
-      pl = kBvhEmpty;
+    if (!__any(pl != kPairEmpty)) break;
+    if (pl != kPairEmpty) {
+      if (leaf(pl)) { e = kPairEmpty; sp = 1; }  // shadowed: done
+      pl = kPairEmpty;
     }
   }
 }
@@ -458,18 +474,27 @@ __device__ __forceinline__ void other_trace(const DevScene& sc, V3 o, V3 d, doub
 
 __host__ __device__ inline size_t lane_stack_bytes(int depth) { return (size_t)(depth > 0 ? depth : 1) * kTraceBlock * 4; }
 __host__ __device__ inline size_t sph_lds_bytes(const DevScene& sc) { return (size_t)sc.n_diag * sizeof(SphereDiag); }
+// the pair image's sphere records: 48 B each, then the metas (Sph48)
+__host__ __device__ inline size_t sph48_lds_bytes(const DevScene& sc) {
+  return (size_t)sc.n_diag * 48 + (((size_t)sc.n_diag * 4 + 15) & ~(size_t)15);
+}
 __host__ __device__ inline size_t delta_lds_bytes(const DevScene& sc) {
   return sc.lb_cells ? (((size_t)sc.n_lights * sc.n_diag * sizeof(float) + 15) & ~(size_t)15) : 0;
 }
-// LANE 14: [stack (bvh_depth + 1 with the sentinel) x kTraceBlock][pair nodes][sphere records]
+// LANE 14: [16-bit stack (bvh_depth + 1 with the sentinel) x kTraceBlock][pair nodes][Sph48 records]
+// (no pair image without the scene's 16-bit pair codes: rt_bvh.cpp pair_layout)
 __host__ __device__ inline size_t pair_lds_bytes(const DevScene& sc) {
-  return lane_stack_bytes(sc.bvh_depth + 1) + (size_t)sc.n_bvh * sizeof(BvhNode) + sph_lds_bytes(sc);
+  if (!sc.bvh_pair) return (size_t)1 << 40;
+  return ((lane_stack_bytes(sc.bvh_depth + 1) / 2 + 15) & ~(size_t)15) + (size_t)sc.n_bvh * sizeof(BvhNode) +
+         sph48_lds_bytes(sc);
 }
 constexpr unsigned kLdsSpheres = 1u, kLdsDeltas = 2u;  // lane_scene's lds_flags (LANE 0: records; all: distances)
 
 struct LaneScene {
   const unsigned char* nodes;  // pair layout in LDS (14) or BvhNode[] in global memory
-  const SphereDiag* sd;        // sphere records (LDS or global)
+  const SphereDiag* sd;        // sphere records (LDS or global; not LANE 14)
+  Sph48 s48;                   // LANE 14: the sphere records in LDS
+  uint16_t* stack16;           // LANE 14: the per-lane 16-bit LDS stack
   const float* delta;          // light buffer: per-light box distances (LDS or global)
   int* stack;                  // per-lane LDS stack (14, 3) or the wave's stack (0)
   float M[3];                  // bound on |box coordinate| per axis (slab_ray)
@@ -479,18 +504,33 @@ struct LaneScene {
 template <int LANE>
 __device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, unsigned lds_flags, unsigned n_top, int* static_stack,
                                                 unsigned char* dyn) {
-  LaneScene ls{(const unsigned char*)sc.bvh, sc.sph_diag, sc.lb_delta, static_stack, {0.f, 0.f, 0.f}, nullptr, 0};
+  LaneScene ls{(const unsigned char*)sc.bvh, sc.sph_diag, Sph48{nullptr, nullptr}, nullptr, sc.lb_delta, static_stack,
+               {0.f, 0.f, 0.f}, nullptr, 0};
   unsigned char* p = dyn;
   if constexpr (LANE == 14) {
     // pair layout (BvhPair): per axis, the two children's lower bounds form one
     // 8-B pair and their upper bounds the next (lane_trace_pair)
-    ls.stack = (int*)dyn + threadIdx.x;
-    p += lane_stack_bytes(sc.bvh_depth + 1);
+    ls.stack16 = (uint16_t*)dyn + threadIdx.x;
+    p += (lane_stack_bytes(sc.bvh_depth + 1) / 2 + 15) & ~(size_t)15;
     stage_lds((uint4*)p, (const uint4*)sc.bvh_pair, sc.n_bvh * (int)(sizeof(BvhPair) / 16));
     ls.nodes = p;
     p += (size_t)sc.n_bvh * sizeof(BvhPair);
+    // the sphere records, 48 B each (three of a SphereDiag's four 16-B chunks), and the metas
+    {
+      uint4* r = (uint4*)p;
+      const uint4* src = (const uint4*)sc.sph_diag;
+      const int n3 = sc.n_diag * 3, bd = (int)blockDim.x;
+      for (int i = (int)threadIdx.x; i < n3; i += bd) {
+        const int k = i / 3;
+        r[i] = src[4 * k + (i - 3 * k)];
+      }
+      int* mt = (int*)(p + (size_t)sc.n_diag * 48);
+      for (int k = (int)threadIdx.x; k < sc.n_diag; k += bd) mt[k] = (int)sc.sph_diag[k].meta;
+      ls.s48 = Sph48{(const double*)p, (const int*)mt};
+      p += sph48_lds_bytes(sc);
+    }
   }
-  if (LANE == 14 || (LANE == 0 && (lds_flags & kLdsSpheres))) {
+  if (LANE == 0 && (lds_flags & kLdsSpheres)) {
     stage_lds((uint4*)p, (const uint4*)sc.sph_diag, sc.n_diag * (int)(sizeof(SphereDiag) / 16));
     ls.sd = (const SphereDiag*)p;
     p += sph_lds_bytes(sc);
@@ -533,7 +573,8 @@ __device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, unsigned lds
 // the first blocker or at the first box farther from the light than the
 // origin. One 16-B load brings the cell's first kLbInline entries. An origin
 // beyond the light's validity radius (or non-finite) tests every sphere.
-__device__ __forceinline__ void lb_walk(const DevScene& sc, const SphereDiag* sd, const float* delta, unsigned l,
+template <typename SD>  // the sphere records: const SphereDiag* (global or LDS) or Sph48 (the pair image)
+__device__ __forceinline__ void lb_walk(const DevScene& sc, SD sd, const float* delta, unsigned l,
                                         V3 o, V3 d, double dist, Hit& h, unsigned& n_disc, unsigned& n_tests) {
   cLightRec Lr = (cLightRec)sc.lights + l;
   if (dist <= (double)sc.lb_limit[l] && dist >= 1e-30) {
@@ -591,9 +632,11 @@ __device__ __forceinline__ bool shadow_trace(const DevScene& sc, unsigned use_lb
   if constexpr (QUADS) other_trace<true>(sc, o, d, dist, h, n_disc, n_tests, n_boxes);
   if (!(h.key >= 0 && h.t < dist)) {
     if (use_lb) {
-      lb_walk(sc, ls.sd, ls.delta, l, o, d, dist, h, n_disc, n_tests);
+      if constexpr (LANE == 14) lb_walk(sc, ls.s48, ls.delta, l, o, d, dist, h, n_disc, n_tests);
+      else lb_walk(sc, ls.sd, ls.delta, l, o, d, dist, h, n_disc, n_tests);
     } else if constexpr (LANE == 14) {
-      lane_trace_pair<true>(ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, dist, h, n_disc, n_tests, n_boxes, ls.stack);
+      lane_trace_pair<true>(ls.nodes, ls.s48, ls.M, sc.n_bvh > 0, o, d, dist, h, n_disc, n_tests, n_boxes,
+                            ls.stack16);
     } else if constexpr (LANE == 0) {
       Hit hb;  // the wave traversal starts from an empty hit; any blocker is an answer
       bvh_trace<false, true>(sc, nullptr, ls.stack, o, d, dist, hb, n_disc, n_tests, n_boxes);

@@ -894,8 +894,8 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
         trace_rest<false, QUADS, true>(sc, o, d, h, t.disc);
         if constexpr (QUADS) other_trace<false>(sc, o, d, 0.0, h, t.disc, t.tests, t.boxes);
         if constexpr (LANE == 14)
-          lane_trace_pair<false>(ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, t.disc, t.tests, t.boxes,
-                                 ls.stack);
+          lane_trace_pair<false>(ls.nodes, ls.s48, ls.M, sc.n_bvh > 0, o, d, 0.0, h, t.disc, t.tests, t.boxes,
+                                 ls.stack16);
 #ifdef RTAMD_EXP_DUP_TRAV
         if constexpr (LANE == 14) {
           Hit h2;
@@ -903,7 +903,7 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
           V3 o2 = o;
           exp_opaque(o2.x);
           unsigned u0 = 0, u1 = 0, u2 = 0;
-          lane_trace_pair<false>(ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o2, d, 0.0, h2, u0, u1, u2, ls.stack);
+          lane_trace_pair<false>(ls.nodes, ls.s48, ls.M, sc.n_bvh > 0, o2, d, 0.0, h2, u0, u1, u2, ls.stack16);
           exp_sink(h2.t);
         }
 #endif
