@@ -38,6 +38,7 @@ int wf_tuning_apply(WfTuning& t, const char* key, int value) {
       {"treelet", &WfTuning::treelet, 0, 1},       {"treelet_deltas", &WfTuning::treelet_deltas, 0, 1},
       {"shadow_stream", &WfTuning::shadow_stream, 0, 2}, {"adaptive_block", &WfTuning::adaptive_block, 0, 1},
       {"prim_lane", &WfTuning::prim_lane, 0, 1},   {"arena_pct", &WfTuning::arena_pct, 1, 100},
+      {"compact", &WfTuning::compact, 0, 1},
       {"d2h", &WfTuning::d2h, 0, 1}};
   if (!key) return 0;
   for (const Knob& k : knobs) {
@@ -707,7 +708,7 @@ struct FusedTally {
 // calls it (shard_append), `valid` false for the padding lanes.
 template <int LANE, bool QUADS, bool CAM>
 __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera& cam, const WfArgs& a,
-                                            const LaneScene& ls, unsigned i, unsigned slot, bool valid, V3 o, V3 d,
+                                            const LaneScene& ls, unsigned q, unsigned slot, bool valid, V3 o, V3 d,
                                             const Hit& h, FusedTally& t) {
   const unsigned L = (unsigned)sc.n_lights;
   const unsigned remaining = a.max_depth - a.g;
@@ -743,7 +744,7 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
   }
   const bool parent = want_refl || want_refr;
   unsigned pbase, rbase, fbase;
-  shard_append(a, i / 64, parent ? 1u : 0u, want_refl, want_refr, pbase, rbase, fbase, ray_class_r(sc, hit, c),
+  shard_append(a, q, parent ? 1u : 0u, want_refl, want_refr, pbase, rbase, fbase, ray_class_r(sc, hit, c),
                ray_class_f(hit, c));
   if (!valid) return;
   t.hits += hit; t.refl += want_refl; t.refr += want_refr;
@@ -822,7 +823,17 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
 // per-visit and per-test counting and the wave-end atomics altogether: C3
 // 1.021 -> 0.964 ms/frame, an 8-way shard 0.204 -> 0.184 ms.
 // CAM: the launch may read camera rays (generation 0 of a camera render).
-template <bool PRIMARY, bool QUADS, int LANE, bool TALLY, bool CAM = PRIMARY>
+// COMPACT (LANE 14): shading at full width (DESIGN.md "Compacted shading"):
+// the hits of each traversed chunk go to a per-wave LDS queue (misses are
+// written black at once), and the wave shades 64 queued hits at a time, so
+// the shading, shadow rays and spawns run with every lane busy instead of
+// with the chunk's misses idle. The appends of a shaded batch use the index
+// of the chunk whose traversal filled it (at most one batch per chunk), and
+// the wave's last, partial batch the index of one of its chunks that filled
+// none (there is one: a wave that shaded a batch after each of its k chunks
+// queued 64 k hits, so none are left), so every wave-iteration index is a
+// chunk's, used once, and the capacity argument ("Sharded queues") holds.
+template <bool PRIMARY, bool QUADS, int LANE, bool TALLY, bool CAM = PRIMARY, bool COMPACT = false>
 __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, DevCamera cam, WfArgs a) {
   __shared__ int stack_lds[LANE == 3 ? kLaneLdsDepth * kTraceBlock
                            : LANE == 0 ? (kTraceBlock / 64) * (kBvhMaxDepth + 4) : 1];
@@ -870,15 +881,8 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
     if (lane_id() == 0) k0 = atomicAdd(ctr, 1u);
     c = cls + X * (unsigned)__shfl((int)k0, 0, 64);
   }
-  while (c < n_chunks) {
-    unsigned k_next = 0;
-    if (dyn && lane_id() == 0) k_next = atomicAdd(ctr, 1u);
-    const unsigned i = c * 64u + lane_id();
-    // a batch's generation 0: the padding slots after each frame's root rays hold no ray
-    const bool valid = i < a.n && (a.g != 0 || a.n_frames <= 1 || i % a.frame_rays < a.frame_real);
-    const unsigned slot = valid ? shard_slot<true>(pre, a.in_cap, i) : 0u;
-    V3 o = v3(0, 0, 0), d = v3(0, 0, 0);
-    Hit h;
+  // the chunk's rays, traversed: o, d and the hit of ray i (slot) of chunk c
+  auto traverse = [&](unsigned i, bool valid, unsigned slot, V3& o, V3& d, Hit& h) {
     hit_init(h);
     if (valid) {
       wf_ray<CAM>(a, cam, slot, o, d);
@@ -893,11 +897,10 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
         // planes and the other records first: an early nearest hit tightens the culling
         trace_rest<false, QUADS, true>(sc, o, d, h, t.disc);
         if constexpr (QUADS) other_trace<false>(sc, o, d, 0.0, h, t.disc, t.tests, t.boxes);
-        if constexpr (LANE == 14)
+        if constexpr (LANE == 14) {
           lane_trace_pair<false>(ls.nodes, ls.s48, ls.M, sc.n_bvh > 0, o, d, 0.0, h, t.disc, t.tests, t.boxes,
                                  ls.stack16);
 #ifdef RTAMD_EXP_DUP_TRAV
-        if constexpr (LANE == 14) {
           Hit h2;
           hit_init(h2);
           V3 o2 = o;
@@ -905,16 +908,109 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
           unsigned u0 = 0, u1 = 0, u2 = 0;
           lane_trace_pair<false>(ls.nodes, ls.s48, ls.M, sc.n_bvh > 0, o2, d, 0.0, h2, u0, u1, u2, ls.stack16);
           exp_sink(h2.t);
-        }
 #endif
-        else
+        } else {
           lane_trace<false, LANE == 3>((const BvhNode*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, t.disc,
                                        t.tests, t.boxes, ls.stack, ls.top, ls.n_top);
+        }
       }
     }
     hit_finish(h);
-    shade_fused<LANE, QUADS, CAM>(sc, cam, a, ls, i, slot, valid, o, d, h, t);
-    c = dyn ? c_base + X * (unsigned)__shfl((int)k_next, 0, 64) : c + W;
+  };
+  if constexpr (!COMPACT) {
+    while (c < n_chunks) {
+      unsigned k_next = 0;
+      if (dyn && lane_id() == 0) k_next = atomicAdd(ctr, 1u);
+      const unsigned i = c * 64u + lane_id();
+      // a batch's generation 0: the padding slots after each frame's root rays hold no ray
+      const bool valid = i < a.n && (a.g != 0 || a.n_frames <= 1 || i % a.frame_rays < a.frame_real);
+      const unsigned slot = valid ? shard_slot<true>(pre, a.in_cap, i) : 0u;
+      V3 o = v3(0, 0, 0), d = v3(0, 0, 0);
+      Hit h;
+      traverse(i, valid, slot, o, d, h);
+      shade_fused<LANE, QUADS, CAM>(sc, cam, a, ls, c, slot, valid, o, d, h, t);
+      c = dyn ? c_base + X * (unsigned)__shfl((int)k_next, 0, 64) : c + W;
+    }
+  } else {
+    // the wave's queue (kQueue entries, structure of arrays) after the image
+    const unsigned wv = threadIdx.x >> 6, lane = lane_id();
+    unsigned char* qb = lane_dyn + a.q_off;
+    double* qt = (double*)qb + wv * kQueue;                                        // t
+    unsigned* qs = (unsigned*)(qb + 16 * kQueue * 8) + wv * kQueue;                // slot | hin << 31
+    int* qk = (int*)(qb + 16 * kQueue * 12) + wv * kQueue;                         // key
+    unsigned* qc = (unsigned*)(qb + 16 * kQueue * 16) + wv * kQueue;               // (c1k + 1) | (c2k + 1) << 16
+    unsigned qn = 0;     // queued hits (wave-uniform)
+    unsigned spare = 0;  // a chunk of this wave whose traversal filled no batch
+    for (;;) {
+      const bool have = c < n_chunks;
+      unsigned q_idx;
+      if (have) {
+        unsigned k_next = 0;
+        if (dyn && lane == 0) k_next = atomicAdd(ctr, 1u);
+        const unsigned i = c * 64u + lane;
+        const bool valid = i < a.n && (a.g != 0 || a.n_frames <= 1 || i % a.frame_rays < a.frame_real);
+        const unsigned slot = valid ? shard_slot<true>(pre, a.in_cap, i) : 0u;
+        V3 o = v3(0, 0, 0), d = v3(0, 0, 0);
+        Hit h;
+        traverse(i, valid, slot, o, d, h);
+        const bool hit = valid && h.key >= 0;
+        if (valid && !hit) {  // color_at: a miss is black (world.rs:74-75)
+          double* dst = color_dst<CAM>(a, cam, slot);
+          st_d(dst, 0.0); st_d(dst + 1, 0.0); st_d(dst + 2, 0.0);
+        }
+        const unsigned long long m = __ballot(hit);
+        if (hit) {
+          const unsigned p = qn + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+          qt[p] = h.t;
+          qs[p] = slot | ((unsigned)h.hin << 31);
+          qk[p] = h.key;
+          qc[p] = (unsigned)(h.c1k + 1) | ((unsigned)(h.c2k + 1) << 16);
+        }
+        qn += (unsigned)__popcll(m);
+        q_idx = c;
+        c = dyn ? c_base + X * (unsigned)__shfl((int)k_next, 0, 64) : c + W;
+        if (qn < 64u) {
+          spare = q_idx;
+          continue;
+        }
+      } else {
+        if (qn == 0) break;
+        q_idx = spare;  // the wave's last, partial batch
+      }
+      // shade the queue's first min(qn, 64) hits, one per lane
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const unsigned nb = qn < 64u ? qn : 64u;
+      const bool live = lane < nb;
+      Hit h;
+      hit_init(h);
+      unsigned slot = 0;
+      V3 o = v3(0, 0, 0), d = v3(0, 0, 0);
+      if (live) {
+        const unsigned sh = qs[lane];
+        const unsigned cc = qc[lane];
+        slot = sh & 0x7FFFFFFFu;
+        h.t = qt[lane];
+        h.key = qk[lane];
+        h.hin = (int)(sh >> 31);
+        h.c1k = (int)(cc & 0xFFFFu) - 1;
+        h.c2k = (int)(cc >> 16) - 1;
+        wf_ray<CAM>(a, cam, slot, o, d);
+      }
+      // the rest of the queue moves to its front (entries [64, qn) -> [0, qn - 64))
+      const unsigned rest = qn - nb;
+      double rt = 0.0;
+      unsigned rs = 0, rc = 0;
+      int rk = 0;
+      if (lane < rest) { rt = qt[64 + lane]; rs = qs[64 + lane]; rk = qk[64 + lane]; rc = qc[64 + lane]; }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (lane < rest) { qt[lane] = rt; qs[lane] = rs; qk[lane] = rk; qc[lane] = rc; }
+      qn = rest;
+      shade_fused<LANE, QUADS, CAM>(sc, cam, a, ls, q_idx, slot, live, o, d, h, t);
+    }
   }
   if constexpr (!TALLY) return;
   const unsigned long long s = wave_sum(t.disc), st = wave_sum(t.tests), sb = wave_sum(t.boxes);
@@ -1448,7 +1544,22 @@ static hipError_t launch_fused_q(const DevScene& sc, const DevCamera& cam, WfArg
   const bool cam_rays = a.g == 0 && a.camera_mode;  // only generation 0 of a camera render reads camera rays
   if (tn.image == 0 && pair_lds_bytes(sc) <= kWfLdsLimit) {
     dyn = pair_lds_bytes(sc);
-    if (dl && dyn + dl <= kWfLdsLimit) { a.lds_flags |= kLdsDeltas; dyn += dl; }
+    // compacted shading (the hit queues' 16-bit object codes need n_objects < 16383); the
+    // light buffer's distances take what room is left
+    const size_t qoff = (dyn + 15) & ~(size_t)15;
+    const bool compact = tn.compact && sc.n_objects < 16383 && qoff + kQueueLdsBytes <= kWfLdsLimit;
+    if (compact) {
+      a.q_off = (unsigned)qoff;
+      dyn = qoff + kQueueLdsBytes;
+    }
+    if (dl && dyn + dl <= kWfLdsLimit) {  // (lane_scene stages them right after the image: the queue moves up)
+      a.lds_flags |= kLdsDeltas;
+      if (compact) a.q_off = (unsigned)((pair_lds_bytes(sc) + dl + 15) & ~(size_t)15);
+      dyn += dl;
+    }
+    if (compact)
+      return cam_rays ? launch_lds(wf_trace_fused<false, QUADS, 14, TALLY, true, true>, dyn, n, stream, sc, cam, a, tb)
+                      : launch_lds(wf_trace_fused<false, QUADS, 14, TALLY, false, true>, dyn, n, stream, sc, cam, a, tb);
     return cam_rays ? launch_lds(wf_trace_fused<false, QUADS, 14, TALLY, true>, dyn, n, stream, sc, cam, a, tb)
                     : launch_lds(wf_trace_fused<false, QUADS, 14, TALLY, false>, dyn, n, stream, sc, cam, a, tb);
   }

@@ -98,6 +98,7 @@ struct WfTuning {
   int treelet_deltas = 0;  // ... after the light buffer's distances (when they fit)
   int shadow_stream = 1;   // exhaustive pipeline: 1 = shadow traces on a second stream when rendering alone
   int adaptive_block = 0;  // generation pipeline: 1 = small trace launches spread over every CU
+  int compact = 1;         // fast path, pair image: 1 = compacted shading (hit queues in LDS, full-width shading)
   int prim_lane = 0;       // fast path: 1 = primary rays by the per-lane pair traversal (LDS image) instead
                            //     of the wave traversal with shared-origin records
   int arena_pct = 100;     // test hook: the fast path's queue arenas sized to this percentage of the hint,
@@ -277,7 +278,12 @@ struct WfArgs {
   ParentRec* par_base;
   unsigned long long color_cap, par_cap, ray_cap;  // colour slots, parent records, ray slots per buffer
   WfHostRec* hrec;                  // device address of the workspace's host-mapped record
+  unsigned q_off;                   // compacted shading (LANE 14): the waves' hit queues in dynamic LDS
 };
+// compacted shading: entries of a wave's hit queue (t, slot | hin, key, c1k / c2k: 20 B each);
+// it holds at most 63 left from the last batch + one chunk's 64 hits
+constexpr unsigned kQueue = 127;
+constexpr size_t kQueueLdsBytes = (size_t)16 * kQueue * 20;  // the block's 16 waves
 
 // Per-kernel-class timing of the last frame (profiling mode only).
 enum WfClass { WF_PRIMARY = 0, WF_CLOSEST = 1, WF_SHADOW = 2, WF_PREP = 3, WF_COMBINE = 4, WF_NCLASS = 5 };

@@ -214,17 +214,19 @@ def test_skipped_shadow_rays_bitwise(rt, neg_zero):
     assert full.to_numpy().tobytes() == exact.to_numpy().tobytes()
 
 
-@pytest.mark.parametrize("image,shadow_lb", [(0, 1), (0, 0), (3, 1), (3, 0), (1, 1), (1, 0)])
-def test_fused_images_bitwise(rt, image, shadow_lb):
+@pytest.mark.parametrize("image,shadow_lb,compact", [(0, 1, 1), (0, 0, 1), (0, 1, 0), (0, 0, 0), (3, 1, 1),
+                                                    (3, 0, 1), (1, 1, 1), (1, 0, 1)])
+def test_fused_images_bitwise(rt, image, shadow_lb, compact):
     """Every scene image of the fast-path kernels (pair layout in LDS, the
-    default / nodes and records in global memory with an LDS stack / with a
-    scratch stack), with shadow rays through the light buffer or through the
-    BVH, gives the exhaustive frame. The scenes above that do not fit in LDS
-    (3000 spheres) run image 3 on their own."""
+    default, with and without compacted shading / nodes and records in global
+    memory with an LDS stack / with a scratch stack), with shadow rays through
+    the light buffer or through the BVH, gives the exhaustive frame. The scenes
+    above that do not fit in LDS (3000 spheres) run image 3 on their own."""
     w, cam, depth = _glass_cluster(rt, n=250, seed=21, inside=False)
     exact, _ = cam.render(w, depth, want_stats=True)
     w.tune("image", image)
     w.tune("shadow_lb", shadow_lb)
+    w.tune("compact", compact)
     try:
         fast, _ = cam.render(w, depth, want_stats=False)
         p = rt._rtamd._wf_profile(w, -1, True)
@@ -232,6 +234,7 @@ def test_fused_images_bitwise(rt, image, shadow_lb):
     finally:
         w.tune("image", 0)
         w.tune("shadow_lb", 1)
+        w.tune("compact", 1)
     assert fast.to_numpy().tobytes() == exact.to_numpy().tobytes()
 
 

@@ -1,7 +1,8 @@
 #!/bin/bash
 # Time library variants on one box, alternating (dev tool, on the GPU box):
-#   ROUNDS=2 bash tools/exp_time.sh TAG [ARGS="--config c3"] base NAME [NAME ...]
-# `base` is the default build (lib/); NAME is lib_exp_NAME (tools/exp_build.sh).
+#   ROUNDS=2 bash tools/exp_time.sh TAG [ARGS="--config c3"] base NAME[:k=v,k=v] [...]
+# `base` is the default build (lib/); NAME is lib_exp_NAME (tools/exp_build.sh);
+# ":k=v,..." adds tuning knobs (quick_time.py --knob) to that variant.
 # Each run is tools/quick_time.py under its own time limit; the chain stops at
 # the first failure.
 set -o pipefail
@@ -12,10 +13,14 @@ mkdir -p "$OUT"
 PKG=raytracer-challenge-rs_amd
 for i in $(seq 1 "${ROUNDS:-2}"); do
   for v in "$@"; do
-    if [ "$v" = base ]; then lp=""; else lp="$PWD/$PKG/lib_exp_$v"; fi
+    lib=${v%%:*}
+    knobs=""
+    if [ "$lib" != "$v" ]; then for kv in $(echo "${v#*:}" | tr ',' ' '); do knobs="$knobs --knob $kv"; done; fi
+    if [ "$lib" = base ]; then lp=""; else lp="$PWD/$PKG/lib_exp_$lib"; fi
+    log="$OUT/$(echo "$v" | tr ':,=' '___')_$i.log"
     # shellcheck disable=SC2086
     LD_LIBRARY_PATH="$lp${LD_LIBRARY_PATH:+:$LD_LIBRARY_PATH}" timeout -k 10 240 \
-      python tools/quick_time.py --tag "$v" ${ARGS:-} > "$OUT/${v}_$i.log" 2>&1 || { echo "variant $v failed"; tail -5 "$OUT/${v}_$i.log"; exit 1; }
-    grep '^{' "$OUT/${v}_$i.log" | tail -1
+      python tools/quick_time.py --tag "$v" $knobs ${ARGS:-} > "$log" 2>&1 || { echo "variant $v failed"; tail -5 "$log"; exit 1; }
+    grep '^{' "$log" | tail -1
   done
 done
