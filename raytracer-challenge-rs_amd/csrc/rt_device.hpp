@@ -111,17 +111,15 @@ __device__ __forceinline__ void sphere_adc(double a, double dt, double c, MetaFn
     const int meta = meta_fn();
     const double q = sqrt(disc);
     const double t1 = (-dt - q) / a;
-    const double t2 = (-dt + q) / a;
     const int k1 = (meta >> 1) << kKeyShift;
     const bool eligible = !SHADOW || (meta & 1);
-    if (eligible) {
-      if (t1 >= 0.0) {
-        if (better(t1, k1, h.t, h.key)) { h.t = t1; h.key = k1; h.hin = 0; }
-      } else if (t2 >= 0.0) {
-        if (better(t2, k1 + 1, h.t, h.key)) { h.t = t2; h.key = k1 + 1; h.hin = 1; }
-      }
+    if (t1 >= 0.0) {
+      if (eligible && better(t1, k1, h.t, h.key)) { h.t = t1; h.key = k1; h.hin = 0; }
+    } else {  // root 2 matters only now (t1 < 0 or NaN): its division is left out otherwise
+      const double t2 = (-dt + q) / a;
+      if (eligible && t2 >= 0.0 && better(t2, k1 + 1, h.t, h.key)) { h.t = t2; h.key = k1 + 1; h.hin = 1; }
+      if (!SHADOW && t1 < 0.0 && t2 >= 0.0) push_container(h, t1, k1);
     }
-    if (!SHADOW && t1 < 0.0 && t2 >= 0.0) push_container(h, t1, k1);
   }
 }
 template <bool SHADOW, typename MetaFn>

@@ -81,23 +81,29 @@ typedef const RT_CONST PrimRec* cPrimRec;
 
 // The per-lane traversal's slab test runs in binary32 on an interval that is
 // widened to contain the exact (real-arithmetic) one; DESIGN.md §5.2 has the
-// error bound. Per ray and axis: inv = 1/d, and the plane constants
-// c = o*inv -/+ delta with delta = 2^-20 |inv| (M + |o|), where M bounds every
-// box coordinate on that axis (the root's children); the computed entry
-// (exit) distance fma(corner, inv, -c) then never exceeds (falls short of)
-// the exact one: its rounding error is below 2^-23 |inv| (M + |o|) = delta/8.
+// error bound. Per ray and axis: inv = an approximate reciprocal of d in
+// binary32 (slab_inv: relative error below 2^-22, exactly the value the FMAs
+// use), and the plane constants c = o*inv -/+ delta with delta = 2^-20 |inv|
+// (M + |o|), where M bounds every box coordinate on that axis (the root's
+// children); the computed entry (exit) distance fma(corner, inv, -c) then
+// never exceeds (falls short of) the exact one, (corner - o) / d: its error,
+// the reciprocal's included, is below delta/3.
 // An axis whose direction is (nearly) zero or whose origin is huge / NaN is
 // not used for culling at all (interval (-inf, +inf)).
 struct SlabRay {
   float inv[3], c_lo[3], c_hi[3];
 };
+// binary32 reciprocal of a binary64 direction component with 2^-60 <= |d|:
+// (float)d rounds once (2^-24), v_rcp_f32 is within 1 ulp (2^-23); returned
+// widened to binary64 (exact), the value every plane constant is built from.
+__device__ __forceinline__ double slab_inv(double d) { return (double)__builtin_amdgcn_rcpf((float)d); }
 __device__ __forceinline__ SlabRay slab_ray(V3 o, V3 d, const float* M) {
   SlabRay r;
   const double oa[3] = {o.x, o.y, o.z}, da[3] = {d.x, d.y, d.z};
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
     if (fabs(da[a]) >= 0x1p-60 && fabs(oa[a]) <= 0x1p60 && M[a] <= 0x1p60f) {  // NaN fails
-      const double inv = 1.0 / da[a];
+      const double inv = slab_inv(da[a]);
       const double oinv = oa[a] * inv;
       const double delta = 0x1p-20 * fabs(inv) * ((double)M[a] + fabs(oa[a]));
       const float on = (float)(oinv + delta), of = (float)(oinv - delta);
@@ -328,7 +334,7 @@ __device__ __forceinline__ void lane_trace_pair(const unsigned char* nodes, Sph4
     for (int a = 0; a < 3; ++a) {
       bool neg = false;
       if (fabs(da[a]) >= 0x1p-60 && fabs(oa[a]) <= 0x1p60 && M[a] <= 0x1p60f) {  // as slab_ray; NaN fails
-        const double iv = 1.0 / da[a];
+        const double iv = slab_inv(da[a]);
         const double oinv = oa[a] * iv;
         const double delta = 0x1p-20 * fabs(iv) * ((double)M[a] + fabs(oa[a]));
         inv[a] = (float)iv;
@@ -589,7 +595,10 @@ __device__ __forceinline__ void lb_walk(const DevScene& sc, SD sd, const float* 
     if (ax >= ay && ax >= az) { f = wx < 0.0f ? 1u : 0u; wa = ax; wb = wy; wc = wz; }
     else if (ay >= az) { f = wy < 0.0f ? 3u : 2u; wa = ay; wb = wz; wc = wx; }
     else { f = wz < 0.0f ? 5u : 4u; wa = az; wb = wx; wc = wy; }
-    const float u = fminf(fmaxf(wb / wa, -1.0f), 1.0f), v = fminf(fmaxf(wc / wa, -1.0f), 1.0f);
+    // (an approximate reciprocal: within 2 ulp, 2.4e-7 of the cube-face coordinate, far inside the
+    // host's 1e-5 margins)
+    const float rwa = __builtin_amdgcn_rcpf(wa);
+    const float u = fminf(fmaxf(wb * rwa, -1.0f), 1.0f), v = fminf(fmaxf(wc * rwa, -1.0f), 1.0f);
     const unsigned iu = (unsigned)min((int)((u + 1.0f) * half_r), R - 1);
     const unsigned iv = (unsigned)min((int)((v + 1.0f) * half_r), R - 1);
     const LbCell c = sc.lb_cells[l * per_light + (f * (unsigned)R + iv) * (unsigned)R + iu];
