@@ -212,7 +212,10 @@ __device__ __forceinline__ unsigned frame_of(const WfArgs& a, unsigned i, unsign
 // generations read their queue.
 // CAM = false: a launch that never reads camera rays (generations >= 1, or
 // explicit rays), compiled without the camera path and its registers.
-template <bool CAM = true>
+// NT: the ray's last read (non-temporal: it leaves the L2 to the scene); the
+// compacted kernel reads a ray twice (traversal, then shading) and keeps the
+// first read in the L2.
+template <bool CAM = true, bool NT = true>
 __device__ __forceinline__ void wf_ray(const WfArgs& a, const DevCamera& cam, unsigned i, V3& o, V3& d) {
   if (CAM && a.g == 0 && a.camera_mode) {
     unsigned li;
@@ -230,8 +233,12 @@ __device__ __forceinline__ void wf_ray(const WfArgs& a, const DevCamera& cam, un
     }
   } else {
     const f64x2* r = reinterpret_cast<const f64x2*>(a.rays + i);  // 48 B, 16-B aligned
-    const f64x2 r0 = __builtin_nontemporal_load(r), r1 = __builtin_nontemporal_load(r + 1),
-                r2 = __builtin_nontemporal_load(r + 2);
+    f64x2 r0, r1, r2;
+    if constexpr (NT) {
+      r0 = __builtin_nontemporal_load(r); r1 = __builtin_nontemporal_load(r + 1); r2 = __builtin_nontemporal_load(r + 2);
+    } else {
+      r0 = r[0]; r1 = r[1]; r2 = r[2];
+    }
     o = v3(r0.x, r0.y, r1.x);
     d = v3(r1.y, r2.x, r2.y);
   }
@@ -885,7 +892,7 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
   auto traverse = [&](unsigned i, bool valid, unsigned slot, V3& o, V3& d, Hit& h) {
     hit_init(h);
     if (valid) {
-      wf_ray<CAM>(a, cam, slot, o, d);
+      wf_ray<CAM, !COMPACT>(a, cam, slot, o, d);
       if constexpr (LANE == 0) {
         // the chunk's frame (chunks never mix frames): its shared-origin primary records
         const unsigned pf = a.n_frames > 1 ? (c * 64u) / a.frame_rays : 0u;
@@ -959,6 +966,15 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
           st_d(dst, 0.0); st_d(dst + 1, 0.0); st_d(dst + 2, 0.0);
         }
         const unsigned long long m = __ballot(hit);
+#ifdef RTAMD_EXP_DIRECT
+        // a chunk with many hits is shaded at once, in its own lanes (its index is its own)
+        if ((unsigned)__popcll(m) >= (unsigned)(RTAMD_EXP_DIRECT)) {
+          q_idx = c;
+          c = dyn ? c_base + X * (unsigned)__shfl((int)k_next, 0, 64) : c + W;
+          shade_fused<LANE, QUADS, CAM>(sc, cam, a, ls, q_idx, slot, hit, o, d, h, t);
+          continue;
+        }
+#endif
         if (hit) {
           const unsigned p = qn + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
           qt[p] = h.t;
