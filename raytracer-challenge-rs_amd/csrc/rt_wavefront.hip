@@ -993,10 +993,9 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
         if (qn == 0) break;
         q_idx = spare;  // the wave's last, partial batch
       }
-      // shade the queue's first min(qn, 64) hits, one per lane
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // shade the queue's first min(qn, 64) hits, one per lane (the LDS executes a wave's
+      // accesses in order: only the compiler must not reorder them, no fence or wait)
+      asm volatile("" ::: "memory");
       const unsigned nb = qn < 64u ? qn : 64u;
       const bool live = lane < nb;
       Hit h;
@@ -1020,9 +1019,7 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
       unsigned rs = 0, rc = 0;
       int rk = 0;
       if (lane < rest) { rt = qt[64 + lane]; rs = qs[64 + lane]; rk = qk[64 + lane]; rc = qc[64 + lane]; }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      asm volatile("" ::: "memory");
       if (lane < rest) { qt[lane] = rt; qs[lane] = rs; qk[lane] = rk; qc[lane] = rc; }
       qn = rest;
       shade_fused<LANE, QUADS, CAM>(sc, cam, a, ls, q_idx, slot, live, o, d, h, t);
