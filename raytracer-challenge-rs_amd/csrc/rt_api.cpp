@@ -357,7 +357,12 @@ int copy_to_host(rt_scene::HostCtx* s, int d2h, void* dst, const void* src, size
       if (e == hipSuccess) e = hipStreamSynchronize(st);
       const hipError_t u = hipHostUnregister(dst);
       if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("device-to-host copy: ") + hipGetErrorString(e));
-      if (u != hipSuccess) return fail(RT_ERR_HIP, std::string("hipHostUnregister: ") + hipGetErrorString(u));
+      // The frame is in dst and correct: a failed unregister is noted in
+      // rt_last_error's text but does not discard it.
+      if (u != hipSuccess) {
+        (void)hipGetLastError();
+        (void)fail(RT_OK, std::string("note: hipHostUnregister after a completed copy: ") + hipGetErrorString(u));
+      }
       return RT_OK;
     }
     (void)hipGetLastError();  // not registrable (e.g. already pinned memory): the staging chunks below
@@ -558,7 +563,7 @@ const char* rt_last_error(void) { return g_err.c_str(); }
 // n_diag, n_gen, n_planes, n_lights, n_quads, tests[3], boxes[3], bvh,
 // n_bvh_nodes, bvh_depth, n_obvh_nodes, n_other_culled, lb_res, lb_items, sh_rays[2], sh_tests[2]
 // (shadow rays / sphere tests inside the fused primary / secondary launches), fused.
-int rtamd_wf_profile(const rt_scene* cs, int enable, double out[34]) {
+int rtamd_wf_profile(const rt_scene* cs, int enable, double out[36]) {
   if (!cs) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
   rt_scene* s = const_cast<rt_scene*>(cs);
   std::lock_guard<std::mutex> lk(s->mu);
@@ -601,6 +606,8 @@ int rtamd_wf_profile(const rt_scene* cs, int enable, double out[34]) {
     out[28] = s->dev.lb_cells ? s->dev.lb_n_items : 0;
     for (int i = 0; i < 2; ++i) { out[29 + i] = p.sh_rays[i]; out[31 + i] = p.sh_tests[i]; }
     out[33] = p.fused;
+    out[34] = s->dev.bvhw ? s->dev.n_bvhw : 0;
+    out[35] = s->dev.bvhw ? s->dev.bvhw_stack : 0;
   }
   return RT_OK;
 }
@@ -933,6 +940,8 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
     if (image > kFusedLdsLimit) bvh = build_sphere_bvh(diag, 1, &bvh_depth, g_bvh_ct / 100.0);
   }
   const std::vector<BvhPair> bvh_pair = pair_layout(bvh);
+  int wide_stack = 0;
+  const std::vector<BvhWide> bvh_wide = wide_layout(bvh, diag, &wide_stack);
   // ... and over the other bounded records (general spheres, cubes, cylinders
   // with finite caps); the rest stays exhaustive on the fast path too
   std::vector<OtherRec> orec;
@@ -983,7 +992,8 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   const size_t o_qd = align(o_pl + (planes.size() + 1) * sizeof(PlaneRec));
   const size_t o_bv = align(o_qd + (quads.size() + 1) * sizeof(QuadRec));
   const size_t o_bp = align(o_bv + (bvh.size() + 1) * sizeof(BvhNode));
-  const size_t o_ob = align(o_bp + (bvh_pair.size() + 1) * sizeof(BvhPair));
+  const size_t o_bw = align(o_bp + (bvh_pair.size() + 1) * sizeof(BvhPair));
+  const size_t o_ob = align(o_bw + (bvh_wide.size() + 1) * sizeof(BvhWide));
   const size_t o_or = align(o_ob + (obvh.size() + 1) * sizeof(BvhNode));
   const size_t o_fg = align(o_or + (orec.size() + 1) * sizeof(OtherRec));
   const size_t o_fq = align(o_fg + (fx_gen.size() + 1) * sizeof(SphereGen));
@@ -1001,6 +1011,7 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   if (!quads.empty()) std::memcpy(&host[o_qd], quads.data(), quads.size() * sizeof(QuadRec));
   if (!bvh.empty()) std::memcpy(&host[o_bv], bvh.data(), bvh.size() * sizeof(BvhNode));
   if (!bvh_pair.empty()) std::memcpy(&host[o_bp], bvh_pair.data(), bvh_pair.size() * sizeof(BvhPair));
+  if (!bvh_wide.empty()) std::memcpy(&host[o_bw], bvh_wide.data(), bvh_wide.size() * sizeof(BvhWide));
   if (!obvh.empty()) std::memcpy(&host[o_ob], obvh.data(), obvh.size() * sizeof(BvhNode));
   if (!orec.empty()) std::memcpy(&host[o_or], orec.data(), orec.size() * sizeof(OtherRec));
   if (!fx_gen.empty()) std::memcpy(&host[o_fg], fx_gen.data(), fx_gen.size() * sizeof(SphereGen));
@@ -1046,6 +1057,9 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   s->dev.quads = (const QuadRec*)(b + o_qd);
   s->dev.bvh = bvh.empty() ? nullptr : (const BvhNode*)(b + o_bv);
   s->dev.bvh_pair = bvh_pair.empty() ? nullptr : (const BvhPair*)(b + o_bp);
+  s->dev.bvhw = bvh_wide.empty() ? nullptr : (const BvhWide*)(b + o_bw);
+  s->dev.n_bvhw = (int32_t)bvh_wide.size();
+  s->dev.bvhw_stack = wide_stack;
   s->dev.n_bvh = (int32_t)bvh.size();
   s->dev.bvh_depth = bvh_depth;
   s->dev.obvh = obvh.empty() ? nullptr : (const BvhNode*)(b + o_ob);

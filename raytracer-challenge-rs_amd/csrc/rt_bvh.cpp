@@ -361,6 +361,155 @@ std::vector<BvhPair> pair_layout(const std::vector<BvhNode>& nodes) {
   return out;
 }
 
+std::vector<BvhWide> wide_layout(const std::vector<BvhNode>& nodes, const std::vector<SphereDiag>& spheres,
+                                 int* stack) {
+  if (stack) *stack = 0;
+  std::vector<BvhWide> tmp;
+  if (nodes.empty()) return tmp;
+  // a slot: a binary node (code >= 0) or a leaf (BvhNode's leaf code), with its box
+  struct Slot {
+    int32_t code;
+    float lo[3], hi[3];
+  };
+  auto leaf_of = [](int32_t code, int* first, int* cnt) {
+    const int c = -(code + 1);
+    *first = c >> 7;
+    *cnt = c & 127;
+  };
+  auto single = [](int k) { return (int32_t)-(1 + ((k << 7) | 1)); };
+  // one record's own box, binary32 outward (what a one-record binary leaf stores)
+  auto sphere_slot = [&](int k) {
+    const Box b = sphere_box(spheres[k]);
+    Slot s;
+    s.code = single(k);
+    for (int a = 0; a < 3; ++a) { s.lo[a] = f32_down(b.lo[a]); s.hi[a] = f32_up(b.hi[a]); }
+    return s;
+  };
+  auto area = [](const Slot& s) {
+    const double dx = (double)s.hi[0] - s.lo[0], dy = (double)s.hi[1] - s.lo[1], dz = (double)s.hi[2] - s.lo[2];
+    return dx * dy + dy * dz + dz * dx;
+  };
+  auto children = [&](int n, std::vector<Slot>& out) {
+    for (int c = 0; c < 2; ++c) {
+      if (nodes[n].child[c] == kBvhEmpty) continue;
+      Slot s;
+      s.code = nodes[n].child[c];
+      for (int a = 0; a < 3; ++a) { s.lo[a] = nodes[n].lo[c][a]; s.hi[a] = nodes[n].hi[c][a]; }
+      out.push_back(s);
+    }
+  };
+  std::vector<int> need;  // entries a near-first traversal keeps pending below each node
+  bool ok = true;
+  auto emit = [&](auto&& self, std::vector<Slot>& s) -> int {
+    const int idx = (int)tmp.size();
+    tmp.emplace_back();
+    need.push_back(0);
+    int below = 0;
+    for (size_t j = 0; j < 4; ++j) {
+      int32_t c = 0xFFFF;
+      float lo[3] = {0.f, 0.f, 0.f}, hi[3] = {0.f, 0.f, 0.f};
+      if (j < s.size()) {
+        for (int a = 0; a < 3; ++a) { lo[a] = s[j].lo[a]; hi[a] = s[j].hi[a]; }
+        int first = 0, cnt = 0;
+        if (s[j].code >= 0) {
+          std::vector<Slot> sub;
+          children(s[j].code, sub);
+          c = self(self, sub);
+        } else if (leaf_of(s[j].code, &first, &cnt), cnt == 1) {
+          if (first >= 0x7FFF) ok = false;
+          c = 0x8000 | first;
+        } else {
+          // a record range the binary tree keeps in one leaf: nodes of up to four
+          // parts, down to single records
+          std::vector<Slot> sub;
+          const int per = (cnt + 3) / 4;
+          for (int p = first; p < first + cnt; p += per) {
+            const int m = std::min(per, first + cnt - p);
+            if (m == 1) { sub.push_back(sphere_slot(p)); continue; }
+            Slot r = sphere_slot(p);
+            r.code = (int32_t)-(1 + ((p << 7) | m));
+            for (int k = p + 1; k < p + m; ++k) {
+              const Slot q = sphere_slot(k);
+              for (int a = 0; a < 3; ++a) { r.lo[a] = std::min(r.lo[a], q.lo[a]); r.hi[a] = std::max(r.hi[a], q.hi[a]); }
+            }
+            sub.push_back(r);
+          }
+          c = self(self, sub);
+        }
+        if (c < 0x8000) below = std::max(below, need[c]);
+      }
+      BvhWide& w = tmp[idx];
+      w.child[j] = c;
+      w.pad[j] = 0;
+      for (int a = 0; a < 3; ++a) { w.lo[a][j] = lo[a]; w.hi[a][j] = hi[a]; }
+    }
+    need[idx] = (int)s.size() - 1 + below;
+    return idx;
+  };
+  // a node's slots: its binary children, opening the largest-area one (a
+  // binary node, or a leaf of several records that fits whole) until four
+  auto open = [&](std::vector<Slot>& s) {
+    while (s.size() < 4) {
+      int best = -1;
+      for (size_t j = 0; j < s.size(); ++j) {
+        int first, cnt = 1;
+        if (s[j].code < 0) leaf_of(s[j].code, &first, &cnt);
+        const bool can = s[j].code >= 0 || (cnt > 1 && s.size() - 1 + (size_t)cnt <= 4);
+        if (can && (best < 0 || area(s[j]) > area(s[best]))) best = (int)j;
+      }
+      if (best < 0) break;
+      const Slot o = s[best];
+      s.erase(s.begin() + best);
+      if (o.code >= 0) {
+        children(o.code, s);
+      } else {
+        int first, cnt;
+        leaf_of(o.code, &first, &cnt);
+        for (int k = first; k < first + cnt; ++k) s.push_back(sphere_slot(k));
+      }
+    }
+  };
+  auto build = [&](auto&& self, std::vector<Slot>& s) -> int {
+    open(s);
+    return emit(self, s);
+  };
+  {
+    std::vector<Slot> root;
+    children(0, root);
+    build(build, root);
+  }
+  if (!ok || tmp.size() >= 0x8000) return {};
+  if (stack) *stack = need[0];
+  // renumber: breadth-first for the first kTreeletNodes / 2 nodes, then each
+  // remaining subtree depth-first (as treelet_order does for the binary nodes)
+  std::vector<int> order{0};
+  size_t h = 0;
+  for (; h < order.size() && order.size() < kTreeletNodes / 2; ++h)
+    for (int j = 0; j < 4; ++j)
+      if (tmp[order[h]].child[j] < 0x8000) order.push_back(tmp[order[h]].child[j]);
+  std::vector<int> frontier(order.begin() + (long)h, order.end()), st;
+  order.resize(h);
+  for (int f : frontier) {
+    st.assign(1, f);
+    while (!st.empty()) {
+      const int e = st.back();
+      st.pop_back();
+      order.push_back(e);
+      for (int j = 3; j >= 0; --j)
+        if (tmp[e].child[j] < 0x8000) st.push_back(tmp[e].child[j]);
+    }
+  }
+  std::vector<int32_t> remap(tmp.size(), -1);
+  for (size_t i = 0; i < order.size(); ++i) remap[order[i]] = (int32_t)i;
+  std::vector<BvhWide> out(order.size());
+  for (size_t i = 0; i < order.size(); ++i) {
+    out[i] = tmp[order[i]];
+    for (int j = 0; j < 4; ++j)
+      if (out[i].child[j] < 0x8000) out[i].child[j] = remap[out[i].child[j]];
+  }
+  return out;
+}
+
 bool other_box(const OtherRec& r, double lo[3], double hi[3]) {
   // cones stay exhaustive: their a ~ 0 branch pushes t = -c / 2.0 * b
   // (cone.rs:104), a root that need not lie on the cone at all

@@ -22,6 +22,18 @@ std::vector<BvhNode> build_sphere_bvh(std::vector<SphereDiag>& spheres, int leaf
 // The nodes in the pair layout of the per-lane traversal (rt_layout.hpp BvhPair).
 std::vector<BvhPair> pair_layout(const std::vector<BvhNode>& nodes);
 
+// The hierarchy collapsed to four children per node (rt_layout.hpp BvhWide)
+// over the records in leaf order (`spheres`, as build_sphere_bvh left them):
+// each node takes its binary children and opens the one of largest box area
+// (a binary node, or a leaf of several records that fits whole) until it
+// holds four; every leaf of the result is one record (code 0x8000 | index).
+// Node 0 is the root; the first nodes are in breadth-first order (a prefix is
+// the top of the tree, for an LDS treelet). `stack` receives the most entries
+// a near-first traversal keeps pending. Empty when the 16-bit codes cannot
+// index the nodes or records.
+std::vector<BvhWide> wide_layout(const std::vector<BvhNode>& nodes, const std::vector<SphereDiag>& spheres,
+                                 int* stack);
+
 // The other bounded records (general-transform spheres, cubes, closed
 // cylinders with finite caps; rt_layout.hpp OtherRec): other_box gives the
 // padded world box of one (false when the record must stay exhaustive: a

@@ -74,6 +74,25 @@ struct alignas(64) BvhPair {
   uint32_t pad;
 };
 static_assert(sizeof(BvhPair) == 64, "BvhPair must stay 64 B");
+// The same hierarchy collapsed to four children per node, for scenes whose
+// nodes are read from global memory (lane_trace_wide): one 128-B line per
+// node, so a ray makes half the dependent node loads of the binary layout.
+// Slot j's box is lo[a][j], hi[a][j] (one 16-B load per plane and axis),
+// child[j] a 16-bit code: a node index (< 0x8000), 0x8000 | the index of
+// one sphere record (every leaf holds one record), or 0xFFFF (empty). The boxes
+// are the binary nodes' own (a collapsed node's children are its binary
+// descendants) or, below a binary leaf of several records, each record's own
+// padded box (and unions of them) rounded outward to binary32: every box holds
+// what lies below it, so every culling decision stays exact (DESIGN.md "Exact
+// culling").
+struct alignas(128) BvhWide {
+  float lo[3][4];
+  float hi[3][4];
+  int32_t child[4];
+  uint32_t pad[4];
+};
+static_assert(sizeof(BvhWide) == 128, "BvhWide must stay 128 B");
+constexpr unsigned kWideEmpty = 0xFFFFu, kWideLeaf = 0x8000u;  // BvhWide child codes: empty, leaf flag
 // A culled record other than a diagonal sphere: the QuadRec layout, with
 // kind 0 = sphere under a general inverse (rows 0-2 in m).
 typedef QuadRec OtherRec;
@@ -161,6 +180,10 @@ struct DevScene {
   const float* lb_limit;   // per light
   int32_t lb_res;          // R
   int32_t lb_n_items;
+  // the sphere hierarchy collapsed to four children per node (nullptr when its
+  // 16-bit codes cannot index it), and the most stack entries its traversal keeps
+  const BvhWide* bvhw;
+  int32_t n_bvhw, bvhw_stack;
 };
 
 struct DevCamera {

@@ -1,6 +1,5 @@
-// rt_trace.hpp — device-side traversal and shading pieces shared by the
-// generation pipeline (rt_wavefront.hip) and the persistent frame kernel
-// (rt_persist.hip): the exact-culling BVH traversals, the
+// rt_trace.hpp — device-side traversal and shading pieces of the generation
+// pipeline (rt_wavefront.hip): the exact-culling BVH traversals, the
 // light-buffer shadow walk, the per-block LDS scene image, and the small
 // shading helpers. Include only from .hip files compiled with
 // -ffp-contract=off.
@@ -305,6 +304,97 @@ __device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDia
     }
   }
 }
+// Per-lane traversal over the four-wide layout (LANE == 4, BvhWide; scenes read
+// from global memory): a visit loads one 128-B node (seven 16-B loads: the six
+// planes of the four boxes, the four child codes), tests the four boxes, goes
+// on to the nearest child hit and pushes the others farthest first (a
+// four-key sorting network), so a ray makes about half the dependent node
+// loads of the binary walk. The stack is 16-bit, in LDS (entry k of lane t at
+// lds[k * kTraceBlock + t], sc.bvhw_stack entries at most); the first n_top
+// nodes are read from their LDS copy `top`. Culling is the binary walk's rule
+// on boxes that each hold what lies below them, so the hit is the same, and
+// leaves are batched across the wave the same way.
+template <bool SHADOW>
+__device__ __forceinline__ void lane_trace_wide(const BvhWide* nodes, const SphereDiag* sd, const float* M,
+                                                bool has_bvh, V3 o, V3 d, double t_shadow, Hit& h, unsigned& n_disc,
+                                                unsigned& n_tests, unsigned& n_boxes, uint16_t* lds,
+                                                const BvhWide* top, int n_top) {
+  const SlabRay sr = slab_ray(o, d, M);
+  float t_hi = f32_up(SHADOW ? t_shadow : h.t);
+  int sp = 0;
+  auto pop = [&]() -> unsigned { return sp > 0 ? (unsigned)lds[(--sp) * kTraceBlock] : kWideEmpty; };
+  unsigned e = (SHADOW && h.key >= 0 && h.t < t_shadow) || !has_bvh ? kWideEmpty : 0u;
+  auto visit = [&]() {
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 r[7];
+    if ((int)e < n_top) {
+      typedef __attribute__((address_space(3))) const u32x4 lq;
+      lq* b = (lq*)(top + e);
+#pragma unroll
+      for (int k = 0; k < 7; ++k) r[k] = b[k];
+    } else {
+      typedef __attribute__((address_space(1))) const u32x4 gq;
+      gq* b = (gq*)(nodes + e);
+#pragma unroll
+      for (int k = 0; k < 7; ++k) r[k] = b[k];
+    }
+    float key[4];
+    unsigned ch[4];
+    int n = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float lo[3] = {__uint_as_float(r[0][j]), __uint_as_float(r[1][j]), __uint_as_float(r[2][j])};
+      const float hi[3] = {__uint_as_float(r[3][j]), __uint_as_float(r[4][j]), __uint_as_float(r[5][j])};
+      ch[j] = r[6][j];
+      float tj;
+      const bool hj = slab_hit32(lo, hi, sr, t_hi, tj) & (ch[j] != kWideEmpty);
+      key[j] = hj ? tj : INFINITY;
+      n += hj ? 1 : 0;
+    }
+    n_boxes += 4;
+    // ascending by entry distance (a hit's is finite, a miss's +inf)
+    auto cx = [&](int a, int b) {
+      const bool s = key[b] < key[a];
+      const float ka = key[a];
+      const unsigned ca = ch[a];
+      key[a] = s ? key[b] : ka;
+      key[b] = s ? ka : key[b];
+      ch[a] = s ? ch[b] : ca;
+      ch[b] = s ? ca : ch[b];
+    };
+    cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
+    if (n >= 4) lds[(sp++) * kTraceBlock] = (uint16_t)ch[3];
+    if (n >= 3) lds[(sp++) * kTraceBlock] = (uint16_t)ch[2];
+    if (n >= 2) lds[(sp++) * kTraceBlock] = (uint16_t)ch[1];
+    e = n > 0 ? ch[0] : pop();
+  };
+  // a leaf's record; true when a shadow ray is found occluded
+  auto leaf = [&](unsigned code) {
+    leaf_sphere_test<SHADOW>(sd, (int)(code & 0x7FFFu), o, d, h, n_disc);
+    ++n_tests;
+    if constexpr (SHADOW) {
+      return h.key >= 0 && h.t < t_shadow;
+    } else {
+      t_hi = f32_up(h.t);
+      return false;
+    }
+  };
+  // leaves batched across the wave, as lane_trace does
+  unsigned pl = kWideEmpty;
+  for (;;) {
+    for (;;) {
+      if (e >= kWideLeaf && e != kWideEmpty && pl == kWideEmpty) { pl = e; e = pop(); }
+      if (!__any(e < kWideLeaf && pl == kWideEmpty)) break;
+      if (e < kWideLeaf) visit();  // lanes holding a leaf keep going (speculative)
+    }
+    if (!__any(pl != kWideEmpty)) break;
+    if (pl != kWideEmpty) {
+      if (leaf(pl)) { e = kWideEmpty; sp = 0; }  // shadowed: done
+      pl = kWideEmpty;
+    }
+  }
+}
+
 // Per-lane traversal over the pair layout (LANE == 14): the block's LDS copy
 // of each binary node stores, per axis, the two children's lower bounds as
 // one 8-B pair and their upper bounds as the next pair (lo0 lo1 hi0 hi1 per
@@ -494,6 +584,10 @@ __host__ __device__ inline size_t pair_lds_bytes(const DevScene& sc) {
   return ((lane_stack_bytes(sc.bvh_depth + 1) / 2 + 15) & ~(size_t)15) + (size_t)sc.n_bvh * sizeof(BvhNode) +
          sph48_lds_bytes(sc);
 }
+// LANE 4: the 16-bit stack (sc.bvhw_stack entries) x kTraceBlock, before the distances and the treelet
+__host__ __device__ inline size_t wide_stack_bytes(const DevScene& sc) {
+  return ((size_t)(sc.bvhw_stack > 0 ? sc.bvhw_stack : 1) * kTraceBlock * 2 + 15) & ~(size_t)15;
+}
 constexpr unsigned kLdsSpheres = 1u, kLdsDeltas = 2u;  // lane_scene's lds_flags (LANE 0: records; all: distances)
 
 struct LaneScene {
@@ -506,13 +600,25 @@ struct LaneScene {
   float M[3];                  // bound on |box coordinate| per axis (slab_ray)
   const BvhNode* top;          // 3: the LDS copy of the first n_top nodes
   int n_top;
+  const BvhWide* wtop;         // 4: the LDS copy of the first n_top wide nodes
 };
 template <int LANE>
 __device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, unsigned lds_flags, unsigned n_top, int* static_stack,
                                                 unsigned char* dyn) {
   LaneScene ls{(const unsigned char*)sc.bvh, sc.sph_diag, Sph48{nullptr, nullptr}, nullptr, sc.lb_delta, static_stack,
-               {0.f, 0.f, 0.f}, nullptr, 0};
+               {0.f, 0.f, 0.f}, nullptr, 0, nullptr};
   unsigned char* p = dyn;
+  if constexpr (LANE == 4) {  // [16-bit stack][distances][treelet of wide nodes]
+    ls.stack16 = (uint16_t*)dyn + threadIdx.x;
+    p += wide_stack_bytes(sc);
+    ls.nodes = (const unsigned char*)sc.bvhw;
+    if (n_top > 0) {
+      unsigned char* q = p + ((lds_flags & kLdsDeltas) ? delta_lds_bytes(sc) : 0);
+      stage_lds((uint4*)q, (const uint4*)sc.bvhw, (int)n_top * (int)(sizeof(BvhWide) / 16));
+      ls.wtop = (const BvhWide*)q;
+      ls.n_top = (int)n_top;
+    }
+  }
   if constexpr (LANE == 14) {
     // pair layout (BvhPair): per axis, the two children's lower bounds form one
     // 8-B pair and their upper bounds the next (lane_trace_pair)
@@ -646,6 +752,9 @@ __device__ __forceinline__ bool shadow_trace(const DevScene& sc, unsigned use_lb
     } else if constexpr (LANE == 14) {
       lane_trace_pair<true>(ls.nodes, ls.s48, ls.M, sc.n_bvh > 0, o, d, dist, h, n_disc, n_tests, n_boxes,
                             ls.stack16);
+    } else if constexpr (LANE == 4) {
+      lane_trace_wide<true>((const BvhWide*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, dist, h, n_disc, n_tests,
+                            n_boxes, ls.stack16, ls.wtop, ls.n_top);
     } else if constexpr (LANE == 0) {
       Hit hb;  // the wave traversal starts from an empty hit; any blocker is an answer
       bvh_trace<false, true>(sc, nullptr, ls.stack, o, d, dist, hb, n_disc, n_tests, n_boxes);

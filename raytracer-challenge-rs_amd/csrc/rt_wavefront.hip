@@ -38,7 +38,7 @@ int wf_tuning_apply(WfTuning& t, const char* key, int value) {
       {"treelet", &WfTuning::treelet, 0, 1},       {"treelet_deltas", &WfTuning::treelet_deltas, 0, 1},
       {"shadow_stream", &WfTuning::shadow_stream, 0, 2}, {"adaptive_block", &WfTuning::adaptive_block, 0, 1},
       {"prim_lane", &WfTuning::prim_lane, 0, 1},   {"arena_pct", &WfTuning::arena_pct, 1, 100},
-      {"compact", &WfTuning::compact, 0, 1},
+      {"compact", &WfTuning::compact, 0, 1},       {"wide", &WfTuning::wide, 0, 1},
       {"d2h", &WfTuning::d2h, 0, 1}};
   if (!key) return 0;
   for (const Knob& k : knobs) {
@@ -916,6 +916,9 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
           lane_trace_pair<false>(ls.nodes, ls.s48, ls.M, sc.n_bvh > 0, o2, d, 0.0, h2, u0, u1, u2, ls.stack16);
           exp_sink(h2.t);
 #endif
+        } else if constexpr (LANE == 4) {
+          lane_trace_wide<false>((const BvhWide*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, t.disc, t.tests,
+                                 t.boxes, ls.stack16, ls.wtop, ls.n_top);
         } else {
           lane_trace<false, LANE == 3>((const BvhNode*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, t.disc,
                                        t.tests, t.boxes, ls.stack, ls.top, ls.n_top);
@@ -966,15 +969,6 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
           st_d(dst, 0.0); st_d(dst + 1, 0.0); st_d(dst + 2, 0.0);
         }
         const unsigned long long m = __ballot(hit);
-#ifdef RTAMD_EXP_DIRECT
-        // a chunk with many hits is shaded at once, in its own lanes (its index is its own)
-        if ((unsigned)__popcll(m) >= (unsigned)(RTAMD_EXP_DIRECT)) {
-          q_idx = c;
-          c = dyn ? c_base + X * (unsigned)__shfl((int)k_next, 0, 64) : c + W;
-          shade_fused<LANE, QUADS, CAM>(sc, cam, a, ls, q_idx, slot, hit, o, d, h, t);
-          continue;
-        }
-#endif
         if (hit) {
           const unsigned p = qn + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
           qt[p] = h.t;
@@ -1576,6 +1570,18 @@ static hipError_t launch_fused_q(const DevScene& sc, const DevCamera& cam, WfArg
     return cam_rays ? launch_lds(wf_trace_fused<false, QUADS, 14, TALLY, true>, dyn, n, stream, sc, cam, a, tb)
                     : launch_lds(wf_trace_fused<false, QUADS, 14, TALLY, false>, dyn, n, stream, sc, cam, a, tb);
   }
+  if (tn.image != 1 && tn.wide && sc.bvhw && wide_stack_bytes(sc) <= kWfLdsLimit / 2) {
+    // the four-wide hierarchy: its 16-bit stack, then the light buffer's distances
+    // and/or a treelet of its top nodes in the room left
+    const size_t room = kWfLdsLimit - wide_stack_bytes(sc);
+    dyn = wide_stack_bytes(sc);
+    if (dl && dl <= room && (!tn.treelet || tn.treelet_deltas)) { a.lds_flags |= kLdsDeltas; dyn += dl; }
+    if (tn.treelet) {
+      a.n_top = (unsigned)std::min<size_t>((size_t)sc.n_bvhw, (kWfLdsLimit - dyn) / sizeof(BvhWide));
+      dyn += (size_t)a.n_top * sizeof(BvhWide);
+    }
+    return launch_global(4, QUADS, TALLY, cam_rays, sc, cam, a, dyn, n, stream, tb);
+  }
   if (tn.image != 1 && sc.bvh_depth <= kLaneLdsDepth) {
     const size_t room = kWfLdsLimit - (size_t)kLaneLdsDepth * kTraceBlock * 4;
     // the room left beside the stack: the light buffer's distances and/or a treelet
@@ -2042,6 +2048,7 @@ hipError_t wf_launch_global(int lane, bool quads, bool tally, bool cam_rays, con
                             hipEvent_t e1) {
   if (lane == 3) return launch_glb_lane<3>(quads, tally, cam_rays, sc, cam, a, dyn, n, stream, block, e0, e1);
   if (lane == 1) return launch_glb_lane<1>(quads, tally, cam_rays, sc, cam, a, dyn, n, stream, block, e0, e1);
+  if (lane == 4) return launch_glb_lane<4>(quads, tally, cam_rays, sc, cam, a, dyn, n, stream, block, e0, e1);
   return hipErrorInvalidValue;
 }
 #endif  // RT_WF_GLOBAL_TU

@@ -95,10 +95,12 @@ struct WfTuning {
   int shadow_lb = 1;       // 1 = shadow rays through the light buffer when the scene has one
   int image = 0;           // 0 = automatic scene image of the fast-path kernels, 3 / 1 = global memory
   int treelet = 1;         // the global-memory image stages a treelet in LDS
+  int wide = 1;            // the global-memory image: 1 = the four-wide hierarchy (BvhWide) when the scene has one
   int treelet_deltas = 0;  // ... after the light buffer's distances (when they fit)
   int shadow_stream = 1;   // exhaustive pipeline: 1 = shadow traces on a second stream when rendering alone
   int adaptive_block = 0;  // generation pipeline: 1 = small trace launches spread over every CU
-  int compact = 1;         // fast path, pair image: 1 = compacted shading (hit queues in LDS, full-width shading)
+  int compact = 0;         // fast path, pair image: 1 = compacted shading (hit queues in LDS, full-width shading;
+                           //     measured slower on C3, DESIGN.md "Compacted shading")
   int prim_lane = 0;       // fast path: 1 = primary rays by the per-lane pair traversal (LDS image) instead
                            //     of the wave traversal with shared-origin records
   int arena_pct = 100;     // test hook: the fast path's queue arenas sized to this percentage of the hint,

@@ -214,28 +214,71 @@ def test_skipped_shadow_rays_bitwise(rt, neg_zero):
     assert full.to_numpy().tobytes() == exact.to_numpy().tobytes()
 
 
-@pytest.mark.parametrize("image,shadow_lb,compact", [(0, 1, 1), (0, 0, 1), (0, 1, 0), (0, 0, 0), (3, 1, 1),
-                                                    (3, 0, 1), (1, 1, 1), (1, 0, 1)])
-def test_fused_images_bitwise(rt, image, shadow_lb, compact):
+@pytest.mark.parametrize("image,shadow_lb,compact,wide", [(0, 1, 1, 1), (0, 0, 1, 1), (0, 1, 0, 1), (0, 0, 0, 1),
+                                                         (3, 1, 1, 1), (3, 0, 1, 1), (3, 1, 1, 0), (3, 0, 1, 0),
+                                                         (1, 1, 1, 1), (1, 0, 1, 1)])
+def test_fused_images_bitwise(rt, image, shadow_lb, compact, wide):
     """Every scene image of the fast-path kernels (pair layout in LDS, the
     default, with and without compacted shading / nodes and records in global
-    memory with an LDS stack / with a scratch stack), with shadow rays through
-    the light buffer or through the BVH, gives the exhaustive frame. The scenes
-    above that do not fit in LDS (3000 spheres) run image 3 on their own."""
+    memory: the four-wide hierarchy (wide) or the binary one with an LDS stack /
+    with a scratch stack), with shadow rays through the light buffer or through
+    the BVH, gives the exhaustive frame. The scenes above that do not fit in LDS
+    (3000 spheres) run a global image on their own."""
     w, cam, depth = _glass_cluster(rt, n=250, seed=21, inside=False)
     exact, _ = cam.render(w, depth, want_stats=True)
     w.tune("image", image)
     w.tune("shadow_lb", shadow_lb)
     w.tune("compact", compact)
+    w.tune("wide", wide)
     try:
         fast, _ = cam.render(w, depth, want_stats=False)
         p = rt._rtamd._wf_profile(w, -1, True)
         assert p["fused"]
+        assert p["n_bvh_wide"] > 0 and p["wide_stack"] > 0
     finally:
         w.tune("image", 0)
         w.tune("shadow_lb", 1)
-        w.tune("compact", 1)
+        w.tune("compact", 0)
+        w.tune("wide", 1)
     assert fast.to_numpy().tobytes() == exact.to_numpy().tobytes()
+
+
+@pytest.mark.parametrize("leaf", [1, 2, 6])
+def test_wide_hierarchy_bitwise(rt, leaf):
+    """The four-wide hierarchy over the global-memory image (LANE 4): binary
+    leaves of one or several records (opened into one record per leaf),
+    frames, color_at rays from inside glass and shadows through the hierarchy
+    all equal the exhaustive answers and the binary walk's; the two walks count
+    different box tests (each ran)."""
+    import numpy as np
+    rt._rtamd._tuning_set("bvh_leaf", leaf)
+    try:
+        w, cam, depth = _glass_cluster(rt, n=700, seed=5, inside=True)
+        exact, _ = cam.render(w, depth, want_stats=True)
+    finally:
+        rt._rtamd._tuning_set("bvh_leaf", 0)
+    rng = np.random.default_rng(leaf)
+    rays = np.concatenate([rng.uniform(-3, 3, (3000, 3)), rng.normal(size=(3000, 3))], 1)
+    rays[:, 3:] /= np.linalg.norm(rays[:, 3:], axis=1, keepdims=True)
+    col_exact, _ = w.color_at_batch(rays, depth, True, True)
+    boxes = {}
+    w.tune("image", 3)
+    try:
+        for wide in (1, 0):
+            w.tune("wide", wide)
+            for lb in (1, 0):
+                w.tune("shadow_lb", lb)
+                fast, _ = cam.render(w, depth, want_stats=False)
+                assert fast.to_numpy().tobytes() == exact.to_numpy().tobytes(), (wide, lb)
+                col, _ = w.color_at_batch(rays, depth, False)
+                assert col.tobytes() == col_exact.tobytes(), (wide, lb)
+            _, st = cam.render(w, depth, want_stats=True, exhaustive=False)
+            boxes[wide] = st["box_tests_executed"]
+    finally:
+        w.tune("image", 0)
+        w.tune("wide", 1)
+        w.tune("shadow_lb", 1)
+    assert boxes[1] != boxes[0] and boxes[1] > 0
 
 
 @pytest.mark.parametrize("n_streams,kind", [(2, "torch"), (10, "torch"), (4, "plain"), (4, "dedicated")])

@@ -38,6 +38,16 @@ def _check(rt, w, cams, depth, row_block, shard, n_shards, aa=1):
     w.check()
     for k, (b, o) in enumerate(zip(bat, one)):
         assert torch.equal(b, o), k
+    # the same cameras again, into fresh buffers, take the
+    # asynchronous path the bench times (sizes from the scene's learned sizing,
+    # the device queue check afterwards): bitwise the same frames.
+    again = [torch.full_like(b, -3.0) for b in bat]
+    torch.cuda.synchronize()
+    rt.render_frames_device(w, cams, depth, row_block, shard, n_shards, [b.data_ptr() for b in again], st, False, aa)
+    torch.cuda.synchronize()
+    w.check()
+    for k, (b, o) in enumerate(zip(again, one)):
+        assert torch.equal(b, o), ("again", k)
 
 
 @pytest.mark.parametrize("n", [2, 16, 19])
