@@ -1,0 +1,30 @@
+"""Host-side checks of the four-wide hierarchy (rt_bvh.cpp wide_layout,
+rt_layout.hpp BvhWide): compiled with g++ from the library's
+own builder sources and run on random sphere fields of C3 and C5 sizes at the
+leaf sizes the builder takes. Exactness of the culling rests on every slot's
+box holding the records below it, and the LDS stack on the reported bound."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(REPO, "raytracer-challenge-rs_amd", "csrc")
+
+
+@pytest.fixture(scope="module")
+def wide_check(tmp_path_factory):
+    if not shutil.which("g++"):
+        pytest.skip("no g++")
+    exe = str(tmp_path_factory.mktemp("wide") / "wide_check")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", CSRC, os.path.join(REPO, "tests", "cpp", "wide_check.cpp"),
+                    os.path.join(CSRC, "rt_bvh.cpp"), "-o", exe], check=True)
+    return exe
+
+
+@pytest.mark.parametrize("n,leaf,span", [(1, 1, 10), (5, 8, 4), (9, 2, 6), (1000, 2, 12), (1000, 4, 12),
+                                         (3000, 1, 30), (9996, 1, 50), (9996, 2, 50)])
+def test_wide_layout_invariants(wide_check, n, leaf, span):
+    r = subprocess.run([wide_check, str(n), str(leaf), str(span)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr
