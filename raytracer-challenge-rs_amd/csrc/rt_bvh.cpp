@@ -402,12 +402,12 @@ std::vector<BvhWide> wide_layout(const std::vector<BvhNode>& nodes, const std::v
   bool ok = true;
   auto emit = [&](auto&& self, std::vector<Slot>& s) -> int {
     const int idx = (int)tmp.size();
-    tmp.emplace_back();
+    tmp.emplace_back(BvhWide{});
     need.push_back(0);
     int below = 0;
     for (size_t j = 0; j < 4; ++j) {
       int32_t c = 0xFFFF;
-      float lo[3] = {0.f, 0.f, 0.f}, hi[3] = {0.f, 0.f, 0.f};
+      float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
       if (j < s.size()) {
         for (int a = 0; a < 3; ++a) { lo[a] = s[j].lo[a]; hi[a] = s[j].hi[a]; }
         int first = 0, cnt = 0;
@@ -439,8 +439,7 @@ std::vector<BvhWide> wide_layout(const std::vector<BvhNode>& nodes, const std::v
         if (c < 0x8000) below = std::max(below, need[c]);
       }
       BvhWide& w = tmp[idx];
-      w.child[j] = c;
-      w.pad[j] = 0;
+      w.child[j] = (uint16_t)c;
       for (int a = 0; a < 3; ++a) { w.lo[a][j] = lo[a]; w.hi[a][j] = hi[a]; }
     }
     need[idx] = (int)s.size() - 1 + below;

@@ -79,7 +79,8 @@ static_assert(sizeof(BvhPair) == 64, "BvhPair must stay 64 B");
 // node, so a ray makes half the dependent node loads of the binary layout.
 // Slot j's box is lo[a][j], hi[a][j] (one 16-B load per plane and axis),
 // child[j] a 16-bit code: a node index (< 0x8000), 0x8000 | the index of
-// one sphere record (every leaf holds one record), or 0xFFFF (empty). The boxes
+// one sphere record (every leaf holds one record), or 0xFFFF (empty; its box
+// is inverted, lo = +inf and hi = -inf, so no ray with a usable axis meets it). The boxes
 // are the binary nodes' own (a collapsed node's children are its binary
 // descendants) or, below a binary leaf of several records, each record's own
 // padded box (and unions of them) rounded outward to binary32: every box holds
@@ -88,8 +89,8 @@ static_assert(sizeof(BvhPair) == 64, "BvhPair must stay 64 B");
 struct alignas(128) BvhWide {
   float lo[3][4];
   float hi[3][4];
-  int32_t child[4];
-  uint32_t pad[4];
+  uint16_t child[4];
+  uint32_t pad[6];
 };
 static_assert(sizeof(BvhWide) == 128, "BvhWide must stay 128 B");
 constexpr unsigned kWideEmpty = 0xFFFFu, kWideLeaf = 0x8000u;  // BvhWide child codes: empty, leaf flag
