@@ -134,18 +134,23 @@ static_assert(sizeof(LbCell) == 16, "LbCell must stay 16 B");
 // this key exactly like the reference's stable sort (intersection.rs:108-116).
 constexpr int kKeyShift = 2;
 
+// What a hit on an unpatterned object reads (the inverses, the material, kind
+// and pattern kind) fills the first two 128-B lines; patterns, the cylinder /
+// cone bounds and the host-only shadow flag come after.
 struct alignas(64) ShadeRec {
   double inv[12];   // transform_inverse rows 0..2
   double invT[9];   // transform_inverse_transpose upper 3x3 (= inv^T)
   double color[3];
   double ambient, diffuse, specular, shininess;
   double reflective, transparency, refractive_index;
+  int32_t kind, pattern_kind;
   double pat_a[3], pat_b[3];
   double pat_inv[12];
-  int32_t kind, pattern_kind, shadow, pad0;
+  int32_t shadow, pad0;
   double minimum, maximum;  // Cylinder / Cone (local_normal_at)
-  double pad1[4];
+  double pad1[11];
 };
+static_assert(__builtin_offsetof(ShadeRec, pattern_kind) < 256, "hot shading fields in the first two lines");
 static_assert(sizeof(ShadeRec) == 512, "ShadeRec must stay 512 B");
 
 struct LightRec {

@@ -395,141 +395,6 @@ __device__ __forceinline__ void lane_trace_wide(const BvhWide* nodes, const Sphe
   }
 }
 
-// The four-wide walk with the pair layout's face selection (LANE == 5): the
-// ray's direction signs pick, per axis, the block of the four entry planes
-// and the block of the four exit planes (lo[a] or hi[a], byte offsets kept in
-// registers), so one packed FMA per two children gives their entry (exit)
-// distances and no per-axis min/max is needed (the values are slab_hit32's,
-// as in lane_trace_pair). The order is a sort of four 32-bit keys (an entry
-// distance's bits with the slot in the two low bits, a miss all ones: the
-// bits of a non-negative binary32 order as the values do; ties and the two
-// dropped bits only change the visit order) and the slots' child codes come
-// from one 64-bit word. Empty slots have inverted boxes, so they cull
-// themselves for every ray with a usable axis; a ray with none (a huge
-// origin, a NaN) tests every record, as a walk that culls nothing would.
-template <bool SHADOW>
-__device__ __forceinline__ void lane_trace_wide2(const BvhWide* nodes, const SphereDiag* sd, int n_records,
-                                                 const float* M, bool has_bvh, V3 o, V3 d, double t_shadow, Hit& h,
-                                                 unsigned& n_disc, unsigned& n_tests, unsigned& n_boxes,
-                                                 uint16_t* lds, const BvhWide* top, int n_top) {
-  float inv[3], on[3], of[3];
-  unsigned ent[3], ext[3];
-  bool usable = false;
-  {
-    const double oa[3] = {o.x, o.y, o.z}, da[3] = {d.x, d.y, d.z};
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      bool neg = false;
-      if (fabs(da[a]) >= 0x1p-60 && fabs(oa[a]) <= 0x1p60 && M[a] <= 0x1p60f) {  // as slab_ray; NaN fails
-        const double iv = slab_inv(da[a]);
-        const double oinv = oa[a] * iv;
-        const double delta = 0x1p-20 * fabs(iv) * ((double)M[a] + fabs(oa[a]));
-        inv[a] = (float)iv;
-        on[a] = (float)(oinv + delta);
-        of[a] = (float)(oinv - delta);
-        neg = !(iv >= 0.0);
-        usable = true;
-      } else {
-        inv[a] = 0.0f;
-        on[a] = INFINITY;
-        of[a] = -INFINITY;
-      }
-      ent[a] = 16u * a + (neg ? 48u : 0u);  // lo[a] (offset 16a) or hi[a] (48 + 16a)
-      ext[a] = 16u * a + (neg ? 0u : 48u);
-    }
-  }
-#pragma unroll
-  for (int a = 0; a < 3; ++a) asm volatile("" : "+v"(ent[a]), "+v"(ext[a]));
-  float t_hi = f32_up(SHADOW ? t_shadow : h.t);
-  auto stk = [&](int k) -> uint16_t& { return lds[k * kTraceBlock]; };
-  stk(0) = (uint16_t)kWideEmpty;  // sentinel: a pop of it ends the lane's walk
-  int sp = 1;
-  auto pop = [&]() { return (unsigned)stk(--sp); };
-  unsigned e = (SHADOW && h.key >= 0 && h.t < t_shadow) || !has_bvh ? kWideEmpty : 0u;
-  if (e == 0u && !usable) {  // no axis can cull: every record
-    e = kWideEmpty;
-    for (int k = 0; k < n_records; ++k) {
-      leaf_sphere_test<SHADOW>(sd, k, o, d, h, n_disc);
-      ++n_tests;
-      if (SHADOW && h.key >= 0 && h.t < t_shadow) break;
-    }
-  }
-  typedef float f32x4v __attribute__((ext_vector_type(4)));
-  auto visit = [&]() {
-    typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
-    f32x4v E[3], X[3];
-    u32x2v cc;
-    if ((int)e < n_top) {
-      typedef __attribute__((address_space(3))) const unsigned char lb;
-      typedef __attribute__((address_space(3))) const f32x4v l4;
-      typedef __attribute__((address_space(3))) const u32x2v l2;
-      lb* b = (lb*)(top) + e * 128u;
-#pragma unroll
-      for (int a = 0; a < 3; ++a) { E[a] = *(l4*)(b + ent[a]); X[a] = *(l4*)(b + ext[a]); }
-      cc = *(l2*)(b + 96);
-    } else {
-      typedef __attribute__((address_space(1))) const unsigned char gb;
-      typedef __attribute__((address_space(1))) const f32x4v g4;
-      typedef __attribute__((address_space(1))) const u32x2v g2;
-      // 32-bit offsets from the scalar base (global_load ... voffset, s[base:base+1])
-      gb* b = (gb*)(nodes);
-      const unsigned n0 = e * 128u;
-#pragma unroll
-      for (int a = 0; a < 3; ++a) { E[a] = *(g4*)(b + (n0 + ent[a])); X[a] = *(g4*)(b + (n0 + ext[a])); }
-      cc = *(g2*)(b + (n0 + 96u));
-    }
-    const f32x4v tx0 = __builtin_elementwise_fma(E[0], (f32x4v)(inv[0]), (f32x4v)(-on[0]));
-    const f32x4v ty0 = __builtin_elementwise_fma(E[1], (f32x4v)(inv[1]), (f32x4v)(-on[1]));
-    const f32x4v tz0 = __builtin_elementwise_fma(E[2], (f32x4v)(inv[2]), (f32x4v)(-on[2]));
-    const f32x4v tx1 = __builtin_elementwise_fma(X[0], (f32x4v)(inv[0]), (f32x4v)(-of[0]));
-    const f32x4v ty1 = __builtin_elementwise_fma(X[1], (f32x4v)(inv[1]), (f32x4v)(-of[1]));
-    const f32x4v tz1 = __builtin_elementwise_fma(X[2], (f32x4v)(inv[2]), (f32x4v)(-of[2]));
-    unsigned key[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float t0 = fmaxf(fmaxf(tx0[j], ty0[j]), fmaxf(tz0[j], 0.0f));
-      const float t1 = fminf(fminf(tx1[j], ty1[j]), fminf(tz1[j], t_hi));
-      key[j] = t0 <= t1 ? ((__float_as_uint(t0) & ~3u) | (unsigned)j) : ~0u;
-    }
-    n_boxes += 4;
-    auto cx = [&](int a, int b) {
-      const unsigned lo = min(key[a], key[b]), hi = max(key[a], key[b]);
-      key[a] = lo;
-      key[b] = hi;
-    };
-    cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
-    const unsigned long long P = ((unsigned long long)cc.y << 32) | cc.x;
-    auto child = [&](unsigned k) { return (unsigned)(P >> ((k & 3u) << 4)); };  // (low 16 bits)
-    if (key[3] != ~0u) stk(sp++) = (uint16_t)child(key[3]);
-    if (key[2] != ~0u) stk(sp++) = (uint16_t)child(key[2]);
-    if (key[1] != ~0u) stk(sp++) = (uint16_t)child(key[1]);
-    e = key[0] != ~0u ? (child(key[0]) & 0xFFFFu) : pop();
-  };
-  auto leaf = [&](unsigned code) {
-    leaf_sphere_test<SHADOW>(sd, (int)(code & 0x7FFFu), o, d, h, n_disc);
-    ++n_tests;
-    if constexpr (SHADOW) {
-      return h.key >= 0 && h.t < t_shadow;
-    } else {
-      t_hi = f32_up(h.t);
-      return false;
-    }
-  };
-  unsigned pl = kWideEmpty;
-  for (;;) {
-    for (;;) {
-      if (e >= kWideLeaf && e != kWideEmpty && pl == kWideEmpty) { pl = e; e = pop(); }
-      if (!__any(e < kWideLeaf && pl == kWideEmpty)) break;
-      if (e < kWideLeaf) visit();  // lanes holding a leaf keep going (speculative)
-    }
-    if (!__any(pl != kWideEmpty)) break;
-    if (pl != kWideEmpty) {
-      if (leaf(pl)) { e = kWideEmpty; sp = 1; }  // shadowed: done
-      pl = kWideEmpty;
-    }
-  }
-}
-
 // Per-lane traversal over the pair layout (LANE == 14): the block's LDS copy
 // of each binary node stores, per axis, the two children's lower bounds as
 // one 8-B pair and their upper bounds as the next pair (lo0 lo1 hi0 hi1 per
@@ -719,10 +584,9 @@ __host__ __device__ inline size_t pair_lds_bytes(const DevScene& sc) {
   return ((lane_stack_bytes(sc.bvh_depth + 1) / 2 + 15) & ~(size_t)15) + (size_t)sc.n_bvh * sizeof(BvhNode) +
          sph48_lds_bytes(sc);
 }
-// LANE 4 / 5: the 16-bit stack (sc.bvhw_stack entries, and LANE 5's sentinel) x kTraceBlock,
-// before the distances and the treelet
+// LANE 4: the 16-bit stack (sc.bvhw_stack entries) x kTraceBlock, before the distances and the treelet
 __host__ __device__ inline size_t wide_stack_bytes(const DevScene& sc) {
-  return ((size_t)(sc.bvhw_stack + 1) * kTraceBlock * 2 + 15) & ~(size_t)15;
+  return ((size_t)(sc.bvhw_stack > 0 ? sc.bvhw_stack : 1) * kTraceBlock * 2 + 15) & ~(size_t)15;
 }
 constexpr unsigned kLdsSpheres = 1u, kLdsDeltas = 2u;  // lane_scene's lds_flags (LANE 0: records; all: distances)
 
@@ -744,7 +608,7 @@ __device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, unsigned lds
   LaneScene ls{(const unsigned char*)sc.bvh, sc.sph_diag, Sph48{nullptr, nullptr}, nullptr, sc.lb_delta, static_stack,
                {0.f, 0.f, 0.f}, nullptr, 0, nullptr};
   unsigned char* p = dyn;
-  if constexpr (LANE == 4 || LANE == 5) {  // [16-bit stack][distances][treelet of wide nodes]
+  if constexpr (LANE == 4) {  // [16-bit stack][distances][treelet of wide nodes]
     ls.stack16 = (uint16_t*)dyn + threadIdx.x;
     p += wide_stack_bytes(sc);
     ls.nodes = (const unsigned char*)sc.bvhw;
@@ -891,9 +755,7 @@ __device__ __forceinline__ bool shadow_trace(const DevScene& sc, unsigned use_lb
     } else if constexpr (LANE == 4) {
       lane_trace_wide<true>((const BvhWide*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, dist, h, n_disc, n_tests,
                             n_boxes, ls.stack16, ls.wtop, ls.n_top);
-    } else if constexpr (LANE == 5) {
-      lane_trace_wide2<true>((const BvhWide*)ls.nodes, ls.sd, sc.n_diag, ls.M, sc.n_bvh > 0, o, d, dist, h, n_disc,
-                             n_tests, n_boxes, ls.stack16, ls.wtop, ls.n_top);
+
     } else if constexpr (LANE == 0) {
       Hit hb;  // the wave traversal starts from an empty hit; any blocker is an answer
       bvh_trace<false, true>(sc, nullptr, ls.stack, o, d, dist, hb, n_disc, n_tests, n_boxes);

@@ -38,7 +38,7 @@ int wf_tuning_apply(WfTuning& t, const char* key, int value) {
       {"treelet", &WfTuning::treelet, 0, 1},       {"treelet_deltas", &WfTuning::treelet_deltas, 0, 1},
       {"shadow_stream", &WfTuning::shadow_stream, 0, 2}, {"adaptive_block", &WfTuning::adaptive_block, 0, 1},
       {"prim_lane", &WfTuning::prim_lane, 0, 1},   {"arena_pct", &WfTuning::arena_pct, 1, 100},
-      {"compact", &WfTuning::compact, 0, 1},       {"wide", &WfTuning::wide, 0, 2},
+      {"compact", &WfTuning::compact, 0, 1},       {"wide", &WfTuning::wide, 0, 1},
       {"d2h", &WfTuning::d2h, 0, 1}};
   if (!key) return 0;
   for (const Knob& k : knobs) {
@@ -905,11 +905,12 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
         trace_rest<false, QUADS, true>(sc, o, d, h, t.disc);
         if constexpr (QUADS) other_trace<false>(sc, o, d, 0.0, h, t.disc, t.tests, t.boxes);
         if constexpr (LANE == 14) {
+#ifdef RTAMD_EXP_DUP_TRAV
+          Hit h2 = h;  // (the planes' hit, as the walk below starts from)
+#endif
           lane_trace_pair<false>(ls.nodes, ls.s48, ls.M, sc.n_bvh > 0, o, d, 0.0, h, t.disc, t.tests, t.boxes,
                                  ls.stack16);
 #ifdef RTAMD_EXP_DUP_TRAV
-          Hit h2;
-          hit_init(h2);
           V3 o2 = o;
           exp_opaque(o2.x);
           unsigned u0 = 0, u1 = 0, u2 = 0;
@@ -917,11 +918,19 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
           exp_sink(h2.t);
 #endif
         } else if constexpr (LANE == 4) {
+#ifdef RTAMD_EXP_DUP_TRAV
+          Hit h2 = h;  // (the planes' hit, as the walk below starts from)
+#endif
           lane_trace_wide<false>((const BvhWide*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, t.disc, t.tests,
                                  t.boxes, ls.stack16, ls.wtop, ls.n_top);
-        } else if constexpr (LANE == 5) {
-          lane_trace_wide2<false>((const BvhWide*)ls.nodes, ls.sd, sc.n_diag, ls.M, sc.n_bvh > 0, o, d, 0.0, h, t.disc,
-                                  t.tests, t.boxes, ls.stack16, ls.wtop, ls.n_top);
+#ifdef RTAMD_EXP_DUP_TRAV
+          V3 o2 = o;
+          exp_opaque(o2.x);
+          unsigned u0 = 0, u1 = 0, u2 = 0;
+          lane_trace_wide<false>((const BvhWide*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o2, d, 0.0, h2, u0, u1, u2,
+                                 ls.stack16, ls.wtop, ls.n_top);
+          exp_sink(h2.t);
+#endif
         } else {
           lane_trace<false, LANE == 3>((const BvhNode*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, t.disc,
                                        t.tests, t.boxes, ls.stack, ls.top, ls.n_top);
@@ -1583,7 +1592,7 @@ static hipError_t launch_fused_q(const DevScene& sc, const DevCamera& cam, WfArg
       a.n_top = (unsigned)std::min<size_t>((size_t)sc.n_bvhw, (kWfLdsLimit - dyn) / sizeof(BvhWide));
       dyn += (size_t)a.n_top * sizeof(BvhWide);
     }
-    return launch_global(tn.wide == 2 ? 5 : 4, QUADS, TALLY, cam_rays, sc, cam, a, dyn, n, stream, tb);
+    return launch_global(4, QUADS, TALLY, cam_rays, sc, cam, a, dyn, n, stream, tb);
   }
   if (tn.image != 1 && sc.bvh_depth <= kLaneLdsDepth) {
     const size_t room = kWfLdsLimit - (size_t)kLaneLdsDepth * kTraceBlock * 4;
@@ -2052,7 +2061,6 @@ hipError_t wf_launch_global(int lane, bool quads, bool tally, bool cam_rays, con
   if (lane == 3) return launch_glb_lane<3>(quads, tally, cam_rays, sc, cam, a, dyn, n, stream, block, e0, e1);
   if (lane == 1) return launch_glb_lane<1>(quads, tally, cam_rays, sc, cam, a, dyn, n, stream, block, e0, e1);
   if (lane == 4) return launch_glb_lane<4>(quads, tally, cam_rays, sc, cam, a, dyn, n, stream, block, e0, e1);
-  if (lane == 5) return launch_glb_lane<5>(quads, tally, cam_rays, sc, cam, a, dyn, n, stream, block, e0, e1);
   return hipErrorInvalidValue;
 }
 #endif  // RT_WF_GLOBAL_TU

@@ -95,9 +95,8 @@ struct WfTuning {
   int shadow_lb = 1;       // 1 = shadow rays through the light buffer when the scene has one
   int image = 0;           // 0 = automatic scene image of the fast-path kernels, 3 / 1 = global memory
   int treelet = 1;         // the global-memory image stages a treelet in LDS
-  int wide = 1;            // the global-memory image: the four-wide hierarchy (BvhWide) when the scene has one,
-                           //     1 = lane_trace_wide, 2 = lane_trace_wide2 (face selection, key sort); 0 = binary
-  int treelet_deltas = 0;  // ... after the light buffer's distances (when they fit)
+  int wide = 1;            // the global-memory image: 1 = the four-wide hierarchy (BvhWide) when the scene has one
+  int treelet_deltas = 1;  // ... after the light buffer's distances (when they fit)
   int shadow_stream = 1;   // exhaustive pipeline: 1 = shadow traces on a second stream when rendering alone
   int adaptive_block = 0;  // generation pipeline: 1 = small trace launches spread over every CU
   int compact = 0;         // fast path, pair image: 1 = compacted shading (hit queues in LDS, full-width shading;

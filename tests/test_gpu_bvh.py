@@ -215,8 +215,8 @@ def test_skipped_shadow_rays_bitwise(rt, neg_zero):
 
 
 @pytest.mark.parametrize("image,shadow_lb,compact,wide", [(0, 1, 1, 1), (0, 0, 1, 1), (0, 1, 0, 1), (0, 0, 0, 1),
-                                                         (3, 1, 0, 1), (3, 0, 0, 1), (3, 1, 0, 2), (3, 0, 0, 2),
-                                                         (3, 1, 0, 0), (3, 0, 0, 0), (1, 1, 0, 1), (1, 0, 0, 1)])
+                                                         (3, 1, 0, 1), (3, 0, 0, 1), (3, 1, 0, 0), (3, 0, 0, 0),
+                                                         (1, 1, 0, 1), (1, 0, 0, 1)])
 def test_fused_images_bitwise(rt, image, shadow_lb, compact, wide):
     """Every scene image of the fast-path kernels (pair layout in LDS, the
     default, with and without compacted shading / nodes and records in global
@@ -245,7 +245,7 @@ def test_fused_images_bitwise(rt, image, shadow_lb, compact, wide):
 
 @pytest.mark.parametrize("leaf", [1, 2, 6])
 def test_wide_hierarchy_bitwise(rt, leaf):
-    """The four-wide hierarchy over the global-memory image (LANE 4 and 5): binary
+    """The four-wide hierarchy over the global-memory image (LANE 4): binary
     leaves of one or several records (opened into one record per leaf),
     frames, color_at rays from inside glass and shadows through the hierarchy
     all equal the exhaustive answers and the binary walk's; the two walks count
@@ -264,7 +264,7 @@ def test_wide_hierarchy_bitwise(rt, leaf):
     boxes = {}
     w.tune("image", 3)
     try:
-        for wide in (2, 1, 0):
+        for wide in (1, 0):
             w.tune("wide", wide)
             for lb in (1, 0):
                 w.tune("shadow_lb", lb)
@@ -278,7 +278,7 @@ def test_wide_hierarchy_bitwise(rt, leaf):
         w.tune("image", 0)
         w.tune("wide", 1)
         w.tune("shadow_lb", 1)
-    assert boxes[1] != boxes[0] and boxes[1] > 0 and boxes[2] > 0
+    assert boxes[1] != boxes[0] and boxes[1] > 0
 
 
 @pytest.mark.parametrize("n_streams,kind", [(2, "torch"), (10, "torch"), (4, "plain"), (4, "dedicated")])
