@@ -1292,7 +1292,7 @@ hipError_t Wavefront::last_profile(WfProfile* out) {
     out->tests[c] = (double)hc.tests(c);
     out->boxes[c] = (double)hc.boxes(c);
   }
-  if (last_fused_ && lr_.stream) {  // the fast path's generations sized themselves: their rays from the record
+  if (last_fused_) {  // the fast path's generations sized themselves: their rays from the record (any stream, 0 too)
     std::vector<unsigned> rays;
     WF_CHECK(last_counts(rays));
     out->rays[WF_PRIMARY] = rays.empty() ? 0.0 : (double)rays[0];

@@ -84,6 +84,24 @@ def test_bvh_is_the_fast_path(rt):
     assert not rt._rtamd._wf_profile(w, -1, True)["bvh"]
 
 
+@pytest.mark.parametrize("stream", ["default", "torch"])
+def test_profile_counts_the_generations(rt, stream):
+    """The fast path's generations size themselves on the device; the profile
+    (bench.py's roofline) takes their ray counts from the workspace's record,
+    also for a frame rendered on the null stream: the secondary rays equal the
+    counted frame's reflected + refracted rays."""
+    import torch
+    from rtamd import scenes
+    w, cam, depth = scenes.c3(64, 36, n_spheres=200)
+    b = torch.empty((36, 64, 3), dtype=torch.float64, device="cuda")
+    s = torch.cuda.Stream() if stream == "torch" else None
+    torch.cuda.synchronize()
+    st = cam.render_shard_device(w, depth, 8, 0, 1, b.data_ptr(), s.cuda_stream if s else 0, True, exhaustive=False)
+    p = rt._rtamd._wf_profile(w, -1, True)
+    assert p["fused"] and p["rays"]["primary"] == 64 * 36
+    assert p["rays"]["closest"] == st["rays_reflect"] + st["rays_refract"] > 0
+
+
 def test_bvh_vs_oracle_c3(rt, oracle):
     from rtamd import scenes
     w, cam, depth = scenes.c3(128, 72)
