@@ -1554,7 +1554,10 @@ static hipError_t launch_fused_q(const DevScene& sc, const DevCamera& cam, WfArg
   const size_t dl = a.use_lb ? delta_lds_bytes(sc) : 0;
   size_t dyn = 0;
   a.lds_flags = 0;
-  if (primary && !(tn.prim_lane && tn.image == 0 && pair_lds_bytes(sc) <= kWfLdsLimit)) {
+  // primary rays: the wave traversal, or with prim_lane the per-lane walk of the pair image or of
+  // the four-wide hierarchy (the launches below, reading camera rays)
+  const bool wide_ok = tn.image != 1 && tn.wide && sc.bvhw && wide_stack_bytes(sc) <= kWfLdsLimit / 2;
+  if (primary && !(tn.prim_lane && ((tn.image == 0 && pair_lds_bytes(sc) <= kWfLdsLimit) || wide_ok))) {
     const size_t room = kWfLdsLimit - (size_t)(kTraceBlock / 64) * (kBvhMaxDepth + 4) * 4;
     if (sph_lds_bytes(sc) <= room) { a.lds_flags |= kLdsSpheres; dyn += sph_lds_bytes(sc); }
     if (dl && dyn + dl <= room) { a.lds_flags |= kLdsDeltas; dyn += dl; }
@@ -1582,7 +1585,7 @@ static hipError_t launch_fused_q(const DevScene& sc, const DevCamera& cam, WfArg
     return cam_rays ? launch_lds(wf_trace_fused<false, QUADS, 14, TALLY, true>, dyn, n, stream, sc, cam, a, tb)
                     : launch_lds(wf_trace_fused<false, QUADS, 14, TALLY, false>, dyn, n, stream, sc, cam, a, tb);
   }
-  if (tn.image != 1 && tn.wide && sc.bvhw && wide_stack_bytes(sc) <= kWfLdsLimit / 2) {
+  if (wide_ok) {
     // the four-wide hierarchy: its 16-bit stack, then the light buffer's distances
     // and/or a treelet of its top nodes in the room left
     const size_t room = kWfLdsLimit - wide_stack_bytes(sc);

@@ -33,7 +33,7 @@ def _three(rt, make, lb_res=256):
         exact, _ = cam.render(w, depth, want_stats=True)
         p = rt._rtamd._wf_profile(prof_world, -1, True)
     finally:
-        rt._rtamd._tuning_set("lb_res", 256)
+        rt._rtamd._tuning_set("lb_res", -1)  # (the default: by scene size)
     return fast.to_numpy(), bvh.to_numpy(), exact.to_numpy(), p
 
 
@@ -147,4 +147,4 @@ def test_lightbuf_color_at_batch_random_rays(rt):
             assert fast.tobytes() == exact.tobytes(), depth
         assert rt._rtamd._wf_profile(w, -1, True)["lb_res"] == 64
     finally:
-        rt._rtamd._tuning_set("lb_res", 256)
+        rt._rtamd._tuning_set("lb_res", -1)  # (the default: by scene size)
