@@ -266,16 +266,18 @@ def test_ray_classes_single_class_generations(rt, glass):
     assert sf["rays_reflect"] > 10 * sf["rays_primary"]  # the mirrors keep every ray alive
 
 
-@pytest.mark.parametrize("knob,value", [("prim_lane", 1)])
-def test_fast_path_variants_bitwise(rt, knob, value):
+@pytest.mark.parametrize("knob,value,image", [("prim_lane", 1, 0), ("prim_lane", 1, 3)])
+def test_fast_path_variants_bitwise(rt, knob, value, image):
     """The fast path's measured variants: primary rays by the
-    per-lane pair traversal over the LDS image instead of the wave traversal.
-    Each frame equals the exhaustive frame bit for bit, alone and
+    per-lane pair traversal over the LDS image (image 0) or by the per-lane
+    four-wide walk of the global-memory image (image 3) instead of the wave
+    traversal. Each frame equals the exhaustive frame bit for bit, alone and
     in a batch of 3 cameras (root rays not a multiple of 64: padded chunks)."""
     import torch
     from rtamd import scenes
     w, cam, depth = scenes.c3(333, 187)
     exact, _ = _device_frame(cam, w, depth, True)
+    w.tune("image", image)
     w.tune(knob, value)
     try:
         fast, _ = _device_frame(cam, w, depth, False)
@@ -289,3 +291,4 @@ def test_fast_path_variants_bitwise(rt, knob, value):
             assert torch.equal(b, exact)
     finally:
         w.tune(knob, 0)
+        w.tune("image", 0)
