@@ -1001,7 +1001,8 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   const size_t o_fg = align(o_or + (orec.size() + 1) * sizeof(OtherRec));
   const size_t o_fq = align(o_fg + (fx_gen.size() + 1) * sizeof(SphereGen));
   const size_t o_sh = align(o_fq + (fx_quads.size() + 1) * sizeof(QuadRec));
-  const size_t o_li = align(o_sh + shade.size() * sizeof(ShadeRec));
+  const size_t o_rt = align(o_sh + shade.size() * sizeof(ShadeRec));
+  const size_t o_li = align(o_rt + (shade.size() + 1) * 2 * sizeof(double));
   const size_t o_lc = align(o_li + lrec.size() * sizeof(LightRec));
   const size_t o_lv = align(o_lc + lb.cells.size() * sizeof(LbCell));
   const size_t o_ld = align(o_lv + (lb.ov.size() + 1) * sizeof(uint16_t));
@@ -1020,6 +1021,10 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   if (!fx_gen.empty()) std::memcpy(&host[o_fg], fx_gen.data(), fx_gen.size() * sizeof(SphereGen));
   if (!fx_quads.empty()) std::memcpy(&host[o_fq], fx_quads.data(), fx_quads.size() * sizeof(QuadRec));
   if (!shade.empty()) std::memcpy(&host[o_sh], shade.data(), shade.size() * sizeof(ShadeRec));
+  for (size_t i = 0; i < shade.size(); ++i) {
+    const double rt2[2] = {shade[i].reflective, shade[i].transparency};
+    std::memcpy(&host[o_rt + i * 2 * sizeof(double)], rt2, sizeof rt2);
+  }
   if (!lrec.empty()) std::memcpy(&host[o_li], lrec.data(), lrec.size() * sizeof(LightRec));
   if (!lb.cells.empty()) {
     std::memcpy(&host[o_lc], lb.cells.data(), lb.cells.size() * sizeof(LbCell));
@@ -1081,6 +1086,7 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   s->dev.lb_res = lb.res;
   s->dev.lb_n_items = (int32_t)std::min<size_t>(lb.n_items, 0x7FFFFFFF);
   s->dev.shade = (const ShadeRec*)(b + o_sh);
+  s->dev.refl_transp = (const double*)(b + o_rt);
   s->dev.lights = (const LightRec*)(b + o_li);
   s->dev.n_diag = (int32_t)diag.size();
   s->dev.n_gen = (int32_t)gen.size();

@@ -190,6 +190,9 @@ struct DevScene {
   // 16-bit codes cannot index it), and the most stack entries its traversal keeps
   const BvhWide* bvhw;
   int32_t n_bvhw, bvhw_stack;
+  // per object: ShadeRec::reflective, transparency (what wf_combine_parents reads; 16 B a
+  // record, so the table stays in the L2 where the 512-B shading records may not)
+  const double* refl_transp;
 };
 
 struct DevCamera {

@@ -771,10 +771,16 @@ __device__ __forceinline__ bool shadow_trace(const DevScene& sc, unsigned use_lb
 
 // World::shade_hit's combination (world.rs:58-67) of the surface term and the
 // reflected / refracted colours, with the reference's expression.
-__device__ __forceinline__ V3 shade_color(const ShadeRec& m, V3 surface, V3 refl, V3 refr, double schlick_r) {
-  if (m.reflective > 0.0 && m.transparency > 0.0)
+// (From the material's reflective and transparency values alone: wf_combine_parents
+// reads them from the scene's small per-object table.)
+__device__ __forceinline__ V3 shade_color_rt(double reflective, double transparency, V3 surface, V3 refl, V3 refr,
+                                             double schlick_r) {
+  if (reflective > 0.0 && transparency > 0.0)
     return vadd(vadd(surface, vscale(refl, schlick_r)), vscale(refr, 1.0 - schlick_r));
   return vadd(vadd(surface, refl), refr);
+}
+__device__ __forceinline__ V3 shade_color(const ShadeRec& m, V3 surface, V3 refl, V3 refr, double schlick_r) {
+  return shade_color_rt(m.reflective, m.transparency, surface, refl, refr, schlick_r);
 }
 
 

@@ -1161,17 +1161,19 @@ __global__ __launch_bounds__(kWfBlock) void wf_combine_parents(DevScene sc, DevC
   }
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const ParentRec p = parents[shard_slot<false>(pre, sh_cap, i)];
-    const ShadeRec& m = sc.shade[p.obj];
+    // the material's reflective and transparency values (the small per-object table)
+    typedef double f64x2v __attribute__((ext_vector_type(2)));
+    const f64x2v rt = *(const f64x2v*)(sc.refl_transp + 2 * (size_t)p.obj);
     V3 refl = v3(0.0, 0.0, 0.0), refr = v3(0.0, 0.0, 0.0);
     if (p.child_refl >= 0) {
       const double* cc = child_colors + (size_t)p.child_refl * 3;
-      refl = vscale(v3(cc[0], cc[1], cc[2]), m.reflective);  // world.rs:113
+      refl = vscale(v3(cc[0], cc[1], cc[2]), rt.x);  // world.rs:113
     }
     if (p.child_refr >= 0) {
       const double* cc = child_colors + (size_t)p.child_refr * 3;
-      refr = vscale(v3(cc[0], cc[1], cc[2]), m.transparency);  // world.rs:133
+      refr = vscale(v3(cc[0], cc[1], cc[2]), rt.y);  // world.rs:133
     }
-    const V3 col = shade_color(m, v3(p.surface[0], p.surface[1], p.surface[2]), refl, refr, p.schlick);
+    const V3 col = shade_color_rt(rt.x, rt.y, v3(p.surface[0], p.surface[1], p.surface[2]), refl, refr, p.schlick);
     double* out = color_dst(a, cam, p.slot);
     out[0] = col.x; out[1] = col.y; out[2] = col.z;
   }
