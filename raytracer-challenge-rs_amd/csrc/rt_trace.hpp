@@ -305,68 +305,108 @@ __device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDia
   }
 }
 // Per-lane traversal over the four-wide layout (LANE == 4, BvhWide; scenes read
-// from global memory): a visit loads one 128-B node (seven 16-B loads: the six
-// planes of the four boxes, the four child codes), tests the four boxes, goes
-// on to the nearest child hit and pushes the others farthest first (a
-// four-key sorting network), so a ray makes about half the dependent node
-// loads of the binary walk. The stack is 16-bit, in LDS (entry k of lane t at
-// lds[k * kTraceBlock + t], sc.bvhw_stack entries at most); the first n_top
-// nodes are read from their LDS copy `top`. Culling is the binary walk's rule
-// on boxes that each hold what lies below them, so the hit is the same, and
-// leaves are batched across the wave the same way.
-template <bool SHADOW>
-__device__ __forceinline__ void lane_trace_wide(const BvhWide* nodes, const SphereDiag* sd, const float* M,
+// from global memory): a visit loads the parts of one 128-B node it needs (six
+// 16-B loads and one 8-B load: per axis the block of the four entry planes and
+// the block of the four exit planes, chosen by the sign of the ray's direction
+// there as in lane_trace_pair, whose byte offsets sit packed in two registers;
+// the four child codes), tests the four boxes with no per-axis min/max, goes on
+// to the nearest child hit and pushes the others farthest first. The order is
+// a sorting network over four 32-bit keys (the entry distance's bits with the
+// slot in the two low bits, a miss all ones: non-negative binary32 values
+// order as their bits do; ties and the two dropped bits only change the visit
+// order); the slots' child codes come from one 64-bit word. A ray makes about
+// half the dependent node loads of the binary walk. The stack is 16-bit, in
+// LDS (entry k of lane t at lds[k * kTraceBlock + t], sc.bvhw_stack entries at
+// most); the first n_top nodes are read from their LDS copy `top`. Culling is
+// slab_hit32's rule (the same entry and exit values) on boxes that each hold
+// what lies below them, so the hit is the same; empty slots have inverted
+// boxes, which cull themselves for every ray with a usable axis, and a ray
+// with none (a huge origin, a NaN) tests every record, as a walk that culls
+// nothing would. Leaves are batched across the wave as in lane_trace.
+// SD: the sphere records (const SphereDiag* in global memory, or Sph48 in LDS);
+// ALL_LDS: every node is in `top` (LANE 15: the whole hierarchy in LDS).
+template <bool SHADOW, typename SD = const SphereDiag*, bool ALL_LDS = false>
+__device__ __forceinline__ void lane_trace_wide(const BvhWide* nodes, SD sd, const float* M,
                                                 bool has_bvh, V3 o, V3 d, double t_shadow, Hit& h, unsigned& n_disc,
                                                 unsigned& n_tests, unsigned& n_boxes, uint16_t* lds,
-                                                const BvhWide* top, int n_top) {
+                                                const BvhWide* top, int n_top, int n_records) {
   const SlabRay sr = slab_ray(o, d, M);
   float t_hi = f32_up(SHADOW ? t_shadow : h.t);
   int sp = 0;
   auto pop = [&]() -> unsigned { return sp > 0 ? (unsigned)lds[(--sp) * kTraceBlock] : kWideEmpty; };
   unsigned e = (SHADOW && h.key >= 0 && h.t < t_shadow) || !has_bvh ? kWideEmpty : 0u;
+  // per axis the entry planes' block (lo[a] when inv >= 0, else hi[a]) with the
+  // constant `on`, the exit block with `of`
+  float on[3], of[3];
+  unsigned offe = 0, offx = 0;
+  bool usable = false;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const bool neg = sr.inv[a] < 0.0f;
+    on[a] = neg ? sr.c_hi[a] : sr.c_lo[a];
+    of[a] = neg ? sr.c_lo[a] : sr.c_hi[a];
+    usable |= sr.inv[a] != 0.0f;
+    offe |= (16u * a + (neg ? 48u : 0u)) << (8 * a);
+    offx |= (16u * a + (neg ? 0u : 48u)) << (8 * a);
+  }
+  asm volatile("" : "+v"(offe), "+v"(offx));
+  if (e == 0u && !usable) {  // no axis can cull (empty slots' inverted boxes need one): every record
+    e = kWideEmpty;
+    for (int k = 0; k < n_records; ++k) {
+      leaf_sphere_test<SHADOW>(sd, k, o, d, h, n_disc);
+      ++n_tests;
+      if (SHADOW && h.key >= 0 && h.t < t_shadow) break;
+    }
+  }
   auto visit = [&]() {
     typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-    u32x4 r[7];
-    if ((int)e < n_top) {
-      typedef __attribute__((address_space(3))) const u32x4 lq;
-      lq* b = (lq*)(top + e);
+    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+    u32x4 E[3], X[3];
+    u32x2 cc;
+    if (ALL_LDS || (int)e < n_top) {
+      typedef __attribute__((address_space(3))) const unsigned char lb;
+      lb* b = (lb*)(top) + e * 128u;
 #pragma unroll
-      for (int k = 0; k < 7; ++k) r[k] = b[k];
+      for (int a = 0; a < 3; ++a) {
+        E[a] = *(__attribute__((address_space(3))) const u32x4*)(b + ((offe >> (8 * a)) & 0xFFu));
+        X[a] = *(__attribute__((address_space(3))) const u32x4*)(b + ((offx >> (8 * a)) & 0xFFu));
+      }
+      cc = *(__attribute__((address_space(3))) const u32x2*)(b + 96);
     } else {
-      typedef __attribute__((address_space(1))) const u32x4 gq;
-      gq* b = (gq*)(nodes + e);
+      typedef __attribute__((address_space(1))) const unsigned char gb;
+      gb* b = (gb*)(nodes);
+      const unsigned n0 = e * 128u;
 #pragma unroll
-      for (int k = 0; k < 7; ++k) r[k] = b[k];
+      for (int a = 0; a < 3; ++a) {
+        E[a] = *(__attribute__((address_space(1))) const u32x4*)(b + (n0 + ((offe >> (8 * a)) & 0xFFu)));
+        X[a] = *(__attribute__((address_space(1))) const u32x4*)(b + (n0 + ((offx >> (8 * a)) & 0xFFu)));
+      }
+      cc = *(__attribute__((address_space(1))) const u32x2*)(b + (n0 + 96u));
     }
-    float key[4];
-    unsigned ch[4];
-    int n = 0;
+    unsigned key[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float lo[3] = {__uint_as_float(r[0][j]), __uint_as_float(r[1][j]), __uint_as_float(r[2][j])};
-      const float hi[3] = {__uint_as_float(r[3][j]), __uint_as_float(r[4][j]), __uint_as_float(r[5][j])};
-      ch[j] = (r[6][j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-      float tj;
-      const bool hj = slab_hit32(lo, hi, sr, t_hi, tj) & (ch[j] != kWideEmpty);
-      key[j] = hj ? tj : INFINITY;
-      n += hj ? 1 : 0;
+      const float t0 = fmaxf(fmaxf(fmaf(__uint_as_float(E[0][j]), sr.inv[0], -on[0]),
+                                   fmaf(__uint_as_float(E[1][j]), sr.inv[1], -on[1])),
+                             fmaxf(fmaf(__uint_as_float(E[2][j]), sr.inv[2], -on[2]), 0.0f));
+      const float t1 = fminf(fminf(fmaf(__uint_as_float(X[0][j]), sr.inv[0], -of[0]),
+                                   fmaf(__uint_as_float(X[1][j]), sr.inv[1], -of[1])),
+                             fminf(fmaf(__uint_as_float(X[2][j]), sr.inv[2], -of[2]), t_hi));
+      key[j] = t0 <= t1 ? ((__float_as_uint(t0) & ~3u) | (unsigned)j) : ~0u;
     }
     n_boxes += 4;
-    // ascending by entry distance (a hit's is finite, a miss's +inf)
     auto cx = [&](int a, int b) {
-      const bool s = key[b] < key[a];
-      const float ka = key[a];
-      const unsigned ca = ch[a];
-      key[a] = s ? key[b] : ka;
-      key[b] = s ? ka : key[b];
-      ch[a] = s ? ch[b] : ca;
-      ch[b] = s ? ca : ch[b];
+      const unsigned lo = min(key[a], key[b]), hi = max(key[a], key[b]);
+      key[a] = lo;
+      key[b] = hi;
     };
     cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
-    if (n >= 4) lds[(sp++) * kTraceBlock] = (uint16_t)ch[3];
-    if (n >= 3) lds[(sp++) * kTraceBlock] = (uint16_t)ch[2];
-    if (n >= 2) lds[(sp++) * kTraceBlock] = (uint16_t)ch[1];
-    e = n > 0 ? ch[0] : pop();
+    const unsigned long long P = ((unsigned long long)cc.y << 32) | cc.x;
+    auto child = [&](unsigned k) { return (unsigned)(P >> ((k & 3u) << 4)); };  // (low 16 bits)
+    if (key[3] != ~0u) lds[(sp++) * kTraceBlock] = (uint16_t)child(key[3]);
+    if (key[2] != ~0u) lds[(sp++) * kTraceBlock] = (uint16_t)child(key[2]);
+    if (key[1] != ~0u) lds[(sp++) * kTraceBlock] = (uint16_t)child(key[1]);
+    e = key[0] != ~0u ? (child(key[0]) & 0xFFFFu) : pop();
   };
   // a leaf's record; true when a shadow ray is found occluded
   auto leaf = [&](unsigned code) {
@@ -465,8 +505,13 @@ __device__ __forceinline__ void lane_trace_pair(const unsigned char* nodes, Sph4
     const f32x2 tz1 = __builtin_elementwise_fma(xz, (f32x2)(inv[2]), (f32x2)(-of[2]));
     const float t0 = fmaxf(fmaxf(tx0.x, ty0.x), fmaxf(tz0.x, 0.0f));
     const float t1 = fmaxf(fmaxf(tx0.y, ty0.y), fmaxf(tz0.y, 0.0f));
-    const float u0 = fminf(fminf(tx1.x, ty1.x), fminf(tz1.x, t_hi));
-    const float u1 = fminf(fminf(tx1.y, ty1.y), fminf(tz1.y, t_hi));
+    // (t_hi is canonical already: a v_min_f32 of our own keeps the compiler from
+    // re-canonicalising it in every visit; C3 closest class 0.866 -> 0.857 ms)
+    float zt0, zt1;
+    asm("v_min_f32 %0, %1, %2" : "=v"(zt0) : "v"(tz1.x), "v"(t_hi));
+    asm("v_min_f32 %0, %1, %2" : "=v"(zt1) : "v"(tz1.y), "v"(t_hi));
+    const float u0 = fminf(fminf(tx1.x, ty1.x), zt0);
+    const float u1 = fminf(fminf(tx1.y, ty1.y), zt1);
     const bool h0 = t0 <= u0;
     const bool h1 = (t1 <= u1) & (cc.y != kPairEmpty);
     n_boxes += 2;
@@ -588,6 +633,11 @@ __host__ __device__ inline size_t pair_lds_bytes(const DevScene& sc) {
 __host__ __device__ inline size_t wide_stack_bytes(const DevScene& sc) {
   return ((size_t)(sc.bvhw_stack > 0 ? sc.bvhw_stack : 1) * kTraceBlock * 2 + 15) & ~(size_t)15;
 }
+// LANE 15: [16-bit stack][every wide node][Sph48 records]
+__host__ __device__ inline size_t wide_lds_bytes(const DevScene& sc) {
+  if (!sc.bvhw) return (size_t)1 << 40;
+  return wide_stack_bytes(sc) + (size_t)sc.n_bvhw * sizeof(BvhWide) + sph48_lds_bytes(sc);
+}
 constexpr unsigned kLdsSpheres = 1u, kLdsDeltas = 2u;  // lane_scene's lds_flags (LANE 0: records; all: distances)
 
 struct LaneScene {
@@ -608,6 +658,26 @@ __device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, unsigned lds
   LaneScene ls{(const unsigned char*)sc.bvh, sc.sph_diag, Sph48{nullptr, nullptr}, nullptr, sc.lb_delta, static_stack,
                {0.f, 0.f, 0.f}, nullptr, 0, nullptr};
   unsigned char* p = dyn;
+  if constexpr (LANE == 15) {  // [16-bit stack][every wide node][Sph48 records and metas]
+    ls.stack16 = (uint16_t*)dyn + threadIdx.x;
+    p += wide_stack_bytes(sc);
+    stage_lds((uint4*)p, (const uint4*)sc.bvhw, sc.n_bvhw * (int)(sizeof(BvhWide) / 16));
+    ls.wtop = (const BvhWide*)p;
+    ls.nodes = p;
+    ls.n_top = sc.n_bvhw;
+    p += (size_t)sc.n_bvhw * sizeof(BvhWide);
+    uint4* r = (uint4*)p;
+    const uint4* src = (const uint4*)sc.sph_diag;
+    const int n3 = sc.n_diag * 3, bd = (int)blockDim.x;
+    for (int i = (int)threadIdx.x; i < n3; i += bd) {
+      const int k = i / 3;
+      r[i] = src[4 * k + (i - 3 * k)];
+    }
+    int* mt = (int*)(p + (size_t)sc.n_diag * 48);
+    for (int k = (int)threadIdx.x; k < sc.n_diag; k += bd) mt[k] = (int)sc.sph_diag[k].meta;
+    ls.s48 = Sph48{(const double*)p, (const int*)mt};
+    p += sph48_lds_bytes(sc);
+  }
   if constexpr (LANE == 4) {  // [16-bit stack][distances][treelet of wide nodes]
     ls.stack16 = (uint16_t*)dyn + threadIdx.x;
     p += wide_stack_bytes(sc);
@@ -747,14 +817,17 @@ __device__ __forceinline__ bool shadow_trace(const DevScene& sc, unsigned use_lb
   if constexpr (QUADS) other_trace<true>(sc, o, d, dist, h, n_disc, n_tests, n_boxes);
   if (!(h.key >= 0 && h.t < dist)) {
     if (use_lb) {
-      if constexpr (LANE == 14) lb_walk(sc, ls.s48, ls.delta, l, o, d, dist, h, n_disc, n_tests);
+      if constexpr (LANE == 14 || LANE == 15) lb_walk(sc, ls.s48, ls.delta, l, o, d, dist, h, n_disc, n_tests);
       else lb_walk(sc, ls.sd, ls.delta, l, o, d, dist, h, n_disc, n_tests);
     } else if constexpr (LANE == 14) {
       lane_trace_pair<true>(ls.nodes, ls.s48, ls.M, sc.n_bvh > 0, o, d, dist, h, n_disc, n_tests, n_boxes,
                             ls.stack16);
+    } else if constexpr (LANE == 15) {
+      lane_trace_wide<true, Sph48, true>((const BvhWide*)ls.nodes, ls.s48, ls.M, sc.n_bvh > 0, o, d, dist, h, n_disc,
+                                         n_tests, n_boxes, ls.stack16, ls.wtop, ls.n_top, sc.n_diag);
     } else if constexpr (LANE == 4) {
       lane_trace_wide<true>((const BvhWide*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, dist, h, n_disc, n_tests,
-                            n_boxes, ls.stack16, ls.wtop, ls.n_top);
+                            n_boxes, ls.stack16, ls.wtop, ls.n_top, sc.n_diag);
 
     } else if constexpr (LANE == 0) {
       Hit hb;  // the wave traversal starts from an empty hit; any blocker is an answer

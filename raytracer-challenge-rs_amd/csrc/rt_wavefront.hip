@@ -39,6 +39,7 @@ int wf_tuning_apply(WfTuning& t, const char* key, int value) {
       {"shadow_stream", &WfTuning::shadow_stream, 0, 2}, {"adaptive_block", &WfTuning::adaptive_block, 0, 1},
       {"prim_lane", &WfTuning::prim_lane, 0, 1},   {"arena_pct", &WfTuning::arena_pct, 1, 100},
       {"compact", &WfTuning::compact, 0, 1},       {"wide", &WfTuning::wide, 0, 1},
+      {"lds_wide", &WfTuning::lds_wide, 0, 1},
       {"d2h", &WfTuning::d2h, 0, 1}};
   if (!key) return 0;
   for (const Knob& k : knobs) {
@@ -917,18 +918,21 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
           lane_trace_pair<false>(ls.nodes, ls.s48, ls.M, sc.n_bvh > 0, o2, d, 0.0, h2, u0, u1, u2, ls.stack16);
           exp_sink(h2.t);
 #endif
+        } else if constexpr (LANE == 15) {
+          lane_trace_wide<false, Sph48, true>((const BvhWide*)ls.nodes, ls.s48, ls.M, sc.n_bvh > 0, o, d, 0.0, h,
+                                              t.disc, t.tests, t.boxes, ls.stack16, ls.wtop, ls.n_top, sc.n_diag);
         } else if constexpr (LANE == 4) {
 #ifdef RTAMD_EXP_DUP_TRAV
           Hit h2 = h;  // (the planes' hit, as the walk below starts from)
 #endif
           lane_trace_wide<false>((const BvhWide*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, t.disc, t.tests,
-                                 t.boxes, ls.stack16, ls.wtop, ls.n_top);
+                                 t.boxes, ls.stack16, ls.wtop, ls.n_top, sc.n_diag);
 #ifdef RTAMD_EXP_DUP_TRAV
           V3 o2 = o;
           exp_opaque(o2.x);
           unsigned u0 = 0, u1 = 0, u2 = 0;
           lane_trace_wide<false>((const BvhWide*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o2, d, 0.0, h2, u0, u1, u2,
-                                 ls.stack16, ls.wtop, ls.n_top);
+                                 ls.stack16, ls.wtop, ls.n_top, sc.n_diag);
           exp_sink(h2.t);
 #endif
         } else {
@@ -1566,6 +1570,13 @@ static hipError_t launch_fused_q(const DevScene& sc, const DevCamera& cam, WfArg
     return launch_lds(wf_trace_fused<true, QUADS, 0, TALLY>, dyn, n, stream, sc, cam, a, tb);
   }
   const bool cam_rays = a.g == 0 && a.camera_mode;  // only generation 0 of a camera render reads camera rays
+  if (tn.image == 0 && tn.lds_wide && wide_lds_bytes(sc) + dl <= kWfLdsLimit) {
+    // the four-wide hierarchy and the 48-B sphere records in LDS, with the light buffer's distances
+    dyn = wide_lds_bytes(sc);
+    if (dl) { a.lds_flags |= kLdsDeltas; dyn += dl; }
+    return cam_rays ? launch_lds(wf_trace_fused<false, QUADS, 15, TALLY, true>, dyn, n, stream, sc, cam, a, tb)
+                    : launch_lds(wf_trace_fused<false, QUADS, 15, TALLY, false>, dyn, n, stream, sc, cam, a, tb);
+  }
   if (tn.image == 0 && pair_lds_bytes(sc) <= kWfLdsLimit) {
     dyn = pair_lds_bytes(sc);
     // compacted shading (the hit queues' 16-bit object codes need n_objects < 16383); the
