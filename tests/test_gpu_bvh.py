@@ -133,12 +133,16 @@ def test_bvh_color_at_batch_random_rays(rt):
         assert fast.tobytes() == exact.tobytes(), depth
 
 
-@pytest.mark.parametrize("offset", [0.0, 1e5, -3e7])
-def test_bvh_binary32_slabs_far_and_axis_rays(rt, offset):
+@pytest.mark.parametrize("offset,image,lds_wide", [(0.0, 0, 0), (1e5, 0, 0), (-3e7, 0, 0), (0.0, 3, 0), (1e5, 3, 0),
+                                                   (-3e7, 3, 0), (1e5, 0, 1), (-3e7, 0, 1)])
+def test_bvh_binary32_slabs_far_and_axis_rays(rt, offset, image, lds_wide):
     """The per-lane traversal's binary32 slab test (DESIGN.md §5.2 error
     bound): a cluster far from the origin, rays from just outside it with
     direction components exactly 0, grazing rays tangent to spheres, and
-    origins on box faces, all bitwise equal to the exhaustive loop."""
+    origins on box faces, all bitwise equal to the exhaustive loop; for the
+    pair image (image 0), the four-wide walk over global memory (image 3) and
+    the four-wide image in LDS (lds_wide), whose empty slots' inverted boxes
+    must cull themselves for axis-parallel rays too."""
     rng = np.random.default_rng(int(abs(offset)) % 997 + 3)
     w = rt.World()
     centres, radii = [], []
@@ -172,10 +176,16 @@ def test_bvh_binary32_slabs_far_and_axis_rays(rt, offset):
     d[1::3, 1:] = 0.0
     d /= np.linalg.norm(d, axis=1, keepdims=True)
     rays = np.vstack([np.array(rays), np.hstack([o, d])])
-    for depth in (0, 3):
-        fast, _ = w.color_at_batch(rays, depth, want_stats=False)
-        exact, _ = w.color_at_batch(rays, depth, want_stats=True)
-        assert fast.tobytes() == exact.tobytes(), depth
+    w.tune("image", image)
+    w.tune("lds_wide", lds_wide)
+    try:
+        for depth in (0, 3):
+            fast, _ = w.color_at_batch(rays, depth, want_stats=False)
+            exact, _ = w.color_at_batch(rays, depth, want_stats=True)
+            assert fast.tobytes() == exact.tobytes(), depth
+    finally:
+        w.tune("image", 0)
+        w.tune("lds_wide", 0)
     assert rt._rtamd._wf_profile(w, -1, True)["n_bvh_nodes"] > 0
 
 
@@ -232,10 +242,10 @@ def test_skipped_shadow_rays_bitwise(rt, neg_zero):
     assert full.to_numpy().tobytes() == exact.to_numpy().tobytes()
 
 
-@pytest.mark.parametrize("image,shadow_lb,compact,wide", [(0, 1, 1, 1), (0, 0, 1, 1), (0, 1, 0, 1), (0, 0, 0, 1),
-                                                         (3, 1, 0, 1), (3, 0, 0, 1), (3, 1, 0, 0), (3, 0, 0, 0),
-                                                         (1, 1, 0, 1), (1, 0, 0, 1)])
-def test_fused_images_bitwise(rt, image, shadow_lb, compact, wide):
+@pytest.mark.parametrize("image,shadow_lb,compact,wide,lds_wide", [
+    (0, 1, 1, 1, 0), (0, 0, 1, 1, 0), (0, 1, 0, 1, 0), (0, 0, 0, 1, 0), (0, 1, 0, 1, 1), (0, 0, 0, 1, 1),
+    (3, 1, 0, 1, 0), (3, 0, 0, 1, 0), (3, 1, 0, 0, 0), (3, 0, 0, 0, 0), (1, 1, 0, 1, 0), (1, 0, 0, 1, 0)])
+def test_fused_images_bitwise(rt, image, shadow_lb, compact, wide, lds_wide):
     """Every scene image of the fast-path kernels (pair layout in LDS, the
     default, with and without compacted shading / nodes and records in global
     memory: the four-wide hierarchy (wide) or the binary one with an LDS stack /
@@ -248,6 +258,7 @@ def test_fused_images_bitwise(rt, image, shadow_lb, compact, wide):
     w.tune("shadow_lb", shadow_lb)
     w.tune("compact", compact)
     w.tune("wide", wide)
+    w.tune("lds_wide", lds_wide)
     try:
         fast, _ = cam.render(w, depth, want_stats=False)
         p = rt._rtamd._wf_profile(w, -1, True)
@@ -258,6 +269,7 @@ def test_fused_images_bitwise(rt, image, shadow_lb, compact, wide):
         w.tune("shadow_lb", 1)
         w.tune("compact", 0)
         w.tune("wide", 1)
+        w.tune("lds_wide", 0)
     assert fast.to_numpy().tobytes() == exact.to_numpy().tobytes()
 
 
@@ -280,10 +292,11 @@ def test_wide_hierarchy_bitwise(rt, leaf):
     rays[:, 3:] /= np.linalg.norm(rays[:, 3:], axis=1, keepdims=True)
     col_exact, _ = w.color_at_batch(rays, depth, True, True)
     boxes = {}
-    w.tune("image", 3)
     try:
-        for wide in (1, 0):
+        for image, wide, lds_wide in ((3, 1, 0), (0, 1, 1), (3, 0, 0)):
+            w.tune("image", image)
             w.tune("wide", wide)
+            w.tune("lds_wide", lds_wide)
             for lb in (1, 0):
                 w.tune("shadow_lb", lb)
                 fast, _ = cam.render(w, depth, want_stats=False)
@@ -291,12 +304,13 @@ def test_wide_hierarchy_bitwise(rt, leaf):
                 col, _ = w.color_at_batch(rays, depth, False)
                 assert col.tobytes() == col_exact.tobytes(), (wide, lb)
             _, st = cam.render(w, depth, want_stats=True, exhaustive=False)
-            boxes[wide] = st["box_tests_executed"]
+            boxes[(image, wide)] = st["box_tests_executed"]
     finally:
         w.tune("image", 0)
         w.tune("wide", 1)
+        w.tune("lds_wide", 0)
         w.tune("shadow_lb", 1)
-    assert boxes[1] != boxes[0] and boxes[1] > 0
+    assert boxes[(3, 1)] != boxes[(3, 0)] and boxes[(3, 1)] > 0 and boxes[(0, 1)] > 0
 
 
 @pytest.mark.parametrize("n_streams,kind", [(2, "torch"), (10, "torch"), (4, "plain"), (4, "dedicated")])
