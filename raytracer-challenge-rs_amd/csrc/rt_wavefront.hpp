@@ -96,7 +96,7 @@ struct WfTuning {
   int image = 0;           // 0 = automatic scene image of the fast-path kernels, 3 / 1 = global memory
   int treelet = 1;         // the global-memory image stages a treelet in LDS
   int wide = 1;            // the global-memory image: 1 = the four-wide hierarchy (BvhWide) when the scene has one
-  int lds_wide = 0;        // fast path: 1 = the four-wide hierarchy and 48-B records in LDS (LANE 15) when they fit
+  int lds_wide = 1;        // fast path: 1 = the four-wide hierarchy and 48-B records in LDS (LANE 15) when they fit
   int treelet_deltas = 1;  // ... after the light buffer's distances (when they fit)
   int shadow_stream = 1;   // exhaustive pipeline: 1 = shadow traces on a second stream when rendering alone
   int adaptive_block = 0;  // generation pipeline: 1 = small trace launches spread over every CU

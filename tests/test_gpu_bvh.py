@@ -185,7 +185,7 @@ def test_bvh_binary32_slabs_far_and_axis_rays(rt, offset, image, lds_wide):
             assert fast.tobytes() == exact.tobytes(), depth
     finally:
         w.tune("image", 0)
-        w.tune("lds_wide", 0)
+        w.tune("lds_wide", 1)
     assert rt._rtamd._wf_profile(w, -1, True)["n_bvh_nodes"] > 0
 
 
@@ -269,7 +269,7 @@ def test_fused_images_bitwise(rt, image, shadow_lb, compact, wide, lds_wide):
         w.tune("shadow_lb", 1)
         w.tune("compact", 0)
         w.tune("wide", 1)
-        w.tune("lds_wide", 0)
+        w.tune("lds_wide", 1)
     assert fast.to_numpy().tobytes() == exact.to_numpy().tobytes()
 
 
@@ -308,7 +308,7 @@ def test_wide_hierarchy_bitwise(rt, leaf):
     finally:
         w.tune("image", 0)
         w.tune("wide", 1)
-        w.tune("lds_wide", 0)
+        w.tune("lds_wide", 1)
         w.tune("shadow_lb", 1)
     assert boxes[(3, 1)] != boxes[(3, 0)] and boxes[(3, 1)] > 0 and boxes[(0, 1)] > 0
 
