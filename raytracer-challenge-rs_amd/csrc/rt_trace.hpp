@@ -329,7 +329,7 @@ template <bool SHADOW, typename SD = const SphereDiag*, bool ALL_LDS = false>
 __device__ __forceinline__ void lane_trace_wide(const BvhWide* nodes, SD sd, const float* M,
                                                 bool has_bvh, V3 o, V3 d, double t_shadow, Hit& h, unsigned& n_disc,
                                                 unsigned& n_tests, unsigned& n_boxes, uint16_t* lds,
-                                                const BvhWide* top, int n_top, int n_records, int n_stack = 0) {
+                                                const BvhWide* top, int n_top, int n_records) {
   const SlabRay sr = slab_ray(o, d, M);
   float t_hi = f32_up(SHADOW ? t_shadow : h.t);
   int sp = 0;
@@ -366,17 +366,12 @@ __device__ __forceinline__ void lane_trace_wide(const BvhWide* nodes, SD sd, con
     if (ALL_LDS || (int)e < n_top) {
       typedef __attribute__((address_space(3))) const unsigned char lb;
       lb* b = (lb*)(top) + e * 128u;
-#ifdef RTAMD_EXP_WIDEA
       cc = *(__attribute__((address_space(3))) const u32x2*)(b + 96);
-#endif
 #pragma unroll
       for (int a = 0; a < 3; ++a) {
         E[a] = *(__attribute__((address_space(3))) const u32x4*)(b + ((offe >> (8 * a)) & 0xFFu));
         X[a] = *(__attribute__((address_space(3))) const u32x4*)(b + ((offx >> (8 * a)) & 0xFFu));
       }
-#ifndef RTAMD_EXP_WIDEA
-      cc = *(__attribute__((address_space(3))) const u32x2*)(b + 96);
-#endif
     } else {
       typedef __attribute__((address_space(1))) const unsigned char gb;
       gb* b = (gb*)(nodes);
@@ -394,16 +389,10 @@ __device__ __forceinline__ void lane_trace_wide(const BvhWide* nodes, SD sd, con
       const float t0 = fmaxf(fmaxf(fmaf(__uint_as_float(E[0][j]), sr.inv[0], -on[0]),
                                    fmaf(__uint_as_float(E[1][j]), sr.inv[1], -on[1])),
                              fmaxf(fmaf(__uint_as_float(E[2][j]), sr.inv[2], -on[2]), 0.0f));
-#ifdef RTAMD_EXP_WIDEA
       float zt;  // (t_hi is canonical: no per-visit re-canonicalisation, as in lane_trace_pair)
       asm("v_min_f32 %0, %1, %2" : "=v"(zt) : "v"(fmaf(__uint_as_float(X[2][j]), sr.inv[2], -of[2])), "v"(t_hi));
       const float t1 = fminf(fminf(fmaf(__uint_as_float(X[0][j]), sr.inv[0], -of[0]),
                                    fmaf(__uint_as_float(X[1][j]), sr.inv[1], -of[1])), zt);
-#else
-      const float t1 = fminf(fminf(fmaf(__uint_as_float(X[0][j]), sr.inv[0], -of[0]),
-                                   fmaf(__uint_as_float(X[1][j]), sr.inv[1], -of[1])),
-                             fminf(fmaf(__uint_as_float(X[2][j]), sr.inv[2], -of[2]), t_hi));
-#endif
       key[j] = t0 <= t1 ? ((__float_as_uint(t0) & ~3u) | (unsigned)j) : ~0u;
     }
     n_boxes += 4;
@@ -415,20 +404,9 @@ __device__ __forceinline__ void lane_trace_wide(const BvhWide* nodes, SD sd, con
     cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
     const unsigned long long P = ((unsigned long long)cc.y << 32) | cc.x;
     auto child = [&](unsigned k) { return (unsigned)(P >> ((k & 3u) << 4)); };  // (low 16 bits)
-#ifdef RTAMD_EXP_WIDEB
-    // unconditional pushes: a miss writes the lane's spare entry past the stack's bound
-    const int spare = n_stack;
-#pragma unroll
-    for (int k = 3; k >= 1; --k) {
-      const bool v = key[k] != ~0u;
-      lds[(v ? sp : spare) * kTraceBlock] = (uint16_t)child(key[k]);
-      sp += v ? 1 : 0;
-    }
-#else
     if (key[3] != ~0u) lds[(sp++) * kTraceBlock] = (uint16_t)child(key[3]);
     if (key[2] != ~0u) lds[(sp++) * kTraceBlock] = (uint16_t)child(key[2]);
     if (key[1] != ~0u) lds[(sp++) * kTraceBlock] = (uint16_t)child(key[1]);
-#endif
     e = key[0] != ~0u ? (child(key[0]) & 0xFFFFu) : pop();
   };
   // a leaf's record; true when a shadow ray is found occluded
@@ -654,7 +632,7 @@ __host__ __device__ inline size_t pair_lds_bytes(const DevScene& sc) {
 }
 // LANE 4: the 16-bit stack (sc.bvhw_stack entries) x kTraceBlock, before the distances and the treelet
 __host__ __device__ inline size_t wide_stack_bytes(const DevScene& sc) {
-  return ((size_t)(sc.bvhw_stack + 1) * kTraceBlock * 2 + 15) & ~(size_t)15;  // (+ one spare entry)
+  return ((size_t)(sc.bvhw_stack > 0 ? sc.bvhw_stack : 1) * kTraceBlock * 2 + 15) & ~(size_t)15;
 }
 // LANE 15: [16-bit stack][every wide node][Sph48 records]
 __host__ __device__ inline size_t wide_lds_bytes(const DevScene& sc) {
@@ -847,10 +825,10 @@ __device__ __forceinline__ bool shadow_trace(const DevScene& sc, unsigned use_lb
                             ls.stack16);
     } else if constexpr (LANE == 15) {
       lane_trace_wide<true, Sph48, true>((const BvhWide*)ls.nodes, ls.s48, ls.M, sc.n_bvh > 0, o, d, dist, h, n_disc,
-                                         n_tests, n_boxes, ls.stack16, ls.wtop, ls.n_top, sc.n_diag, sc.bvhw_stack);
+                                         n_tests, n_boxes, ls.stack16, ls.wtop, ls.n_top, sc.n_diag);
     } else if constexpr (LANE == 4) {
       lane_trace_wide<true>((const BvhWide*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, dist, h, n_disc, n_tests,
-                            n_boxes, ls.stack16, ls.wtop, ls.n_top, sc.n_diag, sc.bvhw_stack);
+                            n_boxes, ls.stack16, ls.wtop, ls.n_top, sc.n_diag);
 
     } else if constexpr (LANE == 0) {
       Hit hb;  // the wave traversal starts from an empty hit; any blocker is an answer

@@ -920,14 +920,13 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
 #endif
         } else if constexpr (LANE == 15) {
           lane_trace_wide<false, Sph48, true>((const BvhWide*)ls.nodes, ls.s48, ls.M, sc.n_bvh > 0, o, d, 0.0, h,
-                                              t.disc, t.tests, t.boxes, ls.stack16, ls.wtop, ls.n_top, sc.n_diag,
-                                              sc.bvhw_stack);
+                                              t.disc, t.tests, t.boxes, ls.stack16, ls.wtop, ls.n_top, sc.n_diag);
         } else if constexpr (LANE == 4) {
 #ifdef RTAMD_EXP_DUP_TRAV
           Hit h2 = h;  // (the planes' hit, as the walk below starts from)
 #endif
           lane_trace_wide<false>((const BvhWide*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, t.disc, t.tests,
-                                 t.boxes, ls.stack16, ls.wtop, ls.n_top, sc.n_diag, sc.bvhw_stack);
+                                 t.boxes, ls.stack16, ls.wtop, ls.n_top, sc.n_diag);
 #ifdef RTAMD_EXP_DUP_TRAV
           V3 o2 = o;
           exp_opaque(o2.x);
