@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstring>
 #include <limits>
+#include <thread>
 
 namespace rtamd {
 namespace {
@@ -592,8 +593,6 @@ LightBuffer build_light_buffer(const std::vector<SphereDiag>& sph, const std::ve
   std::vector<std::array<double, 6>> rel(n);
   std::vector<double> delta(n);
   std::vector<char> finite(n), caster(n), near(n);
-  std::vector<std::array<int, 4>> rect;  // per record and face: i_lo, i_hi, j_lo, j_hi (i_lo < 0: none)
-  std::vector<std::vector<uint16_t>> lists(per);
   for (size_t l = 0; l < lights.size(); ++l) {
     const double* L = lights[l].pos;
     if (!(std::isfinite(L[0]) && std::isfinite(L[1]) && std::isfinite(L[2]))) continue;  // limit -1: exhaustive
@@ -645,32 +644,73 @@ LightBuffer build_light_buffer(const std::vector<SphereDiag>& sph, const std::ve
       r[2] = lb_cell_index(std::max(-1.0, std::min(1.0, v_lo)), R);
       r[3] = lb_cell_index(std::max(-1.0, std::min(1.0, v_hi)), R);
     };
-    for (auto& v : lists) v.clear();
-    for (int i = 0; i < n; ++i) {
-      if (!caster[i]) continue;
-      for (int f = 0; f < 6; ++f) {
-        int r[4];
+    // the lists as one flat array (counts, offsets, fill; each face's cells get
+    // entries only from that face's rectangles, so the six faces are built in
+    // parallel, each in increasing record order), then every cell sorted and
+    // encoded in parallel over contiguous blocks of cells
+    // (small maps: one thread, the threads would cost more than they save)
+    const bool par = per >= ((size_t)1 << 17);
+    const unsigned nt = par ? std::max(1u, std::min(16u, std::thread::hardware_concurrency())) : 1u;
+    std::vector<std::array<int, 4>> rects((size_t)n * 6);
+    std::vector<uint32_t> cnt(per + 1, 0);
+    auto for_faces = [&](auto&& fn) {
+      if (!par) {
+        for (int f = 0; f < 6; ++f) fn(f);
+        return;
+      }
+      std::vector<std::thread> th;
+      for (int f = 0; f < 6; ++f) th.emplace_back(fn, f);
+      for (std::thread& t : th) t.join();
+    };
+    for_faces([&](int f) {
+      for (int i = 0; i < n; ++i) {
+        int* r = rects[(size_t)i * 6 + f].data();
+        r[0] = -1;
+        if (!caster[i]) continue;
         if (near[i]) { r[0] = 0; r[1] = R - 1; r[2] = 0; r[3] = R - 1; }
         else face_rect(i, f, r);
         if (r[0] < 0) continue;
         for (int j = r[2]; j <= r[3]; ++j)
-          for (int k = r[0]; k <= r[1]; ++k) lists[(size_t)f * R * R + (size_t)j * R + k].push_back((uint16_t)i);
+          for (int k = r[0]; k <= r[1]; ++k) ++cnt[(size_t)f * R * R + (size_t)j * R + k];
       }
-    }
+    });
+    std::vector<uint64_t> off(per + 1, 0);
+    for (size_t c = 0; c < per; ++c) off[c + 1] = off[c] + cnt[c];
+    std::vector<uint16_t> items(off[per]);
+    for_faces([&](int f) {
+      std::vector<uint64_t> pos(off.begin() + (long)f * R * R, off.begin() + (long)(f + 1) * R * R);
+      for (int i = 0; i < n; ++i) {
+        const int* r = rects[(size_t)i * 6 + f].data();
+        if (r[0] < 0) continue;
+        for (int j = r[2]; j <= r[3]; ++j)
+          for (int k = r[0]; k <= r[1]; ++k) items[pos[(size_t)j * R + k]++] = (uint16_t)i;
+      }
+    });
+    // entries past the inline ones go to lb.ov, cell by cell
+    std::vector<uint64_t> ovo(per + 1, 0);
+    for (size_t c = 0; c < per; ++c) ovo[c + 1] = ovo[c] + (cnt[c] > (uint32_t)kLbInline ? cnt[c] - kLbInline : 0);
+    const size_t ov0 = lb.ov.size();
+    lb.ov.resize(ov0 + ovo[per]);
     const float* dl = &lb.delta[l * n];
-    for (size_t c = 0; c < per; ++c) {
-      std::vector<uint16_t>& v = lists[c];
-      std::sort(v.begin(), v.end(), [&](uint16_t x, uint16_t y) { return dl[x] < dl[y] || (dl[x] == dl[y] && x < y); });
-      uint16_t in[kLbInline] = {0, 0, 0, 0, 0};
-      for (size_t k = 0; k < v.size() && k < (size_t)kLbInline; ++k) in[k] = v[k];
-      LbCell& cell = lb.cells[l * per + c];
-      cell.w0 = (uint32_t)std::min<size_t>(v.size(), 0xFFFF) | (uint32_t)in[0] << 16;
-      cell.w1 = in[1] | (uint32_t)in[2] << 16;
-      cell.w2 = in[3] | (uint32_t)in[4] << 16;
-      cell.ov = (uint32_t)lb.ov.size();
-      for (size_t k = kLbInline; k < v.size(); ++k) lb.ov.push_back(v[k]);
-      lb.n_items += v.size();
-    }
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t)
+      th.emplace_back([&, t]() {  // (contiguous blocks of cells: no two threads share a line)
+        for (size_t c = per * t / nt; c < per * (t + 1) / nt; ++c) {
+          uint16_t* v = items.data() + off[c];
+          const size_t m = cnt[c];
+          std::sort(v, v + m, [&](uint16_t x, uint16_t y) { return dl[x] < dl[y] || (dl[x] == dl[y] && x < y); });
+          uint16_t in[kLbInline] = {0, 0, 0, 0, 0};
+          for (size_t k = 0; k < m && k < (size_t)kLbInline; ++k) in[k] = v[k];
+          LbCell& cell = lb.cells[l * per + c];
+          cell.w0 = (uint32_t)std::min<size_t>(m, 0xFFFF) | (uint32_t)in[0] << 16;
+          cell.w1 = in[1] | (uint32_t)in[2] << 16;
+          cell.w2 = in[3] | (uint32_t)in[4] << 16;
+          cell.ov = (uint32_t)(ov0 + ovo[c]);
+          for (size_t k = kLbInline; k < m; ++k) lb.ov[ov0 + ovo[c] + (k - kLbInline)] = v[k];
+        }
+      });
+    for (std::thread& t : th) t.join();
+    lb.n_items += off[per];
   }
   return lb;
 }
