@@ -601,8 +601,12 @@ __device__ __forceinline__ void prep_one(const DevScene& sc, const WfArgs& a, un
 // final colour. Only nodes with a reflected or refracted child are queued
 // (ParentRec) for wf_combine_parents, which runs once the children's colours
 // exist. Scene images of the kernels (LANE):
-//   14: pair-layout nodes + sphere records + per-lane stack in LDS (the default)
-//    3: nodes and records in global memory, per-lane stack in LDS
+//   15: the four-wide hierarchy + 48-B sphere records + 16-bit stack in LDS
+//       (the default where they fit)
+//   14: pair-layout nodes + sphere records + per-lane stack in LDS
+//    4: the four-wide hierarchy and records in global memory, a treelet of its
+//       top nodes and the 16-bit stack in LDS (the default for larger scenes)
+//    3: binary nodes and records in global memory, per-lane stack in LDS
 //    1: nodes and records in global memory, per-lane stack in scratch (trees
 //       deeper than kLaneLdsDepth)
 //    0: primary rays, wave (packet) traversal over global nodes (one LDS stack
