@@ -37,7 +37,7 @@ int wf_tuning_apply(WfTuning& t, const char* key, int value) {
       {"shadow_lb", &WfTuning::shadow_lb, 0, 1},   {"image", &WfTuning::image, 0, 3},
       {"treelet", &WfTuning::treelet, 0, 1},       {"treelet_deltas", &WfTuning::treelet_deltas, 0, 1},
       {"shadow_stream", &WfTuning::shadow_stream, 0, 2}, {"adaptive_block", &WfTuning::adaptive_block, 0, 1},
-      {"prim_lane", &WfTuning::prim_lane, 0, 1},   {"arena_pct", &WfTuning::arena_pct, 1, 100},
+      {"prim_lane", &WfTuning::prim_lane, 0, 2},   {"arena_pct", &WfTuning::arena_pct, 1, 100},
       {"compact", &WfTuning::compact, 0, 1},       {"wide", &WfTuning::wide, 0, 1},
       {"lds_wide", &WfTuning::lds_wide, 0, 1},
       {"d2h", &WfTuning::d2h, 0, 1}};
@@ -1567,7 +1567,12 @@ static hipError_t launch_fused_q(const DevScene& sc, const DevCamera& cam, WfArg
   // primary rays: the wave traversal, or with prim_lane the per-lane walk of the pair image or of
   // the four-wide hierarchy (the launches below, reading camera rays)
   const bool wide_ok = tn.image != 1 && tn.wide && sc.bvhw && wide_stack_bytes(sc) <= kWfLdsLimit / 2;
-  if (primary && !(tn.prim_lane && ((tn.image == 0 && pair_lds_bytes(sc) <= kWfLdsLimit) || wide_ok))) {
+  // prim_lane 1: any per-lane image; 2 (default): the LDS images only (C3 primary class 0.128 ->
+  // 0.125 ms/frame with the LDS four-wide image; C5's global image 2.06 -> 2.16 ms, so not there)
+  const bool lds_img = tn.image == 0 && (pair_lds_bytes(sc) <= kWfLdsLimit ||
+                                         (tn.lds_wide && wide_lds_bytes(sc) + dl <= kWfLdsLimit));
+  const bool lane_prim = tn.prim_lane == 1 ? (lds_img || wide_ok) : tn.prim_lane == 2 ? lds_img : false;
+  if (primary && !lane_prim) {
     const size_t room = kWfLdsLimit - (size_t)(kTraceBlock / 64) * (kBvhMaxDepth + 4) * 4;
     if (sph_lds_bytes(sc) <= room) { a.lds_flags |= kLdsSpheres; dyn += sph_lds_bytes(sc); }
     if (dl && dyn + dl <= room) { a.lds_flags |= kLdsDeltas; dyn += dl; }

@@ -102,8 +102,8 @@ struct WfTuning {
   int adaptive_block = 0;  // generation pipeline: 1 = small trace launches spread over every CU
   int compact = 0;         // fast path, pair image: 1 = compacted shading (hit queues in LDS, full-width shading;
                            //     measured slower on C3, DESIGN.md "Compacted shading")
-  int prim_lane = 0;       // fast path: 1 = primary rays by the per-lane pair traversal (LDS image) instead
-                           //     of the wave traversal with shared-origin records
+  int prim_lane = 2;       // fast path: primary rays by the per-lane walk instead of the wave traversal with
+                           //     shared-origin records: 1 = over any image, 2 = over the LDS images only, 0 = never
   int arena_pct = 100;     // test hook: the fast path's queue arenas sized to this percentage of the hint,
                            //     shrinking them (< 100: forces overflows, DESIGN.md "Device-sized generations")
   int d2h = 1;             // host-canvas copies: 1 = pin the caller's buffer for the call and DMA into it, 0 = pinned chunks

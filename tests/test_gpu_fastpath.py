@@ -266,7 +266,8 @@ def test_ray_classes_single_class_generations(rt, glass):
     assert sf["rays_reflect"] > 10 * sf["rays_primary"]  # the mirrors keep every ray alive
 
 
-@pytest.mark.parametrize("knob,value,image", [("prim_lane", 1, 0), ("prim_lane", 1, 3)])
+@pytest.mark.parametrize("knob,value,image", [("prim_lane", 1, 0), ("prim_lane", 1, 3), ("prim_lane", 0, 0),
+                                              ("prim_lane", 2, 3)])
 def test_fast_path_variants_bitwise(rt, knob, value, image):
     """The fast path's measured variants: primary rays by the
     per-lane pair traversal over the LDS image (image 0) or by the per-lane
@@ -290,5 +291,5 @@ def test_fast_path_variants_bitwise(rt, knob, value, image):
         for b in bufs:
             assert torch.equal(b, exact)
     finally:
-        w.tune(knob, 0)
+        w.tune(knob, 2)  # (the default: the per-lane walk for primary rays over the LDS images)
         w.tune("image", 0)
