@@ -242,8 +242,11 @@ struct rt_scene {
   // the workspace for a render on `st` (stream-ordered after its previous user)
   hipError_t acquire(hipStream_t st, WfSlot** out) {
     WfSlot* pick = nullptr;
+    // this stream's workspace, unless a synchronous call in flight holds it (pinned): two
+    // calls on one stream must not share a workspace's counters and overflow record (the
+    // call takes another workspace; stream order still runs the two renders in turn)
     for (WfSlot& w : wfs)
-      if (w.stream == st) pick = &w;
+      if (w.stream == st && w.pins == 0) pick = &w;
     size_t unpinned = 0;
     for (WfSlot& w : wfs) unpinned += w.pins == 0;
     if (!pick && (wfs.size() < kMaxWorkspaces || unpinned == 0)) {
@@ -461,12 +464,16 @@ int check_faults(rt_scene* s) {
 // until it fits (every synchronous entry point returns a complete frame).
 // Asynchronous renders report an overflow later (check_faults). With `lk`
 // (the scene's lock, held on entry and on return) the waits run unlocked;
-// the workspace stays pinned to this call meanwhile.
+// the workspace stays pinned to this call meanwhile. `used` receives the
+// workspace; with `keep_pin` it stays pinned after the return (the caller
+// reads it back and unpins it, under the scene's lock). `count`: the render
+// counts the reference's rays (read_stats) without synchronising.
 int run_render(rt_scene* s, const DevCamera& cam, const double* d_rays, uint32_t n_tasks, uint32_t aa,
                uint32_t max_depth, uint32_t row_block, uint32_t shard, uint32_t n_shards, double* d_out,
                hipStream_t stream, DevStats* stats_out = nullptr, float* ms_out = nullptr, uint32_t flags = 0,
                rt_scene::WfSlot** used = nullptr, const FrameTable* batch = nullptr, unsigned n_frames = 1,
-               bool sync = false, std::unique_lock<std::mutex>* lk = nullptr) {
+               bool sync = false, std::unique_lock<std::mutex>* lk = nullptr, bool count = false,
+               bool keep_pin = false) {
   if (max_depth > (uint32_t)kMaxDepth)
     return fail(RT_ERR_INVALID_ARGUMENT, "max_depth > " + std::to_string(kMaxDepth));
   if (!valid_aa(aa)) return fail(RT_ERR_INVALID_ARGUMENT, "aa_samples must be 1, 2, 4, 8 or 16");
@@ -483,16 +490,17 @@ int run_render(rt_scene* s, const DevCamera& cam, const double* d_rays, uint32_t
   hipError_t e = s->acquire(stream, &w);
   if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("wavefront render: ") + hipGetErrorString(e));
   const unsigned wf_flags = ((flags & RT_RENDER_EXHAUSTIVE) ? WF_EXHAUSTIVE : 0u) |
-                            ((used || stats_out) ? WF_COUNT : 0u) | (ms_out ? WF_TIME : 0u);
+                            ((count || stats_out) ? WF_COUNT : 0u) | (ms_out ? WF_TIME : 0u);
   sync = sync || stats_out || ms_out;
-  struct Pin {  // the workspace is this call's until it returns
+  struct Pin {  // the workspace is this call's until it returns (keep_pin: until the caller unpins it)
     rt_scene::WfSlot* w;
     bool on;
     ~Pin() {
       if (on) --w->pins;
     }
-  } pin{w, sync};
-  if (sync) ++w->pins;
+  } pin{w, sync && !keep_pin};
+  if (sync || keep_pin) ++w->pins;
+  if (keep_pin && used) *used = w;
   for (int attempt = 0;; ++attempt) {
     e = w->wf->render(s->dev, cam, d_rays == nullptr, d_rays, n_tasks, aa, max_depth, row_block, shard, n_shards,
                       d_out, stream, s->sizing, nullptr, nullptr, s->tune, s->wfs.size() == 1, wf_flags, batch,
@@ -1505,8 +1513,22 @@ int rt_render_multi(rt_scene* const* scenes, int n_devices, const rt_camera_desc
   RT_HIP(hipSetDevice(0));
   int rc = ensure_dev_buffer(&mc.recv, &mc.recv_cap, per * n_devices);
   if (rc != RT_OK) return rc;
-  // every device renders its shard (asynchronously, each on its scene's stream)
+  // every device renders its shard (asynchronously, each on its scene's stream); the
+  // workspaces this call renders on stay pinned until it has read their overflow
+  // records (no other call takes them over, and no other call's records are read)
   std::vector<rt_scene::WfSlot*> used(n_devices, nullptr);
+  auto unpin_all = [&]() {
+    for (int i = 0; i < n_devices; ++i)
+      if (used[i]) {
+        std::lock_guard<std::mutex> lk(scenes[i]->mu);
+        --used[i]->pins;
+        used[i] = nullptr;
+      }
+  };
+  struct Unpin {
+    decltype(unpin_all)& f;
+    ~Unpin() { f(); }
+  } unpin_on_return{unpin_all};
   int attempt = 0;
 render_all:
   for (int i = 0; i < n_devices; ++i) {
@@ -1515,8 +1537,8 @@ render_all:
     const uint32_t rows = rt_shard_rows(H, row_block, i, n_devices);
     if (stats) RT_HIP(hipEventRecord(mc.ev0[i], scenes[i]->stream));
     rc = run_render(scenes[i], to_dev_camera(*camera), nullptr, rows * W * aa_samples, aa_samples, max_depth,
-                    row_block, i, n_devices, mc.send[i], scenes[i]->stream, nullptr, nullptr, 0,
-                    stats ? &used[i] : nullptr);
+                    row_block, i, n_devices, mc.send[i], scenes[i]->stream, nullptr, nullptr, 0, &used[i], nullptr,
+                    1, false, nullptr, stats != nullptr, true);
     if (rc != RT_OK) return rc;
     if (stats) RT_HIP(hipEventRecord(mc.ev1[i], scenes[i]->stream));
   }
@@ -1547,20 +1569,21 @@ render_all:
     RT_HIP(hipSetDevice(i));
     RT_HIP(hipStreamSynchronize(scenes[i]->stream));
   }
-  // a shard that overflowed its queue arenas: the arenas have grown, render the frame again
+  // a shard that overflowed its queue arenas (this call's workspaces only): the arenas
+  // have grown, render the frame again
   bool again = false;
   for (int i = 0; i < n_devices; ++i) {
+    if (!used[i]) continue;  // an empty shard
     RT_HIP(hipSetDevice(i));
     std::lock_guard<std::mutex> lk(scenes[i]->mu);
-    for (rt_scene::WfSlot& w : scenes[i]->wfs) {
-      bool was = false;
-      w.wf->learn(scenes[i]->sizing);
-      RT_HIP(w.wf->take_overflow(&was));
-      again = again || was;
-    }
+    bool was = false;
+    used[i]->wf->learn(scenes[i]->sizing);
+    RT_HIP(used[i]->wf->take_overflow(&was));
+    again = again || was;
   }
   if (again) {
     if (++attempt > 24) return fail(RT_ERR_HIP, "wavefront queue arenas: the frame does not fit");
+    unpin_all();  // (the counters are read from the last attempt's workspaces)
     goto render_all;
   }
   if (stats) {

@@ -824,10 +824,10 @@ __device__ __forceinline__ bool shadow_trace(const DevScene& sc, unsigned use_lb
       lane_trace_pair<true>(ls.nodes, ls.s48, ls.M, sc.n_bvh > 0, o, d, dist, h, n_disc, n_tests, n_boxes,
                             ls.stack16);
     } else if constexpr (LANE == 15) {
-      lane_trace_wide<true, Sph48, true>((const BvhWide*)ls.nodes, ls.s48, ls.M, sc.n_bvh > 0, o, d, dist, h, n_disc,
+      lane_trace_wide<true, Sph48, true>((const BvhWide*)ls.nodes, ls.s48, ls.M, sc.bvhw != nullptr, o, d, dist, h, n_disc,
                                          n_tests, n_boxes, ls.stack16, ls.wtop, ls.n_top, sc.n_diag);
     } else if constexpr (LANE == 4) {
-      lane_trace_wide<true>((const BvhWide*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, dist, h, n_disc, n_tests,
+      lane_trace_wide<true>((const BvhWide*)ls.nodes, ls.sd, ls.M, sc.bvhw != nullptr, o, d, dist, h, n_disc, n_tests,
                             n_boxes, ls.stack16, ls.wtop, ls.n_top, sc.n_diag);
 
     } else if constexpr (LANE == 0) {

@@ -38,7 +38,7 @@ int wf_tuning_apply(WfTuning& t, const char* key, int value) {
       {"treelet", &WfTuning::treelet, 0, 1},       {"treelet_deltas", &WfTuning::treelet_deltas, 0, 1},
       {"shadow_stream", &WfTuning::shadow_stream, 0, 2}, {"adaptive_block", &WfTuning::adaptive_block, 0, 1},
       {"prim_lane", &WfTuning::prim_lane, 0, 2},   {"arena_pct", &WfTuning::arena_pct, 1, 100},
-      {"compact", &WfTuning::compact, 0, 1},       {"wide", &WfTuning::wide, 0, 1},
+      {"wide", &WfTuning::wide, 0, 1},
       {"lds_wide", &WfTuning::lds_wide, 0, 1},
       {"d2h", &WfTuning::d2h, 0, 1}};
   if (!key) return 0;
@@ -213,9 +213,7 @@ __device__ __forceinline__ unsigned frame_of(const WfArgs& a, unsigned i, unsign
 // generations read their queue.
 // CAM = false: a launch that never reads camera rays (generations >= 1, or
 // explicit rays), compiled without the camera path and its registers.
-// NT: the ray's last read (non-temporal: it leaves the L2 to the scene); the
-// compacted kernel reads a ray twice (traversal, then shading) and keeps the
-// first read in the L2.
+// NT: the ray's last read (non-temporal: it leaves the L2 to the scene).
 template <bool CAM = true, bool NT = true>
 __device__ __forceinline__ void wf_ray(const WfArgs& a, const DevCamera& cam, unsigned i, V3& o, V3& d) {
   if (CAM && a.g == 0 && a.camera_mode) {
@@ -676,6 +674,7 @@ __device__ __forceinline__ unsigned bind_generation(WfArgs& a, const unsigned* p
     a.gsh[g] = sh_cap;
     a.gtab[g + 1] = WfGenTab{out_cap, 0u, c_next, t.par_off + (unsigned long long)kShards * sh_cap};
     if (!fits) {  // host-mapped: plain vector stores, the flag last
+      a.cnt->overflow = 1u;  // this pass's canvases are poisoned at its end (poison_frames)
       volatile WfHostRec* r = a.hrec;
       r->need_colors = need_c;
       r->need_parents = need_p;
@@ -697,12 +696,6 @@ __device__ __forceinline__ unsigned bind_generation(WfArgs& a, const unsigned* p
   a.parents = a.par_base + t.par_off;
   return n;
 }
-
-// Phase-cost experiments (dev builds only, -DRTAMD_EXP_DUP_*: a phase runs a
-// second time on opaque copies of its inputs, its result sunk; the frame is
-// unchanged and the added time is the phase's cost). tools/exp_time.sh.
-__device__ __forceinline__ void exp_opaque(double& x) { asm volatile("" : "+v"(x)); }
-__device__ __forceinline__ void exp_sink(double x) { asm volatile("" ::"v"(x)); }
 
 // Per-lane tallies of a fused trace kernel (summed per wave at the end).
 struct FusedTally {
@@ -730,14 +723,6 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
   const ShadeRec* m = nullptr;
   if (valid && h.key >= 0) {
     c = prepare(sc, o, d, h);
-#ifdef RTAMD_EXP_DUP_PREP
-    {
-      V3 o2 = o;
-      exp_opaque(o2.x);
-      const Comps c2 = prepare(sc, o2, d, h);
-      exp_sink(c2.over.x + c2.normal.y + c2.n1);
-    }
-#endif
     hit = true;
     m = &sc.shade[c.obj];
     // reflected_color (world.rs:107-114)
@@ -792,24 +777,8 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
     } else {
       const bool shadowed = shadow_trace<LANE, QUADS>(sc, a.use_lb, ls, l, c.over, sdir, dist, t.sh_disc, t.sh_tests,
                                                       t.sh_boxes);
-#ifdef RTAMD_EXP_DUP_SHADOW
-      {
-        V3 o2 = c.over;
-        exp_opaque(o2.x);
-        unsigned u0 = 0, u1 = 0, u2 = 0;
-        exp_sink(shadow_trace<LANE, QUADS>(sc, a.use_lb, ls, l, o2, sdir, dist, u0, u1, u2) ? 1.0 : 0.0);
-      }
-#endif
       ++t.sh_rays;
       term = lighting(*m, Lr, c.over, c.eyev, c.normal, shadowed, sdir);
-#ifdef RTAMD_EXP_DUP_LIGHT
-      {
-        V3 o2 = c.over;
-        exp_opaque(o2.x);
-        const V3 t2 = lighting(*m, Lr, o2, c.eyev, c.normal, shadowed, sdir);
-        exp_sink(t2.x + t2.y + t2.z);
-      }
-#endif
     }
     surface = vadd(surface, term);
   }
@@ -835,17 +804,7 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
 // per-visit and per-test counting and the wave-end atomics altogether: C3
 // 1.021 -> 0.964 ms/frame, an 8-way shard 0.204 -> 0.184 ms.
 // CAM: the launch may read camera rays (generation 0 of a camera render).
-// COMPACT (LANE 14): shading at full width (DESIGN.md "Compacted shading"):
-// the hits of each traversed chunk go to a per-wave LDS queue (misses are
-// written black at once), and the wave shades 64 queued hits at a time, so
-// the shading, shadow rays and spawns run with every lane busy instead of
-// with the chunk's misses idle. The appends of a shaded batch use the index
-// of the chunk whose traversal filled it (at most one batch per chunk), and
-// the wave's last, partial batch the index of one of its chunks that filled
-// none (there is one: a wave that shaded a batch after each of its k chunks
-// queued 64 k hits, so none are left), so every wave-iteration index is a
-// chunk's, used once, and the capacity argument ("Sharded queues") holds.
-template <bool PRIMARY, bool QUADS, int LANE, bool TALLY, bool CAM = PRIMARY, bool COMPACT = false>
+template <bool PRIMARY, bool QUADS, int LANE, bool TALLY, bool CAM = PRIMARY>
 __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, DevCamera cam, WfArgs a) {
   __shared__ int stack_lds[LANE == 3 ? kLaneLdsDepth * kTraceBlock
                            : LANE == 0 ? (kTraceBlock / 64) * (kBvhMaxDepth + 4) : 1];
@@ -897,7 +856,7 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
   auto traverse = [&](unsigned i, bool valid, unsigned slot, V3& o, V3& d, Hit& h) {
     hit_init(h);
     if (valid) {
-      wf_ray<CAM, !COMPACT>(a, cam, slot, o, d);
+      wf_ray<CAM>(a, cam, slot, o, d);
       if constexpr (LANE == 0) {
         // the chunk's frame (chunks never mix frames): its shared-origin primary records
         const unsigned pf = a.n_frames > 1 ? (c * 64u) / a.frame_rays : 0u;
@@ -910,35 +869,14 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
         trace_rest<false, QUADS, true>(sc, o, d, h, t.disc);
         if constexpr (QUADS) other_trace<false>(sc, o, d, 0.0, h, t.disc, t.tests, t.boxes);
         if constexpr (LANE == 14) {
-#ifdef RTAMD_EXP_DUP_TRAV
-          Hit h2 = h;  // (the planes' hit, as the walk below starts from)
-#endif
           lane_trace_pair<false>(ls.nodes, ls.s48, ls.M, sc.n_bvh > 0, o, d, 0.0, h, t.disc, t.tests, t.boxes,
                                  ls.stack16);
-#ifdef RTAMD_EXP_DUP_TRAV
-          V3 o2 = o;
-          exp_opaque(o2.x);
-          unsigned u0 = 0, u1 = 0, u2 = 0;
-          lane_trace_pair<false>(ls.nodes, ls.s48, ls.M, sc.n_bvh > 0, o2, d, 0.0, h2, u0, u1, u2, ls.stack16);
-          exp_sink(h2.t);
-#endif
         } else if constexpr (LANE == 15) {
-          lane_trace_wide<false, Sph48, true>((const BvhWide*)ls.nodes, ls.s48, ls.M, sc.n_bvh > 0, o, d, 0.0, h,
+          lane_trace_wide<false, Sph48, true>((const BvhWide*)ls.nodes, ls.s48, ls.M, sc.bvhw != nullptr, o, d, 0.0, h,
                                               t.disc, t.tests, t.boxes, ls.stack16, ls.wtop, ls.n_top, sc.n_diag);
         } else if constexpr (LANE == 4) {
-#ifdef RTAMD_EXP_DUP_TRAV
-          Hit h2 = h;  // (the planes' hit, as the walk below starts from)
-#endif
-          lane_trace_wide<false>((const BvhWide*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, t.disc, t.tests,
+          lane_trace_wide<false>((const BvhWide*)ls.nodes, ls.sd, ls.M, sc.bvhw != nullptr, o, d, 0.0, h, t.disc, t.tests,
                                  t.boxes, ls.stack16, ls.wtop, ls.n_top, sc.n_diag);
-#ifdef RTAMD_EXP_DUP_TRAV
-          V3 o2 = o;
-          exp_opaque(o2.x);
-          unsigned u0 = 0, u1 = 0, u2 = 0;
-          lane_trace_wide<false>((const BvhWide*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o2, d, 0.0, h2, u0, u1, u2,
-                                 ls.stack16, ls.wtop, ls.n_top, sc.n_diag);
-          exp_sink(h2.t);
-#endif
         } else {
           lane_trace<false, LANE == 3>((const BvhNode*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, t.disc,
                                        t.tests, t.boxes, ls.stack, ls.top, ls.n_top);
@@ -947,97 +885,18 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
     }
     hit_finish(h);
   };
-  if constexpr (!COMPACT) {
-    while (c < n_chunks) {
-      unsigned k_next = 0;
-      if (dyn && lane_id() == 0) k_next = atomicAdd(ctr, 1u);
-      const unsigned i = c * 64u + lane_id();
-      // a batch's generation 0: the padding slots after each frame's root rays hold no ray
-      const bool valid = i < a.n && (a.g != 0 || a.n_frames <= 1 || i % a.frame_rays < a.frame_real);
-      const unsigned slot = valid ? shard_slot<true>(pre, a.in_cap, i) : 0u;
-      V3 o = v3(0, 0, 0), d = v3(0, 0, 0);
-      Hit h;
-      traverse(i, valid, slot, o, d, h);
-      shade_fused<LANE, QUADS, CAM>(sc, cam, a, ls, c, slot, valid, o, d, h, t);
-      c = dyn ? c_base + X * (unsigned)__shfl((int)k_next, 0, 64) : c + W;
-    }
-  } else {
-    // the wave's queue (kQueue entries, structure of arrays) after the image
-    const unsigned wv = threadIdx.x >> 6, lane = lane_id();
-    unsigned char* qb = lane_dyn + a.q_off;
-    double* qt = (double*)qb + wv * kQueue;                                        // t
-    unsigned* qs = (unsigned*)(qb + 16 * kQueue * 8) + wv * kQueue;                // slot | hin << 31
-    int* qk = (int*)(qb + 16 * kQueue * 12) + wv * kQueue;                         // key
-    unsigned* qc = (unsigned*)(qb + 16 * kQueue * 16) + wv * kQueue;               // (c1k + 1) | (c2k + 1) << 16
-    unsigned qn = 0;     // queued hits (wave-uniform)
-    unsigned spare = 0;  // a chunk of this wave whose traversal filled no batch
-    for (;;) {
-      const bool have = c < n_chunks;
-      unsigned q_idx;
-      if (have) {
-        unsigned k_next = 0;
-        if (dyn && lane == 0) k_next = atomicAdd(ctr, 1u);
-        const unsigned i = c * 64u + lane;
-        const bool valid = i < a.n && (a.g != 0 || a.n_frames <= 1 || i % a.frame_rays < a.frame_real);
-        const unsigned slot = valid ? shard_slot<true>(pre, a.in_cap, i) : 0u;
-        V3 o = v3(0, 0, 0), d = v3(0, 0, 0);
-        Hit h;
-        traverse(i, valid, slot, o, d, h);
-        const bool hit = valid && h.key >= 0;
-        if (valid && !hit) {  // color_at: a miss is black (world.rs:74-75)
-          double* dst = color_dst<CAM>(a, cam, slot);
-          st_d(dst, 0.0); st_d(dst + 1, 0.0); st_d(dst + 2, 0.0);
-        }
-        const unsigned long long m = __ballot(hit);
-        if (hit) {
-          const unsigned p = qn + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
-          qt[p] = h.t;
-          qs[p] = slot | ((unsigned)h.hin << 31);
-          qk[p] = h.key;
-          qc[p] = (unsigned)(h.c1k + 1) | ((unsigned)(h.c2k + 1) << 16);
-        }
-        qn += (unsigned)__popcll(m);
-        q_idx = c;
-        c = dyn ? c_base + X * (unsigned)__shfl((int)k_next, 0, 64) : c + W;
-        if (qn < 64u) {
-          spare = q_idx;
-          continue;
-        }
-      } else {
-        if (qn == 0) break;
-        q_idx = spare;  // the wave's last, partial batch
-      }
-      // shade the queue's first min(qn, 64) hits, one per lane (the LDS executes a wave's
-      // accesses in order: only the compiler must not reorder them, no fence or wait)
-      asm volatile("" ::: "memory");
-      const unsigned nb = qn < 64u ? qn : 64u;
-      const bool live = lane < nb;
-      Hit h;
-      hit_init(h);
-      unsigned slot = 0;
-      V3 o = v3(0, 0, 0), d = v3(0, 0, 0);
-      if (live) {
-        const unsigned sh = qs[lane];
-        const unsigned cc = qc[lane];
-        slot = sh & 0x7FFFFFFFu;
-        h.t = qt[lane];
-        h.key = qk[lane];
-        h.hin = (int)(sh >> 31);
-        h.c1k = (int)(cc & 0xFFFFu) - 1;
-        h.c2k = (int)(cc >> 16) - 1;
-        wf_ray<CAM>(a, cam, slot, o, d);
-      }
-      // the rest of the queue moves to its front (entries [64, qn) -> [0, qn - 64))
-      const unsigned rest = qn - nb;
-      double rt = 0.0;
-      unsigned rs = 0, rc = 0;
-      int rk = 0;
-      if (lane < rest) { rt = qt[64 + lane]; rs = qs[64 + lane]; rk = qk[64 + lane]; rc = qc[64 + lane]; }
-      asm volatile("" ::: "memory");
-      if (lane < rest) { qt[lane] = rt; qs[lane] = rs; qk[lane] = rk; qc[lane] = rc; }
-      qn = rest;
-      shade_fused<LANE, QUADS, CAM>(sc, cam, a, ls, q_idx, slot, live, o, d, h, t);
-    }
+  while (c < n_chunks) {
+    unsigned k_next = 0;
+    if (dyn && lane_id() == 0) k_next = atomicAdd(ctr, 1u);
+    const unsigned i = c * 64u + lane_id();
+    // a batch's generation 0: the padding slots after each frame's root rays hold no ray
+    const bool valid = i < a.n && (a.g != 0 || a.n_frames <= 1 || i % a.frame_rays < a.frame_real);
+    const unsigned slot = valid ? shard_slot<true>(pre, a.in_cap, i) : 0u;
+    V3 o = v3(0, 0, 0), d = v3(0, 0, 0);
+    Hit h;
+    traverse(i, valid, slot, o, d, h);
+    shade_fused<LANE, QUADS, CAM>(sc, cam, a, ls, c, slot, valid, o, d, h, t);
+    c = dyn ? c_base + X * (unsigned)__shfl((int)k_next, 0, 64) : c + W;
   }
   if constexpr (!TALLY) return;
   const unsigned long long s = wave_sum(t.disc), st = wave_sum(t.tests), sb = wave_sum(t.boxes);
@@ -1139,6 +998,23 @@ __global__ __launch_bounds__(kWfBlock) void wf_combine(DevScene sc, DevCamera ca
 // (device-sized generations). Generation 0's pass, the frame's last, also
 // records the frame's ray count per generation in the workspace's host-mapped
 // record (a.out_cnt: generation 1's ray counters), which sizes later frames.
+// An asynchronous frame whose recursion outgrew the arenas (bind_generation)
+// is incomplete, and it must never look valid in the caller's buffer (the
+// reference's render never returns a partial canvas, camera.rs:133-148): the
+// pass's last launch fills every canvas of the pass (each frame of a batch,
+// `per_frame` outputs of 3 doubles) with NaN instead of colours. The call that
+// finds the overflow (the next on the scene, or rt_scene_check) reports it;
+// synchronous calls render such a frame again before they return.
+__device__ __forceinline__ void poison_frames(const WfArgs& a, double* single, unsigned per_frame) {
+  const unsigned nf = a.n_frames > 1 ? a.n_frames : 1u;
+  const double nan = __builtin_nan("");
+  const size_t n = (size_t)per_frame * 3, stride = (size_t)gridDim.x * blockDim.x;
+  for (unsigned f = 0; f < nf; ++f) {
+    double* o = a.n_frames > 1 ? a.frames->out[f] : single;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) o[i] = nan;
+  }
+}
+
 __global__ __launch_bounds__(kWfBlock) void wf_combine_parents(DevScene sc, DevCamera cam, WfArgs a) {
   const unsigned stride = gridDim.x * blockDim.x;
   __shared__ unsigned s_pre[kPreList];
@@ -1166,6 +1042,10 @@ __global__ __launch_bounds__(kWfBlock) void wf_combine_parents(DevScene sc, DevC
       r->n_gens = a.max_depth + 1;
       r->frames = r->frames + 1;
     }
+  }
+  if (a.g == 0 && a.colors_direct && a.cnt->overflow) {  // (averaged frames: wf_average poisons them)
+    poison_frames(a, a.colors, a.frame_real);
+    return;
   }
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const ParentRec p = parents[shard_slot<false>(pre, sh_cap, i)];
@@ -1195,6 +1075,10 @@ __global__ __launch_bounds__(kWfBlock) void wf_average(WfArgs a, unsigned hsize,
   const unsigned stride = gridDim.x * blockDim.x;
   const unsigned aa = a.aa;
   const unsigned pix_frame = a.n_frames > 1 ? a.frame_real / aa : n_pix;
+  if (a.cnt && a.cnt->overflow) {  // the fast path's pass outgrew its arenas: poison_frames
+    poison_frames(a, out, pix_frame);
+    return;
+  }
   for (unsigned p = blockIdx.x * blockDim.x + threadIdx.x; p < n_pix; p += stride) {
     const unsigned f = p / pix_frame, lp = p - f * pix_frame;
     const size_t s0 = (size_t)f * (a.n_frames > 1 ? a.frame_rays : 0u) + (size_t)lp * aa;
@@ -1569,8 +1453,8 @@ static hipError_t launch_fused_q(const DevScene& sc, const DevCamera& cam, WfArg
   const bool wide_ok = tn.image != 1 && tn.wide && sc.bvhw && wide_stack_bytes(sc) <= kWfLdsLimit / 2;
   // prim_lane 1: any per-lane image; 2 (default): the LDS images only (C3 primary class 0.128 ->
   // 0.125 ms/frame with the LDS four-wide image; C5's global image 2.06 -> 2.16 ms, so not there)
-  const bool lds_img = tn.image == 0 && (pair_lds_bytes(sc) <= kWfLdsLimit ||
-                                         (tn.lds_wide && wide_lds_bytes(sc) + dl <= kWfLdsLimit));
+  const bool wide_lds = sc.bvhw && tn.lds_wide && wide_lds_bytes(sc) + dl <= kWfLdsLimit;
+  const bool lds_img = tn.image == 0 && (pair_lds_bytes(sc) <= kWfLdsLimit || wide_lds);
   const bool lane_prim = tn.prim_lane == 1 ? (lds_img || wide_ok) : tn.prim_lane == 2 ? lds_img : false;
   if (primary && !lane_prim) {
     const size_t room = kWfLdsLimit - (size_t)(kTraceBlock / 64) * (kBvhMaxDepth + 4) * 4;
@@ -1579,7 +1463,7 @@ static hipError_t launch_fused_q(const DevScene& sc, const DevCamera& cam, WfArg
     return launch_lds(wf_trace_fused<true, QUADS, 0, TALLY>, dyn, n, stream, sc, cam, a, tb);
   }
   const bool cam_rays = a.g == 0 && a.camera_mode;  // only generation 0 of a camera render reads camera rays
-  if (tn.image == 0 && tn.lds_wide && wide_lds_bytes(sc) + dl <= kWfLdsLimit) {
+  if (tn.image == 0 && wide_lds) {
     // the four-wide hierarchy and the 48-B sphere records in LDS, with the light buffer's distances
     dyn = wide_lds_bytes(sc);
     if (dl) { a.lds_flags |= kLdsDeltas; dyn += dl; }
@@ -1587,23 +1471,13 @@ static hipError_t launch_fused_q(const DevScene& sc, const DevCamera& cam, WfArg
                     : launch_lds(wf_trace_fused<false, QUADS, 15, TALLY, false>, dyn, n, stream, sc, cam, a, tb);
   }
   if (tn.image == 0 && pair_lds_bytes(sc) <= kWfLdsLimit) {
+    // the pair layout in LDS (scenes whose four-wide image does not fit beside the distances);
+    // the light buffer's distances take what room is left
     dyn = pair_lds_bytes(sc);
-    // compacted shading (the hit queues' 16-bit object codes need n_objects < 16383); the
-    // light buffer's distances take what room is left
-    const size_t qoff = (dyn + 15) & ~(size_t)15;
-    const bool compact = tn.compact && sc.n_objects < 16383 && qoff + kQueueLdsBytes <= kWfLdsLimit;
-    if (compact) {
-      a.q_off = (unsigned)qoff;
-      dyn = qoff + kQueueLdsBytes;
-    }
-    if (dl && dyn + dl <= kWfLdsLimit) {  // (lane_scene stages them right after the image: the queue moves up)
+    if (dl && dyn + dl <= kWfLdsLimit) {
       a.lds_flags |= kLdsDeltas;
-      if (compact) a.q_off = (unsigned)((pair_lds_bytes(sc) + dl + 15) & ~(size_t)15);
       dyn += dl;
     }
-    if (compact)
-      return cam_rays ? launch_lds(wf_trace_fused<false, QUADS, 14, TALLY, true, true>, dyn, n, stream, sc, cam, a, tb)
-                      : launch_lds(wf_trace_fused<false, QUADS, 14, TALLY, false, true>, dyn, n, stream, sc, cam, a, tb);
     return cam_rays ? launch_lds(wf_trace_fused<false, QUADS, 14, TALLY, true>, dyn, n, stream, sc, cam, a, tb)
                     : launch_lds(wf_trace_fused<false, QUADS, 14, TALLY, false>, dyn, n, stream, sc, cam, a, tb);
   }
@@ -1758,7 +1632,24 @@ hipError_t Wavefront::render_fast(const DevScene& sc, const DevCamera& cam, bool
     want_p *= tn.arena_pct / 100.0;
     want_r = std::max(camera_mode ? 0.0 : (double)n0, want_r * tn.arena_pct / 100.0);
   }
-  WF_CHECK(ensure_arenas((unsigned long long)want_c, (unsigned long long)want_p, (unsigned long long)want_r, squeeze));
+  hipError_t ea = ensure_arenas((unsigned long long)want_c, (unsigned long long)want_p, (unsigned long long)want_r,
+                                squeeze);
+  // Sizes guessed before the scene has learned any frame (rho, mu) can exceed what the
+  // device holds (a large canvas, branch 2, deep recursion): halve them down to the
+  // smallest useful arenas. A frame that outgrows them overflows: a synchronous call
+  // renders it again with the arenas grown, an asynchronous one is poisoned (NaN) and
+  // reported (poison_frames, rt_scene_check).
+  const double floor_c = (double)n0 + min_region * D, floor_p = min_region / 2.0 * D;
+  const double floor_r = std::max(camera_mode ? 0.0 : (double)n0, min_region);
+  for (int k = 0; ea == hipErrorOutOfMemory && k < 16 && (want_c > floor_c || want_p > floor_p || want_r > floor_r);
+       ++k) {
+    (void)hipGetLastError();
+    want_c = std::max(floor_c, want_c / 2.0);
+    want_p = std::max(floor_p, want_p / 2.0);
+    want_r = std::max(floor_r, want_r / 2.0);
+    ea = ensure_arenas((unsigned long long)want_c, (unsigned long long)want_p, (unsigned long long)want_r, true);
+  }
+  WF_CHECK(ea);
   if (!camera_mode)  // batch rays: n0 x 6 doubles -> generation 0's ray buffer
     WF_CHECK(hipMemcpy2DAsync(rays_[0], sizeof(WfRay), d_in_rays, 6 * sizeof(double), 6 * sizeof(double), n0,
                               hipMemcpyDeviceToDevice, stream));
@@ -1825,6 +1716,7 @@ hipError_t Wavefront::render_fast(const DevScene& sc, const DevCamera& cam, bool
     WfArgs v{};
     v.aa = aa; v.rows = frame_real / aa / cam.hsize;
     v.n_frames = n_frames; v.frame_rays = n0 / n_frames; v.frame_real = frame_real; v.frames = d_frames_;
+    v.cnt = d_cnt_;
     WF_LAUNCH(wf_average, dim3(occupancy_grid(wf_average, kWfBlock, 0, n_pix)), dim3(kWfBlock), 0, stream, v,
               cam.hsize, colors_, n_pix, d_out);
     WF_CHECK(hipGetLastError());

@@ -100,8 +100,6 @@ struct WfTuning {
   int treelet_deltas = 1;  // ... after the light buffer's distances (when they fit)
   int shadow_stream = 1;   // exhaustive pipeline: 1 = shadow traces on a second stream when rendering alone
   int adaptive_block = 0;  // generation pipeline: 1 = small trace launches spread over every CU
-  int compact = 0;         // fast path, pair image: 1 = compacted shading (hit queues in LDS, full-width shading;
-                           //     measured slower on C3, DESIGN.md "Compacted shading")
   int prim_lane = 2;       // fast path: primary rays by the per-lane walk instead of the wave traversal with
                            //     shared-origin records: 1 = over any image, 2 = over the LDS images only, 0 = never
   int arena_pct = 100;     // test hook: the fast path's queue arenas sized to this percentage of the hint,
@@ -139,6 +137,9 @@ constexpr int kChunkStride = 32;
 struct WfCounters {
   unsigned chunk[kMaxGen * kChunkClasses * kChunkStride];
   unsigned n_refl[kMaxGen], n_refr[kMaxGen], n_hit[kMaxGen];
+  // this pass (frame or batch) outgrew its arenas (bind_generation): its
+  // canvases are filled with NaN by the last launch (poison_frames)
+  unsigned overflow;
   WfWorkRow work[kWorkRows];
   unsigned long long disc(int c) const {
     unsigned long long t = 0;
@@ -281,12 +282,7 @@ struct WfArgs {
   ParentRec* par_base;
   unsigned long long color_cap, par_cap, ray_cap;  // colour slots, parent records, ray slots per buffer
   WfHostRec* hrec;                  // device address of the workspace's host-mapped record
-  unsigned q_off;                   // compacted shading (LANE 14): the waves' hit queues in dynamic LDS
 };
-// compacted shading: entries of a wave's hit queue (t, slot | hin, key, c1k / c2k: 20 B each);
-// it holds at most 63 left from the last batch + one chunk's 64 hits
-constexpr unsigned kQueue = 127;
-constexpr size_t kQueueLdsBytes = (size_t)16 * kQueue * 20;  // the block's 16 waves
 
 // Per-kernel-class timing of the last frame (profiling mode only).
 enum WfClass { WF_PRIMARY = 0, WF_CLOSEST = 1, WF_SHADOW = 2, WF_PREP = 3, WF_COMBINE = 4, WF_NCLASS = 5 };

@@ -242,12 +242,12 @@ def test_skipped_shadow_rays_bitwise(rt, neg_zero):
     assert full.to_numpy().tobytes() == exact.to_numpy().tobytes()
 
 
-@pytest.mark.parametrize("image,shadow_lb,compact,wide,lds_wide", [
-    (0, 1, 1, 1, 0), (0, 0, 1, 1, 0), (0, 1, 0, 1, 0), (0, 0, 0, 1, 0), (0, 1, 0, 1, 1), (0, 0, 0, 1, 1),
-    (3, 1, 0, 1, 0), (3, 0, 0, 1, 0), (3, 1, 0, 0, 0), (3, 0, 0, 0, 0), (1, 1, 0, 1, 0), (1, 0, 0, 1, 0)])
-def test_fused_images_bitwise(rt, image, shadow_lb, compact, wide, lds_wide):
+@pytest.mark.parametrize("image,shadow_lb,wide,lds_wide", [
+    (0, 1, 1, 0), (0, 0, 1, 0), (0, 1, 1, 1), (0, 0, 1, 1),
+    (3, 1, 1, 0), (3, 0, 1, 0), (3, 1, 0, 0), (3, 0, 0, 0), (1, 1, 1, 0), (1, 0, 1, 0)])
+def test_fused_images_bitwise(rt, image, shadow_lb, wide, lds_wide):
     """Every scene image of the fast-path kernels (pair layout in LDS, the
-    default, with and without compacted shading / nodes and records in global
+    four-wide hierarchy in LDS (the default), nodes and records in global
     memory: the four-wide hierarchy (wide) or the binary one with an LDS stack /
     with a scratch stack), with shadow rays through the light buffer or through
     the BVH, gives the exhaustive frame. The scenes above that do not fit in LDS
@@ -256,7 +256,6 @@ def test_fused_images_bitwise(rt, image, shadow_lb, compact, wide, lds_wide):
     exact, _ = cam.render(w, depth, want_stats=True)
     w.tune("image", image)
     w.tune("shadow_lb", shadow_lb)
-    w.tune("compact", compact)
     w.tune("wide", wide)
     w.tune("lds_wide", lds_wide)
     try:
@@ -267,7 +266,6 @@ def test_fused_images_bitwise(rt, image, shadow_lb, compact, wide, lds_wide):
     finally:
         w.tune("image", 0)
         w.tune("shadow_lb", 1)
-        w.tune("compact", 0)
         w.tune("wide", 1)
         w.tune("lds_wide", 1)
     assert fast.to_numpy().tobytes() == exact.to_numpy().tobytes()

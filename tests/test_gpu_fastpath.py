@@ -172,9 +172,10 @@ def test_arena_overflow_sync_rerenders_async_reports(rt):
     the hint (test hook arena_pct):
     - a synchronous render (rt_render to a host canvas) notices it, grows the
       arenas and renders again: its frame is complete;
-    - an asynchronous render (rt_render_shard_device) leaves an incomplete
-      frame, which rt_scene_check (or the next call) reports; the arenas have
-      grown, so the next frame is complete."""
+    - an asynchronous render (rt_render_shard_device) cannot finish the frame:
+      its canvas is filled with NaN on the device (never a partial frame that
+      looks valid, camera.rs:133-148), and rt_scene_check (or the next call)
+      reports it; the arenas have grown, so the next frame is complete."""
     import torch
     from rtamd import scenes
     w, cam, depth = scenes.c3(96, 54, n_spheres=200)
@@ -193,7 +194,7 @@ def test_arena_overflow_sync_rerenders_async_reports(rt):
         torch.cuda.synchronize()
     finally:
         w.tune("arena_pct", 100)
-    assert not torch.equal(buf, exact)  # incomplete: the children of an overflowing generation were dropped
+    assert _valid_or_poisoned(buf, exact) == "poisoned"
     with pytest.raises(rt.RtError, match="overflow"):
         w.check()
     cam.render_shard_device(w, depth, 8, 0, 1, buf.data_ptr(), st.cuda_stream, False)
@@ -293,3 +294,59 @@ def test_fast_path_variants_bitwise(rt, knob, value, image):
     finally:
         w.tune(knob, 2)  # (the default: the per-lane walk for primary rays over the LDS images)
         w.tune("image", 0)
+
+
+def _valid_or_poisoned(buf, exact):
+    """An asynchronous frame is either complete (bitwise the exhaustive frame)
+    or entirely NaN (it outgrew its queue arenas); anything else fails."""
+    import torch
+    if torch.equal(buf, exact):
+        return "complete"
+    assert bool(torch.isnan(buf).all()), "an incomplete frame that is not poisoned"
+    return "poisoned"
+
+
+@pytest.mark.parametrize("aa", [1, 4])
+def test_arena_overflow_batch_poisoned(rt, aa):
+    """rt_render_frames_device (batches) with forced overflows (arena_pct): every
+    frame of an overflowing pass is all NaN, never a partial canvas, for plain
+    and AA frames (wf_average); the overflow is reported once; after it the
+    arenas fit and the same batch renders every frame bitwise. With arenas at
+    60 % of the hint a pass may or may not fit: each frame is still either
+    complete or poisoned."""
+    import torch
+    from rtamd import scenes
+    w, cam, depth = scenes.c3(128, 72, n_spheres=300)
+    exact = torch.empty((72, 128, 3), dtype=torch.float64, device="cuda")
+    cam.render_shard_device(w, depth, 8, 0, 1, exact.data_ptr(), torch.cuda.current_stream().cuda_stream, True,
+                            exhaustive=True, aa_samples=aa)
+    torch.cuda.synchronize()
+    st = rt.render_stream(False)
+    bufs = [torch.full_like(exact, -1.0) for _ in range(5)]
+
+    def batch():
+        rt.render_frames_device(w, [cam] * len(bufs), depth, 8, 0, 1, [b.data_ptr() for b in bufs], st.cuda_stream,
+                                False, aa)
+        torch.cuda.synchronize()
+    batch()  # learn the scene's sizes
+    w.check()
+    for pct, want in ((2, "poisoned"), (60, None)):
+        w.tune("arena_pct", pct)
+        try:
+            for b in bufs:
+                b.fill_(-1.0)
+            batch()
+        finally:
+            w.tune("arena_pct", 100)
+        kinds = {_valid_or_poisoned(b, exact) for b in bufs}
+        assert len(kinds) == 1  # one pass: all its frames complete, or all poisoned
+        if want:
+            assert kinds == {want}
+        if kinds == {"poisoned"}:
+            with pytest.raises(rt.RtError, match="overflow"):
+                w.check()
+        w.check()  # reported once
+        batch()
+        w.check()
+        for b in bufs:
+            assert torch.equal(b, exact)

@@ -1,0 +1,217 @@
+"""Round-5 measurement probe (dev tool, one GPU).
+
+Sections (--what, comma separated):
+  e2e       the drop-in entry point (rt_render -> host Canvas, camera.rs:133-148):
+            one frame's render alone, the 49.8 MB device-to-host copy alone, rt_render
+            as shipped, and row bands rendered on two streams with each band's copy
+            queued behind its render (the overlap the banded rt_render would get)
+  assembly  rank 0's budget at N = 8 on C3 (rtamd.distributed): the
+            un-interleave of a 16-frame batch, rank 0's shard (7/8) and a full shard
+            (6/8) rendered alone in the bench's regime (batches of 16 on 4 streams), and
+            rank 0's shard with an emulated receive stream (7 x 6.27 MB per frame
+            written into its gather buffer by a copy on a side stream) plus the
+            un-interleave behind each batch
+  pow       channels of the fast frame that differ from the oracle (material.rs:76
+            powf vs the device pow) on 4096 C3 and 2048 C5 pixels, and how close
+            any channel's v*255 comes to a .5 rounding boundary of the PPM quantiser
+Prints one JSON object per section.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "raytracer-challenge-rs_amd")]
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import rtamd  # noqa: E402
+from rtamd import scenes  # noqa: E402
+from rtamd.distributed import StreamFrameAssembler  # noqa: E402
+
+
+def sync():
+    torch.cuda.synchronize()
+
+
+def timeit(fn, reps):
+    fn()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    sync()
+    return (time.perf_counter() - t0) / reps * 1e3
+
+
+def e2e(reps):
+    w, cam, depth = scenes.c3()
+    w.upload(0)
+    H, W = cam.vsize, cam.hsize
+    dev = torch.empty((H, W, 3), dtype=torch.float64, device="cuda")
+    host = torch.empty((H, W, 3), dtype=torch.float64).pin_memory()
+    s0 = torch.cuda.current_stream()
+    out = {}
+    out["render_only_ms"] = timeit(lambda: cam.render_shard_device(w, depth, 8, 0, 1, dev.data_ptr(), s0.cuda_stream,
+                                                                   False), reps)
+    out["d2h_only_ms"] = timeit(lambda: host.copy_(dev, non_blocking=True), reps)
+    out["d2h_GBps"] = dev.numel() * 8 / out["d2h_only_ms"] / 1e6
+    ts = []
+    cam.render(w, depth, want_stats=False)
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        cam.render(w, depth, want_stats=False)
+        ts.append((time.perf_counter() - t0) * 1e3)
+    out["rt_render_ms"] = ts
+    ref = dev.clone()
+    streams = [rtamd.render_stream(False) for _ in range(2)]
+    for K in (2, 3, 4, 6, 8):
+        rb = (H + K - 1) // K
+
+        def banded():
+            for k in range(K):
+                y0 = k * rb
+                y1 = min(H, y0 + rb)
+                st = streams[k % 2]
+                cam.render_shard_device(w, depth, rb, k, K, dev[y0:y1].data_ptr(), st.cuda_stream, False)
+                with torch.cuda.stream(st):
+                    host[y0:y1].copy_(dev[y0:y1], non_blocking=True)
+        out[f"banded_{K}_ms"] = timeit(banded, reps)
+    dev.fill_(-1)
+    banded()
+    sync()
+    out["banded_bitwise"] = bool(torch.equal(host, ref.cpu()))
+    # bands on streams of descending priority: the first band gets the CUs first, so it
+    # finishes early and its copy overlaps the later bands' renders
+    lo, hi = torch.cuda.Stream.priority_range()
+    out["priority_range"] = [lo, hi]
+    pstreams = [torch.cuda.Stream(priority=p) for p in sorted({hi, (lo + hi) // 2, lo})]
+    out["stream_priorities"] = [s.priority for s in pstreams]
+    for K in (2, 3, 4):
+        rb = (H + K - 1) // K
+        for mode in ("prio", "stagger"):
+            evs = [torch.cuda.Event() for _ in range(K)]
+
+            def pbanded():
+                for k in range(K):
+                    y0 = k * rb
+                    y1 = min(H, y0 + rb)
+                    st = pstreams[min(k, len(pstreams) - 1)] if mode == "prio" else streams[k % 2]
+                    if mode == "stagger" and k > 0:
+                        st.wait_event(evs[k - 1])  # band k starts when band k-1's render is done
+                    cam.render_shard_device(w, depth, rb, k, K, dev[y0:y1].data_ptr(), st.cuda_stream, False)
+                    evs[k].record(st)
+                    with torch.cuda.stream(st):
+                        host[y0:y1].copy_(dev[y0:y1], non_blocking=True)
+            out[f"{mode}_{K}_ms"] = timeit(pbanded, reps)
+            dev.fill_(-1)
+            pbanded()
+            sync()
+            out[f"{mode}_{K}_bitwise"] = bool(torch.equal(host, ref.cpu()))
+    for K in (2, 3, 4):  # one band alone (render only), for the model
+        rb = (H + K - 1) // K
+        out[f"band_1of{K}_render_ms"] = timeit(
+            lambda: cam.render_shard_device(w, depth, rb, 0, K, dev.data_ptr(), s0.cuda_stream, False), reps)
+    return out
+
+
+def assembly(reps):
+    w, cam, depth = scenes.c3()
+    w.upload(0)
+    w.tune("shadow_stream", 0)
+    H, W, B, N, NB, F = cam.vsize, cam.hsize, 8, 8, 16, 4
+    out = {"config": "C3 1920x1080, N=8, 8-row blocks, batches of 16 on 4 streams"}
+    fa = StreamFrameAssembler(H, W, B, 0, N, torch.device("cuda", 0), slots=F, batch=NB)
+    gb, cv = fa.gather_buf[0], fa.canvas[0]
+    out["gather_buf_MB"] = gb.numel() * 8 / 1e6
+    out["unweave_batch_ms"] = timeit(lambda: torch.index_select(gb, 0, fa.inv_batch, out=cv), reps)
+    out["unweave_per_frame_ms"] = out["unweave_batch_ms"] / NB
+    rstreams = [rtamd.render_stream(False) for _ in range(F)]
+    rx_stream = torch.cuda.Stream()
+    shards = {}
+    for shard in (7, 6):
+        rows = rtamd.shard_rows(H, B, shard, N)
+        shards[shard] = [torch.empty((NB, rows, W, 3), dtype=torch.float64, device="cuda") for _ in range(F)]
+    peers = torch.empty((N - 1, NB * fa.max_rows, W, 3), dtype=torch.float64, device="cuda")
+    frames = 64
+
+    def run(shard, rx=False, unweave=False):
+        for b in range(frames // NB):
+            k = b % F
+            rs = rstreams[k]
+            rtamd.render_frames_device(w, [cam] * NB, depth, B, shard, N,
+                                       [shards[shard][k][j].data_ptr() for j in range(NB)], rs.cuda_stream)
+            if rx:  # the 7 peers' shards of this batch land in the gather buffer (43.9 MB per frame)
+                with torch.cuda.stream(rx_stream):
+                    fa.gather_buf[k][fa.max_rows * NB:].copy_(peers.view(-1, W, 3), non_blocking=True)
+                rs.wait_stream(rx_stream)
+            if unweave:
+                with torch.cuda.stream(rs):
+                    torch.index_select(fa.gather_buf[k], 0, fa.inv_batch, out=fa.canvas[k])
+
+    for label, shard, rx, uw in (("render_shard7", 7, False, False), ("render_shard6", 6, False, False),
+                                 ("shard7_rx", 7, True, False), ("shard7_rx_unweave", 7, True, True),
+                                 ("shard7_unweave", 7, False, True)):
+        out[label + "_ms_per_frame"] = timeit(lambda: run(shard, rx, uw), max(1, reps // 2)) / frames
+    out["rx_copy_alone_ms_per_frame"] = timeit(
+        lambda: fa.gather_buf[0][fa.max_rows * NB:].copy_(peers.view(-1, W, 3)), reps) / NB
+    out["whole_frame_ms"] = None
+    whole = [torch.empty((H, W, 3), dtype=torch.float64, device="cuda") for _ in range(8 * F)]
+
+    def run_whole():
+        for b in range(frames // 8):
+            k = b % F
+            rtamd.render_frames_device(w, [cam] * 8, depth, B, 0, 1, [whole[k * 8 + j].data_ptr() for j in range(8)],
+                                       rstreams[k].cuda_stream)
+    out["whole_frame_ms"] = timeit(run_whole, max(1, reps // 2)) / frames
+    return out
+
+
+def pow_ulps():
+    from oracle import pyoracle
+    out = {}
+    nthreads = 16
+    for name, n, seed in (("c3", 4096, 3), ("c5", 2048, 5)):
+        w, cam, depth = getattr(scenes, name)()
+        buf = torch.empty((cam.vsize, cam.hsize, 3), dtype=torch.float64, device="cuda")
+        cam.render_shard_device(w, depth, 8, 0, 1, buf.data_ptr(), torch.cuda.current_stream().cuda_stream, False)
+        sync()
+        rng = np.random.default_rng(seed)
+        xy = np.stack([rng.integers(0, cam.hsize, n), rng.integers(0, cam.vsize, n)], 1)
+        ow = pyoracle.OracleWorld.from_world(w)
+        ref, _ = ow.render_pixels(cam.desc_bytes(), depth, xy, nthreads)
+        got = buf[xy[:, 1], xy[:, 0]].cpu().numpy()
+        d = got - ref
+        ulps = np.abs(got.view(np.int64) - ref.view(np.int64))
+        s = ref * 255.0
+        dist = np.abs(s - np.floor(s) - 0.5)  # distance of v*255 from the nearest .5 (quantiser boundary)
+        diff = d != 0
+        out[name] = {"pixels": n, "channels": int(d.size), "channels_differ": int(diff.sum()),
+                     "differing_min_dist_to_half_of_v255": float(dist[diff].min()) if diff.any() else None,
+                     "max_abs_delta": float(np.abs(d).max()), "max_ulps": int(ulps.max()),
+                     "min_dist_to_half_of_v255": float(dist.min()),
+                     "ppm_same": rtamd.canvas_to_ppm(got[None]) == pyoracle.canvas_to_ppm(ref[None])}
+        del buf
+        torch.cuda.empty_cache()
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--what", default="e2e,assembly,pow")
+    ap.add_argument("--reps", type=int, default=10)
+    a = ap.parse_args()
+    for what in a.what.split(","):
+        t0 = time.perf_counter()
+        res = {"e2e": lambda: e2e(a.reps), "assembly": lambda: assembly(a.reps), "pow": pow_ulps}[what]()
+        res["section"] = what
+        res["seconds"] = round(time.perf_counter() - t0, 1)
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
