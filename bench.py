@@ -95,7 +95,8 @@ import torch.distributed as dist  # noqa: E402
 
 import rtamd  # noqa: E402
 from rtamd import scenes  # noqa: E402
-from rtamd.distributed import FrameAssembler, RcclStreamAssembler, StreamFrameAssembler, shard_of  # noqa: E402
+from rtamd.distributed import (FrameAssembler, RcclStreamAssembler, StreamFrameAssembler, block_patterns,  # noqa: E402
+                               root_share_default, shard_of)
 
 WF_CLOSEST = 1  # kernel class index (csrc/rt_wavefront.hpp WfClass)
 METRIC = "Mrays/s (primary+secondary) on 1920×1080/1000-sphere/depth-5; 1→8 GPU scaling"
@@ -143,6 +144,10 @@ def parse():
                    help="render streams: library-made plain (raw), library-made CU-masked (cumask), torch")
     p.add_argument("--fake-shard", default=None,
                    help="dev: r/n renders only rank r's rows of an n-way split on this one process (no gather)")
+    p.add_argument("--root-share", type=float, default=None,
+                   help="N GPUs: rank 0 (which also assembles every frame) renders this fraction of an equal row "
+                        "share, through block patterns (rt_render_block_pattern_device); default: measured per "
+                        "config and N (rtamd.distributed.root_share_default); 1 = the plain interleave")
     p.add_argument("--verify", action="store_true",
                    help="dev: check the last assembled frame against a one-GPU render of the whole frame")
     p.add_argument("--dist-backend", default="nccl", help="dev: torch.distributed backend (nccl = RCCL)")
@@ -349,8 +354,15 @@ def main():
         sys.exit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE {world_size}")
     n = world_size
     srank, sn = shard_of(rank, n), n  # the shard this process renders (rank 0 assembles: the smallest)
+    prank, pn = rank, n  # the rank whose rows this process renders (pattern mode)
     if a.fake_shard:
-        srank, sn = (int(x) for x in a.fake_shard.split("/"))
+        prank, pn = (int(x) for x in a.fake_shard.split("/"))
+        srank, sn = shard_of(prank, pn), pn
+    # rank 0 receives and un-interleaves every frame: with a share below 1 it renders fewer
+    # row blocks than the others (block patterns, DESIGN.md §6, profiles/r05_assembly_n8.txt)
+    share = a.root_share if a.root_share is not None else root_share_default(a.config, pn)
+    pattern = block_patterns(pn, share) if pn > 1 and share < 1.0 else None
+    my_mask = pattern[1][prank] if pattern else None
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if n > 1:
@@ -371,6 +383,16 @@ def main():
     if a.exhaustive:
         world.tune("accel", 0)
     W, H, B = cam.hsize, cam.vsize, a.row_block
+
+    def render(cams, ptrs, stream_handle, want_stats=False, exhaustive=False):
+        """This rank's rows of the frames `cams` into the device buffers `ptrs`."""
+        if pattern:
+            return rtamd.render_block_pattern_device(world, cams, depth, B, pattern[0], my_mask, ptrs, stream_handle,
+                                                     want_stats, 1, exhaustive)
+        if len(cams) == 1:
+            return cams[0].render_shard_device(world, depth, B, srank, sn, ptrs[0], stream_handle, want_stats,
+                                               exhaustive=exhaustive)
+        return rtamd.render_frames_device(world, cams, depth, B, srank, sn, ptrs, stream_handle)
     # Batches of NB frames (one rt_render_frames_device call: every launch of the
     # pipeline carries the NB frames; DESIGN.md §5.7) on F streams: batch b renders on
     # stream b % F (the library keeps one workspace per stream, so the batches overlap
@@ -408,7 +430,7 @@ def main():
     fa = None
     if n > 1 and a.assembler == "rccl" and F > 1:
         try:
-            fa = RcclStreamAssembler(H, W, B, rank, n, dev, streams=rstreams, batch=NB)
+            fa = RcclStreamAssembler(H, W, B, rank, n, dev, streams=rstreams, batch=NB, pattern=pattern)
         except Exception as e:  # fall back to the torch process groups
             print(f"warning: RCCL stream assembler unavailable ({e}); using per-stream process groups",
                   file=sys.stderr, flush=True)
@@ -418,10 +440,13 @@ def main():
     elif per_stream:
         groups = [dist.new_group(list(range(n))) for _ in range(F)]
         fa = StreamFrameAssembler(H, W, B, rank, n, dev, streams=rstreams if F > 1 else None, groups=groups,
-                                  slots=F, batch=NB)
+                                  slots=F, batch=NB, pattern=pattern)
     else:
-        fa = FrameAssembler(H, W, B, rank, n, dev, slots=F * NB if not events else (F + 1 if F > 1 else 2))
-    assert len(fa.rows) == rtamd.shard_rows(H, B, srank, n)
+        fa = FrameAssembler(H, W, B, rank, n, dev, slots=F * NB if not events else (F + 1 if F > 1 else 2),
+                            pattern=pattern if n > 1 else None)
+    if not a.fake_shard:
+        assert len(fa.rows) == (rtamd.pattern_rows(H, B, pattern[0], my_mask) if pattern
+                                else rtamd.shard_rows(H, B, srank, n))
     shard = fa.shard
     free_ev = [None] * len(fa.shards)
     frame_no = [0]
@@ -441,11 +466,7 @@ def main():
         if not events:
             nf = NB if nf is None else nf
             rs = rstreams[(s // NB) % F]
-            if NB == 1:
-                cam.render_shard_device(world, depth, B, srank, sn, fa.slot(s).data_ptr(), rs.cuda_stream, False)
-            else:
-                rtamd.render_frames_device(world, [cam] * nf, depth, B, srank, sn,
-                                           [fa.slot(s + j).data_ptr() for j in range(nf)], rs.cuda_stream)
+            render([cam] * nf, [fa.slot(s + j).data_ptr() for j in range(nf)], rs.cuda_stream)
             if a.emulate_gather:
                 k = s % F
                 gs = gstreams[k]
@@ -466,7 +487,7 @@ def main():
         slot = s % len(fa.shards)
         if rs is not stream and free_ev[slot] is not None:
             rs.wait_event(free_ev[slot])
-        cam.render_shard_device(world, depth, B, srank, sn, fa.slot(s).data_ptr(), rs.cuda_stream, False)
+        render([cam], [fa.slot(s).data_ptr()], rs.cuda_stream)
         if rs is not stream:
             stream.wait_stream(rs)
         fa.submit(s)
@@ -486,8 +507,7 @@ def main():
 
     # exact work counters of one frame (deterministic), from a counted warm-up launch
     # (this first launch also sizes the wavefront queues of this camera/shard)
-    st = cam.render_shard_device(world, depth, B, srank, sn, shard.data_ptr(), stream.cuda_stream, True,
-                                 exhaustive=True)
+    st = render([cam], [shard.data_ptr()], stream.cuda_stream, True, exhaustive=True)
     assert st["exhaustive"]
     # the exhaustive frame (the reference's every-shape loop) that the timed fast-path frames must equal
     ref_shard = shard.clone()
@@ -553,18 +573,13 @@ def main():
     rtamd._rtamd._wf_profile(world, 1, False)
     for s0 in range(0, a.steps, NB):
         nf = min(NB, a.steps - s0)
-        if NB == 1:
-            cam.render_shard_device(world, depth, B, srank, sn, shard.data_ptr(), stream.cuda_stream, False)
-        else:
-            rtamd.render_frames_device(world, [cam] * nf, depth, B, srank, sn, [b.data_ptr() for b in sbufs[:nf]],
-                                       stream.cuda_stream)
+        render([cam] * nf, [b.data_ptr() for b in sbufs[:nf]], stream.cuda_stream)
     torch.cuda.synchronize()
     del sbufs
     rtamd._rtamd._wf_profile(world, 0, False)
     # the fast path's own counters (what the kernels executed and traced), one counted
     # frame on the same workspace: the timed and profiled kernels do not count
-    fst = cam.render_shard_device(world, depth, B, srank, sn, shard.data_ptr(), stream.cuda_stream, True,
-                                  exhaustive=False)
+    fst = render([cam], [shard.data_ptr()], stream.cuda_stream, True, exhaustive=False)
     breakdown = rtamd._rtamd._wf_profile(world, -1, True)  # class times of the profiled frames, counters of the counted one
     prof = breakdown
     if a.verify and rank == 0:  # dev: the assembled last frame equals a one-GPU render of the whole frame
@@ -612,9 +627,12 @@ def main():
                              f"2 lights, reflect+refract depth {depth}"),
                 "width": W, "height": H, "spheres": a.spheres, "depth": depth,
                 "rays_per_frame": int(rays_per_frame),
-                "parallelism": (f"{n} GPUs, one process each: interleaved {B}-row blocks, one gather per batch to "
-                                f"rank 0 ({gather_desc})" if n > 1 else "1 GPU: wavefront pipeline") +
-                               f"; batches of {NB} frames on {F} streams",
+                "parallelism": (f"{n} GPUs, one process each: interleaved {B}-row blocks"
+                                + (f" (periods of {pattern[0]} blocks, rank 0 {bin(pattern[1][0]).count('1')} and "
+                                   f"the others {bin(pattern[1][-1]).count('1')} per period)" if pattern else "")
+                                + f", one gather per batch to rank 0 ({gather_desc})" if n > 1
+                                else "1 GPU: wavefront pipeline") + f"; batches of {NB} frames on {F} streams",
+                "root_share": share if n > 1 else None,
                 "frames_in_flight": F * NB,
                 "batch": NB,
                 "render_streams_n": F,

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 5
+#define RT_ABI_VERSION 6
 
 /* ---- status codes ------------------------------------------------------ */
 enum {
@@ -260,6 +260,28 @@ int rt_render_frames_device(const rt_scene* scene, const rt_camera_desc* cameras
 uint32_t rt_shard_rows(uint32_t vsize, uint32_t row_block, uint32_t shard,
                        uint32_t n_shards);
 
+/* (ABI 6) rt_render_frames_device over a block PATTERN instead of an
+ * interleaved shard: the canvas's row blocks (row_block rows each) are dealt
+ * in periods of `period` blocks (1..64), and this render owns the blocks whose
+ * position in their period is a set bit of `mask` (non-zero, below
+ * 2^period). Its rows go to d_out_rgb[f] in increasing y order. A shard
+ * (shard s of n) is the pattern (period n, mask 1 << s); uneven patterns let a
+ * multi-GPU caller give one rank fewer rows than the others (the rank that
+ * also assembles the canvas; rtamd.distributed.block_patterns), as the
+ * reference's render_multithreaded gives its last thread the remainder
+ * (camera.rs:157-172). `flags`: RT_RENDER_*. Asynchronous and deferred errors
+ * as rt_render_frames_device. */
+int rt_render_block_pattern_device(const rt_scene* scene, const rt_camera_desc* cameras,
+                                   uint32_t n_frames, uint32_t max_depth,
+                                   uint32_t aa_samples, uint32_t row_block,
+                                   uint32_t period, uint64_t mask, uint32_t flags,
+                                   double* const* d_out_rgb, void* stream,
+                                   rt_stats* stats);
+
+/* (ABI 6) Number of rows a block pattern owns (0 for an invalid pattern). */
+uint32_t rt_pattern_rows(uint32_t vsize, uint32_t row_block, uint32_t period,
+                         uint64_t mask);
+
 /* `World::color_at(&Ray, remaining)` (world.rs:70-81) for a batch of rays.
  * rays: n*6 doubles (origin xyz, direction xyz); out_rgb: n*3 doubles (host). */
 int rt_color_at_batch(const rt_scene* scene, const double* rays, size_t n,
@@ -343,7 +365,7 @@ const char* rt_last_error(void);
 int rt_abi_version(void);
 int rt_device_count(void);
 
-/* Sizes of the ABI structs as this library was built (ABI 5). A foreign
+/* Sizes of the ABI structs as this library was built (ABI 6). A foreign
  * binding (INTEGRATION.md's Rust `#[repr(C)]` mirrors) asserts its own
  * `size_of` against these before its first call: rt_stats is filled in full
  * (sizeof(rt_stats) bytes) by every entry point that takes one. */
@@ -357,8 +379,12 @@ size_t rt_sizeof_stats(void);       /* 112 */
  * the scene has rendered (DESIGN.md "Device-sized generations"); a frame
  * whose recursion outgrows them is detected on the device, left incomplete,
  * and reported as RT_ERR_HIP by the NEXT call on the scene, or by this one,
- * after the arenas have grown (render that frame again). Synchronous calls
- * never report it: they grow the arenas and render again themselves. Callers
+ * after the arenas have grown (render that frame again). Such a frame never
+ * looks valid: every pixel of its canvas (of every canvas of its batch) is
+ * NaN. Synchronous calls never report it: they grow the arenas and render
+ * again themselves. Until a scene has rendered a frame, the arenas are sized
+ * from default ratios, so a first asynchronous frame of a deeply recursive
+ * scene may be one of these. Callers
  * that render asynchronously call it after their last frame to learn about
  * every frame. RT_OK when all frames were complete. */
 int rt_scene_check(const rt_scene* scene);

@@ -443,6 +443,29 @@ PYBIND11_MODULE(_rtamd, m) {
   }, py::arg("world"), py::arg("cameras"), py::arg("max_depth"), py::arg("row_block"), py::arg("shard"),
      py::arg("n_shards"), py::arg("d_outs"), py::arg("stream") = 0, py::arg("want_stats") = false,
      py::arg("aa_samples") = 1);
+  m.def("pattern_rows", &rt_pattern_rows);
+  m.def("render_block_pattern_device", [](const World& w, std::vector<const Camera*> cams, unsigned max_depth,
+                                          unsigned row_block, unsigned period, uint64_t mask,
+                                          std::vector<uintptr_t> d_outs, uintptr_t stream, bool want_stats,
+                                          unsigned aa_samples, bool exhaustive) {
+    if (cams.size() != d_outs.size()) throw std::invalid_argument("one device buffer per camera");
+    std::vector<rt_camera_desc> descs;
+    for (const Camera* c : cams) descs.push_back(c->desc());
+    std::vector<double*> outs;
+    for (uintptr_t p : d_outs) outs.push_back((double*)p);
+    rt_stats st{};
+    int rc;
+    {
+      py::gil_scoped_release nogil;
+      rc = rt_render_block_pattern_device(w.scene(), descs.data(), (uint32_t)descs.size(), max_depth, aa_samples,
+                                          row_block, period, mask, exhaustive ? RT_RENDER_EXHAUSTIVE : 0u,
+                                          outs.data(), (void*)stream, want_stats ? &st : nullptr);
+    }
+    check(rc, "rt_render_block_pattern_device");
+    return stats_dict(st);
+  }, py::arg("world"), py::arg("cameras"), py::arg("max_depth"), py::arg("row_block"), py::arg("period"),
+     py::arg("mask"), py::arg("d_outs"), py::arg("stream") = 0, py::arg("want_stats") = false,
+     py::arg("aa_samples") = 1, py::arg("exhaustive") = false);
 
   // scene-parser/src/lib.rs: the YAML front-end (C++ restatement)
   py::register_exception<SceneParserError>(m, "SceneParserError");

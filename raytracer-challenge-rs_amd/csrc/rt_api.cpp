@@ -473,7 +473,7 @@ int run_render(rt_scene* s, const DevCamera& cam, const double* d_rays, uint32_t
                hipStream_t stream, DevStats* stats_out = nullptr, float* ms_out = nullptr, uint32_t flags = 0,
                rt_scene::WfSlot** used = nullptr, const FrameTable* batch = nullptr, unsigned n_frames = 1,
                bool sync = false, std::unique_lock<std::mutex>* lk = nullptr, bool count = false,
-               bool keep_pin = false) {
+               bool keep_pin = false, uint32_t blk_period = 0, uint64_t blk_mask = 0) {
   if (max_depth > (uint32_t)kMaxDepth)
     return fail(RT_ERR_INVALID_ARGUMENT, "max_depth > " + std::to_string(kMaxDepth));
   if (!valid_aa(aa)) return fail(RT_ERR_INVALID_ARGUMENT, "aa_samples must be 1, 2, 4, 8 or 16");
@@ -504,7 +504,7 @@ int run_render(rt_scene* s, const DevCamera& cam, const double* d_rays, uint32_t
   for (int attempt = 0;; ++attempt) {
     e = w->wf->render(s->dev, cam, d_rays == nullptr, d_rays, n_tasks, aa, max_depth, row_block, shard, n_shards,
                       d_out, stream, s->sizing, nullptr, nullptr, s->tune, s->wfs.size() == 1, wf_flags, batch,
-                      n_frames);
+                      n_frames, blk_period, blk_mask);
     if (e == hipSuccess) e = hipEventRecord(w->done, stream);
     if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("wavefront render: ") + hipGetErrorString(e));
     if (!sync) break;
@@ -1167,13 +1167,25 @@ int rt_render_shard_device_ex(const rt_scene* scene, const rt_camera_desc* camer
   });
 }
 
-int rt_render_frames_device(const rt_scene* scene, const rt_camera_desc* cameras, uint32_t n_frames,
-                            uint32_t max_depth, uint32_t aa_samples, uint32_t row_block, uint32_t shard,
-                            uint32_t n_shards, double* const* d_out_rgb, void* stream, rt_stats* stats) {
-  return guarded([&]() -> int {
+uint32_t rt_pattern_rows(uint32_t vsize, uint32_t row_block, uint32_t period, uint64_t mask) {
+  if (row_block == 0 || period == 0 || period > 64 || mask == 0 || (period < 64 && (mask >> period) != 0)) return 0;
+  uint32_t rows = 0;
+  for (uint64_t blk = 0; blk * row_block < vsize; ++blk)
+    if ((mask >> (blk % period)) & 1u) rows += std::min<uint32_t>(row_block, vsize - (uint32_t)(blk * row_block));
+  return rows;
+}
+
+namespace {
+// rt_render_frames_device (blk_period 0: shard `shard` of `n_shards`) and
+// rt_render_block_pattern_device (the blocks of a period pattern).
+int render_frames(const rt_scene* scene, const rt_camera_desc* cameras, uint32_t n_frames, uint32_t max_depth,
+                  uint32_t aa_samples, uint32_t row_block, uint32_t shard, uint32_t n_shards, uint32_t blk_period,
+                  uint64_t blk_mask, uint32_t flags, double* const* d_out_rgb, void* stream, rt_stats* stats) {
   if (!scene || (n_frames && (!cameras || !d_out_rgb))) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
   if (row_block == 0 || n_shards == 0 || shard >= n_shards)
     return fail(RT_ERR_INVALID_ARGUMENT, "bad shard specification");
+  if (blk_period && rt_pattern_rows(1u << 30, 1, blk_period, blk_mask) == 0)
+    return fail(RT_ERR_INVALID_ARGUMENT, "bad block pattern (period 1..64, a non-empty mask below 2^period)");
   if (!valid_aa(aa_samples)) return fail(RT_ERR_INVALID_ARGUMENT, "aa_samples must be 1, 2, 4, 8 or 16");
   for (uint32_t f = 0; f < n_frames; ++f) {
     if (!d_out_rgb[f]) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
@@ -1189,7 +1201,8 @@ int rt_render_frames_device(const rt_scene* scene, const rt_camera_desc* cameras
   std::unique_lock<std::mutex> lk(s->mu);
   auto t0 = std::chrono::steady_clock::now();
   RT_DEVICE(s->device);
-  const uint32_t rows = rt_shard_rows(cameras[0].vsize, row_block, shard, n_shards);
+  const uint32_t rows = blk_period ? rt_pattern_rows(cameras[0].vsize, row_block, blk_period, blk_mask)
+                                  : rt_shard_rows(cameras[0].vsize, row_block, shard, n_shards);
   const uint64_t per = (uint64_t)rows * cameras[0].hsize * aa_samples;
   const uint64_t padded = (per + 63) & ~(uint64_t)63;
   if (padded >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "shard too large");
@@ -1197,7 +1210,8 @@ int rt_render_frames_device(const rt_scene* scene, const rt_camera_desc* cameras
   // one pass of the generation pipeline per group of kMaxFrames frames; a
   // render that cannot batch (counted, or a scene without the fast path's
   // hierarchies) goes frame by frame, with the counters summed
-  const bool batch = !stats && s->tune.accel != 0 && (s->dev.n_bvh > 0 || s->dev.n_obvh > 0) && per > 0;
+  const bool batch = !stats && !(flags & RT_RENDER_EXHAUSTIVE) && s->tune.accel != 0 &&
+                     (s->dev.n_bvh > 0 || s->dev.n_obvh > 0) && per > 0;
   DevStats sum{};
   float ms_sum = 0.f;
   // a pass holds at most ~2^25 root rays (16 C3 frames; 2 C5 frames), which bounds the
@@ -1213,8 +1227,8 @@ int rt_render_frames_device(const rt_scene* scene, const rt_camera_desc* cameras
     DevStats ds{};
     float ms = 0.f;
     int rc = run_render(s, tab.cam[0], nullptr, (uint32_t)per, aa_samples, max_depth, row_block, shard, n_shards,
-                        tab.out[0], st, stats ? &ds : nullptr, stats ? &ms : nullptr, 0, nullptr,
-                        nf > 1 ? &tab : nullptr, nf, false, &lk);
+                        tab.out[0], st, stats ? &ds : nullptr, stats ? &ms : nullptr, flags, nullptr,
+                        nf > 1 ? &tab : nullptr, nf, false, &lk, false, false, blk_period, blk_mask);
     if (rc != RT_OK) return rc;
     if (stats) {
       sum.rays_primary += ds.rays_primary; sum.rays_reflect += ds.rays_reflect;
@@ -1231,6 +1245,27 @@ int rt_render_frames_device(const rt_scene* scene, const rt_camera_desc* cameras
   if (stats)
     fill_stats(stats, sum, ms_sum, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
   return RT_OK;
+}
+}  // namespace
+
+int rt_render_frames_device(const rt_scene* scene, const rt_camera_desc* cameras, uint32_t n_frames,
+                            uint32_t max_depth, uint32_t aa_samples, uint32_t row_block, uint32_t shard,
+                            uint32_t n_shards, double* const* d_out_rgb, void* stream, rt_stats* stats) {
+  return guarded([&]() -> int {
+  return render_frames(scene, cameras, n_frames, max_depth, aa_samples, row_block, shard, n_shards, 0, 0, 0,
+                       d_out_rgb, stream, stats);
+  });
+}
+
+int rt_render_block_pattern_device(const rt_scene* scene, const rt_camera_desc* cameras, uint32_t n_frames,
+                                   uint32_t max_depth, uint32_t aa_samples, uint32_t row_block, uint32_t period,
+                                   uint64_t mask, uint32_t flags, double* const* d_out_rgb, void* stream,
+                                   rt_stats* stats) {
+  return guarded([&]() -> int {
+  if (period == 0) return fail(RT_ERR_INVALID_ARGUMENT, "bad block pattern (period 1..64)");
+  if (flags & ~(uint32_t)RT_RENDER_EXHAUSTIVE) return fail(RT_ERR_INVALID_ARGUMENT, "unknown render flags");
+  return render_frames(scene, cameras, n_frames, max_depth, aa_samples, row_block, 0, 1, period, mask, flags,
+                       d_out_rgb, stream, stats);
   });
 }
 

@@ -223,7 +223,19 @@ __device__ __forceinline__ void wf_ray(const WfArgs& a, const DevCamera& cam, un
     uint32_t x, lr, smp;
     gen0_pixel(a.aa, a.rows, cf.hsize, li, x, lr, smp);
     const uint32_t blk = lr / a.row_block, off = lr - blk * a.row_block;
-    const uint32_t y = (blk * a.n_shards + a.shard) * a.row_block + off;
+    uint32_t gb = blk * a.n_shards + a.shard;  // the canvas block of local block blk
+    if (a.blk_period) {  // a block pattern: the j-th set bit of the mask in period k
+      unsigned long long m = a.blk_mask;
+      const uint32_t per = (uint32_t)__popcll(m), k = blk / per;
+      uint32_t j = blk - k * per, pos = 0;
+#pragma unroll
+      for (uint32_t w = 32; w >= 1; w >>= 1) {
+        const uint32_t c = (uint32_t)__popcll(m & ((1ull << w) - 1ull));
+        if (j >= c) { j -= c; m >>= w; pos += w; }
+      }
+      gb = k * a.blk_period + pos;
+    }
+    const uint32_t y = gb * a.row_block + off;
     if (a.aa == 1) {
       ray_for_pixel(cf, x, y, o, d);
     } else {
@@ -1522,8 +1534,13 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
                              unsigned n0, unsigned aa, unsigned max_depth, unsigned row_block, unsigned shard,
                              unsigned n_shards, double* d_out, hipStream_t stream, WfSizing& sz, DevStats* stats,
                              float* ms_kernel, const WfTuning& tn, bool solo, unsigned flags,
-                             const FrameTable* batch, unsigned n_frames) {
+                             const FrameTable* batch, unsigned n_frames, unsigned blk_period,
+                             unsigned long long blk_mask) {
   if (max_depth + 2 > (unsigned)kMaxGen) return hipErrorInvalidValue;
+  if (blk_period > 64 || (blk_period && (blk_mask == 0 || (blk_period < 64 && (blk_mask >> blk_period) != 0))))
+    return hipErrorInvalidValue;
+  blk_period_ = blk_period;
+  blk_mask_ = blk_period ? blk_mask : 0ull;
   if (aa == 0 || aa > 16 || (aa & (aa - 1)) != 0 || (!camera_mode && aa != 1) || n0 % aa != 0)
     return hipErrorInvalidValue;
   if (n_frames == 0 || n_frames > kMaxFrames || (n_frames > 1 && !batch)) return hipErrorInvalidValue;
@@ -1674,6 +1691,7 @@ hipError_t Wavefront::render_fast(const DevScene& sc, const DevCamera& cam, bool
   a.max_depth = max_depth;
   a.camera_mode = camera_mode ? 1u : 0u;
   a.row_block = row_block; a.shard = shard; a.n_shards = n_shards;
+  a.blk_period = blk_period_; a.blk_mask = blk_mask_;
   a.skip_shadow = skip_shadow ? 1u : 0u;
   a.count = count ? 1u : 0u;
   a.use_lb = (tn.shadow_lb && sc.lb_cells) ? 1u : 0u;
@@ -1801,6 +1819,7 @@ hipError_t Wavefront::render_exhaustive(const DevScene& sc, const DevCamera& cam
     a.g = g; a.max_depth = max_depth;
     a.camera_mode = camera_mode ? 1u : 0u;
     a.row_block = row_block; a.shard = shard; a.n_shards = n_shards;
+    a.blk_period = blk_period_; a.blk_mask = blk_mask_;
     a.skip_shadow = skip_shadow ? 1u : 0u;
     a.count = count ? 1u : 0u;
     // 1. closest hit
@@ -1871,6 +1890,7 @@ hipError_t Wavefront::render_exhaustive(const DevScene& sc, const DevCamera& cam
     a.g = (unsigned)g; a.max_depth = max_depth;
     a.camera_mode = camera_mode ? 1u : 0u;
     a.row_block = row_block; a.shard = shard; a.n_shards = n_shards;
+    a.blk_period = blk_period_; a.blk_mask = blk_mask_;
     if (a.n == 0) continue;
     WF_CHECK(pmark(stream, WF_COMBINE, true));
     WF_LAUNCH(wf_combine, dim3(occupancy_grid(wf_combine, kWfBlock, 0, a.n)), dim3(kWfBlock), 0, stream, sc, cam, a);

@@ -252,6 +252,13 @@ struct WfArgs {
   unsigned g, max_depth;
   unsigned camera_mode; // g == 0 rays come from the camera (1) or from `rays` (0)
   unsigned row_block, shard, n_shards;
+  // a block-pattern render (rt_render_block_pattern_device): the canvas's row
+  // blocks are dealt in periods of blk_period blocks, of which this render owns
+  // the positions set in blk_mask; its local block i is canvas block
+  // (i / popcount(mask)) * period + the (i mod popcount(mask))-th set bit.
+  // blk_period 0: the interleaved shard (block b -> shard b mod n_shards).
+  unsigned long long blk_mask;
+  unsigned blk_period;
   unsigned disc_slot;   // WfCounters::disc index of this trace launch
   unsigned aa;          // AA samples per pixel (generation 0 in camera mode)
   unsigned rows;        // local rows of the camera shard (generation-0 tiling)
@@ -323,11 +330,14 @@ class Wavefront {
   // sphere_disc_ge0); WF_COUNT counts the reference's rays of this render
   // (read later by read_stats). A non-null `stats` implies WF_COUNT and
   // synchronises to fill it.
+  // `blk_period` / `blk_mask`: a block-pattern render (WfArgs::blk_mask) instead of
+  // shard `shard` of `n_shards` (blk_period 0).
   hipError_t render(const DevScene& sc, const DevCamera& cam, bool camera_mode, const double* d_in_rays,
                     unsigned n0, unsigned aa, unsigned max_depth, unsigned row_block, unsigned shard,
                     unsigned n_shards, double* d_out, hipStream_t stream, WfSizing& sz, DevStats* stats,
                     float* ms_kernel, const WfTuning& tn, bool solo = true, unsigned flags = 0,
-                    const FrameTable* batch = nullptr, unsigned n_frames = 1);
+                    const FrameTable* batch = nullptr, unsigned n_frames = 1, unsigned blk_period = 0,
+                    unsigned long long blk_mask = 0);
   // The counters of the last render (rendered with WF_COUNT); synchronises its stream.
   hipError_t read_stats(DevStats* out);
   // Device time of the last render rendered with WF_TIME (after it completed).
@@ -393,6 +403,8 @@ class Wavefront {
   // generation counts of the last render (fast path: from the host-mapped record; synchronises)
   hipError_t last_counts(std::vector<unsigned>& rays);
   bool last_bvh_ = false, last_fused_ = false;
+  unsigned blk_period_ = 0;  // the current render's block pattern (render())
+  unsigned long long blk_mask_ = 0;
   bool profiling_ = false;
   int pmask_ = (1 << WF_NCLASS) - 1;
   std::vector<hipEvent_t> pev_;        // event pool (pairs)

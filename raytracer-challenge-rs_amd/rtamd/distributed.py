@@ -1,5 +1,9 @@
 """Multi-GPU frame assembly: one process per GPU, interleaved row blocks.
 
+With `pattern` (block_patterns) the blocks are dealt in periods in which rank 0,
+which also receives and un-interleaves every frame, owns fewer blocks than the
+others (rt_render_block_pattern_device renders such a pattern).
+
 The reference parallelises `render_multithreaded` over contiguous row blocks
 of a shared canvas (camera.rs:157-172). Here the frame is split into blocks of
 `row_block` rows dealt round-robin to the shards (block b -> shard b mod N, same
@@ -27,6 +31,67 @@ def shard_row_ids(height, row_block, shard, n_shards):
     return [y for y in range(height) if (y // row_block) % n_shards == shard]
 
 
+def pattern_row_ids(height, row_block, period, mask):
+    """Canvas rows owned by a block pattern (rt_render_block_pattern_device:
+    block b belongs to it iff bit b % period of mask is set), in the order its
+    buffer stores them. shard_row_ids(h, b, s, n) == pattern_row_ids(h, b, n, 1 << s)."""
+    return [y for y in range(height) if (mask >> ((y // row_block) % period)) & 1]
+
+
+def block_patterns(n_ranks, root_share=1.0, max_period=64):
+    """Row-block patterns for `n_ranks` ranks (ABI 6, rt_render_block_pattern_device):
+    returns (period, masks), masks[r] the blocks of rank r. Rank 0 also receives
+    and un-interleaves every frame, so it takes `root_share` of an equal share
+    (rounded to what a period of at most `max_period` blocks can express); the
+    others take equal shares. Within a period each rank's blocks are spread
+    evenly (the position goes to the rank furthest behind its quota), so dense
+    and empty regions of the frame spread over the ranks as with the plain
+    interleave, which is the case root_share = 1 (period n, masks 1 << r)."""
+    if n_ranks <= 1:
+        return 1, [1]
+    best = None
+    for c in range(1, max_period + 1):
+        c0 = max(1, int(round(c * root_share)))
+        period = c0 + (n_ranks - 1) * c
+        if period > max_period:
+            break
+        err = abs(c0 / c - root_share)
+        if best is None or err < best[0] - 1e-9:
+            best = (err, c0, c, period)
+    _, c0, c, period = best
+    quota = [c0] + [c] * (n_ranks - 1)
+    got = [0] * n_ranks
+    masks = [0] * n_ranks
+    for pos in range(period):
+        r = min((r for r in range(n_ranks) if got[r] < quota[r]), key=lambda r: ((got[r] + 0.5) / quota[r], r))
+        masks[r] |= 1 << pos
+        got[r] += 1
+    return period, masks
+
+
+def root_share_default(config, n_ranks):
+    """Rank 0's share of an equal row split in bench.py's N-rank runs: its render
+    time plus its assembly (the receive of N-1 shards and the un-interleave)
+    should equal the other ranks' render time. Measured on one MI355X for C3
+    (profiles/r05_assembly_n8.txt): a row block of an N-way shard renders in
+    about 0.0060-0.0067 ms per frame, the un-interleave costs 0.020 ms per frame
+    and the receive of 7 shards 0.014 ms, which gives 0.97 / 0.91 / 0.74 of an
+    equal share at N = 2 / 4 / 8. C5 frames are 57x longer, so its assembly is
+    within a few per cent of a rank's work: an equal split."""
+    if config != "c3" or n_ranks <= 1:
+        return 1.0
+    return {2: 0.97, 4: 0.9, 8: 0.75}.get(n_ranks, max(0.6, 1.0 - 0.034 * n_ranks))
+
+
+def rank_row_ids(height, row_block, rank, n_ranks, pattern=None):
+    """Canvas rows rank `rank` renders: its interleaved shard (shard_of), or with
+    `pattern` = block_patterns(...) its block pattern, in buffer order."""
+    if pattern is None:
+        return shard_row_ids(height, row_block, shard_of(rank, n_ranks), n_ranks)
+    period, masks = pattern
+    return pattern_row_ids(height, row_block, period, masks[rank])
+
+
 class FrameAssembler:
     """Shard buffers + the gather/un-interleave step of one (H, W) frame.
 
@@ -39,12 +104,13 @@ class FrameAssembler:
     overwritten only by a gather issued after the un-interleave that read it.
     """
 
-    def __init__(self, height, width, row_block, rank, n_shards, device, dtype=torch.float64, slots=1):
+    def __init__(self, height, width, row_block, rank, n_shards, device, dtype=torch.float64, slots=1, pattern=None):
         self.H, self.W, self.B = height, width, row_block
         self.rank, self.n = rank, n_shards
         self.shard_index = shard_of(rank, n_shards)
-        self.rows = shard_row_ids(height, row_block, self.shard_index, n_shards)
-        self.max_rows = max(len(shard_row_ids(height, row_block, s, n_shards)) for s in range(n_shards))
+        self.pattern = pattern
+        self.rows = rank_row_ids(height, row_block, rank, n_shards, pattern)
+        self.max_rows = max(len(rank_row_ids(height, row_block, r, n_shards, pattern)) for r in range(n_shards))
         # padded so that every rank sends the same element count
         self.shards = [torch.zeros((self.max_rows, width, 3), dtype=dtype, device=device) for _ in range(slots)]
         self.shard = self.shards[0]
@@ -60,7 +126,7 @@ class FrameAssembler:
             self.canvas = torch.empty((height, width, 3), dtype=dtype, device=device)
             inv = [0] * height
             for s in range(n_shards):  # gather position s holds rank s's shard
-                for i, y in enumerate(shard_row_ids(height, row_block, shard_of(s, n_shards), n_shards)):
+                for i, y in enumerate(rank_row_ids(height, row_block, s, n_shards, pattern)):
                     inv[y] = s * self.max_rows + i
             self.inv_idx = torch.tensor(inv, device=device)
 
@@ -133,7 +199,7 @@ class StreamFrameAssembler:
     """
 
     def __init__(self, height, width, row_block, rank, n_shards, device, streams=None, groups=None,
-                 dtype=torch.float64, slots=1, batch=1):
+                 dtype=torch.float64, slots=1, batch=1, pattern=None):
         self.H, self.W, self.B = height, width, row_block
         self.rank, self.n = rank, n_shards
         self.streams = streams
@@ -141,8 +207,9 @@ class StreamFrameAssembler:
         self.NB = max(1, batch)
         self.groups = groups if groups is not None else [None] * self.F
         self.shard_index = shard_of(rank, n_shards)
-        self.rows = shard_row_ids(height, row_block, self.shard_index, n_shards)
-        self.max_rows = max(len(shard_row_ids(height, row_block, s, n_shards)) for s in range(n_shards))
+        self.pattern = pattern
+        self.rows = rank_row_ids(height, row_block, rank, n_shards, pattern)
+        self.max_rows = max(len(rank_row_ids(height, row_block, r, n_shards, pattern)) for r in range(n_shards))
         # stream k's batch: NB padded shard slots, back to back (one gather sends them all)
         self.shards = [torch.zeros((self.NB * self.max_rows, width, 3), dtype=dtype, device=device)
                        for _ in range(self.F)]
@@ -157,7 +224,7 @@ class StreamFrameAssembler:
                            for _ in range(self.F)]
             one, inv = [0] * height, [0] * (self.NB * height)
             for s in range(n_shards):  # gather position s holds rank s's shard slots
-                for i, y in enumerate(shard_row_ids(height, row_block, shard_of(s, n_shards), n_shards)):
+                for i, y in enumerate(rank_row_ids(height, row_block, s, n_shards, pattern)):
                     one[y] = s * self.max_rows + i  # one frame's gather (no batch)
                     for j in range(self.NB):  # canvas j, row y <- rank s's slot j, row i
                         inv[j * height + y] = s * per + j * self.max_rows + i
@@ -237,9 +304,9 @@ class RcclStreamAssembler(StreamFrameAssembler):
     `streams` entries may be None (CPU tests: the current stream)."""
 
     def __init__(self, height, width, row_block, rank, n_shards, device, streams, dtype=torch.float64, lib=None,
-                 timeout_ms=60000, batch=1):
+                 timeout_ms=60000, batch=1, pattern=None):
         super().__init__(height, width, row_block, rank, n_shards, device, streams=streams,
-                         groups=[None] * len(streams), dtype=dtype, batch=batch)
+                         groups=[None] * len(streams), dtype=dtype, batch=batch, pattern=pattern)
         if lib is None:
             from . import _rtamd as lib
         self._lib = lib

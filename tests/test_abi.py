@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_shard_rows():
     lib = ctypes.CDLL(LIB)
-    assert lib.rt_abi_version() == 5
+    assert lib.rt_abi_version() == 6
     f = lib.rt_shard_rows
     f.restype = ctypes.c_uint32
     f.argtypes = [ctypes.c_uint32] * 4
@@ -46,6 +46,35 @@ def test_abi_version_and_shard_rows():
     for H, B, S in [(1080, 8, 1), (1080, 8, 2), (1080, 8, 8), (1081, 16, 3), (5, 8, 4), (0, 4, 2)]:
         assert sum(f(H, B, s, S) for s in range(S)) == H
     assert f(100, 0, 0, 1) == 0 and f(100, 4, 3, 3) == 0
+
+
+def test_pattern_rows_partition():
+    """rt_pattern_rows (ABI 6): a shard is the pattern (n, 1 << s); the masks of
+    rtamd.distributed.block_patterns cover every row exactly once, rank 0's
+    share reduced; invalid patterns own nothing."""
+    import sys
+    sys.path.insert(0, PKG)
+    from rtamd.distributed import block_patterns, pattern_row_ids
+    lib = ctypes.CDLL(LIB)
+    g, s = lib.rt_pattern_rows, lib.rt_shard_rows
+    g.restype = s.restype = ctypes.c_uint32
+    g.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]
+    s.argtypes = [ctypes.c_uint32] * 4
+    for H, B, S in [(1080, 8, 1), (1080, 8, 8), (1081, 16, 3), (4096, 8, 8), (5, 8, 4)]:
+        for k in range(S):
+            assert g(H, B, S, 1 << k) == s(H, B, k, S)
+    for n, share in [(2, 0.93), (4, 0.86), (8, 0.75), (8, 0.5), (8, 1.0), (3, 0.8)]:
+        period, masks = block_patterns(n, share)
+        assert 1 <= period <= 64 and len(masks) == n
+        assert sum(masks) == (1 << period) - 1 and all(m and not (m & o) for i, m in enumerate(masks)
+                                                       for o in masks[i + 1:])
+        for H, B in [(1080, 8), (4096, 8), (1081, 5)]:
+            rows = [pattern_row_ids(H, B, period, m) for m in masks]
+            assert sorted(y for r in rows for y in r) == list(range(H))
+            assert [len(r) for r in rows] == [g(H, B, period, m) for m in masks]
+        if share < 1.0:
+            assert bin(masks[0]).count("1") < min(bin(m).count("1") for m in masks[1:])
+    assert g(100, 4, 0, 1) == 0 and g(100, 4, 3, 8) == 0 and g(100, 4, 3, 0) == 0 and g(100, 4, 65, 1) == 0
 
 
 def test_duplicate_shapes_rejected_before_any_device_work(rt):

@@ -137,26 +137,32 @@ def _ref_canvas(kind):
     every row and column distinct."""
     if kind == "golden":
         return torch.from_numpy(np.load(os.path.join(HERE, "golden", "c3_64x36_s200.npz"))["canvas"])
-    H, W = 1080, 6
+    H, W = (4096, 4) if kind == "c5rows" else (1080, 6)  # C5: 4096 rows, 512 blocks of 8
     y = torch.arange(H, dtype=torch.float64).view(H, 1, 1)
     x = torch.arange(W, dtype=torch.float64).view(1, W, 1)
     c = torch.arange(3, dtype=torch.float64).view(1, 1, 3)
     return y * 1000.0 + x * 10.0 + c / 4.0
 
 
-def _stream_worker(rank, world_size, port, row_block, n_frames, n_slots, out_path, batch=1, kind="golden"):
+def _stream_worker(rank, world_size, port, row_block, n_frames, n_slots, out_path, batch=1, kind="golden",
+                   share=None):
     """StreamFrameAssembler (bench.py's N>1 path): frame f is golden + f, one
     process group per slot; every submit returns frame f assembled (batch > 1:
-    every batch's last submit gathers and assembles the batch)."""
+    every batch's last submit gathers and assembles the batch). `share`: rank
+    0's share of the rows (block patterns, bench.py --root-share)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world_size)
     try:
-        from rtamd.distributed import StreamFrameAssembler
+        from rtamd.distributed import StreamFrameAssembler, block_patterns
         ref = _ref_canvas(kind)
         H, W = ref.shape[:2]
         groups = [dist.new_group(list(range(world_size))) for _ in range(n_slots)]
+        pattern = block_patterns(world_size, share) if share is not None else None
         fa = StreamFrameAssembler(H, W, row_block, rank, world_size, torch.device("cpu"), groups=groups,
-                                  slots=n_slots, batch=batch)
+                                  slots=n_slots, batch=batch, pattern=pattern)
+        if pattern is not None:
+            import rtamd
+            assert len(fa.rows) == rtamd.pattern_rows(H, row_block, pattern[0], pattern[1][rank])
         done = []
         for f in range(n_frames):
             buf = fa.slot(f)
@@ -249,11 +255,13 @@ class _FakeRccl:
             dist.gather(src, None, dst=0)
 
 
-def _rccl_assembler_worker(rank, world_size, port, fail_at, n_frames, out_path, batch=1, kind="golden", F=3):
+def _rccl_assembler_worker(rank, world_size, port, fail_at, n_frames, out_path, batch=1, kind="golden", F=3,
+                           share=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world_size)
     try:
-        from rtamd.distributed import RcclStreamAssembler
+        from rtamd.distributed import RcclStreamAssembler, block_patterns
+        pattern = block_patterns(world_size, share) if share is not None else None
         ref = _ref_canvas(kind)
         H, W = ref.shape[:2]
         lib = _FakeRccl(rank, fail_at)
@@ -267,7 +275,7 @@ def _rccl_assembler_worker(rank, world_size, port, fail_at, n_frames, out_path, 
             np.save(out_path + f".{rank}", np.array([len(lib.made)]))
             return
         fa = RcclStreamAssembler(H, W, 8, rank, world_size, torch.device("cpu"), streams=[None] * F, lib=lib,
-                                 batch=batch)
+                                 batch=batch, pattern=pattern)
         assert fa.comms == [1000 * (rank + 1) + k for k in range(F)]
         for t in fa.shards:
             lib.tensors[t.data_ptr()] = t
@@ -370,5 +378,49 @@ def test_gloo_rccl_stream_assembler_bench_n8_config(tmp_path, world_size):
     got = np.load(out)
     ref = _ref_canvas("c3rows").numpy()
     assert got.shape == (n_frames,) + ref.shape
+    for f in range(n_frames):
+        assert np.array_equal(got[f], ref + f), f
+
+
+# bench.py's C5 run at 8 GPUs (--config c5): batches of one frame, ONE render
+# stream (bench.py: F = 1, NB = 1 for C5), so StreamFrameAssembler gathers on
+# the current stream over one process group; 4096 rows in 8-row blocks (512
+# blocks, 64 per rank). Every assembled frame whole and in order.
+def test_gloo_stream_assembler_bench_c5_n8_config(tmp_path):
+    out = str(tmp_path / "frames.npy")
+    n_frames = 5
+    mp.spawn(_stream_worker, args=(8, _free_port(), 8, n_frames, 1, out, 1, "c5rows"), nprocs=8, join=True)
+    got = np.load(out)
+    ref = _ref_canvas("c5rows").numpy()
+    assert got.shape == (n_frames,) + ref.shape
+    for f in range(n_frames):
+        assert np.array_equal(got[f], ref + f), f
+
+
+# The N = 4 / 8 runs' uneven split (bench.py: root_share_default for C3): rank 0,
+# which assembles every frame, renders fewer row blocks (block patterns, ABI 6).
+@pytest.mark.parametrize("world_size,share", [(8, 0.75), (4, 0.9), (2, 0.97)])
+def test_gloo_stream_assembler_root_share(tmp_path, world_size, share):
+    out = str(tmp_path / "frames.npy")
+    n_frames = 37
+    mp.spawn(_stream_worker, args=(world_size, _free_port(), 8, n_frames, 4, out, 16, "c3rows", share),
+             nprocs=world_size, join=True)
+    got = np.load(out)
+    ref = _ref_canvas("c3rows").numpy()
+    assert got.shape == (n_frames,) + ref.shape
+    for f in range(n_frames):
+        assert np.array_equal(got[f], ref + f), f
+
+
+@pytest.mark.parametrize("world_size", [8])
+def test_gloo_rccl_stream_assembler_root_share(tmp_path, world_size):
+    """The default N>1 assembler (library communicators, faked) with bench.py's
+    N = 8 split of C3 (rank 0 at 0.75 of an equal share)."""
+    out = str(tmp_path / "frames.npy")
+    n_frames = 37
+    mp.spawn(_rccl_assembler_worker, args=(world_size, _free_port(), None, n_frames, out, 16, "c3rows", 4, 0.75),
+             nprocs=world_size, join=True)
+    got = np.load(out)
+    ref = _ref_canvas("c3rows").numpy()
     for f in range(n_frames):
         assert np.array_equal(got[f], ref + f), f

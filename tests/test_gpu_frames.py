@@ -164,3 +164,51 @@ def test_frames_pass_cap(rt):
     from rtamd import scenes
     w, _, depth = scenes.c3(1024, 1024, n_spheres=200)
     _check(rt, w, _cameras(rt, 3, 1024, 1024), depth, 8, 0, 1, aa=16)
+
+
+@pytest.mark.parametrize("n_ranks,share,aa", [(8, 0.75, 1), (4, 0.9, 1), (3, 0.8, 4), (8, 1.0, 1), (2, 0.5, 2)])
+def test_block_pattern_frames_bitwise(rt, n_ranks, share, aa):
+    """rt_render_block_pattern_device (ABI 6): every rank's rows of a block
+    pattern (rtamd.distributed.block_patterns, rank 0 at `share` of an equal
+    share), for a batch of cameras and one camera, equal the same rows of the
+    whole exhaustive frame bit for bit; the ranks' rows cover the frame once.
+    The plain pattern (share 1) equals rt_render_frames_device's shards."""
+    import torch
+    from rtamd import scenes
+    from rtamd.distributed import block_patterns, pattern_row_ids
+    w, _, depth = scenes.c3(120, 77, n_spheres=300)
+    cams = _cameras(rt, 3, 120, 77)
+    st = torch.cuda.current_stream().cuda_stream
+    whole = []
+    for c in cams:
+        b = torch.empty((77, 120, 3), dtype=torch.float64, device="cuda")
+        c.render_shard_device(w, depth, 8, 0, 1, b.data_ptr(), st, True, aa, exhaustive=True)
+        whole.append(b)
+    period, masks = block_patterns(n_ranks, share)
+    covered = []
+    for r, m in enumerate(masks):
+        rows = pattern_row_ids(77, 8, period, m)
+        assert len(rows) == rt.pattern_rows(77, 8, period, m)
+        covered += rows
+        bufs = [torch.full((len(rows), 120, 3), -1.0, dtype=torch.float64, device="cuda") for _ in cams]
+        rt.render_block_pattern_device(w, cams, depth, 8, period, m, [b.data_ptr() for b in bufs], st, False, aa)
+        one = torch.full_like(bufs[0], -2.0)
+        rt.render_block_pattern_device(w, cams[:1], depth, 8, period, m, [one.data_ptr()], st, False, aa)
+        torch.cuda.synchronize()
+        w.check()
+        idx = torch.tensor(rows, device="cuda")
+        for k, b in enumerate(bufs):
+            assert torch.equal(b, whole[k].index_select(0, idx)), (r, k)
+        assert torch.equal(one, bufs[0])
+        if share == 1.0:  # the plain interleave: mask 1 << r is shard r of n
+            sh = torch.full_like(one, -3.0)
+            cams[0].render_shard_device(w, depth, 8, r, n_ranks, sh.data_ptr(), st, False, aa)
+            torch.cuda.synchronize()
+            assert torch.equal(sh, one)
+    assert sorted(covered) == list(range(77))
+    with pytest.raises(rt.RtError, match="block pattern"):
+        rt.render_block_pattern_device(w, cams[:1], depth, 8, 8, 1 << 9, [whole[0].data_ptr()], st)
+    counted = rt.render_block_pattern_device(w, cams[:1], depth, 8, period, masks[0], [whole[0].data_ptr()], st,
+                                             True, aa, True)
+    assert counted["exhaustive"] and counted["rays_primary"] == aa * 120 * len(pattern_row_ids(77, 8, period,
+                                                                                               masks[0]))

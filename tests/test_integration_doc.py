@@ -94,7 +94,7 @@ def test_library_reports_the_same_sizes():
         f = getattr(lib, fn)
         f.restype = ctypes.c_size_t
         assert f() == SIZES[cname] == layout(c_structs()[cname])[0]
-    assert lib.rt_abi_version() == 5
+    assert lib.rt_abi_version() == 6
 
 
 def _rust_kind(t):
