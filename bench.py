@@ -727,18 +727,21 @@ def verify_frames(fa, last, ref_shard, last_step, n, rank, H):
                        "(every-shape loop) frame rendered before timing"}
 
 
-def pmc_summary_path(a, W, H, n):
-    """The newest committed PMC summary measured on this workload."""
+def pmc_summary_path(a, W, H, n, build):
+    """The committed PMC summary (tools/profile.sh) of THIS build (its `build`
+    field equals rtamd.buildinfo.build_id(), the hash of the library's sources)
+    measured on this workload; "" when the kernels benched here were never
+    profiled (then the roofline carries no traffic rather than another build's)."""
     if a.pmc_summary:
         return a.pmc_summary
     import glob
-    cands = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary*.json")), reverse=True)
-    for c in cands:
+    for c in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary*.json")), reverse=True):
         try:
             pm = json.load(open(c))
         except (OSError, ValueError):
             continue
-        if (pm.get("width"), pm.get("height"), pm.get("spheres"), pm.get("n_gpus")) == (W, H, a.spheres, n):
+        if (pm.get("width"), pm.get("height"), pm.get("spheres"), pm.get("n_gpus"), pm.get("build")) == \
+                (W, H, a.spheres, n, build):
             return c
     return ""
 
@@ -801,7 +804,10 @@ def roofline(prof, breakdown, W, H, a, n, ref_work, frame_ms, nb=1):
     achieved = ops / (kernel_ms * 1e-3) / 1e12
     achieved_survey = survey_ops / (kernel_ms * 1e-3) / 1e12
     traffic, traffic_src, counters = None, None, None
-    pmc_path = pmc_summary_path(a, W, H, n)
+    from rtamd.buildinfo import build_id
+    build = build_id()
+    traffic_src = f"no PMC summary of this build ({build}) on this workload in profiles/"
+    pmc_path = pmc_summary_path(a, W, H, n, build)
     if pmc_path and os.path.exists(pmc_path):
         a.pmc_summary = pmc_path
         try:
@@ -844,6 +850,7 @@ def roofline(prof, breakdown, W, H, a, n, ref_work, frame_ms, nb=1):
         "traversal": "bvh" if prof["bvh"] else "exhaustive",
         "reference_work_tflops": round(ref_work / (frame_ms * 1e-3) / 1e12, 3),
         "traffic_source": traffic_src,
+        "build": build,
         "pmc": counters,
         "kernels": kernels,
     }

@@ -112,6 +112,17 @@ typedef struct rt_shape_desc {
   int32_t _pad2;
 } rt_shape_desc;
 
+/* (ABI 6) A `Group` (geometry/shape/group.rs:13-18) of the flattened World:
+ * its bounding box as Group::intersect tests it (BaseShape::bounding_box of
+ * the group, the union of its children's boxes, group.rs:71-94,128-133), and
+ * the group that contains it (-1: a member of World::objects). Groups are
+ * listed parents first. */
+typedef struct rt_group_desc {
+  double min[3], max[3];
+  int32_t parent;
+  int32_t _pad;
+} rt_group_desc;
+
 /* `PointLight` (light.rs:4-24), in `World::lights` insertion order. */
 typedef struct rt_light_desc {
   double position[3];
@@ -187,6 +198,20 @@ int rt_camera_init(uint32_t hsize, uint32_t vsize, double field_of_view,
 int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes,
                     const rt_light_desc* lights, size_t n_lights, int device,
                     rt_scene** out);
+
+/* (ABI 6) rt_scene_create for a World whose objects include Groups
+ * (group.rs): `shapes` are the primitives in the order World::intersect's
+ * flat_map reaches them (each group's children in order, depth first), with
+ * their final transforms (the groups' transforms baked in, group.rs:71-94,
+ * 128-133) and materials (Group::set_material, :96-102); shape_group[i] is the
+ * innermost group of shape i (-1: none). A shape inside groups is intersected
+ * only by rays that meet the box of every group around it
+ * (BoundingBox::intersects, bounding_box.rs:95-136, its |d| < EPSILON rule
+ * included), exactly as the reference's Group::intersect skips its children. */
+int rt_scene_create_groups(const rt_shape_desc* shapes, size_t n_shapes,
+                           const int32_t* shape_group, const rt_group_desc* groups,
+                           size_t n_groups, const rt_light_desc* lights,
+                           size_t n_lights, int device, rt_scene** out);
 void rt_scene_destroy(rt_scene* scene);
 
 /* ---- render entry points -------------------------------------------------- */

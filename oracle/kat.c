@@ -748,6 +748,67 @@ int main(void) {
     CHECK(n == strlen(expect) && memcmp(buf, expect, n) == 0);
   }
 
+  /* ------------------------------------------------ bounding_box.rs / group.rs */
+  CASE("bounding_box_intersects_cube_at_origin") { /* bounding_box.rs:315-357 */
+    obbox b = {or_t3(-1, -1, -1), or_t3(1, 1, 1)};
+    const double tc[13][7] = {{5, 0.5, 0, -1, 0, 0, 1},  {-5, 0.5, 0, 1, 0, 0, 1}, {0.5, 5, 0, 0, -1, 0, 1},
+                              {0.5, -5, 0, 0, 1, 0, 1},  {0.5, 0, 5, 0, 0, -1, 1}, {0.5, 0, -5, 0, 0, 1, 1},
+                              {0, 0.5, 0, 0, 0, 1, 1},   {-2, 0, 0, 2, 4, 6, 0},   {0, -2, 0, 6, 2, 4, 0},
+                              {0, 0, -2, 4, 6, 2, 0},    {2, 0, 2, 0, 0, -1, 0},   {0, 2, 2, 0, -1, 0, 0},
+                              {2, 2, 0, -1, 0, 0, 0}};
+    for (int i = 0; i < 13; ++i) {
+      oray r = {or_t3(tc[i][0], tc[i][1], tc[i][2]), or_normalize(or_t3(tc[i][3], tc[i][4], tc[i][5]))};
+      CHECK(or_bbox_intersects(&b, &r) == (int)tc[i][6]);
+    }
+  }
+  CASE("bounding_box_intersects_non_cubic") { /* bounding_box.rs:359-401 */
+    obbox b = {or_t3(5, -2, 0), or_t3(11, 4, 7)};
+    const double tc[13][7] = {{15, 1, 2, -1, 0, 0, 1}, {-5, -1, 4, 1, 0, 0, 1},   {7, 6, 5, 0, -1, 0, 1},
+                              {9, -5, 6, 0, 1, 0, 1},  {8, 2, 12, 0, 0, -1, 1},   {6, 0, -5, 0, 0, 1, 1},
+                              {8, 1, 3.5, 0, 0, 1, 1}, {9, -1, -8, 2, 4, 6, 0},   {8, 3, -4, 6, 2, 4, 0},
+                              {9, -1, -2, 4, 6, 2, 0}, {4, 0, 9, 0, 0, -1, 0},    {8, 6, -1, 0, -1, 0, 0},
+                              {12, 5, 4, -1, 0, 0, 0}};
+    for (int i = 0; i < 13; ++i) {
+      oray r = {or_t3(tc[i][0], tc[i][1], tc[i][2]), or_normalize(or_t3(tc[i][3], tc[i][4], tc[i][5]))};
+      CHECK(or_bbox_intersects(&b, &r) == (int)tc[i][6]);
+    }
+  }
+  CASE("group_box_gates_its_children") { /* bounding_box.rs:403-441, group.rs:49-58, :263-278 */
+    /* a group around a unit sphere: a ray that misses the group's box intersects no child
+     * (no local_intersect call); one that meets it intersects the child */
+    oworld gw;
+    or_world_init(&gw);
+    obbox b = {or_t3(-1, -1, -1), or_t3(1, 1, 1)};
+    or_world_add_group(&gw, b, -1);
+    oshape s = or_sphere_default();
+    s.gate = 1;
+    or_world_add_object(&gw, &s);
+    rt_stats st;
+    memset(&st, 0, sizeof st);
+    int n = 0;
+    oray miss = R(0, 0, -5, 0, 1, 0);
+    free(or_world_intersect(&gw, &miss, &n, &st));
+    CHECK(n == 0 && st.sphere_tests == 0);
+    oray hit = R(0, 0, -5, 0, 0, 1);
+    free(or_world_intersect(&gw, &hit, &n, &st));
+    CHECK(n == 2 && st.sphere_tests == 1);
+    /* intersect_transformed_group (group.rs:263-278): scaling(2) group, child at translation(5): the
+     * child's baked transform is scaling(2) * translation(5, 0, 0); the group's box is its box */
+    or_world_free(&gw);
+    or_world_init(&gw);
+    oshape c = or_sphere_default();
+    omat sc = or_scaling(2, 2, 2), tr = or_translation(5, 0, 0), m = om_mul(&sc, &tr);
+    set_tf(&c, m);
+    or_world_add_group(&gw, c.bbox, -1);
+    c.gate = 1;
+    or_world_add_object(&gw, &c);
+    oray r = R(10, 0, -10, 0, 0, 1);
+    oxs* xs = or_world_intersect(&gw, &r, &n, NULL);
+    CHECK(n == 2);
+    free(xs);
+    or_world_free(&gw);
+  }
+
   or_world_free(&w);
   printf("KAT %d/%d\n", g_total - g_failed, g_total);
   return g_failed ? 1 : 0;

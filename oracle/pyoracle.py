@@ -50,6 +50,10 @@ def _load():
     lib.oracle_world_add_desc.argtypes = [P, ctypes.c_char_p]
     lib.oracle_world_add_desc.restype = I
     lib.oracle_world_add_light.argtypes = [P, D, D]
+    lib.oracle_world_add_group.argtypes = [P, ctypes.c_char_p]
+    lib.oracle_world_add_group.restype = I
+    lib.oracle_world_set_last_group.argtypes = [P, I]
+    lib.oracle_world_set_last_group.restype = I
     lib.oracle_matrix_inverse.argtypes = [D, D]
     lib.oracle_matrix_inverse.restype = I
     lib.oracle_camera_init.argtypes = [U, U, ctypes.c_double, D, ctypes.c_char_p]
@@ -89,18 +93,29 @@ def _dptr(a):
 class OracleWorld:
     """The reference `World`, rebuilt from C-ABI descriptor bytes."""
 
-    def __init__(self, descs=b"", lights=(), default=False):
+    def __init__(self, descs=b"", lights=(), default=False, groups=b"", shape_groups=None):
+        """`groups`: rt_group_desc bytes (parents first), `shape_groups`: the
+        innermost group of each shape (-1: none) — a World with Groups
+        flattened as rt_scene_create_groups takes it (group.rs)."""
         L = lib()
         self._w = L.oracle_world_new()
         if default:
             L.oracle_world_set_default(self._w)
             return
+        gsz = 56  # sizeof(rt_group_desc)
+        assert len(groups) % gsz == 0, "group descriptor size mismatch"
+        for i in range(0, len(groups), gsz):
+            if L.oracle_world_add_group(self._w, groups[i:i + gsz]) < 0:
+                raise ValueError(f"oracle rejected group {i // gsz}")
         sz = L.oracle_sizeof_shape_desc()
         assert len(descs) % sz == 0, "descriptor size mismatch"
         for i in range(0, len(descs), sz):
             rc = L.oracle_world_add_desc(self._w, descs[i:i + sz])
             if rc != 0:
                 raise ValueError(f"oracle rejected shape {i // sz}: rc={rc}")
+            if shape_groups is not None and shape_groups[i // sz] >= 0:
+                if L.oracle_world_set_last_group(self._w, int(shape_groups[i // sz])) != 0:
+                    raise ValueError(f"oracle rejected the group of shape {i // sz}")
         for pos, inten in lights:
             p = np.asarray(pos, dtype=np.float64)
             c = np.asarray(inten, dtype=np.float64)
@@ -110,7 +125,8 @@ class OracleWorld:
     def from_world(cls, world):
         """From an rtamd.World (host API): descriptors + lights."""
         lb = np.frombuffer(world.lights_bytes(), dtype=np.float64).reshape(-1, 6)
-        return cls(world.descs_bytes(), [(r[:3], r[3:]) for r in lb])
+        return cls(world.descs_bytes(), [(r[:3], r[3:]) for r in lb], groups=world.groups_bytes(),
+                   shape_groups=world.shape_groups())
 
     def __del__(self):
         if getattr(self, "_w", None) and _lib is not None:

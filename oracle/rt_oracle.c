@@ -216,6 +216,31 @@ static obbox or_bbox_transform(const obbox* b, const omat* m) { /* :71-89 */
 static int or_bbox_eq(const obbox* a, const obbox* b) { /* :20-24 */
   return or_t3_eq_ignore_inf(a->min, b->min) && or_t3_eq_ignore_inf(a->max, b->max);
 }
+/* :118-136: per axis (min - o) / d and (max - o) / d, or the numerators times
+ * infinity when |d| < EPSILON (0 * inf is NaN), ordered */
+static void or_bbox_check_axis(double origin, double direction, double mn, double mx, double* t0, double* t1) {
+  double tmin_numerator = mn - origin;
+  double tmax_numerator = mx - origin;
+  double tmin, tmax;
+  if (fabs(direction) >= OR_EPSILON) {
+    tmin = tmin_numerator / direction;
+    tmax = tmax_numerator / direction;
+  } else {
+    tmin = tmin_numerator * INFINITY;
+    tmax = tmax_numerator * INFINITY;
+  }
+  if (tmin > tmax) { *t0 = tmax; *t1 = tmin; } else { *t0 = tmin; *t1 = tmax; }
+}
+/* :95-116 (f64::max / f64::min ignore a NaN operand: fmax / fmin) */
+int or_bbox_intersects(const obbox* b, const oray* r) {
+  double x0, x1, y0, y1, z0, z1;
+  or_bbox_check_axis(r->origin.x, r->direction.x, b->min.x, b->max.x, &x0, &x1);
+  or_bbox_check_axis(r->origin.y, r->direction.y, b->min.y, b->max.y, &y0, &y1);
+  or_bbox_check_axis(r->origin.z, r->direction.z, b->min.z, b->max.z, &z0, &z1);
+  double tmin = fmax(fmax(x0, y0), z0);
+  double tmax = fmin(fmin(x1, y1), z1);
+  return tmin <= tmax;
+}
 
 /* -------------------------------------------------------- pattern/{mod,stripe,gradient,ring,checkers,test_pattern}.rs */
 opattern or_pattern(int kind, ot3 a, ot3 b) { /* pattern/mod.rs:23-31,60-91 */
@@ -557,10 +582,20 @@ void or_sort_intersections(oxs* xs, int n) {
   free(tmp);
 }
 /* world.rs:31-38: flat_map over objects, collect, intersections() (copy + sort) */
+/* group.rs:49-58: Group::intersect returns nothing when the ray misses the
+ * group's box, so none of its children (nested groups included) is
+ * intersected; a flattened primitive is intersected iff the ray meets the box
+ * of every group around it. */
+static int or_group_gate(const oworld* w, int gate, const oray* r) {
+  for (int g = gate - 1; g >= 0; g = w->groups[g].parent)
+    if (!or_bbox_intersects(&w->groups[g].box, r)) return 0;
+  return 1;
+}
 oxs* or_world_intersect(const oworld* w, const oray* r, int* n_out, rt_stats* st) {
   int cap = 8, n = 0;
   oxs* xs = (oxs*)malloc(sizeof(oxs) * cap);
   for (int i = 0; i < w->n; ++i) {
+    if (w->objects[i].gate && !or_group_gate(w, w->objects[i].gate, r)) continue;
     double t[OR_MAX_LOCAL_XS];
     int k = or_shape_intersect(&w->objects[i], r, t, st);
     for (int j = 0; j < k; ++j) {
@@ -659,7 +694,16 @@ double or_schlick(const ocomps* c) {
 
 /* --------------------------------------------------------------- world.rs */
 void or_world_init(oworld* w) { memset(w, 0, sizeof *w); }
-void or_world_free(oworld* w) { free(w->objects); free(w->lights); memset(w, 0, sizeof *w); }
+void or_world_free(oworld* w) { free(w->objects); free(w->lights); free(w->groups); memset(w, 0, sizeof *w); }
+int or_world_add_group(oworld* w, obbox box, int parent) {
+  if (w->ng == w->capg) {
+    w->capg = w->capg ? 2 * w->capg : 8;
+    w->groups = (ogroup*)realloc(w->groups, sizeof(ogroup) * w->capg);
+  }
+  w->groups[w->ng].box = box;
+  w->groups[w->ng].parent = parent;
+  return w->ng++;
+}
 int or_world_add_object(oworld* w, const oshape* s) { /* :87-89 */
   if (w->n == w->cap) {
     w->cap = w->cap ? 2 * w->cap : 8;
@@ -923,6 +967,18 @@ int oracle_world_add_desc(oworld* w, const rt_shape_desc* d) {
   }
   s.shadow = d->casts_shadow ? 1 : 0;
   or_world_add_object(w, &s);
+  return RT_OK;
+}
+/* A Group (rt_group_desc: its box, the enclosing group) and the innermost
+ * group of the shape added last (the flattened World, group.rs). */
+int oracle_world_add_group(oworld* w, const rt_group_desc* g) {
+  if (g->parent < -1 || g->parent >= w->ng) return RT_ERR_INVALID_ARGUMENT;
+  obbox b = {or_v3(g->min), or_v3(g->max)};
+  return or_world_add_group(w, b, g->parent);
+}
+int oracle_world_set_last_group(oworld* w, int group) {
+  if (w->n == 0 || group < -1 || group >= w->ng) return RT_ERR_INVALID_ARGUMENT;
+  w->objects[w->n - 1].gate = group + 1;
   return RT_OK;
 }
 int oracle_world_export_desc(const oworld* w, rt_shape_desc* out, size_t cap) {

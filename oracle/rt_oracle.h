@@ -61,15 +61,19 @@ typedef struct {
   int shadow;
   double minimum, maximum; /* Cylinder / Cone (cylinder.rs:12-18, cone.rs:12-18) */
   int closed;
+  int gate; /* 1 + the innermost Group around the shape (oworld.groups), 0: none */
 } oshape;
+typedef struct { obbox box; int parent; } ogroup; /* a Group's bounding box; parent: enclosing group, -1 none */
 
 typedef struct { ot3 position, intensity; } olight;
 
 typedef struct {
-  oshape* objects;
+  oshape* objects; /* the primitives, Groups flattened (group.rs:49-58 visits children in order) */
   int n, cap;
   olight* lights;
   int nl, capl;
+  ogroup* groups;
+  int ng, capg;
 } oworld;
 
 typedef struct { double t; int obj; } oxs; /* Intersection (u, v are None) */
@@ -155,6 +159,8 @@ void or_world_default(oworld* w);
 int or_local_intersect(const oshape* s, const oray* local, double t_out[OR_MAX_LOCAL_XS]);
 int or_shape_intersect(const oshape* s, const oray* r, double t_out[OR_MAX_LOCAL_XS], rt_stats* st);
 oxs* or_world_intersect(const oworld* w, const oray* r, int* n_out, rt_stats* st);
+int or_bbox_intersects(const obbox* b, const oray* r);
+int or_world_add_group(oworld* w, obbox box, int parent);
 void or_sort_intersections(oxs* xs, int n);
 int or_hit(const oxs* xs, int n); /* index into xs or -1 */
 ot3 or_local_normal_at(const oshape* s, ot3 local_point);

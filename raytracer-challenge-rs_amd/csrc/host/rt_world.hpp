@@ -75,6 +75,33 @@ struct PointLight {
   PointLight(const Point& p, const Color& i) : position(p), intensity(i) {}
 };
 
+// bounding_box.rs:5-93: what a Group's box is made of (Group::intersect tests
+// it, group.rs:49-58). Every shape carries one, re-derived by set_transform
+// (geometry/mod.rs:74-85) through the same corner products as the reference,
+// infinite corners (planes, open cylinders) and their NaNs included.
+struct BoundingBox {
+  Point min = Point(kInf, kInf, kInf), max = Point(-kInf, -kInf, -kInf);
+  static constexpr double kInf = std::numeric_limits<double>::infinity();
+  BoundingBox() = default;
+  BoundingBox(const Point& mn, const Point& mx) : min(mn), max(mx) {}
+  void add_point(const Point& p) {  // :39-59
+    if (p.x > max.x) max.x = p.x;
+    if (p.y > max.y) max.y = p.y;
+    if (p.z > max.z) max.z = p.z;
+    if (p.x < min.x) min.x = p.x;
+    if (p.y < min.y) min.y = p.y;
+    if (p.z < min.z) min.z = p.z;
+  }
+  void add_box(const BoundingBox& b) { add_point(b.min); add_point(b.max); }  // :61-64
+  BoundingBox transform(const Matrix& m) const {  // :76-93
+    const Point pts[8] = {min, Point(min.x, min.y, max.z), Point(min.x, max.y, min.z), Point(min.x, max.y, max.z),
+                          Point(max.x, min.y, min.z), Point(max.x, min.y, max.z), Point(max.x, max.y, min.z), max};
+    BoundingBox nb;
+    for (const Point& p : pts) nb.add_point(m * p);
+    return nb;
+  }
+};
+
 // geometry/mod.rs:12-108 (BaseShape + the parts of `trait Shape` on the path)
 struct Shape {
   int kind = RT_SHAPE_SPHERE;
@@ -86,10 +113,16 @@ struct Shape {
   double minimum = -std::numeric_limits<double>::infinity();
   double maximum = std::numeric_limits<double>::infinity();
   bool closed = false;
+  BoundingBox bbox = BoundingBox(Point(-1, -1, -1), Point(1, 1, 1));  // sphere.rs:20 / cube.rs:22
   void set_transform(const Matrix& t) {  // geometry/mod.rs:74-85
-    transform_inverse = t.inverse();
+    bbox = bbox.transform(transform_inverse);
+    const Matrix inv = t.inverse();
+    transform_inverse = inv;
     transform = t;
+    bbox = bbox.transform(transform);
   }
+  void set_material(const Material& m) { material = m; }  // geometry/mod.rs:66-68
+  BoundingBox parent_space_bounds() const { return bbox.transform(Matrix::identity(4, 4)); }  // :97-99
   void no_shadow() { shadow = false; }            // :105-107
   bool has_shadow() const { return shadow; }      // :101-103
   Matrix transform_inverse_transpose() const { return transform_inverse.transpose(); }
@@ -105,6 +138,7 @@ inline Shape glass_sphere() {
 inline Shape Plane() {  // plane.rs:19-31
   Shape s;
   s.kind = RT_SHAPE_PLANE;
+  s.bbox = BoundingBox(Point(-BoundingBox::kInf, 0.0, -BoundingBox::kInf), Point(BoundingBox::kInf, 0.0, BoundingBox::kInf));
   return s;
 }
 inline Shape Cube() {  // cube.rs:17-26
@@ -118,6 +152,7 @@ inline Shape Cylinder(double minimum = -std::numeric_limits<double>::infinity(),
   Shape s;
   s.kind = RT_SHAPE_CYLINDER;
   s.minimum = minimum; s.maximum = maximum; s.closed = closed;
+  s.bbox = BoundingBox(Point(-1.0, minimum, -1.0), Point(1.0, maximum, 1.0));  // cylinder.rs:30-33
   return s;
 }
 // cone.rs:20-46
@@ -125,7 +160,66 @@ inline Shape Cone(double minimum = -std::numeric_limits<double>::infinity(),
                   double maximum = std::numeric_limits<double>::infinity(), bool closed = false) {
   Shape s = Cylinder(minimum, maximum, closed);
   s.kind = RT_SHAPE_CONE;
+  const double a = std::fabs(minimum), b = std::fabs(maximum), limit = std::fmax(a, b);  // f64::max (cone.rs:29-31)
+  s.bbox = BoundingBox(Point(-limit, minimum, -limit), Point(limit, maximum, limit));
   return s;
+}
+
+// geometry/shape/group.rs:13-198: a Group holds shapes and groups in order. Its
+// transform is baked into every descendant (set_transform / add_child call the
+// children's set_transform with the product, group.rs:71-94,128-133), so a
+// child's transform is final; its box is the union of its children's boxes.
+struct Group;
+struct GroupChild {  // Box<dyn Shape> of a Group: a primitive or a group
+  std::shared_ptr<Shape> shape;
+  std::shared_ptr<Group> group;
+};
+struct Group {
+  Matrix transform = Matrix::identity(4, 4);
+  Matrix transform_inverse = Matrix::identity(4, 4);
+  Material material;
+  BoundingBox bbox;  // BaseShape::default: empty
+  std::vector<GroupChild> children;
+  void set_transform(const Matrix& t);                          // group.rs:71-94
+  void set_material(const Material& m);                         // group.rs:96-102
+  void add_child(const Shape& s) { add(GroupChild{std::make_shared<Shape>(s), nullptr}); }  // group.rs:128-133
+  void add_child(const Group& g) { add(GroupChild{nullptr, std::make_shared<Group>(g)}); }
+  BoundingBox parent_space_bounds() const { return bbox.transform(Matrix::identity(4, 4)); }
+
+ private:
+  void add(GroupChild c);
+};
+inline const Matrix& child_transform(const GroupChild& c) { return c.shape ? c.shape->transform : c.group->transform; }
+inline const BoundingBox& child_bounds(const GroupChild& c) { return c.shape ? c.shape->bbox : c.group->bbox; }
+inline void child_set_transform(GroupChild& c, const Matrix& t) {
+  if (c.shape) c.shape->set_transform(t);
+  else c.group->set_transform(t);
+}
+inline void Group::set_transform(const Matrix& t) {
+  const Matrix inverse_old = transform_inverse;  // remove the current transform from the children
+  for (GroupChild& c : children) child_set_transform(c, inverse_old * child_transform(c));
+  const Matrix inv = t.inverse();
+  transform = t;
+  transform_inverse = inv;
+  BoundingBox nb;
+  for (GroupChild& c : children) {  // apply the new one
+    child_set_transform(c, transform * child_transform(c));
+    nb.add_box(child_bounds(c));
+  }
+  bbox = nb;
+}
+inline void Group::set_material(const Material& m) {
+  material = m;
+  for (GroupChild& c : children) {
+    if (c.shape) c.shape->set_material(m);
+    else c.group->set_material(m);
+  }
+}
+inline void Group::add(GroupChild c) {
+  child_set_transform(c, transform * child_transform(c));
+  const BoundingBox cbox = c.shape ? c.shape->parent_space_bounds() : c.group->parent_space_bounds();
+  bbox.add_box(cbox);
+  children.push_back(std::move(c));
 }
 
 // canvas.rs:8-52 + image/ppm.rs
@@ -249,19 +343,55 @@ class World {
     w->add_object(s2);
     return w;
   }
-  void add_object(const Shape& s) { drop(); objects_.push_back(s); }     // :87-89
+  void add_object(const Shape& s) { drop(); objects_.push_back(GroupChild{std::make_shared<Shape>(s), nullptr}); }  // :87-89
+  void add_object(const Group& g) { drop(); objects_.push_back(GroupChild{nullptr, std::make_shared<Group>(g)}); }
   void add_light(const PointLight& l) { drop(); lights_.push_back(l); }  // :83-85
   size_t n_objects() const { return objects_.size(); }
   size_t n_lights() const { return lights_.size(); }
-  Shape& object(size_t i) { drop(); return objects_.at(i); }
-  const Shape& object_c(size_t i) const { return objects_.at(i); }
-  PointLight& light(size_t i) { drop(); return lights_.at(i); }
-  std::vector<rt_shape_desc> descs() const {
-    std::vector<rt_shape_desc> v;
-    v.reserve(objects_.size());
-    for (const Shape& s : objects_) v.push_back(to_desc(s));
-    return v;
+  Shape& object(size_t i) {
+    drop();
+    if (!objects_.at(i).shape) throw std::invalid_argument("World::object: object is a Group");
+    return *objects_[i].shape;
   }
+  const Shape& object_c(size_t i) const {
+    if (!objects_.at(i).shape) throw std::invalid_argument("World::object: object is a Group");
+    return *objects_[i].shape;
+  }
+  PointLight& light(size_t i) { drop(); return lights_.at(i); }
+  // The flattened World (rt_scene_create_groups): the primitives in the order
+  // World::intersect's flat_map reaches them (group.rs:49-58: each group's
+  // children in order), the innermost group of each (-1: none), and the groups
+  // (their boxes, parents first).
+  struct Flat {
+    std::vector<rt_shape_desc> shapes;
+    std::vector<int32_t> shape_group;
+    std::vector<rt_group_desc> groups;
+  };
+  Flat flatten() const {
+    Flat f;
+    struct Walk {
+      Flat& f;
+      void node(const GroupChild& c, int32_t parent) {
+        if (c.shape) {
+          f.shapes.push_back(to_desc(*c.shape));
+          f.shape_group.push_back(parent);
+          return;
+        }
+        rt_group_desc g;
+        std::memset(&g, 0, sizeof g);
+        const BoundingBox& b = c.group->bbox;
+        g.min[0] = b.min.x; g.min[1] = b.min.y; g.min[2] = b.min.z;
+        g.max[0] = b.max.x; g.max[1] = b.max.y; g.max[2] = b.max.z;
+        g.parent = parent;
+        f.groups.push_back(g);
+        const int32_t me = (int32_t)f.groups.size() - 1;
+        for (const GroupChild& k : c.group->children) node(k, me);
+      }
+    } w{f};
+    for (const GroupChild& c : objects_) w.node(c, -1);
+    return f;
+  }
+  std::vector<rt_shape_desc> descs() const { return flatten().shapes; }
   std::vector<rt_light_desc> light_descs() const {
     std::vector<rt_light_desc> v(lights_.size());
     for (size_t i = 0; i < lights_.size(); ++i) {
@@ -281,10 +411,11 @@ class World {
     if (device < 0) device = scene_ ? scene_device_ : 0;
     if (!scene_ || scene_device_ != device) {
       const_cast<World*>(this)->drop();
-      auto d = descs();
+      const Flat f = flatten();
       auto l = light_descs();
       rt_scene* s = nullptr;
-      check(rt_scene_create(d.data(), d.size(), l.data(), l.size(), device, &s), "rt_scene_create");
+      check(rt_scene_create_groups(f.shapes.data(), f.shapes.size(), f.shape_group.data(), f.groups.data(),
+                                   f.groups.size(), l.data(), l.size(), device, &s), "rt_scene_create");
       scene_ = s;
       scene_device_ = device;
     }
@@ -315,7 +446,7 @@ class World {
     if (scene_) rt_scene_destroy(scene_);
     scene_ = nullptr;
   }
-  std::vector<Shape> objects_;
+  std::vector<GroupChild> objects_;
   std::vector<PointLight> lights_;
   mutable rt_scene* scene_ = nullptr;
   mutable int scene_device_ = -1;

@@ -209,9 +209,33 @@ PYBIND11_MODULE(_rtamd, m) {
       .def_readonly("transform_inverse", &Shape::transform_inverse)
       .def("transform_inverse_transpose", &Shape::transform_inverse_transpose)
       .def("set_transform", &Shape::set_transform)
+      .def("set_material", &Shape::set_material)
       .def("no_shadow", &Shape::no_shadow)
       .def("has_shadow", &Shape::has_shadow)
+      .def("get_bounds", [](const Shape& s) { return py::make_tuple(s.bbox.min, s.bbox.max); })
+      .def("parent_space_bounds", [](const Shape& s) {
+        const BoundingBox b = s.parent_space_bounds();
+        return py::make_tuple(b.min, b.max);
+      })
       .def("desc_bytes", [](const Shape& s) { rt_shape_desc d = to_desc(s); return pod_bytes(&d, sizeof d); });
+  // geometry/shape/group.rs: children by value (a copy of the shape or group is moved in, as
+  // add_child takes its Box); child(i) returns a copy of child i
+  py::class_<Group>(m, "Group")
+      .def(py::init<>())
+      .def("add_child", [](Group& g, const Shape& s) { g.add_child(s); })
+      .def("add_child", [](Group& g, const Group& c) { g.add_child(c); })
+      .def("set_transform", &Group::set_transform)
+      .def("set_material", &Group::set_material)
+      .def_readonly("transform", &Group::transform)
+      .def_readonly("transform_inverse", &Group::transform_inverse)
+      .def_readonly("material", &Group::material)
+      .def("n_children", [](const Group& g) { return g.children.size(); })
+      .def("child", [](const Group& g, size_t i) -> py::object {
+        const GroupChild& c = g.children.at(i);
+        if (c.shape) return py::cast(*c.shape);
+        return py::cast(*c.group);
+      })
+      .def("get_bounds", [](const Group& g) { return py::make_tuple(g.bbox.min, g.bbox.max); });
   m.def("Sphere", &Sphere);
   m.def("glass_sphere", &glass_sphere);
   m.def("Plane", &Plane);
@@ -289,7 +313,8 @@ PYBIND11_MODULE(_rtamd, m) {
   py::class_<World>(m, "World")
       .def(py::init<>())
       .def_static("default", &World::make_default)
-      .def("add_object", &World::add_object)
+      .def("add_object", [](World& w, const Shape& s) { w.add_object(s); })
+      .def("add_object", [](World& w, const Group& g) { w.add_object(g); })
       .def("add_light", &World::add_light)
       .def("n_objects", &World::n_objects)
       .def("n_lights", &World::n_lights)
@@ -312,6 +337,11 @@ PYBIND11_MODULE(_rtamd, m) {
         auto d = w.descs();
         return pod_bytes(d.data(), d.size() * sizeof(rt_shape_desc));
       })
+      .def("groups_bytes", [](const World& w) {  // rt_group_desc[], parents first
+        auto f = w.flatten();
+        return pod_bytes(f.groups.data(), f.groups.size() * sizeof(rt_group_desc));
+      })
+      .def("shape_groups", [](const World& w) { return w.flatten().shape_group; })  // innermost group per shape
       .def("lights_bytes", [](const World& w) {
         auto l = w.light_descs();
         return pod_bytes(l.data(), l.size() * sizeof(rt_light_desc));

@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <exception>
+#include <functional>
 #include <new>
 #include <chrono>
 #include <cmath>
@@ -155,6 +156,10 @@ struct rt_scene {
     size_t ppm_rows_cap = 0;  // rows
     void* h_stage[2] = {nullptr, nullptr};  // device-to-host copies into caller memory: two pinned chunks
     hipEvent_t stage_ev[2] = {nullptr, nullptr};
+    // banded host renders (render_banded): a stream per band after the first, and the
+    // events that start each band when the previous band's render is done
+    hipStream_t band_stream[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t band_ev[4] = {nullptr, nullptr, nullptr, nullptr};
     bool busy = false;
   };
   std::deque<HostCtx> ctxs;  // deque: a context's address survives the pool's growth
@@ -218,6 +223,13 @@ struct rt_scene {
         if (c.h_stage[k]) (void)hipHostFree(c.h_stage[k]);
         if (c.stage_ev[k]) (void)hipEventDestroy(c.stage_ev[k]);
       }
+      for (hipStream_t bs : c.band_stream)
+        if (bs) {
+          (void)hipStreamSynchronize(bs);
+          (void)hipStreamDestroy(bs);
+        }
+      for (hipEvent_t be : c.band_ev)
+        if (be) (void)hipEventDestroy(be);
     }
   }
   // A host context for one call (under `mu`); returned by release_ctx.
@@ -864,10 +876,27 @@ int rt_camera_init(uint32_t hsize, uint32_t vsize, double field_of_view, const d
 int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light_desc* lights,
                     size_t n_lights, int device, rt_scene** out) {
   return guarded([&]() -> int {
-  if (!out || (n_shapes && !shapes) || (n_lights && !lights))
+  return rt_scene_create_groups(shapes, n_shapes, nullptr, nullptr, 0, lights, n_lights, device, out);
+  });
+}
+
+int rt_scene_create_groups(const rt_shape_desc* shapes, size_t n_shapes, const int32_t* shape_group,
+                           const rt_group_desc* groups, size_t n_groups, const rt_light_desc* lights,
+                           size_t n_lights, int device, rt_scene** out) {
+  return guarded([&]() -> int {
+  if (!out || (n_shapes && !shapes) || (n_lights && !lights) || (n_groups && (!groups || !shape_group)))
     return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
   *out = nullptr;
   if (n_shapes > (size_t)(1u << 29)) return fail(RT_ERR_INVALID_ARGUMENT, "too many shapes");
+  if (n_groups > (size_t)(1u << 24)) return fail(RT_ERR_INVALID_ARGUMENT, "too many groups");
+  for (size_t g = 0; g < n_groups; ++g)
+    if (groups[g].parent < -1 || groups[g].parent >= (int32_t)g)
+      return fail(RT_ERR_INVALID_ARGUMENT, "group " + std::to_string(g) + ": its parent must be -1 or an earlier group");
+  // a shape's gate: 1 + its innermost group (0: none)
+  auto gate_of = [&](size_t i) -> int32_t { return shape_group && n_groups ? shape_group[i] + 1 : 0; };
+  for (size_t i = 0; i < n_shapes; ++i)
+    if (gate_of(i) < 0 || gate_of(i) > (int32_t)n_groups)
+      return fail(RT_ERR_INVALID_ARGUMENT, "shape " + std::to_string(i) + ": bad group index");
   for (size_t i = 0; i < n_shapes; ++i) {
     if (shapes[i].kind < RT_SHAPE_SPHERE || shapes[i].kind > RT_SHAPE_CONE)
       return fail(RT_ERR_UNSUPPORTED_SHAPE, "shape " + std::to_string(i) +
@@ -893,8 +922,9 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   for (size_t i = 0; i < n_shapes; ++i) {
     const rt_shape_desc& d = shapes[i];
     const int64_t meta = ((int64_t)i << 1) | (d.casts_shadow ? 1 : 0);
+    const int32_t gate = gate_of(i);  // shapes inside groups: general records with their group gate
     if (d.kind == RT_SHAPE_SPHERE) {
-      if (is_diag_inverse(d.inverse)) {
+      if (is_diag_inverse(d.inverse) && gate == 0) {
         SphereDiag r{};
         r.s[0] = d.inverse[0]; r.s[1] = d.inverse[5]; r.s[2] = d.inverse[10];
         r.t[0] = d.inverse[3]; r.t[1] = d.inverse[7]; r.t[2] = d.inverse[11];
@@ -904,12 +934,14 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
         SphereGen r{};
         for (int e = 0; e < 12; ++e) r.m[e] = d.inverse[e];
         r.meta = meta;
+        r.gate = gate;
         gen.push_back(r);
       }
     } else if (d.kind == RT_SHAPE_PLANE) {
       PlaneRec r{};
       for (int e = 0; e < 4; ++e) r.m[e] = d.inverse[4 + e];
       r.meta = meta;
+      r.gate = gate;
       planes.push_back(r);
     } else {
       QuadRec r{};
@@ -919,6 +951,7 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
       r.kind = d.kind;
       r.closed = d.closed ? 1 : 0;
       r.meta = (int32_t)meta;
+      r.gate = gate;
       quads.push_back(r);
     }
     ShadeRec& s = shade[i];
@@ -958,17 +991,23 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   std::vector<SphereGen> fx_gen;
   std::vector<QuadRec> fx_quads;
   double blo[3], bhi[3];
+  // (shapes inside groups stay outside the hierarchy: their group gate goes with them)
   for (const SphereGen& g : gen) {
     OtherRec r{};
     for (int e = 0; e < 12; ++e) r.m[e] = g.m[e];
     r.kind = 0;
     r.meta = (int32_t)g.meta;
-    if (other_box(r, blo, bhi)) orec.push_back(r);
+    if (g.gate == 0 && other_box(r, blo, bhi)) orec.push_back(r);
     else fx_gen.push_back(g);
   }
   for (const QuadRec& q : quads) {
-    if (other_box(q, blo, bhi)) orec.push_back(q);
+    if (q.gate == 0 && other_box(q, blo, bhi)) orec.push_back(q);
     else fx_quads.push_back(q);
+  }
+  std::vector<GroupRec> grec(n_groups);
+  for (size_t g = 0; g < n_groups; ++g) {
+    for (int c = 0; c < 3; ++c) { grec[g].lo[c] = groups[g].min[c]; grec[g].hi[c] = groups[g].max[c]; }
+    grec[g].parent = groups[g].parent + 1;
   }
   int obvh_depth = 0;
   std::vector<BvhNode> obvh = build_other_bvh(orec, leaf, &obvh_depth, g_bvh_ct / 100.0);
@@ -1015,7 +1054,8 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   const size_t o_lv = align(o_lc + lb.cells.size() * sizeof(LbCell));
   const size_t o_ld = align(o_lv + (lb.ov.size() + 1) * sizeof(uint16_t));
   const size_t o_ll = align(o_ld + lb.delta.size() * sizeof(float));
-  const size_t total = align(o_ll + lb.limit.size() * sizeof(float)) + 256;
+  const size_t o_gr = align(o_ll + lb.limit.size() * sizeof(float));
+  const size_t total = align(o_gr + grec.size() * sizeof(GroupRec)) + 256;
   std::vector<unsigned char> host(total, 0);
   if (!diag.empty()) std::memcpy(&host[o_diag], diag.data(), diag.size() * sizeof(SphereDiag));
   if (!gen.empty()) std::memcpy(&host[o_gen], gen.data(), gen.size() * sizeof(SphereGen));
@@ -1034,6 +1074,7 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
     std::memcpy(&host[o_rt + i * 2 * sizeof(double)], rt2, sizeof rt2);
   }
   if (!lrec.empty()) std::memcpy(&host[o_li], lrec.data(), lrec.size() * sizeof(LightRec));
+  if (!grec.empty()) std::memcpy(&host[o_gr], grec.data(), grec.size() * sizeof(GroupRec));
   if (!lb.cells.empty()) {
     std::memcpy(&host[o_lc], lb.cells.data(), lb.cells.size() * sizeof(LbCell));
     if (!lb.ov.empty()) std::memcpy(&host[o_lv], lb.ov.data(), lb.ov.size() * sizeof(uint16_t));
@@ -1096,6 +1137,8 @@ int rt_scene_create(const rt_shape_desc* shapes, size_t n_shapes, const rt_light
   s->dev.shade = (const ShadeRec*)(b + o_sh);
   s->dev.refl_transp = (const double*)(b + o_rt);
   s->dev.lights = (const LightRec*)(b + o_li);
+  s->dev.groups = (const GroupRec*)(b + o_gr);
+  s->dev.n_groups = (int32_t)n_groups;
   s->dev.n_diag = (int32_t)diag.size();
   s->dev.n_gen = (int32_t)gen.size();
   s->dev.n_planes = (int32_t)planes.size();
@@ -1167,8 +1210,12 @@ int rt_render_shard_device_ex(const rt_scene* scene, const rt_camera_desc* camer
   });
 }
 
+static bool valid_pattern(uint32_t period, uint64_t mask) {
+  return period >= 1 && period <= 64 && mask != 0 && (period == 64 || (mask >> period) == 0);
+}
+
 uint32_t rt_pattern_rows(uint32_t vsize, uint32_t row_block, uint32_t period, uint64_t mask) {
-  if (row_block == 0 || period == 0 || period > 64 || mask == 0 || (period < 64 && (mask >> period) != 0)) return 0;
+  if (row_block == 0 || !valid_pattern(period, mask)) return 0;
   uint32_t rows = 0;
   for (uint64_t blk = 0; blk * row_block < vsize; ++blk)
     if ((mask >> (blk % period)) & 1u) rows += std::min<uint32_t>(row_block, vsize - (uint32_t)(blk * row_block));
@@ -1184,7 +1231,7 @@ int render_frames(const rt_scene* scene, const rt_camera_desc* cameras, uint32_t
   if (!scene || (n_frames && (!cameras || !d_out_rgb))) return fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
   if (row_block == 0 || n_shards == 0 || shard >= n_shards)
     return fail(RT_ERR_INVALID_ARGUMENT, "bad shard specification");
-  if (blk_period && rt_pattern_rows(1u << 30, 1, blk_period, blk_mask) == 0)
+  if (blk_period && !valid_pattern(blk_period, blk_mask))
     return fail(RT_ERR_INVALID_ARGUMENT, "bad block pattern (period 1..64, a non-empty mask below 2^period)");
   if (!valid_aa(aa_samples)) return fail(RT_ERR_INVALID_ARGUMENT, "aa_samples must be 1, 2, 4, 8 or 16");
   for (uint32_t f = 0; f < n_frames; ++f) {
@@ -1269,6 +1316,113 @@ int rt_render_block_pattern_device(const rt_scene* scene, const rt_camera_desc* 
   });
 }
 
+namespace {
+// `Camera::render` into a host canvas with the device-to-host copy overlapped
+// (rt_render_ex): the frame's rows are cut into `bands`
+// contiguous bands of 64-block patterns (rt_render_block_pattern_device's
+// mapping with one period over the whole canvas). Band k renders on its own
+// stream (its own workspace), starting when band k-1's render is done, so the
+// GPU works on one band at a time as in a whole-frame render, and band k's copy
+// to the host runs behind its render while band k+1 renders. Every pixel is
+// that of the whole-frame render (a pattern only chooses which rows a render
+// owns). The caller's canvas must be pinned (rt_host_buffer_alloc) or
+// registrable for the call (d2h = 1); RT_ERR_NO_DEVICE asks the caller for
+// the one-render path. A band that overflowed its arenas is rendered again,
+// synchronously, before the call returns (every synchronous call returns a
+// complete frame).
+int render_banded(rt_scene* s, std::unique_lock<std::mutex>& lk, rt_scene::HostCtx* c, const rt_camera_desc& cam,
+                  uint32_t max_depth, uint32_t aa, double* out_rgb) {
+  const uint32_t W = cam.hsize, H = cam.vsize;
+  const int bands = std::max(2, std::min(4, s->tune.bands));
+  const uint32_t rb = (H + 63) / 64, nb = (H + rb - 1) / rb;  // nb <= 64 blocks of rb rows: one period
+  if (nb < (uint32_t)bands * 2) return RT_ERR_NO_DEVICE;
+  // band k = blocks [b[k], b[k+1]): the first band takes band_pct of the rows, the rest share the remainder
+  uint32_t b[5] = {0, 0, 0, 0, 0};
+  b[1] = std::max<uint32_t>(1, std::min<uint32_t>(nb - (uint32_t)bands + 1, (uint32_t)((uint64_t)nb * s->tune.band_pct / 100)));
+  for (int k = 2; k < bands; ++k) b[k] = b[k - 1] + std::max<uint32_t>(1, (nb - b[1]) / (uint32_t)(bands - 1));
+  b[bands] = nb;
+  const size_t bytes = (size_t)W * H * 3 * sizeof(double);
+  bool registered = false;
+  if (!pinned_block(out_rgb, bytes)) {
+    if (s->tune.d2h != 1 || hipHostRegister(out_rgb, bytes, hipHostRegisterDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      return RT_ERR_NO_DEVICE;  // (a buffer the DMA engine cannot write: the one-render path stages it)
+    }
+    registered = true;
+  }
+  struct Unregister {
+    void* p;
+    bool on;
+    ~Unregister() {
+      if (on && hipHostUnregister(p) != hipSuccess) (void)hipGetLastError();
+    }
+  } unreg{out_rgb, registered};
+  hipStream_t st[4] = {c->stream, nullptr, nullptr, nullptr};
+  for (int k = 1; k < bands; ++k) {
+    if (!c->band_stream[k - 1]) RT_HIP(hipStreamCreateWithFlags(&c->band_stream[k - 1], hipStreamNonBlocking));
+    st[k] = c->band_stream[k - 1];
+  }
+  for (int k = 0; k < bands; ++k)
+    if (!c->band_ev[k]) RT_HIP(hipEventCreateWithFlags(&c->band_ev[k], hipEventDisableTiming));
+  const DevCamera dc = to_dev_camera(cam);
+  const uint64_t all = nb == 64 ? ~0ull : ((1ull << nb) - 1ull);
+  rt_scene::WfSlot* used[4] = {nullptr, nullptr, nullptr, nullptr};
+  auto unpin = [&](int k) {
+    if (used[k]) {
+      --used[k]->pins;
+      used[k] = nullptr;
+    }
+  };
+  struct UnpinAll {
+    std::function<void()> f;
+    ~UnpinAll() { f(); }
+  } unpin_all{[&]() {
+    if (!lk.owns_lock()) lk.lock();
+    for (int k = 0; k < bands; ++k) unpin(k);
+  }};
+  uint32_t y0[5];
+  for (int k = 0; k <= bands; ++k) y0[k] = std::min(H, b[k] * rb);
+  auto mask_of = [&](int k) {
+    const uint64_t below_end = b[k + 1] >= 64 ? ~0ull : ((1ull << b[k + 1]) - 1ull);
+    const uint64_t below_start = (1ull << b[k]) - 1ull;
+    return all & below_end & ~below_start;
+  };
+  for (int k = 0; k < bands; ++k) {
+    if (k > 0) RT_HIP(hipStreamWaitEvent(st[k], c->band_ev[k - 1], 0));  // band k after band k-1's render
+    const uint32_t rows = y0[k + 1] - y0[k];
+    int rc = run_render(s, dc, nullptr, rows * W * aa, aa, max_depth, rb, 0, 1, c->d_out + (size_t)y0[k] * W * 3, st[k],
+                        nullptr, nullptr, 0, &used[k], nullptr, 1, false, &lk, false, true, nb, mask_of(k));
+    if (rc != RT_OK) return rc;
+    RT_HIP(hipEventRecord(c->band_ev[k], st[k]));
+    RT_HIP(hipMemcpyAsync(out_rgb + (size_t)y0[k] * W * 3, c->d_out + (size_t)y0[k] * W * 3,
+                          (size_t)rows * W * 3 * sizeof(double), hipMemcpyDeviceToHost, st[k]));
+  }
+  lk.unlock();  // the workspaces stay pinned to this call
+  for (int k = 0; k < bands; ++k) RT_HIP(hipStreamSynchronize(st[k]));
+  lk.lock();
+  for (int k = 0; k < bands; ++k) {
+    if (!used[k]) continue;
+    used[k]->wf->learn(s->sizing);
+    bool over = false;
+    RT_HIP(used[k]->wf->take_overflow(&over));
+    unpin(k);
+    if (!over) continue;
+    // (its canvas rows are NaN: render the band again, synchronously, with the arenas grown)
+    const uint32_t rows = y0[k + 1] - y0[k];
+    int rc = run_render(s, dc, nullptr, rows * W * aa, aa, max_depth, rb, 0, 1, c->d_out + (size_t)y0[k] * W * 3,
+                        st[k], nullptr, nullptr, 0, nullptr, nullptr, 1, true, &lk, false, false, nb, mask_of(k));
+    if (rc != RT_OK) return rc;
+    RT_HIP(hipMemcpyAsync(out_rgb + (size_t)y0[k] * W * 3, c->d_out + (size_t)y0[k] * W * 3,
+                          (size_t)rows * W * 3 * sizeof(double), hipMemcpyDeviceToHost, st[k]));
+    lk.unlock();
+    const hipError_t e = hipStreamSynchronize(st[k]);
+    lk.lock();
+    if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("banded render: ") + hipGetErrorString(e));
+  }
+  return RT_OK;
+}
+}  // namespace
+
 int rt_render_aa(const rt_scene* scene, const rt_camera_desc* camera, uint32_t max_depth, uint32_t aa_samples,
                  double* out_rgb, rt_stats* stats) {
   return guarded([&]() -> int {
@@ -1292,6 +1446,12 @@ int rt_render_ex(const rt_scene* scene, const rt_camera_desc* camera, uint32_t m
   RT_TAKE_CTX(cx);
   int rc = ensure_dev_buffer(&cx.c->d_out, &cx.c->out_cap, n_pix * 3);
   if (rc != RT_OK) return rc;
+  // a large frame without counters: bands, each band's copy behind its render (render_banded)
+  if (!stats && flags == 0 && s->tune.bands > 1 && s->tune.accel != 0 && (s->dev.n_bvh > 0 || s->dev.n_obvh > 0) &&
+      n_pix * aa_samples >= ((uint64_t)1 << 20)) {
+    rc = render_banded(s, lk, cx.c, *camera, max_depth, aa_samples, out_rgb);
+    if (rc != RT_ERR_NO_DEVICE) return rc;  // (RT_ERR_NO_DEVICE: not bandable, render it whole below)
+  }
   DevStats ds{};
   float ms = 0.f;
   rc = run_render(s, to_dev_camera(*camera), nullptr, (uint32_t)(n_pix * aa_samples), aa_samples, max_depth,

@@ -54,6 +54,7 @@ typedef const RT_CONST SphereDiag* cSphereDiag;
 typedef const RT_CONST SphereGen* cSphereGen;
 typedef const RT_CONST PlaneRec* cPlaneRec;
 typedef const RT_CONST QuadRec* cQuadRec;
+typedef const RT_CONST GroupRec* cGroupRec;
 typedef const RT_CONST LightRec* cLightRec;
 
 typedef double d2 __attribute__((ext_vector_type(2)));  // ds_read_b128 operand
@@ -250,6 +251,48 @@ __device__ __forceinline__ void quad_test(QP q, V3 o, V3 d, Hit& h) {
   if (!SHADOW && (n_neg & 1)) push_container(h, neg_t, k0 + neg_i);
 }
 
+// BoundingBox::intersects (bounding_box.rs:95-136) of a Group's box, with the
+// reference's operations: per axis (min - o) / d and (max - o) / d, or, when
+// |d| < EPSILON, the numerators times infinity (0 * inf = NaN), swapped when
+// reversed; then f64::max / f64::min, which ignore a NaN operand (fmax / fmin).
+__device__ __forceinline__ void bbox_check_axis(double origin, double direction, double mn, double mx, double& t0,
+                                                double& t1) {
+  const double tmin_numerator = mn - origin, tmax_numerator = mx - origin;
+  double tmin, tmax;
+  if (fabs(direction) >= kEpsilon) {
+    tmin = tmin_numerator / direction;
+    tmax = tmax_numerator / direction;
+  } else {
+    tmin = tmin_numerator * INFINITY;
+    tmax = tmax_numerator * INFINITY;
+  }
+  if (tmin > tmax) { t0 = tmax; t1 = tmin; } else { t0 = tmin; t1 = tmax; }
+}
+__device__ __forceinline__ bool bbox_intersects(cGroupRec g, V3 o, V3 d) {
+  double x0, x1, y0, y1, z0, z1;
+  bbox_check_axis(o.x, d.x, g->lo[0], g->hi[0], x0, x1);
+  bbox_check_axis(o.y, d.y, g->lo[1], g->hi[1], y0, y1);
+  bbox_check_axis(o.z, d.z, g->lo[2], g->hi[2], z0, z1);
+  const double tmin = fmax(fmax(x0, y0), z0), tmax = fmin(fmin(x1, y1), z1);
+  return tmin <= tmax;
+}
+// Group::intersect (group.rs:49-58): a shape inside groups is intersected only
+// when the ray meets the box of every group around it, innermost first (the
+// reference tests them outermost first and stops at the first miss; either
+// order gives the same answer). `gate` = the record's gate (0: no group).
+// A shape that fails it adds no intersection and no local_intersect call.
+__device__ __forceinline__ bool group_gate(const DevScene& sc, int gate, V3 o, V3 d) {
+  const cGroupRec groups = (cGroupRec)sc.groups;
+  for (int g = gate; g > 0; g = groups[g - 1].parent)
+    if (!bbox_intersects(groups + (g - 1), o, d)) return false;
+  return true;
+}
+// Shapes a group's box kept out of a ray's World::intersect, by kind (the
+// counted launches subtract them from the reference's rays x shapes).
+struct GateSkips {
+  unsigned sph = 0, plane = 0, other = 0;
+};
+
 // The records outside the sphere BVH (general-transform spheres, planes,
 // cubes / cylinders / cones), tested exhaustively from global memory.
 // QUADS = false compiles the solids out (kernel variants for scenes without
@@ -257,10 +300,15 @@ __device__ __forceinline__ void quad_test(QP q, V3 o, V3 d, Hit& h) {
 // FAST: the fast path's remainder (the records outside both hierarchies;
 // the other bounded records are traversed by other_trace).
 template <bool SHADOW, bool QUADS = true, bool FAST = false>
-__device__ __forceinline__ void trace_rest(const DevScene& sc, V3 o, V3 d, Hit& h, unsigned& n_disc) {
+__device__ __forceinline__ void trace_rest(const DevScene& sc, V3 o, V3 d, Hit& h, unsigned& n_disc,
+                                           GateSkips* skips = nullptr) {
   cSphereGen sg = (cSphereGen)(FAST ? sc.fx_gen : sc.sph_gen);
   const int n_gen = FAST ? sc.n_fx_gen : sc.n_gen;
   for (int j = 0; j < n_gen; ++j) {
+    if (sg[j].gate && !group_gate(sc, sg[j].gate, o, d)) {
+      if (skips) ++skips->sph;
+      continue;
+    }
     double m[12];
 #pragma unroll
     for (int e = 0; e < 12; ++e) m[e] = sg[j].m[e];
@@ -271,6 +319,10 @@ __device__ __forceinline__ void trace_rest(const DevScene& sc, V3 o, V3 d, Hit& 
   }
   cPlaneRec pl = (cPlaneRec)sc.planes;
   for (int j = 0; j < sc.n_planes; ++j) {
+    if (pl[j].gate && !group_gate(sc, pl[j].gate, o, d)) {
+      if (skips) ++skips->plane;
+      continue;
+    }
     const double oy = pl[j].m[0] * o.x + pl[j].m[1] * o.y + pl[j].m[2] * o.z + pl[j].m[3];
     const double dy = pl[j].m[0] * d.x + pl[j].m[1] * d.y + pl[j].m[2] * d.z;
     plane_test<SHADOW>(oy, dy, (int)pl[j].meta, h);
@@ -278,7 +330,13 @@ __device__ __forceinline__ void trace_rest(const DevScene& sc, V3 o, V3 d, Hit& 
   if constexpr (QUADS) {
     cQuadRec qr = (cQuadRec)(FAST ? sc.fx_quads : sc.quads);
     const int n_quads = FAST ? sc.n_fx_quads : sc.n_quads;
-    for (int j = 0; j < n_quads; ++j) quad_test<SHADOW>(qr + j, o, d, h);
+    for (int j = 0; j < n_quads; ++j) {
+      if (qr[j].gate && !group_gate(sc, qr[j].gate, o, d)) {
+        if (skips) ++skips->other;
+        continue;
+      }
+      quad_test<SHADOW>(qr + j, o, d, h);
+    }
   }
 }
 
@@ -311,11 +369,12 @@ __device__ __forceinline__ void diag_test(cSphereDiag r, V3 o, V3 d, Hit& h, uns
 // loads): the batch entry points (rt_hit_batch, rt_is_shadowed_batch) and
 // the wavefront fallback when the trace image does not fit in LDS.
 template <bool SHADOW>
-__device__ __forceinline__ void trace(const DevScene& sc, V3 o, V3 d, Hit& h, unsigned& n_disc) {
+__device__ __forceinline__ void trace(const DevScene& sc, V3 o, V3 d, Hit& h, unsigned& n_disc,
+                                      GateSkips* skips = nullptr) {
   hit_init(h);
   cSphereDiag sd = (cSphereDiag)sc.sph_diag;
   for (int j = 0; j < sc.n_diag; ++j) diag_test<SHADOW>(sd + j, o, d, h, n_disc);
-  trace_rest<SHADOW>(sc, o, d, h, n_disc);
+  trace_rest<SHADOW>(sc, o, d, h, n_disc, skips);
   hit_finish(h);
 }
 

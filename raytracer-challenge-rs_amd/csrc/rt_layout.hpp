@@ -26,22 +26,37 @@ struct alignas(64) SphereDiag {  // translation . axis scaling (e.g. all C3/C5 s
   int64_t meta;
   int64_t pad;
 };
+// `gate`: 0, or 1 + the innermost Group the shape belongs to (GroupRec): the
+// shape is tested only by rays that meet the bounding box of that group and of
+// every group enclosing it (Group::intersect, group.rs:49-58; group_gate).
+// Shapes inside groups are always one of these three records.
 struct alignas(64) SphereGen {  // any invertible affine transform
   double m[12];                 // inverse rows 0..2
   int64_t meta;
-  int64_t pad[3];
+  int32_t gate, pad0;
+  int64_t pad[2];
 };
 struct alignas(64) PlaneRec {
   double m[4];  // inverse row 1: m10 m11 m12 m13
   int64_t meta;
-  int64_t pad[3];
+  int32_t gate, pad0;
+  int64_t pad[2];
 };
 struct alignas(64) QuadRec {  // cube.rs / cylinder.rs / cone.rs
   double m[12];  // inverse rows 0..2
   double minimum, maximum;
   int32_t kind, closed;
-  int32_t meta, pad;
+  int32_t meta, gate;
 };
+// A Group's bounding box as the reference's Group::intersect tests it
+// (BaseShape::bounding_box of the group, bounding_box.rs:95-136), and 1 + the
+// group enclosing it (0: a top-level group of World::objects).
+struct alignas(64) GroupRec {
+  double lo[3], hi[3];
+  int32_t parent, pad0;
+  int64_t pad;
+};
+static_assert(sizeof(GroupRec) == 64, "GroupRec must stay 64 B");
 static_assert(sizeof(QuadRec) == 128, "QuadRec must stay 128 B");
 
 // Bounding-volume hierarchies (built on the host, rt_bvh.cpp): one over the
@@ -193,6 +208,9 @@ struct DevScene {
   // per object: ShadeRec::reflective, transparency (what wf_combine_parents reads; 16 B a
   // record, so the table stays in the L2 where the 512-B shading records may not)
   const double* refl_transp;
+  // Groups (group.rs): the records' gates index this table (rt_scene_create_groups)
+  const GroupRec* groups;
+  int32_t n_groups, pad_groups;
 };
 
 struct DevCamera {

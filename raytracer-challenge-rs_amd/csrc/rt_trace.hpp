@@ -811,10 +811,10 @@ __device__ __forceinline__ void lb_walk(const DevScene& sc, SD sd, const float* 
 template <int LANE, bool QUADS>
 __device__ __forceinline__ bool shadow_trace(const DevScene& sc, unsigned use_lb, const LaneScene& ls, unsigned l,
                                              V3 o, V3 d, double dist, unsigned& n_disc, unsigned& n_tests,
-                                             unsigned& n_boxes) {
+                                             unsigned& n_boxes, GateSkips* skips = nullptr) {
   Hit h;
   hit_init(h);
-  trace_rest<true, QUADS, true>(sc, o, d, h, n_disc);
+  trace_rest<true, QUADS, true>(sc, o, d, h, n_disc, skips);
   if constexpr (QUADS) other_trace<true>(sc, o, d, dist, h, n_disc, n_tests, n_boxes);
   if (!(h.key >= 0 && h.t < dist)) {
     if (use_lb) {

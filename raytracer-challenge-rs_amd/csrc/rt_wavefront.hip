@@ -40,7 +40,8 @@ int wf_tuning_apply(WfTuning& t, const char* key, int value) {
       {"prim_lane", &WfTuning::prim_lane, 0, 2},   {"arena_pct", &WfTuning::arena_pct, 1, 100},
       {"wide", &WfTuning::wide, 0, 1},
       {"lds_wide", &WfTuning::lds_wide, 0, 1},
-      {"d2h", &WfTuning::d2h, 0, 1}};
+      {"d2h", &WfTuning::d2h, 0, 1},               {"bands", &WfTuning::bands, 1, 4},
+      {"band_pct", &WfTuning::band_pct, 5, 95}};
   if (!key) return 0;
   for (const Knob& k : knobs) {
     if (std::strcmp(key, k.name) != 0) continue;
@@ -388,7 +389,7 @@ __device__ WfLds wf_lds_stage(const DevScene& sc, const PrimRec* prim, unsigned 
 // padding records, so record j+1 always exists.
 template <bool PRIMARY, bool SHADOW, bool QUADS>
 __device__ __forceinline__ void wf_trace_lds(const DevScene& sc, const WfLds& lv, V3 o, V3 d, Hit& h,
-                                             unsigned& n_disc) {
+                                             unsigned& n_disc, GateSkips& sk) {
   hit_init(h);
   const d2* r = (const d2*)lv.diag;
   if constexpr (PRIMARY) {
@@ -431,6 +432,8 @@ __device__ __forceinline__ void wf_trace_lds(const DevScene& sc, const WfLds& lv
                           a1.x * d.z, [&] { return lv.diag_meta[j]; }, h, n_disc);
   }
   for (int j = 0; j < sc.n_gen; ++j) {
+    const int gate = ((cSphereGen)sc.sph_gen)[j].gate;  // (shapes inside groups: group_gate)
+    if (gate && !group_gate(sc, gate, o, d)) { ++sk.sph; continue; }
     double m[12];
 #pragma unroll
     for (int e = 0; e < 12; ++e) m[e] = lv.gen[12 * j + e];
@@ -440,14 +443,31 @@ __device__ __forceinline__ void wf_trace_lds(const DevScene& sc, const WfLds& lv
     sphere_test<SHADOW>(lo.x, lo.y, lo.z, ld.x, ld.y, ld.z, [&] { return lv.gen_meta[j]; }, h, n_disc);
   }
   for (int j = 0; j < sc.n_planes; ++j) {  // plane.rs:53-60
+    const int gate = ((cPlaneRec)sc.planes)[j].gate;
+    if (gate && !group_gate(sc, gate, o, d)) { ++sk.plane; continue; }
     const double m0 = lv.plane[4 * j], m1 = lv.plane[4 * j + 1], m2 = lv.plane[4 * j + 2], m3 = lv.plane[4 * j + 3];
     plane_test<SHADOW>(m0 * o.x + m1 * o.y + m2 * o.z + m3, m0 * d.x + m1 * d.y + m2 * d.z, lv.plane_meta[j], h);
   }
   if constexpr (QUADS) {
     cQuadRec qr = (cQuadRec)sc.quads;  // cubes / cylinders / cones: scalar loads
-    for (int j = 0; j < sc.n_quads; ++j) quad_test<SHADOW>(qr + j, o, d, h);
+    for (int j = 0; j < sc.n_quads; ++j) {
+      if (qr[j].gate && !group_gate(sc, qr[j].gate, o, d)) { ++sk.other; continue; }
+      quad_test<SHADOW>(qr + j, o, d, h);
+    }
   }
   hit_finish(h);
+}
+
+// The counted launches' group skips (GateSkips), summed per wave into the
+// calling wave's counter row.
+__device__ __forceinline__ void add_gate_skips(WfCounters* cnt, const GateSkips& sk) {
+  const unsigned long long a = wave_sum(sk.sph), b = wave_sum(sk.plane), c = wave_sum(sk.other);
+  if (lane_id() == 0 && (a | b | c)) {
+    WfWorkRow* w = work_row(cnt);
+    if (a) atomicAdd(&w->gated[0], a);
+    if (b) atomicAdd(&w->gated[1], b);
+    if (c) atomicAdd(&w->gated[2], c);
+  }
 }
 
 // ---------------------------------------------------------- trace kernels
@@ -455,6 +475,7 @@ template <bool USE_LDS, bool PRIMARY, bool QUADS, int TW>
 __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest(DevScene sc, DevCamera cam, WfArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   unsigned n_disc = 0;
+  GateSkips sk;
   WfLds lv{};
   if constexpr (USE_LDS) lv = wf_lds_stage<PRIMARY>(sc, a.prim, lds_raw);
   __shared__ unsigned s_pre[kPreRays];
@@ -465,14 +486,15 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_closest(DevScene sc,
     V3 o, d;
     wf_ray(a, cam, slot, o, d);
     Hit h;
-    if constexpr (USE_LDS) wf_trace_lds<PRIMARY, false, QUADS>(sc, lv, o, d, h, n_disc);
-    else trace<false>(sc, o, d, h, n_disc);
+    if constexpr (USE_LDS) wf_trace_lds<PRIMARY, false, QUADS>(sc, lv, o, d, h, n_disc, sk);
+    else trace<false>(sc, o, d, h, n_disc, &sk);
     WfHit w;
     w.t = h.t; w.key = h.key; w.c1k = h.c1k; w.c2k = h.c2k; w.hin = h.hin;
     a.hits[slot] = w;
   }
   const unsigned long long s = wave_sum(n_disc);
   if (lane_id() == 0 && s) atomicAdd(&work_row(a.cnt)->disc[a.disc_slot], s);
+  if (sc.n_groups) add_gate_skips(a.cnt, sk);
 }
 
 // World::is_shadowed (world.rs:95-105): shadowed iff some shadow-casting
@@ -483,6 +505,7 @@ template <bool USE_LDS, bool QUADS, int TW>
 __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow(DevScene sc, WfArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   unsigned n_disc = 0;
+  GateSkips sk;
   WfLds lv{};
   if constexpr (USE_LDS) lv = wf_lds_stage<false>(sc, nullptr, lds_raw);
   __shared__ unsigned s_pre[kPreList];
@@ -494,12 +517,13 @@ __global__ __launch_bounds__(kTraceBlock, TW) void wf_trace_shadow(DevScene sc, 
     unsigned slot;
     shadow_ray(sc, a, shard_slot<false>(pre, a.sh_cap, i), o, d, dist, slot);
     Hit h;
-    if constexpr (USE_LDS) wf_trace_lds<false, true, QUADS>(sc, lv, o, d, h, n_disc);
-    else trace<true>(sc, o, d, h, n_disc);
+    if constexpr (USE_LDS) wf_trace_lds<false, true, QUADS>(sc, lv, o, d, h, n_disc, sk);
+    else trace<true>(sc, o, d, h, n_disc, &sk);
     shadow_result(sc, a, slot, h.key >= 0 && h.t < dist, o, d);
   }
   const unsigned long long s = wave_sum(n_disc);
   if (lane_id() == 0 && s) atomicAdd(&work_row(a.cnt)->disc[a.disc_slot], s);
+  if (sc.n_groups) add_gate_skips(a.cnt, sk);
 }
 
 // The classes of a node's children in the next generation's queue (shard_append):
@@ -711,6 +735,7 @@ __device__ __forceinline__ unsigned bind_generation(WfArgs& a, const unsigned* p
 
 // Per-lane tallies of a fused trace kernel (summed per wave at the end).
 struct FusedTally {
+  GateSkips gsk;                                     // shapes groups kept out of a ray (counted launches)
   unsigned disc = 0, tests = 0, boxes = 0;           // closest-hit work
   unsigned sh_disc = 0, sh_tests = 0, sh_boxes = 0;  // shadow-ray work
   unsigned sh_rays = 0;                              // shadow rays traced
@@ -788,7 +813,7 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
       // the light is behind the surface: lighting() is the ambient term either way
     } else {
       const bool shadowed = shadow_trace<LANE, QUADS>(sc, a.use_lb, ls, l, c.over, sdir, dist, t.sh_disc, t.sh_tests,
-                                                      t.sh_boxes);
+                                                      t.sh_boxes, &t.gsk);
       ++t.sh_rays;
       term = lighting(*m, Lr, c.over, c.eyev, c.normal, shadowed, sdir);
     }
@@ -874,11 +899,11 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
         const unsigned pf = a.n_frames > 1 ? (c * 64u) / a.frame_rays : 0u;
         bvh_trace<PRIMARY, false>(sc, (cPrimRec)(a.prim + (size_t)pf * ((unsigned)sc.n_diag + 4)), stk, o, d, 0.0, h,
                                   t.disc, t.tests, t.boxes);
-        trace_rest<false, QUADS, true>(sc, o, d, h, t.disc);
+        trace_rest<false, QUADS, true>(sc, o, d, h, t.disc, &t.gsk);
         if constexpr (QUADS) other_trace<false>(sc, o, d, 0.0, h, t.disc, t.tests, t.boxes);
       } else {
         // planes and the other records first: an early nearest hit tightens the culling
-        trace_rest<false, QUADS, true>(sc, o, d, h, t.disc);
+        trace_rest<false, QUADS, true>(sc, o, d, h, t.disc, &t.gsk);
         if constexpr (QUADS) other_trace<false>(sc, o, d, 0.0, h, t.disc, t.tests, t.boxes);
         if constexpr (LANE == 14) {
           lane_trace_pair<false>(ls.nodes, ls.s48, ls.M, sc.n_bvh > 0, o, d, 0.0, h, t.disc, t.tests, t.boxes,
@@ -911,6 +936,7 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
     c = dyn ? c_base + X * (unsigned)__shfl((int)k_next, 0, 64) : c + W;
   }
   if constexpr (!TALLY) return;
+  if (sc.n_groups) add_gate_skips(a.cnt, t.gsk);
   const unsigned long long s = wave_sum(t.disc), st = wave_sum(t.tests), sb = wave_sum(t.boxes);
   const unsigned long long hs = wave_sum(t.sh_disc), hst = wave_sum(t.sh_tests), hsb = wave_sum(t.sh_boxes);
   const unsigned long long hr = wave_sum(t.sh_rays);
@@ -1551,7 +1577,9 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
   const bool count = stats != nullptr || (flags & WF_COUNT) != 0;
   const bool bvh = tn.accel != 0 && !exhaustive && (sc.n_bvh > 0 || sc.n_obvh > 0);
   const bool fused = bvh;
-  const bool skip_shadow = !exhaustive && tn.skip_shadow != 0;
+  // (a counted render of a scene with groups traces every shadow ray: the reference's shape
+  // tests then come from the group gates each ray met, GateSkips)
+  const bool skip_shadow = !exhaustive && tn.skip_shadow != 0 && !(count && sc.n_groups > 0);
   // a batch of frames: the fast path's generations over every frame's root
   // rays (uncounted camera renders only; the caller renders others one by one)
   const unsigned frame_real = n0;
@@ -1937,16 +1965,17 @@ hipError_t Wavefront::read_stats(DevStats* out) {
   const unsigned long long shadows = hits * (unsigned long long)lr_.L;
   s.rays_primary = lr_.n0;
   s.rays_shadow = shadows;
-  s.sphere_tests = (rays + shadows) * (lr_.n_diag + lr_.n_gen);
-  s.plane_tests = (rays + shadows) * lr_.n_planes;
-  s.other_tests = (rays + shadows) * lr_.n_quads;
+  // (minus the shapes whose group's box a ray missed: Group::intersect never calls them)
+  s.sphere_tests = (rays + shadows) * (lr_.n_diag + lr_.n_gen) - hc.gated(0);
+  s.plane_tests = (rays + shadows) * lr_.n_planes - hc.gated(1);
+  s.other_tests = (rays + shadows) * lr_.n_quads - hc.gated(2);
   s.sphere_disc_ge0 = lr_.exact_disc ? hc.disc(0) + hc.disc(1) + hc.disc(2) : ~0ull;
   s.exhaustive = lr_.exact_disc ? 1u : 0u;
   // what the kernels did
   s.rays_shadow_traced = traced_shadows;
   const unsigned long long traced = rays + traced_shadows;
-  s.sphere_tests_executed = lr_.bvh ? hc.tests(0) + hc.tests(1) + hc.tests(2) + traced * lr_.n_gen
-                                    : traced * (lr_.n_diag + lr_.n_gen);
+  s.sphere_tests_executed = (lr_.bvh ? hc.tests(0) + hc.tests(1) + hc.tests(2) + traced * lr_.n_gen
+                                     : traced * (lr_.n_diag + lr_.n_gen)) - hc.gated(0);
   s.box_tests_executed = hc.boxes(0) + hc.boxes(1) + hc.boxes(2);
   *out = s;
   return hipSuccess;

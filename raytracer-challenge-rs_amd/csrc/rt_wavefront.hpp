@@ -105,6 +105,10 @@ struct WfTuning {
   int arena_pct = 100;     // test hook: the fast path's queue arenas sized to this percentage of the hint,
                            //     shrinking them (< 100: forces overflows, DESIGN.md "Device-sized generations")
   int d2h = 1;             // host-canvas copies: 1 = pin the caller's buffer for the call and DMA into it, 0 = pinned chunks
+  int bands = 2;           // rt_render into a host canvas: row bands rendered one after the other on two streams, each
+                           //     band's device-to-host copy overlapping the next band's render (1 = one render, then
+                           //     one copy)
+  int band_pct = 55;       // ... the first band's share of the rows (percent)
 };
 // Applies `key` = `value` to `t`: 1 = applied, 0 = not a render-time key, -1 = bad value.
 int wf_tuning_apply(WfTuning& t, const char* key, int value);
@@ -129,6 +133,7 @@ struct alignas(128) WfWorkRow {
   unsigned long long boxes[3];  // BVH mode: child-box tests executed (lanes x boxes)
   unsigned long long sh_rays[2];   // fused kernels: shadow rays traced, [0] primary / [1] secondary launches
   unsigned long long sh_tests[2];  // fused kernels: shadow sphere tests executed, per launch class
+  unsigned long long gated[3];     // shapes a group's box kept out of a ray: spheres, planes, others (GateSkips)
 };
 // Fused launches hand out their rays in chunks of 64 (one wave-iteration) from
 // per-XCD counters, kChunkClasses per generation, each on a 128-B line.
@@ -164,6 +169,11 @@ struct WfCounters {
   unsigned long long sh_tests(int c) const {
     unsigned long long t = 0;
     for (int r = 0; r < kWorkRows; ++r) t += work[r].sh_tests[c];
+    return t;
+  }
+  unsigned long long gated(int c) const {
+    unsigned long long t = 0;
+    for (int r = 0; r < kWorkRows; ++r) t += work[r].gated[c];
     return t;
   }
 };

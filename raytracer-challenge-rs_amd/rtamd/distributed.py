@@ -75,12 +75,15 @@ def root_share_default(config, n_ranks):
     should equal the other ranks' render time. Measured on one MI355X for C3
     (profiles/r05_assembly_n8.txt): a row block of an N-way shard renders in
     about 0.0060-0.0067 ms per frame, the un-interleave costs 0.020 ms per frame
-    and the receive of 7 shards 0.014 ms, which gives 0.97 / 0.91 / 0.74 of an
-    equal share at N = 2 / 4 / 8. C5 frames are 57x longer, so its assembly is
-    within a few per cent of a rank's work: an equal split."""
+    and the receive of 7 shards 0.014-0.015 ms, which gives about 0.97 / 0.9 /
+    0.7 of an equal share at N = 2 / 4 / 8; at N = 8, 0.68 (2 of every 23 blocks
+    against 3) balanced rank 0 (0.109 ms per frame with its emulated receive and
+    un-interleave) with the busiest other rank (0.109 ms), where 0.75 left rank
+    0 at 0.123 ms. C5 frames are 57x longer, so its assembly is within a few
+    per cent of a rank's work: an equal split."""
     if config != "c3" or n_ranks <= 1:
         return 1.0
-    return {2: 0.97, 4: 0.9, 8: 0.75}.get(n_ranks, max(0.6, 1.0 - 0.034 * n_ranks))
+    return {2: 0.97, 4: 0.9, 8: 0.68}.get(n_ranks, max(0.6, 1.0 - 0.04 * n_ranks))
 
 
 def rank_row_ids(height, row_block, rank, n_ranks, pattern=None):

@@ -365,4 +365,119 @@ def solids(width=160, height=120):
     return w, _camera(width, height, PI / 3.0, (0.0, 2.0, -5.5), (0, 0.8, 0)), 6
 
 
-CONFIGS = {"c1": c1, "c2": c2, "c3": c3, "c5": c5, "zoo": zoo, "first_scene": first_scene, "solids": solids}
+def _hexagon_side():
+    """bin/hexagon.rs:45-69: a corner sphere and an edge cylinder in a group."""
+    corner = rt.Sphere()
+    corner.set_transform(rt.translation(0, 0, -1) * rt.scaling(0.25, 0.25, 0.25))
+    edge = rt.Cylinder(0.0, 1.0, False)
+    edge.set_transform(rt.Matrix.identity(4, 4).scale(0.25, 1.0, 0.25).rotate_z(-PI / 2.0).rotate_y(-PI / 6.0)
+                       .translate(0, 0, -1))
+    side = rt.Group()
+    side.add_child(corner)
+    side.add_child(edge)
+    return side
+
+
+def hexagon(width=2560, height=1440):
+    """The reference demo bin/hexagon.rs:23-87: six groups (a sphere and an open
+    cylinder each) rotated about y inside a hexagon group, a checkers material
+    set on the whole hierarchy, the hexagon scaled by 1.5; two lights;
+    Camera::render (depth 5)."""
+    hexa = rt.Group()
+    for n in range(6):
+        side = _hexagon_side()
+        side.set_transform(rt.rotation_y(n * PI / 3.0))
+        hexa.add_child(side)
+    m = rt.Material()
+    m.set_pattern(rt.checkers_pattern(rt.Color(1.0, 0.0, 0.0), rt.Color(0.0, 1.0, 0.0)))
+    hexa.set_material(m)
+    hexa.set_transform(rt.scaling(1.5, 1.5, 1.5))
+    w = rt.World()
+    w.add_light(rt.PointLight(rt.Point(-10, 10, -10), rt.Color(1.0, 1.0, 1.0)))
+    w.add_light(rt.PointLight(rt.Point(-5.0, 10.0, -6.0), rt.Color(0.33, 0.33, 0.33)))
+    w.add_object(hexa)
+    return w, _camera(width, height, PI / 3.0, (0.0, 2.5, -5.0), (0, 0, 0)), 5
+
+
+def groups(width=160, height=120):
+    """Group coverage (group.rs, bounding_box.rs): nested groups with their own
+    transforms, set_material on an inner group, a glass sphere and a glass cube
+    in a group (containers across group members), a cone and a cube in a
+    rotated group, a group holding a plane (a plane's box turns NaN under
+    set_transform, so the group's box is its other child's and the plane is
+    seen only through that box: the reference's own quirk), shapes added after
+    set_transform and set_material, and ungrouped shapes beside them."""
+    w = rt.World()
+    floor = rt.Plane()
+    floor.material.set_pattern(rt.checkers_pattern(rt.Color(0.8, 0.8, 0.8), rt.Color(0.3, 0.3, 0.4)))
+    floor.material.reflective = 0.2
+    w.add_object(floor)
+    # outer (translated) > inner (rotated, reflective material) > glass sphere + glass cube
+    inner = rt.Group()
+    gs = rt.glass_sphere()
+    gs.set_transform(rt.translation(0.0, 1.0, 0.0) * rt.scaling(0.7, 0.7, 0.7))
+    inner.add_child(gs)
+    gc = rt.Cube()
+    gc.set_transform(rt.translation(0.6, 0.9, -0.4) * rt.scaling(0.35, 0.35, 0.35))
+    gc.material.transparency = 0.9
+    gc.material.refractive_index = 1.3
+    inner.add_child(gc)
+    inner.set_transform(rt.rotation_y(0.4))
+    glass = rt.Material()
+    glass.transparency = 0.8
+    glass.reflective = 0.7
+    glass.refractive_index = 1.45
+    glass.color = rt.Color(0.05, 0.1, 0.1)
+    glass.diffuse = 0.2
+    glass.specular = 0.9
+    glass.shininess = 200.0
+    inner.set_material(glass)  # both members, recursively (group.rs:96-102)
+    outer = rt.Group()
+    outer.add_child(inner)
+    cyl = rt.Cylinder(0.0, 1.5, True)
+    cyl.set_transform(rt.translation(-1.6, 0.0, 0.5) * rt.scaling(0.3, 1.0, 0.3))
+    cyl.material.color = rt.Color(0.9, 0.5, 0.1)
+    outer.add_child(cyl)
+    outer.set_transform(rt.translation(-0.8, 0.0, 0.6))  # (after its children: baked into them)
+    w.add_object(outer)
+    # a rotated group: cone + cube, material set on the group, then one more child
+    rot = rt.Group()
+    cone = rt.Cone(-1.0, 0.0, True)
+    cone.set_transform(rt.translation(0.0, 1.0, 0.0) * rt.scaling(0.4, 1.0, 0.4))
+    rot.add_child(cone)
+    cube = rt.Cube()
+    cube.set_transform(rt.translation(0.6, 0.3, 0.0) * rt.scaling(0.3, 0.3, 0.3))
+    rot.add_child(cube)
+    rot.set_transform(rt.translation(1.6, 0.0, -0.2) * rt.rotation_y(-0.7) * rt.rotation_z(0.2))
+    mm = rt.Material()
+    mm.set_pattern(rt.stripe_pattern(rt.Color(1.0, 0.9, 0.2), rt.Color(0.2, 0.4, 1.0)))
+    mm.reflective = 0.3
+    rot.set_material(mm)
+    late = rt.Sphere()
+    late.set_transform(rt.translation(0.0, 2.2, 0.0) * rt.scaling(0.3, 0.3, 0.3))
+    late.material.color = rt.Color(0.9, 0.1, 0.1)
+    rot.add_child(late)
+    w.add_object(rot)
+    # a group with a plane and a small sphere: the plane shows only inside the sphere's box
+    pg = rt.Group()
+    wall = rt.Plane()
+    wall.set_transform(rt.translation(0.0, 0.0, 4.0) * rt.rotation_x(PI / 2.0))
+    wall.material.color = rt.Color(0.2, 0.8, 0.3)
+    pg.add_child(wall)
+    ball = rt.Sphere()
+    ball.set_transform(rt.translation(0.3, 1.6, 3.0) * rt.scaling(0.8, 0.8, 0.8))
+    ball.material.reflective = 0.5
+    pg.add_child(ball)
+    w.add_object(pg)
+    free = rt.Sphere()
+    free.set_transform(rt.translation(0.2, 0.35, -1.6) * rt.scaling(0.35, 0.35, 0.35))
+    free.material.color = rt.Color(0.2, 0.3, 0.9)
+    free.material.reflective = 0.4
+    w.add_object(free)
+    w.add_light(rt.PointLight(rt.Point(-6, 8, -8), rt.Color(1.0, 1.0, 1.0)))
+    w.add_light(rt.PointLight(rt.Point(4.0, 5.0, -5.0), rt.Color(0.35, 0.35, 0.35)))
+    return w, _camera(width, height, PI / 3.0, (0.0, 2.2, -5.5), (0, 0.9, 0)), 6
+
+
+CONFIGS = {"c1": c1, "c2": c2, "c3": c3, "c5": c5, "zoo": zoo, "first_scene": first_scene, "solids": solids,
+           "hexagon": hexagon, "groups": groups}

@@ -350,3 +350,31 @@ def test_arena_overflow_batch_poisoned(rt, aa):
         w.check()
         for b in bufs:
             assert torch.equal(b, exact)
+
+
+@pytest.mark.parametrize("bands,pct", [(2, 55), (3, 40), (4, 25), (1, 55)])
+def test_host_render_banded_bitwise(rt, bands, pct):
+    """rt_render into a host canvas (Camera::render -> Canvas, camera.rs:133-148)
+    of the full 1920x1080 C3 frame in row bands, each band's device-to-host copy
+    behind its render: bitwise the exhaustive frame, into a
+    pageable and into a pinned canvas; with arenas forced to overflow, every band
+    is still complete (re-rendered before the call returns)."""
+    import torch
+    from rtamd import scenes
+    w, cam, depth = scenes.c3()
+    exact, _ = _device_frame(cam, w, depth, True)
+    ref = exact.cpu().numpy().tobytes()
+    w.tune("bands", bands)
+    w.tune("band_pct", pct)
+    try:
+        for _ in range(2):
+            host, _ = cam.render(w, depth, want_stats=False)
+            assert host.to_numpy().tobytes() == ref
+        w.tune("arena_pct", 30)
+        host, _ = cam.render(w, depth, want_stats=False)
+        assert host.to_numpy().tobytes() == ref
+    finally:
+        w.tune("arena_pct", 100)
+        w.tune("bands", 2)
+        w.tune("band_pct", 55)
+    w.check()

@@ -23,8 +23,8 @@ DOC = os.path.join(REPO, "INTEGRATION.md")
 LIB = os.path.join(PKG, "lib", "librtamd.so")
 
 STRUCTS = {"RtShapeDesc": "rt_shape_desc", "RtLightDesc": "rt_light_desc", "RtCameraDesc": "rt_camera_desc",
-           "RtStats": "rt_stats"}
-SIZES = {"rt_shape_desc": 680, "rt_light_desc": 48, "rt_camera_desc": 160, "rt_stats": 112}
+           "RtStats": "rt_stats", "RtGroupDesc": "rt_group_desc"}
+SIZES = {"rt_shape_desc": 680, "rt_light_desc": 48, "rt_camera_desc": 160, "rt_stats": 112, "rt_group_desc": 56}
 
 RUST_SCALAR = {"i32": ctypes.c_int32, "u32": ctypes.c_uint32, "u64": ctypes.c_uint64, "f64": ctypes.c_double,
                "usize": ctypes.c_size_t, "u8": ctypes.c_uint8, "c_int": ctypes.c_int32}

@@ -45,7 +45,8 @@ EXPECTED = [
     "intersect_constrained_cylinder", "intersect_caps_closed_cylinder", "normal_vector_on_cylinder_end_cap",
     "bounded_cylinder_bounding_box", "intersect_cone_with_ray", "intersect_cone_parallel_to_half",
     "intersect_cone_end_caps", "computing_normal_vector_cone", "bounded_cone_bounding_box",
-    "rays_for_pixel_offsets",
+    "rays_for_pixel_offsets", "bounding_box_intersects_cube_at_origin", "bounding_box_intersects_non_cubic",
+    "group_box_gates_its_children"
 ]
 
 

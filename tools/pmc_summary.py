@@ -23,7 +23,10 @@ def klass(n):
     """Kernel class of a demangled name: primary / closest / shadow / prep /
     combine / frame (wf_frame_init: one per rendered frame)."""
     if "wf_trace_fused<" in n:  # fused generation: closest hit + shading + shadow rays + spawn
-        return "primary" if _targs(n, "wf_trace_fused")[0] == "true" else "closest"
+        # generation 0 of a camera render: PRIMARY (the wave traversal) or CAM (the per-lane
+        # walks over the LDS images read camera rays: template argument 5)
+        t = _targs(n, "wf_trace_fused")
+        return "primary" if t[0] == "true" or (len(t) >= 5 and t[4] == "true") else "closest"
     if "wf_trace_closest_bvh<" in n:
         return "primary" if _targs(n, "wf_trace_closest_bvh")[0] == "true" else "closest"
     if "wf_trace_closest<" in n:

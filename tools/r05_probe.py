@@ -67,6 +67,18 @@ def e2e(reps):
         cam.render(w, depth, want_stats=False)
         ts.append((time.perf_counter() - t0) * 1e3)
     out["rt_render_ms"] = ts
+    for bands, pct in ((1, 55), (2, 50), (2, 55), (2, 60), (3, 40), (3, 50), (4, 34)):  # rt_render's row bands
+        w.tune("bands", bands)
+        w.tune("band_pct", pct)
+        cam.render(w, depth, want_stats=False)
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            cam.render(w, depth, want_stats=False)
+            ts.append((time.perf_counter() - t0) * 1e3)
+        out[f"rt_render_bands{bands}_{pct}_ms"] = sorted(ts)[len(ts) // 2]
+    w.tune("bands", 2)
+    w.tune("band_pct", 55)
     ref = dev.clone()
     streams = [rtamd.render_stream(False) for _ in range(2)]
     for K in (2, 3, 4, 6, 8):
@@ -119,47 +131,68 @@ def e2e(reps):
     return out
 
 
-def assembly(reps):
+def assembly(reps, share=None):
+    """Rank 0's cost at N = 8 on C3, measured on one GPU: rank 0's rows and a full
+    rank's rows rendered alone in the bench's regime (batches of 16 on 4 streams),
+    then rank 0's rows with its receive emulated (the 7 peers' shards of each batch
+    copied into its gather buffer by a side stream, 7 x ~6.3 MB per frame) and the
+    un-interleave (index_select through the inverse row map) behind each batch, as
+    RcclStreamAssembler queues it. `share`: rank 0's share of an equal split (block
+    patterns, rtamd.distributed.block_patterns); None = the plain interleave."""
+    from rtamd.distributed import block_patterns
     w, cam, depth = scenes.c3()
     w.upload(0)
     w.tune("shadow_stream", 0)
     H, W, B, N, NB, F = cam.vsize, cam.hsize, 8, 8, 16, 4
-    out = {"config": "C3 1920x1080, N=8, 8-row blocks, batches of 16 on 4 streams"}
-    fa = StreamFrameAssembler(H, W, B, 0, N, torch.device("cuda", 0), slots=F, batch=NB)
+    pattern = block_patterns(N, share) if share is not None and share < 1.0 else None
+    out = {"config": "C3 1920x1080, N=8, 8-row blocks, batches of 16 on 4 streams",
+           "root_share": share if pattern else 1.0,
+           "pattern": {"period": pattern[0], "blocks_per_period": [bin(m).count("1") for m in pattern[1]]}
+           if pattern else None}
+    fa = StreamFrameAssembler(H, W, B, 0, N, torch.device("cuda", 0), slots=F, batch=NB, pattern=pattern)
     gb, cv = fa.gather_buf[0], fa.canvas[0]
     out["gather_buf_MB"] = gb.numel() * 8 / 1e6
     out["unweave_batch_ms"] = timeit(lambda: torch.index_select(gb, 0, fa.inv_batch, out=cv), reps)
     out["unweave_per_frame_ms"] = out["unweave_batch_ms"] / NB
     rstreams = [rtamd.render_stream(False) for _ in range(F)]
     rx_stream = torch.cuda.Stream()
-    shards = {}
-    for shard in (7, 6):
-        rows = rtamd.shard_rows(H, B, shard, N)
-        shards[shard] = [torch.empty((NB, rows, W, 3), dtype=torch.float64, device="cuda") for _ in range(F)]
-    peers = torch.empty((N - 1, NB * fa.max_rows, W, 3), dtype=torch.float64, device="cuda")
+
+    def rows_of(r):
+        if pattern:
+            return rtamd.pattern_rows(H, B, pattern[0], pattern[1][r])
+        return rtamd.shard_rows(H, B, N - 1 - r, N)
+
+    def render(r, cams, ptrs, st):
+        if pattern:
+            rtamd.render_block_pattern_device(w, cams, depth, B, pattern[0], pattern[1][r], ptrs, st)
+        else:
+            rtamd.render_frames_device(w, cams, depth, B, N - 1 - r, N, ptrs, st)
+    rmax = max(range(1, N), key=rows_of)  # the peer with the most rows
+    out["rows_rank0"], out["rows_peer_max"], out["peer_max_rank"] = rows_of(0), rows_of(rmax), rmax
+    out["rx_MB_per_frame"] = sum(rows_of(r) for r in range(1, N)) * W * 24 / 1e6
+    bufs = {r: [torch.empty((NB, rows_of(r), W, 3), dtype=torch.float64, device="cuda") for _ in range(F)]
+            for r in (0, rmax)}
+    peers = torch.empty(((N - 1) * NB * fa.max_rows, W, 3), dtype=torch.float64, device="cuda")
     frames = 64
 
-    def run(shard, rx=False, unweave=False):
+    def run(r, rx=False, unweave=False):
         for b in range(frames // NB):
             k = b % F
             rs = rstreams[k]
-            rtamd.render_frames_device(w, [cam] * NB, depth, B, shard, N,
-                                       [shards[shard][k][j].data_ptr() for j in range(NB)], rs.cuda_stream)
-            if rx:  # the 7 peers' shards of this batch land in the gather buffer (43.9 MB per frame)
+            render(r, [cam] * NB, [bufs[r][k][j].data_ptr() for j in range(NB)], rs.cuda_stream)
+            if rx:  # the 7 peers' shards of this batch land in the gather buffer
                 with torch.cuda.stream(rx_stream):
-                    fa.gather_buf[k][fa.max_rows * NB:].copy_(peers.view(-1, W, 3), non_blocking=True)
+                    fa.gather_buf[k][fa.max_rows * NB:].copy_(peers, non_blocking=True)
                 rs.wait_stream(rx_stream)
             if unweave:
                 with torch.cuda.stream(rs):
                     torch.index_select(fa.gather_buf[k], 0, fa.inv_batch, out=fa.canvas[k])
 
-    for label, shard, rx, uw in (("render_shard7", 7, False, False), ("render_shard6", 6, False, False),
-                                 ("shard7_rx", 7, True, False), ("shard7_rx_unweave", 7, True, True),
-                                 ("shard7_unweave", 7, False, True)):
-        out[label + "_ms_per_frame"] = timeit(lambda: run(shard, rx, uw), max(1, reps // 2)) / frames
-    out["rx_copy_alone_ms_per_frame"] = timeit(
-        lambda: fa.gather_buf[0][fa.max_rows * NB:].copy_(peers.view(-1, W, 3)), reps) / NB
-    out["whole_frame_ms"] = None
+    for label, r, rx, uw in (("render_rank0", 0, False, False), ("render_peer_max", rmax, False, False),
+                             ("rank0_rx", 0, True, False), ("rank0_unweave", 0, False, True),
+                             ("rank0_rx_unweave", 0, True, True)):
+        out[label + "_ms_per_frame"] = timeit(lambda: run(r, rx, uw), max(1, reps // 2)) / frames
+    out["rx_copy_alone_ms_per_frame"] = timeit(lambda: fa.gather_buf[0][fa.max_rows * NB:].copy_(peers), reps) / NB
     whole = [torch.empty((H, W, 3), dtype=torch.float64, device="cuda") for _ in range(8 * F)]
 
     def run_whole():
@@ -168,6 +201,18 @@ def assembly(reps):
             rtamd.render_frames_device(w, [cam] * 8, depth, B, 0, 1, [whole[k * 8 + j].data_ptr() for j in range(8)],
                                        rstreams[k].cuda_stream)
     out["whole_frame_ms"] = timeit(run_whole, max(1, reps // 2)) / frames
+    t_root = out["rank0_rx_unweave_ms_per_frame"]
+    t_peer = out["render_peer_max_ms_per_frame"]
+    out["projection"] = {
+        "rank0_ms": t_root, "peer_render_ms": t_peer, "frame_ms": max(t_root, t_peer),
+        "speedup_vs_1gpu": out["whole_frame_ms"] / max(t_root, t_peer),
+        "xgmi_ms_per_frame_at_64GBps_per_link": rows_of(rmax) * W * 24 / 64e9 * 1e3,
+        "xgmi_ms_per_frame_at_50GBps_per_link": rows_of(rmax) * W * 24 / 50e9 * 1e3,
+        "note": "one GPU: rank 0's receive is a device copy on a side stream; the peers' sends and the xGMI "
+                "link time (each peer's shard over its own link, overlapped with later batches) are not "
+                "measured: a peer's link carries rows_peer_max x W x 24 B per frame"}
+    del fa, bufs, peers, whole
+    torch.cuda.empty_cache()
     return out
 
 
@@ -204,10 +249,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--what", default="e2e,assembly,pow")
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--share", type=float, default=0.75, help="assembly_share: rank 0's share of an equal split")
     a = ap.parse_args()
     for what in a.what.split(","):
         t0 = time.perf_counter()
-        res = {"e2e": lambda: e2e(a.reps), "assembly": lambda: assembly(a.reps), "pow": pow_ulps}[what]()
+        res = {"e2e": lambda: e2e(a.reps), "assembly": lambda: assembly(a.reps),
+               "assembly_share": lambda: assembly(a.reps, a.share), "pow": pow_ulps}[what]()
         res["section"] = what
         res["seconds"] = round(time.perf_counter() - t0, 1)
         print(json.dumps(res), flush=True)
