@@ -15,6 +15,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../../include/rt_render.h"
@@ -93,12 +94,51 @@ struct BoundingBox {
     if (p.z < min.z) min.z = p.z;
   }
   void add_box(const BoundingBox& b) { add_point(b.min); add_point(b.max); }  // :61-64
+  bool contains_point(const Point& p) const {  // :66-70 (RangeInclusive::contains: NaN is outside)
+    return min.x <= p.x && p.x <= max.x && min.y <= p.y && p.y <= max.y && min.z <= p.z && p.z <= max.z;
+  }
+  bool contains_box(const BoundingBox& b) const { return contains_point(b.min) && contains_point(b.max); }  // :72-74
   BoundingBox transform(const Matrix& m) const {  // :76-93
     const Point pts[8] = {min, Point(min.x, min.y, max.z), Point(min.x, max.y, min.z), Point(min.x, max.y, max.z),
                           Point(max.x, min.y, min.z), Point(max.x, min.y, max.z), Point(max.x, max.y, min.z), max};
     BoundingBox nb;
     for (const Point& p : pts) nb.add_point(m * p);
     return nb;
+  }
+  // :95-136, the same slab test as the device gate (rt_device.hpp bbox_intersects)
+  static void check_axis(double origin, double direction, double mn, double mx, double& t0, double& t1) {
+    const double n0 = mn - origin, n1 = mx - origin;
+    if (std::fabs(direction) >= EPSILON) {
+      t0 = n0 / direction;
+      t1 = n1 / direction;
+    } else {
+      t0 = n0 * kInf;
+      t1 = n1 * kInf;
+    }
+    if (t0 > t1) std::swap(t0, t1);
+  }
+  bool intersects(const Ray& r) const {
+    double x0, x1, y0, y1, z0, z1;
+    check_axis(r.origin.x, r.direction.x, min.x, max.x, x0, x1);
+    check_axis(r.origin.y, r.direction.y, min.y, max.y, y0, y1);
+    check_axis(r.origin.z, r.direction.z, min.z, max.z, z0, z1);
+    const double tmin = std::fmax(std::fmax(x0, y0), z0);  // f64::max / f64::min ignore a NaN operand
+    const double tmax = std::fmin(std::fmin(x1, y1), z1);
+    return tmin <= tmax;
+  }
+  // :138-169: halves along the widest axis (ties to x, then y, through `equal`)
+  std::pair<BoundingBox, BoundingBox> split() const {
+    const double dx = std::fabs(max.x - min.x), dy = std::fabs(max.y - min.y), dz = std::fabs(max.z - min.z);
+    const double greatest = std::fmax(std::fmax(dx, dy), dz);
+    double x0 = min.x, y0 = min.y, z0 = min.z, x1 = max.x, y1 = max.y, z1 = max.z;
+    if (equal(greatest, dx)) {
+      x0 = x1 = x0 + dx / 2.0;
+    } else if (equal(greatest, dy)) {
+      y0 = y1 = y0 + dy / 2.0;
+    } else {
+      z0 = z1 = z0 + dz / 2.0;
+    }
+    return {BoundingBox(min, Point(x1, y1, z1)), BoundingBox(Point(x0, y0, z0), max)};
   }
 };
 
@@ -185,6 +225,11 @@ struct Group {
   void add_child(const Shape& s) { add(GroupChild{std::make_shared<Shape>(s), nullptr}); }  // group.rs:128-133
   void add_child(const Group& g) { add(GroupChild{nullptr, std::make_shared<Group>(g)}); }
   BoundingBox parent_space_bounds() const { return bbox.transform(Matrix::identity(4, 4)); }
+  // group.rs:108-122: children whose parent-space box fits one half of this box
+  // move into a new subgroup per half (partition_children :135-189,
+  // make_subgroup :191-197; the subgroup is pushed without widening this box),
+  // then every child group divides in turn
+  void divide(size_t threshold);
 
  private:
   void add(GroupChild c);
@@ -220,6 +265,29 @@ inline void Group::add(GroupChild c) {
   const BoundingBox cbox = c.shape ? c.shape->parent_space_bounds() : c.group->parent_space_bounds();
   bbox.add_box(cbox);
   children.push_back(std::move(c));
+}
+inline void Group::divide(size_t threshold) {
+  if (threshold <= children.size()) {
+    const std::pair<BoundingBox, BoundingBox> halves = bbox.split();
+    std::vector<GroupChild> part[2];
+    for (int h = 0; h < 2; ++h) {
+      const BoundingBox& hb = h ? halves.second : halves.first;
+      std::vector<GroupChild> keep;
+      for (GroupChild& c : children) {
+        const BoundingBox cb = c.shape ? c.shape->parent_space_bounds() : c.group->parent_space_bounds();
+        (hb.contains_box(cb) ? part[h] : keep).push_back(std::move(c));
+      }
+      children = std::move(keep);
+    }
+    for (int h = 0; h < 2; ++h) {
+      if (part[h].empty()) continue;
+      auto g = std::make_shared<Group>();
+      for (GroupChild& c : part[h]) g->add(std::move(c));
+      children.push_back(GroupChild{nullptr, std::move(g)});
+    }
+  }
+  for (GroupChild& c : children)
+    if (c.group) c.group->divide(threshold);
 }
 
 // canvas.rs:8-52 + image/ppm.rs

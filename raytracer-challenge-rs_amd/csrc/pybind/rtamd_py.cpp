@@ -212,11 +212,8 @@ PYBIND11_MODULE(_rtamd, m) {
       .def("set_material", &Shape::set_material)
       .def("no_shadow", &Shape::no_shadow)
       .def("has_shadow", &Shape::has_shadow)
-      .def("get_bounds", [](const Shape& s) { return py::make_tuple(s.bbox.min, s.bbox.max); })
-      .def("parent_space_bounds", [](const Shape& s) {
-        const BoundingBox b = s.parent_space_bounds();
-        return py::make_tuple(b.min, b.max);
-      })
+      .def("get_bounds", [](const Shape& s) { return s.bbox; })
+      .def("parent_space_bounds", &Shape::parent_space_bounds)
       .def("desc_bytes", [](const Shape& s) { rt_shape_desc d = to_desc(s); return pod_bytes(&d, sizeof d); });
   // geometry/shape/group.rs: children by value (a copy of the shape or group is moved in, as
   // add_child takes its Box); child(i) returns a copy of child i
@@ -235,7 +232,22 @@ PYBIND11_MODULE(_rtamd, m) {
         if (c.shape) return py::cast(*c.shape);
         return py::cast(*c.group);
       })
-      .def("get_bounds", [](const Group& g) { return py::make_tuple(g.bbox.min, g.bbox.max); });
+      .def("get_bounds", [](const Group& g) { return g.bbox; })
+      .def("parent_space_bounds", &Group::parent_space_bounds)
+      .def("divide", &Group::divide, py::arg("threshold"));
+  // bounding_box.rs: the box type behind Group culling
+  py::class_<BoundingBox>(m, "BoundingBox")
+      .def(py::init<>())
+      .def(py::init<const Point&, const Point&>())
+      .def_readwrite("min", &BoundingBox::min)
+      .def_readwrite("max", &BoundingBox::max)
+      .def("add_point", &BoundingBox::add_point)
+      .def("add_bounding_box", &BoundingBox::add_box)
+      .def("contains_point", &BoundingBox::contains_point)
+      .def("contains_bounding_box", &BoundingBox::contains_box)
+      .def("transform", &BoundingBox::transform)
+      .def("intersects", &BoundingBox::intersects)
+      .def("split", &BoundingBox::split);
   m.def("Sphere", &Sphere);
   m.def("glass_sphere", &glass_sphere);
   m.def("Plane", &Plane);

@@ -479,5 +479,37 @@ def groups(width=160, height=120):
     return w, _camera(width, height, PI / 3.0, (0.0, 2.2, -5.5), (0, 0.9, 0)), 6
 
 
+def divided(width=128, height=72, n=5, threshold=2, seed=11):
+    """Group::divide (group.rs:108-197, bounding_box.rs:138-169): an n x n x 2
+    lattice of small spheres, cubes and cylinders (shuffled, random materials,
+    some glass) in one group, divided with `threshold` into nested subgroups,
+    then translated (the translation is baked into every level); a floor
+    outside the group."""
+    import random
+    rnd = random.Random(seed)
+    g = rt.Group()
+    cells = [(i, j, k) for i in range(n) for j in range(n) for k in range(2)]
+    rnd.shuffle(cells)
+    for idx, (i, j, k) in enumerate(cells):
+        s = (rt.Sphere, rt.Cube, lambda: rt.Cylinder(-1.0, 1.0, True))[idx % 3]()
+        r = 0.22 + 0.1 * rnd.random()
+        s.set_transform(rt.translation(i - (n - 1) / 2.0, 0.4 + 0.9 * k, j * 0.9) * rt.scaling(r, r, r))
+        s.material.color = rt.Color(rnd.random(), rnd.random(), rnd.random())
+        s.material.reflective = 0.3 * rnd.random()
+        if idx % 7 == 3:
+            s.material.transparency = 0.8
+            s.material.refractive_index = 1.4
+        g.add_child(s)
+    g.divide(threshold)
+    g.set_transform(rt.translation(0.0, 0.0, 0.5))
+    w = rt.World()
+    floor = rt.Plane()
+    floor.material.set_pattern(rt.checkers_pattern(rt.Color(0.9, 0.9, 0.9), rt.Color(0.2, 0.2, 0.25)))
+    w.add_object(floor)
+    w.add_object(g)
+    w.add_light(rt.PointLight(rt.Point(-6, 8, -8), rt.Color(1.0, 1.0, 1.0)))
+    return w, _camera(width, height, PI / 3.0, (0.0, 3.5, -5.5), (0.0, 0.6, 1.5)), 5
+
+
 CONFIGS = {"c1": c1, "c2": c2, "c3": c3, "c5": c5, "zoo": zoo, "first_scene": first_scene, "solids": solids,
-           "hexagon": hexagon, "groups": groups}
+           "hexagon": hexagon, "groups": groups, "divided": divided}

@@ -14,7 +14,8 @@ Per case <name> (aa > 1: `render_multithreaded` with that many AA samples):
   index.json        per case: scene, size, depth, the exact counters, sha256
                     of the PPM and of the canvas bytes
 
-Run from the repo root:  python tests/golden/make_golden.py
+Run from the repo root:  python tests/golden/make_golden.py [case ...]
+(with case names, only those are regenerated and merged into index.json)
 """
 import hashlib
 import json
@@ -49,15 +50,25 @@ CASES = [
     ("solids_40x30_aa16", "solids", {"width": 40, "height": 30}, 16),
     ("c3_48x27_s100_aa2", "c3", {"width": 48, "height": 27, "n_spheres": 100}, 2),
     ("zoo_32x24_aa8", "zoo", {"width": 32, "height": 24}, 8),
+    # Group bounding-box gates (group.rs:60-75, bounding_box.rs:95-136)
+    ("hexagon_64x36", "hexagon", {"width": 64, "height": 36}),
+    ("groups_80x60", "groups", {"width": 80, "height": 60}),
+    ("groups_40x30_aa4", "groups", {"width": 40, "height": 30}, 4),
+    ("divided_96x54", "divided", {"width": 96, "height": 54}),
 ]
 COUNTERS = ("rays_primary", "rays_reflect", "rays_refract", "rays_shadow",
             "sphere_tests", "plane_tests", "sphere_disc_ge0", "other_tests")
 
 
-def main():
+def main(only=()):
     index = {}
+    if only:
+        with open(os.path.join(HERE, "index.json")) as f:
+            index = json.load(f)
     for case in CASES:
         name, kind, kw = case[:3]
+        if only and name not in only:
+            continue
         aa = case[3] if len(case) > 3 else 1
         w, cam, depth = scene(rtamd, kind, kw)
         ow = pyoracle.OracleWorld.from_world(w)
@@ -79,4 +90,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(tuple(sys.argv[1:]))

@@ -11,6 +11,9 @@ Sections (--what, comma separated):
             rank 0's shard with an emulated receive stream (7 x 6.27 MB per frame
             written into its gather buffer by a copy on a side stream) plus the
             un-interleave behind each batch
+  assembly_share  the same with rank 0 rendering a block pattern of --share of an
+            equal split (rtamd.distributed.block_patterns), projected N = 8 speedup
+  bands     rt_render into a host canvas per (bands, band_pct) knob pair, round-robin
   pow       channels of the fast frame that differ from the oracle (material.rs:76
             powf vs the device pow) on 4096 C3 and 2048 C5 pixels, and how close
             any channel's v*255 comes to a .5 rounding boundary of the PPM quantiser
@@ -129,6 +132,27 @@ def e2e(reps):
         out[f"band_1of{K}_render_ms"] = timeit(
             lambda: cam.render_shard_device(w, depth, rb, 0, K, dev.data_ptr(), s0.cuda_stream, False), reps)
     return out
+
+
+def bands(reps):
+    """rt_render (host canvas) on C3 per (bands, band_pct), round-robin over the
+    configurations so that clock drift hits all of them alike; median and min."""
+    w, cam, depth = scenes.c3()
+    w.upload(0)
+    cfgs = [(1, 50), (2, 55), (2, 60), (2, 65), (2, 70), (3, 40), (3, 45), (3, 50), (4, 35), (4, 40)]
+    ts = {c: [] for c in cfgs}
+    for c in cfgs:  # warm every configuration's workspaces
+        w.tune("bands", c[0])
+        w.tune("band_pct", c[1])
+        cam.render(w, depth, want_stats=False)
+    for _ in range(reps):
+        for c in cfgs:
+            w.tune("bands", c[0])
+            w.tune("band_pct", c[1])
+            t0 = time.perf_counter()
+            cam.render(w, depth, want_stats=False)
+            ts[c].append((time.perf_counter() - t0) * 1e3)
+    return {f"bands{b}_{p}": {"median_ms": sorted(v)[len(v) // 2], "min_ms": min(v)} for (b, p), v in ts.items()}
 
 
 def assembly(reps, share=None):
@@ -254,7 +278,8 @@ def main():
     for what in a.what.split(","):
         t0 = time.perf_counter()
         res = {"e2e": lambda: e2e(a.reps), "assembly": lambda: assembly(a.reps),
-               "assembly_share": lambda: assembly(a.reps, a.share), "pow": pow_ulps}[what]()
+               "assembly_share": lambda: assembly(a.reps, a.share), "pow": pow_ulps,
+               "bands": lambda: bands(a.reps)}[what]()
         res["section"] = what
         res["seconds"] = round(time.perf_counter() - t0, 1)
         print(json.dumps(res), flush=True)
