@@ -325,6 +325,7 @@ __device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDia
 // nothing would. Leaves are batched across the wave as in lane_trace.
 // SD: the sphere records (const SphereDiag* in global memory, or Sph48 in LDS);
 // ALL_LDS: every node is in `top` (LANE 15: the whole hierarchy in LDS).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 template <bool SHADOW, typename SD = const SphereDiag*, bool ALL_LDS = false>
 __device__ __forceinline__ void lane_trace_wide(const BvhWide* nodes, SD sd, const float* M,
                                                 bool has_bvh, V3 o, V3 d, double t_shadow, Hit& h, unsigned& n_disc,
@@ -350,6 +351,8 @@ __device__ __forceinline__ void lane_trace_wide(const BvhWide* nodes, SD sd, con
     offx |= (16u * a + (neg ? 0u : 48u)) << (8 * a);
   }
   asm volatile("" : "+v"(offe), "+v"(offx));
+  const f32x2 A[3] = {{sr.inv[0], -on[0]}, {sr.inv[1], -on[1]}, {sr.inv[2], -on[2]}};
+  const f32x2 B[2] = {{-of[0], -of[1]}, {-of[2], 0.0f}};
   if (e == 0u && !usable) {  // no axis can cull (empty slots' inverted boxes need one): every record
     e = kWideEmpty;
     for (int k = 0; k < n_records; ++k) {
@@ -383,16 +386,38 @@ __device__ __forceinline__ void lane_trace_wide(const BvhWide* nodes, SD sd, con
       }
       cc = *(__attribute__((address_space(1))) const u32x2*)(b + (n0 + 96u));
     }
+    // the 24 plane distances as 12 packed FMAs (v_pk_fma_f32: two lanes of
+    // binary32 fma per issue, each the fmaf of the scalar form); the per-ray
+    // constants are broadcast from register pairs by op_sel (A[a] = {inv, -on},
+    // B = {-of0, -of1}, {-of2, -}), so they take 10 registers, not 18
+    f32x2 tn[2][3], tx[2][3];
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        const f32x2 en = {__uint_as_float(E[a][2 * p]), __uint_as_float(E[a][2 * p + 1])};
+        const f32x2 ex = {__uint_as_float(X[a][2 * p]), __uint_as_float(X[a][2 * p + 1])};
+        asm("v_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "=v"(tn[p][a]) : "v"(en), "v"(A[a]));
+        if (a == 0)
+          asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(tx[p][a]) : "v"(ex), "v"(A[a]), "v"(B[0]));
+        else if (a == 1)
+          asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "=v"(tx[p][a]) : "v"(ex), "v"(A[a]), "v"(B[0]));
+        else
+          asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(tx[p][a]) : "v"(ex), "v"(A[a]), "v"(B[1]));
+      }
     unsigned key[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float t0 = fmaxf(fmaxf(fmaf(__uint_as_float(E[0][j]), sr.inv[0], -on[0]),
-                                   fmaf(__uint_as_float(E[1][j]), sr.inv[1], -on[1])),
-                             fmaxf(fmaf(__uint_as_float(E[2][j]), sr.inv[2], -on[2]), 0.0f));
-      float zt;  // (t_hi is canonical: no per-visit re-canonicalisation, as in lane_trace_pair)
-      asm("v_min_f32 %0, %1, %2" : "=v"(zt) : "v"(fmaf(__uint_as_float(X[2][j]), sr.inv[2], -of[2])), "v"(t_hi));
-      const float t1 = fminf(fminf(fmaf(__uint_as_float(X[0][j]), sr.inv[0], -of[0]),
-                                   fmaf(__uint_as_float(X[1][j]), sr.inv[1], -of[1])), zt);
+      const int p = j >> 1, c = j & 1;
+      // fmaxf(fmaxf(x, y), fmaxf(z, 0)) and fminf(fminf(x, y), fminf(z, t_hi)) as the
+      // compiler emits them (v_max_f32 / v_max3_f32, v_min_f32 / v_min3_f32: the
+      // same NaN-ignoring rule), written out because operands from an asm would
+      // otherwise be canonicalised first (a pk_fma never yields a signalling NaN)
+      float zn, zt, t0, t1;
+      asm("v_max_f32 %0, 0, %1" : "=v"(zn) : "v"(tn[p][2][c]));
+      asm("v_max3_f32 %0, %1, %2, %3" : "=v"(t0) : "v"(tn[p][0][c]), "v"(tn[p][1][c]), "v"(zn));
+      asm("v_min_f32 %0, %1, %2" : "=v"(zt) : "v"(tx[p][2][c]), "v"(t_hi));  // (t_hi is canonical)
+      asm("v_min3_f32 %0, %1, %2, %3" : "=v"(t1) : "v"(tx[p][0][c]), "v"(tx[p][1][c]), "v"(zt));
       key[j] = t0 <= t1 ? ((__float_as_uint(t0) & ~3u) | (unsigned)j) : ~0u;
     }
     n_boxes += 4;
@@ -451,7 +476,6 @@ __device__ __forceinline__ void lane_trace_wide(const BvhWide* nodes, SD sd, con
 // The pair image's child codes are 16-bit (rt_layout.hpp BvhPair: a node
 // index below 0x8000, a leaf 0x8000 | first << 3 | (count - 1), 0xFFFF
 // empty), so the per-lane LDS stack holds 16-bit entries.
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr int kPairEmpty = 0xFFFF;
 template <bool SHADOW>
 __device__ __forceinline__ void lane_trace_pair(const unsigned char* nodes, Sph48 sd, const float* M,
