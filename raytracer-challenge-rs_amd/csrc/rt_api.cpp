@@ -485,7 +485,8 @@ int run_render(rt_scene* s, const DevCamera& cam, const double* d_rays, uint32_t
                hipStream_t stream, DevStats* stats_out = nullptr, float* ms_out = nullptr, uint32_t flags = 0,
                rt_scene::WfSlot** used = nullptr, const FrameTable* batch = nullptr, unsigned n_frames = 1,
                bool sync = false, std::unique_lock<std::mutex>* lk = nullptr, bool count = false,
-               bool keep_pin = false, uint32_t blk_period = 0, uint64_t blk_mask = 0) {
+               bool keep_pin = false, uint32_t blk_period = 0, uint64_t blk_mask = 0,
+               hipEvent_t gen_ev = nullptr, int gen_ev_g = -1, bool* gen_ev_recorded = nullptr) {
   if (max_depth > (uint32_t)kMaxDepth)
     return fail(RT_ERR_INVALID_ARGUMENT, "max_depth > " + std::to_string(kMaxDepth));
   if (!valid_aa(aa)) return fail(RT_ERR_INVALID_ARGUMENT, "aa_samples must be 1, 2, 4, 8 or 16");
@@ -514,9 +515,14 @@ int run_render(rt_scene* s, const DevCamera& cam, const double* d_rays, uint32_t
   if (sync || keep_pin) ++w->pins;
   if (keep_pin && used) *used = w;
   for (int attempt = 0;; ++attempt) {
+    if (gen_ev) w->wf->set_gen_event(gen_ev, gen_ev_g);
     e = w->wf->render(s->dev, cam, d_rays == nullptr, d_rays, n_tasks, aa, max_depth, row_block, shard, n_shards,
                       d_out, stream, s->sizing, nullptr, nullptr, s->tune, s->wfs.size() == 1, wf_flags, batch,
                       n_frames, blk_period, blk_mask);
+    if (gen_ev) {
+      if (gen_ev_recorded) *gen_ev_recorded = w->wf->gen_event_recorded();
+      w->wf->set_gen_event(nullptr, -1);
+    }
     if (e == hipSuccess) e = hipEventRecord(w->done, stream);
     if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("wavefront render: ") + hipGetErrorString(e));
     if (!sync) break;
@@ -1390,10 +1396,14 @@ int render_banded(rt_scene* s, std::unique_lock<std::mutex>& lk, rt_scene::HostC
   for (int k = 0; k < bands; ++k) {
     if (k > 0) RT_HIP(hipStreamWaitEvent(st[k], c->band_ev[k - 1], 0));  // band k after band k-1's render
     const uint32_t rows = y0[k + 1] - y0[k];
+    // band k+1 starts after band k's render, or (band_gen >= 0) after its generation band_gen's launch
+    const bool early = s->tune.band_gen >= 0 && k + 1 < bands;
+    bool recorded = false;
     int rc = run_render(s, dc, nullptr, rows * W * aa, aa, max_depth, rb, 0, 1, c->d_out + (size_t)y0[k] * W * 3, st[k],
-                        nullptr, nullptr, 0, &used[k], nullptr, 1, false, &lk, false, true, nb, mask_of(k));
+                        nullptr, nullptr, 0, &used[k], nullptr, 1, false, &lk, false, true, nb, mask_of(k),
+                        early ? c->band_ev[k] : nullptr, s->tune.band_gen, &recorded);
     if (rc != RT_OK) return rc;
-    RT_HIP(hipEventRecord(c->band_ev[k], st[k]));
+    if (!recorded) RT_HIP(hipEventRecord(c->band_ev[k], st[k]));
     RT_HIP(hipMemcpyAsync(out_rgb + (size_t)y0[k] * W * 3, c->d_out + (size_t)y0[k] * W * 3,
                           (size_t)rows * W * 3 * sizeof(double), hipMemcpyDeviceToHost, st[k]));
   }

@@ -312,8 +312,8 @@ __device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDia
 // the four child codes), tests the four boxes with no per-axis min/max, goes on
 // to the nearest child hit and pushes the others farthest first. The order is
 // a sorting network over four 32-bit keys (the entry distance's bits with the
-// slot in the two low bits, a miss all ones: non-negative binary32 values
-// order as their bits do; ties and the two dropped bits only change the visit
+// slot times 16 in the six low bits, a miss all ones: non-negative binary32 values
+// order as their bits do; ties and the six dropped bits only change the visit
 // order); the slots' child codes come from one 64-bit word. A ray makes about
 // half the dependent node loads of the binary walk. The stack is 16-bit, in
 // LDS (entry k of lane t at lds[k * kTraceBlock + t], sc.bvhw_stack entries at
@@ -333,8 +333,13 @@ __device__ __forceinline__ void lane_trace_wide(const BvhWide* nodes, SD sd, con
                                                 const BvhWide* top, int n_top, int n_records) {
   const SlabRay sr = slab_ray(o, d, M);
   float t_hi = f32_up(SHADOW ? t_shadow : h.t);
-  int sp = 0;
-  auto pop = [&]() -> unsigned { return sp > 0 ? (unsigned)lds[(--sp) * kTraceBlock] : kWideEmpty; };
+  // the stack as a pointer to its next free entry (a push or pop is one add)
+  uint16_t* tp = lds;
+  auto pop = [&]() -> unsigned {
+    if (tp == lds) return kWideEmpty;
+    tp -= kTraceBlock;
+    return (unsigned)*tp;
+  };
   unsigned e = (SHADOW && h.key >= 0 && h.t < t_shadow) || !has_bvh ? kWideEmpty : 0u;
   // per axis the entry planes' block (lo[a] when inv >= 0, else hi[a]) with the
   // constant `on`, the exit block with `of`
@@ -418,7 +423,9 @@ __device__ __forceinline__ void lane_trace_wide(const BvhWide* nodes, SD sd, con
       asm("v_max3_f32 %0, %1, %2, %3" : "=v"(t0) : "v"(tn[p][0][c]), "v"(tn[p][1][c]), "v"(zn));
       asm("v_min_f32 %0, %1, %2" : "=v"(zt) : "v"(tx[p][2][c]), "v"(t_hi));  // (t_hi is canonical)
       asm("v_min3_f32 %0, %1, %2, %3" : "=v"(t1) : "v"(tx[p][0][c]), "v"(tx[p][1][c]), "v"(zt));
-      key[j] = t0 <= t1 ? ((__float_as_uint(t0) & ~3u) | (unsigned)j) : ~0u;
+      // the key: the entry distance's bits above the low six, the slot times 16
+      // below them (the shift that selects its child code from the 64-bit word)
+      key[j] = t0 <= t1 ? ((__float_as_uint(t0) & ~63u) | (16u * (unsigned)j)) : ~0u;
     }
     n_boxes += 4;
     auto cx = [&](int a, int b) {
@@ -428,10 +435,14 @@ __device__ __forceinline__ void lane_trace_wide(const BvhWide* nodes, SD sd, con
     };
     cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
     const unsigned long long P = ((unsigned long long)cc.y << 32) | cc.x;
-    auto child = [&](unsigned k) { return (unsigned)(P >> ((k & 3u) << 4)); };  // (low 16 bits)
-    if (key[3] != ~0u) lds[(sp++) * kTraceBlock] = (uint16_t)child(key[3]);
-    if (key[2] != ~0u) lds[(sp++) * kTraceBlock] = (uint16_t)child(key[2]);
-    if (key[1] != ~0u) lds[(sp++) * kTraceBlock] = (uint16_t)child(key[1]);
+    auto child = [&](unsigned k) { return (unsigned)(P >> (k & 63u)); };  // (low 16 bits)
+    auto push = [&](unsigned k) {
+      *tp = (uint16_t)child(k);
+      tp += kTraceBlock;
+    };
+    if (key[3] != ~0u) push(key[3]);
+    if (key[2] != ~0u) push(key[2]);
+    if (key[1] != ~0u) push(key[1]);
     e = key[0] != ~0u ? (child(key[0]) & 0xFFFFu) : pop();
   };
   // a leaf's record; true when a shadow ray is found occluded
@@ -455,7 +466,7 @@ __device__ __forceinline__ void lane_trace_wide(const BvhWide* nodes, SD sd, con
     }
     if (!__any(pl != kWideEmpty)) break;
     if (pl != kWideEmpty) {
-      if (leaf(pl)) { e = kWideEmpty; sp = 0; }  // shadowed: done
+      if (leaf(pl)) { e = kWideEmpty; tp = lds; }  // shadowed: done
       pl = kWideEmpty;
     }
   }

@@ -41,7 +41,7 @@ int wf_tuning_apply(WfTuning& t, const char* key, int value) {
       {"wide", &WfTuning::wide, 0, 1},
       {"lds_wide", &WfTuning::lds_wide, 0, 1},
       {"d2h", &WfTuning::d2h, 0, 1},               {"bands", &WfTuning::bands, 1, 4},
-      {"band_pct", &WfTuning::band_pct, 5, 95}};
+      {"band_pct", &WfTuning::band_pct, 5, 95},   {"band_gen", &WfTuning::band_gen, -1, 8}};
   if (!key) return 0;
   for (const Knob& k : knobs) {
     if (std::strcmp(key, k.name) != 0) continue;
@@ -1741,7 +1741,12 @@ hipError_t Wavefront::render_fast(const DevScene& sc, const DevCamera& cam, bool
     WF_CHECK(pmark(stream, ccls, true));
     WF_CHECK(launch_fused(sc, cam, a, prim_launch, g == 0 ? n0 : kAnyRays, stream, count, tn));
     WF_CHECK(pmark(stream, ccls, false));
+    if (gen_ev_ && (int)g == gen_ev_g_) {
+      WF_CHECK(hipEventRecord(gen_ev_, stream));
+      gen_ev_done_ = true;
+    }
   }
+  gen_ev_ = nullptr;
   // combine, deepest generation first (only the nodes with children; the last
   // generation has none). Generation 0's pass records the frame's counts.
   static int combine_grid = 0;

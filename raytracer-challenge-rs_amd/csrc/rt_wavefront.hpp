@@ -109,6 +109,7 @@ struct WfTuning {
                            //     band's device-to-host copy overlapping the next band's render (1 = one render, then
                            //     one copy)
   int band_pct = 55;       // ... the first band's share of the rows (percent)
+  int band_gen = -1;       // ... band k+1 starts when band k's generation band_gen has run (-1: its whole render)
 };
 // Applies `key` = `value` to `t`: 1 = applied, 0 = not a render-time key, -1 = bad value.
 int wf_tuning_apply(WfTuning& t, const char* key, int value);
@@ -362,6 +363,12 @@ class Wavefront {
   // The learned sizes from this workspace's last recorded frame (non-blocking:
   // the record of a frame still in flight may be stale).
   void learn(WfSizing& sz) const;
+  // The next fast-path render records `ev` on its stream right after the launch
+  // of generation g (rt_render's bands: the next band may start while this one's
+  // deeper, smaller generations run); gen_event_recorded() tells whether it did
+  // (a render with fewer generations, or an exhaustive one, does not).
+  void set_gen_event(hipEvent_t ev, int g) { gen_ev_ = ev; gen_ev_g_ = g; gen_ev_done_ = false; }
+  bool gen_event_recorded() const { return gen_ev_done_; }
 
  private:
   hipError_t render_fast(const DevScene& sc, const DevCamera& cam, bool camera_mode, const double* d_in_rays,
@@ -413,6 +420,9 @@ class Wavefront {
   // generation counts of the last render (fast path: from the host-mapped record; synchronises)
   hipError_t last_counts(std::vector<unsigned>& rays);
   bool last_bvh_ = false, last_fused_ = false;
+  hipEvent_t gen_ev_ = nullptr;  // set_gen_event: recorded on the stream after generation gen_ev_g_'s launch
+  int gen_ev_g_ = -1;
+  bool gen_ev_done_ = false;
   unsigned blk_period_ = 0;  // the current render's block pattern (render())
   unsigned long long blk_mask_ = 0;
   bool profiling_ = false;

@@ -352,20 +352,23 @@ def test_arena_overflow_batch_poisoned(rt, aa):
             assert torch.equal(b, exact)
 
 
-@pytest.mark.parametrize("bands,pct", [(2, 55), (3, 40), (4, 25), (1, 55)])
-def test_host_render_banded_bitwise(rt, bands, pct):
+@pytest.mark.parametrize("bands,pct,gen", [(2, 55, -1), (3, 40, -1), (4, 25, -1), (1, 55, -1), (2, 60, 1),
+                                           (3, 45, 0), (4, 35, 2)])
+def test_host_render_banded_bitwise(rt, bands, pct, gen):
     """rt_render into a host canvas (Camera::render -> Canvas, camera.rs:133-148)
     of the full 1920x1080 C3 frame in row bands, each band's device-to-host copy
     behind its render: bitwise the exhaustive frame, into a
     pageable and into a pinned canvas; with arenas forced to overflow, every band
-    is still complete (re-rendered before the call returns)."""
-    import torch
+    is still complete (re-rendered before the call returns). `gen` >= 0: each
+    band starts once the previous band's generation `gen` has been launched
+    (band_gen), so consecutive bands' renders overlap."""
     from rtamd import scenes
     w, cam, depth = scenes.c3()
     exact, _ = _device_frame(cam, w, depth, True)
     ref = exact.cpu().numpy().tobytes()
     w.tune("bands", bands)
     w.tune("band_pct", pct)
+    w.tune("band_gen", gen)
     try:
         for _ in range(2):
             host, _ = cam.render(w, depth, want_stats=False)
@@ -377,4 +380,5 @@ def test_host_render_banded_bitwise(rt, bands, pct):
         w.tune("arena_pct", 100)
         w.tune("bands", 2)
         w.tune("band_pct", 55)
+        w.tune("band_gen", -1)
     w.check()
