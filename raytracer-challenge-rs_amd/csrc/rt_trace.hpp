@@ -312,8 +312,8 @@ __device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDia
 // the four child codes), tests the four boxes with no per-axis min/max, goes on
 // to the nearest child hit and pushes the others farthest first. The order is
 // a sorting network over four 32-bit keys (the entry distance's bits with the
-// slot times 16 in the six low bits, a miss all ones: non-negative binary32 values
-// order as their bits do; ties and the six dropped bits only change the visit
+// slot in the two low bits, a miss all ones: non-negative binary32 values
+// order as their bits do; ties and the two dropped bits only change the visit
 // order); the slots' child codes come from one 64-bit word. A ray makes about
 // half the dependent node loads of the binary walk. The stack is 16-bit, in
 // LDS (entry k of lane t at lds[k * kTraceBlock + t], sc.bvhw_stack entries at
@@ -325,7 +325,6 @@ __device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDia
 // nothing would. Leaves are batched across the wave as in lane_trace.
 // SD: the sphere records (const SphereDiag* in global memory, or Sph48 in LDS);
 // ALL_LDS: every node is in `top` (LANE 15: the whole hierarchy in LDS).
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 template <bool SHADOW, typename SD = const SphereDiag*, bool ALL_LDS = false>
 __device__ __forceinline__ void lane_trace_wide(const BvhWide* nodes, SD sd, const float* M,
                                                 bool has_bvh, V3 o, V3 d, double t_shadow, Hit& h, unsigned& n_disc,
@@ -333,13 +332,8 @@ __device__ __forceinline__ void lane_trace_wide(const BvhWide* nodes, SD sd, con
                                                 const BvhWide* top, int n_top, int n_records) {
   const SlabRay sr = slab_ray(o, d, M);
   float t_hi = f32_up(SHADOW ? t_shadow : h.t);
-  // the stack as a pointer to its next free entry (a push or pop is one add)
-  uint16_t* tp = lds;
-  auto pop = [&]() -> unsigned {
-    if (tp == lds) return kWideEmpty;
-    tp -= kTraceBlock;
-    return (unsigned)*tp;
-  };
+  int sp = 0;
+  auto pop = [&]() -> unsigned { return sp > 0 ? (unsigned)lds[(--sp) * kTraceBlock] : kWideEmpty; };
   unsigned e = (SHADOW && h.key >= 0 && h.t < t_shadow) || !has_bvh ? kWideEmpty : 0u;
   // per axis the entry planes' block (lo[a] when inv >= 0, else hi[a]) with the
   // constant `on`, the exit block with `of`
@@ -356,8 +350,6 @@ __device__ __forceinline__ void lane_trace_wide(const BvhWide* nodes, SD sd, con
     offx |= (16u * a + (neg ? 0u : 48u)) << (8 * a);
   }
   asm volatile("" : "+v"(offe), "+v"(offx));
-  const f32x2 A[3] = {{sr.inv[0], -on[0]}, {sr.inv[1], -on[1]}, {sr.inv[2], -on[2]}};
-  const f32x2 B[2] = {{-of[0], -of[1]}, {-of[2], 0.0f}};
   if (e == 0u && !usable) {  // no axis can cull (empty slots' inverted boxes need one): every record
     e = kWideEmpty;
     for (int k = 0; k < n_records; ++k) {
@@ -391,41 +383,17 @@ __device__ __forceinline__ void lane_trace_wide(const BvhWide* nodes, SD sd, con
       }
       cc = *(__attribute__((address_space(1))) const u32x2*)(b + (n0 + 96u));
     }
-    // the 24 plane distances as 12 packed FMAs (v_pk_fma_f32: two lanes of
-    // binary32 fma per issue, each the fmaf of the scalar form); the per-ray
-    // constants are broadcast from register pairs by op_sel (A[a] = {inv, -on},
-    // B = {-of0, -of1}, {-of2, -}), so they take 10 registers, not 18
-    f32x2 tn[2][3], tx[2][3];
-#pragma unroll
-    for (int p = 0; p < 2; ++p)
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        const f32x2 en = {__uint_as_float(E[a][2 * p]), __uint_as_float(E[a][2 * p + 1])};
-        const f32x2 ex = {__uint_as_float(X[a][2 * p]), __uint_as_float(X[a][2 * p + 1])};
-        asm("v_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "=v"(tn[p][a]) : "v"(en), "v"(A[a]));
-        if (a == 0)
-          asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(tx[p][a]) : "v"(ex), "v"(A[a]), "v"(B[0]));
-        else if (a == 1)
-          asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "=v"(tx[p][a]) : "v"(ex), "v"(A[a]), "v"(B[0]));
-        else
-          asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(tx[p][a]) : "v"(ex), "v"(A[a]), "v"(B[1]));
-      }
     unsigned key[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int p = j >> 1, c = j & 1;
-      // fmaxf(fmaxf(x, y), fmaxf(z, 0)) and fminf(fminf(x, y), fminf(z, t_hi)) as the
-      // compiler emits them (v_max_f32 / v_max3_f32, v_min_f32 / v_min3_f32: the
-      // same NaN-ignoring rule), written out because operands from an asm would
-      // otherwise be canonicalised first (a pk_fma never yields a signalling NaN)
-      float zn, zt, t0, t1;
-      asm("v_max_f32 %0, 0, %1" : "=v"(zn) : "v"(tn[p][2][c]));
-      asm("v_max3_f32 %0, %1, %2, %3" : "=v"(t0) : "v"(tn[p][0][c]), "v"(tn[p][1][c]), "v"(zn));
-      asm("v_min_f32 %0, %1, %2" : "=v"(zt) : "v"(tx[p][2][c]), "v"(t_hi));  // (t_hi is canonical)
-      asm("v_min3_f32 %0, %1, %2, %3" : "=v"(t1) : "v"(tx[p][0][c]), "v"(tx[p][1][c]), "v"(zt));
-      // the key: the entry distance's bits above the low six, the slot times 16
-      // below them (the shift that selects its child code from the 64-bit word)
-      key[j] = t0 <= t1 ? ((__float_as_uint(t0) & ~63u) | (16u * (unsigned)j)) : ~0u;
+      const float t0 = fmaxf(fmaxf(fmaf(__uint_as_float(E[0][j]), sr.inv[0], -on[0]),
+                                   fmaf(__uint_as_float(E[1][j]), sr.inv[1], -on[1])),
+                             fmaxf(fmaf(__uint_as_float(E[2][j]), sr.inv[2], -on[2]), 0.0f));
+      float zt;  // (t_hi is canonical: no per-visit re-canonicalisation, as in lane_trace_pair)
+      asm("v_min_f32 %0, %1, %2" : "=v"(zt) : "v"(fmaf(__uint_as_float(X[2][j]), sr.inv[2], -of[2])), "v"(t_hi));
+      const float t1 = fminf(fminf(fmaf(__uint_as_float(X[0][j]), sr.inv[0], -of[0]),
+                                   fmaf(__uint_as_float(X[1][j]), sr.inv[1], -of[1])), zt);
+      key[j] = t0 <= t1 ? ((__float_as_uint(t0) & ~3u) | (unsigned)j) : ~0u;
     }
     n_boxes += 4;
     auto cx = [&](int a, int b) {
@@ -435,14 +403,10 @@ __device__ __forceinline__ void lane_trace_wide(const BvhWide* nodes, SD sd, con
     };
     cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
     const unsigned long long P = ((unsigned long long)cc.y << 32) | cc.x;
-    auto child = [&](unsigned k) { return (unsigned)(P >> (k & 63u)); };  // (low 16 bits)
-    auto push = [&](unsigned k) {
-      *tp = (uint16_t)child(k);
-      tp += kTraceBlock;
-    };
-    if (key[3] != ~0u) push(key[3]);
-    if (key[2] != ~0u) push(key[2]);
-    if (key[1] != ~0u) push(key[1]);
+    auto child = [&](unsigned k) { return (unsigned)(P >> ((k & 3u) << 4)); };  // (low 16 bits)
+    if (key[3] != ~0u) lds[(sp++) * kTraceBlock] = (uint16_t)child(key[3]);
+    if (key[2] != ~0u) lds[(sp++) * kTraceBlock] = (uint16_t)child(key[2]);
+    if (key[1] != ~0u) lds[(sp++) * kTraceBlock] = (uint16_t)child(key[1]);
     e = key[0] != ~0u ? (child(key[0]) & 0xFFFFu) : pop();
   };
   // a leaf's record; true when a shadow ray is found occluded
@@ -466,7 +430,7 @@ __device__ __forceinline__ void lane_trace_wide(const BvhWide* nodes, SD sd, con
     }
     if (!__any(pl != kWideEmpty)) break;
     if (pl != kWideEmpty) {
-      if (leaf(pl)) { e = kWideEmpty; tp = lds; }  // shadowed: done
+      if (leaf(pl)) { e = kWideEmpty; sp = 0; }  // shadowed: done
       pl = kWideEmpty;
     }
   }
@@ -487,6 +451,7 @@ __device__ __forceinline__ void lane_trace_wide(const BvhWide* nodes, SD sd, con
 // The pair image's child codes are 16-bit (rt_layout.hpp BvhPair: a node
 // index below 0x8000, a leaf 0x8000 | first << 3 | (count - 1), 0xFFFF
 // empty), so the per-lane LDS stack holds 16-bit entries.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr int kPairEmpty = 0xFFFF;
 template <bool SHADOW>
 __device__ __forceinline__ void lane_trace_pair(const unsigned char* nodes, Sph48 sd, const float* M,
