@@ -1342,10 +1342,21 @@ int render_banded(rt_scene* s, std::unique_lock<std::mutex>& lk, rt_scene::HostC
   const int bands = std::max(2, std::min(4, s->tune.bands));
   const uint32_t rb = (H + 63) / 64, nb = (H + rb - 1) / rb;  // nb <= 64 blocks of rb rows: one period
   if (nb < (uint32_t)bands * 2) return RT_ERR_NO_DEVICE;
-  // band k = blocks [b[k], b[k+1]): the first band takes band_pct of the rows, the rest share the remainder
+  // band k = blocks [b[k], b[k+1]): the first band takes band_pct of the rows, the
+  // others share the remainder in sizes falling by band_ratio percent per band
   uint32_t b[5] = {0, 0, 0, 0, 0};
   b[1] = std::max<uint32_t>(1, std::min<uint32_t>(nb - (uint32_t)bands + 1, (uint32_t)((uint64_t)nb * s->tune.band_pct / 100)));
-  for (int k = 2; k < bands; ++k) b[k] = b[k - 1] + std::max<uint32_t>(1, (nb - b[1]) / (uint32_t)(bands - 1));
+  {
+    double wsum = 0.0, wk = 1.0;
+    for (int k = 1; k < bands; ++k, wk *= s->tune.band_ratio / 100.0) wsum += wk;
+    double acc = 0.0;
+    wk = 1.0;
+    for (int k = 2; k < bands; ++k, wk *= s->tune.band_ratio / 100.0) {
+      acc += wk;
+      const uint32_t at = b[1] + (uint32_t)((nb - b[1]) * acc / wsum + 0.5);
+      b[k] = std::min<uint32_t>(nb - (uint32_t)(bands - k), std::max<uint32_t>(b[k - 1] + 1, at));
+    }
+  }
   b[bands] = nb;
   const size_t bytes = (size_t)W * H * 3 * sizeof(double);
   bool registered = false;

@@ -41,7 +41,8 @@ int wf_tuning_apply(WfTuning& t, const char* key, int value) {
       {"wide", &WfTuning::wide, 0, 1},
       {"lds_wide", &WfTuning::lds_wide, 0, 1},
       {"d2h", &WfTuning::d2h, 0, 1},               {"bands", &WfTuning::bands, 1, 4},
-      {"band_pct", &WfTuning::band_pct, 5, 95},   {"band_gen", &WfTuning::band_gen, -1, 8}};
+      {"band_pct", &WfTuning::band_pct, 5, 95},   {"band_gen", &WfTuning::band_gen, -1, 8},
+      {"band_ratio", &WfTuning::band_ratio, 30, 100}};
   if (!key) return 0;
   for (const Knob& k : knobs) {
     if (std::strcmp(key, k.name) != 0) continue;

@@ -105,11 +105,12 @@ struct WfTuning {
   int arena_pct = 100;     // test hook: the fast path's queue arenas sized to this percentage of the hint,
                            //     shrinking them (< 100: forces overflows, DESIGN.md "Device-sized generations")
   int d2h = 1;             // host-canvas copies: 1 = pin the caller's buffer for the call and DMA into it, 0 = pinned chunks
-  int bands = 2;           // rt_render into a host canvas: row bands rendered one after the other on two streams, each
-                           //     band's device-to-host copy overlapping the next band's render (1 = one render, then
-                           //     one copy)
-  int band_pct = 55;       // ... the first band's share of the rows (percent)
-  int band_gen = -1;       // ... band k+1 starts when band k's generation band_gen has run (-1: its whole render)
+  int bands = 4;           // rt_render into a host canvas: row bands rendered one after the other on their own
+                           //     streams, each band's device-to-host copy overlapping the next bands' renders (1 = one
+                           //     render, then one copy)
+  int band_pct = 35;       // ... the first band's share of the rows (percent)
+  int band_ratio = 100;    // ... each later band's size, percent of the one before (100: equal shares)
+  int band_gen = 1;        // ... band k+1 starts when band k's generation band_gen has run (-1: its whole render)
 };
 // Applies `key` = `value` to `t`: 1 = applied, 0 = not a render-time key, -1 = bad value.
 int wf_tuning_apply(WfTuning& t, const char* key, int value);

@@ -352,9 +352,10 @@ def test_arena_overflow_batch_poisoned(rt, aa):
             assert torch.equal(b, exact)
 
 
-@pytest.mark.parametrize("bands,pct,gen", [(2, 55, -1), (3, 40, -1), (4, 25, -1), (1, 55, -1), (2, 60, 1),
-                                           (3, 45, 0), (4, 35, 2)])
-def test_host_render_banded_bitwise(rt, bands, pct, gen):
+@pytest.mark.parametrize("bands,pct,gen,ratio", [(4, 35, 1, 100), (2, 55, -1, 100), (3, 40, -1, 100),
+                                                 (4, 25, -1, 100), (1, 55, -1, 100), (2, 60, 1, 100),
+                                                 (3, 45, 0, 70), (4, 45, 2, 60)])
+def test_host_render_banded_bitwise(rt, bands, pct, gen, ratio):
     """rt_render into a host canvas (Camera::render -> Canvas, camera.rs:133-148)
     of the full 1920x1080 C3 frame in row bands, each band's device-to-host copy
     behind its render: bitwise the exhaustive frame, into a
@@ -369,6 +370,7 @@ def test_host_render_banded_bitwise(rt, bands, pct, gen):
     w.tune("bands", bands)
     w.tune("band_pct", pct)
     w.tune("band_gen", gen)
+    w.tune("band_ratio", ratio)
     try:
         for _ in range(2):
             host, _ = cam.render(w, depth, want_stats=False)
@@ -378,7 +380,8 @@ def test_host_render_banded_bitwise(rt, bands, pct, gen):
         assert host.to_numpy().tobytes() == ref
     finally:
         w.tune("arena_pct", 100)
-        w.tune("bands", 2)
-        w.tune("band_pct", 55)
-        w.tune("band_gen", -1)
+        w.tune("bands", 4)
+        w.tune("band_pct", 35)
+        w.tune("band_gen", 1)
+        w.tune("band_ratio", 100)
     w.check()

@@ -80,8 +80,8 @@ def e2e(reps):
             cam.render(w, depth, want_stats=False)
             ts.append((time.perf_counter() - t0) * 1e3)
         out[f"rt_render_bands{bands}_{pct}_ms"] = sorted(ts)[len(ts) // 2]
-    w.tune("bands", 2)
-    w.tune("band_pct", 55)
+    w.tune("bands", 4)
+    w.tune("band_pct", 35)
     ref = dev.clone()
     streams = [rtamd.render_stream(False) for _ in range(2)]
     for K in (2, 3, 4, 6, 8):
@@ -139,14 +139,16 @@ def bands(reps):
     configurations so that clock drift hits all of them alike; median and min."""
     w, cam, depth = scenes.c3()
     w.upload(0)
-    cfgs = [(1, 50, -1), (2, 55, -1), (2, 60, -1), (2, 65, -1), (3, 45, -1), (4, 40, -1),
-            (2, 55, 0), (2, 60, 0), (2, 60, 1), (2, 65, 1), (2, 60, 2), (3, 40, 0), (3, 45, 1), (4, 35, 0), (4, 40, 1)]
+    cfgs = [(1, 50, -1, 100), (2, 60, -1, 100), (2, 65, 1, 100), (3, 45, 1, 100), (3, 45, 1, 70), (3, 50, 1, 60),
+            (4, 40, 1, 100), (4, 35, 1, 100), (4, 45, 1, 100), (4, 40, 2, 100), (4, 40, 0, 100), (4, 40, 1, 75),
+            (4, 35, 1, 80), (4, 45, 1, 70), (4, 30, 1, 90)]
     ts = {c: [] for c in cfgs}
 
     def setc(c):
         w.tune("bands", c[0])
         w.tune("band_pct", c[1])
         w.tune("band_gen", c[2])
+        w.tune("band_ratio", c[3])
     ref = None
     for c in cfgs:  # warm every configuration's workspaces; every frame bitwise equal
         setc(c)
@@ -159,9 +161,9 @@ def bands(reps):
             t0 = time.perf_counter()
             cam.render(w, depth, want_stats=False)
             ts[c].append((time.perf_counter() - t0) * 1e3)
-    w.tune("band_gen", -1)
-    return {f"bands{b}_{p}_gen{g}": {"median_ms": round(sorted(v)[len(v) // 2], 4), "min_ms": round(min(v), 4)}
-            for (b, p, g), v in ts.items()}
+    setc((4, 35, 1, 100))
+    return {f"bands{b}_{p}_gen{g}_r{r}": {"median_ms": round(sorted(v)[len(v) // 2], 4), "min_ms": round(min(v), 4)}
+            for (b, p, g, r), v in ts.items()}
 
 
 def assembly(reps, share=None):
