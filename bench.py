@@ -253,8 +253,11 @@ def end_to_end(world, cam, depth, frames=3):
     `rt_canvas_to_ppm` (image/ppm.rs:24-51), per frame, one frame at a time."""
     # warm: the scene's workspaces, and two pooled pinned canvases (a loop holds the
     # previous frame's canvas while the next one renders)
+    # (and a few more frames: the band workspaces' arenas settle on their learned sizes)
     warm = [cam.render(world, depth, want_stats=False)[0] for _ in range(2)]
     del warm
+    for _ in range(3):
+        cam.render(world, depth, want_stats=False)
     t0 = time.perf_counter()
     for _ in range(frames):
         canvas, _ = cam.render(world, depth, want_stats=False)
