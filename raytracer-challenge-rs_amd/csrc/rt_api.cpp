@@ -210,6 +210,10 @@ struct rt_scene {
   int n_objects = 0, n_lights = 0;
   WfTuning tune;  // this scene's render-time tuning (read under `mu` by every render)
   WfSizing sizing;  // the fast path's queue arenas, learned from this scene's frames (under `mu`)
+  // ... and from the row bands of rt_render (render_banded): a band's rays per root ray
+  // differ from a whole frame's (a band of floor reflects more than the frame), and
+  // must not resize the arenas of whole-frame renders (a regrowth reallocates them)
+  WfSizing band_sizing;
   ~rt_scene() {
     for (WfSlot& w : wfs)
       if (w.done) (void)hipEventDestroy(w.done);
@@ -486,7 +490,9 @@ int run_render(rt_scene* s, const DevCamera& cam, const double* d_rays, uint32_t
                rt_scene::WfSlot** used = nullptr, const FrameTable* batch = nullptr, unsigned n_frames = 1,
                bool sync = false, std::unique_lock<std::mutex>* lk = nullptr, bool count = false,
                bool keep_pin = false, uint32_t blk_period = 0, uint64_t blk_mask = 0,
-               hipEvent_t gen_ev = nullptr, int gen_ev_g = -1, bool* gen_ev_recorded = nullptr) {
+               hipEvent_t gen_ev = nullptr, int gen_ev_g = -1, bool* gen_ev_recorded = nullptr,
+               WfSizing* sizing = nullptr) {
+  WfSizing& sz = sizing ? *sizing : s->sizing;
   if (max_depth > (uint32_t)kMaxDepth)
     return fail(RT_ERR_INVALID_ARGUMENT, "max_depth > " + std::to_string(kMaxDepth));
   if (!valid_aa(aa)) return fail(RT_ERR_INVALID_ARGUMENT, "aa_samples must be 1, 2, 4, 8 or 16");
@@ -517,7 +523,7 @@ int run_render(rt_scene* s, const DevCamera& cam, const double* d_rays, uint32_t
   for (int attempt = 0;; ++attempt) {
     if (gen_ev) w->wf->set_gen_event(gen_ev, gen_ev_g);
     e = w->wf->render(s->dev, cam, d_rays == nullptr, d_rays, n_tasks, aa, max_depth, row_block, shard, n_shards,
-                      d_out, stream, s->sizing, nullptr, nullptr, s->tune, s->wfs.size() == 1, wf_flags, batch,
+                      d_out, stream, sz, nullptr, nullptr, s->tune, s->wfs.size() == 1, wf_flags, batch,
                       n_frames, blk_period, blk_mask);
     if (gen_ev) {
       if (gen_ev_recorded) *gen_ev_recorded = w->wf->gen_event_recorded();
@@ -530,7 +536,7 @@ int run_render(rt_scene* s, const DevCamera& cam, const double* d_rays, uint32_t
     e = hipStreamSynchronize(stream);
     if (lk) lk->lock();
     if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("wavefront render: ") + hipGetErrorString(e));
-    w->wf->learn(s->sizing);
+    w->wf->learn(sz);
     bool over = false;
     e = w->wf->take_overflow(&over);
     if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("wavefront arenas: ") + hipGetErrorString(e));
@@ -1095,6 +1101,7 @@ int rt_scene_create_groups(const rt_shape_desc* shapes, size_t n_shapes, const i
   for (size_t i = 0; i < n_shapes; ++i)
     branch = std::max(branch, (shapes[i].reflective != 0.0 ? 1 : 0) + (shapes[i].transparency != 0.0 ? 1 : 0));
   s->sizing.branch = branch;
+  s->band_sizing.branch = branch;
   {
     std::lock_guard<std::mutex> tlk(g_tune_mu);
     s->tune = g_tune_defaults;
@@ -1412,7 +1419,7 @@ int render_banded(rt_scene* s, std::unique_lock<std::mutex>& lk, rt_scene::HostC
     bool recorded = false;
     int rc = run_render(s, dc, nullptr, rows * W * aa, aa, max_depth, rb, 0, 1, c->d_out + (size_t)y0[k] * W * 3, st[k],
                         nullptr, nullptr, 0, &used[k], nullptr, 1, false, &lk, false, true, nb, mask_of(k),
-                        early ? c->band_ev[k] : nullptr, s->tune.band_gen, &recorded);
+                        early ? c->band_ev[k] : nullptr, s->tune.band_gen, &recorded, &s->band_sizing);
     if (rc != RT_OK) return rc;
     if (!recorded) RT_HIP(hipEventRecord(c->band_ev[k], st[k]));
     RT_HIP(hipMemcpyAsync(out_rgb + (size_t)y0[k] * W * 3, c->d_out + (size_t)y0[k] * W * 3,
@@ -1423,7 +1430,7 @@ int render_banded(rt_scene* s, std::unique_lock<std::mutex>& lk, rt_scene::HostC
   lk.lock();
   for (int k = 0; k < bands; ++k) {
     if (!used[k]) continue;
-    used[k]->wf->learn(s->sizing);
+    used[k]->wf->learn(s->band_sizing);
     bool over = false;
     RT_HIP(used[k]->wf->take_overflow(&over));
     unpin(k);
@@ -1431,7 +1438,8 @@ int render_banded(rt_scene* s, std::unique_lock<std::mutex>& lk, rt_scene::HostC
     // (its canvas rows are NaN: render the band again, synchronously, with the arenas grown)
     const uint32_t rows = y0[k + 1] - y0[k];
     int rc = run_render(s, dc, nullptr, rows * W * aa, aa, max_depth, rb, 0, 1, c->d_out + (size_t)y0[k] * W * 3,
-                        st[k], nullptr, nullptr, 0, nullptr, nullptr, 1, true, &lk, false, false, nb, mask_of(k));
+                        st[k], nullptr, nullptr, 0, nullptr, nullptr, 1, true, &lk, false, false, nb, mask_of(k),
+                        nullptr, -1, nullptr, &s->band_sizing);
     if (rc != RT_OK) return rc;
     RT_HIP(hipMemcpyAsync(out_rgb + (size_t)y0[k] * W * 3, c->d_out + (size_t)y0[k] * W * 3,
                           (size_t)rows * W * 3 * sizeof(double), hipMemcpyDeviceToHost, st[k]));
