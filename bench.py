@@ -281,31 +281,36 @@ def end_to_end(world, cam, depth, frames=3):
                     "bytes checked equal); not the headline value"}
 
 
-def distinct_cameras(world, depth, rstreams, dev, headline, frames=64, nb=8):
+def distinct_cameras(world, depth, rstreams, dev, headline, frames=64, nb=8, passes=3):
     """An animation over the C3 scene: `frames` cameras along an arc
     (scenes.c3_orbit), each rendered for the first time, in batches of `nb` on
     the render streams (batch b on stream b % F, as the headline). Nothing is
     calibrated per camera: every generation of every frame sizes itself on the
-    device. Mrays/s counts each camera's own reference rays (one counted
-    fast-path render per camera, after timing); the frames left in the
-    buffers (the last batch of every stream) are checked bitwise against
-    their exhaustive frames."""
-    cams = [scenes.c3_orbit(k, frames) for k in range(frames)]
-    H, W = cams[0].vsize, cams[0].hsize
+    device. `passes` timed passes, each over a new arc (0.8, 0.9, 1.0 rad: no
+    camera repeats); the value is the median pass. Mrays/s counts each camera's
+    own reference rays (one counted fast-path render per camera, after timing);
+    the frames left in the buffers (the last batch of every stream) are checked
+    bitwise against their exhaustive frames."""
     F = len(rstreams)
-    bufs = [[torch.empty((H, W, 3), dtype=torch.float64, device=dev) for _ in range(nb)] for _ in range(F)]
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for b in range(frames // nb):
-        rs = rstreams[b % F]
-        rtamd.render_frames_device(world, cams[b * nb:(b + 1) * nb], depth, 8, 0, 1,
-                                   [x.data_ptr() for x in bufs[b % F]], rs.cuda_stream)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    n_batches = frames // nb
+    results = []
+    for p in range(passes):
+        cams = [scenes.c3_orbit(k, frames, arc=0.8 + 0.1 * p) for k in range(frames)]
+        H, W = cams[0].vsize, cams[0].hsize
+        bufs = [[torch.empty((H, W, 3), dtype=torch.float64, device=dev) for _ in range(nb)] for _ in range(F)]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for b in range(n_batches):
+            rs = rstreams[b % F]
+            rtamd.render_frames_device(world, cams[b * nb:(b + 1) * nb], depth, 8, 0, 1,
+                                       [x.data_ptr() for x in bufs[b % F]], rs.cuda_stream)
+        torch.cuda.synchronize()
+        results.append((time.perf_counter() - t0, cams, bufs))
     world.check()  # every frame complete (no arena overflow)
+    dts = sorted(r[0] for r in results)
+    dt, cams, bufs = next(r for r in results if r[0] == dts[len(dts) // 2])
     ok = True
     ref = torch.empty((H, W, 3), dtype=torch.float64, device=dev)
-    n_batches = frames // nb
     for b in range(max(0, n_batches - F), n_batches):
         for j in range(nb):
             cams[b * nb + j].render_shard_device(world, depth, 8, 0, 1, ref.data_ptr(),
@@ -317,14 +322,15 @@ def distinct_cameras(world, depth, rstreams, dev, headline, frames=64, nb=8):
         st = c.render_shard_device(world, depth, 8, 0, 1, ref.data_ptr(), torch.cuda.current_stream().cuda_stream,
                                    True, exhaustive=False)
         rays += st["rays_primary"] + st["rays_reflect"] + st["rays_refract"] + st["rays_shadow"]
-    del bufs, ref
+    del bufs, ref, results
     value = rays / dt / 1e6
     return {"value": round(value, 3), "unit": "Mrays/s", "frames": n_batches * nb, "batch": nb, "streams": F,
             "ms_per_frame": round(dt / (n_batches * nb) * 1e3, 4), "vs_headline": round(value / headline, 4),
+            "passes_ms_per_frame": [round(x / (n_batches * nb) * 1e3, 4) for x in dts],
             "parity": {"vs_exhaustive": "bitwise", "ok": ok, "frames_checked": min(F, n_batches) * nb},
-            "note": "C3 scene, a new camera every frame (scenes.c3_orbit: a 0.8-rad arc around the look-at point), "
-                    "batches of 8 on the render streams, no per-camera calibration or cache; value = the cameras' "
-                    "own reference rays / wall time"}
+            "note": "C3 scene, a new camera every frame (scenes.c3_orbit: arcs of 0.8, 0.9 and 1.0 rad around the "
+                    "look-at point, one timed pass each, the median pass reported), batches of 8 on the render streams, "
+                    "no per-camera calibration or cache; value = the cameras' own reference rays / wall time"}
 
 
 def cold_start(dev_index):

@@ -178,7 +178,11 @@ struct rt_scene {
     unsigned long long tick = 0;
     int pins = 0;
   };
-  static constexpr size_t kMaxWorkspaces = 8;
+  // (16: a caller with 4 render streams, rt_render's 4 band streams, its own context
+  // stream and a current stream stays below it, so no workspace is taken over by a
+  // stream whose frames need larger arenas: a takeover that regrows them frees and
+  // reallocates device memory, which synchronises the device)
+  static constexpr size_t kMaxWorkspaces = 16;
   std::deque<WfSlot> wfs;
   unsigned long long tick = 0;
   WfSlot* last_wf = nullptr;

@@ -311,10 +311,10 @@ def test_wide_hierarchy_bitwise(rt, leaf):
     assert boxes[(3, 1)] != boxes[(3, 0)] and boxes[(3, 1)] > 0 and boxes[(0, 1)] > 0
 
 
-@pytest.mark.parametrize("n_streams,kind", [(2, "torch"), (10, "torch"), (4, "plain"), (4, "dedicated")])
+@pytest.mark.parametrize("n_streams,kind", [(2, "torch"), (18, "torch"), (4, "plain"), (4, "dedicated")])
 def test_frames_in_flight_bitwise(rt, n_streams, kind):
     """Frames rendered concurrently on several streams (one workspace per
-    stream; with 10 streams, more than the pool's 8 workspaces, so workspaces
+    stream; with 18 streams, more than the pool's 16 workspaces, so workspaces
     change hands in stream order) all equal the exhaustive frame, for the
     whole frame and for an 8-way shard, on torch streams and on the
     library's render streams (rtamd.render_stream, plain and CU-masked)."""
