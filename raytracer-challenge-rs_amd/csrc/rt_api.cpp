@@ -131,6 +131,8 @@ extern "C" __attribute__((visibility("hidden"))) int rtamd_fail(int code, const 
   return code;
 }
 
+constexpr int kMaxBands = 4;  // rt_render's row bands (WfTuning::bands, render_banded; more were slower: a stream each)
+
 struct rt_scene {
   int device = 0;
   DevScene dev{};
@@ -158,8 +160,8 @@ struct rt_scene {
     hipEvent_t stage_ev[2] = {nullptr, nullptr};
     // banded host renders (render_banded): a stream per band after the first, and the
     // events that start each band when the previous band's render is done
-    hipStream_t band_stream[3] = {nullptr, nullptr, nullptr};
-    hipEvent_t band_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipStream_t band_stream[kMaxBands - 1] = {};
+    hipEvent_t band_ev[kMaxBands] = {};
     bool busy = false;
   };
   std::deque<HostCtx> ctxs;  // deque: a context's address survives the pool's growth
@@ -1350,12 +1352,12 @@ namespace {
 int render_banded(rt_scene* s, std::unique_lock<std::mutex>& lk, rt_scene::HostCtx* c, const rt_camera_desc& cam,
                   uint32_t max_depth, uint32_t aa, double* out_rgb) {
   const uint32_t W = cam.hsize, H = cam.vsize;
-  const int bands = std::max(2, std::min(4, s->tune.bands));
+  const int bands = std::max(2, std::min(kMaxBands, s->tune.bands));
   const uint32_t rb = (H + 63) / 64, nb = (H + rb - 1) / rb;  // nb <= 64 blocks of rb rows: one period
   if (nb < (uint32_t)bands * 2) return RT_ERR_NO_DEVICE;
   // band k = blocks [b[k], b[k+1]): the first band takes band_pct of the rows, the
   // others share the remainder in sizes falling by band_ratio percent per band
-  uint32_t b[5] = {0, 0, 0, 0, 0};
+  uint32_t b[kMaxBands + 1] = {};
   b[1] = std::max<uint32_t>(1, std::min<uint32_t>(nb - (uint32_t)bands + 1, (uint32_t)((uint64_t)nb * s->tune.band_pct / 100)));
   {
     double wsum = 0.0, wk = 1.0;
@@ -1385,7 +1387,7 @@ int render_banded(rt_scene* s, std::unique_lock<std::mutex>& lk, rt_scene::HostC
       if (on && hipHostUnregister(p) != hipSuccess) (void)hipGetLastError();
     }
   } unreg{out_rgb, registered};
-  hipStream_t st[4] = {c->stream, nullptr, nullptr, nullptr};
+  hipStream_t st[kMaxBands] = {c->stream};
   for (int k = 1; k < bands; ++k) {
     if (!c->band_stream[k - 1]) RT_HIP(hipStreamCreateWithFlags(&c->band_stream[k - 1], hipStreamNonBlocking));
     st[k] = c->band_stream[k - 1];
@@ -1394,7 +1396,7 @@ int render_banded(rt_scene* s, std::unique_lock<std::mutex>& lk, rt_scene::HostC
     if (!c->band_ev[k]) RT_HIP(hipEventCreateWithFlags(&c->band_ev[k], hipEventDisableTiming));
   const DevCamera dc = to_dev_camera(cam);
   const uint64_t all = nb == 64 ? ~0ull : ((1ull << nb) - 1ull);
-  rt_scene::WfSlot* used[4] = {nullptr, nullptr, nullptr, nullptr};
+  rt_scene::WfSlot* used[kMaxBands] = {};
   auto unpin = [&](int k) {
     if (used[k]) {
       --used[k]->pins;
@@ -1408,7 +1410,7 @@ int render_banded(rt_scene* s, std::unique_lock<std::mutex>& lk, rt_scene::HostC
     if (!lk.owns_lock()) lk.lock();
     for (int k = 0; k < bands; ++k) unpin(k);
   }};
-  uint32_t y0[5];
+  uint32_t y0[kMaxBands + 1];
   for (int k = 0; k <= bands; ++k) y0[k] = std::min(H, b[k] * rb);
   auto mask_of = [&](int k) {
     const uint64_t below_end = b[k + 1] >= 64 ? ~0ull : ((1ull << b[k + 1]) - 1ull);

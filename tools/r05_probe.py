@@ -139,9 +139,9 @@ def bands(reps):
     configurations so that clock drift hits all of them alike; median and min."""
     w, cam, depth = scenes.c3()
     w.upload(0)
-    cfgs = [(1, 50, -1, 100), (2, 60, -1, 100), (2, 65, 1, 100), (3, 45, 1, 100), (3, 45, 1, 70), (3, 50, 1, 60),
-            (4, 40, 1, 100), (4, 35, 1, 100), (4, 45, 1, 100), (4, 40, 2, 100), (4, 40, 0, 100), (4, 40, 1, 75),
-            (4, 35, 1, 80), (4, 45, 1, 70), (4, 30, 1, 90)]
+    cfgs = [(1, 50, -1, 100), (4, 35, 1, 100), (4, 30, 1, 100), (5, 30, 1, 100), (5, 25, 1, 100), (6, 25, 1, 100),
+            (6, 20, 1, 100), (8, 20, 1, 100), (8, 15, 1, 100), (6, 30, 1, 80), (8, 25, 1, 80), (5, 30, 2, 100),
+            (6, 25, 2, 100), (6, 25, 0, 100), (8, 20, 0, 100)]
     ts = {c: [] for c in cfgs}
 
     def setc(c):
