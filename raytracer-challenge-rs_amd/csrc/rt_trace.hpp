@@ -620,8 +620,12 @@ __host__ __device__ inline size_t sph_lds_bytes(const DevScene& sc) { return (si
 __host__ __device__ inline size_t sph48_lds_bytes(const DevScene& sc) {
   return (size_t)sc.n_diag * 48 + (((size_t)sc.n_diag * 4 + 15) & ~(size_t)15);
 }
+// The light buffer's distances in LDS as binary16 lower bounds of the binary32
+// ones (2 B each): a stored value never exceeds the true distance, so a walk
+// that stops at the first stored distance beyond the origin stops no earlier
+// than the exact walk would (lb_walk).
 __host__ __device__ inline size_t delta_lds_bytes(const DevScene& sc) {
-  return sc.lb_cells ? (((size_t)sc.n_lights * sc.n_diag * sizeof(float) + 15) & ~(size_t)15) : 0;
+  return sc.lb_cells ? (((size_t)sc.n_lights * sc.n_diag * sizeof(_Float16) + 15) & ~(size_t)15) : 0;
 }
 // LANE 14: [16-bit stack (bvh_depth + 1 with the sentinel) x kTraceBlock][pair nodes][Sph48 records]
 // (no pair image without the scene's 16-bit pair codes: rt_bvh.cpp pair_layout)
@@ -646,7 +650,8 @@ struct LaneScene {
   const SphereDiag* sd;        // sphere records (LDS or global; not LANE 14)
   Sph48 s48;                   // LANE 14: the sphere records in LDS
   uint16_t* stack16;           // LANE 14: the per-lane 16-bit LDS stack
-  const float* delta;          // light buffer: per-light box distances (LDS or global)
+  const float* delta;          // light buffer: per-light box distances (global)
+  const _Float16* delta16;     // ... their binary16 lower bounds in LDS (when staged), else null
   int* stack;                  // per-lane LDS stack (14, 3) or the wave's stack (0)
   float M[3];                  // bound on |box coordinate| per axis (slab_ray)
   const BvhNode* top;          // 3: the LDS copy of the first n_top nodes
@@ -656,8 +661,8 @@ struct LaneScene {
 template <int LANE>
 __device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, unsigned lds_flags, unsigned n_top, int* static_stack,
                                                 unsigned char* dyn) {
-  LaneScene ls{(const unsigned char*)sc.bvh, sc.sph_diag, Sph48{nullptr, nullptr}, nullptr, sc.lb_delta, static_stack,
-               {0.f, 0.f, 0.f}, nullptr, 0, nullptr};
+  LaneScene ls{(const unsigned char*)sc.bvh, sc.sph_diag, Sph48{nullptr, nullptr}, nullptr, sc.lb_delta, nullptr,
+               static_stack, {0.f, 0.f, 0.f}, nullptr, 0, nullptr};
   unsigned char* p = dyn;
   if constexpr (LANE == 15) {  // [16-bit stack][every wide node][Sph48 records and metas]
     ls.stack16 = (uint16_t*)dyn + threadIdx.x;
@@ -725,7 +730,10 @@ __device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, unsigned lds
     ls.n_top = (int)n_top;
   }
   if (lds_flags & kLdsDeltas) {
-    float* ld = (float*)p;
+    // binary16 lower bounds: a positive value rounded toward zero (= down), anything
+    // else 0 (a stored 0 never ends a walk: the walk compares with a positive distance)
+    _Float16* ld = (_Float16*)p;
+    auto down16 = [](float v) -> _Float16 { return v > 0.0f ? __builtin_amdgcn_cvt_pkrtz(v, 0.0f)[0] : (_Float16)0.0f; };
     const int nd = sc.n_lights * sc.n_diag, bd = (int)blockDim.x;
     int i = (int)threadIdx.x;
     for (; i + 7 * bd < nd; i += 8 * bd) {  // eight loads in flight per thread
@@ -733,10 +741,10 @@ __device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, unsigned lds
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] = sc.lb_delta[i + k * bd];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) ld[i + k * bd] = v[k];
+      for (int k = 0; k < 8; ++k) ld[i + k * bd] = down16(v[k]);
     }
-    for (; i < nd; i += bd) ld[i] = sc.lb_delta[i];
-    ls.delta = ld;
+    for (; i < nd; i += bd) ld[i] = down16(sc.lb_delta[i]);
+    ls.delta16 = ld;
   }
   __syncthreads();
   for (int ax = 0; ax < 3; ++ax) {  // the root's two child boxes contain every box below them
@@ -757,8 +765,9 @@ __device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, unsigned lds
 // origin. One 16-B load brings the cell's first kLbInline entries. An origin
 // beyond the light's validity radius (or non-finite) tests every sphere.
 template <typename SD>  // the sphere records: const SphereDiag* (global or LDS) or Sph48 (the pair image)
-__device__ __forceinline__ void lb_walk(const DevScene& sc, SD sd, const float* delta, unsigned l,
-                                        V3 o, V3 d, double dist, Hit& h, unsigned& n_disc, unsigned& n_tests) {
+__device__ __forceinline__ void lb_walk(const DevScene& sc, SD sd, const float* delta, const _Float16* delta16,
+                                        unsigned l, V3 o, V3 d, double dist, Hit& h, unsigned& n_disc,
+                                        unsigned& n_tests) {
   cLightRec Lr = (cLightRec)sc.lights + l;
   if (dist <= (double)sc.lb_limit[l] && dist >= 1e-30) {
     const int R = sc.lb_res;
@@ -784,13 +793,14 @@ __device__ __forceinline__ void lb_walk(const DevScene& sc, SD sd, const float* 
     unsigned long long q = (unsigned long long)(c.w0 >> 16) | (unsigned long long)c.w1 << 16 |
                            (unsigned long long)(c.w2 & 0xFFFFu) << 48;
     const float* dl = delta + (size_t)l * sc.n_diag;
+    const _Float16* dl16 = delta16 ? delta16 + (size_t)l * sc.n_diag : nullptr;
     const float dist_up = f32_up(dist);
     for (unsigned k = 0; k < cnt; ++k) {
       unsigned idx;
       if (k < 4u) { idx = (unsigned)(q & 0xFFFFu); q >>= 16; }
       else if (k == 4u) idx = c.w2 >> 16;
       else idx = sc.lb_ov[c.ov + k - (unsigned)kLbInline];
-      if (dl[idx] > dist_up) break;  // this box and all after it lie beyond the origin
+      if ((dl16 ? (float)dl16[idx] : dl[idx]) > dist_up) break;  // this box and all after it lie beyond the origin
       leaf_sphere_test<true>(sd, (int)idx, o, d, h, n_disc);
       ++n_tests;
       if (h.key >= 0 && h.t < dist) break;
@@ -818,8 +828,8 @@ __device__ __forceinline__ bool shadow_trace(const DevScene& sc, unsigned use_lb
   if constexpr (QUADS) other_trace<true>(sc, o, d, dist, h, n_disc, n_tests, n_boxes);
   if (!(h.key >= 0 && h.t < dist)) {
     if (use_lb) {
-      if constexpr (LANE == 14 || LANE == 15) lb_walk(sc, ls.s48, ls.delta, l, o, d, dist, h, n_disc, n_tests);
-      else lb_walk(sc, ls.sd, ls.delta, l, o, d, dist, h, n_disc, n_tests);
+      if constexpr (LANE == 14 || LANE == 15) lb_walk(sc, ls.s48, ls.delta, ls.delta16, l, o, d, dist, h, n_disc, n_tests);
+      else lb_walk(sc, ls.sd, ls.delta, ls.delta16, l, o, d, dist, h, n_disc, n_tests);
     } else if constexpr (LANE == 14) {
       lane_trace_pair<true>(ls.nodes, ls.s48, ls.M, sc.n_bvh > 0, o, d, dist, h, n_disc, n_tests, n_boxes,
                             ls.stack16);
