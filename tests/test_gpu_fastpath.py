@@ -352,6 +352,31 @@ def test_arena_overflow_batch_poisoned(rt, aa):
             assert torch.equal(b, exact)
 
 
+@pytest.mark.parametrize("aa", [2, 4])
+def test_host_render_banded_aa_bitwise(rt, aa):
+    """render_multithreaded with AA (camera.rs:150-253) into a host canvas of
+    the full C3 frame goes through the row bands too (n_pix * aa >= 2^20): each
+    band averages its own pixels' samples; bitwise the exhaustive device frame,
+    and identical to the unbanded host render."""
+    import torch
+    from rtamd import scenes
+    w, cam, depth = scenes.c3()
+    buf = torch.empty((cam.vsize, cam.hsize, 3), dtype=torch.float64, device="cuda")
+    cam.render_shard_device(w, depth, 8, 0, 1, buf.data_ptr(), torch.cuda.current_stream().cuda_stream, True,
+                            exhaustive=True, aa_samples=aa)
+    torch.cuda.synchronize()
+    ref = buf.cpu().numpy().tobytes()
+    cam.render_opts.aa_samples(getattr(rt.AASamples, f"X{aa}"))
+    banded, _ = cam.render_multithreaded(w, depth, want_stats=False)
+    assert banded.to_numpy().tobytes() == ref
+    w.tune("bands", 1)
+    try:
+        whole, _ = cam.render_multithreaded(w, depth, want_stats=False)
+    finally:
+        w.tune("bands", 4)
+    assert whole.to_numpy().tobytes() == ref
+
+
 @pytest.mark.parametrize("bands,pct,gen,ratio", [(4, 35, 1, 100), (2, 55, -1, 100), (3, 40, -1, 100),
                                                  (4, 25, -1, 100), (1, 55, -1, 100), (2, 60, 1, 100),
                                                  (3, 45, 0, 70), (4, 45, 2, 60)])
