@@ -219,7 +219,12 @@ void rt_scene_destroy(rt_scene* scene);
 /* `Camera::render(&mut self, &World) -> Canvas` (camera.rs:133-148) with
  * `MAX_RECURSION_DEPTH` replaced by `max_depth` (world.rs:16; 5 = reference).
  * `out_rgb` is a caller-owned HOST buffer of vsize*hsize*3 doubles, row-major
- * `y*w + x` (canvas.rs:44-48). Synchronous. */
+ * `y*w + x` (canvas.rs:44-48). Synchronous. A large frame (>= 2^20 samples)
+ * without `stats` is rendered in row bands on the call's own streams, each
+ * band's copy to `out_rgb` running behind its render while the next bands
+ * render; the pixels are the whole-frame render's. The copy goes straight into
+ * `out_rgb` by DMA when it comes from rt_host_buffer_alloc (the fast case),
+ * else the buffer is page-locked for the call. */
 int rt_render(const rt_scene* scene, const rt_camera_desc* camera,
               uint32_t max_depth, double* out_rgb, rt_stats* stats);
 
