@@ -225,6 +225,67 @@ def test_flattened_hierarchy(rt):
             assert (boxes[i, :3] >= boxes[p, :3] - 1e-9).all() and (boxes[i, 3:] <= boxes[p, 3:] + 1e-9).all()
 
 
+def _normal_on_child_world(rt):
+    """geometry/mod.rs:126-150: a sphere translated by (5, 0, 0) inside a group
+    scaled by (1, 2, 3) inside a group rotated by pi/2 about y."""
+    g1 = rt.Group()
+    g1.set_transform(rt.rotation_y(math.pi / 2.0))
+    g2 = rt.Group()
+    g2.set_transform(rt.scaling(1, 2, 3))
+    s = rt.Sphere()
+    s.set_transform(rt.translation(5, 0, 0))
+    g2.add_child(s)
+    g1.add_child(g2)
+    w = rt.World()
+    w.add_object(g1)
+    w.add_light(rt.PointLight(rt.Point(-10, 10, -10), rt.Color(1, 1, 1)))
+    return w
+
+
+NORMAL_KAT = ((1.7321, 1.1547, -5.5774), (0.2857, 0.42854, -0.85716))  # geometry/mod.rs:148-153
+
+
+def test_normal_on_child_object_oracle(rt, oracle):
+    """The transforms baked into a nested group's member give the reference's
+    normal (geometry/mod.rs:126-153): a ray cast at the KAT's point along the
+    KAT's normal hits there and prepare_computations returns that normal."""
+    w = _normal_on_child_world(rt)
+    p, n = (np.array(v) for v in NORMAL_KAT)
+    h = oracle.OracleWorld.from_world(w).hit(p + 2.0 * n, -n)
+    assert h[0] == 0
+    assert np.abs(h[2:5] - p).max() < 1e-3 and np.abs(h[14:17] - n).max() < 1e-3
+
+
+@pytest.mark.gpu
+def test_gpu_group_hits_bitwise_vs_oracle(rt, oracle):
+    """World::intersect + hit + prepare_computations through group gates: the
+    KAT's nested-group normal, and random rays through the groups scene, bitwise
+    equal to the oracle (geometry exact; schlick within 1e-12)."""
+    w = _normal_on_child_world(rt)
+    p, n = (np.array(v) for v in NORMAL_KAT)
+    ray = np.array([list(p + 2.0 * n) + list(-n)])
+    g = w.hit_batch(ray)
+    ref = oracle.OracleWorld.from_world(w).hit(ray[0, :3], ray[0, 3:])
+    assert np.array_equal(g[0, :23], ref[:23])
+    from rtamd import scenes
+    rng = np.random.default_rng(5)
+    for make in (lambda: scenes.groups(32, 24), lambda: scenes.divided(32, 18), lambda: scenes.hexagon(32, 18)):
+        w, _, _ = make()
+        ow = oracle.OracleWorld.from_world(w)
+        k = 3000
+        o = rng.uniform([-3, 0.05, -6], [3, 3, 3], size=(k, 3))
+        d = rng.normal(size=(k, 3))
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        rays = np.hstack([o, d])
+        g = w.hit_batch(rays)
+        ref = np.array([ow.hit(r[:3], r[3:]) for r in rays])
+        hits = ref[:, 0] >= 0
+        assert hits.sum() > 50
+        assert np.array_equal(g[:, 0], ref[:, 0])
+        assert np.array_equal(g[hits, 1:23], ref[hits, 1:23])
+        assert np.abs(g[hits, 23] - ref[hits, 23]).max() <= 1e-12
+
+
 # --- GPU -------------------------------------------------------------------------
 
 TOL = 1e-5
