@@ -166,3 +166,37 @@ def test_host_buffer_pool_reuse_and_render():
     cam.render_shard_device(w, depth, 8, 0, 1, d.data_ptr(), 0, False)
     torch.cuda.synchronize()
     assert a.to_numpy().tobytes() == d.cpu().numpy().tobytes()
+
+
+def test_scene_create_groups_validation_without_gpu(rt):
+    """rt_scene_create_groups (ABI 6) checks its group table before any device
+    work: a parent must be -1 or an earlier group, a shape's group must exist;
+    a valid hierarchy then fails only for want of a device (no CPU fallback)."""
+    import struct
+    lib = ctypes.CDLL(LIB)
+    f = lib.rt_scene_create_groups
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int32), ctypes.c_char_p, ctypes.c_size_t,
+                  ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+    s1, s2 = rt.Sphere(), rt.Sphere()
+    s2.set_transform(rt.translation(3, 0, 0))
+    shapes = s1.desc_bytes() + s2.desc_bytes()
+
+    def group(parent):  # rt_group_desc: min[3], max[3], parent, _pad (56 B)
+        return struct.pack("<6dii", -1, -1, -1, 4, 1, 1, parent, 0)
+
+    def create(groups, sg):
+        out = ctypes.c_void_p()
+        arr = (ctypes.c_int32 * len(sg))(*sg)
+        rc = f(shapes, 2, arr, groups, len(groups) // 56, None, 0, 0, ctypes.byref(out))
+        if rc == 0:  # (a GPU is present)
+            lib.rt_scene_destroy.argtypes = [ctypes.c_void_p]
+            lib.rt_scene_destroy(out)
+        return rc
+
+    assert create(group(-1) + group(5), [0, 1]) == -1  # parent after the group
+    assert create(group(-1) + group(1), [0, 1]) == -1  # a group its own parent
+    assert create(group(-2), [0, 0]) == -1
+    assert create(group(-1), [0, 3]) == -1  # no group 3
+    assert create(group(-1), [-2, 0]) == -1
+    assert create(group(-1) + group(0), [1, -1]) in (0, -8)  # valid: RT_ERR_NO_DEVICE without a GPU
