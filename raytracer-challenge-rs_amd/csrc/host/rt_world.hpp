@@ -220,6 +220,26 @@ struct Group {
   Material material;
   BoundingBox bbox;  // BaseShape::default: empty
   std::vector<GroupChild> children;
+  // A Group owns its children (Vec<Box<dyn Shape>>): copies are deep, so a copy
+  // added to another group (add_child takes its own) or handed out (child(i))
+  // never shares a shape with the original
+  Group() = default;
+  Group(const Group& o)
+      : transform(o.transform), transform_inverse(o.transform_inverse), material(o.material), bbox(o.bbox) {
+    children.reserve(o.children.size());
+    for (const GroupChild& c : o.children)
+      children.push_back(c.shape ? GroupChild{std::make_shared<Shape>(*c.shape), nullptr}
+                                 : GroupChild{nullptr, std::make_shared<Group>(*c.group)});
+  }
+  Group& operator=(const Group& o) {
+    if (this != &o) {
+      Group t(o);
+      *this = std::move(t);
+    }
+    return *this;
+  }
+  Group(Group&&) = default;
+  Group& operator=(Group&&) = default;
   void set_transform(const Matrix& t);                          // group.rs:71-94
   void set_material(const Material& m);                         // group.rs:96-102
   void add_child(const Shape& s) { add(GroupChild{std::make_shared<Shape>(s), nullptr}); }  // group.rs:128-133

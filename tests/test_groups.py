@@ -164,6 +164,24 @@ def test_transform_is_baked_into_children(rt):  # group.rs:71-94,128-133
     assert g.child(0).transform == rt.translation(0, 1, 0) * rt.translation(5, 0, 0)
 
 
+def test_groups_own_their_children(rt):
+    """add_child takes the group (Box<dyn Shape>, group.rs:128-133): a group added
+    to another, then transformed through its parent, leaves the caller's object
+    as it was; child(i) hands out a copy."""
+    inner = rt.Group()
+    s = rt.Sphere()
+    s.set_transform(rt.translation(1, 0, 0))
+    inner.add_child(s)
+    outer = rt.Group()
+    outer.add_child(inner)
+    outer.set_transform(rt.scaling(2, 2, 2))
+    assert inner.child(0).transform == rt.translation(1, 0, 0)
+    assert outer.child(0).child(0).transform == rt.scaling(2, 2, 2) * rt.translation(1, 0, 0)
+    c = outer.child(0)
+    c.set_transform(rt.translation(0, 5, 0))
+    assert outer.child(0).child(0).transform == rt.scaling(2, 2, 2) * rt.translation(1, 0, 0)
+
+
 def test_set_material_recurses(rt):  # group.rs:96-102
     inner = rt.Group()
     inner.add_child(rt.Sphere())
