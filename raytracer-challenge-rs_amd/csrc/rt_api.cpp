@@ -1003,6 +1003,7 @@ int rt_scene_create_groups(const rt_shape_desc* shapes, size_t n_shapes, const i
   const std::vector<BvhPair> bvh_pair = pair_layout(bvh);
   int wide_stack = 0;
   const std::vector<BvhWide> bvh_wide = wide_layout(bvh, diag, &wide_stack);
+  const std::vector<BvhWide16> bvh_wide16 = wide16_layout(bvh_wide);
   // ... and over the other bounded records (general spheres, cubes, cylinders
   // with finite caps); the rest stays exhaustive on the fast path too
   std::vector<OtherRec> orec;
@@ -1061,7 +1062,8 @@ int rt_scene_create_groups(const rt_shape_desc* shapes, size_t n_shapes, const i
   const size_t o_bv = align(o_qd + (quads.size() + 1) * sizeof(QuadRec));
   const size_t o_bp = align(o_bv + (bvh.size() + 1) * sizeof(BvhNode));
   const size_t o_bw = align(o_bp + (bvh_pair.size() + 1) * sizeof(BvhPair));
-  const size_t o_ob = align(o_bw + (bvh_wide.size() + 1) * sizeof(BvhWide));
+  const size_t o_bh = align(o_bw + (bvh_wide.size() + 1) * sizeof(BvhWide));
+  const size_t o_ob = align(o_bh + (bvh_wide16.size() + 1) * sizeof(BvhWide16));
   const size_t o_or = align(o_ob + (obvh.size() + 1) * sizeof(BvhNode));
   const size_t o_fg = align(o_or + (orec.size() + 1) * sizeof(OtherRec));
   const size_t o_fq = align(o_fg + (fx_gen.size() + 1) * sizeof(SphereGen));
@@ -1082,6 +1084,7 @@ int rt_scene_create_groups(const rt_shape_desc* shapes, size_t n_shapes, const i
   if (!bvh.empty()) std::memcpy(&host[o_bv], bvh.data(), bvh.size() * sizeof(BvhNode));
   if (!bvh_pair.empty()) std::memcpy(&host[o_bp], bvh_pair.data(), bvh_pair.size() * sizeof(BvhPair));
   if (!bvh_wide.empty()) std::memcpy(&host[o_bw], bvh_wide.data(), bvh_wide.size() * sizeof(BvhWide));
+  if (!bvh_wide16.empty()) std::memcpy(&host[o_bh], bvh_wide16.data(), bvh_wide16.size() * sizeof(BvhWide16));
   if (!obvh.empty()) std::memcpy(&host[o_ob], obvh.data(), obvh.size() * sizeof(BvhNode));
   if (!orec.empty()) std::memcpy(&host[o_or], orec.data(), orec.size() * sizeof(OtherRec));
   if (!fx_gen.empty()) std::memcpy(&host[o_fg], fx_gen.data(), fx_gen.size() * sizeof(SphereGen));
@@ -1134,6 +1137,7 @@ int rt_scene_create_groups(const rt_shape_desc* shapes, size_t n_shapes, const i
   s->dev.bvh = bvh.empty() ? nullptr : (const BvhNode*)(b + o_bv);
   s->dev.bvh_pair = bvh_pair.empty() ? nullptr : (const BvhPair*)(b + o_bp);
   s->dev.bvhw = bvh_wide.empty() ? nullptr : (const BvhWide*)(b + o_bw);
+  s->dev.bvhw16 = bvh_wide16.empty() ? nullptr : (const BvhWide16*)(b + o_bh);
   s->dev.n_bvhw = (int32_t)bvh_wide.size();
   s->dev.bvhw_stack = wide_stack;
   s->dev.n_bvh = (int32_t)bvh.size();

@@ -75,6 +75,31 @@ float f32_up(double x) {
   if ((double)f < x) f = std::nextafter(f, INFINITY);
   return f;
 }
+// binary16 rounded outward, as bit patterns (BvhWide): the largest binary16
+// value <= x (f16_bits_down) or the smallest >= x (f16_bits_up); past the
+// largest finite value, the infinity on that side
+static uint16_t f16_bits(double q) {  // q: a binary16 value (or an infinity)
+  const uint16_t sign = std::signbit(q) ? 0x8000u : 0u;
+  const double a = std::fabs(q);
+  if (std::isinf(a)) return sign | 0x7C00u;
+  if (a < 0x1p-14) return sign;  // zero (f16_floor makes no subnormals)
+  int e;
+  const double m = std::frexp(a, &e);  // a = m 2^e, m in [0.5, 1)
+  return sign | (uint16_t)((e + 14) << 10) | (uint16_t)((m * 2.0 - 1.0) * 1024.0);
+}
+// (no subnormal results: a value below the smallest normal goes to 0 or to
+// -2^-14, so no flush of subnormal inputs can move a plane inward)
+static double f16_floor(double x) {
+  if (std::isnan(x)) return -INFINITY;
+  if (std::isinf(x)) return x;
+  const double ax = std::fabs(x);
+  if (ax < 0x1p-14) return x >= 0.0 ? 0.0 : -0x1p-14;
+  int e;
+  std::frexp(ax, &e);
+  const double u = std::ldexp(1.0, e - 11);  // the spacing at |x|
+  const double q = std::floor(x / u) * u;
+  return q < -65504.0 ? -INFINITY : q > 65504.0 ? 65504.0 : q;
+}
 
 // Binned-SAH builder over item boxes; produces the node array and the leaf
 // order of the items (`order[k]` = original index of the k-th leaf item).
@@ -324,6 +349,9 @@ double invert3(const double* m, double F[3][3]) {
 
 }  // namespace
 
+uint16_t f16_bits_down(double x) { return f16_bits(f16_floor(x)); }
+uint16_t f16_bits_up(double x) { return f16_bits(-f16_floor(-x)); }
+
 std::vector<BvhNode> build_sphere_bvh(std::vector<SphereDiag>& spheres, int leaf_size, int* depth, double trav_cost) {
   std::vector<Box> boxes(spheres.size());
   for (size_t i = 0; i < spheres.size(); ++i) boxes[i] = sphere_box(spheres[i]);
@@ -480,11 +508,11 @@ std::vector<BvhWide> wide_layout(const std::vector<BvhNode>& nodes, const std::v
   }
   if (!ok || tmp.size() >= 0x8000) return {};
   if (stack) *stack = need[0];
-  // renumber: breadth-first for the first kTreeletNodes / 2 nodes, then each
+  // renumber: breadth-first for the first kTreeletNodes nodes, then each
   // remaining subtree depth-first (as treelet_order does for the binary nodes)
   std::vector<int> order{0};
   size_t h = 0;
-  for (; h < order.size() && order.size() < kTreeletNodes / 2; ++h)
+  for (; h < order.size() && order.size() < kTreeletNodes; ++h)
     for (int j = 0; j < 4; ++j)
       if (tmp[order[h]].child[j] < 0x8000) order.push_back(tmp[order[h]].child[j]);
   std::vector<int> frontier(order.begin() + (long)h, order.end()), st;
@@ -506,6 +534,19 @@ std::vector<BvhWide> wide_layout(const std::vector<BvhNode>& nodes, const std::v
     out[i] = tmp[order[i]];
     for (int j = 0; j < 4; ++j)
       if (out[i].child[j] < 0x8000) out[i].child[j] = remap[out[i].child[j]];
+  }
+  return out;
+}
+
+std::vector<BvhWide16> wide16_layout(const std::vector<BvhWide>& w) {
+  std::vector<BvhWide16> out(w.size());
+  for (size_t i = 0; i < w.size(); ++i) {
+    for (int a = 0; a < 3; ++a)
+      for (int j = 0; j < 4; ++j) {
+        out[i].lo[a][j] = f16_bits_down(w[i].lo[a][j]);
+        out[i].hi[a][j] = f16_bits_up(w[i].hi[a][j]);
+      }
+    for (int j = 0; j < 4; ++j) out[i].child[j] = w[i].child[j];
   }
   return out;
 }

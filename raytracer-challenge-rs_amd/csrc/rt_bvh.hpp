@@ -31,6 +31,11 @@ std::vector<BvhPair> pair_layout(const std::vector<BvhNode>& nodes);
 // the top of the tree, for an LDS treelet). `stack` receives the most entries
 // a near-first traversal keeps pending. Empty when the 16-bit codes cannot
 // index the nodes or records.
+// the global-memory copy of a four-wide image: its boxes rounded outward to binary16
+std::vector<BvhWide16> wide16_layout(const std::vector<BvhWide>& w);
+// binary16 bit patterns rounded outward (BvhWide16 boxes)
+uint16_t f16_bits_down(double x);
+uint16_t f16_bits_up(double x);
 std::vector<BvhWide> wide_layout(const std::vector<BvhNode>& nodes, const std::vector<SphereDiag>& spheres,
                                  int* stack);
 

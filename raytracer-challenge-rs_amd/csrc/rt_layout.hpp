@@ -15,6 +15,7 @@
 //   lights         : 6 doubles each (position, intensity), wave-uniform.
 #pragma once
 #include <stdint.h>
+#include <cmath>
 
 namespace rtamd {
 
@@ -89,18 +90,16 @@ struct alignas(64) BvhPair {
   uint32_t pad;
 };
 static_assert(sizeof(BvhPair) == 64, "BvhPair must stay 64 B");
-// The same hierarchy collapsed to four children per node, for scenes whose
-// nodes are read from global memory (lane_trace_wide): one 128-B line per
-// node, so a ray makes half the dependent node loads of the binary layout.
-// Slot j's box is lo[a][j], hi[a][j] (one 16-B load per plane and axis),
-// child[j] a 16-bit code: a node index (< 0x8000), 0x8000 | the index of
-// one sphere record (every leaf holds one record), or 0xFFFF (empty; its box
-// is inverted, lo = +inf and hi = -inf, so no ray with a usable axis meets it). The boxes
-// are the binary nodes' own (a collapsed node's children are its binary
-// descendants) or, below a binary leaf of several records, each record's own
-// padded box (and unions of them) rounded outward to binary32: every box holds
-// what lies below it, so every culling decision stays exact (DESIGN.md "Exact
-// culling").
+// The same hierarchy collapsed to four children per node (lane_trace_wide,
+// LANE 15: the whole image in LDS): one 128-B node. Slot j's box is lo[a][j],
+// hi[a][j] (one 16-B load per plane block and axis), child[j] a 16-bit code: a
+// node index (< 0x8000), 0x8000 | the index of one sphere record (every leaf
+// holds one record), or 0xFFFF (empty; its box is inverted, lo = +inf and hi =
+// -inf, so no ray with a usable axis meets it). The boxes are the binary
+// nodes' own (a collapsed node's children are its binary descendants) or,
+// below a binary leaf of several records, each record's own padded box (and
+// unions of them) rounded outward to binary32: every box holds what lies below
+// it, so every culling decision stays exact (DESIGN.md "Exact culling").
 struct alignas(128) BvhWide {
   float lo[3][4];
   float hi[3][4];
@@ -108,6 +107,31 @@ struct alignas(128) BvhWide {
   uint32_t pad[6];
 };
 static_assert(sizeof(BvhWide) == 128, "BvhWide must stay 128 B");
+// The four-wide image read from global memory (LANE 4, with a treelet of its
+// top nodes in LDS): the same nodes in 64 B, the planes rounded outward again,
+// to binary16 (a coordinate past binary16's range becomes an infinite plane),
+// so each box still holds what lies below it. A visit reads 56 B instead of
+// 104, twice the nodes fit a cache line and the treelet, and v_fma_mix_f32
+// converts each half exactly inside the slab test's FMA. The culling loses
+// little: the area-weighted visit cost of C3's and C5's hierarchies grows by
+// 0.3 % and 0.5 %, the record tests by 1.1 % and 2.6 % (tools/wide_sah.cpp).
+// (The LDS image stays binary32: there the mixed FMAs cost more issue time
+// than the halved LDS reads save, C3 closest class +3 %; from global memory
+// C5 runs 4 % faster)
+struct alignas(64) BvhWide16 {
+  uint16_t lo[3][4];  // binary16 bit patterns
+  uint16_t hi[3][4];
+  uint16_t child[4];
+  uint32_t pad[2];
+};
+static_assert(sizeof(BvhWide16) == 64, "BvhWide16 must stay 64 B");
+// binary16 bits -> value (host checks and tools; the device converts in the FMA)
+inline float wide_f16(uint16_t b) {
+  const int e = (b >> 10) & 31, m = b & 1023;
+  const float v = e == 31 ? (m ? NAN : INFINITY)
+                          : e == 0 ? std::ldexp((float)m, -24) : std::ldexp((float)(1024 + m), e - 25);
+  return (b & 0x8000u) ? -v : v;
+}
 constexpr unsigned kWideEmpty = 0xFFFFu, kWideLeaf = 0x8000u;  // BvhWide child codes: empty, leaf flag
 // A culled record other than a diagonal sphere: the QuadRec layout, with
 // kind 0 = sphere under a general inverse (rows 0-2 in m).
@@ -204,6 +228,7 @@ struct DevScene {
   // the sphere hierarchy collapsed to four children per node (nullptr when its
   // 16-bit codes cannot index it), and the most stack entries its traversal keeps
   const BvhWide* bvhw;
+  const BvhWide16* bvhw16;  // the same nodes in binary16 (the global-memory image)
   int32_t n_bvhw, bvhw_stack;
   // per object: ShadeRec::reflective, transparency (what wf_combine_parents reads; 16 B a
   // record, so the table stays in the L2 where the 512-B shading records may not)

@@ -6,6 +6,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "rt_device.hpp"
 #include "rt_wavefront.hpp"
 
@@ -304,33 +306,44 @@ __device__ __forceinline__ void lane_trace(const BvhNode* nodes, const SphereDia
     }
   }
 }
-// Per-lane traversal over the four-wide layout (LANE == 4, BvhWide; scenes read
-// from global memory): a visit loads the parts of one 128-B node it needs (six
-// 16-B loads and one 8-B load: per axis the block of the four entry planes and
-// the block of the four exit planes, chosen by the sign of the ray's direction
-// there as in lane_trace_pair, whose byte offsets sit packed in two registers;
-// the four child codes), tests the four boxes with no per-axis min/max, goes on
-// to the nearest child hit and pushes the others farthest first. The order is
-// a sorting network over four 32-bit keys (the entry distance's bits with the
-// slot in the two low bits, a miss all ones: non-negative binary32 values
-// order as their bits do; ties and the two dropped bits only change the visit
-// order); the slots' child codes come from one 64-bit word. A ray makes about
-// half the dependent node loads of the binary walk. The stack is 16-bit, in
-// LDS (entry k of lane t at lds[k * kTraceBlock + t], sc.bvhw_stack entries at
-// most); the first n_top nodes are read from their LDS copy `top`. Culling is
+// Per-lane traversal over the four-wide layout (NODE: BvhWide, 128-B binary32
+// nodes, LANE 15 with the whole image in LDS; BvhWide16, 64-B binary16 nodes,
+// LANE 4 from global memory with a treelet in LDS): a visit loads the parts of
+// the node it needs (per axis the block of the four entry planes and the block
+// of the four exit planes, chosen by the sign of the ray's direction there as
+// in lane_trace_pair, whose byte offsets sit packed in two registers: six 16-B
+// loads, or six 8-B ones for binary16; and the four child codes in one 8-B
+// load), tests the four boxes with no per-axis min/max, goes on to the nearest
+// child hit and pushes the others farthest first. The order is a sorting
+// network over four 32-bit keys (the entry distance's bits with the slot in
+// the two low bits, a miss all ones: non-negative binary32 values order as
+// their bits do; ties and the two dropped bits only change the visit order);
+// the slots' child codes come from one 64-bit word. A ray makes about half the
+// dependent node loads of the binary walk. The stack is 16-bit, in LDS (entry
+// k of lane t at lds[k * kTraceBlock + t], sc.bvhw_stack entries at most); the
+// first n_top nodes are read from their LDS copy `top`. Culling is
 // slab_hit32's rule (the same entry and exit values) on boxes that each hold
-// what lies below them, so the hit is the same; empty slots have inverted
-// boxes, which cull themselves for every ray with a usable axis, and a ray
-// with none (a huge origin, a NaN) tests every record, as a walk that culls
-// nothing would. Leaves are batched across the wave as in lane_trace.
+// what lies below them, so the hit is the same. Binary16 planes enter the
+// binary32 FMA exactly (v_fma_mix_f32); since their outward rounding moves a
+// coordinate by up to 2^-10 of its magnitude, slab_ray's bound M is widened by
+// 2^-9 of itself for them (an infinite plane, past binary16's range, gives an
+// infinite distance, or NaN on an axis that culls nothing, which the min/max
+// drop). Empty slots have inverted boxes, which cull themselves for every ray
+// with a usable axis, and a ray with none (a huge origin, a NaN) tests every
+// record, as a walk that culls nothing would. Leaves are batched across the
+// wave as in lane_trace.
 // SD: the sphere records (const SphereDiag* in global memory, or Sph48 in LDS);
 // ALL_LDS: every node is in `top` (LANE 15: the whole hierarchy in LDS).
-template <bool SHADOW, typename SD = const SphereDiag*, bool ALL_LDS = false>
-__device__ __forceinline__ void lane_trace_wide(const BvhWide* nodes, SD sd, const float* M,
+template <bool SHADOW, typename SD = const SphereDiag*, bool ALL_LDS = false, typename NODE = BvhWide>
+__device__ __forceinline__ void lane_trace_wide(const NODE* nodes, SD sd, const float* M,
                                                 bool has_bvh, V3 o, V3 d, double t_shadow, Hit& h, unsigned& n_disc,
                                                 unsigned& n_tests, unsigned& n_boxes, uint16_t* lds,
-                                                const BvhWide* top, int n_top, int n_records) {
-  const SlabRay sr = slab_ray(o, d, M);
+                                                const NODE* top, int n_top, int n_records) {
+  constexpr bool H = sizeof(NODE) == 64;  // BvhWide16
+  constexpr unsigned kBlk = H ? 8u : 16u, kHi = 3u * kBlk, kCc = 6u * kBlk;  // plane block, hi planes, child codes
+  const float w = H ? 1.0f + 0x1p-9f : 1.0f;
+  const float Mw[3] = {M[0] * w, M[1] * w, M[2] * w};
+  const SlabRay sr = slab_ray(o, d, Mw);
   float t_hi = f32_up(SHADOW ? t_shadow : h.t);
   int sp = 0;
   auto pop = [&]() -> unsigned { return sp > 0 ? (unsigned)lds[(--sp) * kTraceBlock] : kWideEmpty; };
@@ -346,8 +359,8 @@ __device__ __forceinline__ void lane_trace_wide(const BvhWide* nodes, SD sd, con
     on[a] = neg ? sr.c_hi[a] : sr.c_lo[a];
     of[a] = neg ? sr.c_lo[a] : sr.c_hi[a];
     usable |= sr.inv[a] != 0.0f;
-    offe |= (16u * a + (neg ? 48u : 0u)) << (8 * a);
-    offx |= (16u * a + (neg ? 0u : 48u)) << (8 * a);
+    offe |= (kBlk * a + (neg ? kHi : 0u)) << (8 * a);
+    offx |= (kBlk * a + (neg ? 0u : kHi)) << (8 * a);
   }
   asm volatile("" : "+v"(offe), "+v"(offx));
   if (e == 0u && !usable) {  // no axis can cull (empty slots' inverted boxes need one): every record
@@ -359,40 +372,45 @@ __device__ __forceinline__ void lane_trace_wide(const BvhWide* nodes, SD sd, con
     }
   }
   auto visit = [&]() {
-    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
     typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-    u32x4 E[3], X[3];
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+    typedef typename std::conditional<H, u32x2, u32x4>::type Blk;  // one block of four planes
+    Blk E[3], X[3];
     u32x2 cc;
     if (ALL_LDS || (int)e < n_top) {
       typedef __attribute__((address_space(3))) const unsigned char lb;
-      lb* b = (lb*)(top) + e * 128u;
-      cc = *(__attribute__((address_space(3))) const u32x2*)(b + 96);
+      lb* b = (lb*)(top) + e * (unsigned)sizeof(NODE);
+      cc = *(__attribute__((address_space(3))) const u32x2*)(b + kCc);
 #pragma unroll
       for (int a = 0; a < 3; ++a) {
-        E[a] = *(__attribute__((address_space(3))) const u32x4*)(b + ((offe >> (8 * a)) & 0xFFu));
-        X[a] = *(__attribute__((address_space(3))) const u32x4*)(b + ((offx >> (8 * a)) & 0xFFu));
+        E[a] = *(__attribute__((address_space(3))) const Blk*)(b + ((offe >> (8 * a)) & 0xFFu));
+        X[a] = *(__attribute__((address_space(3))) const Blk*)(b + ((offx >> (8 * a)) & 0xFFu));
       }
     } else {
       typedef __attribute__((address_space(1))) const unsigned char gb;
       gb* b = (gb*)(nodes);
-      const unsigned n0 = e * 128u;
+      const unsigned n0 = e * (unsigned)sizeof(NODE);
 #pragma unroll
       for (int a = 0; a < 3; ++a) {
-        E[a] = *(__attribute__((address_space(1))) const u32x4*)(b + (n0 + ((offe >> (8 * a)) & 0xFFu)));
-        X[a] = *(__attribute__((address_space(1))) const u32x4*)(b + (n0 + ((offx >> (8 * a)) & 0xFFu)));
+        E[a] = *(__attribute__((address_space(1))) const Blk*)(b + (n0 + ((offe >> (8 * a)) & 0xFFu)));
+        X[a] = *(__attribute__((address_space(1))) const Blk*)(b + (n0 + ((offx >> (8 * a)) & 0xFFu)));
       }
-      cc = *(__attribute__((address_space(1))) const u32x2*)(b + (n0 + 96u));
+      cc = *(__attribute__((address_space(1))) const u32x2*)(b + (n0 + kCc));
     }
+    // plane j of a block (binary16: converted inside the FMA, v_fma_mix_f32)
+    auto pl = [&](const Blk& q, int j) -> float {
+      if constexpr (H) return (float)__builtin_bit_cast(f16x4, q)[j];
+      else return __uint_as_float(q[j]);
+    };
     unsigned key[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float t0 = fmaxf(fmaxf(fmaf(__uint_as_float(E[0][j]), sr.inv[0], -on[0]),
-                                   fmaf(__uint_as_float(E[1][j]), sr.inv[1], -on[1])),
-                             fmaxf(fmaf(__uint_as_float(E[2][j]), sr.inv[2], -on[2]), 0.0f));
+      const float t0 = fmaxf(fmaxf(fmaf(pl(E[0], j), sr.inv[0], -on[0]), fmaf(pl(E[1], j), sr.inv[1], -on[1])),
+                             fmaxf(fmaf(pl(E[2], j), sr.inv[2], -on[2]), 0.0f));
       float zt;  // (t_hi is canonical: no per-visit re-canonicalisation, as in lane_trace_pair)
-      asm("v_min_f32 %0, %1, %2" : "=v"(zt) : "v"(fmaf(__uint_as_float(X[2][j]), sr.inv[2], -of[2])), "v"(t_hi));
-      const float t1 = fminf(fminf(fmaf(__uint_as_float(X[0][j]), sr.inv[0], -of[0]),
-                                   fmaf(__uint_as_float(X[1][j]), sr.inv[1], -of[1])), zt);
+      asm("v_min_f32 %0, %1, %2" : "=v"(zt) : "v"(fmaf(pl(X[2], j), sr.inv[2], -of[2])), "v"(t_hi));
+      const float t1 = fminf(fminf(fmaf(pl(X[0], j), sr.inv[0], -of[0]), fmaf(pl(X[1], j), sr.inv[1], -of[1])), zt);
       key[j] = t0 <= t1 ? ((__float_as_uint(t0) & ~3u) | (unsigned)j) : ~0u;
     }
     n_boxes += 4;
@@ -656,13 +674,14 @@ struct LaneScene {
   float M[3];                  // bound on |box coordinate| per axis (slab_ray)
   const BvhNode* top;          // 3: the LDS copy of the first n_top nodes
   int n_top;
-  const BvhWide* wtop;         // 4: the LDS copy of the first n_top wide nodes
+  const BvhWide* wtop;         // 15: the LDS copy of the wide nodes
+  const BvhWide16* wtop16;     // 4: the LDS copy of the first n_top binary16 wide nodes
 };
 template <int LANE>
 __device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, unsigned lds_flags, unsigned n_top, int* static_stack,
                                                 unsigned char* dyn) {
   LaneScene ls{(const unsigned char*)sc.bvh, sc.sph_diag, Sph48{nullptr, nullptr}, nullptr, sc.lb_delta, nullptr,
-               static_stack, {0.f, 0.f, 0.f}, nullptr, 0, nullptr};
+               static_stack, {0.f, 0.f, 0.f}, nullptr, 0, nullptr, nullptr};
   unsigned char* p = dyn;
   if constexpr (LANE == 15) {  // [16-bit stack][every wide node][Sph48 records and metas]
     ls.stack16 = (uint16_t*)dyn + threadIdx.x;
@@ -684,14 +703,14 @@ __device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, unsigned lds
     ls.s48 = Sph48{(const double*)p, (const int*)mt};
     p += sph48_lds_bytes(sc);
   }
-  if constexpr (LANE == 4) {  // [16-bit stack][distances][treelet of wide nodes]
+  if constexpr (LANE == 4) {  // [16-bit stack][distances][treelet of binary16 wide nodes]
     ls.stack16 = (uint16_t*)dyn + threadIdx.x;
     p += wide_stack_bytes(sc);
-    ls.nodes = (const unsigned char*)sc.bvhw;
+    ls.nodes = (const unsigned char*)sc.bvhw16;
     if (n_top > 0) {
       unsigned char* q = p + ((lds_flags & kLdsDeltas) ? delta_lds_bytes(sc) : 0);
-      stage_lds((uint4*)q, (const uint4*)sc.bvhw, (int)n_top * (int)(sizeof(BvhWide) / 16));
-      ls.wtop = (const BvhWide*)q;
+      stage_lds((uint4*)q, (const uint4*)sc.bvhw16, (int)n_top * (int)(sizeof(BvhWide16) / 16));
+      ls.wtop16 = (const BvhWide16*)q;
       ls.n_top = (int)n_top;
     }
   }
@@ -837,8 +856,8 @@ __device__ __forceinline__ bool shadow_trace(const DevScene& sc, unsigned use_lb
       lane_trace_wide<true, Sph48, true>((const BvhWide*)ls.nodes, ls.s48, ls.M, sc.bvhw != nullptr, o, d, dist, h, n_disc,
                                          n_tests, n_boxes, ls.stack16, ls.wtop, ls.n_top, sc.n_diag);
     } else if constexpr (LANE == 4) {
-      lane_trace_wide<true>((const BvhWide*)ls.nodes, ls.sd, ls.M, sc.bvhw != nullptr, o, d, dist, h, n_disc, n_tests,
-                            n_boxes, ls.stack16, ls.wtop, ls.n_top, sc.n_diag);
+      lane_trace_wide<true>((const BvhWide16*)ls.nodes, ls.sd, ls.M, sc.bvhw16 != nullptr, o, d, dist, h, n_disc,
+                            n_tests, n_boxes, ls.stack16, ls.wtop16, ls.n_top, sc.n_diag);
 
     } else if constexpr (LANE == 0) {
       Hit hb;  // the wave traversal starts from an empty hit; any blocker is an answer

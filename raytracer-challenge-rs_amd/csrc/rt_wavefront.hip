@@ -913,8 +913,8 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
           lane_trace_wide<false, Sph48, true>((const BvhWide*)ls.nodes, ls.s48, ls.M, sc.bvhw != nullptr, o, d, 0.0, h,
                                               t.disc, t.tests, t.boxes, ls.stack16, ls.wtop, ls.n_top, sc.n_diag);
         } else if constexpr (LANE == 4) {
-          lane_trace_wide<false>((const BvhWide*)ls.nodes, ls.sd, ls.M, sc.bvhw != nullptr, o, d, 0.0, h, t.disc, t.tests,
-                                 t.boxes, ls.stack16, ls.wtop, ls.n_top, sc.n_diag);
+          lane_trace_wide<false>((const BvhWide16*)ls.nodes, ls.sd, ls.M, sc.bvhw16 != nullptr, o, d, 0.0, h, t.disc,
+                                 t.tests, t.boxes, ls.stack16, ls.wtop16, ls.n_top, sc.n_diag);
         } else {
           lane_trace<false, LANE == 3>((const BvhNode*)ls.nodes, ls.sd, ls.M, sc.n_bvh > 0, o, d, 0.0, h, t.disc,
                                        t.tests, t.boxes, ls.stack, ls.top, ls.n_top);
@@ -1489,7 +1489,7 @@ static hipError_t launch_fused_q(const DevScene& sc, const DevCamera& cam, WfArg
   a.lds_flags = 0;
   // primary rays: the wave traversal, or with prim_lane the per-lane walk of the pair image or of
   // the four-wide hierarchy (the launches below, reading camera rays)
-  const bool wide_ok = tn.image != 1 && tn.wide && sc.bvhw && wide_stack_bytes(sc) <= kWfLdsLimit / 2;
+  const bool wide_ok = tn.image != 1 && tn.wide && sc.bvhw16 && wide_stack_bytes(sc) <= kWfLdsLimit / 2;
   // prim_lane 1: any per-lane image; 2 (default): the LDS images only (C3 primary class 0.128 ->
   // 0.125 ms/frame with the LDS four-wide image; C5's global image 2.06 -> 2.16 ms, so not there)
   const bool wide_lds = sc.bvhw && tn.lds_wide && wide_lds_bytes(sc) + dl <= kWfLdsLimit;
@@ -1527,8 +1527,8 @@ static hipError_t launch_fused_q(const DevScene& sc, const DevCamera& cam, WfArg
     dyn = wide_stack_bytes(sc);
     if (dl && dl <= room && (!tn.treelet || tn.treelet_deltas)) { a.lds_flags |= kLdsDeltas; dyn += dl; }
     if (tn.treelet) {
-      a.n_top = (unsigned)std::min<size_t>((size_t)sc.n_bvhw, (kWfLdsLimit - dyn) / sizeof(BvhWide));
-      dyn += (size_t)a.n_top * sizeof(BvhWide);
+      a.n_top = (unsigned)std::min<size_t>((size_t)sc.n_bvhw, (kWfLdsLimit - dyn) / sizeof(BvhWide16));
+      dyn += (size_t)a.n_top * sizeof(BvhWide16);
     }
     return launch_global(4, QUADS, TALLY, cam_rays, sc, cam, a, dyn, n, stream, tb);
   }

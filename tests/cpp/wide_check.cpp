@@ -3,7 +3,9 @@
 // Checks that every record is reached exactly once, that every slot's box
 // holds the records below it (each record's padded box, so the culling stays
 // exact), that child codes are 16-bit, and that a near-first traversal of
-// random rays never keeps more entries pending than the reported stack bound.
+// random rays never keeps more entries pending than the reported stack bound;
+// that the binary16 copy (wide16_layout) holds the same codes and boxes that
+// hold the binary32 ones; and the binary16 outward rounding itself.
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -20,7 +22,31 @@ static int fail(const char* what, int a, int b) {
   return 1;
 }
 
+// f16_bits_down / f16_bits_up: the nearest binary16 at or below / above x
+// (normal or zero, an infinity past the range), checked against the spacing
+static int check_f16() {
+  std::mt19937_64 g(99);
+  std::uniform_real_distribution<double> u(-1.0, 1.0);
+  for (int i = 0; i < 200000; ++i) {
+    const double x = u(g) * std::ldexp(1.0, (int)(g() % 44) - 24);
+    const float d = wide_f16(f16_bits_down(x)), up = wide_f16(f16_bits_up(x));
+    if (!((double)d <= x && (double)up >= x)) return fail("f16 side", i, 0);
+    const double ax = std::fabs(x);
+    if (ax >= 0x1p-14 && ax <= 65504.0) {
+      int e;
+      std::frexp(ax, &e);
+      const double sp = std::ldexp(1.0, e - 11);  // one binary16 step at |x|
+      if (x - d >= sp || up - x >= sp) return fail("f16 step", i, 0);
+    }
+    if (ax > 65504.0 && !(x > 0 ? std::isinf(up) && d == 65504.0f : std::isinf(d) && up == -65504.0f))
+      return fail("f16 range", i, 0);
+    if (ax < 0x1p-14 && !(x >= 0 ? d == 0.0f && up <= 0x1p-14f : d == -0x1p-14f && up == 0.0f)) return fail("f16 tiny", i, 0);
+  }
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  if (check_f16()) return 1;
   const int n = std::atoi(argv[1]), leaf = std::atoi(argv[2]);
   const double span = argc > 3 ? std::atof(argv[3]) : 50.0;
   std::mt19937_64 g(1234 + n * 7 + leaf);
@@ -38,6 +64,8 @@ int main(int argc, char** argv) {
   const std::vector<BvhNode> b = build_sphere_bvh(sp, leaf, &depth, 1.0);
   const std::vector<BvhWide> w = wide_layout(b, sp, &stack);
   if (w.empty()) return fail("empty", n, leaf);
+  const std::vector<BvhWide16> w16 = wide16_layout(w);
+  if (w16.size() != w.size()) return fail("size16", (int)w16.size(), (int)w.size());
   if (w.size() >= 0x8000) return fail("nodes", (int)w.size(), 0);
   std::vector<int> seen(n, 0), refs(w.size(), 0);
   // containment and coverage: walk from the root
@@ -50,7 +78,13 @@ int main(int argc, char** argv) {
       if (c == kWideEmpty) continue;
       if (c > 0xFFFFu) return fail("code", e, j);
       float lo[3], hi[3];
-      for (int a = 0; a < 3; ++a) { lo[a] = w[e].lo[a][j]; hi[a] = w[e].hi[a][j]; }
+      for (int a = 0; a < 3; ++a) {
+        lo[a] = w[e].lo[a][j];
+        hi[a] = w[e].hi[a][j];
+        // the global-memory copy's binary16 box holds the binary32 one
+        if (!(wide_f16(w16[e].lo[a][j]) <= lo[a] && wide_f16(w16[e].hi[a][j]) >= hi[a])) return fail("box16", e, j);
+      }
+      if (w16[e].child[j] != w[e].child[j]) return fail("code16", e, j);
       std::vector<int> below;
       if (c & kWideLeaf) {
         below.push_back((int)(c & 0x7FFFu));

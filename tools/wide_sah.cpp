@@ -4,6 +4,8 @@
 // "this subtree as at most k slots", k = 1..4), on the C3 / C5 sphere fields.
 // Cost = sum over visited wide nodes of P(visit) * c_visit + sum over record
 // slots of P(test) * c_test, P = area / area(root).
+// Usage: wide_sah [c3|c5] [c_visit] [c_test] [leaf] [f16]
+// (f16: the greedy cost over the binary16 copy's boxes, wide16_layout)
 // Build: g++ -O2 -std=c++17 -pthread -I raytracer-challenge-rs_amd/csrc tools/wide_sah.cpp
 //        raytracer-challenge-rs_amd/csrc/rt_bvh.cpp -o /tmp/wide_sah
 #include <algorithm>
@@ -89,6 +91,8 @@ int main(int argc, char** argv) {
   int depth = 0, stack = 0;
   const std::vector<BvhNode> b = build_sphere_bvh(sp, leaf, &depth, 0.7);
   const std::vector<BvhWide> w = wide_layout(b, sp, &stack);
+  const std::vector<BvhWide16> w16 = wide16_layout(w);
+  const bool f16 = argc > 5 && std::string(argv[5]) == "f16";
   // root area: union of the root node's two child boxes
   B3 root;
   for (int c = 0; c < 2; ++c) {
@@ -99,6 +103,7 @@ int main(int argc, char** argv) {
   const double A0 = root.area();
   // greedy (library) cost
   double greedy = cv;  // the root is always visited
+  double gv = cv, gt = 0.0;  // the visit and test parts
   int wn = 0;
   {
     std::vector<int> todo{0};
@@ -110,10 +115,13 @@ int main(int argc, char** argv) {
         const unsigned c = w[e].child[j];
         if (c == kWideEmpty) continue;
         B3 x;
-        for (int a = 0; a < 3; ++a) { x.lo[a] = w[e].lo[a][j]; x.hi[a] = w[e].hi[a][j]; }
+        for (int a = 0; a < 3; ++a) {
+          x.lo[a] = f16 ? wide_f16(w16[e].lo[a][j]) : w[e].lo[a][j];
+          x.hi[a] = f16 ? wide_f16(w16[e].hi[a][j]) : w[e].hi[a][j];
+        }
         const double p = x.area() / A0;
-        if (c & kWideLeaf) greedy += p * ct;
-        else { greedy += p * cv; todo.push_back((int)c); }
+        if (c & kWideLeaf) { greedy += p * ct; gt += p * ct; }
+        else { greedy += p * cv; gv += p * cv; todo.push_back((int)c); }
       }
     }
   }
@@ -175,7 +183,8 @@ int main(int argc, char** argv) {
   double opt = INFINITY;
   for (int j = 1; j <= 3; ++j) opt = std::min(opt, C[r.a][j] + C[r.b][4 - j]);
   opt += cv;
-  std::printf("%s leaf=%d c_visit=%.2f c_test=%.2f: greedy wide nodes=%d cost=%.3f  optimal cost=%.3f  (%.1f%%)\n",
-              c5 ? "C5" : "C3", leaf, cv, ct, wn, greedy, opt, 100.0 * (opt / greedy - 1.0));
+  std::printf("%s leaf=%d c_visit=%.2f c_test=%.2f%s: greedy wide nodes=%d cost=%.3f (visits %.3f, tests %.3f)  optimal cost=%.3f  (%.1f%%)\n",
+              c5 ? "C5" : "C3", leaf, cv, ct, f16 ? " (binary16 boxes)" : "", wn, greedy, gv, gt, opt,
+              100.0 * (opt / greedy - 1.0));
   return 0;
 }
