@@ -58,7 +58,7 @@ extern "C" int rtamd_nccl_comm_init(int nranks, const unsigned char* id, size_t 
 extern "C" int rtamd_nccl_comm_abort(void* comm);
 extern "C" int rtamd_nccl_gather_f64(const double* send, double* recv, size_t count, int root, void* comm, void* stream);
 extern "C" int rtamd_nccl_comm_destroy(void* comm);
-extern "C" int rtamd_wf_profile(const rt_scene* s, int enable, double out[36]);
+extern "C" int rtamd_wf_profile(const rt_scene* s, int enable, double out[38]);
 extern "C" int rtamd_scene_tuning_set(const rt_scene* s, const char* key, int value);
 
 PYBIND11_MODULE(_rtamd, m) {
@@ -537,7 +537,7 @@ PYBIND11_MODULE(_rtamd, m) {
       }, py::arg("max_depth") = 5)
       .def("render_to", &SceneParser::render_to, py::arg("path"), py::arg("max_depth") = 5);
   m.def("_wf_profile", [](const World& w, int enable, bool read) {
-    double o[36] = {0};
+    double o[38] = {0};
     check(rtamd_wf_profile(w.scene(), enable, read ? o : nullptr), "wf_profile");
     py::dict d;
     if (read) {
@@ -557,6 +557,7 @@ PYBIND11_MODULE(_rtamd, m) {
       shr["primary"] = o[29]; shr["closest"] = o[30]; sht["primary"] = o[31]; sht["closest"] = o[32];
       d["shadow_rays_in"] = shr; d["shadow_tests_in"] = sht; d["fused"] = (bool)o[33];
       d["n_bvh_wide"] = (int)o[34]; d["wide_stack"] = (int)o[35];
+      d["n_lbvh_nodes"] = (int)o[36]; d["n_line_culled"] = (int)o[37];
     }
     return d;
   }, py::arg("world"), py::arg("enable") = -1, py::arg("read") = true);

@@ -602,8 +602,9 @@ const char* rt_last_error(void) { return g_err.c_str(); }
 // ms[5] (primary, closest, shadow, prep, combine), rays[3], disc[3],
 // n_diag, n_gen, n_planes, n_lights, n_quads, tests[3], boxes[3], bvh,
 // n_bvh_nodes, bvh_depth, n_obvh_nodes, n_other_culled, lb_res, lb_items, sh_rays[2], sh_tests[2]
-// (shadow rays / sphere tests inside the fused primary / secondary launches), fused.
-int rtamd_wf_profile(const rt_scene* cs, int enable, double out[36]) {
+// (shadow rays / sphere tests inside the fused primary / secondary launches), fused,
+// n_bvh_wide, wide_stack, n_lbvh_nodes, n_line_culled.
+int rtamd_wf_profile(const rt_scene* cs, int enable, double out[38]) {
   if (!cs) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
   rt_scene* s = const_cast<rt_scene*>(cs);
   std::lock_guard<std::mutex> lk(s->mu);
@@ -648,6 +649,8 @@ int rtamd_wf_profile(const rt_scene* cs, int enable, double out[36]) {
     out[33] = p.fused;
     out[34] = s->dev.bvhw ? s->dev.n_bvhw : 0;
     out[35] = s->dev.bvhw ? s->dev.bvhw_stack : 0;
+    out[36] = s->dev.n_lbvh;
+    out[37] = s->dev.n_lrec;
   }
   return RT_OK;
 }
@@ -1019,8 +1022,10 @@ int rt_scene_create_groups(const rt_shape_desc* shapes, size_t n_shapes, const i
     if (g.gate == 0 && other_box(r, blo, bhi)) orec.push_back(r);
     else fx_gen.push_back(g);
   }
+  std::vector<QuadRec> line_rec;  // open tubes and cones with finite bounds: the line hierarchy
   for (const QuadRec& q : quads) {
     if (q.gate == 0 && other_box(q, blo, bhi)) orec.push_back(q);
+    else if (q.gate == 0 && line_box(q, blo, bhi)) line_rec.push_back(q);
     else fx_quads.push_back(q);
   }
   std::vector<GroupRec> grec(n_groups);
@@ -1030,6 +1035,18 @@ int rt_scene_create_groups(const rt_shape_desc* shapes, size_t n_shapes, const i
   }
   int obvh_depth = 0;
   std::vector<BvhNode> obvh = build_other_bvh(orec, leaf, &obvh_depth, g_bvh_ct / 100.0);
+  if (obvh_depth > kBvhMaxDepth) obvh.clear();  // deeper than other_trace's stack: exhaustive
+  int lbvh_depth = 0;
+  std::vector<ConeCluster> lclus;
+  std::vector<int32_t> lcone;
+  std::vector<BvhNode> lbvh = build_line_bvh(line_rec, &lclus, &lcone, &lbvh_depth);
+  if (lbvh.empty() || lbvh_depth > kBvhMaxDepth) {  // exhaustive, as before the line hierarchy
+    for (const QuadRec& q : line_rec) fx_quads.push_back(q);
+    line_rec.clear();
+    lbvh.clear();
+    lclus.clear();
+    lcone.clear();
+  }
   if (obvh.empty()) {  // (only when there are no records, or more than the leaf codes can index)
     for (const OtherRec& r : orec) {
       if (r.kind == 0) {
@@ -1065,7 +1082,11 @@ int rt_scene_create_groups(const rt_shape_desc* shapes, size_t n_shapes, const i
   const size_t o_bh = align(o_bw + (bvh_wide.size() + 1) * sizeof(BvhWide));
   const size_t o_ob = align(o_bh + (bvh_wide16.size() + 1) * sizeof(BvhWide16));
   const size_t o_or = align(o_ob + (obvh.size() + 1) * sizeof(BvhNode));
-  const size_t o_fg = align(o_or + (orec.size() + 1) * sizeof(OtherRec));
+  const size_t o_lb = align(o_or + (orec.size() + 1) * sizeof(OtherRec));
+  const size_t o_lr = align(o_lb + (lbvh.size() + 1) * sizeof(BvhNode));
+  const size_t o_cc = align(o_lr + (line_rec.size() + 1) * sizeof(QuadRec));
+  const size_t o_lm = align(o_cc + (lclus.size() + 1) * sizeof(ConeCluster));
+  const size_t o_fg = align(o_lm + (lcone.size() + 1) * sizeof(int32_t));
   const size_t o_fq = align(o_fg + (fx_gen.size() + 1) * sizeof(SphereGen));
   const size_t o_sh = align(o_fq + (fx_quads.size() + 1) * sizeof(QuadRec));
   const size_t o_rt = align(o_sh + shade.size() * sizeof(ShadeRec));
@@ -1087,6 +1108,10 @@ int rt_scene_create_groups(const rt_shape_desc* shapes, size_t n_shapes, const i
   if (!bvh_wide16.empty()) std::memcpy(&host[o_bh], bvh_wide16.data(), bvh_wide16.size() * sizeof(BvhWide16));
   if (!obvh.empty()) std::memcpy(&host[o_ob], obvh.data(), obvh.size() * sizeof(BvhNode));
   if (!orec.empty()) std::memcpy(&host[o_or], orec.data(), orec.size() * sizeof(OtherRec));
+  if (!lbvh.empty()) std::memcpy(&host[o_lb], lbvh.data(), lbvh.size() * sizeof(BvhNode));
+  if (!lclus.empty()) std::memcpy(&host[o_cc], lclus.data(), lclus.size() * sizeof(ConeCluster));
+  if (!lcone.empty()) std::memcpy(&host[o_lm], lcone.data(), lcone.size() * sizeof(int32_t));
+  if (!line_rec.empty()) std::memcpy(&host[o_lr], line_rec.data(), line_rec.size() * sizeof(QuadRec));
   if (!fx_gen.empty()) std::memcpy(&host[o_fg], fx_gen.data(), fx_gen.size() * sizeof(SphereGen));
   if (!fx_quads.empty()) std::memcpy(&host[o_fq], fx_quads.data(), fx_quads.size() * sizeof(QuadRec));
   if (!shade.empty()) std::memcpy(&host[o_sh], shade.data(), shade.size() * sizeof(ShadeRec));
@@ -1144,6 +1169,13 @@ int rt_scene_create_groups(const rt_shape_desc* shapes, size_t n_shapes, const i
   s->dev.bvh_depth = bvh_depth;
   s->dev.obvh = obvh.empty() ? nullptr : (const BvhNode*)(b + o_ob);
   s->dev.orec = (const OtherRec*)(b + o_or);
+  s->dev.lbvh = lbvh.empty() ? nullptr : (const BvhNode*)(b + o_lb);
+  s->dev.lclus = (const ConeCluster*)(b + o_cc);
+  s->dev.lcone = (const int32_t*)(b + o_lm);
+  s->dev.n_lclus = (int32_t)lclus.size();
+  s->dev.lrec = (const QuadRec*)(b + o_lr);
+  s->dev.n_lbvh = (int32_t)lbvh.size();
+  s->dev.n_lrec = (int32_t)line_rec.size();
   s->dev.n_obvh = (int32_t)obvh.size();
   s->dev.obvh_depth = obvh_depth;
   s->dev.n_orec = (int32_t)orec.size();
@@ -1281,7 +1313,7 @@ int render_frames(const rt_scene* scene, const rt_camera_desc* cameras, uint32_t
   // render that cannot batch (counted, or a scene without the fast path's
   // hierarchies) goes frame by frame, with the counters summed
   const bool batch = !stats && !(flags & RT_RENDER_EXHAUSTIVE) && s->tune.accel != 0 &&
-                     (s->dev.n_bvh > 0 || s->dev.n_obvh > 0) && per > 0;
+                     (s->dev.n_bvh > 0 || s->dev.n_obvh > 0 || s->dev.n_lbvh > 0) && per > 0;
   DevStats sum{};
   float ms_sum = 0.f;
   // a pass holds at most ~2^25 root rays (16 C3 frames; 2 C5 frames), which bounds the
@@ -1486,7 +1518,7 @@ int rt_render_ex(const rt_scene* scene, const rt_camera_desc* camera, uint32_t m
   int rc = ensure_dev_buffer(&cx.c->d_out, &cx.c->out_cap, n_pix * 3);
   if (rc != RT_OK) return rc;
   // a large frame without counters: bands, each band's copy behind its render (render_banded)
-  if (!stats && flags == 0 && s->tune.bands > 1 && s->tune.accel != 0 && (s->dev.n_bvh > 0 || s->dev.n_obvh > 0) &&
+  if (!stats && flags == 0 && s->tune.bands > 1 && s->tune.accel != 0 && (s->dev.n_bvh > 0 || s->dev.n_obvh > 0 || s->dev.n_lbvh > 0) &&
       n_pix * aa_samples >= ((uint64_t)1 << 20)) {
     rc = render_banded(s, lk, cx.c, *camera, max_depth, aa_samples, out_rgb);
     if (rc != RT_ERR_NO_DEVICE) return rc;  // (RT_ERR_NO_DEVICE: not bandable, render it whole below)

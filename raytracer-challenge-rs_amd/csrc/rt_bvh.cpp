@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <array>
+#include <map>
 #include <cmath>
 #include <cstring>
 #include <limits>
@@ -551,22 +552,9 @@ std::vector<BvhWide16> wide16_layout(const std::vector<BvhWide>& w) {
   return out;
 }
 
-bool other_box(const OtherRec& r, double lo[3], double hi[3]) {
-  // cones stay exhaustive: their a ~ 0 branch pushes t = -c / 2.0 * b
-  // (cone.rs:104), a root that need not lie on the cone at all
-  if (r.kind != 0 && r.kind != 2 && r.kind != 3) return false;
-  double L[3] = {-1.0, -1.0, -1.0}, U[3] = {1.0, 1.0, 1.0};
-  if (r.kind == 3) {  // cylinder: culled only when closed, with finite caps' planes
-    // An OPEN tube stays exhaustive: the culling argument needs "an odd number of
-    // t < 0 roots => the origin lies inside the box" (DESIGN.md §5.2), true for
-    // closed convex solids only. A backward line can cross one wall of an open
-    // tube within [min, max] and leave through the open end, so the tube is a
-    // `containers` entry (intersection.rs:63-90) for a ray that never meets its box.
-    if (!r.closed) return false;
-    if (!std::isfinite(r.minimum) || !std::isfinite(r.maximum) || !(r.minimum <= r.maximum)) return false;
-    L[1] = r.minimum;
-    U[1] = r.maximum;
-  }
+// the padded world box of a record's local region [L, U] under its stored
+// inverse (false: too ill-conditioned for the padding argument)
+static bool region_box(const OtherRec& r, const double L[3], const double U[3], double lo[3], double hi[3]) {
   double F[3][3];
   const double cond = invert3(r.m, F);
   if (!(cond <= 1e6)) return false;  // too ill-conditioned for the padding argument
@@ -586,6 +574,35 @@ bool other_box(const OtherRec& r, double lo[3], double hi[3]) {
   return true;
 }
 
+bool other_box(const OtherRec& r, double lo[3], double hi[3]) {
+  // cones go to the line hierarchy (line_box): their a ~ 0 branch pushes t =
+  // -c / 2.0 * b (cone.rs:104), a root that need not lie on the cone at all
+  if (r.kind != 0 && r.kind != 2 && r.kind != 3) return false;
+  double L[3] = {-1.0, -1.0, -1.0}, U[3] = {1.0, 1.0, 1.0};
+  if (r.kind == 3) {  // cylinder: culled here only when closed, with finite caps' planes
+    // An OPEN tube goes to the line hierarchy: the culling argument here needs
+    // "an odd number of t < 0 roots => the origin lies inside the box"
+    // (DESIGN.md §5.2), true for closed convex solids only. A backward line can
+    // cross one wall of an open tube within [min, max] and leave through the
+    // open end, so the tube is a `containers` entry (intersection.rs:63-90) for
+    // a ray whose [0, t_hi] never meets its box.
+    if (!r.closed) return false;
+    if (!std::isfinite(r.minimum) || !std::isfinite(r.maximum) || !(r.minimum <= r.maximum)) return false;
+    L[1] = r.minimum;
+    U[1] = r.maximum;
+  }
+  return region_box(r, L, U, lo, hi);
+}
+
+bool line_box(const QuadRec& r, double lo[3], double hi[3]) {
+  if (!(r.kind == 4 || (r.kind == 3 && !r.closed))) return false;
+  if (!std::isfinite(r.minimum) || !std::isfinite(r.maximum) || !(r.minimum <= r.maximum)) return false;
+  // the reference's own boxes: cylinder.rs (radius 1), cone.rs:27-46 (radius max(|min|, |max|))
+  const double w = r.kind == 4 ? std::max(std::fabs(r.minimum), std::fabs(r.maximum)) : 1.0;
+  const double L[3] = {-w, r.minimum, -w}, U[3] = {w, r.maximum, w};
+  return region_box(r, L, U, lo, hi);
+}
+
 std::vector<BvhNode> build_other_bvh(std::vector<OtherRec>& recs, int leaf_size, int* depth, double trav_cost) {
   std::vector<Box> boxes(recs.size());
   for (size_t i = 0; i < recs.size(); ++i)
@@ -593,6 +610,59 @@ std::vector<BvhNode> build_other_bvh(std::vector<OtherRec>& recs, int leaf_size,
   std::vector<int> order;
   std::vector<BvhNode> nodes = build_over_boxes(boxes, leaf_size, trav_cost, depth, &order);
   if (!nodes.empty()) apply_order(recs, order);
+  return nodes;
+}
+
+std::vector<BvhNode> build_line_bvh(std::vector<QuadRec>& recs, std::vector<ConeCluster>* clusters,
+                                    std::vector<int32_t>* members, int* depth) {
+  clusters->clear();
+  members->clear();
+  std::vector<Box> boxes(recs.size());
+  for (size_t i = 0; i < recs.size(); ++i)
+    if (!line_box(recs[i], boxes[i].lo, boxes[i].hi)) return {};
+  std::vector<int> order;
+  // one record per leaf where the builder can split (line_trace tests each record of a leaf)
+  std::vector<BvhNode> nodes = build_over_boxes(boxes, 1, 1.0, depth, &order);
+  if (nodes.empty()) return nodes;
+  apply_order(recs, order);
+  // per cone: Q = m0 m0^T - m1 m1^T + m2 m2^T (m_k: row k of the inverse's 3x3
+  // part; a(d) = d^T Q d exactly), and W = sum_k (sum_j |m_kj|)^2: the
+  // reference's a (object direction m d, then dx*dx - dy*dy + dz*dz, every
+  // operation rounded) is within 16 u W dm^2 of d^T Q d (u = 2^-53)
+  const double u = 0x1p-53;
+  const int ij[6][2] = {{0, 0}, {1, 1}, {2, 2}, {0, 1}, {0, 2}, {1, 2}};
+  std::map<std::array<double, 6>, std::vector<int>> by_q;  // cones of one (bitwise) Q, in record order
+  std::map<std::array<double, 6>, double> w_max;
+  for (size_t k = 0; k < recs.size(); ++k) {
+    if (recs[k].kind != 4) continue;
+    const double* m = recs[k].m;
+    const double R[3][3] = {{m[0], m[1], m[2]}, {m[4], m[5], m[6]}, {m[8], m[9], m[10]}};
+    std::array<double, 6> q;
+    for (int e = 0; e < 6; ++e)
+      q[e] = R[0][ij[e][0]] * R[0][ij[e][1]] - R[1][ij[e][0]] * R[1][ij[e][1]] + R[2][ij[e][0]] * R[2][ij[e][1]];
+    double w = 0.0;
+    for (int r = 0; r < 3; ++r) {
+      const double s = std::fabs(R[r][0]) + std::fabs(R[r][1]) + std::fabs(R[r][2]);
+      w += s * s;
+    }
+    by_q[q].push_back((int)k);
+    double& wm = w_max[q];
+    wm = std::max(wm, w);
+  }
+  for (const auto& [q, ks] : by_q) {
+    ConeCluster c{};
+    for (int e = 0; e < 6; ++e) c.q[e] = q[e];
+    const double aq = std::fabs(q[0]) + std::fabs(q[1]) + std::fabs(q[2]) +
+                      2.0 * (std::fabs(q[3]) + std::fabs(q[4]) + std::fabs(q[5]));  // sum of |Q| over nine entries
+    // the reference's rounding (16 u W), the device's g (8 u |Q|), this host
+    // arithmetic's Q (1e-12 |Q|), then a relative margin
+    c.r = (16.0 * u * w_max.at(q) + 8.0 * u * aq + 1e-12 * aq) * (1.0 + 1e-9);
+    if (!std::isfinite(c.r)) return {};
+    c.first = (int32_t)members->size();
+    c.count = (int32_t)ks.size();
+    members->insert(members->end(), ks.begin(), ks.end());
+    clusters->push_back(c);
+  }
   return nodes;
 }
 

@@ -31,23 +31,36 @@ std::vector<BvhPair> pair_layout(const std::vector<BvhNode>& nodes);
 // the top of the tree, for an LDS treelet). `stack` receives the most entries
 // a near-first traversal keeps pending. Empty when the 16-bit codes cannot
 // index the nodes or records.
+std::vector<BvhWide> wide_layout(const std::vector<BvhNode>& nodes, const std::vector<SphereDiag>& spheres,
+                                 int* stack);
+
 // the global-memory copy of a four-wide image: its boxes rounded outward to binary16
 std::vector<BvhWide16> wide16_layout(const std::vector<BvhWide>& w);
 // binary16 bit patterns rounded outward (BvhWide16 boxes)
 uint16_t f16_bits_down(double x);
 uint16_t f16_bits_up(double x);
-std::vector<BvhWide> wide_layout(const std::vector<BvhNode>& nodes, const std::vector<SphereDiag>& spheres,
-                                 int* stack);
 
 // The other bounded records (general-transform spheres, cubes, closed
 // cylinders with finite caps; rt_layout.hpp OtherRec): other_box gives the
-// padded world box of one (false when the record must stay exhaustive: a
-// cone, an open or unbounded cylinder, an ill-conditioned transform). build_other_bvh builds
+// padded world box of one (false for a cone, an open or unbounded cylinder,
+// an ill-conditioned transform: the line hierarchy or the exhaustive loop
+// takes those). build_other_bvh builds
 // the hierarchy over records that all have one (reordered in place into leaf
 // order); empty when there are none.
 bool other_box(const OtherRec& r, double lo[3], double hi[3]);
 std::vector<BvhNode> build_other_bvh(std::vector<OtherRec>& recs, int leaf_size, int* depth = nullptr,
                                      double trav_cost = 1.0);
+
+// The line hierarchy (rt_layout.hpp ConeCluster): line_box
+// gives the padded world box of an open tube or a cone with finite bounds
+// (false for any other record, or an ill-conditioned transform);
+// build_line_bvh builds the hierarchy over records that all have one, leaves
+// of one record where the builder can split (reordered in place into leaf
+// order), and the cones' clusters (cones of one direction quadratic, their
+// members' indices into `recs` in `members`); empty when there are none.
+bool line_box(const QuadRec& r, double lo[3], double hi[3]);
+std::vector<BvhNode> build_line_bvh(std::vector<QuadRec>& recs, std::vector<ConeCluster>* clusters,
+                                    std::vector<int32_t>* members, int* depth = nullptr);
 
 // Light buffer over the shadow-casting records, one cube map of R x R cells
 // per face per light (rt_layout.hpp LbCell; DESIGN.md "Light buffer").

@@ -55,6 +55,7 @@ typedef const RT_CONST SphereGen* cSphereGen;
 typedef const RT_CONST PlaneRec* cPlaneRec;
 typedef const RT_CONST QuadRec* cQuadRec;
 typedef const RT_CONST GroupRec* cGroupRec;
+typedef const RT_CONST ConeCluster* cConeCluster;
 typedef const RT_CONST LightRec* cLightRec;
 
 typedef double d2 __attribute__((ext_vector_type(2)));  // ds_read_b128 operand

@@ -133,6 +133,31 @@ inline float wide_f16(uint16_t b) {
   return (b & 0x8000u) ? -v : v;
 }
 constexpr unsigned kWideEmpty = 0xFFFFu, kWideLeaf = 0x8000u;  // BvhWide child codes: empty, leaf flag
+// Line hierarchy (rt_bvh.cpp build_line_bvh, line_trace): open tubes
+// (cylinder.rs with closed = false) and cones (cone.rs) with finite bounds.
+// Their boxes are tested over the ray's whole line up to the current hit,
+// (-inf, t_hi]: a culled record then has no root at t <= t_hi at all, so it
+// neither hits nor enters `containers` (an open tube is no closed solid, so
+// the [0, t_hi] argument of the other hierarchies does not cover its t < 0
+// roots). A cone's a ~ 0 branch (cone.rs:102-110) pushes t = -c / 2.0 * b,
+// a root anywhere on the line; every other root of a cone lies in its box. So
+// the cones whose a, as the reference computes it, is below EPSILON for a ray
+// are found before the traversal, cluster by cluster (cone_prepass), tested
+// there, and skipped by the traversal. A cluster holds the cones whose
+// direction quadratic is the same (cones equal up to position and a turn
+// about their axis): with the world direction d, |d|_inf = dm and g = d^T Q d
+// (Q: the six distinct entries of the symmetric 3x3 form, xx yy zz xy xz yz),
+// every member i has |fl(a_i) - g| <= r dm^2 (r covers every rounding, host
+// and device), so |g| - r dm^2 >= EPSILON (with a margin) rules out the whole
+// cluster with one test. Members: lcone[first .. first + count) (indices
+// into lrec).
+struct alignas(64) ConeCluster {
+  double q[6];
+  double r;
+  int32_t first, count;
+};
+static_assert(sizeof(ConeCluster) == 64, "ConeCluster must stay 64 B");
+
 // A culled record other than a diagonal sphere: the QuadRec layout, with
 // kind 0 = sphere under a general inverse (rows 0-2 in m).
 typedef QuadRec OtherRec;
@@ -216,8 +241,15 @@ struct DevScene {
   const BvhNode* obvh;      // nullptr when there are no culled other records
   const OtherRec* orec;     // in obvh leaf order
   int32_t n_obvh, obvh_depth, n_orec;
-  const SphereGen* fx_gen;  // general spheres outside the obvh
-  const QuadRec* fx_quads;  // cubes / cylinders / cones outside the obvh
+  // the line hierarchy (line_trace): open tubes and cones with finite bounds,
+  // culled over the whole line up to the hit; the cones' a ~ 0 clusters
+  const BvhNode* lbvh;          // nullptr when there are none
+  const QuadRec* lrec;          // in lbvh leaf order
+  const ConeCluster* lclus;     // the cones' clusters (cone_prepass)
+  const int32_t* lcone;         // cluster members: indices into lrec
+  int32_t n_lbvh, n_lrec, n_lclus;
+  const SphereGen* fx_gen;  // general spheres outside the hierarchies
+  const QuadRec* fx_quads;  // cubes / cylinders / cones outside the hierarchies
   int32_t n_fx_gen, n_fx_quads;
   const LbCell* lb_cells;  // light buffer: n_lights * 6R^2 cells, nullptr when not built
   const uint16_t* lb_ov;

@@ -631,6 +631,98 @@ __device__ __forceinline__ void other_trace(const DevScene& sc, V3 o, V3 d, doub
   }
 }
 
+// The line hierarchy (rt_layout.hpp ConeCluster; DESIGN.md §5.2 "Open tubes
+// and cones"): open tubes and cones with finite bounds, leaves of one record
+// (more only where the builder cannot split). First cone_prepass: per cluster
+// one test rules out that every member takes the reference's a ~ 0 branch
+// (cone.rs:102-110) for this ray; the members of an open cluster are checked
+// with the reference's own a (quad_test's operations) and those below EPSILON
+// are tested in full. Then line_trace: a child is entered when its box meets
+// the ray's line within [t_lo, t_hi] (radiance rays t_lo = -inf: every root at
+// t <= t_hi, the containers' t < 0 ones included; shadow rays t_lo = 0, only
+// [0, distance) blocks); a leaf's records are tested, but for the cones the
+// pre-pass took. Order-independent minima, so the visiting order is free.
+__device__ __forceinline__ bool cone_cluster_open(cConeCluster g, V3 d) {
+  const double dm = fmax(fmax(fabs(d.x), fabs(d.y)), fabs(d.z)), dm2 = dm * dm;
+  const double v = g->q[0] * d.x * d.x + g->q[1] * d.y * d.y + g->q[2] * d.z * d.z +
+                   2.0 * (g->q[3] * d.x * d.y + g->q[4] * d.x * d.z + g->q[5] * d.y * d.z);
+  const double av = fabs(v), rr = g->r * dm2;
+  // closed: |v| - r dm^2 >= EPSILON with a margin for this arithmetic (NaN: open)
+  return !(av - rr - 0x1p-40 * (av + rr) >= kEpsilon);
+}
+// the reference's |a| < EPSILON test of a cone (quad_test's object direction, quad_local_intersect's a)
+template <typename QP>
+__device__ __forceinline__ bool cone_degenerate(QP q, V3 d) {
+  const V3 ld = v3(q->m[0] * d.x + q->m[1] * d.y + q->m[2] * d.z, q->m[4] * d.x + q->m[5] * d.y + q->m[6] * d.z,
+                   q->m[8] * d.x + q->m[9] * d.y + q->m[10] * d.z);
+  const double a = ld.x * ld.x - ld.y * ld.y + ld.z * ld.z;
+  return fabs(a) < kEpsilon;
+}
+template <bool SHADOW>
+__device__ __forceinline__ void cone_prepass(const DevScene& sc, V3 o, V3 d, Hit& h, unsigned& n_tests) {
+  const cConeCluster cl = (cConeCluster)sc.lclus;
+  const cQuadRec lrec = (cQuadRec)sc.lrec;
+  for (int c = 0; c < sc.n_lclus; ++c) {  // wave-uniform: the clusters and their members in scalar loads
+    if (!cone_cluster_open(cl + c, d)) continue;
+    const int first = cl[c].first, count = cl[c].count;
+    for (int j = first; j < first + count; ++j) {
+      const cQuadRec q = lrec + ((const RT_CONST int32_t*)sc.lcone)[j];
+      if (!cone_degenerate(q, d)) continue;
+      quad_test<SHADOW>(q, o, d, h);
+      ++n_tests;
+    }
+  }
+}
+template <bool SHADOW>
+__device__ __forceinline__ void line_trace(const DevScene& sc, V3 o, V3 d, double t_shadow, Hit& h,
+                                           unsigned& n_tests, unsigned& n_boxes) {
+  if (sc.n_lbvh == 0) return;
+  cone_prepass<SHADOW>(sc, o, d, h, n_tests);
+  if (SHADOW && h.key >= 0 && h.t < t_shadow) return;
+  const BvhNode* nodes = sc.lbvh;
+  float M[3];
+  for (int ax = 0; ax < 3; ++ax)  // the root's two child boxes contain every box below them
+    M[ax] = fmaxf(fmaxf(fabsf(nodes[0].lo[0][ax]), fabsf(nodes[0].hi[0][ax])),
+                  fmaxf(fabsf(nodes[0].lo[1][ax]), fabsf(nodes[0].hi[1][ax])));
+  const SlabRay sr = slab_ray(o, d, M);
+  const float t_lo = SHADOW ? 0.0f : -INFINITY;
+  float t_hi = f32_up(SHADOW ? t_shadow : h.t);
+  auto box = [&](const float* lo, const float* hi) {  // slab_hit32's test over [t_lo, t_hi]
+    const float x0 = fmaf(lo[0], sr.inv[0], -sr.c_lo[0]), x1 = fmaf(hi[0], sr.inv[0], -sr.c_hi[0]);
+    const float y0 = fmaf(lo[1], sr.inv[1], -sr.c_lo[1]), y1 = fmaf(hi[1], sr.inv[1], -sr.c_hi[1]);
+    const float z0 = fmaf(lo[2], sr.inv[2], -sr.c_lo[2]), z1 = fmaf(hi[2], sr.inv[2], -sr.c_hi[2]);
+    const float tmin = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), t_lo));
+    const float tmax = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), t_hi));
+    return tmin <= tmax;
+  };
+  int stk[kBvhMaxDepth + 4];
+  int sp = 0, e = 0;
+  while (e != kBvhEmpty) {
+    const BvhNode& nd = nodes[e];
+    int next[2], nn = 0;
+    for (int c = 0; c < 2; ++c) {
+      const int32_t code = nd.child[c];
+      if (code == kBvhEmpty) continue;
+      ++n_boxes;
+      if (!box(nd.lo[c], nd.hi[c])) continue;
+      if (code >= 0) { next[nn++] = code; continue; }
+      const int lc = -(code + 1), first = lc >> 7, cnt = lc & 127;
+      for (int k = first; k < first + cnt; ++k) {
+        const QuadRec* q = sc.lrec + k;
+        if (q->kind == 4 && cone_degenerate(q, d)) continue;  // the pre-pass tested it
+        quad_test<SHADOW>(q, o, d, h);
+        ++n_tests;
+        if constexpr (SHADOW) {
+          if (h.key >= 0 && h.t < t_shadow) return;  // shadowed: done
+        } else {
+          t_hi = f32_up(h.t);
+        }
+      }
+    }
+    if (nn == 2) stk[sp++] = next[1];
+    e = nn > 0 ? next[0] : (sp > 0 ? stk[--sp] : kBvhEmpty);
+  }
+}
 
 __host__ __device__ inline size_t lane_stack_bytes(int depth) { return (size_t)(depth > 0 ? depth : 1) * kTraceBlock * 4; }
 __host__ __device__ inline size_t sph_lds_bytes(const DevScene& sc) { return (size_t)sc.n_diag * sizeof(SphereDiag); }
@@ -844,7 +936,10 @@ __device__ __forceinline__ bool shadow_trace(const DevScene& sc, unsigned use_lb
   Hit h;
   hit_init(h);
   trace_rest<true, QUADS, true>(sc, o, d, h, n_disc, skips);
-  if constexpr (QUADS) other_trace<true>(sc, o, d, dist, h, n_disc, n_tests, n_boxes);
+  if constexpr (QUADS) {
+    other_trace<true>(sc, o, d, dist, h, n_disc, n_tests, n_boxes);
+    line_trace<true>(sc, o, d, dist, h, n_tests, n_boxes);
+  }
   if (!(h.key >= 0 && h.t < dist)) {
     if (use_lb) {
       if constexpr (LANE == 14 || LANE == 15) lb_walk(sc, ls.s48, ls.delta, ls.delta16, l, o, d, dist, h, n_disc, n_tests);

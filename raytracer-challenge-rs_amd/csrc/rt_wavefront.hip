@@ -901,11 +901,17 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
         bvh_trace<PRIMARY, false>(sc, (cPrimRec)(a.prim + (size_t)pf * ((unsigned)sc.n_diag + 4)), stk, o, d, 0.0, h,
                                   t.disc, t.tests, t.boxes);
         trace_rest<false, QUADS, true>(sc, o, d, h, t.disc, &t.gsk);
-        if constexpr (QUADS) other_trace<false>(sc, o, d, 0.0, h, t.disc, t.tests, t.boxes);
+        if constexpr (QUADS) {
+          other_trace<false>(sc, o, d, 0.0, h, t.disc, t.tests, t.boxes);
+          line_trace<false>(sc, o, d, 0.0, h, t.tests, t.boxes);
+        }
       } else {
         // planes and the other records first: an early nearest hit tightens the culling
         trace_rest<false, QUADS, true>(sc, o, d, h, t.disc, &t.gsk);
-        if constexpr (QUADS) other_trace<false>(sc, o, d, 0.0, h, t.disc, t.tests, t.boxes);
+        if constexpr (QUADS) {
+          other_trace<false>(sc, o, d, 0.0, h, t.disc, t.tests, t.boxes);
+          line_trace<false>(sc, o, d, 0.0, h, t.tests, t.boxes);
+        }
         if constexpr (LANE == 14) {
           lane_trace_pair<false>(ls.nodes, ls.s48, ls.M, sc.n_bvh > 0, o, d, 0.0, h, t.disc, t.tests, t.boxes,
                                  ls.stack16);
@@ -1549,7 +1555,7 @@ static hipError_t launch_fused_q(const DevScene& sc, const DevCamera& cam, WfArg
 static hipError_t launch_fused(const DevScene& sc, const DevCamera& cam, const WfArgs& a, bool primary, unsigned n,
                                hipStream_t stream, bool tally, const WfTuning& tn) {
   // QUADS: solids outside the hierarchies, or the hierarchy over the other records
-  const bool quads = sc.n_fx_quads > 0 || sc.n_obvh > 0;
+  const bool quads = sc.n_fx_quads > 0 || sc.n_obvh > 0 || sc.n_lbvh > 0;
   if (tally)
     return quads ? launch_fused_q<true, true>(sc, cam, a, primary, n, stream, tn)
                  : launch_fused_q<false, true>(sc, cam, a, primary, n, stream, tn);
@@ -1576,7 +1582,7 @@ hipError_t Wavefront::render(const DevScene& sc, const DevCamera& cam, bool came
   // reference's every-shape loop is asked for; counting (stats) never changes the algorithm
   const bool exhaustive = (flags & WF_EXHAUSTIVE) != 0;
   const bool count = stats != nullptr || (flags & WF_COUNT) != 0;
-  const bool bvh = tn.accel != 0 && !exhaustive && (sc.n_bvh > 0 || sc.n_obvh > 0);
+  const bool bvh = tn.accel != 0 && !exhaustive && (sc.n_bvh > 0 || sc.n_obvh > 0 || sc.n_lbvh > 0);
   const bool fused = bvh;
   // (a counted render of a scene with groups traces every shadow ray: the reference's shape
   // tests then come from the group gates each ray met, GateSkips)

@@ -511,5 +511,47 @@ def divided(width=128, height=72, n=5, threshold=2, seed=11):
     return w, _camera(width, height, PI / 3.0, (0.0, 3.5, -5.5), (0.0, 0.6, 1.5)), 5
 
 
+def cones(width=320, height=240, n=600, upright=0.5, seed=23):
+    """A field of cones (closed and open, finite bounds, some spanning both
+    nappes) and open tubes, `upright` of the cones upright with one scale, the
+    rest rotated and sheared; glass and mirrors among them, diagonal spheres, a
+    reflective floor. The line hierarchy's workload (rt_bvh.cpp build_line_bvh;
+    cone.rs, cylinder.rs)."""
+    import random
+    rnd = random.Random(seed)
+    u = lambda a, b: a + (b - a) * rnd.random()  # noqa: E731
+    w = rt.World()
+    floor = rt.Plane()
+    floor.material.reflective = 0.3
+    w.add_object(floor)
+    for i in range(n):
+        c = (u(-8, 8), u(0.5, 3.0), u(-6, 10))
+        if i % 4 == 3:
+            s = rt.Cylinder(u(-1.0, 0.0), u(0.2, 1.0), False)
+            tf = rt.translation(*c) * rt.rotation_z(u(-1, 1)) * rt.scaling(0.3, 0.5, 0.3)
+        elif i % 8 == 6:
+            s = rt.Sphere()
+            tf = rt.translation(*c) * rt.scaling(0.3, 0.3, 0.3)
+        else:
+            lo = u(-1.0, 0.3)
+            s = rt.Cone(lo, lo + u(0.3, 1.2), bool(i % 3))
+            if rnd.random() < upright:
+                tf = rt.translation(*c) * rt.scaling(0.4, 0.4, 0.4)
+            else:
+                tf = (rt.translation(*c) * rt.rotation_y(u(0, 6.3)) * rt.rotation_x(u(0, 6.3))
+                      * rt.shearing(*[u(-0.2, 0.2) for _ in range(6)]) * rt.scaling(0.4, 0.5, 0.3))
+        s.set_transform(tf)
+        s.material.color = rt.Color(rnd.random(), rnd.random(), rnd.random())
+        if i % 5 == 1:
+            s.material.transparency = 0.8
+            s.material.refractive_index = u(1.0, 2.0)
+            s.material.reflective = 0.4
+        elif i % 5 == 2:
+            s.material.reflective = u(0.2, 0.9)
+        w.add_object(s)
+    w.add_light(rt.PointLight(rt.Point(-10, 10, -10), rt.Color(1.0, 1.0, 1.0)))
+    return w, _camera(width, height, PI / 3.0, (0.0, 3.0, -12.0), (0.0, 1.0, 2.0)), 5
+
+
 CONFIGS = {"c1": c1, "c2": c2, "c3": c3, "c5": c5, "zoo": zoo, "first_scene": first_scene, "solids": solids,
-           "hexagon": hexagon, "groups": groups, "divided": divided}
+           "hexagon": hexagon, "groups": groups, "divided": divided, "cones": cones}

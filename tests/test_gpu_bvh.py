@@ -344,9 +344,10 @@ def test_frames_in_flight_bitwise(rt, n_streams, kind):
 
 def _general_field(rt, n=360, seed=17):
     """Every shape kind under general transforms (rotated, sheared, scaled):
-    spheres, cubes, closed and open bounded cylinders (culled by the other
-    records' hierarchy), cones and an open-ended cylinder (exhaustive), a
-    few diagonal spheres, glass and mirrors nested in each other."""
+    spheres, cubes and closed bounded cylinders (culled by the other records'
+    hierarchy), open bounded cylinders and cones (the line hierarchy), an
+    infinite cylinder (exhaustive), a few diagonal spheres, glass and mirrors
+    nested in each other."""
     rng = np.random.default_rng(seed)
     w = rt.World()
     floor = rt.Plane()
@@ -426,8 +427,9 @@ def test_open_glass_tubes_stay_containers(rt):
     a ray whose origin lies outside a tube's box can have its backward line
     cross exactly one wall inside [min, max] and leave through the open end,
     which makes the tube a `containers` entry (intersection.rs:63-90) for a
-    ray that never meets the box. Such tubes stay exhaustive on the fast path;
-    fast == exhaustive bitwise on crafted and random rays."""
+    ray whose [0, t_hi] never meets the box. The line hierarchy tests such
+    tubes' boxes over the whole backward line; fast == exhaustive bitwise on
+    crafted and random rays."""
     rng = np.random.default_rng(13)
     w = rt.World()
     w.add_object(rt.Plane())
@@ -462,7 +464,124 @@ def test_open_glass_tubes_stay_containers(rt):
         fast, _ = w.color_at_batch(rays, depth, want_stats=False)
         exact, _ = w.color_at_batch(rays, depth, want_stats=True)
         assert fast.tobytes() == exact.tobytes(), depth
-    assert rt._rtamd._wf_profile(w, -1, True)["n_other_culled"] == 0  # open tubes are never culled
+    p = rt._rtamd._wf_profile(w, -1, True)
+    assert p["n_other_culled"] == 0 and p["n_line_culled"] == 40  # open tubes: the line hierarchy
+
+
+def _cone_field(rt, n=240, seed=23, upright_share=0.5):
+    """Cones (closed and open, finite bounds, some spanning y = 0: two nappes)
+    and open tubes, half of the cones upright with one scale (their gates
+    close tightly), the rest under random rotations and shears; glass and
+    mirrors among them, a floor and diagonal spheres."""
+    rng = np.random.default_rng(seed)
+    w = rt.World()
+    floor = rt.Plane()
+    floor.material.reflective = 0.3
+    w.add_object(floor)
+    for i in range(n):
+        c = rng.uniform([-5, 0.5, -5], [5, 3, 5])
+        if i % 4 == 3:
+            s = rt.Cylinder(float(rng.uniform(-1.0, 0.0)), float(rng.uniform(0.2, 1.0)), False)
+            tf = rt.translation(*c) * rt.rotation_z(float(rng.uniform(-1, 1))) * rt.scaling(0.3, 0.5, 0.3)
+        elif i % 4 == 2 and i % 8 != 2:
+            s = rt.Sphere()
+            tf = rt.translation(*c) * rt.scaling(0.3, 0.3, 0.3)
+        else:
+            lo = float(rng.uniform(-1.0, 0.3))
+            s = rt.Cone(lo, lo + float(rng.uniform(0.3, 1.2)), bool(i % 3))
+            if rng.uniform() < upright_share:
+                tf = rt.translation(*c) * rt.scaling(0.4, 0.4, 0.4)
+            else:
+                tf = (rt.translation(*c) * rt.rotation_y(float(rng.uniform(0, 6.3)))
+                      * rt.rotation_x(float(rng.uniform(0, 6.3)))
+                      * rt.shearing(*[float(x) for x in rng.uniform(-0.2, 0.2, 6)]) * rt.scaling(0.4, 0.5, 0.3))
+        s.set_transform(tf)
+        s.material.color = rt.Color(*rng.uniform(0, 1, 3))
+        if i % 5 == 1:
+            s.material.transparency = 0.8
+            s.material.refractive_index = float(1.0 + rng.uniform(0, 1.0))
+            s.material.reflective = 0.4
+        elif i % 5 == 2:
+            s.material.reflective = float(rng.uniform(0.2, 0.9))
+        w.add_object(s)
+    w.add_light(rt.PointLight(rt.Point(-10, 10, -10), rt.Color(1, 1, 1)))
+    return w
+
+
+@pytest.mark.parametrize("frm,upright", [((0, 2.5, -11), 0.5), ((0.0, 1.5, 0.0), 0.5), ((3.0, 4.0, -6.0), 1.0),
+                                         ((-1.0, 1.0, -2.0), 0.0)])
+def test_line_hierarchy_cones_bitwise(rt, frm, upright):
+    """Cones and open tubes culled by the line hierarchy (their boxes over the
+    whole line up to the hit, each cone behind its a ~ 0 gate, cone.rs:94-134,
+    cylinder.rs:88-119): frames bitwise equal to the exhaustive loop, from
+    outside and inside the field, with every cone upright, none, or half."""
+    w = _cone_field(rt, upright_share=upright)
+    cam = rt.Camera(128, 96, PI / 2.5)
+    cam.set_transform(rt.view_transform(rt.Point(*frm), rt.Point(0, 1, 1), rt.Vector(0, 1, 0)))
+    fast, exact, st = _both(rt, w, cam, 6)
+    assert fast.tobytes() == exact.tobytes()
+    counted, _ = cam.render(w, 6, want_stats=True, exhaustive=False)  # the fast path, counting its work
+    assert counted.to_numpy().tobytes() == exact.tobytes()
+    p = rt._rtamd._wf_profile(w, -1, True)
+    assert p["n_line_culled"] > 150 and p["n_lbvh_nodes"] > 0 and p["fused"]
+
+
+def test_cone_a_zero_branch_rays(rt):
+    """Rays along a cone's generators take the reference's a ~ 0 branch
+    (cone.rs:102-110), whose root t = -c / 2.0 * b lies anywhere on the line,
+    far outside the cone's box: the gates must send these rays to the cone
+    whatever its box says. Upright cones of one scale, directions with
+    dx^2 + dz^2 = dy^2 exactly and perturbed around it (|a| just below and
+    above EPSILON), origins far from every box; then random rays."""
+    rng = np.random.default_rng(31)
+    w = rt.World()
+    centres = []
+    for i in range(60):
+        s = rt.Cone(-1.0, 1.0, bool(i % 2))
+        c = rng.uniform([-6, 1, -6], [6, 3, 6])
+        s.set_transform(rt.translation(*c) * rt.scaling(0.5, 0.5, 0.5))
+        s.material.color = rt.Color(*rng.uniform(0, 1, 3))
+        if i % 3 == 0:
+            s.material.transparency = 0.7
+            s.material.refractive_index = 1.4
+        w.add_object(s)
+        centres.append(c)
+    for i in range(30):  # spheres to hit behind the quirk roots
+        s = rt.Sphere()
+        s.set_transform(rt.translation(*rng.uniform([-8, 0, -8], [8, 4, 8])) * rt.scaling(0.4, 0.4, 0.4))
+        w.add_object(s)
+    w.add_light(rt.PointLight(rt.Point(-10, 10, -10), rt.Color(1, 1, 1)))
+    dirs = []
+    for ex, ez in ((1, 0), (0, 1), (0.6, 0.8), (-0.8, 0.6), (0.28, -0.96)):
+        for sy in (1, -1):
+            for eps in (0.0, 2e-6, -2e-6, 4e-6, 1e-5, -1e-5, 3e-5):
+                d = np.array([ex, sy * (1.0 + eps), ez])
+                dirs.append(d / np.linalg.norm(d))
+    rays = []
+    for k in range(4000):
+        d = dirs[k % len(dirs)]
+        o = rng.uniform([-30, -10, -30], [30, 14, 30])
+        rays.append(np.hstack([o, d]))
+    # the crafted rays do take the branch: (ray, cone) pairs with |a| < EPSILON, |b| >= EPSILON
+    # and a root t = -c / 2.0 * b >= 0 (object space: 2 (o - centre), 2 d)
+    cr = np.array(rays)
+    quirk = 0
+    for c in centres:
+        lo_, ld = 2.0 * (cr[:, :3] - c), 2.0 * cr[:, 3:]
+        a = ld[:, 0] * ld[:, 0] - ld[:, 1] * ld[:, 1] + ld[:, 2] * ld[:, 2]
+        b = 2.0 * lo_[:, 0] * ld[:, 0] - 2.0 * lo_[:, 1] * ld[:, 1] + 2.0 * lo_[:, 2] * ld[:, 2]
+        cc = lo_[:, 0] * lo_[:, 0] - lo_[:, 1] * lo_[:, 1] + lo_[:, 2] * lo_[:, 2]
+        quirk += int(np.sum((np.abs(a) < 1e-5) & (np.abs(b) >= 1e-5) & (-cc / 2.0 * b >= 0.0)))
+    assert quirk > 1000
+    o = rng.uniform([-7, -0.5, -7], [7, 4.5, 7], size=(8000, 3))
+    d = rng.normal(size=(8000, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.vstack([cr, np.hstack([o, d])])
+    for depth in (0, 1, 4):
+        fast, _ = w.color_at_batch(rays, depth, want_stats=False)
+        exact, _ = w.color_at_batch(rays, depth, want_stats=True)
+        assert fast.tobytes() == exact.tobytes(), depth
+    assert rt._rtamd._wf_profile(w, -1, True)["n_line_culled"] == 60
 
 
 def test_other_records_only_scene_takes_fast_path(rt):
