@@ -55,6 +55,8 @@ CASES = [
     ("groups_80x60", "groups", {"width": 80, "height": 60}),
     ("groups_40x30_aa4", "groups", {"width": 40, "height": 30}, 4),
     ("divided_96x54", "divided", {"width": 96, "height": 54}),
+    # cones and open tubes (the line hierarchy: cone.rs, cylinder.rs)
+    ("cones_64x48", "cones", {"width": 64, "height": 48, "n": 120}),
 ]
 COUNTERS = ("rays_primary", "rays_reflect", "rays_refract", "rays_shadow",
             "sphere_tests", "plane_tests", "sphere_disc_ge0", "other_tests")

@@ -94,3 +94,11 @@ def test_gpu_matches_golden(rt, name):
     assert np.abs(g - canvas).max() <= TOL
     assert rt.canvas_to_ppm(g) == ppm
     assert {k: int(st[k]) for k in e["counters"]} == e["counters"]
+    # the fast path (the hierarchies, no counters) against the same fixture
+    if e["aa"] == 1:
+        fast, _ = cam.render(w, depth, want_stats=False)
+    else:
+        fast, _ = cam.render_multithreaded(w, depth, want_stats=False)
+    f = fast.to_numpy()
+    assert np.abs(f - canvas).max() <= TOL
+    assert rt.canvas_to_ppm(f) == ppm
