@@ -105,3 +105,74 @@ def test_concurrent_host_renders_of_one_scene(rt):
     assert bytes(got["ppm"]) == bytes(ppm_alone)
     assert got["col"].tobytes() == col_alone.tobytes()
     assert math.isfinite(float(alone[0].sum()))
+
+
+def _run_threads(jobs, rounds=3):
+    """Run each (key, fn) in its own thread `rounds` times; results of the last round, and errors."""
+    got, errors = {}, []
+
+    def run(key, fn):
+        try:
+            for _ in range(rounds):
+                got[key] = fn()
+        except Exception as e:  # pragma: no cover - reported by the caller
+            errors.append((key, e))
+
+    threads = [threading.Thread(target=run, args=kf) for kf in jobs]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    return got, errors
+
+
+@pytest.mark.gpu
+def test_render_multi_and_render_threads_with_overflows(rt):
+    """rt_render_multi and rt_render from two threads on one scene while every
+    arena overflows (test hook arena_pct = 2 %): each synchronous call takes
+    the overflow flags of the workspaces it used only, re-renders its own frame
+    and returns it complete; no call swallows or reports another's overflow,
+    so the scene is clean afterwards (advisor, round 4)."""
+    from rtamd import scenes
+    w, cam, depth = scenes.c3(96, 54, n_spheres=200)
+    cam2 = scenes.c3_orbit(3, 8, 96, 54)
+    a_ref = cam.render(w, depth, want_stats=False)[0].to_numpy()
+    b_ref = cam2.render(w, depth, want_stats=False)[0].to_numpy()
+    w.tune("arena_pct", 2)
+    try:
+        got, errors = _run_threads([("multi", lambda: cam.render_multi([w], depth, 8)[0].to_numpy()),
+                                    ("render", lambda: cam2.render(w, depth, want_stats=False)[0].to_numpy())])
+    finally:
+        w.tune("arena_pct", 100)
+    assert not errors, errors
+    assert got["multi"].tobytes() == a_ref.tobytes()
+    assert got["render"].tobytes() == b_ref.tobytes()
+    w.check()
+
+
+@pytest.mark.gpu
+def test_counted_device_renders_share_a_stream(rt):
+    """Two threads make synchronous counted calls (rt_render_shard_device_ex
+    with stats) on the same caller stream: each gets a workspace of its own,
+    so each call returns its own frame and its own counters, equal to the same
+    call made alone (advisor, round 4)."""
+    import torch
+    from rtamd import scenes
+    w, cam, depth = scenes.c3(96, 54, n_spheres=200)
+    cam2 = scenes.c3_orbit(5, 8, 96, 54)
+    s0 = torch.cuda.current_stream().cuda_stream
+
+    def call(c):
+        buf = torch.empty((c.vsize, c.hsize, 3), dtype=torch.float64, device="cuda")
+        st = c.render_shard_device(w, depth, 8, 0, 1, buf.data_ptr(), s0, True, exhaustive=False)
+        torch.cuda.synchronize()
+        return buf.cpu().numpy(), {k: st[k] for k in ("rays_primary", "rays_reflect", "rays_refract", "rays_shadow")}
+
+    alone = [call(cam), call(cam2)]
+    assert alone[0][1] != alone[1][1]  # different cameras, different counts
+    got, errors = _run_threads([(0, lambda: call(cam)), (1, lambda: call(cam2))], rounds=4)
+    assert not errors, errors
+    for k in (0, 1):
+        assert got[k][0].tobytes() == alone[k][0].tobytes(), k
+        assert got[k][1] == alone[k][1], k
+    w.check()
