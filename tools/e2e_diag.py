@@ -1,7 +1,8 @@
 """rt_render to a host canvas on C3 (dev tool): per-frame times of a loop that
 drops each canvas before the next render and of one that holds the previous
 canvas (as bench.py's end_to_end), before and after device-resident batches
-on 4 streams (bench.py's timed region)."""
+on 4 streams (bench.py's timed region); the held loop with an idle gap before
+each call, and the device render alone."""
 import json
 import os
 import sys
@@ -15,10 +16,14 @@ import rtamd  # noqa: E402
 from rtamd import scenes  # noqa: E402
 
 
-def loop(cam, w, depth, hold, n=12):
+def loop(cam, w, depth, hold, n=12, gap_ms=0.0):
     ts = []
     keep = None
     for _ in range(n):
+        if gap_ms:
+            t1 = time.perf_counter()
+            while (time.perf_counter() - t1) * 1e3 < gap_ms:
+                pass
         t0 = time.perf_counter()
         c, _ = cam.render(w, depth, want_stats=False)
         ts.append(round((time.perf_counter() - t0) * 1e3, 3))
@@ -40,4 +45,19 @@ for it in range(8):
 torch.cuda.synchronize()
 out["drop_2"] = loop(cam, w, depth, False)
 out["hold_2"] = loop(cam, w, depth, True)
+# the same loop with an idle gap before each call (is a call slowed by the one before it?)
+for gap in (0.5, 2.0):
+    out[f"hold_gap{gap}"] = loop(cam, w, depth, True, gap_ms=gap)
+# one call's phases: the render alone into a device buffer, then the whole call again
+dev = torch.empty((cam.vsize, cam.hsize, 3), dtype=torch.float64, device="cuda")
+s0 = torch.cuda.current_stream()
+ts = []
+for _ in range(12):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    cam.render_shard_device(w, depth, 8, 0, 1, dev.data_ptr(), s0.cuda_stream, False)
+    torch.cuda.synchronize()
+    ts.append(round((time.perf_counter() - t0) * 1e3, 3))
+out["device_render_only"] = ts
+out["hold_3"] = loop(cam, w, depth, True)
 print(json.dumps(out))
