@@ -1013,19 +1013,21 @@ int rt_scene_create_groups(const rt_shape_desc* shapes, size_t n_shapes, const i
   std::vector<SphereGen> fx_gen;
   std::vector<QuadRec> fx_quads;
   double blo[3], bhi[3];
-  // (shapes inside groups stay outside the hierarchy: their group gate goes with them)
+  // (shapes inside groups too: their group gate goes with them, tested before the
+  // shape at the leaf, as the reference tests a group's box before its children)
   for (const SphereGen& g : gen) {
     OtherRec r{};
     for (int e = 0; e < 12; ++e) r.m[e] = g.m[e];
     r.kind = 0;
     r.meta = (int32_t)g.meta;
-    if (g.gate == 0 && other_box(r, blo, bhi)) orec.push_back(r);
+    r.gate = g.gate;
+    if (other_box(r, blo, bhi)) orec.push_back(r);
     else fx_gen.push_back(g);
   }
   std::vector<QuadRec> line_rec;  // open tubes and cones with finite bounds: the line hierarchy
   for (const QuadRec& q : quads) {
-    if (q.gate == 0 && other_box(q, blo, bhi)) orec.push_back(q);
-    else if (q.gate == 0 && line_box(q, blo, bhi)) line_rec.push_back(q);
+    if (other_box(q, blo, bhi)) orec.push_back(q);
+    else if (q.gate == 0 && line_box(q, blo, bhi)) line_rec.push_back(q);  // (grouped tubes and cones: exhaustive)
     else fx_quads.push_back(q);
   }
   std::vector<GroupRec> grec(n_groups);
@@ -1033,13 +1035,24 @@ int rt_scene_create_groups(const rt_shape_desc* shapes, size_t n_shapes, const i
     for (int c = 0; c < 3; ++c) { grec[g].lo[c] = groups[g].min[c]; grec[g].hi[c] = groups[g].max[c]; }
     grec[g].parent = groups[g].parent + 1;
   }
+  // A handful of records is cheaper in the exhaustive loops (wave-uniform, scalar loads) than
+  // behind a per-lane walk from global memory: the hierarchies start at kMinHierRecords
+  // (640x480 frames: the groups scene's 7 grouped records 0.92 ms in the hierarchies, 0.69
+  // exhaustive; solids 0.72 -> 0.60, zoo 0.37 -> 0.29; a divided group of 800: 5.1 against
+  // 32.3), except in a scene without any other hierarchy, where one of
+  // them is what opens the fused generations (the hexagon demo: 1.0 -> 0.53 ms)
+  constexpr size_t kMinHierRecords = 16;
   int obvh_depth = 0;
-  std::vector<BvhNode> obvh = build_other_bvh(orec, leaf, &obvh_depth, g_bvh_ct / 100.0);
+  std::vector<BvhNode> obvh;
+  if (orec.size() >= kMinHierRecords || (bvh.empty() && !orec.empty()))
+    obvh = build_other_bvh(orec, leaf, &obvh_depth, g_bvh_ct / 100.0);
   if (obvh_depth > kBvhMaxDepth) obvh.clear();  // deeper than other_trace's stack: exhaustive
   int lbvh_depth = 0;
   std::vector<ConeCluster> lclus;
   std::vector<int32_t> lcone;
-  std::vector<BvhNode> lbvh = build_line_bvh(line_rec, &lclus, &lcone, &lbvh_depth);
+  std::vector<BvhNode> lbvh;
+  if (line_rec.size() >= kMinHierRecords || (bvh.empty() && obvh.empty() && !line_rec.empty()))
+    lbvh = build_line_bvh(line_rec, &lclus, &lcone, &lbvh_depth);
   if (lbvh.empty() || lbvh_depth > kBvhMaxDepth) {  // exhaustive, as before the line hierarchy
     for (const QuadRec& q : line_rec) fx_quads.push_back(q);
     line_rec.clear();
@@ -1053,6 +1066,7 @@ int rt_scene_create_groups(const rt_shape_desc* shapes, size_t n_shapes, const i
         SphereGen g{};
         for (int e = 0; e < 12; ++e) g.m[e] = r.m[e];
         g.meta = r.meta;
+        g.gate = r.gate;
         fx_gen.push_back(g);
       } else {
         fx_quads.push_back(r);

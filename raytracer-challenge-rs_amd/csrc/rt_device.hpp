@@ -343,9 +343,12 @@ __device__ __forceinline__ void trace_rest(const DevScene& sc, V3 o, V3 d, Hit& 
 
 // One culled other record (rt_layout.hpp OtherRec) with exactly the
 // operations of the exhaustive loops above: a general sphere as trace_rest's
-// general records, a solid as quad_test.
+// general records, a solid as quad_test; a record inside groups only when the
+// ray meets every group box around it (group_gate, as trace_rest).
 template <bool SHADOW>
-__device__ __forceinline__ void other_test(const OtherRec* q, V3 o, V3 d, Hit& h, unsigned& n_disc) {
+__device__ __forceinline__ void other_test(const DevScene& sc, const OtherRec* q, V3 o, V3 d, Hit& h,
+                                           unsigned& n_disc) {
+  if (q->gate && !group_gate(sc, q->gate, o, d)) return;  // Group::intersect (group.rs:49-58)
   if (q->kind == 0) {
     const double* m = q->m;
     const V3 lo = m34_point(m, o);

@@ -619,7 +619,7 @@ __device__ __forceinline__ void other_trace(const DevScene& sc, V3 o, V3 d, doub
       }
     } else {
       const int code = -(e + 1), first = code >> 7, cnt = code & 127;
-      for (int k = first; k < first + cnt; ++k) other_test<SHADOW>(sc.orec + k, o, d, h, n_disc);
+      for (int k = first; k < first + cnt; ++k) other_test<SHADOW>(sc, sc.orec + k, o, d, h, n_disc);
       n_tests += (unsigned)cnt;
       if constexpr (SHADOW) {
         if (h.key >= 0 && h.t < t_shadow) return;  // shadowed: done
@@ -721,6 +721,21 @@ __device__ __forceinline__ void line_trace(const DevScene& sc, V3 o, V3 d, doubl
     }
     if (nn == 2) stk[sp++] = next[1];
     e = nn > 0 ? next[0] : (sp > 0 ? stk[--sp] : kBvhEmpty);
+  }
+}
+// Counted launches (the reference's shape tests come from the group gates
+// each ray met, GateSkips): the gates of the grouped records the other
+// records' hierarchy holds (trace_rest counts those of the records it loops
+// over; the line hierarchy holds no grouped record). Every record is visited
+// here, so only counted launches call it.
+__device__ __forceinline__ void count_hier_gates(const DevScene& sc, V3 o, V3 d, GateSkips& sk) {
+  if (!sc.n_groups) return;
+  const cQuadRec orec = (cQuadRec)sc.orec;
+  for (int k = 0; k < sc.n_orec; ++k) {
+    const int g = orec[k].gate;
+    if (g && !group_gate(sc, g, o, d)) {
+      if (orec[k].kind == 0) ++sk.sph; else ++sk.other;
+    }
   }
 }
 

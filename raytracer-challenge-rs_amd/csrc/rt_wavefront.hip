@@ -815,6 +815,7 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
     } else {
       const bool shadowed = shadow_trace<LANE, QUADS>(sc, a.use_lb, ls, l, c.over, sdir, dist, t.sh_disc, t.sh_tests,
                                                       t.sh_boxes, &t.gsk);
+      if (QUADS && a.count) count_hier_gates(sc, c.over, sdir, t.gsk);
       ++t.sh_rays;
       term = lighting(*m, Lr, c.over, c.eyev, c.normal, shadowed, sdir);
     }
@@ -895,6 +896,7 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
     hit_init(h);
     if (valid) {
       wf_ray<CAM>(a, cam, slot, o, d);
+      if constexpr (TALLY && QUADS) count_hier_gates(sc, o, d, t.gsk);
       if constexpr (LANE == 0) {
         // the chunk's frame (chunks never mix frames): its shared-origin primary records
         const unsigned pf = a.n_frames > 1 ? (c * 64u) / a.frame_rays : 0u;

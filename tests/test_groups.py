@@ -380,3 +380,36 @@ def test_gpu_group_shards_reassemble(rt):
         ys = [y for y in range(cam.vsize) if (y // block) % n_shards == s]
         out[ys] = buf.cpu().numpy()
     assert out.tobytes() == full.tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,kw", GROUP_SCENES)
+def test_gpu_group_counted_fast_path_counters(rt, kind, kw):
+    """Grouped shapes sit in the fast path's hierarchies with their group gate
+    tested at the leaf; a counted fast-path render still reports the
+    reference's ray and shape-test counts (the gates each ray met, counted
+    over every grouped record), equal to the exhaustive loop's."""
+    from rtamd import scenes
+    w, cam, depth = scenes.CONFIGS[kind](**kw)
+    exact, se = cam.render(w, depth, want_stats=True)
+    fast, sf = cam.render(w, depth, want_stats=True, exhaustive=False)
+    assert fast.to_numpy().tobytes() == exact.to_numpy().tobytes()
+    for k in ("rays_primary", "rays_reflect", "rays_refract", "rays_shadow", "sphere_tests", "plane_tests",
+              "other_tests"):
+        if sf.get(k) is not None:
+            assert sf[k] == se[k], k
+
+
+@pytest.mark.gpu
+def test_gpu_divided_group_is_culled(rt):
+    """A Group::divide'd lattice of 12 x 12 x 2 shapes (group.rs:108-197): its
+    shapes are culled by the fast path's hierarchies (group gates at the
+    leaves), frames bitwise equal to the exhaustive loop."""
+    from rtamd import scenes
+    w, cam, depth = scenes.divided(96, 54, n=12, threshold=4)
+    exact, se = cam.render(w, depth, want_stats=True)
+    fast, _ = cam.render(w, depth, want_stats=False)
+    assert fast.to_numpy().tobytes() == exact.to_numpy().tobytes()
+    cam.render(w, depth, want_stats=True, exhaustive=False)
+    p = rt._rtamd._wf_profile(w, -1, True)
+    assert p["fused"] and p["n_other_culled"] >= 190
