@@ -440,13 +440,17 @@ def main():
     if events:
         NB = 1  # the event-coupled dev path assembles frame by frame
     fa = None
+    assembler_fallback = None  # why the RCCL stream assembler was not used (reported in the line)
     if n > 1 and a.assembler == "rccl" and F > 1:
         try:
             fa = RcclStreamAssembler(H, W, B, rank, n, dev, streams=rstreams, batch=NB, pattern=pattern)
         except Exception as e:  # fall back to the torch process groups
+            assembler_fallback = f"{type(e).__name__}: {e}"
             print(f"warning: RCCL stream assembler unavailable ({e}); using per-stream process groups",
                   file=sys.stderr, flush=True)
             fa = None
+    elif n > 1 and a.assembler == "rccl":
+        assembler_fallback = "one render stream (--inflight 1): torch process groups on the current stream"
     if fa is not None:
         pass
     elif per_stream:
@@ -650,6 +654,8 @@ def main():
                 "render_streams_n": F,
                 "render_streams": kind if F > 1 else "current",
                 "assembler": type(fa).__name__ if n > 1 else None,
+                "assembler_fallback": assembler_fallback,
+                "dist_backend": (dist.get_backend() if n > 1 and dist.is_initialized() else None),
             },
             "roofline": roofline(prof, breakdown, W, H, a, n, ref_work, elapsed / a.steps * 1e3, NB),
             "traced_rays_per_frame": int(traced_rays),
@@ -841,22 +847,27 @@ def roofline(prof, breakdown, W, H, a, n, ref_work, frame_ms, nb=1):
     return {
         "bound": "valu_f64",
         "kernel": kname,
-        "achieved": round(achieved, 3),
+        # achieved / frac: SURVEY.md §8(d)'s pricing of the executed tests (the survey's per-unit figure x
+        # the units this kernel's launches process in one frame, / their time)
+        "achieved": round(achieved_survey, 3),
         "peak": PEAK_F64_VALU_TFLOPS,
         "unit": "TFLOP/s",
-        "frac": round(achieved / PEAK_F64_VALU_TFLOPS, 4),
-        "achieved_survey": round(achieved_survey, 3),
-        "frac_survey": round(achieved_survey / PEAK_F64_VALU_TFLOPS, 4),
-        "survey_pricing": "SURVEY.md §8(d): 57 f64 ops per executed sphere test, 34 per plane test, +6 per "
-                          "disc >= 0; box tests unpriced",
+        "frac": round(achieved_survey / PEAK_F64_VALU_TFLOPS, 4),
+        "pricing": "SURVEY.md §8(d): 57 f64 ops per executed sphere test, 34 per plane test, +6 per "
+                   "disc >= 0; box tests unpriced",
+        # the same launches priced by the minimum op count of this code (box tests at 9.5, diagonal
+        # sphere tests at 28; DESIGN.md 'Roofline')
+        "achieved_executed": round(achieved, 3),
+        "frac_executed": round(achieved / PEAK_F64_VALU_TFLOPS, 4),
         "traffic": traffic,
         "kernel_ms": round(kernel_ms, 4),
         "kernel_ms_source": ms_src,
         "kernel_regime": (f"serialized: one batch of {nb} frames at a time (the benched launches, each carrying "
                           f"{nb} frames), time per frame = the batch's / {nb}; the timed region keeps several "
                           "batches in flight, so its per-frame time (ms_per_step) can be below kernel_ms"),
-        "ops_per_frame": ops,
-        "per_unit": f"{OPS_SPHERE_DIAG} f64 ops per sphere test ({OPS_SPHERE_PRIMARY} for the generation "
+        "ops_per_frame": survey_ops,
+        "ops_per_frame_executed": ops,
+        "per_unit_executed": f"{OPS_SPHERE_DIAG} f64 ops per sphere test ({OPS_SPHERE_PRIMARY} for the generation "
                     f"pipeline's primary rays), {OPS_BOX} per BVH box test, {OPS_PLANE} per plane test, "
                     f"{OPS_ROOTS} per root pair (DESIGN.md 'Roofline'); executed tests counted on the device",
         "traversal": "bvh" if prof["bvh"] else "exhaustive",

@@ -339,9 +339,16 @@ int rt_hit_batch(const rt_scene* scene, const double* rays, size_t n,
 /* ---- multi-GPU (one process, several devices; the per-process path for
  *      torch.distributed is rt_render_shard_device) ------------------------ */
 
-/* Render on `n_devices` devices (ordinals 0..n-1) with interleaved row blocks
- * and assemble the canvas with one RCCL gather to device 0. `scenes[i]` must
- * have been created on device i. Output to a HOST buffer like rt_render. */
+/* `Camera::render_multithreaded` across devices (camera.rs:150-217): render on
+ * `n_devices` devices (ordinals 0..n-1) with interleaved blocks of `row_block`
+ * rows (block b on device b mod n; the reference's row-block partition,
+ * camera.rs:157-172). Output to a HOST buffer like rt_render: each device's
+ * DMA engine copies its rows straight into the canvas over its own link, each
+ * device driven by its own host thread; one device renders as rt_render does.
+ * The canvas is registered for the call unless it is a pinned block
+ * (rt_host_buffer_alloc) or pinned by the caller. `scenes[i]` must have been
+ * created on device i. Development knob `multi_gather` (scene 0): every shard
+ * gathered into device 0 with one grouped RCCL ncclGather instead. */
 int rt_render_multi(rt_scene* const* scenes, int n_devices,
                     const rt_camera_desc* camera, uint32_t max_depth,
                     uint32_t aa_samples, uint32_t row_block, double* out_rgb,

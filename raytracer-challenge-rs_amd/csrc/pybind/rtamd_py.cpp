@@ -60,6 +60,9 @@ extern "C" int rtamd_nccl_gather_f64(const double* send, double* recv, size_t co
 extern "C" int rtamd_nccl_comm_destroy(void* comm);
 extern "C" int rtamd_wf_profile(const rt_scene* s, int enable, double out[38]);
 extern "C" int rtamd_scene_tuning_set(const rt_scene* s, const char* key, int value);
+extern "C" int rtamd_render_shard_host(const rt_scene* scene, const rt_camera_desc* camera, uint32_t max_depth,
+                                       uint32_t aa_samples, uint32_t row_block, uint32_t shard, uint32_t n_shards,
+                                       double* out_rgb, rt_stats* stats);
 
 PYBIND11_MODULE(_rtamd, m) {
   m.doc() = "MI355X-native render path of raytracer-challenge-rs (host API over the C-ABI)";
@@ -421,6 +424,22 @@ PYBIND11_MODULE(_rtamd, m) {
         }
         return py::make_tuple(py::bytes(out), stats_dict(st));
       }, py::arg("world"), py::arg("max_depth") = 5, py::arg("aa_samples") = 1, py::arg("want_stats") = false)
+      // canvas_to_ppm(&camera.render(&world)) into the caller's buffer (rt_render_ppm with a
+      // reused output buffer, as a frame loop holds one): returns the text's length
+      .def("render_ppm_into", [](const Camera& c, const World& w, py::buffer out, unsigned max_depth,
+                                 unsigned aa_samples) {
+        py::buffer_info bi = out.request(true);
+        if (bi.ndim != 1 || bi.itemsize != 1) throw std::invalid_argument("expected a writable 1-D byte buffer");
+        size_t len = 0;
+        int rc;
+        {
+          py::gil_scoped_release nogil;
+          rc = rt_render_ppm(w.scene(), &c.desc(), max_depth, aa_samples, (char*)bi.ptr, (size_t)bi.size, &len,
+                             nullptr);
+        }
+        check(rc, "rt_render_ppm");
+        return len;
+      }, py::arg("world"), py::arg("out"), py::arg("max_depth") = 5, py::arg("aa_samples") = 1)
       .def_readwrite("render_opts", &Camera::render_opts, py::return_value_policy::reference_internal)
       .def("render_multithreaded", [](const Camera& c, const World& w, unsigned max_depth, bool want_stats,
                                       py::object exhaustive) {
@@ -453,7 +472,7 @@ PYBIND11_MODULE(_rtamd, m) {
                               unsigned aa_samples) {
         std::vector<rt_scene*> sc;
         for (size_t i = 0; i < worlds.size(); ++i) sc.push_back(const_cast<rt_scene*>(worlds[i]->scene((int)i)));
-        Canvas* out = new Canvas(c.hsize(), c.vsize());
+        Canvas* out = new Canvas(c.hsize(), c.vsize(), Canvas::Uninit{});  // (a pooled pinned block: every pixel is written)
         rt_stats st{};
         int rc;
         {
@@ -465,6 +484,31 @@ PYBIND11_MODULE(_rtamd, m) {
         return py::make_tuple(std::unique_ptr<Canvas>(out), stats_dict(st));
       }, py::arg("worlds"), py::arg("max_depth") = 5, py::arg("row_block") = 8, py::arg("aa_samples") = 1);
   m.def("shard_rows", &rt_shard_rows);
+  // a pinned host buffer from the library's pool (rt_host_buffer_alloc): uint8, freed with the array
+  m.def("host_buffer", [](size_t bytes) {
+    void* p = rt_host_buffer_alloc(bytes);
+    if (!p) throw RtError(RT_ERR_HOST, std::string("rt_host_buffer_alloc: ") + rt_last_error());
+    py::capsule owner(p, [](void* q) { rt_host_buffer_free(q); });
+    return py::array_t<uint8_t>({(py::ssize_t)bytes}, {(py::ssize_t)1}, (uint8_t*)p, owner);
+  }, py::arg("bytes"));
+  // dev/test: one device's part of rt_render_multi (shard rows straight into a full-size host canvas)
+  m.def("_render_shard_host", [](const World& w, const Camera& c, unsigned max_depth, unsigned row_block,
+                                 unsigned shard, unsigned n_shards,
+                                 py::array_t<double, py::array::c_style> out, unsigned aa_samples, bool want_stats) {
+    if (out.ndim() != 3 || (size_t)out.shape(0) != c.vsize() || (size_t)out.shape(1) != c.hsize() || out.shape(2) != 3)
+      throw std::invalid_argument("expected a (vsize, hsize, 3) float64 canvas");
+    double* p = out.mutable_data();
+    rt_stats st{};
+    int rc;
+    {
+      py::gil_scoped_release nogil;
+      rc = rtamd_render_shard_host(w.scene(), &c.desc(), max_depth, aa_samples, row_block, shard, n_shards, p,
+                                   want_stats ? &st : nullptr);
+    }
+    check(rc, "rtamd_render_shard_host");
+    return stats_dict(st);
+  }, py::arg("world"), py::arg("camera"), py::arg("max_depth"), py::arg("row_block"), py::arg("shard"),
+     py::arg("n_shards"), py::arg("out"), py::arg("aa_samples") = 1, py::arg("want_stats") = false);
   m.def("render_frames_device", [](const World& w, std::vector<const Camera*> cams, unsigned max_depth,
                                    unsigned row_block, unsigned shard, unsigned n_shards, std::vector<uintptr_t> d_outs,
                                    uintptr_t stream, bool want_stats, unsigned aa_samples) {

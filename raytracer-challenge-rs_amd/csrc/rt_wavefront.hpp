@@ -111,6 +111,9 @@ struct WfTuning {
   int band_pct = 35;       // ... the first band's share of the rows (percent)
   int band_ratio = 100;    // ... each later band's size, percent of the one before (100: equal shares)
   int band_gen = 1;        // ... band k+1 starts when band k's generation band_gen has run (-1: its whole render)
+  int multi_gather = 0;    // rt_render_multi (scenes[0]'s knob): 1 = every shard gathered into device 0 by one grouped
+                           //     ncclGather, then copied out of device 0 (test hook; 0 = each device copies its rows
+                           //     straight into the host canvas, rt_multi.cpp)
 };
 // Applies `key` = `value` to `t`: 1 = applied, 0 = not a render-time key, -1 = bad value.
 int wf_tuning_apply(WfTuning& t, const char* key, int value);

@@ -15,6 +15,8 @@
 #   pmc        tools/profile.sh TAG (kernel trace + PMC passes of 5 serialized frames)
 #   pmc_c5     the same for C5
 #   quick      tools/quick_time.py (C3 and C5 frame times, two runs)
+#   ppm        tools/ppm_probe.py (where rt_render_ppm's time goes)
+#   multi      tools/multi_probe.py (rt_render_multi's per-device parts, projected N-device frame)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 export TMPDIR=/tmp
@@ -48,6 +50,8 @@ for s in "$@"; do
     pmc) step pmc 900 bash tools/profile.sh "$TAG" || exit 1 ;;
     pmc_c5) BATCH=1 SUMMARY_ARGS="--width 4096 --height 4096 --spheres 9996" step pmc_c5 900 bash tools/profile.sh "${TAG}_c5" --config c5 --width 4096 --height 4096 --spheres 9996 || exit 1 ;;
     quick) step quick 600 python tools/quick_time.py || exit 1 ;;
+    ppm) step ppm 300 python tools/ppm_probe.py || exit 1 ;;
+    multi) step multi 300 python tools/multi_probe.py || exit 1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
