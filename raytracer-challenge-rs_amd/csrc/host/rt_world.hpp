@@ -597,13 +597,28 @@ class Camera {
   // on the device; aa_samples > 1 renders as render_multithreaded does.
   std::string render_ppm(const World& world, unsigned max_depth = 5, unsigned aa_samples = 1,
                          rt_stats* stats = nullptr) const {
-    const size_t bound = 32 + (size_t)12 * desc_.hsize * desc_.vsize + desc_.vsize;
-    std::string s(bound, '\0');
-    size_t len = 0;
-    check(rt_render_ppm(world.scene(), &desc_, max_depth, aa_samples, &s[0], s.size(), &len, stats),
-          "rt_render_ppm");
-    s.resize(len);
+    std::string s;
+    render_ppm_with(world, max_depth, aa_samples, stats, [&](const char* p, size_t n) { s.assign(p, n); });
     return s;
+  }
+  // The text in a pooled pinned block (rt_host_buffer_alloc: the device writes it at
+  // the link's rate, and a frame loop reuses the same pages), handed to `take(p, n)`.
+  template <typename F>
+  void render_ppm_with(const World& world, unsigned max_depth, unsigned aa_samples, rt_stats* stats, F&& take) const {
+    const size_t bound = 32 + (size_t)12 * desc_.hsize * desc_.vsize + desc_.vsize;
+    struct Block {
+      void* p;
+      ~Block() { rt_host_buffer_free(p); }
+    } blk{rt_host_buffer_alloc(bound)};
+    std::string fallback;  // (no pinned memory to be had: a plain buffer, which the library registers)
+    char* buf = (char*)blk.p;
+    if (!buf) {
+      fallback.resize(bound);
+      buf = &fallback[0];
+    }
+    size_t len = 0;
+    check(rt_render_ppm(world.scene(), &desc_, max_depth, aa_samples, buf, bound, &len, stats), "rt_render_ppm");
+    take((const char*)buf, len);
   }
   RenderOpts render_opts;
 

@@ -417,12 +417,16 @@ PYBIND11_MODULE(_rtamd, m) {
       }, py::arg("world"), py::arg("max_depth") = 5, py::arg("want_stats") = true, py::arg("exhaustive") = py::none())
       .def("render_ppm", [](const Camera& c, const World& w, unsigned max_depth, unsigned aa_samples, bool want_stats) {
         rt_stats st{};
-        std::string out;
+        py::object out;
         {
           py::gil_scoped_release nogil;
-          out = c.render_ppm(w, max_depth, aa_samples, want_stats ? &st : nullptr);
+          // the bytes object is made from the pinned text at once (one copy)
+          c.render_ppm_with(w, max_depth, aa_samples, want_stats ? &st : nullptr, [&](const char* p, size_t n) {
+            py::gil_scoped_acquire gil;
+            out = py::bytes(p, n);
+          });
         }
-        return py::make_tuple(py::bytes(out), stats_dict(st));
+        return py::make_tuple(out, stats_dict(st));
       }, py::arg("world"), py::arg("max_depth") = 5, py::arg("aa_samples") = 1, py::arg("want_stats") = false)
       // canvas_to_ppm(&camera.render(&world)) into the caller's buffer (rt_render_ppm with a
       // reused output buffer, as a frame loop holds one): returns the text's length
@@ -469,7 +473,7 @@ PYBIND11_MODULE(_rtamd, m) {
          py::arg("d_out"), py::arg("stream") = 0, py::arg("want_stats") = false, py::arg("aa_samples") = 1,
          py::arg("exhaustive") = py::none())
       .def("render_multi", [](const Camera& c, std::vector<World*> worlds, unsigned max_depth, unsigned row_block,
-                              unsigned aa_samples) {
+                              unsigned aa_samples, bool want_stats) {
         std::vector<rt_scene*> sc;
         for (size_t i = 0; i < worlds.size(); ++i) sc.push_back(const_cast<rt_scene*>(worlds[i]->scene((int)i)));
         Canvas* out = new Canvas(c.hsize(), c.vsize(), Canvas::Uninit{});  // (a pooled pinned block: every pixel is written)
@@ -478,11 +482,12 @@ PYBIND11_MODULE(_rtamd, m) {
         {
           py::gil_scoped_release nogil;
           rc = rt_render_multi(sc.data(), (int)sc.size(), &c.desc(), max_depth, aa_samples, row_block, out->data(),
-                               &st);
+                               want_stats ? &st : nullptr);
         }
         if (rc != RT_OK) { delete out; check(rc, "rt_render_multi"); }
         return py::make_tuple(std::unique_ptr<Canvas>(out), stats_dict(st));
-      }, py::arg("worlds"), py::arg("max_depth") = 5, py::arg("row_block") = 8, py::arg("aa_samples") = 1);
+      }, py::arg("worlds"), py::arg("max_depth") = 5, py::arg("row_block") = 8, py::arg("aa_samples") = 1,
+         py::arg("want_stats") = true);
   m.def("shard_rows", &rt_shard_rows);
   // a pinned host buffer from the library's pool (rt_host_buffer_alloc): uint8, freed with the array
   m.def("host_buffer", [](size_t bytes) {

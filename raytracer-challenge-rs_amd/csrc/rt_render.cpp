@@ -136,18 +136,136 @@ int rt_render_block_pattern_device(const rt_scene* scene, const rt_camera_desc* 
 }  // extern "C"
 
 namespace rtapi {
+namespace {
+// The row bands of a banded host render (render_banded, render_ppm_banded):
+// the frame's rows in nb <= 64 blocks of rb rows (one period of
+// rt_render_block_pattern_device's mapping over the whole canvas), cut into
+// `bands` contiguous runs of blocks. The first band takes band_pct of the rows,
+// the others share the remainder in sizes falling by band_ratio percent per
+// band. False: too few blocks to band.
+struct BandPlan {
+  int bands = 0;
+  uint32_t rb = 0, nb = 0;
+  uint32_t y0[kMaxBands + 1] = {};  // band k = rows [y0[k], y0[k + 1])
+  uint64_t mask[kMaxBands] = {};    // band k's blocks
+};
+bool plan_bands(const rt_scene* s, uint32_t H, BandPlan& p) {
+  p.bands = std::max(2, std::min(kMaxBands, s->tune.bands));
+  p.rb = (H + 63) / 64;
+  p.nb = (H + p.rb - 1) / p.rb;
+  if (p.nb < (uint32_t)p.bands * 2) return false;
+  const uint32_t nb = p.nb;
+  const int bands = p.bands;
+  uint32_t b[kMaxBands + 1] = {};
+  b[1] = std::max<uint32_t>(1, std::min<uint32_t>(nb - (uint32_t)bands + 1, (uint32_t)((uint64_t)nb * s->tune.band_pct / 100)));
+  double wsum = 0.0, wk = 1.0;
+  for (int k = 1; k < bands; ++k, wk *= s->tune.band_ratio / 100.0) wsum += wk;
+  double acc = 0.0;
+  wk = 1.0;
+  for (int k = 2; k < bands; ++k, wk *= s->tune.band_ratio / 100.0) {
+    acc += wk;
+    const uint32_t at = b[1] + (uint32_t)((nb - b[1]) * acc / wsum + 0.5);
+    b[k] = std::min<uint32_t>(nb - (uint32_t)(bands - k), std::max<uint32_t>(b[k - 1] + 1, at));
+  }
+  b[bands] = nb;
+  const uint64_t all = nb == 64 ? ~0ull : ((1ull << nb) - 1ull);
+  for (int k = 0; k <= bands; ++k) p.y0[k] = std::min(H, b[k] * p.rb);
+  for (int k = 0; k < bands; ++k) {
+    const uint64_t below_end = b[k + 1] >= 64 ? ~0ull : ((1ull << b[k + 1]) - 1ull);
+    const uint64_t below_start = (1ull << b[k]) - 1ull;
+    p.mask[k] = all & below_end & ~below_start;
+  }
+  return true;
+}
+
+// The band renders of one call: band k renders on its own stream (its own
+// workspace, pinned to the call), starting when band k-1's render is done (or
+// band_gen >= 0: when its generation band_gen has been launched), so the GPU
+// works on one band at a time as in a whole-frame render while each band's
+// follow-up work (a copy, an encoder) runs behind the later bands. Band k's
+// rows go to d_out + y0[k] rows. On destruction every stream that received
+// work drains first, then the workspaces are unpinned (under the scene's lock):
+// no kernel or copy outlives the call.
+struct BandRender {
+  rt_scene* s;
+  std::unique_lock<std::mutex>& lk;
+  rt_scene::HostCtx* c;
+  const BandPlan& p;
+  hipStream_t st[kMaxBands] = {};
+  rt_scene::WfSlot* used[kMaxBands] = {};
+  int n_enq = 0;  // band streams with work enqueued
+  BandRender(rt_scene* s_, std::unique_lock<std::mutex>& lk_, rt_scene::HostCtx* c_, const BandPlan& p_)
+      : s(s_), lk(lk_), c(c_), p(p_) {}
+  ~BandRender() {
+    for (int k = 0; k < n_enq; ++k)
+      if (hipStreamSynchronize(st[k]) != hipSuccess) (void)hipGetLastError();
+    if (!lk.owns_lock()) lk.lock();
+    for (int k = 0; k < p.bands; ++k) unpin(k);
+  }
+  BandRender(const BandRender&) = delete;
+  BandRender& operator=(const BandRender&) = delete;
+  void unpin(int k) {
+    if (used[k]) {
+      --used[k]->pins;
+      used[k] = nullptr;
+    }
+  }
+  int open() {
+    st[0] = c->stream;
+    for (int k = 1; k < p.bands; ++k) {
+      if (!c->band_stream[k - 1]) RT_HIP(hipStreamCreateWithFlags(&c->band_stream[k - 1], hipStreamNonBlocking));
+      st[k] = c->band_stream[k - 1];
+    }
+    for (int k = 0; k < p.bands; ++k)
+      if (!c->band_ev[k]) RT_HIP(hipEventCreateWithFlags(&c->band_ev[k], hipEventDisableTiming));
+    return RT_OK;
+  }
+  // enqueues band k's render (under the scene's lock)
+  int render(int k, const DevCamera& dc, uint32_t W, uint32_t aa, uint32_t max_depth) {
+    if (k > 0) RT_HIP(hipStreamWaitEvent(st[k], c->band_ev[k - 1], 0));  // band k after band k-1's render
+    const uint32_t rows = p.y0[k + 1] - p.y0[k];
+    const bool early = s->tune.band_gen >= 0 && k + 1 < p.bands;
+    bool recorded = false;
+    n_enq = k + 1;
+    int rc = run_render(s, dc, nullptr, rows * W * aa, aa, max_depth, p.rb, 0, 1, c->d_out + (size_t)p.y0[k] * W * 3,
+                        st[k], nullptr, nullptr, 0, &used[k], nullptr, 1, false, &lk, false, true, p.nb, p.mask[k],
+                        early ? c->band_ev[k] : nullptr, s->tune.band_gen, &recorded, &s->band_sizing);
+    if (rc != RT_OK) return rc;
+    if (!recorded) RT_HIP(hipEventRecord(c->band_ev[k], st[k]));
+    return RT_OK;
+  }
+  // every band stream drained (the scene's lock released meanwhile); the first error
+  int wait_all() {
+    lk.unlock();  // the workspaces stay pinned to this call
+    hipError_t first = hipSuccess;
+    for (int k = 0; k < n_enq; ++k) {
+      const hipError_t e = hipStreamSynchronize(st[k]);
+      if (e != hipSuccess && first == hipSuccess) first = e;
+    }
+    lk.lock();
+    if (first != hipSuccess) return fail(RT_ERR_HIP, std::string("banded render: ") + hipGetErrorString(first));
+    return RT_OK;
+  }
+  // after wait_all: band k's workspace read back (learned sizes, overflow) and unpinned
+  int overflowed(int k, bool* over) {
+    *over = false;
+    if (!used[k]) return RT_OK;
+    used[k]->wf->learn(s->band_sizing);
+    RT_HIP(used[k]->wf->take_overflow(over));
+    unpin(k);
+    return RT_OK;
+  }
+};
+}  // namespace
+
 // `Camera::render` into a host canvas with the device-to-host copy overlapped
-// (rt_render_ex): the frame's rows are cut into `bands`
-// contiguous bands of 64-block patterns (rt_render_block_pattern_device's
-// mapping with one period over the whole canvas). Band k renders on its own
-// stream (its own workspace), starting when band k-1's render is done, so the
-// GPU works on one band at a time as in a whole-frame render, and band k's copy
-// to the host runs behind its render while band k+1 renders. Every pixel is
-// that of the whole-frame render (a pattern only chooses which rows a render
-// owns). The caller's canvas must be pinned (rt_host_buffer_alloc), registered
-// by the caller (`host_ready`: rt_render_multi) or registrable for the call
-// (d2h = 1); RT_ERR_NO_DEVICE asks the caller for the one-render path. A band
-// that overflowed its arenas is rendered again, synchronously, before the call
+// (rt_render_ex): the bands of plan_bands, each band's copy to
+// the host behind its render while the next bands render. Every pixel is that
+// of the whole-frame render (a pattern only chooses which rows a render owns).
+// The caller's canvas must be pinned (rt_host_buffer_alloc), registered by the
+// caller (`host_ready`: rt_render_multi) or registrable for the call (d2h =
+// 1); RT_ERR_NO_DEVICE asks the caller for the one-render path. A band that
+// overflowed its arenas is rendered again, synchronously, before the call
 // returns (every synchronous call returns a complete frame). On every return
 // after the first band is enqueued, every band stream has drained first: no
 // kernel or copy into the canvas outlives the call (its registration, its
@@ -155,25 +273,8 @@ namespace rtapi {
 int render_banded(rt_scene* s, std::unique_lock<std::mutex>& lk, rt_scene::HostCtx* c, const rt_camera_desc& cam,
                   uint32_t max_depth, uint32_t aa, double* out_rgb, bool host_ready) {
   const uint32_t W = cam.hsize, H = cam.vsize;
-  const int bands = std::max(2, std::min(kMaxBands, s->tune.bands));
-  const uint32_t rb = (H + 63) / 64, nb = (H + rb - 1) / rb;  // nb <= 64 blocks of rb rows: one period
-  if (nb < (uint32_t)bands * 2) return RT_ERR_NO_DEVICE;
-  // band k = blocks [b[k], b[k+1]): the first band takes band_pct of the rows, the
-  // others share the remainder in sizes falling by band_ratio percent per band
-  uint32_t b[kMaxBands + 1] = {};
-  b[1] = std::max<uint32_t>(1, std::min<uint32_t>(nb - (uint32_t)bands + 1, (uint32_t)((uint64_t)nb * s->tune.band_pct / 100)));
-  {
-    double wsum = 0.0, wk = 1.0;
-    for (int k = 1; k < bands; ++k, wk *= s->tune.band_ratio / 100.0) wsum += wk;
-    double acc = 0.0;
-    wk = 1.0;
-    for (int k = 2; k < bands; ++k, wk *= s->tune.band_ratio / 100.0) {
-      acc += wk;
-      const uint32_t at = b[1] + (uint32_t)((nb - b[1]) * acc / wsum + 0.5);
-      b[k] = std::min<uint32_t>(nb - (uint32_t)(bands - k), std::max<uint32_t>(b[k - 1] + 1, at));
-    }
-  }
-  b[bands] = nb;
+  BandPlan p;
+  if (!plan_bands(s, H, p)) return RT_ERR_NO_DEVICE;
   const size_t bytes = (size_t)W * H * 3 * sizeof(double);
   bool registered = false;
   if (!host_ready && !pinned_block(out_rgb, bytes)) {
@@ -190,89 +291,111 @@ int render_banded(rt_scene* s, std::unique_lock<std::mutex>& lk, rt_scene::HostC
       if (on && hipHostUnregister(p) != hipSuccess) (void)hipGetLastError();
     }
   } unreg{out_rgb, registered};
-  hipStream_t st[kMaxBands] = {c->stream};
-  for (int k = 1; k < bands; ++k) {
-    if (!c->band_stream[k - 1]) RT_HIP(hipStreamCreateWithFlags(&c->band_stream[k - 1], hipStreamNonBlocking));
-    st[k] = c->band_stream[k - 1];
-  }
-  for (int k = 0; k < bands; ++k)
-    if (!c->band_ev[k]) RT_HIP(hipEventCreateWithFlags(&c->band_ev[k], hipEventDisableTiming));
+  BandRender br(s, lk, c, p);  // (after unreg: it drains its streams before the canvas is unregistered)
+  int rc = br.open();
+  if (rc != RT_OK) return rc;
   const DevCamera dc = to_dev_camera(cam);
-  const uint64_t all = nb == 64 ? ~0ull : ((1ull << nb) - 1ull);
-  rt_scene::WfSlot* used[kMaxBands] = {};
-  auto unpin = [&](int k) {
-    if (used[k]) {
-      --used[k]->pins;
-      used[k] = nullptr;
-    }
+  auto copy = [&](int k) -> int {
+    const size_t off = (size_t)p.y0[k] * W * 3;
+    RT_HIP(hipMemcpyAsync(out_rgb + off, c->d_out + off, (size_t)(p.y0[k + 1] - p.y0[k]) * W * 3 * sizeof(double),
+                          hipMemcpyDeviceToHost, br.st[k]));
+    return RT_OK;
   };
-  struct UnpinAll {
-    std::function<void()> f;
-    ~UnpinAll() { f(); }
-  } unpin_all{[&]() {
-    if (!lk.owns_lock()) lk.lock();
-    for (int k = 0; k < bands; ++k) unpin(k);
-  }};
-  // (declared after the guards above, so it runs before them: the streams drain
-  // before the workspaces are unpinned and the canvas unregistered)
-  struct Drain {
-    hipStream_t* st;
-    int n = 0;  // band streams with work enqueued
-    ~Drain() {
-      for (int k = 0; k < n; ++k)
-        if (hipStreamSynchronize(st[k]) != hipSuccess) (void)hipGetLastError();
-    }
-  } drain{st};
-  uint32_t y0[kMaxBands + 1];
-  for (int k = 0; k <= bands; ++k) y0[k] = std::min(H, b[k] * rb);
-  auto mask_of = [&](int k) {
-    const uint64_t below_end = b[k + 1] >= 64 ? ~0ull : ((1ull << b[k + 1]) - 1ull);
-    const uint64_t below_start = (1ull << b[k]) - 1ull;
-    return all & below_end & ~below_start;
-  };
-  for (int k = 0; k < bands; ++k) {
-    if (k > 0) RT_HIP(hipStreamWaitEvent(st[k], c->band_ev[k - 1], 0));  // band k after band k-1's render
-    const uint32_t rows = y0[k + 1] - y0[k];
-    // band k+1 starts after band k's render, or (band_gen >= 0) after its generation band_gen's launch
-    const bool early = s->tune.band_gen >= 0 && k + 1 < bands;
-    bool recorded = false;
-    drain.n = k + 1;
-    int rc = run_render(s, dc, nullptr, rows * W * aa, aa, max_depth, rb, 0, 1, c->d_out + (size_t)y0[k] * W * 3, st[k],
-                        nullptr, nullptr, 0, &used[k], nullptr, 1, false, &lk, false, true, nb, mask_of(k),
-                        early ? c->band_ev[k] : nullptr, s->tune.band_gen, &recorded, &s->band_sizing);
-    if (rc != RT_OK) return rc;
-    if (!recorded) RT_HIP(hipEventRecord(c->band_ev[k], st[k]));
-    RT_HIP(hipMemcpyAsync(out_rgb + (size_t)y0[k] * W * 3, c->d_out + (size_t)y0[k] * W * 3,
-                          (size_t)rows * W * 3 * sizeof(double), hipMemcpyDeviceToHost, st[k]));
+  for (int k = 0; k < p.bands; ++k) {
+    if ((rc = br.render(k, dc, W, aa, max_depth)) != RT_OK) return rc;
+    if ((rc = copy(k)) != RT_OK) return rc;
   }
-  lk.unlock();  // the workspaces stay pinned to this call
-  hipError_t first = hipSuccess;  // every stream drains before the first error is reported
-  for (int k = 0; k < bands; ++k) {
-    const hipError_t e = hipStreamSynchronize(st[k]);
-    if (e != hipSuccess && first == hipSuccess) first = e;
-  }
-  lk.lock();
-  if (first != hipSuccess) return fail(RT_ERR_HIP, std::string("banded render: ") + hipGetErrorString(first));
-  for (int k = 0; k < bands; ++k) {
-    if (!used[k]) continue;
-    used[k]->wf->learn(s->band_sizing);
+  if ((rc = br.wait_all()) != RT_OK) return rc;
+  for (int k = 0; k < p.bands; ++k) {
     bool over = false;
-    RT_HIP(used[k]->wf->take_overflow(&over));
-    unpin(k);
+    if ((rc = br.overflowed(k, &over)) != RT_OK) return rc;
     if (!over) continue;
     // (its canvas rows are NaN: render the band again, synchronously, with the arenas grown)
-    const uint32_t rows = y0[k + 1] - y0[k];
-    int rc = run_render(s, dc, nullptr, rows * W * aa, aa, max_depth, rb, 0, 1, c->d_out + (size_t)y0[k] * W * 3,
-                        st[k], nullptr, nullptr, 0, nullptr, nullptr, 1, true, &lk, false, false, nb, mask_of(k),
-                        nullptr, -1, nullptr, &s->band_sizing);
+    const uint32_t rows = p.y0[k + 1] - p.y0[k];
+    rc = run_render(s, dc, nullptr, rows * W * aa, aa, max_depth, p.rb, 0, 1, c->d_out + (size_t)p.y0[k] * W * 3,
+                    br.st[k], nullptr, nullptr, 0, nullptr, nullptr, 1, true, &lk, false, false, p.nb, p.mask[k],
+                    nullptr, -1, nullptr, &s->band_sizing);
     if (rc != RT_OK) return rc;
-    RT_HIP(hipMemcpyAsync(out_rgb + (size_t)y0[k] * W * 3, c->d_out + (size_t)y0[k] * W * 3,
-                          (size_t)rows * W * 3 * sizeof(double), hipMemcpyDeviceToHost, st[k]));
+    if ((rc = copy(k)) != RT_OK) return rc;
     lk.unlock();
-    const hipError_t e = hipStreamSynchronize(st[k]);
+    const hipError_t e = hipStreamSynchronize(br.st[k]);
     lk.lock();
     if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("banded render: ") + hipGetErrorString(e));
   }
+  return RT_OK;
+}
+
+// canvas_to_ppm(&camera.render(&world)) in bands (rt_render_ppm; DESIGN.md
+// §5.6): band k renders (BandRender), the device encoder turns its rows into
+// text in a region of its own (at the byte bound of everything before it: 12
+// bytes per pixel, the header first), and a pinned word receives the band's
+// text length behind the encoder. The host waits for each band's length in
+// turn and copies the band's text to its place in `out` on the band's stream,
+// while the later bands still render; only the last band's encoder and copy
+// follow the last render. `*out_len` = the whole text's length; the text is
+// the whole-frame encoder's byte for byte (row lengths and breaks are per
+// row). RT_ERR_NO_DEVICE: not bandable, or a band overflowed its arenas (the
+// caller renders the frame whole, which re-renders until it fits).
+int render_ppm_banded(rt_scene* s, std::unique_lock<std::mutex>& lk, rt_scene::HostCtx* c, const rt_camera_desc& cam,
+                      uint32_t max_depth, uint32_t aa, char* out, size_t cap, size_t* out_len) {
+  const uint32_t W = cam.hsize, H = cam.vsize;
+  BandPlan p;
+  if (!plan_bands(s, H, p)) return RT_ERR_NO_DEVICE;
+  if (!c->h_len) RT_HIP(hipHostMalloc((void**)&c->h_len, kMaxBands * sizeof(unsigned long long), hipHostMallocDefault));
+  for (int k = 0; k < p.bands; ++k)
+    if (!c->len_ev[k]) RT_HIP(hipEventCreateWithFlags(&c->len_ev[k], hipEventDisableTiming));
+  const PpmHeader hd = ppm_header(W, H), none{};
+  bool registered = false;
+  if (out && !pinned_block(out, cap)) {
+    if (hipHostRegister(out, cap, hipHostRegisterDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      return RT_ERR_NO_DEVICE;  // (the one-render path copies through its staging chunks)
+    }
+    registered = true;
+  }
+  struct Unregister {
+    void* p;
+    bool on;
+    ~Unregister() {
+      if (on && hipHostUnregister(p) != hipSuccess) (void)hipGetLastError();
+    }
+  } unreg{out, registered};
+  BandRender br(s, lk, c, p);
+  int rc = br.open();
+  if (rc != RT_OK) return rc;
+  const DevCamera dc = to_dev_camera(cam);
+  unsigned* d_len = (unsigned*)c->d_ppm_rows;
+  unsigned long long* d_off = (unsigned long long*)(((uintptr_t)c->d_ppm_rows + (size_t)H * 4 + 7) & ~(uintptr_t)7);
+  auto text_at = [&](int k) { return (size_t)(k == 0 ? 0 : hd.n) + (size_t)12 * W * p.y0[k]; };
+  for (int k = 0; k < p.bands; ++k) {
+    if ((rc = br.render(k, dc, W, aa, max_depth)) != RT_OK) return rc;
+    const uint32_t rows = p.y0[k + 1] - p.y0[k];
+    unsigned long long* off_k = d_off + p.y0[k] + k;  // rows + 1 offsets per band
+    RT_HIP(ppm_encode_device(c->d_out + (size_t)p.y0[k] * W * 3, W, rows, c->d_ppm + text_at(k),
+                             c->ppm_cap - text_at(k), d_len + p.y0[k], off_k, k == 0 ? hd : none, br.st[k]));
+    RT_HIP(hipMemcpyAsync(c->h_len + k, off_k + rows, sizeof(unsigned long long), hipMemcpyDeviceToHost, br.st[k]));
+    RT_HIP(hipEventRecord(c->len_ev[k], br.st[k]));
+  }
+  lk.unlock();  // (the context and the workspaces are this call's)
+  size_t at = 0;
+  for (int k = 0; k < p.bands; ++k) {
+    RT_HIP(hipEventSynchronize(c->len_ev[k]));
+    const size_t len = (size_t)(k == 0 ? hd.n : 0u) + (size_t)c->h_len[k];
+    if (out && at + len <= cap)
+      RT_HIP(hipMemcpyAsync(out + at, c->d_ppm + text_at(k), len, hipMemcpyDeviceToHost, br.st[k]));
+    at += len;
+  }
+  lk.lock();
+  if ((rc = br.wait_all()) != RT_OK) return rc;
+  bool any_over = false;
+  for (int k = 0; k < p.bands; ++k) {
+    bool over = false;
+    if ((rc = br.overflowed(k, &over)) != RT_OK) return rc;
+    any_over = any_over || over;
+  }
+  if (any_over) return RT_ERR_NO_DEVICE;  // (a band's rows were poisoned: the whole-frame path renders it again)
+  *out_len = at;
+  if (out && cap < at) return fail(RT_ERR_BUFFER_TOO_SMALL, "PPM buffer too small");
   return RT_OK;
 }
 }  // namespace rtapi
@@ -356,10 +479,16 @@ int rt_render_ppm(const rt_scene* scene, const rt_camera_desc* camera, uint32_t 
     if (c->d_ppm_rows) (void)hipFree(c->d_ppm_rows);
     c->d_ppm_rows = nullptr;
     c->ppm_rows_cap = 0;
-    RT_HIP(hipMalloc(&c->d_ppm_rows, (size_t)H * 4 + ((size_t)H + 1) * 8 + 8));
+    // row lengths, then the row offsets (H + 1; in bands, rows + 1 per band)
+    RT_HIP(hipMalloc(&c->d_ppm_rows, (size_t)H * 4 + ((size_t)H + kMaxBands + 1) * 8 + 8));
     c->ppm_rows_cap = H;
   }
   unsigned long long* d_off = (unsigned long long*)(((uintptr_t)c->d_ppm_rows + (size_t)H * 4 + 7) & ~(uintptr_t)7);
+  // a large frame without counters: bands, each band's text copied behind the later bands' renders
+  if (!stats && s->tune.bands > 1 && fast_path(s) && n_pix * aa_samples >= ((uint64_t)1 << 20)) {
+    rc = render_ppm_banded(s, lk, c, *camera, max_depth, aa_samples, out, cap, out_len);
+    if (rc != RT_ERR_NO_DEVICE) return rc;  // (not bandable, or a band overflowed: render it whole below)
+  }
   DevStats ds{};
   float ms = 0.f;
   rc = run_render(s, to_dev_camera(*camera), nullptr, (uint32_t)(n_pix * aa_samples), aa_samples, max_depth, H, 0,

@@ -108,3 +108,37 @@ def test_device_ppm_empty_canvases(rt, oracle):
         n = rt._rtamd.canvas_to_ppm_device(d.data_ptr(), w, h, out.data_ptr(), cap, 0)
         got = out[:n].cpu().numpy().tobytes()
         assert got == _as_bytes(oracle.canvas_to_ppm(img)) == _as_bytes(rt.canvas_to_ppm(img)), (h, w)
+
+
+def test_render_ppm_banded_paths(rt):
+    """rt_render_ppm at C3's full size renders in row bands, each band's text
+    encoded and copied behind the later bands' renders: the
+    text equals the one-render path's (bands = 1) byte for byte, into a pinned
+    block (the binding) and into a reused pageable buffer, with AA X2, and after
+    a forced arena overflow (the call falls back to the whole-frame render); a
+    buffer one byte short is refused."""
+    import numpy as np
+    from rtamd import scenes
+    w, cam, depth = scenes.c3()
+    w.tune("bands", 1)
+    whole, _ = cam.render_ppm(w, depth)
+    whole2, _ = cam.render_ppm(w, depth, 2)
+    w.tune("bands", 4)
+    banded, _ = cam.render_ppm(w, depth)
+    assert banded == whole
+    banded2, _ = cam.render_ppm(w, depth, 2)
+    assert banded2 == whole2
+    buf = np.zeros(len(whole) + 4096, dtype=np.uint8)
+    for _ in range(2):
+        n = cam.render_ppm_into(w, buf, depth)
+        assert n == len(whole) and buf[:n].tobytes() == whole
+    w.tune("arena_pct", 5)
+    try:
+        over, _ = cam.render_ppm(w, depth)
+    finally:
+        w.tune("arena_pct", 100)
+    assert over == whole
+    short = np.zeros(len(whole) - 1, dtype=np.uint8)
+    with pytest.raises(rt.RtError):
+        cam.render_ppm_into(w, short, depth)
+    w.check()

@@ -46,11 +46,11 @@ refb = ref.to_numpy().tobytes()
 res = {"render_to_host_ms": med(lambda: cam.render(w, depth, want_stats=False))}
 got, _ = cam.render_multi([w], depth, B)
 res["multi_direct_n1_bitwise"] = got.to_numpy().tobytes() == refb
-res["multi_direct_n1_ms"] = med(lambda: cam.render_multi([w], depth, B))
+res["multi_direct_n1_ms"] = med(lambda: cam.render_multi([w], depth, B, 1, False))
 w.tune("multi_gather", 1)
 got, _ = cam.render_multi([w], depth, B)
 res["multi_gather_n1_bitwise"] = got.to_numpy().tobytes() == refb
-res["multi_gather_n1_ms"] = med(lambda: cam.render_multi([w], depth, B))
+res["multi_gather_n1_ms"] = med(lambda: cam.render_multi([w], depth, B, 1, False))
 w.tune("multi_gather", 0)
 print(json.dumps(res), flush=True)
 pinned = rtamd._rtamd.host_buffer(H * W * 3 * 8).view(np.float64).reshape(H, W, 3)

@@ -22,11 +22,17 @@ def _targs(n, name):
 def klass(n):
     """Kernel class of a demangled name: primary / closest / shadow / prep /
     combine / frame (wf_frame_init: one per rendered frame)."""
+    if "wf_walk<" in n:  # split generation's walk launch (WfTuning::split): closest hits only
+        return "walk_primary" if _targs(n, "wf_walk")[1] == "true" else "walk"
     if "wf_trace_fused<" in n:  # fused generation: closest hit + shading + shadow rays + spawn
         # generation 0 of a camera render: PRIMARY (the wave traversal) or CAM (the per-lane
-        # walks over the LDS images read camera rays: template argument 5)
+        # walks over the LDS images read camera rays: template argument 5); SPLIT (argument 6):
+        # a split generation's shading launch
         t = _targs(n, "wf_trace_fused")
-        return "primary" if t[0] == "true" or (len(t) >= 5 and t[4] == "true") else "closest"
+        prim = t[0] == "true" or (len(t) >= 5 and t[4] == "true")
+        if len(t) >= 6 and t[5] == "true":
+            return "shade_primary" if prim else "shade"
+        return "primary" if prim else "closest"
     if "wf_trace_closest_bvh<" in n:
         return "primary" if _targs(n, "wf_trace_closest_bvh")[0] == "true" else "closest"
     if "wf_trace_closest<" in n:
