@@ -454,138 +454,6 @@ __device__ __forceinline__ void lane_trace_wide(const NODE* nodes, SD sd, const 
   }
 }
 
-// lane_trace_wide's closest-hit walk as resumable per-lane state (the walk
-// kernel, wf_walk: a lane whose ray is done takes the next ray while the
-// wave's other lanes keep walking). init() is lane_trace_wide's set-up for
-// the ray (o, d) with its hit so far; round() is one pass of its outer loop
-// (visits until no lane can visit, then the wave's batched leaves); a lane is
-// done when done() holds after a round. The visits, the leaf tests and their
-// order per ray are lane_trace_wide's, so the hit is the same bit for bit.
-template <typename SD = Sph48, bool ALL_LDS = true, typename NODE = BvhWide>
-struct WideWalk {
-  static constexpr bool H = sizeof(NODE) == 64;  // BvhWide16
-  static constexpr unsigned kBlk = H ? 8u : 16u, kHi = 3u * kBlk, kCc = 6u * kBlk;
-  float inv[3], on[3], of[3];
-  unsigned offe, offx;
-  float t_hi;
-  int sp;
-  unsigned e, pl;
-
-  __device__ __forceinline__ bool done() const { return e == kWideEmpty && pl == kWideEmpty; }
-
-  // (every lane of the wave calls it; `live` false: the lane stays done)
-  __device__ __forceinline__ void init(bool live, const float* M, bool has_bvh, V3 o, V3 d, Hit& h, SD sd,
-                                       int n_records, unsigned& n_disc, unsigned& n_tests) {
-    pl = kWideEmpty;
-    e = kWideEmpty;
-    sp = 0;
-    if (!live) return;
-    const float w = H ? 1.0f + 0x1p-9f : 1.0f;
-    const float Mw[3] = {M[0] * w, M[1] * w, M[2] * w};
-    const SlabRay sr = slab_ray(o, d, Mw);
-    t_hi = f32_up(h.t);
-    bool usable = false;
-    offe = 0;
-    offx = 0;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      const bool neg = sr.inv[a] < 0.0f;
-      inv[a] = sr.inv[a];
-      on[a] = neg ? sr.c_hi[a] : sr.c_lo[a];
-      of[a] = neg ? sr.c_lo[a] : sr.c_hi[a];
-      usable |= sr.inv[a] != 0.0f;
-      offe |= (kBlk * a + (neg ? kHi : 0u)) << (8 * a);
-      offx |= (kBlk * a + (neg ? 0u : kHi)) << (8 * a);
-    }
-    e = has_bvh ? 0u : kWideEmpty;
-    if (e == 0u && !usable) {  // no axis can cull: every record (as lane_trace_wide)
-      e = kWideEmpty;
-      for (int k = 0; k < n_records; ++k) {
-        leaf_sphere_test<false>(sd, k, o, d, h, n_disc);
-        ++n_tests;
-      }
-    }
-  }
-
-  __device__ __forceinline__ unsigned pop(uint16_t* lds) {
-    return sp > 0 ? (unsigned)lds[(--sp) * kTraceBlock] : kWideEmpty;
-  }
-
-  __device__ __forceinline__ void visit(const NODE* nodes, const NODE* top, int n_top, uint16_t* lds,
-                                        unsigned& n_boxes) {
-    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-    typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-    typedef typename std::conditional<H, u32x2, u32x4>::type Blk;
-    Blk E[3], X[3];
-    u32x2 cc;
-    if (ALL_LDS || (int)e < n_top) {
-      typedef __attribute__((address_space(3))) const unsigned char lb;
-      lb* b = (lb*)(top) + e * (unsigned)sizeof(NODE);
-      cc = *(__attribute__((address_space(3))) const u32x2*)(b + kCc);
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        E[a] = *(__attribute__((address_space(3))) const Blk*)(b + ((offe >> (8 * a)) & 0xFFu));
-        X[a] = *(__attribute__((address_space(3))) const Blk*)(b + ((offx >> (8 * a)) & 0xFFu));
-      }
-    } else {
-      typedef __attribute__((address_space(1))) const unsigned char gb;
-      gb* b = (gb*)(nodes);
-      const unsigned n0 = e * (unsigned)sizeof(NODE);
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        E[a] = *(__attribute__((address_space(1))) const Blk*)(b + (n0 + ((offe >> (8 * a)) & 0xFFu)));
-        X[a] = *(__attribute__((address_space(1))) const Blk*)(b + (n0 + ((offx >> (8 * a)) & 0xFFu)));
-      }
-      cc = *(__attribute__((address_space(1))) const u32x2*)(b + (n0 + kCc));
-    }
-    auto pln = [&](const Blk& q, int j) -> float {
-      if constexpr (H) return (float)__builtin_bit_cast(f16x4, q)[j];
-      else return __uint_as_float(q[j]);
-    };
-    unsigned key[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float t0 = fmaxf(fmaxf(fmaf(pln(E[0], j), inv[0], -on[0]), fmaf(pln(E[1], j), inv[1], -on[1])),
-                             fmaxf(fmaf(pln(E[2], j), inv[2], -on[2]), 0.0f));
-      float zt;
-      asm("v_min_f32 %0, %1, %2" : "=v"(zt) : "v"(fmaf(pln(X[2], j), inv[2], -of[2])), "v"(t_hi));
-      const float t1 = fminf(fminf(fmaf(pln(X[0], j), inv[0], -of[0]), fmaf(pln(X[1], j), inv[1], -of[1])), zt);
-      key[j] = t0 <= t1 ? ((__float_as_uint(t0) & ~3u) | (unsigned)j) : ~0u;
-    }
-    n_boxes += 4;
-    auto cx = [&](int a, int b) {
-      const unsigned lo = min(key[a], key[b]), hi = max(key[a], key[b]);
-      key[a] = lo;
-      key[b] = hi;
-    };
-    cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
-    const unsigned long long P = ((unsigned long long)cc.y << 32) | cc.x;
-    auto child = [&](unsigned k) { return (unsigned)(P >> ((k & 3u) << 4)); };
-    if (key[3] != ~0u) lds[(sp++) * kTraceBlock] = (uint16_t)child(key[3]);
-    if (key[2] != ~0u) lds[(sp++) * kTraceBlock] = (uint16_t)child(key[2]);
-    if (key[1] != ~0u) lds[(sp++) * kTraceBlock] = (uint16_t)child(key[1]);
-    e = key[0] != ~0u ? (child(key[0]) & 0xFFFFu) : pop(lds);
-  }
-
-  // one pass of lane_trace_wide's outer loop over the wave; false when no lane of
-  // the wave had a leaf left (every lane done)
-  __device__ __forceinline__ void round(const NODE* nodes, const NODE* top, int n_top, SD sd, V3 o, V3 d, Hit& h,
-                                        uint16_t* lds, unsigned& n_disc, unsigned& n_tests, unsigned& n_boxes) {
-    for (;;) {
-      if (e >= kWideLeaf && e != kWideEmpty && pl == kWideEmpty) { pl = e; e = pop(lds); }
-      if (!__any(e < kWideLeaf && pl == kWideEmpty)) break;
-      if (e < kWideLeaf) visit(nodes, top, n_top, lds, n_boxes);
-    }
-    if (pl != kWideEmpty) {
-      leaf_sphere_test<false>(sd, (int)(pl & 0x7FFFu), o, d, h, n_disc);
-      ++n_tests;
-      t_hi = f32_up(h.t);
-      pl = kWideEmpty;
-    }
-  }
-};
-
 // Per-lane traversal over the pair layout (LANE == 14): the block's LDS copy
 // of each binary node stores, per axis, the two children's lower bounds as
 // one 8-B pair and their upper bounds as the next pair (lo0 lo1 hi0 hi1 per
@@ -1136,20 +1004,5 @@ typedef double f64x2 __attribute__((ext_vector_type(2)));
 // non-temporal and leave the L2 to the scene (C3 0.947 -> 0.929 ms, C5 60.0
 // -> 58.8 ms per frame). The same marking in wf_combine_parents cost 2 %.
 __device__ __forceinline__ void st_d(double* p, double v) { __builtin_nontemporal_store(v, p); }
-// a split generation's hit record (wf_walk -> the shading launch), streamed like the rays
-__device__ __forceinline__ void st_hit(WfHit* p, const Hit& h) {
-  typedef int i32x2 __attribute__((ext_vector_type(2)));
-  __builtin_nontemporal_store(h.t, &p->t);
-  const i32x2 k0 = {h.key, h.c1k}, k1 = {h.c2k, h.hin};
-  __builtin_nontemporal_store(k0, (i32x2*)&p->key);
-  __builtin_nontemporal_store(k1, (i32x2*)&p->c2k);
-}
-__device__ __forceinline__ void ld_hit(const WfHit* p, Hit& h) {
-  typedef int i32x2 __attribute__((ext_vector_type(2)));
-  h.t = __builtin_nontemporal_load(&p->t);
-  const i32x2 k0 = __builtin_nontemporal_load((const i32x2*)&p->key);
-  const i32x2 k1 = __builtin_nontemporal_load((const i32x2*)&p->c2k);
-  h.key = k0.x; h.c1k = k0.y; h.c2k = k1.x; h.hin = k1.y;
-}
 
 }  // namespace rtamd

@@ -41,8 +41,7 @@ int wf_tuning_apply(WfTuning& t, const char* key, int value) {
       {"lds_wide", &WfTuning::lds_wide, 0, 1},
       {"d2h", &WfTuning::d2h, 0, 1},               {"bands", &WfTuning::bands, 1, 4},
       {"band_pct", &WfTuning::band_pct, 5, 95},   {"band_gen", &WfTuning::band_gen, -1, 8},
-      {"band_ratio", &WfTuning::band_ratio, 30, 100}, {"multi_gather", &WfTuning::multi_gather, 0, 1},
-      {"split", &WfTuning::split, 0, 1},           {"refill", &WfTuning::refill, 1, 64}};
+      {"band_ratio", &WfTuning::band_ratio, 30, 100}, {"multi_gather", &WfTuning::multi_gather, 0, 1}};
   if (!key) return 0;
   for (const Knob& k : knobs) {
     if (std::strcmp(key, k.name) != 0) continue;
@@ -67,7 +66,6 @@ Wavefront::~Wavefront() {
     (void)hipFree(g.shadow_nodes); (void)hipFree(g.geo); (void)hipFree(g.surf);
   }
   (void)hipFree(colors_); (void)hipFree(parents_); (void)hipFree(rays_[0]); (void)hipFree(rays_[1]);
-  (void)hipFree(whits_);
   if (d_gtab_) (void)hipFree(d_gtab_);
   if (d_gsh_) (void)hipFree(d_gsh_);
   if (d_cnt_) (void)hipFree(d_cnt_);
@@ -340,26 +338,6 @@ static hipError_t launch_lds(K kern, size_t lds, unsigned n, hipStream_t stream,
   return hipGetLastError();
 }
 
-// a split generation's two launches (walk, then shading); while the class is timed the
-// walk carries the start event and the shading the stop event
-template <typename KW, typename KS>
-static hipError_t launch_split(KW walk, KS shade, size_t lds_w, size_t lds_s, unsigned n, hipStream_t stream,
-                               const DevScene& sc, const DevCamera& cam, const WfArgs& aw, const WfArgs& as,
-                               int block) {
-  if (lds_w > 0) WF_CHECK(hipFuncSetAttribute((const void*)walk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_w));
-  if (lds_s > 0) WF_CHECK(hipFuncSetAttribute((const void*)shade, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_s));
-  const dim3 gw(occupancy_grid(walk, block, lds_w, n)), gs(occupancy_grid(shade, block, lds_s, n));
-  if (t_ev_start) {
-    hipExtLaunchKernelGGL(walk, gw, dim3(block), lds_w, stream, t_ev_start, nullptr, 0, sc, cam, aw);
-    hipExtLaunchKernelGGL(shade, gs, dim3(block), lds_s, stream, nullptr, t_ev_stop, 0, sc, cam, as);
-    ++t_ev_used;
-  } else {
-    hipLaunchKernelGGL(walk, gw, dim3(block), lds_w, stream, sc, cam, aw);
-    hipLaunchKernelGGL(shade, gs, dim3(block), lds_s, stream, sc, cam, as);
-  }
-  return hipGetLastError();
-}
-
 // ---- the exhaustive pipeline (counted launches: the reference's every-shape loop)
 template <bool QUADS>
 static hipError_t launch_closest_exh(const DevScene& sc, const DevCamera& cam, const WfArgs& a, bool primary,
@@ -425,16 +403,6 @@ static hipError_t launch_fused_q(const DevScene& sc, const DevCamera& cam, WfArg
   if (tn.image == 0 && wide_lds) {
     // the four-wide hierarchy and the 48-B sphere records in LDS, with the light buffer's distances
     dyn = wide_lds_bytes(sc);
-    if (!TALLY && tn.split && a.hits) {
-      // split generation: the walk launch (no distances: it traces no shadow ray), then the shading
-      WfArgs aw = a;
-      const size_t dyn_w = dyn;
-      if (dl) { a.lds_flags |= kLdsDeltas; dyn += dl; }
-      return cam_rays ? launch_split(wf_walk<QUADS, true>, wf_trace_fused<false, QUADS, 15, false, true, true>, dyn_w,
-                                     dyn, n, stream, sc, cam, aw, a, tb)
-                      : launch_split(wf_walk<QUADS, false>, wf_trace_fused<false, QUADS, 15, false, false, true>,
-                                     dyn_w, dyn, n, stream, sc, cam, aw, a, tb);
-    }
     if (dl) { a.lds_flags |= kLdsDeltas; dyn += dl; }
     return cam_rays ? launch_lds(wf_trace_fused<false, QUADS, 15, TALLY, true>, dyn, n, stream, sc, cam, a, tb)
                     : launch_lds(wf_trace_fused<false, QUADS, 15, TALLY, false>, dyn, n, stream, sc, cam, a, tb);
@@ -629,20 +597,8 @@ hipError_t Wavefront::render_fast(const DevScene& sc, const DevCamera& cam, bool
   if (!camera_mode)  // batch rays: n0 x 6 doubles -> generation 0's ray buffer
     WF_CHECK(hipMemcpy2DAsync(rays_[0], sizeof(WfRay), d_in_rays, 6 * sizeof(double), 6 * sizeof(double), n0,
                               hipMemcpyDeviceToDevice, stream));
-  if (tn.split) {  // the split generations' hit records: one per ray slot of any generation
-    const unsigned long long need = std::max<unsigned long long>(n0, ray_cap_);
-    if (whit_cap_ < need) {
-      (void)hipFree(whits_);
-      whits_ = nullptr;
-      whit_cap_ = 0;
-      WF_CHECK(hipMalloc(&whits_, need * sizeof(WfHit)));
-      whit_cap_ = need;
-    }
-  }
   WfArgs a{};
   a.dev_sized = 1;
-  a.hits = tn.split ? whits_ : nullptr;
-  a.refill = (unsigned)tn.refill;
   a.colors_direct = averaged ? 0u : 1u;
   a.gtab = d_gtab_;
   a.gsh = d_gsh_;

@@ -111,9 +111,6 @@ struct WfTuning {
   int band_pct = 35;       // ... the first band's share of the rows (percent)
   int band_ratio = 100;    // ... each later band's size, percent of the one before (100: equal shares)
   int band_gen = 1;        // ... band k+1 starts when band k's generation band_gen has run (-1: its whole render)
-  int split = 0;           // fast path, LANE 15's LDS image: each generation as a walk launch whose lanes take the next
-                           //     ray when theirs is done (wf_walk), then a shading launch
-  int refill = 16;         // ... a wave's idle lanes take new rays once at least this many are idle
   int multi_gather = 0;    // rt_render_multi (scenes[0]'s knob): 1 = every shard gathered into device 0 by one grouped
                            //     ncclGather, then copied out of device 0 (test hook; 0 = each device copies its rows
                            //     straight into the host canvas, rt_multi.cpp)
@@ -307,7 +304,6 @@ struct WfArgs {
   ParentRec* par_base;
   unsigned long long color_cap, par_cap, ray_cap;  // colour slots, parent records, ray slots per buffer
   WfHostRec* hrec;                  // device address of the workspace's host-mapped record
-  unsigned refill;                  // split generations (wf_walk): refill a wave's lanes once this many are idle
 };
 
 // Per-kernel-class timing of the last frame (profiling mode only).
@@ -400,8 +396,6 @@ class Wavefront {
   ParentRec* parents_ = nullptr;
   WfRay* rays_[2] = {nullptr, nullptr};
   unsigned long long color_cap_ = 0, par_cap_ = 0, ray_cap_ = 0;
-  WfHit* whits_ = nullptr;  // split generations: each ray's hit (wf_walk -> the shading launch)
-  unsigned long long whit_cap_ = 0;
   int squeezed_pct_ = 100;  // the arena_pct the arenas were last shrunk to
   WfGenTab* d_gtab_ = nullptr;
   unsigned* d_gsh_ = nullptr;

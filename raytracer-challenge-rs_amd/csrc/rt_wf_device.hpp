@@ -764,10 +764,7 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
 // per-visit and per-test counting and the wave-end atomics altogether: C3
 // 1.021 -> 0.964 ms/frame, an 8-way shard 0.204 -> 0.184 ms.
 // CAM: the launch may read camera rays (generation 0 of a camera render).
-// SPLIT: the shading launch of a split generation (WfTuning::split): the
-// generation's walk launch (wf_walk) has found every ray's hit and left it in
-// a.hits[slot]; this launch reads it instead of walking.
-template <bool PRIMARY, bool QUADS, int LANE, bool TALLY, bool CAM = PRIMARY, bool SPLIT = false>
+template <bool PRIMARY, bool QUADS, int LANE, bool TALLY, bool CAM = PRIMARY>
 __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, DevCamera cam, WfArgs a) {
   __shared__ int stack_lds[LANE == 3 ? kLaneLdsDepth * kTraceBlock
                            : LANE == 0 ? (kTraceBlock / 64) * (kBvhMaxDepth + 4) : 1];
@@ -818,13 +815,6 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
   // the chunk's rays, traversed: o, d and the hit of ray i (slot) of chunk c
   auto traverse = [&](unsigned i, bool valid, unsigned slot, V3& o, V3& d, Hit& h) {
     hit_init(h);
-    if constexpr (SPLIT) {
-      if (valid) {
-        wf_ray<CAM>(a, cam, slot, o, d);
-        ld_hit(a.hits + slot, h);
-      }
-      return;
-    }
     if (valid) {
       wf_ray<CAM>(a, cam, slot, o, d);
       if constexpr (TALLY && QUADS) count_hier_gates(sc, o, d, t.gsk);
@@ -899,107 +889,6 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
     }
   }
 }
-
-// The walk launch of a split generation (WfTuning::split, LANE 15's LDS image):
-// closest hits only. A fused launch's wave walks 64 rays at a time and waits
-// for the slowest of them before it shades; here a lane whose walk is done
-// writes its hit (a.hits[slot], read by the generation's shading launch,
-// wf_trace_fused<..., SPLIT>) and takes the generation's next ray as soon as
-// a.refill lanes of its wave are idle, so the lanes keep walking until the
-// generation runs out of rays. Rays come from the chunks of the fused
-// launches' distribution (a wave's first chunk by its index, the rest from its
-// block class's counter, on the second half of that counter's line: the
-// shading launch uses the first). Every ray's walk is lane_trace_wide's
-// (WideWalk), so every hit is the same bit for bit.
-template <bool QUADS, bool CAM>
-__global__ __launch_bounds__(kTraceBlock, 4) void wf_walk(DevScene sc, DevCamera cam, WfArgs a) {
-  __shared__ int stack_lds[1];
-  extern __shared__ __attribute__((aligned(16))) unsigned char lane_dyn[];
-  __shared__ unsigned s_pre[kPreRays];
-  const unsigned* pre = shard_prefix<true>(a.in_cnt, s_pre);
-  if (a.dev_sized) bind_generation(a, pre);
-  if (blockIdx.x * (blockDim.x / 64u) >= (a.n + 63u) / 64u) return;  // (block-uniform)
-  const LaneScene ls = lane_scene<15>(sc, a.lds_flags, a.n_top, stack_lds, lane_dyn);
-  unsigned n_disc = 0, n_tests = 0, n_boxes = 0;  // (untallied: the split serves the timed frames)
-  GateSkips gsk;
-  const unsigned n_chunks = (a.n + 63u) / 64u;
-  const unsigned waves_per_block = blockDim.x / 64u;
-  const unsigned W = gridDim.x * waves_per_block;
-  const unsigned X = gridDim.x < (unsigned)kChunkClasses ? gridDim.x : (unsigned)kChunkClasses;
-  const unsigned cls = blockIdx.x % X;
-  unsigned* ctr = a.cnt->chunk + ((size_t)a.g * kChunkClasses + cls) * kChunkStride + kChunkStride / 2;
-  const unsigned lane = lane_id();
-  // the wave's unassigned rays [base, end) (wave-uniform); `more`: the counter may hold more chunks
-  const unsigned c0 = blockIdx.x * waves_per_block + threadIdx.x / 64u;
-  unsigned base = c0 * 64u, end = c0 < n_chunks ? min(base + 64u, a.n) : base;
-  bool more = true;
-  bool live = false;
-  unsigned slot = 0;
-  V3 o = v3(0, 0, 0), d = v3(0, 0, 0);
-  Hit h;
-  hit_init(h);
-  WideWalk<> w;
-  w.e = kWideEmpty;
-  w.pl = kWideEmpty;
-  w.sp = 0;
-  for (;;) {
-    unsigned long long idle = __ballot(!live);
-    const unsigned n_idle = (unsigned)__popcll(idle);
-    if ((more || base < end) && (n_idle >= a.refill || n_idle == 64u)) {
-      bool fresh = false;
-      while (idle) {  // serve the idle lanes in lane order (wave-uniform loop)
-        if (base >= end) {
-          if (!more) break;
-          unsigned k = 0;
-          if (lane == 0) k = atomicAdd(ctr, 1u);
-          const unsigned cn = W + cls + X * (unsigned)__shfl((int)k, 0, 64);
-          if (cn >= n_chunks) {
-            more = false;
-            break;
-          }
-          base = cn * 64u;
-          end = min(base + 64u, a.n);
-        }
-        const bool me = (idle >> lane) & 1ull;
-        const unsigned rank = (unsigned)__popcll(idle & ((1ull << lane) - 1ull));
-        const unsigned take = min((unsigned)__popcll(idle), end - base);
-        if (me && rank < take) {
-          const unsigned i = base + rank;
-          // a batch's generation 0: the padding slots after each frame's root rays hold no ray
-          if (a.g != 0 || a.n_frames <= 1 || i % a.frame_rays < a.frame_real) {
-            slot = shard_slot<true>(pre, a.in_cap, i);
-            live = true;
-            fresh = true;
-          }
-        }
-        base += take;
-        idle = __ballot(me && rank >= take);
-      }
-      if (fresh) {
-        wf_ray<CAM>(a, cam, slot, o, d);
-        hit_init(h);
-        // planes and the other records first: an early nearest hit tightens the culling
-        trace_rest<false, QUADS, true>(sc, o, d, h, n_disc, &gsk);
-        if constexpr (QUADS) {
-          other_trace<false>(sc, o, d, 0.0, h, n_disc, n_tests, n_boxes);
-          line_trace<false>(sc, o, d, 0.0, h, n_tests, n_boxes);
-        }
-        w.init(true, ls.M, sc.bvhw != nullptr, o, d, h, ls.s48, sc.n_diag, n_disc, n_tests);
-      }
-    }
-    if (!__any(live)) {
-      if (!more && base >= end) break;
-      continue;
-    }
-    w.round((const BvhWide*)ls.nodes, ls.wtop, ls.n_top, ls.s48, o, d, h, ls.stack16, n_disc, n_tests, n_boxes);
-    if (live && w.done()) {
-      hit_finish(h);
-      st_hit(a.hits + slot, h);
-      live = false;
-    }
-  }
-}
-
 
 // ---- the frame's other kernels (rt_wf_combine.hip), launched by rt_wavefront.hip
 __global__ void wf_frame_init(DevScene sc, DevCamera cam, PrimRec* prim, unsigned do_prim, uint4* zero_a,
