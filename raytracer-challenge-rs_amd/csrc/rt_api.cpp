@@ -4,6 +4,7 @@
 // tuning knobs, plain streams). Scene creation is rt_scene.cpp, the renders
 // rt_render.cpp, multi-GPU rt_multi.cpp (rt_api_internal.hpp lists them).
 #include "rt_api_internal.hpp"
+#include "rt_pow.hpp"
 
 namespace rtapi {
 
@@ -194,7 +195,7 @@ void* rt_host_buffer_alloc(size_t bytes) {
         return b.first;
       }
     void* p = nullptr;
-    if (hipHostMalloc(&p, bytes, hipHostMallocPortable) != hipSuccess || !p) {
+    if (hipHostMalloc(&p, bytes, hipHostMallocPortable | hipHostMallocMapped) != hipSuccess || !p) {
       (void)hipGetLastError();
       g_err = "rt_host_buffer_alloc: hipHostMalloc failed";
       return nullptr;
@@ -305,6 +306,22 @@ uint32_t rt_pattern_rows(uint32_t vsize, uint32_t row_block, uint32_t period, ui
   for (uint64_t blk = 0; blk * row_block < vsize; ++blk)
     if ((mask >> (blk % period)) & 1u) rows += std::min<uint32_t>(row_block, vsize - (uint32_t)(blk * row_block));
   return rows;
+}
+
+// Development/test hooks (not in the public ABI): the specular term's pow
+// (rt_pow.hpp, glibc 2.35's algorithm) for n pairs, on the host (the same
+// source compiled for the CPU; tests/test_pow.py) and on the device (device
+// buffers, stream-ordered then synchronised; tests/test_gpu_pow.py).
+void rtamd_pow_host(const double* x, const double* y, size_t n, double* out) {
+  for (size_t i = 0; i < n; ++i) out[i] = rtamd::pow_glibc(x[i], y[i]);
+}
+int rtamd_pow_device(const double* d_x, const double* d_y, size_t n, double* d_out, void* stream) {
+  return guarded([&]() -> int {
+  if (n >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "batch too large");
+  RT_HIP(launch_pow(d_x, d_y, (int)n, d_out, (hipStream_t)stream));
+  RT_HIP(hipStreamSynchronize((hipStream_t)stream));
+  return RT_OK;
+  });
 }
 
 }  // extern "C"

@@ -145,9 +145,7 @@ struct rt_scene {
     // events that start each band when the previous band's render is done
     hipStream_t band_stream[kMaxBands - 1] = {};
     hipEvent_t band_ev[kMaxBands] = {};
-    // banded rt_render_ppm: each band's text length (pinned words) and the events behind them
-    unsigned long long* h_len = nullptr;
-    hipEvent_t len_ev[kMaxBands] = {};
+    unsigned long long* h_len = nullptr;  // rt_render_ppm: the text's length (a pinned word)
     bool busy = false;
   };
   std::deque<HostCtx> ctxs;  // deque: a context's address survives the pool's growth
@@ -226,8 +224,6 @@ struct rt_scene {
         }
       for (hipEvent_t be : c.band_ev)
         if (be) (void)hipEventDestroy(be);
-      for (hipEvent_t le : c.len_ev)
-        if (le) (void)hipEventDestroy(le);
       if (c.h_len) (void)hipHostFree(c.h_len);
     }
   }
@@ -308,10 +304,6 @@ void add_stats(DevStats& sum, const DevStats& ds);
 // pinned) for the whole call. RT_ERR_NO_DEVICE: not bandable (render it whole).
 int render_banded(rt_scene* s, std::unique_lock<std::mutex>& lk, rt_scene::HostCtx* c, const rt_camera_desc& cam,
                   uint32_t max_depth, uint32_t aa, double* out_rgb, bool host_ready = false);
-// canvas_to_ppm(&camera.render(&world)) in the same bands, each band's text copied
-// behind the later bands' renders. RT_ERR_NO_DEVICE: render it whole.
-int render_ppm_banded(rt_scene* s, std::unique_lock<std::mutex>& lk, rt_scene::HostCtx* c, const rt_camera_desc& cam,
-                      uint32_t max_depth, uint32_t aa, char* out, size_t cap, size_t* out_len);
 // the fast path can serve `s` (a hierarchy to cull with, not switched off)
 inline bool fast_path(const rt_scene* s) {
   return s->tune.accel != 0 && (s->dev.n_bvh > 0 || s->dev.n_obvh > 0 || s->dev.n_lbvh > 0);

@@ -9,6 +9,7 @@
 #include <stdint.h>
 
 #include "rt_layout.hpp"
+#include "rt_pow.hpp"
 
 #pragma clang fp contract(off)
 
@@ -505,10 +506,12 @@ __device__ __forceinline__ V3 pattern_color(const ShadeRec& s, V3 world_point) {
   }
 }
 
-// f64::powf of the specular term (OCML pow). Out of line: inlined into the
-// fused trace kernels, its polynomial constants were hoisted out of the ray
-// loop into VGPRs and spilled across the BVH traversal.
-__device__ __attribute__((noinline)) double spec_pow(double x, double y) { return pow(x, y); }
+// f64::powf of the specular term (material.rs:76): glibc 2.35's pow, operation
+// for operation (rt_pow.hpp), so the colours are the reference host's bit for
+// bit (OCML's pow differed by 1-2 ulps in about 1 of 4000 channels, round 5).
+// Out of line: inlined into the fused trace kernels, its constants were hoisted
+// out of the ray loop into VGPRs and spilled across the BVH traversal.
+__device__ __attribute__((noinline)) double spec_pow(double x, double y) { return pow_glibc(x, y); }
 
 // Material::lighting (material.rs:38-82)
 // `lightv` = (light.position - point).normalize(), which the caller may

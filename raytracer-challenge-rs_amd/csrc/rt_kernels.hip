@@ -71,4 +71,16 @@ hipError_t launch_shadow(const DevScene& sc, const double* d_pts, int n, int lig
   return hipGetLastError();
 }
 
+// Development/test hook: the specular term's pow (rt_pow.hpp) for a batch on the
+// device (tests/test_gpu_pow.py compares it with the host's glibc pow).
+__global__ void pow_batch(const double* x, const double* y, int n, double* out) {
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i < n) out[i] = spec_pow(x[i], y[i]);
+}
+hipError_t launch_pow(const double* d_x, const double* d_y, int n, double* d_out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(pow_batch, dim3((n + 255) / 256), dim3(256), 0, s, d_x, d_y, n, d_out);
+  return hipGetLastError();
+}
+
 }  // namespace rtamd

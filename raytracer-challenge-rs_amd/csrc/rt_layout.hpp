@@ -247,6 +247,7 @@ struct DevScene {
   const QuadRec* lrec;          // in lbvh leaf order
   const ConeCluster* lclus;     // the cones' clusters (cone_prepass)
   const int32_t* lcone;         // cluster members: indices into lrec
+  const int32_t* lrec_clus;     // per line record: its cone's cluster (-1: an open tube)
   int32_t n_lbvh, n_lrec, n_lclus;
   const SphereGen* fx_gen;  // general spheres outside the hierarchies
   const QuadRec* fx_quads;  // cubes / cylinders / cones outside the hierarchies

@@ -159,6 +159,7 @@ __global__ __launch_bounds__(kPpmBlock) void ppm_row_write(const double* rgb, un
 
 size_t ppm_device_max_width() { return kPpmMaxWidth; }
 
+
 hipError_t ppm_encode_device(const double* d_rgb, uint32_t W, uint32_t H, char* d_out, unsigned long long cap,
                              unsigned* d_row_len, unsigned long long* d_row_off, const PpmHeader& hdr,
                              hipStream_t stream) {

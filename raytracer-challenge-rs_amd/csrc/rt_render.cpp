@@ -137,7 +137,7 @@ int rt_render_block_pattern_device(const rt_scene* scene, const rt_camera_desc* 
 
 namespace rtapi {
 namespace {
-// The row bands of a banded host render (render_banded, render_ppm_banded):
+// The row bands of a banded host render (render_banded):
 // the frame's rows in nb <= 64 blocks of rb rows (one period of
 // rt_render_block_pattern_device's mapping over the whole canvas), cut into
 // `bands` contiguous runs of blocks. The first band takes band_pct of the rows,
@@ -182,7 +182,7 @@ bool plan_bands(const rt_scene* s, uint32_t H, BandPlan& p) {
 // workspace, pinned to the call), starting when band k-1's render is done (or
 // band_gen >= 0: when its generation band_gen has been launched), so the GPU
 // works on one band at a time as in a whole-frame render while each band's
-// follow-up work (a copy, an encoder) runs behind the later bands. Band k's
+// copy to the host runs behind the later bands. Band k's
 // rows go to d_out + y0[k] rows. On destruction every stream that received
 // work drains first, then the workspaces are unpinned (under the scene's lock):
 // no kernel or copy outlives the call.
@@ -325,79 +325,6 @@ int render_banded(rt_scene* s, std::unique_lock<std::mutex>& lk, rt_scene::HostC
   return RT_OK;
 }
 
-// canvas_to_ppm(&camera.render(&world)) in bands (rt_render_ppm; DESIGN.md
-// §5.6): band k renders (BandRender), the device encoder turns its rows into
-// text in a region of its own (at the byte bound of everything before it: 12
-// bytes per pixel, the header first), and a pinned word receives the band's
-// text length behind the encoder. The host waits for each band's length in
-// turn and copies the band's text to its place in `out` on the band's stream,
-// while the later bands still render; only the last band's encoder and copy
-// follow the last render. `*out_len` = the whole text's length; the text is
-// the whole-frame encoder's byte for byte (row lengths and breaks are per
-// row). RT_ERR_NO_DEVICE: not bandable, or a band overflowed its arenas (the
-// caller renders the frame whole, which re-renders until it fits).
-int render_ppm_banded(rt_scene* s, std::unique_lock<std::mutex>& lk, rt_scene::HostCtx* c, const rt_camera_desc& cam,
-                      uint32_t max_depth, uint32_t aa, char* out, size_t cap, size_t* out_len) {
-  const uint32_t W = cam.hsize, H = cam.vsize;
-  BandPlan p;
-  if (!plan_bands(s, H, p)) return RT_ERR_NO_DEVICE;
-  if (!c->h_len) RT_HIP(hipHostMalloc((void**)&c->h_len, kMaxBands * sizeof(unsigned long long), hipHostMallocDefault));
-  for (int k = 0; k < p.bands; ++k)
-    if (!c->len_ev[k]) RT_HIP(hipEventCreateWithFlags(&c->len_ev[k], hipEventDisableTiming));
-  const PpmHeader hd = ppm_header(W, H), none{};
-  bool registered = false;
-  if (out && !pinned_block(out, cap)) {
-    if (hipHostRegister(out, cap, hipHostRegisterDefault) != hipSuccess) {
-      (void)hipGetLastError();
-      return RT_ERR_NO_DEVICE;  // (the one-render path copies through its staging chunks)
-    }
-    registered = true;
-  }
-  struct Unregister {
-    void* p;
-    bool on;
-    ~Unregister() {
-      if (on && hipHostUnregister(p) != hipSuccess) (void)hipGetLastError();
-    }
-  } unreg{out, registered};
-  BandRender br(s, lk, c, p);
-  int rc = br.open();
-  if (rc != RT_OK) return rc;
-  const DevCamera dc = to_dev_camera(cam);
-  unsigned* d_len = (unsigned*)c->d_ppm_rows;
-  unsigned long long* d_off = (unsigned long long*)(((uintptr_t)c->d_ppm_rows + (size_t)H * 4 + 7) & ~(uintptr_t)7);
-  auto text_at = [&](int k) { return (size_t)(k == 0 ? 0 : hd.n) + (size_t)12 * W * p.y0[k]; };
-  for (int k = 0; k < p.bands; ++k) {
-    if ((rc = br.render(k, dc, W, aa, max_depth)) != RT_OK) return rc;
-    const uint32_t rows = p.y0[k + 1] - p.y0[k];
-    unsigned long long* off_k = d_off + p.y0[k] + k;  // rows + 1 offsets per band
-    RT_HIP(ppm_encode_device(c->d_out + (size_t)p.y0[k] * W * 3, W, rows, c->d_ppm + text_at(k),
-                             c->ppm_cap - text_at(k), d_len + p.y0[k], off_k, k == 0 ? hd : none, br.st[k]));
-    RT_HIP(hipMemcpyAsync(c->h_len + k, off_k + rows, sizeof(unsigned long long), hipMemcpyDeviceToHost, br.st[k]));
-    RT_HIP(hipEventRecord(c->len_ev[k], br.st[k]));
-  }
-  lk.unlock();  // (the context and the workspaces are this call's)
-  size_t at = 0;
-  for (int k = 0; k < p.bands; ++k) {
-    RT_HIP(hipEventSynchronize(c->len_ev[k]));
-    const size_t len = (size_t)(k == 0 ? hd.n : 0u) + (size_t)c->h_len[k];
-    if (out && at + len <= cap)
-      RT_HIP(hipMemcpyAsync(out + at, c->d_ppm + text_at(k), len, hipMemcpyDeviceToHost, br.st[k]));
-    at += len;
-  }
-  lk.lock();
-  if ((rc = br.wait_all()) != RT_OK) return rc;
-  bool any_over = false;
-  for (int k = 0; k < p.bands; ++k) {
-    bool over = false;
-    if ((rc = br.overflowed(k, &over)) != RT_OK) return rc;
-    any_over = any_over || over;
-  }
-  if (any_over) return RT_ERR_NO_DEVICE;  // (a band's rows were poisoned: the whole-frame path renders it again)
-  *out_len = at;
-  if (out && cap < at) return fail(RT_ERR_BUFFER_TOO_SMALL, "PPM buffer too small");
-  return RT_OK;
-}
 }  // namespace rtapi
 
 extern "C" {
@@ -479,29 +406,64 @@ int rt_render_ppm(const rt_scene* scene, const rt_camera_desc* camera, uint32_t 
     if (c->d_ppm_rows) (void)hipFree(c->d_ppm_rows);
     c->d_ppm_rows = nullptr;
     c->ppm_rows_cap = 0;
-    // row lengths, then the row offsets (H + 1; in bands, rows + 1 per band)
-    RT_HIP(hipMalloc(&c->d_ppm_rows, (size_t)H * 4 + ((size_t)H + kMaxBands + 1) * 8 + 8));
+    RT_HIP(hipMalloc(&c->d_ppm_rows, (size_t)H * 4 + ((size_t)H + 1) * 8 + 8));  // row lengths, row offsets
     c->ppm_rows_cap = H;
   }
   unsigned long long* d_off = (unsigned long long*)(((uintptr_t)c->d_ppm_rows + (size_t)H * 4 + 7) & ~(uintptr_t)7);
-  // a large frame without counters: bands, each band's text copied behind the later bands' renders
-  if (!stats && s->tune.bands > 1 && fast_path(s) && n_pix * aa_samples >= ((uint64_t)1 << 20)) {
-    rc = render_ppm_banded(s, lk, c, *camera, max_depth, aa_samples, out, cap, out_len);
-    if (rc != RT_ERR_NO_DEVICE) return rc;  // (not bandable, or a band overflowed: render it whole below)
-  }
+  if (!c->h_len) RT_HIP(hipHostMalloc((void**)&c->h_len, sizeof(unsigned long long), hipHostMallocDefault));
+  struct Drain {  // no kernel or copy of this call outlives it (the context goes back to the pool)
+    hipStream_t st;
+    ~Drain() {
+      if (hipStreamSynchronize(st) != hipSuccess) (void)hipGetLastError();
+    }
+  } drain{c->stream};
   DevStats ds{};
   float ms = 0.f;
-  rc = run_render(s, to_dev_camera(*camera), nullptr, (uint32_t)(n_pix * aa_samples), aa_samples, max_depth, H, 0,
-                  1, c->d_out, c->stream, stats ? &ds : nullptr, stats ? &ms : nullptr, 0, nullptr, nullptr, 1, true,
-                  &lk);
+  const DevCamera dc = to_dev_camera(*camera);
+  const uint32_t n_tasks = (uint32_t)(n_pix * aa_samples);
+  // The render, the encoder and the text's length in one pass of the stream: the host waits
+  // once, then reads the workspace's overflow record; a frame that outgrew its arenas is
+  // rendered again synchronously (with stats the render is synchronous anyway).
+  rt_scene::WfSlot* used = nullptr;
+  struct Unpin {
+    rt_scene::WfSlot*& w;
+    std::unique_lock<std::mutex>& lk;
+    ~Unpin() {
+      if (!w) return;
+      if (!lk.owns_lock()) lk.lock();
+      --w->pins;
+    }
+  } unpin{used, lk};
+  rc = run_render(s, dc, nullptr, n_tasks, aa_samples, max_depth, H, 0, 1, c->d_out, c->stream, stats ? &ds : nullptr,
+                  stats ? &ms : nullptr, 0, stats ? nullptr : &used, nullptr, 1, stats != nullptr, &lk, false,
+                  stats == nullptr);
   if (rc != RT_OK) return rc;
+  auto encode = [&]() -> int {
+    RT_HIP(ppm_encode_device(c->d_out, W, H, c->d_ppm, c->ppm_cap, (unsigned*)c->d_ppm_rows, d_off, hd, c->stream));
+    RT_HIP(hipMemcpyAsync(c->h_len, d_off + H, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    lk.unlock();
+    const hipError_t e = hipStreamSynchronize(c->stream);
+    lk.lock();
+    if (e != hipSuccess) return fail(RT_ERR_HIP, std::string("rt_render_ppm: ") + hipGetErrorString(e));
+    return RT_OK;
+  };
+  if ((rc = encode()) != RT_OK) return rc;
+  if (used) {
+    used->wf->learn(s->sizing);
+    bool over = false;
+    RT_HIP(used->wf->take_overflow(&over));
+    --used->pins;
+    used = nullptr;
+    if (over) {  // (the canvas was poisoned: render it again, growing the arenas until it fits)
+      rc = run_render(s, dc, nullptr, n_tasks, aa_samples, max_depth, H, 0, 1, c->d_out, c->stream, nullptr, nullptr,
+                      0, nullptr, nullptr, 1, true, &lk);
+      if (rc != RT_OK) return rc;
+      if ((rc = encode()) != RT_OK) return rc;
+    }
+  }
   const int d2h = s->tune.d2h;
   lk.unlock();
-  RT_HIP(ppm_encode_device(c->d_out, W, H, c->d_ppm, c->ppm_cap, (unsigned*)c->d_ppm_rows, d_off, hd, c->stream));
-  unsigned long long body = 0;
-  RT_HIP(hipMemcpyAsync(&body, d_off + H, sizeof body, hipMemcpyDeviceToHost, c->stream));
-  RT_HIP(hipStreamSynchronize(c->stream));
-  *out_len = hd.n + (size_t)body;
+  *out_len = hd.n + (size_t)*c->h_len;
   if (out) {
     if (cap < *out_len) return fail(RT_ERR_BUFFER_TOO_SMALL, "PPM buffer too small");
     if ((rc = copy_to_host(c, d2h, out, c->d_ppm, *out_len, c->stream)) != RT_OK) return rc;

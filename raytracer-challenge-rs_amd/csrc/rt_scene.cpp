@@ -235,6 +235,9 @@ int rt_scene_create_groups(const rt_shape_desc* shapes, size_t n_shapes, const i
     lclus.clear();
     lcone.clear();
   }
+  std::vector<int32_t> lrec_clus(line_rec.size(), -1);  // each cone's cluster (line_trace's pre-pass check)
+  for (size_t c = 0; c < lclus.size(); ++c)
+    for (int32_t j = lclus[c].first; j < lclus[c].first + lclus[c].count; ++j) lrec_clus[(size_t)lcone[(size_t)j]] = (int32_t)c;
   if (obvh.empty()) {  // (only when there are no records, or more than the leaf codes can index)
     for (const OtherRec& r : orec) {
       if (r.kind == 0) {
@@ -275,7 +278,8 @@ int rt_scene_create_groups(const rt_shape_desc* shapes, size_t n_shapes, const i
   const size_t o_lr = align(o_lb + (lbvh.size() + 1) * sizeof(BvhNode));
   const size_t o_cc = align(o_lr + (line_rec.size() + 1) * sizeof(QuadRec));
   const size_t o_lm = align(o_cc + (lclus.size() + 1) * sizeof(ConeCluster));
-  const size_t o_fg = align(o_lm + (lcone.size() + 1) * sizeof(int32_t));
+  const size_t o_lk = align(o_lm + (lcone.size() + 1) * sizeof(int32_t));
+  const size_t o_fg = align(o_lk + (lrec_clus.size() + 1) * sizeof(int32_t));
   const size_t o_fq = align(o_fg + (fx_gen.size() + 1) * sizeof(SphereGen));
   const size_t o_sh = align(o_fq + (fx_quads.size() + 1) * sizeof(QuadRec));
   const size_t o_rt = align(o_sh + shade.size() * sizeof(ShadeRec));
@@ -300,6 +304,7 @@ int rt_scene_create_groups(const rt_shape_desc* shapes, size_t n_shapes, const i
   if (!lbvh.empty()) std::memcpy(&host[o_lb], lbvh.data(), lbvh.size() * sizeof(BvhNode));
   if (!lclus.empty()) std::memcpy(&host[o_cc], lclus.data(), lclus.size() * sizeof(ConeCluster));
   if (!lcone.empty()) std::memcpy(&host[o_lm], lcone.data(), lcone.size() * sizeof(int32_t));
+  if (!lrec_clus.empty()) std::memcpy(&host[o_lk], lrec_clus.data(), lrec_clus.size() * sizeof(int32_t));
   if (!line_rec.empty()) std::memcpy(&host[o_lr], line_rec.data(), line_rec.size() * sizeof(QuadRec));
   if (!fx_gen.empty()) std::memcpy(&host[o_fg], fx_gen.data(), fx_gen.size() * sizeof(SphereGen));
   if (!fx_quads.empty()) std::memcpy(&host[o_fq], fx_quads.data(), fx_quads.size() * sizeof(QuadRec));
@@ -361,6 +366,7 @@ int rt_scene_create_groups(const rt_shape_desc* shapes, size_t n_shapes, const i
   s->dev.lbvh = lbvh.empty() ? nullptr : (const BvhNode*)(b + o_lb);
   s->dev.lclus = (const ConeCluster*)(b + o_cc);
   s->dev.lcone = (const int32_t*)(b + o_lm);
+  s->dev.lrec_clus = (const int32_t*)(b + o_lk);
   s->dev.n_lclus = (int32_t)lclus.size();
   s->dev.lrec = (const QuadRec*)(b + o_lr);
   s->dev.n_lbvh = (int32_t)lbvh.size();

@@ -641,7 +641,11 @@ __device__ __forceinline__ void other_trace(const DevScene& sc, V3 o, V3 d, doub
 // the ray's line within [t_lo, t_hi] (radiance rays t_lo = -inf: every root at
 // t <= t_hi, the containers' t < 0 ones included; shadow rays t_lo = 0, only
 // [0, distance) blocks); a leaf's records are tested, but for the cones the
-// pre-pass took. Order-independent minima, so the visiting order is free.
+// pre-pass took (a cone whose a ~ 0 for this ray is skipped only when its
+// cluster was open, i.e. when the pre-pass tested it; a cone whose cluster the
+// bound ruled out is tested in full here, so a rounding slip in the bound would
+// cost a test, never a root). Order-independent minima, so the visiting order
+// is free.
 __device__ __forceinline__ bool cone_cluster_open(cConeCluster g, V3 d) {
   const double dm = fmax(fmax(fabs(d.x), fabs(d.y)), fabs(d.z)), dm2 = dm * dm;
   const double v = g->q[0] * d.x * d.x + g->q[1] * d.y * d.y + g->q[2] * d.z * d.z +
@@ -709,7 +713,10 @@ __device__ __forceinline__ void line_trace(const DevScene& sc, V3 o, V3 d, doubl
       const int lc = -(code + 1), first = lc >> 7, cnt = lc & 127;
       for (int k = first; k < first + cnt; ++k) {
         const QuadRec* q = sc.lrec + k;
-        if (q->kind == 4 && cone_degenerate(q, d)) continue;  // the pre-pass tested it
+        if (q->kind == 4 && cone_degenerate(q, d)) {
+          const int32_t cc = sc.lrec_clus[k];
+          if (cc >= 0 && cone_cluster_open((cConeCluster)sc.lclus + cc, d)) continue;  // the pre-pass tested it
+        }
         quad_test<SHADOW>(q, o, d, h);
         ++n_tests;
         if constexpr (SHADOW) {

@@ -609,3 +609,68 @@ def test_other_records_only_scene_takes_fast_path(rt):
     executed = sum(p["tests"].values())
     reference = (st["rays_primary"] + st["rays_reflect"] + st["rays_refract"] + st["rays_shadow"]) * 300
     assert executed < reference / 10
+
+
+def test_line_hierarchy_small_a_near_tangent(rt):
+    """The line hierarchy's padding where the roots are least accurate (advisor
+    r05): open tubes and cones with |a| between EPSILON and 10 EPSILON for the
+    ray (directions within a hair of a tube's axis or of a cone's generators)
+    and near-tangent rays (discriminant ~ 0), with small spheres placed just
+    past rays' roots on the shapes, so that a root found on the wrong side of a
+    box's t_hi would change the hit. Fast path == every-shape loop, bitwise."""
+    rng = np.random.default_rng(47)
+    w = rt.World()
+    shapes = []
+    for i in range(48):
+        c = rng.uniform([-8, 1, -8], [8, 3, 8])
+        if i % 2:
+            s = rt.Cylinder(-1.0, 1.0, False)
+            sc = np.array([0.5, 1.0, 0.5])
+        else:
+            s = rt.Cone(-1.0, 1.0, False)
+            sc = np.array([0.5, 0.5, 0.5])
+        s.set_transform(rt.translation(*c) * rt.scaling(*sc))
+        s.material.color = rt.Color(*rng.uniform(0, 1, 3))
+        w.add_object(s)
+        shapes.append((i % 2, c, sc))
+    rays, blockers = [], []
+    for k in range(3000):
+        tube, c, sc = shapes[k % len(shapes)]
+        a = float(rng.uniform(1.05e-5, 1e-4)) * (1 if rng.uniform() < 0.8 else -1)
+        phi = float(rng.uniform(0, 2 * np.pi))
+        side = np.array([-np.sin(phi), 0.0, np.cos(phi)])
+        if tube:  # object direction (ex, 1, ez) with ex^2 + ez^2 = |a|; the line ~1 from the axis
+            r = np.sqrt(abs(a))
+            ld = np.array([r * np.cos(phi), 1.0, r * np.sin(phi)])
+            lo = side * (1.0 + float(rng.uniform(-1e-7, 1e-7))) + np.array([0.0, float(rng.uniform(-3, -1.5)), 0.0])
+            qa, qb = ld[0] ** 2 + ld[2] ** 2, 2 * (lo[0] * ld[0] + lo[2] * ld[2])
+            qc = lo[0] ** 2 + lo[2] ** 2 - 1.0
+        else:  # cone: ex^2 - 1 + ez^2 = a; the line just beside a generator
+            r = np.sqrt(1.0 + a)
+            ld = np.array([r * np.cos(phi), 1.0, r * np.sin(phi)])
+            lo = side * float(rng.uniform(1e-6, 1e-3)) + np.array([0.0, float(rng.uniform(-3, -1.5)), 0.0])
+            qa = ld[0] ** 2 - ld[1] ** 2 + ld[2] ** 2
+            qb = 2 * (lo[0] * ld[0] - lo[1] * ld[1] + lo[2] * ld[2])
+            qc = lo[0] ** 2 - lo[1] ** 2 + lo[2] ** 2
+        d = ld * sc
+        o = lo * sc + c
+        dn = d / np.linalg.norm(d)
+        rays.append(np.hstack([o, dn]))
+        disc = qb * qb - 4 * qa * qc
+        if k % 5 == 0 and disc >= 0 and len(blockers) < 80:
+            for t in sorted(((-qb - np.sqrt(disc)) / (2 * qa), (-qb + np.sqrt(disc)) / (2 * qa))):
+                if t > 0:  # just past the first root ahead (world distance t |d|)
+                    blockers.append(o + dn * (t * np.linalg.norm(d) + float(rng.uniform(1e-3, 5e-2))))
+                    break
+    for b in blockers:
+        s = rt.Sphere()
+        s.set_transform(rt.translation(*b) * rt.scaling(0.02, 0.02, 0.02))
+        w.add_object(s)
+    w.add_light(rt.PointLight(rt.Point(-10, 10, -10), rt.Color(1, 1, 1)))
+    assert len(blockers) > 40
+    rays = np.array(rays)
+    for depth in (0, 1, 3):
+        fast, _ = w.color_at_batch(rays, depth, want_stats=False)
+        exact, _ = w.color_at_batch(rays, depth, want_stats=True)
+        assert fast.tobytes() == exact.tobytes(), depth
+    assert rt._rtamd._wf_profile(w, -1, True)["n_line_culled"] == 48

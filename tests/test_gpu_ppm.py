@@ -110,26 +110,27 @@ def test_device_ppm_empty_canvases(rt, oracle):
         assert got == _as_bytes(oracle.canvas_to_ppm(img)) == _as_bytes(rt.canvas_to_ppm(img)), (h, w)
 
 
-def test_render_ppm_banded_paths(rt):
-    """rt_render_ppm at C3's full size renders in row bands, each band's text
-    encoded and copied behind the later bands' renders: the
-    text equals the one-render path's (bands = 1) byte for byte, into a pinned
-    block (the binding) and into a reused pageable buffer, with AA X2, and after
-    a forced arena overflow (the call falls back to the whole-frame render); a
-    buffer one byte short is refused."""
+def test_render_ppm_buffers_and_overflow(rt):
+    """rt_render_ppm on C3's full frame (one pass of the stream for the render,
+    the encoder and the text's length, then the copy): the same text through
+    the binding (a pooled pinned block, copied into a bytes object by a few
+    threads), into a reused pinned block, into a reused pageable buffer, with
+    AA X2, and after a forced arena overflow (the frame is rendered again before
+    the text is encoded); a buffer one byte short is refused."""
     import numpy as np
     from rtamd import scenes
     w, cam, depth = scenes.c3()
-    w.tune("bands", 1)
-    whole, _ = cam.render_ppm(w, depth)
-    whole2, _ = cam.render_ppm(w, depth, 2)
-    w.tune("bands", 4)
-    banded, _ = cam.render_ppm(w, depth)
-    assert banded == whole
-    banded2, _ = cam.render_ppm(w, depth, 2)
-    assert banded2 == whole2
-    buf = np.zeros(len(whole) + 4096, dtype=np.uint8)
-    for _ in range(2):
+    canvas, _ = cam.render(w, depth, want_stats=False)
+    whole = _as_bytes(rt.canvas_to_ppm(canvas.to_numpy()))
+    ppm, _ = cam.render_ppm(w, depth)
+    assert ppm == whole
+    cam.render_opts.aa_samples(rt.AASamples.X2)
+    canvas2, _ = cam.render_multithreaded(w, depth, want_stats=False)
+    ppm2, _ = cam.render_ppm(w, depth, 2)
+    assert ppm2 == _as_bytes(rt.canvas_to_ppm(canvas2.to_numpy()))
+    pinned = rt._rtamd.host_buffer(len(whole) + 4096)
+    pageable = np.zeros(len(whole) + 4096, dtype=np.uint8)
+    for buf in (pinned, pageable, pinned):
         n = cam.render_ppm_into(w, buf, depth)
         assert n == len(whole) and buf[:n].tobytes() == whole
     w.tune("arena_pct", 5)

@@ -1,6 +1,6 @@
 """rt_render to a host canvas on C3 in a held loop (dev tool, for a kernel and
 copy trace of the banded render: rocprofv3 --kernel-trace --memory-copy-trace
--- python tools/e2e_loop.py); prints the per-frame wall times."""
+-- python tools/archive/e2e_loop.py); prints the per-frame wall times."""
 import json
 import os
 import sys

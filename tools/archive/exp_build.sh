@@ -1,9 +1,9 @@
 #!/bin/bash
 # Build experiment variants of librtamd.so (dev tool, run here on the CPU):
-#   bash tools/exp_build.sh NAME "-DFLAG ..." [NAME "-DFLAG ..." ...]
+#   bash tools/archive/exp_build.sh NAME "-DFLAG ..." [NAME "-DFLAG ..." ...]
 # Each lands in raytracer-challenge-rs_amd/lib_exp_NAME/librtamd.so; the
 # extension picks it up through LD_LIBRARY_PATH (its RUNPATH yields to it),
-# see tools/exp_time.sh.
+# see tools/archive/exp_time.sh.
 set -e
 cd "$(dirname "$0")/../raytracer-challenge-rs_amd"
 while [ $# -ge 2 ]; do

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Time library variants on one box, alternating (dev tool, on the GPU box):
-#   ROUNDS=2 bash tools/exp_time.sh TAG [ARGS="--config c3"] base NAME[:k=v,k=v] [...]
-# `base` is the default build (lib/); NAME is lib_exp_NAME (tools/exp_build.sh);
+#   ROUNDS=2 bash tools/archive/exp_time.sh TAG [ARGS="--config c3"] base NAME[:k=v,k=v] [...]
+# `base` is the default build (lib/); NAME is lib_exp_NAME (tools/archive/exp_build.sh);
 # ":k=v,..." adds tuning knobs (quick_time.py --knob) to that variant.
 # Each run is tools/quick_time.py under its own time limit; the chain stops at
 # the first failure.

@@ -1,6 +1,6 @@
 """Line hierarchy timing (dev tool): renders scenes.cones on one GPU, the fast
 path, and prints one JSON line with the frame time and the executed record
-tests per frame. Run it against two builds (LD_LIBRARY_PATH, tools/exp_time.sh)
+tests per frame. Run it against two builds (LD_LIBRARY_PATH, tools/archive/exp_time.sh)
 to compare the culled cones and open tubes with the exhaustive loop.
 Usage: line_time.py [--n N] [--upright F] [--width W --height H] [--frames K]"""
 import argparse

@@ -1,5 +1,5 @@
 """Sum selected PMC counters per kernel over a rocprofv3 counter_collection.csv
-(dev tool): python tools/pmc_latency.py DIR [DIR ...] -> per kernel name
+(dev tool): python tools/archive/pmc_latency.py DIR [DIR ...] -> per kernel name
 prefix, every counter's total and derived latencies (level / instructions)."""
 import csv
 import glob

@@ -6,7 +6,7 @@
 // slots of P(test) * c_test, P = area / area(root).
 // Usage: wide_sah [c3|c5] [c_visit] [c_test] [leaf] [f16]
 // (f16: the greedy cost over the binary16 copy's boxes, wide16_layout)
-// Build: g++ -O2 -std=c++17 -pthread -I raytracer-challenge-rs_amd/csrc tools/wide_sah.cpp
+// Build: g++ -O2 -std=c++17 -pthread -I raytracer-challenge-rs_amd/csrc tools/archive/wide_sah.cpp
 //        raytracer-challenge-rs_amd/csrc/rt_bvh.cpp -o /tmp/wide_sah
 #include <algorithm>
 #include <cmath>

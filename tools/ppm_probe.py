@@ -60,5 +60,8 @@ pinned = rtamd._rtamd.host_buffer(cap)
 n = timed("render_ppm_into_pinned", lambda: cam.render_ppm_into(w, pinned, depth))
 assert pinned[:n].tobytes() == bytes(ref)
 timed("bytes_of_pinned_text", lambda: bytes(pinned[:n]))
+timed("render_ppm_into_pinned_then_bytes", lambda: bytes(pinned[:cam.render_ppm_into(w, pinned, depth)]))
+timed("host_buffer_alloc_free", lambda: rtamd._rtamd.host_buffer(cap))
+
 out["ppm_bytes"] = n
 print(json.dumps(out), flush=True)
