@@ -664,7 +664,7 @@ def test_line_hierarchy_small_a_near_tangent(rt):
                     break
     for b in blockers:
         s = rt.Sphere()
-        s.set_transform(rt.translation(*b) * rt.scaling(0.02, 0.02, 0.02))
+        s.set_transform(rt.translation(*b) * rt.scaling(0.03, 0.03, 0.03))  # (det >= EPSILON: invertible)
         w.add_object(s)
     w.add_light(rt.PointLight(rt.Point(-10, 10, -10), rt.Color(1, 1, 1)))
     assert len(blockers) > 40
