@@ -201,10 +201,11 @@ def cpu_model():
 
 def cpu_baseline(world, cam, depth, budget_s):
     """Oracle (C port of the reference algorithm: full intersection list + sort
-    + containers walk, recursive color_at) on evenly spaced rows, threads in
-    contiguous row blocks like render_multithreaded (camera.rs:157-172): on
-    every core this process may use, and on one core. Each sample is sized to
-    ~budget_s (the one-core sample to a third of it)."""
+    + containers walk, recursive color_at), threads in contiguous row blocks like
+    render_multithreaded (camera.rs:157-172): on every core this process may
+    use, the whole frame when it takes at most two minutes (C3), else evenly
+    spaced rows sized to ~budget_s; and on one core, rows sized to a third of
+    budget_s."""
     from oracle import pyoracle
     ow = pyoracle.OracleWorld.from_world(world)
     desc = cam.desc_bytes()
@@ -216,10 +217,13 @@ def cpu_baseline(world, cam, depth, budget_s):
         dt = time.perf_counter() - t0
         return dt, st["rays_primary"] + st["rays_reflect"] + st["rays_refract"] + st["rays_shadow"]
 
-    def sample(nthreads, budget):
+    def sample(nthreads, budget, full_limit=0.0):
         # calibrate: one row per thread, spread over the frame
         probe = sorted({int((i + 0.5) * H / nthreads) for i in range(min(nthreads, H))})
         t_probe, r_probe = run(probe, nthreads)
+        if t_probe * H / len(probe) <= full_limit:  # the whole frame fits the limit: SURVEY §8(d)'s full frame
+            dt, rays = run(list(range(H)), nthreads)
+            return list(range(H)), dt, rays, 1
         if t_probe >= 0.5 * budget:  # slow rows (C5): the probe already is the sample
             return probe, t_probe, r_probe, max(1, H // len(probe))
         n_rows = int(max(1, min(H, len(probe) * budget / max(t_probe, 1e-6))))
@@ -229,7 +233,10 @@ def cpu_baseline(world, cam, depth, budget_s):
         return rows, dt, rays, stride
 
     nthreads = host_cores()
-    rows, dt, rays, stride = sample(nthreads, budget_s)
+    # the full frame on every core when it takes at most ~2 minutes (C3 on the GPU box's 16 cores: ~52 s;
+    # a row sample measured 0.79-1.05x of it, the row blocks' load balance depending on the sample,
+    # profiles/r06_cpu_full_frame.json), else evenly spaced rows
+    rows, dt, rays, stride = sample(nthreads, budget_s, full_limit=120.0)
     rows1, dt1, rays1, stride1 = sample(1, budget_s / 3)
     return {
         "value": rays / dt / 1e6,
@@ -240,7 +247,8 @@ def cpu_baseline(world, cam, depth, budget_s):
         "cpus_on_host": os.cpu_count(),
         "single_core": {"value": rays1 / dt1 / 1e6, "unit": "Mrays/s", "cores": 1,
                         "sample": f"{len(rows1)} of {H} rows (every {stride1}th), {rays1} rays in {dt1:.2f}s"},
-        "sample": f"{len(rows)} of {H} rows (every {stride}th), {rays} rays in {dt:.2f}s; "
+        "sample": (f"the full frame ({H} rows), {rays} rays in {dt:.2f}s; " if stride == 1 else
+                   f"{len(rows)} of {H} rows (every {stride}th), {rays} rays in {dt:.2f}s; ") +
                   f"C restatement of the reference algorithm (oracle/rt_oracle.c: full intersection list + "
                   f"sort + containers walk, recursion depth {depth}), {nthreads} threads in row blocks "
                   f"(every CPU this process may use: affinity set, cgroup quota)",

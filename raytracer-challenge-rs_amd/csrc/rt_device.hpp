@@ -508,7 +508,8 @@ __device__ __forceinline__ V3 pattern_color(const ShadeRec& s, V3 world_point) {
 
 // f64::powf of the specular term (material.rs:76): glibc 2.35's pow, operation
 // for operation (rt_pow.hpp), so the colours are the reference host's bit for
-// bit (OCML's pow differed by 1-2 ulps in about 1 of 4000 channels, round 5).
+// bit (OCML's pow differed by 1-2 ulps in about 1 of 4000 channels, round 5);
+// the frame costs the same (profiles/r06_ab_pow.txt: +0.2 %, within noise).
 // Out of line: inlined into the fused trace kernels, its constants were hoisted
 // out of the ray loop into VGPRs and spilled across the BVH traversal.
 __device__ __attribute__((noinline)) double spec_pow(double x, double y) { return pow_glibc(x, y); }

@@ -13,15 +13,13 @@
 // Tables: rt_pow_tables.hpp (tools/gen_pow_tables.py). Checked against the
 // host's glibc pow on random and edge inputs by tests/test_pow.py.
 //
-// Domain: what `lighting` passes (material.rs:74-79): x = reflect_dot_eye > 0
-// finite, y = shininess finite. Other x (zero, negative, inf, NaN) and the
-// special y (zero, |y| < 2^-65, |y| >= 2^63, inf, NaN) take glibc's special
-// cases for positive x only; a negative or non-finite x returns NaN/inf as IEEE
-// pow does for the cases that can reach it (x > 0 always holds in lighting).
+// Every input takes glibc's path, its special cases included (zero, negative,
+// infinite and NaN x; zero, tiny, huge, infinite and NaN y; negative x with
+// an odd integer y gives the sign), so no other pow is ever called (`lighting`
+// itself passes x = reflect_dot_eye > 0, y = shininess).
 #pragma once
 #include <hip/hip_runtime.h>
 
-#include <cmath>
 #include <cstdint>
 
 #include "rt_pow_tables.hpp"
@@ -64,6 +62,8 @@ __host__ __device__ __forceinline__ double pow_log_inline(uint64_t ix, double* t
   return y;
 }
 
+constexpr uint64_t kPowSignBias = 0x800ull << 7;  // SIGN_BIAS: the result's sign through exp_inline
+
 // exp_inline's special case (e_exp.c specialcase): the scale's exponent
 // overflowed (k > 0) or the result is subnormal (k < 0)
 __host__ __device__ __forceinline__ double pow_exp_special(double tmp, uint64_t sbits, uint64_t ki) {
@@ -88,8 +88,8 @@ __host__ __device__ __forceinline__ double pow_exp_special(double tmp, uint64_t 
   return 0x1p-1022 * y;
 }
 
-// exp_inline (e_pow.c): exp(x + xtail)
-__host__ __device__ __forceinline__ double pow_exp_inline(double x, double xtail) {
+// exp_inline (e_pow.c): exp(x + xtail), negated when sign_bias is set
+__host__ __device__ __forceinline__ double pow_exp_inline(double x, double xtail, uint64_t sign_bias) {
   constexpr double InvLn2N = 0x1.71547652b82fep0 * 128, Shift = 0x1.8p52;
   constexpr double NegLn2hiN = -0x1.62e42fefa0000p-8, NegLn2loN = -0x1.cf79abc9e3b3ap-47;
   constexpr double C2 = 0x1.ffffffffffdbdp-2, C3 = 0x1.555555555543cp-3, C4 = 0x1.55555cf172b91p-5,
@@ -97,8 +97,14 @@ __host__ __device__ __forceinline__ double pow_exp_inline(double x, double xtail
   auto top12 = [](double v) { return (uint32_t)(pow_bits(v) >> 52); };
   uint32_t abstop = top12(x) & 0x7ff;
   if (abstop - top12(0x1p-54) >= top12(512.0) - top12(0x1p-54)) {
-    if (abstop - top12(0x1p-54) >= 0x80000000u) return 1.0 + x;  // tiny x
-    if (abstop >= top12(1024.0)) return (pow_bits(x) >> 63) ? 0x1p-767 * 0x1p-767 : 0x1p769 * 0x1p769;
+    if (abstop - top12(0x1p-54) >= 0x80000000u) {  // tiny x
+      const double one = 1.0 + x;
+      return sign_bias ? -one : one;
+    }
+    if (abstop >= top12(1024.0)) {  // __math_uflow / __math_oflow
+      const double r = (pow_bits(x) >> 63) ? 0x1p-767 * 0x1p-767 : 0x1p769 * 0x1p769;
+      return sign_bias ? -r : r;
+    }
     abstop = 0;  // large |x|: specialcase below
   }
   double kd = __builtin_fma(InvLn2N, x, Shift);
@@ -107,7 +113,7 @@ __host__ __device__ __forceinline__ double pow_exp_inline(double x, double xtail
   double r = __builtin_fma(kd, NegLn2loN, __builtin_fma(kd, NegLn2hiN, x));
   r += xtail;
   const uint64_t idx = 2 * (ki % 128);
-  const uint64_t top = ki << (52 - 7);
+  const uint64_t top = (ki + sign_bias) << (52 - 7);
   const double tail = pow_dbl(kExpTab[idx]);
   const uint64_t sbits = kExpTab[idx + 1] + top;
   const double r2 = r * r;
@@ -118,11 +124,23 @@ __host__ __device__ __forceinline__ double pow_exp_inline(double x, double xtail
   return __builtin_fma(scale, tmp, scale);
 }
 
-// pow(x, y) for x > 0 (glibc 2.35 __pow, FMA form)
+// checkint (e_pow.c): 0 = y is not an integer, 1 = an odd integer, 2 = an even one
+__host__ __device__ __forceinline__ int pow_checkint(uint64_t iy) {
+  const int e = (int)(iy >> 52 & 0x7ff);
+  if (e < 0x3ff) return 0;
+  if (e > 0x3ff + 52) return 2;
+  if (iy & ((1ull << (0x3ff + 52 - e)) - 1)) return 0;
+  if (iy & (1ull << (0x3ff + 52 - e))) return 1;
+  return 2;
+}
+
+// pow(x, y) (glibc 2.35 __pow, FMA form)
 __host__ __device__ __forceinline__ double pow_glibc(double x, double y) {
+  uint64_t sign_bias = 0;
   uint64_t ix = pow_bits(x);
   const uint64_t iy = pow_bits(y);
-  const uint32_t topx = (uint32_t)(ix >> 52), topy = (uint32_t)(iy >> 52);
+  uint32_t topx = (uint32_t)(ix >> 52);
+  const uint32_t topy = (uint32_t)(iy >> 52);
   if (topx - 0x001u >= 0x7ffu - 0x001u || (topy & 0x7ffu) - 0x3beu >= 0x43eu - 0x3beu) {
     auto zeroinfnan = [](uint64_t u) { return 2 * u - 1 >= 2 * pow_bits(__builtin_inf()) - 1; };
     if (zeroinfnan(iy)) {
@@ -133,7 +151,18 @@ __host__ __device__ __forceinline__ double pow_glibc(double x, double y) {
       if ((2 * ix < 2 * pow_bits(1.0)) == !(iy >> 63)) return 0.0;
       return y * y;
     }
-    if (zeroinfnan(ix) || (ix >> 63)) return pow(x, y);  // (outside lighting's domain: the platform pow)
+    if (zeroinfnan(ix)) {
+      double x2 = x * x;
+      if ((ix >> 63) && pow_checkint(iy) == 1) x2 = -x2;
+      return (iy >> 63) ? 1.0 / x2 : x2;
+    }
+    if (ix >> 63) {  // finite x < 0
+      const int yint = pow_checkint(iy);
+      if (yint == 0) return (x - x) / (x - x);  // __math_invalid: NaN
+      if (yint == 1) sign_bias = kPowSignBias;
+      ix &= 0x7fffffffffffffffull;
+      topx &= 0x7ffu;
+    }
     if ((topy & 0x7ffu) - 0x3beu >= 0x43eu - 0x3beu) {
       if (ix == pow_bits(1.0)) return 1.0;
       if ((topy & 0x7ffu) < 0x3beu) return ix > pow_bits(1.0) ? 1.0 + y : 1.0 - y;
@@ -149,7 +178,7 @@ __host__ __device__ __forceinline__ double pow_glibc(double x, double y) {
   const double hi = pow_log_inline(ix, &lo);
   const double ehi = y * hi;
   const double elo = __builtin_fma(y, lo, __builtin_fma(y, hi, -ehi));
-  return pow_exp_inline(ehi, elo);
+  return pow_exp_inline(ehi, elo, sign_bias);
 }
 
 }  // namespace rtamd

@@ -26,5 +26,6 @@ def test_device_pow_equals_glibc(rt):
     got = out.cpu().numpy()
     libm = _libm_pow()
     ref = np.array([libm(a, b) for a, b in zip(x.tolist(), y.tolist())])
-    diff = np.flatnonzero(got.view(np.uint64) != ref.view(np.uint64))
+    # (NaN results: the device's default NaN is positive, x86's negative; lighting never makes one)
+    diff = np.flatnonzero((got.view(np.uint64) != ref.view(np.uint64)) & ~(np.isnan(got) & np.isnan(ref)))
     assert diff.size == 0, [(float.hex(x[i]), float.hex(y[i]), float.hex(ref[i]), float.hex(got[i])) for i in diff[:5]]

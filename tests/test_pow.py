@@ -56,7 +56,13 @@ def pow_cases(n, seed=5):
     x[k == 6] = np.ldexp(1.0 + u[k == 6], -1040); y[k == 6] = 0.5 + rng.random((k == 6).sum())
     x[k == 7] = 0.25 + u[k == 7]; y[k == 7] = -50 * rng.random((k == 7).sum())
     x[x == 0.0] = 0.5
-    return x, y
+    # glibc's special cases: zero / negative / infinite / NaN x, zero / tiny / huge / infinite / NaN y,
+    # negative x with odd and even integer y
+    sx = [0.0, -0.0, -2.5, -0.75, np.inf, -np.inf, np.nan, 1.0, 2.0, 0.5, -1.0, 5e-324]
+    sy = [0.0, -0.0, 3.0, -3.0, 2.0, 0.5, 1e-70, 1e70, np.inf, -np.inf, np.nan, 301.0, -1075.5]
+    ex = np.array([a for a in sx for b in sy])
+    ey = np.array([b for a in sx for b in sy])
+    return np.concatenate([x, ex]), np.concatenate([y, ey])
 
 
 def test_pow_equals_glibc_bitwise():
