@@ -266,6 +266,8 @@ struct DevScene {
   // per object: ShadeRec::reflective, transparency (what wf_combine_parents reads; 16 B a
   // record, so the table stays in the L2 where the 512-B shading records may not)
   const double* refl_transp;
+  // per object: the index of its SphereDiag record (-1: not one), after the hierarchy's reordering
+  const int32_t* obj_diag;
   // Groups (group.rs): the records' gates index this table (rt_scene_create_groups)
   const GroupRec* groups;
   int32_t n_groups, pad_groups;

@@ -283,7 +283,8 @@ int rt_scene_create_groups(const rt_shape_desc* shapes, size_t n_shapes, const i
   const size_t o_fq = align(o_fg + (fx_gen.size() + 1) * sizeof(SphereGen));
   const size_t o_sh = align(o_fq + (fx_quads.size() + 1) * sizeof(QuadRec));
   const size_t o_rt = align(o_sh + shade.size() * sizeof(ShadeRec));
-  const size_t o_li = align(o_rt + (shade.size() + 1) * 2 * sizeof(double));
+  const size_t o_od = align(o_rt + (shade.size() + 1) * 2 * sizeof(double));
+  const size_t o_li = align(o_od + (shade.size() + 1) * sizeof(int32_t));
   const size_t o_lc = align(o_li + lrec.size() * sizeof(LightRec));
   const size_t o_lv = align(o_lc + lb.cells.size() * sizeof(LbCell));
   const size_t o_ld = align(o_lv + (lb.ov.size() + 1) * sizeof(uint16_t));
@@ -312,6 +313,11 @@ int rt_scene_create_groups(const rt_shape_desc* shapes, size_t n_shapes, const i
   for (size_t i = 0; i < shade.size(); ++i) {
     const double rt2[2] = {shade[i].reflective, shade[i].transparency};
     std::memcpy(&host[o_rt + i * 2 * sizeof(double)], rt2, sizeof rt2);
+  }
+  {  // each object's SphereDiag record after the hierarchy's reordering (meta = object << 1 | shadow)
+    std::vector<int32_t> obj_diag(shade.size() + 1, -1);
+    for (size_t k = 0; k < diag.size(); ++k) obj_diag[(size_t)(diag[k].meta >> 1)] = (int32_t)k;
+    std::memcpy(&host[o_od], obj_diag.data(), obj_diag.size() * sizeof(int32_t));
   }
   if (!lrec.empty()) std::memcpy(&host[o_li], lrec.data(), lrec.size() * sizeof(LightRec));
   if (!grec.empty()) std::memcpy(&host[o_gr], grec.data(), grec.size() * sizeof(GroupRec));
@@ -386,6 +392,7 @@ int rt_scene_create_groups(const rt_shape_desc* shapes, size_t n_shapes, const i
   s->dev.lb_n_items = (int32_t)std::min<size_t>(lb.n_items, 0x7FFFFFFF);
   s->dev.shade = (const ShadeRec*)(b + o_sh);
   s->dev.refl_transp = (const double*)(b + o_rt);
+  s->dev.obj_diag = (const int32_t*)(b + o_od);
   s->dev.lights = (const LightRec*)(b + o_li);
   s->dev.groups = (const GroupRec*)(b + o_gr);
   s->dev.n_groups = (int32_t)n_groups;

@@ -951,12 +951,23 @@ __device__ __forceinline__ void lb_walk(const DevScene& sc, SD sd, const float* 
 // (direction d, distance dist): the records outside the BVH first (any hit
 // before the light ends the ray), then the light buffer, or the BVH of the
 // kernel's image when the scene has no light buffer.
+// `first` >= 0: a sphere record tested before everything else (shade_fused: the
+// sphere whose inside the point lies on). is_shadowed asks whether ANY
+// shadow-casting object meets the ray before the light, so a blocker found
+// first is the answer whatever the others hold; the ray leaves that sphere
+// through its far side, before a light outside it.
 template <int LANE, bool QUADS>
 __device__ __forceinline__ bool shadow_trace(const DevScene& sc, unsigned use_lb, const LaneScene& ls, unsigned l,
                                              V3 o, V3 d, double dist, unsigned& n_disc, unsigned& n_tests,
-                                             unsigned& n_boxes, GateSkips* skips = nullptr) {
+                                             unsigned& n_boxes, GateSkips* skips = nullptr, int first = -1) {
   Hit h;
   hit_init(h);
+  if (first >= 0) {
+    if constexpr (LANE == 14 || LANE == 15) leaf_sphere_test<true>(ls.s48, first, o, d, h, n_disc);
+    else leaf_sphere_test<true>(ls.sd, first, o, d, h, n_disc);
+    ++n_tests;
+    if (h.key >= 0 && h.t < dist) return true;
+  }
   trace_rest<true, QUADS, true>(sc, o, d, h, n_disc, skips);
   if constexpr (QUADS) {
     other_trace<true>(sc, o, d, dist, h, n_disc, n_tests, n_boxes);

@@ -114,6 +114,7 @@ struct WfTuning {
   int multi_gather = 0;    // rt_render_multi (scenes[0]'s knob): 1 = every shard gathered into device 0 by one grouped
                            //     ncclGather, then copied out of device 0 (test hook; 0 = each device copies its rows
                            //     straight into the host canvas, rt_multi.cpp)
+  int inside_first = 1;    // fast path: 1 = the shadow rays of a hit from inside a sphere record test that sphere first
 };
 // Applies `key` = `value` to `t`: 1 = applied, 0 = not a render-time key, -1 = bad value.
 int wf_tuning_apply(WfTuning& t, const char* key, int value);
@@ -278,6 +279,7 @@ struct WfArgs {
   unsigned aa;          // AA samples per pixel (generation 0 in camera mode)
   unsigned rows;        // local rows of the camera shard (generation-0 tiling)
   unsigned skip_shadow; // leave out shadow rays that cannot change the colour (fast path)
+  unsigned inside_first;  // fast path: a hit from inside a sphere record: its shadow rays test that sphere first
   // sharded queues: this generation's rays (in_cnt == nullptr: dense, slot = index),
   // the next generation's rays and this generation's shadow list
   const unsigned* in_cnt;

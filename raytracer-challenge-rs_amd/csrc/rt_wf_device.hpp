@@ -723,6 +723,8 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
       (m->reflective > 0.0 && m->transparency > 0.0) ? schlick(c.eyev, c.normal, c.n1, c.n2) : 0.0;
   // surface = Sum over the lights of lighting(..., is_shadowed(over_point, light))
   V3 surface = v3(0.0, 0.0, 0.0);  // fold from (0,0,0) (color.rs:96-103)
+  // a hit from inside a sphere record: its shadow rays test that sphere first
+  const int inside_rec = a.inside_first && c.inside ? sc.obj_diag[c.obj] : -1;
   for (unsigned l = 0; l < L; ++l) {
     cLightRec Lr = (cLightRec)sc.lights + l;
     // the shadow ray exactly as World::is_shadowed builds it (world.rs:95-105); its
@@ -735,7 +737,7 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
       // the light is behind the surface: lighting() is the ambient term either way
     } else {
       const bool shadowed = shadow_trace<LANE, QUADS>(sc, a.use_lb, ls, l, c.over, sdir, dist, t.sh_disc, t.sh_tests,
-                                                      t.sh_boxes, &t.gsk);
+                                                      t.sh_boxes, &t.gsk, inside_rec);
       if (QUADS && a.count) count_hier_gates(sc, c.over, sdir, t.gsk);
       ++t.sh_rays;
       term = lighting(*m, Lr, c.over, c.eyev, c.normal, shadowed, sdir);
