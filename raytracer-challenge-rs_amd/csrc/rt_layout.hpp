@@ -266,12 +266,15 @@ struct DevScene {
   // per object: ShadeRec::reflective, transparency (what wf_combine_parents reads; 16 B a
   // record, so the table stays in the L2 where the 512-B shading records may not)
   const double* refl_transp;
-  // per object: the index of its SphereDiag record (-1: not one), after the hierarchy's reordering
+  // per object: the index of its SphereDiag record (-1: not one), after the hierarchy's reordering,
+  // | kOwnOutside when a shadow ray leaving its outside provably never meets it (rt_scene.cpp)
   const int32_t* obj_diag;
   // Groups (group.rs): the records' gates index this table (rt_scene_create_groups)
   const GroupRec* groups;
   int32_t n_groups, pad_groups;
 };
+
+constexpr int32_t kOwnOutside = 0x40000000, kOwnIndex = 0x3FFFFFFF;  // DevScene::obj_diag
 
 struct DevCamera {
   double pixel_size, half_width, half_height;

@@ -314,9 +314,22 @@ int rt_scene_create_groups(const rt_shape_desc* shapes, size_t n_shapes, const i
     const double rt2[2] = {shade[i].reflective, shade[i].transparency};
     std::memcpy(&host[o_rt + i * 2 * sizeof(double)], rt2, sizeof rt2);
   }
-  {  // each object's SphereDiag record after the hierarchy's reordering (meta = object << 1 | shadow)
+  {  // each object's SphereDiag record after the hierarchy's reordering (meta = object << 1 | shadow),
+     // flagged kOwnOutside when its own shadow test may be left out for a hit from outside
+     // (rt_trace.hpp, shadow_trace): the over point then lies EPSILON off the surface in world
+     // space, at least EPSILON / r_max in object space, far above every rounding in the sphere
+     // test when the semi-axes are at most 1e3 and the extent at most 1e6 (the over point's
+     // EPSILON step resolved to 1e-10)
     std::vector<int32_t> obj_diag(shade.size() + 1, -1);
-    for (size_t k = 0; k < diag.size(); ++k) obj_diag[(size_t)(diag[k].meta >> 1)] = (int32_t)k;
+    for (size_t k = 0; k < diag.size(); ++k) {
+      const SphereDiag& r = diag[k];
+      bool own = true;
+      for (int a = 0; a < 3; ++a) {
+        const double sa = std::fabs(r.s[a]), ra = 1.0 / sa, ca = std::fabs(r.t[a] / r.s[a]);
+        own = own && std::isfinite(ra) && std::isfinite(ca) && ra <= 1e3 && ca + ra <= 1e6;
+      }
+      obj_diag[(size_t)(r.meta >> 1)] = (int32_t)k | (own ? kOwnOutside : 0);
+    }
     std::memcpy(&host[o_od], obj_diag.data(), obj_diag.size() * sizeof(int32_t));
   }
   if (!lrec.empty()) std::memcpy(&host[o_li], lrec.data(), lrec.size() * sizeof(LightRec));

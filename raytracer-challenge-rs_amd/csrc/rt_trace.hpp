@@ -900,7 +900,7 @@ __device__ __forceinline__ LaneScene lane_scene(const DevScene& sc, unsigned lds
 template <typename SD>  // the sphere records: const SphereDiag* (global or LDS) or Sph48 (the pair image)
 __device__ __forceinline__ void lb_walk(const DevScene& sc, SD sd, const float* delta, const _Float16* delta16,
                                         unsigned l, V3 o, V3 d, double dist, Hit& h, unsigned& n_disc,
-                                        unsigned& n_tests) {
+                                        unsigned& n_tests, int skip = -1) {
   cLightRec Lr = (cLightRec)sc.lights + l;
   if (dist <= (double)sc.lb_limit[l] && dist >= 1e-30) {
     const int R = sc.lb_res;
@@ -934,12 +934,14 @@ __device__ __forceinline__ void lb_walk(const DevScene& sc, SD sd, const float* 
       else if (k == 4u) idx = c.w2 >> 16;
       else idx = sc.lb_ov[c.ov + k - (unsigned)kLbInline];
       if ((dl16 ? (float)dl16[idx] : dl[idx]) > dist_up) break;  // this box and all after it lie beyond the origin
+      if ((int)idx == skip) continue;
       leaf_sphere_test<true>(sd, (int)idx, o, d, h, n_disc);
       ++n_tests;
       if (h.key >= 0 && h.t < dist) break;
     }
   } else {
     for (int k = 0; k < sc.n_diag; ++k) {
+      if (k == skip) continue;
       leaf_sphere_test<true>(sd, k, o, d, h, n_disc);
       ++n_tests;
       if (h.key >= 0 && h.t < dist) break;
@@ -956,10 +958,21 @@ __device__ __forceinline__ void lb_walk(const DevScene& sc, SD sd, const float* 
 // shadow-casting object meets the ray before the light, so a blocker found
 // first is the answer whatever the others hold; the ray leaves that sphere
 // through its far side, before a light outside it.
+// `skip` >= 0: a sphere record the light-buffer walk leaves out (shade_fused:
+// the sphere hit from outside, the light in front of the surface, i.e. the
+// computed light . normal >= 0, and the record flagged kOwnOutside). Every
+// point o + t d (t >= 0) then lies at least ~EPSILON beyond the tangent plane
+// at the hit (the over point's step; the computed direction's error moves the
+// ray by 1e-16 t), outside the convex ellipsoid; in object space the ray keeps
+// at least EPSILON / r_max >= 1e-8 from the unit sphere, so the test's
+// discriminant is negative or both roots negative, at margins eight orders
+// above its rounding: the reference's test of that sphere never reports a
+// blocker, and leaving it out changes no answer.
 template <int LANE, bool QUADS>
 __device__ __forceinline__ bool shadow_trace(const DevScene& sc, unsigned use_lb, const LaneScene& ls, unsigned l,
                                              V3 o, V3 d, double dist, unsigned& n_disc, unsigned& n_tests,
-                                             unsigned& n_boxes, GateSkips* skips = nullptr, int first = -1) {
+                                             unsigned& n_boxes, GateSkips* skips = nullptr, int first = -1,
+                                             int skip = -1) {
   Hit h;
   hit_init(h);
   if (first >= 0) {
@@ -975,8 +988,8 @@ __device__ __forceinline__ bool shadow_trace(const DevScene& sc, unsigned use_lb
   }
   if (!(h.key >= 0 && h.t < dist)) {
     if (use_lb) {
-      if constexpr (LANE == 14 || LANE == 15) lb_walk(sc, ls.s48, ls.delta, ls.delta16, l, o, d, dist, h, n_disc, n_tests);
-      else lb_walk(sc, ls.sd, ls.delta, ls.delta16, l, o, d, dist, h, n_disc, n_tests);
+      if constexpr (LANE == 14 || LANE == 15) lb_walk(sc, ls.s48, ls.delta, ls.delta16, l, o, d, dist, h, n_disc, n_tests, skip);
+      else lb_walk(sc, ls.sd, ls.delta, ls.delta16, l, o, d, dist, h, n_disc, n_tests, skip);
     } else if constexpr (LANE == 14) {
       lane_trace_pair<true>(ls.nodes, ls.s48, ls.M, sc.n_bvh > 0, o, d, dist, h, n_disc, n_tests, n_boxes,
                             ls.stack16);

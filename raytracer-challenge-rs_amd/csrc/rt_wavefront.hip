@@ -42,7 +42,7 @@ int wf_tuning_apply(WfTuning& t, const char* key, int value) {
       {"d2h", &WfTuning::d2h, 0, 1},               {"bands", &WfTuning::bands, 1, 4},
       {"band_pct", &WfTuning::band_pct, 5, 95},   {"band_gen", &WfTuning::band_gen, -1, 8},
       {"band_ratio", &WfTuning::band_ratio, 30, 100}, {"multi_gather", &WfTuning::multi_gather, 0, 1},
-      {"inside_first", &WfTuning::inside_first, 0, 1}};
+      {"own_sphere", &WfTuning::own_sphere, 0, 2}};
   if (!key) return 0;
   for (const Knob& k : knobs) {
     if (std::strcmp(key, k.name) != 0) continue;
@@ -621,7 +621,7 @@ hipError_t Wavefront::render_fast(const DevScene& sc, const DevCamera& cam, bool
   a.row_block = row_block; a.shard = shard; a.n_shards = n_shards;
   a.blk_period = blk_period_; a.blk_mask = blk_mask_;
   a.skip_shadow = skip_shadow ? 1u : 0u;
-  a.inside_first = (tn.inside_first && sc.obj_diag) ? 1u : 0u;
+  a.own_sphere = sc.obj_diag ? (unsigned)tn.own_sphere : 0u;
   a.count = count ? 1u : 0u;
   a.use_lb = (tn.shadow_lb && sc.lb_cells) ? 1u : 0u;
   const bool use_prim = camera_mode && sc.n_diag > 0;

@@ -114,7 +114,8 @@ struct WfTuning {
   int multi_gather = 0;    // rt_render_multi (scenes[0]'s knob): 1 = every shard gathered into device 0 by one grouped
                            //     ncclGather, then copied out of device 0 (test hook; 0 = each device copies its rows
                            //     straight into the host canvas, rt_multi.cpp)
-  int inside_first = 1;    // fast path: 1 = the shadow rays of a hit from inside a sphere record test that sphere first
+  int own_sphere = 2;      // fast path, the shadow rays of a hit on a sphere record: 1 = from inside, test that sphere
+                           //     first; 2 = also, from outside towards a light in front, leave it out (rt_trace.hpp)
 };
 // Applies `key` = `value` to `t`: 1 = applied, 0 = not a render-time key, -1 = bad value.
 int wf_tuning_apply(WfTuning& t, const char* key, int value);
@@ -279,7 +280,7 @@ struct WfArgs {
   unsigned aa;          // AA samples per pixel (generation 0 in camera mode)
   unsigned rows;        // local rows of the camera shard (generation-0 tiling)
   unsigned skip_shadow; // leave out shadow rays that cannot change the colour (fast path)
-  unsigned inside_first;  // fast path: a hit from inside a sphere record: its shadow rays test that sphere first
+  unsigned own_sphere;    // fast path: WfTuning::own_sphere
   // sharded queues: this generation's rays (in_cnt == nullptr: dense, slot = index),
   // the next generation's rays and this generation's shadow list
   const unsigned* in_cnt;

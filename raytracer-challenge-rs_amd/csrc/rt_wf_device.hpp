@@ -723,8 +723,11 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
       (m->reflective > 0.0 && m->transparency > 0.0) ? schlick(c.eyev, c.normal, c.n1, c.n2) : 0.0;
   // surface = Sum over the lights of lighting(..., is_shadowed(over_point, light))
   V3 surface = v3(0.0, 0.0, 0.0);  // fold from (0,0,0) (color.rs:96-103)
-  // a hit from inside a sphere record: its shadow rays test that sphere first
-  const int inside_rec = a.inside_first && c.inside ? sc.obj_diag[c.obj] : -1;
+  // a hit on a sphere record: from inside, its shadow rays test that sphere first; from outside,
+  // towards a light in front of the surface, they leave it out (shadow_trace)
+  const int own = a.own_sphere ? sc.obj_diag[c.obj] : -1;
+  const int own_first = own >= 0 && c.inside ? (own & kOwnIndex) : -1;
+  const int own_out = own >= 0 && !c.inside && a.own_sphere > 1 && (own & kOwnOutside) ? (own & kOwnIndex) : -1;
   for (unsigned l = 0; l < L; ++l) {
     cLightRec Lr = (cLightRec)sc.lights + l;
     // the shadow ray exactly as World::is_shadowed builds it (world.rs:95-105); its
@@ -737,7 +740,8 @@ __device__ __forceinline__ void shade_fused(const DevScene& sc, const DevCamera&
       // the light is behind the surface: lighting() is the ambient term either way
     } else {
       const bool shadowed = shadow_trace<LANE, QUADS>(sc, a.use_lb, ls, l, c.over, sdir, dist, t.sh_disc, t.sh_tests,
-                                                      t.sh_boxes, &t.gsk, inside_rec);
+                                                      t.sh_boxes, &t.gsk, own_first,
+                                                      own_out >= 0 && vdot(sdir, c.normal) >= 0.0 ? own_out : -1);
       if (QUADS && a.count) count_hier_gates(sc, c.over, sdir, t.gsk);
       ++t.sh_rays;
       term = lighting(*m, Lr, c.over, c.eyev, c.normal, shadowed, sdir);

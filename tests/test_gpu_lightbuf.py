@@ -148,3 +148,40 @@ def test_lightbuf_color_at_batch_random_rays(rt):
         assert rt._rtamd._wf_profile(w, -1, True)["lb_res"] == 64
     finally:
         rt._rtamd._tuning_set("lb_res", -1)  # (the default: by scene size)
+
+
+@pytest.mark.parametrize("own", [0, 1, 2])
+def test_own_sphere_rules(rt, own):
+    """The shadow rays of a hit on a sphere record (WfTuning::own_sphere,
+    rt_trace.hpp shadow_trace): from inside (glass) that sphere is tested
+    first; from outside, towards a light in front of the surface, it is left
+    out. Ellipsoids; patterned spheres, whose shadow rays are traced with the
+    light behind the surface (there the own sphere blocks: the rule keeps it,
+    though lighting() then ignores the answer, so no frame can show it);
+    lights level with the cluster, so many hits lie on a terminator
+    (light . normal ~ 0); a sphere too large for the rule (semi-axis 5e3) and
+    one too far (centre 2e6): the fast frame equals the exhaustive one."""
+
+    def make(rt):
+        w, cam, depth = _cluster(rt, None, n=160, seed=21, lights=[(40.0, 1.5, 0.3), (0.2, 1.4, -0.1), (-6, 9, -6)],
+                                 size=(128, 96))
+        rng = np.random.default_rng(3)
+        for i in range(90):
+            s = rt.Sphere() if i % 2 else rt.glass_sphere()
+            c = rng.uniform([-3, 0.6, -3], [3, 3, 3])
+            s.set_transform(rt.translation(*c) * rt.scaling(*rng.uniform(0.1, 0.6, 3)))
+            if i % 3 == 0:
+                s.material.set_pattern(rt.checkers_pattern(rt.Color(1, 0, 0), rt.Color(0, 0, 1)))
+            w.add_object(s)
+        big = rt.Sphere()
+        big.set_transform(rt.translation(-5e3 - 4.0, 1.0, 0.0) * rt.scaling(5e3, 5e3, 5e3))
+        w.add_object(big)
+        far = rt.Sphere()
+        far.set_transform(rt.translation(0.0, 1.0, 2e6) * rt.scaling(5e5, 5e5, 5e5))
+        w.add_object(far)
+        w.tune("own_sphere", own)
+        return w, cam, depth
+
+    fast, bvh, exact, _ = _three(rt, make)
+    assert fast.tobytes() == exact.tobytes()
+    assert bvh.tobytes() == exact.tobytes()
