@@ -84,6 +84,7 @@ extern "C" int rtamd_nccl_comm_abort(void* comm);
 extern "C" int rtamd_nccl_gather_f64(const double* send, double* recv, size_t count, int root, void* comm, void* stream);
 extern "C" int rtamd_nccl_comm_destroy(void* comm);
 extern "C" int rtamd_wf_profile(const rt_scene* s, int enable, double out[38]);
+extern "C" int rtamd_wf_gen_counts(const rt_scene* s, unsigned* out, int max);
 extern "C" int rtamd_scene_tuning_set(const rt_scene* s, const char* key, int value);
 extern "C" int rtamd_render_shard_host(const rt_scene* scene, const rt_camera_desc* camera, uint32_t max_depth,
                                        uint32_t aa_samples, uint32_t row_block, uint32_t shard, uint32_t n_shards,
@@ -618,6 +619,14 @@ PYBIND11_MODULE(_rtamd, m) {
         return py::make_tuple(std::unique_ptr<Canvas>(out), stats_dict(st));
       }, py::arg("max_depth") = 5)
       .def("render_to", &SceneParser::render_to, py::arg("path"), py::arg("max_depth") = 5);
+  m.def("_wf_gen_counts", [](const World& w) {
+    unsigned o[66] = {0};
+    const int n = rtamd_wf_gen_counts(w.scene(), o, 66);
+    if (n < 0) check(n, "wf_gen_counts");
+    py::list l;
+    for (int i = 0; i < n; ++i) l.append(o[i]);
+    return l;
+  }, py::arg("world"));
   m.def("_wf_profile", [](const World& w, int enable, bool read) {
     double o[38] = {0};
     check(rtamd_wf_profile(w.scene(), enable, read ? o : nullptr), "wf_profile");

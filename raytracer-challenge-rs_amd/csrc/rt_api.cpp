@@ -113,6 +113,21 @@ int rtamd_wf_profile(const rt_scene* cs, int enable, double out[38]) {
   return RT_OK;
 }
 
+// Rays of each generation of the scene's last render (dev tool): returns the
+// number of generations written into out[0 .. max).
+int rtamd_wf_gen_counts(const rt_scene* cs, unsigned* out, int max) {
+  if (!cs || !out || max < 0) return fail(RT_ERR_INVALID_ARGUMENT, "null scene or output");
+  rt_scene* s = const_cast<rt_scene*>(cs);
+  std::lock_guard<std::mutex> lk(s->mu);
+  if (!s->last_wf) return 0;
+  RT_DEVICE(s->device);
+  std::vector<unsigned> rays;
+  RT_HIP(s->last_wf->wf->gen_counts(rays));
+  const int n = std::min<int>((int)rays.size(), max);
+  for (int i = 0; i < n; ++i) out[i] = rays[(size_t)i];
+  return n;
+}
+
 // Development-only tuning hooks (not declared in include/rt_render.h).
 // rtamd_tuning_set: the scene-creation knobs (lb_res, bvh_leaf, bvh_ct) and
 // the render-time defaults copied into scenes created afterwards;

@@ -358,6 +358,8 @@ class Wavefront {
                     unsigned long long blk_mask = 0);
   // The counters of the last render (rendered with WF_COUNT); synchronises its stream.
   hipError_t read_stats(DevStats* out);
+  // Rays of each generation of the last render (synchronises its stream).
+  hipError_t gen_counts(std::vector<unsigned>& rays) { return last_counts(rays); }
   // Device time of the last render rendered with WF_TIME (after it completed).
   hipError_t kernel_ms(float* ms) { return hipEventElapsedTime(ms, ev0_, ev1_); }
   // A fast-path frame of this workspace overflowed its arenas (WfHostRec):
