@@ -6,6 +6,7 @@
 #include <thread>
 #include <vector>
 #include <algorithm>
+#include <atomic>
 
 #include "../../include/rt_render.h"
 
@@ -103,27 +104,55 @@ void ppm_row_write(const double* row, uint32_t w, char* out) {
   }
 }
 
-// f(r0, r1) over the rows, split across a few threads for large canvases.
-template <typename F>
-void for_rows(uint32_t height, size_t work, F f) {
-  unsigned t = std::thread::hardware_concurrency();
-  t = std::max(1u, std::min(t, 8u));
-  if (work < ((size_t)1 << 18) || t == 1 || height < 2 * t) {
-    f(0u, height);
-    return;
+// The rows in kBlocks contiguous blocks, encoded by the calling thread and up
+// to kBlocks - 1 helpers started once: every participant takes blocks from a
+// counter, first measuring them (each row's text length), then, once every
+// block is measured, writing them at their offsets (header + the lengths of the
+// rows before). Any number of participants (one, if no thread can start)
+// finishes every block.
+constexpr unsigned kBlocks = 16;
+
+struct PpmJob {
+  const double* rgb = nullptr;
+  uint32_t width = 0, height = 0;
+  char* out = nullptr;  // nullptr: measure only
+  size_t hn = 0, row_doubles = 0;
+  uint32_t* row_len = nullptr;  // per row, filled by the measuring pass
+  size_t block_len[kBlocks] = {};
+  std::atomic<unsigned> next1{0}, done1{0}, next2{0};
+  uint32_t r0(unsigned b) const { return (uint32_t)(((uint64_t)height * b) / kBlocks); }
+  void run() {
+    for (unsigned b; (b = next1.fetch_add(1)) < kBlocks;) {
+      size_t n = 0;
+      for (uint32_t j = r0(b); j < r0(b + 1); ++j) {
+        row_len[j] = (uint32_t)ppm_row_len(rgb + j * row_doubles, width);
+        n += row_len[j];
+      }
+      block_len[b] = n;
+      done1.fetch_add(1, std::memory_order_release);
+    }
+    if (!out) return;
+    while (done1.load(std::memory_order_acquire) < kBlocks) std::this_thread::yield();
+    for (unsigned b; (b = next2.fetch_add(1)) < kBlocks;) {
+      size_t off = hn;
+      for (unsigned k = 0; k < b; ++k) off += block_len[k];
+      for (uint32_t j = r0(b); j < r0(b + 1); ++j) {
+        ppm_row_write(rgb + j * row_doubles, width, out + off);
+        off += row_len[j];
+      }
+    }
   }
-  std::vector<std::thread> pool;
-  const uint32_t per = (height + t - 1) / t;
-  unsigned k = 1;
-  try {  // nothing may throw across the C ABI: row ranges whose thread cannot start run here
-    for (; k < t && k * per < height; ++k)
-      pool.emplace_back([=] { f(k * per, std::min(height, (k + 1) * per)); });
-  } catch (...) {
+  // run() on the calling thread and up to `t` - 1 helpers
+  void run_on(unsigned t) {
+    std::vector<std::thread> pool;
+    try {  // nothing may throw across the C ABI: blocks whose thread cannot start run here
+      for (unsigned k = 1; k < t; ++k) pool.emplace_back([this] { run(); });
+    } catch (...) {
+    }
+    run();
+    for (std::thread& th : pool) th.join();
   }
-  for (unsigned u = k; u < t && u * per < height; ++u) f(u * per, std::min(height, (u + 1) * per));
-  f(0u, std::min(height, per));
-  for (std::thread& th : pool) th.join();
-}
+};
 
 }  // namespace
 
@@ -134,26 +163,39 @@ int rt_canvas_to_ppm(const double* rgb, uint32_t width, uint32_t height, char* o
   if (!out_len || (width && height && !rgb)) return rtamd_fail(RT_ERR_INVALID_ARGUMENT, "null pointer");
   char hdr[64];
   const size_t hn = (size_t)std::snprintf(hdr, sizeof hdr, "P3\n%u %u\n255\n", width, height);
-  const size_t row_doubles = (size_t)width * 3;
-  std::vector<size_t> off;
+  std::vector<uint32_t> row_len;
   try {
-    off.assign((size_t)height + 1, 0);
+    row_len.assign((size_t)height + 1, 0);
   } catch (...) {  // nothing may throw across the C ABI (as guarded() in rt_api.cpp)
-    return rtamd_fail(RT_ERR_HOST, "out of memory (PPM row offsets)");
+    return rtamd_fail(RT_ERR_HOST, "out of memory (PPM row lengths)");
   }
-  for_rows(height, row_doubles * height, [&](uint32_t r0, uint32_t r1) {
-    for (uint32_t j = r0; j < r1; ++j) off[j + 1] = ppm_row_len(rgb + j * row_doubles, width);
-  });
-  off[0] = hn;
-  for (uint32_t j = 0; j < height; ++j) off[j + 1] += off[j];
-  const size_t len = off[height];
+  const size_t row_doubles = (size_t)width * 3;
+  unsigned t = std::thread::hardware_concurrency();
+  t = std::max(1u, std::min(t, kBlocks));
+  if (row_doubles * height < ((size_t)1 << 18) || height < 2 * kBlocks) t = 1;
+  auto init = [&](PpmJob& j, char* dst) {
+    j.rgb = rgb; j.width = width; j.height = height; j.out = dst; j.hn = hn;
+    j.row_doubles = row_doubles; j.row_len = row_len.data();
+  };
+  // one pass (measure, then write) when the buffer holds the bound (12 bytes per
+  // pixel, a newline per row, the header); otherwise measure, check, then write
+  const size_t bound = hn + (size_t)12 * width * height + height;
+  const bool one_pass = out && cap >= bound;
+  size_t len = hn;
+  {
+    PpmJob j;
+    init(j, one_pass ? out : nullptr);
+    if (one_pass) std::memcpy(out, hdr, hn);
+    j.run_on(t);
+    for (unsigned b = 0; b < kBlocks; ++b) len += j.block_len[b];
+  }
   *out_len = len;
-  if (!out) return RT_OK;
+  if (!out || one_pass) return RT_OK;
   if (len > cap) return rtamd_fail(RT_ERR_BUFFER_TOO_SMALL, "PPM buffer too small");
   std::memcpy(out, hdr, hn);
-  for_rows(height, row_doubles * height, [&](uint32_t r0, uint32_t r1) {
-    for (uint32_t j = r0; j < r1; ++j) ppm_row_write(rgb + j * row_doubles, width, out + off[j]);
-  });
+  PpmJob j;
+  init(j, out);
+  j.run_on(t);
   return RT_OK;
 }
 
