@@ -389,8 +389,9 @@ static hipError_t launch_fused_q(const DevScene& sc, const DevCamera& cam, WfArg
   // primary rays: the wave traversal, or with prim_lane the per-lane walk of the pair image or of
   // the four-wide hierarchy (the launches below, reading camera rays)
   const bool wide_ok = tn.image != 1 && tn.wide && sc.bvhw16 && wide_stack_bytes(sc) <= kWfLdsLimit / 2;
-  // prim_lane 1: any per-lane image; 2 (default): the LDS images only (C3 primary class 0.128 ->
-  // 0.125 ms/frame with the LDS four-wide image; C5's global image 2.06 -> 2.16 ms, so not there)
+  // prim_lane 1 (default): any per-lane image (C3 primary class 0.128 -> 0.125 ms/frame with the LDS
+  // four-wide image; C5's global image: 2.06 -> 2.16 ms with binary32 nodes in round 4, 2.17 -> 2.01
+  // ms with the binary16 ones, round 6); 2: the LDS images only
   const bool wide_lds = sc.bvhw && tn.lds_wide && wide_lds_bytes(sc) + dl <= kWfLdsLimit;
   const bool lds_img = tn.image == 0 && (pair_lds_bytes(sc) <= kWfLdsLimit || wide_lds);
   const bool lane_prim = tn.prim_lane == 1 ? (lds_img || wide_ok) : tn.prim_lane == 2 ? lds_img : false;

@@ -100,8 +100,8 @@ struct WfTuning {
   int treelet_deltas = 1;  // ... after the light buffer's distances (when they fit)
   int shadow_stream = 1;   // exhaustive pipeline: 1 = shadow traces on a second stream when rendering alone
   int adaptive_block = 0;  // generation pipeline: 1 = small trace launches spread over every CU
-  int prim_lane = 2;       // fast path: primary rays by the per-lane walk instead of the wave traversal with
-                           //     shared-origin records: 1 = over any image, 2 = over the LDS images only, 0 = never
+  int prim_lane = 1;       // fast path: primary rays by the per-lane walk instead of the wave traversal with
+                           //     shared-origin records: 1 = over any image (default), 2 = over the LDS images only, 0 = never
   int arena_pct = 100;     // test hook: the fast path's queue arenas sized to this percentage of the hint,
                            //     shrinking them (< 100: forces overflows, DESIGN.md "Device-sized generations")
   int d2h = 1;             // host-canvas copies: 1 = pin the caller's buffer for the call and DMA into it, 0 = pinned chunks

@@ -297,7 +297,7 @@ def test_fast_path_variants_bitwise(rt, knob, value, image):
         for b in bufs:
             assert torch.equal(b, exact)
     finally:
-        w.tune(knob, 2)  # (the default: the per-lane walk for primary rays over the LDS images)
+        w.tune(knob, 1)  # (the default: the per-lane walk for primary rays over any image)
         w.tune("image", 0)
 
 
