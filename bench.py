@@ -8,9 +8,9 @@ of primary + reflection + refraction + shadow rays (each one a
 launched by torch.distributed.run) the frame is split into interleaved 8-row
 blocks, each rank renders its rows into HBM, and the canvas is assembled on
 rank 0 with one RCCL gather (strong scaling: the frame is fixed). F frames
-are rendered in batches of NB (--batch, default for C3 8 on 1-2 GPUs and 16 on 4+, 1 for C5: one
+are rendered in batches of NB (--batch, default for C3 8 on 1-2 GPUs and 16 on 4+, for C5 2 on one GPU, 1 on N: one
 rt_render_frames_device call renders NB frames, every launch of the pipeline
-carrying all of them) on F streams (--inflight, default 4 for C3, 1 for C5),
+carrying all of them) on F streams (--inflight, default 4 for C3, 2 for C5 on one GPU and 1 on N),
 each with its own library workspace, so one batch's short, latency-bound deep
 generations overlap the next batch's work; every frame is complete, gathered
 (one gather per batch) and assembled inside the timed region.
@@ -135,7 +135,7 @@ def parse():
     p.add_argument("--row-block", type=int, default=8)
     p.add_argument("--batch", type=int, default=None,
                    help="frames per render call (rt_render_frames_device, <= 16; default for C3 8 on 1-2 GPUs, "
-                        "16 on 4+; 1 for C5)")
+                        "16 on 4+; 2 for C5 on one GPU, 1 on N)")
     p.add_argument("--inflight", type=int, default=None,
                    help="frames in flight: consecutive frames render on this many streams (own workspaces)")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget for the CPU baseline sample")
@@ -444,11 +444,16 @@ def main():
     # The render streams are plain streams, each on its own hardware queue
     # (GPU_MAX_HW_QUEUES above); CU-masked streams (--stream-kind cumask) also get
     # their own queue, but any cross-stream wait on them costs ~1 ms.
-    # default: 4 streams for C3; one for C5, whose wavefront workspace
-    # (16.8 M primary rays, depth 8) takes tens of GB per frame
-    F = max(1, a.inflight if a.inflight is not None else (4 if a.config == "c3" else 1))
-    # (C3: 8 frames per pass on 1-2 GPUs, 16 on the smaller shards of 4+; C5's frame fills the GPU alone)
-    NB = max(1, min(16, a.batch if a.batch is not None else ((8 if n < 4 else 16) if a.config == "c3" else 1)))
+    # default: 4 streams for C3; two for C5 on one GPU (one on N: the shards' row
+    # blocks), whose wavefront workspace (16.8 M primary rays, depth 8) takes tens of
+    # GB per frame
+    F = max(1, a.inflight if a.inflight is not None else (4 if a.config == "c3" else (2 if n == 1 else 1)))
+    # (C3: 8 frames per pass on 1-2 GPUs, 16 on the smaller shards of 4+; C5: 2 per pass on one GPU. A C5
+    # frame fills the GPU alone, but two passes of two frames in flight overlap one pass's
+    # draining deep generations and combines with the other's work: 43.0 -> 42.2-42.4 ms per
+    # frame, profiles/r06_c5_regime.txt)
+    NB = max(1, min(16, a.batch if a.batch is not None else ((8 if n < 4 else 16) if a.config == "c3" else
+                                                                 (2 if n == 1 else 1))))
     stream = torch.cuda.current_stream()
     kind = a.stream_kind
     if F == 1:
@@ -538,6 +543,19 @@ def main():
         frame_no[0] = s + 1
         last_frame[0] = s
 
+    def settled(fn, tries=4):
+        """fn() until no asynchronous pass of it outgrew its arenas (one GPU)."""
+        for attempt in range(tries):
+            try:
+                fn()
+                torch.cuda.synchronize()
+                world.check()
+                return
+            except rtamd.RtError as e:
+                if "overflow" not in str(e) or attempt == tries - 1:
+                    raise
+                torch.cuda.synchronize()
+
     def run_frames(k, assemble=True):
         """k frames: whole batches, then one partial batch."""
         for _ in range(k // NB):
@@ -565,12 +583,20 @@ def main():
     # (queue arenas, counters), so the timed region never meets a first
     # allocation whatever --warmup is (with batches: a whole batch, and the timed
     # region's partial batch size, on every stream)
-    for _ in range(F):
-        step()
-    if a.steps % NB:
+    def setup():
         for _ in range(F):
-            step(a.steps % NB)
-    fa.flush()
+            step()
+        if a.steps % NB:
+            for _ in range(F):
+                step(a.steps % NB)
+        fa.flush()
+    if n == 1:
+        # a new workspace's first asynchronous pass may outgrow its guessed arenas:
+        # that pass is poisoned and reported by the next call (rt_scene_check), and
+        # the arenas have grown; run the setup again until it completes
+        settled(setup)
+    else:
+        setup()
     torch.cuda.synchronize()
     run_frames(a.warmup)
     fa.flush()
@@ -610,6 +636,9 @@ def main():
     # there includes the CUs it waited for; here each kernel runs alone, as in the
     # rocprofv3 kernel trace.
     sbufs = [torch.empty_like(shard) for _ in range(NB)] if NB > 1 else [shard]
+    # (the current stream's workspace has rendered single frames so far: one untimed
+    # batch of NB first, so that an outgrown arena is not met inside the pass)
+    settled(lambda: render([cam] * NB, [b.data_ptr() for b in sbufs[:NB]], stream.cuda_stream))
     rtamd._rtamd._wf_profile(world, 1, False)
     for s0 in range(0, a.steps, NB):
         nf = min(NB, a.steps - s0)

@@ -39,7 +39,7 @@ for s in "$@"; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench) step bench 600 python bench.py || exit 1; grep '^{' "$OUT/bench.log" > "$OUT/bench.json" ;;
     benchq) step benchq 400 python bench.py --no-cpu-baseline --no-end-to-end || exit 1; grep '^{' "$OUT/benchq.log" > "$OUT/benchq.json" ;;
-    c5) step c5 600 python bench.py --config c5 --steps 3 --warmup 1 --no-cpu-baseline --no-end-to-end || exit 1 ;;
+    c5) step c5 600 python bench.py --config c5 --steps 4 --warmup 2 --no-cpu-baseline --no-end-to-end || exit 1 ;;
     shard) step shard 600 python tools/shard_time.py --ns 1,2,4,8 --frames 100 --ranks || exit 1 ;;
     shardb) step shardb 600 python tools/shard_time.py --ns 1,2,4,8 --frames 160 --batch 8 --ranks || exit 1 ;;
     tsel) step tsel 600 python -u -m pytest $TESTS -m gpu -x -v --timeout 240 --timeout-method thread -p no:cacheprovider || exit 1 ;;
