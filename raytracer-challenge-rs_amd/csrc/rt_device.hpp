@@ -139,6 +139,10 @@ __device__ __forceinline__ void sphere_test(double ox, double oy, double oz, dou
 template <bool SHADOW>
 __device__ __forceinline__ void plane_test(double oy, double dy, int meta, Hit& h) {
   if (!(fabs(dy) < kEpsilon)) {
+    // a shadow ray moving away from the plane (oy, dy of one sign, the quotient far
+    // from underflow): t < 0, no blocker, and its division is left out (the
+    // closest hit needs t < 0 for `containers`)
+    if (SHADOW && (oy > 0.0) == (dy > 0.0) && fabs(oy) > 1e-280 && fabs(dy) < 1e20) return;
     const double t = -oy / dy;
     const int k = (meta >> 1) << kKeyShift;
     const bool eligible = !SHADOW || (meta & 1);
