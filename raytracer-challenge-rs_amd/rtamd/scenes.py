@@ -555,3 +555,128 @@ def cones(width=320, height=240, n=600, upright=0.5, seed=23):
 
 CONFIGS = {"c1": c1, "c2": c2, "c3": c3, "c5": c5, "zoo": zoo, "first_scene": first_scene, "solids": solids,
            "hexagon": hexagon, "groups": groups, "divided": divided, "cones": cones}
+
+
+def fuzz(seed, width=64, height=48, n_spheres=None):
+    """A seeded random scene for parity sweeps (tests/test_gpu_fuzz.py): one to
+    three planes (one may be patterned, reflective, rotated), a cluster of
+    random spheres (non-uniform scales, rotations, some shears; diffuse,
+    mirror, glass with refractive indices 1.0-2.4, some nested), cubes,
+    cylinders and cones (open or closed, random bounds), sometimes a group
+    (transformed after its children, divided or not), patterns of every kind
+    with their own transforms, shadowless objects, one to three lights, a
+    random camera looking into the cluster and a depth of 1 to 6. Everything
+    the fast path culls (the sphere hierarchy, the other records' and the
+    lines' hierarchies, group gates, the light buffer) meets geometry it has
+    not been tuned on. `n_spheres`: that many random spheres instead of 10-119
+    (thousands: the scene images in global memory instead of LDS)."""
+    import random
+    rnd = random.Random(seed)
+    u = rnd.uniform
+    w = rt.World()
+
+    def pattern():
+        c1 = rt.Color(u(0, 1), u(0, 1), u(0, 1))
+        c2 = rt.Color(u(0, 1), u(0, 1), u(0, 1))
+        k = rnd.randrange(5)
+        p = (rt.stripe_pattern, rt.gradient_pattern, rt.ring_pattern, rt.checkers_pattern)[k](c1, c2) \
+            if k < 4 else rt.test_pattern()
+        if rnd.random() < 0.6:
+            p.set_transform(rt.rotation_y(u(-PI, PI)) * rt.scaling(u(0.2, 2.0), u(0.2, 2.0), u(0.2, 2.0)))
+        return p
+
+    def material(m, glass_p=0.25):
+        r = rnd.random()
+        if r < glass_p:
+            m.color = rt.Color(u(0, 0.2), u(0, 0.2), u(0, 0.2))
+            m.diffuse = u(0.0, 0.3)
+            m.ambient = rnd.choice([0.0, 0.1])
+            m.specular = u(0.5, 1.0)
+            m.shininess = rnd.choice([50.0, 200.0, 300.0])
+            m.reflective = u(0.0, 0.95)
+            m.transparency = u(0.5, 1.0)
+            m.refractive_index = rnd.choice([1.0, 1.00029, 1.333, 1.5, 1.52, 2.417])
+        elif r < glass_p + 0.3:
+            m.reflective = u(0.1, 1.0)
+            m.specular = u(0.0, 1.0)
+            m.shininess = rnd.choice([10.0, 200.0])
+        else:
+            if rnd.random() < 0.35:
+                m.set_pattern(pattern())
+            else:
+                m.color = rt.Color(u(0, 1), u(0, 1), u(0, 1))
+            m.ambient = u(0.0, 0.3)
+            m.diffuse = u(0.3, 1.0)
+            m.specular = u(0.0, 1.0)
+            m.shininess = rnd.choice([1.0, 10.0, 50.0, 200.0])
+
+    def placed(shape, scale=(0.15, 0.9), shear=0.2):
+        sx, sy, sz = (u(*scale) for _ in range(3))
+        if rnd.random() < 0.5:
+            sy = sz = sx  # a uniform scale (the diagonal sphere records)
+        m = rt.translation(u(-4, 4), u(0.0, 3.0), u(-2, 6))
+        if rnd.random() < 0.4:
+            m = m * rt.rotation_x(u(-PI, PI)) * rt.rotation_y(u(-PI, PI)) * rt.rotation_z(u(-PI, PI))
+        if rnd.random() < shear:
+            m = m * rt.shearing(u(-0.4, 0.4), 0, 0, u(-0.4, 0.4), 0, u(-0.4, 0.4))
+        shape.set_transform(m * rt.scaling(sx, sy, sz))
+        return shape
+
+    floor = rt.Plane()
+    material(floor.material, glass_p=0.0)
+    floor.material.reflective = rnd.choice([0.0, 0.2, 0.5])
+    w.add_object(floor)
+    for _ in range(rnd.randrange(0, 3)):
+        wall = rt.Plane()
+        wall.set_transform(rt.rotation_y(u(-PI, PI)) * rt.translation(0, 0, u(6, 12)) * rt.rotation_x(PI / 2.0))
+        material(wall.material, glass_p=0.05)
+        w.add_object(wall)
+    n_sph = rnd.randrange(10, 120)
+    for _ in range(n_sph if n_spheres is None else n_spheres):
+        s = placed(rt.Sphere())
+        material(s.material)
+        if rnd.random() < 0.05:
+            s.no_shadow()
+        w.add_object(s)
+    for _ in range(rnd.randrange(0, 3)):  # nested glass: a shell with a core of another index inside
+        shell = rt.glass_sphere()
+        m = rt.translation(u(-3, 3), u(0.5, 2.5), u(-1, 5)) * rt.scaling(u(0.5, 1.2), u(0.5, 1.2), u(0.5, 1.2))
+        shell.set_transform(m)
+        shell.material.refractive_index = rnd.choice([1.0000034, 1.5, 2.4])
+        w.add_object(shell)
+        core = rt.glass_sphere()
+        core.set_transform(m * rt.translation(u(-0.3, 0.3), 0.0, 0.0) * rt.scaling(0.4, 0.4, 0.4))
+        core.material.refractive_index = rnd.choice([1.0, 1.33, 2.4])
+        w.add_object(core)
+    others = []
+    for _ in range(rnd.randrange(0, 14)):
+        k = rnd.randrange(3)
+        if k == 0:
+            o = rt.Cube()
+        else:
+            lo = rnd.choice([-math.inf, u(-2.0, 0.0)])
+            hi = rnd.choice([math.inf, u(0.1, 2.0)])
+            closed = rnd.random() < 0.5 and math.isfinite(lo) and math.isfinite(hi)
+            o = rt.Cylinder(lo, hi, closed) if k == 1 else rt.Cone(lo, hi, closed)
+            if not (math.isfinite(lo) and math.isfinite(hi)):
+                o = rt.Cylinder(-1.0, 1.0, rnd.random() < 0.5) if k == 1 else rt.Cone(-1.0, 0.0, rnd.random() < 0.5)
+        placed(o, scale=(0.1, 0.6))
+        material(o.material)
+        others.append(o)
+    if others and rnd.random() < 0.5:  # some of them in a group, transformed after its children, maybe divided
+        g = rt.Group()
+        for o in others[: len(others) // 2 + 1]:
+            g.add_child(o)
+        if rnd.random() < 0.5:
+            g.divide(rnd.choice([1, 2, 3]))
+        g.set_transform(rt.translation(u(-1, 1), 0.0, u(-1, 1)) * rt.rotation_y(u(-0.5, 0.5)))
+        w.add_object(g)
+        others = others[len(others) // 2 + 1:]
+    for o in others:
+        w.add_object(o)
+    for _ in range(rnd.randrange(1, 4)):
+        w.add_light(rt.PointLight(rt.Point(u(-12, 12), u(3, 15), u(-12, 4)),
+                                  rt.Color(u(0.2, 1.0), u(0.2, 1.0), u(0.2, 1.0))))
+    frm = (u(-6, 6), u(0.5, 5), u(-10, -4))
+    to = (u(-1, 1), u(0.3, 1.5), u(0, 3))
+    return w, _camera(width, height, u(0.6, 1.6), frm, to), rnd.randrange(1, 7)
