@@ -91,3 +91,36 @@ def test_fuzz_scene_large_frame_fast_equals_exhaustive(rt, seed):
     fast, _ = cam.render(w, depth, want_stats=False)
     exh, _ = cam.render(w, depth)
     assert fast.to_numpy().tobytes() == exh.to_numpy().tobytes()
+
+
+@pytest.mark.parametrize("seed", range(300, 316))
+def test_fuzz_ray_batches_vs_oracle(rt, oracle, seed):
+    """World::intersect + hit + prepare_computations, World::is_shadowed and
+    World::color_at for random rays whose origins fill the random scene's volume
+    (many inside spheres and solids): geometry bitwise, shadows equal, colours
+    bit-identical and counters equal."""
+    from rtamd import scenes
+    w, _, depth = scenes.fuzz(seed)
+    ow = oracle.OracleWorld.from_world(w)
+    rng = np.random.default_rng(seed)
+    n = 1500
+    o = rng.uniform([-4.5, -0.2, -2.5], [4.5, 3.5, 6.5], size=(n, 3))
+    d = rng.normal(size=(n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.hstack([o, d])
+    g = w.hit_batch(rays)
+    ref = np.array([ow.hit(r[:3], r[3:]) for r in rays])
+    hits = ref[:, 0] >= 0
+    assert np.array_equal(g[:, 0], ref[:, 0])
+    assert np.array_equal(g[hits, 1:23], ref[hits, 1:23])
+    assert np.abs(g[hits, 23] - ref[hits, 23]).max(initial=0.0) <= 1e-12  # schlick
+    for light in range(w.n_lights()):
+        gs = w.is_shadowed_batch(o, light)
+        rs = np.array([ow.is_shadowed(p, light) for p in o])
+        assert np.array_equal(gs.astype(bool), rs)
+    gc, st = w.color_at_batch(rays, depth)
+    rc, rst = ow.color_at_batch(rays, depth)
+    assert np.abs(gc - rc).max() <= TOL
+    assert int((gc != rc).sum()) == 0
+    for k in rst:
+        assert st[k] == rst[k], (seed, k)
