@@ -42,7 +42,7 @@ int wf_tuning_apply(WfTuning& t, const char* key, int value) {
       {"d2h", &WfTuning::d2h, 0, 1},               {"bands", &WfTuning::bands, 1, 4},
       {"band_pct", &WfTuning::band_pct, 5, 95},   {"band_gen", &WfTuning::band_gen, -1, 8},
       {"band_ratio", &WfTuning::band_ratio, 30, 100}, {"multi_gather", &WfTuning::multi_gather, 0, 1},
-      {"own_sphere", &WfTuning::own_sphere, 0, 2}};
+      {"own_sphere", &WfTuning::own_sphere, 0, 2}, {"spread", &WfTuning::spread, 0, 1}};
   if (!key) return 0;
   for (const Knob& k : knobs) {
     if (std::strcmp(key, k.name) != 0) continue;
@@ -382,6 +382,8 @@ static hipError_t launch_global(int lane, bool quads, bool tally, bool cam_rays,
 template <bool QUADS, bool TALLY>
 static hipError_t launch_fused_q(const DevScene& sc, const DevCamera& cam, WfArgs a, bool primary, unsigned n,
                                  hipStream_t stream, const WfTuning& tn) {
+  // (spread: the whole grid, whatever n; the kernel deals the chunks over every block)
+  if (a.spread && !tn.adaptive_block) n = 1u << 30;
   const int tb = trace_block(n, tn.adaptive_block);
   const size_t dl = a.use_lb ? delta_lds_bytes(sc) : 0;
   size_t dyn = 0;
@@ -623,6 +625,7 @@ hipError_t Wavefront::render_fast(const DevScene& sc, const DevCamera& cam, bool
   a.blk_period = blk_period_; a.blk_mask = blk_mask_;
   a.skip_shadow = skip_shadow ? 1u : 0u;
   a.own_sphere = sc.obj_diag ? (unsigned)tn.own_sphere : 0u;
+  a.spread = tn.spread ? 1u : 0u;
   a.count = count ? 1u : 0u;
   a.use_lb = (tn.shadow_lb && sc.lb_cells) ? 1u : 0u;
   const bool use_prim = camera_mode && sc.n_diag > 0;

@@ -114,6 +114,8 @@ struct WfTuning {
   int multi_gather = 0;    // rt_render_multi (scenes[0]'s knob): 1 = every shard gathered into device 0 by one grouped
                            //     ncclGather, then copied out of device 0 (test hook; 0 = each device copies its rows
                            //     straight into the host canvas, rt_multi.cpp)
+  int spread = 1;          // fast path: a launch with fewer 64-ray chunks than waves deals its chunks round-robin over
+                           //     its blocks (every CU) instead of filling the first blocks (0 = the first blocks)
   int own_sphere = 2;      // fast path, the shadow rays of a hit on a sphere record: 1 = from inside, test that sphere
                            //     first; 2 = also, from outside towards a light in front, leave it out (rt_trace.hpp)
 };
@@ -281,6 +283,7 @@ struct WfArgs {
   unsigned rows;        // local rows of the camera shard (generation-0 tiling)
   unsigned skip_shadow; // leave out shadow rays that cannot change the colour (fast path)
   unsigned own_sphere;    // fast path: WfTuning::own_sphere
+  unsigned spread;        // fast path: WfTuning::spread (a launch of fewer chunks than waves deals them over the blocks)
   // sharded queues: this generation's rays (in_cnt == nullptr: dense, slot = index),
   // the next generation's rays and this generation's shadow list
   const unsigned* in_cnt;
