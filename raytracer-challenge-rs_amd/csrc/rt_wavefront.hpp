@@ -114,8 +114,10 @@ struct WfTuning {
   int multi_gather = 0;    // rt_render_multi (scenes[0]'s knob): 1 = every shard gathered into device 0 by one grouped
                            //     ncclGather, then copied out of device 0 (test hook; 0 = each device copies its rows
                            //     straight into the host canvas, rt_multi.cpp)
-  int spread = 1;          // fast path: a launch with fewer 64-ray chunks than waves deals its chunks round-robin over
-                           //     its blocks (every CU) instead of filling the first blocks (0 = the first blocks)
+  int spread = 0;          // fast path: 1 = a launch with fewer 64-ray chunks than waves deals its chunks round-robin
+                           //     over its blocks (every CU) instead of filling the first blocks: a small frame rendered
+                           //     alone 24-29 % faster, but frames in flight lose (8-way shards +23 %, banded rt_render
+                           //     +4 %: the blocks then hold every CU's LDS with a few waves each), so not the default
   int own_sphere = 2;      // fast path, the shadow rays of a hit on a sphere record: 1 = from inside, test that sphere
                            //     first; 2 = also, from outside towards a light in front, leave it out (rt_trace.hpp)
 };

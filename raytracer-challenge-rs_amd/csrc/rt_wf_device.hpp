@@ -787,8 +787,8 @@ __global__ __launch_bounds__(kTraceBlock, 4) void wf_trace_fused(DevScene sc, De
   // fewer chunks than waves (a small frame, a deep generation): chunk c goes to
   // block c mod grid, so that the chunks spread over every CU instead of filling
   // the first blocks' CUs (a block's waves share one CU: 16 latency-bound walks
-  // on one CU against 4-5 each): a 320x240 frame alone 24-29 % faster
-  // (profiles/r06_spread.txt); launches of more chunks than waves are unchanged
+  // on one CU against 4-5 each): a 320x240 frame alone 24-29 % faster, frames
+  // in flight slower (WfTuning::spread, off by default; profiles/r06_spread.txt)
   const bool spread = a.spread && n_chunks < W;
   if (spread ? blockIdx.x >= n_chunks : blockIdx.x * waves_per_block >= n_chunks) return;
   const LaneScene ls = lane_scene<LANE>(sc, a.lds_flags, a.n_top, stk, lane_dyn);

@@ -13,7 +13,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "raytracer-challenge-rs_amd")]
 from rtamd import scenes  # noqa: E402
 
-VARIANTS = [{}, {"spread": 0}, {"lds_wide": 0}, {"shadow_lb": 0}, {"image": 3}, {"image": 3, "spread": 0}]
+VARIANTS = [{}, {"spread": 1}, {"lds_wide": 0}, {"shadow_lb": 0}, {"image": 3}, {"image": 3, "spread": 1}]
 
 
 def frame_ms(w, cam, depth, n=20):
@@ -45,4 +45,4 @@ for seed in [int(x) for x in sys.argv[1:]] or [130]:
         ms = frame_ms(w, cam, depth)
         print(f"  {str(v) or 'default':24s} {ms:7.3f} ms", flush=True)
         for k in v:
-            w.tune(k, {"lds_wide": 1, "shadow_lb": 1, "prim_lane": 1, "own_sphere": 2, "image": 0, "spread": 1}[k])
+            w.tune(k, {"lds_wide": 1, "shadow_lb": 1, "prim_lane": 1, "own_sphere": 2, "image": 0, "spread": 0}[k])
